@@ -1,0 +1,15 @@
+"""ldnn — an MI355X-native (gfx950 / CDNA4) distributed DNN training framework.
+
+Capabilities mirror Sanasar1/Learning-Deep-Neural-Network-In-Distributed-Computing-Environment
+(see SURVEY.md): a global/local-epoch training driver with the reference's
+flags and 12 metric histories, data-parallel aggregation by all-reduce,
+model averaging and ring / double-ring gossip (equal or self-weighted, on
+gradients or weights), IID / class-skewed / speed-proportional sharding,
+validation, test evaluation with precision/recall/F1, plots, plus what the
+reference lacks: per-step bucketed all-reduce on RCCL overlapped with the
+backward pass, hand-written bf16 MFMA kernels, checkpoint/resume, straggler
+cutoff and failure detection.
+"""
+__version__ = "0.1.0"
+
+from . import ops  # noqa: F401  (loads the native extension, loudly on GPU boxes)

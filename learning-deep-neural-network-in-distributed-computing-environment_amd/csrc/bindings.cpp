@@ -1,0 +1,293 @@
+// pybind11 bindings of the ldnn gfx950 kernels (module `_C`).
+//
+// Thin, allocation-free wrappers: every op writes into caller-provided
+// tensors and launches on the CURRENT HIP stream, so the Python layer can
+// pre-allocate its buffers once and capture whole training steps in hipGraphs.
+#include <torch/extension.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+
+#include "ldnn_kernels.h"
+
+namespace {
+
+// torch on ROCm reports HIP devices as "cuda"; use its masquerading stream/guard API.
+hipStream_t cur_stream(const at::Tensor& t) {
+  return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(t.device().index()).stream();
+}
+
+void check(hipError_t e, const char* what) {
+  TORCH_CHECK(e == hipSuccess, "ldnn kernel '", what, "' failed: ", hipGetErrorString(e));
+}
+
+void check_dev(const at::Tensor& t, at::ScalarType dt, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == dt, name, " has dtype ", t.scalar_type(), ", expected ", dt);
+}
+
+const uint16_t* bf16_ptr(const at::Tensor& t) { return reinterpret_cast<const uint16_t*>(t.data_ptr()); }
+uint16_t* bf16_mut(const at::Tensor& t) { return reinterpret_cast<uint16_t*>(t.data_ptr()); }
+
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+// Leading dimension of a 2-D operand: row stride; the last dim must be dense.
+int64_t ld_of(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.dim() == 2, name, " must be 2-D");
+  TORCH_CHECK(t.stride(1) == 1, name, " must have a unit inner stride");
+  return t.stride(0);
+}
+
+// C = epi(A_op @ B_op)
+//   a: if a_kcontig, [M][K] else [K][M];  b: if b_kcontig, [N][K] else [K][N];  c: [M][N]
+void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, bool a_kcontig, bool b_kcontig,
+          int64_t epi, const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& aux,
+          const c10::optional<at::Tensor>& dbias, double beta) {
+  check_dev(a, at::kBFloat16, "a");
+  check_dev(b, at::kBFloat16, "b");
+  TORCH_CHECK(c.is_cuda() && (c.scalar_type() == at::kBFloat16 || c.scalar_type() == at::kFloat),
+              "c must be a bf16 or fp32 GPU tensor");
+  const bool out_f32 = c.scalar_type() == at::kFloat;
+  const int64_t lda = ld_of(a, "a"), ldb = ld_of(b, "b"), ldc = ld_of(c, "c");
+  const int64_t M = a_kcontig ? a.size(0) : a.size(1);
+  const int64_t K = a_kcontig ? a.size(1) : a.size(0);
+  const int64_t N = b_kcontig ? b.size(0) : b.size(1);
+  const int64_t Kb = b_kcontig ? b.size(1) : b.size(0);
+  TORCH_CHECK(K == Kb, "gemm: inner dims differ (", K, " vs ", Kb, ")");
+  TORCH_CHECK(c.size(0) == M && c.size(1) == N, "gemm: output shape mismatch");
+  // 16-B vector staging: every contiguous extent and row stride is a multiple of 8 elements.
+  TORCH_CHECK(lda % 8 == 0 && ldb % 8 == 0 && ldc % 8 == 0, "gemm: leading dims must be multiples of 8");
+  TORCH_CHECK(K % 8 == 0 || (a_kcontig == false && b_kcontig == false), "gemm: K must be a multiple of 8");
+  TORCH_CHECK(N % 8 == 0, "gemm: N must be a multiple of 8");
+  TORCH_CHECK(a_kcontig || M % 8 == 0, "gemm: M must be a multiple of 8 for a k-strided A");
+  TORCH_CHECK(aligned16(a.data_ptr()) && aligned16(b.data_ptr()) && aligned16(c.data_ptr()),
+              "gemm: operands must be 16-byte aligned");
+  ldnn::GemmParams p{};
+  p.A = bf16_ptr(a);
+  p.B = bf16_ptr(b);
+  p.C = c.data_ptr();
+  p.M = (int)M;
+  p.N = (int)N;
+  p.K = (int)K;
+  p.lda = (int)lda;
+  p.ldb = (int)ldb;
+  p.ldc = (int)ldc;
+  p.beta = (float)beta;
+  if (epi == ldnn::EPI_BIAS || epi == ldnn::EPI_BIAS_RELU || epi == ldnn::EPI_BIAS_SIGMOID) {
+    TORCH_CHECK(bias.has_value(), "gemm: bias epilogue needs a bias tensor");
+    check_dev(*bias, at::kFloat, "bias");
+    TORCH_CHECK(bias->is_contiguous() && bias->numel() >= N && aligned16(bias->data_ptr()), "gemm: bad bias");
+    p.bias = bias->data_ptr<float>();
+  }
+  if (epi == ldnn::EPI_DRELU || epi == ldnn::EPI_DSIGMOID) {
+    TORCH_CHECK(aux.has_value(), "gemm: derivative epilogue needs the saved activation");
+    check_dev(*aux, at::kBFloat16, "aux");
+    TORCH_CHECK(aux->size(0) == M && aux->size(1) == N, "gemm: aux shape mismatch");
+    p.ldaux = (int)ld_of(*aux, "aux");
+    TORCH_CHECK(p.ldaux % 4 == 0 && aligned16(aux->data_ptr()), "gemm: bad aux layout");
+    p.aux = bf16_ptr(*aux);
+  }
+  if (dbias.has_value()) {
+    check_dev(*dbias, at::kFloat, "dbias");
+    TORCH_CHECK(dbias->is_contiguous() && dbias->numel() >= N, "gemm: bad dbias");
+    p.dbias = dbias->data_ptr<float>();
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA g(a.device());
+  check(ldnn::gemm_bf16(p, a_kcontig, b_kcontig, (int)epi, out_f32, cur_stream(a)), "gemm");
+}
+
+void act_fwd(const at::Tensor& x, const at::Tensor& y, int64_t act) {
+  check_dev(x, at::kBFloat16, "x");
+  check_dev(y, at::kBFloat16, "y");
+  TORCH_CHECK(x.is_contiguous() && y.is_contiguous() && x.numel() == y.numel(), "act_fwd: bad tensors");
+  check(ldnn::act_fwd(bf16_ptr(x), bf16_mut(y), x.numel(), (int)act, cur_stream(x)), "act_fwd");
+}
+
+void act_bwd(const at::Tensor& dy, const at::Tensor& y, const at::Tensor& dx, int64_t act) {
+  check_dev(dy, at::kBFloat16, "dy");
+  check_dev(y, at::kBFloat16, "y");
+  check_dev(dx, at::kBFloat16, "dx");
+  TORCH_CHECK(dy.is_contiguous() && y.is_contiguous() && dx.is_contiguous(), "act_bwd: non-contiguous");
+  TORCH_CHECK(dy.numel() == y.numel() && dx.numel() == y.numel(), "act_bwd: size mismatch");
+  check(ldnn::act_bwd(bf16_ptr(dy), bf16_ptr(y), bf16_mut(dx), y.numel(), (int)act, cur_stream(y)), "act_bwd");
+}
+
+void colsum(const at::Tensor& x, const at::Tensor& out, bool accumulate) {
+  check_dev(x, at::kBFloat16, "x");
+  check_dev(out, at::kFloat, "out");
+  TORCH_CHECK(x.dim() == 2 && x.is_contiguous() && x.size(1) % 8 == 0, "colsum: x must be [R][C], C%8==0");
+  TORCH_CHECK(out.is_contiguous() && out.numel() >= x.size(1), "colsum: bad out");
+  check(ldnn::colsum_bf16(bf16_ptr(x), out.data_ptr<float>(), (int)x.size(0), (int)x.size(1), accumulate,
+                          cur_stream(x)),
+        "colsum");
+}
+
+void cast_f32_bf16(const at::Tensor& x, const at::Tensor& y) {
+  check_dev(x, at::kFloat, "x");
+  check_dev(y, at::kBFloat16, "y");
+  TORCH_CHECK(x.is_contiguous() && y.is_contiguous() && x.numel() == y.numel(), "cast: bad tensors");
+  check(ldnn::cast_f32_bf16(x.data_ptr<float>(), bf16_mut(y), x.numel(), cur_stream(x)), "cast_f32_bf16");
+}
+
+void mix3(const at::Tensor& out, const at::Tensor& x, const c10::optional<at::Tensor>& y1,
+          const c10::optional<at::Tensor>& y2, double a, double b, double c,
+          const c10::optional<at::Tensor>& shadow) {
+  check_dev(out, at::kFloat, "out");
+  check_dev(x, at::kFloat, "x");
+  const int64_t n = out.numel();
+  TORCH_CHECK(out.is_contiguous() && x.is_contiguous() && x.numel() == n, "mix3: bad x/out");
+  const float* p1 = nullptr;
+  const float* p2 = nullptr;
+  if (y1.has_value()) {
+    check_dev(*y1, at::kFloat, "y1");
+    TORCH_CHECK(y1->is_contiguous() && y1->numel() == n, "mix3: bad y1");
+    p1 = y1->data_ptr<float>();
+  }
+  if (y2.has_value()) {
+    TORCH_CHECK(p1 != nullptr, "mix3: y2 without y1");
+    check_dev(*y2, at::kFloat, "y2");
+    TORCH_CHECK(y2->is_contiguous() && y2->numel() == n, "mix3: bad y2");
+    p2 = y2->data_ptr<float>();
+  }
+  uint16_t* sh = nullptr;
+  if (shadow.has_value()) {
+    check_dev(*shadow, at::kBFloat16, "shadow");
+    TORCH_CHECK(shadow->is_contiguous() && shadow->numel() == n, "mix3: bad shadow");
+    sh = bf16_mut(*shadow);
+  }
+  check(ldnn::mix3_f32(out.data_ptr<float>(), x.data_ptr<float>(), p1, p2, (float)a, (float)b, (float)c, n, sh,
+                       cur_stream(out)),
+        "mix3");
+}
+
+void softmax_xent(const at::Tensor& logits, const at::Tensor& labels, const at::Tensor& dlogits,
+                  const at::Tensor& stats, const c10::optional<at::Tensor>& dbias, int64_t num_classes,
+                  double grad_scale) {
+  check_dev(logits, at::kBFloat16, "logits");
+  check_dev(dlogits, at::kBFloat16, "dlogits");
+  check_dev(labels, at::kLong, "labels");
+  check_dev(stats, at::kFloat, "stats");
+  TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1 && dlogits.sizes() == logits.sizes() &&
+                  dlogits.strides() == logits.strides(),
+              "xent: logits/dlogits layout mismatch");
+  TORCH_CHECK(labels.is_contiguous() && labels.numel() == logits.size(0), "xent: bad labels");
+  TORCH_CHECK(stats.numel() >= 2, "xent: stats needs 2 floats");
+  // logits may be a [B][C] view of a zero-padded [B][ld] buffer (ld % 8 == 0):
+  // the kernel reads C columns and writes all ld columns of dlogits (pad = 0).
+  const int64_t ld = logits.stride(0);
+  TORCH_CHECK(num_classes <= logits.size(1) && logits.size(1) <= ld, "xent: bad class count / row stride");
+  TORCH_CHECK((int64_t)dlogits.storage().nbytes() >= (dlogits.storage_offset() + logits.size(0) * ld) * 2,
+              "xent: dlogits storage must hold the padded [B][ld] rows");
+  float* db = nullptr;
+  if (dbias.has_value()) {
+    check_dev(*dbias, at::kFloat, "dbias");
+    TORCH_CHECK(dbias->numel() >= ld, "xent: bad dbias");
+    db = dbias->data_ptr<float>();
+  }
+  check(ldnn::softmax_xent(bf16_ptr(logits), labels.data_ptr<int64_t>(), bf16_mut(dlogits),
+                           stats.data_ptr<float>(), db, (int)logits.size(0), (int)num_classes, (int)ld,
+                           (float)grad_scale, cur_stream(logits)),
+        "softmax_xent");
+}
+
+void sgd_step(const at::Tensor& param, const at::Tensor& grad, const at::Tensor& mom,
+              const c10::optional<at::Tensor>& shadow, const at::Tensor& hp, double grad_scale, double momentum,
+              double dampening, double weight_decay, bool nesterov, bool first_step) {
+  check_dev(param, at::kFloat, "param");
+  check_dev(grad, at::kFloat, "grad");
+  check_dev(hp, at::kFloat, "hp");
+  const int64_t n = param.numel();
+  TORCH_CHECK(param.is_contiguous() && grad.is_contiguous() && grad.numel() == n, "sgd: bad param/grad");
+  float* mp = nullptr;
+  if (momentum != 0.0) {
+    check_dev(mom, at::kFloat, "mom");
+    TORCH_CHECK(mom.is_contiguous() && mom.numel() == n, "sgd: bad momentum buffer");
+    mp = mom.data_ptr<float>();
+  }
+  uint16_t* sh = nullptr;
+  if (shadow.has_value()) {
+    check_dev(*shadow, at::kBFloat16, "shadow");
+    TORCH_CHECK(shadow->is_contiguous() && shadow->numel() == n, "sgd: bad shadow");
+    sh = bf16_mut(*shadow);
+  }
+  ldnn::SgdParams sp{(float)momentum, (float)dampening, (float)weight_decay, nesterov ? 1 : 0, first_step ? 1 : 0};
+  check(ldnn::sgd_step(param.data_ptr<float>(), grad.data_ptr<float>(), mp, sh, hp.data_ptr<float>(),
+                       (float)grad_scale, sp, n, cur_stream(param)),
+        "sgd_step");
+}
+
+void adam_step(const at::Tensor& param, const at::Tensor& grad, const at::Tensor& m, const at::Tensor& v,
+               const c10::optional<at::Tensor>& shadow, const at::Tensor& hp, double grad_scale, double beta1,
+               double beta2, double eps, double weight_decay, bool decoupled) {
+  check_dev(param, at::kFloat, "param");
+  check_dev(grad, at::kFloat, "grad");
+  check_dev(m, at::kFloat, "exp_avg");
+  check_dev(v, at::kFloat, "exp_avg_sq");
+  check_dev(hp, at::kFloat, "hp");
+  const int64_t n = param.numel();
+  TORCH_CHECK(param.is_contiguous() && grad.is_contiguous() && m.is_contiguous() && v.is_contiguous() &&
+                  grad.numel() == n && m.numel() == n && v.numel() == n,
+              "adam: bad buffers");
+  uint16_t* sh = nullptr;
+  if (shadow.has_value()) {
+    check_dev(*shadow, at::kBFloat16, "shadow");
+    TORCH_CHECK(shadow->is_contiguous() && shadow->numel() == n, "adam: bad shadow");
+    sh = bf16_mut(*shadow);
+  }
+  ldnn::AdamParams ap{(float)beta1, (float)beta2, (float)eps, (float)weight_decay, decoupled ? 1 : 0};
+  check(ldnn::adam_step(param.data_ptr<float>(), grad.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(),
+                        sh, hp.data_ptr<float>(), (float)grad_scale, ap, n, cur_stream(param)),
+        "adam_step");
+}
+
+void bump_step(const at::Tensor& hp) {
+  check_dev(hp, at::kFloat, "hp");
+  check(ldnn::bump_step(hp.data_ptr<float>(), cur_stream(hp)), "bump_step");
+}
+
+void synth_normal(const at::Tensor& x, int64_t seed, double stddev) {
+  check_dev(x, at::kBFloat16, "x");
+  TORCH_CHECK(x.is_contiguous(), "synth_normal: x must be contiguous");
+  check(ldnn::synth_normal_bf16(bf16_mut(x), x.numel(), (uint64_t)seed, (float)stddev, cur_stream(x)),
+        "synth_normal");
+}
+
+void synth_labels(const at::Tensor& y, int64_t classes, int64_t seed) {
+  check_dev(y, at::kLong, "y");
+  TORCH_CHECK(y.is_contiguous(), "synth_labels: y must be contiguous");
+  check(ldnn::synth_labels(y.data_ptr<int64_t>(), y.numel(), (int)classes, (uint64_t)seed, cur_stream(y)),
+        "synth_labels");
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "ldnn: hand-written gfx950 (MI355X / CDNA4) HIP kernels";
+  m.attr("EPI_NONE") = (int)ldnn::EPI_NONE;
+  m.attr("EPI_BIAS") = (int)ldnn::EPI_BIAS;
+  m.attr("EPI_BIAS_RELU") = (int)ldnn::EPI_BIAS_RELU;
+  m.attr("EPI_BIAS_SIGMOID") = (int)ldnn::EPI_BIAS_SIGMOID;
+  m.attr("EPI_DRELU") = (int)ldnn::EPI_DRELU;
+  m.attr("EPI_DSIGMOID") = (int)ldnn::EPI_DSIGMOID;
+  m.attr("ACT_RELU") = (int)ldnn::ACT_RELU;
+  m.attr("ACT_SIGMOID") = (int)ldnn::ACT_SIGMOID;
+  m.def("gemm", &gemm, "bf16 MFMA GEMM with fused epilogue", py::arg("a"), py::arg("b"), py::arg("c"),
+        py::arg("a_kcontig"), py::arg("b_kcontig"), py::arg("epi") = 0, py::arg("bias") = py::none(),
+        py::arg("aux") = py::none(), py::arg("dbias") = py::none(), py::arg("beta") = 0.0);
+  m.def("act_fwd", &act_fwd);
+  m.def("act_bwd", &act_bwd);
+  m.def("colsum", &colsum, py::arg("x"), py::arg("out"), py::arg("accumulate") = false);
+  m.def("cast_f32_bf16", &cast_f32_bf16);
+  m.def("mix3", &mix3, py::arg("out"), py::arg("x"), py::arg("y1") = py::none(), py::arg("y2") = py::none(),
+        py::arg("a") = 1.0, py::arg("b") = 0.0, py::arg("c") = 0.0, py::arg("shadow") = py::none());
+  m.def("softmax_xent", &softmax_xent, py::arg("logits"), py::arg("labels"), py::arg("dlogits"),
+        py::arg("stats"), py::arg("dbias") = py::none(), py::arg("num_classes"), py::arg("grad_scale"));
+  m.def("sgd_step", &sgd_step, py::arg("param"), py::arg("grad"), py::arg("mom"), py::arg("shadow"),
+        py::arg("hp"), py::arg("grad_scale"), py::arg("momentum"), py::arg("dampening"),
+        py::arg("weight_decay"), py::arg("nesterov"), py::arg("first_step"));
+  m.def("adam_step", &adam_step, py::arg("param"), py::arg("grad"), py::arg("m"), py::arg("v"),
+        py::arg("shadow"), py::arg("hp"), py::arg("grad_scale"), py::arg("beta1"), py::arg("beta2"),
+        py::arg("eps"), py::arg("weight_decay"), py::arg("decoupled"));
+  m.def("bump_step", &bump_step);
+  m.def("synth_normal", &synth_normal);
+  m.def("synth_labels", &synth_labels);
+}

@@ -1,0 +1,78 @@
+// Host-callable launchers of the ldnn gfx950 kernels (no torch dependency:
+// every launcher takes raw device pointers and a hipStream_t, so the same
+// entry points serve the pybind layer, graph capture and C++ tests).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ldnn {
+
+enum Epilogue : int {
+  EPI_NONE = 0,
+  EPI_BIAS = 1,
+  EPI_BIAS_RELU = 2,
+  EPI_BIAS_SIGMOID = 3,
+  EPI_DRELU = 4,
+  EPI_DSIGMOID = 5,
+};
+
+struct GemmParams {
+  const uint16_t* A;
+  const uint16_t* B;
+  void* C;
+  const float* bias;     // [N] fp32 (EPI_BIAS*)
+  const uint16_t* aux;   // [M][ldaux] bf16 saved activation (EPI_D*)
+  float* dbias;          // optional [N] fp32 column-sum accumulator
+  int M, N, K;
+  int lda, ldb, ldc, ldaux;
+  float beta;            // fp32 output only: C = acc + beta * C
+};
+
+hipError_t gemm_bf16(const GemmParams& p, bool a_kcontig, bool b_kcontig, int epi, bool out_f32,
+                     hipStream_t s);
+
+// ---- elementwise / activations (bf16 storage, fp32 math) ---------------------
+enum Act : int { ACT_RELU = 0, ACT_SIGMOID = 1 };
+hipError_t act_fwd(const uint16_t* x, uint16_t* y, int64_t n, int act, hipStream_t s);
+hipError_t act_bwd(const uint16_t* dy, const uint16_t* y, uint16_t* dx, int64_t n, int act, hipStream_t s);
+// dbias[c] (+)= sum_r x[r][c] over a [rows][cols] bf16 matrix (ld = cols)
+hipError_t colsum_bf16(const uint16_t* x, float* out, int rows, int cols, bool accumulate, hipStream_t s);
+hipError_t cast_f32_bf16(const float* x, uint16_t* y, int64_t n, hipStream_t s);
+hipError_t cast_bf16_f32(const uint16_t* x, float* y, int64_t n, hipStream_t s);
+// y = a*x + b*y1 + c*y2 (fp32, in place on x allowed); optional bf16 shadow of y
+hipError_t mix3_f32(float* out, const float* x, const float* y1, const float* y2, float a, float b, float c,
+                    int64_t n, uint16_t* shadow, hipStream_t s);
+// x *= scale (fp32), optional bf16 shadow
+hipError_t scale_f32(float* x, float scale, int64_t n, uint16_t* shadow, hipStream_t s);
+
+// ---- fused softmax cross-entropy (K14 + K15 of SURVEY §2.3) ---------------
+// logits [B][ld] bf16 (first C columns valid), labels int64 [B].
+// Writes dlogits [B][ld] bf16 = (softmax - onehot) * grad_scale (padded columns 0),
+// accumulates sum of per-row loss into stats[0] and #correct into stats[1]
+// (fp32), optionally column sums of dlogits into dbias[ld].
+hipError_t softmax_xent(const uint16_t* logits, const int64_t* labels, uint16_t* dlogits, float* stats,
+                        float* dbias, int B, int C, int ld, float grad_scale, hipStream_t s);
+
+// ---- fused optimizers over flat fp32 buffers -------------------------------
+// hp (device fp32): [0]=lr [1]=step (already incremented for Adam) ; grad_scale multiplies g
+struct SgdParams {
+  float momentum, dampening, weight_decay;
+  int nesterov;
+  int first_step;  // momentum buffer initialised from g (torch semantics)
+};
+hipError_t sgd_step(float* param, const float* grad, float* mom, uint16_t* shadow, const float* hp,
+                    float grad_scale, SgdParams sp, int64_t n, hipStream_t s);
+struct AdamParams {
+  float beta1, beta2, eps, weight_decay;
+  int decoupled;  // AdamW
+};
+hipError_t adam_step(float* param, const float* grad, float* m, float* v, uint16_t* shadow, const float* hp,
+                     float grad_scale, AdamParams ap, int64_t n, hipStream_t s);
+// hp[1] += 1 (graph-capturable step counter)
+hipError_t bump_step(float* hp, hipStream_t s);
+
+// ---- synthetic data (K20): deterministic device-side generator -----------
+hipError_t synth_normal_bf16(uint16_t* x, int64_t n, uint64_t seed, float stddev, hipStream_t s);
+hipError_t synth_labels(int64_t* y, int64_t n, int classes, uint64_t seed, hipStream_t s);
+
+}  // namespace ldnn

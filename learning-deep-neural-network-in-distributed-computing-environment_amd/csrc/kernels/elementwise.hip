@@ -1,0 +1,233 @@
+// Memory-bound helpers: activations, bias-gradient column sums, casts, the
+// aggregation "mix" kernel and device-side synthetic data.
+//
+// All bf16 traffic is vectorised to 16 B per lane (Guideline 13); grids are
+// capped at 2048 workgroups and grid-stride the rest (Guideline 11).
+//
+// mix3_f32 is kernel K18 of SURVEY §2.3: every aggregation formula of the
+// reference -- BAR/communication.py:9-10,17-18,25,31 (equal / weighted
+// all-reduce), BR/communication.py:30,62 (ring), BDR/communication.py:39-40,77
+// (double ring) -- is  out = a*x + b*y1 + c*y2  for suitable (a, b, c), done in
+// one pass, in place, with the bf16 compute shadow refreshed in the same pass.
+#include "ldnn_common.h"
+#include "ldnn_kernels.h"
+
+namespace ldnn {
+
+namespace {
+
+constexpr int kBlock = 256;
+
+inline int grid_for(int64_t work_items) {
+  int64_t g = (work_items + kBlock - 1) / kBlock;
+  if (g < 1) g = 1;
+  if (g > 2048) g = 2048;
+  return (int)g;
+}
+
+template <int ACT>
+__device__ __forceinline__ float act_f(float x) {
+  if constexpr (ACT == ACT_RELU) return fmaxf(x, 0.f);
+  return 1.f / (1.f + __expf(-x));
+}
+template <int ACT>
+__device__ __forceinline__ float act_b(float dy, float y) {
+  if constexpr (ACT == ACT_RELU) return y > 0.f ? dy : 0.f;
+  return dy * y * (1.f - y);
+}
+
+template <int ACT>
+__global__ void act_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int64_t n) {
+  const int64_t nv = n / 8;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nv; i += stride) {
+    u16x8 v = reinterpret_cast<const u16x8*>(x)[i];
+    u16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = f2bf(act_f<ACT>(bf2f(v[j])));
+    reinterpret_cast<u16x8*>(y)[i] = o;
+  }
+  for (int64_t i = nv * 8 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride)
+    y[i] = f2bf(act_f<ACT>(bf2f(x[i])));
+}
+
+template <int ACT>
+__global__ void act_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
+                               bf16_t* __restrict__ dx, int64_t n) {
+  const int64_t nv = n / 8;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nv; i += stride) {
+    u16x8 g = reinterpret_cast<const u16x8*>(dy)[i];
+    u16x8 v = reinterpret_cast<const u16x8*>(y)[i];
+    u16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = f2bf(act_b<ACT>(bf2f(g[j]), bf2f(v[j])));
+    reinterpret_cast<u16x8*>(dx)[i] = o;
+  }
+  for (int64_t i = nv * 8 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride)
+    dx[i] = f2bf(act_b<ACT>(bf2f(dy[i]), bf2f(y[i])));
+}
+
+// Column sums of a [rows][cols] bf16 matrix: a block is 32 column-groups of 8
+// columns (16-B loads) x 8 row lanes; rows are split over gridDim.y.
+__global__ void colsum_kernel(const bf16_t* __restrict__ x, float* __restrict__ out, int rows, int cols,
+                              int rows_per_block) {
+  __shared__ float part[8][32 * 8];
+  const int cg = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const int c0 = (blockIdx.x * 32 + cg) * 8;
+  const int r_begin = blockIdx.y * rows_per_block;
+  const int r_end = min(rows, r_begin + rows_per_block);
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c0 < cols) {
+    for (int r = r_begin + ty; r < r_end; r += 8) {
+      const u16x8 v = *reinterpret_cast<const u16x8*>(x + (size_t)r * cols + c0);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s[j] += bf2f(v[j]);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) part[ty][cg * 8 + j] = s[j];
+  __syncthreads();
+  if (ty == 0 && c0 < cols) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float t = 0.f;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) t += part[q][cg * 8 + j];
+      atomicAdd(out + c0 + j, t);
+    }
+  }
+}
+
+__global__ void cast_f32_bf16_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, int64_t n) {
+  const int64_t nv = n / 4;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nv; i += stride) {
+    const floatx4 v = reinterpret_cast<const floatx4*>(x)[i];
+    reinterpret_cast<u16x4*>(y)[i] = u16x4{f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+  }
+  for (int64_t i = nv * 4 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride) y[i] = f2bf(x[i]);
+}
+
+__global__ void cast_bf16_f32_kernel(const bf16_t* __restrict__ x, float* __restrict__ y, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride) y[i] = bf2f(x[i]);
+}
+
+template <int NIN>
+__global__ void mix_kernel(float* out, const float* x, const float* y1, const float* y2, float a, float b,
+                           float c, int64_t n, bf16_t* shadow) {
+  const int64_t nv = n / 4;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nv; i += stride) {
+    floatx4 v = a * reinterpret_cast<const floatx4*>(x)[i];
+    if constexpr (NIN >= 2) v += b * reinterpret_cast<const floatx4*>(y1)[i];
+    if constexpr (NIN >= 3) v += c * reinterpret_cast<const floatx4*>(y2)[i];
+    reinterpret_cast<floatx4*>(out)[i] = v;
+    if (shadow) reinterpret_cast<u16x4*>(shadow)[i] = u16x4{f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+  }
+  for (int64_t i = nv * 4 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride) {
+    float v = a * x[i];
+    if constexpr (NIN >= 2) v += b * y1[i];
+    if constexpr (NIN >= 3) v += c * y2[i];
+    out[i] = v;
+    if (shadow) shadow[i] = f2bf(v);
+  }
+}
+
+// splitmix64 counter hash -> two uniforms -> Box-Muller normal.
+__device__ __forceinline__ uint64_t smix(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__global__ void synth_normal_kernel(bf16_t* x, int64_t n, uint64_t seed, float stddev) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint64_t h = smix(seed * 0x100000001B3ull + (uint64_t)i);
+    const float u1 = ((h >> 40) + 1) * (1.0f / 16777217.0f);
+    const float u2 = ((h & 0xFFFFFF)) * (1.0f / 16777216.0f);
+    const float z = sqrtf(-2.f * __logf(u1)) * __cosf(6.2831853f * u2);
+    x[i] = f2bf(z * stddev);
+  }
+}
+
+__global__ void synth_labels_kernel(int64_t* y, int64_t n, int classes, uint64_t seed) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride)
+    y[i] = (int64_t)(smix(seed * 0x9E3779B1ull + (uint64_t)i) % (uint64_t)classes);
+}
+
+}  // namespace
+
+hipError_t act_fwd(const uint16_t* x, uint16_t* y, int64_t n, int act, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  const int g = grid_for((n + 7) / 8);
+  if (act == ACT_RELU) act_fwd_kernel<ACT_RELU><<<g, kBlock, 0, s>>>(x, y, n);
+  else act_fwd_kernel<ACT_SIGMOID><<<g, kBlock, 0, s>>>(x, y, n);
+  return hipGetLastError();
+}
+
+hipError_t act_bwd(const uint16_t* dy, const uint16_t* y, uint16_t* dx, int64_t n, int act, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  const int g = grid_for((n + 7) / 8);
+  if (act == ACT_RELU) act_bwd_kernel<ACT_RELU><<<g, kBlock, 0, s>>>(dy, y, dx, n);
+  else act_bwd_kernel<ACT_SIGMOID><<<g, kBlock, 0, s>>>(dy, y, dx, n);
+  return hipGetLastError();
+}
+
+hipError_t colsum_bf16(const uint16_t* x, float* out, int rows, int cols, bool accumulate, hipStream_t s) {
+  if (!accumulate) {
+    hipError_t e = hipMemsetAsync(out, 0, sizeof(float) * cols, s);
+    if (e != hipSuccess) return e;
+  }
+  if (rows <= 0 || cols <= 0) return hipSuccess;
+  const int gx = (cols + 255) / 256;
+  int gy = (rows + 255) / 256;
+  if (gy > 256) gy = 256;
+  const int rpb = (rows + gy - 1) / gy;
+  colsum_kernel<<<dim3(gx, gy), kBlock, 0, s>>>(x, out, rows, cols, rpb);
+  return hipGetLastError();
+}
+
+hipError_t cast_f32_bf16(const float* x, uint16_t* y, int64_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  cast_f32_bf16_kernel<<<grid_for((n + 3) / 4), kBlock, 0, s>>>(x, y, n);
+  return hipGetLastError();
+}
+
+hipError_t cast_bf16_f32(const uint16_t* x, float* y, int64_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  cast_bf16_f32_kernel<<<grid_for(n), kBlock, 0, s>>>(x, y, n);
+  return hipGetLastError();
+}
+
+hipError_t mix3_f32(float* out, const float* x, const float* y1, const float* y2, float a, float b, float c,
+                    int64_t n, uint16_t* shadow, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  const int g = grid_for((n + 3) / 4);
+  if (y2) mix_kernel<3><<<g, kBlock, 0, s>>>(out, x, y1, y2, a, b, c, n, shadow);
+  else if (y1) mix_kernel<2><<<g, kBlock, 0, s>>>(out, x, y1, y2, a, b, c, n, shadow);
+  else mix_kernel<1><<<g, kBlock, 0, s>>>(out, x, y1, y2, a, b, c, n, shadow);
+  return hipGetLastError();
+}
+
+hipError_t scale_f32(float* x, float scale, int64_t n, uint16_t* shadow, hipStream_t s) {
+  return mix3_f32(x, x, nullptr, nullptr, scale, 0.f, 0.f, n, shadow, s);
+}
+
+hipError_t synth_normal_bf16(uint16_t* x, int64_t n, uint64_t seed, float stddev, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  synth_normal_kernel<<<grid_for(n), kBlock, 0, s>>>(x, n, seed, stddev);
+  return hipGetLastError();
+}
+
+hipError_t synth_labels(int64_t* y, int64_t n, int classes, uint64_t seed, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  synth_labels_kernel<<<grid_for(n), kBlock, 0, s>>>(y, n, classes, seed);
+  return hipGetLastError();
+}
+
+}  // namespace ldnn

@@ -1,0 +1,134 @@
+// Fused optimizer updates over flat fp32 master buffers.
+//
+// The reference steps torch.optim.Adam per tensor (BAR/main.py:53,
+// BAR/trainer.py:210: 65 tensors, 44.6 M elements).  Here a model's parameters
+// live in ONE flat fp32 buffer (views per tensor keep the reference state_dict
+// keys), so one launch updates all of them and, in the same pass, refreshes
+// the bf16 compute shadow that the MFMA kernels read.  The all-reduce average
+// (1/world_size) and any loss scaling are folded into `grad_scale`.
+//
+// Hyper-parameters that change between steps (lr, Adam step count) are read
+// from a device buffer `hp`, so a captured hipGraph replays with the current
+// schedule value and no host sync.
+#include "ldnn_common.h"
+#include "ldnn_kernels.h"
+
+namespace ldnn {
+
+namespace {
+
+constexpr int kBlock = 256;
+
+__global__ void sgd_kernel(float* __restrict__ param, const float* __restrict__ grad, float* __restrict__ mom,
+                           bf16_t* __restrict__ shadow, const float* __restrict__ hp, float grad_scale,
+                           SgdParams sp, int64_t n) {
+  const float lr = hp[0];
+  const int64_t nv = n / 4;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nv; i += stride) {
+    floatx4 p = reinterpret_cast<floatx4*>(param)[i];
+    floatx4 g = reinterpret_cast<const floatx4*>(grad)[i] * grad_scale;
+    if (sp.weight_decay != 0.f) g += sp.weight_decay * p;
+    if (sp.momentum != 0.f) {
+      floatx4 b;
+      if (sp.first_step) b = g;
+      else b = sp.momentum * reinterpret_cast<floatx4*>(mom)[i] + (1.f - sp.dampening) * g;
+      reinterpret_cast<floatx4*>(mom)[i] = b;
+      g = sp.nesterov ? g + sp.momentum * b : b;
+    }
+    p -= lr * g;
+    reinterpret_cast<floatx4*>(param)[i] = p;
+    if (shadow) reinterpret_cast<u16x4*>(shadow)[i] = u16x4{f2bf(p[0]), f2bf(p[1]), f2bf(p[2]), f2bf(p[3])};
+  }
+  for (int64_t i = nv * 4 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride) {
+    float p = param[i];
+    float g = grad[i] * grad_scale;
+    if (sp.weight_decay != 0.f) g += sp.weight_decay * p;
+    if (sp.momentum != 0.f) {
+      const float b = sp.first_step ? g : sp.momentum * mom[i] + (1.f - sp.dampening) * g;
+      mom[i] = b;
+      g = sp.nesterov ? g + sp.momentum * b : b;
+    }
+    p -= lr * g;
+    param[i] = p;
+    if (shadow) shadow[i] = f2bf(p);
+  }
+}
+
+__device__ __forceinline__ float adam_elem(float p, float g, float& m, float& v, float lr, float bc1,
+                                           float bc2s, const AdamParams& ap) {
+  if (ap.weight_decay != 0.f) {
+    if (ap.decoupled) p *= (1.f - lr * ap.weight_decay);
+    else g += ap.weight_decay * p;
+  }
+  m = ap.beta1 * m + (1.f - ap.beta1) * g;
+  v = ap.beta2 * v + (1.f - ap.beta2) * g * g;
+  const float denom = sqrtf(v) / bc2s + ap.eps;
+  return p - (lr / bc1) * m / denom;
+}
+
+__global__ void adam_kernel(float* __restrict__ param, const float* __restrict__ grad, float* __restrict__ mm,
+                            float* __restrict__ vv, bf16_t* __restrict__ shadow, const float* __restrict__ hp,
+                            float grad_scale, AdamParams ap, int64_t n) {
+  const float lr = hp[0];
+  const float t = hp[1];
+  const float bc1 = 1.f - powf(ap.beta1, t);
+  const float bc2s = sqrtf(1.f - powf(ap.beta2, t));
+  const int64_t nv = n / 4;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nv; i += stride) {
+    floatx4 p = reinterpret_cast<floatx4*>(param)[i];
+    const floatx4 g = reinterpret_cast<const floatx4*>(grad)[i] * grad_scale;
+    floatx4 m = reinterpret_cast<floatx4*>(mm)[i];
+    floatx4 v = reinterpret_cast<floatx4*>(vv)[i];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float mj = m[j], vj = v[j];
+      p[j] = adam_elem(p[j], g[j], mj, vj, lr, bc1, bc2s, ap);
+      m[j] = mj;
+      v[j] = vj;
+    }
+    reinterpret_cast<floatx4*>(param)[i] = p;
+    reinterpret_cast<floatx4*>(mm)[i] = m;
+    reinterpret_cast<floatx4*>(vv)[i] = v;
+    if (shadow) reinterpret_cast<u16x4*>(shadow)[i] = u16x4{f2bf(p[0]), f2bf(p[1]), f2bf(p[2]), f2bf(p[3])};
+  }
+  for (int64_t i = nv * 4 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride) {
+    float m = mm[i], v = vv[i];
+    const float p = adam_elem(param[i], grad[i] * grad_scale, m, v, lr, bc1, bc2s, ap);
+    param[i] = p;
+    mm[i] = m;
+    vv[i] = v;
+    if (shadow) shadow[i] = f2bf(p);
+  }
+}
+
+__global__ void bump_kernel(float* hp) { hp[1] += 1.f; }
+
+inline int grid_for(int64_t n4) {
+  int64_t g = (n4 + kBlock - 1) / kBlock;
+  return (int)(g < 1 ? 1 : (g > 2048 ? 2048 : g));
+}
+
+}  // namespace
+
+hipError_t sgd_step(float* param, const float* grad, float* mom, uint16_t* shadow, const float* hp,
+                    float grad_scale, SgdParams sp, int64_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  sgd_kernel<<<grid_for((n + 3) / 4), kBlock, 0, s>>>(param, grad, mom, shadow, hp, grad_scale, sp, n);
+  return hipGetLastError();
+}
+
+hipError_t adam_step(float* param, const float* grad, float* m, float* v, uint16_t* shadow, const float* hp,
+                     float grad_scale, AdamParams ap, int64_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  adam_kernel<<<grid_for((n + 3) / 4), kBlock, 0, s>>>(param, grad, m, v, shadow, hp, grad_scale, ap, n);
+  return hipGetLastError();
+}
+
+hipError_t bump_step(float* hp, hipStream_t s) {
+  bump_kernel<<<1, 1, 0, s>>>(hp);
+  return hipGetLastError();
+}
+
+}  // namespace ldnn

@@ -1,0 +1,181 @@
+"""Numerics of the hand-written gfx950 kernels against plain PyTorch fp32
+references of the same op (run on the MI355X box: `pytest -m gpu`)."""
+import pytest
+import torch
+
+import ldnn
+from ldnn.ops import _ext
+
+pytestmark = pytest.mark.gpu
+
+
+def C():
+    return _ext.C()
+
+
+def _ref_gemm(a, b, a_kc, b_kc):
+    A = a.float() if a_kc else a.float().t()
+    B = b.float().t() if b_kc else b.float()
+    return A @ B
+
+
+@pytest.mark.parametrize("a_kc,b_kc", [(True, True), (True, False), (False, True), (False, False)])
+@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (200, 136, 784), (1000, 264, 72), (64, 16, 4096), (384, 512, 1000)])
+def test_gemm_layouts(a_kc, b_kc, M, N, K):
+    if (not a_kc or not b_kc) and K % 8 and (a_kc or b_kc):
+        pytest.skip("k-contiguous operand needs K % 8 == 0")
+    if not a_kc and M % 8:
+        pytest.skip("strided A needs M % 8 == 0")
+    torch.manual_seed(0)
+    dev = "cuda"
+    a = (torch.randn(M, K, device=dev) if a_kc else torch.randn(K, M, device=dev)).bfloat16()
+    b = (torch.randn(N, K, device=dev) if b_kc else torch.randn(K, N, device=dev)).bfloat16()
+    c = torch.empty(M, N, device=dev, dtype=torch.float32)
+    C().gemm(a, b, c, a_kc, b_kc)
+    ref = _ref_gemm(a, b, a_kc, b_kc)
+    torch.cuda.synchronize()
+    err = (c - ref).abs().max().item()
+    assert err <= 1e-3 * K ** 0.5 + 1e-3, err
+    cb = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    C().gemm(a, b, cb, a_kc, b_kc)
+    rel = ((cb.float() - ref).abs().max() / ref.abs().max()).item()
+    assert rel < 1e-2, rel
+
+
+def test_gemm_asymmetric_identity():
+    """A = I with an asymmetric B catches a transposed C write."""
+    n = 128
+    a = torch.eye(n, device="cuda").bfloat16()
+    b = torch.arange(n * n, device="cuda").reshape(n, n).float().remainder(97).bfloat16()
+    c = torch.empty(n, n, device="cuda")
+    C().gemm(a, b, c, True, True)  # C = I @ b^T
+    assert torch.equal(c, b.float().t())
+    C().gemm(a, b, c, True, False)  # C = I @ b
+    assert torch.equal(c, b.float())
+
+
+@pytest.mark.parametrize("epi", ["bias", "relu", "sigmoid"])
+def test_gemm_fwd_epilogues(epi):
+    torch.manual_seed(1)
+    M, N, K = 300, 264, 784
+    x = torch.randn(M, K, device="cuda").bfloat16()
+    w = (torch.randn(N, K, device="cuda") * 0.05).bfloat16()
+    bias = torch.randn(N, device="cuda")
+    y = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    code = {"bias": C().EPI_BIAS, "relu": C().EPI_BIAS_RELU, "sigmoid": C().EPI_BIAS_SIGMOID}[epi]
+    C().gemm(x, w, y, True, True, code, bias=bias)
+    ref = x.float() @ w.float().t() + bias
+    if epi == "relu":
+        ref = ref.relu()
+    elif epi == "sigmoid":
+        ref = ref.sigmoid()
+    torch.testing.assert_close(y.float(), ref, rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("act", ["relu", "sigmoid"])
+def test_gemm_dgrad_epilogue_and_dbias(act):
+    torch.manual_seed(2)
+    M, N, K = 260, 136, 512  # dX[M,K] = dY[M,N] @ W[N,K]
+    dy = torch.randn(M, N, device="cuda").bfloat16()
+    w = torch.randn(N, K, device="cuda").bfloat16()
+    yprev = torch.randn(M, K, device="cuda")
+    yprev = (yprev.relu() if act == "relu" else yprev.sigmoid()).bfloat16()
+    dx = torch.empty(M, K, device="cuda", dtype=torch.bfloat16)
+    db = torch.zeros(K, device="cuda")
+    code = C().EPI_DRELU if act == "relu" else C().EPI_DSIGMOID
+    C().gemm(dy, w, dx, True, False, code, aux=yprev, dbias=db)
+    g = dy.float() @ w.float()
+    y = yprev.float()
+    ref = g * (y > 0) if act == "relu" else g * y * (1 - y)
+    torch.testing.assert_close(dx.float(), ref, rtol=2e-2, atol=5e-2)
+    torch.testing.assert_close(db, dx.float().sum(0), rtol=1e-3, atol=1e-2)
+
+
+def test_gemm_wgrad_beta_accumulate():
+    torch.manual_seed(3)
+    B, N, K = 1000, 264, 784  # dW[N,K] = dY^T X
+    dy = torch.randn(B, N, device="cuda").bfloat16()
+    x = torch.randn(B, K, device="cuda").bfloat16()
+    dw = torch.randn(N, K, device="cuda")
+    base = dw.clone()
+    C().gemm(dy, x, dw, False, False, beta=1.0)
+    ref = base + dy.float().t() @ x.float()
+    torch.testing.assert_close(dw, ref, rtol=1e-4, atol=1e-2)
+
+
+def test_softmax_xent_matches_torch():
+    torch.manual_seed(4)
+    B, Cc, ld = 777, 10, 16
+    full = torch.randn(B, ld, device="cuda").bfloat16()
+    logits = full[:, :Cc]
+    labels = torch.randint(0, Cc, (B,), device="cuda")
+    dl = torch.empty(B, ld, device="cuda", dtype=torch.bfloat16)
+    stats = torch.zeros(2, device="cuda")
+    db = torch.zeros(ld, device="cuda")
+    C().softmax_xent(logits, labels, dl[:, :Cc], stats, dbias=db, num_classes=Cc, grad_scale=1.0 / B)
+    lf = logits.float().requires_grad_(True)
+    loss = torch.nn.functional.cross_entropy(lf, labels)
+    loss.backward()
+    torch.testing.assert_close(stats[0] / B, loss.detach(), rtol=1e-4, atol=1e-4)
+    correct = (lf.detach().argmax(1) == labels).sum().float()
+    assert stats[1].item() == correct.item()
+    torch.testing.assert_close(dl[:, :Cc].float(), lf.grad, rtol=2e-2, atol=1e-4)
+    assert dl[:, Cc:].float().abs().max().item() == 0.0
+    torch.testing.assert_close(db[:Cc], dl[:, :Cc].float().sum(0), rtol=1e-3, atol=1e-5)
+
+
+def test_sgd_momentum_matches_torch():
+    torch.manual_seed(5)
+    n = 10_003
+    p = torch.randn(n, device="cuda")
+    p_ref = p.clone().requires_grad_(True)
+    mom = torch.zeros(n, device="cuda")
+    sh = torch.empty(n, device="cuda", dtype=torch.bfloat16)
+    hp = torch.tensor([0.1, 0.0], device="cuda")
+    opt = torch.optim.SGD([p_ref], lr=0.1, momentum=0.9, weight_decay=1e-4, nesterov=True)
+    for step in range(3):
+        g = torch.randn(n, device="cuda")
+        C().sgd_step(p, g * 2, mom, sh, hp, 0.5, 0.9, 0.0, 1e-4, True, step == 0)
+        p_ref.grad = g.clone()
+        opt.step()
+    torch.testing.assert_close(p, p_ref.detach(), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(sh.float(), p.bfloat16().float())
+
+
+def test_adam_matches_torch():
+    torch.manual_seed(6)
+    n = 4099
+    p = torch.randn(n, device="cuda")
+    p_ref = p.clone().requires_grad_(True)
+    m = torch.zeros(n, device="cuda")
+    v = torch.zeros(n, device="cuda")
+    hp = torch.tensor([1e-3, 0.0], device="cuda")
+    opt = torch.optim.Adam([p_ref], lr=1e-3)
+    for _ in range(4):
+        g = torch.randn(n, device="cuda")
+        C().bump_step(hp)
+        C().adam_step(p, g, m, v, None, hp, 1.0, 0.9, 0.999, 1e-8, 0.0, False)
+        p_ref.grad = g.clone()
+        opt.step()
+    torch.testing.assert_close(p, p_ref.detach(), rtol=1e-5, atol=1e-6)
+
+
+def test_mix3_and_colsum_and_act():
+    torch.manual_seed(7)
+    n = 5003
+    x, y1, y2 = (torch.randn(n, device="cuda") for _ in range(3))
+    out = torch.empty_like(x)
+    sh = torch.empty(n, device="cuda", dtype=torch.bfloat16)
+    C().mix3(out, x, y1, y2, 0.5, 0.25, 0.25, sh)
+    torch.testing.assert_close(out, 0.5 * x + 0.25 * y1 + 0.25 * y2)
+    xb = torch.randn(333, 72, device="cuda").bfloat16()
+    cs = torch.empty(72, device="cuda")
+    C().colsum(xb, cs, False)
+    torch.testing.assert_close(cs, xb.float().sum(0), rtol=1e-4, atol=1e-3)
+    y = torch.empty_like(xb)
+    C().act_fwd(xb, y, C().ACT_SIGMOID)
+    torch.testing.assert_close(y.float(), xb.float().sigmoid(), rtol=1e-2, atol=1e-2)
+    dx = torch.empty_like(xb)
+    C().act_bwd(xb, y, dx, C().ACT_SIGMOID)
+    yf = y.float()
+    torch.testing.assert_close(dx.float(), xb.float() * yf * (1 - yf), rtol=2e-2, atol=1e-2)
