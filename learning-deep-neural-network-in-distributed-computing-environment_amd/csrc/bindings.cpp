@@ -41,7 +41,7 @@ int64_t ld_of(const at::Tensor& t, const char* name) {
 //   a: if a_kcontig, [M][K] else [K][M];  b: if b_kcontig, [N][K] else [K][N];  c: [M][N]
 void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, bool a_kcontig, bool b_kcontig,
           int64_t epi, const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& aux,
-          const c10::optional<at::Tensor>& dbias, double beta) {
+          const c10::optional<at::Tensor>& dbias, double beta, int64_t tile) {
   check_dev(a, at::kBFloat16, "a");
   check_dev(b, at::kBFloat16, "b");
   TORCH_CHECK(c.is_cuda() && (c.scalar_type() == at::kBFloat16 || c.scalar_type() == at::kFloat),
@@ -92,7 +92,9 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, bool a_
     p.dbias = dbias->data_ptr<float>();
   }
   c10::hip::HIPGuardMasqueradingAsCUDA g(a.device());
-  check(ldnn::gemm_bf16(p, a_kcontig, b_kcontig, (int)epi, out_f32, cur_stream(a)), "gemm");
+  if (tile == 0) tile = ldnn::gemm_pick_tile(p.M, p.N, p.K);
+  TORCH_CHECK(tile == 128 || tile == 256, "gemm: tile must be 0 (auto), 128 or 256");
+  check(ldnn::gemm_bf16_tile(p, a_kcontig, b_kcontig, (int)epi, out_f32, (int)tile, cur_stream(a)), "gemm");
 }
 
 void act_fwd(const at::Tensor& x, const at::Tensor& y, int64_t act) {
@@ -272,7 +274,8 @@ PYBIND11_MODULE(_C, m) {
   m.attr("ACT_SIGMOID") = (int)ldnn::ACT_SIGMOID;
   m.def("gemm", &gemm, "bf16 MFMA GEMM with fused epilogue", py::arg("a"), py::arg("b"), py::arg("c"),
         py::arg("a_kcontig"), py::arg("b_kcontig"), py::arg("epi") = 0, py::arg("bias") = py::none(),
-        py::arg("aux") = py::none(), py::arg("dbias") = py::none(), py::arg("beta") = 0.0);
+        py::arg("aux") = py::none(), py::arg("dbias") = py::none(), py::arg("beta") = 0.0,
+        py::arg("tile") = 0);
   m.def("act_fwd", &act_fwd);
   m.def("act_bwd", &act_bwd);
   m.def("colsum", &colsum, py::arg("x"), py::arg("out"), py::arg("accumulate") = false);

@@ -28,8 +28,14 @@ struct GemmParams {
   float beta;            // fp32 output only: C = acc + beta * C
 };
 
+// Picks the tiling (256x256 LDS-DMA kernel or 128x128 kernel) from the shape.
 hipError_t gemm_bf16(const GemmParams& p, bool a_kcontig, bool b_kcontig, int epi, bool out_f32,
                      hipStream_t s);
+// Same with an explicit tile (128 or 256); 256 falls back to 128 for operands >= 2 GiB.
+hipError_t gemm_bf16_tile(const GemmParams& p, bool a_kcontig, bool b_kcontig, int epi, bool out_f32, int tile,
+                          hipStream_t s);
+int gemm_pick_tile(int M, int N, int K);
+constexpr size_t kOOBLimit = 0x80000000ull;
 
 // ---- elementwise / activations (bf16 storage, fp32 math) ---------------------
 enum Act : int { ACT_RELU = 0, ACT_SIGMOID = 1 };

@@ -10,21 +10,31 @@
 //   dgrad dX = dY W   -> A_KC=1, B_KC=0
 //   wgrad dW = dY^T X -> A_KC=0, B_KC=0   (fp32 output straight into the flat grad buffer)
 //
-// Tiling (CDNA4-first, see /opt/skills/guides/cdna_hip_programming.md §5):
-//   * 128x128 output tile, BK = 64, 256 threads = 4 waves (2x2), 64x64 per wave,
-//     v_mfma_f32_16x16x32_bf16 (4x4 accumulators of 16x16 per wave).
+// Two tilings, picked per shape by gemm_bf16():
+//
+//  * gemm256 (large shapes): 256x256 output tile, BK = 64, 512 threads = 8 waves
+//    (2 M x 4 N, 128x64 per wave, 8x4 accumulators of v_mfma_f32_16x16x32_bf16).
+//    Operands are staged HBM/L2 -> LDS by LDS-DMA (buffer_load_dwordx4 ... lds,
+//    no VGPR round trip) into two 64 KiB stages; the next tile's DMA stays in
+//    flight across the compute of the current one (counted vmcnt + raw
+//    s_barrier, never __syncthreads while a DMA is outstanding).  Buffer
+//    resource range checking zero-fills every out-of-range element, so ragged
+//    M / N / K edges need no scalar tail.  One workgroup per CU.
+//  * gemm128 (small / skinny shapes that cannot fill 256 CUs with 256^2 tiles):
+//    128x128 tile, 4 waves (64x64 each), register-staged double buffer.
+//
+// Common to both (cdna_hip_programming.md §5, T1, T2, T10):
 //   * MFMA roles swapped (MFMA-A <- our B tile, MFMA-B <- our A tile) so each lane
-//     ends up owning 4 consecutive output columns: bf16 epilogue stores are 8 B,
-//     fp32 are 16 B, and a bias/activation needs 4 contiguous bias values.
-//   * k-contiguous operands are staged as [128 rows][64 k] with a 16-B chunk XOR
+//     owns 4 consecutive output columns: bf16 epilogue stores are 8 B, fp32 16 B,
+//     and a bias/activation needs 4 contiguous bias values.
+//   * k-contiguous operands live in LDS as [rows][64 k] with a 16-B chunk XOR
 //     swizzle (chunk ^ (row & 7)) -> conflict-free ds_read_b128 fragment reads.
-//   * k-strided operands are staged as [k/8][rows/16][8][16] 256-B blocks and
-//     read with ds_read_b64_tr_b16 (hardware transpose); odd k-blocks store
-//     k-rows 0-3 <-> 4-7 swapped so the two 16-lane groups of a half-wave read
-//     opposite 128-B halves of the bank row (conflict-free).
-//   * Register-staged double-buffered LDS: issue tile t+1's global loads before
-//     computing tile t, write them to the other LDS buffer after, one barrier
-//     per K-step (T3 minimum / T14).  All LDS in ONE __shared__ array.
+//   * k-strided operands live in LDS as [k/8][rows/16][8][16] 256-B blocks read
+//     with ds_read_b64_tr_b16 (hardware transpose); odd k-blocks store k-rows
+//     0-3 <-> 4-7 swapped so the two 16-lane groups of a half-wave hit opposite
+//     128-B halves of the bank row.
+//   * With LDS-DMA the LDS image is lane-linear per wave instruction, so the
+//     swizzle is applied on the per-lane SOURCE address (rule 21).
 //   * XCD-aware bijective block remap + grouped tile order for L2 reuse.
 //
 // Epilogues fuse what the reference runs as separate ATen kernels
@@ -41,66 +51,46 @@ namespace ldnn {
 
 namespace {
 
-constexpr int BM = 128, BN = 128, BK = 64;
-constexpr int kThreads = 256;
-constexpr int kTileBytes = 128 * BK * 2;  // 16 KiB per operand tile
+constexpr int BK = 64;
 constexpr int GROUP_M = 8;
 
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+typedef __attribute__((address_space(3))) void lds_void;
 
-// ---- staging: global -> registers -------------------------------------------
-// 1024 16-B chunks per operand tile, 4 per thread.
-template <bool KC>
-__device__ __forceinline__ void load_tile(u32x4 (&r)[4], const bf16_t* __restrict__ X, int ld, int rows,
-                                          int K, int r0, int k0, int tid) {
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int c = tid + kThreads * i;
-    int row, k;
-    if constexpr (KC) {
-      k = (c & 7) * 8;
-      row = c >> 3;
-    } else {
-      const int half = c & 1, klo = (c >> 1) & 3, rb = (c >> 3) & 7, khi = c >> 6;
-      k = khi * 4 + klo;
-      row = rb * 16 + half * 8;
-    }
-    const int gr = r0 + row, gk = k0 + k;
-    const bool ok = (gr < rows) && (gk < K);
-    const bf16_t* p = KC ? (X + (size_t)gr * ld + gk) : (X + (size_t)gk * ld + gr);
-    if (ok) {
-      r[i] = *reinterpret_cast<const u32x4*>(p);
-    } else {
-      r[i] = u32x4{0u, 0u, 0u, 0u};
-    }
+// ---- LDS image addressing --------------------------------------------------
+// KC image:      [ROWS][64 k], 128-B rows, chunk' = chunk ^ (row & 7)
+// strided image: [8 kb][ROWS/16 rb][8 k][16 r], 256-B blocks, odd kb: k ^= 4
+template <bool KC, int ROWS>
+__device__ __forceinline__ int lds_offset(int row, int k) {
+  if constexpr (KC) {
+    return row * 128 + ((((k >> 3) ^ (row & 7))) << 4) + (k & 7) * 2;
+  } else {
+    const int kb = k >> 3, rb = row >> 4;
+    const int rowp = (k & 7) ^ ((kb & 1) << 2);
+    return (kb * (ROWS / 16) + rb) * 256 + rowp * 32 + (row & 15) * 2;
   }
 }
 
-// ---- staging: registers -> LDS image --------------------------------------
-template <bool KC>
-__device__ __forceinline__ void store_tile(const u32x4 (&r)[4], char* lds, int tid) {
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int c = tid + kThreads * i;
-    int off;
-    if constexpr (KC) {
-      const int kc = c & 7, row = c >> 3;
-      off = row * 128 + ((kc ^ (row & 7)) << 4);
-    } else {
-      const int half = c & 1, klo = (c >> 1) & 3, rb = (c >> 3) & 7, khi = c >> 6;
-      const int k = khi * 4 + klo;
-      const int kb = k >> 3;
-      const int rowp = (k & 7) ^ ((kb & 1) << 2);
-      off = (kb * 8 + rb) * 256 + rowp * 32 + half * 16;
-    }
-    *reinterpret_cast<u32x4*>(lds + off) = r[i];
+// Inverse map: which (row, k) lands at 16-B LDS slot `o` (o multiple of 16).
+template <bool KC, int ROWS>
+__device__ __forceinline__ void lds_slot_to_rk(int o, int& row, int& k) {
+  if constexpr (KC) {
+    row = o >> 7;
+    const int pch = (o >> 4) & 7;
+    k = (pch ^ (row & 7)) * 8;
+  } else {
+    const int blk = o >> 8;
+    const int kb = blk / (ROWS / 16), rb = blk % (ROWS / 16);
+    const int rowp = (o >> 5) & 7, half = (o >> 4) & 1;
+    k = kb * 8 + (rowp ^ ((kb & 1) << 2));
+    row = rb * 16 + half * 8;
   }
 }
 
 // ---- fragment read: 16 rows (row tile rt) x 8 consecutive k (k-sub kk) ------
 // Lane l gets row (l & 15), k = kk*32 + 8*(l >> 4) + j, j = 0..7: the operand map
 // of v_mfma_f32_16x16x32_bf16 for both its A and its B operand.
-template <bool KC>
+template <bool KC, int ROWS>
 __device__ __forceinline__ bf16x8 read_frag(const char* lds, int rt, int kk, int lane) {
   if constexpr (KC) {
     const int row = rt * 16 + (lane & 15);
@@ -110,7 +100,7 @@ __device__ __forceinline__ bf16x8 read_frag(const char* lds, int rt, int kk, int
     const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
     const int kb = kk * 4 + g;
     const int sw = (kb & 1) << 2;
-    const char* blk = lds + (kb * 8 + rt) * 256;
+    const char* blk = lds + (kb * (ROWS / 16) + rt) * 256;
     const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(blk + ((q ^ sw) * 32) + p * 8));
     const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(blk + (((4 + q) ^ sw) * 32) + p * 8));
     return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
@@ -127,82 +117,33 @@ __device__ __forceinline__ float apply_epi(float v, float bias, float aux) {
   return v;
 }
 
-template <bool A_KC, bool B_KC, int EPI, bool OUT_F32>
-__global__ __launch_bounds__(kThreads, 2) void gemm_kernel(GemmParams p) {
-  __shared__ __attribute__((aligned(16))) char smem[4 * kTileBytes];  // [buf][A|B]
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wid = tid >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
-
-  // ---- tile id: XCD remap, then grouped ordering for L2 reuse
-  const int tiles_m = (p.M + BM - 1) / BM, tiles_n = (p.N + BN - 1) / BN;
+// Tile id -> (tm, tn): XCD remap, then GROUP_M-row groups for L2 reuse.
+__device__ __forceinline__ void tile_coords(int M, int N, int BMt, int BNt, int& m0, int& n0) {
+  const int tiles_m = (M + BMt - 1) / BMt, tiles_n = (N + BNt - 1) / BNt;
   const int nwg = tiles_m * tiles_n;
   const int id = xcd_remap(blockIdx.x, nwg);
   const int per_group = GROUP_M * tiles_n;
   const int group = id / per_group;
   const int first_m = group * GROUP_M;
   const int gsize = min(tiles_m - first_m, GROUP_M);
-  const int tm = first_m + (id % per_group) % gsize;
-  const int tn = (id % per_group) / gsize;
-  const int m0 = tm * BM, n0 = tn * BN;
+  m0 = (first_m + (id % per_group) % gsize) * BMt;
+  n0 = ((id % per_group) / gsize) * BNt;
+}
 
-  floatx4 acc[4][4];  // [n-tile j][m-tile i]
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) acc[j][i] = floatx4{0.f, 0.f, 0.f, 0.f};
-
-  const int nk = (p.K + BK - 1) / BK;
-  u32x4 ra[4], rb[4];
-  load_tile<A_KC>(ra, p.A, p.lda, p.M, p.K, m0, 0, tid);
-  load_tile<B_KC>(rb, p.B, p.ldb, p.N, p.K, n0, 0, tid);
-  store_tile<A_KC>(ra, smem, tid);
-  store_tile<B_KC>(rb, smem + kTileBytes, tid);
-  __syncthreads();
-
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    const bool more = (kt + 1) < nk;
-    if (more) {
-      load_tile<A_KC>(ra, p.A, p.lda, p.M, p.K, m0, (kt + 1) * BK, tid);
-      load_tile<B_KC>(rb, p.B, p.ldb, p.N, p.K, n0, (kt + 1) * BK, tid);
-    }
-    const char* la = smem + cur * 2 * kTileBytes;
-    const char* lb = la + kTileBytes;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      bf16x8 fa[4], fb[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) fa[i] = read_frag<A_KC>(la, wm * 4 + i, kk, lane);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) fb[j] = read_frag<B_KC>(lb, wn * 4 + j, kk, lane);
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[j][i], 0, 0, 0);
-    }
-    if (more) {
-      char* nb = smem + (cur ^ 1) * 2 * kTileBytes;
-      store_tile<A_KC>(ra, nb, tid);
-      store_tile<B_KC>(rb, nb + kTileBytes, tid);
-    }
-    __syncthreads();
-  }
-
-  // ---- epilogue: lane owns C[m][n..n+3] for each (i, j)
+// ---- shared epilogue: acc[j][i] is the 16x16 tile (n-tile j, m-tile i) -----
+template <int EPI, bool OUT_F32, int MT, int NT>
+__device__ __forceinline__ void epilogue(const GemmParams& p, floatx4 (&acc)[NT][MT], int mbase, int nbase,
+                                         int lane) {
   const bool do_dbias = p.dbias != nullptr;
-  float colsum[4][4];
+  float colsum[NT][4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
+  for (int j = 0; j < NT; ++j)
 #pragma unroll
     for (int r = 0; r < 4; ++r) colsum[j][r] = 0.f;
 
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int n = n0 + wn * 64 + j * 16 + 4 * (lane >> 4);
+  for (int j = 0; j < NT; ++j) {
+    const int n = nbase + j * 16 + 4 * (lane >> 4);
     const bool nok = n < p.N;  // N % 8 == 0 is enforced on the host
     float bias[4] = {0.f, 0.f, 0.f, 0.f};
     if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_RELU || EPI == EPI_BIAS_SIGMOID) {
@@ -212,8 +153,8 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(GemmParams p) {
       }
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int m = m0 + wm * 64 + i * 16 + (lane & 15);
+    for (int i = 0; i < MT; ++i) {
+      const int m = mbase + i * 16 + (lane & 15);
       if (!(nok && m < p.M)) continue;
       float aux[4] = {0.f, 0.f, 0.f, 0.f};
       if constexpr (EPI == EPI_DRELU || EPI == EPI_DSIGMOID) {
@@ -247,7 +188,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(GemmParams p) {
   if (do_dbias) {
     // reduce over the 16 lanes that share (lane >> 4), i.e. over m
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < NT; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         float s = colsum[j][r];
@@ -259,8 +200,8 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(GemmParams p) {
       }
     if ((lane & 15) == 0) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int n = n0 + wn * 64 + j * 16 + 4 * (lane >> 4);
+      for (int j = 0; j < NT; ++j) {
+        const int n = nbase + j * 16 + 4 * (lane >> 4);
         if (n < p.N) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) atomicAdd(p.dbias + n + r, colsum[j][r]);
@@ -270,33 +211,308 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(GemmParams p) {
   }
 }
 
-template <bool A_KC, bool B_KC, bool OUT_F32>
-hipError_t dispatch_epi(const GemmParams& p, int epi, hipStream_t s) {
-  const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
-  dim3 grid(tiles), block(kThreads);
-  switch (epi) {
-    case EPI_NONE: gemm_kernel<A_KC, B_KC, EPI_NONE, OUT_F32><<<grid, block, 0, s>>>(p); break;
-    case EPI_BIAS: gemm_kernel<A_KC, B_KC, EPI_BIAS, OUT_F32><<<grid, block, 0, s>>>(p); break;
-    case EPI_BIAS_RELU: gemm_kernel<A_KC, B_KC, EPI_BIAS_RELU, OUT_F32><<<grid, block, 0, s>>>(p); break;
-    case EPI_BIAS_SIGMOID: gemm_kernel<A_KC, B_KC, EPI_BIAS_SIGMOID, OUT_F32><<<grid, block, 0, s>>>(p); break;
-    case EPI_DRELU: gemm_kernel<A_KC, B_KC, EPI_DRELU, OUT_F32><<<grid, block, 0, s>>>(p); break;
-    case EPI_DSIGMOID: gemm_kernel<A_KC, B_KC, EPI_DSIGMOID, OUT_F32><<<grid, block, 0, s>>>(p); break;
-    default: return hipErrorInvalidValue;
+// =============================================================================
+// gemm128: register-staged, 128x128x64, 4 waves
+// =============================================================================
+namespace k128 {
+
+constexpr int BM = 128, BN = 128;
+constexpr int kThreads = 256;
+constexpr int kTileBytes = 128 * BK * 2;  // 16 KiB per operand tile
+
+// 1024 16-B chunks per operand tile, 4 per thread.
+template <bool KC>
+__device__ __forceinline__ void load_tile(u32x4 (&r)[4], const bf16_t* __restrict__ X, int ld, int rows,
+                                          int K, int r0, int k0, int tid) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = tid + kThreads * i;
+    int row, k;
+    if constexpr (KC) {
+      k = (c & 7) * 8;
+      row = c >> 3;
+    } else {
+      // lanes 0..7 of a write group cover 4 k-rows x 2 halves -> conflict-free ds_write_b128,
+      // and a wave reads 4 k-rows x 256 B of global memory
+      const int half = c & 1, klo = (c >> 1) & 3, rb = (c >> 3) & 7, khi = c >> 6;
+      k = khi * 4 + klo;
+      row = rb * 16 + half * 8;
+    }
+    const int gr = r0 + row, gk = k0 + k;
+    const bool ok = (gr < rows) && (gk < K);
+    const bf16_t* p = KC ? (X + (size_t)gr * ld + gk) : (X + (size_t)gk * ld + gr);
+    if (ok) {
+      r[i] = *reinterpret_cast<const u32x4*>(p);
+    } else {
+      r[i] = u32x4{0u, 0u, 0u, 0u};
+    }
   }
+}
+
+template <bool KC>
+__device__ __forceinline__ void store_tile(const u32x4 (&r)[4], char* lds, int tid) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = tid + kThreads * i;
+    int row, k;
+    if constexpr (KC) {
+      k = (c & 7) * 8;
+      row = c >> 3;
+    } else {
+      const int half = c & 1, klo = (c >> 1) & 3, rb = (c >> 3) & 7, khi = c >> 6;
+      k = khi * 4 + klo;
+      row = rb * 16 + half * 8;
+    }
+    *reinterpret_cast<u32x4*>(lds + lds_offset<KC, 128>(row, k)) = r[i];
+  }
+}
+
+template <bool A_KC, bool B_KC, int EPI, bool OUT_F32>
+__global__ __launch_bounds__(kThreads, 2) void gemm_kernel(GemmParams p) {
+  __shared__ __attribute__((aligned(16))) char smem[4 * kTileBytes];  // [buf][A|B]
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  int m0, n0;
+  tile_coords(p.M, p.N, BM, BN, m0, n0);
+
+  floatx4 acc[4][4];  // [n-tile j][m-tile i]
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[j][i] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (p.K + BK - 1) / BK;
+  u32x4 ra[4], rb[4];
+  load_tile<A_KC>(ra, p.A, p.lda, p.M, p.K, m0, 0, tid);
+  load_tile<B_KC>(rb, p.B, p.ldb, p.N, p.K, n0, 0, tid);
+  store_tile<A_KC>(ra, smem, tid);
+  store_tile<B_KC>(rb, smem + kTileBytes, tid);
+  __syncthreads();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    const bool more = (kt + 1) < nk;
+    if (more) {
+      load_tile<A_KC>(ra, p.A, p.lda, p.M, p.K, m0, (kt + 1) * BK, tid);
+      load_tile<B_KC>(rb, p.B, p.ldb, p.N, p.K, n0, (kt + 1) * BK, tid);
+    }
+    const char* la = smem + cur * 2 * kTileBytes;
+    const char* lb = la + kTileBytes;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 fa[4], fb[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[i] = read_frag<A_KC, 128>(la, wm * 4 + i, kk, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j] = read_frag<B_KC, 128>(lb, wn * 4 + j, kk, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[j][i], 0, 0, 0);
+    }
+    if (more) {
+      char* nb = smem + (cur ^ 1) * 2 * kTileBytes;
+      store_tile<A_KC>(ra, nb, tid);
+      store_tile<B_KC>(rb, nb + kTileBytes, tid);
+    }
+    __syncthreads();
+  }
+  epilogue<EPI, OUT_F32, 4, 4>(p, acc, m0 + wm * 64, n0 + wn * 64, lane);
+}
+
+}  // namespace k128
+
+// =============================================================================
+// gemm256: LDS-DMA staged, 256x256x64, 8 waves, DMA of tile t+1 in flight
+// across the compute of tile t
+// =============================================================================
+namespace k256 {
+
+constexpr int BM = 256, BN = 256;
+constexpr int kThreads = 512;
+constexpr int kTileBytes = 256 * BK * 2;       // 32 KiB per operand tile
+constexpr int kStageBytes = 2 * kTileBytes;    // A + B
+constexpr int kPiecesPerWave = kTileBytes / 1024 / 8;  // 1-KiB DMA pieces per wave per operand = 4
+constexpr uint32_t kOOB = 0x80000000u;         // any offset >= num_records reads as zero
+
+struct Operand {
+  __amdgpu_buffer_rsrc_t rsrc;
+  int ld, rows, K, r0;
+  int row[kPiecesPerWave];  // tile-relative row of this lane's slot in each piece
+  int k[kPiecesPerWave];    // tile-relative k
+};
+
+template <bool KC>
+__device__ __forceinline__ void init_operand(Operand& op, const bf16_t* X, int ld, int rows, int K, int r0,
+                                             int wid, int lane) {
+  const uint32_t bytes = KC ? (uint32_t)((size_t)rows * ld * 2) : (uint32_t)((size_t)K * ld * 2);
+  op.rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)X, (short)0, (int)bytes, 0x00020000);
+  op.ld = ld;
+  op.rows = rows;
+  op.K = K;
+  op.r0 = r0;
+#pragma unroll
+  for (int i = 0; i < kPiecesPerWave; ++i) {
+    const int piece = i * 8 + wid;
+    lds_slot_to_rk<KC, BM>(piece * 1024 + lane * 16, op.row[i], op.k[i]);
+  }
+}
+
+// Issue the DMA of one operand tile (k0) into LDS at `dst`: 4 x buffer_load_dwordx4 ... lds per lane.
+template <bool KC>
+__device__ __forceinline__ void issue_tile(const Operand& op, char* dst, int k0, int wid, int lane) {
+#pragma unroll
+  for (int i = 0; i < kPiecesPerWave; ++i) {
+    const int gr = op.r0 + op.row[i], gk = k0 + op.k[i];
+    const bool ok = (gr < op.rows) && (gk < op.K);
+    const uint32_t off = KC ? (uint32_t)(((size_t)gr * op.ld + gk) * 2) : (uint32_t)(((size_t)gk * op.ld + gr) * 2);
+    char* piece = dst + (i * 8 + wid) * 1024;  // wave-uniform LDS base (M0); lanes land at +16*lane
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(op.rsrc, (lds_void*)piece, 16, ok ? off : kOOB, 0, 0, 0);
+  }
+}
+
+__device__ __forceinline__ void barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <bool A_KC, bool B_KC, int EPI, bool OUT_F32>
+__global__ __launch_bounds__(kThreads, 2) void gemm_kernel(GemmParams p) {
+  __shared__ __attribute__((aligned(1024))) char smem[2 * kStageBytes];  // [stage][A|B], 128 KiB
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 2, wn = wid & 3;
+  int m0, n0;
+  tile_coords(p.M, p.N, BM, BN, m0, n0);
+
+  Operand oa, ob;
+  init_operand<A_KC>(oa, p.A, p.lda, p.M, p.K, m0, wid, lane);
+  init_operand<B_KC>(ob, p.B, p.ldb, p.N, p.K, n0, wid, lane);
+
+  floatx4 acc[4][8];  // [n-tile j][m-tile i]
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[j][i] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (p.K + BK - 1) / BK;
+  issue_tile<A_KC>(oa, smem, 0, wid, lane);
+  issue_tile<B_KC>(ob, smem + kTileBytes, 0, wid, lane);
+  if (nk > 1) {
+    issue_tile<A_KC>(oa, smem + kStageBytes, BK, wid, lane);
+    issue_tile<B_KC>(ob, smem + kStageBytes + kTileBytes, BK, wid, lane);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // tile 0 landed (tile 1 in flight)
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  barrier();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    char* stage = smem + (kt & 1) * kStageBytes;
+    const char* la = stage;
+    const char* lb = stage + kTileBytes;
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 fb[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j] = read_frag<B_KC, BN>(lb, wn * 4 + j, kk, lane);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        bf16x8 fa[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fa[i] = read_frag<A_KC, BM>(la, wm * 8 + h * 4 + i, kk, lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            acc[j][h * 4 + i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[j][h * 4 + i], 0, 0, 0);
+      }
+    }
+    __builtin_amdgcn_s_setprio(0);
+    barrier();  // every wave is done reading this stage
+    if (kt + 2 < nk) {
+      issue_tile<A_KC>(oa, stage, (kt + 2) * BK, wid, lane);
+      issue_tile<B_KC>(ob, stage + kTileBytes, (kt + 2) * BK, wid, lane);
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // tile kt+1 landed, kt+2 in flight
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    barrier();  // tile kt+1 visible to every wave
+  }
+  epilogue<EPI, OUT_F32, 8, 4>(p, acc, m0 + wm * 128, n0 + wn * 64, lane);
+}
+
+}  // namespace k256
+
+template <int TILE, bool A_KC, bool B_KC, bool OUT_F32>
+hipError_t dispatch_epi(const GemmParams& p, int epi, hipStream_t s) {
+  const int tiles = ((p.M + TILE - 1) / TILE) * ((p.N + TILE - 1) / TILE);
+  dim3 grid(tiles);
+#define LDNN_GEMM_CASE(E)                                                                          \
+  case E:                                                                                          \
+    if constexpr (TILE == 256)                                                                     \
+      k256::gemm_kernel<A_KC, B_KC, E, OUT_F32><<<grid, dim3(k256::kThreads), 0, s>>>(p);         \
+    else                                                                                           \
+      k128::gemm_kernel<A_KC, B_KC, E, OUT_F32><<<grid, dim3(k128::kThreads), 0, s>>>(p);         \
+    break;
+  switch (epi) {
+    LDNN_GEMM_CASE(EPI_NONE)
+    LDNN_GEMM_CASE(EPI_BIAS)
+    LDNN_GEMM_CASE(EPI_BIAS_RELU)
+    LDNN_GEMM_CASE(EPI_BIAS_SIGMOID)
+    LDNN_GEMM_CASE(EPI_DRELU)
+    LDNN_GEMM_CASE(EPI_DSIGMOID)
+    default:
+      return hipErrorInvalidValue;
+  }
+#undef LDNN_GEMM_CASE
   return hipGetLastError();
+}
+
+template <int TILE>
+hipError_t dispatch_layout(const GemmParams& p, bool a_kc, bool b_kc, int epi, bool f32, hipStream_t s) {
+  if (a_kc) {
+    if (b_kc) return f32 ? dispatch_epi<TILE, true, true, true>(p, epi, s) : dispatch_epi<TILE, true, true, false>(p, epi, s);
+    return f32 ? dispatch_epi<TILE, true, false, true>(p, epi, s) : dispatch_epi<TILE, true, false, false>(p, epi, s);
+  }
+  if (b_kc) return f32 ? dispatch_epi<TILE, false, true, true>(p, epi, s) : dispatch_epi<TILE, false, true, false>(p, epi, s);
+  return f32 ? dispatch_epi<TILE, false, false, true>(p, epi, s) : dispatch_epi<TILE, false, false, false>(p, epi, s);
 }
 
 }  // namespace
 
+int gemm_pick_tile(int M, int N, int K) {
+  const int t256 = ((M + 255) / 256) * ((N + 255) / 256);
+  // a 256^2 tile needs the grid to cover most of the 256 CUs and a K loop long
+  // enough to amortise its 2-tile prologue
+  if (t256 >= 192 && K >= 256) return 256;
+  return 128;
+}
+
 hipError_t gemm_bf16(const GemmParams& p, bool a_kcontig, bool b_kcontig, int epi, bool out_f32,
                      hipStream_t s) {
+  return gemm_bf16_tile(p, a_kcontig, b_kcontig, epi, out_f32, gemm_pick_tile(p.M, p.N, p.K), s);
+}
+
+hipError_t gemm_bf16_tile(const GemmParams& p, bool a_kcontig, bool b_kcontig, int epi, bool out_f32, int tile,
+                          hipStream_t s) {
   if (p.M <= 0 || p.N <= 0) return hipSuccess;
-  if (a_kcontig) {
-    if (b_kcontig) return out_f32 ? dispatch_epi<true, true, true>(p, epi, s) : dispatch_epi<true, true, false>(p, epi, s);
-    return out_f32 ? dispatch_epi<true, false, true>(p, epi, s) : dispatch_epi<true, false, false>(p, epi, s);
+  if (tile == 256) {
+    // buffer resources address at most 2 GiB per operand
+    const size_t abytes = (size_t)(a_kcontig ? p.M : p.K) * p.lda * 2;
+    const size_t bbytes = (size_t)(b_kcontig ? p.N : p.K) * p.ldb * 2;
+    if (abytes >= kOOBLimit || bbytes >= kOOBLimit) tile = 128;
   }
-  if (b_kcontig) return out_f32 ? dispatch_epi<false, true, true>(p, epi, s) : dispatch_epi<false, true, false>(p, epi, s);
-  return out_f32 ? dispatch_epi<false, false, true>(p, epi, s) : dispatch_epi<false, false, false>(p, epi, s);
+  if (tile == 256) return dispatch_layout<256>(p, a_kcontig, b_kcontig, epi, out_f32, s);
+  return dispatch_layout<128>(p, a_kcontig, b_kcontig, epi, out_f32, s);
 }
 
 }  // namespace ldnn

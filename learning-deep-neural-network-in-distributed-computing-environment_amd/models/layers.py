@@ -1,0 +1,52 @@
+"""Layer modules whose forward/backward run on the native gfx950 kernels.
+
+They subclass the stock ``torch.nn`` layers, so parameter names, shapes,
+``state_dict`` keys and init hooks are exactly those of the reference
+(BAR/model.py uses nn.Conv2d / nn.BatchNorm2d / nn.Linear / nn.ReLU); only the
+compute path changes.  A layer is bound to the model's FlatParams (bf16
+shadow + flat gradient buffer) by ``ldnn.prepare`` / ``FlatParams(model)``.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from ..ops import functional as LF
+
+
+class Linear(nn.Linear):
+    """nn.Linear with an optional fused activation epilogue ('none'|'relu'|'sigmoid')."""
+
+    def __init__(self, in_features, out_features, bias=True, activation: str = "none", device=None, dtype=None):
+        super().__init__(in_features, out_features, bias=bias, device=device, dtype=dtype)
+        assert activation in LF.ACTS
+        self.activation = activation
+        self._ldnn_flat = None
+
+    def forward(self, x):
+        return LF.linear_act(x, self.weight, self.bias, self.activation, self._ldnn_flat)
+
+    def extra_repr(self):
+        return super().extra_repr() + f", activation={self.activation}"
+
+
+class ReLU(nn.ReLU):
+    def forward(self, x):
+        return LF.relu(x)
+
+
+class Sigmoid(nn.Sigmoid):
+    def forward(self, x):
+        return LF.sigmoid(x)
+
+
+class Flatten(nn.Flatten):
+    pass
+
+
+class CrossEntropyLoss(nn.CrossEntropyLoss):
+    """Mean cross-entropy (the reference's criterion, BAR/main.py:52) on the fused
+    softmax-xent kernel.  Pass ``stats`` to accumulate loss-sum / #correct on device."""
+
+    def forward(self, logits, labels, stats=None):
+        return LF.cross_entropy(logits, labels, stats)

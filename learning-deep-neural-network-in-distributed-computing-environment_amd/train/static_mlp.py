@@ -1,0 +1,243 @@
+"""Static, graph-captured data-parallel training step for MLPs (the flagship path).
+
+The reference's hot loop (BAR/trainer.py:194-223: zero_grad, forward, CE loss,
+backward, optimizer.step, three .item() syncs per step) becomes a fixed
+schedule of native gfx950 kernels over pre-allocated buffers:
+
+  forward   L x  GEMM + fused bias/activation epilogue          (gemm.hip)
+  loss      1 x  fused softmax-xent fwd+bwd+argmax+bias-grad    (xent.hip)
+  backward  per layer, WGRAD FIRST: dW_l = dZ_l^T h_{l-1} (fp32, straight into
+            the flat grad buffer), then dgrad dZ_{l-1} = (dZ_l W_l) * act'(h_{l-1})
+            with the previous layer's bias gradient summed in the same epilogue
+  comm      gradient buckets all-reduced on RCCL as soon as their wgrads are
+            done -- wgrad-first ordering puts the largest layer's gradient on
+            the wire while the remaining dgrad/wgrad GEMMs still run
+  optimizer one fused SGD-momentum / Adam launch per bucket, right after that
+            bucket's all-reduce lands (overlaps the next bucket's transfer);
+            it also refreshes the bf16 weight shadow the GEMMs read
+
+Every stretch of kernels between two collective calls is captured once into a
+hipGraph (torch.cuda.CUDAGraph) and replayed, so a step costs a handful of
+host calls.  Loss and accuracy accumulate on the device; nothing syncs.
+
+Bucket sizing for xGMI: each MI355X has 7 links (~153 GB/s each);
+RCCL spreads a large all-reduce over many channels/links, so buckets are a few
+large contiguous ranges (default >= 8 M fp32 elements) rather than 65 per-tensor
+messages (BAR/communication.py:4-31).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+from ..ops import _ext
+from ..utils.flat_params import FlatParams
+
+
+@dataclass
+class OptimConfig:
+    name: str = "sgd"          # "sgd" | "adam" | "adamw"
+    lr: float = 0.01
+    momentum: float = 0.9
+    dampening: float = 0.0
+    weight_decay: float = 0.0
+    nesterov: bool = False
+    betas: tuple = (0.9, 0.999)
+    eps: float = 1e-8
+
+
+class _Segment:
+    """A stretch of kernel launches replayed from a captured hipGraph after warmup."""
+
+    def __init__(self, fn, use_graph: bool, warmup: int = 2):
+        self.fn, self.use_graph, self.warmup = fn, use_graph, warmup
+        self.calls = 0
+        self.graph = None
+
+    def __call__(self):
+        if not self.use_graph or self.calls < self.warmup:
+            self.calls += 1
+            self.fn()
+            return
+        if self.graph is None:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self.fn()
+            self.graph = g
+        self.graph.replay()
+
+
+class StaticMLPEngine:
+    def __init__(self, model, batch_size: int, optim: OptimConfig | None = None, *, device=None,
+                 process_group=None, world_size: int | None = None, bucket_cap_elems: int = 8 << 20,
+                 use_graphs: bool = True, average_grads: bool = True):
+        from ..models.mlp import MLP
+
+        if not isinstance(model, MLP):
+            raise TypeError("StaticMLPEngine drives ldnn.models.mlp.MLP models")
+        self.device = torch.device(device or "cuda")
+        if not _ext.use_native(torch.empty(0, device=self.device)):
+            raise RuntimeError("StaticMLPEngine needs the native extension on a GPU")
+        self.C = _ext.C()
+        self.model = model.to(self.device)
+        self.B = int(batch_size)
+        self.optim = optim or OptimConfig()
+        self.pg = process_group
+        if world_size is None:
+            world_size = dist.get_world_size(process_group) if dist.is_available() and dist.is_initialized() else 1
+        self.world = world_size
+        self.use_graphs = use_graphs
+        self.layers = list(model.layers)
+        L = len(self.layers)
+        acts = {"none": None, "relu": self.C.EPI_BIAS_RELU, "sigmoid": self.C.EPI_BIAS_SIGMOID}
+        self._fwd_epi = [acts[l.activation] if acts[l.activation] is not None else self.C.EPI_BIAS for l in self.layers]
+        dacts = {"relu": self.C.EPI_DRELU, "sigmoid": self.C.EPI_DSIGMOID, "none": self.C.EPI_NONE}
+        # dgrad of layer l multiplies by the derivative of layer l-1's activation
+        self._dgrad_epi = [None] + [dacts[self.layers[l - 1].activation] for l in range(1, L)]
+        for l in range(L - 1):
+            if self.layers[l].out_features % 8:
+                raise ValueError("hidden widths must be multiples of 8")
+        if self.layers[0].in_features % 8:
+            raise ValueError("input features must be a multiple of 8")
+
+        # flat layout = gradient-ready order: W_L .. W_1, then all biases (one zeroing memset)
+        order = [self.layers[l].weight for l in reversed(range(L))] + [l.bias for l in self.layers]
+        self.flat = FlatParams(model, self.device, order=order)
+        f = self.flat
+        self.W = [f.shadow_storage(l.weight) for l in self.layers]
+        self.bias = [f.master_storage(l.bias) for l in self.layers]
+        self.dW = [f.grad_storage(l.weight) for l in self.layers]
+        self.db = [f.grad_storage(l.bias) for l in self.layers]
+        self._bias_begin = f.seg(self.layers[0].bias).offset
+        npad = [w.shape[0] for w in self.W]
+        self.num_classes = self.layers[-1].out_features
+
+        B, dev, bf = self.B, self.device, torch.bfloat16
+        self.x = torch.zeros(B, self.layers[0].in_features, dtype=bf, device=dev)
+        self.labels = torch.zeros(B, dtype=torch.long, device=dev)
+        self.h = [self.x] + [torch.zeros(B, n, dtype=bf, device=dev) for n in npad]
+        self.dz = [None] + [torch.zeros(B, n, dtype=bf, device=dev) for n in npad]
+        self.stats = torch.zeros(2, dtype=torch.float32, device=dev)    # [loss_sum, correct]
+        self.hp = torch.tensor([self.optim.lr, 0.0], dtype=torch.float32, device=dev)
+        o = self.optim
+        self.mom = torch.zeros_like(f.master) if (o.name == "sgd" and o.momentum != 0) else None
+        if o.name in ("adam", "adamw"):
+            self.exp_avg = torch.zeros_like(f.master)
+            self.exp_avg_sq = torch.zeros_like(f.master)
+        self._grad_scale = 1.0 / self.world if average_grads else 1.0
+
+        # ---- bucket plan: close a bucket after wgrad_l once it holds >= cap elements
+        self.buckets: list[tuple[int, int, int]] = []   # (begin, end, trigger layer or -1 = end)
+        begin = 0
+        for l in reversed(range(L)):
+            seg = f.seg(self.layers[l].weight)
+            end = seg.offset + seg.storage_numel
+            if l > 0 and self.world > 1 and end - begin >= bucket_cap_elems:
+                self.buckets.append((begin, end, l))
+                begin = end
+        self.buckets.append((begin, f.numel, -1))
+        self._build_segments()
+
+    # ------------------------------------------------------------------ kernels
+    def _forward(self):
+        C = self.C
+        for l in range(len(self.layers)):
+            C.gemm(self.h[l], self.W[l], self.h[l + 1], True, True, self._fwd_epi[l], bias=self.bias[l])
+
+    def _loss(self):
+        L = len(self.layers)
+        logits = self.h[L][:, : self.num_classes]
+        self.C.softmax_xent(logits, self.labels, self.dz[L][:, : self.num_classes], self.stats,
+                            dbias=self.db[L - 1], num_classes=self.num_classes, grad_scale=1.0 / self.B)
+
+    def _wgrad(self, l):
+        self.C.gemm(self.dz[l + 1], self.h[l], self.dW[l], False, False)
+
+    def _dgrad(self, l):
+        # dz_l(prev layer output) = (dz_{l+1} W_l) * act'(h_l), bias grad of layer l-1 fused
+        self.C.gemm(self.dz[l + 1], self.W[l], self.dz[l], True, False, self._dgrad_epi[l], aux=self.h[l],
+                    dbias=self.db[l - 1])
+
+    def _opt(self, b, e):
+        f, o, C = self.flat, self.optim, self.C
+        p, g, sh = f.master[b:e], f.grad[b:e], f.shadow[b:e]
+        if o.name == "sgd":
+            mom = self.mom[b:e] if self.mom is not None else p
+            C.sgd_step(p, g, mom, sh, self.hp, self._grad_scale, o.momentum, o.dampening, o.weight_decay,
+                       o.nesterov, False)
+        else:
+            C.adam_step(p, g, self.exp_avg[b:e], self.exp_avg_sq[b:e], sh, self.hp, self._grad_scale,
+                        o.betas[0], o.betas[1], o.eps, o.weight_decay, o.name == "adamw")
+
+    # ------------------------------------------------------------ segmentation
+    def _build_segments(self):
+        L = len(self.layers)
+        # backward walk, cut after each bucket's trigger wgrad
+        triggers = {t: i for i, (_, _, t) in enumerate(self.buckets) if t >= 0}
+        pieces: list[list] = [[]]
+        pieces[0].append(lambda: self.flat.grad[self._bias_begin:].zero_())
+        if self.optim.name in ("adam", "adamw"):
+            pieces[0].append(lambda: self.C.bump_step(self.hp))
+        pieces[0].append(self._forward)
+        pieces[0].append(self._loss)
+        self._cut_buckets = []
+        for l in reversed(range(L)):
+            pieces[-1].append(lambda l=l: self._wgrad(l))
+            if l in triggers:
+                self._cut_buckets.append(triggers[l])
+                pieces.append([])
+            if l > 0:
+                pieces[-1].append(lambda l=l: self._dgrad(l))
+        self._cut_buckets.append(len(self.buckets) - 1)
+
+        def run(fns):
+            def f():
+                for fn in fns:
+                    fn()
+            return f
+
+        if self.world == 1:
+            fns = [fn for p in pieces for fn in p] + [lambda: self._opt(0, self.flat.numel)]
+            self.segments = [_Segment(run(fns), self.use_graphs)]
+            self.opt_segments = []
+        else:
+            self.segments = [_Segment(run(p), self.use_graphs) for p in pieces]
+            self.opt_segments = [_Segment(run([lambda b=b, e=e: self._opt(b, e)]), self.use_graphs)
+                                 for (b, e, _) in self.buckets]
+
+    # --------------------------------------------------------------------- API
+    def set_lr(self, lr: float):
+        self.hp[0].fill_(lr)
+
+    def load_batch(self, x: torch.Tensor, y: torch.Tensor):
+        self.x.copy_(x.reshape(self.B, -1))
+        self.labels.copy_(y)
+
+    def step(self):
+        """One full training step on the batch currently in (self.x, self.labels)."""
+        if self.world == 1:
+            self.segments[0]()
+            return
+        works = []
+        for i, seg in enumerate(self.segments):
+            seg()
+            b, e, _ = self.buckets[self._cut_buckets[i]]
+            works.append(dist.all_reduce(self.flat.grad[b:e], group=self.pg, async_op=True))
+        for w, oseg in zip(works, self.opt_segments):
+            w.wait()
+            oseg()
+
+    def reset_stats(self):
+        self.stats.zero_()
+
+    def read_stats(self, samples: int):
+        s = self.stats.tolist()
+        return s[0] / max(samples, 1), 100.0 * s[1] / max(samples, 1)
+
+    @torch.no_grad()
+    def predict_logits(self, x: torch.Tensor) -> torch.Tensor:
+        self.x.copy_(x.reshape(self.B, -1))
+        self._forward()
+        return self.h[-1][:, : self.num_classes]

@@ -1,0 +1,175 @@
+"""Flat parameter / gradient / bf16-shadow storage for a model.
+
+The reference keeps 65 separate parameter tensors and aggregates them with 65
+separate collectives (BAR/communication.py:4-31).  On MI355X
+that is the wrong shape: every collective and every optimizer launch has a
+fixed cost, and RCCL over xGMI wants few, large messages.  FlatParams moves a
+model's parameters into ONE contiguous fp32 master buffer (each
+``nn.Parameter`` becomes a view into it, so ``state_dict()`` keeps the
+reference key names such as ``prep.0.weight`` / ``fc.bias``), with
+
+* ``grad``   -- one fp32 gradient buffer; ``param.grad`` is a view into it,
+* ``shadow`` -- one bf16 copy of the weights that the MFMA kernels read
+  (refreshed by the fused optimizer in the same pass that updates the master),
+* per-parameter padded *storage* views: a parameter whose leading dim is not a
+  multiple of 8 (e.g. the 10-class classifier) gets zero rows of padding so the
+  GEMM never needs a scalar tail; the padding stays exactly zero because its
+  gradient is always zero.
+
+Segments are 64-element aligned (256 B fp32 / 128 B bf16) so every view is
+16-byte aligned for vector loads.  The order of segments is the order in which
+gradients become ready during backward (reverse of registration), which is
+what gradient bucketing wants.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+import torch.nn as nn
+
+_ALIGN = 64
+
+
+def _pad_rows(shape: torch.Size, multiple: int = 8) -> tuple:
+    if len(shape) == 0:
+        return tuple(shape)
+    rows = shape[0]
+    prow = (rows + multiple - 1) // multiple * multiple
+    return (prow,) + tuple(shape[1:])
+
+
+@dataclass
+class Segment:
+    name: str
+    param: nn.Parameter
+    offset: int        # element offset of the padded storage in the flat buffers
+    numel: int         # logical elements
+    storage_shape: tuple  # padded shape
+    storage_numel: int
+
+
+class FlatParams:
+    """Owns flat master/grad/shadow buffers for ``module``'s parameters."""
+
+    def __init__(self, module: nn.Module, device: torch.device | str | None = None, pad_rows: bool = True,
+                 shadow: bool | None = None, grad_ready_order: bool = True, order: list | None = None):
+        self.module = module
+        params = [(n, p) for n, p in module.named_parameters() if p.requires_grad]
+        if device is None:
+            device = params[0][1].device if params else torch.device("cpu")
+        self.device = torch.device(device)
+        if shadow is None:
+            shadow = self.device.type == "cuda"
+        if order is not None:  # explicit layout (e.g. a static engine's bucket plan)
+            names = {id(p): n for n, p in params}
+            ordered = [(names[id(p)], p) for p in order]
+            assert len(ordered) == len(params), "order must list every trainable parameter once"
+        else:
+            ordered = list(reversed(params)) if grad_ready_order else params
+        segs = []
+        off = 0
+        for name, p in ordered:
+            sshape = _pad_rows(p.shape) if (pad_rows and p.dim() >= 1) else tuple(p.shape)
+            snumel = 1
+            for d in sshape:
+                snumel *= d
+            segs.append(Segment(name, p, off, p.numel(), sshape, snumel))
+            off += (snumel + _ALIGN - 1) // _ALIGN * _ALIGN
+        self.numel = off
+        self.segments = segs
+        self.by_param = {id(s.param): s for s in segs}
+        self.master = torch.zeros(off, dtype=torch.float32, device=self.device)
+        self.grad = torch.zeros(off, dtype=torch.float32, device=self.device)
+        self.shadow = torch.zeros(off, dtype=torch.bfloat16, device=self.device) if shadow else None
+        with torch.no_grad():
+            for s in segs:
+                st = self.storage_view(s, self.master)
+                st.zero_()
+                self._logical(s, st).copy_(s.param.detach().to(self.device, torch.float32))
+                s.param.data = self._logical(s, st)
+                s.param.grad = self._logical(s, self.storage_view(s, self.grad))
+        # gradient-readiness notification: native ops call notify() after writing a
+        # weight gradient; params handled by stock torch ops signal through autograd.
+        self._ready_hooks: list = []
+        for s in segs:
+            s.param.register_post_accumulate_grad_hook(lambda p: self.notify(p))
+        for m in module.modules():
+            if hasattr(m, "_ldnn_flat"):
+                m._ldnn_flat = self
+        self.refresh_shadow()
+
+    def add_ready_hook(self, fn):
+        self._ready_hooks.append(fn)
+
+    def notify(self, *params):
+        for p in params:
+            if p is None:
+                continue
+            for fn in self._ready_hooks:
+                fn(p)
+
+    # ---- views ---------------------------------------------------------------
+    @staticmethod
+    def storage_view(seg: Segment, flat: torch.Tensor) -> torch.Tensor:
+        return flat[seg.offset: seg.offset + seg.storage_numel].view(seg.storage_shape)
+
+    @staticmethod
+    def _logical(seg: Segment, storage: torch.Tensor) -> torch.Tensor:
+        shape = tuple(seg.param.shape)
+        if len(shape) == 0:
+            return storage
+        return storage[: shape[0]]
+
+    def seg(self, p: nn.Parameter) -> Segment:
+        return self.by_param[id(p)]
+
+    def master_storage(self, p):
+        return self.storage_view(self.seg(p), self.master)
+
+    def grad_storage(self, p):
+        return self.storage_view(self.seg(p), self.grad)
+
+    def shadow_storage(self, p):
+        if self.shadow is None:
+            raise RuntimeError("FlatParams was built without a bf16 shadow")
+        return self.storage_view(self.seg(p), self.shadow)
+
+    def params(self):
+        return [s.param for s in self.segments]
+
+    # ---- maintenance --------------------------------------------------------
+    @torch.no_grad()
+    def refresh_shadow(self):
+        """Re-derive the bf16 shadow after the master changed outside the optimizer
+        (initial broadcast, load_state_dict, weight averaging without fused mix)."""
+        if self.shadow is None:
+            return
+        from ..ops import _ext
+
+        if _ext.use_native(self.master):
+            _ext.C().cast_f32_bf16(self.master, self.shadow)
+        else:
+            self.shadow.copy_(self.master)
+
+    @torch.no_grad()
+    def zero_grad(self):
+        self.grad.zero_()
+
+    def reattach_grads(self):
+        """Point every ``param.grad`` back at its flat view (after user code set it to None)."""
+        for s in self.segments:
+            if s.param.grad is None or s.param.grad.data_ptr() != self._logical(s, self.storage_view(s, self.grad)).data_ptr():
+                s.param.grad = self._logical(s, self.storage_view(s, self.grad))
+
+    def ranges(self, params) -> list[tuple[int, int]]:
+        """Merged [begin, end) element ranges of the given parameters' storage."""
+        rs = sorted((self.seg(p).offset, self.seg(p).offset + self.seg(p).storage_numel) for p in params)
+        merged: list[list[int]] = []
+        for b, e in rs:
+            e = (e + _ALIGN - 1) // _ALIGN * _ALIGN
+            if merged and b <= merged[-1][1]:
+                merged[-1][1] = max(merged[-1][1], e)
+            else:
+                merged.append([b, e])
+        return [(b, min(e, self.numel)) for b, e in merged]

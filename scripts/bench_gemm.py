@@ -42,11 +42,13 @@ def main():
         c = torch.empty(M, N, device="cuda", dtype=torch.bfloat16 if akc else torch.float32)
         A = a if akc else a.t()
         B = b.t() if bkc else b
-        t_ours = timeit(lambda: C.gemm(a, b, c, akc, bkc))
-        t_ref = timeit(lambda: torch.matmul(A, B))
         fl = 2.0 * M * N * K
-        row = dict(shape=name, M=M, N=N, K=K, ours_ms=round(t_ours, 4), ours_tflops=round(fl / t_ours / 1e9, 1),
-                   torch_ms=round(t_ref, 4), torch_tflops=round(fl / t_ref / 1e9, 1))
+        row = dict(shape=name, M=M, N=N, K=K, auto_tile=C.gemm.__doc__ and None)
+        for tile in (128, 256):
+            t = min(timeit(lambda: C.gemm(a, b, c, akc, bkc, tile=tile)) for _ in range(3))
+            row[f"t{tile}_tflops"] = round(fl / t / 1e9, 1)
+        t_ref = min(timeit(lambda: torch.matmul(A, B)) for _ in range(3))
+        row["torch_tflops"] = round(fl / t_ref / 1e9, 1)
         print(json.dumps(row), flush=True)
         out.append(row)
     return out

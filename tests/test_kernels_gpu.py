@@ -19,43 +19,45 @@ def _ref_gemm(a, b, a_kc, b_kc):
     return A @ B
 
 
+@pytest.mark.parametrize("tile", [128, 256])
 @pytest.mark.parametrize("a_kc,b_kc", [(True, True), (True, False), (False, True), (False, False)])
-@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (200, 136, 784), (1000, 264, 72), (64, 16, 4096), (384, 512, 1000)])
-def test_gemm_layouts(a_kc, b_kc, M, N, K):
-    if (not a_kc or not b_kc) and K % 8 and (a_kc or b_kc):
-        pytest.skip("k-contiguous operand needs K % 8 == 0")
-    if not a_kc and M % 8:
-        pytest.skip("strided A needs M % 8 == 0")
+@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (200, 136, 784), (1000, 264, 72), (64, 16, 4096),
+                                   (384, 512, 1000), (520, 776, 520)])
+def test_gemm_layouts(tile, a_kc, b_kc, M, N, K):
     torch.manual_seed(0)
     dev = "cuda"
     a = (torch.randn(M, K, device=dev) if a_kc else torch.randn(K, M, device=dev)).bfloat16()
     b = (torch.randn(N, K, device=dev) if b_kc else torch.randn(K, N, device=dev)).bfloat16()
     c = torch.empty(M, N, device=dev, dtype=torch.float32)
-    C().gemm(a, b, c, a_kc, b_kc)
+    C().gemm(a, b, c, a_kc, b_kc, tile=tile)
     ref = _ref_gemm(a, b, a_kc, b_kc)
     torch.cuda.synchronize()
     err = (c - ref).abs().max().item()
     assert err <= 1e-3 * K ** 0.5 + 1e-3, err
     cb = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
-    C().gemm(a, b, cb, a_kc, b_kc)
+    C().gemm(a, b, cb, a_kc, b_kc, tile=tile)
     rel = ((cb.float() - ref).abs().max() / ref.abs().max()).item()
     assert rel < 1e-2, rel
 
 
-def test_gemm_asymmetric_identity():
+@pytest.mark.parametrize("tile", [128, 256])
+def test_gemm_asymmetric_identity(tile):
     """A = I with an asymmetric B catches a transposed C write."""
-    n = 128
+    n = 256
     a = torch.eye(n, device="cuda").bfloat16()
     b = torch.arange(n * n, device="cuda").reshape(n, n).float().remainder(97).bfloat16()
     c = torch.empty(n, n, device="cuda")
-    C().gemm(a, b, c, True, True)  # C = I @ b^T
+    C().gemm(a, b, c, True, True, tile=tile)  # C = I @ b^T
     assert torch.equal(c, b.float().t())
-    C().gemm(a, b, c, True, False)  # C = I @ b
+    C().gemm(a, b, c, True, False, tile=tile)  # C = I @ b
+    assert torch.equal(c, b.float())
+    C().gemm(a.t().contiguous(), b, c, False, False, tile=tile)  # C = I^T @ b
     assert torch.equal(c, b.float())
 
 
+@pytest.mark.parametrize("tile", [128, 256])
 @pytest.mark.parametrize("epi", ["bias", "relu", "sigmoid"])
-def test_gemm_fwd_epilogues(epi):
+def test_gemm_fwd_epilogues(epi, tile):
     torch.manual_seed(1)
     M, N, K = 300, 264, 784
     x = torch.randn(M, K, device="cuda").bfloat16()
@@ -63,7 +65,7 @@ def test_gemm_fwd_epilogues(epi):
     bias = torch.randn(N, device="cuda")
     y = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
     code = {"bias": C().EPI_BIAS, "relu": C().EPI_BIAS_RELU, "sigmoid": C().EPI_BIAS_SIGMOID}[epi]
-    C().gemm(x, w, y, True, True, code, bias=bias)
+    C().gemm(x, w, y, True, True, code, bias=bias, tile=tile)
     ref = x.float() @ w.float().t() + bias
     if epi == "relu":
         ref = ref.relu()
@@ -72,8 +74,9 @@ def test_gemm_fwd_epilogues(epi):
     torch.testing.assert_close(y.float(), ref, rtol=2e-2, atol=2e-2)
 
 
+@pytest.mark.parametrize("tile", [128, 256])
 @pytest.mark.parametrize("act", ["relu", "sigmoid"])
-def test_gemm_dgrad_epilogue_and_dbias(act):
+def test_gemm_dgrad_epilogue_and_dbias(act, tile):
     torch.manual_seed(2)
     M, N, K = 260, 136, 512  # dX[M,K] = dY[M,N] @ W[N,K]
     dy = torch.randn(M, N, device="cuda").bfloat16()
@@ -83,7 +86,7 @@ def test_gemm_dgrad_epilogue_and_dbias(act):
     dx = torch.empty(M, K, device="cuda", dtype=torch.bfloat16)
     db = torch.zeros(K, device="cuda")
     code = C().EPI_DRELU if act == "relu" else C().EPI_DSIGMOID
-    C().gemm(dy, w, dx, True, False, code, aux=yprev, dbias=db)
+    C().gemm(dy, w, dx, True, False, code, aux=yprev, dbias=db, tile=tile)
     g = dy.float() @ w.float()
     y = yprev.float()
     ref = g * (y > 0) if act == "relu" else g * y * (1 - y)
@@ -91,14 +94,15 @@ def test_gemm_dgrad_epilogue_and_dbias(act):
     torch.testing.assert_close(db, dx.float().sum(0), rtol=1e-3, atol=1e-2)
 
 
-def test_gemm_wgrad_beta_accumulate():
+@pytest.mark.parametrize("tile", [128, 256])
+def test_gemm_wgrad_beta_accumulate(tile):
     torch.manual_seed(3)
     B, N, K = 1000, 264, 784  # dW[N,K] = dY^T X
     dy = torch.randn(B, N, device="cuda").bfloat16()
     x = torch.randn(B, K, device="cuda").bfloat16()
     dw = torch.randn(N, K, device="cuda")
     base = dw.clone()
-    C().gemm(dy, x, dw, False, False, beta=1.0)
+    C().gemm(dy, x, dw, False, False, beta=1.0, tile=tile)
     ref = base + dy.float().t() @ x.float()
     torch.testing.assert_close(dw, ref, rtol=1e-4, atol=1e-2)
 
