@@ -131,81 +131,62 @@ __device__ __forceinline__ void tile_coords(int M, int N, int BMt, int BNt, int&
 }
 
 // ---- shared epilogue: acc[j][i] is the 16x16 tile (n-tile j, m-tile i) -----
+// Processed one n-tile at a time (sched_barrier keeps the compiler from hoisting
+// every bias/aux load of the tile up front), with the optional bias-gradient
+// column sum reduced and atomically added per n-tile, so only a handful of
+// registers are live beside the accumulators.
 template <int EPI, bool OUT_F32, int MT, int NT>
 __device__ __forceinline__ void epilogue(const GemmParams& p, floatx4 (&acc)[NT][MT], int mbase, int nbase,
                                          int lane) {
   const bool do_dbias = p.dbias != nullptr;
-  float colsum[NT][4];
-#pragma unroll
-  for (int j = 0; j < NT; ++j)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) colsum[j][r] = 0.f;
-
 #pragma unroll
   for (int j = 0; j < NT; ++j) {
+    __builtin_amdgcn_sched_barrier(0);
     const int n = nbase + j * 16 + 4 * (lane >> 4);
     const bool nok = n < p.N;  // N % 8 == 0 is enforced on the host
-    float bias[4] = {0.f, 0.f, 0.f, 0.f};
+    floatx4 bias = {0.f, 0.f, 0.f, 0.f};
     if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_RELU || EPI == EPI_BIAS_SIGMOID) {
-      if (nok) {
-        const floatx4 b4 = *reinterpret_cast<const floatx4*>(p.bias + n);
-        bias[0] = b4[0]; bias[1] = b4[1]; bias[2] = b4[2]; bias[3] = b4[3];
-      }
+      if (nok) bias = *reinterpret_cast<const floatx4*>(p.bias + n);
     }
+    floatx4 cs = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
       const int m = mbase + i * 16 + (lane & 15);
-      if (!(nok && m < p.M)) continue;
-      float aux[4] = {0.f, 0.f, 0.f, 0.f};
-      if constexpr (EPI == EPI_DRELU || EPI == EPI_DSIGMOID) {
-        const u16x4 a4 = *reinterpret_cast<const u16x4*>(p.aux + (size_t)m * p.ldaux + n);
-        aux[0] = bf2f(a4[0]); aux[1] = bf2f(a4[1]); aux[2] = bf2f(a4[2]); aux[3] = bf2f(a4[3]);
-      }
-      float v[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = apply_epi<EPI>(acc[j][i][r], bias[r], aux[r]);
-      if constexpr (OUT_F32) {
-        float* c = reinterpret_cast<float*>(p.C) + (size_t)m * p.ldc + n;
-        floatx4 o{v[0], v[1], v[2], v[3]};
-        if (p.beta != 0.f) {
-          const floatx4 old = *reinterpret_cast<const floatx4*>(c);
-          o = o + p.beta * old;
+      if (nok && m < p.M) {
+        floatx4 aux = {0.f, 0.f, 0.f, 0.f};
+        if constexpr (EPI == EPI_DRELU || EPI == EPI_DSIGMOID) {
+          const u16x4 a4 = *reinterpret_cast<const u16x4*>(p.aux + (size_t)m * p.ldaux + n);
+          aux = floatx4{bf2f(a4[0]), bf2f(a4[1]), bf2f(a4[2]), bf2f(a4[3])};
         }
-        *reinterpret_cast<floatx4*>(c) = o;
+        floatx4 v;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) colsum[j][r] += o[r];
-      } else {
-        u16x4 o;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = f2bf(v[r]);
-        *reinterpret_cast<u16x4*>(reinterpret_cast<bf16_t*>(p.C) + (size_t)m * p.ldc + n) = o;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) colsum[j][r] += bf2f(o[r]);
+        for (int r = 0; r < 4; ++r) v[r] = apply_epi<EPI>(acc[j][i][r], bias[r], aux[r]);
+        if constexpr (OUT_F32) {
+          float* c = reinterpret_cast<float*>(p.C) + (size_t)m * p.ldc + n;
+          if (p.beta != 0.f) v = v + p.beta * *reinterpret_cast<const floatx4*>(c);
+          *reinterpret_cast<floatx4*>(c) = v;
+          cs += v;
+        } else {
+          const u16x4 o{f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+          *reinterpret_cast<u16x4*>(reinterpret_cast<bf16_t*>(p.C) + (size_t)m * p.ldc + n) = o;
+          cs += floatx4{bf2f(o[0]), bf2f(o[1]), bf2f(o[2]), bf2f(o[3])};
+        }
       }
     }
-  }
-
-  if (do_dbias) {
-    // reduce over the 16 lanes that share (lane >> 4), i.e. over m
-#pragma unroll
-    for (int j = 0; j < NT; ++j)
+    if (do_dbias) {
+      // reduce over the 16 lanes that share (lane >> 4), i.e. over m
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        float s = colsum[j][r];
-        s += __shfl_xor(s, 1, 64);
-        s += __shfl_xor(s, 2, 64);
-        s += __shfl_xor(s, 4, 64);
-        s += __shfl_xor(s, 8, 64);
-        colsum[j][r] = s;
+        float t = cs[r];
+        t += __shfl_xor(t, 1, 64);
+        t += __shfl_xor(t, 2, 64);
+        t += __shfl_xor(t, 4, 64);
+        t += __shfl_xor(t, 8, 64);
+        cs[r] = t;
       }
-    if ((lane & 15) == 0) {
+      if ((lane & 15) == 0 && nok) {
 #pragma unroll
-      for (int j = 0; j < NT; ++j) {
-        const int n = nbase + j * 16 + 4 * (lane >> 4);
-        if (n < p.N) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) atomicAdd(p.dbias + n + r, colsum[j][r]);
-        }
+        for (int r = 0; r < 4; ++r) atomicAdd(p.dbias + n + r, cs[r]);
       }
     }
   }
@@ -405,17 +386,19 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(GemmParams p) {
   const int nk = (p.K + BK - 1) / BK;
   issue_tile<A_KC>(oa, smem, 0, wid, lane);
   issue_tile<B_KC>(ob, smem + kTileBytes, 0, wid, lane);
-  if (nk > 1) {
-    issue_tile<A_KC>(oa, smem + kStageBytes, BK, wid, lane);
-    issue_tile<B_KC>(ob, smem + kStageBytes + kTileBytes, BK, wid, lane);
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // tile 0 landed (tile 1 in flight)
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  barrier();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
+  // One barrier per K-tile: it publishes tile kt (every wave waited for its own
+  // DMA of kt) AND certifies that every wave finished reading stage (kt+1)&1
+  // (tile kt-1), which is then refilled with tile kt+1 while kt is multiplied.
   for (int kt = 0; kt < nk; ++kt) {
     char* stage = smem + (kt & 1) * kStageBytes;
+    barrier();
+    if (kt + 1 < nk) {
+      char* nxt = smem + ((kt + 1) & 1) * kStageBytes;
+      issue_tile<A_KC>(oa, nxt, (kt + 1) * BK, wid, lane);
+      issue_tile<B_KC>(ob, nxt + kTileBytes, (kt + 1) * BK, wid, lane);
+    }
     const char* la = stage;
     const char* lb = stage + kTileBytes;
     __builtin_amdgcn_s_setprio(1);
@@ -437,24 +420,18 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(GemmParams p) {
       }
     }
     __builtin_amdgcn_s_setprio(0);
-    barrier();  // every wave is done reading this stage
-    if (kt + 2 < nk) {
-      issue_tile<A_KC>(oa, stage, (kt + 2) * BK, wid, lane);
-      issue_tile<B_KC>(ob, stage + kTileBytes, (kt + 2) * BK, wid, lane);
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // tile kt+1 landed, kt+2 in flight
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    barrier();  // tile kt+1 visible to every wave
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // own DMA of tile kt+1 landed
   }
   epilogue<EPI, OUT_F32, 8, 4>(p, acc, m0 + wm * 128, n0 + wn * 64, lane);
 }
 
 }  // namespace k256
 
+
 template <int TILE, bool A_KC, bool B_KC, bool OUT_F32>
 hipError_t dispatch_epi(const GemmParams& p, int epi, hipStream_t s) {
-  const int tiles = ((p.M + TILE - 1) / TILE) * ((p.N + TILE - 1) / TILE);
+  constexpr int T = TILE == 128 ? 128 : 256;
+  const int tiles = ((p.M + T - 1) / T) * ((p.N + T - 1) / T);
   dim3 grid(tiles);
 #define LDNN_GEMM_CASE(E)                                                                          \
   case E:                                                                                          \
@@ -505,7 +482,7 @@ hipError_t gemm_bf16(const GemmParams& p, bool a_kcontig, bool b_kcontig, int ep
 hipError_t gemm_bf16_tile(const GemmParams& p, bool a_kcontig, bool b_kcontig, int epi, bool out_f32, int tile,
                           hipStream_t s) {
   if (p.M <= 0 || p.N <= 0) return hipSuccess;
-  if (tile == 256) {
+  if (tile >= 256) {
     // buffer resources address at most 2 GiB per operand
     const size_t abytes = (size_t)(a_kcontig ? p.M : p.K) * p.lda * 2;
     const size_t bbytes = (size_t)(b_kcontig ? p.N : p.K) * p.ldb * 2;
