@@ -13,3 +13,15 @@ cutoff and failure detection.
 __version__ = "0.1.0"
 
 from . import ops  # noqa: F401  (loads the native extension, loudly on GPU boxes)
+
+
+def prepare(model, device=None):
+    """Move `model` to `device` and lay its parameters out in one FlatParams buffer
+    (fp32 master + flat grads + bf16 shadow on the GPU).  Returns the FlatParams."""
+    import torch
+
+    from .parallel.ddp import ensure_flat
+
+    if device is not None:
+        model.to(torch.device(device))
+    return ensure_flat(model, device)

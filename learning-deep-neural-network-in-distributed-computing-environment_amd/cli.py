@@ -1,0 +1,187 @@
+"""Command line entry point: the reference's flags (BAR/main.py:83-97,
+DAR/main.py:87-103, BR/main.py:77-92, BDR/main.py:77-93) plus the MI355X-native
+extensions (SURVEY §5 config row, §7.4 decisions).
+
+Launch (one process per GPU, RCCL over xGMI):
+    python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 train.py [flags]
+CPU / gloo plumbing runs the same way with --device cpu.
+
+Reference flags kept verbatim: --local-rank, --backend {nccl,gloo,mpi}, --epochs_local,
+--epochs_global, --batch_size, --lr, --time_limit, --prev_fraction, --next_fraction,
+--aggregation_type {equal,weighted}, --aggregation_by {gradients,weights},
+--local_weight, --fixed_ratio, --gpu_weight (accepted, unused as in the reference),
+--dist-url (accepted, unused).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+
+import torch
+
+
+def build_parser() -> argparse.ArgumentParser:
+    p = argparse.ArgumentParser(description="ldnn: MI355X-native distributed DNN training")
+    # ---- reference flags
+    p.add_argument("--local-rank", "--local_rank", type=int, dest="local_rank", default=None)
+    p.add_argument("--backend", type=str, default="auto", choices=["auto", "nccl", "gloo", "mpi"],
+                   help="process-group backend; nccl = RCCL on ROCm; mpi maps to the default backend")
+    p.add_argument("--epochs_local", type=int, default=5)
+    p.add_argument("--epochs_global", type=int, default=20)
+    p.add_argument("--batch_size", type=int, default=64)
+    p.add_argument("--lr", type=float, default=1e-3)
+    p.add_argument("--time_limit", type=float, default=60.0)
+    p.add_argument("--prev_fraction", type=float, default=0.5)
+    p.add_argument("--next_fraction", type=float, default=0.5)
+    p.add_argument("--aggregation_type", type=str, default="equal", choices=["equal", "weighted"])
+    p.add_argument("--aggregation_by", type=str, default="gradients", choices=["gradients", "weights"])
+    p.add_argument("--local_weight", type=float, default=0.5)
+    p.add_argument("--fixed_ratio", type=float, default=None,
+                   help="class-skewed ('disbalanced') partition with this fraction of fixed classes")
+    p.add_argument("--gpu_weight", type=float, default=10, help="accepted for compatibility (unused)")
+    p.add_argument("--dist-url", type=str, default=None, help="accepted for compatibility (unused)")
+    # ---- extensions
+    p.add_argument("--topology", type=str, default="allreduce", choices=["allreduce", "ring", "double_ring"])
+    p.add_argument("--partition", type=str, default=None, choices=["balanced", "skewed"],
+                   help="skewed requires --fixed_ratio (default 0.5)")
+    p.add_argument("--partition_rule", type=str, default="reference_duration",
+                   choices=["reference_duration", "throughput", "equal"])
+    p.add_argument("--sync_every", type=str, default="global_epoch", choices=["global_epoch", "step"],
+                   help="global_epoch = reference schedule (SURVEY Q1); step = per-step data parallelism")
+    p.add_argument("--model", type=str, default="enhanced_cnn")
+    p.add_argument("--dataset", type=str, default=None, help="cifar10 | mnist | imagenet | imagenet64 (synthetic "
+                   "unless the CIFAR-10 binary files exist under --data_root)")
+    p.add_argument("--n_train", type=int, default=None)
+    p.add_argument("--n_test", type=int, default=None)
+    p.add_argument("--data_root", type=str, default="data")
+    p.add_argument("--optimizer", type=str, default="adam", choices=["adam", "adamw", "sgd"])
+    p.add_argument("--momentum", type=float, default=0.9)
+    p.add_argument("--weight_decay", type=float, default=0.0)
+    p.add_argument("--step_size", type=int, default=25, help="StepLR step (local epochs), BAR/main.py:54")
+    p.add_argument("--gamma", type=float, default=0.1)
+    p.add_argument("--dtype", type=str, default="bf16", choices=["bf16", "fp32"])
+    p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--device", type=str, default="auto", help="auto | cpu | cuda")
+    p.add_argument("--legacy_gossip", action="store_true", help="reproduce the reference's lost GPU gossip update")
+    p.add_argument("--average_buffers", action="store_true", help="also average BN buffers in weight averaging")
+    p.add_argument("--replace", action="store_true", help="sample re-partitions with replacement (BDR/DAR)")
+    p.add_argument("--no_repartition", action="store_true")
+    p.add_argument("--check_every", type=int, default=20, help="steps between straggler-cutoff rounds")
+    p.add_argument("--bucket_mb", type=float, default=32.0)
+    p.add_argument("--augment", action="store_true", help="GPU flip+crop augmentation")
+    p.add_argument("--out_dir", type=str, default="runs/latest")
+    p.add_argument("--plots", type=str, default="Graphs", help="output folder of the six plots ('' to skip)")
+    p.add_argument("--checkpoint_every", type=int, default=0)
+    p.add_argument("--resume", type=str, default=None, help="checkpoint path or 'latest'")
+    p.add_argument("--timeout", type=float, default=600.0, help="collective timeout (s): failure detection")
+    p.add_argument("--no_eval", action="store_true")
+    p.add_argument("--quiet", action="store_true")
+    return p
+
+
+def main(argv=None):
+    args = build_parser().parse_args(argv)
+    from . import prepare
+    from .data.loader import get_loaders
+    from .models import CrossEntropyLoss, build_model, dataset_for, xavier_init
+    from .optim import StepLR, build_optimizer
+    from .parallel.comm import default_comm
+    from .parallel.ddp import DataParallel
+    from .train.trainer import train_global
+    from .train.validator import evaluate
+    from .utils import distributed as D
+    from .utils.checkpoint import Checkpointer, load_checkpoint
+    from .utils.metrics import MetricsLogger
+
+    backend = None if args.backend in ("auto", "mpi") else args.backend
+    ctx = D.setup(backend, timeout_s=args.timeout, device=None if args.device == "auto" else args.device)
+    rank, world = ctx.rank, ctx.world_size
+    dev = ctx.device
+    torch.manual_seed(args.seed)
+    comm = default_comm()
+
+    dataset = args.dataset or dataset_for(args.model)
+    model = build_model(args.model)
+    xavier_init(model)
+    flat = prepare(model, dev)
+    fixed_ratio = args.fixed_ratio
+    if args.partition == "skewed" and fixed_ratio is None:
+        fixed_ratio = 0.5
+    if args.partition == "balanced":
+        fixed_ratio = None
+
+    dp = None
+    if args.sync_every == "step" and args.topology == "allreduce" and world > 1:
+        dp = DataParallel(model, comm, bucket_cap_mb=args.bucket_mb, average=args.aggregation_type == "equal")
+    else:  # reference A6: broadcast every state_dict entry from rank 0
+        D.broadcast_module(model)
+        flat.refresh_shadow()
+    net = dp if dp is not None else model
+
+    dtype = torch.bfloat16 if (args.dtype == "bf16" and dev.type == "cuda") else torch.float32
+    loaders = get_loaders(args.batch_size, world, rank, net, dev, fixed_ratio, dataset=dataset, comm=comm,
+                          seed=args.seed, partition_rule=args.partition_rule, n_train=args.n_train,
+                          n_test=args.n_test, dtype=dtype, augment=args.augment, data_root=args.data_root)
+    train_loader, val_loader, test_loader, trainset, valset, tr_idx, va_idx = loaders[:7]
+    fixed_classes = loaders[7] if len(loaders) > 7 else None
+
+    criterion = CrossEntropyLoss()
+    optimizer = build_optimizer(args.optimizer, model.parameters(), args.lr, args.momentum, args.weight_decay)
+    scheduler = StepLR(optimizer, step_size=args.step_size, gamma=args.gamma)
+
+    os.makedirs(args.out_dir, exist_ok=True)
+    logger = MetricsLogger(os.path.join(args.out_dir, "metrics.jsonl"), rank)
+    logger.log(kind="config", world_size=world, pg_backend=ctx.backend, resolved_device=str(dev), **vars(args))
+    per_rank = args.topology != "allreduce" or args.sync_every == "global_epoch"
+    ckpt = Checkpointer(os.path.join(args.out_dir, "ckpt"), rank, per_rank=per_rank,
+                        every=args.checkpoint_every) if args.checkpoint_every > 0 else None
+    start, hist = 0, None
+    if args.resume:
+        path = args.resume
+        if path == "latest":
+            path = Checkpointer(os.path.join(args.out_dir, "ckpt"), rank, per_rank=per_rank).latest()
+        if path:
+            sd = load_checkpoint(path, model, optimizer, scheduler)
+            start, hist = sd["global_epoch"], sd["histories"]
+            ex = sd.get("extra", {})
+            if "indices_train" in ex:
+                from .data.loader import DeviceLoader
+
+                tr_idx, va_idx = ex["indices_train"].numpy(), ex["indices_val"].numpy()
+                train_loader = DeviceLoader(trainset, tr_idx, args.batch_size, dev, dtype=dtype, augment=args.augment)
+                val_loader = DeviceLoader(valset, va_idx, args.batch_size, dev, dtype=dtype)
+
+    timelimit = args.time_limit if args.time_limit and args.time_limit > 0 else math.inf
+    histories = train_global(
+        net, train_loader, val_loader, trainset, valset, tr_idx, va_idx, criterion, optimizer, scheduler, dev, rank,
+        world, args.epochs_local, args.epochs_global, timelimit, args.batch_size, args.prev_fraction,
+        args.next_fraction, args.local_weight, args.aggregation_type, args.aggregation_by, comm=comm,
+        topology=args.topology, fixed_classes=fixed_classes, fixed_ratio=fixed_ratio, sync_every=args.sync_every,
+        dp=dp, partition_rule=args.partition_rule, repartition=not args.no_repartition, replace=args.replace,
+        seed=args.seed, legacy_gossip=args.legacy_gossip, average_buffers=args.average_buffers,
+        check_every=args.check_every, progress=not args.quiet, logger=logger, checkpointer=ckpt,
+        start_global_epoch=start, histories=hist, dtype=dtype, verbose=not args.quiet)
+
+    result = {"histories": [list(h) if not isinstance(h, list) else h for h in histories]}
+    if rank == 0 and not args.no_eval:
+        loss, acc, _, _ = evaluate(net, test_loader, criterion, dev, rank, num_classes=trainset.num_classes,
+                                   verbose=not args.quiet)
+        rep = {k: v for k, v in evaluate.last_report.items() if k != "confusion_matrix"}
+        result.update(test_loss=loss, test_acc=acc, **rep)
+        logger.log(kind="test", test_loss=loss, test_acc=acc, **rep)
+    if rank == 0 and args.plots:
+        from .utils.viz import plot_all
+
+        plot_all(histories, args.epochs_global, args.epochs_local, 0, args.plots)
+    if rank == 0:
+        with open(os.path.join(args.out_dir, "histories.json"), "w") as f:
+            json.dump(result, f)
+    logger.close()
+    D.teardown(ctx)
+    return result
+
+
+if __name__ == "__main__":
+    main()

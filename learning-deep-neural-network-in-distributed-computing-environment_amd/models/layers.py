@@ -50,3 +50,31 @@ class CrossEntropyLoss(nn.CrossEntropyLoss):
 
     def forward(self, logits, labels, stats=None):
         return LF.cross_entropy(logits, labels, stats)
+
+
+class Conv2d(nn.Conv2d):
+    """nn.Conv2d (reference key names and init); on the GPU the activations flow in
+    bf16 through the native implicit-GEMM conv kernels when built, else MIOpen."""
+
+    def forward(self, x):
+        return LF.conv2d(x, self)
+
+
+class BatchNorm2d(nn.BatchNorm2d):
+    """Train-mode batch statistics + running-stat EMA exactly as nn.BatchNorm2d;
+    fp32 statistics over bf16 activations on the GPU."""
+
+    def forward(self, x):
+        return LF.batch_norm2d(x, self)
+
+
+class MaxPool2d(nn.MaxPool2d):
+    pass
+
+
+class AvgPool2d(nn.AvgPool2d):
+    pass
+
+
+class AdaptiveAvgPool2d(nn.AdaptiveAvgPool2d):
+    pass

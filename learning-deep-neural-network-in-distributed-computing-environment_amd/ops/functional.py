@@ -27,14 +27,18 @@ def _to_bf16(x: torch.Tensor) -> torch.Tensor:
     return x.to(torch.bfloat16).contiguous()
 
 
-def _padded_rows_view(g: torch.Tensor, npad: int) -> torch.Tensor:
-    """[B, N] gradient -> [B, npad] with zero padding columns (copy only if needed)."""
+def _padded_rows_view(g: torch.Tensor, npad: int, zero_pad_guaranteed: bool = True) -> torch.Tensor:
+    """[B, N] tensor -> [B, npad] (npad >= N, multiple of 8), copying only if needed.
+
+    A [B, N] view whose row stride is already npad was produced by an ldnn op on
+    a padded [B, npad] buffer and is widened in place.  Gradients written by
+    ldnn ops have zero padding; forward activations may carry arbitrary (finite)
+    values there, which is harmless because the matching weight columns are 0."""
     B, N = g.shape
     if N == npad and g.is_contiguous():
         return g
-    if g.stride(1) == 1 and g.stride(0) == npad and g.dtype == torch.bfloat16:
-        # produced by an ldnn op on a zero-padded [B, npad] buffer
-        return g.as_strided((B, npad), (npad, 1))
+    if g.stride(1) == 1 and g.stride(0) == npad and g.dtype == torch.bfloat16 and zero_pad_guaranteed:
+        return g.as_strided((B, npad), (npad, 1), g.storage_offset())
     out = torch.zeros(B, npad, dtype=torch.bfloat16, device=g.device)
     out[:, :N].copy_(g)
     return out
@@ -46,11 +50,15 @@ class _LinearActNative(torch.autograd.Function):
         C = _ext.C()
         x = _to_bf16(x)
         w = flat.shadow_storage(weight)
-        npad, K = w.shape
+        npad, kpad = w.shape
+        K = weight.shape[1]
         assert x.shape[-1] == K, f"Linear expects {K} input features, got {x.shape[-1]}"
         x2 = x.reshape(-1, K)
-        if K % 8:
-            raise ValueError(f"native Linear needs in_features % 8 == 0 (got {K})")
+        if kpad != K:
+            # pad columns must be 0 so the weight-gradient pad columns stay exactly 0
+            # (the producer's pad may hold e.g. sigmoid(0) = 0.5)
+            x2 = _padded_rows_view(x2, kpad)
+            x2[:, K:].zero_()
         y = torch.empty(x2.shape[0], npad, dtype=torch.bfloat16, device=x.device)
         if bias is not None:
             b = flat.master_storage(bias)
@@ -86,6 +94,9 @@ class _LinearActNative(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = torch.empty(x2.shape, dtype=torch.bfloat16, device=x2.device)
             C.gemm(gz, flat.shadow_storage(weight), dx, True, False)
+            K = weight.shape[1]
+            if dx.shape[1] != K:
+                dx = dx[:, :K]
             dx = dx.reshape(ctx.xshape)
         return dx, None, None, None, None
 
@@ -179,3 +190,31 @@ def cross_entropy(logits, labels, stats: torch.Tensor | None = None):
             stats[0] += loss.detach() * labels.numel()
             stats[1] += (lf.argmax(1) == labels).sum()
     return loss
+
+
+# ------------------------------------------------------------------ conv / BN
+def conv2d(x, mod):
+    """Convolution of module `mod` (nn.Conv2d parameters).  GPU: bf16 activations,
+    fp32 master weights cast in-graph (autograd returns fp32 weight grads into the
+    FlatParams buffer).  CPU: fp32 reference."""
+    if x.is_cuda and not _ext._DISABLED:
+        xb = x if x.dtype == torch.bfloat16 else x.to(torch.bfloat16)
+        w = mod.weight.to(torch.bfloat16)
+        b = mod.bias.to(torch.bfloat16) if mod.bias is not None else None
+        return F.conv2d(xb, w, b, mod.stride, mod.padding, mod.dilation, mod.groups)
+    return F.conv2d(x.float(), mod.weight, mod.bias, mod.stride, mod.padding, mod.dilation, mod.groups)
+
+
+def batch_norm2d(x, mod):
+    training = mod.training or not mod.track_running_stats
+    mom = 0.0 if mod.momentum is None else mod.momentum
+    if mod.training and mod.track_running_stats and mod.num_batches_tracked is not None:
+        mod.num_batches_tracked.add_(1)
+        if mod.momentum is None:
+            mom = 1.0 / float(mod.num_batches_tracked)
+    rm = mod.running_mean if (not mod.training or mod.track_running_stats) else None
+    rv = mod.running_var if (not mod.training or mod.track_running_stats) else None
+    if x.is_cuda and x.dtype == torch.bfloat16:
+        y = F.batch_norm(x.float(), rm, rv, mod.weight, mod.bias, training, mom, mod.eps)
+        return y.to(torch.bfloat16)
+    return F.batch_norm(x.float(), rm, rv, mod.weight, mod.bias, training, mom, mod.eps)

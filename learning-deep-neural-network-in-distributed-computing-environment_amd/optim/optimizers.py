@@ -1,0 +1,207 @@
+"""Fused optimizers (reference BAR/main.py:53 uses torch.optim.Adam,
+BASELINE configs use SGD-momentum).
+
+They are ``torch.optim.Optimizer`` subclasses (so the reference's
+``StepLR(optimizer, step_size=25)`` and ``optimizer.param_groups[..]['lr']``
+work unchanged), but when the parameters live in a FlatParams buffer the
+update is ONE fused kernel over the whole model (fp32 master + momentum /
+moments + bf16 shadow refresh, with the data-parallel 1/N folded in) instead
+of a per-tensor loop.  Learning rate and Adam's step count are handed to the
+kernel through a small device tensor, so the update can sit inside a captured
+hipGraph.  Without FlatParams (or on CPU) the same math runs as torch ops.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from ..ops import _ext
+from ..utils.flat_params import owner_of
+
+
+class _FlatOptimizer(torch.optim.Optimizer):
+    def _ls(self) -> dict:
+        """Fused (flat-buffer) optimizer state: momentum / moments / step / hp."""
+        return self.__dict__.setdefault("_ldnn_state", {})
+
+    def state_dict(self):
+        sd = super().state_dict()
+        sd["ldnn_flat_state"] = {k: v for k, v in self._ls().items() if k != "hp"}
+        return sd
+
+    def load_state_dict(self, state_dict):
+        state_dict = dict(state_dict)
+        flat_state = state_dict.pop("ldnn_flat_state", {})
+        super().load_state_dict(state_dict)
+        ls = self._ls()
+        ls.clear()
+        for k, v in flat_state.items():
+            ls[k] = v.clone() if torch.is_tensor(v) else v
+        # re-home buffers onto the parameters' device
+        for group in self.param_groups:
+            f = self._flat_for_group(group)
+            if f is not None:
+                for k, v in list(ls.items()):
+                    if torch.is_tensor(v):
+                        ls[k] = v.to(f.master.device)
+
+    def _flat_for_group(self, group):
+        ps = group["params"]
+        if not ps:
+            return None
+        f = owner_of(ps[0])
+        if f is None or any(owner_of(p) is not f for p in ps) or len(ps) != len(f.segments):
+            return None
+        return f
+
+    def _hp(self, flat, lr):
+        st = self._ls()
+        hp = st.get("hp")
+        if hp is None or hp.device != flat.master.device:
+            hp = torch.zeros(2, dtype=torch.float32, device=flat.master.device)
+            hp[1] = float(st.get("step", 0))
+            st["hp"] = hp
+        hp[0].fill_(lr)
+        return hp
+
+    def _buf(self, name, like):
+        st = self._ls()
+        b = st.get(name)
+        if b is None or b.shape != like.shape or b.device != like.device:
+            b = torch.zeros_like(like)
+            st[name] = b
+        return b
+
+    def zero_grad(self, set_to_none: bool = True):
+        for group in self.param_groups:
+            f = self._flat_for_group(group)
+            if f is not None:
+                f.zero_grad()
+            else:
+                for p in group["params"]:
+                    if p.grad is not None:
+                        if set_to_none and owner_of(p) is None:
+                            p.grad = None
+                        else:
+                            p.grad.zero_()
+
+
+class SGD(_FlatOptimizer):
+    def __init__(self, params, lr=0.01, momentum=0.0, dampening=0.0, weight_decay=0.0, nesterov=False):
+        super().__init__(params, dict(lr=lr, momentum=momentum, dampening=dampening, weight_decay=weight_decay,
+                                      nesterov=nesterov))
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = closure() if closure is not None else None
+        for group in self.param_groups:
+            lr, mu, damp, wd, nest = (group[k] for k in ("lr", "momentum", "dampening", "weight_decay", "nesterov"))
+            f = self._flat_for_group(group)
+            if f is not None:
+                st = self._ls()
+                first = st.get("step", 0) == 0
+                mom = self._buf("momentum", f.master) if mu != 0 else f.master
+                if _ext.use_native(f.master):
+                    _ext.C().sgd_step(f.master, f.grad, mom, f.shadow, self._hp(f, lr), f.grad_scale, mu, damp, wd,
+                                      nest, first)
+                else:
+                    self._sgd_torch(f.master, f.grad * f.grad_scale, mom if mu != 0 else None, lr, mu, damp, wd,
+                                    nest, first)
+                    if f.shadow is not None:
+                        f.shadow.copy_(f.master)
+                st["step"] = st.get("step", 0) + 1
+            else:
+                for p in group["params"]:
+                    if p.grad is None:
+                        continue
+                    ps = self.state.setdefault(p, {})
+                    first = "momentum_buffer" not in ps
+                    if mu != 0 and first:
+                        ps["momentum_buffer"] = torch.zeros_like(p)
+                    self._sgd_torch(p.data, p.grad, ps.get("momentum_buffer"), lr, mu, damp, wd, nest, first)
+        return loss
+
+    @staticmethod
+    def _sgd_torch(p, g, buf, lr, mu, damp, wd, nest, first):
+        if wd != 0:
+            g = g + wd * p
+        if mu != 0:
+            if first:
+                buf.copy_(g)
+            else:
+                buf.mul_(mu).add_(g, alpha=1 - damp)
+            g = g + mu * buf if nest else buf
+        p.add_(g, alpha=-lr)
+
+
+class Adam(_FlatOptimizer):
+    decoupled = False
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0):
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = closure() if closure is not None else None
+        for group in self.param_groups:
+            lr, (b1, b2), eps, wd = group["lr"], group["betas"], group["eps"], group["weight_decay"]
+            f = self._flat_for_group(group)
+            if f is not None:
+                st = self._ls()
+                m, v = self._buf("exp_avg", f.master), self._buf("exp_avg_sq", f.master)
+                if _ext.use_native(f.master):
+                    hp = self._hp(f, lr)
+                    _ext.C().bump_step(hp)
+                    _ext.C().adam_step(f.master, f.grad, m, v, f.shadow, hp, f.grad_scale, b1, b2, eps, wd,
+                                       self.decoupled)
+                    st["step"] = st.get("step", 0) + 1
+                else:
+                    st["step"] = st.get("step", 0) + 1
+                    self._adam_torch(f.master, f.grad * f.grad_scale, m, v, st["step"], lr, b1, b2, eps, wd)
+                    if f.shadow is not None:
+                        f.shadow.copy_(f.master)
+            else:
+                for p in group["params"]:
+                    if p.grad is None:
+                        continue
+                    ps = self.state.setdefault(p, {})
+                    if "exp_avg" not in ps:
+                        ps["exp_avg"] = torch.zeros_like(p)
+                        ps["exp_avg_sq"] = torch.zeros_like(p)
+                        ps["step"] = 0
+                    ps["step"] += 1
+                    self._adam_torch(p.data, p.grad, ps["exp_avg"], ps["exp_avg_sq"], ps["step"], lr, b1, b2, eps,
+                                     wd)
+        return loss
+
+    def _adam_torch(self, p, g, m, v, t, lr, b1, b2, eps, wd):
+        if wd != 0:
+            if self.decoupled:
+                p.mul_(1 - lr * wd)
+            else:
+                g = g + wd * p
+        m.mul_(b1).add_(g, alpha=1 - b1)
+        v.mul_(b2).addcmul_(g, g, value=1 - b2)
+        bc1 = 1 - b1 ** t
+        bc2 = 1 - b2 ** t
+        denom = (v.sqrt() / math.sqrt(bc2)).add_(eps)
+        p.addcdiv_(m, denom, value=-lr / bc1)
+
+
+class AdamW(Adam):
+    decoupled = True
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2):
+        super().__init__(params, lr, betas, eps, weight_decay)
+
+
+def build_optimizer(name: str, params, lr: float, momentum: float = 0.9, weight_decay: float = 0.0):
+    name = name.lower()
+    if name == "sgd":
+        return SGD(params, lr=lr, momentum=momentum, weight_decay=weight_decay)
+    if name == "adam":
+        return Adam(params, lr=lr, weight_decay=weight_decay)
+    if name == "adamw":
+        return AdamW(params, lr=lr, weight_decay=weight_decay)
+    raise ValueError(f"unknown optimizer {name!r}")

@@ -1,0 +1,223 @@
+"""Communicator abstraction over the collectives the reference uses.
+
+The reference talks to two backends: torch.distributed (gloo/nccl; AR
+variants) and mpi4py with host-staged numpy buffers (ring variants,
+BR/communication.py:1-30).  Here one interface serves every topology:
+
+* ``TorchComm``  -- torch.distributed on the default (or a given) group.  With
+  backend "nccl" this is RCCL over xGMI inside an MI355X node: device buffers
+  are sent directly (no host staging), point-to-point gossip uses grouped
+  ``batch_isend_irecv`` (one ncclGroupStart/End) so the ring and double-ring
+  exchanges use distinct xGMI links concurrently.
+* ``FakeWorld`` / ``FakeComm`` -- an in-process world of N ranks run as
+  threads, used by the tests to check aggregation formulas and whole training
+  loops deterministically without any process group (SURVEY §4 "FakeGroup").
+
+Every collective the training driver issues goes through ``Comm.record`` so a
+schedule checker can hash the op sequence and detect rank divergence.
+"""
+from __future__ import annotations
+
+import hashlib
+import threading
+
+import torch
+import torch.distributed as dist
+
+SUM, MAX, MIN = "sum", "max", "min"
+_TORCH_OPS = {SUM: dist.ReduceOp.SUM, MAX: dist.ReduceOp.MAX, MIN: dist.ReduceOp.MIN}
+
+
+class Comm:
+    rank: int = 0
+    world_size: int = 1
+
+    def __init__(self):
+        self._sched = hashlib.sha1()
+        self._nops = 0
+
+    # -- schedule bookkeeping (race / divergence detection)
+    def record(self, op: str, t: torch.Tensor | None = None):
+        desc = op if t is None else f"{op}:{tuple(t.shape)}:{t.dtype}"
+        self._sched.update(desc.encode())
+        self._nops += 1
+
+    def schedule_digest(self) -> tuple[int, str]:
+        return self._nops, self._sched.hexdigest()
+
+    # -- API (implemented by subclasses)
+    def all_reduce(self, t: torch.Tensor, op: str = SUM, async_op: bool = False):
+        raise NotImplementedError
+
+    def broadcast(self, t: torch.Tensor, src: int = 0):
+        raise NotImplementedError
+
+    def all_gather(self, t: torch.Tensor) -> list[torch.Tensor]:
+        raise NotImplementedError
+
+    def barrier(self):
+        raise NotImplementedError
+
+    def sendrecv(self, sends: list[tuple[torch.Tensor, int]], recvs: list[tuple[torch.Tensor, int]]):
+        """Grouped point-to-point: post every send and receive, wait for all."""
+        raise NotImplementedError
+
+
+class _Done:
+    def wait(self):
+        return None
+
+
+class LocalComm(Comm):
+    """World of one: every collective is the identity."""
+
+    def all_reduce(self, t, op=SUM, async_op=False):
+        self.record("all_reduce", t)
+        return _Done() if async_op else None
+
+    def broadcast(self, t, src=0):
+        self.record("broadcast", t)
+
+    def all_gather(self, t):
+        self.record("all_gather", t)
+        return [t.clone()]
+
+    def barrier(self):
+        self.record("barrier")
+
+    def sendrecv(self, sends, recvs):
+        self.record("sendrecv")
+        for (rt, src), (st, dst) in zip(recvs, sends):
+            rt.copy_(st)
+
+
+class TorchComm(Comm):
+    def __init__(self, group=None):
+        super().__init__()
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world_size = dist.get_world_size(group)
+
+    def _global(self, r: int) -> int:
+        return r if self.group is None else dist.get_global_rank(self.group, r)
+
+    def all_reduce(self, t, op=SUM, async_op=False):
+        self.record("all_reduce", t)
+        return dist.all_reduce(t, op=_TORCH_OPS[op], group=self.group, async_op=async_op)
+
+    def broadcast(self, t, src=0):
+        self.record("broadcast", t)
+        dist.broadcast(t, src=self._global(src), group=self.group)
+
+    def all_gather(self, t):
+        self.record("all_gather", t)
+        out = [torch.empty_like(t) for _ in range(self.world_size)]
+        dist.all_gather(out, t.contiguous(), group=self.group)
+        return out
+
+    def barrier(self):
+        self.record("barrier")
+        if dist.get_backend(self.group) == "nccl" and torch.cuda.is_available():
+            dist.barrier(group=self.group, device_ids=[torch.cuda.current_device()])
+        else:
+            dist.barrier(group=self.group)
+
+    def sendrecv(self, sends, recvs):
+        self.record("sendrecv")
+        ops = [dist.P2POp(dist.irecv, t, self._global(src), self.group) for t, src in recvs]
+        ops += [dist.P2POp(dist.isend, t, self._global(dst), self.group) for t, dst in sends]
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+
+
+# ------------------------------------------------------------------ fake world
+class FakeWorld:
+    """N ranks as threads of one process; collectives meet at a barrier."""
+
+    def __init__(self, n: int, timeout: float = 60.0):
+        self.n = n
+        self._bar = threading.Barrier(n, timeout=timeout)
+        self._slots: list = [None] * n
+        self._p2p: dict = {}
+        self._lock = threading.Lock()
+
+    def comm(self, rank: int) -> "FakeComm":
+        return FakeComm(self, rank)
+
+    def run(self, fn, *args, **kwargs) -> list:
+        """Run fn(comm, *args) on every rank; return per-rank results (re-raises errors)."""
+        results: list = [None] * self.n
+        errors: list = []
+
+        def body(r):
+            try:
+                results[r] = fn(self.comm(r), *args, **kwargs)
+            except BaseException as e:  # pragma: no cover - surfaced below
+                errors.append(e)
+                self._bar.abort()
+
+        ts = [threading.Thread(target=body, args=(r,)) for r in range(self.n)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        if errors:
+            raise errors[0]
+        return results
+
+
+class FakeComm(Comm):
+    def __init__(self, world: FakeWorld, rank: int):
+        super().__init__()
+        self.w = world
+        self.rank = rank
+        self.world_size = world.n
+
+    def _exchange(self, value):
+        w = self.w
+        w._slots[self.rank] = value
+        w._bar.wait()
+        vals = list(w._slots)
+        w._bar.wait()
+        return vals
+
+    def all_reduce(self, t, op=SUM, async_op=False):
+        self.record("all_reduce", t)
+        vals = self._exchange(t.detach().clone())
+        if op == SUM:
+            res = torch.stack(vals).sum(0)
+        elif op == MAX:
+            res = torch.stack(vals).amax(0)
+        else:
+            res = torch.stack(vals).amin(0)
+        t.copy_(res.to(t.dtype))
+        return _Done() if async_op else None
+
+    def broadcast(self, t, src=0):
+        self.record("broadcast", t)
+        vals = self._exchange(t.detach().clone())
+        t.copy_(vals[src])
+
+    def all_gather(self, t):
+        self.record("all_gather", t)
+        return [v.clone() for v in self._exchange(t.detach().clone())]
+
+    def barrier(self):
+        self.record("barrier")
+        self._exchange(None)
+
+    def sendrecv(self, sends, recvs):
+        self.record("sendrecv")
+        msgs = {(self.rank, dst): st.detach().clone() for st, dst in sends}
+        allm = self._exchange(msgs)
+        merged = {}
+        for m in allm:
+            merged.update(m)
+        for rt, src in recvs:
+            rt.copy_(merged[(src, self.rank)])
+
+
+def default_comm() -> Comm:
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        return TorchComm()
+    return LocalComm()

@@ -1,0 +1,278 @@
+"""The global / local-epoch training driver (§3.2-3.4).
+
+``train_global`` keeps the reference's signature and its 12-history return
+contract (BAR/trainer.py:11-192):
+
+   1 all_workers_losses         [N][*]        per-batch train losses per worker (rank 0)
+   2 all_epochs_losses          [Eg*El][*]    all workers' batch losses per local epoch (rank 0)
+   3 global_epoch_losses        [Eg][*]       all batch losses of each global epoch (rank 0)
+   4 global_epoch_accuracies    [Eg][El]      worker-mean train accuracy per local epoch (rank 0)
+   5-8 global_{train,val}_{losses,accuracies}  [Eg] means over workers and local epochs (all ranks)
+   9-12 worker_specific_{train,val}_{losses,accuracies}  [Eg*El] rank-0 values (rank 0)
+
+What changes is how it runs on MI355X:
+* the hot loop (train_local_epoch, BAR/trainer.py:194-223) has no host syncs:
+  loss / correct counts / per-batch losses accumulate on the device and are
+  read once per local epoch;
+* metric exchange is batched: instead of 6 collectives per local epoch
+  (C3-C6) every rank packs its local-epoch metrics and batch
+  losses and ONE all-gather per global epoch delivers everything;
+* aggregation is either the reference schedule (``sync_every="global_epoch"``:
+  once per global epoch on gradients or weights, with all-reduce, ring or
+  double-ring topology) or real data parallelism (``sync_every="step"``:
+  bucketed RCCL all-reduce -- or ring / double-ring gossip -- of gradients every
+  step, overlapped with backward);
+* the straggler time limit works (train/straggler.py);
+* re-partitioning uses a seeded RNG and a selectable share rule.
+"""
+from __future__ import annotations
+
+import time
+
+import numpy as np
+import torch
+
+from ..data.loader import get_subset_loaders
+from ..models.layers import CrossEntropyLoss as LdnnCE
+from ..parallel.aggregation import Aggregator
+from ..parallel.comm import MAX, MIN, SUM, Comm, default_comm
+from .straggler import StopLocalTraining, StragglerCutoff
+from .validator import validate
+
+
+def _progress(it, enabled, desc):
+    if not enabled:
+        return it
+    try:
+        from tqdm import tqdm
+
+        return tqdm(it, desc=desc)
+    except Exception:  # pragma: no cover
+        return it
+
+
+def train_local_epoch(model, trainloader, criterion, optimizer, device, scheduler=None, *, dp=None,
+                      step_aggregator=None, cutoff: StragglerCutoff | None = None, max_steps: int | None = None,
+                      step_scheduler: bool = True):
+    """One pass over the rank's shard.  Returns (mean loss, accuracy %, per-batch losses)."""
+    model.train()
+    dev = torch.device(device)
+    nb = len(trainloader) if max_steps is None else min(len(trainloader), max_steps)
+    losses = torch.zeros(max(nb, 1), dtype=torch.float32, device=dev)
+    stats = torch.zeros(2, dtype=torch.float32, device=dev)
+    total, done = 0, 0
+    ldnn_ce = isinstance(criterion, LdnnCE)
+    try:
+        for i, (x, y) in enumerate(trainloader):
+            if i >= nb:
+                break
+            optimizer.zero_grad()
+            out = model(x)
+            if ldnn_ce:
+                loss = criterion(out, y, stats)
+            else:
+                loss = criterion(out.float(), y)
+                with torch.no_grad():
+                    stats[1] += (out.argmax(1) == y).sum()
+            loss.backward()
+            if dp is not None:
+                dp.finish_gradient_sync()
+            if step_aggregator is not None:
+                step_aggregator(model)
+            optimizer.step()
+            losses[i] = loss.detach().float()
+            total += y.numel()
+            done += 1
+            if cutoff is not None:
+                cutoff.step(i)
+    except StopLocalTraining:
+        if step_scheduler and scheduler is not None:
+            scheduler.step()
+        raise
+    if step_scheduler and scheduler is not None:
+        scheduler.step()
+    batch_losses = losses[:done].tolist()  # the one host sync of the epoch
+    correct = stats[1].item()
+    train_loss = float(np.mean(batch_losses)) if batch_losses else 0.0
+    return train_loss, 100.0 * correct / max(total, 1), batch_losses
+
+
+
+
+def _pack(local_records, batch_losses_per_epoch, E_l, max_len, device):
+    """[n_done, (loss, acc, vloss, vacc) x E_l, (len, losses padded to max_len) x E_l]"""
+    buf = torch.full((1 + 4 * E_l + E_l * (1 + max_len),), -1.0, dtype=torch.float64)
+    buf[0] = len(local_records)
+    for e, rec in enumerate(local_records):
+        buf[1 + 4 * e: 5 + 4 * e] = torch.tensor(rec, dtype=torch.float64)
+    base = 1 + 4 * E_l
+    for e, bl in enumerate(batch_losses_per_epoch):
+        o = base + e * (1 + max_len)
+        buf[o] = len(bl)
+        if bl:
+            buf[o + 1: o + 1 + len(bl)] = torch.tensor(bl, dtype=torch.float64)
+    return buf.to(device)
+
+
+def _unpack(buf, E_l, max_len):
+    buf = buf.cpu()
+    n = int(buf[0].item())
+    recs = [tuple(buf[1 + 4 * e: 5 + 4 * e].tolist()) for e in range(n)]
+    base = 1 + 4 * E_l
+    bls = []
+    for e in range(n):
+        o = base + e * (1 + max_len)
+        ln = int(buf[o].item())
+        bls.append(buf[o + 1: o + 1 + ln].tolist())
+    return recs, bls
+
+
+def train_global(model, trainloader, val_loader, trainset, valset, indices_train, indices_val, criterion, optimizer,
+                 scheduler, device, rank, world_size, num_local_epochs, num_global_epochs, timelimit, batch_size,
+                 prev_fraction, next_fraction, local_weight=0.5, aggregation_type="equal",
+                 aggregation_by="gradients", *, comm: Comm | None = None, topology: str = "allreduce",
+                 fixed_classes=None, fixed_ratio=None, sync_every: str = "global_epoch", dp=None,
+                 partition_rule: str = "reference_duration", repartition: bool = True, replace: bool = False,
+                 seed: int = 0, legacy_gossip: bool = False, average_buffers: bool = False,
+                 check_every: int = 20, progress: bool = True, logger=None, checkpointer=None,
+                 start_global_epoch: int = 0, histories=None, dtype=torch.float32, verbose: bool = True):
+    comm = comm or default_comm()
+    N = comm.world_size
+    dev = torch.device(device)
+    rng = np.random.default_rng(seed * 7919 + rank)
+    H = histories or {
+        "all_workers_losses": [[] for _ in range(N)],
+        "all_epochs_losses": [],
+        "global_epoch_losses": [],
+        "global_epoch_accuracies": [],
+        "global_train_losses": [],
+        "global_train_accuracies": [],
+        "global_val_losses": [],
+        "global_val_accuracies": [],
+        "worker_specific_train_losses": [],
+        "worker_specific_train_accuracies": [],
+        "worker_specific_val_losses": [],
+        "worker_specific_val_accuracies": [],
+    }
+    aggregator = Aggregator(topology, aggregation_type, aggregation_by, local_weight, comm, legacy_gossip,
+                            average_buffers)
+    step_aggregator = None
+    if sync_every == "step" and dp is None:
+        # per-step decentralised SGD: gossip (or all-reduce) the gradients every step
+        step_aggregator = Aggregator(topology, aggregation_type, "gradients", local_weight, comm, legacy_gossip)
+    cutoff = StragglerCutoff(comm, timelimit, check_every, dev)
+
+    for global_epoch in _progress(range(start_global_epoch, num_global_epochs), progress and rank == 0,
+                                  "Global Epochs"):
+        t_start = time.perf_counter()
+        cutoff.reset()
+        max_steps = None
+        if sync_every == "step" and N > 1:
+            # per-step collectives need the same number of steps on every rank
+            t = torch.tensor([float(len(trainloader))], device=dev)
+            comm.all_reduce(t, MIN)
+            max_steps = int(t.item())
+        records, batch_losses = [], []
+        for local_epoch in range(num_local_epochs):
+            try:
+                loss, acc, bl = train_local_epoch(model, trainloader, criterion, optimizer, dev, scheduler, dp=dp,
+                                                  step_aggregator=step_aggregator, cutoff=cutoff,
+                                                  max_steps=max_steps)
+            except StopLocalTraining:
+                # cut by the collective time limit: keep LR schedules aligned across ranks
+                for _ in range(num_local_epochs - local_epoch - 1):
+                    if scheduler is not None:
+                        scheduler.step()
+                break
+            val_loss, val_acc = validate(model, val_loader, criterion, dev)
+            records.append((loss, acc, val_loss, val_acc))
+            batch_losses.append(bl)
+            if verbose:
+                print(f"Rank {rank}, Global Epoch {global_epoch + 1}, Local Epoch {local_epoch + 1}, "
+                      f"Loss: {loss}, Accuracy: {acc}")
+                print(f"Worker {rank}, Global Epoch {global_epoch + 1}, Validation Loss: {val_loss:.4f}, "
+                      f"Validation Accuracy: {val_acc:.2f}%")
+        cutoff.finish()
+
+        # ---- one metric exchange per global epoch (replaces C3-C6 per local epoch)
+        lt = torch.tensor([float(max([len(b) for b in batch_losses] + [0]))], device=dev)
+        comm.all_reduce(lt, MAX)
+        max_len = int(lt.item())
+        packed = _pack(records, batch_losses, num_local_epochs, max_len, dev)
+        gathered = comm.all_gather(packed) if N > 1 else [packed]
+        per_rank = [_unpack(g, num_local_epochs, max_len) for g in gathered]
+
+        if rank == 0:
+            cur_losses, cur_accs = [], []
+            for e in range(num_local_epochs):
+                ranks_e = [r for r in range(N) if len(per_rank[r][0]) > e]
+                if not ranks_e:
+                    continue
+                ep_losses = []
+                for r in ranks_e:
+                    H["all_workers_losses"][r].extend(per_rank[r][1][e])
+                    ep_losses.extend(per_rank[r][1][e])
+                H["all_epochs_losses"].append(ep_losses)
+                cur_losses.extend(ep_losses)
+                cur_accs.append(float(np.mean([per_rank[r][0][e][1] for r in ranks_e])))
+            for rec in per_rank[0][0]:
+                H["worker_specific_train_losses"].append(rec[0])
+                H["worker_specific_train_accuracies"].append(rec[1])
+                H["worker_specific_val_losses"].append(rec[2])
+                H["worker_specific_val_accuracies"].append(rec[3])
+            H["global_epoch_losses"].append(cur_losses)
+            H["global_epoch_accuracies"].append(cur_accs)
+        all_recs = [rec for r in range(N) for rec in per_rank[r][0]]
+        if all_recs:
+            arr = np.asarray(all_recs, dtype=np.float64)
+            means = arr.mean(0)
+        else:
+            means = np.zeros(4)
+        H["global_train_losses"].append(float(means[0]))
+        H["global_train_accuracies"].append(float(means[1]))
+        H["global_val_losses"].append(float(means[2]))
+        H["global_val_accuracies"].append(float(means[3]))
+
+        # ---- end-of-global-epoch aggregation (reference schedule, A27)
+        if sync_every == "global_epoch":
+            aggregator(model)
+        elif sync_every == "step" and aggregation_by == "weights":
+            aggregator(model)
+
+        if rank == 0 and progress and verbose:
+            print(f"[global epoch {global_epoch + 1}] train loss {means[0]:.4f} acc {means[1]:.2f}% | "
+                  f"val loss {means[2]:.4f} acc {means[3]:.2f}%")
+
+        # ---- sync + timing + re-partition (A30, A15/A16)
+        comm.barrier()
+        duration = time.perf_counter() - t_start
+        if repartition and prev_fraction + next_fraction > 0:
+            if partition_rule == "reference_duration":
+                td = torch.tensor([duration], dtype=torch.float64, device=dev)
+                comm.all_reduce(td, SUM)
+                share = duration / max(td.item(), 1e-12)
+            else:
+                dts = comm.all_gather(torch.tensor([duration], dtype=torch.float64, device=dev))
+                from ..data.partition import shares_from_durations
+
+                share = shares_from_durations([float(d.item()) for d in dts], partition_rule)[rank]
+            trainloader, val_loader, indices_train, indices_val = get_subset_loaders(
+                trainset, valset, indices_train, indices_val, batch_size, prev_fraction, next_fraction, share, dev,
+                rng, replace, fixed_classes, fixed_ratio, dtype=dtype,
+                augment=getattr(trainloader, "augment", False))
+        if logger is not None:
+            logger.log(kind="global_epoch", global_epoch=global_epoch + 1, duration_s=duration,
+                       train_loss=H["global_train_losses"][-1], train_acc=H["global_train_accuracies"][-1],
+                       val_loss=H["global_val_losses"][-1], val_acc=H["global_val_accuracies"][-1],
+                       n_local_epochs_done=len(records), cut_by_time_limit=cutoff.cut,
+                       shard_size=len(indices_train))
+        if checkpointer is not None:
+            checkpointer.save(global_epoch + 1, model, optimizer, scheduler, H,
+                              extra=dict(indices_train=np.asarray(indices_train),
+                                         indices_val=np.asarray(indices_val), fixed_classes=fixed_classes,
+                                         rng_state=rng.bit_generator.state))
+    train_global.last_loaders = (trainloader, val_loader, indices_train, indices_val)
+    return (H["all_workers_losses"], H["all_epochs_losses"], H["global_epoch_losses"], H["global_epoch_accuracies"],
+            H["global_train_losses"], H["global_train_accuracies"], H["global_val_losses"],
+            H["global_val_accuracies"], H["worker_specific_train_losses"], H["worker_specific_train_accuracies"],
+            H["worker_specific_val_losses"], H["worker_specific_val_accuracies"])

@@ -25,18 +25,31 @@ from __future__ import annotations
 
 from dataclasses import dataclass
 
+import weakref
+
 import torch
 import torch.nn as nn
 
 _ALIGN = 64
 
+# id(param) -> FlatParams that owns it (lets optimizers find the flat buffers)
+_OWNER: "weakref.WeakValueDictionary[int, FlatParams]" = weakref.WeakValueDictionary()
+
+
+def owner_of(p: nn.Parameter):
+    return _OWNER.get(id(p))
+
 
 def _pad_rows(shape: torch.Size, multiple: int = 8) -> tuple:
+    """Padded storage shape: leading dim to a multiple of 8 and, for 2-D
+    (Linear) weights, the inner dim too, so every GEMM operand row is a whole
+    number of 16-byte vectors."""
     if len(shape) == 0:
         return tuple(shape)
-    rows = shape[0]
-    prow = (rows + multiple - 1) // multiple * multiple
-    return (prow,) + tuple(shape[1:])
+    up = lambda v: (v + multiple - 1) // multiple * multiple  # noqa: E731
+    if len(shape) == 2:
+        return (up(shape[0]), up(shape[1]))
+    return (up(shape[0]),) + tuple(shape[1:])
 
 
 @dataclass
@@ -92,6 +105,9 @@ class FlatParams:
         # gradient-readiness notification: native ops call notify() after writing a
         # weight gradient; params handled by stock torch ops signal through autograd.
         self._ready_hooks: list = []
+        self.grad_scale = 1.0  # set to 1/N by data parallelism; consumed by the fused optimizers
+        for s in segs:
+            _OWNER[id(s.param)] = self
         for s in segs:
             s.param.register_post_accumulate_grad_hook(lambda p: self.notify(p))
         for m in module.modules():
@@ -119,6 +135,8 @@ class FlatParams:
         shape = tuple(seg.param.shape)
         if len(shape) == 0:
             return storage
+        if len(shape) == 2:
+            return storage[: shape[0], : shape[1]]
         return storage[: shape[0]]
 
     def seg(self, p: nn.Parameter) -> Segment:
