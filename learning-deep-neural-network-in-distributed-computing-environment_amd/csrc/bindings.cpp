@@ -41,7 +41,7 @@ int64_t ld_of(const at::Tensor& t, const char* name) {
 //   a: if a_kcontig, [M][K] else [K][M];  b: if b_kcontig, [N][K] else [K][N];  c: [M][N]
 void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, bool a_kcontig, bool b_kcontig,
           int64_t epi, const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& aux,
-          const c10::optional<at::Tensor>& dbias, double beta, int64_t tile) {
+          const c10::optional<at::Tensor>& dbias, double beta, int64_t tile, int64_t splitk) {
   check_dev(a, at::kBFloat16, "a");
   check_dev(b, at::kBFloat16, "b");
   TORCH_CHECK(c.is_cuda() && (c.scalar_type() == at::kBFloat16 || c.scalar_type() == at::kFloat),
@@ -91,9 +91,19 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, bool a_
     TORCH_CHECK(dbias->is_contiguous() && dbias->numel() >= N, "gemm: bad dbias");
     p.dbias = dbias->data_ptr<float>();
   }
+  const bool skinny_ok = a_kcontig && b_kcontig && !out_f32 && N <= 64 && !dbias.has_value() && beta == 0.0 &&
+                         (epi == ldnn::EPI_NONE || epi == ldnn::EPI_BIAS || epi == ldnn::EPI_BIAS_RELU ||
+                          epi == ldnn::EPI_BIAS_SIGMOID);
+  if (tile == 0) tile = skinny_ok && K >= 256 ? 16 : ldnn::gemm_pick_tile(p.M, p.N, p.K);
+  TORCH_CHECK(tile == 16 || tile == 128 || tile == 256, "gemm: tile must be 0 (auto), 16 (skinny-N), 128 or 256");
   c10::hip::HIPGuardMasqueradingAsCUDA g(a.device());
-  if (tile == 0) tile = ldnn::gemm_pick_tile(p.M, p.N, p.K);
-  TORCH_CHECK(tile == 128 || tile == 256, "gemm: tile must be 0 (auto), 128 or 256");
+  if (tile == 16) {
+    TORCH_CHECK(skinny_ok, "gemm: the skinny-N kernel needs k-contiguous operands, bf16 out, N <= 64");
+    check(ldnn::gemm_skinny_n(p, (int)epi, cur_stream(a)), "gemm_skinny_n");
+    return;
+  }
+  if (tile == 128 && out_f32 && epi == ldnn::EPI_NONE && !dbias.has_value() && (beta == 0.0 || beta == 1.0))
+    p.splitk = splitk > 0 ? (int)splitk : ldnn::gemm_pick_splitk(p.M, p.N, p.K);
   check(ldnn::gemm_bf16_tile(p, a_kcontig, b_kcontig, (int)epi, out_f32, (int)tile, cur_stream(a)), "gemm");
 }
 
@@ -275,7 +285,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm", &gemm, "bf16 MFMA GEMM with fused epilogue", py::arg("a"), py::arg("b"), py::arg("c"),
         py::arg("a_kcontig"), py::arg("b_kcontig"), py::arg("epi") = 0, py::arg("bias") = py::none(),
         py::arg("aux") = py::none(), py::arg("dbias") = py::none(), py::arg("beta") = 0.0,
-        py::arg("tile") = 0);
+        py::arg("tile") = 0, py::arg("splitk") = 0);
   m.def("act_fwd", &act_fwd);
   m.def("act_bwd", &act_bwd);
   m.def("colsum", &colsum, py::arg("x"), py::arg("out"), py::arg("accumulate") = false);

@@ -26,6 +26,7 @@ struct GemmParams {
   int M, N, K;
   int lda, ldb, ldc, ldaux;
   float beta;            // fp32 output only: C = acc + beta * C
+  int splitk;            // >1: K split over gridDim.y, fp32 atomics into C (EPI_NONE, fp32 out, 128-tile)
 };
 
 // Picks the tiling (256x256 LDS-DMA kernel or 128x128 kernel) from the shape.
@@ -35,6 +36,11 @@ hipError_t gemm_bf16(const GemmParams& p, bool a_kcontig, bool b_kcontig, int ep
 hipError_t gemm_bf16_tile(const GemmParams& p, bool a_kcontig, bool b_kcontig, int epi, bool out_f32, int tile,
                           hipStream_t s);
 int gemm_pick_tile(int M, int N, int K);
+// Split-K factor the 128-tile kernel uses for an fp32 EPI_NONE output (1 = none).
+int gemm_pick_splitk(int M, int N, int K);
+// Skinny-N forward GEMM (N <= 64, both operands k-contiguous, bf16 out): one
+// 16-row strip per workgroup, K split over its 4 waves, reduced in LDS.
+hipError_t gemm_skinny_n(const GemmParams& p, int epi, hipStream_t s);
 constexpr size_t kOOBLimit = 0x80000000ull;
 
 // ---- elementwise / activations (bf16 storage, fp32 math) ---------------------

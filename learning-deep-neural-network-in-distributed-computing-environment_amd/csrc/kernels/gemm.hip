@@ -265,10 +265,15 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(GemmParams p) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) acc[j][i] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = (p.K + BK - 1) / BK;
+  // split-K: this workgroup covers K-tiles [kt0, kt1)
+  const int nk_all = (p.K + BK - 1) / BK;
+  const int per = (nk_all + gridDim.y - 1) / gridDim.y;
+  const int kt0 = blockIdx.y * per;
+  const int nk = max(0, min(nk_all, kt0 + per) - kt0);
+  const int kbase = kt0 * BK;
   u32x4 ra[4], rb[4];
-  load_tile<A_KC>(ra, p.A, p.lda, p.M, p.K, m0, 0, tid);
-  load_tile<B_KC>(rb, p.B, p.ldb, p.N, p.K, n0, 0, tid);
+  load_tile<A_KC>(ra, p.A, p.lda, p.M, p.K, m0, kbase, tid);
+  load_tile<B_KC>(rb, p.B, p.ldb, p.N, p.K, n0, kbase, tid);
   store_tile<A_KC>(ra, smem, tid);
   store_tile<B_KC>(rb, smem + kTileBytes, tid);
   __syncthreads();
@@ -277,8 +282,8 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(GemmParams p) {
     const int cur = kt & 1;
     const bool more = (kt + 1) < nk;
     if (more) {
-      load_tile<A_KC>(ra, p.A, p.lda, p.M, p.K, m0, (kt + 1) * BK, tid);
-      load_tile<B_KC>(rb, p.B, p.ldb, p.N, p.K, n0, (kt + 1) * BK, tid);
+      load_tile<A_KC>(ra, p.A, p.lda, p.M, p.K, m0, kbase + (kt + 1) * BK, tid);
+      load_tile<B_KC>(rb, p.B, p.ldb, p.N, p.K, n0, kbase + (kt + 1) * BK, tid);
     }
     const char* la = smem + cur * 2 * kTileBytes;
     const char* lb = la + kTileBytes;
@@ -301,6 +306,24 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(GemmParams p) {
       store_tile<B_KC>(rb, nb + kTileBytes, tid);
     }
     __syncthreads();
+  }
+  if constexpr (OUT_F32 && EPI == EPI_NONE) {
+    if (gridDim.y > 1) {  // split-K partial: fp32 atomics (C pre-zeroed or accumulated into)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = n0 + wn * 64 + j * 16 + 4 * (lane >> 4);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int m = m0 + wm * 64 + i * 16 + (lane & 15);
+          if (n < p.N && m < p.M) {
+            float* c = reinterpret_cast<float*>(p.C) + (size_t)m * p.ldc + n;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) atomicAdd(c + r, acc[j][i][r]);
+          }
+        }
+      }
+      return;
+    }
   }
   epilogue<EPI, OUT_F32, 4, 4>(p, acc, m0 + wm * 64, n0 + wn * 64, lane);
 }
@@ -428,11 +451,78 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(GemmParams p) {
 }  // namespace k256
 
 
+
+// =============================================================================
+// skinny-N forward GEMM (classifier heads: N <= 64, e.g. 10 classes padded to 16)
+// With N this small a 128x128 tile wastes 7/8 of every MFMA and a 4096x16
+// output has only 32 tiles, so the K loop runs on 32 CUs (latency-bound).
+// Here a workgroup owns a 16-row strip of C; its 4 waves split K in interleaved
+// 32-deep steps, load their fragments straight from global/L2 into registers
+// (operands are read once: no LDS staging pays), and reduce their partial
+// accumulators through LDS before the shared fused epilogue.
+// =============================================================================
+namespace skinny {
+
+constexpr int kW = 8;  // waves per workgroup (K split 8 ways: more loads in flight per strip)
+
+template <int NT, int EPI>
+__global__ __launch_bounds__(kW * 64) void kernel(GemmParams p) {
+  __shared__ floatx4 red[kW - 1][NT][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int m0 = blockIdx.x * 16;
+  const int row = m0 + (lane & 15);
+  const int kq = 8 * (lane >> 4);
+  floatx4 acc[NT][1];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) acc[j][0] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const int nsteps = (p.K + 31) / 32;
+  const bf16x8 zero = {};
+#pragma unroll 8
+  for (int st = w; st < nsteps; st += kW) {
+    const int k = st * 32 + kq;
+    const bool kok = k < p.K;
+    const bf16x8 a = (row < p.M && kok) ? *reinterpret_cast<const bf16x8*>(p.A + (size_t)row * p.lda + k) : zero;
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const int n = j * 16 + (lane & 15);
+      const bf16x8 b = (n < p.N && kok) ? *reinterpret_cast<const bf16x8*>(p.B + (size_t)n * p.ldb + k) : zero;
+      acc[j][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b, a, acc[j][0], 0, 0, 0);
+    }
+  }
+  if (w > 0) {
+#pragma unroll
+    for (int j = 0; j < NT; ++j) red[w - 1][j][lane] = acc[j][0];
+  }
+  __syncthreads();
+  if (w == 0) {
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int q = 0; q < kW - 1; ++q) acc[j][0] += red[q][j][lane];
+    epilogue<EPI, false, 1, NT>(p, acc, m0, 0, lane);
+  }
+}
+
+template <int NT>
+hipError_t launch_nt(const GemmParams& p, int epi, hipStream_t s) {
+  dim3 grid((p.M + 15) / 16), block(kW * 64);
+  switch (epi) {
+    case EPI_NONE: kernel<NT, EPI_NONE><<<grid, block, 0, s>>>(p); break;
+    case EPI_BIAS: kernel<NT, EPI_BIAS><<<grid, block, 0, s>>>(p); break;
+    case EPI_BIAS_RELU: kernel<NT, EPI_BIAS_RELU><<<grid, block, 0, s>>>(p); break;
+    case EPI_BIAS_SIGMOID: kernel<NT, EPI_BIAS_SIGMOID><<<grid, block, 0, s>>>(p); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace skinny
+
 template <int TILE, bool A_KC, bool B_KC, bool OUT_F32>
 hipError_t dispatch_epi(const GemmParams& p, int epi, hipStream_t s) {
   constexpr int T = TILE == 128 ? 128 : 256;
   const int tiles = ((p.M + T - 1) / T) * ((p.N + T - 1) / T);
-  dim3 grid(tiles);
+  dim3 grid(tiles, TILE == 128 ? max(1, p.splitk) : 1);
 #define LDNN_GEMM_CASE(E)                                                                          \
   case E:                                                                                          \
     if constexpr (TILE == 256)                                                                     \
@@ -474,6 +564,16 @@ int gemm_pick_tile(int M, int N, int K) {
   return 128;
 }
 
+int gemm_pick_splitk(int M, int N, int K) {
+  const int tiles = ((M + 127) / 128) * ((N + 127) / 128);
+  // fp32 atomics run at ~1.3 TB/s chip-wide: only worth it when the grid is tiny
+  if (tiles >= 128) return 1;
+  int sk = (512 + tiles - 1) / tiles;  // aim at ~2 workgroups per CU
+  const int max_by_k = K / 512;        // keep >= 8 K-tiles per split
+  if (sk > max_by_k) sk = max_by_k;
+  return sk < 2 ? 1 : (sk > 32 ? 32 : sk);
+}
+
 hipError_t gemm_bf16(const GemmParams& p, bool a_kcontig, bool b_kcontig, int epi, bool out_f32,
                      hipStream_t s) {
   return gemm_bf16_tile(p, a_kcontig, b_kcontig, epi, out_f32, gemm_pick_tile(p.M, p.N, p.K), s);
@@ -489,7 +589,32 @@ hipError_t gemm_bf16_tile(const GemmParams& p, bool a_kcontig, bool b_kcontig, i
     if (abytes >= kOOBLimit || bbytes >= kOOBLimit) tile = 128;
   }
   if (tile == 256) return dispatch_layout<256>(p, a_kcontig, b_kcontig, epi, out_f32, s);
-  return dispatch_layout<128>(p, a_kcontig, b_kcontig, epi, out_f32, s);
+  GemmParams q = p;
+  if (q.splitk > 1) {
+    if (!(out_f32 && epi == EPI_NONE && q.dbias == nullptr)) return hipErrorInvalidValue;
+    if (q.beta == 0.f) {
+      hipError_t e = hipMemset2DAsync(q.C, (size_t)q.ldc * 4, 0, (size_t)q.N * 4, q.M, s);
+      if (e != hipSuccess) return e;
+    } else if (q.beta != 1.f) {
+      return hipErrorInvalidValue;  // split-K accumulates: beta must be 0 or 1
+    }
+  }
+  return dispatch_layout<128>(q, a_kcontig, b_kcontig, epi, out_f32, s);
+}
+
+}  // namespace ldnn
+
+namespace ldnn {
+
+hipError_t gemm_skinny_n(const GemmParams& p, int epi, hipStream_t s) {
+  if (p.M <= 0 || p.N <= 0) return hipSuccess;
+  if (p.N > 64) return hipErrorInvalidValue;
+  switch ((p.N + 15) / 16) {
+    case 1: return skinny::launch_nt<1>(p, epi, s);
+    case 2: return skinny::launch_nt<2>(p, epi, s);
+    case 3: return skinny::launch_nt<3>(p, epi, s);
+    default: return skinny::launch_nt<4>(p, epi, s);
+  }
 }
 
 }  // namespace ldnn

@@ -5,7 +5,7 @@
 // .item() host syncs (loss and correct count are accumulated on the device).
 // It also emits the last Linear layer's bias gradient (column sums of dlogits).
 //
-// One wave per row (lanes stride over classes), 4 waves per block, 64 rows per
+// One wave per row (lanes stride over classes), 4 waves per block, 16 rows per
 // block; per-block partials are combined in LDS and added with one atomic per
 // statistic / bias column.
 #include "ldnn_common.h"
@@ -15,7 +15,7 @@ namespace ldnn {
 
 namespace {
 
-constexpr int kRowsPerBlock = 64;
+constexpr int kRowsPerBlock = 16;  // 4 rows per wave: B = 4096 -> 256 blocks fill the chip
 constexpr int kMaxColsPerLane = 16;  // C <= 1024
 
 __global__ __launch_bounds__(256) void xent_kernel(const bf16_t* __restrict__ logits,
@@ -103,12 +103,103 @@ __global__ __launch_bounds__(256) void xent_kernel(const bf16_t* __restrict__ lo
   }
 }
 
+
+// Small class counts (ld <= 64, e.g. 10 classes padded to 16): one ROW PER LANE.
+// A lane reads its whole row with 16-B loads and needs no cross-lane reduction,
+// so a 4096-row batch is one load round trip instead of a chain of wave
+// shuffles per row.  Column sums for the bias gradient: per-column wave
+// reduction, then one atomic per column per wave.
+template <int LD>
+__global__ __launch_bounds__(256) void xent_rows_kernel(const bf16_t* __restrict__ logits,
+                                                        const int64_t* __restrict__ labels,
+                                                        bf16_t* __restrict__ dlogits, float* __restrict__ stats,
+                                                        float* __restrict__ dbias, int B, int C, int ld,
+                                                        float grad_scale) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool ok = r < B;
+  float x[LD];
+  float loss = 0.f, correct = 0.f;
+  float g[LD];
+#pragma unroll
+  for (int c = 0; c < LD; ++c) g[c] = 0.f;
+  if (ok) {
+    const u16x8* row = reinterpret_cast<const u16x8*>(logits + (size_t)r * ld);
+#pragma unroll
+    for (int v = 0; v < LD / 8; ++v) {
+      const u16x8 q = row[v];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[v * 8 + j] = bf2f(q[j]);
+    }
+    const int lab = (int)labels[r];
+    float mx = -INFINITY;
+    int am = 0;
+#pragma unroll
+    for (int c = 0; c < LD; ++c)
+      if (c < C && x[c] > mx) { mx = x[c]; am = c; }
+    float se = 0.f, xl = 0.f;
+#pragma unroll
+    for (int c = 0; c < LD; ++c)
+      if (c == lab) xl = x[c];
+#pragma unroll
+    for (int c = 0; c < LD; ++c) {
+      if (c < C) {
+        x[c] = __expf(x[c] - mx);
+        se += x[c];
+      }
+    }
+    loss = mx + __logf(se) - xl;  // = logsumexp - x_label
+    correct = (am == lab) ? 1.f : 0.f;
+    const float inv = 1.f / se;
+    u16x8 out[LD / 8];
+#pragma unroll
+    for (int c = 0; c < LD; ++c) {
+      float v = 0.f;
+      if (c < C) v = (x[c] * inv - (c == lab ? 1.f : 0.f)) * grad_scale;
+      const uint16_t b = f2bf(v);
+      out[c / 8][c % 8] = b;
+      g[c] = bf2f(b);
+    }
+    u16x8* drow = reinterpret_cast<u16x8*>(dlogits + (size_t)r * ld);
+#pragma unroll
+    for (int v = 0; v < LD / 8; ++v) drow[v] = out[v];
+  }
+  const int lane = threadIdx.x & 63;
+  loss = wave_sum(loss);
+  correct = wave_sum(correct);
+  if (lane == 0) {
+    atomicAdd(stats + 0, loss);
+    atomicAdd(stats + 1, correct);
+  }
+  if (dbias) {
+#pragma unroll
+    for (int c = 0; c < LD; ++c) {
+      const float t = wave_sum(g[c]);
+      if (lane == 0) atomicAdd(dbias + c, t);
+    }
+  }
+}
+
 }  // namespace
 
 hipError_t softmax_xent(const uint16_t* logits, const int64_t* labels, uint16_t* dlogits, float* stats,
                         float* dbias, int B, int C, int ld, float grad_scale, hipStream_t s) {
   if (ld > kMaxColsPerLane * 64 || C > ld) return hipErrorInvalidValue;
   if (B <= 0) return hipSuccess;
+  const bool vec_ok = (ld % 8 == 0) && ((reinterpret_cast<uintptr_t>(logits) | reinterpret_cast<uintptr_t>(dlogits)) & 15) == 0;
+  if (vec_ok && ld <= 64) {
+    const int g = (B + 255) / 256;
+    switch (ld) {
+      case 8: xent_rows_kernel<8><<<g, 256, 0, s>>>(logits, labels, dlogits, stats, dbias, B, C, ld, grad_scale); break;
+      case 16: xent_rows_kernel<16><<<g, 256, 0, s>>>(logits, labels, dlogits, stats, dbias, B, C, ld, grad_scale); break;
+      case 24: xent_rows_kernel<24><<<g, 256, 0, s>>>(logits, labels, dlogits, stats, dbias, B, C, ld, grad_scale); break;
+      case 32: xent_rows_kernel<32><<<g, 256, 0, s>>>(logits, labels, dlogits, stats, dbias, B, C, ld, grad_scale); break;
+      case 40: xent_rows_kernel<40><<<g, 256, 0, s>>>(logits, labels, dlogits, stats, dbias, B, C, ld, grad_scale); break;
+      case 48: xent_rows_kernel<48><<<g, 256, 0, s>>>(logits, labels, dlogits, stats, dbias, B, C, ld, grad_scale); break;
+      case 56: xent_rows_kernel<56><<<g, 256, 0, s>>>(logits, labels, dlogits, stats, dbias, B, C, ld, grad_scale); break;
+      default: xent_rows_kernel<64><<<g, 256, 0, s>>>(logits, labels, dlogits, stats, dbias, B, C, ld, grad_scale); break;
+    }
+    return hipGetLastError();
+  }
   const int g = (B + kRowsPerBlock - 1) / kRowsPerBlock;
   xent_kernel<<<g, 256, 0, s>>>(logits, labels, dlogits, stats, dbias, B, C, ld, grad_scale);
   return hipGetLastError();

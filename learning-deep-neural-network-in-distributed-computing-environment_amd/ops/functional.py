@@ -58,7 +58,9 @@ class _LinearActNative(torch.autograd.Function):
             # pad columns must be 0 so the weight-gradient pad columns stay exactly 0
             # (the producer's pad may hold e.g. sigmoid(0) = 0.5)
             x2 = _padded_rows_view(x2, kpad)
-            x2[:, K:].zero_()
+            # through .data: the producer saved this buffer for its own backward and
+            # its pad columns never influence that backward (their gradient is 0)
+            x2.data[:, K:].zero_()
         y = torch.empty(x2.shape[0], npad, dtype=torch.bfloat16, device=x.device)
         if bias is not None:
             b = flat.master_storage(bias)

@@ -183,3 +183,37 @@ def test_mix3_and_colsum_and_act():
     C().act_bwd(xb, y, dx, C().ACT_SIGMOID)
     yf = y.float()
     torch.testing.assert_close(dx.float(), xb.float() * yf * (1 - yf), rtol=2e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("splitk", [2, 5, 8])
+@pytest.mark.parametrize("beta", [0.0, 1.0])
+def test_gemm_splitk_wgrad(splitk, beta):
+    torch.manual_seed(11)
+    B, N, K = 4096, 16, 784  # dW[N,K] = dY^T X, skinny M -> split the batch reduction
+    dy = torch.randn(B, N, device="cuda").bfloat16()
+    x = torch.randn(B, K, device="cuda").bfloat16()
+    dw = torch.randn(N, K, device="cuda")
+    base = dw.clone()
+    C().gemm(dy, x, dw, False, False, beta=beta, tile=128, splitk=splitk)
+    ref = beta * base + dy.float().t() @ x.float()
+    torch.testing.assert_close(dw, ref, rtol=1e-4, atol=2e-2)
+
+
+@pytest.mark.parametrize("N", [10, 16, 40, 64])
+@pytest.mark.parametrize("epi", ["none", "bias", "relu"])
+def test_gemm_skinny_n_forward(N, epi):
+    torch.manual_seed(12)
+    M, K = 1000, 4096
+    npad = (N + 7) // 8 * 8
+    x = torch.randn(M, K, device="cuda").bfloat16()
+    w = (torch.randn(npad, K, device="cuda") * 0.02).bfloat16()
+    bias = torch.randn(npad, device="cuda")
+    y = torch.empty(M, npad, device="cuda", dtype=torch.bfloat16)
+    code = {"none": C().EPI_NONE, "bias": C().EPI_BIAS, "relu": C().EPI_BIAS_RELU}[epi]
+    C().gemm(x, w, y, True, True, code, bias=bias if epi != "none" else None, tile=16)
+    ref = x.float() @ w.float().t()
+    if epi != "none":
+        ref = ref + bias
+    if epi == "relu":
+        ref = ref.relu()
+    torch.testing.assert_close(y.float(), ref, rtol=2e-2, atol=2e-2)

@@ -18,6 +18,8 @@ def test_native_linear_autograd(act):
     lin = Linear(200, 84, activation=act)  # 84 -> padded rows, 200 in
     ref = torch.nn.Linear(200, 84)
     ref.load_state_dict(lin.state_dict())
+    with torch.no_grad():  # same bf16-rounded weights, so ReLU masks agree with the kernel's
+        ref.weight.copy_(ref.weight.bfloat16().float())
     flat = ldnn.prepare(lin, "cuda")
     ref = ref.cuda()
     x = torch.randn(96, 200, device="cuda")
@@ -30,7 +32,9 @@ def test_native_linear_autograd(act):
     yr = {"relu": torch.relu, "sigmoid": torch.sigmoid, "none": lambda t: t}[act](yr)
     yr.backward(g)
     torch.testing.assert_close(y.float(), yr, rtol=3e-2, atol=3e-2)
-    torch.testing.assert_close(lin.weight.grad, ref.weight.grad, rtol=3e-2, atol=5e-2)
+    # weight grads: the kernel sums bf16-rounded output gradients; compare relative to the scale
+    scale = ref.weight.grad.abs().max()
+    assert ((lin.weight.grad - ref.weight.grad).abs().max() / scale).item() < 2e-2
     torch.testing.assert_close(lin.bias.grad, ref.bias.grad, rtol=3e-2, atol=5e-2)
     torch.testing.assert_close(xb.grad.float(), xr.grad, rtol=3e-2, atol=3e-2)
     assert flat.grad_storage(lin.weight)[84:].abs().max().item() == 0.0
