@@ -145,9 +145,10 @@ def main():
     ap.add_argument("--bucket-elems", type=int, default=8 << 20)
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--compare-stock", action="store_true")
+    ap.add_argument("--backend", default="auto", help="auto (nccl = RCCL on GPUs) | gloo (testing only)")
     args = ap.parse_args()
 
-    ctx = D.setup()
+    ctx = D.setup(None if args.backend == "auto" else args.backend)
     n = ctx.world_size
     el, extra = run_ldnn(ctx, args)
     ms = el / args.steps * 1e3

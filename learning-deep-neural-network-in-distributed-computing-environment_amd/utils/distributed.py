@@ -52,9 +52,13 @@ def setup(backend: str | None = None, timeout_s: float = 600.0, device: str | No
     rank = env_int("RANK", 0)
     world = env_int("WORLD_SIZE", 1)
     local = env_int("LOCAL_RANK", 0)
-    use_cuda = torch.cuda.device_count() > 0 and device != "cpu"
+    ndev = torch.cuda.device_count()
+    use_cuda = ndev > 0 and device != "cpu"
+    if backend is None:
+        backend = os.environ.get("LDNN_BACKEND") or None
     if device is None or device == "auto":
-        dev = torch.device(f"cuda:{local}") if use_cuda else torch.device("cpu")
+        # one process per GPU; more ranks than GPUs (test oversubscription) wrap around
+        dev = torch.device(f"cuda:{local % ndev}") if use_cuda else torch.device("cpu")
     else:
         dev = torch.device(device if device != "cuda" else f"cuda:{local}")
     if dev.type == "cuda":
