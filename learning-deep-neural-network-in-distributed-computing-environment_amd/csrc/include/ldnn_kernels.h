@@ -50,6 +50,8 @@ hipError_t act_bwd(const uint16_t* dy, const uint16_t* y, uint16_t* dx, int64_t 
 // dbias[c] (+)= sum_r x[r][c] over a [rows][cols] bf16 matrix (ld = cols)
 hipError_t colsum_bf16(const uint16_t* x, float* out, int rows, int cols, bool accumulate, hipStream_t s);
 hipError_t cast_f32_bf16(const float* x, uint16_t* y, int64_t n, hipStream_t s);
+// graph-capture-safe zero fill of a strided fp32 block (instead of hipMemset2DAsync)
+hipError_t zero2d_f32(float* p, int rows, int cols, int ld, hipStream_t s);
 hipError_t cast_bf16_f32(const uint16_t* x, float* y, int64_t n, hipStream_t s);
 // y = a*x + b*y1 + c*y2 (fp32, in place on x allowed); optional bf16 shadow of y
 hipError_t mix3_f32(float* out, const float* x, const float* y1, const float* y2, float a, float b, float c,

@@ -99,6 +99,18 @@ __global__ void colsum_kernel(const bf16_t* __restrict__ x, float* __restrict__ 
   }
 }
 
+// Zero a [rows][cols] fp32 block with row stride ld.  A kernel, not
+// hipMemset2DAsync: memset nodes captured into hipGraphs are not replayed
+// reliably on this stack (found while validating graph-captured split-K wgrads).
+__global__ void zero2d_kernel(float* __restrict__ p, int rows, int cols, int ld) {
+  const int64_t n = (int64_t)rows * cols;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride) {
+    const int r = (int)(i / cols), c = (int)(i % cols);
+    p[(size_t)r * ld + c] = 0.f;
+  }
+}
+
 __global__ void cast_f32_bf16_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, int64_t n) {
   const int64_t nv = n / 4;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -178,9 +190,15 @@ hipError_t act_bwd(const uint16_t* dy, const uint16_t* y, uint16_t* dx, int64_t 
   return hipGetLastError();
 }
 
+hipError_t zero2d_f32(float* p, int rows, int cols, int ld, hipStream_t s) {
+  if (rows <= 0 || cols <= 0) return hipSuccess;
+  zero2d_kernel<<<grid_for((int64_t)rows * cols), kBlock, 0, s>>>(p, rows, cols, ld);
+  return hipGetLastError();
+}
+
 hipError_t colsum_bf16(const uint16_t* x, float* out, int rows, int cols, bool accumulate, hipStream_t s) {
   if (!accumulate) {
-    hipError_t e = hipMemsetAsync(out, 0, sizeof(float) * cols, s);
+    hipError_t e = zero2d_f32(out, 1, cols, cols, s);
     if (e != hipSuccess) return e;
   }
   if (rows <= 0 || cols <= 0) return hipSuccess;

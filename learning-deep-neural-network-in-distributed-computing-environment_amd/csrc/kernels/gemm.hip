@@ -593,7 +593,7 @@ hipError_t gemm_bf16_tile(const GemmParams& p, bool a_kcontig, bool b_kcontig, i
   if (q.splitk > 1) {
     if (!(out_f32 && epi == EPI_NONE && q.dbias == nullptr)) return hipErrorInvalidValue;
     if (q.beta == 0.f) {
-      hipError_t e = hipMemset2DAsync(q.C, (size_t)q.ldc * 4, 0, (size_t)q.N * 4, q.M, s);
+      hipError_t e = zero2d_f32(reinterpret_cast<float*>(q.C), q.M, q.N, q.ldc, s);
       if (e != hipSuccess) return e;
     } else if (q.beta != 1.f) {
       return hipErrorInvalidValue;  // split-K accumulates: beta must be 0 or 1

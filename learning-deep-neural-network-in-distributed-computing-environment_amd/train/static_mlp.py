@@ -63,10 +63,16 @@ class _Segment:
             return
         if self.graph is None:
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            # thread_local: other host threads (RCCL / gloo progress, watchdogs) may keep
+            # using the HIP runtime while this thread captures
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
                 self.fn()
             self.graph = g
         self.graph.replay()
+
+    @property
+    def will_capture(self) -> bool:
+        return self.use_graph and self.graph is None and self.calls >= self.warmup
 
 
 class StaticMLPEngine:
@@ -220,11 +226,19 @@ class StaticMLPEngine:
         if self.world == 1:
             self.segments[0]()
             return
+        # A step that captures a graph runs its collectives synchronously: no
+        # collective may be in flight (touching the grad buffers from another
+        # stream / thread) while a segment is being captured.
+        capturing = any(s.will_capture for s in self.segments + self.opt_segments)
         works = []
         for i, seg in enumerate(self.segments):
             seg()
             b, e, _ = self.buckets[self._cut_buckets[i]]
-            works.append(dist.all_reduce(self.flat.grad[b:e], group=self.pg, async_op=True))
+            w = dist.all_reduce(self.flat.grad[b:e], group=self.pg, async_op=True)
+            if capturing:
+                w.wait()
+                torch.cuda.current_stream().synchronize()
+            works.append(w)
         for w, oseg in zip(works, self.opt_segments):
             w.wait()
             oseg()

@@ -23,22 +23,31 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--backend", default="gloo")
     ap.add_argument("--graphs", type=int, default=1)
+    ap.add_argument("--hidden", type=int, default=512)
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--cap", type=int, default=1 << 17)
+    ap.add_argument("--steps", type=int, default=6)
     a = ap.parse_args()
     ctx = D.setup(a.backend)
     N, r = ctx.world_size, ctx.rank
-    B, H = 256, 512
+    B, H = a.batch, a.hidden
     torch.manual_seed(0)
     model = mlp3(784, H, 10)
     # small bucket cap -> several buckets / segments on the multi-rank path
     eng = StaticMLPEngine(model, B, OptimConfig("sgd", lr=0.05, momentum=0.9), device=ctx.device, world_size=N,
-                          bucket_cap_elems=1 << 17, use_graphs=bool(a.graphs))
-    assert N == 1 or len(eng.buckets) >= 2, eng.buckets
+                          bucket_cap_elems=a.cap, use_graphs=bool(a.graphs))
+    print(f"rank {r}: buckets {eng.buckets}", flush=True)
     g = torch.Generator(device="cpu").manual_seed(5)
-    xs = [torch.randn(N * B, 784, generator=g) for _ in range(6)]
-    ys = [torch.randint(0, 10, (N * B,), generator=g) for _ in range(6)]
-    for i in range(6):
+    S = a.steps
+    xs = [torch.randn(N * B, 784, generator=g) for _ in range(S)]
+    ys = [torch.randint(0, 10, (N * B,), generator=g) for _ in range(S)]
+    for i in range(S):
+        eng.reset_stats()
         eng.load_batch(xs[i][r * B:(r + 1) * B].to(ctx.device).bfloat16(), ys[i][r * B:(r + 1) * B].to(ctx.device))
         eng.step()
+        torch.cuda.synchronize()
+        print(f"rank {r} step {i} loss {eng.read_stats(B)[0]:.5f} finite={bool(torch.isfinite(eng.flat.master).all())}",
+              flush=True)
     torch.cuda.synchronize()
     got = eng.flat.master.detach().cpu().clone()
     if r == 0:
@@ -46,7 +55,7 @@ def main():
         torch.manual_seed(0)
         ref = StaticMLPEngine(mlp3(784, H, 10), N * B, OptimConfig("sgd", lr=0.05, momentum=0.9),
                               device=ctx.device, world_size=1, use_graphs=False)
-        for i in range(6):
+        for i in range(S):
             ref.load_batch(xs[i].to(ctx.device).bfloat16(), ys[i].to(ctx.device))
             ref.step()
         torch.cuda.synchronize()
