@@ -270,6 +270,69 @@ void synth_labels(const at::Tensor& y, int64_t classes, int64_t seed) {
         "synth_labels");
 }
 
+ldnn::ConvShape conv_shape(const at::Tensor& x, const at::Tensor& w, const at::Tensor& y, int64_t stride,
+                           int64_t pad) {
+  // x [N][H][W][C], w [K][R][S][C], y [N][P][Q][K]  (bf16, dense, C % 8 == K % 8 == 0)
+  TORCH_CHECK(x.dim() == 4 && w.dim() == 4 && y.dim() == 4, "conv: NHWC / KRSC 4-D tensors expected");
+  TORCH_CHECK(x.is_contiguous() && w.is_contiguous() && y.is_contiguous(), "conv: tensors must be dense NHWC/KRSC");
+  ldnn::ConvShape s{};
+  s.N = (int)x.size(0); s.H = (int)x.size(1); s.W = (int)x.size(2); s.C = (int)x.size(3);
+  s.K = (int)w.size(0); s.R = (int)w.size(1); s.S = (int)w.size(2);
+  s.P = (int)y.size(1); s.Q = (int)y.size(2);
+  s.stride = (int)stride; s.pad = (int)pad;
+  TORCH_CHECK(w.size(3) == s.C && y.size(0) == s.N && y.size(3) == s.K, "conv: shape mismatch");
+  TORCH_CHECK(s.C % 8 == 0 && s.K % 8 == 0, "conv: channel counts must be padded to multiples of 8");
+  TORCH_CHECK(s.P == (s.H + 2 * s.pad - s.R) / s.stride + 1 && s.Q == (s.W + 2 * s.pad - s.S) / s.stride + 1,
+              "conv: output size inconsistent with stride/padding");
+  TORCH_CHECK(aligned16(x.data_ptr()) && aligned16(w.data_ptr()) && aligned16(y.data_ptr()), "conv: alignment");
+  return s;
+}
+
+void conv_fwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& y, int64_t stride, int64_t pad,
+              const c10::optional<at::Tensor>& bias, int64_t epi) {
+  check_dev(x, at::kBFloat16, "x");
+  check_dev(w, at::kBFloat16, "w");
+  check_dev(y, at::kBFloat16, "y");
+  ldnn::ConvShape s = conv_shape(x, w, y, stride, pad);
+  const float* b = nullptr;
+  if (bias.has_value()) {
+    check_dev(*bias, at::kFloat, "bias");
+    TORCH_CHECK(bias->numel() >= s.K && aligned16(bias->data_ptr()), "conv: bad bias");
+    b = bias->data_ptr<float>();
+  }
+  TORCH_CHECK(epi == ldnn::EPI_NONE || b != nullptr, "conv: bias epilogue needs a bias");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  check(ldnn::conv2d_fwd(s, bf16_ptr(x), bf16_ptr(w), bf16_mut(y), b, (int)epi, cur_stream(x)), "conv2d_fwd");
+}
+
+void conv_dgrad(const at::Tensor& dy, const at::Tensor& w, const at::Tensor& dx, int64_t stride, int64_t pad) {
+  check_dev(dy, at::kBFloat16, "dy");
+  check_dev(w, at::kBFloat16, "w");
+  check_dev(dx, at::kBFloat16, "dx");
+  ldnn::ConvShape s = conv_shape(dx, w, dy, stride, pad);
+  c10::hip::HIPGuardMasqueradingAsCUDA g(dy.device());
+  check(ldnn::conv2d_dgrad(s, bf16_ptr(dy), bf16_ptr(w), bf16_mut(dx), cur_stream(dy)), "conv2d_dgrad");
+}
+
+void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& dw, int64_t stride, int64_t pad,
+                double beta) {
+  check_dev(dy, at::kBFloat16, "dy");
+  check_dev(x, at::kBFloat16, "x");
+  check_dev(dw, at::kFloat, "dw");
+  TORCH_CHECK(dw.dim() == 4 && dw.is_contiguous(), "conv_wgrad: dw must be a dense [K][R][S][C] fp32 tensor");
+  ldnn::ConvShape s{};
+  TORCH_CHECK(x.dim() == 4 && dy.dim() == 4 && x.is_contiguous() && dy.is_contiguous(), "conv_wgrad: layout");
+  s.N = (int)x.size(0); s.H = (int)x.size(1); s.W = (int)x.size(2); s.C = (int)x.size(3);
+  s.K = (int)dw.size(0); s.R = (int)dw.size(1); s.S = (int)dw.size(2);
+  s.P = (int)dy.size(1); s.Q = (int)dy.size(2);
+  s.stride = (int)stride; s.pad = (int)pad;
+  TORCH_CHECK(dw.size(3) == s.C && dy.size(3) == s.K && dy.size(0) == s.N, "conv_wgrad: shape mismatch");
+  TORCH_CHECK(s.C % 8 == 0 && s.K % 8 == 0, "conv_wgrad: channels must be multiples of 8");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(dy.device());
+  check(ldnn::conv2d_wgrad(s, bf16_ptr(dy), bf16_ptr(x), dw.data_ptr<float>(), (float)beta, cur_stream(dy)),
+        "conv2d_wgrad");
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_C, m) {
@@ -301,6 +364,11 @@ PYBIND11_MODULE(_C, m) {
         py::arg("shadow"), py::arg("hp"), py::arg("grad_scale"), py::arg("beta1"), py::arg("beta2"),
         py::arg("eps"), py::arg("weight_decay"), py::arg("decoupled"));
   m.def("bump_step", &bump_step);
+  m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("stride"), py::arg("pad"),
+        py::arg("bias") = py::none(), py::arg("epi") = 0);
+  m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("stride"), py::arg("pad"));
+  m.def("conv_wgrad", &conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("dw"), py::arg("stride"), py::arg("pad"),
+        py::arg("beta") = 0.0);
   m.def("synth_normal", &synth_normal);
   m.def("synth_labels", &synth_labels);
 }

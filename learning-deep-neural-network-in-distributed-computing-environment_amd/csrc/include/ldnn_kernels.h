@@ -43,6 +43,19 @@ int gemm_pick_splitk(int M, int N, int K);
 hipError_t gemm_skinny_n(const GemmParams& p, int epi, hipStream_t s);
 constexpr size_t kOOBLimit = 0x80000000ull;
 
+// ---- implicit-GEMM convolution (conv.hip): NHWC activations, KRSC weights, C/K % 8 == 0
+struct ConvShape {
+  int N, H, W, C;   // input (C padded to a multiple of 8)
+  int K, R, S;      // output channels (padded to a multiple of 8), filter
+  int P, Q;         // output spatial size
+  int stride, pad;
+};
+hipError_t conv2d_fwd(const ConvShape& s, const uint16_t* x, const uint16_t* w, uint16_t* y, const float* bias,
+                      int epi, hipStream_t st);
+hipError_t conv2d_dgrad(const ConvShape& s, const uint16_t* dy, const uint16_t* w, uint16_t* dx, hipStream_t st);
+hipError_t conv2d_wgrad(const ConvShape& s, const uint16_t* dy, const uint16_t* x, float* dw, float beta,
+                        hipStream_t st);
+
 // ---- elementwise / activations (bf16 storage, fp32 math) ---------------------
 enum Act : int { ACT_RELU = 0, ACT_SIGMOID = 1 };
 hipError_t act_fwd(const uint16_t* x, uint16_t* y, int64_t n, int act, hipStream_t s);

@@ -1,0 +1,309 @@
+// Implicit-GEMM 2-D convolution for gfx950: forward,
+// backward-data (dgrad) and backward-weight (wgrad) as bf16 MFMA GEMMs whose
+// operand tiles are GATHERED from NHWC activations while they are staged into
+// LDS -- no im2col buffer is ever materialised.
+//
+// Layouts (channels innermost, padded to a multiple of 8 so every gather is a
+// 16-byte vector of 8 channels):
+//   x  [N][H][W][C]      activations (NHWC, bf16)
+//   w  [K][R][S][C]      weights (KRSC, the bf16 shadow of the fp32 master)
+//   y  [N][P][Q][K]      outputs (NHWC)
+//
+// GEMM views (M x Ngemm, reduction Kd):
+//   fwd   y [NPQ][K]   = A(m=npq, k=rsc) . B(k=rsc, n=k_out)   A gathered from x (zero padding = zeros),
+//                                                            B = w as a [K][RSC] k-contiguous matrix
+//   dgrad dx[NHW][C]   = A(m=nhw, k=rsk) . B(k=rsk, n=c)      A gathered from dy: p = (h+pad-r)/stride
+//                                                            when divisible (zero-insertion form of the
+//                                                            transposed conv, handles stride 2 exactly),
+//                                                            B gathered from w rows (k,r,s)
+//   wgrad dw[K][RSC]   = A(m=k_out, k=npq) . B(k=npq, n=rsc)  A = dy as a [NPQ][K] matrix (k-strided),
+//                                                            B gathered from x; fp32 out, split-K over NPQ
+//
+// The main loop is the 128x128x64 register-staged MFMA tile of gemm.hip (same
+// LDS images, fragment reads and fused epilogue), with the global address of
+// each 16-byte chunk produced by a per-operand gather policy.
+#include "ldnn_common.h"
+#include "ldnn_gemm_tile.h"
+#include "ldnn_kernels.h"
+
+namespace ldnn {
+
+namespace {
+
+struct ConvArgs {
+  ConvShape s;
+  const bf16_t* x;
+  const bf16_t* w;
+  const bf16_t* dy;
+  void* out;
+  const float* bias;
+  int M, N, Kd;  // GEMM view
+  int ldc;
+  float beta;
+};
+
+// ---- gather policies: at(a, row, k) -> address of 8 consecutive elements, or null (= zeros)
+// KC policies: the 8 elements run along the reduction dim k (fixed GEMM row).
+// Strided policies: the 8 elements run along the GEMM row dim (fixed k).
+
+struct FwdA {  // x gathered, row = output pixel npq, k = (r, s, c)
+  static constexpr bool KC = true;
+  __device__ static const bf16_t* at(const ConvArgs& a, int m, int k) {
+    const ConvShape& s = a.s;
+    const int q = m % s.Q, t = m / s.Q, p = t % s.P, n = t / s.P;
+    const int c = k % s.C, rs = k / s.C, r = rs / s.S, sx = rs % s.S;
+    const int ih = p * s.stride - s.pad + r, iw = q * s.stride - s.pad + sx;
+    if (ih < 0 || ih >= s.H || iw < 0 || iw >= s.W) return nullptr;
+    return a.x + (((size_t)n * s.H + ih) * s.W + iw) * s.C + c;
+  }
+};
+
+struct FwdB {  // weights [K][RSC]
+  static constexpr bool KC = true;
+  __device__ static const bf16_t* at(const ConvArgs& a, int n, int k) {
+    return a.w + (size_t)n * a.Kd + k;
+  }
+};
+
+struct DgradA {  // dy gathered, row = input pixel nhw, k = (r, s, kout)
+  static constexpr bool KC = true;
+  __device__ static const bf16_t* at(const ConvArgs& a, int m, int k) {
+    const ConvShape& s = a.s;
+    const int wq = m % s.W, t = m / s.W, h = t % s.H, n = t / s.H;
+    const int ko = k % s.K, rs = k / s.K, r = rs / s.S, sx = rs % s.S;
+    const int ph = h + s.pad - r, pw = wq + s.pad - sx;
+    if (ph < 0 || pw < 0) return nullptr;
+    if (s.stride > 1 && ((ph % s.stride) || (pw % s.stride))) return nullptr;
+    const int p = ph / s.stride, q = pw / s.stride;
+    if (p >= s.P || q >= s.Q) return nullptr;
+    return a.dy + (((size_t)n * s.P + p) * s.Q + q) * s.K + ko;
+  }
+};
+
+struct DgradB {  // weights: k = (r, s, kout) row, 8 consecutive input channels
+  static constexpr bool KC = false;
+  __device__ static const bf16_t* at(const ConvArgs& a, int c, int k) {
+    const ConvShape& s = a.s;
+    const int ko = k % s.K, rs = k / s.K, r = rs / s.S, sx = rs % s.S;
+    return a.w + (((size_t)ko * s.R + r) * s.S + sx) * s.C + c;
+  }
+};
+
+struct WgradA {  // dy as [NPQ][K]: k = npq, 8 consecutive output channels
+  static constexpr bool KC = false;
+  __device__ static const bf16_t* at(const ConvArgs& a, int m, int k) { return a.dy + (size_t)k * a.s.K + m; }
+};
+
+struct WgradB {  // x gathered: k = npq, 8 consecutive j = (r, s, c..c+7)
+  static constexpr bool KC = false;
+  __device__ static const bf16_t* at(const ConvArgs& a, int j, int k) {
+    const ConvShape& s = a.s;
+    const int q = k % s.Q, t = k / s.Q, p = t % s.P, n = t / s.P;
+    const int c = j % s.C, rs = j / s.C, r = rs / s.S, sx = rs % s.S;
+    const int ih = p * s.stride - s.pad + r, iw = q * s.stride - s.pad + sx;
+    if (ih < 0 || ih >= s.H || iw < 0 || iw >= s.W) return nullptr;
+    return a.x + (((size_t)n * s.H + ih) * s.W + iw) * s.C + c;
+  }
+};
+
+constexpr int BM = 128, BN = 128;
+constexpr int kThreads = 256;
+constexpr int kTileBytes = 128 * BK * 2;
+
+template <class OP>
+__device__ __forceinline__ void load_tile(u32x4 (&r)[4], const ConvArgs& a, int rows, int r0, int k0, int tid) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = tid + kThreads * i;
+    int row, k;
+    if constexpr (OP::KC) {
+      k = (c & 7) * 8;
+      row = c >> 3;
+    } else {
+      const int half = c & 1, klo = (c >> 1) & 3, rb = (c >> 3) & 7, khi = c >> 6;
+      k = khi * 4 + klo;
+      row = rb * 16 + half * 8;
+    }
+    const int gr = r0 + row, gk = k0 + k;
+    const bf16_t* ptr = (gr < rows && gk < a.Kd) ? OP::at(a, gr, gk) : nullptr;
+    r[i] = ptr ? *reinterpret_cast<const u32x4*>(ptr) : u32x4{0u, 0u, 0u, 0u};
+  }
+}
+
+template <bool KC>
+__device__ __forceinline__ void store_tile(const u32x4 (&r)[4], char* lds, int tid) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = tid + kThreads * i;
+    int row, k;
+    if constexpr (KC) {
+      k = (c & 7) * 8;
+      row = c >> 3;
+    } else {
+      const int half = c & 1, klo = (c >> 1) & 3, rb = (c >> 3) & 7, khi = c >> 6;
+      k = khi * 4 + klo;
+      row = rb * 16 + half * 8;
+    }
+    *reinterpret_cast<u32x4*>(lds + lds_offset<KC, 128>(row, k)) = r[i];
+  }
+}
+
+template <class OA, class OB, int EPI, bool OUT_F32>
+__global__ __launch_bounds__(kThreads, 2) void conv_gemm_kernel(ConvArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[4 * kTileBytes];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  int m0, n0;
+  tile_coords(a.M, a.N, BM, BN, m0, n0);
+
+  floatx4 acc[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[j][i] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk_all = (a.Kd + BK - 1) / BK;
+  const int per = (nk_all + gridDim.y - 1) / gridDim.y;
+  const int kt0 = blockIdx.y * per;
+  const int nk = max(0, min(nk_all, kt0 + per) - kt0);
+  const int kbase = kt0 * BK;
+  u32x4 ra[4], rb[4];
+  load_tile<OA>(ra, a, a.M, m0, kbase, tid);
+  load_tile<OB>(rb, a, a.N, n0, kbase, tid);
+  store_tile<OA::KC>(ra, smem, tid);
+  store_tile<OB::KC>(rb, smem + kTileBytes, tid);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    const bool more = (kt + 1) < nk;
+    if (more) {
+      load_tile<OA>(ra, a, a.M, m0, kbase + (kt + 1) * BK, tid);
+      load_tile<OB>(rb, a, a.N, n0, kbase + (kt + 1) * BK, tid);
+    }
+    const char* la = smem + cur * 2 * kTileBytes;
+    const char* lb = la + kTileBytes;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 fa[4], fb[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[i] = read_frag<OA::KC, 128>(la, wm * 4 + i, kk, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j] = read_frag<OB::KC, 128>(lb, wn * 4 + j, kk, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[j][i], 0, 0, 0);
+    }
+    if (more) {
+      char* nb = smem + (cur ^ 1) * 2 * kTileBytes;
+      store_tile<OA::KC>(ra, nb, tid);
+      store_tile<OB::KC>(rb, nb + kTileBytes, tid);
+    }
+    __syncthreads();
+  }
+  if constexpr (OUT_F32 && EPI == EPI_NONE) {
+    if (gridDim.y > 1) {  // split-K partial sums
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = n0 + wn * 64 + j * 16 + 4 * (lane >> 4);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int m = m0 + wm * 64 + i * 16 + (lane & 15);
+          if (n < a.N && m < a.M) {
+            float* c = reinterpret_cast<float*>(a.out) + (size_t)m * a.ldc + n;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) atomicAdd(c + r, acc[j][i][r]);
+          }
+        }
+      }
+      return;
+    }
+  }
+  GemmParams p{};
+  p.C = a.out;
+  p.M = a.M;
+  p.N = a.N;
+  p.ldc = a.ldc;
+  p.bias = a.bias;
+  p.beta = a.beta;
+  epilogue<EPI, OUT_F32, 4, 4>(p, acc, m0 + wm * 64, n0 + wn * 64, lane);
+}
+
+inline int splitk_for(int tiles, int Kd) {
+  if (tiles >= 128) return 1;
+  int sk = (512 + tiles - 1) / tiles;
+  const int max_by_k = Kd / 512;
+  if (sk > max_by_k) sk = max_by_k;
+  return sk < 2 ? 1 : (sk > 64 ? 64 : sk);
+}
+
+}  // namespace
+
+hipError_t conv2d_fwd(const ConvShape& s, const uint16_t* x, const uint16_t* w, uint16_t* y, const float* bias,
+                      int epi, hipStream_t st) {
+  ConvArgs a{};
+  a.s = s;
+  a.x = x;
+  a.w = w;
+  a.out = y;
+  a.bias = bias;
+  a.M = s.N * s.P * s.Q;
+  a.N = s.K;
+  a.Kd = s.R * s.S * s.C;
+  a.ldc = s.K;
+  if (a.M <= 0) return hipSuccess;
+  const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
+  dim3 grid(tiles), block(kThreads);
+  switch (epi) {
+    case EPI_NONE: conv_gemm_kernel<FwdA, FwdB, EPI_NONE, false><<<grid, block, 0, st>>>(a); break;
+    case EPI_BIAS: conv_gemm_kernel<FwdA, FwdB, EPI_BIAS, false><<<grid, block, 0, st>>>(a); break;
+    case EPI_BIAS_RELU: conv_gemm_kernel<FwdA, FwdB, EPI_BIAS_RELU, false><<<grid, block, 0, st>>>(a); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t conv2d_dgrad(const ConvShape& s, const uint16_t* dy, const uint16_t* w, uint16_t* dx, hipStream_t st) {
+  ConvArgs a{};
+  a.s = s;
+  a.dy = dy;
+  a.w = w;
+  a.out = dx;
+  a.M = s.N * s.H * s.W;
+  a.N = s.C;
+  a.Kd = s.R * s.S * s.K;
+  a.ldc = s.C;
+  if (a.M <= 0) return hipSuccess;
+  const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
+  conv_gemm_kernel<DgradA, DgradB, EPI_NONE, false><<<dim3(tiles), dim3(kThreads), 0, st>>>(a);
+  return hipGetLastError();
+}
+
+hipError_t conv2d_wgrad(const ConvShape& s, const uint16_t* dy, const uint16_t* x, float* dw, float beta,
+                        hipStream_t st) {
+  ConvArgs a{};
+  a.s = s;
+  a.dy = dy;
+  a.x = x;
+  a.out = dw;
+  a.M = s.K;
+  a.N = s.R * s.S * s.C;
+  a.Kd = s.N * s.P * s.Q;
+  a.ldc = a.N;
+  a.beta = beta;
+  const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
+  const int sk = splitk_for(tiles, a.Kd);
+  if (sk > 1) {
+    if (beta == 0.f) {
+      hipError_t e = zero2d_f32(dw, a.M, a.N, a.ldc, st);
+      if (e != hipSuccess) return e;
+    } else if (beta != 1.f) {
+      return hipErrorInvalidValue;
+    }
+  }
+  conv_gemm_kernel<WgradA, WgradB, EPI_NONE, true><<<dim3(tiles, sk), dim3(kThreads), 0, st>>>(a);
+  return hipGetLastError();
+}
+
+}  // namespace ldnn

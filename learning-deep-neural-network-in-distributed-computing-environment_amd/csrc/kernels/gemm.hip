@@ -45,152 +45,12 @@
 //   output into fp32 `dbias` (bias gradient of the previous layer, one atomic
 //   per column per wave), optional beta-accumulate for fp32 outputs.
 #include "ldnn_common.h"
+#include "ldnn_gemm_tile.h"
 #include "ldnn_kernels.h"
 
 namespace ldnn {
 
 namespace {
-
-constexpr int BK = 64;
-constexpr int GROUP_M = 8;
-
-typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
-typedef __attribute__((address_space(3))) void lds_void;
-
-// ---- LDS image addressing --------------------------------------------------
-// KC image:      [ROWS][64 k], 128-B rows, chunk' = chunk ^ (row & 7)
-// strided image: [8 kb][ROWS/16 rb][8 k][16 r], 256-B blocks, odd kb: k ^= 4
-template <bool KC, int ROWS>
-__device__ __forceinline__ int lds_offset(int row, int k) {
-  if constexpr (KC) {
-    return row * 128 + ((((k >> 3) ^ (row & 7))) << 4) + (k & 7) * 2;
-  } else {
-    const int kb = k >> 3, rb = row >> 4;
-    const int rowp = (k & 7) ^ ((kb & 1) << 2);
-    return (kb * (ROWS / 16) + rb) * 256 + rowp * 32 + (row & 15) * 2;
-  }
-}
-
-// Inverse map: which (row, k) lands at 16-B LDS slot `o` (o multiple of 16).
-template <bool KC, int ROWS>
-__device__ __forceinline__ void lds_slot_to_rk(int o, int& row, int& k) {
-  if constexpr (KC) {
-    row = o >> 7;
-    const int pch = (o >> 4) & 7;
-    k = (pch ^ (row & 7)) * 8;
-  } else {
-    const int blk = o >> 8;
-    const int kb = blk / (ROWS / 16), rb = blk % (ROWS / 16);
-    const int rowp = (o >> 5) & 7, half = (o >> 4) & 1;
-    k = kb * 8 + (rowp ^ ((kb & 1) << 2));
-    row = rb * 16 + half * 8;
-  }
-}
-
-// ---- fragment read: 16 rows (row tile rt) x 8 consecutive k (k-sub kk) ------
-// Lane l gets row (l & 15), k = kk*32 + 8*(l >> 4) + j, j = 0..7: the operand map
-// of v_mfma_f32_16x16x32_bf16 for both its A and its B operand.
-template <bool KC, int ROWS>
-__device__ __forceinline__ bf16x8 read_frag(const char* lds, int rt, int kk, int lane) {
-  if constexpr (KC) {
-    const int row = rt * 16 + (lane & 15);
-    const int chunk = kk * 4 + (lane >> 4);
-    return *reinterpret_cast<const bf16x8*>(lds + row * 128 + ((chunk ^ (row & 7)) << 4));
-  } else {
-    const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
-    const int kb = kk * 4 + g;
-    const int sw = (kb & 1) << 2;
-    const char* blk = lds + (kb * (ROWS / 16) + rt) * 256;
-    const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(blk + ((q ^ sw) * 32) + p * 8));
-    const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(blk + (((4 + q) ^ sw) * 32) + p * 8));
-    return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  }
-}
-
-template <int EPI>
-__device__ __forceinline__ float apply_epi(float v, float bias, float aux) {
-  if constexpr (EPI == EPI_BIAS) return v + bias;
-  if constexpr (EPI == EPI_BIAS_RELU) return fmaxf(v + bias, 0.f);
-  if constexpr (EPI == EPI_BIAS_SIGMOID) return 1.f / (1.f + __expf(-(v + bias)));
-  if constexpr (EPI == EPI_DRELU) return aux > 0.f ? v : 0.f;
-  if constexpr (EPI == EPI_DSIGMOID) return v * aux * (1.f - aux);
-  return v;
-}
-
-// Tile id -> (tm, tn): XCD remap, then GROUP_M-row groups for L2 reuse.
-__device__ __forceinline__ void tile_coords(int M, int N, int BMt, int BNt, int& m0, int& n0) {
-  const int tiles_m = (M + BMt - 1) / BMt, tiles_n = (N + BNt - 1) / BNt;
-  const int nwg = tiles_m * tiles_n;
-  const int id = xcd_remap(blockIdx.x, nwg);
-  const int per_group = GROUP_M * tiles_n;
-  const int group = id / per_group;
-  const int first_m = group * GROUP_M;
-  const int gsize = min(tiles_m - first_m, GROUP_M);
-  m0 = (first_m + (id % per_group) % gsize) * BMt;
-  n0 = ((id % per_group) / gsize) * BNt;
-}
-
-// ---- shared epilogue: acc[j][i] is the 16x16 tile (n-tile j, m-tile i) -----
-// Processed one n-tile at a time (sched_barrier keeps the compiler from hoisting
-// every bias/aux load of the tile up front), with the optional bias-gradient
-// column sum reduced and atomically added per n-tile, so only a handful of
-// registers are live beside the accumulators.
-template <int EPI, bool OUT_F32, int MT, int NT>
-__device__ __forceinline__ void epilogue(const GemmParams& p, floatx4 (&acc)[NT][MT], int mbase, int nbase,
-                                         int lane) {
-  const bool do_dbias = p.dbias != nullptr;
-#pragma unroll
-  for (int j = 0; j < NT; ++j) {
-    __builtin_amdgcn_sched_barrier(0);
-    const int n = nbase + j * 16 + 4 * (lane >> 4);
-    const bool nok = n < p.N;  // N % 8 == 0 is enforced on the host
-    floatx4 bias = {0.f, 0.f, 0.f, 0.f};
-    if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_RELU || EPI == EPI_BIAS_SIGMOID) {
-      if (nok) bias = *reinterpret_cast<const floatx4*>(p.bias + n);
-    }
-    floatx4 cs = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int i = 0; i < MT; ++i) {
-      const int m = mbase + i * 16 + (lane & 15);
-      if (nok && m < p.M) {
-        floatx4 aux = {0.f, 0.f, 0.f, 0.f};
-        if constexpr (EPI == EPI_DRELU || EPI == EPI_DSIGMOID) {
-          const u16x4 a4 = *reinterpret_cast<const u16x4*>(p.aux + (size_t)m * p.ldaux + n);
-          aux = floatx4{bf2f(a4[0]), bf2f(a4[1]), bf2f(a4[2]), bf2f(a4[3])};
-        }
-        floatx4 v;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = apply_epi<EPI>(acc[j][i][r], bias[r], aux[r]);
-        if constexpr (OUT_F32) {
-          float* c = reinterpret_cast<float*>(p.C) + (size_t)m * p.ldc + n;
-          if (p.beta != 0.f) v = v + p.beta * *reinterpret_cast<const floatx4*>(c);
-          *reinterpret_cast<floatx4*>(c) = v;
-          cs += v;
-        } else {
-          const u16x4 o{f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
-          *reinterpret_cast<u16x4*>(reinterpret_cast<bf16_t*>(p.C) + (size_t)m * p.ldc + n) = o;
-          cs += floatx4{bf2f(o[0]), bf2f(o[1]), bf2f(o[2]), bf2f(o[3])};
-        }
-      }
-    }
-    if (do_dbias) {
-      // reduce over the 16 lanes that share (lane >> 4), i.e. over m
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float t = cs[r];
-        t += __shfl_xor(t, 1, 64);
-        t += __shfl_xor(t, 2, 64);
-        t += __shfl_xor(t, 4, 64);
-        t += __shfl_xor(t, 8, 64);
-        cs[r] = t;
-      }
-      if ((lane & 15) == 0 && nok) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) atomicAdd(p.dbias + n + r, cs[r]);
-      }
-    }
-  }
-}
 
 // =============================================================================
 // gemm128: register-staged, 128x128x64, 4 waves

@@ -53,11 +53,19 @@ class CrossEntropyLoss(nn.CrossEntropyLoss):
 
 
 class Conv2d(nn.Conv2d):
-    """nn.Conv2d (reference key names and init); on the GPU the activations flow in
-    bf16 through the native implicit-GEMM conv kernels when built, else MIOpen."""
+    """nn.Conv2d (reference key names and init).  On the GPU the activations flow as
+    NHWC bf16 through the native implicit-GEMM conv kernels (conv.hip), with the
+    weights read from the FlatParams KRSC bf16 shadow; an optional ReLU is fused
+    into the conv epilogue."""
+
+    def __init__(self, *args, activation: str = "none", **kwargs):
+        super().__init__(*args, **kwargs)
+        assert activation in ("none", "relu")
+        self.activation = activation
+        self._ldnn_flat = None
 
     def forward(self, x):
-        return LF.conv2d(x, self)
+        return LF.conv2d(x, self, relu=self.activation == "relu")
 
 
 class BatchNorm2d(nn.BatchNorm2d):

@@ -118,13 +118,24 @@ def linear_act(x, weight, bias=None, act: str = "none", flat=None):
     return y
 
 
+def _flat_dense(t: torch.Tensor) -> torch.Tensor | None:
+    """A 1-D view over the storage of a dense tensor (row-major or channels_last)."""
+    if t.is_contiguous():
+        return t.view(-1)
+    if t.dim() == 4 and t.is_contiguous(memory_format=torch.channels_last):
+        return t.permute(0, 2, 3, 1).reshape(-1)
+    return None
+
+
 class _ActNative(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, act):
         C = _ext.C()
-        xb = _to_bf16(x).contiguous()
-        y = torch.empty_like(xb)
-        C.act_fwd(xb, y, act)
+        xb = x if x.dtype == torch.bfloat16 else x.to(torch.bfloat16)
+        if _flat_dense(xb) is None:
+            xb = xb.contiguous()
+        y = torch.empty_like(xb)  # keeps the memory format (channels_last stays NHWC)
+        C.act_fwd(_flat_dense(xb), _flat_dense(y), act)
         ctx.save_for_backward(y)
         ctx.act = act
         ctx.in_dtype = x.dtype
@@ -133,9 +144,12 @@ class _ActNative(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gy):
         (y,) = ctx.saved_tensors
-        g = _to_bf16(gy).contiguous()
+        g = gy if gy.dtype == torch.bfloat16 else gy.to(torch.bfloat16)
+        if g.stride() != y.stride():
+            g = g.contiguous(memory_format=torch.channels_last) if y.dim() == 4 and not y.is_contiguous() \
+                else g.contiguous()
         dx = torch.empty_like(y)
-        _ext.C().act_bwd(g, y, dx, ctx.act)
+        _ext.C().act_bwd(_flat_dense(g), _flat_dense(y), _flat_dense(dx), ctx.act)
         return dx.to(ctx.in_dtype), None
 
 
@@ -195,16 +209,95 @@ def cross_entropy(logits, labels, stats: torch.Tensor | None = None):
 
 
 # ------------------------------------------------------------------ conv / BN
-def conv2d(x, mod):
-    """Convolution of module `mod` (nn.Conv2d parameters).  GPU: bf16 activations,
-    fp32 master weights cast in-graph (autograd returns fp32 weight grads into the
-    FlatParams buffer).  CPU: fp32 reference."""
-    if x.is_cuda and not _ext._DISABLED:
-        xb = x if x.dtype == torch.bfloat16 else x.to(torch.bfloat16)
-        w = mod.weight.to(torch.bfloat16)
-        b = mod.bias.to(torch.bfloat16) if mod.bias is not None else None
-        return F.conv2d(xb, w, b, mod.stride, mod.padding, mod.dilation, mod.groups)
-    return F.conv2d(x.float(), mod.weight, mod.bias, mod.stride, mod.padding, mod.dilation, mod.groups)
+def _up8(v: int) -> int:
+    return (v + 7) // 8 * 8
+
+
+def as_nhwc(t: torch.Tensor, cp: int, zero_pad: bool = True) -> torch.Tensor:
+    """Logical [N, C, H, W] tensor -> dense NHWC bf16 buffer [N, H, W, cp].
+
+    Channels-last tensors (ours, or torch's channels_last outputs) are widened
+    in place when their channel stride already is cp; anything else is copied
+    into a zero-padded buffer."""
+    N, C, H, W = t.shape
+    if (t.dtype == torch.bfloat16 and t.stride(1) == 1 and t.stride(3) == cp and t.stride(2) == W * cp
+            and t.stride(0) == H * W * cp):
+        buf = t.as_strided((N, H, W, cp), (H * W * cp, W * cp, cp, 1), t.storage_offset())
+        if zero_pad and cp > C:
+            buf.data[..., C:].zero_()
+        return buf
+    buf = torch.zeros(N, H, W, cp, dtype=torch.bfloat16, device=t.device) if cp > C else \
+        torch.empty(N, H, W, cp, dtype=torch.bfloat16, device=t.device)
+    buf[..., :C].copy_(t.permute(0, 2, 3, 1))
+    return buf
+
+
+def nchw_view(buf: torch.Tensor, c: int) -> torch.Tensor:
+    """Dense NHWC buffer -> logical [N, c, H, W] view (channels_last strides)."""
+    return buf[..., :c].permute(0, 3, 1, 2)
+
+
+class _Conv2dNative(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, stride, pad, flat, relu):
+        C = _ext.C()
+        K, Cin, R, S = weight.shape
+        w = flat.shadow_storage(weight)  # [Kp][R][S][Cp]
+        kp, cp = w.shape[0], w.shape[3]
+        xb = as_nhwc(x, cp)
+        N, H, W, _ = xb.shape
+        P, Q = (H + 2 * pad - R) // stride + 1, (W + 2 * pad - S) // stride + 1
+        y = torch.empty(N, P, Q, kp, dtype=torch.bfloat16, device=x.device)
+        b = flat.master_storage(bias) if bias is not None else None
+        epi = (C.EPI_BIAS_RELU if relu else C.EPI_BIAS) if b is not None else C.EPI_NONE
+        if relu and b is None:
+            b = torch.zeros(kp, dtype=torch.float32, device=x.device)
+            epi = C.EPI_BIAS_RELU
+        C.conv_fwd(xb, w, y, stride, pad, b, epi)
+        ctx.save_for_backward(xb, y)
+        ctx.meta = (stride, pad, flat, weight, bias, relu, Cin, x.dtype)
+        return nchw_view(y, K)
+
+    @staticmethod
+    def backward(ctx, gy):
+        C = _ext.C()
+        xb, y = ctx.saved_tensors
+        stride, pad, flat, weight, bias, relu, Cin, in_dtype = ctx.meta
+        kp = y.shape[3]
+        g = as_nhwc(gy if gy.dtype == torch.bfloat16 else gy.to(torch.bfloat16), kp)
+        if relu:
+            gz = torch.empty_like(g)
+            C.act_bwd(g.contiguous(), y, gz, 0)
+            g = gz
+        C.conv_wgrad(g, xb, flat.grad_storage(weight), stride, pad, 1.0)
+        if bias is not None:
+            C.colsum(g.view(-1, kp), flat.grad_storage(bias), True)
+        flat.notify(weight, bias)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dxb = torch.empty_like(xb)
+            C.conv_dgrad(g, flat.shadow_storage(weight), dxb, stride, pad)
+            dx = nchw_view(dxb, Cin)
+            if in_dtype != torch.bfloat16:
+                dx = dx.to(in_dtype)
+        return dx, None, None, None, None, None, None
+
+
+def conv2d(x, mod, relu: bool = False):
+    """Convolution of module `mod` (nn.Conv2d parameters).  GPU: native implicit-GEMM
+    kernels on NHWC bf16 activations and KRSC bf16 weights (groups=1, dilation=1);
+    CPU: the fp32 reference."""
+    if _ext.use_native(x):
+        flat = getattr(mod, "_ldnn_flat", None)
+        ok = (flat is not None and flat.shadow is not None and mod.groups == 1 and mod.dilation == (1, 1)
+              and mod.stride[0] == mod.stride[1] and mod.padding[0] == mod.padding[1]
+              and isinstance(mod.padding, tuple))
+        if not ok:
+            raise RuntimeError("native conv needs groups=1, dilation=1, square stride/padding and "
+                               "the model attached to FlatParams (ldnn.prepare(model))")
+        return _Conv2dNative.apply(x, mod.weight, mod.bias, mod.stride[0], mod.padding[0], flat, relu)
+    y = F.conv2d(x.float(), mod.weight, mod.bias, mod.stride, mod.padding, mod.dilation, mod.groups)
+    return F.relu(y) if relu else y
 
 
 def batch_norm2d(x, mod):

@@ -14,7 +14,9 @@ reference key names such as ``prep.0.weight`` / ``fc.bias``), with
 * per-parameter padded *storage* views: a parameter whose leading dim is not a
   multiple of 8 (e.g. the 10-class classifier) gets zero rows of padding so the
   GEMM never needs a scalar tail; the padding stays exactly zero because its
-  gradient is always zero.
+  gradient is always zero.  Conv weights are stored KRSC (channels innermost,
+  K and C padded to 8) -- the layout the implicit-GEMM conv kernels read --
+  while the Parameter keeps the reference's [K][C][R][S] shape as a permuted view.
 
 Segments are 64-element aligned (256 B fp32 / 128 B bf16) so every view is
 16-byte aligned for vector loads.  The order of segments is the order in which
@@ -49,6 +51,9 @@ def _pad_rows(shape: torch.Size, multiple: int = 8) -> tuple:
     up = lambda v: (v + multiple - 1) // multiple * multiple  # noqa: E731
     if len(shape) == 2:
         return (up(shape[0]), up(shape[1]))
+    if len(shape) == 4:  # conv weight [K][C][R][S] stored KRSC with K and C padded
+        k, c, r, s = shape
+        return (up(k), r, s, up(c))
     return (up(shape[0]),) + tuple(shape[1:])
 
 
@@ -137,6 +142,8 @@ class FlatParams:
             return storage
         if len(shape) == 2:
             return storage[: shape[0], : shape[1]]
+        if len(shape) == 4:  # KRSC storage -> the reference's [K][C][R][S] view
+            return storage[: shape[0], :, :, : shape[1]].permute(0, 3, 1, 2)
         return storage[: shape[0]]
 
     def seg(self, p: nn.Parameter) -> Segment:
