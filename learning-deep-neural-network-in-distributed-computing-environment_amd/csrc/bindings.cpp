@@ -333,6 +333,137 @@ void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& dw,
         "conv2d_wgrad");
 }
 
+float* fptr_opt(const c10::optional<at::Tensor>& t, int64_t n, const char* name) {
+  if (!t.has_value()) return nullptr;
+  check_dev(*t, at::kFloat, name);
+  TORCH_CHECK(t->is_contiguous() && t->numel() >= n, name, ": bad tensor");
+  return t->data_ptr<float>();
+}
+
+// x, y, residual: dense [M][C] bf16 (NHWC flattened); stats: [C] fp32; ws: fp32 [4C + 2C]
+void bn_fwd(const at::Tensor& x, const at::Tensor& y, const c10::optional<at::Tensor>& residual,
+            const c10::optional<at::Tensor>& gamma, const c10::optional<at::Tensor>& beta,
+            const c10::optional<at::Tensor>& running_mean, const c10::optional<at::Tensor>& running_var,
+            const at::Tensor& save_mean, const at::Tensor& save_invstd, const at::Tensor& ws, double eps,
+            double momentum, bool training, bool relu) {
+  check_dev(x, at::kBFloat16, "x");
+  check_dev(y, at::kBFloat16, "y");
+  TORCH_CHECK(x.dim() == 2 && x.is_contiguous() && y.sizes() == x.sizes() && y.is_contiguous(), "bn: [M][C] dense");
+  const int64_t M = x.size(0), C = x.size(1);
+  TORCH_CHECK(C % 8 == 0, "bn: C must be a multiple of 8");
+  ldnn::BnArgs a{};
+  a.x = bf16_ptr(x);
+  a.y = bf16_mut(y);
+  if (residual.has_value()) {
+    check_dev(*residual, at::kBFloat16, "residual");
+    TORCH_CHECK(residual->sizes() == x.sizes() && residual->is_contiguous(), "bn: residual layout");
+    a.residual = bf16_ptr(*residual);
+  }
+  a.gamma = fptr_opt(gamma, C, "gamma");
+  a.beta = fptr_opt(beta, C, "beta");
+  a.running_mean = fptr_opt(running_mean, C, "running_mean");
+  a.running_var = fptr_opt(running_var, C, "running_var");
+  a.save_mean = fptr_opt(save_mean, C, "save_mean");
+  a.save_invstd = fptr_opt(save_invstd, C, "save_invstd");
+  float* w = fptr_opt(ws, 4 * C, "ws");
+  a.scale = w;
+  a.shift = w + C;
+  a.ws = w + 2 * C;
+  a.M = (int)M;
+  a.C = (int)C;
+  a.eps = (float)eps;
+  a.momentum = (float)momentum;
+  a.training = training ? 1 : 0;
+  a.relu = relu ? 1 : 0;
+  TORCH_CHECK(training || (a.running_mean && a.running_var), "bn: eval mode needs running statistics");
+  check(ldnn::bn_forward(a, cur_stream(x)), "bn_forward");
+}
+
+void bn_bwd(const at::Tensor& x, const at::Tensor& y, const at::Tensor& dy, const at::Tensor& dx,
+            const c10::optional<at::Tensor>& dres, const c10::optional<at::Tensor>& gamma,
+            const at::Tensor& save_mean, const at::Tensor& save_invstd, const at::Tensor& ws,
+            const c10::optional<at::Tensor>& dgamma, const c10::optional<at::Tensor>& dbeta, bool relu) {
+  check_dev(x, at::kBFloat16, "x");
+  check_dev(dy, at::kBFloat16, "dy");
+  check_dev(dx, at::kBFloat16, "dx");
+  TORCH_CHECK(x.dim() == 2 && x.is_contiguous() && dy.sizes() == x.sizes() && dy.is_contiguous() &&
+                  dx.sizes() == x.sizes() && dx.is_contiguous(),
+              "bn_bwd: [M][C] dense tensors");
+  const int64_t M = x.size(0), C = x.size(1);
+  ldnn::BnArgs a{};
+  a.x = bf16_ptr(x);
+  a.y = bf16_mut(y);
+  a.gamma = fptr_opt(gamma, C, "gamma");
+  a.save_mean = fptr_opt(save_mean, C, "save_mean");
+  a.save_invstd = fptr_opt(save_invstd, C, "save_invstd");
+  float* w = fptr_opt(ws, 4 * C, "ws");
+  a.ws = w + 2 * C;
+  a.M = (int)M;
+  a.C = (int)C;
+  a.relu = relu ? 1 : 0;
+  uint16_t* dr = nullptr;
+  if (dres.has_value()) {
+    check_dev(*dres, at::kBFloat16, "dres");
+    TORCH_CHECK(dres->sizes() == x.sizes() && dres->is_contiguous(), "bn_bwd: dres layout");
+    dr = bf16_mut(*dres);
+  }
+  check(ldnn::bn_backward(a, bf16_ptr(dy), bf16_mut(dx), dr, fptr_opt(dgamma, C, "dgamma"),
+                          fptr_opt(dbeta, C, "dbeta"), cur_stream(x)),
+        "bn_backward");
+}
+
+// x [N][H][W][C], y [N][P][Q][C] dense bf16; argmax uint8 [N][P][Q][C] for max pooling
+void pool_fwd(const at::Tensor& x, const at::Tensor& y, const c10::optional<at::Tensor>& argmax, int64_t R,
+              int64_t S, int64_t stride, int64_t pad, bool is_max) {
+  check_dev(x, at::kBFloat16, "x");
+  check_dev(y, at::kBFloat16, "y");
+  TORCH_CHECK(x.dim() == 4 && y.dim() == 4 && x.is_contiguous() && y.is_contiguous(), "pool: dense NHWC");
+  uint8_t* am = nullptr;
+  if (is_max) {
+    TORCH_CHECK(argmax.has_value() && argmax->scalar_type() == at::kByte && argmax->numel() == y.numel(),
+                "pool: max pooling needs a uint8 argmax tensor");
+    am = argmax->data_ptr<uint8_t>();
+  }
+  check(ldnn::pool2d_fwd(bf16_ptr(x), bf16_mut(y), am, (int)x.size(0), (int)x.size(1), (int)x.size(2),
+                         (int)x.size(3), (int)y.size(1), (int)y.size(2), (int)R, (int)S, (int)stride, (int)pad, is_max,
+                         cur_stream(x)),
+        "pool2d_fwd");
+}
+
+void pool_bwd(const at::Tensor& dy, const c10::optional<at::Tensor>& argmax, const at::Tensor& dx, int64_t R,
+              int64_t S, int64_t stride, int64_t pad, bool is_max) {
+  check_dev(dy, at::kBFloat16, "dy");
+  check_dev(dx, at::kBFloat16, "dx");
+  TORCH_CHECK(dy.is_contiguous() && dx.is_contiguous(), "pool_bwd: dense NHWC");
+  const uint8_t* am = nullptr;
+  if (is_max) {
+    TORCH_CHECK(argmax.has_value() && argmax->numel() == dy.numel(), "pool_bwd: argmax");
+    am = argmax->data_ptr<uint8_t>();
+  }
+  check(ldnn::pool2d_bwd(bf16_ptr(dy), am, bf16_mut(dx), (int)dx.size(0), (int)dx.size(1), (int)dx.size(2),
+                         (int)dx.size(3), (int)dy.size(1), (int)dy.size(2), (int)R, (int)S, (int)stride, (int)pad,
+                         is_max, cur_stream(dy)),
+        "pool2d_bwd");
+}
+
+void gap_fwd(const at::Tensor& x, const at::Tensor& y) {  // x [N][HW][C], y [N][C]
+  check_dev(x, at::kBFloat16, "x");
+  check_dev(y, at::kBFloat16, "y");
+  TORCH_CHECK(x.dim() == 3 && x.is_contiguous() && y.is_contiguous(), "gap: dense [N][HW][C]");
+  check(ldnn::global_avgpool_fwd(bf16_ptr(x), bf16_mut(y), (int)x.size(0), (int)x.size(1), (int)x.size(2),
+                                 cur_stream(x)),
+        "gap_fwd");
+}
+
+void gap_bwd(const at::Tensor& dy, const at::Tensor& dx) {
+  check_dev(dy, at::kBFloat16, "dy");
+  check_dev(dx, at::kBFloat16, "dx");
+  TORCH_CHECK(dx.dim() == 3 && dx.is_contiguous() && dy.is_contiguous(), "gap_bwd: dense");
+  check(ldnn::global_avgpool_bwd(bf16_ptr(dy), bf16_mut(dx), (int)dx.size(0), (int)dx.size(1), (int)dx.size(2),
+                                 cur_stream(dy)),
+        "gap_bwd");
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_C, m) {
@@ -364,6 +495,16 @@ PYBIND11_MODULE(_C, m) {
         py::arg("shadow"), py::arg("hp"), py::arg("grad_scale"), py::arg("beta1"), py::arg("beta2"),
         py::arg("eps"), py::arg("weight_decay"), py::arg("decoupled"));
   m.def("bump_step", &bump_step);
+  m.def("bn_fwd", &bn_fwd, py::arg("x"), py::arg("y"), py::arg("residual"), py::arg("gamma"), py::arg("beta"),
+        py::arg("running_mean"), py::arg("running_var"), py::arg("save_mean"), py::arg("save_invstd"),
+        py::arg("ws"), py::arg("eps"), py::arg("momentum"), py::arg("training"), py::arg("relu"));
+  m.def("bn_bwd", &bn_bwd, py::arg("x"), py::arg("y"), py::arg("dy"), py::arg("dx"), py::arg("dres"),
+        py::arg("gamma"), py::arg("save_mean"), py::arg("save_invstd"), py::arg("ws"), py::arg("dgamma"),
+        py::arg("dbeta"), py::arg("relu"));
+  m.def("pool_fwd", &pool_fwd);
+  m.def("pool_bwd", &pool_bwd);
+  m.def("gap_fwd", &gap_fwd);
+  m.def("gap_bwd", &gap_bwd);
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("stride"), py::arg("pad"),
         py::arg("bias") = py::none(), py::arg("epi") = 0);
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("stride"), py::arg("pad"));

@@ -56,6 +56,36 @@ hipError_t conv2d_dgrad(const ConvShape& s, const uint16_t* dy, const uint16_t* 
 hipError_t conv2d_wgrad(const ConvShape& s, const uint16_t* dy, const uint16_t* x, float* dw, float beta,
                         hipStream_t st);
 
+// ---- BatchNorm / pooling on NHWC bf16 (bn_pool.hip), C % 8 == 0
+struct BnArgs {
+  const uint16_t* x;          // [M][C] input
+  const uint16_t* residual;   // optional [M][C] added before the ReLU
+  uint16_t* y;                // [M][C] output (also read by backward when relu)
+  const float* gamma;         // [C] (nullable: affine=False)
+  const float* beta;
+  float* running_mean;        // [C] (nullable: no EMA / eval uses them)
+  float* running_var;
+  float* save_mean;           // [C] batch statistics kept for backward
+  float* save_invstd;
+  float* scale;               // [C] workspace: gamma * invstd
+  float* shift;               // [C] workspace: beta - mean * gamma * invstd
+  float* ws;                  // [2C] fp32 reduction workspace
+  int M, C;
+  float eps, momentum;
+  int training, relu;
+};
+hipError_t bn_forward(const BnArgs& a, hipStream_t s);
+// dx (and optionally dres = upstream gradient after the ReLU mask, for the residual
+// branch); dgamma / dbeta are ACCUMULATED (flat gradient buffer)
+hipError_t bn_backward(const BnArgs& a, const uint16_t* dy, uint16_t* dx, uint16_t* dres, float* dgamma,
+                       float* dbeta, hipStream_t s);
+hipError_t pool2d_fwd(const uint16_t* x, uint16_t* y, uint8_t* argmax, int N, int H, int W, int C, int P, int Q,
+                      int R, int S, int stride, int pad, bool is_max, hipStream_t s);
+hipError_t pool2d_bwd(const uint16_t* dy, const uint8_t* argmax, uint16_t* dx, int N, int H, int W, int C, int P,
+                      int Q, int R, int S, int stride, int pad, bool is_max, hipStream_t s);
+hipError_t global_avgpool_fwd(const uint16_t* x, uint16_t* y, int N, int HW, int C, hipStream_t s);
+hipError_t global_avgpool_bwd(const uint16_t* dy, uint16_t* dx, int N, int HW, int C, hipStream_t s);
+
 // ---- elementwise / activations (bf16 storage, fp32 math) ---------------------
 enum Act : int { ACT_RELU = 0, ACT_SIGMOID = 1 };
 hipError_t act_fwd(const uint16_t* x, uint16_t* y, int64_t n, int act, hipStream_t s);

@@ -16,6 +16,14 @@ import torch.nn as nn
 from .layers import AdaptiveAvgPool2d, AvgPool2d, BatchNorm2d, Conv2d, Linear, MaxPool2d, ReLU
 
 
+class ConvBNReLU(nn.Sequential):
+    """Sequential(conv, bn, relu) -- same state_dict keys (prep.0 / prep.1) -- whose
+    BN and ReLU run as one fused pass."""
+
+    def forward(self, x):
+        return self[1].act(self[0](x), relu=True)
+
+
 class ResBlock(nn.Module):
     """conv3x3(stride)-BN-ReLU-conv3x3-BN + shortcut (1x1 conv + BN when the shape
     changes) -> add -> ReLU; convs without bias (BAR/model.py:52-72)."""
@@ -35,16 +43,15 @@ class ResBlock(nn.Module):
         self.relu = ReLU()
 
     def forward(self, x):
-        out = self.relu(self.bn1(self.conv1(x)))
-        out = self.bn2(self.conv2(out))
-        out = out + self.shortcut(x)
-        return self.relu(out)
+        # BAR/model.py:67-72 with BN+ReLU and BN+residual-add+ReLU each fused into one pass
+        out = self.bn1.act(self.conv1(x), relu=True)
+        return self.bn2.act(self.conv2(out), residual=self.shortcut(x), relu=True)
 
 
 class EnhancedCNNModel(nn.Module):
     def __init__(self, num_classes: int = 10, in_channels: int = 3):
         super().__init__()
-        self.prep = nn.Sequential(
+        self.prep = ConvBNReLU(
             Conv2d(in_channels, 64, kernel_size=3, stride=1, padding=1, bias=False),
             BatchNorm2d(64),
             ReLU(),
@@ -72,7 +79,7 @@ class EnhancedCNNSmall(nn.Module):
 
     def __init__(self, num_classes: int = 10, in_channels: int = 3):
         super().__init__()
-        self.prep = nn.Sequential(
+        self.prep = ConvBNReLU(
             Conv2d(in_channels, 64, kernel_size=3, stride=1, padding=1, bias=False),
             BatchNorm2d(64),
             ReLU(),
@@ -98,9 +105,12 @@ class LeNet5(nn.Module):
         super().__init__()
         P = MaxPool2d if pool == "max" else AvgPool2d
         self.features = nn.Sequential(
-            Conv2d(in_channels, 6, kernel_size=5, padding=2), ReLU(), P(2),
-            Conv2d(6, 16, kernel_size=5), ReLU(), P(2),
+            Conv2d(in_channels, 6, kernel_size=5, padding=2, activation="relu"), ReLU(), P(2),
+            Conv2d(6, 16, kernel_size=5, activation="relu"), ReLU(), P(2),
         )
+        # the ReLUs are fused into the conv epilogues; the modules stay for the reference layout
+        self.features[1] = nn.Identity()
+        self.features[4] = nn.Identity()
         self.fc1 = Linear(16 * 5 * 5, 120, activation="relu")
         self.fc2 = Linear(120, 84, activation="relu")
         self.fc3 = Linear(84, num_classes)

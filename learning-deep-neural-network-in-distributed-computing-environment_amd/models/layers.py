@@ -70,19 +70,31 @@ class Conv2d(nn.Conv2d):
 
 class BatchNorm2d(nn.BatchNorm2d):
     """Train-mode batch statistics + running-stat EMA exactly as nn.BatchNorm2d;
-    fp32 statistics over bf16 activations on the GPU."""
+    on the GPU fp32 statistics over NHWC bf16 activations in the native kernels,
+    with optional residual-add + ReLU fused into the same pass (``act``)."""
+
+    def __init__(self, *args, **kwargs):
+        super().__init__(*args, **kwargs)
+        self._ldnn_flat = None
 
     def forward(self, x):
-        return LF.batch_norm2d(x, self)
+        return LF.batch_norm_act(x, self)
+
+    def act(self, x, residual=None, relu: bool = False):
+        """relu?(bn(x) + residual) in one fused pass."""
+        return LF.batch_norm_act(x, self, residual, relu)
 
 
 class MaxPool2d(nn.MaxPool2d):
-    pass
+    def forward(self, x):
+        return LF.pool2d(x, self, True)
 
 
 class AvgPool2d(nn.AvgPool2d):
-    pass
+    def forward(self, x):
+        return LF.pool2d(x, self, False)
 
 
 class AdaptiveAvgPool2d(nn.AdaptiveAvgPool2d):
-    pass
+    def forward(self, x):
+        return LF.adaptive_avg_pool2d(x, self.output_size)

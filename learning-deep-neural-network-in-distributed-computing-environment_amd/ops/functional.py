@@ -300,6 +300,74 @@ def conv2d(x, mod, relu: bool = False):
     return F.relu(y) if relu else y
 
 
+class _BatchNormNative(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, residual, mod, flat, relu):
+        C_ = _ext.C()
+        N, C, H, W = x.shape
+        xb = as_nhwc(x if x.dtype == torch.bfloat16 else x.to(torch.bfloat16), C, zero_pad=False)
+        x2 = xb.view(-1, C)
+        r2 = None
+        if residual is not None:
+            rb = residual if residual.dtype == torch.bfloat16 else residual.to(torch.bfloat16)
+            r2 = as_nhwc(rb, C, zero_pad=False).reshape(-1, C)
+        y = torch.empty(N, H, W, C, dtype=torch.bfloat16, device=x.device)
+        dev = x.device
+        ws = torch.empty(4 * C, dtype=torch.float32, device=dev)
+        smean = torch.empty(C, dtype=torch.float32, device=dev)
+        sinv = torch.empty(C, dtype=torch.float32, device=dev)
+        gamma = flat.master_storage(weight)[:C] if weight is not None else None
+        beta = flat.master_storage(bias)[:C] if bias is not None else None
+        training = mod.training or not mod.track_running_stats
+        mom = mod.momentum
+        if mod.training and mod.track_running_stats:
+            mod.num_batches_tracked.add_(1)
+            mod._ldnn_nbt = getattr(mod, "_ldnn_nbt", 0) + 1
+            if mom is None:
+                mom = 1.0 / mod._ldnn_nbt
+        rm = mod.running_mean if mod.track_running_stats else None
+        rv = mod.running_var if mod.track_running_stats else None
+        C_.bn_fwd(x2, y.view(-1, C), r2, gamma, beta, rm if (training and mod.training) or not training else None,
+                  rv if (training and mod.training) or not training else None, smean, sinv, ws, mod.eps,
+                  mom or 0.0, training, relu)
+        ctx.save_for_backward(x2, y, smean, sinv)
+        ctx.meta = (flat, weight, bias, relu, residual is not None, ws, (N, C, H, W), x.dtype)
+        return nchw_view(y, C)
+
+    @staticmethod
+    def backward(ctx, gy):
+        C_ = _ext.C()
+        x2, y, smean, sinv = ctx.saved_tensors
+        flat, weight, bias, relu, has_res, ws, (N, C, H, W), in_dtype = ctx.meta
+        g2 = as_nhwc(gy if gy.dtype == torch.bfloat16 else gy.to(torch.bfloat16), C, zero_pad=False)
+        g2 = g2.contiguous().view(-1, C)
+        dx = torch.empty(N, H, W, C, dtype=torch.bfloat16, device=x2.device)
+        dres = torch.empty_like(dx) if has_res and ctx.needs_input_grad[3] else None
+        gamma = flat.master_storage(weight)[:C] if weight is not None else None
+        dg = flat.grad_storage(weight)[:C] if weight is not None else None
+        db = flat.grad_storage(bias)[:C] if bias is not None else None
+        C_.bn_bwd(x2, y.view(-1, C), g2, dx.view(-1, C), dres.view(-1, C) if dres is not None else None, gamma,
+                  smean, sinv, ws, dg, db, relu)
+        flat.notify(weight, bias)
+        dxv = nchw_view(dx, C)
+        dresv = nchw_view(dres, C) if dres is not None else None
+        if in_dtype != torch.bfloat16:
+            dxv = dxv.to(in_dtype)
+        return dxv, None, None, dresv, None, None, None
+
+
+def batch_norm_act(x, mod, residual=None, relu: bool = False):
+    """relu?(BatchNorm2d(x) (+ residual)) -- fused into one native pass on the GPU
+    (fp32 statistics over NHWC bf16); the CPU path is the fp32 reference."""
+    flat = getattr(mod, "_ldnn_flat", None)
+    if _ext.use_native(x) and flat is not None and x.shape[1] % 8 == 0 and mod.affine:
+        return _BatchNormNative.apply(x, mod.weight, mod.bias, residual, mod, flat, relu)
+    y = batch_norm2d(x, mod)
+    if residual is not None:
+        y = y + residual
+    return F.relu(y) if relu else y
+
+
 def batch_norm2d(x, mod):
     training = mod.training or not mod.track_running_stats
     mom = 0.0 if mod.momentum is None else mod.momentum
@@ -313,3 +381,78 @@ def batch_norm2d(x, mod):
         y = F.batch_norm(x.float(), rm, rv, mod.weight, mod.bias, training, mom, mod.eps)
         return y.to(torch.bfloat16)
     return F.batch_norm(x.float(), rm, rv, mod.weight, mod.bias, training, mom, mod.eps)
+
+
+# ------------------------------------------------------------------ pooling
+class _PoolNative(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k, stride, pad, is_max):
+        C_ = _ext.C()
+        N, C, H, W = x.shape
+        cp = _up8(C)
+        xb = as_nhwc(x if x.dtype == torch.bfloat16 else x.to(torch.bfloat16), cp)
+        P, Q = (H + 2 * pad - k) // stride + 1, (W + 2 * pad - k) // stride + 1
+        y = torch.empty(N, P, Q, cp, dtype=torch.bfloat16, device=x.device)
+        am = torch.empty(N, P, Q, cp, dtype=torch.uint8, device=x.device) if is_max else None
+        C_.pool_fwd(xb.contiguous(), y, am, k, k, stride, pad, is_max)
+        ctx.save_for_backward(am) if is_max else None
+        ctx.meta = (k, stride, pad, is_max, (N, C, H, W, cp), x.dtype)
+        return nchw_view(y, C)
+
+    @staticmethod
+    def backward(ctx, gy):
+        C_ = _ext.C()
+        k, stride, pad, is_max, (N, C, H, W, cp), in_dtype = ctx.meta
+        am = ctx.saved_tensors[0] if is_max else None
+        g = as_nhwc(gy if gy.dtype == torch.bfloat16 else gy.to(torch.bfloat16), cp).contiguous()
+        dx = torch.empty(N, H, W, cp, dtype=torch.bfloat16, device=gy.device)
+        C_.pool_bwd(g, am, dx, k, k, stride, pad, is_max)
+        out = nchw_view(dx, C)
+        return (out if in_dtype == torch.bfloat16 else out.to(in_dtype)), None, None, None, None
+
+
+def _sq(v):
+    return v if isinstance(v, int) else (v[0] if v[0] == v[1] else None)
+
+
+def pool2d(x, mod, is_max: bool):
+    k, st, pad = _sq(mod.kernel_size), _sq(mod.stride if mod.stride is not None else mod.kernel_size), _sq(mod.padding)
+    simple = (None not in (k, st, pad) and not getattr(mod, "ceil_mode", False)
+              and (not is_max or _sq(mod.dilation) == 1) and (is_max or getattr(mod, "count_include_pad", True))
+              and k * k <= 255)
+    if _ext.use_native(x) and simple and x.dim() == 4:
+        return _PoolNative.apply(x, k, st, pad, is_max)
+    if is_max:
+        return F.max_pool2d(x, mod.kernel_size, mod.stride, mod.padding, mod.dilation, mod.ceil_mode)
+    return F.avg_pool2d(x, mod.kernel_size, mod.stride, mod.padding, mod.ceil_mode, mod.count_include_pad)
+
+
+class _GapNative(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        C_ = _ext.C()
+        N, C, H, W = x.shape
+        cp = _up8(C)
+        xb = as_nhwc(x if x.dtype == torch.bfloat16 else x.to(torch.bfloat16), cp).contiguous()
+        y = torch.empty(N, cp, dtype=torch.bfloat16, device=x.device)
+        C_.gap_fwd(xb.view(N, H * W, cp), y)
+        ctx.meta = (N, C, H, W, cp, x.dtype)
+        return y[:, :C].view(N, C, 1, 1)
+
+    @staticmethod
+    def backward(ctx, gy):
+        C_ = _ext.C()
+        N, C, H, W, cp, in_dtype = ctx.meta
+        g = torch.zeros(N, cp, dtype=torch.bfloat16, device=gy.device)
+        g[:, :C] = gy.reshape(N, C)
+        dx = torch.empty(N, H, W, cp, dtype=torch.bfloat16, device=gy.device)
+        C_.gap_bwd(g, dx.view(N, H * W, cp))
+        out = nchw_view(dx, C)
+        return out if in_dtype == torch.bfloat16 else out.to(in_dtype)
+
+
+def adaptive_avg_pool2d(x, output_size):
+    os_ = output_size if isinstance(output_size, int) else (output_size[0] if output_size[0] == output_size[1] else None)
+    if _ext.use_native(x) and os_ == 1 and x.dim() == 4:
+        return _GapNative.apply(x)
+    return F.adaptive_avg_pool2d(x, output_size)

@@ -1,0 +1,97 @@
+"""Native NHWC BatchNorm (+residual +ReLU) and pooling vs PyTorch fp32 references."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+import ldnn
+from ldnn.models.layers import AdaptiveAvgPool2d, AvgPool2d, BatchNorm2d, MaxPool2d
+from ldnn.ops import functional as LF
+
+pytestmark = pytest.mark.gpu
+
+
+def _cl(x):  # bf16 channels_last copy of a fp32 NCHW tensor
+    return x.bfloat16().contiguous(memory_format=torch.channels_last)
+
+
+@pytest.mark.parametrize("residual,relu", [(False, False), (False, True), (True, True)])
+def test_batchnorm_train_fused(residual, relu):
+    torch.manual_seed(0)
+    N, C, H, W = 8, 64, 16, 16
+    bn = BatchNorm2d(C)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.5, 0.5)
+    ref = torch.nn.BatchNorm2d(C).cuda()
+    ref.load_state_dict(bn.state_dict())
+    ldnn.prepare(bn, "cuda")
+    x = torch.randn(N, C, H, W, device="cuda") * 2 + 0.5
+    r = torch.randn(N, C, H, W, device="cuda") if residual else None
+    xb = _cl(x).requires_grad_(True)
+    rb = _cl(r).requires_grad_(True) if residual else None
+    y = bn.act(xb, rb, relu)
+    xf = xb.detach().float().requires_grad_(True)
+    rf = rb.detach().float().requires_grad_(True) if residual else None
+    yr = ref(xf)
+    if residual:
+        yr = yr + rf
+    if relu:
+        yr = yr.relu()
+    torch.testing.assert_close(y.float(), yr, rtol=2e-2, atol=3e-2)
+    torch.testing.assert_close(bn.running_mean, ref.running_mean, rtol=1e-3, atol=1e-4)
+    torch.testing.assert_close(bn.running_var, ref.running_var, rtol=1e-3, atol=1e-3)
+    g = torch.randn_like(yr)
+    y.float().backward(g)
+    yr.backward(g)
+    torch.testing.assert_close(xb.grad.float(), xf.grad, rtol=3e-2, atol=3e-2 * xf.grad.abs().max().item())
+    torch.testing.assert_close(bn.weight.grad, ref.weight.grad, rtol=2e-2, atol=2e-2 * ref.weight.grad.abs().max().item())
+    torch.testing.assert_close(bn.bias.grad, ref.bias.grad, rtol=2e-2, atol=2e-2 * ref.bias.grad.abs().max().item())
+    if residual:
+        torch.testing.assert_close(rb.grad.float(), rf.grad, rtol=2e-2, atol=2e-2)
+
+
+def test_batchnorm_eval_uses_running_stats():
+    torch.manual_seed(1)
+    C = 32
+    bn = BatchNorm2d(C)
+    with torch.no_grad():
+        bn.running_mean.uniform_(-1, 1)
+        bn.running_var.uniform_(0.5, 2)
+    ref = torch.nn.BatchNorm2d(C).cuda()
+    ref.load_state_dict(bn.state_dict())
+    ldnn.prepare(bn, "cuda")
+    bn.eval()
+    ref.eval()
+    x = torch.randn(4, C, 8, 8, device="cuda")
+    torch.testing.assert_close(bn(_cl(x)).float(), ref(_cl(x).float()), rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("kind,k,st,pad", [("max", 2, 2, 0), ("max", 3, 2, 1), ("avg", 2, 2, 0), ("avg", 3, 1, 1)])
+@pytest.mark.parametrize("C", [6, 64])
+def test_pools(kind, k, st, pad, C):
+    torch.manual_seed(2)
+    mod = MaxPool2d(k, st, pad) if kind == "max" else AvgPool2d(k, st, pad)
+    x = torch.randn(4, C, 14, 14, device="cuda")
+    xb = _cl(x).requires_grad_(True)
+    y = mod(xb)
+    xf = xb.detach().float().requires_grad_(True)
+    yr = F.max_pool2d(xf, k, st, pad) if kind == "max" else F.avg_pool2d(xf, k, st, pad)
+    torch.testing.assert_close(y.float(), yr, rtol=1e-2, atol=1e-2)
+    g = torch.randn_like(yr).bfloat16().float()
+    y.float().backward(g)
+    yr.backward(g)
+    torch.testing.assert_close(xb.grad.float(), xf.grad, rtol=2e-2, atol=2e-2)
+
+
+def test_global_avgpool():
+    torch.manual_seed(3)
+    x = torch.randn(4, 72, 7, 7, device="cuda")
+    xb = _cl(x).requires_grad_(True)
+    y = AdaptiveAvgPool2d(1)(xb)
+    xf = xb.detach().float().requires_grad_(True)
+    yr = F.adaptive_avg_pool2d(xf, 1)
+    torch.testing.assert_close(y.float(), yr, rtol=1e-2, atol=1e-2)
+    g = torch.randn_like(yr)
+    y.float().backward(g)
+    yr.backward(g)
+    torch.testing.assert_close(xb.grad.float(), xf.grad, rtol=2e-2, atol=2e-3)
