@@ -66,7 +66,8 @@ def test_graph_replay_matches_eager_with_splitk():
             e.load_batch(x, y)
             e.step()
     torch.cuda.synchronize()
-    torch.testing.assert_close(e1.flat.master, e2.flat.master, rtol=0, atol=0)
+    # identical up to the arrival order of the split-K / bias-gradient fp32 atomics
+    torch.testing.assert_close(e1.flat.master, e2.flat.master, rtol=1e-6, atol=1e-8)
 
 
 def test_multirank_static_engine_gloo_two_ranks_one_gpu():
