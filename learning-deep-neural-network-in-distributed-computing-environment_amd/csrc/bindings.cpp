@@ -41,7 +41,7 @@ int64_t ld_of(const at::Tensor& t, const char* name) {
 //   a: if a_kcontig, [M][K] else [K][M];  b: if b_kcontig, [N][K] else [K][N];  c: [M][N]
 void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, bool a_kcontig, bool b_kcontig,
           int64_t epi, const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& aux,
-          const c10::optional<at::Tensor>& dbias, double beta, int64_t tile, int64_t splitk) {
+          const c10::optional<at::Tensor>& dbias, double beta, int64_t tile, int64_t splitk, bool direct_epi) {
   check_dev(a, at::kBFloat16, "a");
   check_dev(b, at::kBFloat16, "b");
   TORCH_CHECK(c.is_cuda() && (c.scalar_type() == at::kBFloat16 || c.scalar_type() == at::kFloat),
@@ -72,6 +72,7 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, bool a_
   p.ldb = (int)ldb;
   p.ldc = (int)ldc;
   p.beta = (float)beta;
+  p.direct_epi = direct_epi ? 1 : 0;
   if (epi == ldnn::EPI_BIAS || epi == ldnn::EPI_BIAS_RELU || epi == ldnn::EPI_BIAS_SIGMOID) {
     TORCH_CHECK(bias.has_value(), "gemm: bias epilogue needs a bias tensor");
     check_dev(*bias, at::kFloat, "bias");
@@ -479,7 +480,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm", &gemm, "bf16 MFMA GEMM with fused epilogue", py::arg("a"), py::arg("b"), py::arg("c"),
         py::arg("a_kcontig"), py::arg("b_kcontig"), py::arg("epi") = 0, py::arg("bias") = py::none(),
         py::arg("aux") = py::none(), py::arg("dbias") = py::none(), py::arg("beta") = 0.0,
-        py::arg("tile") = 0, py::arg("splitk") = 0);
+        py::arg("tile") = 0, py::arg("splitk") = 0, py::arg("direct_epi") = false);
   m.def("act_fwd", &act_fwd);
   m.def("act_bwd", &act_bwd);
   m.def("colsum", &colsum, py::arg("x"), py::arg("out"), py::arg("accumulate") = false);

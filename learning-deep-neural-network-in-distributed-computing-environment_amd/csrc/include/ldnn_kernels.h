@@ -27,6 +27,7 @@ struct GemmParams {
   int lda, ldb, ldc, ldaux;
   float beta;            // fp32 output only: C = acc + beta * C
   int splitk;            // >1: K split over gridDim.y, fp32 atomics into C (EPI_NONE, fp32 out, 128-tile)
+  int direct_epi;        // 256-tile bf16 outputs: 1 = per-fragment stores (A/B knob), 0 = LDS-staged rows
 };
 
 // Picks the tiling (256x256 LDS-DMA kernel or 128x128 kernel) from the shape.
