@@ -78,6 +78,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--timeout", type=float, default=600.0, help="collective timeout (s): failure detection")
     p.add_argument("--no_eval", action="store_true")
     p.add_argument("--quiet", action="store_true")
+    p.add_argument("--trace", action="store_true",
+                   help="roctx ranges per phase + HIP-event phase timers (summary in metrics.jsonl)")
     return p
 
 
@@ -153,6 +155,12 @@ def main(argv=None):
                 train_loader = DeviceLoader(trainset, tr_idx, args.batch_size, dev, dtype=dtype, augment=args.augment)
                 val_loader = DeviceLoader(valset, va_idx, args.batch_size, dev, dtype=dtype)
 
+    from .utils import tracing
+
+    timer = None
+    if args.trace:
+        tracing.enable(True)
+        timer = tracing.PhaseTimer(dev, enabled=True)
     timelimit = args.time_limit if args.time_limit and args.time_limit > 0 else math.inf
     histories = train_global(
         net, train_loader, val_loader, trainset, valset, tr_idx, va_idx, criterion, optimizer, scheduler, dev, rank,
@@ -162,7 +170,13 @@ def main(argv=None):
         dp=dp, partition_rule=args.partition_rule, repartition=not args.no_repartition, replace=args.replace,
         seed=args.seed, legacy_gossip=args.legacy_gossip, average_buffers=args.average_buffers,
         check_every=args.check_every, progress=not args.quiet, logger=logger, checkpointer=ckpt,
-        start_global_epoch=start, histories=hist, dtype=dtype, verbose=not args.quiet)
+        start_global_epoch=start, histories=hist, dtype=dtype, verbose=not args.quiet, timer=timer)
+    if timer is not None:
+        phases = timer.summary()
+        logger.log(kind="phase_times", phases=phases)
+        if not args.quiet:
+            for k, v in sorted(phases.items(), key=lambda kv: -kv[1]["total_ms"]):
+                print(f"[rank {rank}] {k:10s} {v['total_ms']:10.2f} ms total  {v['mean_ms']:8.3f} ms x {v['count']}")
 
     result = {"histories": [list(h) if not isinstance(h, list) else h for h in histories]}
     if rank == 0 and not args.no_eval:

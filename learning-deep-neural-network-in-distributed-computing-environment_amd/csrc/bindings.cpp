@@ -7,6 +7,7 @@
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 
+#include <rocprofiler-sdk-roctx/roctx.h>
 #include "ldnn_kernels.h"
 
 namespace {
@@ -95,7 +96,7 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, bool a_
   const bool skinny_ok = a_kcontig && b_kcontig && !out_f32 && N <= 64 && !dbias.has_value() && beta == 0.0 &&
                          (epi == ldnn::EPI_NONE || epi == ldnn::EPI_BIAS || epi == ldnn::EPI_BIAS_RELU ||
                           epi == ldnn::EPI_BIAS_SIGMOID);
-  if (tile == 0) tile = skinny_ok && K >= 256 ? 16 : ldnn::gemm_pick_tile(p.M, p.N, p.K);
+  if (tile == 0) tile = skinny_ok && K >= 256 ? 16 : ldnn::gemm_pick_tile(p.M, p.N, p.K, out_f32);
   TORCH_CHECK(tile == 16 || tile == 128 || tile == 256, "gemm: tile must be 0 (auto), 16 (skinny-N), 128 or 256");
   c10::hip::HIPGuardMasqueradingAsCUDA g(a.device());
   if (tile == 16) {
@@ -202,9 +203,22 @@ void softmax_xent(const at::Tensor& logits, const at::Tensor& labels, const at::
         "softmax_xent");
 }
 
+// up to two [begin, end) element ranges of `grad` to clear after the update reads them
+ldnn::GradZero grad_zero(const std::vector<std::pair<int64_t, int64_t>>& r, int64_t n) {
+  TORCH_CHECK(r.size() <= 2, "optimizer: at most two gradient zero ranges");
+  ldnn::GradZero z;
+  for (size_t i = 0; i < r.size(); ++i) {
+    TORCH_CHECK(0 <= r[i].first && r[i].first <= r[i].second && r[i].second <= n, "optimizer: bad zero range");
+    z.zb[i] = r[i].first;
+    z.ze[i] = r[i].second;
+  }
+  return z;
+}
+
 void sgd_step(const at::Tensor& param, const at::Tensor& grad, const at::Tensor& mom,
               const c10::optional<at::Tensor>& shadow, const at::Tensor& hp, double grad_scale, double momentum,
-              double dampening, double weight_decay, bool nesterov, bool first_step) {
+              double dampening, double weight_decay, bool nesterov, bool first_step,
+              const std::vector<std::pair<int64_t, int64_t>>& zero_ranges) {
   check_dev(param, at::kFloat, "param");
   check_dev(grad, at::kFloat, "grad");
   check_dev(hp, at::kFloat, "hp");
@@ -222,7 +236,8 @@ void sgd_step(const at::Tensor& param, const at::Tensor& grad, const at::Tensor&
     TORCH_CHECK(shadow->is_contiguous() && shadow->numel() == n, "sgd: bad shadow");
     sh = bf16_mut(*shadow);
   }
-  ldnn::SgdParams sp{(float)momentum, (float)dampening, (float)weight_decay, nesterov ? 1 : 0, first_step ? 1 : 0};
+  ldnn::SgdParams sp{(float)momentum, (float)dampening, (float)weight_decay, nesterov ? 1 : 0, first_step ? 1 : 0,
+                     grad_zero(zero_ranges, n)};
   check(ldnn::sgd_step(param.data_ptr<float>(), grad.data_ptr<float>(), mp, sh, hp.data_ptr<float>(),
                        (float)grad_scale, sp, n, cur_stream(param)),
         "sgd_step");
@@ -230,7 +245,8 @@ void sgd_step(const at::Tensor& param, const at::Tensor& grad, const at::Tensor&
 
 void adam_step(const at::Tensor& param, const at::Tensor& grad, const at::Tensor& m, const at::Tensor& v,
                const c10::optional<at::Tensor>& shadow, const at::Tensor& hp, double grad_scale, double beta1,
-               double beta2, double eps, double weight_decay, bool decoupled) {
+               double beta2, double eps, double weight_decay, bool decoupled,
+               const std::vector<std::pair<int64_t, int64_t>>& zero_ranges) {
   check_dev(param, at::kFloat, "param");
   check_dev(grad, at::kFloat, "grad");
   check_dev(m, at::kFloat, "exp_avg");
@@ -246,7 +262,8 @@ void adam_step(const at::Tensor& param, const at::Tensor& grad, const at::Tensor
     TORCH_CHECK(shadow->is_contiguous() && shadow->numel() == n, "adam: bad shadow");
     sh = bf16_mut(*shadow);
   }
-  ldnn::AdamParams ap{(float)beta1, (float)beta2, (float)eps, (float)weight_decay, decoupled ? 1 : 0};
+  ldnn::AdamParams ap{(float)beta1, (float)beta2, (float)eps, (float)weight_decay, decoupled ? 1 : 0,
+                      grad_zero(zero_ranges, n)};
   check(ldnn::adam_step(param.data_ptr<float>(), grad.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(),
                         sh, hp.data_ptr<float>(), (float)grad_scale, ap, n, cur_stream(param)),
         "adam_step");
@@ -489,12 +506,27 @@ PYBIND11_MODULE(_C, m) {
         py::arg("a") = 1.0, py::arg("b") = 0.0, py::arg("c") = 0.0, py::arg("shadow") = py::none());
   m.def("softmax_xent", &softmax_xent, py::arg("logits"), py::arg("labels"), py::arg("dlogits"),
         py::arg("stats"), py::arg("dbias") = py::none(), py::arg("num_classes"), py::arg("grad_scale"));
+  // roctx ranges (rocprofv3 --marker-trace shows them on the timeline)
+  m.def("trace_push", [](const std::string& s) { return roctxRangePushA(s.c_str()); }, py::arg("name"));
+  m.def("trace_pop", []() { return roctxRangePop(); });
+  m.def("trace_mark", [](const std::string& s) { roctxMarkA(s.c_str()); }, py::arg("name"));
+  m.def("trace_name_thread", [](const std::string& s) { roctxNameOsThread(s.c_str()); }, py::arg("name"));
+  m.def(
+      "gemm_plan",
+      [](int64_t M, int64_t N, int64_t K, bool out_f32) {
+        const int tile = ldnn::gemm_pick_tile((int)M, (int)N, (int)K, out_f32);
+        return std::make_pair(tile, tile == 128 ? ldnn::gemm_pick_splitk((int)M, (int)N, (int)K) : 1);
+      },
+      "(tile, splitk) the auto dispatch picks for a (M, N, K) GEMM", py::arg("M"), py::arg("N"), py::arg("K"),
+      py::arg("out_f32"));
   m.def("sgd_step", &sgd_step, py::arg("param"), py::arg("grad"), py::arg("mom"), py::arg("shadow"),
         py::arg("hp"), py::arg("grad_scale"), py::arg("momentum"), py::arg("dampening"),
-        py::arg("weight_decay"), py::arg("nesterov"), py::arg("first_step"));
+        py::arg("weight_decay"), py::arg("nesterov"), py::arg("first_step"),
+        py::arg("zero_ranges") = std::vector<std::pair<int64_t, int64_t>>{});
   m.def("adam_step", &adam_step, py::arg("param"), py::arg("grad"), py::arg("m"), py::arg("v"),
         py::arg("shadow"), py::arg("hp"), py::arg("grad_scale"), py::arg("beta1"), py::arg("beta2"),
-        py::arg("eps"), py::arg("weight_decay"), py::arg("decoupled"));
+        py::arg("eps"), py::arg("weight_decay"), py::arg("decoupled"),
+        py::arg("zero_ranges") = std::vector<std::pair<int64_t, int64_t>>{});
   m.def("bump_step", &bump_step);
   m.def("bn_fwd", &bn_fwd, py::arg("x"), py::arg("y"), py::arg("residual"), py::arg("gamma"), py::arg("beta"),
         py::arg("running_mean"), py::arg("running_var"), py::arg("save_mean"), py::arg("save_invstd"),

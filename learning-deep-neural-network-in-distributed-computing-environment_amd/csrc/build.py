@@ -98,7 +98,8 @@ def build(verbose: bool = False, force: bool = False, jobs: int | None = None) -
         link = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", OUT + ".tmp"] + objs
         for p in lib:
             link += [f"-L{p}", f"-Wl,-rpath,{p}"]
-        link += ["-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python", "-lamdhip64"]
+        link += ["-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python", "-lamdhip64",
+                 f"-L{ROCM}/lib", f"-Wl,-rpath,{ROCM}/lib", "-lrocprofiler-sdk-roctx"]
         _run(link, verbose)
         os.replace(OUT + ".tmp", OUT)
     return OUT

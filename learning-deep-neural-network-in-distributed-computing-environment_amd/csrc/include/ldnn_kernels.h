@@ -36,7 +36,7 @@ hipError_t gemm_bf16(const GemmParams& p, bool a_kcontig, bool b_kcontig, int ep
 // Same with an explicit tile (128 or 256); 256 falls back to 128 for operands >= 2 GiB.
 hipError_t gemm_bf16_tile(const GemmParams& p, bool a_kcontig, bool b_kcontig, int epi, bool out_f32, int tile,
                           hipStream_t s);
-int gemm_pick_tile(int M, int N, int K);
+int gemm_pick_tile(int M, int N, int K, bool out_f32);
 // Split-K factor the 128-tile kernel uses for an fp32 EPI_NONE output (1 = none).
 int gemm_pick_splitk(int M, int N, int K);
 // Skinny-N forward GEMM (N <= 64, both operands k-contiguous, bf16 out): one
@@ -113,18 +113,26 @@ hipError_t softmax_xent(const uint16_t* logits, const int64_t* labels, uint16_t*
 
 // ---- fused optimizers over flat fp32 buffers -------------------------------
 // hp (device fp32): [0]=lr [1]=step (already incremented for Adam) ; grad_scale multiplies g
+// Gradient ranges [zb[i], ze[i]) (element offsets into this launch's range) are
+// zeroed after being consumed: accumulate-into (atomic) gradient producers of the
+// next step then need no separate zeroing launch.
+struct GradZero {
+  int64_t zb[2] = {0, 0}, ze[2] = {0, 0};
+};
 struct SgdParams {
   float momentum, dampening, weight_decay;
   int nesterov;
   int first_step;  // momentum buffer initialised from g (torch semantics)
+  GradZero zero;
 };
-hipError_t sgd_step(float* param, const float* grad, float* mom, uint16_t* shadow, const float* hp,
+hipError_t sgd_step(float* param, float* grad, float* mom, uint16_t* shadow, const float* hp,
                     float grad_scale, SgdParams sp, int64_t n, hipStream_t s);
 struct AdamParams {
   float beta1, beta2, eps, weight_decay;
   int decoupled;  // AdamW
+  GradZero zero;
 };
-hipError_t adam_step(float* param, const float* grad, float* m, float* v, uint16_t* shadow, const float* hp,
+hipError_t adam_step(float* param, float* grad, float* m, float* v, uint16_t* shadow, const float* hp,
                      float grad_scale, AdamParams ap, int64_t n, hipStream_t s);
 // hp[1] += 1 (graph-capturable step counter)
 hipError_t bump_step(float* hp, hipStream_t s);

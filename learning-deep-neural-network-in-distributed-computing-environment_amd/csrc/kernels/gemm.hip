@@ -503,11 +503,12 @@ hipError_t dispatch_layout(const GemmParams& p, bool a_kc, bool b_kc, int epi, b
 
 }  // namespace
 
-int gemm_pick_tile(int M, int N, int K) {
+int gemm_pick_tile(int M, int N, int K, bool out_f32) {
   const int t256 = ((M + 255) / 256) * ((N + 255) / 256);
   // a 256^2 tile needs the grid to cover most of the 256 CUs and a K loop long
-  // enough to amortise its 2-tile prologue
-  if (t256 >= 192 && K >= 256) return 256;
+  // enough to amortise its 2-tile prologue -- or a bf16 output whose LDS-staged
+  // epilogue (row-coalesced stores) is the bottleneck at tiny K
+  if (t256 >= 192 && (K >= 256 || !out_f32)) return 256;
   return 128;
 }
 
@@ -523,7 +524,7 @@ int gemm_pick_splitk(int M, int N, int K) {
 
 hipError_t gemm_bf16(const GemmParams& p, bool a_kcontig, bool b_kcontig, int epi, bool out_f32,
                      hipStream_t s) {
-  return gemm_bf16_tile(p, a_kcontig, b_kcontig, epi, out_f32, gemm_pick_tile(p.M, p.N, p.K), s);
+  return gemm_bf16_tile(p, a_kcontig, b_kcontig, epi, out_f32, gemm_pick_tile(p.M, p.N, p.K, out_f32), s);
 }
 
 hipError_t gemm_bf16_tile(const GemmParams& p, bool a_kcontig, bool b_kcontig, int epi, bool out_f32, int tile,

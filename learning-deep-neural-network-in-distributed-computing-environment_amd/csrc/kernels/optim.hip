@@ -19,7 +19,23 @@ namespace {
 
 constexpr int kBlock = 256;
 
-__global__ void sgd_kernel(float* __restrict__ param, const float* __restrict__ grad, float* __restrict__ mom,
+__device__ __forceinline__ bool in_zero(const GradZero& z, int64_t i) {
+  return (i >= z.zb[0] && i < z.ze[0]) || (i >= z.zb[1] && i < z.ze[1]);
+}
+
+// consume-and-clear the gradient elements [4i, 4i+4) that fall in a zero range
+__device__ __forceinline__ void clear4(const GradZero& z, float* grad, int64_t i) {
+  const int64_t e = 4 * i;
+  if (in_zero(z, e) && in_zero(z, e + 3)) {
+    reinterpret_cast<floatx4*>(grad)[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (in_zero(z, e + j)) grad[e + j] = 0.f;
+  }
+}
+
+__global__ void sgd_kernel(float* __restrict__ param, float* __restrict__ grad, float* __restrict__ mom,
                            bf16_t* __restrict__ shadow, const float* __restrict__ hp, float grad_scale,
                            SgdParams sp, int64_t n) {
   const float lr = hp[0];
@@ -28,6 +44,7 @@ __global__ void sgd_kernel(float* __restrict__ param, const float* __restrict__ 
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nv; i += stride) {
     floatx4 p = reinterpret_cast<floatx4*>(param)[i];
     floatx4 g = reinterpret_cast<const floatx4*>(grad)[i] * grad_scale;
+    clear4(sp.zero, grad, i);
     if (sp.weight_decay != 0.f) g += sp.weight_decay * p;
     if (sp.momentum != 0.f) {
       floatx4 b;
@@ -43,6 +60,7 @@ __global__ void sgd_kernel(float* __restrict__ param, const float* __restrict__ 
   for (int64_t i = nv * 4 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride) {
     float p = param[i];
     float g = grad[i] * grad_scale;
+    if (in_zero(sp.zero, i)) grad[i] = 0.f;
     if (sp.weight_decay != 0.f) g += sp.weight_decay * p;
     if (sp.momentum != 0.f) {
       const float b = sp.first_step ? g : sp.momentum * mom[i] + (1.f - sp.dampening) * g;
@@ -67,7 +85,7 @@ __device__ __forceinline__ float adam_elem(float p, float g, float& m, float& v,
   return p - (lr / bc1) * m / denom;
 }
 
-__global__ void adam_kernel(float* __restrict__ param, const float* __restrict__ grad, float* __restrict__ mm,
+__global__ void adam_kernel(float* __restrict__ param, float* __restrict__ grad, float* __restrict__ mm,
                             float* __restrict__ vv, bf16_t* __restrict__ shadow, const float* __restrict__ hp,
                             float grad_scale, AdamParams ap, int64_t n) {
   const float lr = hp[0];
@@ -79,6 +97,7 @@ __global__ void adam_kernel(float* __restrict__ param, const float* __restrict__
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nv; i += stride) {
     floatx4 p = reinterpret_cast<floatx4*>(param)[i];
     const floatx4 g = reinterpret_cast<const floatx4*>(grad)[i] * grad_scale;
+    clear4(ap.zero, grad, i);
     floatx4 m = reinterpret_cast<floatx4*>(mm)[i];
     floatx4 v = reinterpret_cast<floatx4*>(vv)[i];
 #pragma unroll
@@ -96,6 +115,7 @@ __global__ void adam_kernel(float* __restrict__ param, const float* __restrict__
   for (int64_t i = nv * 4 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride) {
     float m = mm[i], v = vv[i];
     const float p = adam_elem(param[i], grad[i] * grad_scale, m, v, lr, bc1, bc2s, ap);
+    if (in_zero(ap.zero, i)) grad[i] = 0.f;
     param[i] = p;
     mm[i] = m;
     vv[i] = v;
@@ -112,14 +132,14 @@ inline int grid_for(int64_t n4) {
 
 }  // namespace
 
-hipError_t sgd_step(float* param, const float* grad, float* mom, uint16_t* shadow, const float* hp,
+hipError_t sgd_step(float* param, float* grad, float* mom, uint16_t* shadow, const float* hp,
                     float grad_scale, SgdParams sp, int64_t n, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   sgd_kernel<<<grid_for((n + 3) / 4), kBlock, 0, s>>>(param, grad, mom, shadow, hp, grad_scale, sp, n);
   return hipGetLastError();
 }
 
-hipError_t adam_step(float* param, const float* grad, float* m, float* v, uint16_t* shadow, const float* hp,
+hipError_t adam_step(float* param, float* grad, float* m, float* v, uint16_t* shadow, const float* hp,
                      float grad_scale, AdamParams ap, int64_t n, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   adam_kernel<<<grid_for((n + 3) / 4), kBlock, 0, s>>>(param, grad, m, v, shadow, hp, grad_scale, ap, n);

@@ -163,19 +163,28 @@ __global__ __launch_bounds__(256) void xent_rows_kernel(const bf16_t* __restrict
 #pragma unroll
     for (int v = 0; v < LD / 8; ++v) drow[v] = out[v];
   }
-  const int lane = threadIdx.x & 63;
+  // block-level reduction first: one atomic per statistic / bias column per BLOCK
+  // (same-address fp32 atomics serialise in L2; per-wave atomics cost ~9 us here)
+  __shared__ float part[4][LD + 2];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   loss = wave_sum(loss);
   correct = wave_sum(correct);
   if (lane == 0) {
-    atomicAdd(stats + 0, loss);
-    atomicAdd(stats + 1, correct);
+    part[w][LD] = loss;
+    part[w][LD + 1] = correct;
   }
   if (dbias) {
 #pragma unroll
     for (int c = 0; c < LD; ++c) {
       const float t = wave_sum(g[c]);
-      if (lane == 0) atomicAdd(dbias + c, t);
+      if (lane == 0) part[w][c] = t;
     }
+  }
+  __syncthreads();
+  const int t = threadIdx.x;
+  if (t < LD + 2 && (dbias || t >= LD)) {
+    const float v = part[0][t] + part[1][t] + part[2][t] + part[3][t];
+    atomicAdd(t < LD ? dbias + t : stats + (t - LD), v);
   }
 }
 

@@ -134,6 +134,29 @@ class StaticMLPEngine:
             self.exp_avg_sq = torch.zeros_like(f.master)
         self._grad_scale = 1.0 / self.world if average_grads else 1.0
 
+        # Gradients produced by accumulation (split-K wgrad atomics, bias-gradient
+        # atomics of the xent / dgrad epilogues) must start each step at zero.  The
+        # optimizer launch clears them right after consuming them, so the step has
+        # no zeroing launch (FlatParams allocates the grads zeroed for step 1).
+        self._wgrad_splitk = []
+        for l, layer in enumerate(self.layers):
+            M, N = self.dW[l].shape
+            tile, sk = self.C.gemm_plan(M, N, B, True)
+            self._wgrad_splitk.append(sk if tile == 128 else 1)
+        ranges = [(self._bias_begin, f.numel)]
+        for l in range(L):
+            if self._wgrad_splitk[l] > 1:
+                seg = f.seg(self.layers[l].weight)
+                ranges.append((seg.offset, seg.offset + seg.storage_numel))
+        merged = []
+        for b, e in sorted(ranges):
+            if merged and b <= merged[-1][1]:
+                merged[-1] = (merged[-1][0], max(merged[-1][1], e))
+            else:
+                merged.append((b, e))
+        # the optimizer kernels clear up to two ranges; any further ones get a fill launch
+        self._opt_zero, self._fill_zero = merged[:2], merged[2:]
+
         # ---- bucket plan: close a bucket after wgrad_l once it holds >= cap elements
         self.buckets: list[tuple[int, int, int]] = []   # (begin, end, trigger layer or -1 = end)
         begin = 0
@@ -159,7 +182,11 @@ class StaticMLPEngine:
                             dbias=self.db[L - 1], num_classes=self.num_classes, grad_scale=1.0 / self.B)
 
     def _wgrad(self, l):
-        self.C.gemm(self.dz[l + 1], self.h[l], self.dW[l], False, False)
+        sk = self._wgrad_splitk[l]
+        if sk > 1:   # accumulates into the grad the previous optimizer launch cleared
+            self.C.gemm(self.dz[l + 1], self.h[l], self.dW[l], False, False, beta=1.0, tile=128, splitk=sk)
+        else:
+            self.C.gemm(self.dz[l + 1], self.h[l], self.dW[l], False, False)
 
     def _dgrad(self, l):
         # dz_l(prev layer output) = (dz_{l+1} W_l) * act'(h_l), bias grad of layer l-1 fused
@@ -169,13 +196,14 @@ class StaticMLPEngine:
     def _opt(self, b, e):
         f, o, C = self.flat, self.optim, self.C
         p, g, sh = f.master[b:e], f.grad[b:e], f.shadow[b:e]
+        zr = [(max(zb, b) - b, min(ze, e) - b) for zb, ze in self._opt_zero if zb < e and ze > b]
         if o.name == "sgd":
             mom = self.mom[b:e] if self.mom is not None else p
             C.sgd_step(p, g, mom, sh, self.hp, self._grad_scale, o.momentum, o.dampening, o.weight_decay,
-                       o.nesterov, False)
+                       o.nesterov, False, zero_ranges=zr)
         else:
             C.adam_step(p, g, self.exp_avg[b:e], self.exp_avg_sq[b:e], sh, self.hp, self._grad_scale,
-                        o.betas[0], o.betas[1], o.eps, o.weight_decay, o.name == "adamw")
+                        o.betas[0], o.betas[1], o.eps, o.weight_decay, o.name == "adamw", zero_ranges=zr)
 
     # ------------------------------------------------------------ segmentation
     def _build_segments(self):
@@ -183,7 +211,8 @@ class StaticMLPEngine:
         # backward walk, cut after each bucket's trigger wgrad
         triggers = {t: i for i, (_, _, t) in enumerate(self.buckets) if t >= 0}
         pieces: list[list] = [[]]
-        pieces[0].append(lambda: self.flat.grad[self._bias_begin:].zero_())
+        for zb, ze in self._fill_zero:
+            pieces[0].append(lambda zb=zb, ze=ze: self.flat.grad[zb:ze].zero_())
         if self.optim.name in ("adam", "adamw"):
             pieces[0].append(lambda: self.C.bump_step(self.hp))
         pieces[0].append(self._forward)

@@ -35,6 +35,7 @@ import torch
 from ..data.loader import get_subset_loaders
 from ..models.layers import CrossEntropyLoss as LdnnCE
 from ..parallel.aggregation import Aggregator
+from ..utils.tracing import PhaseTimer, null_timer, trace_range
 from ..parallel.comm import MAX, MIN, SUM, Comm, default_comm
 from .straggler import StopLocalTraining, StragglerCutoff
 from .validator import validate
@@ -53,8 +54,13 @@ def _progress(it, enabled, desc):
 
 def train_local_epoch(model, trainloader, criterion, optimizer, device, scheduler=None, *, dp=None,
                       step_aggregator=None, cutoff: StragglerCutoff | None = None, max_steps: int | None = None,
-                      step_scheduler: bool = True):
-    """One pass over the rank's shard.  Returns (mean loss, accuracy %, per-batch losses)."""
+                      step_scheduler: bool = True, timer: PhaseTimer | None = None):
+    """One pass over the rank's shard.  Returns (mean loss, accuracy %, per-batch losses).
+
+    ``timer`` (utils.tracing.PhaseTimer) brackets forward / backward / grad_sync /
+    optimizer with roctx ranges and HIP events (BAR/trainer.py:194-223 has none).
+    """
+    tm = timer or null_timer()
     model.train()
     dev = torch.device(device)
     nb = len(trainloader) if max_steps is None else min(len(trainloader), max_steps)
@@ -67,19 +73,24 @@ def train_local_epoch(model, trainloader, criterion, optimizer, device, schedule
             if i >= nb:
                 break
             optimizer.zero_grad()
-            out = model(x)
-            if ldnn_ce:
-                loss = criterion(out, y, stats)
-            else:
-                loss = criterion(out.float(), y)
-                with torch.no_grad():
-                    stats[1] += (out.argmax(1) == y).sum()
-            loss.backward()
-            if dp is not None:
-                dp.finish_gradient_sync()
-            if step_aggregator is not None:
-                step_aggregator(model)
-            optimizer.step()
+            with tm.phase("forward"):
+                out = model(x)
+                if ldnn_ce:
+                    loss = criterion(out, y, stats)
+                else:
+                    loss = criterion(out.float(), y)
+                    with torch.no_grad():
+                        stats[1] += (out.argmax(1) == y).sum()
+            with tm.phase("backward"):
+                loss.backward()
+            if dp is not None or step_aggregator is not None:
+                with tm.phase("grad_sync"):
+                    if dp is not None:
+                        dp.finish_gradient_sync()
+                    if step_aggregator is not None:
+                        step_aggregator(model)
+            with tm.phase("optimizer"):
+                optimizer.step()
             losses[i] = loss.detach().float()
             total += y.numel()
             done += 1
@@ -135,8 +146,10 @@ def train_global(model, trainloader, val_loader, trainset, valset, indices_train
                  partition_rule: str = "reference_duration", repartition: bool = True, replace: bool = False,
                  seed: int = 0, legacy_gossip: bool = False, average_buffers: bool = False,
                  check_every: int = 20, progress: bool = True, logger=None, checkpointer=None,
-                 start_global_epoch: int = 0, histories=None, dtype=torch.float32, verbose: bool = True):
+                 start_global_epoch: int = 0, histories=None, dtype=torch.float32, verbose: bool = True,
+                 timer: PhaseTimer | None = None):
     comm = comm or default_comm()
+    tm = timer or null_timer()
     N = comm.world_size
     dev = torch.device(device)
     rng = np.random.default_rng(seed * 7919 + rank)
@@ -177,14 +190,15 @@ def train_global(model, trainloader, val_loader, trainset, valset, indices_train
             try:
                 loss, acc, bl = train_local_epoch(model, trainloader, criterion, optimizer, dev, scheduler, dp=dp,
                                                   step_aggregator=step_aggregator, cutoff=cutoff,
-                                                  max_steps=max_steps)
+                                                  max_steps=max_steps, timer=timer)
             except StopLocalTraining:
                 # cut by the collective time limit: keep LR schedules aligned across ranks
                 for _ in range(num_local_epochs - local_epoch - 1):
                     if scheduler is not None:
                         scheduler.step()
                 break
-            val_loss, val_acc = validate(model, val_loader, criterion, dev)
+            with tm.phase("validate"):
+                val_loss, val_acc = validate(model, val_loader, criterion, dev)
             records.append((loss, acc, val_loss, val_acc))
             batch_losses.append(bl)
             if verbose:
@@ -234,17 +248,17 @@ def train_global(model, trainloader, val_loader, trainset, valset, indices_train
         H["global_val_accuracies"].append(float(means[3]))
 
         # ---- end-of-global-epoch aggregation (reference schedule, A27)
-        if sync_every == "global_epoch":
-            aggregator(model)
-        elif sync_every == "step" and aggregation_by == "weights":
-            aggregator(model)
+        if sync_every == "global_epoch" or (sync_every == "step" and aggregation_by == "weights"):
+            with tm.phase("aggregate"):
+                aggregator(model)
 
         if rank == 0 and progress and verbose:
             print(f"[global epoch {global_epoch + 1}] train loss {means[0]:.4f} acc {means[1]:.2f}% | "
                   f"val loss {means[2]:.4f} acc {means[3]:.2f}%")
 
         # ---- sync + timing + re-partition (A30, A15/A16)
-        comm.barrier()
+        with trace_range("barrier"):
+            comm.barrier()
         duration = time.perf_counter() - t_start
         if repartition and prev_fraction + next_fraction > 0:
             if partition_rule == "reference_duration":

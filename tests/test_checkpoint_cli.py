@@ -77,3 +77,32 @@ def test_cli_single_process_cpu_run(tmp_path):
                  "3", "--epochs_local", "1", "--device", "cpu", "--quiet", "--out_dir", str(tmp_path), "--plots", "",
                  "--resume", "latest"])
     assert len(res2["histories"][4]) == 3  # 2 restored + 1 new global epoch
+
+
+def test_cli_trace_phase_times(tmp_path):
+    """--trace: roctx ranges (no-op without the native extension) + per-phase timers in metrics.jsonl."""
+    import json
+
+    from ldnn.cli import main
+    from ldnn.utils import tracing
+
+    try:
+        main(["--model", "mlp2", "--dataset", "mnist", "--n_train", "400", "--n_test", "80", "--epochs_global",
+              "1", "--epochs_local", "1", "--device", "cpu", "--quiet", "--out_dir", str(tmp_path), "--plots", "",
+              "--no_eval", "--trace"])
+    finally:
+        tracing.enable(False)
+    recs = [json.loads(l) for l in open(tmp_path / "metrics.rank0.jsonl")]
+    ph = [r for r in recs if r.get("kind") == "phase_times"][0]["phases"]
+    assert {"forward", "backward", "optimizer", "validate", "aggregate"} <= set(ph)
+    n = ph["forward"]["count"]
+    assert n > 0 and ph["backward"]["count"] == n and ph["optimizer"]["count"] == n
+
+
+def test_phase_timer_disabled_is_free():
+    from ldnn.utils.tracing import PhaseTimer
+
+    t = PhaseTimer(enabled=False)
+    with t.phase("x"):
+        pass
+    assert t.summary() == {}
