@@ -42,7 +42,8 @@ int64_t ld_of(const at::Tensor& t, const char* name) {
 //   a: if a_kcontig, [M][K] else [K][M];  b: if b_kcontig, [N][K] else [K][N];  c: [M][N]
 void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, bool a_kcontig, bool b_kcontig,
           int64_t epi, const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& aux,
-          const c10::optional<at::Tensor>& dbias, double beta, int64_t tile, int64_t splitk, bool direct_epi) {
+          const c10::optional<at::Tensor>& dbias, double beta, int64_t tile, int64_t splitk, bool direct_epi,
+          int64_t variant) {
   check_dev(a, at::kBFloat16, "a");
   check_dev(b, at::kBFloat16, "b");
   TORCH_CHECK(c.is_cuda() && (c.scalar_type() == at::kBFloat16 || c.scalar_type() == at::kFloat),
@@ -74,6 +75,7 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, bool a_
   p.ldc = (int)ldc;
   p.beta = (float)beta;
   p.direct_epi = direct_epi ? 1 : 0;
+  p.variant = (int)variant;
   if (epi == ldnn::EPI_BIAS || epi == ldnn::EPI_BIAS_RELU || epi == ldnn::EPI_BIAS_SIGMOID) {
     TORCH_CHECK(bias.has_value(), "gemm: bias epilogue needs a bias tensor");
     check_dev(*bias, at::kFloat, "bias");
@@ -267,6 +269,81 @@ void adam_step(const at::Tensor& param, const at::Tensor& grad, const at::Tensor
   check(ldnn::adam_step(param.data_ptr<float>(), grad.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(),
                         sh, hp.data_ptr<float>(), (float)grad_scale, ap, n, cur_stream(param)),
         "adam_step");
+}
+
+void head_fwd_xent(const at::Tensor& h, const at::Tensor& W, const at::Tensor& bias, const at::Tensor& labels,
+                   const c10::optional<at::Tensor>& logits, const at::Tensor& dlogits, const at::Tensor& stats,
+                   int64_t num_classes, double grad_scale) {
+  check_dev(h, at::kBFloat16, "h");
+  check_dev(W, at::kBFloat16, "W");
+  check_dev(bias, at::kFloat, "bias");
+  check_dev(labels, at::kLong, "labels");
+  check_dev(dlogits, at::kBFloat16, "dlogits");
+  check_dev(stats, at::kFloat, "stats");
+  TORCH_CHECK(h.dim() == 2 && W.dim() == 2 && dlogits.dim() == 2, "head: 2-D operands");
+  const int64_t B = h.size(0), K = h.size(1), ld = dlogits.size(1);
+  TORCH_CHECK(h.stride(1) == 1 && W.stride(1) == 1 && W.size(1) == K, "head: h / W must be k-contiguous, same K");
+  TORCH_CHECK(dlogits.is_contiguous() && dlogits.size(0) == B && ld % 16 == 0 && ld <= 64,
+              "head: dlogits must be a contiguous [B][ld] buffer, ld a multiple of 16 <= 64");
+  TORCH_CHECK(W.size(0) <= ld && num_classes <= W.size(0), "head: W rows must cover the classes, <= ld");
+  TORCH_CHECK(bias.is_contiguous() && bias.numel() >= ld, "head: bias must be padded to ld");
+  TORCH_CHECK(labels.is_contiguous() && labels.numel() == B, "head: bad labels");
+  TORCH_CHECK(stats.is_contiguous() && stats.numel() >= 2 * ((B + 15) / 16), "head: stats needs 2 floats per 16 rows");
+  TORCH_CHECK(h.stride(0) % 8 == 0 && W.stride(0) % 8 == 0 && K % 8 == 0 && aligned16(h.data_ptr()) &&
+                  aligned16(W.data_ptr()) && aligned16(bias.data_ptr()),
+              "head: 16-B aligned rows required");
+  ldnn::HeadParams p{};
+  p.h = bf16_ptr(h);
+  p.W = bf16_ptr(W);
+  p.bias = bias.data_ptr<float>();
+  p.labels = labels.data_ptr<int64_t>();
+  if (logits.has_value()) {
+    check_dev(*logits, at::kBFloat16, "logits");
+    TORCH_CHECK(logits->is_contiguous() && logits->sizes() == dlogits.sizes(), "head: logits like dlogits");
+    p.logits = bf16_mut(*logits);
+  }
+  p.dlogits = bf16_mut(dlogits);
+  p.stats = stats.data_ptr<float>();
+  p.B = (int)B;
+  p.K = (int)K;
+  p.C = (int)num_classes;
+  p.ld = (int)ld;
+  p.ldh = (int)h.stride(0);
+  p.ldw = (int)W.stride(0);
+  p.ldw_rows = (int)W.size(0);
+  p.grad_scale = (float)grad_scale;
+  c10::hip::HIPGuardMasqueradingAsCUDA g(h.device());
+  check(ldnn::head_fwd_xent(p, cur_stream(h)), "head_fwd_xent");
+}
+
+void head_wgrad(const at::Tensor& dz, const at::Tensor& h, const at::Tensor& dW, const c10::optional<at::Tensor>& db,
+                int64_t splits) {
+  check_dev(dz, at::kBFloat16, "dz");
+  check_dev(h, at::kBFloat16, "h");
+  check_dev(dW, at::kFloat, "dW");
+  const int64_t B = h.size(0), K = h.size(1), ld = dz.size(1);
+  TORCH_CHECK(dz.is_contiguous() && dz.size(0) == B && ld % 16 == 0 && ld <= 64, "head_wgrad: dz [B][ld], ld % 16 == 0");
+  TORCH_CHECK(h.stride(1) == 1 && h.stride(0) % 8 == 0 && K % 8 == 0 && aligned16(h.data_ptr()), "head_wgrad: bad h");
+  TORCH_CHECK(dW.dim() == 2 && dW.size(1) == K && dW.stride(1) == 1 && dW.size(0) <= ld && dW.stride(0) % 4 == 0 &&
+                  aligned16(dW.data_ptr()),
+              "head_wgrad: dW must be [rows <= ld][K] with 16-B aligned rows");
+  ldnn::HeadWgradParams p{};
+  p.dz = bf16_ptr(dz);
+  p.h = bf16_ptr(h);
+  p.dW = dW.data_ptr<float>();
+  if (db.has_value()) {
+    check_dev(*db, at::kFloat, "db");
+    TORCH_CHECK(db->is_contiguous() && db->numel() >= dW.size(0), "head_wgrad: bad db");
+    p.db = db->data_ptr<float>();
+  }
+  p.B = (int)B;
+  p.K = (int)K;
+  p.ld = (int)ld;
+  p.ldh = (int)h.stride(0);
+  p.lddw = (int)dW.stride(0);
+  p.nrows = (int)dW.size(0);
+  c10::hip::HIPGuardMasqueradingAsCUDA g(h.device());
+  check(ldnn::head_wgrad(p, (int)splits, cur_stream(h)), "head_wgrad");
 }
 
 void bump_step(const at::Tensor& hp) {
@@ -497,7 +574,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm", &gemm, "bf16 MFMA GEMM with fused epilogue", py::arg("a"), py::arg("b"), py::arg("c"),
         py::arg("a_kcontig"), py::arg("b_kcontig"), py::arg("epi") = 0, py::arg("bias") = py::none(),
         py::arg("aux") = py::none(), py::arg("dbias") = py::none(), py::arg("beta") = 0.0,
-        py::arg("tile") = 0, py::arg("splitk") = 0, py::arg("direct_epi") = false);
+        py::arg("tile") = 0, py::arg("splitk") = 0, py::arg("direct_epi") = false, py::arg("variant") = 0);
   m.def("act_fwd", &act_fwd);
   m.def("act_bwd", &act_bwd);
   m.def("colsum", &colsum, py::arg("x"), py::arg("out"), py::arg("accumulate") = false);
@@ -528,6 +605,12 @@ PYBIND11_MODULE(_C, m) {
         py::arg("eps"), py::arg("weight_decay"), py::arg("decoupled"),
         py::arg("zero_ranges") = std::vector<std::pair<int64_t, int64_t>>{});
   m.def("bump_step", &bump_step);
+  m.def("head_fwd_xent", &head_fwd_xent, "fused narrow Linear + softmax-xent + argmax (per-16-row stats slots)",
+        py::arg("h"), py::arg("W"), py::arg("bias"), py::arg("labels"), py::arg("logits"), py::arg("dlogits"),
+        py::arg("stats"), py::arg("num_classes"), py::arg("grad_scale"));
+  m.def("head_wgrad", &head_wgrad, "dW = dz^T h (+ db = colsum dz); splits > 1 accumulate atomically",
+        py::arg("dz"), py::arg("h"), py::arg("dW"), py::arg("db") = py::none(), py::arg("splits") = 0);
+  m.def("head_wgrad_splits", &ldnn::head_wgrad_splits, py::arg("B"), py::arg("K"));
   m.def("bn_fwd", &bn_fwd, py::arg("x"), py::arg("y"), py::arg("residual"), py::arg("gamma"), py::arg("beta"),
         py::arg("running_mean"), py::arg("running_var"), py::arg("save_mean"), py::arg("save_invstd"),
         py::arg("ws"), py::arg("eps"), py::arg("momentum"), py::arg("training"), py::arg("relu"));

@@ -15,12 +15,17 @@ typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 typedef __attribute__((address_space(3))) void lds_void;
 
 // ---- LDS image addressing --------------------------------------------------
-// KC image:      [ROWS][64 k], 128-B rows, chunk' = chunk ^ (row & 7)
-// strided image: [8 kb][ROWS/16 rb][8 k][16 r], 256-B blocks, odd kb: k ^= 4
-template <bool KC, int ROWS>
+// KC image, BK 64:  [ROWS][64 k], 128-B rows, chunk' = chunk ^ (row & 7)
+// KC image, BK 32:  [ROWS][32 k],  64-B rows, chunk' = chunk ^ (row & 8 ? 3 : 0)
+//   (ds_read_b128 lane groups {0-3,12-15,20-27}, ... each cover all 64 banks)
+// strided image:    [BK/8 kb][ROWS/16 rb][8 k][16 r], 256-B blocks, odd kb: k ^= 4
+__device__ __forceinline__ int kc32_sw(int row) { return (row & 8) ? 3 : 0; }
+
+template <bool KC, int ROWS, int BKt = BK>
 __device__ __forceinline__ int lds_offset(int row, int k) {
   if constexpr (KC) {
-    return row * 128 + ((((k >> 3) ^ (row & 7))) << 4) + (k & 7) * 2;
+    if constexpr (BKt == 64) return row * 128 + ((((k >> 3) ^ (row & 7))) << 4) + (k & 7) * 2;
+    else return row * 64 + ((((k >> 3) ^ kc32_sw(row))) << 4) + (k & 7) * 2;
   } else {
     const int kb = k >> 3, rb = row >> 4;
     const int rowp = (k & 7) ^ ((kb & 1) << 2);
@@ -29,12 +34,18 @@ __device__ __forceinline__ int lds_offset(int row, int k) {
 }
 
 // Inverse map: which (row, k) lands at 16-B LDS slot `o` (o multiple of 16).
-template <bool KC, int ROWS>
+template <bool KC, int ROWS, int BKt = BK>
 __device__ __forceinline__ void lds_slot_to_rk(int o, int& row, int& k) {
   if constexpr (KC) {
-    row = o >> 7;
-    const int pch = (o >> 4) & 7;
-    k = (pch ^ (row & 7)) * 8;
+    if constexpr (BKt == 64) {
+      row = o >> 7;
+      const int pch = (o >> 4) & 7;
+      k = (pch ^ (row & 7)) * 8;
+    } else {
+      row = o >> 6;
+      const int pch = (o >> 4) & 3;
+      k = (pch ^ kc32_sw(row)) * 8;
+    }
   } else {
     const int blk = o >> 8;
     const int kb = blk / (ROWS / 16), rb = blk % (ROWS / 16);
@@ -47,12 +58,15 @@ __device__ __forceinline__ void lds_slot_to_rk(int o, int& row, int& k) {
 // ---- fragment read: 16 rows (row tile rt) x 8 consecutive k (k-sub kk) ------
 // Lane l gets row (l & 15), k = kk*32 + 8*(l >> 4) + j, j = 0..7: the operand map
 // of v_mfma_f32_16x16x32_bf16 for both its A and its B operand.
-template <bool KC, int ROWS>
+template <bool KC, int ROWS, int BKt = BK>
 __device__ __forceinline__ bf16x8 read_frag(const char* lds, int rt, int kk, int lane) {
   if constexpr (KC) {
     const int row = rt * 16 + (lane & 15);
     const int chunk = kk * 4 + (lane >> 4);
-    return *reinterpret_cast<const bf16x8*>(lds + row * 128 + ((chunk ^ (row & 7)) << 4));
+    if constexpr (BKt == 64)
+      return *reinterpret_cast<const bf16x8*>(lds + row * 128 + ((chunk ^ (row & 7)) << 4));
+    else
+      return *reinterpret_cast<const bf16x8*>(lds + row * 64 + ((chunk ^ kc32_sw(row)) << 4));
   } else {
     const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
     const int kb = kk * 4 + g;

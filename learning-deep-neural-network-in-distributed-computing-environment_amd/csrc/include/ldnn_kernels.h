@@ -28,6 +28,7 @@ struct GemmParams {
   float beta;            // fp32 output only: C = acc + beta * C
   int splitk;            // >1: K split over gridDim.y, fp32 atomics into C (EPI_NONE, fp32 out, 128-tile)
   int direct_epi;        // 256-tile bf16 outputs: 1 = per-fragment stores (A/B knob), 0 = LDS-staged rows
+  int variant;           // 256-tile main loop: 0/1 = 2-stage BK64 (default), 2 = 4-slot BK32 ring, 3 = 5-slot ring
 };
 
 // Picks the tiling (256x256 LDS-DMA kernel or 128x128 kernel) from the shape.
@@ -136,6 +137,30 @@ hipError_t adam_step(float* param, float* grad, float* m, float* v, uint16_t* sh
                      float grad_scale, AdamParams ap, int64_t n, hipStream_t s);
 // hp[1] += 1 (graph-capturable step counter)
 hipError_t bump_step(float* hp, hipStream_t s);
+
+// ---- classifier head (<= 64 classes): fused Linear + softmax-xent, and its wgrad
+struct HeadParams {
+  const uint16_t* h;      // [B][ldh] bf16 input features
+  const uint16_t* W;      // [ldw_rows][ldw] bf16 weight (rows >= C zero-padded)
+  const float* bias;      // [ld] fp32 (zero-padded)
+  const int64_t* labels;  // [B]
+  uint16_t* logits;       // [B][ld] bf16 (optional)
+  uint16_t* dlogits;      // [B][ld] bf16, softmax - onehot, times grad_scale
+  float* stats;           // [ceil(B/16)][2] per-workgroup (loss sum, correct) accumulators
+  int B, K, C, ld, ldh, ldw, ldw_rows;
+  float grad_scale;
+};
+hipError_t head_fwd_xent(const HeadParams& p, hipStream_t s);
+struct HeadWgradParams {
+  const uint16_t* dz;  // [B][ld] bf16
+  const uint16_t* h;   // [B][ldh] bf16
+  float* dW;           // [nrows][lddw] fp32
+  float* db;           // [nrows] fp32 (optional)
+  int B, K, ld, ldh, lddw, nrows;
+};
+// splits > 1 accumulate with atomics into dW / db, which must be cleared; splits <= 0: auto
+hipError_t head_wgrad(const HeadWgradParams& p, int splits, hipStream_t s);
+int head_wgrad_splits(int B, int K);
 
 // ---- synthetic data (K20): deterministic device-side generator -----------
 hipError_t synth_normal_bf16(uint16_t* x, int64_t n, uint64_t seed, float stddev, hipStream_t s);

@@ -397,6 +397,156 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(GemmParams p) {
 
 }  // namespace k256
 
+// =============================================================================
+// gemm256 ring variant (GemmParams::variant 2 / 3, experimental): 256x256
+// output tile, BK = 32 slots in an NS-deep LDS ring (NS x 32 KiB), so the DMA
+// of K-step t+NS-1 is issued while step t is multiplied -- NS-1 K-steps of
+// latency cover instead of one.  One barrier per K-step both publishes step t
+// and frees the slot of step t-1 for refilling.  Measured on MI355X at 4096^3
+// it is SLOWER than the 2-stage BK 64 loop (fwd 1168 vs 1254 TF, dgrad 855 vs
+// 1091, wgrad 782 vs 942): twice the barriers per FLOP cost more than the
+// deeper prefetch buys (profiles/gemm_variants_r1.jsonl).
+// =============================================================================
+namespace k256r {
+
+using k256::barrier;
+constexpr int BM = 256, BN = 256, BKr = 32;
+constexpr int kThreads = 512;
+constexpr int kTileBytes = 256 * BKr * 2;             // 16 KiB per operand per slot
+constexpr int kSlotBytes = 2 * kTileBytes;            // A + B
+constexpr int kPiecesPerWave = kTileBytes / 1024 / 8;  // 2
+constexpr uint32_t kOOB = 0x80000000u;
+
+struct Operand {
+  __amdgpu_buffer_rsrc_t rsrc;
+  int ld, rows, K, r0;
+  int row[kPiecesPerWave];
+  int k[kPiecesPerWave];
+};
+
+template <bool KC>
+__device__ __forceinline__ void init_operand(Operand& op, const bf16_t* X, int ld, int rows, int K, int r0,
+                                             int wid, int lane) {
+  const uint32_t bytes = KC ? (uint32_t)((size_t)rows * ld * 2) : (uint32_t)((size_t)K * ld * 2);
+  op.rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)X, (short)0, (int)bytes, 0x00020000);
+  op.ld = ld;
+  op.rows = rows;
+  op.K = K;
+  op.r0 = r0;
+#pragma unroll
+  for (int i = 0; i < kPiecesPerWave; ++i) lds_slot_to_rk<KC, BM, BKr>((i * 8 + wid) * 1024 + lane * 16, op.row[i], op.k[i]);
+}
+
+template <bool KC>
+__device__ __forceinline__ void issue_tile(const Operand& op, char* dst, int k0, int wid) {
+#pragma unroll
+  for (int i = 0; i < kPiecesPerWave; ++i) {
+    const int gr = op.r0 + op.row[i], gk = k0 + op.k[i];
+    const bool ok = (gr < op.rows) && (gk < op.K);
+    const uint32_t off = KC ? (uint32_t)(((size_t)gr * op.ld + gk) * 2) : (uint32_t)(((size_t)gk * op.ld + gr) * 2);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(op.rsrc, (lds_void*)(dst + (i * 8 + wid) * 1024), 16, ok ? off : kOOB,
+                                             0, 0, 0);
+  }
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// own DMAs of step t landed, with `ahead` later steps (4 instructions each) allowed in flight
+template <int NS>
+__device__ __forceinline__ void wait_step(int ahead) {
+  if constexpr (NS >= 5) {
+    if (ahead >= 3) { wait_vm<12>(); return; }
+  }
+  if constexpr (NS >= 4) {
+    if (ahead >= 2) { wait_vm<8>(); return; }
+  }
+  if (ahead >= 1) { wait_vm<4>(); return; }
+  wait_vm<0>();
+}
+
+template <bool A_KC, bool B_KC, int EPI, bool OUT_F32, int NS>
+__global__ __launch_bounds__(kThreads, 1) void gemm_kernel(GemmParams p) {
+  __shared__ __attribute__((aligned(1024))) char smem[NS * kSlotBytes];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 2, wn = wid & 3;
+  int m0, n0;
+  tile_coords(p.M, p.N, BM, BN, m0, n0);
+
+  Operand oa, ob;
+  init_operand<A_KC>(oa, p.A, p.lda, p.M, p.K, m0, wid, lane);
+  init_operand<B_KC>(ob, p.B, p.ldb, p.N, p.K, n0, wid, lane);
+
+  floatx4 acc[4][8];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[j][i] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (p.K + BKr - 1) / BKr;
+#pragma unroll
+  for (int t = 0; t < NS - 1; ++t) {
+    if (t < nk) {
+      char* slot = smem + t * kSlotBytes;
+      issue_tile<A_KC>(oa, slot, t * BKr, wid);
+      issue_tile<B_KC>(ob, slot + kTileBytes, t * BKr, wid);
+    }
+  }
+
+  int cur = 0;  // slot of step t
+  for (int t = 0; t < nk; ++t) {
+    // steps t+1 .. min(t+NS-2, nk-1) may stay in flight
+    const int ahead = min(NS - 2, nk - 1 - t);
+    wait_step<NS>(ahead);
+    barrier();  // step t visible to all waves; every wave is done with step t-1
+    {
+      const int tn = t + NS - 1;
+      if (tn < nk) {
+        const int sl = cur == 0 ? NS - 1 : cur - 1;  // slot of step t-1
+        char* slot = smem + sl * kSlotBytes;
+        issue_tile<A_KC>(oa, slot, tn * BKr, wid);
+        issue_tile<B_KC>(ob, slot + kTileBytes, tn * BKr, wid);
+      }
+    }
+    const char* la = smem + cur * kSlotBytes;
+    const char* lb = la + kTileBytes;
+    __builtin_amdgcn_s_setprio(1);
+    bf16x8 fb[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) fb[j] = read_frag<B_KC, BN, BKr>(lb, wn * 4 + j, 0, lane);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      bf16x8 fa[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[i] = read_frag<A_KC, BM, BKr>(la, wm * 8 + h * 4 + i, 0, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          acc[j][h * 4 + i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[j][h * 4 + i], 0, 0, 0);
+    }
+    __builtin_amdgcn_s_setprio(0);
+    cur = cur == NS - 1 ? 0 : cur + 1;
+  }
+  if constexpr (!OUT_F32) {
+    barrier();
+    k256::epilogue_lds_bf16<EPI>(p, acc, smem, wid, m0 + wm * 128, n0 + wn * 64, lane);
+  } else {
+    epilogue<EPI, OUT_F32, 8, 4>(p, acc, m0 + wm * 128, n0 + wn * 64, lane);
+  }
+}
+
+}  // namespace k256r
+
 
 
 // =============================================================================
@@ -472,10 +622,16 @@ hipError_t dispatch_epi(const GemmParams& p, int epi, hipStream_t s) {
   dim3 grid(tiles, TILE == 128 ? max(1, p.splitk) : 1);
 #define LDNN_GEMM_CASE(E)                                                                          \
   case E:                                                                                          \
-    if constexpr (TILE == 256)                                                                     \
-      k256::gemm_kernel<A_KC, B_KC, E, OUT_F32><<<grid, dim3(k256::kThreads), 0, s>>>(p);         \
-    else                                                                                           \
+    if constexpr (TILE == 256) {                                                                   \
+      if (p.variant == 2)                                                                          \
+        k256r::gemm_kernel<A_KC, B_KC, E, OUT_F32, 4><<<grid, dim3(k256r::kThreads), 0, s>>>(p);  \
+      else if (p.variant == 3)                                                                     \
+        k256r::gemm_kernel<A_KC, B_KC, E, OUT_F32, 5><<<grid, dim3(k256r::kThreads), 0, s>>>(p);  \
+      else                                                                                         \
+        k256::gemm_kernel<A_KC, B_KC, E, OUT_F32><<<grid, dim3(k256::kThreads), 0, s>>>(p);       \
+    } else {                                                                                       \
       k128::gemm_kernel<A_KC, B_KC, E, OUT_F32><<<grid, dim3(k128::kThreads), 0, s>>>(p);         \
+    }                                                                                              \
     break;
   switch (epi) {
     LDNN_GEMM_CASE(EPI_NONE)

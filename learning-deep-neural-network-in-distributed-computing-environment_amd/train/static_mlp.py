@@ -78,7 +78,7 @@ class _Segment:
 class StaticMLPEngine:
     def __init__(self, model, batch_size: int, optim: OptimConfig | None = None, *, device=None,
                  process_group=None, world_size: int | None = None, bucket_cap_elems: int = 8 << 20,
-                 use_graphs: bool = True, average_grads: bool = True):
+                 use_graphs: bool = True, average_grads: bool = True, use_head_kernels: bool = True):
         from ..models.mlp import MLP
 
         if not isinstance(model, MLP):
@@ -125,7 +125,13 @@ class StaticMLPEngine:
         self.labels = torch.zeros(B, dtype=torch.long, device=dev)
         self.h = [self.x] + [torch.zeros(B, n, dtype=bf, device=dev) for n in npad]
         self.dz = [None] + [torch.zeros(B, n, dtype=bf, device=dev) for n in npad]
-        self.stats = torch.zeros(2, dtype=torch.float32, device=dev)    # [loss_sum, correct]
+        # classifier head kernels (head.hip): fused last Linear + softmax-xent, and a
+        # transposed-read wgrad, for <= 64 (padded) classes
+        self.use_head = (npad[-1] % 16 == 0 and npad[-1] <= 64 and self.layers[-1].in_features % 8 == 0
+                         and use_head_kernels)
+        # [loss_sum, correct] -- one pair per 16-row workgroup of the head kernel
+        nslots = (B + 15) // 16 if self.use_head else 1
+        self.stats = torch.zeros(nslots, 2, dtype=torch.float32, device=dev)
         self.hp = torch.tensor([self.optim.lr, 0.0], dtype=torch.float32, device=dev)
         o = self.optim
         self.mom = torch.zeros_like(f.master) if (o.name == "sgd" and o.momentum != 0) else None
@@ -141,6 +147,9 @@ class StaticMLPEngine:
         self._wgrad_splitk = []
         for l, layer in enumerate(self.layers):
             M, N = self.dW[l].shape
+            if self.use_head and l == L - 1:
+                self._wgrad_splitk.append(self.C.head_wgrad_splits(B, N))
+                continue
             tile, sk = self.C.gemm_plan(M, N, B, True)
             self._wgrad_splitk.append(sk if tile == 128 else 1)
         ranges = [(self._bias_begin, f.numel)]
@@ -170,19 +179,27 @@ class StaticMLPEngine:
         self._build_segments()
 
     # ------------------------------------------------------------------ kernels
-    def _forward(self):
+    def _forward(self, train: bool = False):
         C = self.C
-        for l in range(len(self.layers)):
+        L = len(self.layers)
+        for l in range(L - 1 if (train and self.use_head) else L):
             C.gemm(self.h[l], self.W[l], self.h[l + 1], True, True, self._fwd_epi[l], bias=self.bias[l])
 
     def _loss(self):
         L = len(self.layers)
+        if self.use_head:   # last Linear + softmax-xent + argmax in one launch
+            self.C.head_fwd_xent(self.h[L - 1], self.W[L - 1], self.bias[L - 1], self.labels, self.h[L], self.dz[L],
+                                 self.stats, self.num_classes, 1.0 / self.B)
+            return
         logits = self.h[L][:, : self.num_classes]
         self.C.softmax_xent(logits, self.labels, self.dz[L][:, : self.num_classes], self.stats,
                             dbias=self.db[L - 1], num_classes=self.num_classes, grad_scale=1.0 / self.B)
 
     def _wgrad(self, l):
         sk = self._wgrad_splitk[l]
+        if self.use_head and l == len(self.layers) - 1:   # also emits the head's bias gradient
+            self.C.head_wgrad(self.dz[l + 1], self.h[l], self.dW[l], self.db[l], sk)
+            return
         if sk > 1:   # accumulates into the grad the previous optimizer launch cleared
             self.C.gemm(self.dz[l + 1], self.h[l], self.dW[l], False, False, beta=1.0, tile=128, splitk=sk)
         else:
@@ -215,7 +232,7 @@ class StaticMLPEngine:
             pieces[0].append(lambda zb=zb, ze=ze: self.flat.grad[zb:ze].zero_())
         if self.optim.name in ("adam", "adamw"):
             pieces[0].append(lambda: self.C.bump_step(self.hp))
-        pieces[0].append(self._forward)
+        pieces[0].append(lambda: self._forward(train=True))
         pieces[0].append(self._loss)
         self._cut_buckets = []
         for l in reversed(range(L)):
@@ -276,7 +293,7 @@ class StaticMLPEngine:
         self.stats.zero_()
 
     def read_stats(self, samples: int):
-        s = self.stats.tolist()
+        s = self.stats.sum(0).tolist()
         return s[0] / max(samples, 1), 100.0 * s[1] / max(samples, 1)
 
     @torch.no_grad()

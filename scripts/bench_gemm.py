@@ -47,8 +47,9 @@ def main():
         for tile in (128, 256):
             t = min(timeit(lambda: C.gemm(a, b, c, akc, bkc, tile=tile)) for _ in range(3))
             row[f"t{tile}_tflops"] = round(fl / t / 1e9, 1)
-        t = min(timeit(lambda: C.gemm(a, b, c, akc, bkc, tile=256, direct_epi=True)) for _ in range(3))
-        row["t256_direct_epi_tflops"] = round(fl / t / 1e9, 1)
+        for v in (1, 2, 3):
+            t = min(timeit(lambda: C.gemm(a, b, c, akc, bkc, tile=256, variant=v)) for _ in range(3))
+            row[f"t256_v{v}_tflops"] = round(fl / t / 1e9, 1)
         t_ref = min(timeit(lambda: torch.matmul(A, B)) for _ in range(3))
         row["torch_tflops"] = round(fl / t_ref / 1e9, 1)
         print(json.dumps(row), flush=True)

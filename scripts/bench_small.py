@@ -57,3 +57,11 @@ res["xent_nodb"] = t(lambda: C.softmax_xent(lg[:, :10], labels, dl[:, :10], stat
 res["fill_small"] = t(lambda: db.zero_())
 for k, v in res.items():
     print(f"{k:28s} {v:8.1f} us")
+hstats = torch.zeros(B // 16, 2, device=dev)
+res2 = {}
+res2["head_fwd_xent"] = t(lambda: C.head_fwd_xent(h2, W3, bias3, labels, h3, dz3, hstats, 10, 1.0 / B))
+dW3z = torch.zeros(NC, H, device=dev)
+for sp in (1, 4, 8, 16):
+    res2[f"head_wgrad_s{sp}"] = t(lambda: C.head_wgrad(dz3, h2, dW3z, db3, sp))
+for k, v in res2.items():
+    print(f"{k:28s} {v:8.1f} us")

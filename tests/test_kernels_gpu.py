@@ -40,6 +40,24 @@ def test_gemm_layouts(tile, a_kc, b_kc, M, N, K):
     assert rel < 1e-2, rel
 
 
+@pytest.mark.parametrize("variant", [1, 2, 3])
+@pytest.mark.parametrize("a_kc,b_kc", [(True, True), (True, False), (False, False)])
+@pytest.mark.parametrize("M,N,K", [(520, 776, 520), (256, 256, 32), (296, 264, 4200)])
+def test_gemm256_main_loop_variants(variant, a_kc, b_kc, M, N, K):
+    """2-stage BK64 (1) and the 4-/5-slot BK32 LDS rings (2, 3), ragged edges and odd K-step counts."""
+    torch.manual_seed(1)
+    a = (torch.randn(M, K, device="cuda") if a_kc else torch.randn(K, M, device="cuda")).bfloat16()
+    b = (torch.randn(N, K, device="cuda") if b_kc else torch.randn(K, N, device="cuda")).bfloat16()
+    ref = _ref_gemm(a, b, a_kc, b_kc)
+    c = torch.empty(M, N, device="cuda")
+    C().gemm(a, b, c, a_kc, b_kc, tile=256, variant=variant)
+    torch.cuda.synchronize()
+    assert (c - ref).abs().max().item() <= 1e-3 * K ** 0.5 + 1e-3
+    cb = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    C().gemm(a, b, cb, a_kc, b_kc, tile=256, variant=variant)
+    assert ((cb.float() - ref).abs().max() / ref.abs().max()).item() < 1e-2
+
+
 @pytest.mark.parametrize("tile", [128, 256])
 def test_gemm_asymmetric_identity(tile):
     """A = I with an asymmetric B catches a transposed C write."""
@@ -217,3 +235,47 @@ def test_gemm_skinny_n_forward(N, epi):
     if epi == "relu":
         ref = ref.relu()
     torch.testing.assert_close(y.float(), ref, rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("B,K,ncls,ld", [(4096, 4096, 10, 16), (1000, 784, 10, 16), (333, 520, 40, 48)])
+def test_head_fwd_xent(B, K, ncls, ld):
+    """Fused last Linear + softmax-xent + argmax vs fp32 PyTorch (logits rounded to bf16 first)."""
+    torch.manual_seed(2)
+    h = torch.randn(B, K, device="cuda").bfloat16()
+    W = torch.zeros(ld, K, device="cuda")
+    W[:ncls] = torch.randn(ncls, K, device="cuda") * K ** -0.5
+    W = W.bfloat16()
+    bias = torch.zeros(ld, device="cuda")
+    bias[:ncls] = torch.randn(ncls, device="cuda")
+    y = torch.randint(0, ncls, (B,), device="cuda")
+    logits = torch.empty(B, ld, device="cuda", dtype=torch.bfloat16)
+    dl = torch.empty_like(logits)
+    stats = torch.zeros((B + 15) // 16, 2, device="cuda")
+    C().head_fwd_xent(h, W, bias, y, logits, dl, stats, ncls, 1.0 / B)
+    ref = h.float() @ W.float().t() + bias
+    assert ((logits.float() - ref).abs().max() / ref.abs().max()).item() < 1e-2
+    assert logits[:, ncls:].float().abs().max().item() == 0.0
+    lr = logits.float()[:, :ncls]
+    loss = torch.nn.functional.cross_entropy(lr, y, reduction="sum")
+    s = stats.sum(0)
+    assert abs(s[0].item() - loss.item()) <= 1e-3 * loss.item() + 1e-2
+    assert s[1].item() == (lr.argmax(1) == y).sum().item()
+    g = (torch.softmax(lr, 1) - torch.nn.functional.one_hot(y, ncls).float()) / B
+    assert (dl.float()[:, :ncls] - g).abs().max().item() < 2e-2 / B + 1e-6
+    assert dl[:, ncls:].float().abs().max().item() == 0.0
+
+
+@pytest.mark.parametrize("splits", [1, 3, 0])
+@pytest.mark.parametrize("B,K,ld,rows", [(4096, 4096, 16, 16), (1000, 784, 16, 16), (300, 520, 48, 40)])
+def test_head_wgrad(splits, B, K, ld, rows):
+    torch.manual_seed(3)
+    dz = torch.randn(B, ld, device="cuda")
+    dz[:, rows:] = 0
+    dz = dz.bfloat16()
+    h = torch.randn(B, K, device="cuda").bfloat16()
+    dW = torch.zeros(rows, K, device="cuda")
+    db = torch.zeros(rows, device="cuda")
+    C().head_wgrad(dz, h, dW, db, splits)
+    ref = dz.float()[:, :rows].t() @ h.float()
+    assert ((dW - ref).abs().max() / ref.abs().max()).item() < 1e-4
+    assert (db - dz.float()[:, :rows].sum(0)).abs().max().item() < 1e-2
