@@ -88,7 +88,7 @@ def run_ldnn(ctx, args):
     xavier_init(model)
     eng = StaticMLPEngine(model, args.batch, OptimConfig("sgd", lr=args.lr, momentum=0.9),
                           device=ctx.device, world_size=ctx.world_size, use_graphs=not args.no_graphs,
-                          bucket_cap_elems=args.bucket_elems)
+                          bucket_cap_elems=args.bucket_elems, shard_optimizer=False if args.no_shard else None)
     if ctx.distributed:
         dist.broadcast(eng.flat.master, src=0)
         eng.flat.refresh_shadow()
@@ -144,6 +144,8 @@ def main():
     ap.add_argument("--nbatches", type=int, default=4)
     ap.add_argument("--bucket-elems", type=int, default=8 << 20)
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--no-shard", action="store_true",
+                    help="all-reduce + replicated optimizer instead of reduce-scatter / sharded optimizer / all-gather")
     ap.add_argument("--compare-stock", action="store_true")
     ap.add_argument("--backend", default="auto", help="auto (nccl = RCCL on GPUs) | gloo (testing only)")
     args = ap.parse_args()
@@ -173,7 +175,9 @@ def main():
             "seq_len": None,
             "parallelism": f"dp{n}",
             "optimizer": "sgd momentum 0.9, fp32 master",
-            "grad_allreduce": "fp32 RCCL, bucketed, overlapped" if n > 1 else "none (1 GPU)",
+            "grad_sync": ("none (1 GPU)" if n == 1 else
+                          "fp32 RCCL all-reduce, bucketed, overlapped" if args.no_shard else
+                          "fp32 RCCL reduce-scatter (bucketed, overlapped) + sharded SGD + bf16 weight all-gather"),
         },
     }
     rec.update(extra)

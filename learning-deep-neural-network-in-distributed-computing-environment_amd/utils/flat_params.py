@@ -42,6 +42,15 @@ def owner_of(p: nn.Parameter):
     return _OWNER.get(id(p))
 
 
+def storage_numel(shape, pad_rows: bool = True) -> int:
+    """Elements a parameter of `shape` occupies in the flat buffers (padding + 64-alignment)."""
+    sshape = _pad_rows(torch.Size(shape)) if (pad_rows and len(shape) >= 1) else tuple(shape)
+    n = 1
+    for d in sshape:
+        n *= d
+    return (n + _ALIGN - 1) // _ALIGN * _ALIGN
+
+
 def _pad_rows(shape: torch.Size, multiple: int = 8) -> tuple:
     """Padded storage shape: leading dim to a multiple of 8 and, for 2-D
     (Linear) weights, the inner dim too, so every GEMM operand row is a whole
@@ -71,7 +80,8 @@ class FlatParams:
     """Owns flat master/grad/shadow buffers for ``module``'s parameters."""
 
     def __init__(self, module: nn.Module, device: torch.device | str | None = None, pad_rows: bool = True,
-                 shadow: bool | None = None, grad_ready_order: bool = True, order: list | None = None):
+                 shadow: bool | None = None, grad_ready_order: bool = True, order: list | None = None,
+                 align_after: dict | None = None):
         self.module = module
         params = [(n, p) for n, p in module.named_parameters() if p.requires_grad]
         if device is None:
@@ -94,6 +104,9 @@ class FlatParams:
                 snumel *= d
             segs.append(Segment(name, p, off, p.numel(), sshape, snumel))
             off += (snumel + _ALIGN - 1) // _ALIGN * _ALIGN
+            if align_after and id(p) in align_after:  # e.g. a bucket boundary that must split N ways
+                a = int(align_after[id(p)])
+                off = (off + a - 1) // a * a
         self.numel = off
         self.segments = segs
         self.by_param = {id(s.param): s for s in segs}

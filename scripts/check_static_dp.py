@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--cap", type=int, default=1 << 17)
     ap.add_argument("--steps", type=int, default=6)
+    ap.add_argument("--shard", type=int, default=-1, help="-1 auto (on for N > 1), 0 off, 1 on")
     a = ap.parse_args()
     ctx = D.setup(a.backend)
     N, r = ctx.world_size, ctx.rank
@@ -35,7 +36,9 @@ def main():
     model = mlp3(784, H, 10)
     # small bucket cap -> several buckets / segments on the multi-rank path
     eng = StaticMLPEngine(model, B, OptimConfig("sgd", lr=0.05, momentum=0.9), device=ctx.device, world_size=N,
-                          bucket_cap_elems=a.cap, use_graphs=bool(a.graphs))
+                          bucket_cap_elems=a.cap, use_graphs=bool(a.graphs),
+                          shard_optimizer=None if a.shard < 0 else bool(a.shard))
+    print(f"rank {r}: shard={eng.shard}", flush=True)
     print(f"rank {r}: buckets {eng.buckets}", flush=True)
     g = torch.Generator(device="cpu").manual_seed(5)
     S = a.steps
@@ -46,10 +49,14 @@ def main():
         eng.load_batch(xs[i][r * B:(r + 1) * B].to(ctx.device).bfloat16(), ys[i][r * B:(r + 1) * B].to(ctx.device))
         eng.step()
         torch.cuda.synchronize()
-        print(f"rank {r} step {i} loss {eng.read_stats(B)[0]:.5f} finite={bool(torch.isfinite(eng.flat.master).all())}",
+        print(f"rank {r} step {i} loss {eng.read_stats(B)[0]:.5f} finite={bool(torch.isfinite(eng.flat.shadow).all())}",
               flush=True)
+    eng.gather_master()   # sharded optimizer: make the fp32 master whole on every rank
     torch.cuda.synchronize()
     got = eng.flat.master.detach().cpu().clone()
+    sh = eng.flat.shadow.detach().float().cpu()
+    print(f"rank {r}: shadow == bf16(master): "
+          f"{bool(torch.equal(sh, eng.flat.master.detach().bfloat16().float().cpu()))}", flush=True)
     if r == 0:
         # single-rank reference on the concatenated batch (same kernels, no graphs)
         torch.manual_seed(0)

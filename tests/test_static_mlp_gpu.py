@@ -89,3 +89,37 @@ def test_multirank_static_engine_gloo_two_ranks_one_gpu():
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     assert "STATIC_DP_OK" in r.stdout and "REPLICAS_IDENTICAL" in r.stdout, r.stdout[-3000:]
+
+
+@pytest.mark.parametrize("opt", ["sgd", "adam"])
+def test_sharded_optimizer_path_on_rccl_single_rank(opt, tmp_path):
+    """The reduce-scatter / sharded-optimizer / in-place all-gather path on a real RCCL
+    communicator (world 1, forced), graphs on, several buckets: identical to the
+    single-segment engine."""
+    import torch.distributed as dist
+
+    store = dist.FileStore(str(tmp_path / "store"), 1)
+    dist.init_process_group("nccl", store=store, rank=0, world_size=1, device_id=torch.device("cuda:0"))
+    try:
+        torch.manual_seed(0)
+        B = 512
+        m1, m2 = mlp3(784, 1024, 10), mlp3(784, 1024, 10)
+        m2.load_state_dict(m1.state_dict())
+        cfg = OptimConfig(opt, lr=0.05 if opt == "sgd" else 1e-3, momentum=0.9)
+        e1 = StaticMLPEngine(m1, B, cfg, use_graphs=True, shard_optimizer=True, bucket_cap_elems=1 << 18)
+        e2 = StaticMLPEngine(m2, B, cfg, use_graphs=True)
+        assert e1.shard and len(e1.buckets) >= 2
+        g = torch.Generator(device="cuda").manual_seed(4)
+        for step in range(6):
+            x = torch.randn(B, 784, device="cuda", generator=g).bfloat16()
+            y = torch.randint(0, 10, (B,), device="cuda", generator=g)
+            for e in (e1, e2):
+                e.load_batch(x, y)
+                e.step()
+        e1.gather_master()
+        torch.cuda.synchronize()
+        for p, q in zip(m1.parameters(), m2.parameters()):
+            torch.testing.assert_close(p.detach(), q.detach(), rtol=1e-5, atol=1e-6)
+        assert torch.equal(e1.flat.shadow, e1.flat.master.bfloat16())
+    finally:
+        dist.destroy_process_group()
