@@ -79,7 +79,7 @@ class StaticMLPEngine:
     def __init__(self, model, batch_size: int, optim: OptimConfig | None = None, *, device=None,
                  process_group=None, world_size: int | None = None, bucket_cap_elems: int = 8 << 20,
                  use_graphs: bool = True, average_grads: bool = True, use_head_kernels: bool = True,
-                 shard_optimizer: bool | None = None):
+                 shard_optimizer: bool | None = None, overlap_optimizer: bool = False):
         from ..models.mlp import MLP
 
         if not isinstance(model, MLP):
@@ -202,6 +202,8 @@ class StaticMLPEngine:
             self._opt_zero, self._fill_zero = merged[:2], merged[2:]
 
         self.rank = dist.get_rank(process_group) if self.distributed else 0
+        self.overlap_optimizer = overlap_optimizer
+        self.side = torch.cuda.Stream(device=self.device) if overlap_optimizer else None
         self._pending_gather = []
         if self.shard:
             self.gshard = [torch.zeros((e - b) // self.world, dtype=torch.float32, device=dev)
@@ -240,6 +242,16 @@ class StaticMLPEngine:
         # dz_l(prev layer output) = (dz_{l+1} W_l) * act'(h_l), bias grad of layer l-1 fused
         self.C.gemm(self.dz[l + 1], self.W[l], self.dz[l], True, False, self._dgrad_epi[l], aux=self.h[l],
                     dbias=self.db[l - 1])
+
+    def _fork_opt(self, ranges):
+        self.side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(self.side):
+            for b, e in ranges:
+                if e > b:
+                    self._opt(b, e)
+
+    def _join(self):
+        torch.cuda.current_stream().wait_stream(self.side)
 
     def _shard_range(self, i):
         b, e, _ = self.buckets[i]
@@ -287,7 +299,24 @@ class StaticMLPEngine:
             return f
 
         if not self.distributed:
-            fns = [fn for p in pieces for fn in p] + [lambda: self._opt(0, self.flat.numel)]
+            if L >= 2 and self.overlap_optimizer:
+                # Once the last dgrad (layer 1) has run, every gradient except W_0's is
+                # final and no later kernel reads those weights: their optimizer update
+                # runs on a side stream beside the last wgrad (a 224-tile GEMM that
+                # leaves CUs and HBM bandwidth idle); W_0's update follows on the
+                # main stream.  Fork/join are stream-event edges inside the graph.
+                # Off by default: measured on MI355X the bandwidth-bound SGD slows the
+                # latency-bound wgrad from 68 to 119 us, a net loss (0.654 vs 0.624 ms).
+                w0 = self.flat.seg(self.layers[0].weight).offset
+                side = [(0, w0), (self._bias_begin, self.flat.numel)]
+                fns = []
+                for p in pieces:
+                    for fn in p:
+                        fns.append(fn)
+                fns.insert(len(fns) - 1, lambda: self._fork_opt(side))   # before wgrad(0)
+                fns += [lambda: self._opt(w0, self._bias_begin), self._join]
+            else:
+                fns = [fn for p in pieces for fn in p] + [lambda: self._opt(0, self.flat.numel)]
             self.segments = [_Segment(run(fns), self.use_graphs)]
             self.opt_segments = []
         else:
