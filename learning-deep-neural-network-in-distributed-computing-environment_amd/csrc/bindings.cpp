@@ -43,7 +43,7 @@ int64_t ld_of(const at::Tensor& t, const char* name) {
 void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, bool a_kcontig, bool b_kcontig,
           int64_t epi, const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& aux,
           const c10::optional<at::Tensor>& dbias, double beta, int64_t tile, int64_t splitk, bool direct_epi,
-          int64_t variant) {
+          int64_t variant, const c10::optional<at::Tensor>& ws, const c10::optional<at::Tensor>& cnt) {
   check_dev(a, at::kBFloat16, "a");
   check_dev(b, at::kBFloat16, "b");
   TORCH_CHECK(c.is_cuda() && (c.scalar_type() == at::kBFloat16 || c.scalar_type() == at::kFloat),
@@ -106,8 +106,22 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, bool a_
     check(ldnn::gemm_skinny_n(p, (int)epi, cur_stream(a)), "gemm_skinny_n");
     return;
   }
-  if (tile == 128 && out_f32 && epi == ldnn::EPI_NONE && !dbias.has_value() && (beta == 0.0 || beta == 1.0))
+  if (ws.has_value() || cnt.has_value()) {
+    // in-launch split-K combine: explicit split count, any epilogue, deterministic
+    TORCH_CHECK(ws.has_value() && cnt.has_value() && tile == 128 && splitk > 1,
+                "gemm: ws/cnt (split-K combine) need tile=128 and splitk > 1");
+    check_dev(*ws, at::kFloat, "ws");
+    check_dev(*cnt, at::kInt, "cnt");
+    TORCH_CHECK(ws->is_contiguous() && (size_t)ws->numel() * 4 >= ldnn::gemm_splitk_ws_bytes(p.M, p.N, (int)splitk),
+                "gemm: split-K workspace too small");
+    TORCH_CHECK(cnt->is_contiguous() && cnt->numel() >= ldnn::gemm_tiles128(p.M, p.N), "gemm: too few counters");
+    TORCH_CHECK(aligned16(ws->data_ptr()), "gemm: workspace alignment");
+    p.splitk = (int)splitk;
+    p.ws = ws->data_ptr<float>();
+    p.cnt = cnt->data_ptr<int>();
+  } else if (tile == 128 && out_f32 && epi == ldnn::EPI_NONE && !dbias.has_value() && (beta == 0.0 || beta == 1.0)) {
     p.splitk = splitk > 0 ? (int)splitk : ldnn::gemm_pick_splitk(p.M, p.N, p.K);
+  }
   check(ldnn::gemm_bf16_tile(p, a_kcontig, b_kcontig, (int)epi, out_f32, (int)tile, cur_stream(a)), "gemm");
 }
 
@@ -383,6 +397,24 @@ ldnn::ConvShape conv_shape(const at::Tensor& x, const at::Tensor& w, const at::T
   return s;
 }
 
+// Split-K workspace of a small-M conv (fresh from the caching allocator: stream
+// ordered, graph-capture safe; the counters come zeroed).
+struct ConvWs {
+  at::Tensor slabs, cnt;
+  float* ws() const { return slabs.defined() ? slabs.data_ptr<float>() : nullptr; }
+  int* c() const { return cnt.defined() ? cnt.data_ptr<int>() : nullptr; }
+};
+
+ConvWs conv_ws(const ldnn::ConvShape& s, int op, const at::Tensor& like) {
+  ConvWs w;
+  if (ldnn::get_conv_impl() != 0) return w;
+  const ldnn::ConvWorkspace need = ldnn::conv2d_lds_workspace(s, op);
+  if (need.slab_bytes == 0) return w;
+  w.slabs = at::empty({(int64_t)(need.slab_bytes / 4)}, like.options().dtype(at::kFloat));
+  w.cnt = at::zeros({(int64_t)need.counters}, like.options().dtype(at::kInt));
+  return w;
+}
+
 void conv_fwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& y, int64_t stride, int64_t pad,
               const c10::optional<at::Tensor>& bias, int64_t epi) {
   check_dev(x, at::kBFloat16, "x");
@@ -397,7 +429,9 @@ void conv_fwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& y, int
   }
   TORCH_CHECK(epi == ldnn::EPI_NONE || b != nullptr, "conv: bias epilogue needs a bias");
   c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
-  check(ldnn::conv2d_fwd(s, bf16_ptr(x), bf16_ptr(w), bf16_mut(y), b, (int)epi, cur_stream(x)), "conv2d_fwd");
+  const ConvWs ws = conv_ws(s, 0, x);
+  check(ldnn::conv2d_fwd(s, bf16_ptr(x), bf16_ptr(w), bf16_mut(y), b, (int)epi, cur_stream(x), ws.ws(), ws.c()),
+        "conv2d_fwd");
 }
 
 void conv_dgrad(const at::Tensor& dy, const at::Tensor& w, const at::Tensor& dx, int64_t stride, int64_t pad) {
@@ -406,7 +440,9 @@ void conv_dgrad(const at::Tensor& dy, const at::Tensor& w, const at::Tensor& dx,
   check_dev(dx, at::kBFloat16, "dx");
   ldnn::ConvShape s = conv_shape(dx, w, dy, stride, pad);
   c10::hip::HIPGuardMasqueradingAsCUDA g(dy.device());
-  check(ldnn::conv2d_dgrad(s, bf16_ptr(dy), bf16_ptr(w), bf16_mut(dx), cur_stream(dy)), "conv2d_dgrad");
+  const ConvWs ws = conv_ws(s, 1, dy);
+  check(ldnn::conv2d_dgrad(s, bf16_ptr(dy), bf16_ptr(w), bf16_mut(dx), cur_stream(dy), ws.ws(), ws.c()),
+        "conv2d_dgrad");
 }
 
 void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& dw, int64_t stride, int64_t pad,
@@ -574,7 +610,16 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm", &gemm, "bf16 MFMA GEMM with fused epilogue", py::arg("a"), py::arg("b"), py::arg("c"),
         py::arg("a_kcontig"), py::arg("b_kcontig"), py::arg("epi") = 0, py::arg("bias") = py::none(),
         py::arg("aux") = py::none(), py::arg("dbias") = py::none(), py::arg("beta") = 0.0,
-        py::arg("tile") = 0, py::arg("splitk") = 0, py::arg("direct_epi") = false, py::arg("variant") = 0);
+        py::arg("tile") = 0, py::arg("splitk") = 0, py::arg("direct_epi") = false, py::arg("variant") = 0,
+        py::arg("ws") = py::none(), py::arg("cnt") = py::none());
+  m.def("gemm_splitk_ws", [](int64_t M, int64_t N, int64_t splitk) {
+        return std::make_pair((int64_t)(ldnn::gemm_splitk_ws_bytes((int)M, (int)N, (int)splitk) / 4),
+                              (int64_t)ldnn::gemm_tiles128((int)M, (int)N));
+      }, "(fp32 workspace elements, int32 counters) of a 128-tile split-K combine", py::arg("M"), py::arg("N"),
+      py::arg("splitk"));
+  m.def("set_conv_impl", &ldnn::set_conv_impl, "0 = LDS-DMA fast path where it applies, 1 = generic kernel only",
+        py::arg("impl"));
+  m.def("get_conv_impl", &ldnn::get_conv_impl);
   m.def("act_fwd", &act_fwd);
   m.def("act_bwd", &act_bwd);
   m.def("colsum", &colsum, py::arg("x"), py::arg("out"), py::arg("accumulate") = false);

@@ -163,5 +163,68 @@ __device__ __forceinline__ void epilogue(const GemmParams& p, floatx4 (&acc)[NT]
   }
 }
 
+// ---- in-launch split-K combine ----------------------------------------------
+// (cdna_hip_programming.md §5 "Projection GEMM at M = 256" item 2, write-through
+// form; §6 Guideline 16.)  Every K-slice workgroup stores its fp32 accumulators
+// WRITE-THROUGH (sc1) into its own slab of the tile's workspace, in
+// thread-linear order, so the reducer thread with the same tid reads back
+// exactly the fragments it owns (16-B per lane per register, fully coalesced).
+// Every wave drains its stores, and after a workgroup barrier one lane draws a
+// ticket from the tile's counter (relaxed agent-scope atomic).  The workgroup
+// that draws the last ticket resets the counter, acquires at agent scope, sums
+// ALL slabs in slice order with sc1 loads -- deterministic, independent of the
+// arrival order -- and returns true: the caller then runs its normal epilogue
+// on the full sum.  The others return false.  `cnt` must be zero before the
+// first launch (callers allocate it zeroed); the reducer leaves it zero again.
+// `smem` is any 4 bytes of the kernel's (single) LDS array, free by now.
+constexpr int kSc1 = 16;  // buffer cache-policy bit: sc1 (write-through / L1 bypass)
+
+template <int NT, int MT, int NTHREADS>
+__device__ __forceinline__ bool splitk_combine(floatx4 (&acc)[NT][MT], float* ws, int* cnt, int tile, int splits,
+                                               int split, char* smem) {
+  constexpr uint32_t kSlab = (uint32_t)(NT * MT) * NTHREADS * 16u;
+  const int tid = threadIdx.x;
+  const uint32_t tile_bytes = kSlab * (uint32_t)splits;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      reinterpret_cast<char*>(ws) + (size_t)tile * tile_bytes, (short)0, (int)tile_bytes, 0x00020000);
+  const uint32_t own = (uint32_t)split * kSlab + (uint32_t)tid * 16u;
+#pragma unroll
+  for (int j = 0; j < NT; ++j)
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[j][i]), rs,
+                                             (int)(own + (uint32_t)((j * MT + i) * NTHREADS * 16)), 0, kSc1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // EVERY storing wave drains its slab stores
+  __syncthreads();
+  int* flag = reinterpret_cast<int*>(smem);
+  if (tid == 0) {
+    const int t = __hip_atomic_fetch_add(cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = t == splits - 1 ? 1 : 0;
+    if (last) {
+      __hip_atomic_store(cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    *flag = last;
+  }
+  __syncthreads();
+  if (*flag == 0) return false;
+#pragma unroll
+  for (int j = 0; j < NT; ++j)
+#pragma unroll
+    for (int i = 0; i < MT; ++i) acc[j][i] = floatx4{0.f, 0.f, 0.f, 0.f};
+  for (int s = 0; s < splits; ++s) {
+    const uint32_t o = (uint32_t)s * kSlab + (uint32_t)tid * 16u;
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+        acc[j][i] += __builtin_bit_cast(
+            floatx4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(o + (uint32_t)((j * MT + i) * NTHREADS * 16)),
+                                                           0, kSc1));
+  }
+  return true;
+}
+
 }  // namespace
 }  // namespace ldnn

@@ -26,10 +26,16 @@ struct GemmParams {
   int M, N, K;
   int lda, ldb, ldc, ldaux;
   float beta;            // fp32 output only: C = acc + beta * C
-  int splitk;            // >1: K split over gridDim.y, fp32 atomics into C (EPI_NONE, fp32 out, 128-tile)
+  int splitk;            // >1: K split over gridDim.y (128-tile): fp32 atomics into C (EPI_NONE, fp32 out)
+                         //     or, with ws/cnt, an in-launch deterministic combine (any epilogue)
   int direct_epi;        // 256-tile bf16 outputs: 1 = per-fragment stores (A/B knob), 0 = LDS-staged rows
   int variant;           // 256-tile main loop: 0/1 = 2-stage BK64 (default), 2 = 4-slot BK32 ring, 3 = 5-slot ring
+  float* ws;             // split-K combine: [tiles][splitk] slabs of 64 KiB (gemm_splitk_ws_bytes)
+  int* cnt;              // split-K combine: [tiles] arrival counters, zero before the first launch
 };
+// Workspace of the in-launch split-K combine of a 128-tile GEMM (bytes; counters = tiles).
+size_t gemm_splitk_ws_bytes(int M, int N, int splitk);
+int gemm_tiles128(int M, int N);
 
 // Picks the tiling (256x256 LDS-DMA kernel or 128x128 kernel) from the shape.
 hipError_t gemm_bf16(const GemmParams& p, bool a_kcontig, bool b_kcontig, int epi, bool out_f32,
@@ -52,11 +58,30 @@ struct ConvShape {
   int P, Q;         // output spatial size
   int stride, pad;
 };
+// ws / cnt: optional in-launch split-K workspace for small-M shapes (conv2d_lds_workspace);
+// without it those shapes run unsplit.
 hipError_t conv2d_fwd(const ConvShape& s, const uint16_t* x, const uint16_t* w, uint16_t* y, const float* bias,
-                      int epi, hipStream_t st);
-hipError_t conv2d_dgrad(const ConvShape& s, const uint16_t* dy, const uint16_t* w, uint16_t* dx, hipStream_t st);
+                      int epi, hipStream_t st, float* ws = nullptr, int* cnt = nullptr);
+hipError_t conv2d_dgrad(const ConvShape& s, const uint16_t* dy, const uint16_t* w, uint16_t* dx, hipStream_t st,
+                        float* ws = nullptr, int* cnt = nullptr);
 hipError_t conv2d_wgrad(const ConvShape& s, const uint16_t* dy, const uint16_t* x, float* dw, float beta,
                         hipStream_t st);
+// LDS-DMA fast path (conv_lds.hip): hipErrorNotSupported outside its shape set
+// (fwd needs C % 64 == 0, dgrad K % 64 == 0, stride 1 or 2).
+hipError_t conv2d_fwd_lds(const ConvShape& s, const uint16_t* x, const uint16_t* w, uint16_t* y, const float* bias,
+                          int epi, hipStream_t st, float* ws, int* cnt);
+hipError_t conv2d_dgrad_lds(const ConvShape& s, const uint16_t* dy, const uint16_t* w, uint16_t* dx, hipStream_t st,
+                            float* ws, int* cnt);
+hipError_t conv2d_wgrad_lds(const ConvShape& s, const uint16_t* dy, const uint16_t* x, float* dw, float beta,
+                            hipStream_t st);
+struct ConvWorkspace {
+  size_t slab_bytes = 0;  // fp32 split-K slabs (0: the shape runs unsplit)
+  int counters = 0;       // int arrival counters, zeroed
+};
+ConvWorkspace conv2d_lds_workspace(const ConvShape& s, int op);  // op 0 = fwd, 1 = dgrad
+// 0 = LDS-DMA fast path where it applies (default), 1 = generic kernel only (A/B and tests)
+void set_conv_impl(int impl);
+int get_conv_impl();
 
 // ---- BatchNorm / pooling on NHWC bf16 (bn_pool.hip), C % 8 == 0
 struct BnArgs {

@@ -21,7 +21,10 @@
 //
 // The main loop is the 128x128x64 register-staged MFMA tile of gemm.hip (same
 // LDS images, fragment reads and fused epilogue), with the global address of
-// each 16-byte chunk produced by a per-operand gather policy.
+// each 16-byte chunk produced by a per-operand gather policy.  This generic
+// kernel serves the shapes outside the LDS-DMA fast path of conv_lds.hip
+// (stems with C < 64, 5x5 LeNet convs, K % 64 != 0 dgrads); the dispatchers
+// below try the fast path first.
 #include "ldnn_common.h"
 #include "ldnn_gemm_tile.h"
 #include "ldnn_kernels.h"
@@ -240,8 +243,19 @@ inline int splitk_for(int tiles, int Kd) {
 
 }  // namespace
 
+namespace {
+int g_conv_impl = 0;  // 0: LDS-DMA fast path where it applies, 1: generic kernel only
+}  // namespace
+
+void set_conv_impl(int impl) { g_conv_impl = impl; }
+int get_conv_impl() { return g_conv_impl; }
+
 hipError_t conv2d_fwd(const ConvShape& s, const uint16_t* x, const uint16_t* w, uint16_t* y, const float* bias,
-                      int epi, hipStream_t st) {
+                      int epi, hipStream_t st, float* ws, int* cnt) {
+  if (g_conv_impl == 0) {
+    const hipError_t e = conv2d_fwd_lds(s, x, w, y, bias, epi, st, ws, cnt);
+    if (e != hipErrorNotSupported) return e;
+  }
   ConvArgs a{};
   a.s = s;
   a.x = x;
@@ -264,7 +278,12 @@ hipError_t conv2d_fwd(const ConvShape& s, const uint16_t* x, const uint16_t* w, 
   return hipGetLastError();
 }
 
-hipError_t conv2d_dgrad(const ConvShape& s, const uint16_t* dy, const uint16_t* w, uint16_t* dx, hipStream_t st) {
+hipError_t conv2d_dgrad(const ConvShape& s, const uint16_t* dy, const uint16_t* w, uint16_t* dx, hipStream_t st,
+                        float* ws, int* cnt) {
+  if (g_conv_impl == 0) {
+    const hipError_t e = conv2d_dgrad_lds(s, dy, w, dx, st, ws, cnt);
+    if (e != hipErrorNotSupported) return e;
+  }
   ConvArgs a{};
   a.s = s;
   a.dy = dy;
@@ -282,6 +301,10 @@ hipError_t conv2d_dgrad(const ConvShape& s, const uint16_t* dy, const uint16_t* 
 
 hipError_t conv2d_wgrad(const ConvShape& s, const uint16_t* dy, const uint16_t* x, float* dw, float beta,
                         hipStream_t st) {
+  if (g_conv_impl == 0) {
+    const hipError_t e = conv2d_wgrad_lds(s, dy, x, dw, beta, st);
+    if (e != hipErrorNotSupported) return e;
+  }
   ConvArgs a{};
   a.s = s;
   a.dy = dy;

@@ -1,0 +1,692 @@
+// LDS-DMA implicit-GEMM convolution for gfx950 (the fast path of conv.hip).
+//
+// Same GEMM views as conv.hip (fwd: y[NPQ][K] = x~[NPQ][RSC] . w[K][RSC]^T,
+// dgrad: dx[NHW][C] = dy~[NHW][RSK] . w~[RSK][C], wgrad: dw[K][RSC] =
+// dy[NPQ][K]^T . x~[NPQ][RSC]), but every operand tile is gathered straight
+// from HBM/L2 into LDS by buffer_load_dwordx4 ... lds (no VGPR round trip).
+// The DMA destination is lane-linear, so the whole GATHER lives in each lane's
+// source offset; an out-of-image tap (zero padding, ragged edges) is an offset
+// past the buffer's num_records, which the buffer unit returns as zeros.  No
+// im2col buffer and no integer division in the main loop:
+//
+//   * fwd / dgrad need C (resp. K) % 64 == 0, so each 64-deep K-tile is ONE
+//     filter tap (r, s) and 64 consecutive channels.  (r, s, channel block)
+//     advances incrementally in scalar registers; each lane keeps the
+//     decomposed pixel coordinates of its DMA rows, so an address is two bounds
+//     checks and an add.
+//   * stride-2 dgrad is split into the 4 output-parity classes (grid.z): pixel
+//     (h, w) with h = 2 h2 + ph only receives taps r == (ph + pad) mod 2, so
+//     each class is a dense problem over its own taps -- no zero-inserted MFMA
+//     work (the generic kernel wastes 3/4 of it).
+//   * wgrad reduces over output pixels npq; each lane carries (n, p, q) of its
+//     DMA column and advances it by 64 pixels per K-tile with host-computed
+//     carries (64 = dn*PQ + dp*Q + dq).  Small K x RSC outputs split npq over
+//     gridDim.y and combine with fp32 atomics.
+//   * small-M fwd / dgrad (the 2x2 / 4x4 tail stages) split the reduction over
+//     gridDim.y and combine IN the launch (ldnn_gemm_tile.h splitk_combine):
+//     deterministic, any epilogue, no fp32 round trip through a second kernel.
+//
+// Tiles: 64x64 per wave (4x4 v_mfma_f32_16x16x32_bf16 accumulators), wave grid
+// WM x WN -> 128x128 (2x2), 256x64 (4x1: 64-channel layers), 64x256 (1x4:
+// wgrad of 64-filter layers).  Two LDS stages, the DMA of K-tile t+1 in flight
+// across the MFMAs of tile t (one raw s_barrier per K-tile, never
+// __syncthreads while a DMA is outstanding); 2 workgroups per CU.  LDS images
+// and fragment reads are those of gemm.hip (ldnn_gemm_tile.h).
+#include <algorithm>
+
+#include "ldnn_common.h"
+#include "ldnn_gemm_tile.h"
+#include "ldnn_kernels.h"
+
+namespace ldnn {
+
+namespace convlds {
+
+constexpr uint32_t kOOB = 0x80000000u;      // >= num_records: reads as zero
+constexpr int kSlabBytes4 = 16 * 256 * 16;  // one 4-wave workgroup's fp32 accumulators
+
+struct FastDiv {  // n / d for 0 <= n < 2^31 as (umulhi(n, m) + n) >> s
+  uint32_t m, s;
+};
+
+FastDiv make_fastdiv(uint32_t d) {
+  FastDiv f;
+  uint32_t s = 0;
+  while ((1ull << s) < d) ++s;
+  f.s = s;
+  f.m = (uint32_t)(((1ull << 32) * ((1ull << s) - d)) / d + 1);
+  return f;
+}
+
+__device__ __forceinline__ int fdiv(int n, const FastDiv& f) {
+  return (int)((__umulhi((uint32_t)n, f.m) + (uint32_t)n) >> f.s);
+}
+
+struct LArgs {
+  ConvShape s;
+  void* out;
+  const float* bias;
+  float beta;        // fp32 outputs: out = acc + beta * out
+  int M, N;          // GEMM rows / columns
+  int nk_all;        // K-tiles of the reduction (largest class)
+  int nk_split;      // K-tiles per gridDim.y slice
+  int nb;            // fwd: C/64, dgrad: K/64 channel blocks per tap; 0 = wgrad
+  int Kd;            // wgrad: NPQ (reduction length)
+  int rsc, pq;
+  int classes;       // 4 = stride-2 dgrad parity classes (grid.z), else 1
+  int tiles_x;       // gridDim.x
+  int dn, dp, dq;    // wgrad: 64 = dn*PQ + dp*Q + dq
+  FastDiv f_pq, f_q, f_c, f_s;
+  float* ws;         // split-K combine slabs (nullptr: atomics / no split)
+  int* cnt;          // split-K arrival counters
+};
+
+// Per-workgroup geometry: which rows its class covers and which taps it sums.
+struct Geo {
+  int M;                   // GEMM rows of this class
+  int rows_h, rows_w;      // row = (n, h2, w2) over rows_h x rows_w
+  int hmul, hoff, woff;    // pixel h = hmul*h2 + hoff
+  int r0, s0, step, nS;    // taps r = r0 + step*i (< R), s likewise
+  int nk;                  // K-tiles of this class
+};
+
+__device__ __forceinline__ Geo make_geo(const LArgs& a, bool dgrad) {
+  Geo g;
+  const ConvShape& s = a.s;
+  g.hmul = 1; g.hoff = 0; g.woff = 0; g.r0 = 0; g.s0 = 0; g.step = 1; g.nS = s.S;
+  g.M = a.M;
+  g.nk = a.nk_all;
+  if (!dgrad) {  // fwd rows = output pixels
+    g.rows_h = s.P; g.rows_w = s.Q;
+    return g;
+  }
+  g.rows_h = s.H; g.rows_w = s.W;
+  if (a.classes == 4) {
+    const int ph = blockIdx.z >> 1, pw = blockIdx.z & 1;
+    g.hmul = 2; g.hoff = ph; g.woff = pw;
+    g.rows_h = (s.H - ph + 1) >> 1;
+    g.rows_w = (s.W - pw + 1) >> 1;
+    g.M = s.N * g.rows_h * g.rows_w;
+    g.r0 = (ph + s.pad) & 1;
+    g.s0 = (pw + s.pad) & 1;
+    g.step = 2;
+    const int nR = g.r0 < s.R ? (s.R - g.r0 + 1) >> 1 : 0;
+    g.nS = g.s0 < s.S ? (s.S - g.s0 + 1) >> 1 : 0;
+    g.nk = nR * g.nS * a.nb;
+  }
+  return g;
+}
+
+// Per-K-tile scalar state: tap (r, s) and channel block cb of K-tile kt.
+struct KS {
+  int kt, r, s, cb;
+};
+
+__device__ __forceinline__ KS ks_init(const LArgs& a, const Geo& g, int kt) {
+  KS k;
+  k.kt = kt;
+  if (a.nb > 0 && g.nS > 0) {
+    k.cb = kt % a.nb;
+    const int t = kt / a.nb;
+    k.r = g.r0 + g.step * (t / g.nS);
+    k.s = g.s0 + g.step * (t % g.nS);
+  } else {
+    k.cb = k.r = k.s = 0;
+  }
+  return k;
+}
+
+__device__ __forceinline__ void ks_next(const LArgs& a, const Geo& g, KS& k) {
+  ++k.kt;
+  if (++k.cb == a.nb) {
+    k.cb = 0;
+    k.s += g.step;
+    if (k.s >= a.s.S) {
+      k.s = g.s0;
+      k.r += g.step;
+    }
+  }
+}
+
+// ---- operand gather policies ------------------------------------------------
+// init(): per-lane state of this wave's PPW DMA pieces (1 KiB of LDS each);
+// off(i, ks): byte offset of piece i's 16-B chunk for K-tile ks (kOOB = zeros);
+// advance(): once per K-tile, after that tile's offsets were issued.
+
+template <int ROWS, int PPW, int NW>
+struct FwdA {  // x gathered: row = output pixel npq, k = (r, s, c), C % 64 == 0
+  static constexpr bool KC = true;
+  static constexpr int kRows = ROWS, kPieces = PPW;
+  int base[PPW], ih0[PPW], iw0[PPW];
+  __device__ void init(const LArgs& a, const Geo&, int r0, int wid, int lane, int) {
+    const ConvShape& s = a.s;
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      int row, k;
+      lds_slot_to_rk<true, ROWS>((i * NW + wid) * 1024 + lane * 16, row, k);
+      const int m = r0 + row;
+      const int q = m % s.Q, t = m / s.Q, p = t % s.P, n = t / s.P;
+      ih0[i] = p * s.stride - s.pad;
+      iw0[i] = q * s.stride - s.pad;
+      base[i] = (int)((unsigned)((n * s.H + ih0[i]) * s.W + iw0[i]) * (unsigned)s.C) + k;
+      if (m >= a.M) ih0[i] = -(1 << 20);  // never inside the image
+    }
+  }
+  __device__ __forceinline__ uint32_t off(const LArgs& a, int i, const KS& ks) const {
+    const int ih = ih0[i] + ks.r, iw = iw0[i] + ks.s;
+    const bool ok = (unsigned)ih < (unsigned)a.s.H && (unsigned)iw < (unsigned)a.s.W;
+    const unsigned e = (unsigned)base[i] + (unsigned)((ks.r * a.s.W + ks.s) * a.s.C + ks.cb * 64);
+    return ok ? e * 2u : kOOB;
+  }
+  __device__ __forceinline__ void advance(const LArgs&) {}
+};
+
+template <int ROWS, int PPW, int NW>
+struct WeightKC {  // w as a [K][RSC] k-contiguous matrix (fwd B operand)
+  static constexpr bool KC = true;
+  static constexpr int kRows = ROWS, kPieces = PPW;
+  int base[PPW];
+  __device__ void init(const LArgs& a, const Geo&, int r0, int wid, int lane, int) {
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      int row, k;
+      lds_slot_to_rk<true, ROWS>((i * NW + wid) * 1024 + lane * 16, row, k);
+      const int n = r0 + row;
+      base[i] = n < a.N ? n * a.rsc + k : -1;
+    }
+  }
+  __device__ __forceinline__ uint32_t off(const LArgs&, int i, const KS& ks) const {
+    return base[i] >= 0 ? (uint32_t)(base[i] + ks.kt * 64) * 2u : kOOB;
+  }
+  __device__ __forceinline__ void advance(const LArgs&) {}
+};
+
+template <int ROWS, int PPW, int NW>
+struct DgradA {  // dy gathered: row = input pixel (class-local), k = (r, s, ko), K % 64 == 0
+  static constexpr bool KC = true;
+  static constexpr int kRows = ROWS, kPieces = PPW;
+  int nP[PPW], hp[PPW], wp[PPW], kc[PPW];
+  int sh;  // 1: stride-2 parity class (p = (h + pad - r) / 2, exact by construction)
+  __device__ void init(const LArgs& a, const Geo& g, int r0, int wid, int lane, int) {
+    const ConvShape& s = a.s;
+    sh = g.hmul == 2 ? 1 : 0;
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      int row, k;
+      lds_slot_to_rk<true, ROWS>((i * NW + wid) * 1024 + lane * 16, row, k);
+      const int m = r0 + row;
+      const int w2 = m % g.rows_w, t = m / g.rows_w, h2 = t % g.rows_h, n = t / g.rows_h;
+      nP[i] = n * s.P;
+      hp[i] = m < g.M ? g.hmul * h2 + g.hoff + s.pad : -(1 << 20);
+      wp[i] = g.hmul * w2 + g.woff + s.pad;
+      kc[i] = k;
+    }
+  }
+  __device__ __forceinline__ uint32_t off(const LArgs& a, int i, const KS& ks) const {
+    const int p = (hp[i] - ks.r) >> sh, q = (wp[i] - ks.s) >> sh;
+    const bool ok = (unsigned)p < (unsigned)a.s.P && (unsigned)q < (unsigned)a.s.Q;
+    const unsigned e = ((unsigned)(nP[i] + p) * (unsigned)a.s.Q + (unsigned)q) * (unsigned)a.s.K +
+                       (unsigned)(ks.cb * 64 + kc[i]);
+    return ok ? e * 2u : kOOB;
+  }
+  __device__ __forceinline__ void advance(const LArgs&) {}
+};
+
+template <int ROWS, int PPW, int NW>
+struct DgradB {  // w[ko][r][s][c]: n = c (8 consecutive), k = (r, s, ko)
+  static constexpr bool KC = false;
+  static constexpr int kRows = ROWS, kPieces = PPW;
+  int base[PPW];
+  __device__ void init(const LArgs& a, const Geo&, int r0, int wid, int lane, int) {
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      int row, k;
+      lds_slot_to_rk<false, ROWS>((i * NW + wid) * 1024 + lane * 16, row, k);
+      const int c = r0 + row;
+      base[i] = c < a.N ? k * a.rsc + c : -1;
+    }
+  }
+  __device__ __forceinline__ uint32_t off(const LArgs& a, int i, const KS& ks) const {
+    const int u = ks.cb * 64 * a.rsc + (ks.r * a.s.S + ks.s) * a.s.C;
+    return base[i] >= 0 ? (uint32_t)(base[i] + u) * 2u : kOOB;
+  }
+  __device__ __forceinline__ void advance(const LArgs&) {}
+};
+
+template <int ROWS, int PPW, int NW>
+struct WgradA {  // dy as [NPQ][K]: row = ko (8 consecutive), k = npq
+  static constexpr bool KC = false;
+  static constexpr int kRows = ROWS, kPieces = PPW;
+  int ko[PPW], kl[PPW];
+  __device__ void init(const LArgs& a, const Geo&, int r0, int wid, int lane, int) {
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      int row, k;
+      lds_slot_to_rk<false, ROWS>((i * NW + wid) * 1024 + lane * 16, row, k);
+      ko[i] = r0 + row < a.M ? r0 + row : -1;
+      kl[i] = k;
+    }
+  }
+  __device__ __forceinline__ uint32_t off(const LArgs& a, int i, const KS& ks) const {
+    const int npq = ks.kt * 64 + kl[i];
+    return (ko[i] >= 0 && npq < a.Kd) ? (uint32_t)(npq * a.s.K + ko[i]) * 2u : kOOB;
+  }
+  __device__ __forceinline__ void advance(const LArgs&) {}
+};
+
+template <int ROWS, int PPW, int NW>
+struct WgradB {  // x gathered: row = j = (r, s, c..c+7), k = npq (carried incrementally)
+  static constexpr bool KC = false;
+  static constexpr int kRows = ROWS, kPieces = PPW;
+  int r[PPW], s[PPW], c[PPW], n[PPW], p[PPW], q[PPW];
+  __device__ void init(const LArgs& a, const Geo&, int r0, int wid, int lane, int kt0) {
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      int row, k;
+      lds_slot_to_rk<false, ROWS>((i * NW + wid) * 1024 + lane * 16, row, k);
+      const int j = r0 + row;
+      const int rs = fdiv(j, a.f_c);
+      c[i] = j - rs * a.s.C;
+      r[i] = fdiv(rs, a.f_s);
+      s[i] = rs - r[i] * a.s.S;
+      if (j >= a.N) r[i] = -(1 << 20);  // never inside the image
+      const int npq = kt0 * 64 + k;
+      n[i] = fdiv(npq, a.f_pq);
+      const int pq = npq - n[i] * a.pq;
+      p[i] = fdiv(pq, a.f_q);
+      q[i] = pq - p[i] * a.s.Q;
+    }
+  }
+  __device__ __forceinline__ uint32_t off(const LArgs& a, int i, const KS&) const {
+    const ConvShape& sh = a.s;
+    const int ih = p[i] * sh.stride - sh.pad + r[i], iw = q[i] * sh.stride - sh.pad + s[i];
+    const bool ok = n[i] < sh.N && (unsigned)ih < (unsigned)sh.H && (unsigned)iw < (unsigned)sh.W;
+    const unsigned e = (((unsigned)n[i] * (unsigned)sh.H + (unsigned)ih) * (unsigned)sh.W + (unsigned)iw) *
+                           (unsigned)sh.C + (unsigned)c[i];
+    return ok ? e * 2u : kOOB;
+  }
+  __device__ __forceinline__ void advance(const LArgs& a) {
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      q[i] += a.dq;
+      if (q[i] >= a.s.Q) {
+        q[i] -= a.s.Q;
+        ++p[i];
+      }
+      p[i] += a.dp;
+      if (p[i] >= a.s.P) {
+        p[i] -= a.s.P;
+        ++n[i];
+      }
+      n[i] += a.dn;
+    }
+  }
+};
+
+struct Rsrc {  // buffer descriptor (a struct: the builtin type cannot be a host-visible parameter)
+  __amdgpu_buffer_rsrc_t r;
+};
+
+// DMA one operand tile (K-tile ks) into LDS at dst: PPW x buffer_load_dwordx4 ... lds per lane.
+// (The voffset goes through an explicit int: with the unsigned call result passed
+// straight to the builtin, hipcc silently emits no host launch stub.)
+#define LDNN_DMA_TILE(op, PPW, rsrc, dst, ks)                                                        \
+  do {                                                                                               \
+    _Pragma("unroll") for (int i_ = 0; i_ < (PPW); ++i_) {                                           \
+      const int o_ = (int)(op).off(a, i_, (ks));                                                     \
+      __builtin_amdgcn_raw_ptr_buffer_load_lds((rsrc).r, (lds_void*)((dst) + (i_ * NW + wid) * 1024), \
+                                               16, o_, 0, 0, 0);                                     \
+    }                                                                                                \
+  } while (0)
+
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// Direct epilogue with the class row remap: GEMM row m of a stride-2 dgrad
+// class is pixel (n, 2*h2 + hoff, 2*w2 + woff) of dx.
+__device__ __forceinline__ void store_remapped(const LArgs& a, const Geo& g, floatx4 (&acc)[4][4], int mbase,
+                                               int nbase, int lane) {
+  const ConvShape& s = a.s;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = mbase + i * 16 + (lane & 15);
+    if (m >= g.M) continue;
+    const int w2 = m % g.rows_w, t = m / g.rows_w, h2 = t % g.rows_h, n = t / g.rows_h;
+    const size_t row = ((size_t)n * s.H + g.hmul * h2 + g.hoff) * s.W + g.hmul * w2 + g.woff;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = nbase + j * 16 + 4 * (lane >> 4);
+      if (c >= a.N) continue;
+      const floatx4 v = acc[j][i];
+      *reinterpret_cast<u16x4*>(reinterpret_cast<bf16_t*>(a.out) + row * a.N + c) =
+          u16x4{f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+    }
+  }
+}
+
+template <int WM, int WN, class OA, class OB, int EPI, bool OUT_F32, bool DGRAD>
+__global__ __launch_bounds__(256, 2) void conv_lds_kernel(LArgs a, const bf16_t* pa, uint32_t bytes_a,
+                                                         const bf16_t* pb, uint32_t bytes_b) {
+  constexpr int NW = WM * WN, BM = WM * 64, BN = WN * 64;
+  static_assert(NW == 4, "4-wave workgroups (the launch bounds and the split-K slab size assume it)");
+  static_assert(OA::kRows == BM && OB::kRows == BN && OA::kPieces == BM / 8 / NW && OB::kPieces == BN / 8 / NW,
+                "operand policy geometry");
+  constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128, STAGE = A_BYTES + B_BYTES;
+  constexpr int PPA = BM / 8 / NW, PPB = BN / 8 / NW;
+  static_assert(PPA >= 1 && PPB >= 1 && PPA * NW * 8 == BM && PPB * NW * 8 == BN, "DMA pieces");
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+
+  const Geo g = make_geo(a, DGRAD);
+  const int tiles_m = (g.M + BM - 1) / BM, tiles_n = (a.N + BN - 1) / BN;
+  if ((int)blockIdx.x >= tiles_m * tiles_n) return;  // a smaller parity class: whole workgroup exits
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+  int m0, n0;
+  tile_coords(g.M, a.N, BM, BN, m0, n0);
+  const int kt0 = blockIdx.y * a.nk_split;
+  const int nk = max(0, min(g.nk - kt0, a.nk_split));
+  const bool combine = a.cnt != nullptr && gridDim.y > 1;
+  if (nk == 0 && gridDim.y > 1 && !combine) return;  // an empty atomic slice adds nothing
+
+  floatx4 acc[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[j][i] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  if (nk > 0) {
+    OA oa;
+    OB ob;
+    oa.init(a, g, m0, wid, lane, kt0);
+    ob.init(a, g, n0, wid, lane, kt0);
+    Rsrc ra, rb;
+    ra.r = __builtin_amdgcn_make_buffer_rsrc((void*)pa, (short)0, (int)bytes_a, 0x00020000);
+    rb.r = __builtin_amdgcn_make_buffer_rsrc((void*)pb, (short)0, (int)bytes_b, 0x00020000);
+    KS ks = ks_init(a, g, kt0);
+    LDNN_DMA_TILE(oa, PPA, ra, smem, ks);
+    LDNN_DMA_TILE(ob, PPB, rb, smem + A_BYTES, ks);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+    for (int kt = 0; kt < nk; ++kt) {
+      char* stage = smem + (kt & 1) * STAGE;
+      lds_barrier();  // publishes tile kt; every wave is done reading the other stage
+      if (kt + 1 < nk) {
+        ks_next(a, g, ks);
+        oa.advance(a);
+        ob.advance(a);
+        char* nxt = smem + ((kt + 1) & 1) * STAGE;
+        LDNN_DMA_TILE(oa, PPA, ra, nxt, ks);
+        LDNN_DMA_TILE(ob, PPB, rb, nxt + A_BYTES, ks);
+      }
+      const char* la = stage;
+      const char* lb = stage + A_BYTES;
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        bf16x8 fa[4], fb[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fa[i] = read_frag<OA::KC, BM>(la, wm * 4 + i, kk, lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) fb[j] = read_frag<OB::KC, BN>(lb, wn * 4 + j, kk, lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[j][i], 0, 0, 0);
+      }
+      __builtin_amdgcn_s_setprio(0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // own DMA of tile kt+1 landed
+    }
+  }
+
+  const int mb = m0 + wm * 64, nbase = n0 + wn * 64;
+  if (gridDim.y > 1) {
+    if (combine) {
+      lds_barrier();  // every wave is done with the operand stages (the ticket word lives there)
+      const int tile = blockIdx.z * a.tiles_x + blockIdx.x;
+      if (!splitk_combine<4, 4, NW * 64>(acc, a.ws, a.cnt, tile, gridDim.y, blockIdx.y, smem)) return;
+    } else {
+      if constexpr (OUT_F32 && EPI == EPI_NONE) {  // fp32 atomics into the (cleared / accumulated) output
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int n = nbase + j * 16 + 4 * (lane >> 4);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int m = mb + i * 16 + (lane & 15);
+            if (n < a.N && m < g.M) {
+              float* c = reinterpret_cast<float*>(a.out) + (size_t)m * a.N + n;
+#pragma unroll
+              for (int r = 0; r < 4; ++r) atomicAdd(c + r, acc[j][i][r]);
+            }
+          }
+        }
+      }
+      return;
+    }
+  }
+  if constexpr (DGRAD && !OUT_F32) {
+    if (g.hmul == 2) {
+      store_remapped(a, g, acc, mb, nbase, lane);
+      return;
+    }
+  }
+  GemmParams p{};
+  p.C = a.out;
+  p.M = g.M;
+  p.N = a.N;
+  p.ldc = a.N;
+  p.bias = a.bias;
+  p.beta = a.beta;
+  epilogue<EPI, OUT_F32, 4, 4>(p, acc, mb, nbase, lane);
+}
+
+bool fits(size_t bytes) { return bytes < kOOBLimit; }
+
+LArgs base_args(const ConvShape& s) {
+  LArgs a{};
+  a.s = s;
+  a.rsc = s.R * s.S * s.C;
+  a.pq = s.P * s.Q;
+  a.classes = 1;
+  return a;
+}
+
+bool shape_ok(const ConvShape& s) {
+  return s.N > 0 && s.stride >= 1 && s.stride <= 2 && fits((size_t)s.N * s.H * s.W * s.C * 2) &&
+         fits((size_t)s.K * s.R * s.S * s.C * 2) && fits((size_t)s.N * s.P * s.Q * s.K * 2);
+}
+
+// OA / OB = Policy<rows, DMA pieces per wave (= rows / 8 / 4 waves), 4 waves>.
+template <int WM, int WN, class OA, class OB, bool OUT_F32, bool DGRAD>
+hipError_t launch(LArgs a, int epi, int splits, const bf16_t* pa, size_t ba, const bf16_t* pb, size_t bb,
+                  hipStream_t st) {
+  constexpr int NW = WM * WN;
+  dim3 grid(a.tiles_x, splits, a.classes), block(NW * 64);
+#define LDNN_CONV_LDS(E) \
+  conv_lds_kernel<WM, WN, OA, OB, E, OUT_F32, DGRAD><<<grid, block, 0, st>>>(a, pa, (uint32_t)ba, pb, (uint32_t)bb)
+  switch (epi) {
+    case EPI_NONE:
+      LDNN_CONV_LDS(EPI_NONE);
+      break;
+    case EPI_BIAS:
+      if constexpr (OUT_F32) return hipErrorInvalidValue;
+      else LDNN_CONV_LDS(EPI_BIAS);
+      break;
+    case EPI_BIAS_RELU:
+      if constexpr (OUT_F32) return hipErrorInvalidValue;
+      else LDNN_CONV_LDS(EPI_BIAS_RELU);
+      break;
+    default:
+      return hipErrorInvalidValue;
+  }
+#undef LDNN_CONV_LDS
+  return hipGetLastError();
+}
+
+// In-launch split-K for small-M fwd / dgrad: enough slices for ~1.5
+// workgroups per CU, >= 8 K-tiles each, at most 8.
+int small_m_splits(int tiles, int nk) {
+  if (tiles >= 160 || nk < 16) return 1;
+  int sp = (384 + tiles - 1) / tiles;
+  sp = std::min(sp, nk / 8);
+  sp = std::min(sp, 8);
+  return sp < 2 ? 1 : sp;
+}
+
+struct Plan {
+  int wm, wn;  // wave grid (tile = 64*wm x 64*wn)
+  int tiles_x, classes, splits, nk_all, nk_split;
+};
+
+void finish_plan(Plan& p) {
+  p.splits = small_m_splits(p.tiles_x * p.classes, p.nk_all);
+  p.nk_split = (p.nk_all + p.splits - 1) / p.splits;
+  p.splits = (p.nk_all + p.nk_split - 1) / p.nk_split;
+}
+
+Plan plan_fwd(const ConvShape& s) {
+  Plan p{};
+  p.classes = 1;
+  if (s.K <= 64) { p.wm = 4; p.wn = 1; } else { p.wm = 2; p.wn = 2; }
+  const int M = s.N * s.P * s.Q;
+  p.tiles_x = ((M + p.wm * 64 - 1) / (p.wm * 64)) * ((s.K + p.wn * 64 - 1) / (p.wn * 64));
+  p.nk_all = s.R * s.S * s.C / 64;
+  finish_plan(p);
+  return p;
+}
+
+Plan plan_dgrad(const ConvShape& s) {
+  Plan p{};
+  if (s.C <= 64) { p.wm = 4; p.wn = 1; } else { p.wm = 2; p.wn = 2; }
+  const int tn = (s.C + p.wn * 64 - 1) / (p.wn * 64);
+  const int nb = s.K / 64;
+  if (s.stride == 2) {
+    p.classes = 4;  // class (0, 0) has the most rows, a class with r0 = s0 = 0 the most taps
+    const int h0 = (s.H + 1) >> 1, w0 = (s.W + 1) >> 1;
+    p.tiles_x = ((s.N * h0 * w0 + p.wm * 64 - 1) / (p.wm * 64)) * tn;
+    p.nk_all = ((s.R + 1) >> 1) * ((s.S + 1) >> 1) * nb;
+  } else {
+    p.classes = 1;
+    p.tiles_x = ((s.N * s.H * s.W + p.wm * 64 - 1) / (p.wm * 64)) * tn;
+    p.nk_all = s.R * s.S * nb;
+  }
+  finish_plan(p);
+  return p;
+}
+
+ConvWorkspace ws_of(const Plan& p) {
+  ConvWorkspace w{};
+  if (p.splits > 1) {
+    w.slab_bytes = (size_t)p.tiles_x * p.classes * p.splits * kSlabBytes4;
+    w.counters = p.tiles_x * p.classes;
+  }
+  return w;
+}
+
+}  // namespace convlds
+
+using namespace convlds;
+
+ConvWorkspace conv2d_lds_workspace(const ConvShape& s, int op) {
+  if (!shape_ok(s)) return ConvWorkspace{};
+  if (op == 0 && s.C % 64 == 0) return ws_of(plan_fwd(s));
+  if (op == 1 && s.K % 64 == 0) return ws_of(plan_dgrad(s));
+  return ConvWorkspace{};
+}
+
+// Each returns hipErrorNotSupported when the shape is outside the fast path
+// (conv.hip then runs its generic register-staged kernel).
+hipError_t conv2d_fwd_lds(const ConvShape& s, const uint16_t* x, const uint16_t* w, uint16_t* y, const float* bias,
+                          int epi, hipStream_t st, float* ws, int* cnt) {
+  if (s.C % 64 != 0 || !shape_ok(s)) return hipErrorNotSupported;
+  if (s.N * s.P * s.Q <= 0) return hipSuccess;
+  Plan pl = plan_fwd(s);
+  LArgs a = base_args(s);
+  a.out = y;
+  a.bias = bias;
+  a.M = s.N * s.P * s.Q;
+  a.N = s.K;
+  a.nb = s.C / 64;
+  a.tiles_x = pl.tiles_x;
+  a.nk_all = pl.nk_all;
+  if (pl.splits > 1 && ws != nullptr && cnt != nullptr) {
+    a.ws = ws;
+    a.cnt = cnt;
+    a.nk_split = pl.nk_split;
+  } else {
+    pl.splits = 1;
+    a.nk_split = pl.nk_all;
+  }
+  const size_t bx = (size_t)s.N * s.H * s.W * s.C * 2, bw = (size_t)s.K * a.rsc * 2;
+  if (pl.wm == 4) return launch<4, 1, FwdA<256, 8, 4>, WeightKC<64, 2, 4>, false, false>(a, epi, pl.splits, x, bx, w, bw, st);
+  return launch<2, 2, FwdA<128, 4, 4>, WeightKC<128, 4, 4>, false, false>(a, epi, pl.splits, x, bx, w, bw, st);
+}
+
+hipError_t conv2d_dgrad_lds(const ConvShape& s, const uint16_t* dy, const uint16_t* w, uint16_t* dx, hipStream_t st,
+                            float* ws, int* cnt) {
+  if (s.K % 64 != 0 || !shape_ok(s)) return hipErrorNotSupported;
+  if (s.N * s.H * s.W <= 0) return hipSuccess;
+  Plan pl = plan_dgrad(s);
+  LArgs a = base_args(s);
+  a.out = dx;
+  a.M = s.N * s.H * s.W;
+  a.N = s.C;
+  a.nb = s.K / 64;
+  a.classes = pl.classes;
+  a.tiles_x = pl.tiles_x;
+  a.nk_all = pl.nk_all;
+  if (pl.splits > 1 && ws != nullptr && cnt != nullptr) {
+    a.ws = ws;
+    a.cnt = cnt;
+    a.nk_split = pl.nk_split;
+  } else {
+    pl.splits = 1;
+    a.nk_split = pl.nk_all;
+  }
+  const size_t bdy = (size_t)s.N * s.P * s.Q * s.K * 2, bw = (size_t)s.K * a.rsc * 2;
+  if (pl.wm == 4) return launch<4, 1, DgradA<256, 8, 4>, DgradB<64, 2, 4>, false, true>(a, EPI_NONE, pl.splits, dy, bdy, w, bw, st);
+  return launch<2, 2, DgradA<128, 4, 4>, DgradB<128, 4, 4>, false, true>(a, EPI_NONE, pl.splits, dy, bdy, w, bw, st);
+}
+
+hipError_t conv2d_wgrad_lds(const ConvShape& s, const uint16_t* dy, const uint16_t* x, float* dw, float beta,
+                            hipStream_t st) {
+  if (!shape_ok(s) || s.C % 8 != 0 || s.K % 8 != 0) return hipErrorNotSupported;
+  if (beta != 0.f && beta != 1.f) return hipErrorNotSupported;
+  LArgs a = base_args(s);
+  a.out = dw;
+  a.beta = beta;
+  a.M = s.K;
+  a.N = a.rsc;
+  a.Kd = s.N * s.P * s.Q;
+  a.nk_all = (a.Kd + 63) / 64;
+  a.nb = 0;
+  const int pq = s.P * s.Q;
+  a.dn = 64 / pq;
+  a.dp = (64 % pq) / s.Q;
+  a.dq = (64 % pq) % s.Q;
+  a.f_pq = make_fastdiv(pq);
+  a.f_q = make_fastdiv(s.Q);
+  a.f_c = make_fastdiv(s.C);
+  a.f_s = make_fastdiv(s.S);
+  const bool narrow = s.K <= 64;
+  const int BM = narrow ? 64 : 128, BN = narrow ? 256 : 128;
+  a.tiles_x = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
+  // split the npq reduction so the grid covers ~2 workgroups per CU, >= 8 K-tiles each
+  int splits = 1;
+  if (a.tiles_x < 256) splits = std::max(1, std::min((512 + a.tiles_x - 1) / a.tiles_x, a.nk_all / 8));
+  a.nk_split = (a.nk_all + splits - 1) / splits;
+  splits = (a.nk_all + a.nk_split - 1) / a.nk_split;
+  if (splits > 1 && beta == 0.f) {  // the atomics accumulate into a cleared output
+    hipError_t e = zero2d_f32(dw, a.M, a.N, a.N, st);
+    if (e != hipSuccess) return e;
+  }
+  const size_t bdy = (size_t)s.N * s.P * s.Q * s.K * 2, bx = (size_t)s.N * s.H * s.W * s.C * 2;
+  if (narrow) return launch<1, 4, WgradA<64, 2, 4>, WgradB<256, 8, 4>, true, false>(a, EPI_NONE, splits, dy, bdy, x, bx, st);
+  return launch<2, 2, WgradA<128, 4, 4>, WgradB<128, 4, 4>, true, false>(a, EPI_NONE, splits, dy, bdy, x, bx, st);
+}
+
+}  // namespace ldnn

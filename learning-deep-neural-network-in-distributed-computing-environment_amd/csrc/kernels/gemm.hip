@@ -167,18 +167,24 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(GemmParams p) {
     }
     __syncthreads();
   }
-  if constexpr (OUT_F32 && EPI == EPI_NONE) {
-    if (gridDim.y > 1) {  // split-K partial: fp32 atomics (C pre-zeroed or accumulated into)
+  if (gridDim.y > 1) {
+    if (p.cnt != nullptr) {
+      // in-launch deterministic combine: the last slice to arrive sums every slab
+      // and runs the full epilogue (bias / activation / dbias / beta / bf16 out)
+      if (!splitk_combine<4, 4, kThreads>(acc, p.ws, p.cnt, blockIdx.x, gridDim.y, blockIdx.y, smem)) return;
+    } else {
+      if constexpr (OUT_F32 && EPI == EPI_NONE) {  // fp32 atomics (C pre-zeroed or accumulated into)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int n = n0 + wn * 64 + j * 16 + 4 * (lane >> 4);
+        for (int j = 0; j < 4; ++j) {
+          const int n = n0 + wn * 64 + j * 16 + 4 * (lane >> 4);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int m = m0 + wm * 64 + i * 16 + (lane & 15);
-          if (n < p.N && m < p.M) {
-            float* c = reinterpret_cast<float*>(p.C) + (size_t)m * p.ldc + n;
+          for (int i = 0; i < 4; ++i) {
+            const int m = m0 + wm * 64 + i * 16 + (lane & 15);
+            if (n < p.N && m < p.M) {
+              float* c = reinterpret_cast<float*>(p.C) + (size_t)m * p.ldc + n;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) atomicAdd(c + r, acc[j][i][r]);
+              for (int r = 0; r < 4; ++r) atomicAdd(c + r, acc[j][i][r]);
+            }
           }
         }
       }
@@ -678,6 +684,12 @@ int gemm_pick_splitk(int M, int N, int K) {
   return sk < 2 ? 1 : (sk > 32 ? 32 : sk);
 }
 
+int gemm_tiles128(int M, int N) { return ((M + 127) / 128) * ((N + 127) / 128); }
+
+size_t gemm_splitk_ws_bytes(int M, int N, int splitk) {
+  return (size_t)gemm_tiles128(M, N) * (size_t)splitk * (size_t)(16 * k128::kThreads * 16);
+}
+
 hipError_t gemm_bf16(const GemmParams& p, bool a_kcontig, bool b_kcontig, int epi, bool out_f32,
                      hipStream_t s) {
   return gemm_bf16_tile(p, a_kcontig, b_kcontig, epi, out_f32, gemm_pick_tile(p.M, p.N, p.K, out_f32), s);
@@ -694,7 +706,7 @@ hipError_t gemm_bf16_tile(const GemmParams& p, bool a_kcontig, bool b_kcontig, i
   }
   if (tile == 256) return dispatch_layout<256>(p, a_kcontig, b_kcontig, epi, out_f32, s);
   GemmParams q = p;
-  if (q.splitk > 1) {
+  if (q.splitk > 1 && q.cnt == nullptr) {
     if (!(out_f32 && epi == EPI_NONE && q.dbias == nullptr)) return hipErrorInvalidValue;
     if (q.beta == 0.f) {
       hipError_t e = zero2d_f32(reinterpret_cast<float*>(q.C), q.M, q.N, q.ldc, s);

@@ -79,7 +79,7 @@ class StaticMLPEngine:
     def __init__(self, model, batch_size: int, optim: OptimConfig | None = None, *, device=None,
                  process_group=None, world_size: int | None = None, bucket_cap_elems: int = 8 << 20,
                  use_graphs: bool = True, average_grads: bool = True, use_head_kernels: bool = True,
-                 shard_optimizer: bool | None = None, overlap_optimizer: bool = False):
+                 shard_optimizer: bool | None = None, overlap_optimizer: bool = False, wgrad_combine: bool = True):
         from ..models.mlp import MLP
 
         if not isinstance(model, MLP):
@@ -175,17 +175,32 @@ class StaticMLPEngine:
         # atomics of the xent / dgrad epilogues) must start each step at zero.  The
         # optimizer launch clears them right after consuming them, so the step has
         # no zeroing launch (FlatParams allocates the grads zeroed for step 1).
-        self._wgrad_splitk = []
+        #
+        # A wgrad whose 128-tile grid leaves CUs idle (e.g. the 4096 x 784 first
+        # layer: 224 tiles, one 64-step K loop each) splits its batch reduction and
+        # combines the slices IN the launch (gemm.hip k128 + splitk_combine): every
+        # CU gets two workgroups, the result is deterministic and overwrites the
+        # gradient (no clearing needed).  Tiny grids keep fp32-atomic split-K.
+        self._wgrad_splitk, self._wgrad_ws = [], []
         for l, layer in enumerate(self.layers):
             M, N = self.dW[l].shape
+            self._wgrad_ws.append(None)
             if self.use_head and l == L - 1:
                 self._wgrad_splitk.append(self.C.head_wgrad_splits(B, N))
                 continue
             tile, sk = self.C.gemm_plan(M, N, B, True)
+            tiles = ((M + 127) // 128) * ((N + 127) // 128)
+            if tile == 128 and wgrad_combine and 64 <= tiles < 256 and B // 64 >= 32:
+                sk = max(2, min(4, (2 * 256) // tiles))   # <= 2 workgroups per CU
+                ne, nc = self.C.gemm_splitk_ws(M, N, sk)
+                self._wgrad_ws[l] = (torch.empty(ne, dtype=torch.float32, device=self.device),
+                                     torch.zeros(nc, dtype=torch.int32, device=self.device))
+                self._wgrad_splitk.append(sk)
+                continue
             self._wgrad_splitk.append(sk if tile == 128 else 1)
         ranges = [(self._bias_begin, f.numel)]
         for l in range(L):
-            if self._wgrad_splitk[l] > 1:
+            if self._wgrad_splitk[l] > 1 and self._wgrad_ws[l] is None:  # atomic accumulation
                 seg = f.seg(self.layers[l].weight)
                 ranges.append((seg.offset, seg.offset + seg.storage_numel))
         merged = []
@@ -233,7 +248,10 @@ class StaticMLPEngine:
         if self.use_head and l == len(self.layers) - 1:   # also emits the head's bias gradient
             self.C.head_wgrad(self.dz[l + 1], self.h[l], self.dW[l], self.db[l], sk)
             return
-        if sk > 1:   # accumulates into the grad the previous optimizer launch cleared
+        if self._wgrad_ws[l] is not None:   # in-launch split-K combine, overwrites the gradient
+            ws, cnt = self._wgrad_ws[l]
+            self.C.gemm(self.dz[l + 1], self.h[l], self.dW[l], False, False, tile=128, splitk=sk, ws=ws, cnt=cnt)
+        elif sk > 1:   # accumulates into the grad the previous optimizer launch cleared
             self.C.gemm(self.dz[l + 1], self.h[l], self.dW[l], False, False, beta=1.0, tile=128, splitk=sk)
         else:
             self.C.gemm(self.dz[l + 1], self.h[l], self.dW[l], False, False)

@@ -37,7 +37,11 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-stock", action="store_true")
+    ap.add_argument("--conv-impl", type=int, default=0, help="0 = LDS-DMA fast path, 1 = generic conv kernel only")
     a = ap.parse_args()
+    from ldnn.ops import _ext as _e
+
+    _e.C().set_conv_impl(a.conv_impl)
     shape = SHAPES[dataset_for(a.model)]
     nc = 1000 if a.model == "resnet18" else 10
     x = torch.randn(a.batch, *shape, device="cuda")
@@ -57,7 +61,7 @@ def main():
         opt.step()
 
     t = run(step_ldnn, a.steps, a.warmup)
-    rec = {"model": a.model, "batch": a.batch, "ldnn_ms": round(t * 1e3, 3), "ldnn_samples_per_s": round(a.batch / t, 1)}
+    rec = {"model": a.model, "batch": a.batch, "conv_impl": a.conv_impl, "ldnn_ms": round(t * 1e3, 3), "ldnn_samples_per_s": round(a.batch / t, 1)}
     if not a.no_stock:
         import torch.nn as nn
 

@@ -17,6 +17,15 @@ SHAPES = [
     (8, 1, 28, 28, 6, 5, 1, 2),       # LeNet conv1 (C 1 -> 8, K 6 -> 8)
     (8, 6, 14, 14, 16, 5, 1, 0),      # LeNet conv2
     (2, 3, 64, 64, 64, 7, 2, 3),      # ResNet stem
+    # LDS-DMA fast path (C / K multiples of 64): 64-channel tiles, ragged rows,
+    # stride-2 parity-class dgrad, split-K combine of the small-M tail stages
+    (2, 64, 56, 56, 64, 3, 1, 1),     # ResNet layer1 (256x64 tiles)
+    (3, 64, 7, 9, 64, 3, 1, 1),       # ragged M, non-square
+    (2, 128, 15, 15, 256, 3, 2, 1),   # odd H/W stride-2 (uneven parity classes)
+    (2, 256, 14, 14, 512, 1, 2, 0),   # 1x1 stride-2 shortcut (empty odd classes)
+    (4, 512, 4, 4, 1024, 3, 2, 1),    # EnhancedCNN layer4 first conv (split-K combine)
+    (4, 1024, 2, 2, 1024, 3, 1, 1),   # EnhancedCNN tail (split-K combine, huge K)
+    (2, 64, 9, 9, 128, 5, 1, 2),      # 5x5 taps on the fast path
 ]
 
 
@@ -68,3 +77,38 @@ def test_conv_fwd_dgrad_wgrad(N, C, H, W, K, R, st, pad):
     Cc.conv_wgrad(gyn, xn, dw, st, pad)
     gotw = dw[:K, :, :, :C].permute(0, 3, 1, 2)
     torch.testing.assert_close(gotw, wg.grad, rtol=2e-2, atol=1e-2 * wg.grad.abs().max().item())
+
+
+@pytest.mark.parametrize("N,C,H,W,K,R,st,pad", [(2, 64, 17, 17, 128, 3, 2, 1), (4, 512, 4, 4, 1024, 3, 2, 1),
+                                                (2, 128, 16, 16, 64, 3, 1, 1), (4, 1024, 2, 2, 1024, 3, 1, 1)])
+def test_lds_fast_path_matches_generic_kernel(N, C, H, W, K, R, st, pad):
+    """The LDS-DMA kernels (set_conv_impl(0)) agree with the generic register-staged
+    kernels (set_conv_impl(1)) on every output, and repeated launches of the
+    split-K combine give bit-identical results (counters reset, order-independent)."""
+    torch.manual_seed(1)
+    Cc = _ext.C()
+    P = (H + 2 * pad - R) // st + 1
+    x = torch.randn(N, H, W, C, device="cuda").bfloat16()
+    w = (torch.randn(K, R, R, C, device="cuda") * (1.0 / (C * R * R) ** 0.5)).bfloat16()
+    gy = torch.randn(N, P, P, K, device="cuda").bfloat16()
+    bias = torch.randn(K, device="cuda")
+    outs = {}
+    try:
+        for impl in (1, 0, 0):
+            Cc.set_conv_impl(impl)
+            y = torch.empty(N, P, P, K, device="cuda", dtype=torch.bfloat16)
+            Cc.conv_fwd(x, w, y, st, pad, bias, Cc.EPI_BIAS_RELU)
+            dx = torch.empty(N, H, W, C, device="cuda", dtype=torch.bfloat16)
+            Cc.conv_dgrad(gy, w, dx, st, pad)
+            dw = torch.randn(K, R, R, C, device="cuda")
+            base = dw.clone()
+            Cc.conv_wgrad(gy, x, dw, st, pad, 1.0)  # beta = 1 accumulates
+            outs.setdefault(impl, []).append((y.float(), dx.float(), dw - base))
+    finally:
+        Cc.set_conv_impl(0)
+    (yg, dxg, dwg), = outs[1]
+    (y0, dx0, dw0), (y1, dx1, dw1) = outs[0]
+    torch.testing.assert_close(y0, yg, rtol=2e-2, atol=2e-2 * yg.abs().max().item())
+    torch.testing.assert_close(dx0, dxg, rtol=2e-2, atol=2e-2 * dxg.abs().max().item())
+    torch.testing.assert_close(dw0, dwg, rtol=1e-3, atol=1e-3 * dwg.abs().max().item())
+    assert torch.equal(y0, y1) and torch.equal(dx0, dx1)

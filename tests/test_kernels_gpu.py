@@ -279,3 +279,54 @@ def test_head_wgrad(splits, B, K, ld, rows):
     ref = dz.float()[:, :rows].t() @ h.float()
     assert ((dW - ref).abs().max() / ref.abs().max()).item() < 1e-4
     assert (db - dz.float()[:, :rows].sum(0)).abs().max().item() < 1e-2
+
+
+@pytest.mark.parametrize("splitk", [2, 3, 5])
+@pytest.mark.parametrize("case", ["wgrad_f32", "fwd_relu_bf16", "dgrad_dbias_bf16", "wgrad_beta"])
+def test_gemm_splitk_inlaunch_combine(splitk, case):
+    """128-tile split-K with the in-launch slab combine: any epilogue, deterministic
+    (two launches bit-identical: the arrival counters reset themselves)."""
+    torch.manual_seed(11)
+    M, N, K = 520, 392, 4096
+    ws_elems, ncnt = C().gemm_splitk_ws(M, N, splitk)
+    ws = torch.empty(ws_elems, device="cuda")
+    cnt = torch.zeros(ncnt, device="cuda", dtype=torch.int32)
+    if case in ("wgrad_f32", "wgrad_beta"):
+        a = torch.randn(K, M, device="cuda").bfloat16()
+        b = torch.randn(K, N, device="cuda").bfloat16()
+        ref = a.float().t() @ b.float()
+        outs = []
+        for _ in range(2):
+            c = torch.ones(M, N, device="cuda") if case == "wgrad_beta" else torch.empty(M, N, device="cuda")
+            C().gemm(a, b, c, False, False, beta=1.0 if case == "wgrad_beta" else 0.0, tile=128, splitk=splitk,
+                     ws=ws, cnt=cnt)
+            outs.append(c)
+        exp = ref + 1.0 if case == "wgrad_beta" else ref
+        torch.testing.assert_close(outs[0], exp, rtol=1e-4, atol=1e-3 * K ** 0.5)
+    elif case == "fwd_relu_bf16":
+        a = torch.randn(M, K, device="cuda").bfloat16()
+        b = (torch.randn(N, K, device="cuda") * 0.02).bfloat16()
+        bias = torch.randn(N, device="cuda")
+        ref = (a.float() @ b.float().t() + bias).relu()
+        outs = []
+        for _ in range(2):
+            c = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+            C().gemm(a, b, c, True, True, C().EPI_BIAS_RELU, bias=bias, tile=128, splitk=splitk, ws=ws, cnt=cnt)
+            outs.append(c)
+        torch.testing.assert_close(outs[0].float(), ref, rtol=2e-2, atol=2e-2)
+    else:
+        dy = torch.randn(M, K, device="cuda").bfloat16()
+        w = (torch.randn(K, N, device="cuda") * 0.02).bfloat16()
+        yprev = torch.randn(M, N, device="cuda").relu().bfloat16()
+        outs = []
+        for _ in range(2):
+            dx = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+            db = torch.zeros(N, device="cuda")
+            C().gemm(dy, w, dx, True, False, C().EPI_DRELU, aux=yprev, dbias=db, tile=128, splitk=splitk, ws=ws,
+                     cnt=cnt)
+            outs.append(dx)
+        ref = (dy.float() @ w.float()) * (yprev.float() > 0)
+        torch.testing.assert_close(outs[0].float(), ref, rtol=2e-2, atol=5e-2)
+        torch.testing.assert_close(db, outs[1].float().sum(0), rtol=1e-3, atol=1e-2)
+    assert torch.equal(outs[0], outs[1])
+    assert int(cnt.abs().sum().item()) == 0
