@@ -78,6 +78,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--timeout", type=float, default=600.0, help="collective timeout (s): failure detection")
     p.add_argument("--no_eval", action="store_true")
     p.add_argument("--quiet", action="store_true")
+    p.add_argument("--graphs", action="store_true",
+                   help="replay each training step from one hipGraph (single-process / per-epoch aggregation)")
     p.add_argument("--trace", action="store_true",
                    help="roctx ranges per phase + HIP-event phase timers (summary in metrics.jsonl)")
     return p
@@ -170,7 +172,8 @@ def main(argv=None):
         dp=dp, partition_rule=args.partition_rule, repartition=not args.no_repartition, replace=args.replace,
         seed=args.seed, legacy_gossip=args.legacy_gossip, average_buffers=args.average_buffers,
         check_every=args.check_every, progress=not args.quiet, logger=logger, checkpointer=ckpt,
-        start_global_epoch=start, histories=hist, dtype=dtype, verbose=not args.quiet, timer=timer)
+        start_global_epoch=start, histories=hist, dtype=dtype, verbose=not args.quiet, timer=timer,
+        graphs=args.graphs)
     if timer is not None:
         phases = timer.summary()
         logger.log(kind="phase_times", phases=phases)

@@ -411,7 +411,7 @@ ConvWs conv_ws(const ldnn::ConvShape& s, int op, const at::Tensor& like) {
   const ldnn::ConvWorkspace need = ldnn::conv2d_lds_workspace(s, op);
   if (need.slab_bytes == 0) return w;
   w.slabs = at::empty({(int64_t)(need.slab_bytes / 4)}, like.options().dtype(at::kFloat));
-  w.cnt = at::zeros({(int64_t)need.counters}, like.options().dtype(at::kInt));
+  if (need.counters > 0) w.cnt = at::zeros({(int64_t)need.counters}, like.options().dtype(at::kInt));
   return w;
 }
 
@@ -460,7 +460,8 @@ void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& dw,
   TORCH_CHECK(dw.size(3) == s.C && dy.size(3) == s.K && dy.size(0) == s.N, "conv_wgrad: shape mismatch");
   TORCH_CHECK(s.C % 8 == 0 && s.K % 8 == 0, "conv_wgrad: channels must be multiples of 8");
   c10::hip::HIPGuardMasqueradingAsCUDA g(dy.device());
-  check(ldnn::conv2d_wgrad(s, bf16_ptr(dy), bf16_ptr(x), dw.data_ptr<float>(), (float)beta, cur_stream(dy)),
+  const ConvWs ws = conv_ws(s, 2, dy);
+  check(ldnn::conv2d_wgrad(s, bf16_ptr(dy), bf16_ptr(x), dw.data_ptr<float>(), (float)beta, cur_stream(dy), ws.ws()),
         "conv2d_wgrad");
 }
 
@@ -496,10 +497,7 @@ void bn_fwd(const at::Tensor& x, const at::Tensor& y, const c10::optional<at::Te
   a.running_var = fptr_opt(running_var, C, "running_var");
   a.save_mean = fptr_opt(save_mean, C, "save_mean");
   a.save_invstd = fptr_opt(save_invstd, C, "save_invstd");
-  float* w = fptr_opt(ws, 4 * C, "ws");
-  a.scale = w;
-  a.shift = w + C;
-  a.ws = w + 2 * C;
+  a.ws = fptr_opt(ws, ldnn::bn_workspace_floats((int)C), "ws");
   a.M = (int)M;
   a.C = (int)C;
   a.eps = (float)eps;
@@ -527,8 +525,7 @@ void bn_bwd(const at::Tensor& x, const at::Tensor& y, const at::Tensor& dy, cons
   a.gamma = fptr_opt(gamma, C, "gamma");
   a.save_mean = fptr_opt(save_mean, C, "save_mean");
   a.save_invstd = fptr_opt(save_invstd, C, "save_invstd");
-  float* w = fptr_opt(ws, 4 * C, "ws");
-  a.ws = w + 2 * C;
+  a.ws = fptr_opt(ws, ldnn::bn_workspace_floats((int)C), "ws");
   a.M = (int)M;
   a.C = (int)C;
   a.relu = relu ? 1 : 0;
@@ -659,6 +656,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_fwd", &bn_fwd, py::arg("x"), py::arg("y"), py::arg("residual"), py::arg("gamma"), py::arg("beta"),
         py::arg("running_mean"), py::arg("running_var"), py::arg("save_mean"), py::arg("save_invstd"),
         py::arg("ws"), py::arg("eps"), py::arg("momentum"), py::arg("training"), py::arg("relu"));
+  m.def("bn_workspace_floats", &ldnn::bn_workspace_floats, "fp32 workspace of one BatchNorm (zero it once, keep it)",
+        py::arg("C"));
   m.def("bn_bwd", &bn_bwd, py::arg("x"), py::arg("y"), py::arg("dy"), py::arg("dx"), py::arg("dres"),
         py::arg("gamma"), py::arg("save_mean"), py::arg("save_invstd"), py::arg("ws"), py::arg("dgamma"),
         py::arg("dbeta"), py::arg("relu"));

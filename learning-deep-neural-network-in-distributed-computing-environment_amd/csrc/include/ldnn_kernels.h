@@ -65,7 +65,7 @@ hipError_t conv2d_fwd(const ConvShape& s, const uint16_t* x, const uint16_t* w, 
 hipError_t conv2d_dgrad(const ConvShape& s, const uint16_t* dy, const uint16_t* w, uint16_t* dx, hipStream_t st,
                         float* ws = nullptr, int* cnt = nullptr);
 hipError_t conv2d_wgrad(const ConvShape& s, const uint16_t* dy, const uint16_t* x, float* dw, float beta,
-                        hipStream_t st);
+                        hipStream_t st, float* ws = nullptr);
 // LDS-DMA fast path (conv_lds.hip): hipErrorNotSupported outside its shape set
 // (fwd needs C % 64 == 0, dgrad K % 64 == 0, stride 1 or 2).
 hipError_t conv2d_fwd_lds(const ConvShape& s, const uint16_t* x, const uint16_t* w, uint16_t* y, const float* bias,
@@ -73,12 +73,13 @@ hipError_t conv2d_fwd_lds(const ConvShape& s, const uint16_t* x, const uint16_t*
 hipError_t conv2d_dgrad_lds(const ConvShape& s, const uint16_t* dy, const uint16_t* w, uint16_t* dx, hipStream_t st,
                             float* ws, int* cnt);
 hipError_t conv2d_wgrad_lds(const ConvShape& s, const uint16_t* dy, const uint16_t* x, float* dw, float beta,
-                            hipStream_t st);
+                            hipStream_t st, float* ws);
 struct ConvWorkspace {
   size_t slab_bytes = 0;  // fp32 split-K slabs (0: the shape runs unsplit)
   int counters = 0;       // int arrival counters, zeroed
 };
-ConvWorkspace conv2d_lds_workspace(const ConvShape& s, int op);  // op 0 = fwd, 1 = dgrad
+// op 0 = fwd, 1 = dgrad (in-launch combine: slabs + counters), 2 = wgrad (partial slabs, no counters)
+ConvWorkspace conv2d_lds_workspace(const ConvShape& s, int op);
 // 0 = LDS-DMA fast path where it applies (default), 1 = generic kernel only (A/B and tests)
 void set_conv_impl(int impl);
 int get_conv_impl();
@@ -94,13 +95,15 @@ struct BnArgs {
   float* running_var;
   float* save_mean;           // [C] batch statistics kept for backward
   float* save_invstd;
-  float* scale;               // [C] workspace: gamma * invstd
-  float* shift;               // [C] workspace: beta - mean * gamma * invstd
-  float* ws;                  // [2C] fp32 reduction workspace
+  float* scale;               // unused (kept for layout compatibility): scale / shift live in ws
+  float* shift;
+  float* ws;                  // [bn_workspace_floats(C)] fp32, zeroed ONCE by the owner and kept
+                              // (accumulators are cleared by the kernels that consume them)
   int M, C;
   float eps, momentum;
   int training, relu;
 };
+int bn_workspace_floats(int C);
 hipError_t bn_forward(const BnArgs& a, hipStream_t s);
 // dx (and optionally dres = upstream gradient after the ReLU mask, for the residual
 // branch); dgamma / dbeta are ACCUMULATED (flat gradient buffer)

@@ -4,10 +4,13 @@
 // BASELINE LeNet / ResNet-18 pools).
 //
 // With channels innermost, every per-channel reduction is a column sum over an
-// [M = N*H*W][C] matrix: blocks own 256 channels (32 lanes x 8 channels via
-// 16-B loads) x 8 row lanes, split rows over gridDim.y, reduce in LDS and add
-// one fp32 atomic per channel per block.  Statistics are fp32 throughout; the
-// normalise / affine / residual / ReLU pass is one vectorised elementwise sweep.
+// [M = N*H*W][C] matrix (geometry at bn_reduce_kernel).  Statistics are fp32
+// throughout; the normalise / affine / residual / ReLU pass and the backward
+// dx = A g + B x + D pass are single vectorised sweeps in which every thread
+// owns a fixed group of 8 channels.  Launches per BN: forward 3 (reduce,
+// finalize, apply), backward 3 (reduce, finalize with dgamma/dbeta, apply).
+#include <algorithm>
+
 #include "ldnn_common.h"
 #include "ldnn_kernels.h"
 
@@ -22,18 +25,71 @@ inline int grid_for(int64_t n) {
   return (int)(g < 1 ? 1 : (g > 2048 ? 2048 : g));
 }
 
-// ---- per-channel partial sums: acc[0][c] += sum x, acc[1][c] += sum x^2 -----
-// (backward variant: acc[0] += sum g, acc[1] += sum g * xhat, with g = dy * relu'(y))
+// ---- per-channel column reductions over [M][C] ------------------------------
+// Geometry: a 256-thread block covers up to 2048 channels as `lanes` 16-B column
+// vectors x `rl` row lanes (lanes = min(C/8, 256), rl = 256 / lanes), so every
+// thread keeps ONE fixed group of 8 channels -- all lanes busy at C = 64, the
+// per-channel constants loaded once -- and a wave reads whole contiguous row
+// runs.  Rows split over gridDim.y; the row loop is unrolled 4 deep so each
+// thread has 4 independent 16-B loads per tensor in flight.  Block partials are
+// reduced in LDS and added with one fp32 atomic per channel per block into an
+// accumulator that the finalize kernel consumes and clears (no zeroing launch).
+//   forward:  acc[c] += sum x,          acc[C + c] += sum x^2
+//   backward: acc[c] += sum g,          acc[C + c] += sum g * xhat,  g = dy * relu'(y)
+struct RedGeo {
+  int lanes, rl, gx, gy, rpb;
+};
+
+RedGeo red_geo(int M, int C) {
+  RedGeo g;
+  const int cv = C / 8;
+  g.lanes = cv < 256 ? cv : 256;
+  g.rl = 256 / g.lanes;
+  g.gx = (cv + 255) / 256;
+  int gy = std::max(1, 1024 / g.gx);               // ~4 blocks per CU in total
+  const int min_rows = 8 * g.rl;                   // >= 8 rows per row lane
+  gy = std::min(gy, std::max(1, (M + min_rows - 1) / min_rows));
+  g.rpb = (M + gy - 1) / gy;
+  g.gy = (M + g.rpb - 1) / g.rpb;
+  return g;
+}
+
 template <bool BWD, bool RELU>
-__global__ void chan_reduce_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
-                                   const bf16_t* __restrict__ y, const float* __restrict__ mean,
-                                   const float* __restrict__ invstd, float* __restrict__ acc, int M, int C,
-                                   int rows_per_block) {
-  __shared__ float part[2][8][32 * 8];
-  const int cg = threadIdx.x & 31, ty = threadIdx.x >> 5;
-  const int c0 = (blockIdx.x * 32 + cg) * 8;
-  const int r_begin = blockIdx.y * rows_per_block;
-  const int r_end = min(M, r_begin + rows_per_block);
+__device__ __forceinline__ void red_row(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
+                                        const bf16_t* __restrict__ y, size_t o, const float (&mu)[8],
+                                        const float (&is)[8], float (&s0)[8], float (&s1)[8]) {
+  const u16x8 xv = *reinterpret_cast<const u16x8*>(x + o);
+  if constexpr (BWD) {
+    const u16x8 gv = *reinterpret_cast<const u16x8*>(dy + o);
+    u16x8 yv;
+    if constexpr (RELU) yv = *reinterpret_cast<const u16x8*>(y + o);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float g = bf2f(gv[j]);
+      if constexpr (RELU) g = bf2f(yv[j]) > 0.f ? g : 0.f;
+      s0[j] += g;
+      s1[j] += g * (bf2f(xv[j]) - mu[j]) * is[j];
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float v = bf2f(xv[j]);
+      s0[j] += v;
+      s1[j] += v * v;
+    }
+  }
+}
+
+template <bool BWD, bool RELU>
+__global__ __launch_bounds__(256) void bn_reduce_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
+                                                        const bf16_t* __restrict__ y, const float* __restrict__ mean,
+                                                        const float* __restrict__ invstd, float* __restrict__ acc,
+                                                        int M, int C, int rpb, int lanes, int rl) {
+  __shared__ float red[2][256 * 8];
+  const int tid = threadIdx.x, lane = tid % lanes, rlane = tid / lanes;
+  const int cv0 = blockIdx.x * 256 + lane;
+  const int c0 = cv0 * 8;
+  const bool active = rlane < rl && c0 < C;
   float s0[8], s1[8], mu[8], is[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -42,7 +98,7 @@ __global__ void chan_reduce_kernel(const bf16_t* __restrict__ x, const bf16_t* _
     mu[j] = 0.f;
     is[j] = 0.f;
   }
-  if (c0 < C) {
+  if (active) {
     if constexpr (BWD) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -50,49 +106,40 @@ __global__ void chan_reduce_kernel(const bf16_t* __restrict__ x, const bf16_t* _
         is[j] = invstd[c0 + j];
       }
     }
-    for (int r = r_begin + ty; r < r_end; r += 8) {
-      const size_t o = (size_t)r * C + c0;
-      const u16x8 xv = *reinterpret_cast<const u16x8*>(x + o);
-      if constexpr (BWD) {
-        const u16x8 gv = *reinterpret_cast<const u16x8*>(dy + o);
-        u16x8 yv;
-        if constexpr (RELU) yv = *reinterpret_cast<const u16x8*>(y + o);
+    const int r_end = min(M, (int)(blockIdx.y + 1) * rpb);
+    int r = blockIdx.y * rpb + rlane;
+    for (; r + 3 * rl < r_end; r += 4 * rl) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          float g = bf2f(gv[j]);
-          if constexpr (RELU) g = bf2f(yv[j]) > 0.f ? g : 0.f;
-          s0[j] += g;
-          s1[j] += g * (bf2f(xv[j]) - mu[j]) * is[j];
-        }
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float v = bf2f(xv[j]);
-          s0[j] += v;
-          s1[j] += v * v;
-        }
-      }
+      for (int u = 0; u < 4; ++u) red_row<BWD, RELU>(x, dy, y, (size_t)(r + u * rl) * C + c0, mu, is, s0, s1);
     }
+    for (; r < r_end; r += rl) red_row<BWD, RELU>(x, dy, y, (size_t)r * C + c0, mu, is, s0, s1);
   }
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    part[0][ty][cg * 8 + j] = s0[j];
-    part[1][ty][cg * 8 + j] = s1[j];
-  }
-  __syncthreads();
-  if (ty < 2 && c0 < C) {
+  const int row = lanes * 8;
+  if (rlane < rl) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      float t = 0.f;
-#pragma unroll
-      for (int q = 0; q < 8; ++q) t += part[ty][q][cg * 8 + j];
-      atomicAdd(acc + ty * C + c0 + j, t);
+      red[0][rlane * row + lane * 8 + j] = s0[j];
+      red[1][rlane * row + lane * 8 + j] = s1[j];
+    }
+  }
+  __syncthreads();
+  for (int ch = tid; ch < row; ch += 256) {
+    float t0 = 0.f, t1 = 0.f;
+    for (int q = 0; q < rl; ++q) {
+      t0 += red[0][q * row + ch];
+      t1 += red[1][q * row + ch];
+    }
+    const int c = blockIdx.x * 2048 + ch;
+    if (c < C) {
+      atomicAdd(acc + c, t0);
+      atomicAdd(acc + C + c, t1);
     }
   }
 }
 
-// mean / invstd / scale / shift (+ running-stat EMA, PyTorch semantics: unbiased var)
-__global__ void bn_finalize_kernel(const float* __restrict__ acc, const float* __restrict__ gamma,
+// mean / invstd / scale / shift (+ running-stat EMA, PyTorch semantics: unbiased
+// var); consumes the forward accumulator and clears it for the next call
+__global__ void bn_finalize_kernel(float* __restrict__ acc, const float* __restrict__ gamma,
                                    const float* __restrict__ beta, float* __restrict__ running_mean,
                                    float* __restrict__ running_var, float* __restrict__ save_mean,
                                    float* __restrict__ save_invstd, float* __restrict__ scale,
@@ -101,6 +148,8 @@ __global__ void bn_finalize_kernel(const float* __restrict__ acc, const float* _
   if (c >= C) return;
   const float m = acc[c] / (float)M;
   const float var = fmaxf(acc[C + c] / (float)M - m * m, 0.f);
+  acc[c] = 0.f;
+  acc[C + c] = 0.f;
   const float is = rsqrtf(var + eps);
   save_mean[c] = m;
   save_invstd[c] = is;
@@ -125,62 +174,97 @@ __global__ void bn_eval_coeff_kernel(const float* __restrict__ gamma, const floa
   shift[c] = b - rm[c] * g * is;
 }
 
-// y = relu?( x * scale[c] + shift[c] (+ res) )
+// backward coefficients: dx = A g + B x + D  (A = gamma*invstd,
+// B = -gamma*invstd^2 * S1/M, D = -gamma*invstd*S0/M - B*mean); dgamma += S1,
+// dbeta += S0 straight into the flat gradient buffer; clears the accumulator
+__global__ void bn_bwd_finalize_kernel(float* __restrict__ acc, const float* __restrict__ gamma,
+                                       const float* __restrict__ mean, const float* __restrict__ invstd,
+                                       float* __restrict__ coef, float* __restrict__ dgamma,
+                                       float* __restrict__ dbeta, int M, int C) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float S0 = acc[c], S1 = acc[C + c];
+  acc[c] = 0.f;
+  acc[C + c] = 0.f;
+  const float gm = gamma ? gamma[c] : 1.f, is = invstd[c], invM = 1.f / (float)M;
+  const float A = gm * is, B = -gm * is * is * S1 * invM;
+  coef[c] = A;
+  coef[C + c] = B;
+  coef[2 * C + c] = -gm * is * S0 * invM - B * mean[c];
+  if (dgamma) dgamma[c] += S1;
+  if (dbeta) dbeta[c] += S0;
+}
+
+__device__ __forceinline__ void load8(const float* p, float (&v)[8]) {
+  const floatx4 a = *reinterpret_cast<const floatx4*>(p), b = *reinterpret_cast<const floatx4*>(p + 4);
+  v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3];
+  v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
+}
+
+// y = relu?( x * scale[c] + shift[c] (+ res) ) -- same fixed-channel geometry
 template <bool RES, bool RELU>
-__global__ void bn_apply_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
-                                const float* __restrict__ scale, const float* __restrict__ shift,
-                                bf16_t* __restrict__ y, int64_t nvec, int C) {
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nvec; i += stride) {
-    const int c0 = (int)((i * 8) % C);
-    const u16x8 xv = reinterpret_cast<const u16x8*>(x)[i];
+__global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
+                                                       const float* __restrict__ scale,
+                                                       const float* __restrict__ shift, bf16_t* __restrict__ y,
+                                                       int M, int C, int rpb, int lanes, int rl) {
+  const int tid = threadIdx.x, lane = tid % lanes, rlane = tid / lanes;
+  const int c0 = (blockIdx.x * 256 + lane) * 8;
+  if (rlane >= rl || c0 >= C) return;
+  float sc[8], sh[8];
+  load8(scale + c0, sc);
+  load8(shift + c0, sh);
+  const int r_end = min(M, (int)(blockIdx.y + 1) * rpb);
+#pragma unroll 4
+  for (int r = blockIdx.y * rpb + rlane; r < r_end; r += rl) {
+    const size_t o = (size_t)r * C + c0;
+    const u16x8 xv = *reinterpret_cast<const u16x8*>(x + o);
     u16x8 rv;
-    if constexpr (RES) rv = reinterpret_cast<const u16x8*>(res)[i];
-    const floatx4 sa = *reinterpret_cast<const floatx4*>(scale + c0);
-    const floatx4 sb = *reinterpret_cast<const floatx4*>(scale + c0 + 4);
-    const floatx4 ha = *reinterpret_cast<const floatx4*>(shift + c0);
-    const floatx4 hb = *reinterpret_cast<const floatx4*>(shift + c0 + 4);
-    u16x8 o;
+    if constexpr (RES) rv = *reinterpret_cast<const u16x8*>(res + o);
+    u16x8 out;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      float v = bf2f(xv[j]) * (j < 4 ? sa[j] : sb[j - 4]) + (j < 4 ? ha[j] : hb[j - 4]);
+      float v = bf2f(xv[j]) * sc[j] + sh[j];
       if constexpr (RES) v += bf2f(rv[j]);
       if constexpr (RELU) v = fmaxf(v, 0.f);
-      o[j] = f2bf(v);
+      out[j] = f2bf(v);
     }
-    reinterpret_cast<u16x8*>(y)[i] = o;
+    *reinterpret_cast<u16x8*>(y + o) = out;
   }
 }
 
-// dx = gamma*invstd * (g - (sum g)/M - xhat * (sum g xhat)/M);  g = dy * relu'(y)
+// dx = A g + B x + D, g = dy * relu'(y); dres = g (the residual branch's gradient)
 template <bool RELU>
-__global__ void bn_bwd_apply_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
-                                    const bf16_t* __restrict__ y, const float* __restrict__ mean,
-                                    const float* __restrict__ invstd, const float* __restrict__ gamma,
-                                    const float* __restrict__ acc, bf16_t* __restrict__ dx, bf16_t* __restrict__ dres,
-                                    int64_t nvec, int C, float invM) {
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nvec; i += stride) {
-    const int c0 = (int)((i * 8) % C);
-    const u16x8 xv = reinterpret_cast<const u16x8*>(x)[i];
-    const u16x8 gv = reinterpret_cast<const u16x8*>(dy)[i];
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16_t* __restrict__ x,
+                                                           const bf16_t* __restrict__ dy,
+                                                           const bf16_t* __restrict__ y,
+                                                           const float* __restrict__ coef, bf16_t* __restrict__ dx,
+                                                           bf16_t* __restrict__ dres, int M, int C, int rpb,
+                                                           int lanes, int rl) {
+  const int tid = threadIdx.x, lane = tid % lanes, rlane = tid / lanes;
+  const int c0 = (blockIdx.x * 256 + lane) * 8;
+  if (rlane >= rl || c0 >= C) return;
+  float A[8], B[8], D[8];
+  load8(coef + c0, A);
+  load8(coef + C + c0, B);
+  load8(coef + 2 * C + c0, D);
+  const int r_end = min(M, (int)(blockIdx.y + 1) * rpb);
+#pragma unroll 4
+  for (int r = blockIdx.y * rpb + rlane; r < r_end; r += rl) {
+    const size_t o = (size_t)r * C + c0;
+    const u16x8 xv = *reinterpret_cast<const u16x8*>(x + o);
+    const u16x8 gv = *reinterpret_cast<const u16x8*>(dy + o);
     u16x8 yv;
-    if constexpr (RELU) yv = reinterpret_cast<const u16x8*>(y)[i];
-    u16x8 o, og;
+    if constexpr (RELU) yv = *reinterpret_cast<const u16x8*>(y + o);
+    u16x8 out, og;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int c = c0 + j;
       float g = bf2f(gv[j]);
       if constexpr (RELU) g = bf2f(yv[j]) > 0.f ? g : 0.f;
-      const float is = invstd[c];
-      const float xh = (bf2f(xv[j]) - mean[c]) * is;
-      const float gm = gamma ? gamma[c] : 1.f;
-      const float v = gm * is * (g - acc[c] * invM - xh * acc[C + c] * invM);
-      o[j] = f2bf(v);
+      out[j] = f2bf(A[j] * g + B[j] * bf2f(xv[j]) + D[j]);
       og[j] = f2bf(g);
     }
-    reinterpret_cast<u16x8*>(dx)[i] = o;
-    if (dres) reinterpret_cast<u16x8*>(dres)[i] = og;
+    *reinterpret_cast<u16x8*>(dx + o) = out;
+    if (dres) *reinterpret_cast<u16x8*>(dres + o) = og;
   }
 }
 
@@ -318,43 +402,43 @@ __global__ void gap_bwd_kernel(const bf16_t* __restrict__ dy, bf16_t* __restrict
   }
 }
 
-void reduce_grid(int M, int C, dim3& grid, int& rpb) {
-  const int gx = (C + 255) / 256;
-  int gy = (M + 511) / 512;
-  const int cap = max(1, 2048 / gx);
-  if (gy > cap) gy = cap;
-  rpb = (M + gy - 1) / gy;
-  grid = dim3(gx, gy);
-}
-
 }  // namespace
+
+// Workspace (fp32, zeroed once, kept by the caller -- e.g. per BatchNorm module):
+//   [0, C) scale | [C, 2C) shift | [2C, 4C) forward accumulator | [4C, 6C)
+//   backward accumulator | [6C, 9C) backward coefficients A, B, D.
+// Both accumulators are cleared by the kernel that consumes them.
+int bn_workspace_floats(int C) { return 10 * C; }
 
 hipError_t bn_forward(const BnArgs& a, hipStream_t s) {
   const int M = a.M, C = a.C;
   if (C % 8) return hipErrorInvalidValue;
-  const int64_t nvec = (int64_t)M * C / 8;
+  if (M <= 0) return hipSuccess;
+  const RedGeo g = red_geo(M, C);
+  const dim3 grid(g.gx, g.gy);
   if (a.training) {
-    hipError_t e = zero2d_f32(a.ws, 1, 2 * C, 2 * C, s);
-    if (e != hipSuccess) return e;
-    dim3 grid;
-    int rpb;
-    reduce_grid(M, C, grid, rpb);
-    chan_reduce_kernel<false, false><<<grid, kBlock, 0, s>>>(a.x, nullptr, nullptr, nullptr, nullptr, a.ws, M, C, rpb);
-    bn_finalize_kernel<<<(C + 255) / 256, 256, 0, s>>>(a.ws, a.gamma, a.beta, a.running_mean, a.running_var,
-                                                       a.save_mean, a.save_invstd, a.scale, a.shift, M, C, a.eps,
+    float* acc = a.ws + 2 * C;
+    bn_reduce_kernel<false, false><<<grid, 256, 0, s>>>(a.x, nullptr, nullptr, nullptr, nullptr, acc, M, C, g.rpb,
+                                                        g.lanes, g.rl);
+    bn_finalize_kernel<<<(C + 255) / 256, 256, 0, s>>>(acc, a.gamma, a.beta, a.running_mean, a.running_var,
+                                                       a.save_mean, a.save_invstd, a.ws, a.ws + C, M, C, a.eps,
                                                        a.momentum);
   } else {
-    bn_eval_coeff_kernel<<<(C + 255) / 256, 256, 0, s>>>(a.gamma, a.beta, a.running_mean, a.running_var, a.scale,
-                                                         a.shift, C, a.eps);
+    bn_eval_coeff_kernel<<<(C + 255) / 256, 256, 0, s>>>(a.gamma, a.beta, a.running_mean, a.running_var, a.ws,
+                                                         a.ws + C, C, a.eps);
   }
-  const int g = grid_for(nvec);
+  const float* sc = a.ws;
+  const float* sh = a.ws + C;
+#define LDNN_BN_APPLY(RES, RELU) \
+  bn_apply_kernel<RES, RELU><<<grid, 256, 0, s>>>(a.x, a.residual, sc, sh, a.y, M, C, g.rpb, g.lanes, g.rl)
   if (a.residual) {
-    if (a.relu) bn_apply_kernel<true, true><<<g, kBlock, 0, s>>>(a.x, a.residual, a.scale, a.shift, a.y, nvec, C);
-    else bn_apply_kernel<true, false><<<g, kBlock, 0, s>>>(a.x, a.residual, a.scale, a.shift, a.y, nvec, C);
+    if (a.relu) LDNN_BN_APPLY(true, true);
+    else LDNN_BN_APPLY(true, false);
   } else {
-    if (a.relu) bn_apply_kernel<false, true><<<g, kBlock, 0, s>>>(a.x, nullptr, a.scale, a.shift, a.y, nvec, C);
-    else bn_apply_kernel<false, false><<<g, kBlock, 0, s>>>(a.x, nullptr, a.scale, a.shift, a.y, nvec, C);
+    if (a.relu) LDNN_BN_APPLY(false, true);
+    else LDNN_BN_APPLY(false, false);
   }
+#undef LDNN_BN_APPLY
   return hipGetLastError();
 }
 
@@ -362,31 +446,23 @@ hipError_t bn_backward(const BnArgs& a, const uint16_t* dy, uint16_t* dx, uint16
                        float* dbeta, hipStream_t s) {
   const int M = a.M, C = a.C;
   if (C % 8) return hipErrorInvalidValue;
-  hipError_t e = zero2d_f32(a.ws, 1, 2 * C, 2 * C, s);
-  if (e != hipSuccess) return e;
-  dim3 grid;
-  int rpb;
-  reduce_grid(M, C, grid, rpb);
+  if (M <= 0) return hipSuccess;
+  const RedGeo g = red_geo(M, C);
+  const dim3 grid(g.gx, g.gy);
+  float* acc = a.ws + 4 * C;
+  float* coef = a.ws + 6 * C;
   if (a.relu)
-    chan_reduce_kernel<true, true><<<grid, kBlock, 0, s>>>(a.x, dy, a.y, a.save_mean, a.save_invstd, a.ws, M, C, rpb);
+    bn_reduce_kernel<true, true><<<grid, 256, 0, s>>>(a.x, dy, a.y, a.save_mean, a.save_invstd, acc, M, C, g.rpb,
+                                                      g.lanes, g.rl);
   else
-    chan_reduce_kernel<true, false><<<grid, kBlock, 0, s>>>(a.x, dy, nullptr, a.save_mean, a.save_invstd, a.ws, M, C,
-                                                           rpb);
-  const int64_t nvec = (int64_t)M * C / 8;
-  const int g = grid_for(nvec);
+    bn_reduce_kernel<true, false><<<grid, 256, 0, s>>>(a.x, dy, nullptr, a.save_mean, a.save_invstd, acc, M, C,
+                                                       g.rpb, g.lanes, g.rl);
+  bn_bwd_finalize_kernel<<<(C + 255) / 256, 256, 0, s>>>(acc, a.gamma, a.save_mean, a.save_invstd, coef, dgamma,
+                                                         dbeta, M, C);
   if (a.relu)
-    bn_bwd_apply_kernel<true><<<g, kBlock, 0, s>>>(a.x, dy, a.y, a.save_mean, a.save_invstd, a.gamma, a.ws, dx, dres,
-                                                   nvec, C, 1.f / (float)M);
+    bn_bwd_apply_kernel<true><<<grid, 256, 0, s>>>(a.x, dy, a.y, coef, dx, dres, M, C, g.rpb, g.lanes, g.rl);
   else
-    bn_bwd_apply_kernel<false><<<g, kBlock, 0, s>>>(a.x, dy, nullptr, a.save_mean, a.save_invstd, a.gamma, a.ws, dx,
-                                                    dres, nvec, C, 1.f / (float)M);
-  // dgamma += sum g*xhat ; dbeta += sum g  (accumulate into the flat gradient buffer)
-  if (dgamma || dbeta) {
-    if (dgamma) e = mix3_f32(dgamma, dgamma, a.ws + C, nullptr, 1.f, 1.f, 0.f, C, nullptr, s);
-    if (e != hipSuccess) return e;
-    if (dbeta) e = mix3_f32(dbeta, dbeta, a.ws, nullptr, 1.f, 1.f, 0.f, C, nullptr, s);
-    if (e != hipSuccess) return e;
-  }
+    bn_bwd_apply_kernel<false><<<grid, 256, 0, s>>>(a.x, dy, nullptr, coef, dx, dres, M, C, g.rpb, g.lanes, g.rl);
   return hipGetLastError();
 }
 

@@ -300,9 +300,9 @@ hipError_t conv2d_dgrad(const ConvShape& s, const uint16_t* dy, const uint16_t* 
 }
 
 hipError_t conv2d_wgrad(const ConvShape& s, const uint16_t* dy, const uint16_t* x, float* dw, float beta,
-                        hipStream_t st) {
+                        hipStream_t st, float* ws) {
   if (g_conv_impl == 0) {
-    const hipError_t e = conv2d_wgrad_lds(s, dy, x, dw, beta, st);
+    const hipError_t e = conv2d_wgrad_lds(s, dy, x, dw, beta, st, ws);
     if (e != hipErrorNotSupported) return e;
   }
   ConvArgs a{};

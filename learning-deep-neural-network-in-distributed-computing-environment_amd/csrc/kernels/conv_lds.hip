@@ -77,8 +77,8 @@ struct LArgs {
   int tiles_x;       // gridDim.x
   int dn, dp, dq;    // wgrad: 64 = dn*PQ + dp*Q + dq
   FastDiv f_pq, f_q, f_c, f_s;
-  float* ws;         // split-K combine slabs (nullptr: atomics / no split)
-  int* cnt;          // split-K arrival counters
+  float* ws;         // split-K: combine slabs (with cnt) or wgrad partial slabs [split][M][N] (without)
+  int* cnt;          // split-K arrival counters of the in-launch combine
 };
 
 // Per-workgroup geometry: which rows its class covers and which taps it sums.
@@ -390,7 +390,7 @@ __global__ __launch_bounds__(256, 2) void conv_lds_kernel(LArgs a, const bf16_t*
   const int kt0 = blockIdx.y * a.nk_split;
   const int nk = max(0, min(g.nk - kt0, a.nk_split));
   const bool combine = a.cnt != nullptr && gridDim.y > 1;
-  if (nk == 0 && gridDim.y > 1 && !combine) return;  // an empty atomic slice adds nothing
+  if (nk == 0 && gridDim.y > 1 && !combine && a.ws == nullptr) return;  // an empty atomic slice adds nothing
 
   floatx4 acc[4][4];
 #pragma unroll
@@ -449,6 +449,18 @@ __global__ __launch_bounds__(256, 2) void conv_lds_kernel(LArgs a, const bf16_t*
       lds_barrier();  // every wave is done with the operand stages (the ticket word lives there)
       const int tile = blockIdx.z * a.tiles_x + blockIdx.x;
       if (!splitk_combine<4, 4, NW * 64>(acc, a.ws, a.cnt, tile, gridDim.y, blockIdx.y, smem)) return;
+    } else if (a.ws != nullptr) {
+      // wgrad: this slice's fp32 partial tile into its own slab; a separate
+      // reduction kernel sums the slabs over all CUs (deterministic, no atomics)
+      if constexpr (OUT_F32 && EPI == EPI_NONE) {
+        GemmParams p{};
+        p.C = a.ws + (size_t)blockIdx.y * a.M * a.N;
+        p.M = g.M;
+        p.N = a.N;
+        p.ldc = a.N;
+        epilogue<EPI_NONE, true, 4, 4>(p, acc, mb, nbase, lane);
+      }
+      return;
     } else {
       if constexpr (OUT_F32 && EPI == EPI_NONE) {  // fp32 atomics into the (cleared / accumulated) output
 #pragma unroll
@@ -484,7 +496,39 @@ __global__ __launch_bounds__(256, 2) void conv_lds_kernel(LArgs a, const bf16_t*
   epilogue<EPI, OUT_F32, 4, 4>(p, acc, mb, nbase, lane);
 }
 
+// out[i] = sum_s ws[s][i] (+ beta * out[i]): the cross-CU reduction of wgrad slabs.
+__global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__ ws, float* __restrict__ out,
+                                                       int64_t n4, int splits, float beta) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += stride) {
+    floatx4 v = reinterpret_cast<const floatx4*>(ws)[i];
+    for (int sp = 1; sp < splits; ++sp) v += reinterpret_cast<const floatx4*>(ws)[(int64_t)sp * n4 + i];
+    if (beta != 0.f) v += beta * reinterpret_cast<const floatx4*>(out)[i];
+    reinterpret_cast<floatx4*>(out)[i] = v;
+  }
+}
+
 bool fits(size_t bytes) { return bytes < kOOBLimit; }
+
+struct WgradPlan {
+  bool narrow;
+  int tiles, splits, nk_all, nk_split;
+};
+
+WgradPlan plan_wgrad(const ConvShape& s) {
+  WgradPlan p;
+  p.narrow = s.K <= 64;
+  const int BM = p.narrow ? 64 : 128, BN = p.narrow ? 256 : 128;
+  const int M = s.K, N = s.R * s.S * s.C;
+  p.tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  p.nk_all = (s.N * s.P * s.Q + 63) / 64;
+  // split the npq reduction over ~1.5 workgroups per CU, >= 8 K-tiles per slice
+  int splits = 1;
+  if (p.tiles < 256) splits = std::max(1, std::min((384 + p.tiles - 1) / p.tiles, p.nk_all / 8));
+  p.nk_split = (p.nk_all + splits - 1) / splits;
+  p.splits = (p.nk_all + p.nk_split - 1) / p.nk_split;
+  return p;
+}
 
 LArgs base_args(const ConvShape& s) {
   LArgs a{};
@@ -595,6 +639,12 @@ ConvWorkspace conv2d_lds_workspace(const ConvShape& s, int op) {
   if (!shape_ok(s)) return ConvWorkspace{};
   if (op == 0 && s.C % 64 == 0) return ws_of(plan_fwd(s));
   if (op == 1 && s.K % 64 == 0) return ws_of(plan_dgrad(s));
+  if (op == 2 && s.C % 8 == 0 && s.K % 8 == 0) {
+    const WgradPlan p = plan_wgrad(s);
+    ConvWorkspace w{};
+    if (p.splits > 1) w.slab_bytes = (size_t)p.splits * s.K * s.R * s.S * s.C * 4;
+    return w;
+  }
   return ConvWorkspace{};
 }
 
@@ -653,16 +703,19 @@ hipError_t conv2d_dgrad_lds(const ConvShape& s, const uint16_t* dy, const uint16
 }
 
 hipError_t conv2d_wgrad_lds(const ConvShape& s, const uint16_t* dy, const uint16_t* x, float* dw, float beta,
-                            hipStream_t st) {
+                            hipStream_t st, float* ws) {
   if (!shape_ok(s) || s.C % 8 != 0 || s.K % 8 != 0) return hipErrorNotSupported;
   if (beta != 0.f && beta != 1.f) return hipErrorNotSupported;
+  const WgradPlan pl = plan_wgrad(s);
   LArgs a = base_args(s);
   a.out = dw;
   a.beta = beta;
   a.M = s.K;
   a.N = a.rsc;
   a.Kd = s.N * s.P * s.Q;
-  a.nk_all = (a.Kd + 63) / 64;
+  a.nk_all = pl.nk_all;
+  a.nk_split = pl.nk_split;
+  a.tiles_x = pl.tiles;
   a.nb = 0;
   const int pq = s.P * s.Q;
   a.dn = 64 / pq;
@@ -672,21 +725,26 @@ hipError_t conv2d_wgrad_lds(const ConvShape& s, const uint16_t* dy, const uint16
   a.f_q = make_fastdiv(s.Q);
   a.f_c = make_fastdiv(s.C);
   a.f_s = make_fastdiv(s.S);
-  const bool narrow = s.K <= 64;
-  const int BM = narrow ? 64 : 128, BN = narrow ? 256 : 128;
-  a.tiles_x = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
-  // split the npq reduction so the grid covers ~2 workgroups per CU, >= 8 K-tiles each
-  int splits = 1;
-  if (a.tiles_x < 256) splits = std::max(1, std::min((512 + a.tiles_x - 1) / a.tiles_x, a.nk_all / 8));
-  a.nk_split = (a.nk_all + splits - 1) / splits;
-  splits = (a.nk_all + a.nk_split - 1) / a.nk_split;
-  if (splits > 1 && beta == 0.f) {  // the atomics accumulate into a cleared output
-    hipError_t e = zero2d_f32(dw, a.M, a.N, a.N, st);
-    if (e != hipSuccess) return e;
+  const int splits = pl.splits;
+  if (splits > 1) {
+    if (ws != nullptr) {
+      a.ws = ws;  // partial slabs + slab_sum_kernel
+    } else if (beta == 0.f) {  // no workspace: fp32 atomics into a cleared output
+      hipError_t e = zero2d_f32(dw, a.M, a.N, a.N, st);
+      if (e != hipSuccess) return e;
+    }
   }
   const size_t bdy = (size_t)s.N * s.P * s.Q * s.K * 2, bx = (size_t)s.N * s.H * s.W * s.C * 2;
-  if (narrow) return launch<1, 4, WgradA<64, 2, 4>, WgradB<256, 8, 4>, true, false>(a, EPI_NONE, splits, dy, bdy, x, bx, st);
-  return launch<2, 2, WgradA<128, 4, 4>, WgradB<128, 4, 4>, true, false>(a, EPI_NONE, splits, dy, bdy, x, bx, st);
+  hipError_t e;
+  if (pl.narrow)
+    e = launch<1, 4, WgradA<64, 2, 4>, WgradB<256, 8, 4>, true, false>(a, EPI_NONE, splits, dy, bdy, x, bx, st);
+  else
+    e = launch<2, 2, WgradA<128, 4, 4>, WgradB<128, 4, 4>, true, false>(a, EPI_NONE, splits, dy, bdy, x, bx, st);
+  if (e != hipSuccess || splits == 1 || ws == nullptr) return e;
+  const int64_t n4 = (int64_t)a.M * a.N / 4;
+  const int grid = (int)std::min<int64_t>(2048, (n4 + 255) / 256);
+  slab_sum_kernel<<<grid, 256, 0, st>>>(ws, dw, n4, splits, beta);
+  return hipGetLastError();
 }
 
 }  // namespace ldnn

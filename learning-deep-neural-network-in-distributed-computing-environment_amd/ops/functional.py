@@ -300,6 +300,17 @@ def conv2d(x, mod, relu: bool = False):
     return F.relu(y) if relu else y
 
 
+def _bn_workspace(mod, C: int, dev, C_) -> torch.Tensor:
+    """The module's persistent BN workspace (zeroed once: the kernels keep their
+    accumulators clear), so a BN costs no zero-fill launch per call."""
+    ws = getattr(mod, "_ldnn_bn_ws", None)
+    n = C_.bn_workspace_floats(C)
+    if ws is None or ws.device != dev or ws.numel() < n:
+        ws = torch.zeros(n, dtype=torch.float32, device=dev)
+        mod._ldnn_bn_ws = ws
+    return ws
+
+
 class _BatchNormNative(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, residual, mod, flat, relu):
@@ -313,7 +324,7 @@ class _BatchNormNative(torch.autograd.Function):
             r2 = as_nhwc(rb, C, zero_pad=False).reshape(-1, C)
         y = torch.empty(N, H, W, C, dtype=torch.bfloat16, device=x.device)
         dev = x.device
-        ws = torch.empty(4 * C, dtype=torch.float32, device=dev)
+        ws = _bn_workspace(mod, C, dev, C_)
         smean = torch.empty(C, dtype=torch.float32, device=dev)
         sinv = torch.empty(C, dtype=torch.float32, device=dev)
         gamma = flat.master_storage(weight)[:C] if weight is not None else None

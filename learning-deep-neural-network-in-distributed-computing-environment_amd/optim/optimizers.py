@@ -59,11 +59,23 @@ class _FlatOptimizer(torch.optim.Optimizer):
         st = self._ls()
         hp = st.get("hp")
         if hp is None or hp.device != flat.master.device:
+            if getattr(self, "_ldnn_capturing", False):
+                raise RuntimeError("run an eager optimizer step before capturing it into a graph")
             hp = torch.zeros(2, dtype=torch.float32, device=flat.master.device)
             hp[1] = float(st.get("step", 0))
             st["hp"] = hp
-        hp[0].fill_(lr)
+        # inside a hipGraph capture the lr write is NOT recorded: the graph reads hp,
+        # and GraphedStep refreshes it (sync_hyperparams) whenever the lr changes
+        if not getattr(self, "_ldnn_capturing", False):
+            hp[0].fill_(lr)
         return hp
+
+    @torch.no_grad()
+    def sync_hyperparams(self):
+        """Write the current learning rate into the device hyper-parameter tensor."""
+        hp = self._ls().get("hp")
+        if hp is not None:
+            hp[0].fill_(self.param_groups[0]["lr"])
 
     def _buf(self, name, like):
         st = self._ls()

@@ -54,11 +54,13 @@ def _progress(it, enabled, desc):
 
 def train_local_epoch(model, trainloader, criterion, optimizer, device, scheduler=None, *, dp=None,
                       step_aggregator=None, cutoff: StragglerCutoff | None = None, max_steps: int | None = None,
-                      step_scheduler: bool = True, timer: PhaseTimer | None = None):
+                      step_scheduler: bool = True, timer: PhaseTimer | None = None, graphs: bool = False):
     """One pass over the rank's shard.  Returns (mean loss, accuracy %, per-batch losses).
 
     ``timer`` (utils.tracing.PhaseTimer) brackets forward / backward / grad_sync /
     optimizer with roctx ranges and HIP events (BAR/trainer.py:194-223 has none).
+    ``graphs``: replay each full-size step from one hipGraph (train/graphed.py) when
+    the step issues no per-step collectives.
     """
     tm = timer or null_timer()
     model.train()
@@ -68,10 +70,23 @@ def train_local_epoch(model, trainloader, criterion, optimizer, device, schedule
     stats = torch.zeros(2, dtype=torch.float32, device=dev)
     total, done = 0, 0
     ldnn_ce = isinstance(criterion, LdnnCE)
+    use_graph = (graphs and dev.type == "cuda" and dp is None and step_aggregator is None and ldnn_ce
+                 and timer is None)
     try:
         for i, (x, y) in enumerate(trainloader):
             if i >= nb:
                 break
+            if use_graph and (i > 0 or getattr(model, "_ldnn_graphed", None) is not None):
+                # the first batch ran eagerly (momentum / optimizer state exist), so the
+                # capture needs no extra warmup steps and training semantics are unchanged
+                gs = _graphed_step(model, criterion, optimizer, x, y)
+                if x.shape == gs.x.shape:
+                    losses[i] = gs(x, y).detach().float()
+                    total += y.numel()
+                    done += 1
+                    if cutoff is not None:
+                        cutoff.step(i)
+                    continue
             optimizer.zero_grad()
             with tm.phase("forward"):
                 out = model(x)
@@ -102,12 +117,26 @@ def train_local_epoch(model, trainloader, criterion, optimizer, device, schedule
         raise
     if step_scheduler and scheduler is not None:
         scheduler.step()
+    gs = getattr(model, "_ldnn_graphed", None) if use_graph else None
+    if gs is not None:
+        gs.flush_stats(stats)
     batch_losses = losses[:done].tolist()  # the one host sync of the epoch
     correct = stats[1].item()
     train_loss = float(np.mean(batch_losses)) if batch_losses else 0.0
     return train_loss, 100.0 * correct / max(total, 1), batch_losses
 
 
+
+
+def _graphed_step(model, criterion, optimizer, x, y):
+    """The model's cached GraphedStep (captured on the first graphed batch)."""
+    from .graphed import GraphedStep
+
+    gs = getattr(model, "_ldnn_graphed", None)
+    if gs is None or gs.optimizer is not optimizer or gs.criterion is not criterion:
+        gs = GraphedStep(model, criterion, optimizer, x, y, warmup=0)
+        model._ldnn_graphed = gs
+    return gs
 
 
 def _pack(local_records, batch_losses_per_epoch, E_l, max_len, device):
@@ -147,7 +176,7 @@ def train_global(model, trainloader, val_loader, trainset, valset, indices_train
                  seed: int = 0, legacy_gossip: bool = False, average_buffers: bool = False,
                  check_every: int = 20, progress: bool = True, logger=None, checkpointer=None,
                  start_global_epoch: int = 0, histories=None, dtype=torch.float32, verbose: bool = True,
-                 timer: PhaseTimer | None = None):
+                 timer: PhaseTimer | None = None, graphs: bool = False):
     comm = comm or default_comm()
     tm = timer or null_timer()
     N = comm.world_size
@@ -190,7 +219,7 @@ def train_global(model, trainloader, val_loader, trainset, valset, indices_train
             try:
                 loss, acc, bl = train_local_epoch(model, trainloader, criterion, optimizer, dev, scheduler, dp=dp,
                                                   step_aggregator=step_aggregator, cutoff=cutoff,
-                                                  max_steps=max_steps, timer=timer)
+                                                  max_steps=max_steps, timer=timer, graphs=graphs)
             except StopLocalTraining:
                 # cut by the collective time limit: keep LR schedules aligned across ranks
                 for _ in range(num_local_epochs - local_epoch - 1):

@@ -38,6 +38,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-stock", action="store_true")
     ap.add_argument("--conv-impl", type=int, default=0, help="0 = LDS-DMA fast path, 1 = generic conv kernel only")
+    ap.add_argument("--graph", action="store_true", help="replay the ldnn step from one hipGraph (train.graphed)")
     a = ap.parse_args()
     from ldnn.ops import _ext as _e
 
@@ -60,8 +61,16 @@ def main():
         crit(m(xb), y).backward()
         opt.step()
 
+    if a.graph:
+        from ldnn.train.graphed import GraphedStep
+
+        gs = GraphedStep(m, crit, opt, xb, y)
+
+        def step_ldnn():  # noqa: F811
+            gs(xb, y)
+
     t = run(step_ldnn, a.steps, a.warmup)
-    rec = {"model": a.model, "batch": a.batch, "conv_impl": a.conv_impl, "ldnn_ms": round(t * 1e3, 3), "ldnn_samples_per_s": round(a.batch / t, 1)}
+    rec = {"model": a.model, "batch": a.batch, "conv_impl": a.conv_impl, "graph": a.graph, "ldnn_ms": round(t * 1e3, 3), "ldnn_samples_per_s": round(a.batch / t, 1)}
     if not a.no_stock:
         import torch.nn as nn
 

@@ -20,7 +20,7 @@ SHAPES = [
     # LDS-DMA fast path (C / K multiples of 64): 64-channel tiles, ragged rows,
     # stride-2 parity-class dgrad, split-K combine of the small-M tail stages
     (2, 64, 56, 56, 64, 3, 1, 1),     # ResNet layer1 (256x64 tiles)
-    (3, 64, 7, 9, 64, 3, 1, 1),       # ragged M, non-square
+    (3, 64, 7, 7, 64, 3, 1, 1),       # ragged M (147 rows)
     (2, 128, 15, 15, 256, 3, 2, 1),   # odd H/W stride-2 (uneven parity classes)
     (2, 256, 14, 14, 512, 1, 2, 0),   # 1x1 stride-2 shortcut (empty odd classes)
     (4, 512, 4, 4, 1024, 3, 2, 1),    # EnhancedCNN layer4 first conv (split-K combine)

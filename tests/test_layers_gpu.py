@@ -129,3 +129,68 @@ def test_cnn_native_matches_cpu_fp32(name, shape):
         g, h = p.grad.float().cpu().flatten(), q.grad.flatten()
         cos = torch.nn.functional.cosine_similarity(g, h, dim=0).item()
         assert cos > 0.98, (n, cos)
+
+
+@pytest.mark.parametrize("name,shape,opt_name", [("lenet5", (256, 1, 28, 28), "sgd"),
+                                                 ("enhanced_cnn_small", (32, 3, 32, 32), "adam")])
+def test_graphed_step_matches_eager(name, shape, opt_name):
+    """A training step replayed from one hipGraph (train.graphed.GraphedStep) gives the
+    same parameters as the same steps run eagerly, including an lr change between
+    replays (the graph reads lr from the optimizer's device tensor)."""
+    from ldnn.optim import SGD, Adam
+    from ldnn.train.graphed import GraphedStep
+
+    torch.manual_seed(0)
+    m1, m2 = build_model(name), build_model(name)
+    xavier_init(m1)
+    m2.load_state_dict(m1.state_dict())
+    ldnn.prepare(m1, "cuda")
+    ldnn.prepare(m2, "cuda")
+    mk = (lambda p: SGD(p, lr=0.05, momentum=0.9)) if opt_name == "sgd" else (lambda p: Adam(p, lr=1e-3))
+    o1, o2 = mk(m1.parameters()), mk(m2.parameters())
+    crit = CrossEntropyLoss()
+    g = torch.Generator(device="cuda").manual_seed(1)
+    xs = [torch.randn(*shape, device="cuda", generator=g).bfloat16() for _ in range(5)]
+    ys = [torch.randint(0, 10, (shape[0],), device="cuda", generator=g) for _ in range(5)]
+    # one eager step each first (optimizer state exists), then capture without extra steps
+    for m, o in ((m1, o1), (m2, o2)):
+        o.zero_grad()
+        crit(m(xs[0]), ys[0]).backward()
+        o.step()
+    gs = GraphedStep(m1, crit, o1, xs[1], ys[1], warmup=0)
+    for i in range(1, 5):
+        if i == 3:
+            for o in (o1, o2):
+                o.param_groups[0]["lr"] *= 0.1
+        gs(xs[i], ys[i])
+        o2.zero_grad()
+        crit(m2(xs[i]), ys[i]).backward()
+        o2.step()
+    torch.cuda.synchronize()
+    for (n, p), (_, q) in zip(m1.named_parameters(), m2.named_parameters()):
+        torch.testing.assert_close(p.detach(), q.detach(), rtol=1e-3, atol=1e-4, msg=n)
+    for (n, b), (_, c) in zip(m1.named_buffers(), m2.named_buffers()):
+        torch.testing.assert_close(b, c, rtol=1e-3, atol=1e-4, msg=n)
+
+
+def test_train_global_with_graphs_matches_eager():
+    from ldnn.data.loader import get_loaders
+    from ldnn.optim import SGD, StepLR
+    from ldnn.train.trainer import train_global
+
+    res = []
+    for graphs in (False, True):
+        torch.manual_seed(0)
+        m = build_model("lenet5")
+        xavier_init(m)
+        ldnn.prepare(m, "cuda")
+        tr, va, te, trs, vas, ti, vi = get_loaders(128, 1, 0, m, "cuda", dataset="mnist", n_train=1500, n_test=100,
+                                                   dtype=torch.bfloat16)
+        opt = SGD(m.parameters(), lr=0.02, momentum=0.9)
+        H = train_global(m, tr, va, trs, vas, ti, vi, CrossEntropyLoss(), opt, StepLR(opt, 2), "cuda", 0, 1, 3, 2,
+                         60.0, 128, 0.5, 0.5, progress=False, verbose=False, repartition=False, graphs=graphs)
+        res.append((H, [p.detach().clone() for p in m.parameters()]))
+    (h0, p0), (h1, p1) = res
+    for a, b in zip(p0, p1):
+        torch.testing.assert_close(a, b, rtol=1e-3, atol=1e-4)
+    assert abs(h0[4][-1] - h1[4][-1]) < 1e-3 and abs(h0[5][-1] - h1[5][-1]) < 1e-6
