@@ -477,7 +477,7 @@ void bn_fwd(const at::Tensor& x, const at::Tensor& y, const c10::optional<at::Te
             const c10::optional<at::Tensor>& gamma, const c10::optional<at::Tensor>& beta,
             const c10::optional<at::Tensor>& running_mean, const c10::optional<at::Tensor>& running_var,
             const at::Tensor& save_mean, const at::Tensor& save_invstd, const at::Tensor& ws, double eps,
-            double momentum, bool training, bool relu) {
+            double momentum, bool training, bool relu, const c10::optional<at::Tensor>& num_batches) {
   check_dev(x, at::kBFloat16, "x");
   check_dev(y, at::kBFloat16, "y");
   TORCH_CHECK(x.dim() == 2 && x.is_contiguous() && y.sizes() == x.sizes() && y.is_contiguous(), "bn: [M][C] dense");
@@ -505,6 +505,10 @@ void bn_fwd(const at::Tensor& x, const at::Tensor& y, const c10::optional<at::Te
   a.training = training ? 1 : 0;
   a.relu = relu ? 1 : 0;
   TORCH_CHECK(training || (a.running_mean && a.running_var), "bn: eval mode needs running statistics");
+  if (num_batches.has_value() && training) {
+    check_dev(*num_batches, at::kLong, "num_batches");
+    a.num_batches = num_batches->data_ptr<int64_t>();
+  }
   check(ldnn::bn_forward(a, cur_stream(x)), "bn_forward");
 }
 
@@ -655,7 +659,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("head_wgrad_splits", &ldnn::head_wgrad_splits, py::arg("B"), py::arg("K"));
   m.def("bn_fwd", &bn_fwd, py::arg("x"), py::arg("y"), py::arg("residual"), py::arg("gamma"), py::arg("beta"),
         py::arg("running_mean"), py::arg("running_var"), py::arg("save_mean"), py::arg("save_invstd"),
-        py::arg("ws"), py::arg("eps"), py::arg("momentum"), py::arg("training"), py::arg("relu"));
+        py::arg("ws"), py::arg("eps"), py::arg("momentum"), py::arg("training"), py::arg("relu"),
+        py::arg("num_batches") = py::none());
   m.def("bn_workspace_floats", &ldnn::bn_workspace_floats, "fp32 workspace of one BatchNorm (zero it once, keep it)",
         py::arg("C"));
   m.def("bn_bwd", &bn_bwd, py::arg("x"), py::arg("y"), py::arg("dy"), py::arg("dx"), py::arg("dres"),

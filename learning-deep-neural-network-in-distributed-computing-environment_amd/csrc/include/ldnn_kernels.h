@@ -102,6 +102,7 @@ struct BnArgs {
   int M, C;
   float eps, momentum;
   int training, relu;
+  int64_t* num_batches;       // optional BatchNorm2d.num_batches_tracked, += 1 per training forward
 };
 int bn_workspace_floats(int C);
 hipError_t bn_forward(const BnArgs& a, hipStream_t s);

@@ -7,8 +7,11 @@
 // [M = N*H*W][C] matrix (geometry at bn_reduce_kernel).  Statistics are fp32
 // throughout; the normalise / affine / residual / ReLU pass and the backward
 // dx = A g + B x + D pass are single vectorised sweeps in which every thread
-// owns a fixed group of 8 channels.  Launches per BN: forward 3 (reduce,
-// finalize, apply), backward 3 (reduce, finalize with dgamma/dbeta, apply).
+// owns a fixed group of 8 channels.  Launches per BN: forward 2 (reduce with
+// the finalize fused into its last block, apply), backward 2 (reduce + fused
+// coefficients / dgamma / dbeta, apply).  Backward coefficients:
+// dx = A g + B x + D, A = gamma*invstd, B = -gamma*invstd^2 * sum(g xhat)/M,
+// D = -gamma*invstd*sum(g)/M - B*mean.
 #include <algorithm>
 
 #include "ldnn_common.h"
@@ -80,11 +83,76 @@ __device__ __forceinline__ void red_row(const bf16_t* __restrict__ x, const bf16
   }
 }
 
+// What the last reduce block to finish does with the totals (fused finalize).
+struct BnFin {
+  float* acc;                 // [2C] accumulators (left zeroed for the next call)
+  int* ticket;                // arrival counter (left zero)
+  const float* gamma;
+  const float* beta;
+  float* running_mean;
+  float* running_var;
+  float* save_mean;           // fwd: written; bwd: read
+  float* save_invstd;
+  float* coef;                // fwd: scale | shift ; bwd: A | B | D
+  float* dgamma;              // bwd: accumulated
+  float* dbeta;
+  int64_t* num_batches;       // fwd: += 1 (BatchNorm2d.num_batches_tracked), nullable
+  float eps, momentum;
+};
+
+// Totals of every block are complete in `acc` when the last block draws its
+// ticket: the fp32 atomics execute at the memory side and every block waits
+// for its own (vmcnt) before adding to the ticket; the finalizer reads AND
+// clears the totals with atomic exchanges (memory-side too, so no cache can
+// hand it a stale line).
+template <bool BWD>
+__device__ __forceinline__ void bn_finalize_last(const BnFin& f, int M, int C) {
+  __shared__ int last;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int nblk = gridDim.x * gridDim.y;
+    const int t = __hip_atomic_fetch_add(f.ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = t == nblk - 1;
+    if (last) __hip_atomic_store(f.ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (!last) return;
+  const float invM = 1.f / (float)M;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    const float S0 = atomicExch(f.acc + c, 0.f), S1 = atomicExch(f.acc + C + c, 0.f);
+    const float gm = f.gamma ? f.gamma[c] : 1.f;
+    if constexpr (!BWD) {
+      const float m = S0 * invM;
+      const float var = fmaxf(S1 * invM - m * m, 0.f);
+      const float is = rsqrtf(var + f.eps);
+      f.save_mean[c] = m;
+      f.save_invstd[c] = is;
+      const float b = f.beta ? f.beta[c] : 0.f;
+      f.coef[c] = gm * is;
+      f.coef[C + c] = b - m * gm * is;
+      if (f.running_mean) {
+        f.running_mean[c] = (1.f - f.momentum) * f.running_mean[c] + f.momentum * m;
+        const float unb = M > 1 ? var * (float)M / (float)(M - 1) : var;
+        f.running_var[c] = (1.f - f.momentum) * f.running_var[c] + f.momentum * unb;
+      }
+    } else {
+      const float is = f.save_invstd[c];
+      const float A = gm * is, B = -gm * is * is * S1 * invM;
+      f.coef[c] = A;
+      f.coef[C + c] = B;
+      f.coef[2 * C + c] = -gm * is * S0 * invM - B * f.save_mean[c];
+      if (f.dgamma) f.dgamma[c] += S1;
+      if (f.dbeta) f.dbeta[c] += S0;
+    }
+  }
+  if (!BWD && threadIdx.x == 0 && f.num_batches) f.num_batches[0] += 1;
+}
+
 template <bool BWD, bool RELU>
 __global__ __launch_bounds__(256) void bn_reduce_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
                                                         const bf16_t* __restrict__ y, const float* __restrict__ mean,
                                                         const float* __restrict__ invstd, float* __restrict__ acc,
-                                                        int M, int C, int rpb, int lanes, int rl) {
+                                                        int M, int C, int rpb, int lanes, int rl, BnFin fin) {
   __shared__ float red[2][256 * 8];
   const int tid = threadIdx.x, lane = tid % lanes, rlane = tid / lanes;
   const int cv0 = blockIdx.x * 256 + lane;
@@ -135,32 +203,8 @@ __global__ __launch_bounds__(256) void bn_reduce_kernel(const bf16_t* __restrict
       atomicAdd(acc + C + c, t1);
     }
   }
-}
-
-// mean / invstd / scale / shift (+ running-stat EMA, PyTorch semantics: unbiased
-// var); consumes the forward accumulator and clears it for the next call
-__global__ void bn_finalize_kernel(float* __restrict__ acc, const float* __restrict__ gamma,
-                                   const float* __restrict__ beta, float* __restrict__ running_mean,
-                                   float* __restrict__ running_var, float* __restrict__ save_mean,
-                                   float* __restrict__ save_invstd, float* __restrict__ scale,
-                                   float* __restrict__ shift, int M, int C, float eps, float momentum) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  const float m = acc[c] / (float)M;
-  const float var = fmaxf(acc[C + c] / (float)M - m * m, 0.f);
-  acc[c] = 0.f;
-  acc[C + c] = 0.f;
-  const float is = rsqrtf(var + eps);
-  save_mean[c] = m;
-  save_invstd[c] = is;
-  const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
-  scale[c] = g * is;
-  shift[c] = b - m * g * is;
-  if (running_mean) {
-    running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * m;
-    const float unb = M > 1 ? var * (float)M / (float)(M - 1) : var;
-    running_var[c] = (1.f - momentum) * running_var[c] + momentum * unb;
-  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's atomics have completed
+  bn_finalize_last<BWD>(fin, M, C);
 }
 
 __global__ void bn_eval_coeff_kernel(const float* __restrict__ gamma, const float* __restrict__ beta,
@@ -172,27 +216,6 @@ __global__ void bn_eval_coeff_kernel(const float* __restrict__ gamma, const floa
   const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
   scale[c] = g * is;
   shift[c] = b - rm[c] * g * is;
-}
-
-// backward coefficients: dx = A g + B x + D  (A = gamma*invstd,
-// B = -gamma*invstd^2 * S1/M, D = -gamma*invstd*S0/M - B*mean); dgamma += S1,
-// dbeta += S0 straight into the flat gradient buffer; clears the accumulator
-__global__ void bn_bwd_finalize_kernel(float* __restrict__ acc, const float* __restrict__ gamma,
-                                       const float* __restrict__ mean, const float* __restrict__ invstd,
-                                       float* __restrict__ coef, float* __restrict__ dgamma,
-                                       float* __restrict__ dbeta, int M, int C) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  const float S0 = acc[c], S1 = acc[C + c];
-  acc[c] = 0.f;
-  acc[C + c] = 0.f;
-  const float gm = gamma ? gamma[c] : 1.f, is = invstd[c], invM = 1.f / (float)M;
-  const float A = gm * is, B = -gm * is * is * S1 * invM;
-  coef[c] = A;
-  coef[C + c] = B;
-  coef[2 * C + c] = -gm * is * S0 * invM - B * mean[c];
-  if (dgamma) dgamma[c] += S1;
-  if (dbeta) dbeta[c] += S0;
 }
 
 __device__ __forceinline__ void load8(const float* p, float (&v)[8]) {
@@ -406,9 +429,10 @@ __global__ void gap_bwd_kernel(const bf16_t* __restrict__ dy, bf16_t* __restrict
 
 // Workspace (fp32, zeroed once, kept by the caller -- e.g. per BatchNorm module):
 //   [0, C) scale | [C, 2C) shift | [2C, 4C) forward accumulator | [4C, 6C)
-//   backward accumulator | [6C, 9C) backward coefficients A, B, D.
-// Both accumulators are cleared by the kernel that consumes them.
-int bn_workspace_floats(int C) { return 10 * C; }
+//   backward accumulator | [6C, 9C) backward coefficients A, B, D | [10C]
+//   forward ticket | [10C + 16] backward ticket.
+// Accumulators and tickets are left zero by the reduce kernel's last block.
+int bn_workspace_floats(int C) { return 10 * C + 32; }
 
 hipError_t bn_forward(const BnArgs& a, hipStream_t s) {
   const int M = a.M, C = a.C;
@@ -417,12 +441,21 @@ hipError_t bn_forward(const BnArgs& a, hipStream_t s) {
   const RedGeo g = red_geo(M, C);
   const dim3 grid(g.gx, g.gy);
   if (a.training) {
-    float* acc = a.ws + 2 * C;
-    bn_reduce_kernel<false, false><<<grid, 256, 0, s>>>(a.x, nullptr, nullptr, nullptr, nullptr, acc, M, C, g.rpb,
-                                                        g.lanes, g.rl);
-    bn_finalize_kernel<<<(C + 255) / 256, 256, 0, s>>>(acc, a.gamma, a.beta, a.running_mean, a.running_var,
-                                                       a.save_mean, a.save_invstd, a.ws, a.ws + C, M, C, a.eps,
-                                                       a.momentum);
+    BnFin f{};
+    f.acc = a.ws + 2 * C;
+    f.ticket = reinterpret_cast<int*>(a.ws + 10 * C);
+    f.gamma = a.gamma;
+    f.beta = a.beta;
+    f.running_mean = a.running_mean;
+    f.running_var = a.running_var;
+    f.save_mean = a.save_mean;
+    f.save_invstd = a.save_invstd;
+    f.coef = a.ws;
+    f.num_batches = a.num_batches;
+    f.eps = a.eps;
+    f.momentum = a.momentum;
+    bn_reduce_kernel<false, false><<<grid, 256, 0, s>>>(a.x, nullptr, nullptr, nullptr, nullptr, f.acc, M, C, g.rpb,
+                                                        g.lanes, g.rl, f);
   } else {
     bn_eval_coeff_kernel<<<(C + 255) / 256, 256, 0, s>>>(a.gamma, a.beta, a.running_mean, a.running_var, a.ws,
                                                          a.ws + C, C, a.eps);
@@ -449,20 +482,25 @@ hipError_t bn_backward(const BnArgs& a, const uint16_t* dy, uint16_t* dx, uint16
   if (M <= 0) return hipSuccess;
   const RedGeo g = red_geo(M, C);
   const dim3 grid(g.gx, g.gy);
-  float* acc = a.ws + 4 * C;
-  float* coef = a.ws + 6 * C;
+  BnFin f{};
+  f.acc = a.ws + 4 * C;
+  f.ticket = reinterpret_cast<int*>(a.ws + 10 * C + 16);
+  f.gamma = a.gamma;
+  f.save_mean = a.save_mean;
+  f.save_invstd = a.save_invstd;
+  f.coef = a.ws + 6 * C;
+  f.dgamma = dgamma;
+  f.dbeta = dbeta;
   if (a.relu)
-    bn_reduce_kernel<true, true><<<grid, 256, 0, s>>>(a.x, dy, a.y, a.save_mean, a.save_invstd, acc, M, C, g.rpb,
-                                                      g.lanes, g.rl);
+    bn_reduce_kernel<true, true><<<grid, 256, 0, s>>>(a.x, dy, a.y, a.save_mean, a.save_invstd, f.acc, M, C, g.rpb,
+                                                      g.lanes, g.rl, f);
   else
-    bn_reduce_kernel<true, false><<<grid, 256, 0, s>>>(a.x, dy, nullptr, a.save_mean, a.save_invstd, acc, M, C,
-                                                       g.rpb, g.lanes, g.rl);
-  bn_bwd_finalize_kernel<<<(C + 255) / 256, 256, 0, s>>>(acc, a.gamma, a.save_mean, a.save_invstd, coef, dgamma,
-                                                         dbeta, M, C);
+    bn_reduce_kernel<true, false><<<grid, 256, 0, s>>>(a.x, dy, nullptr, a.save_mean, a.save_invstd, f.acc, M, C,
+                                                       g.rpb, g.lanes, g.rl, f);
   if (a.relu)
-    bn_bwd_apply_kernel<true><<<grid, 256, 0, s>>>(a.x, dy, a.y, coef, dx, dres, M, C, g.rpb, g.lanes, g.rl);
+    bn_bwd_apply_kernel<true><<<grid, 256, 0, s>>>(a.x, dy, a.y, f.coef, dx, dres, M, C, g.rpb, g.lanes, g.rl);
   else
-    bn_bwd_apply_kernel<false><<<grid, 256, 0, s>>>(a.x, dy, nullptr, coef, dx, dres, M, C, g.rpb, g.lanes, g.rl);
+    bn_bwd_apply_kernel<false><<<grid, 256, 0, s>>>(a.x, dy, nullptr, f.coef, dx, dres, M, C, g.rpb, g.lanes, g.rl);
   return hipGetLastError();
 }
 

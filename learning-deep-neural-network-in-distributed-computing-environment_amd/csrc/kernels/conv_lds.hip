@@ -76,6 +76,7 @@ struct LArgs {
   int classes;       // 4 = stride-2 dgrad parity classes (grid.z), else 1
   int tiles_x;       // gridDim.x
   int dn, dp, dq;    // wgrad: 64 = dn*PQ + dp*Q + dq
+  int taps_per_tile; // fwd with C < 64: 64 / C
   FastDiv f_pq, f_q, f_c, f_s;
   float* ws;         // split-K: combine slabs (with cnt) or wgrad partial slabs [split][M][N] (without)
   int* cnt;          // split-K arrival counters of the in-launch combine
@@ -182,10 +183,42 @@ struct FwdA {  // x gathered: row = output pixel npq, k = (r, s, c), C % 64 == 0
 };
 
 template <int ROWS, int PPW, int NW>
+struct FwdASmallC {  // x gathered for C in {8, 16, 32}: a 64-deep K-tile spans 64/C filter taps
+  static constexpr bool KC = true;
+  static constexpr int kRows = ROWS, kPieces = PPW;
+  int base[PPW], ih0[PPW], iw0[PPW], tl[PPW], cc[PPW];
+  __device__ void init(const LArgs& a, const Geo&, int r0, int wid, int lane, int) {
+    const ConvShape& s = a.s;
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      int row, k;
+      lds_slot_to_rk<true, ROWS>((i * NW + wid) * 1024 + lane * 16, row, k);
+      const int m = r0 + row;
+      const int q = m % s.Q, t = m / s.Q, p = t % s.P, n = t / s.P;
+      ih0[i] = p * s.stride - s.pad;
+      iw0[i] = q * s.stride - s.pad;
+      base[i] = (int)((unsigned)((n * s.H + ih0[i]) * s.W + iw0[i]) * (unsigned)s.C);
+      if (m >= a.M) ih0[i] = -(1 << 20);  // never inside the image
+      tl[i] = k / s.C;                    // tap within the K-tile
+      cc[i] = k % s.C;                    // channel offset within the tap
+    }
+  }
+  __device__ __forceinline__ uint32_t off(const LArgs& a, int i, const KS& ks) const {
+    const int tap = ks.kt * a.taps_per_tile + tl[i];
+    const int r = fdiv(tap, a.f_s), sx = tap - r * a.s.S;
+    const int ih = ih0[i] + r, iw = iw0[i] + sx;
+    const bool ok = tap < a.s.R * a.s.S && (unsigned)ih < (unsigned)a.s.H && (unsigned)iw < (unsigned)a.s.W;
+    const unsigned e = (unsigned)base[i] + (unsigned)((r * a.s.W + sx) * a.s.C + cc[i]);
+    return ok ? e * 2u : kOOB;
+  }
+  __device__ __forceinline__ void advance(const LArgs&) {}
+};
+
+template <int ROWS, int PPW, int NW>
 struct WeightKC {  // w as a [K][RSC] k-contiguous matrix (fwd B operand)
   static constexpr bool KC = true;
   static constexpr int kRows = ROWS, kPieces = PPW;
-  int base[PPW];
+  int base[PPW], kl[PPW];
   __device__ void init(const LArgs& a, const Geo&, int r0, int wid, int lane, int) {
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
@@ -193,10 +226,12 @@ struct WeightKC {  // w as a [K][RSC] k-contiguous matrix (fwd B operand)
       lds_slot_to_rk<true, ROWS>((i * NW + wid) * 1024 + lane * 16, row, k);
       const int n = r0 + row;
       base[i] = n < a.N ? n * a.rsc + k : -1;
+      kl[i] = k;
     }
   }
-  __device__ __forceinline__ uint32_t off(const LArgs&, int i, const KS& ks) const {
-    return base[i] >= 0 ? (uint32_t)(base[i] + ks.kt * 64) * 2u : kOOB;
+  __device__ __forceinline__ uint32_t off(const LArgs& a, int i, const KS& ks) const {
+    const bool ok = base[i] >= 0 && ks.kt * 64 + kl[i] < a.rsc;  // RSC % 64 != 0 for small C
+    return ok ? (uint32_t)(base[i] + ks.kt * 64) * 2u : kOOB;
   }
   __device__ __forceinline__ void advance(const LArgs&) {}
 };
@@ -497,12 +532,30 @@ __global__ __launch_bounds__(256, 2) void conv_lds_kernel(LArgs a, const bf16_t*
 }
 
 // out[i] = sum_s ws[s][i] (+ beta * out[i]): the cross-CU reduction of wgrad slabs.
+// A block is 32 float4 columns x 8 split lanes (each lane sums every 8th slab,
+// 4 loads in flight), reduced through LDS: enough blocks to cover the chip even
+// for a 64 x 576 weight, and a fixed summation order (deterministic).
 __global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__ ws, float* __restrict__ out,
                                                        int64_t n4, int splits, float beta) {
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += stride) {
-    floatx4 v = reinterpret_cast<const floatx4*>(ws)[i];
-    for (int sp = 1; sp < splits; ++sp) v += reinterpret_cast<const floatx4*>(ws)[(int64_t)sp * n4 + i];
+  __shared__ floatx4 part[8][32];
+  const int col = threadIdx.x & 31, sl = threadIdx.x >> 5;
+  const int64_t i = (int64_t)blockIdx.x * 32 + col;
+  floatx4 v = {0.f, 0.f, 0.f, 0.f};
+  if (i < n4) {
+    const floatx4* w = reinterpret_cast<const floatx4*>(ws) + i;
+    int sp = sl;
+    for (; sp + 24 < splits; sp += 32) {
+      const floatx4 a = w[(int64_t)sp * n4], b = w[(int64_t)(sp + 8) * n4];
+      const floatx4 c = w[(int64_t)(sp + 16) * n4], d = w[(int64_t)(sp + 24) * n4];
+      v += (a + b) + (c + d);
+    }
+    for (; sp < splits; sp += 8) v += w[(int64_t)sp * n4];
+  }
+  part[sl][col] = v;
+  __syncthreads();
+  if (sl == 0 && i < n4) {
+#pragma unroll
+    for (int q = 1; q < 8; ++q) v += part[q][col];
     if (beta != 0.f) v += beta * reinterpret_cast<const floatx4*>(out)[i];
     reinterpret_cast<floatx4*>(out)[i] = v;
   }
@@ -650,9 +703,35 @@ ConvWorkspace conv2d_lds_workspace(const ConvShape& s, int op) {
 
 // Each returns hipErrorNotSupported when the shape is outside the fast path
 // (conv.hip then runs its generic register-staged kernel).
+// Stems and other small-C convolutions (C in {8, 16, 32}, e.g. the 7x7 ResNet stem
+// on 3 -> 8 padded channels): K-tiles span several taps, one 256x64 / 128x128 tile.
+hipError_t conv2d_fwd_lds_small_c(const ConvShape& s, const uint16_t* x, const uint16_t* w, uint16_t* y,
+                                  const float* bias, int epi, hipStream_t st) {
+  LArgs a = base_args(s);
+  a.out = y;
+  a.bias = bias;
+  a.M = s.N * s.P * s.Q;
+  a.N = s.K;
+  a.nb = 0;
+  a.taps_per_tile = 64 / s.C;
+  a.f_s = make_fastdiv(s.S);
+  a.nk_all = (a.rsc + 63) / 64;
+  a.nk_split = a.nk_all;
+  const bool narrow = s.K <= 64;
+  a.tiles_x = ((a.M + (narrow ? 255 : 127)) / (narrow ? 256 : 128)) * ((s.K + (narrow ? 63 : 127)) / (narrow ? 64 : 128));
+  const size_t bx = (size_t)s.N * s.H * s.W * s.C * 2, bw = (size_t)s.K * a.rsc * 2;
+  if (narrow) return launch<4, 1, FwdASmallC<256, 8, 4>, WeightKC<64, 2, 4>, false, false>(a, epi, 1, x, bx, w, bw, st);
+  return launch<2, 2, FwdASmallC<128, 4, 4>, WeightKC<128, 4, 4>, false, false>(a, epi, 1, x, bx, w, bw, st);
+}
+
 hipError_t conv2d_fwd_lds(const ConvShape& s, const uint16_t* x, const uint16_t* w, uint16_t* y, const float* bias,
                           int epi, hipStream_t st, float* ws, int* cnt) {
-  if (s.C % 64 != 0 || !shape_ok(s)) return hipErrorNotSupported;
+  if (!shape_ok(s)) return hipErrorNotSupported;
+  if (s.C == 8 || s.C == 16 || s.C == 32) {
+    if (s.N * s.P * s.Q <= 0) return hipSuccess;
+    return conv2d_fwd_lds_small_c(s, x, w, y, bias, epi, st);
+  }
+  if (s.C % 64 != 0) return hipErrorNotSupported;
   if (s.N * s.P * s.Q <= 0) return hipSuccess;
   Plan pl = plan_fwd(s);
   LArgs a = base_args(s);
@@ -742,8 +821,7 @@ hipError_t conv2d_wgrad_lds(const ConvShape& s, const uint16_t* dy, const uint16
     e = launch<2, 2, WgradA<128, 4, 4>, WgradB<128, 4, 4>, true, false>(a, EPI_NONE, splits, dy, bdy, x, bx, st);
   if (e != hipSuccess || splits == 1 || ws == nullptr) return e;
   const int64_t n4 = (int64_t)a.M * a.N / 4;
-  const int grid = (int)std::min<int64_t>(2048, (n4 + 255) / 256);
-  slab_sum_kernel<<<grid, 256, 0, st>>>(ws, dw, n4, splits, beta);
+  slab_sum_kernel<<<(unsigned)((n4 + 31) / 32), 256, 0, st>>>(ws, dw, n4, splits, beta);
   return hipGetLastError();
 }
 

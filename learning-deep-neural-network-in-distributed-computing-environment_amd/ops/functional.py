@@ -331,8 +331,12 @@ class _BatchNormNative(torch.autograd.Function):
         beta = flat.master_storage(bias)[:C] if bias is not None else None
         training = mod.training or not mod.track_running_stats
         mom = mod.momentum
+        nbt = None
         if mod.training and mod.track_running_stats:
-            mod.num_batches_tracked.add_(1)
+            # num_batches_tracked += 1 happens inside the fused BN statistics kernel
+            nbt = mod.num_batches_tracked if mod.num_batches_tracked.is_cuda else None
+            if nbt is None:
+                mod.num_batches_tracked.add_(1)
             mod._ldnn_nbt = getattr(mod, "_ldnn_nbt", 0) + 1
             if mom is None:
                 mom = 1.0 / mod._ldnn_nbt
@@ -340,7 +344,7 @@ class _BatchNormNative(torch.autograd.Function):
         rv = mod.running_var if mod.track_running_stats else None
         C_.bn_fwd(x2, y.view(-1, C), r2, gamma, beta, rm if (training and mod.training) or not training else None,
                   rv if (training and mod.training) or not training else None, smean, sinv, ws, mod.eps,
-                  mom or 0.0, training, relu)
+                  mom or 0.0, training, relu, nbt)
         ctx.save_for_backward(x2, y, smean, sinv)
         ctx.meta = (flat, weight, bias, relu, residual is not None, ws, (N, C, H, W), x.dtype)
         return nchw_view(y, C)

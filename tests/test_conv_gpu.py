@@ -80,7 +80,9 @@ def test_conv_fwd_dgrad_wgrad(N, C, H, W, K, R, st, pad):
 
 
 @pytest.mark.parametrize("N,C,H,W,K,R,st,pad", [(2, 64, 17, 17, 128, 3, 2, 1), (4, 512, 4, 4, 1024, 3, 2, 1),
-                                                (2, 128, 16, 16, 64, 3, 1, 1), (4, 1024, 2, 2, 1024, 3, 1, 1)])
+                                                (2, 128, 16, 16, 64, 3, 1, 1), (4, 1024, 2, 2, 1024, 3, 1, 1),
+                                                (2, 8, 40, 40, 64, 7, 2, 3), (3, 16, 9, 9, 32, 3, 1, 1),
+                                                (2, 32, 12, 12, 128, 5, 1, 2)])
 def test_lds_fast_path_matches_generic_kernel(N, C, H, W, K, R, st, pad):
     """The LDS-DMA kernels (set_conv_impl(0)) agree with the generic register-staged
     kernels (set_conv_impl(1)) on every output, and repeated launches of the
