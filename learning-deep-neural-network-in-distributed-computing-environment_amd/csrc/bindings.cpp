@@ -125,6 +125,88 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, bool a_
   check(ldnn::gemm_bf16_tile(p, a_kcontig, b_kcontig, (int)epi, out_f32, (int)tile, cur_stream(a)), "gemm");
 }
 
+// Weight-gradient GEMM whose epilogue applies SGD / Adam to `master` (fp32
+// [M][N] storage, the layout of the gradient it replaces) and refreshes the bf16
+// shadow: the gradient never goes to HBM.  kind: "sgd" | "adam" | "adamw".
+void gemm_opt(const at::Tensor& a, const at::Tensor& b, const at::Tensor& master, bool a_kcontig, bool b_kcontig,
+              const std::string& kind, const c10::optional<at::Tensor>& m, const c10::optional<at::Tensor>& v,
+              const c10::optional<at::Tensor>& shadow, const at::Tensor& hp, double grad_scale, double momentum,
+              double dampening, double weight_decay, bool nesterov, double beta1, double beta2, double eps,
+              int64_t tile, int64_t splitk, const c10::optional<at::Tensor>& ws,
+              const c10::optional<at::Tensor>& cnt) {
+  check_dev(a, at::kBFloat16, "a");
+  check_dev(b, at::kBFloat16, "b");
+  check_dev(master, at::kFloat, "master");
+  check_dev(hp, at::kFloat, "hp");
+  const int64_t lda = ld_of(a, "a"), ldb = ld_of(b, "b"), ldc = ld_of(master, "master");
+  const int64_t M = a_kcontig ? a.size(0) : a.size(1);
+  const int64_t K = a_kcontig ? a.size(1) : a.size(0);
+  const int64_t N = b_kcontig ? b.size(0) : b.size(1);
+  TORCH_CHECK((b_kcontig ? b.size(1) : b.size(0)) == K, "gemm_opt: inner dims differ");
+  TORCH_CHECK(master.size(0) == M && master.size(1) == N, "gemm_opt: master shape mismatch");
+  TORCH_CHECK(lda % 8 == 0 && ldb % 8 == 0 && ldc % 4 == 0 && N % 8 == 0, "gemm_opt: leading dims");
+  TORCH_CHECK(a_kcontig || M % 8 == 0, "gemm_opt: M must be a multiple of 8 for a k-strided A");
+  auto same = [&](const c10::optional<at::Tensor>& t, const char* name) -> float* {
+    if (!t.has_value()) return nullptr;
+    check_dev(*t, at::kFloat, name);
+    TORCH_CHECK(t->sizes() == master.sizes() && t->strides() == master.strides(), "gemm_opt: ", name, " layout");
+    return t->data_ptr<float>();
+  };
+  ldnn::GemmParams p{};
+  p.A = bf16_ptr(a);
+  p.B = bf16_ptr(b);
+  p.C = master.data_ptr();
+  p.M = (int)M;
+  p.N = (int)N;
+  p.K = (int)K;
+  p.lda = (int)lda;
+  p.ldb = (int)ldb;
+  p.ldc = (int)ldc;
+  p.opt.master = master.data_ptr<float>();
+  p.opt.m = same(m, "m");
+  p.opt.v = same(v, "v");
+  if (shadow.has_value()) {
+    check_dev(*shadow, at::kBFloat16, "shadow");
+    TORCH_CHECK(shadow->sizes() == master.sizes() && shadow->strides() == master.strides(), "gemm_opt: shadow layout");
+    p.opt.shadow = bf16_mut(*shadow);
+  }
+  p.opt.hp = hp.data_ptr<float>();
+  p.opt.grad_scale = (float)grad_scale;
+  p.opt.momentum = (float)momentum;
+  p.opt.dampening = (float)dampening;
+  p.opt.weight_decay = (float)weight_decay;
+  p.opt.nesterov = nesterov ? 1 : 0;
+  p.opt.beta1 = (float)beta1;
+  p.opt.beta2 = (float)beta2;
+  p.opt.eps = (float)eps;
+  int epi;
+  if (kind == "sgd") {
+    epi = ldnn::EPI_OPT_SGD;
+    TORCH_CHECK(momentum == 0.0 || p.opt.m, "gemm_opt: SGD momentum needs its buffer");
+  } else if (kind == "adam" || kind == "adamw") {
+    epi = ldnn::EPI_OPT_ADAM;
+    p.opt.decoupled = kind == "adamw" ? 1 : 0;
+    TORCH_CHECK(p.opt.m && p.opt.v, "gemm_opt: Adam needs exp_avg and exp_avg_sq");
+  } else {
+    TORCH_CHECK(false, "gemm_opt: unknown optimizer ", kind);
+  }
+  TORCH_CHECK(aligned16(a.data_ptr()) && aligned16(b.data_ptr()) && aligned16(master.data_ptr()), "gemm_opt: alignment");
+  if (tile == 0) tile = ldnn::gemm_pick_tile(p.M, p.N, p.K, true);
+  if (splitk > 1) {
+    TORCH_CHECK(tile == 128 && ws.has_value() && cnt.has_value(), "gemm_opt: split-K needs the in-launch combine");
+    check_dev(*ws, at::kFloat, "ws");
+    check_dev(*cnt, at::kInt, "cnt");
+    TORCH_CHECK((size_t)ws->numel() * 4 >= ldnn::gemm_splitk_ws_bytes(p.M, p.N, (int)splitk) &&
+                    cnt->numel() >= ldnn::gemm_tiles128(p.M, p.N),
+                "gemm_opt: split-K workspace too small");
+    p.splitk = (int)splitk;
+    p.ws = ws->data_ptr<float>();
+    p.cnt = cnt->data_ptr<int>();
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA g(a.device());
+  check(ldnn::gemm_bf16_tile(p, a_kcontig, b_kcontig, epi, true, (int)tile, cur_stream(a)), "gemm_opt");
+}
+
 void act_fwd(const at::Tensor& x, const at::Tensor& y, int64_t act) {
   check_dev(x, at::kBFloat16, "x");
   check_dev(y, at::kBFloat16, "y");
@@ -621,6 +703,13 @@ PYBIND11_MODULE(_C, m) {
   m.def("set_conv_impl", &ldnn::set_conv_impl, "0 = LDS-DMA fast path where it applies, 1 = generic kernel only",
         py::arg("impl"));
   m.def("get_conv_impl", &ldnn::get_conv_impl);
+  m.def("gemm_opt", &gemm_opt, "weight-gradient GEMM with the optimizer update fused into its epilogue",
+        py::arg("a"), py::arg("b"), py::arg("master"), py::arg("a_kcontig"), py::arg("b_kcontig"), py::arg("kind"),
+        py::arg("m") = py::none(), py::arg("v") = py::none(), py::arg("shadow") = py::none(), py::arg("hp"),
+        py::arg("grad_scale") = 1.0, py::arg("momentum") = 0.0, py::arg("dampening") = 0.0,
+        py::arg("weight_decay") = 0.0, py::arg("nesterov") = false, py::arg("beta1") = 0.9, py::arg("beta2") = 0.999,
+        py::arg("eps") = 1e-8, py::arg("tile") = 0, py::arg("splitk") = 0, py::arg("ws") = py::none(),
+        py::arg("cnt") = py::none());
   m.def("act_fwd", &act_fwd);
   m.def("act_bwd", &act_bwd);
   m.def("colsum", &colsum, py::arg("x"), py::arg("out"), py::arg("accumulate") = false);

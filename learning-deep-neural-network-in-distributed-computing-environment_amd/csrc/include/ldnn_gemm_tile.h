@@ -101,6 +101,60 @@ __device__ __forceinline__ void tile_coords(int M, int N, int BMt, int BNt, int&
   n0 = ((id % per_group) / gsize) * BNt;
 }
 
+// ---- fused optimizer update of 4 consecutive weights (EPI_OPT_*) -------------
+// Same arithmetic as optim.hip's sgd / adam kernels (torch semantics), applied
+// in the wgrad epilogue so the gradient never round-trips through HBM.
+struct OptConst {
+  float lr, bc1, bc2s;
+};
+
+template <int EPI>
+__device__ __forceinline__ OptConst opt_const(const OptEpi& o) {
+  OptConst c;
+  c.lr = o.hp[0];
+  c.bc1 = 1.f;
+  c.bc2s = 1.f;
+  if constexpr (EPI == EPI_OPT_ADAM) {
+    const float t = o.hp[1];
+    c.bc1 = 1.f - powf(o.beta1, t);
+    c.bc2s = sqrtf(1.f - powf(o.beta2, t));
+  }
+  return c;
+}
+
+template <int EPI>
+__device__ __forceinline__ void opt_update4(const OptEpi& o, const OptConst& k, size_t off, floatx4 g) {
+  floatx4 p = *reinterpret_cast<const floatx4*>(o.master + off);
+  g = g * o.grad_scale;
+  if constexpr (EPI == EPI_OPT_SGD) {
+    if (o.weight_decay != 0.f) g += o.weight_decay * p;
+    if (o.m != nullptr) {
+      floatx4 b = o.momentum * *reinterpret_cast<const floatx4*>(o.m + off) + (1.f - o.dampening) * g;
+      *reinterpret_cast<floatx4*>(o.m + off) = b;
+      g = o.nesterov ? g + o.momentum * b : b;
+    }
+    p -= k.lr * g;
+  } else {
+    floatx4 m = *reinterpret_cast<const floatx4*>(o.m + off);
+    floatx4 v = *reinterpret_cast<const floatx4*>(o.v + off);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float gr = g[r], pr = p[r];
+      if (o.weight_decay != 0.f) {
+        if (o.decoupled) pr *= (1.f - k.lr * o.weight_decay);
+        else gr += o.weight_decay * pr;
+      }
+      m[r] = o.beta1 * m[r] + (1.f - o.beta1) * gr;
+      v[r] = o.beta2 * v[r] + (1.f - o.beta2) * gr * gr;
+      p[r] = pr - (k.lr / k.bc1) * m[r] / (sqrtf(v[r]) / k.bc2s + o.eps);
+    }
+    *reinterpret_cast<floatx4*>(o.m + off) = m;
+    *reinterpret_cast<floatx4*>(o.v + off) = v;
+  }
+  *reinterpret_cast<floatx4*>(o.master + off) = p;
+  if (o.shadow) *reinterpret_cast<u16x4*>(o.shadow + off) = u16x4{f2bf(p[0]), f2bf(p[1]), f2bf(p[2]), f2bf(p[3])};
+}
+
 // ---- shared epilogue: acc[j][i] is the 16x16 tile (n-tile j, m-tile i) -----
 // Processed one n-tile at a time (sched_barrier keeps the compiler from hoisting
 // every bias/aux load of the tile up front), with the optional bias-gradient
@@ -109,6 +163,21 @@ __device__ __forceinline__ void tile_coords(int M, int N, int BMt, int BNt, int&
 template <int EPI, bool OUT_F32, int MT, int NT>
 __device__ __forceinline__ void epilogue(const GemmParams& p, floatx4 (&acc)[NT][MT], int mbase, int nbase,
                                          int lane) {
+  if constexpr (EPI == EPI_OPT_SGD || EPI == EPI_OPT_ADAM) {
+    static_assert(OUT_F32, "optimizer epilogues take the fp32 gradient");
+    const OptConst k = opt_const<EPI>(p.opt);
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const int n = nbase + j * 16 + 4 * (lane >> 4);
+      if (n >= p.N) continue;
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        const int m = mbase + i * 16 + (lane & 15);
+        if (m < p.M) opt_update4<EPI>(p.opt, k, (size_t)m * p.ldc + n, acc[j][i]);
+      }
+    }
+    return;
+  }
   const bool do_dbias = p.dbias != nullptr;
 #pragma unroll
   for (int j = 0; j < NT; ++j) {

@@ -14,6 +14,21 @@ enum Epilogue : int {
   EPI_BIAS_SIGMOID = 3,
   EPI_DRELU = 4,
   EPI_DSIGMOID = 5,
+  // fp32-output weight-gradient GEMMs only: the epilogue applies the optimizer to
+  // the weights instead of storing the gradient (GemmParams::opt)
+  EPI_OPT_SGD = 6,
+  EPI_OPT_ADAM = 7,
+};
+
+// Fused optimizer epilogue: gradient element (m, n) updates master[m*ldc + n].
+struct OptEpi {
+  float* master;          // fp32 weights (ldc row stride, like C)
+  float* m;               // SGD momentum / Adam exp_avg (nullable for momentum-free SGD)
+  float* v;               // Adam exp_avg_sq
+  uint16_t* shadow;       // bf16 copy the GEMMs read (nullable)
+  const float* hp;        // device [lr, step]
+  float grad_scale, momentum, dampening, weight_decay, beta1, beta2, eps;
+  int nesterov, decoupled;
 };
 
 struct GemmParams {
@@ -32,6 +47,7 @@ struct GemmParams {
   int variant;           // 256-tile main loop: 0/1 = 2-stage BK64 (default), 2 = 4-slot BK32 ring, 3 = 5-slot ring
   float* ws;             // split-K combine: [tiles][splitk] slabs of 64 KiB (gemm_splitk_ws_bytes)
   int* cnt;              // split-K combine: [tiles] arrival counters, zero before the first launch
+  OptEpi opt;            // EPI_OPT_*: the weights this gradient updates
 };
 // Workspace of the in-launch split-K combine of a 128-tile GEMM (bytes; counters = tiles).
 size_t gemm_splitk_ws_bytes(int M, int N, int splitk);

@@ -646,6 +646,22 @@ hipError_t dispatch_epi(const GemmParams& p, int epi, hipStream_t s) {
     LDNN_GEMM_CASE(EPI_BIAS_SIGMOID)
     LDNN_GEMM_CASE(EPI_DRELU)
     LDNN_GEMM_CASE(EPI_DSIGMOID)
+    case EPI_OPT_SGD:
+    case EPI_OPT_ADAM:
+      if constexpr (OUT_F32 && TILE == 256) {  // the big weight gradients (plain 2-stage main loop)
+        if (epi == EPI_OPT_SGD)
+          k256::gemm_kernel<A_KC, B_KC, EPI_OPT_SGD, true><<<grid, dim3(k256::kThreads), 0, s>>>(p);
+        else
+          k256::gemm_kernel<A_KC, B_KC, EPI_OPT_ADAM, true><<<grid, dim3(k256::kThreads), 0, s>>>(p);
+      } else if constexpr (OUT_F32) {
+        if (epi == EPI_OPT_SGD)
+          k128::gemm_kernel<A_KC, B_KC, EPI_OPT_SGD, true><<<grid, dim3(k128::kThreads), 0, s>>>(p);
+        else
+          k128::gemm_kernel<A_KC, B_KC, EPI_OPT_ADAM, true><<<grid, dim3(k128::kThreads), 0, s>>>(p);
+      } else {
+        return hipErrorInvalidValue;
+      }
+      break;
     default:
       return hipErrorInvalidValue;
   }

@@ -79,7 +79,8 @@ class StaticMLPEngine:
     def __init__(self, model, batch_size: int, optim: OptimConfig | None = None, *, device=None,
                  process_group=None, world_size: int | None = None, bucket_cap_elems: int = 8 << 20,
                  use_graphs: bool = True, average_grads: bool = True, use_head_kernels: bool = True,
-                 shard_optimizer: bool | None = None, overlap_optimizer: bool = False, wgrad_combine: bool = True):
+                 shard_optimizer: bool | None = None, overlap_optimizer: bool = False, wgrad_combine: bool = True,
+                 fuse_optimizer: bool | None = None):
         from ..models.mlp import MLP
 
         if not isinstance(model, MLP):
@@ -216,6 +217,17 @@ class StaticMLPEngine:
         else:
             self._opt_zero, self._fill_zero = merged[:2], merged[2:]
 
+        # Single process: the optimizer update of every big weight runs IN its wgrad
+        # GEMM's epilogue (gemm_opt): the fp32 gradient never goes to HBM and the
+        # separate optimizer pass shrinks to the head + biases.  Needs dgrad(l)
+        # before wgrad(l) (dgrad reads the old W_l) and a wgrad that is not an
+        # atomic split-K.  (Multi-rank steps must all-reduce the gradient first.)
+        if fuse_optimizer is None:
+            fuse_optimizer = not self.distributed and not overlap_optimizer
+        if overlap_optimizer:
+            fuse_optimizer = False  # the side-stream variant updates whole ranges itself
+        self._fused = [bool(fuse_optimizer) and not self.distributed and not (self.use_head and l == L - 1)
+                       and (self._wgrad_splitk[l] == 1 or self._wgrad_ws[l] is not None) for l in range(L)]
         self.rank = dist.get_rank(process_group) if self.distributed else 0
         self.overlap_optimizer = overlap_optimizer
         self.side = torch.cuda.Stream(device=self.device) if overlap_optimizer else None
@@ -255,6 +267,39 @@ class StaticMLPEngine:
             self.C.gemm(self.dz[l + 1], self.h[l], self.dW[l], False, False, beta=1.0, tile=128, splitk=sk)
         else:
             self.C.gemm(self.dz[l + 1], self.h[l], self.dW[l], False, False)
+
+    def _wgrad_opt(self, l):
+        """wgrad of layer l with the optimizer update fused into the epilogue."""
+        f, o = self.flat, self.optim
+        w = self.layers[l].weight
+        seg = f.seg(w)
+        view = lambda t: f.storage_view(seg, t)  # noqa: E731
+        m = v = None
+        if o.name == "sgd":
+            m = view(self.mom) if self.mom is not None else None
+        else:
+            m, v = view(self.exp_avg), view(self.exp_avg_sq)
+        sk = self._wgrad_splitk[l]
+        ws, cnt = self._wgrad_ws[l] if self._wgrad_ws[l] is not None else (None, None)
+        self.C.gemm_opt(self.dz[l + 1], self.h[l], view(f.master), False, False, o.name, m=m, v=v,
+                        shadow=view(f.shadow), hp=self.hp, grad_scale=self._grad_scale, momentum=o.momentum,
+                        dampening=o.dampening, weight_decay=o.weight_decay, nesterov=o.nesterov,
+                        beta1=o.betas[0], beta2=o.betas[1], eps=o.eps, tile=128 if ws is not None else 0,
+                        splitk=sk if ws is not None else 0, ws=ws, cnt=cnt)
+
+    def _unfused_ranges(self):
+        """Flat ranges the standalone optimizer launch still updates (unfused weights + biases)."""
+        f = self.flat
+        rs = [(f.seg(l.weight).offset, f.seg(l.weight).offset + f.seg(l.weight).storage_numel)
+              for i, l in enumerate(self.layers) if not self._fused[i]]
+        rs.append((self._bias_begin, f.numel))
+        merged = []
+        for b, e in sorted(rs):
+            if merged and b <= merged[-1][1]:
+                merged[-1] = (merged[-1][0], max(merged[-1][1], e))
+            else:
+                merged.append((b, e))
+        return merged
 
     def _dgrad(self, l):
         # dz_l(prev layer output) = (dz_{l+1} W_l) * act'(h_l), bias grad of layer l-1 fused
@@ -302,6 +347,11 @@ class StaticMLPEngine:
         pieces[0].append(self._loss)
         self._cut_buckets = []
         for l in reversed(range(L)):
+            if self._fused[l]:  # dgrad reads the old W_l, then the fused wgrad updates it
+                if l > 0:
+                    pieces[-1].append(lambda l=l: self._dgrad(l))
+                pieces[-1].append(lambda l=l: self._wgrad_opt(l))
+                continue
             pieces[-1].append(lambda l=l: self._wgrad(l))
             if l in triggers:
                 self._cut_buckets.append(triggers[l])
@@ -333,6 +383,9 @@ class StaticMLPEngine:
                         fns.append(fn)
                 fns.insert(len(fns) - 1, lambda: self._fork_opt(side))   # before wgrad(0)
                 fns += [lambda: self._opt(w0, self._bias_begin), self._join]
+            elif any(self._fused):
+                fns = [fn for p in pieces for fn in p] + [lambda b=b, e=e: self._opt(b, e)
+                                                          for b, e in self._unfused_ranges()]
             else:
                 fns = [fn for p in pieces for fn in p] + [lambda: self._opt(0, self.flat.numel)]
             self.segments = [_Segment(run(fns), self.use_graphs)]

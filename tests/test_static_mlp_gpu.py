@@ -145,3 +145,28 @@ def test_wgrad_inlaunch_splitk_combine_matches_unsplit():
             e.step()
     torch.cuda.synchronize()
     torch.testing.assert_close(e1.flat.master, e2.flat.master, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("opt", ["sgd", "adam"])
+def test_fused_optimizer_epilogue_matches_separate_launch(opt):
+    """Single-GPU engine with the optimizer fused into the wgrad epilogues (256-tile
+    4096 x 4096 layer, 128-tile first layer) == the engine with one separate fused
+    optimizer launch over the flat buffers."""
+    torch.manual_seed(0)
+    B = 512
+    m1, m2 = mlp3(784, 4096, 10), mlp3(784, 4096, 10)
+    m2.load_state_dict(m1.state_dict())
+    cfg = OptimConfig(opt, lr=0.05 if opt == "sgd" else 1e-3, momentum=0.9, weight_decay=1e-4)
+    e1 = StaticMLPEngine(m1, B, cfg, use_graphs=True)
+    e2 = StaticMLPEngine(m2, B, cfg, use_graphs=True, fuse_optimizer=False)
+    assert any(e1._fused) and not any(e2._fused)
+    g = torch.Generator(device="cuda").manual_seed(9)
+    for i in range(5):
+        x = torch.randn(B, 784, device="cuda", generator=g).bfloat16()
+        y = torch.randint(0, 10, (B,), device="cuda", generator=g)
+        for e in (e1, e2):
+            e.load_batch(x, y)
+            e.step()
+    torch.cuda.synchronize()
+    torch.testing.assert_close(e1.flat.master, e2.flat.master, rtol=1e-5, atol=1e-6)
+    assert torch.equal(e1.flat.shadow, e1.flat.master.bfloat16())
