@@ -217,13 +217,17 @@ class StaticMLPEngine:
         else:
             self._opt_zero, self._fill_zero = merged[:2], merged[2:]
 
-        # Single process: the optimizer update of every big weight runs IN its wgrad
-        # GEMM's epilogue (gemm_opt): the fp32 gradient never goes to HBM and the
-        # separate optimizer pass shrinks to the head + biases.  Needs dgrad(l)
-        # before wgrad(l) (dgrad reads the old W_l) and a wgrad that is not an
-        # atomic split-K.  (Multi-rank steps must all-reduce the gradient first.)
+        # fuse_optimizer (single process): the optimizer update of every big weight
+        # runs IN its wgrad GEMM's epilogue (gemm_opt): the fp32 gradient never goes
+        # to HBM and the separate optimizer pass shrinks to the head + biases.  Needs
+        # dgrad(l) before wgrad(l) (dgrad reads the old W_l) and a wgrad that is not
+        # an atomic split-K.  Off by default: measured on MI355X (mlp3 4096, batch
+        # 4096) the step is SLOWER, 0.674 vs 0.616 ms -- all 256 output tiles finish
+        # together, so the 18 B/weight read-modify-write runs as an uncovered tail
+        # with fragment-shaped (16 rows x 64 B) accesses, instead of the separate
+        # optimizer's fully coalesced stream.
         if fuse_optimizer is None:
-            fuse_optimizer = not self.distributed and not overlap_optimizer
+            fuse_optimizer = False
         if overlap_optimizer:
             fuse_optimizer = False  # the side-stream variant updates whole ranges itself
         self._fused = [bool(fuse_optimizer) and not self.distributed and not (self.use_head and l == L - 1)
