@@ -33,6 +33,7 @@
 // __syncthreads while a DMA is outstanding); 2 workgroups per CU.  LDS images
 // and fragment reads are those of gemm.hip (ldnn_gemm_tile.h).
 #include <algorithm>
+#include <cstdlib>
 
 #include "ldnn_common.h"
 #include "ldnn_gemm_tile.h"
@@ -51,6 +52,7 @@ struct FastDiv {  // n / d for 0 <= n < 2^31 as (umulhi(n, m) + n) >> s
 
 FastDiv make_fastdiv(uint32_t d) {
   FastDiv f;
+  if (d == 0) d = 1;  // an empty parity class: never divided by
   uint32_t s = 0;
   while ((1ull << s) < d) ++s;
   f.s = s;
@@ -78,6 +80,8 @@ struct LArgs {
   int dn, dp, dq;    // wgrad: 64 = dn*PQ + dp*Q + dq
   int taps_per_tile; // fwd with C < 64: 64 / C
   FastDiv f_pq, f_q, f_c, f_s;
+  FastDiv f_p, f_w, f_h;         // row decompositions: fwd (P, Q), dgrad (H, W)
+  FastDiv f_cw[2], f_ch[2];      // stride-2 dgrad class rows: (W - pw + 1) / 2, (H - ph + 1) / 2
   float* ws;         // split-K: combine slabs (with cnt) or wgrad partial slabs [split][M][N] (without)
   int* cnt;          // split-K arrival counters of the in-launch combine
 };
@@ -89,6 +93,7 @@ struct Geo {
   int hmul, hoff, woff;    // pixel h = hmul*h2 + hoff
   int r0, s0, step, nS;    // taps r = r0 + step*i (< R), s likewise
   int nk;                  // K-tiles of this class
+  FastDiv f_rw, f_rh;      // division by rows_w / rows_h
 };
 
 __device__ __forceinline__ Geo make_geo(const LArgs& a, bool dgrad) {
@@ -99,14 +104,18 @@ __device__ __forceinline__ Geo make_geo(const LArgs& a, bool dgrad) {
   g.nk = a.nk_all;
   if (!dgrad) {  // fwd rows = output pixels
     g.rows_h = s.P; g.rows_w = s.Q;
+    g.f_rh = a.f_p; g.f_rw = a.f_q;
     return g;
   }
   g.rows_h = s.H; g.rows_w = s.W;
+  g.f_rh = a.f_h; g.f_rw = a.f_w;
   if (a.classes == 4) {
     const int ph = blockIdx.z >> 1, pw = blockIdx.z & 1;
     g.hmul = 2; g.hoff = ph; g.woff = pw;
     g.rows_h = (s.H - ph + 1) >> 1;
     g.rows_w = (s.W - pw + 1) >> 1;
+    g.f_rh = a.f_ch[ph];
+    g.f_rw = a.f_cw[pw];
     g.M = s.N * g.rows_h * g.rows_w;
     g.r0 = (ph + s.pad) & 1;
     g.s0 = (pw + s.pad) & 1;
@@ -159,14 +168,14 @@ struct FwdA {  // x gathered: row = output pixel npq, k = (r, s, c), C % 64 == 0
   static constexpr bool KC = true;
   static constexpr int kRows = ROWS, kPieces = PPW;
   int base[PPW], ih0[PPW], iw0[PPW];
-  __device__ void init(const LArgs& a, const Geo&, int r0, int wid, int lane, int) {
+  __device__ void init(const LArgs& a, const Geo& g, int r0, int wid, int lane, int) {
     const ConvShape& s = a.s;
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
       int row, k;
       lds_slot_to_rk<true, ROWS>((i * NW + wid) * 1024 + lane * 16, row, k);
       const int m = r0 + row;
-      const int q = m % s.Q, t = m / s.Q, p = t % s.P, n = t / s.P;
+      const int t = fdiv(m, g.f_rw), q = m - t * s.Q, n = fdiv(t, g.f_rh), p = t - n * s.P;
       ih0[i] = p * s.stride - s.pad;
       iw0[i] = q * s.stride - s.pad;
       base[i] = (int)((unsigned)((n * s.H + ih0[i]) * s.W + iw0[i]) * (unsigned)s.C) + k;
@@ -187,20 +196,20 @@ struct FwdASmallC {  // x gathered for C in {8, 16, 32}: a 64-deep K-tile spans 
   static constexpr bool KC = true;
   static constexpr int kRows = ROWS, kPieces = PPW;
   int base[PPW], ih0[PPW], iw0[PPW], tl[PPW], cc[PPW];
-  __device__ void init(const LArgs& a, const Geo&, int r0, int wid, int lane, int) {
+  __device__ void init(const LArgs& a, const Geo& g, int r0, int wid, int lane, int) {
     const ConvShape& s = a.s;
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
       int row, k;
       lds_slot_to_rk<true, ROWS>((i * NW + wid) * 1024 + lane * 16, row, k);
       const int m = r0 + row;
-      const int q = m % s.Q, t = m / s.Q, p = t % s.P, n = t / s.P;
+      const int t = fdiv(m, g.f_rw), q = m - t * s.Q, n = fdiv(t, g.f_rh), p = t - n * s.P;
       ih0[i] = p * s.stride - s.pad;
       iw0[i] = q * s.stride - s.pad;
       base[i] = (int)((unsigned)((n * s.H + ih0[i]) * s.W + iw0[i]) * (unsigned)s.C);
       if (m >= a.M) ih0[i] = -(1 << 20);  // never inside the image
-      tl[i] = k / s.C;                    // tap within the K-tile
-      cc[i] = k % s.C;                    // channel offset within the tap
+      tl[i] = k >> __builtin_ctz(s.C);    // tap within the K-tile (C is a power of two)
+      cc[i] = k & (s.C - 1);              // channel offset within the tap
     }
   }
   __device__ __forceinline__ uint32_t off(const LArgs& a, int i, const KS& ks) const {
@@ -250,7 +259,7 @@ struct DgradA {  // dy gathered: row = input pixel (class-local), k = (r, s, ko)
       int row, k;
       lds_slot_to_rk<true, ROWS>((i * NW + wid) * 1024 + lane * 16, row, k);
       const int m = r0 + row;
-      const int w2 = m % g.rows_w, t = m / g.rows_w, h2 = t % g.rows_h, n = t / g.rows_h;
+      const int t = fdiv(m, g.f_rw), w2 = m - t * g.rows_w, n = fdiv(t, g.f_rh), h2 = t - n * g.rows_h;
       nP[i] = n * s.P;
       hp[i] = m < g.M ? g.hmul * h2 + g.hoff + s.pad : -(1 << 20);
       wp[i] = g.hmul * w2 + g.woff + s.pad;
@@ -389,7 +398,7 @@ __device__ __forceinline__ void store_remapped(const LArgs& a, const Geo& g, flo
   for (int i = 0; i < 4; ++i) {
     const int m = mbase + i * 16 + (lane & 15);
     if (m >= g.M) continue;
-    const int w2 = m % g.rows_w, t = m / g.rows_w, h2 = t % g.rows_h, n = t / g.rows_h;
+    const int t = fdiv(m, g.f_rw), w2 = m - t * g.rows_w, n = fdiv(t, g.f_rh), h2 = t - n * g.rows_h;
     const size_t row = ((size_t)n * s.H + g.hmul * h2 + g.hoff) * s.W + g.hmul * w2 + g.woff;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -402,9 +411,18 @@ __device__ __forceinline__ void store_remapped(const LArgs& a, const Geo& g, flo
   }
 }
 
-template <int WM, int WN, class OA, class OB, int EPI, bool OUT_F32, bool DGRAD>
-__global__ __launch_bounds__(256, 2) void conv_lds_kernel(LArgs a, const bf16_t* pa, uint32_t bytes_a,
-                                                         const bf16_t* pb, uint32_t bytes_b) {
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// NS = LDS stages in the ring.  NS = 2: two workgroups per CU, the DMA of K-tile
+// kt+1 in flight while kt is multiplied.  NS = 3 / 4 (grids of at most one
+// workgroup per CU): K-tiles kt+1 .. kt+NS-1 in flight, a counted vmcnt (never 0
+// in the steady state) retires only tile kt before the barrier that publishes it.
+template <int WM, int WN, class OA, class OB, int EPI, bool OUT_F32, bool DGRAD, int NS>
+__global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void conv_lds_kernel(LArgs a, const bf16_t* pa, uint32_t bytes_a,
+                                                                       const bf16_t* pb, uint32_t bytes_b) {
   constexpr int NW = WM * WN, BM = WM * 64, BN = WN * 64;
   static_assert(NW == 4, "4-wave workgroups (the launch bounds and the split-K slab size assume it)");
   static_assert(OA::kRows == BM && OB::kRows == BN && OA::kPieces == BM / 8 / NW && OB::kPieces == BN / 8 / NW,
@@ -412,7 +430,9 @@ __global__ __launch_bounds__(256, 2) void conv_lds_kernel(LArgs a, const bf16_t*
   constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128, STAGE = A_BYTES + B_BYTES;
   constexpr int PPA = BM / 8 / NW, PPB = BN / 8 / NW;
   static_assert(PPA >= 1 && PPB >= 1 && PPA * NW * 8 == BM && PPB * NW * 8 == BN, "DMA pieces");
-  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+  constexpr int PER_TILE = PPA + PPB;  // DMA instructions per lane per K-tile
+  static_assert(NS >= 2 && NS * STAGE <= 160 * 1024 && PER_TILE * (NS - 2) < 64, "LDS ring");
+  __shared__ __attribute__((aligned(1024))) char smem[NS * STAGE];
 
   const Geo g = make_geo(a, DGRAD);
   const int tiles_m = (g.M + BM - 1) / BM, tiles_n = (a.N + BN - 1) / BN;
@@ -442,39 +462,59 @@ __global__ __launch_bounds__(256, 2) void conv_lds_kernel(LArgs a, const bf16_t*
     ra.r = __builtin_amdgcn_make_buffer_rsrc((void*)pa, (short)0, (int)bytes_a, 0x00020000);
     rb.r = __builtin_amdgcn_make_buffer_rsrc((void*)pb, (short)0, (int)bytes_b, 0x00020000);
     KS ks = ks_init(a, g, kt0);
-    LDNN_DMA_TILE(oa, PPA, ra, smem, ks);
-    LDNN_DMA_TILE(ob, PPB, rb, smem + A_BYTES, ks);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // prologue: K-tiles 0 .. NS-2 into stages 0 .. NS-2
+#pragma unroll
+    for (int t = 0; t < NS - 1; ++t) {
+      if (t < nk) {
+        if (t > 0) {
+          ks_next(a, g, ks);
+          oa.advance(a);
+          ob.advance(a);
+        }
+        LDNN_DMA_TILE(oa, PPA, ra, smem + t * STAGE, ks);
+        LDNN_DMA_TILE(ob, PPB, rb, smem + t * STAGE + A_BYTES, ks);
+      }
+    }
 
+    int cur = 0;  // stage of K-tile kt
     for (int kt = 0; kt < nk; ++kt) {
-      char* stage = smem + (kt & 1) * STAGE;
-      lds_barrier();  // publishes tile kt; every wave is done reading the other stage
-      if (kt + 1 < nk) {
+      // own DMA of tile kt landed (tiles kt+1 .. kt+NS-2 may stay in flight)
+      if (NS == 2 || kt + NS - 2 >= nk) {
+        wait_vm<0>();
+      } else {
+        wait_vm<PER_TILE * (NS - 2)>();
+      }
+      lds_barrier();  // publishes tile kt; every wave is done reading tile kt-1's stage
+      if (kt + NS - 1 < nk) {
         ks_next(a, g, ks);
         oa.advance(a);
         ob.advance(a);
-        char* nxt = smem + ((kt + 1) & 1) * STAGE;
+        char* nxt = smem + (cur == 0 ? NS - 1 : cur - 1) * STAGE;  // stage of tile kt-1
         LDNN_DMA_TILE(oa, PPA, ra, nxt, ks);
         LDNN_DMA_TILE(ob, PPB, rb, nxt + A_BYTES, ks);
       }
-      const char* la = stage;
-      const char* lb = stage + A_BYTES;
+      const char* la = smem + cur * STAGE;
+      const char* lb = la + A_BYTES;
       __builtin_amdgcn_s_setprio(1);
+      // all 16 fragments of the K-tile first (64 VGPRs): the reads of the second
+      // K-half are in flight while the first half's 16 MFMAs run
+      bf16x8 fa[2][4], fb[2][4];
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
-        bf16x8 fa[4], fb[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) fa[i] = read_frag<OA::KC, BM>(la, wm * 4 + i, kk, lane);
+        for (int i = 0; i < 4; ++i) fa[kk][i] = read_frag<OA::KC, BM>(la, wm * 4 + i, kk, lane);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) fb[j] = read_frag<OB::KC, BN>(lb, wn * 4 + j, kk, lane);
+        for (int j = 0; j < 4; ++j) fb[kk][j] = read_frag<OB::KC, BN>(lb, wn * 4 + j, kk, lane);
+      }
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
           for (int i = 0; i < 4; ++i)
-            acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[j][i], 0, 0, 0);
-      }
+            acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[kk][j], fa[kk][i], acc[j][i], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // own DMA of tile kt+1 landed
+      cur = cur == NS - 1 ? 0 : cur + 1;
     }
   }
 
@@ -589,6 +629,14 @@ LArgs base_args(const ConvShape& s) {
   a.rsc = s.R * s.S * s.C;
   a.pq = s.P * s.Q;
   a.classes = 1;
+  a.f_p = make_fastdiv(s.P);
+  a.f_q = make_fastdiv(s.Q);
+  a.f_h = make_fastdiv(s.H);
+  a.f_w = make_fastdiv(s.W);
+  for (int c = 0; c < 2; ++c) {
+    a.f_cw[c] = make_fastdiv((s.W - c + 1) >> 1);
+    a.f_ch[c] = make_fastdiv((s.H - c + 1) >> 1);
+  }
   return a;
 }
 
@@ -597,14 +645,31 @@ bool shape_ok(const ConvShape& s) {
          fits((size_t)s.K * s.R * s.S * s.C * 2) && fits((size_t)s.N * s.P * s.Q * s.K * 2);
 }
 
+// LDS ring depth.  Default NS = 2 (two workgroups = 8 waves per CU).  The deep
+// ring (NS 3 / 4 at one workgroup per CU, 2-3 K-tiles in flight) is kept for
+// tuning behind LDNN_CONV_NS=4: measured on MI355X over the ResNet-18 @224 conv
+// shapes (scripts/conv_micro.py, profiles/conv_ring_depth_r1.txt) it is SLOWER on
+// every shape (fwd+dgrad+wgrad 922 vs 710 us): the second workgroup's waves hide
+// the per-wave ds_read / barrier latency better than deeper DMA prefetch does.
+int ring_env() {
+  static const int v = [] {
+    const char* e = std::getenv("LDNN_CONV_NS");
+    return e ? std::atoi(e) : 0;
+  }();
+  return v;
+}
+
+bool deep_ring(int) { return ring_env() >= 3; }
+
 // OA / OB = Policy<rows, DMA pieces per wave (= rows / 8 / 4 waves), 4 waves>.
-template <int WM, int WN, class OA, class OB, bool OUT_F32, bool DGRAD>
-hipError_t launch(LArgs a, int epi, int splits, const bf16_t* pa, size_t ba, const bf16_t* pb, size_t bb,
-                  hipStream_t st) {
+template <int WM, int WN, class OA, class OB, bool OUT_F32, bool DGRAD, int NS>
+hipError_t launch_ns(LArgs a, int epi, int splits, const bf16_t* pa, size_t ba, const bf16_t* pb, size_t bb,
+                     hipStream_t st) {
   constexpr int NW = WM * WN;
   dim3 grid(a.tiles_x, splits, a.classes), block(NW * 64);
-#define LDNN_CONV_LDS(E) \
-  conv_lds_kernel<WM, WN, OA, OB, E, OUT_F32, DGRAD><<<grid, block, 0, st>>>(a, pa, (uint32_t)ba, pb, (uint32_t)bb)
+#define LDNN_CONV_LDS(E)                                                                                      \
+  conv_lds_kernel<WM, WN, OA, OB, E, OUT_F32, DGRAD, NS><<<grid, block, 0, st>>>(a, pa, (uint32_t)ba, pb, \
+                                                                                  (uint32_t)bb)
   switch (epi) {
     case EPI_NONE:
       LDNN_CONV_LDS(EPI_NONE);
@@ -622,6 +687,16 @@ hipError_t launch(LArgs a, int epi, int splits, const bf16_t* pa, size_t ba, con
   }
 #undef LDNN_CONV_LDS
   return hipGetLastError();
+}
+
+template <int WM, int WN, class OA, class OB, bool OUT_F32, bool DGRAD>
+hipError_t launch(LArgs a, int epi, int splits, const bf16_t* pa, size_t ba, const bf16_t* pb, size_t bb,
+                  hipStream_t st) {
+  constexpr int STAGE = (WM + WN) * 64 * 128;
+  constexpr int DEEP = 4 * STAGE <= 128 * 1024 ? 4 : 3;
+  if (deep_ring(a.tiles_x * splits * a.classes))
+    return launch_ns<WM, WN, OA, OB, OUT_F32, DGRAD, DEEP>(a, epi, splits, pa, ba, pb, bb, st);
+  return launch_ns<WM, WN, OA, OB, OUT_F32, DGRAD, 2>(a, epi, splits, pa, ba, pb, bb, st);
 }
 
 // In-launch split-K for small-M fwd / dgrad: enough slices for ~1.5
