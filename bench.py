@@ -88,7 +88,8 @@ def run_ldnn(ctx, args):
     xavier_init(model)
     eng = StaticMLPEngine(model, args.batch, OptimConfig("sgd", lr=args.lr, momentum=0.9),
                           device=ctx.device, world_size=ctx.world_size, use_graphs=not args.no_graphs,
-                          bucket_cap_elems=args.bucket_elems, shard_optimizer=False if args.no_shard else None)
+                          bucket_cap_elems=args.bucket_elems, shard_optimizer=False if args.no_shard else None,
+                          library_gemms=not args.no_library_gemms)
     if ctx.distributed:
         dist.broadcast(eng.flat.master, src=0)
         eng.flat.refresh_shadow()
@@ -146,6 +147,8 @@ def main():
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--no-shard", action="store_true",
                     help="all-reduce + replicated optimizer instead of reduce-scatter / sharded optimizer / all-gather")
+    ap.add_argument("--no-library-gemms", action="store_true",
+                    help="run the plain GEMMs (fp32 wgrads, bias+ReLU forwards) on ldnn's MFMA kernels instead of hipBLASLt")
     ap.add_argument("--compare-stock", action="store_true")
     ap.add_argument("--backend", default="auto", help="auto (nccl = RCCL on GPUs) | gloo (testing only)")
     args = ap.parse_args()
@@ -175,6 +178,8 @@ def main():
             "seq_len": None,
             "parallelism": f"dp{n}",
             "optimizer": "sgd momentum 0.9, fp32 master",
+            "gemms": ("ldnn MFMA kernels" if args.no_library_gemms else
+                      "hipBLASLt: fp32 wgrads + bias/ReLU fwd; ldnn MFMA: fused dgrad (dReLU + dbias), classifier head"),
             "grad_sync": ("none (1 GPU)" if n == 1 else
                           "fp32 RCCL all-reduce, bucketed, overlapped" if args.no_shard else
                           "fp32 RCCL reduce-scatter (bucketed, overlapped) + sharded SGD + bf16 weight all-gather"),

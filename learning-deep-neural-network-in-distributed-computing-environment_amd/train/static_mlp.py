@@ -80,7 +80,7 @@ class StaticMLPEngine:
                  process_group=None, world_size: int | None = None, bucket_cap_elems: int = 8 << 20,
                  use_graphs: bool = True, average_grads: bool = True, use_head_kernels: bool = True,
                  shard_optimizer: bool | None = None, overlap_optimizer: bool = False, wgrad_combine: bool = True,
-                 fuse_optimizer: bool | None = None):
+                 fuse_optimizer: bool | None = None, library_gemms: bool | None = None):
         from ..models.mlp import MLP
 
         if not isinstance(model, MLP):
@@ -182,12 +182,30 @@ class StaticMLPEngine:
         # combines the slices IN the launch (gemm.hip k128 + splitk_combine): every
         # CU gets two workgroups, the result is deterministic and overwrites the
         # gradient (no clearing needed).  Tiny grids keep fp32-atomic split-K.
+        # library_gemms: the PLAIN GEMMs of the step -- the fp32 weight gradients and
+        # the bias(+ReLU) forwards -- go to hipBLASLt (torch.mm out_dtype=fp32 /
+        # torch._addmm_activation, both writing into the engine's static buffers);
+        # the fused ones stay on ldnn's MFMA kernels: dgrad with the activation
+        # derivative and the bias-gradient column sums in its epilogue, and the
+        # classifier head (fwd + softmax-xent + argmax, transposed-read wgrad).
+        # Measured on MI355X (scripts/bench_blaslt.py, profiles/mlp_gemm_library_r1.jsonl):
+        # hipBLASLt is 8-22 % faster on those plain shapes, ldnn wins the fused dgrad.
+        if library_gemms is None:
+            library_gemms = hasattr(torch, "_addmm_activation")
+        hidden = [l for l in range(L) if not (self.use_head and l == L - 1)]
+        self._lib_wgrad = [bool(library_gemms) and l in hidden for l in range(L)]
+        self._lib_fwd = [bool(library_gemms) and l in hidden and self.layers[l].activation in ("relu", "none")
+                         for l in range(L)]
+        self.bias_bf16 = [f.shadow_storage(l.bias) for l in self.layers]
         self._wgrad_splitk, self._wgrad_ws = [], []
         for l, layer in enumerate(self.layers):
             M, N = self.dW[l].shape
             self._wgrad_ws.append(None)
             if self.use_head and l == L - 1:
                 self._wgrad_splitk.append(self.C.head_wgrad_splits(B, N))
+                continue
+            if self._lib_wgrad[l]:   # overwrites the gradient: no clearing, no split-K
+                self._wgrad_splitk.append(1)
                 continue
             tile, sk = self.C.gemm_plan(M, N, B, True)
             tiles = ((M + 127) // 128) * ((N + 127) // 128)
@@ -231,6 +249,7 @@ class StaticMLPEngine:
         if overlap_optimizer:
             fuse_optimizer = False  # the side-stream variant updates whole ranges itself
         self._fused = [bool(fuse_optimizer) and not self.distributed and not (self.use_head and l == L - 1)
+                       and not self._lib_wgrad[l]
                        and (self._wgrad_splitk[l] == 1 or self._wgrad_ws[l] is not None) for l in range(L)]
         self.rank = dist.get_rank(process_group) if self.distributed else 0
         self.overlap_optimizer = overlap_optimizer
@@ -247,6 +266,12 @@ class StaticMLPEngine:
         C = self.C
         L = len(self.layers)
         for l in range(L - 1 if (train and self.use_head) else L):
+            if self._lib_fwd[l]:
+                if self.layers[l].activation == "relu":
+                    torch._addmm_activation(self.bias_bf16[l], self.h[l], self.W[l].t(), out=self.h[l + 1])
+                else:
+                    torch.addmm(self.bias_bf16[l], self.h[l], self.W[l].t(), out=self.h[l + 1])
+                continue
             C.gemm(self.h[l], self.W[l], self.h[l + 1], True, True, self._fwd_epi[l], bias=self.bias[l])
 
     def _loss(self):
@@ -263,6 +288,9 @@ class StaticMLPEngine:
         sk = self._wgrad_splitk[l]
         if self.use_head and l == len(self.layers) - 1:   # also emits the head's bias gradient
             self.C.head_wgrad(self.dz[l + 1], self.h[l], self.dW[l], self.db[l], sk)
+            return
+        if self._lib_wgrad[l]:   # plain GEMM, fp32 out: hipBLASLt straight into the flat grad buffer
+            torch.mm(self.dz[l + 1].t(), self.h[l], out_dtype=torch.float32, out=self.dW[l])
             return
         if self._wgrad_ws[l] is not None:   # in-launch split-K combine, overwrites the gradient
             ws, cnt = self._wgrad_ws[l]

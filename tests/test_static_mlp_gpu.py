@@ -9,9 +9,10 @@ from ldnn.train.static_mlp import OptimConfig, StaticMLPEngine
 pytestmark = pytest.mark.gpu
 
 
+@pytest.mark.parametrize("library", [False, True])
 @pytest.mark.parametrize("opt", ["sgd", "adam"])
 @pytest.mark.parametrize("graphs", [False, True])
-def test_engine_matches_fp32_reference(opt, graphs):
+def test_engine_matches_fp32_reference(opt, graphs, library):
     torch.manual_seed(0)
     B = 256
     model = mlp3(784, 512, 10)
@@ -21,7 +22,8 @@ def test_engine_matches_fp32_reference(opt, graphs):
         dst.data.copy_(src.data)
     ref = ref.cuda()
     cfg = OptimConfig(opt, lr=0.05 if opt == "sgd" else 1e-3, momentum=0.9)
-    eng = StaticMLPEngine(model, B, cfg, use_graphs=graphs)
+    eng = StaticMLPEngine(model, B, cfg, use_graphs=graphs, library_gemms=library)
+    assert any(eng._lib_wgrad) == library and any(eng._lib_fwd) == library
     if opt == "sgd":
         ropt = torch.optim.SGD(ref.parameters(), lr=0.05, momentum=0.9)
     else:
@@ -133,8 +135,9 @@ def test_wgrad_inlaunch_splitk_combine_matches_unsplit():
     B = 2048
     m1, m2 = mlp3(784, 1024, 10), mlp3(784, 1024, 10)
     m2.load_state_dict(m1.state_dict())
-    e1 = StaticMLPEngine(m1, B, OptimConfig("sgd", lr=0.05, momentum=0.9), use_graphs=True)
-    e2 = StaticMLPEngine(m2, B, OptimConfig("sgd", lr=0.05, momentum=0.9), use_graphs=False, wgrad_combine=False)
+    e1 = StaticMLPEngine(m1, B, OptimConfig("sgd", lr=0.05, momentum=0.9), use_graphs=True, library_gemms=False)
+    e2 = StaticMLPEngine(m2, B, OptimConfig("sgd", lr=0.05, momentum=0.9), use_graphs=False, wgrad_combine=False,
+                         library_gemms=False)
     assert any(w is not None for w in e1._wgrad_ws) and all(w is None for w in e2._wgrad_ws)
     g = torch.Generator(device="cuda").manual_seed(7)
     for i in range(6):
@@ -157,8 +160,8 @@ def test_fused_optimizer_epilogue_matches_separate_launch(opt):
     m1, m2 = mlp3(784, 4096, 10), mlp3(784, 4096, 10)
     m2.load_state_dict(m1.state_dict())
     cfg = OptimConfig(opt, lr=0.05 if opt == "sgd" else 1e-3, momentum=0.9, weight_decay=1e-4)
-    e1 = StaticMLPEngine(m1, B, cfg, use_graphs=True, fuse_optimizer=True)
-    e2 = StaticMLPEngine(m2, B, cfg, use_graphs=True, fuse_optimizer=False)
+    e1 = StaticMLPEngine(m1, B, cfg, use_graphs=True, fuse_optimizer=True, library_gemms=False)
+    e2 = StaticMLPEngine(m2, B, cfg, use_graphs=True, fuse_optimizer=False, library_gemms=False)
     assert any(e1._fused) and not any(e2._fused)
     g = torch.Generator(device="cuda").manual_seed(9)
     for i in range(5):
@@ -171,3 +174,29 @@ def test_fused_optimizer_epilogue_matches_separate_launch(opt):
     # same arithmetic; only FMA contraction differs between the two kernels
     torch.testing.assert_close(e1.flat.master, e2.flat.master, rtol=1e-4, atol=2e-5)
     assert torch.equal(e1.flat.shadow, e1.flat.master.bfloat16())
+
+
+def test_library_gemm_engine_matches_native_engine():
+    """hipBLASLt plain GEMMs (fp32 wgrads, bias+ReLU forwards) inside the graph-captured
+    step == the all-ldnn-kernel engine, up to bf16 rounding of the bias in the forward."""
+    torch.manual_seed(0)
+    B = 1024
+    m1, m2 = mlp3(784, 1024, 10), mlp3(784, 1024, 10)
+    m2.load_state_dict(m1.state_dict())
+    cfg = OptimConfig("sgd", lr=0.05, momentum=0.9)
+    e1 = StaticMLPEngine(m1, B, cfg, use_graphs=True, library_gemms=True)
+    e2 = StaticMLPEngine(m2, B, cfg, use_graphs=True, library_gemms=False)
+    g = torch.Generator(device="cuda").manual_seed(5)
+    l1, l2 = [], []
+    for i in range(6):
+        x = torch.randn(B, 784, device="cuda", generator=g).bfloat16()
+        y = torch.randint(0, 10, (B,), device="cuda", generator=g)
+        for e, ls in ((e1, l1), (e2, l2)):
+            e.reset_stats()
+            e.load_batch(x, y)
+            e.step()
+            ls.append(e.read_stats(B)[0])
+    torch.cuda.synchronize()
+    for a, b in zip(l1, l2):
+        assert abs(a - b) < 1e-2 * max(1.0, abs(b)), (l1, l2)
+    torch.testing.assert_close(e1.flat.master, e2.flat.master, rtol=2e-2, atol=2e-3)
