@@ -369,7 +369,9 @@ void adam_step(const at::Tensor& param, const at::Tensor& grad, const at::Tensor
 
 void head_fwd_xent(const at::Tensor& h, const at::Tensor& W, const at::Tensor& bias, const at::Tensor& labels,
                    const c10::optional<at::Tensor>& logits, const at::Tensor& dlogits, const at::Tensor& stats,
-                   int64_t num_classes, double grad_scale) {
+                   int64_t num_classes, double grad_scale, const c10::optional<at::Tensor>& dh,
+                   const c10::optional<at::Tensor>& dbias, int64_t dgrad_epi,
+                   const c10::optional<at::Tensor>& dbias_ws) {
   check_dev(h, at::kBFloat16, "h");
   check_dev(W, at::kBFloat16, "W");
   check_dev(bias, at::kFloat, "bias");
@@ -408,6 +410,30 @@ void head_fwd_xent(const at::Tensor& h, const at::Tensor& W, const at::Tensor& b
   p.ldw = (int)W.stride(0);
   p.ldw_rows = (int)W.size(0);
   p.grad_scale = (float)grad_scale;
+  if (dh.has_value()) {
+    check_dev(*dh, at::kBFloat16, "dh");
+    TORCH_CHECK(dh->dim() == 2 && dh->size(0) == B && dh->size(1) == K && dh->stride(1) == 1 &&
+                    dh->stride(0) % 8 == 0 && aligned16(dh->data_ptr()),
+                "head: dh must be [B][K] with 16-B aligned rows");
+    TORCH_CHECK(K <= ldnn::head_dgrad_max_k(), "head: fused dgrad needs K <= ", ldnn::head_dgrad_max_k());
+    TORCH_CHECK(dgrad_epi == ldnn::EPI_NONE || dgrad_epi == ldnn::EPI_DRELU || dgrad_epi == ldnn::EPI_DSIGMOID,
+                "head: dgrad_epi must be EPI_NONE / EPI_DRELU / EPI_DSIGMOID");
+    p.dh = bf16_mut(*dh);
+    p.lddh = (int)dh->stride(0);
+    p.dgrad_epi = (int)dgrad_epi;
+    if (dbias.has_value()) {
+      check_dev(*dbias, at::kFloat, "dbias");
+      TORCH_CHECK(dbias->is_contiguous() && dbias->numel() >= K && aligned16(dbias->data_ptr()),
+                  "head: dbias must hold K floats, 16-B aligned");
+      TORCH_CHECK(dbias_ws.has_value(), "head: dbias needs dbias_ws (head_dgrad_ws_floats(B, K) fp32)");
+      check_dev(*dbias_ws, at::kFloat, "dbias_ws");
+      TORCH_CHECK(dbias_ws->is_contiguous() && dbias_ws->numel() >= (int64_t)ldnn::head_dgrad_ws_floats((int)B, (int)K) &&
+                      aligned16(dbias_ws->data_ptr()),
+                  "head: dbias_ws too small");
+      p.dbias = dbias->data_ptr<float>();
+      p.dbias_ws = dbias_ws->data_ptr<float>();
+    }
+  }
   c10::hip::HIPGuardMasqueradingAsCUDA g(h.device());
   check(ldnn::head_fwd_xent(p, cur_stream(h)), "head_fwd_xent");
 }
@@ -742,9 +768,12 @@ PYBIND11_MODULE(_C, m) {
   m.def("bump_step", &bump_step);
   m.def("head_fwd_xent", &head_fwd_xent, "fused narrow Linear + softmax-xent + argmax (per-16-row stats slots)",
         py::arg("h"), py::arg("W"), py::arg("bias"), py::arg("labels"), py::arg("logits"), py::arg("dlogits"),
-        py::arg("stats"), py::arg("num_classes"), py::arg("grad_scale"));
+        py::arg("stats"), py::arg("num_classes"), py::arg("grad_scale"), py::arg("dh") = py::none(), py::arg("dbias") = py::none(),
+        py::arg("dgrad_epi") = (int64_t)ldnn::EPI_DRELU, py::arg("dbias_ws") = py::none());
+  m.def("head_dgrad_ws_floats", &ldnn::head_dgrad_ws_floats, py::arg("B"), py::arg("K"));
   m.def("head_wgrad", &head_wgrad, "dW = dz^T h (+ db = colsum dz); splits > 1 accumulate atomically",
         py::arg("dz"), py::arg("h"), py::arg("dW"), py::arg("db") = py::none(), py::arg("splits") = 0);
+  m.def("head_dgrad_max_k", &ldnn::head_dgrad_max_k);
   m.def("head_wgrad_splits", &ldnn::head_wgrad_splits, py::arg("B"), py::arg("K"));
   m.def("bn_fwd", &bn_fwd, py::arg("x"), py::arg("y"), py::arg("residual"), py::arg("gamma"), py::arg("beta"),
         py::arg("running_mean"), py::arg("running_var"), py::arg("save_mean"), py::arg("save_invstd"),

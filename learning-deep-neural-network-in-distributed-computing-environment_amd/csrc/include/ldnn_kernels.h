@@ -194,8 +194,18 @@ struct HeadParams {
   float* stats;           // [ceil(B/16)][2] per-workgroup (loss sum, correct) accumulators
   int B, K, C, ld, ldh, ldw, ldw_rows;
   float grad_scale;
+  // optional fused dgrad of the head (K <= head_dgrad_max_k()):
+  // dh = (dlogits W) * act'(h) [B][lddh] bf16, dbias += column sums of dh
+  uint16_t* dh;
+  float* dbias;         // += column sums of dh (via dbias_ws: head_dgrad_ws_floats(B, K) floats)
+  float* dbias_ws;
+  int lddh, dgrad_epi;  // EPI_NONE / EPI_DRELU / EPI_DSIGMOID
 };
 hipError_t head_fwd_xent(const HeadParams& p, hipStream_t s);
+int head_dgrad_max_k();
+size_t head_dgrad_ws_floats(int B, int K);
+// out[i] = sum_s ws[s][i] (+ beta * out[i]) over n4 float4 columns and `splits` slabs
+hipError_t slab_sum(const float* ws, float* out, int64_t n4, int splits, float beta, hipStream_t s);
 struct HeadWgradParams {
   const uint16_t* dz;  // [B][ld] bf16
   const uint16_t* h;   // [B][ldh] bf16

@@ -776,6 +776,12 @@ ConvWorkspace conv2d_lds_workspace(const ConvShape& s, int op) {
   return ConvWorkspace{};
 }
 
+hipError_t slab_sum(const float* ws, float* out, int64_t n4, int splits, float beta, hipStream_t st) {
+  if (n4 <= 0) return hipSuccess;
+  slab_sum_kernel<<<(unsigned)((n4 + 31) / 32), 256, 0, st>>>(ws, out, n4, splits, beta);
+  return hipGetLastError();
+}
+
 // Each returns hipErrorNotSupported when the shape is outside the fast path
 // (conv.hip then runs its generic register-staged kernel).
 // Stems and other small-C convolutions (C in {8, 16, 32}, e.g. the 7x7 ResNet stem

@@ -12,6 +12,16 @@
 //                  per-workgroup slot: no same-address atomics), one launch.
 //                  16 rows per workgroup, 8 waves split K (skinny-N GEMM), the
 //                  row softmax runs on the reduced accumulators in registers.
+//                  With p.dh set it also runs the head's DGRAD: the workgroup's
+//                  16 rows of h (<= 128 KiB) are staged in LDS as they stream in
+//                  for the logits, so dh = (dlogits W) * act'(h) needs no second
+//                  read of h, and the previous layer's bias gradient (column sums
+//                  of dh) is reduced from per-workgroup slabs.  Measured on MI355X
+//                  at 4096 x 4096 (scripts/bench_head.py) it is NOT faster than the
+//                  separate K = 16 dgrad GEMM (fwd 11 -> 32 us fused vs 11 + 22.6):
+//                  the 32 MB dh store (5.4 us), the class-loop FMAs (5.5 us) and the
+//                  slab reduction (5 us) all land after the h stream instead of
+//                  overlapping it, so the engine leaves it off by default.
 //  head_wgrad:     dW = dlogits^T h (+ db = column sums of dlogits).  The
 //                  reduction runs over the batch, the strided dimension of both
 //                  operands, so each wave stages its 32-row chunks through a
@@ -32,36 +42,18 @@ namespace {
 // ---------------------------------------------------------------------------
 constexpr int kFwdWaves = 8;
 
-template <int NT>
-__global__ __launch_bounds__(kFwdWaves * 64) void head_fwd_xent_kernel(HeadParams p) {
-  __shared__ floatx4 red[kFwdWaves - 1][NT][64];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int m0 = blockIdx.x * 16;
-  const int row = m0 + (lane & 15);
-  const int kq = 8 * (lane >> 4);
-  floatx4 acc[NT];
-#pragma unroll
-  for (int j = 0; j < NT; ++j) acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
-  const int nsteps = (p.K + 31) / 32;
-  const bf16x8 zero = {};
-#pragma unroll 8
-  for (int st = w; st < nsteps; st += kFwdWaves) {
-    const int k = st * 32 + kq;
-    const bool kok = k < p.K;
-    const bf16x8 a = (row < p.B && kok) ? *reinterpret_cast<const bf16x8*>(p.h + (size_t)row * p.ldh + k) : zero;
-#pragma unroll
-    for (int j = 0; j < NT; ++j) {
-      const int n = j * 16 + (lane & 15);
-      const bf16x8 b = (n < p.ldw_rows && kok) ? *reinterpret_cast<const bf16x8*>(p.W + (size_t)n * p.ldw + k) : zero;
-      acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b, a, acc[j], 0, 0, 0);
-    }
-  }
-  if (w > 0) {
-#pragma unroll
-    for (int j = 0; j < NT; ++j) red[w - 1][j][lane] = acc[j];
-  }
-  __syncthreads();
-  if (w != 0) return;
+constexpr int kHeadDgradMaxK = 4096;  // 16 rows x 4096 bf16 = 128 KiB of LDS
+
+// 16-B chunk q of staged row r.  Rows are K rounded up to 128 elements apart (a
+// whole number of 16-chunk groups), and the chunk is XORed with the row so the 16
+// rows of one k-chunk land on different banks without leaving their row.
+__device__ __forceinline__ int hs_off(int r, int q, int K) {
+  return r * ((K + 127) & ~127) * 2 + ((q ^ (r & 15)) << 4);
+}
+
+template <int NT, bool DG>
+__device__ __forceinline__ void head_softmax_xent(const HeadParams& p, floatx4 (&acc)[NT], floatx4 (*red)[NT][64],
+                                                  float* dls, int lane, int row, int m0) {
 #pragma unroll
   for (int j = 0; j < NT; ++j)
 #pragma unroll
@@ -127,6 +119,21 @@ __global__ __launch_bounds__(kFwdWaves * 64) void head_fwd_xent_kernel(HeadParam
       *reinterpret_cast<u16x4*>(p.dlogits + (size_t)row * p.ld + c0) = g;
     }
   }
+  if constexpr (DG) {  // the same bf16-rounded dlogits the head wgrad reads back
+    // (every lane's reads of red above are done before any lane writes dls over it)
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const int c0 = j * 16 + 4 * (lane >> 4);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int c = c0 + r;
+        const float gv = (rok && c < p.C) ? bf2f(f2bf((x[j][r] * inv - (c == lab ? 1.f : 0.f)) * p.grad_scale)) : 0.f;
+        dls[(lane & 15) * p.ld + c] = gv;
+      }
+    }
+  }
   // per-workgroup loss / correct: lanes 0..15 hold one row each
   float loss = (rok && lane < 16) ? (mx + __logf(se) - xl) : 0.f;
   float corr = (rok && lane < 16 && am == lab) ? 1.f : 0.f;
@@ -138,6 +145,103 @@ __global__ __launch_bounds__(kFwdWaves * 64) void head_fwd_xent_kernel(HeadParam
   if (lane == 0) {  // this workgroup's own slot: plain read-modify-write, replay-safe
     p.stats[2 * blockIdx.x] += loss;
     p.stats[2 * blockIdx.x + 1] += corr;
+  }
+}
+
+// dh[m0 + r][8q .. 8q+7] = act'(h) * sum_c dlogits[r][c] W[c][8q ..], for the 16 rows
+// of this workgroup; thread t owns column chunks q = t, t + 512, ... (coalesced
+// 16-B stores), keeps the 16 x 8 accumulators in registers over the classes, and
+// adds its column sums to the previous layer's bias gradient.
+template <int DEPI>
+__device__ __forceinline__ void head_dgrad_rows(const HeadParams& p, const char* hs, const float* dls, int m0) {
+  const int nq = p.K >> 3;
+  const int rows = min(16, p.B - m0);
+  for (int q = threadIdx.x; q < nq; q += kFwdWaves * 64) {
+    float acc[16][8];
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[r][i] = 0.f;
+    for (int c = 0; c < p.C; ++c) {
+      const u16x8 wv = *reinterpret_cast<const u16x8*>(p.W + (size_t)c * p.ldw + 8 * q);
+      float wf[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) wf[i] = bf2f(wv[i]);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float g = dls[r * p.ld + c];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[r][i] = fmaf(g, wf[i], acc[r][i]);
+      }
+    }
+    float cs[8] = {};
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      if (r >= rows) continue;
+      const u16x8 hv = *reinterpret_cast<const u16x8*>(hs + hs_off(r, q, p.K));
+      u16x8 o;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float hf = bf2f(hv[i]);
+        float v = acc[r][i];
+        if constexpr (DEPI == EPI_DRELU) v = hf > 0.f ? v : 0.f;
+        else if constexpr (DEPI == EPI_DSIGMOID) v *= hf * (1.f - hf);
+        o[i] = f2bf(v);
+        cs[i] += bf2f(o[i]);
+      }
+      *reinterpret_cast<u16x8*>(p.dh + (size_t)(m0 + r) * p.lddh + 8 * q) = o;
+    }
+    if (p.dbias != nullptr) {  // this workgroup's column sums -> its slab (summed by slab_sum after)
+      float* dst = p.dbias_ws + (size_t)blockIdx.x * p.K + 8 * q;
+      reinterpret_cast<floatx4*>(dst)[0] = floatx4{cs[0], cs[1], cs[2], cs[3]};
+      reinterpret_cast<floatx4*>(dst)[1] = floatx4{cs[4], cs[5], cs[6], cs[7]};
+    }
+  }
+}
+
+// DEPI: -1 = no fused dgrad; EPI_NONE / EPI_DRELU / EPI_DSIGMOID = dgrad with that
+// activation derivative
+template <int NT, int DEPI>
+__global__ __launch_bounds__(kFwdWaves * 64) void head_fwd_xent_kernel(HeadParams p) {
+  constexpr bool DG = DEPI >= 0;
+  constexpr int kRedBytes = (kFwdWaves - 1) * NT * 64 * 16;
+  __shared__ __attribute__((aligned(16))) char smem[kRedBytes + (DG ? 16 * kHeadDgradMaxK * 2 : 0)];
+  floatx4(*red)[NT][64] = reinterpret_cast<floatx4(*)[NT][64]>(smem);
+  char* hs = smem + kRedBytes;
+  float* dls = reinterpret_cast<float*>(smem);  // [16][ld] dlogits, over red once wave 0 has consumed it
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int m0 = blockIdx.x * 16;
+  const int row = m0 + (lane & 15);
+  const int kq = 8 * (lane >> 4);
+  floatx4 acc[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const int nsteps = (p.K + 31) / 32;
+  const bf16x8 zero = {};
+#pragma unroll 16  // (K = 4096: all 16 of a wave's loads in flight at once)
+  for (int st = w; st < nsteps; st += kFwdWaves) {
+    const int k = st * 32 + kq;
+    const bool kok = k < p.K;
+    const bf16x8 a = (row < p.B && kok) ? *reinterpret_cast<const bf16x8*>(p.h + (size_t)row * p.ldh + k) : zero;
+    if constexpr (DG) {
+      if (kok) *reinterpret_cast<bf16x8*>(hs + hs_off(lane & 15, k >> 3, p.K)) = a;
+    }
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const int n = j * 16 + (lane & 15);
+      const bf16x8 b = (n < p.ldw_rows && kok) ? *reinterpret_cast<const bf16x8*>(p.W + (size_t)n * p.ldw + k) : zero;
+      acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b, a, acc[j], 0, 0, 0);
+    }
+  }
+  if (w > 0) {
+#pragma unroll
+    for (int j = 0; j < NT; ++j) red[w - 1][j][lane] = acc[j];
+  }
+  __syncthreads();
+  if (w == 0) head_softmax_xent<NT, DG>(p, acc, red, dls, lane, row, m0);
+  if constexpr (DG) {
+    __syncthreads();  // dlogits of the 16 rows in LDS, h staged
+    head_dgrad_rows<DEPI>(p, hs, dls, m0);
   }
 }
 
@@ -175,20 +279,25 @@ __global__ __launch_bounds__(kWgWaves * 64) void head_wgrad_kernel(HeadWgradPara
 
   // loader lanes: h chunk [32 rows][64 cols] = 4 x (8 rows x 128 B); dz chunk [32][16 NT]
   const int hr = lane >> 3, hc = (lane & 7) * 8;
-  for (int b0 = b_begin + w * kWgRows; b0 < b_end; b0 += kWgWaves * kWgRows) {
-    u16x8 hv[4];
+  u16x8 hv[4], dv[NT];
+  // chunk loads are software-pipelined: chunk b0 + stride is in flight while
+  // chunk b0 is staged and multiplied
+  auto load_chunk = [&](int b0) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int b = b0 + i * 8 + hr, c = col0 + hc;
       hv[i] = (b < b_end && c < p.K) ? *reinterpret_cast<const u16x8*>(p.h + (size_t)b * p.ldh + c) : u16x8{};
     }
-    u16x8 dv[NT];
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
       // lane: row (lane >> 1), 8 classes at j*16 + (lane & 1)*8
       const int b = b0 + (lane >> 1), c = j * 16 + (lane & 1) * 8;
       dv[j] = (b < b_end && c < p.ld) ? *reinterpret_cast<const u16x8*>(p.dz + (size_t)b * p.ld + c) : u16x8{};
     }
+  };
+  constexpr int kStride = kWgWaves * kWgRows;
+  if (b_begin + w * kWgRows < b_end) load_chunk(b_begin + w * kWgRows);
+  for (int b0 = b_begin + w * kWgRows; b0 < b_end; b0 += kStride) {
     // stage into the transposed-read images (strided layout of ldnn_gemm_tile.h)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -200,7 +309,8 @@ __global__ __launch_bounds__(kWgWaves * 64) void head_wgrad_kernel(HeadWgradPara
       const int r = lane >> 1;
       *reinterpret_cast<u16x8*>(ld + lds_offset<false, 16 * NT>(j * 16 + (lane & 1) * 8, r)) = dv[j];
     }
-    __builtin_amdgcn_s_waitcnt(0xc07f);
+    if (b0 + kStride < b_end) load_chunk(b0 + kStride);
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0) only: the prefetch stays in flight
     __builtin_amdgcn_wave_barrier();
     bf16x8 fd[NT];
 #pragma unroll
@@ -273,20 +383,42 @@ __global__ __launch_bounds__(kWgWaves * 64) void head_wgrad_kernel(HeadWgradPara
   }
 }
 
+template <int DEPI>
+hipError_t launch_head_fwd(const HeadParams& p, hipStream_t s) {
+  const dim3 grid((p.B + 15) / 16), block(kFwdWaves * 64);
+  switch (p.ld / 16) {
+    case 1: head_fwd_xent_kernel<1, DEPI><<<grid, block, 0, s>>>(p); break;
+    case 2: head_fwd_xent_kernel<2, DEPI><<<grid, block, 0, s>>>(p); break;
+    case 3: head_fwd_xent_kernel<3, DEPI><<<grid, block, 0, s>>>(p); break;
+    default: head_fwd_xent_kernel<4, DEPI><<<grid, block, 0, s>>>(p); break;
+  }
+  return hipGetLastError();
+}
+
 }  // namespace
 
 hipError_t head_fwd_xent(const HeadParams& p, hipStream_t s) {
   if (p.B <= 0) return hipSuccess;
   if (p.ld > 64 || p.ld % 16 != 0 || p.C > p.ld || p.ldw_rows > p.ld || p.K % 8 != 0) return hipErrorInvalidValue;
-  const dim3 grid((p.B + 15) / 16), block(kFwdWaves * 64);
-  switch (p.ld / 16) {
-    case 1: head_fwd_xent_kernel<1><<<grid, block, 0, s>>>(p); break;
-    case 2: head_fwd_xent_kernel<2><<<grid, block, 0, s>>>(p); break;
-    case 3: head_fwd_xent_kernel<3><<<grid, block, 0, s>>>(p); break;
-    default: head_fwd_xent_kernel<4><<<grid, block, 0, s>>>(p); break;
+  if (p.dh == nullptr) return launch_head_fwd<-1>(p, s);
+  if (p.K > kHeadDgradMaxK || p.lddh % 8 != 0 || (p.dbias != nullptr && p.dbias_ws == nullptr))
+    return hipErrorInvalidValue;
+  hipError_t e;
+  switch (p.dgrad_epi) {
+    case EPI_NONE: e = launch_head_fwd<EPI_NONE>(p, s); break;
+    case EPI_DRELU: e = launch_head_fwd<EPI_DRELU>(p, s); break;
+    case EPI_DSIGMOID: e = launch_head_fwd<EPI_DSIGMOID>(p, s); break;
+    default: return hipErrorInvalidValue;
   }
-  return hipGetLastError();
+  // per-workgroup column sums -> bias gradient: 256 same-address fp32 atomics per
+  // column measured 100+ us; a slab reduction over the chip costs a few
+  if (e != hipSuccess || p.dbias == nullptr) return e;
+  return slab_sum(p.dbias_ws, p.dbias, p.K / 4, (p.B + 15) / 16, 1.f, s);
 }
+
+size_t head_dgrad_ws_floats(int B, int K) { return (size_t)((B + 15) / 16) * K; }
+
+int head_dgrad_max_k() { return kHeadDgradMaxK; }
 
 int head_wgrad_splits(int B, int K) {
   const int cols = (K + kWgCols - 1) / kWgCols;

@@ -33,6 +33,7 @@ from __future__ import annotations
 import torch
 
 from ..optim.optimizers import _FlatOptimizer
+from .static_mlp import no_gc
 
 
 class GraphedStep:
@@ -56,7 +57,7 @@ class GraphedStep:
         self.graph = torch.cuda.CUDAGraph()
         self._set_capture(True)
         try:
-            with torch.cuda.graph(self.graph):
+            with no_gc(), torch.cuda.graph(self.graph):
                 self.loss = self._eager()
         finally:
             self._set_capture(False)

@@ -27,6 +27,8 @@ messages (BAR/communication.py:4-31).
 """
 from __future__ import annotations
 
+import contextlib
+import gc
 from dataclasses import dataclass
 
 import torch
@@ -48,6 +50,21 @@ class OptimConfig:
     eps: float = 1e-8
 
 
+@contextlib.contextmanager
+def no_gc():
+    """No Python garbage collection during a graph capture: a collection there can
+    destroy an unreachable engine's captured graphs, and destroying a graph exec on
+    the capturing thread invalidates the capture (the process aborts)."""
+    gc.collect()
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        yield
+    finally:
+        if was:
+            gc.enable()
+
+
 class _Segment:
     """A stretch of kernel launches replayed from a captured hipGraph after warmup."""
 
@@ -65,7 +82,7 @@ class _Segment:
             g = torch.cuda.CUDAGraph()
             # thread_local: other host threads (RCCL / gloo progress, watchdogs) may keep
             # using the HIP runtime while this thread captures
-            with torch.cuda.graph(g, capture_error_mode="thread_local"):
+            with no_gc(), torch.cuda.graph(g, capture_error_mode="thread_local"):
                 self.fn()
             self.graph = g
         self.graph.replay()
@@ -80,7 +97,8 @@ class StaticMLPEngine:
                  process_group=None, world_size: int | None = None, bucket_cap_elems: int = 8 << 20,
                  use_graphs: bool = True, average_grads: bool = True, use_head_kernels: bool = True,
                  shard_optimizer: bool | None = None, overlap_optimizer: bool = False, wgrad_combine: bool = True,
-                 fuse_optimizer: bool | None = None, library_gemms: bool | None = None):
+                 fuse_optimizer: bool | None = None, library_gemms: bool | None = None,
+                 fuse_head_dgrad: bool = False):
         from ..models.mlp import MLP
 
         if not isinstance(model, MLP):
@@ -161,6 +179,14 @@ class StaticMLPEngine:
         # transposed-read wgrad, for <= 64 (padded) classes
         self.use_head = (npad[-1] % 16 == 0 and npad[-1] <= 64 and self.layers[-1].in_features % 8 == 0
                          and use_head_kernels)
+        # fuse_head_dgrad: the head kernel also runs the head's dgrad (dz_{L-1} =
+        # dlogits W * act') from its LDS copy of h_{L-1}, instead of a K = 16 GEMM that
+        # re-reads h_{L-1}.  Off by default: measured on MI355X at 4096 x 4096 it is
+        # not faster (head.hip header)
+        self.head_dgrad = (bool(fuse_head_dgrad) and self.use_head and L >= 2
+                           and self.layers[-1].in_features <= self.C.head_dgrad_max_k())
+        self._head_db_ws = (torch.empty(self.C.head_dgrad_ws_floats(B, self.layers[-1].in_features),
+                                        dtype=torch.float32, device=self.device) if self.head_dgrad else None)
         # [loss_sum, correct] -- one pair per 16-row workgroup of the head kernel
         nslots = (B + 15) // 16 if self.use_head else 1
         self.stats = torch.zeros(nslots, 2, dtype=torch.float32, device=dev)
@@ -276,7 +302,13 @@ class StaticMLPEngine:
 
     def _loss(self):
         L = len(self.layers)
-        if self.use_head:   # last Linear + softmax-xent + argmax in one launch
+        if self.use_head:   # last Linear + softmax-xent + argmax (+ the head's dgrad) in one launch
+            if self.head_dgrad:
+                self.C.head_fwd_xent(self.h[L - 1], self.W[L - 1], self.bias[L - 1], self.labels, self.h[L],
+                                     self.dz[L], self.stats, self.num_classes, 1.0 / self.B, dh=self.dz[L - 1],
+                                     dbias=self.db[L - 2], dgrad_epi=self._dgrad_epi[L - 1],
+                                     dbias_ws=self._head_db_ws)
+                return
             self.C.head_fwd_xent(self.h[L - 1], self.W[L - 1], self.bias[L - 1], self.labels, self.h[L], self.dz[L],
                                  self.stats, self.num_classes, 1.0 / self.B)
             return
@@ -388,7 +420,7 @@ class StaticMLPEngine:
             if l in triggers:
                 self._cut_buckets.append(triggers[l])
                 pieces.append([])
-            if l > 0:
+            if l > 0 and not (self.head_dgrad and l == L - 1):   # (else done by the head kernel)
                 pieces[-1].append(lambda l=l: self._dgrad(l))
         self._cut_buckets.append(len(self.buckets) - 1)
 

@@ -265,6 +265,46 @@ def test_head_fwd_xent(B, K, ncls, ld):
     assert dl[:, ncls:].float().abs().max().item() == 0.0
 
 
+@pytest.mark.parametrize("epi", ["drelu", "dsigmoid", "none"])
+@pytest.mark.parametrize("B,K,ncls,ld", [(4096, 4096, 10, 16), (1000, 784, 10, 16), (70, 520, 40, 48)])
+def test_head_fwd_xent_fused_dgrad(B, K, ncls, ld, epi):
+    """The head kernel's fused dgrad: dh = (dlogits W) * act'(h) from its LDS copy of h,
+    plus the previous layer's bias gradient (column sums of dh), vs fp32 PyTorch on the
+    kernel's own bf16 dlogits; the loss path is unchanged by the fusion."""
+    torch.manual_seed(4)
+    h = torch.randn(B, K, device="cuda")
+    if epi == "drelu":
+        h = h.relu()
+    elif epi == "dsigmoid":
+        h = h.sigmoid()
+    h = h.bfloat16()
+    W = torch.zeros(ld, K, device="cuda")
+    W[:ncls] = torch.randn(ncls, K, device="cuda") * K ** -0.5
+    W = W.bfloat16()
+    bias = torch.zeros(ld, device="cuda")
+    y = torch.randint(0, ncls, (B,), device="cuda")
+    dl, dl2 = (torch.empty(B, ld, device="cuda", dtype=torch.bfloat16) for _ in range(2))
+    st, st2 = torch.zeros((B + 15) // 16, 2, device="cuda"), torch.zeros((B + 15) // 16, 2, device="cuda")
+    dh = torch.full((B, K), 7.0, device="cuda").bfloat16()
+    db = torch.zeros(K, device="cuda")
+    cc = C()
+    code = {"drelu": cc.EPI_DRELU, "dsigmoid": cc.EPI_DSIGMOID, "none": cc.EPI_NONE}[epi]
+    ws = torch.empty(cc.head_dgrad_ws_floats(B, K), device="cuda")
+    cc.head_fwd_xent(h, W, bias, y, None, dl, st, ncls, 1.0 / B, dh=dh, dbias=db, dgrad_epi=code, dbias_ws=ws)
+    cc.head_fwd_xent(h, W, bias, y, None, dl2, st2, ncls, 1.0 / B)
+    assert torch.equal(dl, dl2) and torch.equal(st, st2)
+    ref = dl.float()[:, :ncls] @ W.float()[:ncls]
+    hf = h.float()
+    if epi == "drelu":
+        ref = ref * (hf > 0)
+    elif epi == "dsigmoid":
+        ref = ref * hf * (1 - hf)
+    scale = ref.abs().max().item()
+    assert (dh.float() - ref).abs().max().item() <= 1e-2 * scale
+    cs = dh.float().sum(0)
+    torch.testing.assert_close(db, cs, rtol=1e-3, atol=1e-4 * cs.abs().max().item())
+
+
 @pytest.mark.parametrize("splits", [1, 3, 0])
 @pytest.mark.parametrize("B,K,ld,rows", [(4096, 4096, 16, 16), (1000, 784, 16, 16), (300, 520, 48, 40)])
 def test_head_wgrad(splits, B, K, ld, rows):

@@ -200,3 +200,25 @@ def test_library_gemm_engine_matches_native_engine():
     for a, b in zip(l1, l2):
         assert abs(a - b) < 1e-2 * max(1.0, abs(b)), (l1, l2)
     torch.testing.assert_close(e1.flat.master, e2.flat.master, rtol=2e-2, atol=2e-3)
+
+
+def test_fused_head_dgrad_engine_matches_separate_dgrad():
+    """fuse_head_dgrad=True (the head kernel writes dz_{L-1} and the previous bias
+    gradient) trains exactly like the separate K = 16 dgrad GEMM path."""
+    torch.manual_seed(0)
+    B = 512
+    m1, m2 = mlp3(784, 1024, 10), mlp3(784, 1024, 10)
+    m2.load_state_dict(m1.state_dict())
+    cfg = OptimConfig("sgd", lr=0.05, momentum=0.9)
+    e1 = StaticMLPEngine(m1, B, cfg, use_graphs=True, fuse_head_dgrad=True)
+    e2 = StaticMLPEngine(m2, B, cfg, use_graphs=True, fuse_head_dgrad=False)
+    assert e1.head_dgrad and not e2.head_dgrad
+    g = torch.Generator(device="cuda").manual_seed(6)
+    for i in range(5):
+        x = torch.randn(B, 784, device="cuda", generator=g).bfloat16()
+        y = torch.randint(0, 10, (B,), device="cuda", generator=g)
+        for e in (e1, e2):
+            e.load_batch(x, y)
+            e.step()
+    torch.cuda.synchronize()
+    torch.testing.assert_close(e1.flat.master, e2.flat.master, rtol=1e-3, atol=1e-4)
