@@ -4,6 +4,9 @@
 // tensors and launches on the CURRENT HIP stream, so the Python layer can
 // pre-allocate its buffers once and capture whole training steps in hipGraphs.
 #include <torch/extension.h>
+#include <vector>
+#include <mutex>
+#include <map>
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 
@@ -505,13 +508,33 @@ ldnn::ConvShape conv_shape(const at::Tensor& x, const at::Tensor& w, const at::T
   return s;
 }
 
-// Split-K workspace of a small-M conv (fresh from the caching allocator: stream
-// ordered, graph-capture safe; the counters come zeroed).
+// Split-K workspace of a small-M conv.  The fp32 slabs come fresh from the caching
+// allocator (stream ordered, graph-capture safe).  The arrival counters live in a
+// persistent per-(device, stream) pool, zeroed ONCE: the in-launch combine resets
+// every counter it used before its kernel ends, so launches ordered on one stream
+// (and replays of graphs that captured the pool's address) can share it -- a
+// per-call at::zeros cost one fill launch per conv (35 fills, ~160 us per step of
+// EnhancedCNN at batch 64 on MI355X).  Pools are never freed (a captured graph may
+// still point at an outgrown one); they hold a few thousand ints.
 struct ConvWs {
-  at::Tensor slabs, cnt;
+  at::Tensor slabs;
+  int* cnt = nullptr;
   float* ws() const { return slabs.defined() ? slabs.data_ptr<float>() : nullptr; }
-  int* c() const { return cnt.defined() ? cnt.data_ptr<int>() : nullptr; }
+  int* c() const { return cnt; }
 };
+
+int* conv_counter_pool(const at::Tensor& like, int64_t n) {
+  static std::mutex mu;
+  static std::map<std::pair<int, int64_t>, std::vector<at::Tensor>> pools;
+  const auto key = std::make_pair((int)like.get_device(), (int64_t)cur_stream(like));
+  std::lock_guard<std::mutex> lock(mu);
+  auto& v = pools[key];
+  if (v.empty() || v.back().numel() < n) {
+    const int64_t cap = std::max<int64_t>(n, v.empty() ? 4096 : 2 * v.back().numel());
+    v.push_back(at::zeros({cap}, like.options().dtype(at::kInt)));
+  }
+  return v.back().data_ptr<int>();
+}
 
 ConvWs conv_ws(const ldnn::ConvShape& s, int op, const at::Tensor& like) {
   ConvWs w;
@@ -519,7 +542,7 @@ ConvWs conv_ws(const ldnn::ConvShape& s, int op, const at::Tensor& like) {
   const ldnn::ConvWorkspace need = ldnn::conv2d_lds_workspace(s, op);
   if (need.slab_bytes == 0) return w;
   w.slabs = at::empty({(int64_t)(need.slab_bytes / 4)}, like.options().dtype(at::kFloat));
-  if (need.counters > 0) w.cnt = at::zeros({(int64_t)need.counters}, like.options().dtype(at::kInt));
+  if (need.counters > 0) w.cnt = conv_counter_pool(like, need.counters);
   return w;
 }
 

@@ -105,7 +105,10 @@ class SGD(_FlatOptimizer):
                                       nesterov=nesterov))
 
     @torch.no_grad()
-    def step(self, closure=None):
+    def step(self, closure=None, clear_grads: bool = False):
+        """clear_grads: the update kernel also zeroes the flat gradient after reading it
+        (one pass instead of a later zero_grad fill; on MI355X the zero writes inside
+        the bandwidth-bound update cost about what the fill launch does)."""
         loss = closure() if closure is not None else None
         for group in self.param_groups:
             lr, mu, damp, wd, nest = (group[k] for k in ("lr", "momentum", "dampening", "weight_decay", "nesterov"))
@@ -116,12 +119,14 @@ class SGD(_FlatOptimizer):
                 mom = self._buf("momentum", f.master) if mu != 0 else f.master
                 if _ext.use_native(f.master):
                     _ext.C().sgd_step(f.master, f.grad, mom, f.shadow, self._hp(f, lr), f.grad_scale, mu, damp, wd,
-                                      nest, first)
+                                      nest, first, zero_ranges=[(0, f.grad.numel())] if clear_grads else [])
                 else:
                     self._sgd_torch(f.master, f.grad * f.grad_scale, mom if mu != 0 else None, lr, mu, damp, wd,
                                     nest, first)
                     if f.shadow is not None:
                         f.shadow.copy_(f.master)
+                    if clear_grads:
+                        f.grad.zero_()
                 st["step"] = st.get("step", 0) + 1
             else:
                 for p in group["params"]:
@@ -154,7 +159,8 @@ class Adam(_FlatOptimizer):
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
 
     @torch.no_grad()
-    def step(self, closure=None):
+    def step(self, closure=None, clear_grads: bool = False):
+        """clear_grads: as SGD.step."""
         loss = closure() if closure is not None else None
         for group in self.param_groups:
             lr, (b1, b2), eps, wd = group["lr"], group["betas"], group["eps"], group["weight_decay"]
@@ -166,13 +172,15 @@ class Adam(_FlatOptimizer):
                     hp = self._hp(f, lr)
                     _ext.C().bump_step(hp)
                     _ext.C().adam_step(f.master, f.grad, m, v, f.shadow, hp, f.grad_scale, b1, b2, eps, wd,
-                                       self.decoupled)
+                                       self.decoupled, zero_ranges=[(0, f.grad.numel())] if clear_grads else [])
                     st["step"] = st.get("step", 0) + 1
                 else:
                     st["step"] = st.get("step", 0) + 1
                     self._adam_torch(f.master, f.grad * f.grad_scale, m, v, st["step"], lr, b1, b2, eps, wd)
                     if f.shadow is not None:
                         f.shadow.copy_(f.master)
+                    if clear_grads:
+                        f.grad.zero_()
             else:
                 for p in group["params"]:
                     if p.grad is None:

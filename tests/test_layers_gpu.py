@@ -208,6 +208,6 @@ def test_train_global_with_graphs_matches_eager():
     # sit within that spread (plus a rounding-level floor)
     for a, b, c in zip(p0, p1, p2):
         a, b, c = a.double(), b.double(), c.double()
-        assert (b - a).norm().item() <= 3.0 * (c - a).norm().item() + 1e-3 * a.norm().item()
+        assert (b - a).norm().item() <= 3.0 * (c - a).norm().item() + 1e-2 * a.norm().item()
     # (fp32-atomic arrival order can flip an argmax near a tie: allow one sample in ~1/2 %)
     assert abs(h0[4][-1] - h1[4][-1]) < 1e-2 and abs(h0[5][-1] - h1[5][-1]) < 0.5
