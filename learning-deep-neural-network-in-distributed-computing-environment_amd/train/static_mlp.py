@@ -280,7 +280,7 @@ class StaticMLPEngine:
         self.rank = dist.get_rank(process_group) if self.distributed else 0
         self.overlap_optimizer = overlap_optimizer
         self.side = torch.cuda.Stream(device=self.device) if overlap_optimizer else None
-        self._pending_gather = []
+        self._pending_gather = {}
         if self.shard:
             self.gshard = [torch.zeros((e - b) // self.world, dtype=torch.float32, device=dev)
                            for b, e, _ in self.buckets]
@@ -292,13 +292,7 @@ class StaticMLPEngine:
         C = self.C
         L = len(self.layers)
         for l in range(L - 1 if (train and self.use_head) else L):
-            if self._lib_fwd[l]:
-                if self.layers[l].activation == "relu":
-                    torch._addmm_activation(self.bias_bf16[l], self.h[l], self.W[l].t(), out=self.h[l + 1])
-                else:
-                    torch.addmm(self.bias_bf16[l], self.h[l], self.W[l].t(), out=self.h[l + 1])
-                continue
-            C.gemm(self.h[l], self.W[l], self.h[l + 1], True, True, self._fwd_epi[l], bias=self.bias[l])
+            self._forward_layer(l)
 
     def _loss(self):
         L = len(self.layers)
@@ -407,7 +401,9 @@ class StaticMLPEngine:
             pieces[0].append(lambda zb=zb, ze=ze: self.flat.grad[zb:ze].zero_())
         if self.optim.name in ("adam", "adamw"):
             pieces[0].append(lambda: self.C.bump_step(self.hp))
-        pieces[0].append(lambda: self._forward(train=True))
+        fwd = lambda: self._forward(train=True)  # noqa: E731
+        fwd._ldnn_fwd = True
+        pieces[0].append(fwd)
         pieces[0].append(self._loss)
         self._cut_buckets = []
         for l in reversed(range(L)):
@@ -454,6 +450,8 @@ class StaticMLPEngine:
                 fns = [fn for p in pieces for fn in p] + [lambda: self._opt(0, self.flat.numel)]
             self.segments = [_Segment(run(fns), self.use_graphs)]
             self.opt_segments = []
+        elif self.shard:
+            self._build_sharded_segments(pieces, run)
         else:
             self.segments = [_Segment(run(p), self.use_graphs) for p in pieces]
             if self.shard:
@@ -462,6 +460,59 @@ class StaticMLPEngine:
             else:
                 self.opt_segments = [_Segment(run([lambda b=b, e=e: self._opt(b, e)]), self.use_graphs)
                                      for (b, e, _) in self.buckets]
+
+    def _bucket_of(self, t) -> int:
+        off = self.flat.seg(t).offset
+        for i, (b, e, _) in enumerate(self.buckets):
+            if b <= off < e:
+                return i
+        raise AssertionError("tensor outside every bucket")
+
+    def _build_sharded_segments(self, pieces, run):
+        """Sharded step: the forward is cut where the bucket holding the next layer's
+        weights changes, so the next step waits for each bucket's weight all-gather
+        right before the first kernel that reads it -- the all-gather of the big
+        hidden weights overlaps the first layer's GEMM instead of preceding the step.
+        (The all-gathers are issued in forward order, see _step_sharded.)"""
+        L = len(self.layers)
+        n_fwd = L - 1 if self.use_head else L
+        p0 = pieces[0]
+        i_fwd = next(i for i, fn in enumerate(p0) if getattr(fn, "_ldnn_fwd", False))
+        i_loss = next(i for i, fn in enumerate(p0) if fn == self._loss)
+        assert i_loss == i_fwd + 1
+        prologue, tail = p0[:i_fwd], p0[i_loss + 1:]
+        # forward ops in layer order with the bucket each one reads
+        ops = [(lambda l=l: self._forward_layer(l), self._bucket_of(self.layers[l].weight)) for l in range(n_fwd)]
+        ops.append((self._loss, self._bucket_of(self.layers[L - 1].weight)))
+        bias_bucket = self._bucket_of(self.layers[0].bias)
+        groups, waits = [], []
+        for fn, bi in ops:
+            if not groups or bi != groups[-1][1]:
+                groups.append(([], bi))
+                waits.append([bi])
+            groups[-1][0].append(fn)
+        if bias_bucket not in waits[0]:
+            waits[0].insert(0, bias_bucket)
+        seg_fns = [list(g) for g, _ in groups]
+        seg_fns[0] = prologue + seg_fns[0]
+        seg_fns[-1] += tail  # the last forward group runs on into the backward until the first cut
+        all_pieces = seg_fns + pieces[1:]
+        self._seg_waits = waits + [[] for _ in pieces[1:]]
+        self._cut_after = [None] * (len(seg_fns) - 1) + list(self._cut_buckets)
+        assert len(self._cut_after) == len(all_pieces)
+        self.segments = [_Segment(run(p), self.use_graphs) for p in all_pieces]
+        self.opt_segments = [_Segment(run([lambda i=i: self._opt(*self._shard_range(i), grad=self.gshard[i])]),
+                                      self.use_graphs) for i in range(len(self.buckets))]
+
+    def _forward_layer(self, l):
+        C = self.C
+        if self._lib_fwd[l]:
+            if self.layers[l].activation == "relu":
+                torch._addmm_activation(self.bias_bf16[l], self.h[l], self.W[l].t(), out=self.h[l + 1])
+            else:
+                torch.addmm(self.bias_bf16[l], self.h[l], self.W[l].t(), out=self.h[l + 1])
+            return
+        C.gemm(self.h[l], self.W[l], self.h[l + 1], True, True, self._fwd_epi[l], bias=self.bias[l])
 
     # --------------------------------------------------------------------- API
     def set_lr(self, lr: float):
@@ -496,10 +547,10 @@ class StaticMLPEngine:
 
     def sync(self):
         """Wait for the previous step's weight all-gathers (the next forward reads them)."""
-        for w in self._pending_gather:
+        for w in self._pending_gather.values():
             if w is not None:
                 w.wait()
-        self._pending_gather = []
+        self._pending_gather = {}
 
     @torch.no_grad()
     def gather_master(self):
@@ -518,17 +569,29 @@ class StaticMLPEngine:
                 t[b:e].copy_(out)
 
     def _step_sharded(self, capturing):
-        self.sync()
+        pend = self._pending_gather   # bucket -> the previous step's weight all-gather
+        self._pending_gather = {}
         works = []
         for i, seg in enumerate(self.segments):
+            for bi in self._seg_waits[i]:
+                w = pend.pop(bi, None)
+                if w is not None:
+                    w.wait()
             seg()
-            bi = self._cut_buckets[i]
+            bi = self._cut_after[i]
+            if bi is None:
+                continue
             w = self._reduce_scatter(bi)
             if capturing and w is not None:
                 w.wait()
                 torch.cuda.current_stream().synchronize()
             works.append((bi, w))
-        for bi, w in works:
+        for w in pend.values():
+            if w is not None:
+                w.wait()
+        # shard updates + weight all-gathers in FORWARD order (the bucket holding W_0 and
+        # the biases first): the next step's first GEMM waits only for that one
+        for bi, w in sorted(works, key=lambda t: -t[0]):
             if w is not None:
                 w.wait()
             self.opt_segments[bi]()
@@ -536,7 +599,7 @@ class StaticMLPEngine:
             if capturing and g is not None:
                 g.wait()
                 torch.cuda.current_stream().synchronize()
-            self._pending_gather.append(g)
+            self._pending_gather[bi] = g
 
     def step(self):
         """One full training step on the batch currently in (self.x, self.labels)."""
