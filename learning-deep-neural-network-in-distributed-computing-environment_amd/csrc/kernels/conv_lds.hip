@@ -36,6 +36,7 @@
 #include <cstdlib>
 
 #include "ldnn_common.h"
+#include "ldnn_fastdiv.h"
 #include "ldnn_gemm_tile.h"
 #include "ldnn_kernels.h"
 
@@ -45,24 +46,6 @@ namespace convlds {
 
 constexpr uint32_t kOOB = 0x80000000u;      // >= num_records: reads as zero
 constexpr int kSlabBytes4 = 16 * 256 * 16;  // one 4-wave workgroup's fp32 accumulators
-
-struct FastDiv {  // n / d for 0 <= n < 2^31 as (umulhi(n, m) + n) >> s
-  uint32_t m, s;
-};
-
-FastDiv make_fastdiv(uint32_t d) {
-  FastDiv f;
-  if (d == 0) d = 1;  // an empty parity class: never divided by
-  uint32_t s = 0;
-  while ((1ull << s) < d) ++s;
-  f.s = s;
-  f.m = (uint32_t)(((1ull << 32) * ((1ull << s) - d)) / d + 1);
-  return f;
-}
-
-__device__ __forceinline__ int fdiv(int n, const FastDiv& f) {
-  return (int)((__umulhi((uint32_t)n, f.m) + (uint32_t)n) >> f.s);
-}
 
 struct LArgs {
   ConvShape s;

@@ -1,0 +1,26 @@
+#!/bin/bash
+# Host-side AddressSanitizer + UndefinedBehaviorSanitizer build and run of the native
+# planning code (tests/native/host_selftest.cpp).  Each -fsanitize= goes after
+# -Xarch_host: only the HOST half of every hipcc compile is instrumented; the device
+# code is built normally and never launched (no GPU needed, runs on the CPU box).
+set -euo pipefail
+ROOT="$(cd "$(dirname "$0")/.." && pwd)"
+CS="$ROOT/learning-deep-neural-network-in-distributed-computing-environment_amd/csrc"
+OUT="$ROOT/build/host_selftest"
+mkdir -p "$OUT"
+HIPCC=${HIPCC:-/opt/rocm/bin/hipcc}
+SAN="-Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host -fno-sanitize-recover=all -Xarch_host -fno-omit-frame-pointer"
+FLAGS="--offload-arch=gfx950 -O1 -g -std=c++17 -I$CS/include $SAN"
+SRCS="conv_lds bn_pool head elementwise"
+pids=()
+for f in $SRCS; do
+  src="$CS/kernels/$f.hip"; obj="$OUT/$f.o"
+  if [ ! -f "$obj" ] || [ "$src" -nt "$obj" ] || [ -n "$(find "$CS/include" -newer "$obj" -name '*.h')" ]; then
+    $HIPCC $FLAGS -c "$src" -o "$obj" 2> "$OUT/$f.log" & pids+=($!)
+  fi
+done
+for p in "${pids[@]}"; do wait "$p"; done
+$HIPCC $FLAGS -c "$ROOT/tests/native/host_selftest.cpp" -x hip -o "$OUT/main.o" 2> "$OUT/main.log"
+$HIPCC --offload-arch=gfx950 -fno-gpu-sanitize -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined \
+  "$OUT"/*.o -o "$OUT/selftest"
+ASAN_OPTIONS=detect_leaks=0:abort_on_error=1 UBSAN_OPTIONS=print_stacktrace=1 "$OUT/selftest"
