@@ -546,8 +546,16 @@ ConvWs conv_ws(const ldnn::ConvShape& s, int op, const at::Tensor& like) {
   return w;
 }
 
-void conv_fwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& y, int64_t stride, int64_t pad,
-              const c10::optional<at::Tensor>& bias, int64_t epi) {
+float* fptr_opt(const c10::optional<at::Tensor>& t, int64_t n, const char* name);
+
+// Returns whether the following BatchNorm's statistics were accumulated and
+// finalized by the conv epilogue (bn_ws given, LDS-DMA path, no epilogue op).
+bool conv_fwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& y, int64_t stride, int64_t pad,
+              const c10::optional<at::Tensor>& bias, int64_t epi, const c10::optional<at::Tensor>& bn_ws,
+              const c10::optional<at::Tensor>& bn_gamma, const c10::optional<at::Tensor>& bn_beta,
+              const c10::optional<at::Tensor>& bn_running_mean, const c10::optional<at::Tensor>& bn_running_var,
+              const c10::optional<at::Tensor>& bn_save_mean, const c10::optional<at::Tensor>& bn_save_invstd,
+              double bn_eps, double bn_momentum, const c10::optional<at::Tensor>& bn_num_batches) {
   check_dev(x, at::kBFloat16, "x");
   check_dev(w, at::kBFloat16, "w");
   check_dev(y, at::kBFloat16, "y");
@@ -561,8 +569,36 @@ void conv_fwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& y, int
   TORCH_CHECK(epi == ldnn::EPI_NONE || b != nullptr, "conv: bias epilogue needs a bias");
   c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   const ConvWs ws = conv_ws(s, 0, x);
-  check(ldnn::conv2d_fwd(s, bf16_ptr(x), bf16_ptr(w), bf16_mut(y), b, (int)epi, cur_stream(x), ws.ws(), ws.c()),
+  ldnn::BnFin fin{};
+  const ldnn::BnFin* finp = nullptr;
+  if (bn_ws.has_value()) {
+    TORCH_CHECK(epi == ldnn::EPI_NONE, "conv: fused BN statistics need a plain (EPI_NONE) conv");
+    const int C = s.K;
+    ldnn::BnArgs a{};
+    a.M = s.N * s.P * s.Q;
+    a.C = C;
+    a.gamma = fptr_opt(bn_gamma, C, "bn_gamma");
+    a.beta = fptr_opt(bn_beta, C, "bn_beta");
+    a.running_mean = fptr_opt(bn_running_mean, C, "bn_running_mean");
+    a.running_var = fptr_opt(bn_running_var, C, "bn_running_var");
+    a.save_mean = fptr_opt(bn_save_mean, C, "bn_save_mean");
+    a.save_invstd = fptr_opt(bn_save_invstd, C, "bn_save_invstd");
+    TORCH_CHECK(a.save_mean && a.save_invstd, "conv: fused BN statistics need save_mean / save_invstd");
+    a.ws = fptr_opt(bn_ws, ldnn::bn_workspace_floats(C), "bn_ws");
+    a.eps = (float)bn_eps;
+    a.momentum = (float)bn_momentum;
+    if (bn_num_batches.has_value()) {
+      check_dev(*bn_num_batches, at::kLong, "bn_num_batches");
+      a.num_batches = bn_num_batches->data_ptr<int64_t>();
+    }
+    fin = ldnn::bn_forward_fin_conv(a);
+    finp = &fin;
+  }
+  bool done = false;
+  check(ldnn::conv2d_fwd(s, bf16_ptr(x), bf16_ptr(w), bf16_mut(y), b, (int)epi, cur_stream(x), ws.ws(), ws.c(),
+                         finp, &done),
         "conv2d_fwd");
+  return done;
 }
 
 void conv_dgrad(const at::Tensor& dy, const at::Tensor& w, const at::Tensor& dx, int64_t stride, int64_t pad) {
@@ -608,7 +644,8 @@ void bn_fwd(const at::Tensor& x, const at::Tensor& y, const c10::optional<at::Te
             const c10::optional<at::Tensor>& gamma, const c10::optional<at::Tensor>& beta,
             const c10::optional<at::Tensor>& running_mean, const c10::optional<at::Tensor>& running_var,
             const at::Tensor& save_mean, const at::Tensor& save_invstd, const at::Tensor& ws, double eps,
-            double momentum, bool training, bool relu, const c10::optional<at::Tensor>& num_batches) {
+            double momentum, bool training, bool relu, const c10::optional<at::Tensor>& num_batches,
+            bool stats_ready) {
   check_dev(x, at::kBFloat16, "x");
   check_dev(y, at::kBFloat16, "y");
   TORCH_CHECK(x.dim() == 2 && x.is_contiguous() && y.sizes() == x.sizes() && y.is_contiguous(), "bn: [M][C] dense");
@@ -639,6 +676,11 @@ void bn_fwd(const at::Tensor& x, const at::Tensor& y, const c10::optional<at::Te
   if (num_batches.has_value() && training) {
     check_dev(*num_batches, at::kLong, "num_batches");
     a.num_batches = num_batches->data_ptr<int64_t>();
+  }
+  if (stats_ready) {  // the producing conv's epilogue already finalized scale / shift into ws
+    TORCH_CHECK(training, "bn: stats_ready is a training-mode path");
+    check(ldnn::bn_forward_apply(a, cur_stream(x)), "bn_forward_apply");
+    return;
   }
   check(ldnn::bn_forward(a, cur_stream(x)), "bn_forward");
 }
@@ -801,7 +843,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_fwd", &bn_fwd, py::arg("x"), py::arg("y"), py::arg("residual"), py::arg("gamma"), py::arg("beta"),
         py::arg("running_mean"), py::arg("running_var"), py::arg("save_mean"), py::arg("save_invstd"),
         py::arg("ws"), py::arg("eps"), py::arg("momentum"), py::arg("training"), py::arg("relu"),
-        py::arg("num_batches") = py::none());
+        py::arg("num_batches") = py::none(), py::arg("stats_ready") = false);
   m.def("bn_workspace_floats", &ldnn::bn_workspace_floats, "fp32 workspace of one BatchNorm (zero it once, keep it)",
         py::arg("C"));
   m.def("bn_bwd", &bn_bwd, py::arg("x"), py::arg("y"), py::arg("dy"), py::arg("dx"), py::arg("dres"),
@@ -812,7 +854,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("gap_fwd", &gap_fwd);
   m.def("gap_bwd", &gap_bwd);
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("stride"), py::arg("pad"),
-        py::arg("bias") = py::none(), py::arg("epi") = 0);
+        py::arg("bias") = py::none(), py::arg("epi") = 0, py::arg("bn_ws") = py::none(),
+        py::arg("bn_gamma") = py::none(), py::arg("bn_beta") = py::none(), py::arg("bn_running_mean") = py::none(),
+        py::arg("bn_running_var") = py::none(), py::arg("bn_save_mean") = py::none(),
+        py::arg("bn_save_invstd") = py::none(), py::arg("bn_eps") = 1e-5, py::arg("bn_momentum") = 0.1,
+        py::arg("bn_num_batches") = py::none());
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("stride"), py::arg("pad"));
   m.def("conv_wgrad", &conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("dw"), py::arg("stride"), py::arg("pad"),
         py::arg("beta") = 0.0);

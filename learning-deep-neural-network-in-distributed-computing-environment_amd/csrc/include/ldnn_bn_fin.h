@@ -1,0 +1,66 @@
+// BatchNorm statistics finalize, shared by the BN reduce kernel (bn_pool.hip) and
+// the conv forward epilogue that accumulates the following BN's statistics
+// (conv_lds.hip): the last of `nblk` contributing workgroups turns the fp32
+// totals into mean / invstd, running-stat EMA and the apply coefficients.
+#pragma once
+
+#include "ldnn_common.h"
+#include "ldnn_kernels.h"
+
+namespace ldnn {
+
+constexpr int kBnCopies = 8;  // accumulator copies of the conv-epilogue statistics path
+
+// Totals of every block are complete in `acc` when the last block draws its
+// ticket: the fp32 atomics execute at the memory side and every block waits
+// for its own (vmcnt) before adding to the ticket; the finalizer reads AND
+// clears the totals with atomic exchanges (memory-side too, so no cache can
+// hand it a stale line).
+// ncopies: the totals are spread over that many [2C] accumulator copies (summed here)
+template <bool BWD>
+__device__ __forceinline__ void bn_finalize_last(const BnFin& f, int M, int C, int nblk, int ncopies) {
+  __shared__ int last;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int t = __hip_atomic_fetch_add(f.ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = t == nblk - 1;
+    if (last) __hip_atomic_store(f.ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (!last) return;
+  const float invM = 1.f / (float)M;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    float S0 = 0.f, S1 = 0.f;
+    for (int k = 0; k < ncopies; ++k) {
+      S0 += atomicExch(f.acc + (size_t)k * 2 * C + c, 0.f);
+      S1 += atomicExch(f.acc + (size_t)k * 2 * C + C + c, 0.f);
+    }
+    const float gm = f.gamma ? f.gamma[c] : 1.f;
+    if constexpr (!BWD) {
+      const float m = S0 * invM;
+      const float var = fmaxf(S1 * invM - m * m, 0.f);
+      const float is = rsqrtf(var + f.eps);
+      f.save_mean[c] = m;
+      f.save_invstd[c] = is;
+      const float b = f.beta ? f.beta[c] : 0.f;
+      f.coef[c] = gm * is;
+      f.coef[C + c] = b - m * gm * is;
+      if (f.running_mean) {
+        f.running_mean[c] = (1.f - f.momentum) * f.running_mean[c] + f.momentum * m;
+        const float unb = M > 1 ? var * (float)M / (float)(M - 1) : var;
+        f.running_var[c] = (1.f - f.momentum) * f.running_var[c] + f.momentum * unb;
+      }
+    } else {
+      const float is = f.save_invstd[c];
+      const float A = gm * is, B = -gm * is * is * S1 * invM;
+      f.coef[c] = A;
+      f.coef[C + c] = B;
+      f.coef[2 * C + c] = -gm * is * S0 * invM - B * f.save_mean[c];
+      if (f.dgamma) f.dgamma[c] += S1;
+      if (f.dbeta) f.dbeta[c] += S0;
+    }
+  }
+  if (!BWD && threadIdx.x == 0 && f.num_batches) f.num_batches[0] += 1;
+}
+
+}  // namespace ldnn

@@ -76,8 +76,13 @@ struct ConvShape {
 };
 // ws / cnt: optional in-launch split-K workspace for small-M shapes (conv2d_lds_workspace);
 // without it those shapes run unsplit.
+struct BnFin;  // (BatchNorm finalize state, below)
+// bn (optional): also accumulate the following training-mode BatchNorm's statistics
+// over the bf16 outputs and finalize them; *bn_done reports whether that happened
+// (only the LDS-DMA path does it, for EPI_NONE).
 hipError_t conv2d_fwd(const ConvShape& s, const uint16_t* x, const uint16_t* w, uint16_t* y, const float* bias,
-                      int epi, hipStream_t st, float* ws = nullptr, int* cnt = nullptr);
+                      int epi, hipStream_t st, float* ws = nullptr, int* cnt = nullptr, const BnFin* bn = nullptr,
+                      bool* bn_done = nullptr);
 hipError_t conv2d_dgrad(const ConvShape& s, const uint16_t* dy, const uint16_t* w, uint16_t* dx, hipStream_t st,
                         float* ws = nullptr, int* cnt = nullptr);
 hipError_t conv2d_wgrad(const ConvShape& s, const uint16_t* dy, const uint16_t* x, float* dw, float beta,
@@ -85,7 +90,7 @@ hipError_t conv2d_wgrad(const ConvShape& s, const uint16_t* dy, const uint16_t* 
 // LDS-DMA fast path (conv_lds.hip): hipErrorNotSupported outside its shape set
 // (fwd needs C % 64 == 0, dgrad K % 64 == 0, stride 1 or 2).
 hipError_t conv2d_fwd_lds(const ConvShape& s, const uint16_t* x, const uint16_t* w, uint16_t* y, const float* bias,
-                          int epi, hipStream_t st, float* ws, int* cnt);
+                          int epi, hipStream_t st, float* ws, int* cnt, const BnFin* bn = nullptr);
 hipError_t conv2d_dgrad_lds(const ConvShape& s, const uint16_t* dy, const uint16_t* w, uint16_t* dx, hipStream_t st,
                             float* ws, int* cnt);
 hipError_t conv2d_wgrad_lds(const ConvShape& s, const uint16_t* dy, const uint16_t* x, float* dw, float beta,
@@ -122,6 +127,27 @@ struct BnArgs {
 };
 int bn_workspace_floats(int C);
 hipError_t bn_forward(const BnArgs& a, hipStream_t s);
+struct BnFin {
+  float* acc;                 // [2C] accumulators (left zeroed for the next call)
+  int* ticket;                // arrival counter (left zero)
+  const float* gamma;
+  const float* beta;
+  float* running_mean;
+  float* running_var;
+  float* save_mean;           // fwd: written; bwd: read
+  float* save_invstd;
+  float* coef;                // fwd: scale | shift ; bwd: A | B | D
+  float* dgamma;              // bwd: accumulated
+  float* dbeta;
+  int64_t* num_batches;       // fwd: += 1 (BatchNorm2d.num_batches_tracked), nullable
+  float eps, momentum;
+};
+// Training-mode forward finalize state of a BN (its ws accumulators / ticket / coef).
+BnFin bn_forward_fin(const BnArgs& a);
+// ... for a producing conv's epilogue (its kBnCopies accumulator copies in ws).
+BnFin bn_forward_fin_conv(const BnArgs& a);
+// The apply pass alone, with the scale / shift a fused statistics pass left in a.ws.
+hipError_t bn_forward_apply(const BnArgs& a, hipStream_t s);
 // dx (and optionally dres = upstream gradient after the ReLU mask, for the residual
 // branch); dgamma / dbeta are ACCUMULATED (flat gradient buffer)
 hipError_t bn_backward(const BnArgs& a, const uint16_t* dy, uint16_t* dx, uint16_t* dres, float* dgamma,

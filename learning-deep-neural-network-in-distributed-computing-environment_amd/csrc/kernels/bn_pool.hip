@@ -16,6 +16,7 @@
 
 #include "ldnn_common.h"
 #include "ldnn_kernels.h"
+#include "ldnn_bn_fin.h"
 
 namespace ldnn {
 
@@ -83,71 +84,6 @@ __device__ __forceinline__ void red_row(const bf16_t* __restrict__ x, const bf16
   }
 }
 
-// What the last reduce block to finish does with the totals (fused finalize).
-struct BnFin {
-  float* acc;                 // [2C] accumulators (left zeroed for the next call)
-  int* ticket;                // arrival counter (left zero)
-  const float* gamma;
-  const float* beta;
-  float* running_mean;
-  float* running_var;
-  float* save_mean;           // fwd: written; bwd: read
-  float* save_invstd;
-  float* coef;                // fwd: scale | shift ; bwd: A | B | D
-  float* dgamma;              // bwd: accumulated
-  float* dbeta;
-  int64_t* num_batches;       // fwd: += 1 (BatchNorm2d.num_batches_tracked), nullable
-  float eps, momentum;
-};
-
-// Totals of every block are complete in `acc` when the last block draws its
-// ticket: the fp32 atomics execute at the memory side and every block waits
-// for its own (vmcnt) before adding to the ticket; the finalizer reads AND
-// clears the totals with atomic exchanges (memory-side too, so no cache can
-// hand it a stale line).
-template <bool BWD>
-__device__ __forceinline__ void bn_finalize_last(const BnFin& f, int M, int C) {
-  __shared__ int last;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const int nblk = gridDim.x * gridDim.y;
-    const int t = __hip_atomic_fetch_add(f.ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = t == nblk - 1;
-    if (last) __hip_atomic_store(f.ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __syncthreads();
-  if (!last) return;
-  const float invM = 1.f / (float)M;
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    const float S0 = atomicExch(f.acc + c, 0.f), S1 = atomicExch(f.acc + C + c, 0.f);
-    const float gm = f.gamma ? f.gamma[c] : 1.f;
-    if constexpr (!BWD) {
-      const float m = S0 * invM;
-      const float var = fmaxf(S1 * invM - m * m, 0.f);
-      const float is = rsqrtf(var + f.eps);
-      f.save_mean[c] = m;
-      f.save_invstd[c] = is;
-      const float b = f.beta ? f.beta[c] : 0.f;
-      f.coef[c] = gm * is;
-      f.coef[C + c] = b - m * gm * is;
-      if (f.running_mean) {
-        f.running_mean[c] = (1.f - f.momentum) * f.running_mean[c] + f.momentum * m;
-        const float unb = M > 1 ? var * (float)M / (float)(M - 1) : var;
-        f.running_var[c] = (1.f - f.momentum) * f.running_var[c] + f.momentum * unb;
-      }
-    } else {
-      const float is = f.save_invstd[c];
-      const float A = gm * is, B = -gm * is * is * S1 * invM;
-      f.coef[c] = A;
-      f.coef[C + c] = B;
-      f.coef[2 * C + c] = -gm * is * S0 * invM - B * f.save_mean[c];
-      if (f.dgamma) f.dgamma[c] += S1;
-      if (f.dbeta) f.dbeta[c] += S0;
-    }
-  }
-  if (!BWD && threadIdx.x == 0 && f.num_batches) f.num_batches[0] += 1;
-}
-
 template <bool BWD, bool RELU>
 __global__ __launch_bounds__(256) void bn_reduce_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
                                                         const bf16_t* __restrict__ y, const float* __restrict__ mean,
@@ -204,7 +140,7 @@ __global__ __launch_bounds__(256) void bn_reduce_kernel(const bf16_t* __restrict
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's atomics have completed
-  bn_finalize_last<BWD>(fin, M, C);
+  bn_finalize_last<BWD>(fin, M, C, gridDim.x * gridDim.y, 1);
 }
 
 __global__ void bn_eval_coeff_kernel(const float* __restrict__ gamma, const float* __restrict__ beta,
@@ -432,34 +368,40 @@ __global__ void gap_bwd_kernel(const bf16_t* __restrict__ dy, bf16_t* __restrict
 //   backward accumulator | [6C, 9C) backward coefficients A, B, D | [10C]
 //   forward ticket | [10C + 16] backward ticket.
 // Accumulators and tickets are left zero by the reduce kernel's last block.
-int bn_workspace_floats(int C) { return 10 * C + 32; }
+//   [10C + 32, 26C + 32) kBnCopies x [2C] forward accumulators of the conv-epilogue
+//   statistics path (bn_forward_fin_conv).
+int bn_workspace_floats(int C) { return 10 * C + 32 + kBnCopies * 2 * C; }
 
-hipError_t bn_forward(const BnArgs& a, hipStream_t s) {
+BnFin bn_forward_fin(const BnArgs& a) {
+  const int C = a.C;
+  BnFin f{};
+  f.acc = a.ws + 2 * C;
+  f.ticket = reinterpret_cast<int*>(a.ws + 10 * C);
+  f.gamma = a.gamma;
+  f.beta = a.beta;
+  f.running_mean = a.running_mean;
+  f.running_var = a.running_var;
+  f.save_mean = a.save_mean;
+  f.save_invstd = a.save_invstd;
+  f.coef = a.ws;
+  f.num_batches = a.num_batches;
+  f.eps = a.eps;
+  f.momentum = a.momentum;
+  return f;
+}
+
+BnFin bn_forward_fin_conv(const BnArgs& a) {
+  BnFin f = bn_forward_fin(a);
+  f.acc = a.ws + 10 * a.C + 32;
+  return f;
+}
+
+hipError_t bn_forward_apply(const BnArgs& a, hipStream_t s) {
   const int M = a.M, C = a.C;
   if (C % 8) return hipErrorInvalidValue;
   if (M <= 0) return hipSuccess;
   const RedGeo g = red_geo(M, C);
   const dim3 grid(g.gx, g.gy);
-  if (a.training) {
-    BnFin f{};
-    f.acc = a.ws + 2 * C;
-    f.ticket = reinterpret_cast<int*>(a.ws + 10 * C);
-    f.gamma = a.gamma;
-    f.beta = a.beta;
-    f.running_mean = a.running_mean;
-    f.running_var = a.running_var;
-    f.save_mean = a.save_mean;
-    f.save_invstd = a.save_invstd;
-    f.coef = a.ws;
-    f.num_batches = a.num_batches;
-    f.eps = a.eps;
-    f.momentum = a.momentum;
-    bn_reduce_kernel<false, false><<<grid, 256, 0, s>>>(a.x, nullptr, nullptr, nullptr, nullptr, f.acc, M, C, g.rpb,
-                                                        g.lanes, g.rl, f);
-  } else {
-    bn_eval_coeff_kernel<<<(C + 255) / 256, 256, 0, s>>>(a.gamma, a.beta, a.running_mean, a.running_var, a.ws,
-                                                         a.ws + C, C, a.eps);
-  }
   const float* sc = a.ws;
   const float* sh = a.ws + C;
 #define LDNN_BN_APPLY(RES, RELU) \
@@ -473,6 +415,23 @@ hipError_t bn_forward(const BnArgs& a, hipStream_t s) {
   }
 #undef LDNN_BN_APPLY
   return hipGetLastError();
+}
+
+hipError_t bn_forward(const BnArgs& a, hipStream_t s) {
+  const int M = a.M, C = a.C;
+  if (C % 8) return hipErrorInvalidValue;
+  if (M <= 0) return hipSuccess;
+  const RedGeo g = red_geo(M, C);
+  const dim3 grid(g.gx, g.gy);
+  if (a.training) {
+    const BnFin f = bn_forward_fin(a);
+    bn_reduce_kernel<false, false><<<grid, 256, 0, s>>>(a.x, nullptr, nullptr, nullptr, nullptr, f.acc, M, C, g.rpb,
+                                                        g.lanes, g.rl, f);
+  } else {
+    bn_eval_coeff_kernel<<<(C + 255) / 256, 256, 0, s>>>(a.gamma, a.beta, a.running_mean, a.running_var, a.ws,
+                                                         a.ws + C, C, a.eps);
+  }
+  return bn_forward_apply(a, s);
 }
 
 hipError_t bn_backward(const BnArgs& a, const uint16_t* dy, uint16_t* dx, uint16_t* dres, float* dgamma,

@@ -251,10 +251,14 @@ void set_conv_impl(int impl) { g_conv_impl = impl; }
 int get_conv_impl() { return g_conv_impl; }
 
 hipError_t conv2d_fwd(const ConvShape& s, const uint16_t* x, const uint16_t* w, uint16_t* y, const float* bias,
-                      int epi, hipStream_t st, float* ws, int* cnt) {
+                      int epi, hipStream_t st, float* ws, int* cnt, const BnFin* bn, bool* bn_done) {
+  if (bn_done) *bn_done = false;
   if (g_conv_impl == 0) {
-    const hipError_t e = conv2d_fwd_lds(s, x, w, y, bias, epi, st, ws, cnt);
-    if (e != hipErrorNotSupported) return e;
+    const hipError_t e = conv2d_fwd_lds(s, x, w, y, bias, epi, st, ws, cnt, bn);
+    if (e != hipErrorNotSupported) {
+      if (bn_done) *bn_done = bn != nullptr && e == hipSuccess;
+      return e;
+    }
   }
   ConvArgs a{};
   a.s = s;

@@ -37,6 +37,7 @@
 
 #include "ldnn_common.h"
 #include "ldnn_fastdiv.h"
+#include "ldnn_bn_fin.h"
 #include "ldnn_gemm_tile.h"
 #include "ldnn_kernels.h"
 
@@ -67,6 +68,8 @@ struct LArgs {
   FastDiv f_cw[2], f_ch[2];      // stride-2 dgrad class rows: (W - pw + 1) / 2, (H - ph + 1) / 2
   float* ws;         // split-K: combine slabs (with cnt) or wgrad partial slabs [split][M][N] (without)
   int* cnt;          // split-K arrival counters of the in-launch combine
+  int bn_stats;      // fwd: accumulate + finalize the next BatchNorm's statistics (bn)
+  BnFin bn;
 };
 
 // Per-workgroup geometry: which rows its class covers and which taps it sums.
@@ -372,6 +375,69 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("" ::: "memory");
 }
 
+__device__ __forceinline__ int tiles_of(const LArgs& a) { return a.tiles_x; }
+
+// The following training-mode BatchNorm's statistics from this tile's bf16 outputs
+// (exactly the values BN reads): per channel sum and sum of squares over the
+// tile's valid rows -- 16 row lanes by shuffles, the WM wave rows through LDS --
+// then ONE pair of fp32 atomics per channel per tile, into one of kBnCopies
+// accumulator copies (tile % kBnCopies: 8x less same-address serialisation).  The
+// last of the grid's `tiles` workgroups sums the copies and finalizes (mean,
+// invstd, running-stat EMA, apply coefficients), so the BN needs no reduce pass.
+template <int WM, int WN>
+__device__ __forceinline__ void bn_stats_epilogue(const LArgs& a, const Geo& g, floatx4 (&acc)[4][4], int mbase,
+                                                  int n0, int wm, int wn, int lane, int tile, char* smem) {
+  constexpr int BN = WN * 64;
+  float* red = reinterpret_cast<float*>(smem);  // [WM][BN][2]
+  __syncthreads();  // every wave is done with the operand stages
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float s0[4] = {0.f, 0.f, 0.f, 0.f}, s1[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (mbase + i * 16 + (lane & 15) >= g.M) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float v = bf2f(f2bf(acc[j][i][r]));
+        s0[r] += v;
+        s1[r] += v * v;
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        s0[r] += __shfl_xor(s0[r], o, 64);
+        s1[r] += __shfl_xor(s1[r], o, 64);
+      }
+    }
+    if ((lane & 15) == 0) {
+      const int lc = wn * 64 + j * 16 + 4 * (lane >> 4);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        red[(wm * BN + lc + r) * 2] = s0[r];
+        red[(wm * BN + lc + r) * 2 + 1] = s1[r];
+      }
+    }
+  }
+  __syncthreads();
+  float* accc = a.bn.acc + (size_t)(tile % kBnCopies) * 2 * a.N;
+  for (int t = threadIdx.x; t < BN; t += blockDim.x) {
+    const int c = n0 + t;
+    if (c >= a.N) continue;
+    float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+    for (int q = 0; q < WM; ++q) {
+      s0 += red[(q * BN + t) * 2];
+      s1 += red[(q * BN + t) * 2 + 1];
+    }
+    atomicAdd(accc + c, s0);
+    atomicAdd(accc + a.N + c, s1);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's atomics have completed
+  bn_finalize_last<false>(a.bn, g.M, a.N, tiles_of(a), kBnCopies);
+}
+
 // Direct epilogue with the class row remap: GEMM row m of a stride-2 dgrad
 // class is pixel (n, 2*h2 + hoff, 2*w2 + woff) of dx.
 __device__ __forceinline__ void store_remapped(const LArgs& a, const Geo& g, floatx4 (&acc)[4][4], int mbase,
@@ -552,6 +618,9 @@ __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void conv_lds_kernel(LArgs a,
   p.bias = a.bias;
   p.beta = a.beta;
   epilogue<EPI, OUT_F32, 4, 4>(p, acc, mb, nbase, lane);
+  if constexpr (!DGRAD && !OUT_F32 && EPI == EPI_NONE) {
+    if (a.bn_stats) bn_stats_epilogue<WM, WN>(a, g, acc, mb, n0, wm, wn, lane, blockIdx.x, smem);
+  }
 }
 
 // out[i] = sum_s ws[s][i] (+ beta * out[i]): the cross-CU reduction of wgrad slabs.
@@ -770,8 +839,12 @@ hipError_t slab_sum(const float* ws, float* out, int64_t n4, int splits, float b
 // Stems and other small-C convolutions (C in {8, 16, 32}, e.g. the 7x7 ResNet stem
 // on 3 -> 8 padded channels): K-tiles span several taps, one 256x64 / 128x128 tile.
 hipError_t conv2d_fwd_lds_small_c(const ConvShape& s, const uint16_t* x, const uint16_t* w, uint16_t* y,
-                                  const float* bias, int epi, hipStream_t st) {
+                                  const float* bias, int epi, hipStream_t st, const BnFin* bn) {
   LArgs a = base_args(s);
+  if (bn != nullptr && epi == EPI_NONE) {
+    a.bn_stats = 1;
+    a.bn = *bn;
+  }
   a.out = y;
   a.bias = bias;
   a.M = s.N * s.P * s.Q;
@@ -789,16 +862,21 @@ hipError_t conv2d_fwd_lds_small_c(const ConvShape& s, const uint16_t* x, const u
 }
 
 hipError_t conv2d_fwd_lds(const ConvShape& s, const uint16_t* x, const uint16_t* w, uint16_t* y, const float* bias,
-                          int epi, hipStream_t st, float* ws, int* cnt) {
+                          int epi, hipStream_t st, float* ws, int* cnt, const BnFin* bn) {
   if (!shape_ok(s)) return hipErrorNotSupported;
+  if (bn != nullptr && epi != EPI_NONE) return hipErrorInvalidValue;
   if (s.C == 8 || s.C == 16 || s.C == 32) {
-    if (s.N * s.P * s.Q <= 0) return hipSuccess;
-    return conv2d_fwd_lds_small_c(s, x, w, y, bias, epi, st);
+    if (s.N * s.P * s.Q <= 0) return hipErrorNotSupported;
+    return conv2d_fwd_lds_small_c(s, x, w, y, bias, epi, st, bn);
   }
   if (s.C % 64 != 0) return hipErrorNotSupported;
-  if (s.N * s.P * s.Q <= 0) return hipSuccess;
+  if (s.N * s.P * s.Q <= 0) return bn != nullptr ? hipErrorNotSupported : hipSuccess;
   Plan pl = plan_fwd(s);
   LArgs a = base_args(s);
+  if (bn != nullptr) {
+    a.bn_stats = 1;
+    a.bn = *bn;
+  }
   a.out = y;
   a.bias = bias;
   a.M = s.N * s.P * s.Q;

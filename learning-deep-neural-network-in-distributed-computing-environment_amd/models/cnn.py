@@ -13,12 +13,16 @@ from __future__ import annotations
 
 import torch.nn as nn
 
-from .layers import AdaptiveAvgPool2d, AvgPool2d, BatchNorm2d, Conv2d, Linear, MaxPool2d, ReLU
+from .layers import AdaptiveAvgPool2d, AvgPool2d, BatchNorm2d, Conv2d, Linear, MaxPool2d, ReLU, pair_conv_bn
 
 
 class ConvBNReLU(nn.Sequential):
     """Sequential(conv, bn, relu) -- same state_dict keys (prep.0 / prep.1) -- whose
     BN and ReLU run as one fused pass."""
+
+    def __init__(self, *mods):
+        super().__init__(*mods)
+        pair_conv_bn(self[0], self[1])
 
     def forward(self, x):
         return self[1].act(self[0](x), relu=True)
@@ -41,6 +45,10 @@ class ResBlock(nn.Module):
                 BatchNorm2d(out_channels),
             )
         self.relu = ReLU()
+        pair_conv_bn(self.conv1, self.bn1)
+        pair_conv_bn(self.conv2, self.bn2)
+        if len(self.shortcut):
+            pair_conv_bn(self.shortcut[0], self.shortcut[1])
 
     def forward(self, x):
         # BAR/model.py:67-72 with BN+ReLU and BN+residual-add+ReLU each fused into one pass

@@ -8,6 +8,8 @@ shadow + flat gradient buffer) by ``ldnn.prepare`` / ``FlatParams(model)``.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 
@@ -63,9 +65,28 @@ class Conv2d(nn.Conv2d):
         assert activation in ("none", "relu")
         self.activation = activation
         self._ldnn_flat = None
+        self.__dict__["_ldnn_stats_bn"] = None  # (not a submodule: state_dict keys unchanged)
 
     def forward(self, x):
-        return LF.conv2d(x, self, relu=self.activation == "relu")
+        return LF.conv2d(x, self, relu=self.activation == "relu",
+                         bn=self._ldnn_stats_bn if FUSE_BN_STATS else None)
+
+
+# Conv-epilogue BatchNorm statistics (pair_conv_bn) are opt-in: measured on MI355X
+# (scripts/bench_cnn.py --graph) the epilogue's atomics + last-tile finalize add
+# ~12 us to each forward conv while the BN reduce pass they replace costs ~9.5 us:
+# EnhancedCNN batch 64 2.462 vs 2.424 ms, batch 256 3.606 vs 3.581 ms, ResNet-18
+# batch 64 3.80 vs 3.67 ms.  LDNN_FUSE_BN_STATS=1 (or setting this flag) turns it on.
+FUSE_BN_STATS = os.environ.get("LDNN_FUSE_BN_STATS", "0") == "1"
+
+
+def pair_conv_bn(conv: "Conv2d", bn: "BatchNorm2d") -> None:
+    """Declare that `bn` consumes exactly `conv`'s output: in training mode the conv
+    kernel's epilogue then accumulates and finalizes the BN's batch statistics
+    (conv_lds.hip bn_stats_epilogue) and the BN runs only its apply pass.  Only for
+    architectures where that dataflow is fixed (the BN also checks it is handed the
+    very buffer the conv wrote before it trusts the statistics)."""
+    conv.__dict__["_ldnn_stats_bn"] = bn
 
 
 class BatchNorm2d(nn.BatchNorm2d):

@@ -6,7 +6,7 @@ from __future__ import annotations
 
 import torch.nn as nn
 
-from .layers import AdaptiveAvgPool2d, BatchNorm2d, Conv2d, Linear, MaxPool2d, ReLU
+from .layers import AdaptiveAvgPool2d, BatchNorm2d, Conv2d, Linear, MaxPool2d, ReLU, pair_conv_bn
 
 
 class BasicBlock(nn.Module):
@@ -20,6 +20,10 @@ class BasicBlock(nn.Module):
         self.conv2 = Conv2d(planes, planes, 3, 1, 1, bias=False)
         self.bn2 = BatchNorm2d(planes)
         self.downsample = downsample
+        pair_conv_bn(self.conv1, self.bn1)
+        pair_conv_bn(self.conv2, self.bn2)
+        if downsample is not None:
+            pair_conv_bn(downsample[0], downsample[1])
 
     def forward(self, x):
         idt = x if self.downsample is None else self.downsample(x)
@@ -35,6 +39,7 @@ class ResNet(nn.Module):
         self.bn1 = BatchNorm2d(width)
         self.relu = ReLU()
         self.maxpool = MaxPool2d(3, 2, 1)
+        pair_conv_bn(self.conv1, self.bn1)
         self.layer1 = self._make(width, layers[0], 1)
         self.layer2 = self._make(width * 2, layers[1], 2)
         self.layer3 = self._make(width * 4, layers[2], 2)

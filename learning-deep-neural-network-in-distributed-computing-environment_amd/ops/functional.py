@@ -237,9 +237,32 @@ def nchw_view(buf: torch.Tensor, c: int) -> torch.Tensor:
     return buf[..., :c].permute(0, 3, 1, 2)
 
 
+def _bn_train_state(mod, dev):
+    """(running_mean, running_var, momentum, num_batches tensor) of a training-mode BN
+    forward, with the Python-side bookkeeping of one call (num_batches_tracked)."""
+    mom = mod.momentum
+    nbt = None
+    if mod.training and mod.track_running_stats:
+        # num_batches_tracked += 1 happens inside the fused BN statistics kernel
+        nbt = mod.num_batches_tracked if mod.num_batches_tracked.is_cuda else None
+        if nbt is None:
+            mod.num_batches_tracked.add_(1)
+        mod._ldnn_nbt = getattr(mod, "_ldnn_nbt", 0) + 1
+        if mom is None:
+            mom = 1.0 / mod._ldnn_nbt
+    rm = mod.running_mean if mod.track_running_stats else None
+    rv = mod.running_var if mod.track_running_stats else None
+    return rm, rv, mom, nbt
+
+
+def _fused_bn_ok(bn, K: int, kp: int, bias, relu: bool) -> bool:
+    return (bn is not None and bn.training and bn.affine and kp == K == bn.num_features and bias is None
+            and not relu and getattr(bn, "_ldnn_flat", None) is not None)
+
+
 class _Conv2dNative(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, stride, pad, flat, relu):
+    def forward(ctx, x, weight, bias, stride, pad, flat, relu, bn=None):
         C = _ext.C()
         K, Cin, R, S = weight.shape
         w = flat.shadow_storage(weight)  # [Kp][R][S][Cp]
@@ -253,7 +276,29 @@ class _Conv2dNative(torch.autograd.Function):
         if relu and b is None:
             b = torch.zeros(kp, dtype=torch.float32, device=x.device)
             epi = C.EPI_BIAS_RELU
-        C.conv_fwd(xb, w, y, stride, pad, b, epi)
+        if _fused_bn_ok(bn, K, kp, bias, relu):
+            # the conv epilogue accumulates + finalizes the next BN's batch statistics
+            dev = x.device
+            ws = _bn_workspace(bn, K, dev, C)
+            smean = torch.empty(K, dtype=torch.float32, device=dev)
+            sinv = torch.empty(K, dtype=torch.float32, device=dev)
+            bflat = bn._ldnn_flat
+            gamma = bflat.master_storage(bn.weight)[:K]
+            beta = bflat.master_storage(bn.bias)[:K]
+            snap = (getattr(bn, "_ldnn_nbt", 0), bn.num_batches_tracked.clone()
+                    if bn.track_running_stats and not bn.num_batches_tracked.is_cuda else None)
+            rm, rv, mom, nbt = _bn_train_state(bn, dev)
+            done = C.conv_fwd(xb, w, y, stride, pad, b, epi, bn_ws=ws, bn_gamma=gamma, bn_beta=beta,
+                              bn_running_mean=rm, bn_running_var=rv, bn_save_mean=smean, bn_save_invstd=sinv,
+                              bn_eps=bn.eps, bn_momentum=mom or 0.0, bn_num_batches=nbt)
+            if done:
+                bn.__dict__["_ldnn_pre"] = (y.data_ptr(), smean, sinv)
+            else:  # generic conv path: the BN runs its own statistics pass (undo the bookkeeping)
+                bn._ldnn_nbt = snap[0]
+                if snap[1] is not None:
+                    bn.num_batches_tracked.copy_(snap[1])
+        else:
+            C.conv_fwd(xb, w, y, stride, pad, b, epi)
         ctx.save_for_backward(xb, y)
         ctx.meta = (stride, pad, flat, weight, bias, relu, Cin, x.dtype)
         return nchw_view(y, K)
@@ -280,10 +325,10 @@ class _Conv2dNative(torch.autograd.Function):
             dx = nchw_view(dxb, Cin)
             if in_dtype != torch.bfloat16:
                 dx = dx.to(in_dtype)
-        return dx, None, None, None, None, None, None
+        return dx, None, None, None, None, None, None, None
 
 
-def conv2d(x, mod, relu: bool = False):
+def conv2d(x, mod, relu: bool = False, bn=None):
     """Convolution of module `mod` (nn.Conv2d parameters).  GPU: native implicit-GEMM
     kernels on NHWC bf16 activations and KRSC bf16 weights (groups=1, dilation=1);
     CPU: the fp32 reference."""
@@ -295,7 +340,7 @@ def conv2d(x, mod, relu: bool = False):
         if not ok:
             raise RuntimeError("native conv needs groups=1, dilation=1, square stride/padding and "
                                "the model attached to FlatParams (ldnn.prepare(model))")
-        return _Conv2dNative.apply(x, mod.weight, mod.bias, mod.stride[0], mod.padding[0], flat, relu)
+        return _Conv2dNative.apply(x, mod.weight, mod.bias, mod.stride[0], mod.padding[0], flat, relu, bn)
     y = F.conv2d(x.float(), mod.weight, mod.bias, mod.stride, mod.padding, mod.dilation, mod.groups)
     return F.relu(y) if relu else y
 
@@ -330,21 +375,17 @@ class _BatchNormNative(torch.autograd.Function):
         gamma = flat.master_storage(weight)[:C] if weight is not None else None
         beta = flat.master_storage(bias)[:C] if bias is not None else None
         training = mod.training or not mod.track_running_stats
-        mom = mod.momentum
-        nbt = None
-        if mod.training and mod.track_running_stats:
-            # num_batches_tracked += 1 happens inside the fused BN statistics kernel
-            nbt = mod.num_batches_tracked if mod.num_batches_tracked.is_cuda else None
-            if nbt is None:
-                mod.num_batches_tracked.add_(1)
-            mod._ldnn_nbt = getattr(mod, "_ldnn_nbt", 0) + 1
-            if mom is None:
-                mom = 1.0 / mod._ldnn_nbt
-        rm = mod.running_mean if mod.track_running_stats else None
-        rv = mod.running_var if mod.track_running_stats else None
-        C_.bn_fwd(x2, y.view(-1, C), r2, gamma, beta, rm if (training and mod.training) or not training else None,
-                  rv if (training and mod.training) or not training else None, smean, sinv, ws, mod.eps,
-                  mom or 0.0, training, relu, nbt)
+        pre = mod.__dict__.pop("_ldnn_pre", None)
+        if pre is not None and mod.training and pre[0] == x2.data_ptr():
+            # statistics already accumulated + finalized by the producing conv's epilogue
+            smean, sinv = pre[1], pre[2]
+            C_.bn_fwd(x2, y.view(-1, C), r2, gamma, beta, None, None, smean, sinv, ws, mod.eps, 0.0, True, relu,
+                      None, stats_ready=True)
+        else:
+            rm, rv, mom, nbt = _bn_train_state(mod, dev)
+            C_.bn_fwd(x2, y.view(-1, C), r2, gamma, beta, rm if (training and mod.training) or not training else None,
+                      rv if (training and mod.training) or not training else None, smean, sinv, ws, mod.eps,
+                      mom or 0.0, training, relu, nbt)
         ctx.save_for_backward(x2, y, smean, sinv)
         ctx.meta = (flat, weight, bias, relu, residual is not None, ws, (N, C, H, W), x.dtype)
         return nchw_view(y, C)

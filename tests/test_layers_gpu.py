@@ -211,3 +211,51 @@ def test_train_global_with_graphs_matches_eager():
         assert (b - a).norm().item() <= 3.0 * (c - a).norm().item() + 1e-2 * a.norm().item()
     # (fp32-atomic arrival order can flip an argmax near a tie: allow one sample in ~1/2 %)
     assert abs(h0[4][-1] - h1[4][-1]) < 1e-2 and abs(h0[5][-1] - h1[5][-1]) < 0.5
+
+
+@pytest.mark.parametrize("name,shape", [("enhanced_cnn_small", (32, 3, 32, 32)), ("resnet18", (8, 3, 96, 96))])
+def test_conv_epilogue_bn_statistics_match_separate_pass(name, shape, monkeypatch):
+    """Training-mode BN whose statistics the producing conv's epilogue accumulated and
+    finalized (conv_lds.hip bn_stats_epilogue) == the BN's own reduce pass: outputs,
+    running statistics, num_batches_tracked and gradients."""
+    import ldnn.models.layers as layers_mod
+    from ldnn.models.layers import Conv2d
+
+    monkeypatch.setattr(layers_mod, "FUSE_BN_STATS", True)
+
+    torch.manual_seed(0)
+    m1, m2, m3 = build_model(name), build_model(name), build_model(name)
+    xavier_init(m1)
+    for mm in (m2, m3):
+        mm.load_state_dict(m1.state_dict())
+        for m in mm.modules():  # m2, m3: unpaired -> separate BN statistics pass
+            if isinstance(m, Conv2d):
+                m.__dict__["_ldnn_stats_bn"] = None
+    for mm in (m1, m2, m3):
+        ldnn.prepare(mm, "cuda")
+    assert any(getattr(m, "_ldnn_stats_bn", None) is not None for m in m1.modules())
+    x = torch.randn(*shape, device="cuda").bfloat16()
+    y = torch.randint(0, 10, (shape[0],), device="cuda")
+    crit = CrossEntropyLoss()
+    outs = []
+    for m in (m1, m2, m3):
+        m.train()
+        for _ in range(2):
+            out = m(x)
+            crit(out, y).backward()
+        outs.append(out.float())
+    torch.cuda.synchronize()
+    # (batch statistics over as few as 16 values per channel in the last stage:
+    # compare the logits as a whole, fp32 summation order differs between the paths)
+    rel = ((outs[0] - outs[1]).norm() / outs[1].norm()).item()
+    assert rel < 2e-2, rel
+    for (n, b1), (_, b2) in zip(m1.named_buffers(), m2.named_buffers()):
+        if "num_batches" in n:
+            assert torch.equal(b1.cpu(), b2.cpu()), n
+        else:
+            torch.testing.assert_close(b1, b2, rtol=1e-2, atol=1e-3, msg=n)
+    # gradients: within the spread of two runs of the SAME (separate-pass) path, whose
+    # fp32 atomics already differ in arrival order
+    for (n, p1), (_, p2), (_, p3) in zip(m1.named_parameters(), m2.named_parameters(), m3.named_parameters()):
+        g1, g2, g3 = (p.grad.flatten().double() for p in (p1, p2, p3))
+        assert (g1 - g2).norm().item() <= 3.0 * (g3 - g2).norm().item() + 2e-2 * g2.norm().item(), n
