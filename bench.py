@@ -89,7 +89,8 @@ def run_ldnn(ctx, args):
     eng = StaticMLPEngine(model, args.batch, OptimConfig("sgd", lr=args.lr, momentum=0.9),
                           device=ctx.device, world_size=ctx.world_size, use_graphs=not args.no_graphs,
                           bucket_cap_elems=args.bucket_elems, shard_optimizer=False if args.no_shard else None,
-                          library_gemms=not args.no_library_gemms)
+                          library_gemms=not args.no_library_gemms,
+                          early_optimizer={"on": True, "off": False, "auto": None}[args.early_opt])
     if ctx.distributed:
         dist.broadcast(eng.flat.master, src=0)
         eng.flat.refresh_shadow()
@@ -149,6 +150,8 @@ def main():
                     help="all-reduce + replicated optimizer instead of reduce-scatter / sharded optimizer / all-gather")
     ap.add_argument("--no-library-gemms", action="store_true",
                     help="run the plain GEMMs (fp32 wgrads, bias+ReLU forwards) on ldnn's MFMA kernels instead of hipBLASLt")
+    ap.add_argument("--early-opt", choices=["auto", "on", "off"], default="auto",
+                    help="1 GPU: update W_{L-1}..W_1 on a side stream beside the last dgrad GEMM")
     ap.add_argument("--compare-stock", action="store_true")
     ap.add_argument("--backend", default="auto", help="auto (nccl = RCCL on GPUs) | gloo (testing only)")
     args = ap.parse_args()

@@ -98,7 +98,7 @@ class StaticMLPEngine:
                  use_graphs: bool = True, average_grads: bool = True, use_head_kernels: bool = True,
                  shard_optimizer: bool | None = None, overlap_optimizer: bool = False, wgrad_combine: bool = True,
                  fuse_optimizer: bool | None = None, library_gemms: bool | None = None,
-                 fuse_head_dgrad: bool = False):
+                 fuse_head_dgrad: bool = False, early_optimizer: bool | None = None):
         from ..models.mlp import MLP
 
         if not isinstance(model, MLP):
@@ -279,7 +279,27 @@ class StaticMLPEngine:
                        and (self._wgrad_splitk[l] == 1 or self._wgrad_ws[l] is not None) for l in range(L)]
         self.rank = dist.get_rank(process_group) if self.distributed else 0
         self.overlap_optimizer = overlap_optimizer
-        self.side = torch.cuda.Stream(device=self.device) if overlap_optimizer else None
+        # early_optimizer (single process, L >= 2): the update of W_{L-1} .. W_1 runs on
+        # a side stream as soon as wgrad(1) has produced the last of their gradients,
+        # BESIDE dgrad(1) -- a 256-workgroup MFMA GEMM holding one workgroup per CU with
+        # ~100 VGPRs/lane, so the bandwidth-bound update's waves fit next to it.  dgrad(1)
+        # still reads the old bf16 W_1, so W_1's new shadow goes to a scratch copy that
+        # the main stream moves into place after the join; W_0 and the biases update
+        # on the main stream after the last wgrad, as before.
+        # Off by default: measured on MI355X (profiles/mlp3_early_optimizer_timeline_r1.txt)
+        # the co-resident update slows dgrad(1) from ~134 to ~210 us, more than the
+        # 60 us it hides (0.641 vs 0.599 ms/step).
+        if early_optimizer is None:
+            early_optimizer = False
+        self.early_optimizer = (bool(early_optimizer) and not self.distributed and L >= 2
+                                and not overlap_optimizer and not any(self._fused))
+        self._w1_span = None
+        if self.early_optimizer:
+            s1 = f.seg(self.layers[1].weight)
+            self._w1_span = (s1.offset, s1.offset + s1.storage_numel)
+            self._w0_begin = f.seg(self.layers[0].weight).offset
+            self._early_scratch = torch.empty(s1.storage_numel, dtype=torch.bfloat16, device=self.device)
+        self.side = torch.cuda.Stream(device=self.device) if (overlap_optimizer or self.early_optimizer) else None
         self._pending_gather = {}
         if self.shard:
             self.gshard = [torch.zeros((e - b) // self.world, dtype=torch.float32, device=dev)
@@ -379,9 +399,25 @@ class StaticMLPEngine:
         s = (e - b) // self.world
         return b + self.rank * s, b + (self.rank + 1) * s
 
-    def _opt(self, b, e, grad=None):
+    def _early_opt(self):
+        """Side stream (see early_optimizer): update W_{L-1} .. W_1 beside dgrad(1)."""
+        s1b, s1e = self._w1_span
+        self.side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(self.side):
+            if s1b > 0:
+                self._opt(0, s1b)   # shadows no later kernel of this step reads
+            self._opt(s1b, s1e, shadow=self._early_scratch)
+
+    def _early_join(self):
+        s1b, s1e = self._w1_span
+        self._join()
+        self.flat.shadow[s1b:s1e].copy_(self._early_scratch)
+        self._opt(s1e, self.flat.numel)
+
+    def _opt(self, b, e, grad=None, shadow=None):
         f, o, C = self.flat, self.optim, self.C
-        p, g, sh = f.master[b:e], (f.grad[b:e] if grad is None else grad), f.shadow[b:e]
+        p, g = f.master[b:e], (f.grad[b:e] if grad is None else grad)
+        sh = f.shadow[b:e] if shadow is None else shadow
         zr = [(max(zb, b) - b, min(ze, e) - b) for zb, ze in self._opt_zero if zb < e and ze > b]
         if o.name == "sgd":
             mom = self.mom[b:e] if self.mom is not None else p
@@ -412,7 +448,9 @@ class StaticMLPEngine:
                     pieces[-1].append(lambda l=l: self._dgrad(l))
                 pieces[-1].append(lambda l=l: self._wgrad_opt(l))
                 continue
-            pieces[-1].append(lambda l=l: self._wgrad(l))
+            wg = lambda l=l: self._wgrad(l)  # noqa: E731
+            wg._ldnn_wgrad = l
+            pieces[-1].append(wg)
             if l in triggers:
                 self._cut_buckets.append(triggers[l])
                 pieces.append([])
@@ -443,6 +481,11 @@ class StaticMLPEngine:
                         fns.append(fn)
                 fns.insert(len(fns) - 1, lambda: self._fork_opt(side))   # before wgrad(0)
                 fns += [lambda: self._opt(w0, self._bias_begin), self._join]
+            elif self.early_optimizer:
+                fns = [fn for p in pieces for fn in p]
+                i1 = next(i for i, fn in enumerate(fns) if getattr(fn, "_ldnn_wgrad", None) == 1)
+                fns.insert(i1 + 1, self._early_opt)   # fork right after wgrad(1)
+                fns.append(self._early_join)          # after wgrad(0)
             elif any(self._fused):
                 fns = [fn for p in pieces for fn in p] + [lambda b=b, e=e: self._opt(b, e)
                                                           for b, e in self._unfused_ranges()]

@@ -222,3 +222,31 @@ def test_fused_head_dgrad_engine_matches_separate_dgrad():
             e.step()
     torch.cuda.synchronize()
     torch.testing.assert_close(e1.flat.master, e2.flat.master, rtol=1e-3, atol=1e-4)
+
+
+@pytest.mark.parametrize("opt,dims", [("sgd", (784, 1024, 10)), ("adam", (784, 1024, 10)),
+                                      ("sgd", (784, 512, 512, 10))])
+def test_early_optimizer_side_stream_matches_serial(opt, dims):
+    """early_optimizer=True (W_{L-1}..W_1 updated on a side stream beside dgrad(1),
+    W_1's new shadow parked in a scratch copy) trains like the serial step, and the
+    bf16 shadow is the rounded master after every step."""
+    from ldnn.models.mlp import MLP
+    torch.manual_seed(0)
+    B = 512
+    mk = lambda: MLP(dims[0], dims[1:-1], dims[-1])  # noqa: E731
+    m1, m2 = mk(), mk()
+    m2.load_state_dict(m1.state_dict())
+    cfg = OptimConfig(opt, lr=0.05 if opt == "sgd" else 1e-3, momentum=0.9)
+    e1 = StaticMLPEngine(m1, B, cfg, use_graphs=True, early_optimizer=True)
+    e2 = StaticMLPEngine(m2, B, cfg, use_graphs=True, early_optimizer=False)
+    assert e1.early_optimizer and not e2.early_optimizer
+    g = torch.Generator(device="cuda").manual_seed(7)
+    for i in range(5):
+        x = torch.randn(B, dims[0], device="cuda", generator=g).bfloat16()
+        y = torch.randint(0, dims[-1], (B,), device="cuda", generator=g)
+        for e in (e1, e2):
+            e.load_batch(x, y)
+            e.step()
+    torch.cuda.synchronize()
+    torch.testing.assert_close(e1.flat.master, e2.flat.master, rtol=1e-3, atol=1e-4)
+    assert torch.equal(e1.flat.shadow, e1.flat.master.bfloat16())
