@@ -236,6 +236,22 @@ void colsum(const at::Tensor& x, const at::Tensor& out, bool accumulate) {
         "colsum");
 }
 
+void act_bwd_colsum(const at::Tensor& dy, const at::Tensor& y, const at::Tensor& dx, const at::Tensor& out,
+                    int64_t act, bool accumulate) {
+  check_dev(dy, at::kBFloat16, "dy");
+  check_dev(y, at::kBFloat16, "y");
+  check_dev(dx, at::kBFloat16, "dx");
+  check_dev(out, at::kFloat, "out");
+  TORCH_CHECK(y.dim() == 2 && y.is_contiguous() && dy.is_contiguous() && dx.is_contiguous() &&
+                  out.is_contiguous(), "act_bwd_colsum: tensors must be contiguous, y 2-D");
+  TORCH_CHECK(dy.sizes() == y.sizes() && dx.sizes() == y.sizes(), "act_bwd_colsum: size mismatch");
+  TORCH_CHECK(y.size(1) % 8 == 0 && out.numel() >= y.size(1), "act_bwd_colsum: cols % 8 != 0 or short out");
+  TORCH_CHECK(act == ldnn::ACT_RELU || act == ldnn::ACT_SIGMOID, "act_bwd_colsum: act must be relu/sigmoid");
+  check(ldnn::act_bwd_colsum(bf16_ptr(dy), bf16_ptr(y), bf16_mut(dx), out.data_ptr<float>(), (int)y.size(0),
+                             (int)y.size(1), (int)act, accumulate, cur_stream(y)),
+        "act_bwd_colsum");
+}
+
 void cast_f32_bf16(const at::Tensor& x, const at::Tensor& y) {
   check_dev(x, at::kFloat, "x");
   check_dev(y, at::kBFloat16, "y");
@@ -804,6 +820,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("act_fwd", &act_fwd);
   m.def("act_bwd", &act_bwd);
   m.def("colsum", &colsum, py::arg("x"), py::arg("out"), py::arg("accumulate") = false);
+  m.def("act_bwd_colsum", &act_bwd_colsum, py::arg("dy"), py::arg("y"), py::arg("dx"), py::arg("out"),
+        py::arg("act"), py::arg("accumulate") = true);
   m.def("cast_f32_bf16", &cast_f32_bf16);
   m.def("mix3", &mix3, py::arg("out"), py::arg("x"), py::arg("y1") = py::none(), py::arg("y2") = py::none(),
         py::arg("a") = 1.0, py::arg("b") = 0.0, py::arg("c") = 0.0, py::arg("shadow") = py::none());

@@ -99,6 +99,71 @@ __global__ void colsum_kernel(const bf16_t* __restrict__ x, float* __restrict__ 
   }
 }
 
+// Activation backward fused with the bias-gradient column sums:
+//   dx = act'(y) * dy,   out[c] (+)= sum_r dx[r][c]
+// The dgrad GEMM of a library (hipBLASLt) step writes dy = dz_{l+1} W_l; this
+// one pass applies layer l-1's activation derivative and emits its bias
+// gradient (3 bf16 streams, no re-read of dx for a separate colsum).  dy may
+// alias dx (in place).  Same block shape as colsum_kernel: 32 column groups of
+// 8 columns (16-B accesses) x 8 row lanes; rows split over gridDim.y; the
+// column sums are taken from the fp32 derivative before rounding.
+template <int ACT>
+__global__ void act_bwd_colsum_kernel(const bf16_t* dy, const bf16_t* __restrict__ y, bf16_t* dx,
+                                      float* __restrict__ out, int rows, int cols, int rows_per_block) {
+  __shared__ float part[8][32 * 8];
+  const int cg = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const int c0 = (blockIdx.x * 32 + cg) * 8;
+  const int r_begin = blockIdx.y * rows_per_block;
+  const int r_end = min(rows, r_begin + rows_per_block);
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c0 < cols) {
+    int r = r_begin + ty;
+    for (; r + 8 < r_end; r += 16) {   // two rows in flight per lane
+      const size_t o0 = (size_t)r * cols + c0, o1 = o0 + (size_t)8 * cols;
+      const u16x8 g0 = *reinterpret_cast<const u16x8*>(dy + o0);
+      const u16x8 v0 = *reinterpret_cast<const u16x8*>(y + o0);
+      const u16x8 g1 = *reinterpret_cast<const u16x8*>(dy + o1);
+      const u16x8 v1 = *reinterpret_cast<const u16x8*>(y + o1);
+      u16x8 d0, d1;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float a = act_b<ACT>(bf2f(g0[j]), bf2f(v0[j]));
+        const float b = act_b<ACT>(bf2f(g1[j]), bf2f(v1[j]));
+        s[j] += a + b;
+        d0[j] = f2bf(a);
+        d1[j] = f2bf(b);
+      }
+      *reinterpret_cast<u16x8*>(dx + o0) = d0;
+      *reinterpret_cast<u16x8*>(dx + o1) = d1;
+    }
+    for (; r < r_end; r += 8) {
+      const size_t o0 = (size_t)r * cols + c0;
+      const u16x8 g0 = *reinterpret_cast<const u16x8*>(dy + o0);
+      const u16x8 v0 = *reinterpret_cast<const u16x8*>(y + o0);
+      u16x8 d0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float a = act_b<ACT>(bf2f(g0[j]), bf2f(v0[j]));
+        s[j] += a;
+        d0[j] = f2bf(a);
+      }
+      *reinterpret_cast<u16x8*>(dx + o0) = d0;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) part[ty][cg * 8 + j] = s[j];
+  __syncthreads();
+  if (ty == 0 && c0 < cols) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float t = 0.f;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) t += part[q][cg * 8 + j];
+      atomicAdd(out + c0 + j, t);
+    }
+  }
+}
+
 // Zero a [rows][cols] fp32 block with row stride ld.  A kernel, not
 // hipMemset2DAsync: memset nodes captured into hipGraphs are not replayed
 // reliably on this stack (found while validating graph-captured split-K wgrads).
@@ -207,6 +272,24 @@ hipError_t colsum_bf16(const uint16_t* x, float* out, int rows, int cols, bool a
   if (gy > 256) gy = 256;
   const int rpb = (rows + gy - 1) / gy;
   colsum_kernel<<<dim3(gx, gy), kBlock, 0, s>>>(x, out, rows, cols, rpb);
+  return hipGetLastError();
+}
+
+hipError_t act_bwd_colsum(const uint16_t* dy, const uint16_t* y, uint16_t* dx, float* out, int rows, int cols,
+                          int act, bool accumulate, hipStream_t s) {
+  if (!accumulate) {
+    hipError_t e = zero2d_f32(out, 1, cols, cols, s);
+    if (e != hipSuccess) return e;
+  }
+  if (rows <= 0 || cols <= 0) return hipSuccess;
+  const int gx = (cols + 255) / 256;
+  int gy = (rows + 255) / 256;
+  if (gy > 256) gy = 256;
+  const int rpb = (rows + gy - 1) / gy;
+  if (act == ACT_RELU)
+    act_bwd_colsum_kernel<ACT_RELU><<<dim3(gx, gy), kBlock, 0, s>>>(dy, y, dx, out, rows, cols, rpb);
+  else
+    act_bwd_colsum_kernel<ACT_SIGMOID><<<dim3(gx, gy), kBlock, 0, s>>>(dy, y, dx, out, rows, cols, rpb);
   return hipGetLastError();
 }
 

@@ -98,7 +98,8 @@ class StaticMLPEngine:
                  use_graphs: bool = True, average_grads: bool = True, use_head_kernels: bool = True,
                  shard_optimizer: bool | None = None, overlap_optimizer: bool = False, wgrad_combine: bool = True,
                  fuse_optimizer: bool | None = None, library_gemms: bool | None = None,
-                 fuse_head_dgrad: bool = False, early_optimizer: bool | None = None):
+                 fuse_head_dgrad: bool = False, early_optimizer: bool | None = None,
+                 library_dgrad: bool | None = None):
         from ..models.mlp import MLP
 
         if not isinstance(model, MLP):
@@ -222,6 +223,23 @@ class StaticMLPEngine:
         self._lib_wgrad = [bool(library_gemms) and l in hidden for l in range(L)]
         self._lib_fwd = [bool(library_gemms) and l in hidden and self.layers[l].activation in ("relu", "none")
                          for l in range(L)]
+        # library_dgrad: dgrad(l) as a plain hipBLASLt GEMM (bf16 out, in place into dz_l)
+        # followed by ONE fused pass (elementwise.hip act_bwd_colsum) that applies layer
+        # l-1's activation derivative and emits its bias gradient.  Measured on MI355X
+        # (mlp3 784-4096-4096-10, batch 16384, profiles/mlp3_b16384_kernels_r1.txt):
+        # ldnn's fused dgrad (dReLU + dbias in the MFMA epilogue) runs the 16384 x 4096
+        # x 4096 dgrad at ~0.86 PFLOP/s (639 us) and the K=16 head dgrad in 131 us;
+        # hipBLASLt takes 406 + 51 us and the 3-stream pass 2 x 68 us (2.054 -> 1.844
+        # ms/step).  Default: on whenever the library GEMMs are.
+        # (Splitting the 784-wide wgrad over batch slices with a batched hipBLASLt GEMM
+        # was faster in isolation, 160 vs 192 us, scripts/bench_wgrad_split.py, but
+        # neutral in the step, so the wgrads stay single GEMMs.)
+        if library_dgrad is None:
+            library_dgrad = bool(library_gemms)
+        self._lib_dgrad = [bool(library_dgrad) and l > 0 and self.layers[l - 1].activation in ("relu", "sigmoid")
+                           for l in range(L)]
+        self._act_code = [None] + [{"relu": self.C.ACT_RELU, "sigmoid": self.C.ACT_SIGMOID}.get(
+            self.layers[l - 1].activation) for l in range(1, L)]
         self.bias_bf16 = [f.shadow_storage(l.bias) for l in self.layers]
         self._wgrad_splitk, self._wgrad_ws = [], []
         for l, layer in enumerate(self.layers):
@@ -381,6 +399,10 @@ class StaticMLPEngine:
 
     def _dgrad(self, l):
         # dz_l(prev layer output) = (dz_{l+1} W_l) * act'(h_l), bias grad of layer l-1 fused
+        if self._lib_dgrad[l]:
+            torch.mm(self.dz[l + 1], self.W[l], out=self.dz[l])
+            self.C.act_bwd_colsum(self.dz[l], self.h[l], self.dz[l], self.db[l - 1], self._act_code[l], True)
+            return
         self.C.gemm(self.dz[l + 1], self.W[l], self.dz[l], True, False, self._dgrad_epi[l], aux=self.h[l],
                     dbias=self.db[l - 1])
 

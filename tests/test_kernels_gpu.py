@@ -370,3 +370,26 @@ def test_gemm_splitk_inlaunch_combine(splitk, case):
         torch.testing.assert_close(db, outs[1].float().sum(0), rtol=1e-3, atol=1e-2)
     assert torch.equal(outs[0], outs[1])
     assert int(cnt.abs().sum().item()) == 0
+
+
+@pytest.mark.parametrize("act", ["relu", "sigmoid"])
+@pytest.mark.parametrize("inplace", [False, True])
+@pytest.mark.parametrize("accumulate", [False, True])
+@pytest.mark.parametrize("rows,cols", [(1003, 264), (4096, 512), (7, 8)])
+def test_act_bwd_colsum_matches_fp32(act, inplace, accumulate, rows, cols):
+    """elementwise.hip act_bwd_colsum: dx = act'(y) * dy and out (+)= colsum(dx), vs torch fp32."""
+    torch.manual_seed(rows + cols)
+    dy = torch.randn(rows, cols, device="cuda").bfloat16()
+    pre = torch.randn(rows, cols, device="cuda")
+    y = (pre.relu() if act == "relu" else pre.sigmoid()).bfloat16()
+    yf, gf = y.float(), dy.float()
+    ref_dx = gf * (yf > 0).float() if act == "relu" else gf * yf * (1 - yf)
+    base = torch.randn(cols, device="cuda")
+    out = base.clone()
+    dx = dy.clone() if inplace else torch.empty_like(dy)
+    src = dx if inplace else dy
+    code = C().ACT_RELU if act == "relu" else C().ACT_SIGMOID
+    C().act_bwd_colsum(src, y, dx, out, code, accumulate)
+    torch.testing.assert_close(dx.float(), ref_dx, rtol=1e-2, atol=1e-2)
+    ref_out = ref_dx.sum(0) + (base if accumulate else 0)
+    torch.testing.assert_close(out, ref_out, rtol=1e-3, atol=1e-3 * (rows ** 0.5))

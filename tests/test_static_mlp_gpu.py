@@ -176,16 +176,18 @@ def test_fused_optimizer_epilogue_matches_separate_launch(opt):
     assert torch.equal(e1.flat.shadow, e1.flat.master.bfloat16())
 
 
-def test_library_gemm_engine_matches_native_engine():
-    """hipBLASLt plain GEMMs (fp32 wgrads, bias+ReLU forwards) inside the graph-captured
-    step == the all-ldnn-kernel engine, up to bf16 rounding of the bias in the forward."""
+@pytest.mark.parametrize("B", [1024, 4096])
+def test_library_gemm_engine_matches_native_engine(B):
+    """hipBLASLt plain GEMMs (fp32 wgrads, bias+ReLU forwards,
+    dgrads + the fused dReLU/bias-grad pass) inside the graph-captured step == the all-ldnn-kernel engine, up to
+    bf16 rounding of the bias in the forward."""
     torch.manual_seed(0)
-    B = 1024
     m1, m2 = mlp3(784, 1024, 10), mlp3(784, 1024, 10)
     m2.load_state_dict(m1.state_dict())
     cfg = OptimConfig("sgd", lr=0.05, momentum=0.9)
     e1 = StaticMLPEngine(m1, B, cfg, use_graphs=True, library_gemms=True)
     e2 = StaticMLPEngine(m2, B, cfg, use_graphs=True, library_gemms=False)
+    assert any(e1._lib_dgrad) and not any(e2._lib_dgrad)
     g = torch.Generator(device="cuda").manual_seed(5)
     l1, l2 = [], []
     for i in range(6):
@@ -250,3 +252,32 @@ def test_early_optimizer_side_stream_matches_serial(opt, dims):
     torch.cuda.synchronize()
     torch.testing.assert_close(e1.flat.master, e2.flat.master, rtol=1e-3, atol=1e-4)
     assert torch.equal(e1.flat.shadow, e1.flat.master.bfloat16())
+
+
+@pytest.mark.parametrize("act", ["relu", "sigmoid"])
+def test_library_dgrad_matches_fused_dgrad(act):
+    """hipBLASLt dgrad + fused act'/bias-grad pass (library_dgrad) == ldnn's dgrad with
+    the activation derivative and bias column sums in its MFMA epilogue."""
+    from ldnn.models.mlp import MLP
+    torch.manual_seed(0)
+    B = 1024
+    m1, m2 = MLP(784, (1024, 512), 10, activation=act), MLP(784, (1024, 512), 10, activation=act)
+    m2.load_state_dict(m1.state_dict())
+    cfg = OptimConfig("sgd", lr=0.05, momentum=0.9)
+    e1 = StaticMLPEngine(m1, B, cfg, use_graphs=True, library_gemms=True, library_dgrad=True)
+    e2 = StaticMLPEngine(m2, B, cfg, use_graphs=True, library_gemms=True, library_dgrad=False)
+    assert any(e1._lib_dgrad) and not any(e2._lib_dgrad)
+    g = torch.Generator(device="cuda").manual_seed(5)
+    l1, l2 = [], []
+    for i in range(6):
+        x = torch.randn(B, 784, device="cuda", generator=g).bfloat16()
+        y = torch.randint(0, 10, (B,), device="cuda", generator=g)
+        for e, ls in ((e1, l1), (e2, l2)):
+            e.reset_stats()
+            e.load_batch(x, y)
+            e.step()
+            ls.append(e.read_stats(B)[0])
+    torch.cuda.synchronize()
+    for a, b in zip(l1, l2):
+        assert abs(a - b) < 1e-2 * max(1.0, abs(b)), (l1, l2)
+    torch.testing.assert_close(e1.flat.master, e2.flat.master, rtol=2e-2, atol=2e-3)
