@@ -95,7 +95,8 @@ def run_ldnn(ctx, args):
                           device=ctx.device, world_size=ctx.world_size, use_graphs=not args.no_graphs,
                           bucket_cap_elems=args.bucket_elems, shard_optimizer=False if args.no_shard else None,
                           library_gemms=not args.no_library_gemms,
-                          early_optimizer={"on": True, "off": False, "auto": None}[args.early_opt])
+                          early_optimizer={"on": True, "off": False, "auto": None}[args.early_opt],
+                          fuse_head_dgrad=False if args.no_fuse_head_dgrad else None)
     if ctx.distributed:
         dist.broadcast(eng.flat.master, src=0)
         eng.flat.refresh_shadow()
@@ -155,6 +156,8 @@ def main():
                     help="all-reduce + replicated optimizer instead of reduce-scatter / sharded optimizer / all-gather")
     ap.add_argument("--no-library-gemms", action="store_true",
                     help="run the plain GEMMs (fp32 wgrads, bias+ReLU forwards) on ldnn's MFMA kernels instead of hipBLASLt")
+    ap.add_argument("--no-fuse-head-dgrad", action="store_true",
+                    help="separate head dgrad GEMM instead of the head kernel's fused dgrad (dReLU + dbias)")
     ap.add_argument("--early-opt", choices=["auto", "on", "off"], default="auto",
                     help="1 GPU: update W_{L-1}..W_1 on a side stream beside the last dgrad GEMM")
     ap.add_argument("--compare-stock", action="store_true")
@@ -187,7 +190,8 @@ def main():
             "parallelism": f"dp{n}",
             "optimizer": "sgd momentum 0.9, fp32 master",
             "gemms": ("ldnn MFMA kernels" if args.no_library_gemms else
-                      "hipBLASLt: fp32 wgrads, bias/ReLU fwd, dgrad; ldnn: fused dReLU+dbias pass, fused classifier head (Linear + softmax-xent + argmax), SGD"),
+                      "hipBLASLt: fp32 wgrads, bias/ReLU fwd, hidden dgrad; ldnn: fused dReLU+dbias pass, "
+                      "classifier head (Linear + softmax-xent + argmax + head dgrad), SGD"),
             "grad_sync": ("none (1 GPU)" if n == 1 else
                           "fp32 RCCL all-reduce, bucketed, overlapped" if args.no_shard else
                           "fp32 RCCL reduce-scatter (bucketed, overlapped) + sharded SGD + bf16 weight all-gather"),
