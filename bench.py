@@ -96,7 +96,8 @@ def run_ldnn(ctx, args):
                           bucket_cap_elems=args.bucket_elems, shard_optimizer=False if args.no_shard else None,
                           library_gemms=not args.no_library_gemms,
                           early_optimizer={"on": True, "off": False, "auto": None}[args.early_opt],
-                          fuse_head_dgrad=False if args.no_fuse_head_dgrad else None)
+                          fuse_head_dgrad=False if args.no_fuse_head_dgrad else None,
+                          concurrent_wgrad=args.concurrent_wgrad)
     if ctx.distributed:
         dist.broadcast(eng.flat.master, src=0)
         eng.flat.refresh_shadow()
@@ -156,6 +157,8 @@ def main():
                     help="all-reduce + replicated optimizer instead of reduce-scatter / sharded optimizer / all-gather")
     ap.add_argument("--no-library-gemms", action="store_true",
                     help="run the plain GEMMs (fp32 wgrads, bias+ReLU forwards) on ldnn's MFMA kernels instead of hipBLASLt")
+    ap.add_argument("--concurrent-wgrad", action="store_true",
+                    help="1 GPU: wgrad(1) on a side stream beside dgrad(1) + wgrad(0)")
     ap.add_argument("--no-fuse-head-dgrad", action="store_true",
                     help="separate head dgrad GEMM instead of the head kernel's fused dgrad (dReLU + dbias)")
     ap.add_argument("--early-opt", choices=["auto", "on", "off"], default="auto",

@@ -99,7 +99,7 @@ class StaticMLPEngine:
                  shard_optimizer: bool | None = None, overlap_optimizer: bool = False, wgrad_combine: bool = True,
                  fuse_optimizer: bool | None = None, library_gemms: bool | None = None,
                  fuse_head_dgrad: bool | None = None, early_optimizer: bool | None = None,
-                 library_dgrad: bool | None = None):
+                 library_dgrad: bool | None = None, concurrent_wgrad: bool = False):
         from ..models.mlp import MLP
 
         if not isinstance(model, MLP):
@@ -326,7 +326,16 @@ class StaticMLPEngine:
             self._w1_span = (s1.offset, s1.offset + s1.storage_numel)
             self._w0_begin = f.seg(self.layers[0].weight).offset
             self._early_scratch = torch.empty(s1.storage_numel, dtype=torch.bfloat16, device=self.device)
-        self.side = torch.cuda.Stream(device=self.device) if (overlap_optimizer or self.early_optimizer) else None
+        # concurrent_wgrad (single process, L >= 2, plain schedule): wgrad(1) runs on a
+        # side stream BESIDE dgrad(1) -> act pass -> wgrad(0) (they share only reads of
+        # dz_2 / h_1), so the 784-wide wgrad(0), whose grid covers < 256 CUs, fills in
+        # next to the full-grid wgrad(1) instead of running alone.  Off by default:
+        # measured neutral on MI355X (batch 16384: 1.785/1.787 vs 1.789/1.782 ms/step;
+        # batch 4096: 0.559 vs 0.566) -- the two hipBLASLt GEMMs do not co-run usefully.
+        self.concurrent_wgrad = (bool(concurrent_wgrad) and not self.distributed and L >= 2
+                                 and not overlap_optimizer and not self.early_optimizer and not any(self._fused))
+        self.side = (torch.cuda.Stream(device=self.device)
+                     if (overlap_optimizer or self.early_optimizer or self.concurrent_wgrad) else None)
         self._pending_gather = {}
         if self.shard:
             self.gshard = [torch.zeros((e - b) // self.world, dtype=torch.float32, device=dev)
@@ -421,6 +430,11 @@ class StaticMLPEngine:
             for b, e in ranges:
                 if e > b:
                     self._opt(b, e)
+
+    def _fork_wgrad(self, l):
+        self.side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(self.side):
+            self._wgrad(l)
 
     def _join(self):
         torch.cuda.current_stream().wait_stream(self.side)
@@ -520,6 +534,11 @@ class StaticMLPEngine:
             elif any(self._fused):
                 fns = [fn for p in pieces for fn in p] + [lambda b=b, e=e: self._opt(b, e)
                                                           for b, e in self._unfused_ranges()]
+            elif self.concurrent_wgrad:
+                fns = [fn for p in pieces for fn in p]
+                i1 = next(i for i, fn in enumerate(fns) if getattr(fn, "_ldnn_wgrad", None) == 1)
+                fns[i1] = lambda: self._fork_wgrad(1)
+                fns += [self._join, lambda: self._opt(0, self.flat.numel)]
             else:
                 fns = [fn for p in pieces for fn in p] + [lambda: self._opt(0, self.flat.numel)]
             self.segments = [_Segment(run(fns), self.use_graphs)]

@@ -281,3 +281,30 @@ def test_library_dgrad_matches_fused_dgrad(act):
     for a, b in zip(l1, l2):
         assert abs(a - b) < 1e-2 * max(1.0, abs(b)), (l1, l2)
     torch.testing.assert_close(e1.flat.master, e2.flat.master, rtol=2e-2, atol=2e-3)
+
+
+@pytest.mark.parametrize("graphs", [False, True])
+def test_concurrent_wgrad_side_stream_matches_serial(graphs):
+    """wgrad(1) on a side stream beside dgrad(1) + wgrad(0) == the serial schedule."""
+    torch.manual_seed(0)
+    B = 2048
+    m1, m2 = mlp3(784, 1024, 10), mlp3(784, 1024, 10)
+    m2.load_state_dict(m1.state_dict())
+    cfg = OptimConfig("sgd", lr=0.05, momentum=0.9)
+    e1 = StaticMLPEngine(m1, B, cfg, use_graphs=graphs, concurrent_wgrad=True)
+    e2 = StaticMLPEngine(m2, B, cfg, use_graphs=graphs, concurrent_wgrad=False)
+    assert e1.concurrent_wgrad and not e2.concurrent_wgrad
+    g = torch.Generator(device="cuda").manual_seed(3)
+    l1, l2 = [], []
+    for i in range(6):
+        x = torch.randn(B, 784, device="cuda", generator=g).bfloat16()
+        y = torch.randint(0, 10, (B,), device="cuda", generator=g)
+        for e, ls in ((e1, l1), (e2, l2)):
+            e.reset_stats()
+            e.load_batch(x, y)
+            e.step()
+            ls.append(e.read_stats(B)[0])
+    torch.cuda.synchronize()
+    for a, b in zip(l1, l2):
+        assert abs(a - b) < 1e-2 * max(1.0, abs(b)), (l1, l2)
+    torch.testing.assert_close(e1.flat.master, e2.flat.master, rtol=2e-2, atol=2e-3)
