@@ -21,7 +21,12 @@
 //                  separate K = 16 dgrad GEMM (fwd 11 -> 32 us fused vs 11 + 22.6):
 //                  the 32 MB dh store (5.4 us), the class-loop FMAs (5.5 us) and the
 //                  slab reduction (5 us) all land after the h stream instead of
-//                  overlapping it, so the engine leaves it off by default.
+//                  overlapping it.  At batch 16384 with the hipBLASLt dgrad it wins
+//                  (129 us fused incl. the slab sum vs 51 + 68 us + the head fwd; step
+//                  1.848 vs 1.887 ms), so the engine turns it on with library_dgrad.
+//                  The dgrad re-reads h from global memory (L2 / Infinity Cache) by
+//                  default; LDNN_HEAD_DG_LDS=1 stages it in LDS -- measured equal
+//                  (1.870 vs 1.868 ms/step), the global variant needs 7 KiB of LDS.
 //  head_wgrad:     dW = dlogits^T h (+ db = column sums of dlogits).  The
 //                  reduction runs over the batch, the strided dimension of both
 //                  operands, so each wave stages its 32-row chunks through a
@@ -29,6 +34,8 @@
 //                  (hardware transpose) into MFMA fragments.  64 output
 //                  columns x a batch slice per workgroup; slices combine with
 //                  fp32 atomics into the (pre-cleared) gradient.
+#include <cstdlib>
+
 #include "ldnn_common.h"
 #include "ldnn_gemm_tile.h"
 #include "ldnn_kernels.h"
@@ -152,7 +159,7 @@ __device__ __forceinline__ void head_softmax_xent(const HeadParams& p, floatx4 (
 // of this workgroup; thread t owns column chunks q = t, t + 512, ... (coalesced
 // 16-B stores), keeps the 16 x 8 accumulators in registers over the classes, and
 // adds its column sums to the previous layer's bias gradient.
-template <int DEPI>
+template <int DEPI, bool HS>
 __device__ __forceinline__ void head_dgrad_rows(const HeadParams& p, const char* hs, const float* dls, int m0) {
   const int nq = p.K >> 3;
   const int rows = min(16, p.B - m0);
@@ -178,7 +185,8 @@ __device__ __forceinline__ void head_dgrad_rows(const HeadParams& p, const char*
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       if (r >= rows) continue;
-      const u16x8 hv = *reinterpret_cast<const u16x8*>(hs + hs_off(r, q, p.K));
+      const u16x8 hv = HS ? *reinterpret_cast<const u16x8*>(hs + hs_off(r, q, p.K))
+                          : *reinterpret_cast<const u16x8*>(p.h + (size_t)(m0 + r) * p.ldh + 8 * q);
       u16x8 o;
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
@@ -200,12 +208,16 @@ __device__ __forceinline__ void head_dgrad_rows(const HeadParams& p, const char*
 }
 
 // DEPI: -1 = no fused dgrad; EPI_NONE / EPI_DRELU / EPI_DSIGMOID = dgrad with that
-// activation derivative
-template <int NT, int DEPI>
+// activation derivative.  HS: the dgrad reads h from the workgroup's LDS copy
+// (138 KiB of LDS: one workgroup per CU, so the h stream, the softmax and the dgrad
+// of a CU never overlap) instead of re-reading its 16 rows from global memory,
+// where they were just streamed through L2 / the 256 MB Infinity Cache and where
+// the 7 KiB workgroups co-reside and overlap their phases.
+template <int NT, int DEPI, bool HS>
 __global__ __launch_bounds__(kFwdWaves * 64) void head_fwd_xent_kernel(HeadParams p) {
   constexpr bool DG = DEPI >= 0;
   constexpr int kRedBytes = (kFwdWaves - 1) * NT * 64 * 16;
-  __shared__ __attribute__((aligned(16))) char smem[kRedBytes + (DG ? 16 * kHeadDgradMaxK * 2 : 0)];
+  __shared__ __attribute__((aligned(16))) char smem[kRedBytes + (DG && HS ? 16 * kHeadDgradMaxK * 2 : 0)];
   floatx4(*red)[NT][64] = reinterpret_cast<floatx4(*)[NT][64]>(smem);
   char* hs = smem + kRedBytes;
   float* dls = reinterpret_cast<float*>(smem);  // [16][ld] dlogits, over red once wave 0 has consumed it
@@ -223,7 +235,7 @@ __global__ __launch_bounds__(kFwdWaves * 64) void head_fwd_xent_kernel(HeadParam
     const int k = st * 32 + kq;
     const bool kok = k < p.K;
     const bf16x8 a = (row < p.B && kok) ? *reinterpret_cast<const bf16x8*>(p.h + (size_t)row * p.ldh + k) : zero;
-    if constexpr (DG) {
+    if constexpr (DG && HS) {
       if (kok) *reinterpret_cast<bf16x8*>(hs + hs_off(lane & 15, k >> 3, p.K)) = a;
     }
 #pragma unroll
@@ -241,7 +253,7 @@ __global__ __launch_bounds__(kFwdWaves * 64) void head_fwd_xent_kernel(HeadParam
   if (w == 0) head_softmax_xent<NT, DG>(p, acc, red, dls, lane, row, m0);
   if constexpr (DG) {
     __syncthreads();  // dlogits of the 16 rows in LDS, h staged
-    head_dgrad_rows<DEPI>(p, hs, dls, m0);
+    head_dgrad_rows<DEPI, HS>(p, hs, dls, m0);
   }
 }
 
@@ -383,16 +395,30 @@ __global__ __launch_bounds__(kWgWaves * 64) void head_wgrad_kernel(HeadWgradPara
   }
 }
 
-template <int DEPI>
+template <int DEPI, bool HS>
 hipError_t launch_head_fwd(const HeadParams& p, hipStream_t s) {
   const dim3 grid((p.B + 15) / 16), block(kFwdWaves * 64);
   switch (p.ld / 16) {
-    case 1: head_fwd_xent_kernel<1, DEPI><<<grid, block, 0, s>>>(p); break;
-    case 2: head_fwd_xent_kernel<2, DEPI><<<grid, block, 0, s>>>(p); break;
-    case 3: head_fwd_xent_kernel<3, DEPI><<<grid, block, 0, s>>>(p); break;
-    default: head_fwd_xent_kernel<4, DEPI><<<grid, block, 0, s>>>(p); break;
+    case 1: head_fwd_xent_kernel<1, DEPI, HS><<<grid, block, 0, s>>>(p); break;
+    case 2: head_fwd_xent_kernel<2, DEPI, HS><<<grid, block, 0, s>>>(p); break;
+    case 3: head_fwd_xent_kernel<3, DEPI, HS><<<grid, block, 0, s>>>(p); break;
+    default: head_fwd_xent_kernel<4, DEPI, HS><<<grid, block, 0, s>>>(p); break;
   }
   return hipGetLastError();
+}
+
+// LDNN_HEAD_DG_LDS=1 selects the LDS-staged h for the fused head dgrad
+bool head_dg_lds() {
+  static const bool v = [] {
+    const char* e = std::getenv("LDNN_HEAD_DG_LDS");
+    return e != nullptr && e[0] == '1';
+  }();
+  return v;
+}
+
+template <int DEPI>
+hipError_t launch_head_fwd_dg(const HeadParams& p, hipStream_t s) {
+  return head_dg_lds() ? launch_head_fwd<DEPI, true>(p, s) : launch_head_fwd<DEPI, false>(p, s);
 }
 
 }  // namespace
@@ -400,14 +426,14 @@ hipError_t launch_head_fwd(const HeadParams& p, hipStream_t s) {
 hipError_t head_fwd_xent(const HeadParams& p, hipStream_t s) {
   if (p.B <= 0) return hipSuccess;
   if (p.ld > 64 || p.ld % 16 != 0 || p.C > p.ld || p.ldw_rows > p.ld || p.K % 8 != 0) return hipErrorInvalidValue;
-  if (p.dh == nullptr) return launch_head_fwd<-1>(p, s);
+  if (p.dh == nullptr) return launch_head_fwd<-1, false>(p, s);
   if (p.K > kHeadDgradMaxK || p.lddh % 8 != 0 || (p.dbias != nullptr && p.dbias_ws == nullptr))
     return hipErrorInvalidValue;
   hipError_t e;
   switch (p.dgrad_epi) {
-    case EPI_NONE: e = launch_head_fwd<EPI_NONE>(p, s); break;
-    case EPI_DRELU: e = launch_head_fwd<EPI_DRELU>(p, s); break;
-    case EPI_DSIGMOID: e = launch_head_fwd<EPI_DSIGMOID>(p, s); break;
+    case EPI_NONE: e = launch_head_fwd_dg<EPI_NONE>(p, s); break;
+    case EPI_DRELU: e = launch_head_fwd_dg<EPI_DRELU>(p, s); break;
+    case EPI_DSIGMOID: e = launch_head_fwd_dg<EPI_DSIGMOID>(p, s); break;
     default: return hipErrorInvalidValue;
   }
   // per-workgroup column sums -> bias gradient: 256 same-address fp32 atomics per
