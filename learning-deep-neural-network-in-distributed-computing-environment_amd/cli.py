@@ -70,6 +70,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--no_repartition", action="store_true")
     p.add_argument("--check_every", type=int, default=20, help="steps between straggler-cutoff rounds")
     p.add_argument("--bucket_mb", type=float, default=32.0)
+    p.add_argument("--grad_comm_dtype", choices=["fp32", "bf16"], default="fp32",
+                   help="dtype of the per-step gradient all-reduce (bf16 halves the xGMI bytes)")
     p.add_argument("--augment", action="store_true", help="GPU flip+crop augmentation")
     p.add_argument("--out_dir", type=str, default="runs/latest")
     p.add_argument("--plots", type=str, default="Graphs", help="output folder of the six plots ('' to skip)")
@@ -118,7 +120,8 @@ def main(argv=None):
 
     dp = None
     if args.sync_every == "step" and args.topology == "allreduce" and world > 1:
-        dp = DataParallel(model, comm, bucket_cap_mb=args.bucket_mb, average=args.aggregation_type == "equal")
+        dp = DataParallel(model, comm, bucket_cap_mb=args.bucket_mb, average=args.aggregation_type == "equal",
+                          comm_dtype=torch.bfloat16 if args.grad_comm_dtype == "bf16" else None)
     else:  # reference A6: broadcast every state_dict entry from rank 0
         D.broadcast_module(model)
         flat.refresh_shadow()

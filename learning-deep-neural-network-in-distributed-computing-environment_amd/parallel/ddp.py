@@ -16,7 +16,12 @@ BAR/trainer.py:141-150 vs :205,210).  This is the real thing, MI355X-style:
   through post-accumulate-grad hooks -- so communication overlaps the rest of
   the backward pass;
 * averaging (1/N) is folded into the fused optimizer (``flat.grad_scale``)
-  instead of a separate division kernel.
+  instead of a separate division kernel;
+* ``comm_dtype=torch.bfloat16`` halves the xGMI bytes (the 178 MB
+  fp32 gradient of EnhancedCNNModel against a ~0.17 ms step at batch 64): each
+  bucket is cast into a persistent bf16 staging buffer on the compute stream,
+  all-reduced in bf16, and widened back into the fp32 gradient after the wait.
+  The optimizer still runs on fp32 master weights.
 """
 from __future__ import annotations
 
@@ -38,8 +43,10 @@ def ensure_flat(module: nn.Module, device=None) -> FlatParams:
 
 
 class GradBucketer:
-    def __init__(self, flat: FlatParams, comm: Comm, bucket_cap_elems: int = 8 << 20):
+    def __init__(self, flat: FlatParams, comm: Comm, bucket_cap_elems: int = 8 << 20,
+                 comm_dtype: torch.dtype | None = None):
         self.flat, self.comm = flat, comm
+        self.comm_dtype = None if comm_dtype in (None, torch.float32) else comm_dtype
         self.buckets: list[dict] = []
         cur = None
         for seg in flat.segments:
@@ -57,6 +64,8 @@ class GradBucketer:
         for i, b in enumerate(self.buckets):
             for p in b["params"]:
                 self.of_param[id(p)] = i
+        self._stage = ([torch.empty(b["end"] - b["begin"], dtype=self.comm_dtype, device=flat.grad.device)
+                        for b in self.buckets] if self.comm_dtype is not None else None)
         self.works: list = []
         self._pending: list[int] = []
         self._launched: list[bool] = []
@@ -73,7 +82,13 @@ class GradBucketer:
     def _launch(self, i):
         b = self.buckets[i]
         self._launched[i] = True
-        self.works.append(self.comm.all_reduce(self.flat.grad[b["begin"]: b["end"]], SUM, async_op=True))
+        g = self.flat.grad[b["begin"]: b["end"]]
+        if self._stage is not None:
+            st = self._stage[i]
+            st.copy_(g)
+            self.works.append((self.comm.all_reduce(st, SUM, async_op=True), i))
+        else:
+            self.works.append((self.comm.all_reduce(g, SUM, async_op=True), None))
 
     def _on_ready(self, p):
         if not self.active or id(p) in self._seen:
@@ -92,9 +107,12 @@ class GradBucketer:
         for i in range(len(self.buckets)):  # params that got no gradient this step
             if not self._launched[i]:
                 self._launch(i)
-        for w in self.works:
+        for w, i in self.works:
             if w is not None:
                 w.wait()
+            if i is not None:
+                b = self.buckets[i]
+                self.flat.grad[b["begin"]: b["end"]].copy_(self._stage[i])
         self.works = []
         self.active = False
 
@@ -103,7 +121,7 @@ class DataParallel(nn.Module):
     """Wrap a model for synchronous per-step DP (SURVEY P1 done per step)."""
 
     def __init__(self, module: nn.Module, comm: Comm | None = None, bucket_cap_mb: float = 32.0,
-                 broadcast_init: bool = True, average: bool = True):
+                 broadcast_init: bool = True, average: bool = True, comm_dtype: torch.dtype | None = None):
         super().__init__()
         self.module = module
         self.comm = comm or default_comm()
@@ -115,7 +133,7 @@ class DataParallel(nn.Module):
                     self.comm.broadcast(b, 0)
             self.flat.refresh_shadow()
         self.flat.grad_scale = (1.0 / self.comm.world_size) if average else 1.0
-        self.bucketer = GradBucketer(self.flat, self.comm, int(bucket_cap_mb * (1 << 20) / 4))
+        self.bucketer = GradBucketer(self.flat, self.comm, int(bucket_cap_mb * (1 << 20) / 4), comm_dtype=comm_dtype)
 
     def forward(self, *args, **kwargs):
         if self.training and torch.is_grad_enabled() and self.comm.world_size > 1:

@@ -30,7 +30,7 @@ def _init(rank, world, port, timeout=60):
     dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout))
 
 
-def _dp_worker(rank, world, port, out):
+def _dp_worker(rank, world, port, out, comm_dtype=None):
     _init(rank, world, port)
     import ldnn
     from ldnn.models.mlp import mlp2
@@ -41,7 +41,7 @@ def _dp_worker(rank, world, port, out):
     torch.manual_seed(123 + rank)  # different init on purpose: DataParallel must broadcast rank 0's
     m = mlp2(784, 32, 10)
     ldnn.prepare(m, "cpu")
-    dp = DataParallel(m, TorchComm(), bucket_cap_mb=0.01)  # tiny buckets -> several overlapped messages
+    dp = DataParallel(m, TorchComm(), bucket_cap_mb=0.01, comm_dtype=comm_dtype)  # tiny buckets -> several messages
     assert len(dp.bucketer.buckets) > 1
     opt = SGD(m.parameters(), lr=0.1, momentum=0.9)
     g = torch.Generator().manual_seed(7)
@@ -58,9 +58,10 @@ def _dp_worker(rank, world, port, out):
     dist.destroy_process_group()
 
 
-def test_bucketed_dp_equals_big_batch_single_process(tmp_path):
+@pytest.mark.parametrize("comm_dtype", [None, torch.bfloat16])
+def test_bucketed_dp_equals_big_batch_single_process(tmp_path, comm_dtype):
     world, port, out = 2, _port(), str(tmp_path / "dp.pt")
-    mp.spawn(_dp_worker, args=(world, port, out), nprocs=world, join=True)
+    mp.spawn(_dp_worker, args=(world, port, out, comm_dtype), nprocs=world, join=True)
     sys.path.insert(0, ROOT)
     import ldnn
     from ldnn.models.mlp import mlp2
@@ -78,8 +79,9 @@ def test_bucketed_dp_equals_big_batch_single_process(tmp_path):
         torch.nn.functional.cross_entropy(m(x), y).backward()
         opt.step()
     got = torch.load(out, weights_only=True)
+    tol = dict(rtol=1e-5, atol=1e-6) if comm_dtype is None else dict(rtol=2e-2, atol=2e-3)  # bf16 gradient sums
     for k, v in m.state_dict().items():
-        torch.testing.assert_close(got[k], v, rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(got[k], v, **tol)
 
 
 def _gossip_worker(rank, world, port, q):
