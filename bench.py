@@ -97,7 +97,8 @@ def run_ldnn(ctx, args):
                           library_gemms=not args.no_library_gemms,
                           early_optimizer={"on": True, "off": False, "auto": None}[args.early_opt],
                           fuse_head_dgrad=False if args.no_fuse_head_dgrad else None,
-                          concurrent_wgrad=args.concurrent_wgrad, overlap_optimizer=args.overlap_opt)
+                          concurrent_wgrad=args.concurrent_wgrad, overlap_optimizer=args.overlap_opt,
+                          pad_input=args.pad_input)
     if ctx.distributed:
         dist.broadcast(eng.flat.master, src=0)
         eng.flat.refresh_shadow()
@@ -157,6 +158,8 @@ def main():
                     help="all-reduce + replicated optimizer instead of reduce-scatter / sharded optimizer / all-gather")
     ap.add_argument("--no-library-gemms", action="store_true",
                     help="run the plain GEMMs (fp32 wgrads, bias+ReLU forwards) on ldnn's MFMA kernels instead of hipBLASLt")
+    ap.add_argument("--pad-input", action="store_true",
+                    help="pad the 784-wide first layer to K = 832 for hipBLASLt (measured slightly slower)")
     ap.add_argument("--overlap-opt", action="store_true",
                     help="1 GPU: optimizer update of all weights but W_0 on a side stream beside wgrad(0)")
     ap.add_argument("--concurrent-wgrad", action="store_true",

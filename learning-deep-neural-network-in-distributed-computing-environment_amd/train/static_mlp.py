@@ -99,7 +99,7 @@ class StaticMLPEngine:
                  shard_optimizer: bool | None = None, overlap_optimizer: bool = False, wgrad_combine: bool = True,
                  fuse_optimizer: bool | None = None, library_gemms: bool | None = None,
                  fuse_head_dgrad: bool | None = None, early_optimizer: bool | None = None,
-                 library_dgrad: bool | None = None, concurrent_wgrad: bool = False):
+                 library_dgrad: bool | None = None, concurrent_wgrad: bool = False, pad_input: bool = False):
         from ..models.mlp import MLP
 
         if not isinstance(model, MLP):
@@ -249,6 +249,25 @@ class StaticMLPEngine:
                            for l in range(L)]
         self._act_code = [None] + [{"relu": self.C.ACT_RELU, "sigmoid": self.C.ACT_SIGMOID}.get(
             self.layers[l - 1].activation) for l in range(1, L)]
+        # pad_input: with both first-layer GEMMs on hipBLASLt, the input width is padded
+        # to a multiple of 64 with zero columns (784 -> 832): measured on MI355X at batch
+        # 16384 (scripts/bench_k_pad.py, profiles/first_layer_kpad_b16384_r1.jsonl) the
+        # fwd goes 108 -> 92 us and the wgrad 173 -> 155 us.  The forward reads a padded
+        # bf16 copy of W_0 refreshed right before it (6.4 MB), the wgrad writes a padded
+        # fp32 scratch whose real columns are copied into the flat gradient.  Off by
+        # default: in the step it measured slightly SLOWER (batch 16384: 1.863/1.861 vs
+        # 1.859/1.853 ms; batch 4096: 0.583 vs 0.571) -- the in-step wgrad kept its
+        # 128x128 hipBLASLt solution (194 us) and the two copies ate the forward's gain.
+        K0 = self.layers[0].in_features
+        self.in_pad = 0
+        if pad_input and K0 % 64 and self._lib_fwd[0] and self._lib_wgrad[0]:
+            Kp = (K0 + 63) // 64 * 64
+            self.in_pad = Kp
+            self.xp = torch.zeros(B, Kp, dtype=bf, device=dev)
+            self.x = self.xp[:, :K0]
+            self.h[0] = self.xp
+            self.W0p = torch.zeros(self.W[0].shape[0], Kp, dtype=bf, device=dev)
+            self.dW0p = torch.zeros(self.W[0].shape[0], Kp, dtype=torch.float32, device=dev)
         self.bias_bf16 = [f.shadow_storage(l.bias) for l in self.layers]
         self._wgrad_splitk, self._wgrad_ws = [], []
         for l, layer in enumerate(self.layers):
@@ -372,6 +391,10 @@ class StaticMLPEngine:
             self.C.head_wgrad(self.dz[l + 1], self.h[l], self.dW[l], self.db[l], sk)
             return
         if self._lib_wgrad[l]:   # plain GEMM, fp32 out: hipBLASLt straight into the flat grad buffer
+            if l == 0 and self.in_pad:
+                torch.mm(self.dz[1].t(), self.xp, out_dtype=torch.float32, out=self.dW0p)
+                self.dW[0].copy_(self.dW0p[:, : self.layers[0].in_features])
+                return
             torch.mm(self.dz[l + 1].t(), self.h[l], out_dtype=torch.float32, out=self.dW[l])
             return
         if self._wgrad_ws[l] is not None:   # in-launch split-K combine, overwrites the gradient
@@ -600,10 +623,14 @@ class StaticMLPEngine:
     def _forward_layer(self, l):
         C = self.C
         if self._lib_fwd[l]:
+            W = self.W[l]
+            if l == 0 and self.in_pad:   # padded copy of the current (possibly just all-gathered) W_0
+                self.W0p[:, : self.layers[0].in_features].copy_(W)
+                W = self.W0p
             if self.layers[l].activation == "relu":
-                torch._addmm_activation(self.bias_bf16[l], self.h[l], self.W[l].t(), out=self.h[l + 1])
+                torch._addmm_activation(self.bias_bf16[l], self.h[l], W.t(), out=self.h[l + 1])
             else:
-                torch.addmm(self.bias_bf16[l], self.h[l], self.W[l].t(), out=self.h[l + 1])
+                torch.addmm(self.bias_bf16[l], self.h[l], W.t(), out=self.h[l + 1])
             return
         C.gemm(self.h[l], self.W[l], self.h[l + 1], True, True, self._fwd_epi[l], bias=self.bias[l])
 

@@ -308,3 +308,30 @@ def test_concurrent_wgrad_side_stream_matches_serial(graphs):
     for a, b in zip(l1, l2):
         assert abs(a - b) < 1e-2 * max(1.0, abs(b)), (l1, l2)
     torch.testing.assert_close(e1.flat.master, e2.flat.master, rtol=2e-2, atol=2e-3)
+
+
+def test_padded_input_matches_unpadded():
+    """784 -> 832 zero-padded first layer (pad_input) == the unpadded hipBLASLt GEMMs."""
+    torch.manual_seed(0)
+    B = 1024
+    m1, m2 = mlp3(784, 1024, 10), mlp3(784, 1024, 10)
+    m2.load_state_dict(m1.state_dict())
+    cfg = OptimConfig("adam", lr=1e-3)
+    e1 = StaticMLPEngine(m1, B, cfg, use_graphs=True, pad_input=True)
+    e2 = StaticMLPEngine(m2, B, cfg, use_graphs=True, pad_input=False)
+    assert e1.in_pad == 832 and e2.in_pad == 0
+    g = torch.Generator(device="cuda").manual_seed(9)
+    l1, l2 = [], []
+    for i in range(6):
+        x = torch.randn(B, 784, device="cuda", generator=g).bfloat16()
+        y = torch.randint(0, 10, (B,), device="cuda", generator=g)
+        for e, ls in ((e1, l1), (e2, l2)):
+            e.reset_stats()
+            e.load_batch(x, y)
+            e.step()
+            ls.append(e.read_stats(B)[0])
+    torch.cuda.synchronize()
+    for a, b in zip(l1, l2):
+        assert abs(a - b) < 1e-2 * max(1.0, abs(b)), (l1, l2)
+    torch.testing.assert_close(e1.flat.master, e2.flat.master, rtol=2e-2, atol=2e-3)
+    assert e1.xp[:, 784:].abs().max().item() == 0 and e1.W0p[:, 784:].abs().max().item() == 0
