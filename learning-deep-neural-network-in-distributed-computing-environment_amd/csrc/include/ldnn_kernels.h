@@ -60,6 +60,16 @@ hipError_t gemm_bf16(const GemmParams& p, bool a_kcontig, bool b_kcontig, int ep
 hipError_t gemm_bf16_tile(const GemmParams& p, bool a_kcontig, bool b_kcontig, int epi, bool out_f32, int tile,
                           hipStream_t s);
 int gemm_pick_tile(int M, int N, int K, bool out_f32);
+// Ping-pong 256x256 kernel (gemm_pp.hip): same contract; p.splitk > 1 needs the
+// in-launch combine workspace p.ws (gemm_pp_ws_bytes) and p.cnt (gemm_pp_tiles
+// zeroed counters).  Operands must each be < 2 GiB.
+hipError_t gemm_pp(const GemmParams& p, bool a_kcontig, bool b_kcontig, int epi, bool out_f32, hipStream_t s);
+size_t gemm_pp_ws_bytes(int M, int N, int splitk);
+int gemm_pp_tiles(int M, int N);
+// Four-wave 256x256 kernel (gemm_q.hip, 128x128 per wave): same contract as gemm_pp
+// (tiles = gemm_pp_tiles, split-K workspace gemm_q_ws_bytes).
+hipError_t gemm_q(const GemmParams& p, bool a_kcontig, bool b_kcontig, int epi, bool out_f32, hipStream_t s);
+size_t gemm_q_ws_bytes(int M, int N, int splitk);
 // Split-K factor the 128-tile kernel uses for an fp32 EPI_NONE output (1 = none).
 int gemm_pick_splitk(int M, int N, int K);
 // Skinny-N forward GEMM (N <= 64, both operands k-contiguous, bf16 out): one

@@ -251,84 +251,6 @@ __device__ __forceinline__ void barrier() {
   asm volatile("" ::: "memory");
 }
 
-// LDS-staged bf16 epilogue: each wave parks its fp32 128x64 tile in LDS (two
-// 64-row halves of 16 KiB, 16-B chunk XOR-swizzled by row so the staging
-// writes are conflict-free), then re-reads it ROW-wise: 8 lanes cover one
-// 64-column row segment, so aux loads and output stores are full 128-B row
-// runs instead of 16 rows x 32 B per instruction.  Bias-gradient column sums
-// stay per lane (8 fixed columns) and are shuffle-reduced once at the end.
-template <int EPI>
-__device__ __forceinline__ void epilogue_lds_bf16(const GemmParams& p, floatx4 (&acc)[4][8], char* smem, int wid,
-                                                  int mbase, int nbase, int lane) {
-  float* wbuf = reinterpret_cast<float*>(smem + wid * 16384);  // [64 rows][64 cols] fp32, swizzled
-  const int col8 = lane & 7;                                     // this lane's 8 columns
-  const int n = nbase + col8 * 8;
-  const bool nok = n < p.N;
-  float bias[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_RELU || EPI == EPI_BIAS_SIGMOID) {
-    if (nok) {
-      const floatx4 b0 = *reinterpret_cast<const floatx4*>(p.bias + n);
-      const floatx4 b1 = *reinterpret_cast<const floatx4*>(p.bias + n + 4);
-      bias[0] = b0[0]; bias[1] = b0[1]; bias[2] = b0[2]; bias[3] = b0[3];
-      bias[4] = b1[0]; bias[5] = b1[1]; bias[6] = b1[2]; bias[7] = b1[3];
-    }
-  }
-  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    // stage m-tiles 4h..4h+3: lane holds C[m = i*16 + (l&15)][n = j*16 + 4*(l>>4) + r]
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int row = i * 16 + (lane & 15);
-        const int chunk = j * 4 + (lane >> 4);  // 16-B chunk (4 floats) within the 256-B row
-        *reinterpret_cast<floatx4*>(reinterpret_cast<char*>(wbuf) + row * 256 + ((chunk ^ (row & 15)) << 4)) =
-            acc[j][h * 4 + i];
-      }
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): own staging writes landed (wave-private region)
-    __builtin_amdgcn_wave_barrier();
-#pragma unroll 2
-    for (int it = 0; it < 8; ++it) {
-      const int row = it * 8 + (lane >> 3);
-      const int m = mbase + h * 64 + row;
-      const char* rb = reinterpret_cast<const char*>(wbuf) + row * 256;
-      const floatx4 v0 = *reinterpret_cast<const floatx4*>(rb + (((2 * col8) ^ (row & 15)) << 4));
-      const floatx4 v1 = *reinterpret_cast<const floatx4*>(rb + (((2 * col8 + 1) ^ (row & 15)) << 4));
-      if (!(nok && m < p.M)) continue;
-      float aux[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      if constexpr (EPI == EPI_DRELU || EPI == EPI_DSIGMOID) {
-        const u16x8 a8 = *reinterpret_cast<const u16x8*>(p.aux + (size_t)m * p.ldaux + n);
-#pragma unroll
-        for (int q = 0; q < 8; ++q) aux[q] = bf2f(a8[q]);
-      }
-      u16x8 o;
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const float v = apply_epi<EPI>(q < 4 ? v0[q] : v1[q - 4], bias[q], aux[q]);
-        o[q] = f2bf(v);
-        cs[q] += bf2f(o[q]);
-      }
-      *reinterpret_cast<u16x8*>(reinterpret_cast<bf16_t*>(p.C) + (size_t)m * p.ldc + n) = o;
-    }
-    __builtin_amdgcn_wave_barrier();
-  }
-  if (p.dbias != nullptr) {
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      float t = cs[q];
-      t += __shfl_xor(t, 8, 64);
-      t += __shfl_xor(t, 16, 64);
-      t += __shfl_xor(t, 32, 64);
-      cs[q] = t;
-    }
-    if (lane < 8 && nok) {
-#pragma unroll
-      for (int q = 0; q < 8; ++q) atomicAdd(p.dbias + n + q, cs[q]);
-    }
-  }
-}
-
 template <bool A_KC, bool B_KC, int EPI, bool OUT_F32>
 __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(GemmParams p) {
   __shared__ __attribute__((aligned(1024))) char smem[2 * kStageBytes];  // [stage][A|B], 128 KiB
@@ -545,7 +467,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(GemmParams p) {
   }
   if constexpr (!OUT_F32) {
     barrier();
-    k256::epilogue_lds_bf16<EPI>(p, acc, smem, wid, m0 + wm * 128, n0 + wn * 64, lane);
+    epilogue_lds_bf16<EPI>(p, acc, smem, wid, m0 + wm * 128, n0 + wn * 64, lane);
   } else {
     epilogue<EPI, OUT_F32, 8, 4>(p, acc, m0 + wm * 128, n0 + wn * 64, lane);
   }

@@ -1,0 +1,440 @@
+// Four-wave 256x256 bf16 MFMA GEMM for gfx950: the big GEMMs of the MLP step.
+//
+//   C[m][n] = epi( sum_k A(m,k) * B(k,n) )   fp32 accumulation; same operand
+//   layouts / epilogues / GemmParams contract as gemm.hip (A_KC, B_KC, EPI_*).
+//
+// Design (measured on MI355X against gemm.hip's 8-wave k256 and gemm_pp.hip,
+// profiles/gemm_q_r2.txt):
+//  * ONE wave per SIMD, each owning a 128 x 128 block of C: 8 x 8 accumulator
+//    tiles of v_mfma_f32_16x16x32_bf16 = 256 accumulator registers (AGPR half of
+//    the unified 512-entry file at 1 wave/SIMD), 128 VGPRs of operand fragments.
+//    Per K-tile a wave reads (128 + 128) x 64 x 2 B = 32 KiB from LDS for 2 MFLOP,
+//    two thirds of the LDS traffic per FLOP of a 128x64-per-wave layout; the
+//    8-wave kernels were LDS-read bound (SQ_WAIT_INST_LDS, profiles/).
+//  * Software pipeline inside the wave: the K-tile is two 32-deep sub-steps; the
+//    fragments of sub-step s+1 are read while the 64 MFMAs of sub-step s run
+//    (two fragment register sets), so the MFMA pipe never waits on LDS.
+//  * Operands HBM/L2 -> LDS by LDS-DMA (buffer_load_dwordx4 ... lds): 2 K-tile
+//    stages x (A + B) x 32 KiB = 128 KiB.  Tile t+2's DMA is issued right after
+//    the one per-tile barrier (which certifies every wave finished reading the
+//    stage tile t used), so a DMA has one full K-tile (~128 MFMAs per SIMD) to land.
+//  * Per-tile buffer resource rebased to the K-tile (scalar), per-lane offsets
+//    precomputed once: the loop issues 16 DMA instructions per wave with no
+//    address VALU.  Range checking of the resource zero-fills rows past the
+//    operand; a K tail (K % 64 != 0) of a k-contiguous operand is masked per slot.
+//  * LDS images, fragment reads, XCD-aware tile order and the fused epilogues are
+//    shared with gemm.hip (ldnn_gemm_tile.h).
+#include "ldnn_common.h"
+#include "ldnn_gemm_tile.h"
+#include "ldnn_kernels.h"
+
+namespace ldnn {
+namespace {
+namespace kq {
+
+constexpr int BM = 256, BN = 256;
+constexpr int kThreads = 256;
+constexpr int kTile = 256 * BK * 2;      // 32 KiB: one operand's K-tile
+constexpr int kStage = 2 * kTile;        // A + B
+constexpr int kPieces = kTile / 1024 / 4;  // 1-KiB DMA pieces per wave per operand = 8
+constexpr uint32_t kOOB = 0x80000000u;
+
+struct Op {
+  const char* base;
+  uint32_t bytes;            // extent of the operand (range check)
+  uint32_t voff[kPieces];    // this lane's slot offset relative to the K-tile base
+  int kslot;                 // k-contiguous operand: k of this lane's slot (K-tail mask)
+  uint32_t kstep;            // bytes per unit of k
+};
+
+template <bool KC>
+__device__ __forceinline__ void init_op(Op& op, const bf16_t* X, int ld, int rows, int K, int r0, int wid,
+                                        int lane) {
+  op.base = reinterpret_cast<const char*>(X);
+  op.bytes = KC ? (uint32_t)((size_t)rows * ld * 2) : (uint32_t)((size_t)K * ld * 2);
+  op.kstep = KC ? 2u : (uint32_t)ld * 2u;
+  op.kslot = 0;
+#pragma unroll
+  for (int i = 0; i < kPieces; ++i) {
+    int row, k;
+    lds_slot_to_rk<KC, BM>((i * 4 + wid) * 1024 + lane * 16, row, k);
+    const uint32_t r = (uint32_t)(r0 + row);
+    op.voff[i] = KC ? (r * (uint32_t)ld + (uint32_t)k) * 2u : ((uint32_t)k * (uint32_t)ld + r) * 2u;
+    if (KC) op.kslot = k;  // the same for every piece of a lane
+  }
+}
+
+// DMA the K-tile at k0 of one operand into `dst` (8 x buffer_load_dwordx4 ... lds per lane).
+// k0 >= kend (a prefetch past this workgroup's K range) zero-fills without reading.
+template <bool KC>
+__device__ __forceinline__ void issue(const Op& op, char* dst, int k0, int K, int kend, int wid) {
+  const bool past = k0 >= kend;
+  const uint32_t shift = past ? 0u : (uint32_t)k0 * op.kstep;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(op.base + shift), (short)0, past ? 0 : (int)(op.bytes - shift), 0x00020000);
+  const bool kill = KC && (k0 + op.kslot >= K);
+#pragma unroll
+  for (int i = 0; i < kPieces; ++i)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(dst + (i * 4 + wid) * 1024), 16,
+                                             kill ? kOOB : op.voff[i], 0, 0, 0);
+}
+
+template <bool KC>
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_at(const Op& op, int k0, int kend) {
+  const bool past = k0 >= kend;
+  const uint32_t shift = past ? 0u : (uint32_t)k0 * op.kstep;
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(op.base + shift), (short)0, past ? 0 : (int)(op.bytes - shift),
+                                           0x00020000);
+}
+__device__ __forceinline__ void dma1(__amdgpu_buffer_rsrc_t rs, char* dst, const Op& op, int i, bool kill, int wid) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(dst + (i * 4 + wid) * 1024), 16, kill ? kOOB : op.voff[i],
+                                           0, 0, 0);
+}
+
+// Fragment read (same image / lane map as read_frag in ldnn_gemm_tile.h), issued
+// as inline asm: hipcc cannot tell the builtin ds_read_b64_tr_b16 from an alias of
+// the in-flight LDS-DMA writes and would drain the DMA (vmcnt(0)) before every
+// one, and its own counted lgkm waits (which do not see asm reads) over-wait once
+// the two kinds mix.  The compiler counts none of these reads: each consuming
+// sub-step starts with an explicit lgkmcnt(0) (lgkm_all; the barrier does it for
+// sub-step 1) -- the reads were issued a whole sub-step earlier.
+__device__ __forceinline__ uint32_t lds_addr(const char* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+template <bool KC, bool ASM = true>
+__device__ __forceinline__ bf16x8 frag(const char* lds, int rt, int kk, int lane) {
+  if constexpr (KC && !ASM) {
+    return read_frag<true, BM>(lds, rt, kk, lane);
+  } else if constexpr (KC) {
+    const int row = rt * 16 + (lane & 15);
+    const int chunk = kk * 4 + (lane >> 4);
+    bf16x8 v;
+    asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(lds_addr(lds) + (uint32_t)(row * 128 + ((chunk ^ (row & 7)) << 4)))
+                 : "memory");
+    return v;
+  } else {
+    const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+    const int kb = kk * 4 + g;
+    const int sw = (kb & 1) << 2;
+    const uint32_t blk = lds_addr(lds) + (uint32_t)((kb * (BM / 16) + rt) * 256);
+    bf16x4 lo, hi;
+    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(blk + ((q ^ sw) * 32) + pp * 8) : "memory");
+    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(hi) : "v"(blk + (((4 + q) ^ sw) * 32) + pp * 8) : "memory");
+    return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  }
+}
+__device__ __forceinline__ void lgkm_all() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+template <bool KC, bool ASM>
+__device__ __forceinline__ void read8(bf16x8 (&f)[8], const char* lds, int rt0, int kk, int lane) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) f[i] = frag<KC, ASM>(lds, rt0 + i, kk, lane);
+}
+
+// 64 MFMAs: acc[n-tile j][m-tile i] += B_j^T A_i (MFMA-A <- B fragment: lanes own 4 consecutive columns)
+// The accumulators are pinned to AGPRs ("+a"): with 256 of them the register
+// allocator otherwise splits their live ranges across the two register halves and
+// shuffles them with hundreds of v_accvgpr moves per K-tile.  Operands come from
+// ds_reads (the compiler waits lgkmcnt before each asm); MFMA -> MFMA accumulate
+// chains need no padding, and the AGPR <-> VALU hand-offs around the loop are
+// padded explicitly (mma_fence).
+__device__ __forceinline__ void mfma1(floatx4& acc, const bf16x8& b, const bf16x8& a) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(b), "v"(a) : "memory");
+}
+// 64 MFMAs of one 32-deep sub-step with `extra(q)` issued before MFMA q (q = 0..63):
+// the LDS reads / DMA of the pipeline trickle out between the MFMAs instead of
+// stalling the wave's issue in one burst (the texture path accepts a 1-KiB DMA
+// instruction only every few tens of cycles per CU).  The "memory" clobber pins
+// that order.
+template <typename F>
+__device__ __forceinline__ void mma(floatx4 (&acc)[8][8], const bf16x8 (&fa)[8], const bf16x8 (&fb)[8], F&& extra) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      extra(i * 8 + j);
+      mfma1(acc[j][i], fb[j], fa[i]);
+    }
+}
+// wait states between an MFMA that wrote an accumulator and a VALU / v_accvgpr_read of it
+// (and between v_accvgpr_write initialisation and the first MFMA)
+__device__ __forceinline__ void mma_fence() { asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory"); }
+
+__device__ __forceinline__ void barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// Row-coalesced epilogue of a wave's 128 x 128 tile (bf16 or fp32 output): the
+// fp32 accumulators are parked in the wave's 32 KiB LDS slice one 64-row half at
+// a time ([64][128] fp32, 512-B rows, 16-B chunks XOR-swizzled by row), then
+// re-read ROW-wise -- 16 lanes cover one 128-column row, 4 rows per instruction
+// -- so the saved-activation (aux) loads and the output stores are full 256-B
+// (bf16) / 512-B (fp32) row runs.  All 16 aux rows of a half are loaded before
+// the staging writes, so their latency overlaps it instead of serialising.
+// Bias-gradient column sums stay per lane (8 fixed columns) and are reduced
+// across the 4 row lanes once, then one atomic per column per wave.
+template <int EPI, bool OUT_F32>
+__device__ __forceinline__ void epilogue_q(const GemmParams& p, floatx4 (&acc)[8][8], char* smem, int wid, int mbase,
+                                           int nbase, int lane) {
+  char* wbuf = smem + wid * 32768;
+  const int c8 = lane & 15;  // this lane's 8 columns
+  const int n = nbase + c8 * 8;
+  const bool nok = n < p.N;  // N % 8 == 0
+  constexpr bool kAux = EPI == EPI_DRELU || EPI == EPI_DSIGMOID;
+  constexpr bool kBias = EPI == EPI_BIAS || EPI == EPI_BIAS_RELU || EPI == EPI_BIAS_SIGMOID;
+  float bias[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if constexpr (kBias) {
+    if (nok) {
+      const floatx4 b0 = *reinterpret_cast<const floatx4*>(p.bias + n);
+      const floatx4 b1 = *reinterpret_cast<const floatx4*>(p.bias + n + 4);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        bias[q] = b0[q];
+        bias[q + 4] = b1[q];
+      }
+    }
+  }
+  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    u16x8 a8[16];
+    if constexpr (kAux) {
+#pragma unroll
+      for (int it = 0; it < 16; ++it) {
+        const int m = mbase + h * 64 + it * 4 + (lane >> 4);
+        a8[it] = (nok && m < p.M) ? *reinterpret_cast<const u16x8*>(p.aux + (size_t)m * p.ldaux + n) : u16x8{};
+      }
+    }
+    // lane holds C[m = i*16 + (l&15)][n = j*16 + 4*(l>>4) + r]
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int row = i * 16 + (lane & 15);
+        const int chunk = j * 4 + (lane >> 4);
+        *reinterpret_cast<floatx4*>(wbuf + row * 512 + ((chunk ^ (row & 31)) << 4)) = acc[j][h * 4 + i];
+      }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): own staging writes landed (wave-private slice)
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int it = 0; it < 16; ++it) {
+      const int row = it * 4 + (lane >> 4);
+      const int m = mbase + h * 64 + row;
+      const char* rb = wbuf + row * 512;
+      const floatx4 v0 = *reinterpret_cast<const floatx4*>(rb + (((2 * c8) ^ (row & 31)) << 4));
+      const floatx4 v1 = *reinterpret_cast<const floatx4*>(rb + (((2 * c8 + 1) ^ (row & 31)) << 4));
+      if (!(nok && m < p.M)) continue;
+      float o[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float aux = kAux ? bf2f(a8[it][q]) : 0.f;
+        o[q] = apply_epi<EPI>(q < 4 ? v0[q] : v1[q - 4], bias[q], aux);
+      }
+      if constexpr (OUT_F32) {
+        float* c = reinterpret_cast<float*>(p.C) + (size_t)m * p.ldc + n;
+        floatx4 w0{o[0], o[1], o[2], o[3]}, w1{o[4], o[5], o[6], o[7]};
+        if (p.beta != 0.f) {
+          w0 += p.beta * *reinterpret_cast<const floatx4*>(c);
+          w1 += p.beta * *reinterpret_cast<const floatx4*>(c + 4);
+        }
+        *reinterpret_cast<floatx4*>(c) = w0;
+        *reinterpret_cast<floatx4*>(c + 4) = w1;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          cs[q] += w0[q];
+          cs[q + 4] += w1[q];
+        }
+      } else {
+        u16x8 ob;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          ob[q] = f2bf(o[q]);
+          cs[q] += bf2f(ob[q]);
+        }
+        *reinterpret_cast<u16x8*>(reinterpret_cast<bf16_t*>(p.C) + (size_t)m * p.ldc + n) = ob;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (p.dbias != nullptr) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      float t = cs[q];
+      t += __shfl_xor(t, 16, 64);
+      t += __shfl_xor(t, 32, 64);
+      cs[q] = t;
+    }
+    if (lane < 16 && nok) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) atomicAdd(p.dbias + n + q, cs[q]);
+    }
+  }
+}
+
+// XF: experiment flags (0 in production): bit0 no in-loop DMA, bit1 no DMA wait, bit2 no in-loop ds_reads
+template <bool A_KC, bool B_KC, int EPI, bool OUT_F32, int XF = 0>
+__global__ __launch_bounds__(kThreads, 1) void gemm_kernel(GemmParams p) {
+  constexpr bool kDma = !(XF & 1), kWait = !(XF & 2), kRead = !(XF & 4);
+  // all-k-contiguous kernels let the compiler track their ds_read_b128s (measured faster);
+  // any k-strided operand switches every fragment read to asm (see frag)
+  constexpr bool kAsm = !(A_KC && B_KC);
+  __shared__ __attribute__((aligned(1024))) char smem[2 * kStage];  // 128 KiB, the only LDS object
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  int m0, n0;
+  tile_coords(p.M, p.N, BM, BN, m0, n0);
+
+  const int nk_all = (p.K + BK - 1) / BK;
+  const int per = (nk_all + gridDim.y - 1) / gridDim.y;
+  const int kt0 = blockIdx.y * per;
+  const int nk = max(0, min(nk_all, kt0 + per) - kt0);
+  const int kbase = kt0 * BK;
+
+  Op oa, ob;
+  init_op<A_KC>(oa, p.A, p.lda, p.M, p.K, m0, wid, lane);
+  init_op<B_KC>(ob, p.B, p.ldb, p.N, p.K, n0, wid, lane);
+
+  floatx4 acc[8][8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[j][i] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  const int kend = kbase + nk * BK;
+  auto stage = [&](int t, char* dst) {
+    const int k0 = kbase + t * BK;
+    issue<A_KC>(oa, dst, k0, p.K, kend, wid);
+    issue<B_KC>(ob, dst + kTile, k0, p.K, kend, wid);
+  };
+
+  bf16x8 fa0[8], fb0[8], fa1[8], fb1[8];
+  mma_fence();
+  if (nk > 0) {
+    stage(0, smem);
+    stage(1, smem + kStage);
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // tile 0 landed, tile 1 in flight
+    barrier();
+    read8<A_KC, kAsm>(fa0, smem, wm * 8, 0, lane);
+    read8<B_KC, kAsm>(fb0, smem + kTile, wn * 8, 0, lane);
+  }
+  for (int t = 0; t < nk; ++t) {
+    char* const cur = smem + (t & 1) * kStage;
+    char* const nxt = smem + ((t + 1) & 1) * kStage;
+    // sub-step 0: fragments of sub-step 1 stream in between the MFMAs
+    lgkm_all();  // the fragment reads of F0
+    // (reads every 2nd MFMA: all issued by MFMA 30, so the barrier's lgkmcnt(0) finds them done)
+    mma(acc, fa0, fb0, [&](int q) {
+      const int r = q >> 1;
+      if ((kRead || t == 0) && !(q & 1) && r < 16) {
+        if (r < 8) fa1[r] = frag<A_KC, kAsm>(cur, wm * 8 + r, 1, lane);
+        else fb1[r - 8] = frag<B_KC, kAsm>(cur + kTile, wn * 8 + r - 8, 1, lane);
+      }
+    });
+    // one barrier per K-tile: every wave finished reading `cur`, tile t+1 (own DMA waited) published
+    if (kWait) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    barrier();
+    // sub-step 1: tile t+2's DMA into `cur` and tile t+1's first fragments, between the MFMAs
+    const int k2 = kbase + (t + 2) * BK;
+    const __amdgpu_buffer_rsrc_t ra = rsrc_at<A_KC>(oa, k2, kend), rb = rsrc_at<B_KC>(ob, k2, kend);
+    const bool killa = A_KC && (k2 + oa.kslot >= p.K), killb = B_KC && (k2 + ob.kslot >= p.K);
+    // (DMA every 4th MFMA, reads every 2nd from MFMA 1 on)
+    mma(acc, fa1, fb1, [&](int q) {
+      const int r = q >> 2;
+      if (kDma && !(q & 3)) {
+        if (r < 8) dma1(ra, cur, oa, r, killa, wid);
+        else dma1(rb, cur + kTile, ob, r - 8, killb, wid);
+      }
+      const int rr = q >> 1;
+      if (kRead && (q & 1) && rr < 16) {
+        if (rr < 8) fa0[rr] = frag<A_KC, kAsm>(nxt, wm * 8 + rr, 0, lane);
+        else fb0[rr - 8] = frag<B_KC, kAsm>(nxt + kTile, wn * 8 + rr - 8, 0, lane);
+      }
+    });
+  }
+  mma_fence();
+
+  if (gridDim.y > 1) {
+    if (!splitk_combine<8, 8, kThreads>(acc, p.ws, p.cnt, blockIdx.x, gridDim.y, blockIdx.y, smem)) return;
+  }
+  if constexpr (EPI != EPI_OPT_SGD && EPI != EPI_OPT_ADAM) {
+    barrier();  // every wave is done with the operand stages: LDS belongs to the epilogue
+    epilogue_q<EPI, OUT_F32>(p, acc, smem, wid, m0 + wm * 128, n0 + wn * 128, lane);
+  } else {
+    epilogue<EPI, OUT_F32, 8, 8>(p, acc, m0 + wm * 128, n0 + wn * 128, lane);
+  }
+}
+
+template <bool A_KC, bool B_KC, bool OUT_F32>
+hipError_t dispatch_epi(const GemmParams& p, int epi, hipStream_t s) {
+  const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
+  const dim3 grid(tiles, max(1, p.splitk)), block(kThreads);
+  if (p.variant > 32) {  // experiment builds (fwd layout, bias+ReLU only)
+    if constexpr (A_KC && B_KC && !OUT_F32) {
+      if (epi != EPI_BIAS_RELU) return hipErrorInvalidValue;
+      switch (p.variant - 32) {
+        case 1: gemm_kernel<true, true, EPI_BIAS_RELU, false, 1><<<grid, block, 0, s>>>(p); break;
+        case 2: gemm_kernel<true, true, EPI_BIAS_RELU, false, 2><<<grid, block, 0, s>>>(p); break;
+        case 4: gemm_kernel<true, true, EPI_BIAS_RELU, false, 4><<<grid, block, 0, s>>>(p); break;
+        case 5: gemm_kernel<true, true, EPI_BIAS_RELU, false, 5><<<grid, block, 0, s>>>(p); break;
+        default: return hipErrorInvalidValue;
+      }
+      return hipGetLastError();
+    }
+    return hipErrorInvalidValue;
+  }
+  switch (epi) {
+#define LDNN_Q_CASE(E) \
+  case E: gemm_kernel<A_KC, B_KC, E, OUT_F32><<<grid, block, 0, s>>>(p); break;
+    LDNN_Q_CASE(EPI_NONE)
+    LDNN_Q_CASE(EPI_BIAS)
+    LDNN_Q_CASE(EPI_BIAS_RELU)
+    LDNN_Q_CASE(EPI_BIAS_SIGMOID)
+    LDNN_Q_CASE(EPI_DRELU)
+    LDNN_Q_CASE(EPI_DSIGMOID)
+#undef LDNN_Q_CASE
+    case EPI_OPT_SGD:
+      if constexpr (OUT_F32) {
+        gemm_kernel<A_KC, B_KC, EPI_OPT_SGD, true><<<grid, block, 0, s>>>(p);
+        break;
+      }
+      return hipErrorInvalidValue;
+    case EPI_OPT_ADAM:
+      if constexpr (OUT_F32) {
+        gemm_kernel<A_KC, B_KC, EPI_OPT_ADAM, true><<<grid, block, 0, s>>>(p);
+        break;
+      }
+      return hipErrorInvalidValue;
+    default:
+      return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace kq
+}  // namespace
+
+size_t gemm_q_ws_bytes(int M, int N, int splitk) {
+  const size_t tiles = (size_t)((M + kq::BM - 1) / kq::BM) * ((N + kq::BN - 1) / kq::BN);
+  return tiles * (size_t)splitk * (size_t)(64 * kq::kThreads * 16);
+}
+
+hipError_t gemm_q(const GemmParams& p, bool a_kc, bool b_kc, int epi, bool out_f32, hipStream_t s) {
+  if (p.M <= 0 || p.N <= 0) return hipSuccess;
+  const size_t abytes = (size_t)(a_kc ? p.M : p.K) * p.lda * 2;
+  const size_t bbytes = (size_t)(b_kc ? p.N : p.K) * p.ldb * 2;
+  if (abytes >= kOOBLimit || bbytes >= kOOBLimit) return hipErrorInvalidValue;
+  if (p.splitk > 1 && (p.ws == nullptr || p.cnt == nullptr)) return hipErrorInvalidValue;
+  if (a_kc) {
+    if (b_kc) return out_f32 ? kq::dispatch_epi<true, true, true>(p, epi, s) : kq::dispatch_epi<true, true, false>(p, epi, s);
+    return out_f32 ? kq::dispatch_epi<true, false, true>(p, epi, s) : kq::dispatch_epi<true, false, false>(p, epi, s);
+  }
+  if (b_kc) return out_f32 ? kq::dispatch_epi<false, true, true>(p, epi, s) : kq::dispatch_epi<false, true, false>(p, epi, s);
+  return out_f32 ? kq::dispatch_epi<false, false, true>(p, epi, s) : kq::dispatch_epi<false, false, false>(p, epi, s);
+}
+
+}  // namespace ldnn
