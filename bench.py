@@ -94,7 +94,7 @@ def run_ldnn(ctx, args):
     eng = StaticMLPEngine(model, args.batch, OptimConfig("sgd", lr=args.lr, momentum=0.9),
                           device=ctx.device, world_size=ctx.world_size, use_graphs=not args.no_graphs,
                           bucket_cap_elems=args.bucket_elems, shard_optimizer=False if args.no_shard else None,
-                          library_gemms=not args.no_library_gemms,
+                          library_gemms=args.gemms == "library",
                           early_optimizer={"on": True, "off": False, "auto": None}[args.early_opt],
                           fuse_head_dgrad=False if args.no_fuse_head_dgrad else None,
                           concurrent_wgrad=args.concurrent_wgrad, overlap_optimizer=args.overlap_opt,
@@ -111,7 +111,8 @@ def run_ldnn(ctx, args):
 
     el = timed(ctx, step, args.steps, args.warmup)
     loss, acc = eng.read_stats(args.batch * (args.steps + args.warmup))
-    return el, dict(train_loss=round(loss, 4), n_params=sum(p.numel() for p in model.parameters()))
+    return el, dict(train_loss=round(loss, 4), n_params=sum(p.numel() for p in model.parameters()),
+                    in_pad=eng.in_pad)
 
 
 def run_stock(ctx, args):
@@ -156,10 +157,11 @@ def main():
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--no-shard", action="store_true",
                     help="all-reduce + replicated optimizer instead of reduce-scatter / sharded optimizer / all-gather")
-    ap.add_argument("--no-library-gemms", action="store_true",
-                    help="run the plain GEMMs (fp32 wgrads, bias+ReLU forwards) on ldnn's MFMA kernels instead of hipBLASLt")
+    ap.add_argument("--gemms", choices=["ldnn", "library"], default="ldnn",
+                    help="ldnn: every GEMM on ldnn's own MFMA kernels (default); library: the plain GEMMs "
+                         "(fp32 wgrads, bias+ReLU forwards, hidden dgrad) on hipBLASLt, as an A/B baseline")
     ap.add_argument("--pad-input", action="store_true",
-                    help="pad the 784-wide first layer to K = 832 for hipBLASLt (measured slightly slower)")
+                    help="with --gemms library: pad the 784-wide first layer to K = 832 (measured slightly slower)")
     ap.add_argument("--overlap-opt", action="store_true",
                     help="1 GPU: optimizer update of all weights but W_0 on a side stream beside wgrad(0)")
     ap.add_argument("--concurrent-wgrad", action="store_true",
@@ -175,6 +177,7 @@ def main():
     ctx = D.setup(None if args.backend == "auto" else args.backend)
     n = ctx.world_size
     el, extra = run_ldnn(ctx, args)
+    comm = "RCCL" if ctx.backend == "nccl" else ctx.backend
     ms = el / args.steps * 1e3
     value = args.batch * n * args.steps / el
     rec = {
@@ -197,12 +200,14 @@ def main():
             "seq_len": None,
             "parallelism": f"dp{n}",
             "optimizer": "sgd momentum 0.9, fp32 master",
-            "gemms": ("ldnn MFMA kernels" if args.no_library_gemms else
+            "gemms": ("ldnn MFMA kernels only: bias+ReLU fwd, fused dReLU+dbias dgrad, fp32 wgrads (split-K "
+                      "in-launch combine for the 784-wide one), classifier head (Linear + softmax-xent + argmax + "
+                      "head dgrad), SGD" if args.gemms == "ldnn" else
                       "hipBLASLt: fp32 wgrads, bias/ReLU fwd, hidden dgrad; ldnn: fused dReLU+dbias pass, "
                       "classifier head (Linear + softmax-xent + argmax + head dgrad), SGD"),
             "grad_sync": ("none (1 GPU)" if n == 1 else
-                          "fp32 RCCL all-reduce, bucketed, overlapped" if args.no_shard else
-                          "fp32 RCCL reduce-scatter (bucketed, overlapped) + sharded SGD + bf16 weight all-gather"),
+                          f"fp32 {comm} all-reduce, bucketed, overlapped" if args.no_shard else
+                          f"fp32 {comm} reduce-scatter (bucketed, overlapped) + sharded SGD + bf16 weight all-gather"),
         },
     }
     rec.update(extra)

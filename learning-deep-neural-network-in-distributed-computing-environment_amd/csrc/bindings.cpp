@@ -109,8 +109,14 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, bool a_
     check(ldnn::gemm_skinny_n(p, (int)epi, cur_stream(a)), "gemm_skinny_n");
     return;
   }
-  if (tile == 256 && variant >= 4) {  // ping-pong kernel (gemm_pp.hip) / four-wave kernel (gemm_q.hip, variant 32)
-    const bool q = variant >= 32;
+  // variant (low byte): 0 = auto (the four-wave gemm_q kernel where it wins, else k256),
+  // 1 = gemm.hip k256, 2/3 = k256 ring experiments, 4.. = gemm_pp, 32.. = gemm_q
+  if (tile == 256 && (variant & 255) == 0 && ldnn::gemm_q_preferred(p.M, p.N, p.K)) {
+    variant |= 32;
+    p.variant = (int)variant;
+  }
+  if (tile == 256 && (variant & 255) >= 4) {  // ping-pong kernel (gemm_pp.hip) / four-wave kernel (gemm_q.hip, variant 32)
+    const bool q = (variant & 255) >= 32;
     if (splitk > 1) {
       TORCH_CHECK(ws.has_value() && cnt.has_value(), "gemm: the pp kernel's split-K needs ws and cnt");
       check_dev(*ws, at::kFloat, "ws");

@@ -70,6 +70,10 @@ int gemm_pp_tiles(int M, int N);
 // (tiles = gemm_pp_tiles, split-K workspace gemm_q_ws_bytes).
 hipError_t gemm_q(const GemmParams& p, bool a_kcontig, bool b_kcontig, int epi, bool out_f32, hipStream_t s);
 size_t gemm_q_ws_bytes(int M, int N, int splitk);
+// Whether gemm_q beats gemm.hip's k256 on a 256-tile shape (measured on MI355X,
+// profiles/gemm_q_r2.txt: it loses at short K, where its one-wave-per-SIMD
+// prologue/epilogue is not amortised).
+inline bool gemm_q_preferred(int M, int N, int K) { return K >= 1024; }
 // Split-K factor the 128-tile kernel uses for an fp32 EPI_NONE output (1 = none).
 int gemm_pick_splitk(int M, int N, int K);
 // Skinny-N forward GEMM (N <= 64, both operands k-contiguous, bf16 out): one

@@ -253,7 +253,9 @@ __device__ __forceinline__ void epilogue_q(const GemmParams& p, floatx4 (&acc)[8
           ob[q] = f2bf(o[q]);
           cs[q] += bf2f(ob[q]);
         }
-        *reinterpret_cast<u16x8*>(reinterpret_cast<bf16_t*>(p.C) + (size_t)m * p.ldc + n) = ob;
+        u16x8* dst = reinterpret_cast<u16x8*>(reinterpret_cast<bf16_t*>(p.C) + (size_t)m * p.ldc + n);
+        if (p.variant & 4096) __builtin_nontemporal_store(ob, dst);
+        else *dst = ob;
       }
     }
     __builtin_amdgcn_wave_barrier();
@@ -287,7 +289,19 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(GemmParams p) {
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid >> 1, wn = wid & 1;
   int m0, n0;
-  tile_coords(p.M, p.N, BM, BN, m0, n0);
+  {
+    // XCD remap, then groups of G tile-rows (G from variant bits 8..11 in experiments; default 4:
+    // measured on MI355X equal to 8 on the forward, +7 % on the dgrad, profiles/gemm_q_r2.txt)
+    const int tiles_m = (p.M + BM - 1) / BM, tiles_n = (p.N + BN - 1) / BN;
+    const int gsel = (p.variant >> 8) & 15;
+    const int G = gsel ? (1 << (gsel - 1)) : 4;
+    const int id = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+    const int per_group = G * tiles_n;
+    const int first_m = (id / per_group) * G;
+    const int gsize = min(tiles_m - first_m, G);
+    m0 = (first_m + (id % per_group) % gsize) * BM;
+    n0 = ((id % per_group) / gsize) * BN;
+  }
 
   const int nk_all = (p.K + BK - 1) / BK;
   const int per = (nk_all + gridDim.y - 1) / gridDim.y;
@@ -373,10 +387,10 @@ template <bool A_KC, bool B_KC, bool OUT_F32>
 hipError_t dispatch_epi(const GemmParams& p, int epi, hipStream_t s) {
   const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
   const dim3 grid(tiles, max(1, p.splitk)), block(kThreads);
-  if (p.variant > 32) {  // experiment builds (fwd layout, bias+ReLU only)
+  if ((p.variant & 255) > 32) {  // experiment builds (fwd layout, bias+ReLU only)
     if constexpr (A_KC && B_KC && !OUT_F32) {
       if (epi != EPI_BIAS_RELU) return hipErrorInvalidValue;
-      switch (p.variant - 32) {
+      switch ((p.variant & 255) - 32) {
         case 1: gemm_kernel<true, true, EPI_BIAS_RELU, false, 1><<<grid, block, 0, s>>>(p); break;
         case 2: gemm_kernel<true, true, EPI_BIAS_RELU, false, 2><<<grid, block, 0, s>>>(p); break;
         case 4: gemm_kernel<true, true, EPI_BIAS_RELU, false, 4><<<grid, block, 0, s>>>(p); break;

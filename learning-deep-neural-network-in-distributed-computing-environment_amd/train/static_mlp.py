@@ -187,12 +187,16 @@ class StaticMLPEngine:
         # Default (None): on with the library dgrad, where the alternative is a K = 16
         # hipBLASLt GEMM plus the separate dReLU/bias pass over h_{L-1}: measured on
         # MI355X at batch 16384, 1.848 vs 1.887 ms/step.
+        # library_gemms: route the plain GEMMs to hipBLASLt (kept as an A/B baseline).
+        # Default off: every GEMM of the step runs on ldnn's own MFMA kernels (the
+        # four-wave gemm_q.hip for the long-K shapes), with the activation
+        # derivative and bias-gradient sums fused into the dgrad epilogue.
         if library_gemms is None:
-            library_gemms = hasattr(torch, "_addmm_activation")
+            library_gemms = False
         if library_dgrad is None:
             library_dgrad = bool(library_gemms)
         if fuse_head_dgrad is None:
-            fuse_head_dgrad = bool(library_dgrad)
+            fuse_head_dgrad = True
         self.head_dgrad = (bool(fuse_head_dgrad) and self.use_head and L >= 2
                            and self.layers[-1].in_features <= self.C.head_dgrad_max_k())
         self._head_db_ws = (torch.empty(self.C.head_dgrad_ws_floats(B, self.layers[-1].in_features),
@@ -226,8 +230,6 @@ class StaticMLPEngine:
         # classifier head (fwd + softmax-xent + argmax, transposed-read wgrad).
         # Measured on MI355X (scripts/bench_blaslt.py, profiles/mlp_gemm_library_r1.jsonl):
         # hipBLASLt is 8-22 % faster on those plain shapes, ldnn wins the fused dgrad.
-        if library_gemms is None:
-            library_gemms = hasattr(torch, "_addmm_activation")
         hidden = [l for l in range(L) if not (self.use_head and l == L - 1)]
         self._lib_wgrad = [bool(library_gemms) and l in hidden for l in range(L)]
         self._lib_fwd = [bool(library_gemms) and l in hidden and self.layers[l].activation in ("relu", "none")
@@ -260,7 +262,10 @@ class StaticMLPEngine:
         # 128x128 hipBLASLt solution (194 us) and the two copies ate the forward's gain.
         K0 = self.layers[0].in_features
         self.in_pad = 0
-        if pad_input and K0 % 64 and self._lib_fwd[0] and self._lib_wgrad[0]:
+        if pad_input and not (K0 % 64 and self._lib_fwd[0] and self._lib_wgrad[0]):
+            raise ValueError("pad_input applies only when both first-layer GEMMs run on hipBLASLt "
+                             "(library_gemms=True) and the input width is not a multiple of 64")
+        if pad_input:
             Kp = (K0 + 63) // 64 * 64
             self.in_pad = Kp
             self.xp = torch.zeros(B, Kp, dtype=bf, device=dev)
@@ -279,13 +284,24 @@ class StaticMLPEngine:
             if self._lib_wgrad[l]:   # overwrites the gradient: no clearing, no split-K
                 self._wgrad_splitk.append(1)
                 continue
+            t256 = ((M + 255) // 256) * ((N + 255) // 256)
+            if B >= 4096 and t256 < 192:
+                # long-K wgrad whose 256-tile grid leaves CUs idle (the 4096 x 784 first
+                # layer: 64 tiles): the four-wave kernel splits the batch reduction over
+                # gridDim.y and combines the slices in the launch (deterministic, overwrites)
+                sk = max(2, min(8, round(256 / t256)))
+                ne, nc = self.C.gemm_pp_ws(M, N, sk)
+                self._wgrad_ws[l] = (torch.empty(ne, dtype=torch.float32, device=self.device),
+                                     torch.zeros(nc, dtype=torch.int32, device=self.device), 256)
+                self._wgrad_splitk.append(sk)
+                continue
             tile, sk = self.C.gemm_plan(M, N, B, True)
             tiles = ((M + 127) // 128) * ((N + 127) // 128)
             if tile == 128 and wgrad_combine and 64 <= tiles < 256 and B // 64 >= 32:
                 sk = max(2, min(4, (2 * 256) // tiles))   # <= 2 workgroups per CU
                 ne, nc = self.C.gemm_splitk_ws(M, N, sk)
                 self._wgrad_ws[l] = (torch.empty(ne, dtype=torch.float32, device=self.device),
-                                     torch.zeros(nc, dtype=torch.int32, device=self.device))
+                                     torch.zeros(nc, dtype=torch.int32, device=self.device), 128)
                 self._wgrad_splitk.append(sk)
                 continue
             self._wgrad_splitk.append(sk if tile == 128 else 1)
@@ -322,7 +338,8 @@ class StaticMLPEngine:
             fuse_optimizer = False  # the side-stream variant updates whole ranges itself
         self._fused = [bool(fuse_optimizer) and not self.distributed and not (self.use_head and l == L - 1)
                        and not self._lib_wgrad[l]
-                       and (self._wgrad_splitk[l] == 1 or self._wgrad_ws[l] is not None) for l in range(L)]
+                       and (self._wgrad_splitk[l] == 1 or (self._wgrad_ws[l] is not None
+                                                           and self._wgrad_ws[l][2] == 128)) for l in range(L)]
         self.rank = dist.get_rank(process_group) if self.distributed else 0
         self.overlap_optimizer = overlap_optimizer
         # early_optimizer (single process, L >= 2): the update of W_{L-1} .. W_1 runs on
@@ -398,8 +415,9 @@ class StaticMLPEngine:
             torch.mm(self.dz[l + 1].t(), self.h[l], out_dtype=torch.float32, out=self.dW[l])
             return
         if self._wgrad_ws[l] is not None:   # in-launch split-K combine, overwrites the gradient
-            ws, cnt = self._wgrad_ws[l]
-            self.C.gemm(self.dz[l + 1], self.h[l], self.dW[l], False, False, tile=128, splitk=sk, ws=ws, cnt=cnt)
+            ws, cnt, tile = self._wgrad_ws[l]
+            self.C.gemm(self.dz[l + 1], self.h[l], self.dW[l], False, False, tile=tile, splitk=sk, ws=ws, cnt=cnt,
+                        variant=32 if tile == 256 else 0)
         elif sk > 1:   # accumulates into the grad the previous optimizer launch cleared
             self.C.gemm(self.dz[l + 1], self.h[l], self.dW[l], False, False, beta=1.0, tile=128, splitk=sk)
         else:
@@ -417,7 +435,7 @@ class StaticMLPEngine:
         else:
             m, v = view(self.exp_avg), view(self.exp_avg_sq)
         sk = self._wgrad_splitk[l]
-        ws, cnt = self._wgrad_ws[l] if self._wgrad_ws[l] is not None else (None, None)
+        ws, cnt, _ = self._wgrad_ws[l] if self._wgrad_ws[l] is not None else (None, None, None)
         self.C.gemm_opt(self.dz[l + 1], self.h[l], view(f.master), False, False, o.name, m=m, v=v,
                         shadow=view(f.shadow), hp=self.hp, grad_scale=self._grad_scale, momentum=o.momentum,
                         dampening=o.dampening, weight_decay=o.weight_decay, nesterov=o.nesterov,
@@ -570,12 +588,8 @@ class StaticMLPEngine:
             self._build_sharded_segments(pieces, run)
         else:
             self.segments = [_Segment(run(p), self.use_graphs) for p in pieces]
-            if self.shard:
-                self.opt_segments = [_Segment(run([lambda i=i: self._opt(*self._shard_range(i), grad=self.gshard[i])]),
-                                              self.use_graphs) for i in range(len(self.buckets))]
-            else:
-                self.opt_segments = [_Segment(run([lambda b=b, e=e: self._opt(b, e)]), self.use_graphs)
-                                     for (b, e, _) in self.buckets]
+            self.opt_segments = [_Segment(run([lambda b=b, e=e: self._opt(b, e)]), self.use_graphs)
+                                 for (b, e, _) in self.buckets]
 
     def _bucket_of(self, t) -> int:
         off = self.flat.seg(t).offset

@@ -63,7 +63,8 @@ def cases(B):
     mk_n = lambda v: (lambda: C.gemm(dz2, W1, dz1, True, False, tile=256, variant=v))  # noqa: E731
     out.append(("dgrad1n", 2.0 * B * 4096 * 4096, dz1, ref_n, lib, mk_n))
     # wgrads (fp32 out): dW = dz^T h
-    for K0, name, sk in ((4096, "1", 1), (784, "0", 4)):
+    import os
+    for K0, name, sk in ((4096, "1", 1), (784, "0", int(os.environ.get("WG0_SPLITK", "4")))):
         dz = rnd(B, 4096) * 0.01
         dz = dz.bfloat16()
         h = rnd(B, K0)
