@@ -98,7 +98,7 @@ def run_ldnn(ctx, args):
                           early_optimizer={"on": True, "off": False, "auto": None}[args.early_opt],
                           fuse_head_dgrad=False if args.no_fuse_head_dgrad else None,
                           concurrent_wgrad=args.concurrent_wgrad, overlap_optimizer=args.overlap_opt,
-                          pad_input=args.pad_input)
+                          pad_input=args.pad_input, head_dgrad_mode=args.head_dgrad_mode)
     if ctx.distributed:
         dist.broadcast(eng.flat.master, src=0)
         eng.flat.refresh_shadow()
@@ -168,6 +168,8 @@ def main():
                     help="1 GPU: wgrad(1) on a side stream beside dgrad(1) + wgrad(0)")
     ap.add_argument("--no-fuse-head-dgrad", action="store_true",
                     help="separate head dgrad GEMM instead of the head kernel's fused dgrad (dReLU + dbias)")
+    ap.add_argument("--head-dgrad-mode", type=int, default=-1,
+                    help="-1 auto (streaming dh kernel for <= 16 classes), 1 fused (h re-read), 2 fused (h in LDS)")
     ap.add_argument("--early-opt", choices=["auto", "on", "off"], default="auto",
                     help="1 GPU: update W_{L-1}..W_1 on a side stream beside the last dgrad GEMM")
     ap.add_argument("--compare-stock", action="store_true")

@@ -416,7 +416,7 @@ void head_fwd_xent(const at::Tensor& h, const at::Tensor& W, const at::Tensor& b
                    const c10::optional<at::Tensor>& logits, const at::Tensor& dlogits, const at::Tensor& stats,
                    int64_t num_classes, double grad_scale, const c10::optional<at::Tensor>& dh,
                    const c10::optional<at::Tensor>& dbias, int64_t dgrad_epi,
-                   const c10::optional<at::Tensor>& dbias_ws) {
+                   const c10::optional<at::Tensor>& dbias_ws, int64_t dgrad_mode) {
   check_dev(h, at::kBFloat16, "h");
   check_dev(W, at::kBFloat16, "W");
   check_dev(bias, at::kFloat, "bias");
@@ -460,7 +460,12 @@ void head_fwd_xent(const at::Tensor& h, const at::Tensor& W, const at::Tensor& b
     TORCH_CHECK(dh->dim() == 2 && dh->size(0) == B && dh->size(1) == K && dh->stride(1) == 1 &&
                     dh->stride(0) % 8 == 0 && aligned16(dh->data_ptr()),
                 "head: dh must be [B][K] with 16-B aligned rows");
-    TORCH_CHECK(K <= ldnn::head_dgrad_max_k(), "head: fused dgrad needs K <= ", ldnn::head_dgrad_max_k());
+    if (dgrad_mode < 0) dgrad_mode = ld == 16 ? 0 : 1;  // auto: the streaming dgrad where it applies
+    TORCH_CHECK(dgrad_mode >= 0 && dgrad_mode <= 2, "head: dgrad_mode must be -1 (auto), 0, 1 or 2");
+    TORCH_CHECK(dgrad_mode != 0 || ld == 16, "head: the streaming dgrad (mode 0) needs ld == 16");
+    TORCH_CHECK(dgrad_mode == 0 || K <= ldnn::head_dgrad_max_k(), "head: fused dgrad needs K <= ",
+                ldnn::head_dgrad_max_k());
+    p.dgrad_mode = (int)dgrad_mode;
     TORCH_CHECK(dgrad_epi == ldnn::EPI_NONE || dgrad_epi == ldnn::EPI_DRELU || dgrad_epi == ldnn::EPI_DSIGMOID,
                 "head: dgrad_epi must be EPI_NONE / EPI_DRELU / EPI_DSIGMOID");
     p.dh = bf16_mut(*dh);
@@ -470,13 +475,16 @@ void head_fwd_xent(const at::Tensor& h, const at::Tensor& W, const at::Tensor& b
       check_dev(*dbias, at::kFloat, "dbias");
       TORCH_CHECK(dbias->is_contiguous() && dbias->numel() >= K && aligned16(dbias->data_ptr()),
                   "head: dbias must hold K floats, 16-B aligned");
-      TORCH_CHECK(dbias_ws.has_value(), "head: dbias needs dbias_ws (head_dgrad_ws_floats(B, K) fp32)");
-      check_dev(*dbias_ws, at::kFloat, "dbias_ws");
-      TORCH_CHECK(dbias_ws->is_contiguous() && dbias_ws->numel() >= (int64_t)ldnn::head_dgrad_ws_floats((int)B, (int)K) &&
-                      aligned16(dbias_ws->data_ptr()),
-                  "head: dbias_ws too small");
       p.dbias = dbias->data_ptr<float>();
-      p.dbias_ws = dbias_ws->data_ptr<float>();
+      if (dgrad_mode != 0) {  // the fused modes reduce per-workgroup slabs
+        TORCH_CHECK(dbias_ws.has_value(), "head: dbias needs dbias_ws (head_dgrad_ws_floats(B, K) fp32)");
+        check_dev(*dbias_ws, at::kFloat, "dbias_ws");
+        TORCH_CHECK(dbias_ws->is_contiguous() &&
+                        dbias_ws->numel() >= (int64_t)ldnn::head_dgrad_ws_floats((int)B, (int)K) &&
+                        aligned16(dbias_ws->data_ptr()),
+                    "head: dbias_ws too small");
+        p.dbias_ws = dbias_ws->data_ptr<float>();
+      }
     }
   }
   c10::hip::HIPGuardMasqueradingAsCUDA g(h.device());
@@ -883,7 +891,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("head_fwd_xent", &head_fwd_xent, "fused narrow Linear + softmax-xent + argmax (per-16-row stats slots)",
         py::arg("h"), py::arg("W"), py::arg("bias"), py::arg("labels"), py::arg("logits"), py::arg("dlogits"),
         py::arg("stats"), py::arg("num_classes"), py::arg("grad_scale"), py::arg("dh") = py::none(), py::arg("dbias") = py::none(),
-        py::arg("dgrad_epi") = (int64_t)ldnn::EPI_DRELU, py::arg("dbias_ws") = py::none());
+        py::arg("dgrad_epi") = (int64_t)ldnn::EPI_DRELU, py::arg("dbias_ws") = py::none(),
+        py::arg("dgrad_mode") = (int64_t)-1);
   m.def("head_dgrad_ws_floats", &ldnn::head_dgrad_ws_floats, py::arg("B"), py::arg("K"));
   m.def("head_wgrad", &head_wgrad, "dW = dz^T h (+ db = colsum dz); splits > 1 accumulate atomically",
         py::arg("dz"), py::arg("h"), py::arg("dW"), py::arg("db") = py::none(), py::arg("splits") = 0);

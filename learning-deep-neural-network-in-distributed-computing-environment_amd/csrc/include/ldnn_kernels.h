@@ -243,6 +243,11 @@ struct HeadParams {
   float* dbias;         // += column sums of dh (via dbias_ws: head_dgrad_ws_floats(B, K) floats)
   float* dbias_ws;
   int lddh, dgrad_epi;  // EPI_NONE / EPI_DRELU / EPI_DSIGMOID
+  // 0: forward-only head kernel + the streaming dgrad kernel (needs ld == 16; dbias by
+  //    atomics, no dbias_ws); 1: dgrad fused into the head kernel, h re-read from
+  //    global memory; 2: fused, h staged in LDS (1 / 2 need K <= head_dgrad_max_k()
+  //    and dbias_ws for dbias)
+  int dgrad_mode;
 };
 hipError_t head_fwd_xent(const HeadParams& p, hipStream_t s);
 int head_dgrad_max_k();

@@ -24,9 +24,14 @@
 //                  overlapping it.  At batch 16384 with the hipBLASLt dgrad it wins
 //                  (129 us fused incl. the slab sum vs 51 + 68 us + the head fwd; step
 //                  1.848 vs 1.887 ms), so the engine turns it on with library_dgrad.
-//                  The dgrad re-reads h from global memory (L2 / Infinity Cache) by
-//                  default; LDNN_HEAD_DG_LDS=1 stages it in LDS -- measured equal
-//                  (1.870 vs 1.868 ms/step), the global variant needs 7 KiB of LDS.
+//                  The dgrad re-reads h from global memory (L2 / Infinity Cache)
+//                  (HeadParams::dgrad_mode 1) or stages it in LDS (mode 2) --
+//                  measured equal (1.870 vs 1.868 ms/step).
+//                  Mode 0 (default for <= 16 classes) instead runs the forward-only
+//                  head kernel and then head_dgrad_stream_kernel: the dgrad as a
+//                  pure h -> dh stream with the bias-gradient sums in the same pass
+//                  (round 2: the fused kernel's per-16-row phases serialise on a CU
+//                  and its 1024 per-workgroup slabs cost a 15 us reduction).
 //  head_wgrad:     dW = dlogits^T h (+ db = column sums of dlogits).  The
 //                  reduction runs over the batch, the strided dimension of both
 //                  operands, so each wave stages its 32-row chunks through a
@@ -34,8 +39,6 @@
 //                  (hardware transpose) into MFMA fragments.  64 output
 //                  columns x a batch slice per workgroup; slices combine with
 //                  fp32 atomics into the (pre-cleared) gradient.
-#include <cstdlib>
-
 #include "ldnn_common.h"
 #include "ldnn_gemm_tile.h"
 #include "ldnn_kernels.h"
@@ -395,6 +398,95 @@ __global__ __launch_bounds__(kWgWaves * 64) void head_wgrad_kernel(HeadWgradPara
   }
 }
 
+// ---------------------------------------------------------------------------
+// streaming head dgrad (<= 16 classes): dh = (dlogits W) * act'(h), dbias += colsums
+// ---------------------------------------------------------------------------
+// A pure stream over h (read) and dh (write) -- the two tensors that cost bytes --
+// laid out like act_bwd_colsum (elementwise.hip): a thread owns 8 columns and walks
+// rows 8 apart, so every h load / dh store is a 16-B piece of a 512-B row run.  The
+// thread keeps W[c][its 8 columns] for all 16 (padded) classes in registers; each
+// row's 16 bf16 dlogits (32 B, the same for the 32 lanes of a row) come from L1.
+// The column sums are reduced over the workgroup's 8 row lanes in LDS and added
+// with one atomic per column per workgroup.  Two rows per iteration keep 4 loads in
+// flight per lane.
+template <int DEPI>
+__global__ __launch_bounds__(256) void head_dgrad_stream_kernel(HeadParams p, int rows_per_block) {
+  __shared__ float part[8][256];
+  const int cg = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const int c0 = (blockIdx.x * 32 + cg) * 8;
+  const int r_begin = blockIdx.y * rows_per_block;
+  const int r_end = min(p.B, r_begin + rows_per_block);
+  const bool cok = c0 < p.K;
+  float wf[16][8];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+    u16x8 w = {};
+    if (cok && c < p.ldw_rows) w = *reinterpret_cast<const u16x8*>(p.W + (size_t)c * p.ldw + c0);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) wf[c][i] = bf2f(w[i]);
+  }
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  auto row_out = [&](const u16x8& g0, const u16x8& g1, const u16x8& hv, int r) {
+    float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      const float gc = bf2f(c < 8 ? g0[c] : g1[c - 8]);  // padded classes hold 0
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = fmaf(gc, wf[c][i], v[i]);
+    }
+    u16x8 o;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float hf = bf2f(hv[i]);
+      float x = v[i];
+      if constexpr (DEPI == EPI_DRELU) x = hf > 0.f ? x : 0.f;
+      else if constexpr (DEPI == EPI_DSIGMOID) x *= hf * (1.f - hf);
+      o[i] = f2bf(x);
+      s[i] += bf2f(o[i]);
+    }
+    *reinterpret_cast<u16x8*>(p.dh + (size_t)r * p.lddh + c0) = o;
+  };
+  if (cok) {
+    int r = r_begin + ty;
+    for (; r + 8 < r_end; r += 16) {
+      const u16x8* gp0 = reinterpret_cast<const u16x8*>(p.dlogits + (size_t)r * p.ld);
+      const u16x8* gp1 = reinterpret_cast<const u16x8*>(p.dlogits + (size_t)(r + 8) * p.ld);
+      const u16x8 a0 = gp0[0], a1 = gp0[1], b0 = gp1[0], b1 = gp1[1];
+      const u16x8 h0 = *reinterpret_cast<const u16x8*>(p.h + (size_t)r * p.ldh + c0);
+      const u16x8 h1 = *reinterpret_cast<const u16x8*>(p.h + (size_t)(r + 8) * p.ldh + c0);
+      row_out(a0, a1, h0, r);
+      row_out(b0, b1, h1, r + 8);
+    }
+    for (; r < r_end; r += 8) {
+      const u16x8* gp0 = reinterpret_cast<const u16x8*>(p.dlogits + (size_t)r * p.ld);
+      row_out(gp0[0], gp0[1], *reinterpret_cast<const u16x8*>(p.h + (size_t)r * p.ldh + c0), r);
+    }
+  }
+  if (p.dbias == nullptr) return;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) part[ty][cg * 8 + j] = s[j];
+  __syncthreads();
+  if (ty == 0 && cok) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float t = 0.f;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) t += part[q][cg * 8 + j];
+      atomicAdd(p.dbias + c0 + j, t);
+    }
+  }
+}
+
+template <int DEPI>
+hipError_t launch_head_dgrad_stream(const HeadParams& p, hipStream_t s) {
+  const int gx = (p.K + 255) / 256;
+  int gy = (p.B + 255) / 256;
+  if (gy > 256) gy = 256;
+  const int rpb = (p.B + gy - 1) / gy;
+  head_dgrad_stream_kernel<DEPI><<<dim3(gx, gy), 256, 0, s>>>(p, rpb);
+  return hipGetLastError();
+}
+
 template <int DEPI, bool HS>
 hipError_t launch_head_fwd(const HeadParams& p, hipStream_t s) {
   const dim3 grid((p.B + 15) / 16), block(kFwdWaves * 64);
@@ -407,18 +499,23 @@ hipError_t launch_head_fwd(const HeadParams& p, hipStream_t s) {
   return hipGetLastError();
 }
 
-// LDNN_HEAD_DG_LDS=1 selects the LDS-staged h for the fused head dgrad
-bool head_dg_lds() {
-  static const bool v = [] {
-    const char* e = std::getenv("LDNN_HEAD_DG_LDS");
-    return e != nullptr && e[0] == '1';
-  }();
-  return v;
+template <int DEPI>
+hipError_t launch_head_fwd_dg(const HeadParams& p, hipStream_t s) {
+  return p.dgrad_mode == 2 ? launch_head_fwd<DEPI, true>(p, s) : launch_head_fwd<DEPI, false>(p, s);
 }
 
 template <int DEPI>
-hipError_t launch_head_fwd_dg(const HeadParams& p, hipStream_t s) {
-  return head_dg_lds() ? launch_head_fwd<DEPI, true>(p, s) : launch_head_fwd<DEPI, false>(p, s);
+hipError_t head_dgrad_dispatch(const HeadParams& p, hipStream_t s) {
+  if (p.dgrad_mode == 0) {  // streaming: forward-only head kernel, then the dgrad stream
+    hipError_t e = launch_head_fwd<-1, false>(p, s);
+    if (e != hipSuccess) return e;
+    return launch_head_dgrad_stream<DEPI>(p, s);
+  }
+  hipError_t e = launch_head_fwd_dg<DEPI>(p, s);
+  // per-workgroup column sums -> bias gradient: 256 same-address fp32 atomics per
+  // column measured 100+ us; a slab reduction over the chip costs a few
+  if (e != hipSuccess || p.dbias == nullptr) return e;
+  return slab_sum(p.dbias_ws, p.dbias, p.K / 4, (p.B + 15) / 16, 1.f, s);
 }
 
 }  // namespace
@@ -427,19 +524,16 @@ hipError_t head_fwd_xent(const HeadParams& p, hipStream_t s) {
   if (p.B <= 0) return hipSuccess;
   if (p.ld > 64 || p.ld % 16 != 0 || p.C > p.ld || p.ldw_rows > p.ld || p.K % 8 != 0) return hipErrorInvalidValue;
   if (p.dh == nullptr) return launch_head_fwd<-1, false>(p, s);
-  if (p.K > kHeadDgradMaxK || p.lddh % 8 != 0 || (p.dbias != nullptr && p.dbias_ws == nullptr))
+  if (p.lddh % 8 != 0) return hipErrorInvalidValue;
+  if (p.dgrad_mode < 0 || p.dgrad_mode > 2 || (p.dgrad_mode == 0 && p.ld != 16)) return hipErrorInvalidValue;
+  if (p.dgrad_mode != 0 && (p.K > kHeadDgradMaxK || (p.dbias != nullptr && p.dbias_ws == nullptr)))
     return hipErrorInvalidValue;
-  hipError_t e;
   switch (p.dgrad_epi) {
-    case EPI_NONE: e = launch_head_fwd_dg<EPI_NONE>(p, s); break;
-    case EPI_DRELU: e = launch_head_fwd_dg<EPI_DRELU>(p, s); break;
-    case EPI_DSIGMOID: e = launch_head_fwd_dg<EPI_DSIGMOID>(p, s); break;
+    case EPI_NONE: return head_dgrad_dispatch<EPI_NONE>(p, s);
+    case EPI_DRELU: return head_dgrad_dispatch<EPI_DRELU>(p, s);
+    case EPI_DSIGMOID: return head_dgrad_dispatch<EPI_DSIGMOID>(p, s);
     default: return hipErrorInvalidValue;
   }
-  // per-workgroup column sums -> bias gradient: 256 same-address fp32 atomics per
-  // column measured 100+ us; a slab reduction over the chip costs a few
-  if (e != hipSuccess || p.dbias == nullptr) return e;
-  return slab_sum(p.dbias_ws, p.dbias, p.K / 4, (p.B + 15) / 16, 1.f, s);
 }
 
 size_t head_dgrad_ws_floats(int B, int K) { return (size_t)((B + 15) / 16) * K; }

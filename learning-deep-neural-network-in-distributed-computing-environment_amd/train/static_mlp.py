@@ -99,7 +99,8 @@ class StaticMLPEngine:
                  shard_optimizer: bool | None = None, overlap_optimizer: bool = False, wgrad_combine: bool = True,
                  fuse_optimizer: bool | None = None, library_gemms: bool | None = None,
                  fuse_head_dgrad: bool | None = None, early_optimizer: bool | None = None,
-                 library_dgrad: bool | None = None, concurrent_wgrad: bool = False, pad_input: bool = False):
+                 library_dgrad: bool | None = None, concurrent_wgrad: bool = False, pad_input: bool = False,
+                 head_dgrad_mode: int = -1):
         from ..models.mlp import MLP
 
         if not isinstance(model, MLP):
@@ -197,8 +198,13 @@ class StaticMLPEngine:
             library_dgrad = bool(library_gemms)
         if fuse_head_dgrad is None:
             fuse_head_dgrad = True
+        # head_dgrad_mode (head.hip): -1 auto = 0 for <= 16 classes (forward-only head
+        # kernel + a streaming dh pass with the bias-gradient sums), 1 / 2 = dgrad fused
+        # into the head kernel (h re-read from global / staged in LDS)
+        self.head_dgrad_mode = int(head_dgrad_mode)
         self.head_dgrad = (bool(fuse_head_dgrad) and self.use_head and L >= 2
-                           and self.layers[-1].in_features <= self.C.head_dgrad_max_k())
+                           and (npad[-1] == 16 and self.head_dgrad_mode in (-1, 0)
+                                or self.layers[-1].in_features <= self.C.head_dgrad_max_k()))
         self._head_db_ws = (torch.empty(self.C.head_dgrad_ws_floats(B, self.layers[-1].in_features),
                                         dtype=torch.float32, device=self.device) if self.head_dgrad else None)
         # [loss_sum, correct] -- one pair per 16-row workgroup of the head kernel
@@ -393,7 +399,7 @@ class StaticMLPEngine:
                 self.C.head_fwd_xent(self.h[L - 1], self.W[L - 1], self.bias[L - 1], self.labels, self.h[L],
                                      self.dz[L], self.stats, self.num_classes, 1.0 / self.B, dh=self.dz[L - 1],
                                      dbias=self.db[L - 2], dgrad_epi=self._dgrad_epi[L - 1],
-                                     dbias_ws=self._head_db_ws)
+                                     dbias_ws=self._head_db_ws, dgrad_mode=self.head_dgrad_mode)
                 return
             self.C.head_fwd_xent(self.h[L - 1], self.W[L - 1], self.bias[L - 1], self.labels, self.h[L], self.dz[L],
                                  self.stats, self.num_classes, 1.0 / self.B)

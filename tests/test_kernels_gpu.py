@@ -265,12 +265,18 @@ def test_head_fwd_xent(B, K, ncls, ld):
     assert dl[:, ncls:].float().abs().max().item() == 0.0
 
 
+@pytest.mark.parametrize("mode", [0, 1, 2])
 @pytest.mark.parametrize("epi", ["drelu", "dsigmoid", "none"])
-@pytest.mark.parametrize("B,K,ncls,ld", [(4096, 4096, 10, 16), (1000, 784, 10, 16), (70, 520, 40, 48)])
-def test_head_fwd_xent_fused_dgrad(B, K, ncls, ld, epi):
-    """The head kernel's fused dgrad: dh = (dlogits W) * act'(h) from its LDS copy of h,
-    plus the previous layer's bias gradient (column sums of dh), vs fp32 PyTorch on the
-    kernel's own bf16 dlogits; the loss path is unchanged by the fusion."""
+@pytest.mark.parametrize("B,K,ncls,ld", [(4096, 4096, 10, 16), (1000, 784, 10, 16), (70, 520, 10, 16),
+                                         (70, 520, 40, 48)])
+def test_head_fwd_xent_fused_dgrad(B, K, ncls, ld, epi, mode):
+    """The head's dgrad: dh = (dlogits W) * act'(h) plus the previous layer's bias
+    gradient (column sums of dh), vs fp32 PyTorch on the kernel's own bf16 dlogits, in
+    every dgrad_mode (0 = streaming kernel, 1 = fused re-reading h, 2 = fused from an
+    LDS copy of h), incl. a partial last 16-row workgroup (B = 70); the loss path is
+    unchanged by the dgrad."""
+    if mode == 0 and ld != 16:
+        pytest.skip("the streaming dgrad needs ld == 16")
     torch.manual_seed(4)
     h = torch.randn(B, K, device="cuda")
     if epi == "drelu":
@@ -290,7 +296,8 @@ def test_head_fwd_xent_fused_dgrad(B, K, ncls, ld, epi):
     cc = C()
     code = {"drelu": cc.EPI_DRELU, "dsigmoid": cc.EPI_DSIGMOID, "none": cc.EPI_NONE}[epi]
     ws = torch.empty(cc.head_dgrad_ws_floats(B, K), device="cuda")
-    cc.head_fwd_xent(h, W, bias, y, None, dl, st, ncls, 1.0 / B, dh=dh, dbias=db, dgrad_epi=code, dbias_ws=ws)
+    cc.head_fwd_xent(h, W, bias, y, None, dl, st, ncls, 1.0 / B, dh=dh, dbias=db, dgrad_epi=code, dbias_ws=ws,
+                     dgrad_mode=mode)
     cc.head_fwd_xent(h, W, bias, y, None, dl2, st2, ncls, 1.0 / B)
     assert torch.equal(dl, dl2) and torch.equal(st, st2)
     ref = dl.float()[:, :ncls] @ W.float()[:ncls]
