@@ -81,7 +81,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--no_eval", action="store_true")
     p.add_argument("--quiet", action="store_true")
     p.add_argument("--graphs", action="store_true",
-                   help="replay each training step from one hipGraph (single-process / per-epoch aggregation)")
+                   help="replay each training step from hipGraphs; with --sync_every step the bucket "
+                        "all-reduces are captured into the step graph beside the backward (RCCL)")
     p.add_argument("--trace", action="store_true",
                    help="roctx ranges per phase + HIP-event phase timers (summary in metrics.jsonl)")
     return p

@@ -821,7 +821,43 @@ void gap_bwd(const at::Tensor& dy, const at::Tensor& dx) {
 
 }  // namespace
 
+// A HIP event whose record inside a stream capture becomes an EXTERNAL event-record
+// node of the graph (hipEventRecordExternal): a stream outside the graph can then
+// wait on a point in the middle of a graph replay -- how GraphedDPStep starts a
+// bucket's RCCL all-reduce while the rest of the backward graph still runs.
+// (torch.cuda.Event(external=True) refuses ROCm; HIP itself supports the node.)
+struct GraphEvent {
+  hipEvent_t ev = nullptr;
+  GraphEvent() { check(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreateWithFlags"); }
+  ~GraphEvent() {
+    if (ev != nullptr) (void)hipEventDestroy(ev);
+  }
+  GraphEvent(const GraphEvent&) = delete;
+  GraphEvent& operator=(const GraphEvent&) = delete;
+  void record_external(uint64_t stream) {
+    check(hipEventRecordWithFlags(ev, reinterpret_cast<hipStream_t>(stream), hipEventRecordExternal),
+          "hipEventRecordWithFlags(external)");
+  }
+  void record(uint64_t stream) { check(hipEventRecord(ev, reinterpret_cast<hipStream_t>(stream)), "hipEventRecord"); }
+  void wait(uint64_t stream) {
+    check(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream), ev, 0), "hipStreamWaitEvent");
+  }
+  bool query() {
+    const hipError_t e = hipEventQuery(ev);
+    if (e == hipErrorNotReady) return false;
+    check(e, "hipEventQuery");
+    return true;
+  }
+};
+
 PYBIND11_MODULE(_C, m) {
+  py::class_<GraphEvent>(m, "GraphEvent")
+      .def(py::init<>())
+      .def("record_external", &GraphEvent::record_external, py::arg("stream"),
+           "record on a raw hipStream_t; inside a capture this is an external event-record node")
+      .def("record", &GraphEvent::record, py::arg("stream"))
+      .def("wait", &GraphEvent::wait, py::arg("stream"), "make the raw hipStream_t wait for the last record")
+      .def("query", &GraphEvent::query);
   m.doc() = "ldnn: hand-written gfx950 (MI355X / CDNA4) HIP kernels";
   m.attr("EPI_NONE") = (int)ldnn::EPI_NONE;
   m.attr("EPI_BIAS") = (int)ldnn::EPI_BIAS;

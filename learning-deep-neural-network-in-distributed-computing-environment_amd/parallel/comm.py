@@ -31,6 +31,9 @@ _TORCH_OPS = {SUM: dist.ReduceOp.SUM, MAX: dist.ReduceOp.MAX, MIN: dist.ReduceOp
 class Comm:
     rank: int = 0
     world_size: int = 1
+    # True when collectives run on device buffers ordered by HIP streams (RCCL):
+    # they may then be issued from a side stream behind in-graph events
+    device_collectives: bool = False
 
     def __init__(self):
         self._sched = hashlib.sha1()
@@ -97,6 +100,8 @@ class TorchComm(Comm):
         self.group = group
         self.rank = dist.get_rank(group)
         self.world_size = dist.get_world_size(group)
+        self.backend = dist.get_backend(group)
+        self.device_collectives = self.backend == "nccl"
 
     def _global(self, r: int) -> int:
         return r if self.group is None else dist.get_global_rank(self.group, r)

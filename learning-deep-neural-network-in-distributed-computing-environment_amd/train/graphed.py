@@ -116,3 +116,175 @@ class GraphedStep:
         loss.backward()
         self.optimizer.step()
         return loss.detach()
+
+
+class GraphedDPStep:
+    """A data-parallel training step (per-step gradient all-reduce) replayed from
+    hipGraphs, with the bucket all-reduces overlapping the backward pass.
+
+    The reference's DP hot loop (BAR/trainer.py:194-223 + communication.py:21-25)
+    is the eager step plus 65 blocking per-tensor all-reduces.  ``DataParallel``
+    (parallel/ddp.py) already buckets the flat gradient and launches each bucket's
+    all-reduce from backward hooks -- but eagerly, one Python launch per kernel.
+
+    mode "in_graph" (default with RCCL): ONE graph per step.  The bucket-readiness
+    hooks fire once during capture; at each the capture forks onto a side stream
+    and captures that bucket's RCCL all-reduce there (after the bucket's bf16
+    staging copy when comm_dtype is bf16), so in every replay bucket i travels over
+    xGMI while the backward nodes of buckets i+1.. still run; the capture joins the
+    side stream before the (widen +) fused optimizer nodes.  1/N averaging is
+    folded into the optimizer (flat.grad_scale).
+    mode "after" (host-staged backends such as gloo, or on request): graph G1 =
+    zero_grad + forward + backward, then the bucket collectives from Python, then
+    graph G2 = (widen +) optimizer.
+
+    ``comm_fn(i, buf)`` (tests) replaces the collective of bucket i and is issued
+    exactly where the collective would be.
+    """
+
+    def __init__(self, dp, criterion, optimizer, x_example: torch.Tensor, y_example: torch.Tensor,
+                 stats: torch.Tensor | None = None, mode: str | None = None, comm_fn=None):
+        from ..parallel.comm import SUM
+
+        if not x_example.is_cuda:
+            raise ValueError("GraphedDPStep needs GPU tensors")
+        self.dp, self.model, self.criterion, self.optimizer = dp, dp.module, criterion, optimizer
+        self.bk, self.flat, self.comm = dp.bucketer, dp.flat, dp.comm
+        self._SUM = SUM
+        self.comm_fn = comm_fn
+        self.x = x_example.detach().clone()
+        self.y = y_example.detach().clone()
+        self.stats = stats if stats is not None else torch.zeros(2, dtype=torch.float32, device=self.x.device)
+        self._lrs = None
+        if mode is None:
+            mode = "in_graph" if (getattr(self.comm, "device_collectives", False) or comm_fn is not None) else "after"
+        if mode not in ("in_graph", "after"):
+            raise ValueError(f"unknown GraphedDPStep mode {mode!r}")
+        self.mode = mode
+        nb = len(self.bk.buckets)
+        self.side = torch.cuda.Stream(device=self.x.device) if mode == "in_graph" else None
+        self._cap = None
+        self.flat.add_ready_hook(self._on_ready)
+        torch.cuda.synchronize(self.x.device)
+        self.stats.zero_()
+        self.g1 = torch.cuda.CUDAGraph()
+        self.g2 = torch.cuda.CUDAGraph() if mode == "after" else None
+        self._set_capture(True)
+        try:
+            self._cap = {"pending": [len(b["params"]) for b in self.bk.buckets], "fired": [False] * nb,
+                         "seen": set(), "works": []}
+            with no_gc(), torch.cuda.graph(self.g1):
+                self.optimizer.zero_grad()
+                out = self.model(self.x)
+                try:
+                    loss = self.criterion(out, self.y, self.stats)
+                except TypeError:
+                    loss = self.criterion(out.float(), self.y)
+                loss.backward()
+                for i in range(nb):  # buckets whose parameters got no gradient
+                    if not self._cap["fired"][i]:
+                        self._fire(i)
+                if mode == "in_graph":
+                    for w in self._cap["works"]:
+                        if w is not None:
+                            w.wait()
+                    torch.cuda.current_stream().wait_stream(self.side)
+                    self._widen_and_step()
+            self._cap = None
+            self.loss = loss
+            if mode == "after":
+                with no_gc(), torch.cuda.graph(self.g2, pool=self.g1.pool()):
+                    self._widen_and_step()
+        finally:
+            self._cap = None
+            self._set_capture(False)
+        self._sync_lr(force=True)
+
+    # ---------------------------------------------------------------- capture
+    def _set_capture(self, on: bool):
+        if isinstance(self.optimizer, _FlatOptimizer):
+            self.optimizer._ldnn_capturing = on
+
+    def _widen_and_step(self):
+        if self.bk._stage is not None:
+            for i, b in enumerate(self.bk.buckets):
+                self.flat.grad[b["begin"]: b["end"]].copy_(self.bk._stage[i])
+        self.optimizer.step()
+
+    def _fire(self, i):
+        """(capture) bucket i's gradients are complete at this point of the graph."""
+        self._cap["fired"][i] = True
+        if self.bk._stage is not None:
+            b = self.bk.buckets[i]
+            self.bk._stage[i].copy_(self.flat.grad[b["begin"]: b["end"]])
+        if self.mode == "in_graph":
+            self.side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(self.side):
+                self._cap["works"].append(self._collective(i, async_op=True))
+
+    def _on_ready(self, p):
+        c = self._cap
+        if c is None or id(p) in c["seen"]:
+            return
+        c["seen"].add(id(p))
+        i = self.bk.of_param.get(id(p))
+        if i is None:
+            return
+        c["pending"][i] -= 1
+        if c["pending"][i] == 0 and not c["fired"][i]:
+            self._fire(i)
+
+    def _sync_lr(self, force: bool = False):
+        lrs = [g["lr"] for g in self.optimizer.param_groups]
+        if force or lrs != self._lrs:
+            if isinstance(self.optimizer, _FlatOptimizer):
+                self.optimizer.sync_hyperparams()
+            self._lrs = lrs
+
+    def _buf(self, i):
+        if self.bk._stage is not None:
+            return self.bk._stage[i]
+        b = self.bk.buckets[i]
+        return self.flat.grad[b["begin"]: b["end"]]
+
+    def _collective(self, i, async_op=False):
+        buf = self._buf(i)
+        if self.comm_fn is not None:
+            self.comm_fn(i, buf)
+            return None
+        return self.comm.all_reduce(buf, self._SUM, async_op=async_op)
+
+    # -------------------------------------------------------------------- API
+    def flush_stats(self, into: torch.Tensor):
+        into.add_(self.stats)
+        self.stats.zero_()
+
+    def __call__(self, x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+        if x.shape != self.x.shape or y.shape != self.y.shape:
+            return self._eager_step(x, y)
+        self.x.copy_(x, non_blocking=True)
+        self.y.copy_(y, non_blocking=True)
+        self._sync_lr()
+        self.g1.replay()
+        if self.mode == "after":
+            if not getattr(self.comm, "device_collectives", False):
+                torch.cuda.current_stream().synchronize()  # a host-staged backend reads the buffers
+            works = [self._collective(i, async_op=True) for i in range(len(self.bk.buckets))]
+            for w in works:
+                if w is not None:
+                    w.wait()
+            self.g2.replay()
+        return self.loss
+
+    def _eager_step(self, x, y):
+        """Odd-shaped batch (the last one of an epoch): the eager bucketed DP step."""
+        self.optimizer.zero_grad()
+        out = self.dp(x)
+        try:
+            loss = self.criterion(out, y, self.stats)
+        except TypeError:
+            loss = self.criterion(out.float(), y)
+        loss.backward()
+        self.dp.finish_gradient_sync()
+        self.optimizer.step()
+        return loss.detach()

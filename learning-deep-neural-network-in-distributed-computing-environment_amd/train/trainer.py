@@ -59,8 +59,10 @@ def train_local_epoch(model, trainloader, criterion, optimizer, device, schedule
 
     ``timer`` (utils.tracing.PhaseTimer) brackets forward / backward / grad_sync /
     optimizer with roctx ranges and HIP events (BAR/trainer.py:194-223 has none).
-    ``graphs``: replay each full-size step from one hipGraph (train/graphed.py) when
-    the step issues no per-step collectives.
+    ``graphs``: replay each full-size step from hipGraphs (train/graphed.py): one graph
+    for a single-process step; with per-step data parallelism (``dp``) a forward+
+    backward graph whose in-graph bucket events start the RCCL all-reduces while the
+    backward still runs, then an optimizer graph (GraphedDPStep).
     """
     tm = timer or null_timer()
     model.train()
@@ -70,8 +72,7 @@ def train_local_epoch(model, trainloader, criterion, optimizer, device, schedule
     stats = torch.zeros(2, dtype=torch.float32, device=dev)
     total, done = 0, 0
     ldnn_ce = isinstance(criterion, LdnnCE)
-    use_graph = (graphs and dev.type == "cuda" and dp is None and step_aggregator is None and ldnn_ce
-                 and timer is None)
+    use_graph = (graphs and dev.type == "cuda" and step_aggregator is None and ldnn_ce and timer is None)
     try:
         for i, (x, y) in enumerate(trainloader):
             if i >= nb:
@@ -79,7 +80,7 @@ def train_local_epoch(model, trainloader, criterion, optimizer, device, schedule
             if use_graph and (i > 0 or getattr(model, "_ldnn_graphed", None) is not None):
                 # the first batch ran eagerly (momentum / optimizer state exist), so the
                 # capture needs no extra warmup steps and training semantics are unchanged
-                gs = _graphed_step(model, criterion, optimizer, x, y)
+                gs = _graphed_step(model, criterion, optimizer, x, y, dp)
                 if x.shape == gs.x.shape:
                     losses[i] = gs(x, y).detach().float()
                     total += y.numel()
@@ -128,13 +129,16 @@ def train_local_epoch(model, trainloader, criterion, optimizer, device, schedule
 
 
 
-def _graphed_step(model, criterion, optimizer, x, y):
-    """The model's cached GraphedStep (captured on the first graphed batch)."""
-    from .graphed import GraphedStep
+def _graphed_step(model, criterion, optimizer, x, y, dp=None):
+    """The model's cached GraphedStep / GraphedDPStep (captured on the first graphed batch)."""
+    from .graphed import GraphedDPStep, GraphedStep
 
     gs = getattr(model, "_ldnn_graphed", None)
-    if gs is None or gs.optimizer is not optimizer or gs.criterion is not criterion:
-        gs = GraphedStep(model, criterion, optimizer, x, y, warmup=0)
+    if gs is None or gs.optimizer is not optimizer or gs.criterion is not criterion or getattr(gs, "dp", None) is not dp:
+        if dp is not None:
+            gs = GraphedDPStep(dp, criterion, optimizer, x, y)
+        else:
+            gs = GraphedStep(model, criterion, optimizer, x, y, warmup=0)
         model._ldnn_graphed = gs
     return gs
 

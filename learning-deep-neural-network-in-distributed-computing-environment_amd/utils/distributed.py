@@ -47,11 +47,41 @@ def env_int(name: str, default: int) -> int:
         return default
 
 
+def _first_env(names, default: int) -> int:
+    for n in names:
+        if n in os.environ:
+            return env_int(n, default)
+    return default
+
+
+# Launchers the reference's variants are started with: torchrun (BAR/DAR) and
+# `mpirun -np N` (BR/DR/BDR/DDR, BR/main.py:15-17 -- Open MPI, MPICH / Hydra PMI,
+# PMIx, Slurm).  No mpi4py: the ranks rendezvous over the c10d TCP store.
+_RANK_VARS = ("RANK", "OMPI_COMM_WORLD_RANK", "PMI_RANK", "PMIX_RANK", "SLURM_PROCID")
+_SIZE_VARS = ("WORLD_SIZE", "OMPI_COMM_WORLD_SIZE", "PMI_SIZE", "SLURM_NTASKS")
+_LOCAL_VARS = ("LOCAL_RANK", "OMPI_COMM_WORLD_LOCAL_RANK", "MPI_LOCALRANKID", "PMI_LOCAL_RANK", "SLURM_LOCALID")
+
+
+def launch_env() -> tuple[int, int, int]:
+    """(rank, world_size, local_rank) from torchrun, mpirun or Slurm environment variables."""
+    rank = _first_env(_RANK_VARS, 0)
+    world = _first_env(_SIZE_VARS, 1)
+    local = _first_env(_LOCAL_VARS, -1)
+    if local < 0:
+        local = rank  # single node: ranks are local
+    return rank, world, local
+
+
 def setup(backend: str | None = None, timeout_s: float = 600.0, device: str | None = None) -> DistContext:
     """Initialise (if needed) the default process group and bind this rank's device."""
-    rank = env_int("RANK", 0)
-    world = env_int("WORLD_SIZE", 1)
-    local = env_int("LOCAL_RANK", 0)
+    rank, world, local = launch_env()
+    if world > 1:  # env:// rendezvous reads these (mpirun does not set them)
+        os.environ.setdefault("RANK", str(rank))
+        os.environ.setdefault("WORLD_SIZE", str(world))
+        os.environ.setdefault("LOCAL_RANK", str(local))
+        # a failed / timed-out RCCL collective aborts the communicator and raises in
+        # the caller instead of leaving the other ranks hung
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
     ndev = torch.cuda.device_count()
     use_cuda = ndev > 0 and device != "cpu"
     if backend is None:

@@ -153,3 +153,26 @@ def test_cli_two_ranks_end_to_end(tmp_path):
     assert (tmp_path / "histories.json").exists()
     assert len(list((tmp_path / "Graphs").glob("*.png"))) == 6
     assert len(list((tmp_path / "ckpt").glob("*.pt"))) >= 2  # per-rank checkpoints for gossip
+
+
+def test_mpirun_style_env_bootstrap():
+    """`mpirun -np N python train.py` (BR/main.py:15-17) sets OMPI_COMM_WORLD_* / PMI_*,
+    not RANK / WORLD_SIZE: setup() must still form the process group (no mpi4py)."""
+    import subprocess
+
+    port = _port()
+    procs = []
+    for r in range(2):
+        env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+        if r == 0:  # Open MPI names
+            env.update(OMPI_COMM_WORLD_RANK="0", OMPI_COMM_WORLD_SIZE="2", OMPI_COMM_WORLD_LOCAL_RANK="0")
+        else:       # MPICH / Hydra PMI names
+            env.update(PMI_RANK="1", PMI_SIZE="2")
+        env.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "scripts", "mpienv_worker.py"), ROOT],
+                                      env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    outs = [p.communicate(timeout=120) for p in procs]
+    for p, (o, e) in zip(procs, outs):
+        assert p.returncode == 0, e[-2000:]
+    text = "".join(o for o, _ in outs)
+    assert "MPIENV rank=0 world=2 local=0 sum=3.0" in text and "MPIENV rank=1 world=2 local=1 sum=3.0" in text, text

@@ -1,0 +1,124 @@
+"""Graph-captured data-parallel steps (train/graphed.py GraphedDPStep): the bucket
+collectives run on a side-stream branch of the step graph while the backward
+still runs (in_graph), or between a backward graph and an optimizer graph (after)."""
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+import torch
+
+import ldnn
+from ldnn.models import CrossEntropyLoss, build_model, xavier_init
+from ldnn.optim import SGD
+from ldnn.parallel.comm import LocalComm
+from ldnn.parallel.ddp import DataParallel
+from ldnn.train.graphed import GraphedDPStep, GraphedStep
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _models(name, n):
+    torch.manual_seed(0)
+    ms = [build_model(name) for _ in range(n)]
+    xavier_init(ms[0])
+    for m in ms[1:]:
+        m.load_state_dict(ms[0].state_dict())
+    for m in ms:
+        ldnn.prepare(m, "cuda")
+    return ms
+
+
+def _close_updates(pa, pb, p0, rel=2e-2):
+    for a, b, r in zip(pa, pb, p0):
+        da, db = (a.detach() - r).double(), (b.detach() - r).double()
+        assert (da - db).norm().item() <= rel * db.norm().item() + 1e-6, ((da - db).norm().item(), db.norm().item())
+
+
+@pytest.mark.parametrize("mode", ["in_graph", "after"])
+@pytest.mark.parametrize("comm_dtype", [None, torch.bfloat16])
+def test_side_stream_collective_waits_for_its_bucket(comm_dtype, mode):
+    """Ordering check without a second rank: the 'collective' doubles each bucket where
+    the all-reduce would run (a side-stream branch of the graph for in_graph).  Only if
+    it runs after the bucket's gradients were written and before the optimizer is the
+    result == plain SGD at twice the lr."""
+    shape = (512, 1, 28, 28)
+    m1, m2 = _models("lenet5", 2)
+    crit = CrossEntropyLoss()
+    dp = DataParallel(m1, LocalComm(), bucket_cap_mb=0.05, broadcast_init=False, comm_dtype=comm_dtype)
+    assert len(dp.bucketer.buckets) >= 3
+    o1, o2 = SGD(m1.parameters(), lr=0.01, momentum=0.0), SGD(m2.parameters(), lr=0.02, momentum=0.0)
+    g = torch.Generator(device="cuda").manual_seed(1)
+    xs = [torch.randn(*shape, device="cuda", generator=g).bfloat16() for _ in range(4)]
+    ys = [torch.randint(0, 10, (shape[0],), device="cuda", generator=g) for _ in range(4)]
+    p0 = [p.detach().clone() for p in m2.parameters()]
+    # one eager step each first (optimizer state exists before capture), the same x2 on m1
+    for m, o, k in ((m1, o1, 2.0), (m2, o2, 1.0)):
+        o.zero_grad()
+        crit(m(xs[0]), ys[0]).backward()
+        m._ldnn_flat.grad.mul_(k)
+        o.step()
+    gd = GraphedDPStep(dp, crit, o1, xs[0], ys[0], mode=mode, comm_fn=lambda i, buf: buf.mul_(2.0))
+    gs = GraphedStep(m2, crit, o2, xs[0], ys[0], warmup=0)
+    for i in range(1, 4):
+        gd(xs[i], ys[i])
+        gs(xs[i], ys[i])
+    torch.cuda.synchronize()
+    _close_updates(list(m1.parameters()), list(m2.parameters()), p0, rel=2e-2 if comm_dtype is None else 5e-2)
+
+
+def test_rccl_world1_overlap_path(tmp_path):
+    """The real RCCL path (TorchComm on a 1-rank communicator: the bucket all-reduces
+    captured into the step graph on a side-stream branch) trains like the
+    single-process graphed step."""
+    import torch.distributed as dist
+
+    from ldnn.parallel.comm import TorchComm
+
+    store = dist.FileStore(str(tmp_path / "store"), 1)
+    dist.init_process_group("nccl", store=store, rank=0, world_size=1, device_id=torch.device("cuda:0"))
+    try:
+        shape = (256, 1, 28, 28)
+        m1, m2 = _models("lenet5", 2)
+        crit = CrossEntropyLoss()
+        comm = TorchComm()
+        assert comm.device_collectives
+        dp = DataParallel(m1, comm, bucket_cap_mb=0.05, broadcast_init=False)
+        o1, o2 = SGD(m1.parameters(), lr=0.02, momentum=0.9), SGD(m2.parameters(), lr=0.02, momentum=0.9)
+        g = torch.Generator(device="cuda").manual_seed(2)
+        xs = [torch.randn(*shape, device="cuda", generator=g).bfloat16() for _ in range(5)]
+        ys = [torch.randint(0, 10, (shape[0],), device="cuda", generator=g) for _ in range(5)]
+        p0 = [p.detach().clone() for p in m2.parameters()]
+        for m, o in ((m1, o1), (m2, o2)):
+            o.zero_grad()
+            crit(m(xs[0]), ys[0]).backward()
+            o.step()
+        gd = GraphedDPStep(dp, crit, o1, xs[0], ys[0])
+        assert gd.mode == "in_graph"
+        gs = GraphedStep(m2, crit, o2, xs[0], ys[0], warmup=0)
+        for i in range(1, 5):
+            gd(xs[i], ys[i])
+            gs(xs[i], ys[i])
+        # the odd-shaped last batch of an epoch falls back to the eager bucketed step
+        gd(xs[0][:100], ys[0][:100])
+        gs(xs[0][:100], ys[0][:100])
+        torch.cuda.synchronize()
+        _close_updates(list(m1.parameters()), list(m2.parameters()), p0)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_graphed_dp_two_ranks_gloo_equals_big_batch():
+    """2 ranks (gloo, sharing the GPU) through train_local_epoch(graphs=True, dp=...)
+    end with the parameters of ONE graphed rank on the concatenated batches."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+           "--master-port", str(port), os.path.join(ROOT, "scripts", "check_graphed_dp.py")]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "GRAPHED_DP_OK" in r.stdout, r.stdout[-3000:]
