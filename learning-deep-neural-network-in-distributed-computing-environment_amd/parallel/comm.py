@@ -25,6 +25,12 @@ import torch
 import torch.distributed as dist
 
 SUM, MAX, MIN = "sum", "max", "min"
+
+
+class RankDivergenceError(RuntimeError):
+    """The ranks issued different collective sequences (different op counts / kinds /
+    shapes).  Raised by Comm.check_schedule instead of letting a mismatched collective
+    hang until the process-group timeout."""
 _TORCH_OPS = {SUM: dist.ReduceOp.SUM, MAX: dist.ReduceOp.MAX, MIN: dist.ReduceOp.MIN}
 
 
@@ -47,6 +53,22 @@ class Comm:
 
     def schedule_digest(self) -> tuple[int, str]:
         return self._nops, self._sched.hexdigest()
+
+    def check_schedule(self, where: str = "", device=None):
+        """Cross-check every rank's collective schedule (op count + running hash of
+        op / shape / dtype) with one small all-gather; raise RankDivergenceError on
+        the first mismatch.  The training driver calls it once per global epoch and
+        every ``check_every`` steps of per-step synchronisation -- the class of bug
+        the reference's dead time-limit break would cause."""
+        if self.world_size <= 1:
+            return
+        n, h = self.schedule_digest()
+        v = torch.tensor([n, int(h[:15], 16)], dtype=torch.int64,
+                         device=device if device is not None else "cpu")
+        got = [t.cpu() for t in self.all_gather(v)]
+        if any(not torch.equal(got[0], g) for g in got):
+            desc = ", ".join(f"rank {r}: {int(g[0])} ops #{int(g[1]):015x}" for r, g in enumerate(got))
+            raise RankDivergenceError(f"collective schedules diverged{' at ' + where if where else ''}: {desc}")
 
     # -- API (implemented by subclasses)
     def all_reduce(self, t: torch.Tensor, op: str = SUM, async_op: bool = False):

@@ -54,15 +54,18 @@ def _progress(it, enabled, desc):
 
 def train_local_epoch(model, trainloader, criterion, optimizer, device, scheduler=None, *, dp=None,
                       step_aggregator=None, cutoff: StragglerCutoff | None = None, max_steps: int | None = None,
-                      step_scheduler: bool = True, timer: PhaseTimer | None = None, graphs: bool = False):
+                      step_scheduler: bool = True, timer: PhaseTimer | None = None, graphs: bool = False,
+                      check_comm=None, check_every: int = 50):
     """One pass over the rank's shard.  Returns (mean loss, accuracy %, per-batch losses).
 
     ``timer`` (utils.tracing.PhaseTimer) brackets forward / backward / grad_sync /
     optimizer with roctx ranges and HIP events (BAR/trainer.py:194-223 has none).
     ``graphs``: replay each full-size step from hipGraphs (train/graphed.py): one graph
-    for a single-process step; with per-step data parallelism (``dp``) a forward+
-    backward graph whose in-graph bucket events start the RCCL all-reduces while the
-    backward still runs, then an optimizer graph (GraphedDPStep).
+    for a single-process step; with per-step data parallelism (``dp``) one graph whose
+    side-stream branch runs the bucket RCCL all-reduces beside the backward
+    (GraphedDPStep).
+    ``check_comm``: with per-step synchronisation, cross-check the ranks' collective
+    schedules every ``check_every`` steps (Comm.check_schedule).
     """
     tm = timer or null_timer()
     model.train()
@@ -87,6 +90,8 @@ def train_local_epoch(model, trainloader, criterion, optimizer, device, schedule
                     done += 1
                     if cutoff is not None:
                         cutoff.step(i)
+                    if check_comm is not None and (i + 1) % check_every == 0:
+                        check_comm.check_schedule(f"step {i + 1}", dev if check_comm.device_collectives else None)
                     continue
             optimizer.zero_grad()
             with tm.phase("forward"):
@@ -112,6 +117,8 @@ def train_local_epoch(model, trainloader, criterion, optimizer, device, schedule
             done += 1
             if cutoff is not None:
                 cutoff.step(i)
+            if check_comm is not None and (i + 1) % check_every == 0:
+                check_comm.check_schedule(f"step {i + 1}", dev if check_comm.device_collectives else None)
     except StopLocalTraining:
         if step_scheduler and scheduler is not None:
             scheduler.step()
@@ -223,7 +230,9 @@ def train_global(model, trainloader, val_loader, trainset, valset, indices_train
             try:
                 loss, acc, bl = train_local_epoch(model, trainloader, criterion, optimizer, dev, scheduler, dp=dp,
                                                   step_aggregator=step_aggregator, cutoff=cutoff,
-                                                  max_steps=max_steps, timer=timer, graphs=graphs)
+                                                  max_steps=max_steps, timer=timer, graphs=graphs,
+                                                  check_comm=comm if (sync_every == "step" and N > 1) else None,
+                                                  check_every=max(check_every, 1) * 5)
             except StopLocalTraining:
                 # cut by the collective time limit: keep LR schedules aligned across ranks
                 for _ in range(num_local_epochs - local_epoch - 1):
@@ -248,6 +257,9 @@ def train_global(model, trainloader, val_loader, trainset, valset, indices_train
         packed = _pack(records, batch_losses, num_local_epochs, max_len, dev)
         gathered = comm.all_gather(packed) if N > 1 else [packed]
         per_rank = [_unpack(g, num_local_epochs, max_len) for g in gathered]
+        # every rank must have issued the same collectives so far (RankDivergenceError otherwise)
+        comm.check_schedule(f"global epoch {global_epoch + 1}", dev if getattr(comm, "device_collectives", False)
+                            else None)
 
         if rank == 0:
             cur_losses, cur_accs = [], []

@@ -176,3 +176,34 @@ def test_mpirun_style_env_bootstrap():
         assert p.returncode == 0, e[-2000:]
     text = "".join(o for o, _ in outs)
     assert "MPIENV rank=0 world=2 local=0 sum=3.0" in text and "MPIENV rank=1 world=2 local=1 sum=3.0" in text, text
+
+
+def _diverge_worker(rank, world, port, q):
+    _init(rank, world, port)
+    from ldnn.parallel.comm import RankDivergenceError, TorchComm
+
+    c = TorchComm()
+    t = torch.ones(3)
+    c.all_reduce(t)
+    c.check_schedule("aligned")          # same schedule so far: no error
+    if rank == 0:
+        c.record("all_reduce", torch.ones(7))   # rank 0 took a different path (an extra op)
+    try:
+        c.check_schedule("after divergence")
+        q.put((rank, "no error"))
+    except RankDivergenceError as e:
+        q.put((rank, str(e)))
+    dist.destroy_process_group()
+
+
+def test_schedule_divergence_is_detected():
+    """Comm.check_schedule all-gathers every rank's (op count, op-sequence hash) and
+    raises RankDivergenceError on EVERY rank when they differ (SURVEY §5 race detection)."""
+    world, port = 2, _port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    mp.spawn(_diverge_worker, args=(world, port, q), nprocs=world, join=True)
+    res = dict(q.get(timeout=30) for _ in range(world))
+    for r in range(world):
+        assert "collective schedules diverged at after divergence" in res[r], res
+        assert "rank 0: 3 ops" in res[r] and "rank 1: 2 ops" in res[r], res
