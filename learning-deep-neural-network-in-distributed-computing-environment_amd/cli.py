@@ -66,7 +66,10 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--device", type=str, default="auto", help="auto | cpu | cuda")
     p.add_argument("--legacy_gossip", action="store_true", help="reproduce the reference's lost GPU gossip update")
     p.add_argument("--average_buffers", action="store_true", help="also average BN buffers in weight averaging")
-    p.add_argument("--replace", action="store_true", help="sample re-partitions with replacement (BDR/DAR)")
+    p.add_argument("--replace", nargs="?", const="on", default="auto", choices=["auto", "on", "off"],
+                   help="sample the per-global-epoch re-partition with replacement.  auto (default) follows the "
+                        "reference variant: on for class-skewed shards (DAR/DR/DDR dataloader.py:123,129) and for "
+                        "the balanced double ring (BDR/dataloader.py:94,100), off for BAR/BR")
     p.add_argument("--no_repartition", action="store_true")
     p.add_argument("--check_every", type=int, default=20, help="steps between straggler-cutoff rounds")
     p.add_argument("--bucket_mb", type=float, default=32.0)
@@ -86,6 +89,13 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--trace", action="store_true",
                    help="roctx ranges per phase + HIP-event phase timers (summary in metrics.jsonl)")
     return p
+
+
+def resolve_replace(flag: str, fixed_ratio, topology: str) -> bool:
+    """--replace auto -> the reference variant's sampling (see the flag's help)."""
+    if flag == "auto":
+        return fixed_ratio is not None or topology == "double_ring"
+    return flag == "on"
 
 
 def main(argv=None):
@@ -119,6 +129,8 @@ def main(argv=None):
     if args.partition == "balanced":
         fixed_ratio = None
 
+    replace = resolve_replace(args.replace, fixed_ratio, args.topology)
+
     dp = None
     if args.sync_every == "step" and args.topology == "allreduce" and world > 1:
         dp = DataParallel(model, comm, bucket_cap_mb=args.bucket_mb, average=args.aggregation_type == "equal",
@@ -145,21 +157,28 @@ def main(argv=None):
     per_rank = args.topology != "allreduce" or args.sync_every == "global_epoch"
     ckpt = Checkpointer(os.path.join(args.out_dir, "ckpt"), rank, per_rank=per_rank,
                         every=args.checkpoint_every) if args.checkpoint_every > 0 else None
-    start, hist = 0, None
+    start, hist, rng_state = 0, None, None
     if args.resume:
         path = args.resume
         if path == "latest":
             path = Checkpointer(os.path.join(args.out_dir, "ckpt"), rank, per_rank=per_rank).latest()
         if path:
-            sd = load_checkpoint(path, model, optimizer, scheduler)
+            sd = load_checkpoint(path, model, optimizer, scheduler, rank=rank)
+            flat.refresh_shadow()
             start, hist = sd["global_epoch"], sd["histories"]
             ex = sd.get("extra", {})
+            rng_state = ex.get("rng_state")
             if "indices_train" in ex:
                 from .data.loader import DeviceLoader
+                from .train.trainer import loader_seed
 
                 tr_idx, va_idx = ex["indices_train"].numpy(), ex["indices_val"].numpy()
-                train_loader = DeviceLoader(trainset, tr_idx, args.batch_size, dev, dtype=dtype, augment=args.augment)
+                train_loader = DeviceLoader(trainset, tr_idx, args.batch_size, dev, dtype=dtype, augment=args.augment,
+                                            seed=loader_seed(args.seed, rank, start))
                 val_loader = DeviceLoader(valset, va_idx, args.batch_size, dev, dtype=dtype)
+            if ex.get("fixed_classes") is not None:
+                fc = ex["fixed_classes"]
+                fixed_classes = fc.tolist() if torch.is_tensor(fc) else list(fc)
 
     from .utils import tracing
 
@@ -173,11 +192,11 @@ def main(argv=None):
         world, args.epochs_local, args.epochs_global, timelimit, args.batch_size, args.prev_fraction,
         args.next_fraction, args.local_weight, args.aggregation_type, args.aggregation_by, comm=comm,
         topology=args.topology, fixed_classes=fixed_classes, fixed_ratio=fixed_ratio, sync_every=args.sync_every,
-        dp=dp, partition_rule=args.partition_rule, repartition=not args.no_repartition, replace=args.replace,
+        dp=dp, partition_rule=args.partition_rule, repartition=not args.no_repartition, replace=replace,
         seed=args.seed, legacy_gossip=args.legacy_gossip, average_buffers=args.average_buffers,
         check_every=args.check_every, progress=not args.quiet, logger=logger, checkpointer=ckpt,
         start_global_epoch=start, histories=hist, dtype=dtype, verbose=not args.quiet, timer=timer,
-        graphs=args.graphs)
+        graphs=args.graphs, rng_state=rng_state)
     if timer is not None:
         phases = timer.summary()
         logger.log(kind="phase_times", phases=phases)

@@ -65,6 +65,8 @@ class DeviceLoader:
         self._a = (1.0 / (scale * s)).view(1, c, 1, 1)
         self._b = (-m / s).view(1, c, 1, 1)
         self._gen = torch.Generator().manual_seed(seed)
+        self.seed = int(seed)
+        self._aug_gen = None
         self.epoch = 0
 
     def __len__(self):
@@ -80,7 +82,9 @@ class DeviceLoader:
         x = self.images.index_select(0, idx)
         x = torch.addcmul(self._b, x.to(torch.float32), self._a)
         if self.augment:
-            x = _flip_crop(x)
+            if self._aug_gen is None:
+                self._aug_gen = torch.Generator(device=self.device).manual_seed(self.seed + 1)
+            x = _flip_crop(x, self._aug_gen)
         return x.to(self.dtype), self.labels.index_select(0, idx)
 
     def __iter__(self):
@@ -96,15 +100,18 @@ class DeviceLoader:
             yield self._batch(order[s: s + bs])
 
 
-def _flip_crop(x: torch.Tensor, pad: int = 4) -> torch.Tensor:
-    """GPU random horizontal flip + padded random crop (light replacement for the
-    reference's CPU AutoAugment, BAR/dataloader.py:16)."""
+def _flip_crop(x: torch.Tensor, gen: torch.Generator | None = None, pad: int = 4) -> torch.Tensor:
+    """GPU random horizontal flip + padded random crop, an independent flip and crop
+    offset per sample drawn from the loader's seeded generator."""
     B, C, H, W = x.shape
-    flip = torch.rand(B, device=x.device) < 0.5
+    flip = torch.rand(B, device=x.device, generator=gen) < 0.5
     x = torch.where(flip.view(B, 1, 1, 1), x.flip(3), x)
     xp = torch.nn.functional.pad(x, (pad, pad, pad, pad))
-    dx, dy = np.random.randint(0, 2 * pad + 1, size=2)
-    return xp[:, :, dy: dy + H, dx: dx + W].contiguous()
+    off = torch.randint(0, 2 * pad + 1, (2, B), device=x.device, generator=gen)
+    iy = (off[0].view(B, 1, 1, 1) + torch.arange(H, device=x.device).view(1, 1, H, 1)).expand(B, C, H, W + 2 * pad)
+    xr = xp.gather(2, iy)
+    ix = (off[1].view(B, 1, 1, 1) + torch.arange(W, device=x.device).view(1, 1, 1, W)).expand(B, C, H, W)
+    return xr.gather(3, ix)
 
 
 # ---------------------------------------------------------------- probe (A12)
@@ -149,7 +156,7 @@ def estimate_epoch_duration(trainloader, world_size, model, device, num_batches:
 
 # --------------------------------------------------------- reference factory
 def get_loaders(batch_size, world_size, rank, model, device, fixed_ratio=None, *, dataset: str = "cifar10",
-                comm=None, seed: int = 0, val_fraction: float = 0.2, partition_rule: str = "throughput",
+                comm=None, seed: int = 0, val_fraction: float = 0.2, partition_rule: str = "reference_duration",
                 probe_batches: int = 10, n_train: int | None = None, n_test: int | None = None,
                 dtype=torch.float32, augment: bool = False, data_root: str = "data"):
     """Build (train, val, test) loaders for this rank (BAR/dataloader.py:9-51).
@@ -180,7 +187,8 @@ def get_loaders(batch_size, world_size, rank, model, device, fixed_ratio=None, *
         train_indices, fixed = P.skewed_partition(trainset.targets, shares, rank, fixed_ratio,
                                                   trainset.num_classes, rng)
         val_indices, _ = P.skewed_partition(valset.targets, shares, rank, fixed_ratio, valset.num_classes, rng)
-    train_loader = DeviceLoader(trainset, train_indices, batch_size, device, dtype=dtype, augment=augment)
+    train_loader = DeviceLoader(trainset, train_indices, batch_size, device, dtype=dtype, augment=augment,
+                                seed=(seed * 1_000_003 + rank * 10_007) & 0x7FFFFFFF)
     val_loader = DeviceLoader(valset, val_indices, batch_size, device, dtype=dtype)
     test_loader = DeviceLoader(testset, None, batch_size, device, dtype=dtype)
     out = (train_loader, val_loader, test_loader, trainset, valset, train_indices, val_indices)
@@ -189,7 +197,7 @@ def get_loaders(batch_size, world_size, rank, model, device, fixed_ratio=None, *
 
 def get_subset_loaders(trainset, valset, train_indices, val_indices, batch_size, prev_fraction, next_fraction,
                        share, device, rng: np.random.Generator, replace: bool = False, fixed_classes=None,
-                       fixed_ratio=None, dtype=torch.float32, augment: bool = False):
+                       fixed_ratio=None, dtype=torch.float32, augment: bool = False, loader_seed: int = 0):
     """Re-partition for the next global epoch (BAR/dataloader.py:107-117)."""
     kw = {}
     if fixed_classes is not None:
@@ -198,5 +206,5 @@ def get_subset_loaders(trainset, valset, train_indices, val_indices, batch_size,
                           labels=trainset.targets if kw else None, **kw)
     va = P.next_partition(len(valset), val_indices, share, prev_fraction, next_fraction, rng, replace,
                           labels=valset.targets if kw else None, **kw)
-    return (DeviceLoader(trainset, tr, batch_size, device, dtype=dtype, augment=augment),
+    return (DeviceLoader(trainset, tr, batch_size, device, dtype=dtype, augment=augment, seed=loader_seed),
             DeviceLoader(valset, va, batch_size, device, dtype=dtype), tr, va)

@@ -150,6 +150,21 @@ def _graphed_step(model, criterion, optimizer, x, y, dp=None):
     return gs
 
 
+def loader_seed(seed: int, rank: int, global_epoch: int) -> int:
+    """Seed of a rank's training loader for a global epoch (augmentation draws): a
+    pure function of (seed, rank, epoch), so a resumed run replays the same draws."""
+    return (seed * 1_000_003 + rank * 10_007 + global_epoch * 101) & 0x7FFFFFFF
+
+
+def _plain(x):
+    """Checkpoint round trip (weights_only) turns numpy RNG state leaves into tensors / str keys."""
+    if isinstance(x, dict):
+        return {k: _plain(v) for k, v in x.items()}
+    if torch.is_tensor(x):
+        return x.item() if x.numel() == 1 else x.tolist()
+    return x
+
+
 def _pack(local_records, batch_losses_per_epoch, E_l, max_len, device):
     """[n_done, (loss, acc, vloss, vacc) x E_l, (len, losses padded to max_len) x E_l]"""
     buf = torch.full((1 + 4 * E_l + E_l * (1 + max_len),), -1.0, dtype=torch.float64)
@@ -187,12 +202,16 @@ def train_global(model, trainloader, val_loader, trainset, valset, indices_train
                  seed: int = 0, legacy_gossip: bool = False, average_buffers: bool = False,
                  check_every: int = 20, progress: bool = True, logger=None, checkpointer=None,
                  start_global_epoch: int = 0, histories=None, dtype=torch.float32, verbose: bool = True,
-                 timer: PhaseTimer | None = None, graphs: bool = False):
+                 timer: PhaseTimer | None = None, graphs: bool = False, rng_state=None):
+    """``rng_state`` (resume): the re-partition RNG state saved in the checkpoint's
+    ``extra`` -- with it, a resumed run draws the same shards as an uninterrupted one."""
     comm = comm or default_comm()
     tm = timer or null_timer()
     N = comm.world_size
     dev = torch.device(device)
     rng = np.random.default_rng(seed * 7919 + rank)
+    if rng_state is not None:
+        rng.bit_generator.state = _plain(rng_state)
     H = histories or {
         "all_workers_losses": [[] for _ in range(N)],
         "all_epochs_losses": [],
@@ -318,7 +337,8 @@ def train_global(model, trainloader, val_loader, trainset, valset, indices_train
             trainloader, val_loader, indices_train, indices_val = get_subset_loaders(
                 trainset, valset, indices_train, indices_val, batch_size, prev_fraction, next_fraction, share, dev,
                 rng, replace, fixed_classes, fixed_ratio, dtype=dtype,
-                augment=getattr(trainloader, "augment", False))
+                augment=getattr(trainloader, "augment", False),
+                loader_seed=loader_seed(seed, rank, global_epoch + 1))
         if logger is not None:
             logger.log(kind="global_epoch", global_epoch=global_epoch + 1, duration_s=duration,
                        train_loss=H["global_train_losses"][-1], train_acc=H["global_train_accuracies"][-1],

@@ -12,9 +12,11 @@ Format: one ``torch.save`` dict per file, loadable with ``weights_only=True``
   extra        shard indices, fixed classes, RNG state, config
   torch_rng    CPU / GPU RNG states
 
-Synchronous modes (all replicas identical) are written by rank 0 only;
-gossip / independent-worker modes (replicas differ) write one file per rank.
-Writes go to a temp file then os.replace (atomic).
+Synchronous modes (all replicas identical) are written by rank 0 only, plus a
+small per-rank ``xtra_geNNNN_rankR.pt`` with each other rank's own shard indices
+and partition-RNG state (so a resumed run re-partitions exactly as an
+uninterrupted one); gossip / independent-worker modes (replicas differ) write one
+full file per rank.  Writes go to a temp file then os.replace (atomic).
 """
 from __future__ import annotations
 
@@ -59,11 +61,20 @@ class Checkpointer:
                        and (self.per_rank or "_rank" not in f))
         return os.path.join(self.dir, cands[-1]) if cands else None
 
+    def extra_path(self, global_epoch: int, rank: int | None = None) -> str:
+        r = self.rank if rank is None else rank
+        return os.path.join(self.dir, f"xtra_ge{global_epoch:04d}_rank{r}.pt")
+
     def save(self, global_epoch, model, optimizer=None, scheduler=None, histories=None, extra=None, config=None):
         if global_epoch % self.every:
             return None
         if not self.per_rank and self.rank != 0:
-            return None
+            p = self.extra_path(global_epoch)
+            torch.save({"format": "ldnn-xtra-v1", "global_epoch": int(global_epoch), "extra": _to_safe(extra or {})},
+                       p + ".tmp")
+            os.replace(p + ".tmp", p)
+            self._prune()
+            return p
         sd = {
             "format": "ldnn-ckpt-v1",
             "global_epoch": int(global_epoch),
@@ -85,9 +96,13 @@ class Checkpointer:
         return p
 
     def _prune(self):
-        suffix = f"_rank{self.rank}.pt" if self.per_rank else ".pt"
-        files = sorted(f for f in os.listdir(self.dir) if f.startswith("ckpt_ge") and f.endswith(suffix)
-                       and (self.per_rank or "_rank" not in f))
+        if not self.per_rank and self.rank != 0:
+            files = sorted(f for f in os.listdir(self.dir) if f.startswith("xtra_ge") and
+                           f.endswith(f"_rank{self.rank}.pt"))
+        else:
+            suffix = f"_rank{self.rank}.pt" if self.per_rank else ".pt"
+            files = sorted(f for f in os.listdir(self.dir) if f.startswith("ckpt_ge") and f.endswith(suffix)
+                           and (self.per_rank or "_rank" not in f))
         for f in files[: max(0, len(files) - self.keep)]:
             try:
                 os.remove(os.path.join(self.dir, f))
@@ -95,9 +110,17 @@ class Checkpointer:
                 pass
 
 
-def load_checkpoint(path: str, model, optimizer=None, scheduler=None, map_location="cpu") -> dict:
-    """Restore model / optimizer / scheduler in place; returns the checkpoint dict."""
+def load_checkpoint(path: str, model, optimizer=None, scheduler=None, map_location="cpu",
+                    rank: int | None = None) -> dict:
+    """Restore model / optimizer / scheduler (and the torch CPU / GPU RNG) in place;
+    returns the checkpoint dict.  For a rank-0 (synchronous-mode) checkpoint,
+    ``rank`` > 0 swaps in that rank's own ``extra`` (shards, partition RNG)."""
     sd = torch.load(path, map_location=map_location, weights_only=True)
+    base = os.path.basename(path)
+    if rank and "_rank" not in base and base.startswith("ckpt_ge"):
+        xp = os.path.join(os.path.dirname(path), f"xtra_ge{int(sd['global_epoch']):04d}_rank{rank}.pt")
+        if os.path.exists(xp):
+            sd["extra"] = torch.load(xp, map_location=map_location, weights_only=True)["extra"]
     with torch.no_grad():
         model.load_state_dict(sd["model"])
     for m in model.modules():
@@ -111,4 +134,6 @@ def load_checkpoint(path: str, model, optimizer=None, scheduler=None, map_locati
         scheduler.load_state_dict(sd["scheduler"])
     if "torch_rng" in sd:
         torch.set_rng_state(sd["torch_rng"])
+    if "cuda_rng" in sd and torch.cuda.is_available():
+        torch.cuda.set_rng_state(sd["cuda_rng"])
     return sd

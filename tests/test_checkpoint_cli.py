@@ -41,7 +41,7 @@ def test_save_load_gives_identical_next_step(tmp_path):
     sch2 = StepLR(opt2, 1, gamma=0.5)
     sd = load_checkpoint(p, m2, opt2, sch2)
     assert sd["global_epoch"] == 3 and sd["histories"]["global_train_losses"] == [1.0, 0.5]
-    assert opt2.param_groups[0]["lr"] == opt.param_groups[0]["lr"] * 1.0 or True
+    assert opt2.param_groups[0]["lr"] == opt.param_groups[0]["lr"] and sch2.last_epoch == sch.last_epoch
     got_next = _step(m2, opt2, x, y)
     assert abs(got_next - ref_next) < 1e-6
     # reference state_dict key names survive the round trip
@@ -106,3 +106,18 @@ def test_phase_timer_disabled_is_free():
     with t.phase("x"):
         pass
     assert t.summary() == {}
+
+
+def test_replace_follows_reference_variant():
+    """--replace auto: with replacement for the class-skewed variants (DAR/DR/DDR
+    dataloader.py:123,129) and the balanced double ring (BDR:94,100), without for BAR/BR."""
+    p = build_parser()
+    assert p.parse_args([]).replace == "auto" and p.parse_args(["--replace"]).replace == "on"
+    assert p.parse_args(["--replace", "off"]).replace == "off"
+    from ldnn.cli import resolve_replace
+
+    assert resolve_replace("auto", None, "allreduce") is False
+    assert resolve_replace("auto", None, "ring") is False
+    assert resolve_replace("auto", None, "double_ring") is True
+    assert resolve_replace("auto", 0.5, "allreduce") is True
+    assert resolve_replace("off", 0.5, "ring") is False and resolve_replace("on", None, "ring") is True
