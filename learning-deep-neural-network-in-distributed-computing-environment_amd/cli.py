@@ -86,6 +86,14 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--graphs", action="store_true",
                    help="replay each training step from hipGraphs; with --sync_every step the bucket "
                         "all-reduces are captured into the step graph beside the backward (RCCL)")
+    p.add_argument("--engine", choices=["auto", "autograd", "static"], default="auto",
+                   help="static: MLP models run on the graph-captured static engine (train/static_mlp.py: native "
+                        "kernels, fused loss + optimizer, per-step DP = its own RCCL reduce-scatter / sharded update "
+                        "/ all-gather); autograd: the generic module path; auto: static for MLPs on a GPU whenever "
+                        "the topology / schedule allows it")
+    p.add_argument("--ref_samples_per_s", type=float, default=None,
+                   help="one GPU's measured samples/s for this model and batch: metrics.jsonl then also logs the "
+                        "data-parallel scaling efficiency per global epoch")
     p.add_argument("--trace", action="store_true",
                    help="roctx ranges per phase + HIP-event phase timers (summary in metrics.jsonl)")
     return p
@@ -96,6 +104,27 @@ def resolve_replace(flag: str, fixed_ratio, topology: str) -> bool:
     if flag == "auto":
         return fixed_ratio is not None or topology == "double_ring"
     return flag == "on"
+
+
+def resolve_engine(args, model, dev, world: int) -> bool:
+    """--engine auto|autograd|static -> run the static MLP engine?"""
+    from .models.mlp import MLP
+    from .ops import _ext
+
+    why = None
+    if not isinstance(model, MLP):
+        why = f"--model {args.model} is not an MLP"
+    elif dev.type != "cuda" or not _ext.use_native(torch.empty(0, device=dev)):
+        why = "the static engine needs the native extension on a GPU"
+    elif args.sync_every == "step" and world > 1 and args.topology != "allreduce":
+        why = "per-step gossip (--topology ring/double_ring with --sync_every step) runs on the autograd path"
+    elif args.sync_every == "step" and world > 1 and args.aggregation_type != "equal":
+        why = "per-step weighted all-reduce runs on the autograd path"
+    elif args.grad_comm_dtype != "fp32":
+        why = "--grad_comm_dtype bf16 runs on the autograd path"
+    if args.engine == "static" and why is not None:
+        raise SystemExit(f"--engine static: {why}")
+    return args.engine != "autograd" and why is None
 
 
 def main(argv=None):
@@ -122,7 +151,18 @@ def main(argv=None):
     dataset = args.dataset or dataset_for(args.model)
     model = build_model(args.model)
     xavier_init(model)
-    flat = prepare(model, dev)
+    use_engine = resolve_engine(args, model, dev, world)
+    if use_engine:
+        from .train.engine_adapter import build_engine
+
+        step_dp = args.sync_every == "step" and world > 1
+        net, optimizer = build_engine(model.to(dev), args.batch_size, args.optimizer, args.lr, dev,
+                                      momentum=args.momentum, weight_decay=args.weight_decay,
+                                      world_size=world if step_dp else 1, use_graphs=True,
+                                      bucket_cap_elems=int(args.bucket_mb * (1 << 20)) // 4)
+        flat = net.engine.flat
+    else:
+        flat = prepare(model, dev)
     fixed_ratio = args.fixed_ratio
     if args.partition == "skewed" and fixed_ratio is None:
         fixed_ratio = 0.5
@@ -132,13 +172,17 @@ def main(argv=None):
     replace = resolve_replace(args.replace, fixed_ratio, args.topology)
 
     dp = None
-    if args.sync_every == "step" and args.topology == "allreduce" and world > 1:
+    if use_engine:   # the engine synchronises its own gradients (per-step DP) or is a plain replica
+        D.broadcast_module(model)
+        flat.refresh_shadow()
+    elif args.sync_every == "step" and args.topology == "allreduce" and world > 1:
         dp = DataParallel(model, comm, bucket_cap_mb=args.bucket_mb, average=args.aggregation_type == "equal",
                           comm_dtype=torch.bfloat16 if args.grad_comm_dtype == "bf16" else None)
     else:  # reference A6: broadcast every state_dict entry from rank 0
         D.broadcast_module(model)
         flat.refresh_shadow()
-    net = dp if dp is not None else model
+    if not use_engine:
+        net = dp if dp is not None else model
 
     dtype = torch.bfloat16 if (args.dtype == "bf16" and dev.type == "cuda") else torch.float32
     loaders = get_loaders(args.batch_size, world, rank, net, dev, fixed_ratio, dataset=dataset, comm=comm,
@@ -148,12 +192,14 @@ def main(argv=None):
     fixed_classes = loaders[7] if len(loaders) > 7 else None
 
     criterion = CrossEntropyLoss()
-    optimizer = build_optimizer(args.optimizer, model.parameters(), args.lr, args.momentum, args.weight_decay)
+    if not use_engine:
+        optimizer = build_optimizer(args.optimizer, model.parameters(), args.lr, args.momentum, args.weight_decay)
     scheduler = StepLR(optimizer, step_size=args.step_size, gamma=args.gamma)
 
     os.makedirs(args.out_dir, exist_ok=True)
     logger = MetricsLogger(os.path.join(args.out_dir, "metrics.jsonl"), rank)
-    logger.log(kind="config", world_size=world, pg_backend=ctx.backend, resolved_device=str(dev), **vars(args))
+    logger.log(kind="config", world_size=world, pg_backend=ctx.backend, resolved_device=str(dev),
+               resolved_engine="static" if use_engine else "autograd", **vars(args))
     per_rank = args.topology != "allreduce" or args.sync_every == "global_epoch"
     ckpt = Checkpointer(os.path.join(args.out_dir, "ckpt"), rank, per_rank=per_rank,
                         every=args.checkpoint_every) if args.checkpoint_every > 0 else None
@@ -163,7 +209,7 @@ def main(argv=None):
         if path == "latest":
             path = Checkpointer(os.path.join(args.out_dir, "ckpt"), rank, per_rank=per_rank).latest()
         if path:
-            sd = load_checkpoint(path, model, optimizer, scheduler, rank=rank)
+            sd = load_checkpoint(path, net if use_engine else model, optimizer, scheduler, rank=rank)
             flat.refresh_shadow()
             start, hist = sd["global_epoch"], sd["histories"]
             ex = sd.get("extra", {})
@@ -196,7 +242,7 @@ def main(argv=None):
         seed=args.seed, legacy_gossip=args.legacy_gossip, average_buffers=args.average_buffers,
         check_every=args.check_every, progress=not args.quiet, logger=logger, checkpointer=ckpt,
         start_global_epoch=start, histories=hist, dtype=dtype, verbose=not args.quiet, timer=timer,
-        graphs=args.graphs, rng_state=rng_state)
+        graphs=args.graphs, rng_state=rng_state, ref_samples_per_s=args.ref_samples_per_s)
     if timer is not None:
         phases = timer.summary()
         logger.log(kind="phase_times", phases=phases)

@@ -1,0 +1,173 @@
+"""The static MLP engine behind the reference's training API.
+
+The reference drives one model through ``train_global`` -> ``train_local_epoch``
+(BAR/main.py:57-59, BAR/trainer.py:11,194-223) with an ``optimizer`` and a
+``StepLR`` scheduler.  ``StaticMLPEngine`` (train/static_mlp.py) is the fast
+MI355X step for the MLP configs -- graph-replayed native kernels, fused loss,
+fused optimizer and, with per-step data parallelism, its own bucketed RCCL
+reduce-scatter / sharded update / all-gather -- but it owns its optimizer state
+and steps a fixed batch shape.  Two adapters let the unchanged driver run it:
+
+* ``EngineModule`` -- an ``nn.Module`` holding the MLP (whose parameters are
+  views of the engine's flat fp32 master) and the engine.  ``forward`` is the
+  MLP's own forward on the engine's bf16 shadow (validate / evaluate / probe);
+  ``state_dict`` gathers a sharded master first and returns the MLP's own keys
+  (``layers.0.weight`` ...), so checkpoints load into a plain ``mlp3``.
+* ``EngineOptimizer`` -- a ``torch.optim.Optimizer`` over the same parameters:
+  ``StepLR`` and ``param_groups[0]['lr']`` work as in the reference; its
+  ``state_dict`` carries the engine's momentum / Adam moments (gathered from the
+  shards) and ``load_state_dict`` puts them back.  ``step()`` is a no-op: the
+  engine's fused update runs inside its step.
+
+``train_local_epoch`` recognises an ``EngineModule`` and runs ``engine_local_epoch``:
+one ``load_batch`` + ``step`` per full batch, the per-batch losses read from the
+engine's on-device statistics (one small reduction per step, one host read per
+epoch).  A trailing partial batch is skipped (the engine's shapes are static;
+the count is reported as ``engine_local_epoch.last_skipped``).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from .static_mlp import OptimConfig, StaticMLPEngine
+from .straggler import StopLocalTraining
+
+
+class EngineModule(nn.Module):
+    def __init__(self, model: nn.Module, engine: StaticMLPEngine):
+        super().__init__()
+        self.module = model
+        self.__dict__["engine"] = engine   # not a submodule: state_dict keys stay the MLP's
+
+    def forward(self, x):
+        self.engine.sync()   # the previous step's weight all-gathers (sharded DP)
+        return self.module(x)
+
+    def state_dict(self, *args, **kwargs):
+        self.engine.gather_master()
+        return self.module.state_dict(*args, **kwargs)
+
+    def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
+        r = self.module.load_state_dict(state_dict, strict=strict)
+        self.engine.flat.refresh_shadow()
+        return r
+
+    def full_batches(self, loader) -> int:
+        return int(loader.num_samples) // self.engine.B if hasattr(loader, "num_samples") else len(loader)
+
+
+class EngineOptimizer(torch.optim.Optimizer):
+    def __init__(self, engine: StaticMLPEngine, params):
+        o = engine.optim
+        defaults = dict(lr=o.lr)
+        if o.name == "sgd":
+            defaults.update(momentum=o.momentum, dampening=o.dampening, weight_decay=o.weight_decay,
+                            nesterov=o.nesterov)
+        else:
+            defaults.update(betas=o.betas, eps=o.eps, weight_decay=o.weight_decay)
+        super().__init__(params, defaults)
+        self.__dict__["engine"] = engine
+
+    @torch.no_grad()
+    def step(self, closure=None):   # the engine's step runs the fused update
+        return closure() if closure is not None else None
+
+    def zero_grad(self, set_to_none: bool = True):   # the update kernels clear the gradients
+        pass
+
+    def sync_hyperparams(self):
+        self.engine.set_lr(self.param_groups[0]["lr"])
+
+    def state_dict(self):
+        sd = super().state_dict()
+        sd["ldnn_engine_state"] = self.engine.optimizer_state()
+        return sd
+
+    def load_state_dict(self, state_dict):
+        state_dict = dict(state_dict)
+        es = state_dict.pop("ldnn_engine_state", None)
+        super().load_state_dict(state_dict)
+        if es is not None:
+            self.engine.load_optimizer_state(es)
+        self.sync_hyperparams()
+
+
+def build_engine(model, batch_size: int, optimizer: str, lr: float, device, *, momentum: float = 0.9,
+                 weight_decay: float = 0.0, world_size: int = 1, process_group=None, use_graphs: bool = True,
+                 bucket_cap_elems: int = 8 << 20):
+    """(EngineModule, EngineOptimizer) for an ldnn MLP.  ``world_size`` > 1 = per-step
+    data parallelism inside the engine (reduce-scatter + sharded update + all-gather
+    over RCCL); 1 = an independent replica (the reference's global-epoch schedule
+    aggregates it through the Aggregator like any other model)."""
+    name = optimizer.lower()
+    oc = (OptimConfig("sgd", lr=lr, momentum=momentum, weight_decay=weight_decay) if name == "sgd"
+          else OptimConfig(name, lr=lr, weight_decay=weight_decay))
+    eng = StaticMLPEngine(model, batch_size, oc, device=device, world_size=world_size, process_group=process_group,
+                          use_graphs=use_graphs, bucket_cap_elems=bucket_cap_elems)
+    return EngineModule(model, eng), EngineOptimizer(eng, model.parameters())
+
+
+def engine_local_epoch(model: EngineModule, trainloader, optimizer, scheduler=None, *, cutoff=None,
+                       max_steps: int | None = None, step_scheduler: bool = True, check_comm=None,
+                       check_every: int = 50):
+    """train_local_epoch for an EngineModule: (mean loss, accuracy %, per-batch losses)."""
+    eng = model.engine
+    dev = eng.device
+    if isinstance(optimizer, EngineOptimizer):
+        optimizer.sync_hyperparams()
+    else:
+        eng.set_lr(optimizer.param_groups[0]["lr"])
+    model.train()
+    nb = model.full_batches(trainloader)
+    if max_steps is not None:
+        nb = min(nb, max_steps)
+    # cum[i] = running (loss sum, #correct) after step i -- one tiny reduction per step
+    cum = torch.zeros(max(nb, 1) + 1, 2, dtype=torch.float64, device=dev)
+    eng.reset_stats()
+    done, skipped = 0, 0
+    try:
+        for i, (x, y) in enumerate(trainloader):
+            if done >= nb:
+                skipped += y.numel() if y.numel() != eng.B else 0
+                break
+            if y.numel() != eng.B:   # static shapes: a partial batch cannot run
+                skipped += y.numel()
+                continue
+            eng.load_batch(x, y)
+            eng.step()
+            torch.sum(eng.stats, 0, dtype=torch.float64, out=cum[done + 1])
+            done += 1
+            if cutoff is not None:
+                cutoff.step(done - 1)
+            if check_comm is not None and done % check_every == 0:
+                check_comm.check_schedule(f"step {done}", dev if check_comm.device_collectives else None)
+    except StopLocalTraining:
+        if isinstance(optimizer, EngineOptimizer):
+            optimizer.step()   # a no-op; keeps torch's scheduler-order check quiet
+        if step_scheduler and scheduler is not None:
+            scheduler.step()
+        _finish(model, done, skipped)
+        raise
+    if done and isinstance(optimizer, EngineOptimizer):
+        optimizer.step()
+    if step_scheduler and scheduler is not None:
+        scheduler.step()
+    return _finish(model, done, skipped, cum)
+
+
+def _finish(model, done, skipped, cum=None):
+    engine_local_epoch.last_skipped = skipped
+    engine_local_epoch.last_samples = done * model.engine.B
+    if cum is None or done == 0:
+        return 0.0, 0.0, []
+    c = cum[: done + 1].cpu()   # the one host sync of the epoch
+    model.engine.sync()
+    per = (c[1:, 0] - c[:-1, 0]) / model.engine.B
+    losses = per.tolist()
+    correct = float(c[done, 1])
+    return float(per.mean()), 100.0 * correct / (done * model.engine.B), losses
+
+
+engine_local_epoch.last_skipped = 0
+engine_local_epoch.last_samples = 0

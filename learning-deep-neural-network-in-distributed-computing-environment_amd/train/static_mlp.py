@@ -251,8 +251,6 @@ class StaticMLPEngine:
         # (Splitting the 784-wide wgrad over batch slices with a batched hipBLASLt GEMM
         # was faster in isolation, 160 vs 192 us, scripts/bench_wgrad_split.py, but
         # neutral in the step, so the wgrads stay single GEMMs.)
-        if library_dgrad is None:
-            library_dgrad = bool(library_gemms)
         self._lib_dgrad = [bool(library_dgrad) and l > 0 and self.layers[l - 1].activation in ("relu", "sigmoid")
                            for l in range(L)]
         self._act_code = [None] + [{"relu": self.C.ACT_RELU, "sigmoid": self.C.ACT_SIGMOID}.get(
@@ -766,6 +764,31 @@ class StaticMLPEngine:
         for w, oseg in zip(works, self.opt_segments):
             w.wait()
             oseg()
+
+    @torch.no_grad()
+    def optimizer_state(self) -> dict:
+        """Whole optimizer state (momentum / Adam moments over the flat layout, Adam's
+        step count, lr), gathered from the shards first when the optimizer is sharded."""
+        self.gather_master()
+        st = {"name": self.optim.name, "lr": float(self.hp[0].item()), "step": float(self.hp[1].item()),
+              "numel": int(self.flat.numel)}
+        for k in ("mom", "exp_avg", "exp_avg_sq"):
+            t = getattr(self, k, None)
+            if t is not None:
+                st[k] = t.detach().cpu().clone()
+        return st
+
+    @torch.no_grad()
+    def load_optimizer_state(self, st: dict):
+        if st.get("name", self.optim.name) != self.optim.name or int(st.get("numel", self.flat.numel)) != self.flat.numel:
+            raise ValueError(f"optimizer state of {st.get('name')!r} / {st.get('numel')} elements does not fit "
+                             f"this engine ({self.optim.name!r} / {self.flat.numel})")
+        for k in ("mom", "exp_avg", "exp_avg_sq"):
+            t = getattr(self, k, None)
+            if t is not None and st.get(k) is not None:
+                t.copy_(st[k].to(t.device))
+        self.hp[0].fill_(float(st.get("lr", self.hp[0].item())))
+        self.hp[1].fill_(float(st.get("step", 0.0)))
 
     def reset_stats(self):
         self.stats.zero_()

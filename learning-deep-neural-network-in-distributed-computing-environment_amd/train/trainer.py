@@ -67,6 +67,13 @@ def train_local_epoch(model, trainloader, criterion, optimizer, device, schedule
     ``check_comm``: with per-step synchronisation, cross-check the ranks' collective
     schedules every ``check_every`` steps (Comm.check_schedule).
     """
+    from .engine_adapter import EngineModule, engine_local_epoch
+
+    if isinstance(model, EngineModule):   # the static MLP engine (train/engine_adapter.py)
+        out = engine_local_epoch(model, trainloader, optimizer, scheduler, cutoff=cutoff, max_steps=max_steps,
+                                 step_scheduler=step_scheduler, check_comm=check_comm, check_every=check_every)
+        train_local_epoch.last_samples = engine_local_epoch.last_samples
+        return out
     tm = timer or null_timer()
     model.train()
     dev = torch.device(device)
@@ -130,10 +137,12 @@ def train_local_epoch(model, trainloader, criterion, optimizer, device, schedule
         gs.flush_stats(stats)
     batch_losses = losses[:done].tolist()  # the one host sync of the epoch
     correct = stats[1].item()
+    train_local_epoch.last_samples = total
     train_loss = float(np.mean(batch_losses)) if batch_losses else 0.0
     return train_loss, 100.0 * correct / max(total, 1), batch_losses
 
 
+train_local_epoch.last_samples = 0
 
 
 def _graphed_step(model, criterion, optimizer, x, y, dp=None):
@@ -165,13 +174,17 @@ def _plain(x):
     return x
 
 
-def _pack(local_records, batch_losses_per_epoch, E_l, max_len, device):
-    """[n_done, (loss, acc, vloss, vacc) x E_l, (len, losses padded to max_len) x E_l]"""
-    buf = torch.full((1 + 4 * E_l + E_l * (1 + max_len),), -1.0, dtype=torch.float64)
+_HDR = 2   # [n local epochs done, samples trained this global epoch]
+
+
+def _pack(local_records, batch_losses_per_epoch, E_l, max_len, device, samples: int = 0):
+    """[n_done, samples, (loss, acc, vloss, vacc) x E_l, (len, losses padded to max_len) x E_l]"""
+    buf = torch.full((_HDR + 4 * E_l + E_l * (1 + max_len),), -1.0, dtype=torch.float64)
     buf[0] = len(local_records)
+    buf[1] = samples
     for e, rec in enumerate(local_records):
-        buf[1 + 4 * e: 5 + 4 * e] = torch.tensor(rec, dtype=torch.float64)
-    base = 1 + 4 * E_l
+        buf[_HDR + 4 * e: _HDR + 4 + 4 * e] = torch.tensor(rec, dtype=torch.float64)
+    base = _HDR + 4 * E_l
     for e, bl in enumerate(batch_losses_per_epoch):
         o = base + e * (1 + max_len)
         buf[o] = len(bl)
@@ -181,16 +194,17 @@ def _pack(local_records, batch_losses_per_epoch, E_l, max_len, device):
 
 
 def _unpack(buf, E_l, max_len):
+    """-> (records, batch losses per local epoch, samples)"""
     buf = buf.cpu()
     n = int(buf[0].item())
-    recs = [tuple(buf[1 + 4 * e: 5 + 4 * e].tolist()) for e in range(n)]
-    base = 1 + 4 * E_l
+    recs = [tuple(buf[_HDR + 4 * e: _HDR + 4 + 4 * e].tolist()) for e in range(n)]
+    base = _HDR + 4 * E_l
     bls = []
     for e in range(n):
         o = base + e * (1 + max_len)
         ln = int(buf[o].item())
         bls.append(buf[o + 1: o + 1 + ln].tolist())
-    return recs, bls
+    return recs, bls, int(buf[1].item())
 
 
 def train_global(model, trainloader, val_loader, trainset, valset, indices_train, indices_val, criterion, optimizer,
@@ -202,9 +216,16 @@ def train_global(model, trainloader, val_loader, trainset, valset, indices_train
                  seed: int = 0, legacy_gossip: bool = False, average_buffers: bool = False,
                  check_every: int = 20, progress: bool = True, logger=None, checkpointer=None,
                  start_global_epoch: int = 0, histories=None, dtype=torch.float32, verbose: bool = True,
-                 timer: PhaseTimer | None = None, graphs: bool = False, rng_state=None):
+                 timer: PhaseTimer | None = None, graphs: bool = False, rng_state=None,
+                 ref_samples_per_s: float | None = None):
     """``rng_state`` (resume): the re-partition RNG state saved in the checkpoint's
-    ``extra`` -- with it, a resumed run draws the same shards as an uninterrupted one."""
+    ``extra`` -- with it, a resumed run draws the same shards as an uninterrupted one.
+
+    Throughput reporting (``logger``): every global epoch logs the samples trained
+    by all ranks, whole-job samples/s over the epoch's wall time (training,
+    validation, exchange, aggregation, barrier) and, given ``ref_samples_per_s``
+    (one GPU's measured rate for the same model / batch), the data-parallel scaling
+    efficiency = samples/s / (N x ref)."""
     comm = comm or default_comm()
     tm = timer or null_timer()
     N = comm.world_size
@@ -239,12 +260,13 @@ def train_global(model, trainloader, val_loader, trainset, valset, indices_train
         t_start = time.perf_counter()
         cutoff.reset()
         max_steps = None
-        if sync_every == "step" and N > 1:
+        if sync_every == "step" and N > 1 or getattr(model, "engine", None) is not None and model.engine.distributed:
             # per-step collectives need the same number of steps on every rank
-            t = torch.tensor([float(len(trainloader))], device=dev)
+            nsteps = model.full_batches(trainloader) if hasattr(model, "full_batches") else len(trainloader)
+            t = torch.tensor([float(nsteps)], device=dev)
             comm.all_reduce(t, MIN)
             max_steps = int(t.item())
-        records, batch_losses = [], []
+        records, batch_losses, samples = [], [], 0
         for local_epoch in range(num_local_epochs):
             try:
                 loss, acc, bl = train_local_epoch(model, trainloader, criterion, optimizer, dev, scheduler, dp=dp,
@@ -258,6 +280,7 @@ def train_global(model, trainloader, val_loader, trainset, valset, indices_train
                     if scheduler is not None:
                         scheduler.step()
                 break
+            samples += train_local_epoch.last_samples
             with tm.phase("validate"):
                 val_loss, val_acc = validate(model, val_loader, criterion, dev)
             records.append((loss, acc, val_loss, val_acc))
@@ -273,9 +296,11 @@ def train_global(model, trainloader, val_loader, trainset, valset, indices_train
         lt = torch.tensor([float(max([len(b) for b in batch_losses] + [0]))], device=dev)
         comm.all_reduce(lt, MAX)
         max_len = int(lt.item())
-        packed = _pack(records, batch_losses, num_local_epochs, max_len, dev)
+        packed = _pack(records, batch_losses, num_local_epochs, max_len, dev, samples)
         gathered = comm.all_gather(packed) if N > 1 else [packed]
         per_rank = [_unpack(g, num_local_epochs, max_len) for g in gathered]
+        samples_per_rank = [pr[2] for pr in per_rank]
+        total_samples = sum(samples_per_rank)
         # every rank must have issued the same collectives so far (RankDivergenceError otherwise)
         comm.check_schedule(f"global epoch {global_epoch + 1}", dev if getattr(comm, "device_collectives", False)
                             else None)
@@ -344,7 +369,11 @@ def train_global(model, trainloader, val_loader, trainset, valset, indices_train
                        train_loss=H["global_train_losses"][-1], train_acc=H["global_train_accuracies"][-1],
                        val_loss=H["global_val_losses"][-1], val_acc=H["global_val_accuracies"][-1],
                        n_local_epochs_done=len(records), cut_by_time_limit=cutoff.cut,
-                       shard_size=len(indices_train))
+                       shard_size=len(indices_train), samples=total_samples,
+                       samples_per_s=total_samples / max(duration, 1e-12),
+                       train_samples_per_s_per_rank=[s_ / max(duration, 1e-12) for s_ in samples_per_rank],
+                       **({"scaling_efficiency": total_samples / max(duration, 1e-12) / (N * ref_samples_per_s)}
+                          if ref_samples_per_s else {}))
         if checkpointer is not None:
             checkpointer.save(global_epoch + 1, model, optimizer, scheduler, H,
                               extra=dict(indices_train=np.asarray(indices_train),
