@@ -75,7 +75,13 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--bucket_mb", type=float, default=32.0)
     p.add_argument("--grad_comm_dtype", choices=["fp32", "bf16"], default="fp32",
                    help="dtype of the per-step gradient all-reduce (bf16 halves the xGMI bytes)")
-    p.add_argument("--augment", action="store_true", help="GPU flip+crop augmentation")
+    p.add_argument("--augment", nargs="?", const="autoaugment", default="none",
+                   choices=["none", "autoaugment", "flipcrop", "autoaugment+flipcrop"],
+                   help="training-set augmentation in the native input kernel (augment.hip); bare --augment = "
+                        "AutoAugment(CIFAR10), the reference's train transform (BAR/dataloader.py:16)")
+    p.add_argument("--augment_val", action="store_true",
+                   help="also augment the validation shard: the reference's split of an augmented train set "
+                        "(BAR/dataloader.py:29-35) does that")
     p.add_argument("--out_dir", type=str, default="runs/latest")
     p.add_argument("--plots", type=str, default="Graphs", help="output folder of the six plots ('' to skip)")
     p.add_argument("--checkpoint_every", type=int, default=0)
@@ -187,7 +193,8 @@ def main(argv=None):
     dtype = torch.bfloat16 if (args.dtype == "bf16" and dev.type == "cuda") else torch.float32
     loaders = get_loaders(args.batch_size, world, rank, net, dev, fixed_ratio, dataset=dataset, comm=comm,
                           seed=args.seed, partition_rule=args.partition_rule, n_train=args.n_train,
-                          n_test=args.n_test, dtype=dtype, augment=args.augment, data_root=args.data_root)
+                          n_test=args.n_test, dtype=dtype, augment=args.augment, data_root=args.data_root,
+                          augment_val=args.augment_val)
     train_loader, val_loader, test_loader, trainset, valset, tr_idx, va_idx = loaders[:7]
     fixed_classes = loaders[7] if len(loaders) > 7 else None
 
@@ -221,7 +228,9 @@ def main(argv=None):
                 tr_idx, va_idx = ex["indices_train"].numpy(), ex["indices_val"].numpy()
                 train_loader = DeviceLoader(trainset, tr_idx, args.batch_size, dev, dtype=dtype, augment=args.augment,
                                             seed=loader_seed(args.seed, rank, start))
-                val_loader = DeviceLoader(valset, va_idx, args.batch_size, dev, dtype=dtype)
+                val_loader = DeviceLoader(valset, va_idx, args.batch_size, dev, dtype=dtype,
+                                          augment=args.augment if args.augment_val else False,
+                                          seed=(loader_seed(args.seed, rank, start) * 31 + 7) & 0x7FFFFFFF)
             if ex.get("fixed_classes") is not None:
                 fc = ex["fixed_classes"]
                 fixed_classes = fc.tolist() if torch.is_tensor(fc) else list(fc)

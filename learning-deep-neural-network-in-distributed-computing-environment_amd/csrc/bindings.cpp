@@ -4,6 +4,7 @@
 // tensors and launches on the CURRENT HIP stream, so the Python layer can
 // pre-allocate its buffers once and capture whole training steps in hipGraphs.
 #include <torch/extension.h>
+#include <pybind11/stl.h>
 #include <vector>
 #include <mutex>
 #include <map>
@@ -43,14 +44,24 @@ int64_t ld_of(const at::Tensor& t, const char* name) {
 
 // C = epi(A_op @ B_op)
 //   a: if a_kcontig, [M][K] else [K][M];  b: if b_kcontig, [N][K] else [K][N];  c: [M][N]
-void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, bool a_kcontig, bool b_kcontig,
+void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c_in, bool a_kcontig, bool b_kcontig,
           int64_t epi, const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& aux,
           const c10::optional<at::Tensor>& dbias, double beta, int64_t tile, int64_t splitk, bool direct_epi,
-          int64_t variant, const c10::optional<at::Tensor>& ws, const c10::optional<at::Tensor>& cnt) {
+          int64_t variant, const c10::optional<at::Tensor>& ws, const c10::optional<at::Tensor>& cnt,
+          const c10::optional<at::Tensor>& mask_out, const c10::optional<at::Tensor>& mask_in) {
   check_dev(a, at::kBFloat16, "a");
   check_dev(b, at::kBFloat16, "b");
-  TORCH_CHECK(c.is_cuda() && (c.scalar_type() == at::kBFloat16 || c.scalar_type() == at::kFloat),
+  TORCH_CHECK(c_in.is_cuda() && (c_in.scalar_type() == at::kBFloat16 || c_in.scalar_type() == at::kFloat),
               "c must be a bf16 or fp32 GPU tensor");
+  // a 3-D c = [splitk][M][N] receives the split-K partial products of the four-wave
+  // kernel, one slab per split (no in-launch combine; sum them with slab_sum)
+  const bool slabs = c_in.dim() == 3;
+  if (slabs) {
+    TORCH_CHECK(c_in.is_contiguous() && c_in.size(0) == splitk && splitk > 1 && epi == ldnn::EPI_NONE &&
+                    !ws.has_value() && !dbias.has_value() && beta == 0.0,
+                "gemm: slab output needs a dense [splitk][M][N] c, splitk > 1, EPI_NONE, no ws / dbias / beta");
+  }
+  const at::Tensor c = slabs ? c_in.select(0, 0) : c_in;
   const bool out_f32 = c.scalar_type() == at::kFloat;
   const int64_t lda = ld_of(a, "a"), ldb = ld_of(b, "b"), ldc = ld_of(c, "c");
   const int64_t M = a_kcontig ? a.size(0) : a.size(1);
@@ -79,11 +90,31 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, bool a_
   p.beta = (float)beta;
   p.direct_epi = direct_epi ? 1 : 0;
   p.variant = (int)variant;
-  if (epi == ldnn::EPI_BIAS || epi == ldnn::EPI_BIAS_RELU || epi == ldnn::EPI_BIAS_SIGMOID) {
+  if (epi == ldnn::EPI_BIAS || epi == ldnn::EPI_BIAS_RELU || epi == ldnn::EPI_BIAS_SIGMOID ||
+      epi == ldnn::EPI_BIAS_RELU_MASK) {
     TORCH_CHECK(bias.has_value(), "gemm: bias epilogue needs a bias tensor");
     check_dev(*bias, at::kFloat, "bias");
     TORCH_CHECK(bias->is_contiguous() && bias->numel() >= N && aligned16(bias->data_ptr()), "gemm: bad bias");
     p.bias = bias->data_ptr<float>();
+  }
+  bool force_q = slabs;
+  if (mask_out.has_value() || mask_in.has_value()) {
+    // ReLU bit masks (four-wave kernel): the forward writes them, the dgrad reads them
+    const at::Tensor& mk = mask_out.has_value() ? *mask_out : *mask_in;
+    check_dev(mk, at::kByte, "mask");
+    TORCH_CHECK(!(mask_out.has_value() && mask_in.has_value()), "gemm: mask_out and mask_in are exclusive");
+    TORCH_CHECK(mk.dim() == 2 && mk.size(0) == M && mk.size(1) * 8 >= N && mk.stride(1) == 1, "gemm: bad mask shape");
+    TORCH_CHECK(!out_f32 && (mask_out.has_value() ? epi == ldnn::EPI_BIAS_RELU : epi == ldnn::EPI_DRELU),
+                "gemm: mask_out goes with EPI_BIAS_RELU, mask_in with EPI_DRELU (bf16 out)");
+    p.ldmask = (int)mk.stride(0);
+    if (mask_out.has_value()) {
+      p.mask_out = mk.data_ptr<uint8_t>();
+      epi = ldnn::EPI_BIAS_RELU_MASK;
+    } else {
+      p.mask_in = mk.data_ptr<uint8_t>();
+      epi = ldnn::EPI_DRELU_MASK;
+    }
+    force_q = true;
   }
   if (epi == ldnn::EPI_DRELU || epi == ldnn::EPI_DSIGMOID) {
     TORCH_CHECK(aux.has_value(), "gemm: derivative epilogue needs the saved activation");
@@ -101,6 +132,17 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, bool a_
   const bool skinny_ok = a_kcontig && b_kcontig && !out_f32 && N <= 64 && !dbias.has_value() && beta == 0.0 &&
                          (epi == ldnn::EPI_NONE || epi == ldnn::EPI_BIAS || epi == ldnn::EPI_BIAS_RELU ||
                           epi == ldnn::EPI_BIAS_SIGMOID);
+  if (force_q) {  // masks / slab output exist only in the four-wave kernel
+    TORCH_CHECK(tile == 0 || tile == 256, "gemm: masks / slab output need tile 256");
+    tile = 256;
+    if ((variant & 255) < 32) variant = (variant & ~255) | 32;
+    p.variant = (int)variant;
+  }
+  if (slabs) {
+    p.splitk = (int)splitk;
+    p.c_split_stride = M * ldc;
+    TORCH_CHECK(c_in.stride(0) == M * ldc, "gemm: slab stride");
+  }
   if (tile == 0) tile = skinny_ok && K >= 256 ? 16 : ldnn::gemm_pick_tile(p.M, p.N, p.K, out_f32);
   TORCH_CHECK(tile == 16 || tile == 128 || tile == 256, "gemm: tile must be 0 (auto), 16 (skinny-N), 128 or 256");
   c10::hip::HIPGuardMasqueradingAsCUDA g(a.device());
@@ -117,7 +159,7 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, bool a_
   }
   if (tile == 256 && (variant & 255) >= 4) {  // ping-pong kernel (gemm_pp.hip) / four-wave kernel (gemm_q.hip, variant 32)
     const bool q = (variant & 255) >= 32;
-    if (splitk > 1) {
+    if (splitk > 1 && !slabs) {
       TORCH_CHECK(ws.has_value() && cnt.has_value(), "gemm: the pp kernel's split-K needs ws and cnt");
       check_dev(*ws, at::kFloat, "ws");
       check_dev(*cnt, at::kInt, "cnt");
@@ -540,6 +582,68 @@ void synth_labels(const at::Tensor& y, int64_t classes, int64_t seed) {
         "synth_labels");
 }
 
+// out[b] = normalise(augment(images[index[b]])), see augment.hip / data/autoaugment.py
+void augment_batch(const at::Tensor& images, const at::Tensor& index, const at::Tensor& out, const at::Tensor& a,
+                   const at::Tensor& b, int64_t seed, int64_t mode, int64_t pad, int64_t fixed_op, int64_t fixed_bin,
+                   int64_t fixed_sign, const std::vector<double>& mags, const std::vector<double>& rot_cos,
+                   const std::vector<double>& rot_sin, const std::vector<int64_t>& pol_op,
+                   const std::vector<double>& pol_prob, const std::vector<int64_t>& pol_bin,
+                   const std::vector<int64_t>& signed_op) {
+  check_dev(images, at::kByte, "images");
+  check_dev(index, at::kLong, "index");
+  check_dev(a, at::kFloat, "a");
+  check_dev(b, at::kFloat, "b");
+  TORCH_CHECK(out.is_cuda() && (out.scalar_type() == at::kBFloat16 || out.scalar_type() == at::kFloat),
+              "augment: out must be a bf16 or fp32 GPU tensor");
+  TORCH_CHECK(images.dim() == 4 && images.is_contiguous(), "augment: images must be a dense [N][C][H][W] tensor");
+  TORCH_CHECK(index.dim() == 1 && index.is_contiguous(), "augment: index must be a dense 1-D tensor");
+  const int64_t B = index.numel(), C = images.size(1), H = images.size(2), W = images.size(3);
+  TORCH_CHECK(out.is_contiguous() && out.dim() == 4 && out.size(0) == B && out.size(1) == C && out.size(2) == H &&
+              out.size(3) == W, "augment: out must be a dense [B][C][H][W] tensor");
+  TORCH_CHECK(a.numel() >= C && b.numel() >= C, "augment: a / b need one value per channel");
+  TORCH_CHECK(C >= 1 && C <= 3 && C * H * W <= ldnn::kAugMaxPixels, "augment: images of ", C, "x", H, "x", W,
+              " do not fit the LDS-resident kernel");
+  TORCH_CHECK((int64_t)mags.size() == ldnn::kAugOps * ldnn::kAugBins && (int64_t)rot_cos.size() == ldnn::kAugBins &&
+              (int64_t)rot_sin.size() == ldnn::kAugBins && (int64_t)signed_op.size() == ldnn::kAugOps,
+              "augment: bad magnitude tables");
+  TORCH_CHECK(pol_op.size() == pol_prob.size() && pol_op.size() == pol_bin.size() && pol_op.size() % 2 == 0 &&
+              (int64_t)pol_op.size() <= ldnn::kAugPolicySlots, "augment: bad policy table");
+  TORCH_CHECK(fixed_op < ldnn::kAugOps && fixed_bin < ldnn::kAugBins, "augment: bad fixed op");
+  ldnn::AugParams p{};
+  p.images = images.data_ptr<uint8_t>();
+  p.index = index.data_ptr<int64_t>();
+  p.out = out.data_ptr();
+  p.a = a.data_ptr<float>();
+  p.b = b.data_ptr<float>();
+  p.n_images = images.size(0);
+  p.B = (int)B;
+  p.C = (int)C;
+  p.H = (int)H;
+  p.W = (int)W;
+  p.seed = (uint64_t)seed;
+  p.mode = (int)mode;
+  p.pad = (int)pad;
+  p.fixed_op = (int)fixed_op;
+  p.fixed_bin = (int)fixed_bin;
+  p.fixed_sign = (int)fixed_sign;
+  p.n_policies = (int)(pol_op.size() / 2);
+  for (int o = 0; o < ldnn::kAugOps; ++o) {
+    for (int k = 0; k < ldnn::kAugBins; ++k) p.mags[o][k] = (float)mags[o * ldnn::kAugBins + k];
+    p.signed_op[o] = (int)signed_op[o];
+  }
+  for (int k = 0; k < ldnn::kAugBins; ++k) {
+    p.rot_cos[k] = (float)rot_cos[k];
+    p.rot_sin[k] = (float)rot_sin[k];
+  }
+  for (size_t i = 0; i < pol_op.size(); ++i) {
+    p.pol_op[i] = (int)pol_op[i];
+    p.pol_prob[i] = (float)pol_prob[i];
+    p.pol_bin[i] = (int)pol_bin[i];
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA g(images.device());
+  check(ldnn::augment_batch(p, out.scalar_type() == at::kFloat, cur_stream(images)), "augment_batch");
+}
+
 ldnn::ConvShape conv_shape(const at::Tensor& x, const at::Tensor& w, const at::Tensor& y, int64_t stride,
                            int64_t pad) {
   // x [N][H][W][C], w [K][R][S][C], y [N][P][Q][K]  (bf16, dense, C % 8 == K % 8 == 0)
@@ -871,7 +975,19 @@ PYBIND11_MODULE(_C, m) {
         py::arg("a_kcontig"), py::arg("b_kcontig"), py::arg("epi") = 0, py::arg("bias") = py::none(),
         py::arg("aux") = py::none(), py::arg("dbias") = py::none(), py::arg("beta") = 0.0,
         py::arg("tile") = 0, py::arg("splitk") = 0, py::arg("direct_epi") = false, py::arg("variant") = 0,
-        py::arg("ws") = py::none(), py::arg("cnt") = py::none());
+        py::arg("ws") = py::none(), py::arg("cnt") = py::none(), py::arg("mask_out") = py::none(),
+        py::arg("mask_in") = py::none());
+  m.def("slab_sum", [](const at::Tensor& ws, const at::Tensor& out, double beta) {
+        // out = sum over the leading dim of ws (+ beta * out); fp32, dense, same trailing size
+        check_dev(ws, at::kFloat, "ws");
+        check_dev(out, at::kFloat, "out");
+        TORCH_CHECK(ws.is_contiguous() && out.is_contiguous() && ws.dim() >= 2 && ws[0].numel() == out.numel() &&
+                        out.numel() % 4 == 0 && aligned16(ws.data_ptr()) && aligned16(out.data_ptr()),
+                    "slab_sum: ws must be a dense [splits][...] fp32 tensor matching the dense out");
+        c10::hip::HIPGuardMasqueradingAsCUDA g(ws.device());
+        check(ldnn::slab_sum(ws.data_ptr<float>(), out.data_ptr<float>(), out.numel() / 4, (int)ws.size(0),
+                             (float)beta, cur_stream(ws)), "slab_sum");
+      }, "sum of split-K partial slabs", py::arg("ws"), py::arg("out"), py::arg("beta") = 0.0);
   m.def("gemm_splitk_ws", [](int64_t M, int64_t N, int64_t splitk) {
         return std::make_pair((int64_t)(ldnn::gemm_splitk_ws_bytes((int)M, (int)N, (int)splitk) / 4),
                               (int64_t)ldnn::gemm_tiles128((int)M, (int)N));
@@ -958,4 +1074,5 @@ PYBIND11_MODULE(_C, m) {
         py::arg("beta") = 0.0);
   m.def("synth_normal", &synth_normal);
   m.def("synth_labels", &synth_labels);
+  m.def("augment_batch", &augment_batch, "gather + AutoAugment / flip+crop + normalise (augment.hip)");
 }

@@ -81,9 +81,9 @@ __device__ __forceinline__ bf16x8 read_frag(const char* lds, int rt, int kk, int
 template <int EPI>
 __device__ __forceinline__ float apply_epi(float v, float bias, float aux) {
   if constexpr (EPI == EPI_BIAS) return v + bias;
-  if constexpr (EPI == EPI_BIAS_RELU) return fmaxf(v + bias, 0.f);
+  if constexpr (EPI == EPI_BIAS_RELU || EPI == EPI_BIAS_RELU_MASK) return fmaxf(v + bias, 0.f);
   if constexpr (EPI == EPI_BIAS_SIGMOID) return 1.f / (1.f + __expf(-(v + bias)));
-  if constexpr (EPI == EPI_DRELU) return aux > 0.f ? v : 0.f;
+  if constexpr (EPI == EPI_DRELU || EPI == EPI_DRELU_MASK) return aux > 0.f ? v : 0.f;
   if constexpr (EPI == EPI_DSIGMOID) return v * aux * (1.f - aux);
   return v;
 }

@@ -18,6 +18,11 @@ enum Epilogue : int {
   // the weights instead of storing the gradient (GemmParams::opt)
   EPI_OPT_SGD = 6,
   EPI_OPT_ADAM = 7,
+  // four-wave kernel (gemm_q.hip) only: ReLU as a bit mask instead of the bf16
+  // activation -- the forward writes mask_out[m][n/8] (bit q = output (m, n+q) > 0)
+  // beside the activation; the dgrad reads mask_in instead of 16 B of aux per 8 columns
+  EPI_BIAS_RELU_MASK = 8,
+  EPI_DRELU_MASK = 9,
 };
 
 // Fused optimizer epilogue: gradient element (m, n) updates master[m*ldc + n].
@@ -48,6 +53,11 @@ struct GemmParams {
   float* ws;             // split-K combine: [tiles][splitk] slabs of 64 KiB (gemm_splitk_ws_bytes)
   int* cnt;              // split-K combine: [tiles] arrival counters, zero before the first launch
   OptEpi opt;            // EPI_OPT_*: the weights this gradient updates
+  int64_t c_split_stride;  // gemm_q split-K (gridDim.y > 1) without a combine: split y writes its
+                           // partial product to C + y * c_split_stride elements (then slab_sum)
+  uint8_t* mask_out;       // EPI_BIAS_RELU_MASK: [M][ldmask] ReLU bits
+  const uint8_t* mask_in;  // EPI_DRELU_MASK: [M][ldmask] ReLU bits of the saved activation
+  int ldmask;              // bytes per mask row (>= N / 8)
 };
 // Workspace of the in-launch split-K combine of a 128-tile GEMM (bytes; counters = tiles).
 size_t gemm_splitk_ws_bytes(int M, int N, int splitk);
@@ -268,5 +278,31 @@ int head_wgrad_splits(int B, int K);
 // ---- synthetic data (K20): deterministic device-side generator -----------
 hipError_t synth_normal_bf16(uint16_t* x, int64_t n, uint64_t seed, float stddev, hipStream_t s);
 hipError_t synth_labels(int64_t* y, int64_t n, int classes, uint64_t seed, hipStream_t s);
+
+// ---- input pipeline (K20): gather + AutoAugment / flip+crop + normalise -----
+constexpr int kAugOps = 15, kAugBins = 10, kAugPolicySlots = 64;
+struct AugParams {
+  const uint8_t* images;  // [n_images][C][H][W] uint8, resident dataset
+  const int64_t* index;   // [B] dataset rows of the batch
+  void* out;              // [B][C][H][W] bf16 or fp32: x * a[c] + b[c]
+  const float* a;         // [C]
+  const float* b;         // [C]
+  int64_t n_images;
+  int B, C, H, W;
+  uint64_t seed;          // batch seed (per-sample draws are counter hashes of it)
+  int mode;               // bit0 AutoAugment policy, bit1 random flip + padded crop
+  int pad;                // crop padding
+  int fixed_op, fixed_bin, fixed_sign;  // fixed_op >= 0: apply only this op (tests)
+  int n_policies;         // sub-policies (2 slots each)
+  float mags[kAugOps][kAugBins];
+  float rot_cos[kAugBins], rot_sin[kAugBins];
+  int pol_op[kAugPolicySlots];
+  float pol_prob[kAugPolicySlots];
+  int pol_bin[kAugPolicySlots];
+  int signed_op[kAugOps];
+};
+// largest C*H*W the LDS-resident kernel takes (two ping-pong images + scratch)
+constexpr int kAugMaxPixels = 28 * 1024;
+hipError_t augment_batch(const AugParams& p, bool out_f32, hipStream_t s);
 
 }  // namespace ldnn

@@ -183,7 +183,8 @@ __device__ __forceinline__ void epilogue_q(const GemmParams& p, floatx4 (&acc)[8
   const int n = nbase + c8 * 8;
   const bool nok = n < p.N;  // N % 8 == 0
   constexpr bool kAux = EPI == EPI_DRELU || EPI == EPI_DSIGMOID;
-  constexpr bool kBias = EPI == EPI_BIAS || EPI == EPI_BIAS_RELU || EPI == EPI_BIAS_SIGMOID;
+  constexpr bool kMaskIn = EPI == EPI_DRELU_MASK, kMaskOut = EPI == EPI_BIAS_RELU_MASK;
+  constexpr bool kBias = EPI == EPI_BIAS || EPI == EPI_BIAS_RELU || EPI == EPI_BIAS_SIGMOID || kMaskOut;
   float bias[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if constexpr (kBias) {
     if (nok) {
@@ -200,11 +201,19 @@ __device__ __forceinline__ void epilogue_q(const GemmParams& p, floatx4 (&acc)[8
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     u16x8 a8[16];
+    uint32_t mk[16];
     if constexpr (kAux) {
 #pragma unroll
       for (int it = 0; it < 16; ++it) {
         const int m = mbase + h * 64 + it * 4 + (lane >> 4);
         a8[it] = (nok && m < p.M) ? *reinterpret_cast<const u16x8*>(p.aux + (size_t)m * p.ldaux + n) : u16x8{};
+      }
+    }
+    if constexpr (kMaskIn) {  // one byte per row and 8 columns: 1/16 of the aux bytes
+#pragma unroll
+      for (int it = 0; it < 16; ++it) {
+        const int m = mbase + h * 64 + it * 4 + (lane >> 4);
+        mk[it] = (nok && m < p.M) ? (uint32_t)p.mask_in[(size_t)m * p.ldmask + (n >> 3)] : 0u;
       }
     }
     // lane holds C[m = i*16 + (l&15)][n = j*16 + 4*(l>>4) + r]
@@ -229,7 +238,7 @@ __device__ __forceinline__ void epilogue_q(const GemmParams& p, floatx4 (&acc)[8
       float o[8];
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
-        const float aux = kAux ? bf2f(a8[it][q]) : 0.f;
+        const float aux = kAux ? bf2f(a8[it][q]) : (kMaskIn ? (float)((mk[it] >> q) & 1u) : 0.f);
         o[q] = apply_epi<EPI>(q < 4 ? v0[q] : v1[q - 4], bias[q], aux);
       }
       if constexpr (OUT_F32) {
@@ -256,6 +265,12 @@ __device__ __forceinline__ void epilogue_q(const GemmParams& p, floatx4 (&acc)[8
         u16x8* dst = reinterpret_cast<u16x8*>(reinterpret_cast<bf16_t*>(p.C) + (size_t)m * p.ldc + n);
         if (p.variant & 4096) __builtin_nontemporal_store(ob, dst);
         else *dst = ob;
+        if constexpr (kMaskOut) {
+          uint32_t bits = 0;
+#pragma unroll
+          for (int q = 0; q < 8; ++q) bits |= (bf2f(ob[q]) > 0.f ? 1u : 0u) << q;
+          p.mask_out[(size_t)m * p.ldmask + (n >> 3)] = (uint8_t)bits;
+        }
       }
     }
     __builtin_amdgcn_wave_barrier();
@@ -372,12 +387,17 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(GemmParams p) {
   }
   mma_fence();
 
+  GemmParams pe = p;
   if (gridDim.y > 1) {
-    if (!splitk_combine<8, 8, kThreads>(acc, p.ws, p.cnt, blockIdx.x, gridDim.y, blockIdx.y, smem)) return;
+    if (p.c_split_stride > 0) {  // partial products to separate slabs (summed by slab_sum)
+      pe.C = reinterpret_cast<char*>(p.C) + (size_t)blockIdx.y * (size_t)p.c_split_stride * (OUT_F32 ? 4u : 2u);
+    } else if (!splitk_combine<8, 8, kThreads>(acc, p.ws, p.cnt, blockIdx.x, gridDim.y, blockIdx.y, smem)) {
+      return;
+    }
   }
   if constexpr (EPI != EPI_OPT_SGD && EPI != EPI_OPT_ADAM) {
     barrier();  // every wave is done with the operand stages: LDS belongs to the epilogue
-    epilogue_q<EPI, OUT_F32>(p, acc, smem, wid, m0 + wm * 128, n0 + wn * 128, lane);
+    epilogue_q<EPI, OUT_F32>(pe, acc, smem, wid, m0 + wm * 128, n0 + wn * 128, lane);
   } else {
     epilogue<EPI, OUT_F32, 8, 8>(p, acc, m0 + wm * 128, n0 + wn * 128, lane);
   }
@@ -411,6 +431,18 @@ hipError_t dispatch_epi(const GemmParams& p, int epi, hipStream_t s) {
     LDNN_Q_CASE(EPI_DRELU)
     LDNN_Q_CASE(EPI_DSIGMOID)
 #undef LDNN_Q_CASE
+    case EPI_BIAS_RELU_MASK:
+      if constexpr (!OUT_F32) {
+        gemm_kernel<A_KC, B_KC, EPI_BIAS_RELU_MASK, false><<<grid, block, 0, s>>>(p);
+        break;
+      }
+      return hipErrorInvalidValue;
+    case EPI_DRELU_MASK:
+      if constexpr (!OUT_F32) {
+        gemm_kernel<A_KC, B_KC, EPI_DRELU_MASK, false><<<grid, block, 0, s>>>(p);
+        break;
+      }
+      return hipErrorInvalidValue;
     case EPI_OPT_SGD:
       if constexpr (OUT_F32) {
         gemm_kernel<A_KC, B_KC, EPI_OPT_SGD, true><<<grid, block, 0, s>>>(p);
@@ -442,7 +474,10 @@ hipError_t gemm_q(const GemmParams& p, bool a_kc, bool b_kc, int epi, bool out_f
   const size_t abytes = (size_t)(a_kc ? p.M : p.K) * p.lda * 2;
   const size_t bbytes = (size_t)(b_kc ? p.N : p.K) * p.ldb * 2;
   if (abytes >= kOOBLimit || bbytes >= kOOBLimit) return hipErrorInvalidValue;
-  if (p.splitk > 1 && (p.ws == nullptr || p.cnt == nullptr)) return hipErrorInvalidValue;
+  if (p.splitk > 1 && p.c_split_stride == 0 && (p.ws == nullptr || p.cnt == nullptr)) return hipErrorInvalidValue;
+  if ((epi == EPI_BIAS_RELU_MASK && p.mask_out == nullptr) || (epi == EPI_DRELU_MASK && p.mask_in == nullptr) ||
+      ((epi == EPI_BIAS_RELU_MASK || epi == EPI_DRELU_MASK) && (p.ldmask * 8 < p.N || p.N % 8 != 0)))
+    return hipErrorInvalidValue;
   if (a_kc) {
     if (b_kc) return out_f32 ? kq::dispatch_epi<true, true, true>(p, epi, s) : kq::dispatch_epi<true, true, false>(p, epi, s);
     return out_f32 ? kq::dispatch_epi<true, false, true>(p, epi, s) : kq::dispatch_epi<true, false, false>(p, epi, s);

@@ -16,6 +16,8 @@ import time
 import numpy as np
 import torch
 
+from ..ops import _ext
+from . import autoaugment as AA
 from . import partition as P
 from .datasets import ArrayDataset, build_dataset, channel_stats, random_split_indices
 
@@ -34,25 +36,48 @@ def _resident(t: torch.Tensor, device) -> torch.Tensor:
     return r
 
 
+AUGMENT_MODES = {"none": 0, "autoaugment": AA.MODE_AUTOAUGMENT, "flipcrop": AA.MODE_FLIP_CROP,
+                 "autoaugment+flipcrop": AA.MODE_AUTOAUGMENT | AA.MODE_FLIP_CROP}
+
+
+def augment_mode(augment) -> int:
+    """False/None/'none' -> 0; True/'autoaugment' -> AutoAugment(CIFAR10) (the reference's
+    train transform, BAR/dataloader.py:16); 'flipcrop'; 'autoaugment+flipcrop'."""
+    if augment is None or augment is False:
+        return 0
+    if augment is True:
+        return AA.MODE_AUTOAUGMENT
+    if augment not in AUGMENT_MODES:
+        raise ValueError(f"augment must be one of {sorted(AUGMENT_MODES)}, got {augment!r}")
+    return AUGMENT_MODES[augment]
+
+
 class DeviceLoader:
     """Batches of (normalised image, label) gathered on the device.
 
     ``indices`` select rows of ``dataset`` (a shard); iteration order is the
     shard order (shuffle=False, as in the reference) or a seeded per-epoch
-    permutation."""
+    permutation.  On a GPU with a uint8 dataset each batch is ONE native launch
+    (augment.hip): gather + optional AutoAugment / flip+crop + normalise + cast.
+    The augmentation draws are counter hashes of (seed, epoch, batch, sample):
+    reproducible, and identical on the CPU path (data/autoaugment.py)."""
 
     def __init__(self, dataset: ArrayDataset, indices, batch_size: int, device, shuffle: bool = False,
                  drop_last: bool = False, seed: int = 0, mean=None, std=None, dtype=torch.float32,
-                 augment: bool = False):
+                 augment=False, pad: int = 4):
         self.dataset = dataset
         self.device = torch.device(device)
         self.batch_size = int(batch_size)
         self.shuffle, self.drop_last = shuffle, drop_last
         self.dtype = dtype
         self.augment = augment
+        self.mode = augment_mode(augment)
+        self.pad = int(pad)
         self.images = _resident(dataset.images, self.device)
         self.labels = _resident(dataset.labels, self.device)
         idx = np.arange(len(dataset)) if indices is None else np.asarray(indices, dtype=np.int64)
+        if idx.size and (idx.min() < 0 or idx.max() >= len(dataset)):
+            raise IndexError(f"shard indices outside [0, {len(dataset)})")
         self.indices_np = idx
         self.indices = torch.as_tensor(idx, dtype=torch.long, device=self.device)
         mean = mean if mean is not None else dataset.mean
@@ -66,8 +91,12 @@ class DeviceLoader:
         self._b = (-m / s).view(1, c, 1, 1)
         self._gen = torch.Generator().manual_seed(seed)
         self.seed = int(seed)
-        self._aug_gen = None
         self.epoch = 0
+        self._native = (self.device.type == "cuda" and self.images.dtype == torch.uint8
+                        and self.dtype in (torch.bfloat16, torch.float32) and _ext.use_native(self.images)
+                        and c * dataset.images.shape[2] * dataset.images.shape[3] <= AA_MAX_PIXELS)
+        if self.mode and self.images.dtype != torch.uint8:
+            raise ValueError("augmentation needs a uint8 dataset")
 
     def __len__(self):
         n = len(self.indices_np)
@@ -78,13 +107,18 @@ class DeviceLoader:
         n = len(self.indices_np)
         return (n // self.batch_size) * self.batch_size if self.drop_last else n
 
-    def _batch(self, idx: torch.Tensor):
-        x = self.images.index_select(0, idx)
+    def _batch(self, idx: torch.Tensor, seed: int = 0):
+        if self._native:
+            _, C, H, W = self.images.shape
+            out = torch.empty(idx.numel(), C, H, W, dtype=self.dtype, device=self.device)
+            augment_native(self.images, idx, out, self._a.reshape(-1), self._b.reshape(-1), seed, self.mode, self.pad)
+            return out, self.labels.index_select(0, idx)
+        if self.mode:   # CPU (or non-native) path: the kernel's NumPy reference, same draws
+            raw = AA.augment_reference(self.images.cpu().numpy(), idx.cpu().numpy(), seed, self.mode, self.pad)
+            x = torch.from_numpy(raw).to(self.device)
+        else:
+            x = self.images.index_select(0, idx)
         x = torch.addcmul(self._b, x.to(torch.float32), self._a)
-        if self.augment:
-            if self._aug_gen is None:
-                self._aug_gen = torch.Generator(device=self.device).manual_seed(self.seed + 1)
-            x = _flip_crop(x, self._aug_gen)
         return x.to(self.dtype), self.labels.index_select(0, idx)
 
     def __iter__(self):
@@ -92,26 +126,39 @@ class DeviceLoader:
         if self.shuffle:
             perm = torch.randperm(len(order), generator=self._gen).to(self.device)
             order = order[perm]
+        epoch = self.epoch
         self.epoch += 1
         bs = self.batch_size
         n = len(order)
         end = (n // bs) * bs if self.drop_last else n
-        for s in range(0, end, bs):
-            yield self._batch(order[s: s + bs])
+        for k, s in enumerate(range(0, end, bs)):
+            yield self._batch(order[s: s + bs], AA.batch_seed(self.seed, epoch, k) if self.mode else 0)
 
 
-def _flip_crop(x: torch.Tensor, gen: torch.Generator | None = None, pad: int = 4) -> torch.Tensor:
-    """GPU random horizontal flip + padded random crop, an independent flip and crop
-    offset per sample drawn from the loader's seeded generator."""
-    B, C, H, W = x.shape
-    flip = torch.rand(B, device=x.device, generator=gen) < 0.5
-    x = torch.where(flip.view(B, 1, 1, 1), x.flip(3), x)
-    xp = torch.nn.functional.pad(x, (pad, pad, pad, pad))
-    off = torch.randint(0, 2 * pad + 1, (2, B), device=x.device, generator=gen)
-    iy = (off[0].view(B, 1, 1, 1) + torch.arange(H, device=x.device).view(1, 1, H, 1)).expand(B, C, H, W + 2 * pad)
-    xr = xp.gather(2, iy)
-    ix = (off[1].view(B, 1, 1, 1) + torch.arange(W, device=x.device).view(1, 1, 1, W)).expand(B, C, H, W)
-    return xr.gather(3, ix)
+AA_MAX_PIXELS = 28 * 1024   # csrc kAugMaxPixels
+_AA_TABLES: dict = {}
+
+
+def _aa_tables(H: int, W: int):
+    t = _AA_TABLES.get((H, W))
+    if t is None:
+        mags = AA.magnitude_table(H, W)
+        rc, rs = zip(*[AA.rotation_cs(v) for v in mags[AA.OP["Rotate"]]])
+        ops, prob, bins, signed = AA.policy_table()
+        t = ([float(v) for v in mags.reshape(-1)], [float(v) for v in rc], [float(v) for v in rs],
+             [int(v) for v in ops], [float(v) for v in prob], [int(v) for v in bins], [int(v) for v in signed])
+        _AA_TABLES[(H, W)] = t
+    return t
+
+
+def augment_native(images, idx, out, a, b, seed: int, mode: int, pad: int = 4, fixed=None):
+    """One augment.hip launch: out = normalise(augment(images[idx])).  ``fixed`` =
+    (op id, magnitude bin, sign bit) applies just that op (kernel test hook)."""
+    H, W = images.shape[2], images.shape[3]
+    fo, fb, fs = fixed if fixed is not None else (-1, 0, 0)
+    _ext.C().augment_batch(images, idx, out, a.contiguous(), b.contiguous(), int(seed), int(mode), int(pad),
+                           int(fo), int(fb), int(fs), *_aa_tables(H, W))
+    return out
 
 
 # ---------------------------------------------------------------- probe (A12)
@@ -158,7 +205,7 @@ def estimate_epoch_duration(trainloader, world_size, model, device, num_batches:
 def get_loaders(batch_size, world_size, rank, model, device, fixed_ratio=None, *, dataset: str = "cifar10",
                 comm=None, seed: int = 0, val_fraction: float = 0.2, partition_rule: str = "reference_duration",
                 probe_batches: int = 10, n_train: int | None = None, n_test: int | None = None,
-                dtype=torch.float32, augment: bool = False, data_root: str = "data"):
+                dtype=torch.float32, augment=False, data_root: str = "data", augment_val: bool = False):
     """Build (train, val, test) loaders for this rank (BAR/dataloader.py:9-51).
 
     Returns the reference's 7-tuple (IID) or 8-tuple (+fixed_classes) when
@@ -189,7 +236,8 @@ def get_loaders(batch_size, world_size, rank, model, device, fixed_ratio=None, *
         val_indices, _ = P.skewed_partition(valset.targets, shares, rank, fixed_ratio, valset.num_classes, rng)
     train_loader = DeviceLoader(trainset, train_indices, batch_size, device, dtype=dtype, augment=augment,
                                 seed=(seed * 1_000_003 + rank * 10_007) & 0x7FFFFFFF)
-    val_loader = DeviceLoader(valset, val_indices, batch_size, device, dtype=dtype)
+    val_loader = DeviceLoader(valset, val_indices, batch_size, device, dtype=dtype,
+                              augment=augment if augment_val else False, seed=(seed * 7 + rank * 13 + 5) & 0x7FFFFFFF)
     test_loader = DeviceLoader(testset, None, batch_size, device, dtype=dtype)
     out = (train_loader, val_loader, test_loader, trainset, valset, train_indices, val_indices)
     return out + (fixed,) if fixed_ratio is not None else out
@@ -197,7 +245,8 @@ def get_loaders(batch_size, world_size, rank, model, device, fixed_ratio=None, *
 
 def get_subset_loaders(trainset, valset, train_indices, val_indices, batch_size, prev_fraction, next_fraction,
                        share, device, rng: np.random.Generator, replace: bool = False, fixed_classes=None,
-                       fixed_ratio=None, dtype=torch.float32, augment: bool = False, loader_seed: int = 0):
+                       fixed_ratio=None, dtype=torch.float32, augment=False, loader_seed: int = 0,
+                       augment_val: bool = False):
     """Re-partition for the next global epoch (BAR/dataloader.py:107-117)."""
     kw = {}
     if fixed_classes is not None:
@@ -207,4 +256,5 @@ def get_subset_loaders(trainset, valset, train_indices, val_indices, batch_size,
     va = P.next_partition(len(valset), val_indices, share, prev_fraction, next_fraction, rng, replace,
                           labels=valset.targets if kw else None, **kw)
     return (DeviceLoader(trainset, tr, batch_size, device, dtype=dtype, augment=augment, seed=loader_seed),
-            DeviceLoader(valset, va, batch_size, device, dtype=dtype), tr, va)
+            DeviceLoader(valset, va, batch_size, device, dtype=dtype, augment=augment if augment_val else False,
+                         seed=(loader_seed * 31 + 7) & 0x7FFFFFFF), tr, va)

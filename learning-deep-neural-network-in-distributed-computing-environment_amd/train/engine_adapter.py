@@ -53,6 +53,11 @@ class EngineModule(nn.Module):
         self.engine.flat.refresh_shadow()
         return r
 
+    def prepare_collective_read(self):
+        """Collective (every rank): make the sharded master / optimizer state whole, so a
+        rank-0-only state_dict() / checkpoint afterwards issues no collective."""
+        self.engine.gather_master()
+
     def full_batches(self, loader) -> int:
         return int(loader.num_samples) // self.engine.B if hasattr(loader, "num_samples") else len(loader)
 

@@ -100,7 +100,7 @@ class StaticMLPEngine:
                  fuse_optimizer: bool | None = None, library_gemms: bool | None = None,
                  fuse_head_dgrad: bool | None = None, early_optimizer: bool | None = None,
                  library_dgrad: bool | None = None, concurrent_wgrad: bool = False, pad_input: bool = False,
-                 head_dgrad_mode: int = -1):
+                 head_dgrad_mode: int = -1, relu_masks: bool = True, wgrad_slabs: bool = True):
         from ..models.mlp import MLP
 
         if not isinstance(model, MLP):
@@ -278,10 +278,20 @@ class StaticMLPEngine:
             self.W0p = torch.zeros(self.W[0].shape[0], Kp, dtype=bf, device=dev)
             self.dW0p = torch.zeros(self.W[0].shape[0], Kp, dtype=torch.float32, device=dev)
         self.bias_bf16 = [f.shadow_storage(l.bias) for l in self.layers]
-        self._wgrad_splitk, self._wgrad_ws = [], []
+        # relu_masks: a ReLU hidden layer's forward (four-wave kernel) also writes a bit
+        # mask of its output (1 bit per activation, 1/16 of the bf16 bytes), and the dgrad
+        # that needs relu'(h_l) reads the mask instead of h_l -- the dgrad epilogue's
+        # 128 MB aux stream at batch 16384 becomes 8 MB (gemm_q.hip EPI_*_MASK).
+        self.mask = [None] * (L + 1)
+        for l in range(1, L):
+            if (relu_masks and self.layers[l - 1].activation == "relu" and not self._lib_fwd[l - 1]
+                    and not self._lib_dgrad[l] and not (self.use_head and l == L - 1 and fuse_head_dgrad)):
+                self.mask[l] = torch.zeros(B, (npad[l - 1] + 7) // 8, dtype=torch.uint8, device=dev)
+        self._wgrad_splitk, self._wgrad_ws, self._wgrad_slab = [], [], []
         for l, layer in enumerate(self.layers):
             M, N = self.dW[l].shape
             self._wgrad_ws.append(None)
+            self._wgrad_slab.append(None)
             if self.use_head and l == L - 1:
                 self._wgrad_splitk.append(self.C.head_wgrad_splits(B, N))
                 continue
@@ -294,6 +304,14 @@ class StaticMLPEngine:
                 # layer: 64 tiles): the four-wave kernel splits the batch reduction over
                 # gridDim.y and combines the slices in the launch (deterministic, overwrites)
                 sk = max(2, min(8, round(256 / t256)))
+                if wgrad_slabs:
+                    # the splits write separate fp32 slabs and one chip-wide slab_sum adds them:
+                    # measured on MI355X (4096 x 784 x 16384) the in-launch combine, where the
+                    # last-arriving workgroup of a tile re-reads every split's 256 KiB alone,
+                    # cost ~90 of the kernel's 177 us
+                    self._wgrad_slab[l] = torch.empty(sk, M, N, dtype=torch.float32, device=self.device)
+                    self._wgrad_splitk.append(sk)
+                    continue
                 ne, nc = self.C.gemm_pp_ws(M, N, sk)
                 self._wgrad_ws[l] = (torch.empty(ne, dtype=torch.float32, device=self.device),
                                      torch.zeros(nc, dtype=torch.int32, device=self.device), 256)
@@ -311,7 +329,7 @@ class StaticMLPEngine:
             self._wgrad_splitk.append(sk if tile == 128 else 1)
         ranges = [(self._bias_begin, f.numel)]
         for l in range(L):
-            if self._wgrad_splitk[l] > 1 and self._wgrad_ws[l] is None:  # atomic accumulation
+            if self._wgrad_splitk[l] > 1 and self._wgrad_ws[l] is None and self._wgrad_slab[l] is None:  # atomics
                 seg = f.seg(self.layers[l].weight)
                 ranges.append((seg.offset, seg.offset + seg.storage_numel))
         merged = []
@@ -377,6 +395,7 @@ class StaticMLPEngine:
         self.side = (torch.cuda.Stream(device=self.device)
                      if (overlap_optimizer or self.early_optimizer or self.concurrent_wgrad) else None)
         self._pending_gather = {}
+        self._master_whole = True
         if self.shard:
             self.gshard = [torch.zeros((e - b) // self.world, dtype=torch.float32, device=dev)
                            for b, e, _ in self.buckets]
@@ -417,6 +436,10 @@ class StaticMLPEngine:
                 self.dW[0].copy_(self.dW0p[:, : self.layers[0].in_features])
                 return
             torch.mm(self.dz[l + 1].t(), self.h[l], out_dtype=torch.float32, out=self.dW[l])
+            return
+        if self._wgrad_slab[l] is not None:   # split-K into slabs + one summing pass, overwrites
+            self.C.gemm(self.dz[l + 1], self.h[l], self._wgrad_slab[l], False, False, tile=256, splitk=sk)
+            self.C.slab_sum(self._wgrad_slab[l], self.dW[l])
             return
         if self._wgrad_ws[l] is not None:   # in-launch split-K combine, overwrites the gradient
             ws, cnt, tile = self._wgrad_ws[l]
@@ -465,6 +488,10 @@ class StaticMLPEngine:
         if self._lib_dgrad[l]:
             torch.mm(self.dz[l + 1], self.W[l], out=self.dz[l])
             self.C.act_bwd_colsum(self.dz[l], self.h[l], self.dz[l], self.db[l - 1], self._act_code[l], True)
+            return
+        if self.mask[l] is not None:
+            self.C.gemm(self.dz[l + 1], self.W[l], self.dz[l], True, False, self.C.EPI_DRELU, dbias=self.db[l - 1],
+                        mask_in=self.mask[l])
             return
         self.C.gemm(self.dz[l + 1], self.W[l], self.dz[l], True, False, self._dgrad_epi[l], aux=self.h[l],
                     dbias=self.db[l - 1])
@@ -650,6 +677,10 @@ class StaticMLPEngine:
             else:
                 torch.addmm(self.bias_bf16[l], self.h[l], W.t(), out=self.h[l + 1])
             return
+        if self.mask[l + 1] is not None:
+            C.gemm(self.h[l], self.W[l], self.h[l + 1], True, True, C.EPI_BIAS_RELU, bias=self.bias[l],
+                   mask_out=self.mask[l + 1])
+            return
         C.gemm(self.h[l], self.W[l], self.h[l + 1], True, True, self._fwd_epi[l], bias=self.bias[l])
 
     # --------------------------------------------------------------------- API
@@ -693,9 +724,11 @@ class StaticMLPEngine:
     @torch.no_grad()
     def gather_master(self):
         """Make every rank's fp32 master (and optimizer state) whole again after sharded
-        steps -- needed before state_dict / checkpoint / evaluation of model.parameters()."""
-        if not self.shard:
+        steps -- needed before state_dict / checkpoint / evaluation of model.parameters().
+        A collective: every rank calls it (a no-op until the next step once done)."""
+        if not self.shard or self._master_whole:
             return
+        self._master_whole = True
         self.sync()
         bufs = [self.flat.master] + [t for t in (self.mom, getattr(self, "exp_avg", None),
                                                    getattr(self, "exp_avg_sq", None)) if t is not None]
@@ -741,6 +774,7 @@ class StaticMLPEngine:
 
     def step(self):
         """One full training step on the batch currently in (self.x, self.labels)."""
+        self._master_whole = False
         if not self.distributed:
             self.segments[0]()
             return

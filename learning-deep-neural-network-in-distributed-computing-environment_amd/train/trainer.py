@@ -337,6 +337,9 @@ def train_global(model, trainloader, val_loader, trainset, valset, indices_train
         H["global_val_accuracies"].append(float(means[3]))
 
         # ---- end-of-global-epoch aggregation (reference schedule, A27)
+        prep = getattr(model, "prepare_collective_read", None)
+        if prep is not None:   # e.g. a sharded static engine: whole master on every rank
+            prep()
         if sync_every == "global_epoch" or (sync_every == "step" and aggregation_by == "weights"):
             with tm.phase("aggregate"):
                 aggregator(model)
@@ -362,7 +365,7 @@ def train_global(model, trainloader, val_loader, trainset, valset, indices_train
             trainloader, val_loader, indices_train, indices_val = get_subset_loaders(
                 trainset, valset, indices_train, indices_val, batch_size, prev_fraction, next_fraction, share, dev,
                 rng, replace, fixed_classes, fixed_ratio, dtype=dtype,
-                augment=getattr(trainloader, "augment", False),
+                augment=getattr(trainloader, "augment", False), augment_val=bool(getattr(val_loader, "mode", 0)),
                 loader_seed=loader_seed(seed, rank, global_epoch + 1))
         if logger is not None:
             logger.log(kind="global_epoch", global_epoch=global_epoch + 1, duration_s=duration,

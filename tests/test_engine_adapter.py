@@ -130,7 +130,7 @@ def test_cli_static_engine_gloo_two_ranks_resume(tmp_path):
     h = full["histories"]
     assert len(h) == 12 and len(h[4]) == 3 and all(v == v for v in h[4])
     assert h[4][-1] < h[4][0]   # it learns
-    recs = [json.loads(l) for l in open(tmp_path / "full" / "metrics.jsonl")]
+    recs = [json.loads(l) for l in open(tmp_path / "full" / "metrics.rank0.jsonl")]
     cfg = next(r for r in recs if r.get("kind") == "config")
     assert cfg["resolved_engine"] == "static"
     ge = [r for r in recs if r.get("kind") == "global_epoch"]

@@ -171,3 +171,48 @@ def test_auto_picks_q_for_long_k():
     C().gemm(a, b, c0, True, True)
     C().gemm(a, b, c1, True, True, tile=256, variant=32)
     assert torch.equal(c0, c1)
+
+
+@pytest.mark.parametrize("M,N,K", [(520, 776, 784), (1024, 512, 1040)])
+def test_relu_mask_forward_and_dgrad(M, N, K):
+    """EPI_BIAS_RELU_MASK writes the bf16 output AND mask bits (bit q of byte [m][n/8] =
+    out[m][n+q] > 0); EPI_DRELU_MASK reading those bits equals EPI_DRELU reading the bf16
+    activation (same accumulators, same derivative, same bias-gradient sums)."""
+    c = C()
+    x, w = _ops(M, N, K, True, True, seed=3)
+    bias = torch.randn(N, device="cuda")
+    h_ref = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    h = torch.empty_like(h_ref)
+    mask = torch.full((M, (N + 7) // 8), 0xAA, dtype=torch.uint8, device="cuda")
+    c.gemm(x, w, h_ref, True, True, c.EPI_BIAS_RELU, bias=bias, tile=256, variant=32)
+    c.gemm(x, w, h, True, True, c.EPI_BIAS_RELU, bias=bias, mask_out=mask)
+    assert torch.equal(h, h_ref)
+    bits = ((h.float() > 0).view(M, -1, 8).to(torch.int32) << torch.arange(8, device="cuda")).sum(-1)
+    assert torch.equal(mask[:, : N // 8].to(torch.int32), bits)
+    # dgrad: dz_prev = (dz W2) * relu'(h), K2 = 640 outputs of the next layer
+    dz, w2 = _ops(M, N, 640, True, False, seed=4)   # dz [M][640], w2 [640][N] (k-strided B)
+    out_a, out_m = (torch.empty(M, N, device="cuda", dtype=torch.bfloat16) for _ in range(2))
+    db_a, db_m = torch.zeros(N, device="cuda"), torch.zeros(N, device="cuda")
+    c.gemm(dz, w2, out_a, True, False, c.EPI_DRELU, aux=h, dbias=db_a, tile=256, variant=32)
+    c.gemm(dz, w2, out_m, True, False, c.EPI_DRELU, dbias=db_m, mask_in=mask)
+    assert torch.equal(out_a, out_m)
+    torch.testing.assert_close(db_m, db_a, rtol=1e-5, atol=1e-3)
+    ref = (dz.float() @ w2.float()) * (h.float() > 0)
+    torch.testing.assert_close(out_m.float(), ref, rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("sk", [2, 4])
+def test_split_slabs_plus_slab_sum(sk):
+    """Split-K partial products into [sk][M][N] slabs (no in-launch combine) + slab_sum."""
+    c = C()
+    M, N, K = 1032, 784, 4096
+    a, b = _ops(M, N, K, False, False, seed=5)
+    slabs = torch.full((sk, M, N), float("nan"), device="cuda")
+    out = torch.empty(M, N, device="cuda")
+    c.gemm(a, b, slabs, False, False, tile=256, splitk=sk)
+    c.slab_sum(slabs, out)
+    ref = _ref(a, b, False, False)
+    torch.testing.assert_close(out, ref, rtol=1e-4, atol=1e-3)
+    one = torch.empty(M, N, device="cuda")
+    c.gemm(a, b, one, False, False, tile=256, variant=32)
+    torch.testing.assert_close(out, one, rtol=1e-5, atol=1e-4)
