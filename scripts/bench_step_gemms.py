@@ -61,6 +61,7 @@ def main():
     out = torch.empty(B, H, device="cuda", dtype=torch.bfloat16)
     dW0, dW1 = torch.empty(H, K0, device="cuda"), torch.empty(H, H, device="cuda")
     db = torch.zeros(H, device="cuda")
+    mask = torch.zeros(B, H // 8, dtype=torch.uint8, device="cuda")
     fl = lambda M, N, K: 2.0 * M * N * K  # noqa: E731
 
     def rec(name, flops, d):
@@ -76,6 +77,8 @@ def main():
             "auto": lambda: C.gemm(x, W0, out, True, True, C.EPI_BIAS_RELU, bias=b),
             "q": lambda: C.gemm(x, W0, out, True, True, C.EPI_BIAS_RELU, bias=b, tile=256, variant=32),
             "k128": lambda: C.gemm(x, W0, out, True, True, C.EPI_BIAS_RELU, bias=b, tile=128),
+            "k256": lambda: C.gemm(x, W0, out, True, True, C.EPI_BIAS_RELU, bias=b, tile=256, variant=1),
+            "q_mask": lambda: C.gemm(x, W0, out, True, True, C.EPI_BIAS_RELU, bias=b, mask_out=mask),
             "lib": lambda: torch._addmm_activation(b.bfloat16(), x, W0.t(), out=out)})
     if not only or "fwd1" in only:
         rec("fwd1", fl(B, H, H), {
@@ -86,6 +89,9 @@ def main():
         rec("dgrad1", fl(B, H, H), {
             "q_drelu": lambda: C.gemm(dz2, W1, out, True, False, C.EPI_DRELU, aux=h1, dbias=db, tile=256, variant=32),
             "q_none": lambda: C.gemm(dz2, W1, out, True, False, C.EPI_NONE, tile=256, variant=32),
+            "q_drelu_nodb": lambda: C.gemm(dz2, W1, out, True, False, C.EPI_DRELU, aux=h1, tile=256, variant=32),
+            "q_mask": lambda: C.gemm(dz2, W1, out, True, False, C.EPI_DRELU, dbias=db, mask_in=mask),
+            "q_mask_nodb": lambda: C.gemm(dz2, W1, out, True, False, C.EPI_DRELU, mask_in=mask),
             "qT_drelu": lambda: C.gemm(dz2, W1t, out, True, True, C.EPI_DRELU, aux=h1, dbias=db, tile=256,
                                        variant=32),
             "qT_none": lambda: C.gemm(dz2, W1t, out, True, True, C.EPI_NONE, tile=256, variant=32),
