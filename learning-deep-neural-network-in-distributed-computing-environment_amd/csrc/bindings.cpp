@@ -977,6 +977,37 @@ PYBIND11_MODULE(_C, m) {
         py::arg("tile") = 0, py::arg("splitk") = 0, py::arg("direct_epi") = false, py::arg("variant") = 0,
         py::arg("ws") = py::none(), py::arg("cnt") = py::none(), py::arg("mask_out") = py::none(),
         py::arg("mask_in") = py::none());
+  m.def("transpose_bf16", [](const at::Tensor& in, const at::Tensor& out) {
+        check_dev(in, at::kBFloat16, "in");
+        check_dev(out, at::kBFloat16, "out");
+        TORCH_CHECK(in.dim() == 2 && out.dim() == 2 && out.size(0) == in.size(1) && out.size(1) == in.size(0),
+                    "transpose_bf16: out must be [cols][rows] of in");
+        const int64_t ldi = ld_of(in, "in"), ldo = ld_of(out, "out");
+        TORCH_CHECK(in.size(0) % 8 == 0 && in.size(1) % 8 == 0 && ldi % 8 == 0 && ldo % 8 == 0 &&
+                        aligned16(in.data_ptr()) && aligned16(out.data_ptr()),
+                    "transpose_bf16: dims / strides must be multiples of 8, pointers 16-B aligned");
+        c10::hip::HIPGuardMasqueradingAsCUDA g(in.device());
+        check(ldnn::transpose_bf16(bf16_ptr(in), bf16_mut(out), (int)in.size(0), (int)in.size(1), (int)ldi, (int)ldo,
+                                   cur_stream(in)), "transpose_bf16");
+      }, "out = in^T (bf16)", py::arg("in"), py::arg("out"));
+  m.def("slab_sum_cols", [](const at::Tensor& ws, const at::Tensor& out, const c10::optional<at::Tensor>& extra) {
+        // ws [splits][rows][ldw] fp32 -> out [rows][ncols] (+ extra[rows] = column ncols of the sum)
+        check_dev(ws, at::kFloat, "ws");
+        check_dev(out, at::kFloat, "out");
+        TORCH_CHECK(ws.dim() == 3 && ws.is_contiguous() && out.dim() == 2 && out.size(0) == ws.size(1) &&
+                        out.stride(1) == 1 && aligned16(ws.data_ptr()), "slab_sum_cols: bad shapes");
+        float* ex = nullptr;
+        if (extra.has_value()) {
+          check_dev(*extra, at::kFloat, "extra");
+          TORCH_CHECK(extra->is_contiguous() && extra->numel() >= ws.size(1), "slab_sum_cols: bad extra");
+          ex = extra->data_ptr<float>();
+        }
+        c10::hip::HIPGuardMasqueradingAsCUDA g(ws.device());
+        check(ldnn::slab_sum_cols(ws.data_ptr<float>(), (int)ws.size(0), (int)ws.size(1), (int)ws.size(2),
+                                  out.data_ptr<float>(), (int)out.stride(0), (int)out.size(1), ex, cur_stream(ws)),
+              "slab_sum_cols");
+      }, "sum split-K slabs into out (and one extra column)", py::arg("ws"), py::arg("out"),
+      py::arg("extra") = py::none());
   m.def("slab_sum", [](const at::Tensor& ws, const at::Tensor& out, double beta) {
         // out = sum over the leading dim of ws (+ beta * out); fp32, dense, same trailing size
         check_dev(ws, at::kFloat, "ws");

@@ -113,8 +113,10 @@ hipError_t conv2d_wgrad(const ConvShape& s, const uint16_t* dy, const uint16_t* 
                         hipStream_t st, float* ws = nullptr);
 // LDS-DMA fast path (conv_lds.hip): hipErrorNotSupported outside its shape set
 // (fwd needs C % 64 == 0, dgrad K % 64 == 0, stride 1 or 2).
+// bn_used: whether the epilogue accumulated the BN statistics (a slab split-K shape does not)
 hipError_t conv2d_fwd_lds(const ConvShape& s, const uint16_t* x, const uint16_t* w, uint16_t* y, const float* bias,
-                          int epi, hipStream_t st, float* ws, int* cnt, const BnFin* bn = nullptr);
+                          int epi, hipStream_t st, float* ws, int* cnt, const BnFin* bn = nullptr,
+                          bool* bn_used = nullptr);
 hipError_t conv2d_dgrad_lds(const ConvShape& s, const uint16_t* dy, const uint16_t* w, uint16_t* dx, hipStream_t st,
                             float* ws, int* cnt);
 hipError_t conv2d_wgrad_lds(const ConvShape& s, const uint16_t* dy, const uint16_t* x, float* dw, float beta,
@@ -195,6 +197,11 @@ hipError_t act_bwd_colsum(const uint16_t* dy, const uint16_t* y, uint16_t* dx, f
 hipError_t cast_f32_bf16(const float* x, uint16_t* y, int64_t n, hipStream_t s);
 // graph-capture-safe zero fill of a strided fp32 block (instead of hipMemset2DAsync)
 hipError_t zero2d_f32(float* p, int rows, int cols, int ld, hipStream_t s);
+// out[c][r] = in[r][c], bf16, rows / cols / strides multiples of 8
+hipError_t transpose_bf16(const uint16_t* in, uint16_t* out, int rows, int cols, int ldi, int ldo, hipStream_t s);
+// sum split-K slabs [splits][rows][ldw] into out[rows][ncols] (stride ldo); extra[r] = column ncols
+hipError_t slab_sum_cols(const float* ws, int splits, int rows, int ldw, float* out, int ldo, int ncols, float* extra,
+                         hipStream_t s);
 hipError_t cast_bf16_f32(const uint16_t* x, float* y, int64_t n, hipStream_t s);
 // y = a*x + b*y1 + c*y2 (fp32, in place on x allowed); optional bf16 shadow of y
 hipError_t mix3_f32(float* out, const float* x, const float* y1, const float* y2, float a, float b, float c,

@@ -254,9 +254,10 @@ hipError_t conv2d_fwd(const ConvShape& s, const uint16_t* x, const uint16_t* w, 
                       int epi, hipStream_t st, float* ws, int* cnt, const BnFin* bn, bool* bn_done) {
   if (bn_done) *bn_done = false;
   if (g_conv_impl == 0) {
-    const hipError_t e = conv2d_fwd_lds(s, x, w, y, bias, epi, st, ws, cnt, bn);
+    bool used = false;
+    const hipError_t e = conv2d_fwd_lds(s, x, w, y, bias, epi, st, ws, cnt, bn, &used);
     if (e != hipErrorNotSupported) {
-      if (bn_done) *bn_done = bn != nullptr && e == hipSuccess;
+      if (bn_done) *bn_done = used && e == hipSuccess;
       return e;
     }
   }

@@ -574,16 +574,16 @@ __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void conv_lds_kernel(LArgs a,
       const int tile = blockIdx.z * a.tiles_x + blockIdx.x;
       if (!splitk_combine<4, 4, NW * 64>(acc, a.ws, a.cnt, tile, gridDim.y, blockIdx.y, smem)) return;
     } else if (a.ws != nullptr) {
-      // wgrad: this slice's fp32 partial tile into its own slab; a separate
-      // reduction kernel sums the slabs over all CUs (deterministic, no atomics)
-      if constexpr (OUT_F32 && EPI == EPI_NONE) {
-        GemmParams p{};
-        p.C = a.ws + (size_t)blockIdx.y * a.M * a.N;
-        p.M = g.M;
-        p.N = a.N;
-        p.ldc = a.N;
-        epilogue<EPI_NONE, true, 4, 4>(p, acc, mb, nbase, lane);
-      }
+      // wgrad, and small-M fwd / stride-1 dgrad: this slice's fp32 partial tile into
+      // its own slab; a separate chip-wide kernel sums the slabs (slab_sum_kernel /
+      // conv_slab_epilogue_kernel with the bias / ReLU epilogue) -- deterministic, no
+      // atomics, and no single workgroup re-reading every slice of its tile
+      GemmParams p{};
+      p.C = a.ws + (size_t)blockIdx.y * a.M * a.N;
+      p.M = g.M;
+      p.N = a.N;
+      p.ldc = a.N;
+      epilogue<EPI_NONE, true, 4, 4>(p, acc, mb, nbase, lane);
       return;
     } else {
       if constexpr (OUT_F32 && EPI == EPI_NONE) {  // fp32 atomics into the (cleared / accumulated) output
@@ -621,6 +621,48 @@ __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void conv_lds_kernel(LArgs a,
   if constexpr (!DGRAD && !OUT_F32 && EPI == EPI_NONE) {
     if (a.bn_stats) bn_stats_epilogue<WM, WN>(a, g, acc, mb, n0, wm, wn, lane, blockIdx.x, smem);
   }
+}
+
+// bf16 out[m][n] = epi(sum_s ws[s][m][n] (+ bias[n])): the split-K reduction of the
+// small-M fwd / dgrad slabs, 8 consecutive outputs per thread (two float4 per slab,
+// one 16-B store), all CUs.
+template <int EPI>
+__global__ __launch_bounds__(256) void conv_slab_epilogue_kernel(const float* __restrict__ ws, bf16_t* __restrict__ out,
+                                                                 int64_t n8, int N, int splits,
+                                                                 const float* __restrict__ bias) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n8) return;
+  const floatx4* w = reinterpret_cast<const floatx4*>(ws) + 2 * i;
+  const int64_t stride4 = 2 * n8;
+  floatx4 v0 = w[0], v1 = w[1];
+  for (int sp = 1; sp < splits; ++sp) {
+    v0 += w[sp * stride4];
+    v1 += w[sp * stride4 + 1];
+  }
+  const int n = (int)((i * 8) % N);
+  u16x8 o;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const float b = (EPI == EPI_NONE) ? 0.f : bias[n + q];
+    o[q] = f2bf(apply_epi<EPI>(q < 4 ? v0[q] : v1[q - 4], b, 0.f));
+  }
+  reinterpret_cast<u16x8*>(out)[i] = o;
+}
+
+hipError_t conv_slab_epilogue(const float* ws, uint16_t* out, int M, int N, int splits, const float* bias, int epi,
+                              hipStream_t st) {
+  const int64_t n8 = (int64_t)M * N / 8;
+  if (n8 <= 0) return hipSuccess;
+  const unsigned g = (unsigned)((n8 + 255) / 256);
+  switch (epi) {
+    case EPI_NONE: conv_slab_epilogue_kernel<EPI_NONE><<<g, 256, 0, st>>>(ws, out, n8, N, splits, bias); break;
+    case EPI_BIAS: conv_slab_epilogue_kernel<EPI_BIAS><<<g, 256, 0, st>>>(ws, out, n8, N, splits, bias); break;
+    case EPI_BIAS_RELU:
+      conv_slab_epilogue_kernel<EPI_BIAS_RELU><<<g, 256, 0, st>>>(ws, out, n8, N, splits, bias);
+      break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
 }
 
 // out[i] = sum_s ws[s][i] (+ beta * out[i]): the cross-CU reduction of wgrad slabs.
@@ -751,6 +793,15 @@ hipError_t launch(LArgs a, int epi, int splits, const bf16_t* pa, size_t ba, con
   return launch_ns<WM, WN, OA, OB, OUT_F32, DGRAD, 2>(a, epi, splits, pa, ba, pb, bb, st);
 }
 
+// LDNN_CONV_SLAB=0: small-M fwd / dgrad use the in-launch combine (A/B knob)
+bool slab_env_off() {
+  static const bool v = [] {
+    const char* e = std::getenv("LDNN_CONV_SLAB");
+    return e != nullptr && e[0] == '0';
+  }();
+  return v;
+}
+
 // In-launch split-K for small-M fwd / dgrad: enough slices for ~1.5
 // workgroups per CU, >= 8 K-tiles each, at most 8.
 int small_m_splits(int tiles, int nk) {
@@ -761,15 +812,32 @@ int small_m_splits(int tiles, int nk) {
   return sp < 2 ? 1 : sp;
 }
 
+// Slab split-K for small-M fwd / stride-1 dgrad: the splits write fp32 slabs and a
+// chip-wide kernel sums them, so a deep split costs no per-tile serial combine:
+// ~2 workgroups per CU (the weights of a 2x2 / 4x4 tail stage stream from HBM at
+// the per-CU rate, so the more CUs read them the sooner they land), >= 3 K-tiles
+// per slice, at most 32 slices.
+int slab_splits(int tiles, int nk) {
+  if (tiles >= 160 || nk < 8) return 1;
+  int sp = (512 + tiles - 1) / tiles;
+  sp = std::min(sp, nk / 3);
+  sp = std::min(sp, 32);
+  return sp < 2 ? 1 : sp;
+}
+
 struct Plan {
   int wm, wn;  // wave grid (tile = 64*wm x 64*wn)
   int tiles_x, classes, splits, nk_all, nk_split;
+  bool slab;   // split-K via fp32 slabs + conv_slab_epilogue (else the in-launch combine)
+  int M, N;    // GEMM output (slab size)
 };
 
 void finish_plan(Plan& p) {
-  p.splits = small_m_splits(p.tiles_x * p.classes, p.nk_all);
+  p.slab = p.classes == 1 && !slab_env_off();
+  p.splits = p.slab ? slab_splits(p.tiles_x, p.nk_all) : small_m_splits(p.tiles_x * p.classes, p.nk_all);
   p.nk_split = (p.nk_all + p.splits - 1) / p.splits;
   p.splits = (p.nk_all + p.nk_split - 1) / p.nk_split;
+  if (p.splits < 2) p.slab = false;
 }
 
 Plan plan_fwd(const ConvShape& s) {
@@ -779,6 +847,8 @@ Plan plan_fwd(const ConvShape& s) {
   const int M = s.N * s.P * s.Q;
   p.tiles_x = ((M + p.wm * 64 - 1) / (p.wm * 64)) * ((s.K + p.wn * 64 - 1) / (p.wn * 64));
   p.nk_all = s.R * s.S * s.C / 64;
+  p.M = M;
+  p.N = s.K;
   finish_plan(p);
   return p;
 }
@@ -798,13 +868,17 @@ Plan plan_dgrad(const ConvShape& s) {
     p.tiles_x = ((s.N * s.H * s.W + p.wm * 64 - 1) / (p.wm * 64)) * tn;
     p.nk_all = s.R * s.S * nb;
   }
+  p.M = s.N * s.H * s.W;
+  p.N = s.C;
   finish_plan(p);
   return p;
 }
 
 ConvWorkspace ws_of(const Plan& p) {
   ConvWorkspace w{};
-  if (p.splits > 1) {
+  if (p.splits > 1 && p.slab) {
+    w.slab_bytes = (size_t)p.splits * p.M * p.N * 4;
+  } else if (p.splits > 1) {
     w.slab_bytes = (size_t)p.tiles_x * p.classes * p.splits * kSlabBytes4;
     w.counters = p.tiles_x * p.classes;
   }
@@ -862,7 +936,8 @@ hipError_t conv2d_fwd_lds_small_c(const ConvShape& s, const uint16_t* x, const u
 }
 
 hipError_t conv2d_fwd_lds(const ConvShape& s, const uint16_t* x, const uint16_t* w, uint16_t* y, const float* bias,
-                          int epi, hipStream_t st, float* ws, int* cnt, const BnFin* bn) {
+                          int epi, hipStream_t st, float* ws, int* cnt, const BnFin* bn, bool* bn_used) {
+  if (bn_used) *bn_used = bn != nullptr;
   if (!shape_ok(s)) return hipErrorNotSupported;
   if (bn != nullptr && epi != EPI_NONE) return hipErrorInvalidValue;
   if (s.C == 8 || s.C == 16 || s.C == 32) {
@@ -873,6 +948,10 @@ hipError_t conv2d_fwd_lds(const ConvShape& s, const uint16_t* x, const uint16_t*
   if (s.N * s.P * s.Q <= 0) return bn != nullptr ? hipErrorNotSupported : hipSuccess;
   Plan pl = plan_fwd(s);
   LArgs a = base_args(s);
+  if (bn != nullptr && pl.slab) {  // slab split-K: the next BN runs its own statistics pass
+    bn = nullptr;
+    if (bn_used) *bn_used = false;
+  }
   if (bn != nullptr) {
     a.bn_stats = 1;
     a.bn = *bn;
@@ -884,7 +963,11 @@ hipError_t conv2d_fwd_lds(const ConvShape& s, const uint16_t* x, const uint16_t*
   a.nb = s.C / 64;
   a.tiles_x = pl.tiles_x;
   a.nk_all = pl.nk_all;
-  if (pl.splits > 1 && ws != nullptr && cnt != nullptr) {
+  const bool slab = pl.splits > 1 && pl.slab && ws != nullptr;
+  if (slab) {
+    a.ws = ws;
+    a.nk_split = pl.nk_split;
+  } else if (pl.splits > 1 && !pl.slab && ws != nullptr && cnt != nullptr) {
     a.ws = ws;
     a.cnt = cnt;
     a.nk_split = pl.nk_split;
@@ -893,8 +976,11 @@ hipError_t conv2d_fwd_lds(const ConvShape& s, const uint16_t* x, const uint16_t*
     a.nk_split = pl.nk_all;
   }
   const size_t bx = (size_t)s.N * s.H * s.W * s.C * 2, bw = (size_t)s.K * a.rsc * 2;
-  if (pl.wm == 4) return launch<4, 1, FwdA<256, 8, 4>, WeightKC<64, 2, 4>, false, false>(a, epi, pl.splits, x, bx, w, bw, st);
-  return launch<2, 2, FwdA<128, 4, 4>, WeightKC<128, 4, 4>, false, false>(a, epi, pl.splits, x, bx, w, bw, st);
+  hipError_t e;
+  if (pl.wm == 4) e = launch<4, 1, FwdA<256, 8, 4>, WeightKC<64, 2, 4>, false, false>(a, epi, pl.splits, x, bx, w, bw, st);
+  else e = launch<2, 2, FwdA<128, 4, 4>, WeightKC<128, 4, 4>, false, false>(a, epi, pl.splits, x, bx, w, bw, st);
+  if (e != hipSuccess || !slab) return e;
+  return conv_slab_epilogue(ws, y, a.M, a.N, pl.splits, bias, epi, st);
 }
 
 hipError_t conv2d_dgrad_lds(const ConvShape& s, const uint16_t* dy, const uint16_t* w, uint16_t* dx, hipStream_t st,
@@ -910,7 +996,11 @@ hipError_t conv2d_dgrad_lds(const ConvShape& s, const uint16_t* dy, const uint16
   a.classes = pl.classes;
   a.tiles_x = pl.tiles_x;
   a.nk_all = pl.nk_all;
-  if (pl.splits > 1 && ws != nullptr && cnt != nullptr) {
+  const bool slab = pl.splits > 1 && pl.slab && ws != nullptr;
+  if (slab) {
+    a.ws = ws;
+    a.nk_split = pl.nk_split;
+  } else if (pl.splits > 1 && !pl.slab && ws != nullptr && cnt != nullptr) {
     a.ws = ws;
     a.cnt = cnt;
     a.nk_split = pl.nk_split;
@@ -919,8 +1009,11 @@ hipError_t conv2d_dgrad_lds(const ConvShape& s, const uint16_t* dy, const uint16
     a.nk_split = pl.nk_all;
   }
   const size_t bdy = (size_t)s.N * s.P * s.Q * s.K * 2, bw = (size_t)s.K * a.rsc * 2;
-  if (pl.wm == 4) return launch<4, 1, DgradA<256, 8, 4>, DgradB<64, 2, 4>, false, true>(a, EPI_NONE, pl.splits, dy, bdy, w, bw, st);
-  return launch<2, 2, DgradA<128, 4, 4>, DgradB<128, 4, 4>, false, true>(a, EPI_NONE, pl.splits, dy, bdy, w, bw, st);
+  hipError_t e;
+  if (pl.wm == 4) e = launch<4, 1, DgradA<256, 8, 4>, DgradB<64, 2, 4>, false, true>(a, EPI_NONE, pl.splits, dy, bdy, w, bw, st);
+  else e = launch<2, 2, DgradA<128, 4, 4>, DgradB<128, 4, 4>, false, true>(a, EPI_NONE, pl.splits, dy, bdy, w, bw, st);
+  if (e != hipSuccess || !slab) return e;
+  return conv_slab_epilogue(ws, dx, a.M, a.N, pl.splits, nullptr, EPI_NONE, st);
 }
 
 hipError_t conv2d_wgrad_lds(const ConvShape& s, const uint16_t* dy, const uint16_t* x, float* dw, float beta,

@@ -176,6 +176,52 @@ __global__ void zero2d_kernel(float* __restrict__ p, int rows, int cols, int ld)
   }
 }
 
+// out[c][r] = in[r][c] (bf16, rows and cols multiples of 8): 64 x 64 tiles staged in
+// LDS, 16-B loads and stores on both sides.
+__global__ __launch_bounds__(256) void transpose_bf16_kernel(const bf16_t* __restrict__ in, bf16_t* __restrict__ out,
+                                                             int rows, int cols, int ldi, int ldo) {
+  __shared__ uint16_t t[64][72];
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  for (int p = threadIdx.x; p < 512; p += 256) {
+    const int r = p >> 3, c8 = (p & 7) * 8;
+    u16x8 v = {};
+    if (r0 + r < rows && c0 + c8 < cols) v = *reinterpret_cast<const u16x8*>(in + (size_t)(r0 + r) * ldi + c0 + c8);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) t[r][c8 + q] = v[q];
+  }
+  __syncthreads();
+  for (int p = threadIdx.x; p < 512; p += 256) {
+    const int c = p >> 3, r8 = (p & 7) * 8;
+    if (c0 + c < cols && r0 + r8 < rows) {
+      u16x8 o;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) o[q] = t[r8 + q][c];
+      *reinterpret_cast<u16x8*>(out + (size_t)(c0 + c) * ldo + r0 + r8) = o;
+    }
+  }
+}
+
+// split-K slabs ws[s][r][0 .. ldw) -> out[r][0 .. ncols) (row stride ldo) and, when
+// extra != nullptr, extra[r] = column ncols (a GEMM whose B operand carries a ones
+// column: the bias gradient comes out of the weight-gradient GEMM)
+__global__ __launch_bounds__(256) void slab_sum_cols_kernel(const float* __restrict__ ws, int splits, int rows, int ldw,
+                                                            float* __restrict__ out, int ldo, int ncols,
+                                                            float* __restrict__ extra) {
+  const int g4 = (ncols + 4) / 4;  // float4 groups per row, incl. the one holding column ncols
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)rows * g4) return;
+  const int r = (int)(i / g4), c = (int)(i % g4) * 4;
+  const size_t slab = (size_t)rows * ldw;
+  const floatx4* w = reinterpret_cast<const floatx4*>(ws + (size_t)r * ldw + c);
+  floatx4 v = w[0];
+  for (int sp = 1; sp < splits; ++sp) v += *reinterpret_cast<const floatx4*>(ws + sp * slab + (size_t)r * ldw + c);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (c + q < ncols) out[(size_t)r * ldo + c + q] = v[q];
+    else if (c + q == ncols && extra != nullptr) extra[r] = v[q];
+  }
+}
+
 __global__ void cast_f32_bf16_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, int64_t n) {
   const int64_t nv = n / 4;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -252,6 +298,22 @@ hipError_t act_bwd(const uint16_t* dy, const uint16_t* y, uint16_t* dx, int64_t 
   const int g = grid_for((n + 7) / 8);
   if (act == ACT_RELU) act_bwd_kernel<ACT_RELU><<<g, kBlock, 0, s>>>(dy, y, dx, n);
   else act_bwd_kernel<ACT_SIGMOID><<<g, kBlock, 0, s>>>(dy, y, dx, n);
+  return hipGetLastError();
+}
+
+hipError_t transpose_bf16(const uint16_t* in, uint16_t* out, int rows, int cols, int ldi, int ldo, hipStream_t s) {
+  if (rows <= 0 || cols <= 0) return hipSuccess;
+  if (rows % 8 || cols % 8 || ldi % 8 || ldo % 8) return hipErrorInvalidValue;
+  transpose_bf16_kernel<<<dim3((cols + 63) / 64, (rows + 63) / 64), 256, 0, s>>>(in, out, rows, cols, ldi, ldo);
+  return hipGetLastError();
+}
+
+hipError_t slab_sum_cols(const float* ws, int splits, int rows, int ldw, float* out, int ldo, int ncols, float* extra,
+                         hipStream_t s) {
+  if (rows <= 0 || ncols <= 0) return hipSuccess;
+  if (ldw % 4 || ncols + (extra ? 1 : 0) > ldw || ((ncols + 4) / 4) * 4 > ldw) return hipErrorInvalidValue;
+  const int64_t n = (int64_t)rows * ((ncols + 4) / 4);
+  slab_sum_cols_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(ws, splits, rows, ldw, out, ldo, ncols, extra);
   return hipGetLastError();
 }
 

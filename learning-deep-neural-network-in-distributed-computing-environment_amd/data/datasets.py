@@ -54,9 +54,15 @@ class ArrayDataset:
 
 
 def synthetic(kind: str = "cifar10", n: int = 50_000, num_classes: int | None = None, seed: int = 0,
-              noise: float = 0.9, proto_seed: int | None = None) -> ArrayDataset:
+              noise: float = 0.9, proto_seed: int | None = None, hard: bool = False) -> ArrayDataset:
     """Seeded, learnable synthetic images: x = clip(proto[y] + noise), uint8.
-    `proto_seed` fixes the class prototypes (share it between train and test sets)."""
+    `proto_seed` fixes the class prototypes (share it between train and test sets).
+
+    ``hard`` (dataset names ``*-hard``): a task that does NOT saturate, so topology /
+    skew effects show in the curves -- low-contrast overlapping prototypes (amplitude
+    0.3 around grey), a random +-3 px shift and contrast jitter per image, and 15 %
+    of the labels (train and test alike) redrawn uniformly, which caps the reachable
+    test accuracy near 86 %."""
     shape = SHAPES[kind]
     k = num_classes or CLASSES[kind]
     g = torch.Generator().manual_seed(seed if proto_seed is None else proto_seed)
@@ -64,6 +70,8 @@ def synthetic(kind: str = "cifar10", n: int = 50_000, num_classes: int | None = 
     base = max(2, shape[1] // 8)
     protos = torch.rand(k, shape[0], base, base, generator=g)
     protos = torch.nn.functional.interpolate(protos, size=shape[1:], mode="bilinear", align_corners=False)
+    if hard:
+        protos = 0.5 + 0.3 * (protos - 0.5)
     gl = torch.Generator().manual_seed(seed + 1)
     labels = torch.randint(0, k, (n,), generator=gl)
     imgs = torch.empty((n, *shape), dtype=torch.uint8)
@@ -71,9 +79,21 @@ def synthetic(kind: str = "cifar10", n: int = 50_000, num_classes: int | None = 
     gn = torch.Generator().manual_seed(seed + 2)
     for s in range(0, n, chunk):
         e = min(n, s + chunk)
-        x = protos[labels[s:e]] + noise * torch.randn((e - s, *shape), generator=gn)
+        p = protos[labels[s:e]]
+        if hard:
+            sid = torch.randint(0, 49, (e - s,), generator=gn)   # per-image (dy, dx) in [-3, 3]^2
+            p = p.clone()
+            for q in range(49):
+                sel = sid == q
+                if sel.any():
+                    p[sel] = torch.roll(p[sel], shifts=(q // 7 - 3, q % 7 - 3), dims=(2, 3))
+            p = 0.5 + (p - 0.5) * (0.6 + 0.8 * torch.rand(e - s, 1, 1, 1, generator=gn))
+        x = p + noise * torch.randn((e - s, *shape), generator=gn)
         imgs[s:e] = (x.clamp(0, 1) * 255).round().to(torch.uint8)
-    return ArrayDataset(imgs, labels, k, name=f"synthetic-{kind}")
+    if hard:
+        flip = torch.rand(n, generator=gl) < 0.15
+        labels = torch.where(flip, torch.randint(0, k, (n,), generator=gl), labels)
+    return ArrayDataset(imgs, labels, k, name=f"synthetic-{kind}{'-hard' if hard else ''}")
 
 
 def load_cifar10(root: str = "data") -> tuple[ArrayDataset, ArrayDataset] | None:
@@ -131,9 +151,11 @@ def build_dataset(name: str, n_train: int | None = None, n_test: int | None = No
         if real is not None:
             return real
     kind = name.replace("synthetic-", "")
+    hard = kind.endswith("-hard")
+    kind = kind[: -len("-hard")] if hard else kind
     ntr = n_train or {"mnist": 60_000, "cifar10": 50_000}.get(kind, 10_000)
     nte = n_test or max(1, ntr // 5)
-    tr = synthetic(kind, ntr, seed=seed, proto_seed=seed)
-    te = synthetic(kind, nte, seed=seed + 1000, proto_seed=seed)
+    tr = synthetic(kind, ntr, seed=seed, proto_seed=seed, hard=hard)
+    te = synthetic(kind, nte, seed=seed + 1000, proto_seed=seed, hard=hard)
     te.name = tr.name + "-test"
     return tr, te

@@ -100,7 +100,8 @@ class StaticMLPEngine:
                  fuse_optimizer: bool | None = None, library_gemms: bool | None = None,
                  fuse_head_dgrad: bool | None = None, early_optimizer: bool | None = None,
                  library_dgrad: bool | None = None, concurrent_wgrad: bool = False, pad_input: bool = False,
-                 head_dgrad_mode: int = -1, relu_masks: bool = True, wgrad_slabs: bool = True):
+                 head_dgrad_mode: int = -1, relu_masks: bool = True, wgrad_slabs: bool = True,
+                 transposed_dgrad: bool = True, bias_ones_column: bool = True):
         from ..models.mlp import MLP
 
         if not isinstance(model, MLP):
@@ -287,6 +288,14 @@ class StaticMLPEngine:
             if (relu_masks and self.layers[l - 1].activation == "relu" and not self._lib_fwd[l - 1]
                     and not self._lib_dgrad[l] and not (self.use_head and l == L - 1 and fuse_head_dgrad)):
                 self.mask[l] = torch.zeros(B, (npad[l - 1] + 7) // 8, dtype=torch.uint8, device=dev)
+        self._db0_from_wgrad = False
+        # transposed_dgrad: dgrad(l) reads a transposed bf16 copy of W_l, refreshed by one
+        # transpose pass right before it, so both GEMM operands are k-contiguous (measured
+        # on MI355X, 16384 x 4096 x 4096: 384-434 vs 430-483 us for the k-strided W)
+        self.Wt = [None] * L
+        for l in range(1, L):
+            if transposed_dgrad and not self._lib_dgrad[l] and not (self.use_head and l == L - 1 and self.head_dgrad):
+                self.Wt[l] = torch.zeros(self.W[l].shape[1], self.W[l].shape[0], dtype=bf, device=dev)
         self._wgrad_splitk, self._wgrad_ws, self._wgrad_slab = [], [], []
         for l, layer in enumerate(self.layers):
             M, N = self.dW[l].shape
@@ -309,7 +318,21 @@ class StaticMLPEngine:
                     # measured on MI355X (4096 x 784 x 16384) the in-launch combine, where the
                     # last-arriving workgroup of a tile re-reads every split's 256 KiB alone,
                     # cost ~90 of the kernel's 177 us
-                    self._wgrad_slab[l] = torch.empty(sk, M, N, dtype=torch.float32, device=self.device)
+                    Nw = N
+                    if (l == 0 and bias_ones_column and not pad_input and L >= 2 and self.mask[1] is not None
+                            and self.layers[0].bias is not None and (N + 255) // 256 == (N + 8 + 255) // 256):
+                        # bias_ones_column: the input buffer carries a ones column after its K0
+                        # features, so this wgrad's product has one more column = sum over the
+                        # batch of dz_1 = the first layer's bias gradient, in the free part of the
+                        # last 256-wide tile; dgrad(1) then needs no bias-gradient sums (measured
+                        # on MI355X: the dgrad epilogue's column sums + atomics cost 13-30 us)
+                        Nw = N + 8
+                        self.xp = torch.zeros(B, Nw, dtype=bf, device=dev)
+                        self.xp[:, N] = 1.0
+                        self.x = self.xp[:, :N]
+                        self.h[0] = self.x
+                        self._db0_from_wgrad = True
+                    self._wgrad_slab[l] = torch.empty(sk, M, Nw, dtype=torch.float32, device=self.device)
                     self._wgrad_splitk.append(sk)
                     continue
                 ne, nc = self.C.gemm_pp_ws(M, N, sk)
@@ -438,6 +461,10 @@ class StaticMLPEngine:
             torch.mm(self.dz[l + 1].t(), self.h[l], out_dtype=torch.float32, out=self.dW[l])
             return
         if self._wgrad_slab[l] is not None:   # split-K into slabs + one summing pass, overwrites
+            if l == 0 and self._db0_from_wgrad:   # + the ones column: dW_0 and the bias gradient
+                self.C.gemm(self.dz[1], self.xp, self._wgrad_slab[0], False, False, tile=256, splitk=sk)
+                self.C.slab_sum_cols(self._wgrad_slab[0], self.dW[0], self.db[0])
+                return
             self.C.gemm(self.dz[l + 1], self.h[l], self._wgrad_slab[l], False, False, tile=256, splitk=sk)
             self.C.slab_sum(self._wgrad_slab[l], self.dW[l])
             return
@@ -489,9 +516,16 @@ class StaticMLPEngine:
             torch.mm(self.dz[l + 1], self.W[l], out=self.dz[l])
             self.C.act_bwd_colsum(self.dz[l], self.h[l], self.dz[l], self.db[l - 1], self._act_code[l], True)
             return
+        db = None if (l == 1 and self._db0_from_wgrad) else self.db[l - 1]
+        W, w_kc = self.W[l], False
+        if self.Wt[l] is not None:
+            self.C.transpose_bf16(self.W[l], self.Wt[l])
+            W, w_kc = self.Wt[l], True
         if self.mask[l] is not None:
-            self.C.gemm(self.dz[l + 1], self.W[l], self.dz[l], True, False, self.C.EPI_DRELU, dbias=self.db[l - 1],
-                        mask_in=self.mask[l])
+            self.C.gemm(self.dz[l + 1], W, self.dz[l], True, w_kc, self.C.EPI_DRELU, dbias=db, mask_in=self.mask[l])
+            return
+        if w_kc:
+            self.C.gemm(self.dz[l + 1], W, self.dz[l], True, True, self._dgrad_epi[l], aux=self.h[l], dbias=db)
             return
         self.C.gemm(self.dz[l + 1], self.W[l], self.dz[l], True, False, self._dgrad_epi[l], aux=self.h[l],
                     dbias=self.db[l - 1])

@@ -70,6 +70,11 @@ static void conv_plans() {
                 }
                 if (op == 2 && w.slab_bytes > 0)  // wgrad partial slabs: whole [K][RSC] fp32 copies
                   CHECK(w.slab_bytes % ((size_t)K * R * R * C * 4) == 0);
+                if (op < 2 && w.slab_bytes > 0 && w.counters == 0) {  // small-M slab split-K: whole outputs
+                  const size_t out = op == 0 ? (size_t)N * s.P * s.Q * K * 4 : (size_t)N * H * H * C * 4;
+                  CHECK(w.slab_bytes % out == 0 && w.slab_bytes / out >= 2 && w.slab_bytes / out <= 32);
+                  CHECK(op == 0 || st == 1);  // stride-2 dgrad classes keep the in-launch combine
+                }
               }
               ++shapes;
             }

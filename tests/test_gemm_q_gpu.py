@@ -216,3 +216,18 @@ def test_split_slabs_plus_slab_sum(sk):
     one = torch.empty(M, N, device="cuda")
     c.gemm(a, b, one, False, False, tile=256, variant=32)
     torch.testing.assert_close(out, one, rtol=1e-5, atol=1e-3)  # fp32 summation order only
+
+
+def test_transpose_and_slab_sum_cols():
+    c = C()
+    x = torch.randn(520, 776, device="cuda").bfloat16()
+    out = torch.empty(776, 520, device="cuda", dtype=torch.bfloat16)
+    c.transpose_bf16(x, out)
+    assert torch.equal(out, x.t())
+    ws = torch.randn(3, 264, 792, device="cuda")
+    dst = torch.full((264, 784), float("nan"), device="cuda")
+    extra = torch.full((264,), float("nan"), device="cuda")
+    c.slab_sum_cols(ws, dst, extra)
+    tot = ws.sum(0)
+    torch.testing.assert_close(dst, tot[:, :784], rtol=1e-6, atol=1e-5)
+    torch.testing.assert_close(extra, tot[:, 784], rtol=1e-6, atol=1e-5)

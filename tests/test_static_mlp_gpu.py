@@ -386,16 +386,20 @@ def test_wgrad_q_splitk_matches_library_gemms():
 
 @pytest.mark.parametrize("opt", ["sgd", "adam"])
 def test_relu_masks_and_wgrad_slabs_match_plain_engine(opt):
-    """The engine with ReLU bit masks (fwd writes, dgrad reads) and the split-slab wgrad
-    equals the engine reading the bf16 activations and combining split-K in the launch."""
+    """The engine with ReLU bit masks (fwd writes, dgrad reads), the split-slab wgrad, the
+    transposed-W dgrad and the first-layer bias gradient from the wgrad's ones column
+    equals the engine reading the bf16 activations, k-strided W, in-launch split-K combine
+    and dgrad-epilogue bias sums."""
     torch.manual_seed(0)
     B = 4096
     m1, m2 = mlp3(784, 1024, 10), mlp3(784, 1024, 10)
     m2.load_state_dict(m1.state_dict())
     cfg = OptimConfig(opt, lr=0.05 if opt == "sgd" else 1e-3, momentum=0.9)
     e1 = StaticMLPEngine(m1, B, cfg, use_graphs=True)
-    e2 = StaticMLPEngine(m2, B, cfg, use_graphs=True, relu_masks=False, wgrad_slabs=False)
-    assert e1.mask[1] is not None and e1._wgrad_slab[0] is not None
+    e2 = StaticMLPEngine(m2, B, cfg, use_graphs=True, relu_masks=False, wgrad_slabs=False, transposed_dgrad=False,
+                         bias_ones_column=False)
+    assert e1.mask[1] is not None and e1._wgrad_slab[0] is not None and e1.Wt[1] is not None
+    assert e1._db0_from_wgrad and e1.xp.shape[1] == 792 and not e2._db0_from_wgrad
     assert e2.mask[1] is None and e2._wgrad_slab[0] is None
     g = torch.Generator(device="cuda").manual_seed(8)
     for _ in range(5):
