@@ -833,7 +833,11 @@ struct Plan {
 };
 
 void finish_plan(Plan& p) {
-  p.slab = p.classes == 1 && !slab_env_off();
+  // slabs only for the deep tails (< 48 output tiles): measured on MI355X at 64 - 160
+  // tiles (EnhancedCNN 8x8 / 16x16 stages, ResNet-18 7x7) the slab traffic cost what
+  // the in-launch combine does (ResNet-18 b64 3.94 vs 3.89 ms), at 16 / 32 tiles the
+  // slabs win (EnhancedCNN 4x4 / 2x2 convs 28 / 38 -> 25 / 28 us)
+  p.slab = p.classes == 1 && p.tiles_x < 48 && !slab_env_off();
   p.splits = p.slab ? slab_splits(p.tiles_x, p.nk_all) : small_m_splits(p.tiles_x * p.classes, p.nk_all);
   p.nk_split = (p.nk_all + p.splits - 1) / p.splits;
   p.splits = (p.nk_all + p.nk_split - 1) / p.nk_split;

@@ -151,10 +151,20 @@ class TorchComm(Comm):
 
     def sendrecv(self, sends, recvs):
         self.record("sendrecv")
+        # gloo moves GPU tensors point-to-point through a slow per-op path (measured: a
+        # 178 MB ring exchange ~10 s vs 0.1 s for the same bytes from host memory), so the
+        # plumbing backend stages them through host buffers; RCCL sends device-direct
+        stage = self.backend == "gloo" and any(t.is_cuda for t, _ in list(sends) + list(recvs))
+        if stage:
+            sends = [(t.detach().cpu(), dst) for t, dst in sends]
+            dev_recvs, recvs = recvs, [(torch.empty(t.shape, dtype=t.dtype), src) for t, src in recvs]
         ops = [dist.P2POp(dist.irecv, t, self._global(src), self.group) for t, src in recvs]
         ops += [dist.P2POp(dist.isend, t, self._global(dst), self.group) for t, dst in sends]
         for w in dist.batch_isend_irecv(ops):
             w.wait()
+        if stage:
+            for (t, _), (c, _) in zip(dev_recvs, recvs):
+                t.copy_(c)
 
 
 # ------------------------------------------------------------------ fake world

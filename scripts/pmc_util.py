@@ -1,0 +1,49 @@
+"""Compact per-kernel PMC table from scripts/pmc_step.sh passes:
+  mfma%   = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs)
+            (MFMA_BUSY sums 16 cycles per v_mfma_f32_16x16x32_bf16 over all SIMDs; GRBM_GUI_ACTIVE
+             sums the 8 XCDs' busy cycles, so GRBM / 8 = the kernel's GPU cycles)
+  ldsconf = SQ_LDS_BANK_CONFLICT / SQ_INSTS_LDS (extra LDS cycles per LDS instruction)
+  waitlds = SQ_WAIT_INST_LDS / SQ_WAVE_CYCLES
+  l2hit%  = TCC_HIT / (TCC_HIT + TCC_MISS)
+  usage: python scripts/pmc_util.py gpurun_out/pmc_<tag> [min_calls]"""
+import collections
+import csv
+import glob
+import sys
+
+d = sys.argv[1]
+cnt = collections.defaultdict(lambda: collections.defaultdict(list))
+for f in glob.glob(f"{d}/p*/**/*counter_collection.csv", recursive=True):
+    p = f.split("/")[len(d.rstrip("/").split("/"))]
+    for r in csv.DictReader(open(f)):
+        cnt[r["Kernel_Name"]][(p, r["Counter_Name"])].append(float(r["Counter_Value"]))
+
+
+def avg(c, k, p=None):
+    vals = [v for (pp, kk), v in c.items() if kk == k and (p is None or pp == p)]
+    vals = [x for v in vals for x in v]
+    return sum(vals) / len(vals) if vals else float("nan")
+
+
+def short(n):
+    n = n.replace("void ", "").replace("ldnn::", "").replace("(anonymous namespace)::", "").split("(")[0]
+    return n[:70]
+
+
+rows = []
+for name, c in cnt.items():
+    calls = max(len(v) for v in c.values())
+    g1 = avg(c, "GRBM_GUI_ACTIVE", "p1")
+    g2 = avg(c, "GRBM_GUI_ACTIVE", "p2")
+    mf = avg(c, "SQ_VALU_MFMA_BUSY_CYCLES") / (1024 * g1 / 8) if g1 == g1 else float("nan")
+    busy = avg(c, "SQ_BUSY_CYCLES") / (g1 / 8)
+    lds = avg(c, "SQ_INSTS_LDS")
+    conf = avg(c, "SQ_LDS_BANK_CONFLICT") / lds if lds and lds == lds else float("nan")
+    wl = avg(c, "SQ_WAIT_INST_LDS") / avg(c, "SQ_WAVE_CYCLES")
+    h, m = avg(c, "TCC_HIT_sum"), avg(c, "TCC_MISS_sum")
+    rows.append((g1, short(name), calls, mf, busy, conf, wl, h / (h + m) if h == h and m == m else float("nan")))
+print(f"{'GRBM/8 cyc':>11} {'calls':>5} {'mfma%':>6} {'ldsconf':>7} {'waitlds':>7} {'l2hit%':>6}  kernel")
+for g1, n, calls, mf, busy, conf, wl, hit in sorted(rows, key=lambda r: -r[0] * r[2]):
+    if calls < (int(sys.argv[2]) if len(sys.argv) > 2 else 1):
+        continue
+    print(f"{g1 / 8:11.0f} {calls:5d} {100 * mf:6.1f} {conf:7.3f} {wl:7.3f} {100 * hit:6.1f}  {n}")
