@@ -112,7 +112,7 @@ def run_ldnn(ctx, args):
     el = timed(ctx, step, args.steps, args.warmup)
     loss, acc = eng.read_stats(args.batch * (args.steps + args.warmup))
     return el, dict(train_loss=round(loss, 4), n_params=sum(p.numel() for p in model.parameters()),
-                    in_pad=eng.in_pad)
+                    in_pad=eng.in_pad, gemm_kernels=eng.describe())
 
 
 def run_stock(ctx, args):

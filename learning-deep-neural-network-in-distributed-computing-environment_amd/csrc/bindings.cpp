@@ -799,7 +799,7 @@ void bn_fwd(const at::Tensor& x, const at::Tensor& y, const c10::optional<at::Te
             const c10::optional<at::Tensor>& running_mean, const c10::optional<at::Tensor>& running_var,
             const at::Tensor& save_mean, const at::Tensor& save_invstd, const at::Tensor& ws, double eps,
             double momentum, bool training, bool relu, const c10::optional<at::Tensor>& num_batches,
-            bool stats_ready) {
+            bool stats_ready, const c10::optional<at::Tensor>& mask) {
   check_dev(x, at::kBFloat16, "x");
   check_dev(y, at::kBFloat16, "y");
   TORCH_CHECK(x.dim() == 2 && x.is_contiguous() && y.sizes() == x.sizes() && y.is_contiguous(), "bn: [M][C] dense");
@@ -827,6 +827,11 @@ void bn_fwd(const at::Tensor& x, const at::Tensor& y, const c10::optional<at::Te
   a.training = training ? 1 : 0;
   a.relu = relu ? 1 : 0;
   TORCH_CHECK(training || (a.running_mean && a.running_var), "bn: eval mode needs running statistics");
+  if (mask.has_value()) {  // ReLU bit mask [M][C/8] for the backward
+    check_dev(*mask, at::kByte, "mask");
+    TORCH_CHECK(relu && mask->is_contiguous() && mask->numel() == M * C / 8, "bn: mask needs relu and [M][C/8] bytes");
+    a.mask = mask->data_ptr<uint8_t>();
+  }
   if (num_batches.has_value() && training) {
     check_dev(*num_batches, at::kLong, "num_batches");
     a.num_batches = num_batches->data_ptr<int64_t>();
@@ -842,7 +847,8 @@ void bn_fwd(const at::Tensor& x, const at::Tensor& y, const c10::optional<at::Te
 void bn_bwd(const at::Tensor& x, const at::Tensor& y, const at::Tensor& dy, const at::Tensor& dx,
             const c10::optional<at::Tensor>& dres, const c10::optional<at::Tensor>& gamma,
             const at::Tensor& save_mean, const at::Tensor& save_invstd, const at::Tensor& ws,
-            const c10::optional<at::Tensor>& dgamma, const c10::optional<at::Tensor>& dbeta, bool relu) {
+            const c10::optional<at::Tensor>& dgamma, const c10::optional<at::Tensor>& dbeta, bool relu,
+            const c10::optional<at::Tensor>& mask) {
   check_dev(x, at::kBFloat16, "x");
   check_dev(dy, at::kBFloat16, "dy");
   check_dev(dx, at::kBFloat16, "dx");
@@ -860,6 +866,11 @@ void bn_bwd(const at::Tensor& x, const at::Tensor& y, const at::Tensor& dy, cons
   a.M = (int)M;
   a.C = (int)C;
   a.relu = relu ? 1 : 0;
+  if (mask.has_value()) {  // relu'(y) from the forward's bit mask instead of y
+    check_dev(*mask, at::kByte, "mask");
+    TORCH_CHECK(relu && mask->is_contiguous() && mask->numel() == M * C / 8, "bn_bwd: mask needs relu, [M][C/8]");
+    a.mask = mask->data_ptr<uint8_t>();
+  }
   uint16_t* dr = nullptr;
   if (dres.has_value()) {
     check_dev(*dres, at::kBFloat16, "dres");
@@ -1084,12 +1095,12 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_fwd", &bn_fwd, py::arg("x"), py::arg("y"), py::arg("residual"), py::arg("gamma"), py::arg("beta"),
         py::arg("running_mean"), py::arg("running_var"), py::arg("save_mean"), py::arg("save_invstd"),
         py::arg("ws"), py::arg("eps"), py::arg("momentum"), py::arg("training"), py::arg("relu"),
-        py::arg("num_batches") = py::none(), py::arg("stats_ready") = false);
+        py::arg("num_batches") = py::none(), py::arg("stats_ready") = false, py::arg("mask") = py::none());
   m.def("bn_workspace_floats", &ldnn::bn_workspace_floats, "fp32 workspace of one BatchNorm (zero it once, keep it)",
         py::arg("C"));
   m.def("bn_bwd", &bn_bwd, py::arg("x"), py::arg("y"), py::arg("dy"), py::arg("dx"), py::arg("dres"),
         py::arg("gamma"), py::arg("save_mean"), py::arg("save_invstd"), py::arg("ws"), py::arg("dgamma"),
-        py::arg("dbeta"), py::arg("relu"));
+        py::arg("dbeta"), py::arg("relu"), py::arg("mask") = py::none());
   m.def("pool_fwd", &pool_fwd);
   m.def("pool_bwd", &pool_bwd);
   m.def("gap_fwd", &gap_fwd);

@@ -150,6 +150,8 @@ struct BnArgs {
   float eps, momentum;
   int training, relu;
   int64_t* num_batches;       // optional BatchNorm2d.num_batches_tracked, += 1 per training forward
+  uint8_t* mask;              // optional [M][C/8] ReLU bits: written by a relu forward, read by the
+                              // backward instead of y (1/16 of y's bytes per read)
 };
 int bn_workspace_floats(int C);
 hipError_t bn_forward(const BnArgs& a, hipStream_t s);

@@ -58,19 +58,24 @@ RedGeo red_geo(int M, int C) {
   return g;
 }
 
-template <bool BWD, bool RELU>
+// RELU: g = dy * relu'(y); MASK: relu'(y) from the forward's bit mask (mask + o / 8)
+template <bool BWD, bool RELU, bool MASK = false>
 __device__ __forceinline__ void red_row(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
                                         const bf16_t* __restrict__ y, size_t o, const float (&mu)[8],
-                                        const float (&is)[8], float (&s0)[8], float (&s1)[8]) {
+                                        const float (&is)[8], float (&s0)[8], float (&s1)[8],
+                                        const uint8_t* __restrict__ mask = nullptr) {
   const u16x8 xv = *reinterpret_cast<const u16x8*>(x + o);
   if constexpr (BWD) {
     const u16x8 gv = *reinterpret_cast<const u16x8*>(dy + o);
     u16x8 yv;
-    if constexpr (RELU) yv = *reinterpret_cast<const u16x8*>(y + o);
+    uint32_t mb = 0;
+    if constexpr (RELU && MASK) mb = mask[o >> 3];
+    else if constexpr (RELU) yv = *reinterpret_cast<const u16x8*>(y + o);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float g = bf2f(gv[j]);
-      if constexpr (RELU) g = bf2f(yv[j]) > 0.f ? g : 0.f;
+      if constexpr (RELU && MASK) g = ((mb >> j) & 1u) ? g : 0.f;
+      else if constexpr (RELU) g = bf2f(yv[j]) > 0.f ? g : 0.f;
       s0[j] += g;
       s1[j] += g * (bf2f(xv[j]) - mu[j]) * is[j];
     }
@@ -84,11 +89,12 @@ __device__ __forceinline__ void red_row(const bf16_t* __restrict__ x, const bf16
   }
 }
 
-template <bool BWD, bool RELU>
+template <bool BWD, bool RELU, bool MASK = false>
 __global__ __launch_bounds__(256) void bn_reduce_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
                                                         const bf16_t* __restrict__ y, const float* __restrict__ mean,
                                                         const float* __restrict__ invstd, float* __restrict__ acc,
-                                                        int M, int C, int rpb, int lanes, int rl, BnFin fin) {
+                                                        int M, int C, int rpb, int lanes, int rl, BnFin fin,
+                                                        const uint8_t* __restrict__ mask = nullptr) {
   __shared__ float red[2][256 * 8];
   const int tid = threadIdx.x, lane = tid % lanes, rlane = tid / lanes;
   const int cv0 = blockIdx.x * 256 + lane;
@@ -114,9 +120,10 @@ __global__ __launch_bounds__(256) void bn_reduce_kernel(const bf16_t* __restrict
     int r = blockIdx.y * rpb + rlane;
     for (; r + 3 * rl < r_end; r += 4 * rl) {
 #pragma unroll
-      for (int u = 0; u < 4; ++u) red_row<BWD, RELU>(x, dy, y, (size_t)(r + u * rl) * C + c0, mu, is, s0, s1);
+      for (int u = 0; u < 4; ++u)
+        red_row<BWD, RELU, MASK>(x, dy, y, (size_t)(r + u * rl) * C + c0, mu, is, s0, s1, mask);
     }
-    for (; r < r_end; r += rl) red_row<BWD, RELU>(x, dy, y, (size_t)r * C + c0, mu, is, s0, s1);
+    for (; r < r_end; r += rl) red_row<BWD, RELU, MASK>(x, dy, y, (size_t)r * C + c0, mu, is, s0, s1, mask);
   }
   const int row = lanes * 8;
   if (rlane < rl) {
@@ -161,11 +168,12 @@ __device__ __forceinline__ void load8(const float* p, float (&v)[8]) {
 }
 
 // y = relu?( x * scale[c] + shift[c] (+ res) ) -- same fixed-channel geometry
-template <bool RES, bool RELU>
+template <bool RES, bool RELU, bool MASK = false>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
                                                        const float* __restrict__ scale,
                                                        const float* __restrict__ shift, bf16_t* __restrict__ y,
-                                                       int M, int C, int rpb, int lanes, int rl) {
+                                                       int M, int C, int rpb, int lanes, int rl,
+                                                       uint8_t* __restrict__ mask = nullptr) {
   const int tid = threadIdx.x, lane = tid % lanes, rlane = tid / lanes;
   const int c0 = (blockIdx.x * 256 + lane) * 8;
   if (rlane >= rl || c0 >= C) return;
@@ -188,17 +196,23 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict_
       out[j] = f2bf(v);
     }
     *reinterpret_cast<u16x8*>(y + o) = out;
+    if constexpr (RELU && MASK) {
+      uint32_t mb = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) mb |= (bf2f(out[j]) > 0.f ? 1u : 0u) << j;
+      mask[o >> 3] = (uint8_t)mb;
+    }
   }
 }
 
 // dx = A g + B x + D, g = dy * relu'(y); dres = g (the residual branch's gradient)
-template <bool RELU>
+template <bool RELU, bool MASK = false>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16_t* __restrict__ x,
                                                            const bf16_t* __restrict__ dy,
                                                            const bf16_t* __restrict__ y,
                                                            const float* __restrict__ coef, bf16_t* __restrict__ dx,
                                                            bf16_t* __restrict__ dres, int M, int C, int rpb,
-                                                           int lanes, int rl) {
+                                                           int lanes, int rl, const uint8_t* __restrict__ mask = nullptr) {
   const int tid = threadIdx.x, lane = tid % lanes, rlane = tid / lanes;
   const int c0 = (blockIdx.x * 256 + lane) * 8;
   if (rlane >= rl || c0 >= C) return;
@@ -213,12 +227,15 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16_t* __restr
     const u16x8 xv = *reinterpret_cast<const u16x8*>(x + o);
     const u16x8 gv = *reinterpret_cast<const u16x8*>(dy + o);
     u16x8 yv;
-    if constexpr (RELU) yv = *reinterpret_cast<const u16x8*>(y + o);
+    uint32_t mb = 0;
+    if constexpr (RELU && MASK) mb = mask[o >> 3];
+    else if constexpr (RELU) yv = *reinterpret_cast<const u16x8*>(y + o);
     u16x8 out, og;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float g = bf2f(gv[j]);
-      if constexpr (RELU) g = bf2f(yv[j]) > 0.f ? g : 0.f;
+      if constexpr (RELU && MASK) g = ((mb >> j) & 1u) ? g : 0.f;
+      else if constexpr (RELU) g = bf2f(yv[j]) > 0.f ? g : 0.f;
       out[j] = f2bf(A[j] * g + B[j] * bf2f(xv[j]) + D[j]);
       og[j] = f2bf(g);
     }
@@ -404,14 +421,18 @@ hipError_t bn_forward_apply(const BnArgs& a, hipStream_t s) {
   const dim3 grid(g.gx, g.gy);
   const float* sc = a.ws;
   const float* sh = a.ws + C;
-#define LDNN_BN_APPLY(RES, RELU) \
-  bn_apply_kernel<RES, RELU><<<grid, 256, 0, s>>>(a.x, a.residual, sc, sh, a.y, M, C, g.rpb, g.lanes, g.rl)
+#define LDNN_BN_APPLY(RES, RELU, MASK)                                                                  \
+  bn_apply_kernel<RES, RELU, MASK><<<grid, 256, 0, s>>>(a.x, a.residual, sc, sh, a.y, M, C, g.rpb, g.lanes, g.rl, \
+                                                        a.mask)
+  const bool mk = a.relu && a.mask != nullptr;
   if (a.residual) {
-    if (a.relu) LDNN_BN_APPLY(true, true);
-    else LDNN_BN_APPLY(true, false);
+    if (mk) LDNN_BN_APPLY(true, true, true);
+    else if (a.relu) LDNN_BN_APPLY(true, true, false);
+    else LDNN_BN_APPLY(true, false, false);
   } else {
-    if (a.relu) LDNN_BN_APPLY(false, true);
-    else LDNN_BN_APPLY(false, false);
+    if (mk) LDNN_BN_APPLY(false, true, true);
+    else if (a.relu) LDNN_BN_APPLY(false, true, false);
+    else LDNN_BN_APPLY(false, false, false);
   }
 #undef LDNN_BN_APPLY
   return hipGetLastError();
@@ -450,13 +471,19 @@ hipError_t bn_backward(const BnArgs& a, const uint16_t* dy, uint16_t* dx, uint16
   f.coef = a.ws + 6 * C;
   f.dgamma = dgamma;
   f.dbeta = dbeta;
-  if (a.relu)
+  if (a.relu && a.mask)
+    bn_reduce_kernel<true, true, true><<<grid, 256, 0, s>>>(a.x, dy, nullptr, a.save_mean, a.save_invstd, f.acc, M,
+                                                            C, g.rpb, g.lanes, g.rl, f, a.mask);
+  else if (a.relu)
     bn_reduce_kernel<true, true><<<grid, 256, 0, s>>>(a.x, dy, a.y, a.save_mean, a.save_invstd, f.acc, M, C, g.rpb,
                                                       g.lanes, g.rl, f);
   else
     bn_reduce_kernel<true, false><<<grid, 256, 0, s>>>(a.x, dy, nullptr, a.save_mean, a.save_invstd, f.acc, M, C,
                                                        g.rpb, g.lanes, g.rl, f);
-  if (a.relu)
+  if (a.relu && a.mask)
+    bn_bwd_apply_kernel<true, true><<<grid, 256, 0, s>>>(a.x, dy, nullptr, f.coef, dx, dres, M, C, g.rpb, g.lanes,
+                                                         g.rl, a.mask);
+  else if (a.relu)
     bn_bwd_apply_kernel<true><<<grid, 256, 0, s>>>(a.x, dy, a.y, f.coef, dx, dres, M, C, g.rpb, g.lanes, g.rl);
   else
     bn_bwd_apply_kernel<false><<<grid, 256, 0, s>>>(a.x, dy, nullptr, f.coef, dx, dres, M, C, g.rpb, g.lanes, g.rl);

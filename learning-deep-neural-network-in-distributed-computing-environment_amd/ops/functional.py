@@ -375,18 +375,23 @@ class _BatchNormNative(torch.autograd.Function):
         gamma = flat.master_storage(weight)[:C] if weight is not None else None
         beta = flat.master_storage(bias)[:C] if bias is not None else None
         training = mod.training or not mod.track_running_stats
+        # ReLU as a bit mask for the backward (its reduce and apply passes read 1/16 of
+        # y's bytes); only when a backward will run
+        mask = (torch.empty(x2.shape[0] * C // 8, dtype=torch.uint8, device=dev)
+                if relu and any(ctx.needs_input_grad) and BN_RELU_MASK else None)
         pre = mod.__dict__.pop("_ldnn_pre", None)
         if pre is not None and mod.training and pre[0] == x2.data_ptr():
             # statistics already accumulated + finalized by the producing conv's epilogue
             smean, sinv = pre[1], pre[2]
             C_.bn_fwd(x2, y.view(-1, C), r2, gamma, beta, None, None, smean, sinv, ws, mod.eps, 0.0, True, relu,
-                      None, stats_ready=True)
+                      None, stats_ready=True, mask=mask)
         else:
             rm, rv, mom, nbt = _bn_train_state(mod, dev)
             C_.bn_fwd(x2, y.view(-1, C), r2, gamma, beta, rm if (training and mod.training) or not training else None,
                       rv if (training and mod.training) or not training else None, smean, sinv, ws, mod.eps,
-                      mom or 0.0, training, relu, nbt)
-        ctx.save_for_backward(x2, y, smean, sinv)
+                      mom or 0.0, training, relu, nbt, mask=mask)
+        ctx.mask = mask
+        ctx.save_for_backward(x2, y if mask is None else x2.new_empty(0), smean, sinv)
         ctx.meta = (flat, weight, bias, relu, residual is not None, ws, (N, C, H, W), x.dtype)
         return nchw_view(y, C)
 
@@ -402,14 +407,21 @@ class _BatchNormNative(torch.autograd.Function):
         gamma = flat.master_storage(weight)[:C] if weight is not None else None
         dg = flat.grad_storage(weight)[:C] if weight is not None else None
         db = flat.grad_storage(bias)[:C] if bias is not None else None
-        C_.bn_bwd(x2, y.view(-1, C), g2, dx.view(-1, C), dres.view(-1, C) if dres is not None else None, gamma,
-                  smean, sinv, ws, dg, db, relu)
+        mask = ctx.mask
+        yv = y.view(-1, C) if mask is None else x2   # (y is not read when the mask is given)
+        C_.bn_bwd(x2, yv, g2, dx.view(-1, C), dres.view(-1, C) if dres is not None else None, gamma,
+                  smean, sinv, ws, dg, db, relu, mask=mask)
         flat.notify(weight, bias)
         dxv = nchw_view(dx, C)
         dresv = nchw_view(dres, C) if dres is not None else None
         if in_dtype != torch.bfloat16:
             dxv = dxv.to(in_dtype)
         return dxv, None, None, dresv, None, None, None
+
+
+# BatchNorm + ReLU keeps a bit mask of the output for its backward (measured A/B in
+# profiles/, LDNN_BN_RELU_MASK=0 reads the bf16 output instead)
+BN_RELU_MASK = __import__("os").environ.get("LDNN_BN_RELU_MASK", "1") != "0"
 
 
 def batch_norm_act(x, mod, residual=None, relu: bool = False):

@@ -833,6 +833,35 @@ class StaticMLPEngine:
             w.wait()
             oseg()
 
+    def describe(self) -> dict:
+        """Which kernel runs each GEMM of the step (bench.py reports it)."""
+        L, d = len(self.layers), {}
+        for l in range(L):
+            if self.use_head and l == L - 1:
+                d[f"fwd{l}"] = "ldnn head_fwd_xent (Linear + softmax-xent + argmax)"
+                d[f"wgrad{l}"] = "ldnn head_wgrad"
+                if self.head_dgrad:
+                    d[f"dgrad{l}"] = ("ldnn head_dgrad_stream (dReLU + bias-gradient sums)" if self.head_dgrad_mode in
+                                      (-1, 0) else "ldnn head_fwd_xent fused dgrad")
+                continue
+            d[f"fwd{l}"] = ("hipBLASLt" if self._lib_fwd[l] else
+                            "ldnn gemm_q (bias+ReLU" + (" + ReLU bit mask" if self.mask[l + 1] is not None else "")
+                            + " epilogue)")
+            if self._lib_wgrad[l]:
+                d[f"wgrad{l}"] = "hipBLASLt"
+            elif self._wgrad_slab[l] is not None:
+                d[f"wgrad{l}"] = (f"ldnn gemm_q split-K x{self._wgrad_splitk[l]} slabs + slab_sum"
+                                  + (" (+ bias grad from a ones column)" if l == 0 and self._db0_from_wgrad else ""))
+            else:
+                d[f"wgrad{l}"] = "ldnn gemm" + (f" split-K x{self._wgrad_splitk[l]}" if self._wgrad_splitk[l] > 1 else "")
+            if l > 0:
+                d[f"dgrad{l}"] = ("hipBLASLt + act_bwd_colsum" if self._lib_dgrad[l] else
+                                  "ldnn gemm_q" + (" on transposed W" if self.Wt[l] is not None else "")
+                                  + (" (dReLU from bit mask)" if self.mask[l] is not None else " (fused derivative)"))
+        d["optimizer"] = f"ldnn fused {self.optim.name} (flat fp32 master + bf16 shadow)"
+        d["library_gemms"] = sum(v.startswith("hipBLASLt") for v in d.values())
+        return d
+
     @torch.no_grad()
     def optimizer_state(self) -> dict:
         """Whole optimizer state (momentum / Adam moments over the flat layout, Adam's

@@ -97,3 +97,25 @@ def test_global_avgpool():
     y.float().backward(g)
     yr.backward(g)
     torch.testing.assert_close(xb.grad.float(), xf.grad, rtol=2e-2, atol=2e-3)
+
+
+@pytest.mark.parametrize("residual", [False, True])
+def test_bn_relu_mask_matches_reading_y(residual, monkeypatch):
+    """BN + ReLU backward from the forward's bit mask == from the bf16 output (bitwise)."""
+    torch.manual_seed(1)
+    N, C, H, W = 4, 128, 8, 8
+    outs = []
+    for use_mask in (True, False):
+        monkeypatch.setattr(LF, "BN_RELU_MASK", use_mask)
+        torch.manual_seed(1)
+        bn = BatchNorm2d(C)
+        ldnn.prepare(bn, "cuda")
+        x = _cl(torch.randn(N, C, H, W, device="cuda")).requires_grad_(True)
+        r = _cl(torch.randn(N, C, H, W, device="cuda")).requires_grad_(True) if residual else None
+        y = bn.act(x, r, True)
+        y.float().backward(torch.linspace(-1, 1, y.numel(), device="cuda").view_as(y))
+        outs.append((y.detach().clone(), x.grad.clone(), bn.weight.grad.clone(), bn.bias.grad.clone(),
+                     r.grad.clone() if residual else None))
+    for a, b in zip(*outs):
+        if a is not None:
+            torch.testing.assert_close(a, b, rtol=1e-6, atol=1e-6)
