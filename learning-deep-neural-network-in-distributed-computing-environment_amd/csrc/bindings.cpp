@@ -458,7 +458,9 @@ void head_fwd_xent(const at::Tensor& h, const at::Tensor& W, const at::Tensor& b
                    const c10::optional<at::Tensor>& logits, const at::Tensor& dlogits, const at::Tensor& stats,
                    int64_t num_classes, double grad_scale, const c10::optional<at::Tensor>& dh,
                    const c10::optional<at::Tensor>& dbias, int64_t dgrad_epi,
-                   const c10::optional<at::Tensor>& dbias_ws, int64_t dgrad_mode) {
+                   const c10::optional<at::Tensor>& dbias_ws, int64_t dgrad_mode,
+                   const c10::optional<at::Tensor>& dw, const c10::optional<at::Tensor>& db_head,
+                   const c10::optional<at::Tensor>& dw_ws) {
   check_dev(h, at::kBFloat16, "h");
   check_dev(W, at::kBFloat16, "W");
   check_dev(bias, at::kFloat, "bias");
@@ -503,10 +505,27 @@ void head_fwd_xent(const at::Tensor& h, const at::Tensor& W, const at::Tensor& b
                     dh->stride(0) % 8 == 0 && aligned16(dh->data_ptr()),
                 "head: dh must be [B][K] with 16-B aligned rows");
     if (dgrad_mode < 0) dgrad_mode = ld == 16 ? 0 : 1;  // auto: the streaming dgrad where it applies
-    TORCH_CHECK(dgrad_mode >= 0 && dgrad_mode <= 2, "head: dgrad_mode must be -1 (auto), 0, 1 or 2");
-    TORCH_CHECK(dgrad_mode != 0 || ld == 16, "head: the streaming dgrad (mode 0) needs ld == 16");
-    TORCH_CHECK(dgrad_mode == 0 || K <= ldnn::head_dgrad_max_k(), "head: fused dgrad needs K <= ",
+    TORCH_CHECK(dgrad_mode >= 0 && dgrad_mode <= 3, "head: dgrad_mode must be -1 (auto), 0, 1, 2 or 3");
+    TORCH_CHECK((dgrad_mode != 0 && dgrad_mode != 3) || ld == 16, "head: the streaming dgrad (mode 0 / 3) needs ld == 16");
+    TORCH_CHECK(dgrad_mode == 0 || dgrad_mode == 3 || K <= ldnn::head_dgrad_max_k(), "head: fused dgrad needs K <= ",
                 ldnn::head_dgrad_max_k());
+    if (dgrad_mode == 3) {  // + the head's own weight / bias gradients from the same pass over h
+      TORCH_CHECK(dw.has_value() && dw_ws.has_value(), "head: mode 3 needs dw and dw_ws");
+      check_dev(*dw, at::kFloat, "dw");
+      check_dev(*dw_ws, at::kFloat, "dw_ws");
+      TORCH_CHECK(dw->dim() == 2 && dw->is_contiguous() && dw->size(1) == K && dw->size(0) == W.size(0) &&
+                      aligned16(dw->data_ptr()), "head: dw must be a dense [W rows][K] fp32 tensor");
+      TORCH_CHECK(dw_ws->is_contiguous() && dw_ws->numel() >= (int64_t)ldnn::head_dw_splits((int)B) * 16 * K &&
+                      aligned16(dw_ws->data_ptr()), "head: dw_ws too small (head_dw_splits(B) x 16 x K)");
+      p.dw = dw->data_ptr<float>();
+      p.dw_ws = dw_ws->data_ptr<float>();
+      p.lddw = (int)K;
+      if (db_head.has_value()) {
+        check_dev(*db_head, at::kFloat, "db_head");
+        TORCH_CHECK(db_head->is_contiguous() && db_head->numel() >= W.size(0), "head: bad db_head");
+        p.db_head = db_head->data_ptr<float>();
+      }
+    }
     p.dgrad_mode = (int)dgrad_mode;
     TORCH_CHECK(dgrad_epi == ldnn::EPI_NONE || dgrad_epi == ldnn::EPI_DRELU || dgrad_epi == ldnn::EPI_DSIGMOID,
                 "head: dgrad_epi must be EPI_NONE / EPI_DRELU / EPI_DSIGMOID");
@@ -518,7 +537,7 @@ void head_fwd_xent(const at::Tensor& h, const at::Tensor& W, const at::Tensor& b
       TORCH_CHECK(dbias->is_contiguous() && dbias->numel() >= K && aligned16(dbias->data_ptr()),
                   "head: dbias must hold K floats, 16-B aligned");
       p.dbias = dbias->data_ptr<float>();
-      if (dgrad_mode != 0) {  // the fused modes reduce per-workgroup slabs
+      if (dgrad_mode == 1 || dgrad_mode == 2) {  // the fused modes reduce per-workgroup slabs
         TORCH_CHECK(dbias_ws.has_value(), "head: dbias needs dbias_ws (head_dgrad_ws_floats(B, K) fp32)");
         check_dev(*dbias_ws, at::kFloat, "dbias_ws");
         TORCH_CHECK(dbias_ws->is_contiguous() &&
@@ -1086,8 +1105,10 @@ PYBIND11_MODULE(_C, m) {
         py::arg("h"), py::arg("W"), py::arg("bias"), py::arg("labels"), py::arg("logits"), py::arg("dlogits"),
         py::arg("stats"), py::arg("num_classes"), py::arg("grad_scale"), py::arg("dh") = py::none(), py::arg("dbias") = py::none(),
         py::arg("dgrad_epi") = (int64_t)ldnn::EPI_DRELU, py::arg("dbias_ws") = py::none(),
-        py::arg("dgrad_mode") = (int64_t)-1);
+        py::arg("dgrad_mode") = (int64_t)-1, py::arg("dw") = py::none(), py::arg("db_head") = py::none(),
+        py::arg("dw_ws") = py::none());
   m.def("head_dgrad_ws_floats", &ldnn::head_dgrad_ws_floats, py::arg("B"), py::arg("K"));
+  m.def("head_dw_splits", &ldnn::head_dw_splits, py::arg("B"));
   m.def("head_wgrad", &head_wgrad, "dW = dz^T h (+ db = colsum dz); splits > 1 accumulate atomically",
         py::arg("dz"), py::arg("h"), py::arg("dW"), py::arg("db") = py::none(), py::arg("splits") = 0);
   m.def("head_dgrad_max_k", &ldnn::head_dgrad_max_k);

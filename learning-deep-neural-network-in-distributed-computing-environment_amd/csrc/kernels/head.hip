@@ -39,6 +39,8 @@
 //                  (hardware transpose) into MFMA fragments.  64 output
 //                  columns x a batch slice per workgroup; slices combine with
 //                  fp32 atomics into the (pre-cleared) gradient.
+#include <algorithm>
+
 #include "ldnn_common.h"
 #include "ldnn_gemm_tile.h"
 #include "ldnn_kernels.h"
@@ -477,6 +479,115 @@ __global__ __launch_bounds__(256) void head_dgrad_stream_kernel(HeadParams p, in
   }
 }
 
+// Mode 3: the streaming dgrad fused with the head's wgrad -- ONE pass over h produces
+// dh = (dlogits W) * act'(h) (+ its column sums = the previous layer's bias gradient) AND
+// the head's dW = dlogits^T h (+ db_head = column sums of dlogits), instead of the dgrad
+// stream and head_wgrad each reading h (128 MB at batch 16384 x 4096).  A thread owns 4
+// columns and walks rows 4 apart (a wave = one 512-B row run): per row 16 x 4 FMAs for
+// dh and 16 x 4 for dW, both accumulated in registers; the workgroup's four waves fold
+// their dW partials with LDS float atomics and write one [16][256] fp32 slab per
+// workgroup row-slice, summed by slab_sum into dW (deterministic, no global atomics).
+constexpr int kDwSplits = 32;
+
+template <int DEPI>
+__global__ __launch_bounds__(256) void head_stream_dw_kernel(HeadParams p, int rows_per_block) {
+  __shared__ float pdw[16][256];
+  __shared__ float pdb[4][256];
+  __shared__ float pdl[16];
+  const int cg = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int c0 = (blockIdx.x * 64 + cg) * 4;
+  const int r_begin = blockIdx.y * rows_per_block;
+  const int r_end = min(p.B, r_begin + rows_per_block);
+  const bool cok = c0 < p.K;
+  for (int i = threadIdx.x; i < 16 * 256; i += 256) (&pdw[0][0])[i] = 0.f;
+  if (threadIdx.x < 16) pdl[threadIdx.x] = 0.f;
+  float wf[16][4], acc[16][4], dls[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+    u16x4 w = {};
+    if (cok && c < p.ldw_rows) w = *reinterpret_cast<const u16x4*>(p.W + (size_t)c * p.ldw + c0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      wf[c][i] = bf2f(w[i]);
+      acc[c][i] = 0.f;
+    }
+    dls[c] = 0.f;
+  }
+  float s[4] = {0.f, 0.f, 0.f, 0.f};
+  __syncthreads();
+  if (cok) {
+#pragma unroll 2
+    for (int r = r_begin + ty; r < r_end; r += 4) {
+      const u16x8* gp = reinterpret_cast<const u16x8*>(p.dlogits + (size_t)r * p.ld);
+      const u16x8 g0 = gp[0], g1 = gp[1];
+      const u16x4 hv = *reinterpret_cast<const u16x4*>(p.h + (size_t)r * p.ldh + c0);
+      float hf[4], v[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) hf[i] = bf2f(hv[i]);
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        const float gc = bf2f(c < 8 ? g0[c] : g1[c - 8]);  // padded classes hold 0
+        dls[c] += gc;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          v[i] = fmaf(gc, wf[c][i], v[i]);
+          acc[c][i] = fmaf(gc, hf[i], acc[c][i]);
+        }
+      }
+      u16x4 o;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float x = v[i];
+        if constexpr (DEPI == EPI_DRELU) x = hf[i] > 0.f ? x : 0.f;
+        else if constexpr (DEPI == EPI_DSIGMOID) x *= hf[i] * (1.f - hf[i]);
+        o[i] = f2bf(x);
+        s[i] += bf2f(o[i]);
+      }
+      *reinterpret_cast<u16x4*>(p.dh + (size_t)r * p.lddh + c0) = o;
+    }
+  }
+  // fold the 4 waves' partials
+#pragma unroll
+  for (int c = 0; c < 16; ++c)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) atomicAdd(&pdw[c][cg * 4 + i], acc[c][i]);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) pdb[ty][cg * 4 + i] = s[i];
+  if (blockIdx.x == 0 && cg == 0) {
+#pragma unroll
+    for (int c = 0; c < 16; ++c) atomicAdd(&pdl[c], dls[c]);
+  }
+  __syncthreads();
+  // slab [blockIdx.y][16][K]: row c of this workgroup's 256 columns
+  float* slab = p.dw_ws + (size_t)blockIdx.y * 16 * p.K;
+  for (int q = threadIdx.x; q < 16 * 64; q += 256) {
+    const int c = q >> 6, col = (q & 63) * 4;
+    if (blockIdx.x * 256 + col < p.K)
+      *reinterpret_cast<floatx4*>(slab + (size_t)c * p.K + blockIdx.x * 256 + col) =
+          *reinterpret_cast<const floatx4*>(&pdw[c][col]);
+  }
+  if (p.dbias != nullptr) {
+    const int col = threadIdx.x;
+    if (blockIdx.x * 256 + col < p.K)
+      atomicAdd(p.dbias + blockIdx.x * 256 + col, pdb[0][col] + pdb[1][col] + pdb[2][col] + pdb[3][col]);
+  }
+  if (p.db_head != nullptr && blockIdx.x == 0 && threadIdx.x < 16 && threadIdx.x < p.ldw_rows)
+    atomicAdd(p.db_head + threadIdx.x, pdl[threadIdx.x]);
+}
+
+template <int DEPI>
+hipError_t launch_head_stream_dw(const HeadParams& p, hipStream_t s) {
+  const int gx = (p.K + 255) / 256;
+  const int gy = head_dw_splits(p.B);
+  const int rpb = (p.B + gy - 1) / gy;
+  head_stream_dw_kernel<DEPI><<<dim3(gx, gy), 256, 0, s>>>(p, rpb);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  // dW rows (16 padded classes) = sum of the gy slabs
+  if (p.lddw == p.K) return slab_sum(p.dw_ws, p.dw, (int64_t)p.ldw_rows * p.K / 4, gy, 0.f, s);
+  return hipErrorInvalidValue;
+}
+
 template <int DEPI>
 hipError_t launch_head_dgrad_stream(const HeadParams& p, hipStream_t s) {
   const int gx = (p.K + 255) / 256;
@@ -506,6 +617,11 @@ hipError_t launch_head_fwd_dg(const HeadParams& p, hipStream_t s) {
 
 template <int DEPI>
 hipError_t head_dgrad_dispatch(const HeadParams& p, hipStream_t s) {
+  if (p.dgrad_mode == 3) {  // forward-only head kernel, then the fused dgrad + wgrad stream
+    hipError_t e = launch_head_fwd<-1, false>(p, s);
+    if (e != hipSuccess) return e;
+    return launch_head_stream_dw<DEPI>(p, s);
+  }
   if (p.dgrad_mode == 0) {  // streaming: forward-only head kernel, then the dgrad stream
     hipError_t e = launch_head_fwd<-1, false>(p, s);
     if (e != hipSuccess) return e;
@@ -525,8 +641,13 @@ hipError_t head_fwd_xent(const HeadParams& p, hipStream_t s) {
   if (p.ld > 64 || p.ld % 16 != 0 || p.C > p.ld || p.ldw_rows > p.ld || p.K % 8 != 0) return hipErrorInvalidValue;
   if (p.dh == nullptr) return launch_head_fwd<-1, false>(p, s);
   if (p.lddh % 8 != 0) return hipErrorInvalidValue;
-  if (p.dgrad_mode < 0 || p.dgrad_mode > 2 || (p.dgrad_mode == 0 && p.ld != 16)) return hipErrorInvalidValue;
-  if (p.dgrad_mode != 0 && (p.K > kHeadDgradMaxK || (p.dbias != nullptr && p.dbias_ws == nullptr)))
+  if (p.dgrad_mode < 0 || p.dgrad_mode > 3 || ((p.dgrad_mode == 0 || p.dgrad_mode == 3) && p.ld != 16))
+    return hipErrorInvalidValue;
+  if (p.dgrad_mode == 3 && (p.dw_ws == nullptr || p.dw == nullptr || p.lddw != p.K || p.K % 4 != 0 ||
+                            p.ldw_rows > 16 || p.ldw % 4 != 0 || p.ldh % 4 != 0 || p.lddh % 4 != 0))
+    return hipErrorInvalidValue;
+  if ((p.dgrad_mode == 1 || p.dgrad_mode == 2) &&
+      (p.K > kHeadDgradMaxK || (p.dbias != nullptr && p.dbias_ws == nullptr)))
     return hipErrorInvalidValue;
   switch (p.dgrad_epi) {
     case EPI_NONE: return head_dgrad_dispatch<EPI_NONE>(p, s);
@@ -537,6 +658,8 @@ hipError_t head_fwd_xent(const HeadParams& p, hipStream_t s) {
 }
 
 size_t head_dgrad_ws_floats(int B, int K) { return (size_t)((B + 15) / 16) * K; }
+
+int head_dw_splits(int B) { return std::max(1, std::min(kDwSplits, (B + 127) / 128)); }
 
 int head_dgrad_max_k() { return kHeadDgradMaxK; }
 

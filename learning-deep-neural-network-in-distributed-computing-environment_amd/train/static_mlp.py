@@ -101,7 +101,7 @@ class StaticMLPEngine:
                  fuse_head_dgrad: bool | None = None, early_optimizer: bool | None = None,
                  library_dgrad: bool | None = None, concurrent_wgrad: bool = False, pad_input: bool = False,
                  head_dgrad_mode: int = -1, relu_masks: bool = True, wgrad_slabs: bool = True,
-                 transposed_dgrad: bool = True, bias_ones_column: bool = True):
+                 transposed_dgrad: bool = True, bias_ones_column: bool = True, fuse_head_wgrad: bool = True):
         from ..models.mlp import MLP
 
         if not isinstance(model, MLP):
@@ -204,10 +204,19 @@ class StaticMLPEngine:
         # into the head kernel (h re-read from global / staged in LDS)
         self.head_dgrad_mode = int(head_dgrad_mode)
         self.head_dgrad = (bool(fuse_head_dgrad) and self.use_head and L >= 2
-                           and (npad[-1] == 16 and self.head_dgrad_mode in (-1, 0)
+                           and (npad[-1] == 16 and self.head_dgrad_mode in (-1, 0, 3)
                                 or self.layers[-1].in_features <= self.C.head_dgrad_max_k()))
         self._head_db_ws = (torch.empty(self.C.head_dgrad_ws_floats(B, self.layers[-1].in_features),
                                         dtype=torch.float32, device=self.device) if self.head_dgrad else None)
+        # fuse_head_wgrad (streaming head dgrad, <= 16 classes): the dgrad stream also
+        # produces the head's dW / db from the same pass over h_{L-1} (head.hip mode 3):
+        # one read of the 128 MB activation instead of two (dgrad stream + head_wgrad)
+        self.head_dw = (fuse_head_wgrad and self.head_dgrad and npad[-1] == 16 and self.head_dgrad_mode in (-1, 0, 3)
+                        and self.layers[-1].in_features % 4 == 0)
+        if self.head_dw:
+            self.head_dgrad_mode = 3
+            self._head_dw_ws = torch.empty(self.C.head_dw_splits(B) * 16 * self.layers[-1].in_features,
+                                           dtype=torch.float32, device=self.device)
         # [loss_sum, correct] -- one pair per 16-row workgroup of the head kernel
         nslots = (B + 15) // 16 if self.use_head else 1
         self.stats = torch.zeros(nslots, 2, dtype=torch.float32, device=dev)
@@ -301,8 +310,8 @@ class StaticMLPEngine:
             M, N = self.dW[l].shape
             self._wgrad_ws.append(None)
             self._wgrad_slab.append(None)
-            if self.use_head and l == L - 1:
-                self._wgrad_splitk.append(self.C.head_wgrad_splits(B, N))
+            if self.use_head and l == L - 1:   # (the fused head stream overwrites dW: no clearing)
+                self._wgrad_splitk.append(1 if self.head_dw else self.C.head_wgrad_splits(B, N))
                 continue
             if self._lib_wgrad[l]:   # overwrites the gradient: no clearing, no split-K
                 self._wgrad_splitk.append(1)
@@ -326,8 +335,10 @@ class StaticMLPEngine:
                         # batch of dz_1 = the first layer's bias gradient, in the free part of the
                         # last 256-wide tile; dgrad(1) then needs no bias-gradient sums (measured
                         # on MI355X: the dgrad epilogue's column sums + atomics cost 13-30 us)
+                        # (rows padded to a multiple of 64 elements: every row starts on a 128-B line)
                         Nw = N + 8
-                        self.xp = torch.zeros(B, Nw, dtype=bf, device=dev)
+                        self.xp_full = torch.zeros(B, (Nw + 63) // 64 * 64, dtype=bf, device=dev)
+                        self.xp = self.xp_full[:, :Nw]
                         self.xp[:, N] = 1.0
                         self.x = self.xp[:, :N]
                         self.h[0] = self.x
@@ -436,10 +447,11 @@ class StaticMLPEngine:
         L = len(self.layers)
         if self.use_head:   # last Linear + softmax-xent + argmax (+ the head's dgrad) in one launch
             if self.head_dgrad:
+                hw = dict(dw=self.dW[L - 1], db_head=self.db[L - 1], dw_ws=self._head_dw_ws) if self.head_dw else {}
                 self.C.head_fwd_xent(self.h[L - 1], self.W[L - 1], self.bias[L - 1], self.labels, self.h[L],
                                      self.dz[L], self.stats, self.num_classes, 1.0 / self.B, dh=self.dz[L - 1],
                                      dbias=self.db[L - 2], dgrad_epi=self._dgrad_epi[L - 1],
-                                     dbias_ws=self._head_db_ws, dgrad_mode=self.head_dgrad_mode)
+                                     dbias_ws=self._head_db_ws, dgrad_mode=self.head_dgrad_mode, **hw)
                 return
             self.C.head_fwd_xent(self.h[L - 1], self.W[L - 1], self.bias[L - 1], self.labels, self.h[L], self.dz[L],
                                  self.stats, self.num_classes, 1.0 / self.B)
@@ -451,6 +463,8 @@ class StaticMLPEngine:
     def _wgrad(self, l):
         sk = self._wgrad_splitk[l]
         if self.use_head and l == len(self.layers) - 1:   # also emits the head's bias gradient
+            if self.head_dw:   # already produced by the head's fused dgrad + wgrad stream
+                return
             self.C.head_wgrad(self.dz[l + 1], self.h[l], self.dW[l], self.db[l], sk)
             return
         if self._lib_wgrad[l]:   # plain GEMM, fp32 out: hipBLASLt straight into the flat grad buffer
@@ -840,7 +854,10 @@ class StaticMLPEngine:
             if self.use_head and l == L - 1:
                 d[f"fwd{l}"] = "ldnn head_fwd_xent (Linear + softmax-xent + argmax)"
                 d[f"wgrad{l}"] = "ldnn head_wgrad"
-                if self.head_dgrad:
+                if self.head_dw:
+                    d[f"wgrad{l}"] = d[f"dgrad{l}"] = ("ldnn head_stream_dw (dgrad + dReLU + bias sums + the head's "
+                                                       "dW / db in one pass over h)")
+                elif self.head_dgrad:
                     d[f"dgrad{l}"] = ("ldnn head_dgrad_stream (dReLU + bias-gradient sums)" if self.head_dgrad_mode in
                                       (-1, 0) else "ldnn head_fwd_xent fused dgrad")
                 continue
