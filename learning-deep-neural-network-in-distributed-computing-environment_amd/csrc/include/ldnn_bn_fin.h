@@ -9,16 +9,27 @@
 
 namespace ldnn {
 
-constexpr int kBnCopies = 8;  // accumulator copies of the conv-epilogue statistics path
+constexpr int kBnCopies = 8;  // accumulator copies of the BN statistics (conv epilogue and BN reduce)
 
 // Totals of every block are complete in `acc` when the last block draws its
 // ticket: the fp32 atomics execute at the memory side and every block waits
 // for its own (vmcnt) before adding to the ticket; the finalizer reads AND
 // clears the totals with atomic exchanges (memory-side too, so no cache can
-// hand it a stale line).
-// ncopies: the totals are spread over that many [2C] accumulator copies (summed here)
-template <bool BWD>
-__device__ __forceinline__ void bn_finalize_last(const BnFin& f, int M, int C, int nblk, int ncopies) {
+// hand it a stale line).  (Measured: making the contributions returning atomics
+// costs ~0.2 ms per ResNet-18 b64 step and changes no result beyond arrival-order
+// noise, profiles/cnn_bn_reduce_r2.jsonl.)
+// NCOP: the totals are spread over NCOP [2C] accumulator copies (contributors
+// pick copy `block % NCOP`, NCOP x less same-address serialisation at the
+// memory-side atomic units).  The finalizer sums the copies into the caller's LDS
+// scratch (`cap` floats, free once the caller's own reduction has been read)
+// with all NCOP exchanges of an element in flight together, then finalizes per
+// channel; with 2C > cap it sums the copies in the per-channel loop.  (The
+// scratch is the caller's: a static LDS array here would cost the conv kernels
+// that inline this occupancy.)
+__device__ __forceinline__ void bn_acc_add(float* p, float v) { atomicAdd(p, v); }
+
+template <bool BWD, int NCOP>
+__device__ __forceinline__ void bn_finalize_last(const BnFin& f, int M, int C, int nblk, float* tot, int cap) {
   __shared__ int last;
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -28,12 +39,31 @@ __device__ __forceinline__ void bn_finalize_last(const BnFin& f, int M, int C, i
   }
   __syncthreads();
   if (!last) return;
+  const bool lds = 2 * C <= cap;
+  if (lds) {
+    for (int i = threadIdx.x; i < 2 * C; i += blockDim.x) {
+      float v[NCOP];
+#pragma unroll
+      for (int k = 0; k < NCOP; ++k) v[k] = atomicExch(f.acc + (size_t)k * 2 * C + i, 0.f);
+      float t = 0.f;
+#pragma unroll
+      for (int k = 0; k < NCOP; ++k) t += v[k];
+      tot[i] = t;
+    }
+    __syncthreads();
+  }
   const float invM = 1.f / (float)M;
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
     float S0 = 0.f, S1 = 0.f;
-    for (int k = 0; k < ncopies; ++k) {
-      S0 += atomicExch(f.acc + (size_t)k * 2 * C + c, 0.f);
-      S1 += atomicExch(f.acc + (size_t)k * 2 * C + C + c, 0.f);
+    if (lds) {
+      S0 = tot[c];
+      S1 = tot[C + c];
+    } else {
+#pragma unroll
+      for (int k = 0; k < NCOP; ++k) {
+        S0 += atomicExch(f.acc + (size_t)k * 2 * C + c, 0.f);
+        S1 += atomicExch(f.acc + (size_t)k * 2 * C + C + c, 0.f);
+      }
     }
     const float gm = f.gamma ? f.gamma[c] : 1.f;
     if constexpr (!BWD) {

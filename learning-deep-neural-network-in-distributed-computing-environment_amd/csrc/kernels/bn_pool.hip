@@ -13,6 +13,7 @@
 // dx = A g + B x + D, A = gamma*invstd, B = -gamma*invstd^2 * sum(g xhat)/M,
 // D = -gamma*invstd*sum(g)/M - B*mean.
 #include <algorithm>
+#include <cstdlib>
 
 #include "ldnn_common.h"
 #include "ldnn_kernels.h"
@@ -44,14 +45,37 @@ struct RedGeo {
   int lanes, rl, gx, gy, rpb;
 };
 
-RedGeo red_geo(int M, int C) {
+int env_int_or(const char* name, int dflt) {
+  const char* e = std::getenv(name);
+  return e ? std::atoi(e) : dflt;
+}
+
+// reduce geometry knobs (A/B): total blocks and rows per row lane of the reduce kernels;
+// 512 x 8 measured best with 8 accumulator copies (profiles/cnn_bn_reduce_r2.jsonl)
+int bn_red_blocks() {
+  static const int v = std::max(8, env_int_or("LDNN_BN_RED_BLOCKS", 512));
+  return v;
+}
+int bn_red_rows() {
+  static const int v = std::max(1, env_int_or("LDNN_BN_RED_ROWS", 8));
+  return v;
+}
+
+// accumulator copies the reduce blocks spread over (A/B: LDNN_BN_NCOP_FWD / _BWD)
+int bn_ncop(bool bwd) {
+  static const int f = std::min(kBnCopies, std::max(1, env_int_or("LDNN_BN_NCOP_FWD", kBnCopies)));
+  static const int b = std::min(kBnCopies, std::max(1, env_int_or("LDNN_BN_NCOP_BWD", kBnCopies)));
+  return bwd ? b : f;
+}
+
+RedGeo red_geo(int M, int C, bool reduce = false) {
   RedGeo g;
   const int cv = C / 8;
   g.lanes = cv < 256 ? cv : 256;
   g.rl = 256 / g.lanes;
   g.gx = (cv + 255) / 256;
-  int gy = std::max(1, 1024 / g.gx);               // ~4 blocks per CU in total
-  const int min_rows = 8 * g.rl;                   // >= 8 rows per row lane
+  int gy = std::max(1, (reduce ? bn_red_blocks() : 1024) / g.gx);   // ~4 blocks per CU in total
+  const int min_rows = (reduce ? bn_red_rows() : 8) * g.rl;          // >= 8 rows per row lane
   gy = std::min(gy, std::max(1, (M + min_rows - 1) / min_rows));
   g.rpb = (M + gy - 1) / gy;
   g.gy = (M + g.rpb - 1) / g.rpb;
@@ -94,7 +118,7 @@ __global__ __launch_bounds__(256) void bn_reduce_kernel(const bf16_t* __restrict
                                                         const bf16_t* __restrict__ y, const float* __restrict__ mean,
                                                         const float* __restrict__ invstd, float* __restrict__ acc,
                                                         int M, int C, int rpb, int lanes, int rl, BnFin fin,
-                                                        const uint8_t* __restrict__ mask = nullptr) {
+                                                        const uint8_t* __restrict__ mask, int ncop) {
   __shared__ float red[2][256 * 8];
   const int tid = threadIdx.x, lane = tid % lanes, rlane = tid / lanes;
   const int cv0 = blockIdx.x * 256 + lane;
@@ -141,13 +165,14 @@ __global__ __launch_bounds__(256) void bn_reduce_kernel(const bf16_t* __restrict
       t1 += red[1][q * row + ch];
     }
     const int c = blockIdx.x * 2048 + ch;
+    float* accc = acc + (size_t)((blockIdx.x + gridDim.x * blockIdx.y) % ncop) * 2 * C;
     if (c < C) {
-      atomicAdd(acc + c, t0);
-      atomicAdd(acc + C + c, t1);
+      bn_acc_add(accc + c, t0);
+      bn_acc_add(accc + C + c, t1);
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's atomics have completed
-  bn_finalize_last<BWD>(fin, M, C, gridDim.x * gridDim.y, 1);
+  bn_finalize_last<BWD, kBnCopies>(fin, M, C, gridDim.x * gridDim.y, &red[0][0], 2 * 256 * 8);
 }
 
 __global__ void bn_eval_coeff_kernel(const float* __restrict__ gamma, const float* __restrict__ beta,
@@ -381,18 +406,19 @@ __global__ void gap_bwd_kernel(const bf16_t* __restrict__ dy, bf16_t* __restrict
 }  // namespace
 
 // Workspace (fp32, zeroed once, kept by the caller -- e.g. per BatchNorm module):
-//   [0, C) scale | [C, 2C) shift | [2C, 4C) forward accumulator | [4C, 6C)
-//   backward accumulator | [6C, 9C) backward coefficients A, B, D | [10C]
-//   forward ticket | [10C + 16] backward ticket.
-// Accumulators and tickets are left zero by the reduce kernel's last block.
-//   [10C + 32, 26C + 32) kBnCopies x [2C] forward accumulators of the conv-epilogue
-//   statistics path (bn_forward_fin_conv).
-int bn_workspace_floats(int C) { return 10 * C + 32 + kBnCopies * 2 * C; }
+//   [0, C) scale | [C, 2C) shift | [6C, 9C) backward coefficients A, B, D |
+//   [10C] forward ticket | [10C + 16] backward ticket |
+//   [10C + 32, 26C + 32) kBnCopies x [2C] forward accumulators, shared by the BN
+//   reduce and the conv-epilogue statistics path (one BN's statistics come from
+//   exactly one of the two) |
+//   [26C + 32, 42C + 32) kBnCopies x [2C] backward accumulators.
+// Accumulators and tickets are left zero by the finalizing block.
+int bn_workspace_floats(int C) { return 10 * C + 32 + 2 * kBnCopies * 2 * C; }
 
 BnFin bn_forward_fin(const BnArgs& a) {
   const int C = a.C;
   BnFin f{};
-  f.acc = a.ws + 2 * C;
+  f.acc = a.ws + 10 * C + 32;
   f.ticket = reinterpret_cast<int*>(a.ws + 10 * C);
   f.gamma = a.gamma;
   f.beta = a.beta;
@@ -407,11 +433,7 @@ BnFin bn_forward_fin(const BnArgs& a) {
   return f;
 }
 
-BnFin bn_forward_fin_conv(const BnArgs& a) {
-  BnFin f = bn_forward_fin(a);
-  f.acc = a.ws + 10 * a.C + 32;
-  return f;
-}
+BnFin bn_forward_fin_conv(const BnArgs& a) { return bn_forward_fin(a); }
 
 hipError_t bn_forward_apply(const BnArgs& a, hipStream_t s) {
   const int M = a.M, C = a.C;
@@ -442,12 +464,12 @@ hipError_t bn_forward(const BnArgs& a, hipStream_t s) {
   const int M = a.M, C = a.C;
   if (C % 8) return hipErrorInvalidValue;
   if (M <= 0) return hipSuccess;
-  const RedGeo g = red_geo(M, C);
+  const RedGeo g = red_geo(M, C, true);
   const dim3 grid(g.gx, g.gy);
   if (a.training) {
     const BnFin f = bn_forward_fin(a);
     bn_reduce_kernel<false, false><<<grid, 256, 0, s>>>(a.x, nullptr, nullptr, nullptr, nullptr, f.acc, M, C, g.rpb,
-                                                        g.lanes, g.rl, f);
+                                                        g.lanes, g.rl, f, nullptr, bn_ncop(false));
   } else {
     bn_eval_coeff_kernel<<<(C + 255) / 256, 256, 0, s>>>(a.gamma, a.beta, a.running_mean, a.running_var, a.ws,
                                                          a.ws + C, C, a.eps);
@@ -462,8 +484,10 @@ hipError_t bn_backward(const BnArgs& a, const uint16_t* dy, uint16_t* dx, uint16
   if (M <= 0) return hipSuccess;
   const RedGeo g = red_geo(M, C);
   const dim3 grid(g.gx, g.gy);
+  const RedGeo gr = red_geo(M, C, true);   // the reduce's own geometry (knobs above)
+  const dim3 grid_r(gr.gx, gr.gy);
   BnFin f{};
-  f.acc = a.ws + 4 * C;
+  f.acc = a.ws + 10 * C + 32 + kBnCopies * 2 * C;
   f.ticket = reinterpret_cast<int*>(a.ws + 10 * C + 16);
   f.gamma = a.gamma;
   f.save_mean = a.save_mean;
@@ -472,14 +496,14 @@ hipError_t bn_backward(const BnArgs& a, const uint16_t* dy, uint16_t* dx, uint16
   f.dgamma = dgamma;
   f.dbeta = dbeta;
   if (a.relu && a.mask)
-    bn_reduce_kernel<true, true, true><<<grid, 256, 0, s>>>(a.x, dy, nullptr, a.save_mean, a.save_invstd, f.acc, M,
-                                                            C, g.rpb, g.lanes, g.rl, f, a.mask);
+    bn_reduce_kernel<true, true, true><<<grid_r, 256, 0, s>>>(a.x, dy, nullptr, a.save_mean, a.save_invstd, f.acc, M,
+                                                            C, gr.rpb, gr.lanes, gr.rl, f, a.mask, bn_ncop(true));
   else if (a.relu)
-    bn_reduce_kernel<true, true><<<grid, 256, 0, s>>>(a.x, dy, a.y, a.save_mean, a.save_invstd, f.acc, M, C, g.rpb,
-                                                      g.lanes, g.rl, f);
+    bn_reduce_kernel<true, true><<<grid_r, 256, 0, s>>>(a.x, dy, a.y, a.save_mean, a.save_invstd, f.acc, M, C, gr.rpb,
+                                                      gr.lanes, gr.rl, f, nullptr, bn_ncop(true));
   else
-    bn_reduce_kernel<true, false><<<grid, 256, 0, s>>>(a.x, dy, nullptr, a.save_mean, a.save_invstd, f.acc, M, C,
-                                                       g.rpb, g.lanes, g.rl, f);
+    bn_reduce_kernel<true, false><<<grid_r, 256, 0, s>>>(a.x, dy, nullptr, a.save_mean, a.save_invstd, f.acc, M, C,
+                                                       gr.rpb, gr.lanes, gr.rl, f, nullptr, bn_ncop(true));
   if (a.relu && a.mask)
     bn_bwd_apply_kernel<true, true><<<grid, 256, 0, s>>>(a.x, dy, nullptr, f.coef, dx, dres, M, C, g.rpb, g.lanes,
                                                          g.rl, a.mask);

@@ -386,7 +386,8 @@ __device__ __forceinline__ int tiles_of(const LArgs& a) { return a.tiles_x; }
 // invstd, running-stat EMA, apply coefficients), so the BN needs no reduce pass.
 template <int WM, int WN>
 __device__ __forceinline__ void bn_stats_epilogue(const LArgs& a, const Geo& g, floatx4 (&acc)[4][4], int mbase,
-                                                  int n0, int wm, int wn, int lane, int tile, char* smem) {
+                                                  int n0, int wm, int wn, int lane, int tile, char* smem,
+                                                  int lds_floats) {
   constexpr int BN = WN * 64;
   float* red = reinterpret_cast<float*>(smem);  // [WM][BN][2]
   __syncthreads();  // every wave is done with the operand stages
@@ -431,11 +432,11 @@ __device__ __forceinline__ void bn_stats_epilogue(const LArgs& a, const Geo& g, 
       s0 += red[(q * BN + t) * 2];
       s1 += red[(q * BN + t) * 2 + 1];
     }
-    atomicAdd(accc + c, s0);
-    atomicAdd(accc + a.N + c, s1);
+    bn_acc_add(accc + c, s0);
+    bn_acc_add(accc + a.N + c, s1);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's atomics have completed
-  bn_finalize_last<false>(a.bn, g.M, a.N, tiles_of(a), kBnCopies);
+  bn_finalize_last<false, kBnCopies>(a.bn, g.M, a.N, tiles_of(a), red, lds_floats);
 }
 
 // Direct epilogue with the class row remap: GEMM row m of a stride-2 dgrad
@@ -619,7 +620,7 @@ __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void conv_lds_kernel(LArgs a,
   p.beta = a.beta;
   epilogue<EPI, OUT_F32, 4, 4>(p, acc, mb, nbase, lane);
   if constexpr (!DGRAD && !OUT_F32 && EPI == EPI_NONE) {
-    if (a.bn_stats) bn_stats_epilogue<WM, WN>(a, g, acc, mb, n0, wm, wn, lane, blockIdx.x, smem);
+    if (a.bn_stats) bn_stats_epilogue<WM, WN>(a, g, acc, mb, n0, wm, wn, lane, blockIdx.x, smem, NS * STAGE / 4);
   }
 }
 

@@ -101,7 +101,7 @@ class StaticMLPEngine:
                  fuse_head_dgrad: bool | None = None, early_optimizer: bool | None = None,
                  library_dgrad: bool | None = None, concurrent_wgrad: bool = False, pad_input: bool = False,
                  head_dgrad_mode: int = -1, relu_masks: bool = True, wgrad_slabs: bool = True,
-                 transposed_dgrad: bool = True, bias_ones_column: bool = True, fuse_head_wgrad: bool = True):
+                 transposed_dgrad: bool = True, bias_ones_column: bool = True, fuse_head_wgrad: bool = False):
         from ..models.mlp import MLP
 
         if not isinstance(model, MLP):
@@ -210,7 +210,10 @@ class StaticMLPEngine:
                                         dtype=torch.float32, device=self.device) if self.head_dgrad else None)
         # fuse_head_wgrad (streaming head dgrad, <= 16 classes): the dgrad stream also
         # produces the head's dW / db from the same pass over h_{L-1} (head.hip mode 3):
-        # one read of the 128 MB activation instead of two (dgrad stream + head_wgrad)
+        # one read of the 128 MB activation instead of two (dgrad stream + head_wgrad).
+        # Off by default: measured on MI355X at batch 16384 it is VALU-bound (2 x 16 fp32
+        # FMAs per element on the vector ALUs): 135 us vs 61 + 26 us for the dgrad stream
+        # plus the MFMA head_wgrad (1.740 vs 1.710 ms/step)
         self.head_dw = (fuse_head_wgrad and self.head_dgrad and npad[-1] == 16 and self.head_dgrad_mode in (-1, 0, 3)
                         and self.layers[-1].in_features % 4 == 0)
         if self.head_dw:

@@ -425,7 +425,7 @@ def test_fused_head_stream_dw_matches_separate_head_wgrad(B):
     m1, m2 = mlp3(784, 1024, 10), mlp3(784, 1024, 10)
     m2.load_state_dict(m1.state_dict())
     cfg = OptimConfig("sgd", lr=0.05, momentum=0.9)
-    e1 = StaticMLPEngine(m1, B, cfg, use_graphs=True)
+    e1 = StaticMLPEngine(m1, B, cfg, use_graphs=True, fuse_head_wgrad=True)
     e2 = StaticMLPEngine(m2, B, cfg, use_graphs=True, fuse_head_wgrad=False)
     assert e1.head_dw and e1.head_dgrad_mode == 3 and not e2.head_dw
     g = torch.Generator(device="cuda").manual_seed(3)
