@@ -1061,6 +1061,9 @@ PYBIND11_MODULE(_C, m) {
       py::arg("N"), py::arg("splitk"));
   m.def("set_conv_impl", &ldnn::set_conv_impl, "0 = LDS-DMA fast path where it applies, 1 = generic kernel only",
         py::arg("impl"));
+  m.def("set_conv_q", &ldnn::set_conv_q, "big-tile conv path: 0 off (default), 1 every eligible shape",
+        py::arg("mode"));
+  m.def("get_conv_q", &ldnn::get_conv_q);
   m.def("get_conv_impl", &ldnn::get_conv_impl);
   m.def("gemm_opt", &gemm_opt, "weight-gradient GEMM with the optimizer update fused into its epilogue",
         py::arg("a"), py::arg("b"), py::arg("master"), py::arg("a_kcontig"), py::arg("b_kcontig"), py::arg("kind"),

@@ -130,6 +130,9 @@ ConvWorkspace conv2d_lds_workspace(const ConvShape& s, int op);
 // 0 = LDS-DMA fast path where it applies (default), 1 = generic kernel only (A/B and tests)
 void set_conv_impl(int impl);
 int get_conv_impl();
+// big-tile conv_q path (conv_lds.hip): 0 = off (default, measured slower), 1 = every eligible shape
+void set_conv_q(int mode);
+int get_conv_q();
 
 // ---- BatchNorm / pooling on NHWC bf16 (bn_pool.hip), C % 8 == 0
 struct BnArgs {

@@ -1,0 +1,41 @@
+"""One training step's kernels in launch order from a rocprofv3 kernel trace:
+duration, grid, short name -- the per-layer view the per-name summary hides.
+
+    python scripts/step_timeline.py <trace_dir_or_csv> [--marker sgd_kernel] [--step -2]
+"""
+import argparse
+import csv
+import glob
+import os
+import re
+
+
+def short(name):
+    n = name.replace("ldnn::", "").replace("(anonymous namespace)::", "").replace("convlds::", "")
+    n = re.sub(r"\(.*$", "", n)
+    n = re.sub(r"^void ", "", n)
+    return n[:90]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("path")
+    ap.add_argument("--marker", default="sgd_kernel")
+    ap.add_argument("--step", type=int, default=-2)
+    a = ap.parse_args()
+    f = a.path if a.path.endswith(".csv") else glob.glob(os.path.join(a.path, "*kernel_trace.csv"))[0]
+    rows = sorted(csv.DictReader(open(f)), key=lambda r: int(r["Start_Timestamp"]))
+    ends = [i for i, r in enumerate(rows) if a.marker in r["Kernel_Name"]]
+    lo = ends[a.step - 1] + 1
+    hi = ends[a.step]
+    tot = 0.0
+    for r in rows[lo:hi + 1]:
+        us = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+        tot += us
+        g = int(r["Grid_Size_X"]) // max(1, int(r["Workgroup_Size_X"]))
+        print(f"{us:8.1f} {g:6d}x{r['Grid_Size_Y']:>4s}  {short(r['Kernel_Name'])}")
+    print(f"{tot:8.1f} total ({hi - lo + 1} kernels)")
+
+
+if __name__ == "__main__":
+    main()
