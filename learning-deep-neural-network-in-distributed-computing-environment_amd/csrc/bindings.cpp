@@ -1007,6 +1007,20 @@ PYBIND11_MODULE(_C, m) {
         py::arg("tile") = 0, py::arg("splitk") = 0, py::arg("direct_epi") = false, py::arg("variant") = 0,
         py::arg("ws") = py::none(), py::arg("cnt") = py::none(), py::arg("mask_out") = py::none(),
         py::arg("mask_in") = py::none());
+  m.def("nchw_to_nhwc", [](const at::Tensor& src, const at::Tensor& dst) {
+        TORCH_CHECK(src.is_cuda() && src.dim() == 4 && src.is_contiguous() &&
+                        (src.scalar_type() == at::kFloat || src.scalar_type() == at::kBFloat16),
+                    "nchw_to_nhwc: src must be a contiguous NCHW fp32 / bf16 CUDA tensor");
+        check_dev(dst, at::kBFloat16, "dst");
+        const int64_t N = src.size(0), C = src.size(1), H = src.size(2), W = src.size(3);
+        TORCH_CHECK(dst.dim() == 4 && dst.is_contiguous() && dst.size(0) == N && dst.size(1) == H && dst.size(2) == W &&
+                        dst.size(3) >= C && dst.size(3) % 8 == 0 && aligned16(dst.data_ptr()),
+                    "nchw_to_nhwc: dst must be contiguous [N][H][W][cp], cp >= C, cp % 8 == 0");
+        c10::hip::HIPGuardMasqueradingAsCUDA g(src.device());
+        check(ldnn::nchw_to_nhwc(src.data_ptr(), src.scalar_type() == at::kFloat, bf16_mut(dst), (int)N, (int)C,
+                                 (int)(H * W), (int)dst.size(3), cur_stream(src)),
+              "nchw_to_nhwc");
+      }, "NCHW fp32/bf16 -> NHWC bf16 with zeroed pad channels", py::arg("src"), py::arg("dst"));
   m.def("transpose_bf16", [](const at::Tensor& in, const at::Tensor& out) {
         check_dev(in, at::kBFloat16, "in");
         check_dev(out, at::kBFloat16, "out");

@@ -20,7 +20,9 @@ constexpr int kBnCopies = 8;  // accumulator copies of the BN statistics (conv e
 // noise, profiles/cnn_bn_reduce_r2.jsonl.)
 // NCOP: the totals are spread over NCOP [2C] accumulator copies (contributors
 // pick copy `block % NCOP`, NCOP x less same-address serialisation at the
-// memory-side atomic units).  The finalizer sums the copies into the caller's LDS
+// memory-side atomic units); ncop = 1 at run time when few blocks contribute (the
+// finalizer's exchanges are its latency: 8 copies of a 1024-channel BN cost a
+// single finalizing block ~10 us).  The finalizer sums the copies into the caller's LDS
 // scratch (`cap` floats, free once the caller's own reduction has been read)
 // with all NCOP exchanges of an element in flight together, then finalizes per
 // channel; with 2C > cap it sums the copies in the per-channel loop.  (The
@@ -29,7 +31,8 @@ constexpr int kBnCopies = 8;  // accumulator copies of the BN statistics (conv e
 __device__ __forceinline__ void bn_acc_add(float* p, float v) { atomicAdd(p, v); }
 
 template <bool BWD, int NCOP>
-__device__ __forceinline__ void bn_finalize_last(const BnFin& f, int M, int C, int nblk, float* tot, int cap) {
+__device__ __forceinline__ void bn_finalize_last(const BnFin& f, int M, int C, int nblk, float* tot, int cap,
+                                                 int ncop = NCOP) {
   __shared__ int last;
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -41,14 +44,32 @@ __device__ __forceinline__ void bn_finalize_last(const BnFin& f, int M, int C, i
   if (!last) return;
   const bool lds = 2 * C <= cap;
   if (lds) {
-    for (int i = threadIdx.x; i < 2 * C; i += blockDim.x) {
-      float v[NCOP];
+    const int n2 = 2 * C, nt = blockDim.x;
+    if (ncop == 1) {  // one copy: 8 elements per thread in flight together (large C, few blocks)
+      for (int i0 = threadIdx.x; i0 < n2; i0 += 8 * nt) {
+        float v[8];
 #pragma unroll
-      for (int k = 0; k < NCOP; ++k) v[k] = atomicExch(f.acc + (size_t)k * 2 * C + i, 0.f);
-      float t = 0.f;
+        for (int u = 0; u < 8; ++u) v[u] = i0 + u * nt < n2 ? atomicExch(f.acc + i0 + u * nt, 0.f) : 0.f;
 #pragma unroll
-      for (int k = 0; k < NCOP; ++k) t += v[k];
-      tot[i] = t;
+        for (int u = 0; u < 8; ++u)
+          if (i0 + u * nt < n2) tot[i0 + u * nt] = v[u];
+      }
+    } else {  // NCOP copies: two elements x NCOP exchanges in flight
+      for (int i0 = threadIdx.x; i0 < n2; i0 += 2 * nt) {
+        float v[2][NCOP];
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int k = 0; k < NCOP; ++k)
+            v[u][k] = i0 + u * nt < n2 ? atomicExch(f.acc + (size_t)k * n2 + i0 + u * nt, 0.f) : 0.f;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          float t = 0.f;
+#pragma unroll
+          for (int k = 0; k < NCOP; ++k) t += v[u][k];
+          if (i0 + u * nt < n2) tot[i0 + u * nt] = t;
+        }
+      }
     }
     __syncthreads();
   }
@@ -61,6 +82,7 @@ __device__ __forceinline__ void bn_finalize_last(const BnFin& f, int M, int C, i
     } else {
 #pragma unroll
       for (int k = 0; k < NCOP; ++k) {
+        if (k >= ncop) break;
         S0 += atomicExch(f.acc + (size_t)k * 2 * C + c, 0.f);
         S1 += atomicExch(f.acc + (size_t)k * 2 * C + C + c, 0.f);
       }

@@ -62,10 +62,12 @@ int bn_red_rows() {
 }
 
 // accumulator copies the reduce blocks spread over (A/B: LDNN_BN_NCOP_FWD / _BWD)
-int bn_ncop(bool bwd) {
-  static const int f = std::min(kBnCopies, std::max(1, env_int_or("LDNN_BN_NCOP_FWD", kBnCopies)));
-  static const int b = std::min(kBnCopies, std::max(1, env_int_or("LDNN_BN_NCOP_BWD", kBnCopies)));
-  return bwd ? b : f;
+// (1 or kBnCopies: copies only pay when many blocks contend for the same addresses)
+int bn_ncop(bool bwd, int nblk) {
+  static const int f = env_int_or("LDNN_BN_NCOP_FWD", kBnCopies) > 1 ? kBnCopies : 1;
+  static const int b = env_int_or("LDNN_BN_NCOP_BWD", kBnCopies) > 1 ? kBnCopies : 1;
+  static const int min_blk = env_int_or("LDNN_BN_NCOP_MIN_BLOCKS", 64);
+  return nblk < min_blk ? 1 : (bwd ? b : f);
 }
 
 RedGeo red_geo(int M, int C, bool reduce = false) {
@@ -172,7 +174,7 @@ __global__ __launch_bounds__(256) void bn_reduce_kernel(const bf16_t* __restrict
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's atomics have completed
-  bn_finalize_last<BWD, kBnCopies>(fin, M, C, gridDim.x * gridDim.y, &red[0][0], 2 * 256 * 8);
+  bn_finalize_last<BWD, kBnCopies>(fin, M, C, gridDim.x * gridDim.y, &red[0][0], 2 * 256 * 8, ncop);
 }
 
 __global__ void bn_eval_coeff_kernel(const float* __restrict__ gamma, const float* __restrict__ beta,
@@ -469,7 +471,7 @@ hipError_t bn_forward(const BnArgs& a, hipStream_t s) {
   if (a.training) {
     const BnFin f = bn_forward_fin(a);
     bn_reduce_kernel<false, false><<<grid, 256, 0, s>>>(a.x, nullptr, nullptr, nullptr, nullptr, f.acc, M, C, g.rpb,
-                                                        g.lanes, g.rl, f, nullptr, bn_ncop(false));
+                                                        g.lanes, g.rl, f, nullptr, bn_ncop(false, g.gx * g.gy));
   } else {
     bn_eval_coeff_kernel<<<(C + 255) / 256, 256, 0, s>>>(a.gamma, a.beta, a.running_mean, a.running_var, a.ws,
                                                          a.ws + C, C, a.eps);
@@ -497,13 +499,13 @@ hipError_t bn_backward(const BnArgs& a, const uint16_t* dy, uint16_t* dx, uint16
   f.dbeta = dbeta;
   if (a.relu && a.mask)
     bn_reduce_kernel<true, true, true><<<grid_r, 256, 0, s>>>(a.x, dy, nullptr, a.save_mean, a.save_invstd, f.acc, M,
-                                                            C, gr.rpb, gr.lanes, gr.rl, f, a.mask, bn_ncop(true));
+                                                            C, gr.rpb, gr.lanes, gr.rl, f, a.mask, bn_ncop(true, gr.gx * gr.gy));
   else if (a.relu)
     bn_reduce_kernel<true, true><<<grid_r, 256, 0, s>>>(a.x, dy, a.y, a.save_mean, a.save_invstd, f.acc, M, C, gr.rpb,
-                                                      gr.lanes, gr.rl, f, nullptr, bn_ncop(true));
+                                                      gr.lanes, gr.rl, f, nullptr, bn_ncop(true, gr.gx * gr.gy));
   else
     bn_reduce_kernel<true, false><<<grid_r, 256, 0, s>>>(a.x, dy, nullptr, a.save_mean, a.save_invstd, f.acc, M, C,
-                                                       gr.rpb, gr.lanes, gr.rl, f, nullptr, bn_ncop(true));
+                                                       gr.rpb, gr.lanes, gr.rl, f, nullptr, bn_ncop(true, gr.gx * gr.gy));
   if (a.relu && a.mask)
     bn_bwd_apply_kernel<true, true><<<grid, 256, 0, s>>>(a.x, dy, nullptr, f.coef, dx, dres, M, C, g.rpb, g.lanes,
                                                          g.rl, a.mask);

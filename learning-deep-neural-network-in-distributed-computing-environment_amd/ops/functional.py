@@ -226,6 +226,12 @@ def as_nhwc(t: torch.Tensor, cp: int, zero_pad: bool = True) -> torch.Tensor:
         if zero_pad and cp > C:
             buf.data[..., C:].zero_()
         return buf
+    if (cp % 8 == 0 and t.is_contiguous() and t.dtype in (torch.float32, torch.bfloat16)
+            and _ext.use_native(t)):
+        # one native pass: gather + cast + zeroed pad channels (no fill + permute copy)
+        buf = torch.empty(N, H, W, cp, dtype=torch.bfloat16, device=t.device)
+        _ext.C().nchw_to_nhwc(t, buf)
+        return buf
     buf = torch.zeros(N, H, W, cp, dtype=torch.bfloat16, device=t.device) if cp > C else \
         torch.empty(N, H, W, cp, dtype=torch.bfloat16, device=t.device)
     buf[..., :C].copy_(t.permute(0, 2, 3, 1))

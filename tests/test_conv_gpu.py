@@ -147,3 +147,15 @@ def test_big_tile_conv_matches_small_tile_kernel(N, C, H, W, K, R, st, pad):
     (y0, dx0), (y1, dx1) = outs[0], outs[1]
     torch.testing.assert_close(y1, y0, rtol=2e-2, atol=2e-2 * y0.abs().max().item())
     torch.testing.assert_close(dx1, dx0, rtol=2e-2, atol=2e-2 * dx0.abs().max().item())
+
+
+@pytest.mark.parametrize("dtype,C,cp", [(torch.float32, 3, 8), (torch.bfloat16, 3, 8), (torch.float32, 16, 16),
+                                        (torch.bfloat16, 20, 32)])
+def test_nchw_to_nhwc_pad(dtype, C, cp):
+    """Native NCHW -> NHWC bf16 conversion with zeroed pad channels == permute + pad."""
+    x = torch.randn(3, C, 13, 17, device="cuda").to(dtype)
+    out = torch.full((3, 13, 17, cp), 7.0, device="cuda", dtype=torch.bfloat16)
+    _ext.C().nchw_to_nhwc(x, out)
+    ref = torch.zeros(3, 13, 17, cp, device="cuda", dtype=torch.bfloat16)
+    ref[..., :C] = x.permute(0, 2, 3, 1).to(torch.bfloat16)
+    assert torch.equal(out, ref)
