@@ -927,11 +927,14 @@ WgradPlan plan_wgrad(const ConvShape& s) {
   return p;
 }
 
-// LDNN_CONV_TAPMAJOR=1: filter taps fastest in the fwd / dgrad K-tile order (A/B)
+// Filter taps fastest in the fwd / dgrad K-tile order (default; LDNN_CONV_TAPMAJOR=0
+// restores channel blocks fastest): consecutive K-tiles re-read shifted rows of one
+// channel block, which the L2 / L1 serve warm -- alternated same-box A/B ResNet-18
+// b64 3.89 -> 3.85 ms (profiles/cnn_fuse_stats_tapmajor_ab_r2.jsonl)
 int tap_major_env() {
   static const int v = [] {
     const char* e = std::getenv("LDNN_CONV_TAPMAJOR");
-    return e ? std::atoi(e) : 0;
+    return e ? std::atoi(e) : 1;
   }();
   return v;
 }

@@ -72,12 +72,13 @@ class Conv2d(nn.Conv2d):
                          bn=self._ldnn_stats_bn if FUSE_BN_STATS else None)
 
 
-# Conv-epilogue BatchNorm statistics (pair_conv_bn) are opt-in: measured on MI355X
-# (scripts/bench_cnn.py --graph) the epilogue's atomics + last-tile finalize add
-# ~12 us to each forward conv while the BN reduce pass they replace costs ~9.5 us:
-# EnhancedCNN batch 64 2.462 vs 2.424 ms, batch 256 3.606 vs 3.581 ms, ResNet-18
-# batch 64 3.80 vs 3.67 ms.  LDNN_FUSE_BN_STATS=1 (or setting this flag) turns it on.
-FUSE_BN_STATS = os.environ.get("LDNN_FUSE_BN_STATS", "0") == "1"
+# Conv-epilogue BatchNorm statistics (pair_conv_bn) are on by default since the
+# finalize became parallel (8 accumulator copies summed into LDS, exchanges batched):
+# alternated same-box A/B (scripts/ab_cnn.sh, profiles/cnn_fuse_stats_tapmajor_ab_r2.jsonl)
+# with the tap-major conv K order: ResNet-18 b64 3.89 -> 3.82 ms, EnhancedCNN b64
+# 2.45 -> 2.42 ms.  (Round 1, with a serial finalize, it lost: 3.80 vs 3.67 ms.)
+# LDNN_FUSE_BN_STATS=0 turns it off.
+FUSE_BN_STATS = os.environ.get("LDNN_FUSE_BN_STATS", "1") == "1"
 
 
 def pair_conv_bn(conv: "Conv2d", bn: "BatchNorm2d") -> None:

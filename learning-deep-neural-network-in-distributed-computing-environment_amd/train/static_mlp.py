@@ -873,7 +873,8 @@ class StaticMLPEngine:
                 d[f"wgrad{l}"] = (f"ldnn gemm_q split-K x{self._wgrad_splitk[l]} slabs + slab_sum"
                                   + (" (+ bias grad from a ones column)" if l == 0 and self._db0_from_wgrad else ""))
             else:
-                d[f"wgrad{l}"] = "ldnn gemm" + (f" split-K x{self._wgrad_splitk[l]}" if self._wgrad_splitk[l] > 1 else "")
+                d[f"wgrad{l}"] = ("ldnn gemm (auto: gemm_q four-wave 256x256 where gemm_q_preferred, else k256)"
+                                  + (f" split-K x{self._wgrad_splitk[l]}" if self._wgrad_splitk[l] > 1 else ""))
             if l > 0:
                 d[f"dgrad{l}"] = ("hipBLASLt + act_bwd_colsum" if self._lib_dgrad[l] else
                                   "ldnn gemm_q" + (" on transposed W" if self.Wt[l] is not None else "")
