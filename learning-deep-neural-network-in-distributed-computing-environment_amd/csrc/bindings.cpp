@@ -867,7 +867,7 @@ void bn_bwd(const at::Tensor& x, const at::Tensor& y, const at::Tensor& dy, cons
             const c10::optional<at::Tensor>& dres, const c10::optional<at::Tensor>& gamma,
             const at::Tensor& save_mean, const at::Tensor& save_invstd, const at::Tensor& ws,
             const c10::optional<at::Tensor>& dgamma, const c10::optional<at::Tensor>& dbeta, bool relu,
-            const c10::optional<at::Tensor>& mask) {
+            const c10::optional<at::Tensor>& mask, bool grad_assign) {
   check_dev(x, at::kBFloat16, "x");
   check_dev(dy, at::kBFloat16, "dy");
   check_dev(dx, at::kBFloat16, "dx");
@@ -897,7 +897,7 @@ void bn_bwd(const at::Tensor& x, const at::Tensor& y, const at::Tensor& dy, cons
     dr = bf16_mut(*dres);
   }
   check(ldnn::bn_backward(a, bf16_ptr(dy), bf16_mut(dx), dr, fptr_opt(dgamma, C, "dgamma"),
-                          fptr_opt(dbeta, C, "dbeta"), cur_stream(x)),
+                          fptr_opt(dbeta, C, "dbeta"), cur_stream(x), grad_assign),
         "bn_backward");
 }
 
@@ -1138,7 +1138,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("C"));
   m.def("bn_bwd", &bn_bwd, py::arg("x"), py::arg("y"), py::arg("dy"), py::arg("dx"), py::arg("dres"),
         py::arg("gamma"), py::arg("save_mean"), py::arg("save_invstd"), py::arg("ws"), py::arg("dgamma"),
-        py::arg("dbeta"), py::arg("relu"), py::arg("mask") = py::none());
+        py::arg("dbeta"), py::arg("relu"), py::arg("mask") = py::none(), py::arg("grad_assign") = false);
   m.def("pool_fwd", &pool_fwd);
   m.def("pool_bwd", &pool_bwd);
   m.def("gap_fwd", &gap_fwd);

@@ -108,8 +108,8 @@ __device__ __forceinline__ void bn_finalize_last(const BnFin& f, int M, int C, i
       f.coef[c] = A;
       f.coef[C + c] = B;
       f.coef[2 * C + c] = -gm * is * S0 * invM - B * f.save_mean[c];
-      if (f.dgamma) f.dgamma[c] += S1;
-      if (f.dbeta) f.dbeta[c] += S0;
+      if (f.dgamma) f.dgamma[c] = f.grad_assign ? S1 : f.dgamma[c] + S1;
+      if (f.dbeta) f.dbeta[c] = f.grad_assign ? S0 : f.dbeta[c] + S0;
     }
   }
   if (!BWD && threadIdx.x == 0 && f.num_batches) f.num_batches[0] += 1;

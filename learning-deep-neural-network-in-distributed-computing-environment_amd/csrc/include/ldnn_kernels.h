@@ -168,8 +168,9 @@ struct BnFin {
   float* save_mean;           // fwd: written; bwd: read
   float* save_invstd;
   float* coef;                // fwd: scale | shift ; bwd: A | B | D
-  float* dgamma;              // bwd: accumulated
+  float* dgamma;              // bwd: accumulated (grad_assign: overwritten)
   float* dbeta;
+  int grad_assign;            // bwd: 1 = dgamma / dbeta = the totals (first write of the step)
   int64_t* num_batches;       // fwd: += 1 (BatchNorm2d.num_batches_tracked), nullable
   float eps, momentum;
 };
@@ -182,7 +183,7 @@ hipError_t bn_forward_apply(const BnArgs& a, hipStream_t s);
 // dx (and optionally dres = upstream gradient after the ReLU mask, for the residual
 // branch); dgamma / dbeta are ACCUMULATED (flat gradient buffer)
 hipError_t bn_backward(const BnArgs& a, const uint16_t* dy, uint16_t* dx, uint16_t* dres, float* dgamma,
-                       float* dbeta, hipStream_t s);
+                       float* dbeta, hipStream_t s, bool grad_assign = false);
 hipError_t pool2d_fwd(const uint16_t* x, uint16_t* y, uint8_t* argmax, int N, int H, int W, int C, int P, int Q,
                       int R, int S, int stride, int pad, bool is_max, hipStream_t s);
 hipError_t pool2d_bwd(const uint16_t* dy, const uint8_t* argmax, uint16_t* dx, int N, int H, int W, int C, int P,

@@ -480,7 +480,7 @@ hipError_t bn_forward(const BnArgs& a, hipStream_t s) {
 }
 
 hipError_t bn_backward(const BnArgs& a, const uint16_t* dy, uint16_t* dx, uint16_t* dres, float* dgamma,
-                       float* dbeta, hipStream_t s) {
+                       float* dbeta, hipStream_t s, bool grad_assign) {
   const int M = a.M, C = a.C;
   if (C % 8) return hipErrorInvalidValue;
   if (M <= 0) return hipSuccess;
@@ -497,6 +497,7 @@ hipError_t bn_backward(const BnArgs& a, const uint16_t* dy, uint16_t* dx, uint16
   f.coef = a.ws + 6 * C;
   f.dgamma = dgamma;
   f.dbeta = dbeta;
+  f.grad_assign = grad_assign ? 1 : 0;
   if (a.relu && a.mask)
     bn_reduce_kernel<true, true, true><<<grid_r, 256, 0, s>>>(a.x, dy, nullptr, a.save_mean, a.save_invstd, f.acc, M,
                                                             C, gr.rpb, gr.lanes, gr.rl, f, a.mask, bn_ncop(true, gr.gx * gr.gy));

@@ -87,10 +87,11 @@ class _LinearActNative(torch.autograd.Function):
             C.act_bwd(g.contiguous(), y, gz, ctx.act)
         else:
             gz = g.contiguous()
-        # weight grad straight into the flat fp32 gradient buffer (accumulate)
-        C.gemm(gz, x2, flat.grad_storage(weight), False, False, beta=1.0)
+        # weight grad straight into the flat fp32 gradient buffer (accumulate, or
+        # overwrite as the step's first write: FlatParams.grad_beta)
+        C.gemm(gz, x2, flat.grad_storage(weight), False, False, beta=flat.grad_beta(weight))
         if bias is not None:
-            C.colsum(gz, flat.grad_storage(bias), True)
+            C.colsum(gz, flat.grad_storage(bias), flat.grad_beta(bias) != 0.0)
         flat.notify(weight, bias)
         dx = None
         if ctx.needs_input_grad[0]:
@@ -320,9 +321,9 @@ class _Conv2dNative(torch.autograd.Function):
             gz = torch.empty_like(g)
             C.act_bwd(g.contiguous(), y, gz, 0)
             g = gz
-        C.conv_wgrad(g, xb, flat.grad_storage(weight), stride, pad, 1.0)
+        C.conv_wgrad(g, xb, flat.grad_storage(weight), stride, pad, flat.grad_beta(weight))
         if bias is not None:
-            C.colsum(g.view(-1, kp), flat.grad_storage(bias), True)
+            C.colsum(g.view(-1, kp), flat.grad_storage(bias), flat.grad_beta(bias) != 0.0)
         flat.notify(weight, bias)
         dx = None
         if ctx.needs_input_grad[0]:
@@ -413,10 +414,17 @@ class _BatchNormNative(torch.autograd.Function):
         gamma = flat.master_storage(weight)[:C] if weight is not None else None
         dg = flat.grad_storage(weight)[:C] if weight is not None else None
         db = flat.grad_storage(bias)[:C] if bias is not None else None
+        # first write of the step: the finalize stores dgamma / dbeta instead of adding
+        fresh = [(t, flat.grad_beta(p) == 0.0) for t, p in ((dg, weight), (db, bias)) if p is not None]
+        assign = all(f for _, f in fresh)
+        if not assign:  # mixed (only if a caller accumulated one of them): clear the fresh ones
+            for t, f in fresh:
+                if f:
+                    t.zero_()
         mask = ctx.mask
         yv = y.view(-1, C) if mask is None else x2   # (y is not read when the mask is given)
         C_.bn_bwd(x2, yv, g2, dx.view(-1, C), dres.view(-1, C) if dres is not None else None, gamma,
-                  smean, sinv, ws, dg, db, relu, mask=mask)
+                  smean, sinv, ws, dg, db, relu, mask=mask, grad_assign=assign)
         flat.notify(weight, bias)
         dxv = nchw_view(dx, C)
         dresv = nchw_view(dres, C) if dres is not None else None

@@ -20,6 +20,9 @@ from ..ops import _ext
 from ..utils.flat_params import owner_of
 
 
+_LAZY_ZERO = __import__("os").environ.get("LDNN_LAZY_ZERO", "1") != "0"
+
+
 class _FlatOptimizer(torch.optim.Optimizer):
     def _ls(self) -> dict:
         """Fused (flat-buffer) optimizer state: momentum / moments / step / hp."""
@@ -89,7 +92,8 @@ class _FlatOptimizer(torch.optim.Optimizer):
         for group in self.param_groups:
             f = self._flat_for_group(group)
             if f is not None:
-                f.zero_grad()
+                # (set_to_none: the next backward's first write overwrites; LDNN_LAZY_ZERO=0 fills)
+                f.zero_grad(lazy=set_to_none and _LAZY_ZERO)
             else:
                 for p in group["params"]:
                     if p.grad is not None:
@@ -114,6 +118,7 @@ class SGD(_FlatOptimizer):
             lr, mu, damp, wd, nest = (group[k] for k in ("lr", "momentum", "dampening", "weight_decay", "nesterov"))
             f = self._flat_for_group(group)
             if f is not None:
+                f.finalize_grads()
                 st = self._ls()
                 first = st.get("step", 0) == 0
                 mom = self._buf("momentum", f.master) if mu != 0 else f.master
@@ -166,6 +171,7 @@ class Adam(_FlatOptimizer):
             lr, (b1, b2), eps, wd = group["lr"], group["betas"], group["eps"], group["weight_decay"]
             f = self._flat_for_group(group)
             if f is not None:
+                f.finalize_grads()
                 st = self._ls()
                 m, v = self._buf("exp_avg", f.master), self._buf("exp_avg_sq", f.master)
                 if _ext.use_native(f.master):

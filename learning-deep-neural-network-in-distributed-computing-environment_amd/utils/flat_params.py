@@ -123,6 +123,12 @@ class FlatParams:
         # gradient-readiness notification: native ops call notify() after writing a
         # weight gradient; params handled by stock torch ops signal through autograd.
         self._ready_hooks: list = []
+        # first-write gradients: native ops ask grad_beta() before writing a gradient;
+        # after a lazy zero_grad the first writer overwrites (beta 0) instead of
+        # accumulating onto a zero-filled buffer -- no fill pass, and the fp32 wgrad
+        # epilogues store without reading.
+        self._native: set = set()   # params whose gradients native ops write
+        self._stale: set = set()    # params whose gradient is logically zero, not cleared
         self.grad_scale = 1.0  # set to 1/N by data parallelism; consumed by the fused optimizers
         for s in segs:
             _OWNER[id(s.param)] = self
@@ -190,9 +196,38 @@ class FlatParams:
         else:
             self.shadow.copy_(self.master)
 
+    def grad_beta(self, p) -> float:
+        """0.0 when ``p``'s gradient is logically zero (lazy zero_grad, not written yet
+        this step): the caller overwrites; else 1.0 (accumulate)."""
+        i = id(p)
+        self._native.add(i)
+        if i in self._stale:
+            self._stale.discard(i)
+            return 0.0
+        return 1.0
+
     @torch.no_grad()
-    def zero_grad(self):
-        self.grad.zero_()
+    def zero_grad(self, lazy: bool = False):
+        """lazy: gradients that native ops write are only marked zero (their first
+        writer overwrites, grad_beta); the rest are cleared now."""
+        if not lazy or not self._native:
+            self.grad.zero_()
+            self._stale.clear()
+            return
+        others = [s.param for s in self.segments if id(s.param) not in self._native]
+        for b, e in (self.ranges(others) if others else []):
+            self.grad[b:e].zero_()
+        self._stale = set(self._native)
+
+    @torch.no_grad()
+    def finalize_grads(self):
+        """Clear gradients still marked zero (their op did not run this step) before a
+        consumer reads the flat buffer (optimizer, aggregation)."""
+        if self._stale:
+            for s in self.segments:
+                if id(s.param) in self._stale:
+                    self.storage_view(s, self.grad).zero_()
+            self._stale.clear()
 
     def reattach_grads(self):
         """Point every ``param.grad`` back at its flat view (after user code set it to None)."""

@@ -16,7 +16,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import ldnn  # noqa: E402
 from ldnn.models import CrossEntropyLoss, build_model, dataset_for, xavier_init  # noqa: E402
 from ldnn.data.datasets import SHAPES  # noqa: E402
-from ldnn.optim import SGD  # noqa: E402
+from ldnn.optim import SGD, Adam  # noqa: E402
 
 
 def run(step, steps, warmup):
@@ -39,6 +39,8 @@ def main():
     ap.add_argument("--no-stock", action="store_true")
     ap.add_argument("--conv-impl", type=int, default=0, help="0 = LDS-DMA fast path, 1 = generic conv kernel only")
     ap.add_argument("--graph", action="store_true", help="replay the ldnn step from one hipGraph (train.graphed)")
+    ap.add_argument("--optimizer", choices=["sgd", "adam"], default="sgd",
+                    help="sgd = momentum 0.9; adam = the reference config (BAR/main.py:53, lr 1e-3)")
     a = ap.parse_args()
     from ldnn.ops import _ext as _e
 
@@ -52,7 +54,7 @@ def main():
     m = build_model(a.model)
     xavier_init(m)
     ldnn.prepare(m, "cuda")
-    opt = SGD(m.parameters(), lr=0.01, momentum=0.9)
+    opt = (Adam(m.parameters(), lr=1e-3) if a.optimizer == "adam" else SGD(m.parameters(), lr=0.01, momentum=0.9))
     crit = CrossEntropyLoss()
     xb = x.bfloat16()
 
@@ -70,7 +72,7 @@ def main():
             gs(xb, y)
 
     t = run(step_ldnn, a.steps, a.warmup)
-    rec = {"model": a.model, "batch": a.batch, "conv_impl": a.conv_impl, "graph": a.graph, "ldnn_ms": round(t * 1e3, 3), "ldnn_samples_per_s": round(a.batch / t, 1)}
+    rec = {"model": a.model, "batch": a.batch, "optimizer": a.optimizer, "conv_impl": a.conv_impl, "graph": a.graph, "ldnn_ms": round(t * 1e3, 3), "ldnn_samples_per_s": round(a.batch / t, 1)}
     if not a.no_stock:
         import torch.nn as nn
 
@@ -82,7 +84,8 @@ def main():
         from ldnn.ops import _ext
 
         _ext._DISABLED = True
-        ropt = torch.optim.SGD(ref.parameters(), lr=0.01, momentum=0.9)
+        ropt = (torch.optim.Adam(ref.parameters(), lr=1e-3) if a.optimizer == "adam" else
+                torch.optim.SGD(ref.parameters(), lr=0.01, momentum=0.9))
         ce = nn.CrossEntropyLoss()
         xc = x.contiguous(memory_format=torch.channels_last)
 

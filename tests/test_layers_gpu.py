@@ -265,3 +265,49 @@ def test_conv_epilogue_bn_statistics_match_separate_pass(name, shape, monkeypatc
     for (n, p1), (_, p2), (_, p3) in named[-max(2, len(named) // 4):]:
         g1, g2, g3 = (p.grad.flatten().double() for p in (p1, p2, p3))
         assert (g1 - g2).norm().item() <= 3.0 * (g3 - g2).norm().item() + 5e-2 * g2.norm().item(), n
+
+
+def test_lazy_zero_grad_first_write_matches_filled_buffer():
+    """zero_grad(set_to_none=True) on the flat optimizers only marks the natively written
+    gradients zero; their first writer of the step overwrites (conv / Linear wgrad
+    beta 0, colsum without accumulate, BN dgamma / dbeta assign).  Same gradients as
+    a filled buffer + accumulate, and a second backward still accumulates."""
+    from ldnn.models.layers import BatchNorm2d, Conv2d, Linear
+    from ldnn.optim import SGD
+
+    class Net(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.c = Conv2d(16, 64, 3, padding=1, bias=True)
+            self.bn = BatchNorm2d(64)
+            self.fc = Linear(64, 10)
+
+        def forward(self, x):
+            h = self.bn.act(self.c(x), relu=True)
+            return self.fc(h.float().mean((2, 3)))
+
+    torch.manual_seed(0)
+    nets = [Net(), Net()]
+    nets[1].load_state_dict(nets[0].state_dict())
+    opts = []
+    for n in nets:
+        ldnn.prepare(n, "cuda")
+        opts.append(SGD(n.parameters(), lr=0.0))
+    x = torch.randn(8, 16, 12, 12, device="cuda").bfloat16()
+    y = torch.randint(0, 10, (8,), device="cuda")
+    crit = CrossEntropyLoss()
+    for n in nets:  # dirty the gradients first
+        crit(n(x * 3), y).backward()
+    opts[0].zero_grad()                     # lazy: marks only
+    opts[1].zero_grad(set_to_none=False)    # fill
+    for n in nets:
+        crit(n(x), y).backward()
+    flat0 = opts[0]._flat_for_group(opts[0].param_groups[0])
+    assert not flat0._stale  # every native gradient was written
+    g = [[p.grad.detach().clone() for p in n.parameters()] for n in nets]
+    for a, b in zip(*g):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-6)
+    # a second backward without zero_grad accumulates (beta 1)
+    crit(nets[0](x), y).backward()
+    for p, a in zip(nets[0].parameters(), g[0]):
+        torch.testing.assert_close(p.grad, 2 * a, rtol=1e-3, atol=1e-5)
