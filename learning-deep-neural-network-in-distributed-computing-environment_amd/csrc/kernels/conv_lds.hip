@@ -907,6 +907,11 @@ __global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__
 
 bool fits(size_t bytes) { return bytes < kOOBLimit; }
 
+int env_int(const char* name, int dflt) {
+  const char* e = std::getenv(name);
+  return e ? std::atoi(e) : dflt;
+}
+
 struct WgradPlan {
   bool narrow;
   int tiles, splits, nk_all, nk_split;
@@ -921,7 +926,8 @@ WgradPlan plan_wgrad(const ConvShape& s) {
   p.nk_all = (s.N * s.P * s.Q + 63) / 64;
   // split the npq reduction over ~1.5 workgroups per CU, >= 8 K-tiles per slice
   int splits = 1;
-  if (p.tiles < 256) splits = std::max(1, std::min((384 + p.tiles - 1) / p.tiles, p.nk_all / 8));
+  static const int target = env_int("LDNN_CONV_WGRAD_TARGET", 384);  // workgroups to aim for (A/B knob)
+  if (p.tiles < 256) splits = std::max(1, std::min((target + p.tiles - 1) / p.tiles, p.nk_all / 8));
   p.nk_split = (p.nk_all + splits - 1) / splits;
   p.splits = (p.nk_all + p.nk_split - 1) / p.nk_split;
   return p;
@@ -1025,11 +1031,20 @@ bool slab_env_off() {
   return v;
 }
 
-// In-launch split-K for small-M fwd / dgrad: enough slices for ~1.5
-// workgroups per CU, >= 8 K-tiles each, at most 8.
+// In-launch split-K for small-M fwd / dgrad (below 256 tiles: ResNet-18's 14x14
+// stage, 196 tiles, A/B 3.76 -> 3.68 ms at b64, profiles/cnn_split_tiles_ab_r2.jsonl):
+// enough slices for ~1.5 workgroups per CU, >= 8 K-tiles each, at most 8.
+int split_tiles_env() {  // LDNN_CONV_SPLIT_TILES: tile count below which fwd / dgrad split K (A/B knob)
+  static const int v = [] {
+    const char* e = std::getenv("LDNN_CONV_SPLIT_TILES");
+    return e ? std::atoi(e) : 256;
+  }();
+  return v;
+}
 int small_m_splits(int tiles, int nk) {
-  if (tiles >= 160 || nk < 16) return 1;
-  int sp = (384 + tiles - 1) / tiles;
+  if (tiles >= split_tiles_env() || nk < 16) return 1;
+  static const int target = env_int("LDNN_CONV_SPLIT_TARGET", 384);  // workgroups to aim for (A/B knob)
+  int sp = (target + tiles - 1) / tiles;
   sp = std::min(sp, nk / 8);
   sp = std::min(sp, 8);
   return sp < 2 ? 1 : sp;
