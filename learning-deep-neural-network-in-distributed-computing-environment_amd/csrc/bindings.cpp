@@ -1078,6 +1078,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("set_conv_q", &ldnn::set_conv_q, "big-tile conv path: 0 off (default), 1 every eligible shape",
         py::arg("mode"));
   m.def("get_conv_q", &ldnn::get_conv_q);
+  m.def("set_conv_halo", &ldnn::set_conv_halo,
+        "halo-staged 3x3 stride-1 conv: 0 off, 1 default (dgrad + 256x64 fwd tiles), 2 every eligible shape",
+        py::arg("mode"));
+  m.def("get_conv_halo", &ldnn::get_conv_halo);
   m.def("get_conv_impl", &ldnn::get_conv_impl);
   m.def("gemm_opt", &gemm_opt, "weight-gradient GEMM with the optimizer update fused into its epilogue",
         py::arg("a"), py::arg("b"), py::arg("master"), py::arg("a_kcontig"), py::arg("b_kcontig"), py::arg("kind"),

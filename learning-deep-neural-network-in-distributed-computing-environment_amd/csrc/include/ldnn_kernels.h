@@ -133,6 +133,10 @@ int get_conv_impl();
 // big-tile conv_q path (conv_lds.hip): 0 = off (default, measured slower), 1 = every eligible shape
 void set_conv_q(int mode);
 int get_conv_q();
+// halo-staged 3x3 stride-1 conv path (conv_lds.hip): 0 = off, 1 = default dispatch
+// (dgrad + 256x64 fwd tiles), 2 = also the 128x128 fwd tiles
+void set_conv_halo(int mode);
+int get_conv_halo();
 
 // ---- BatchNorm / pooling on NHWC bf16 (bn_pool.hip), C % 8 == 0
 struct BnArgs {

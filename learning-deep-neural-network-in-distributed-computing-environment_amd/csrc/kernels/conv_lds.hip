@@ -487,6 +487,71 @@ __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// Shared tail of the fwd / dgrad / wgrad kernels: split-K hand-off (in-launch
+// combine, fp32 slab, or fp32 atomics), the stride-2 dgrad row remap, the fused
+// epilogue and the next BatchNorm's statistics.  smem: the kernel's whole LDS
+// (lds_floats floats), free once every wave is past its operand reads.
+template <int WM, int WN, int EPI, bool OUT_F32, bool DGRAD>
+__device__ __forceinline__ void conv_tail(const LArgs& a, const Geo& g, floatx4 (&acc)[4][4], int m0, int n0, int wm,
+                                          int wn, int lane, char* smem, int lds_floats) {
+  constexpr int NW = WM * WN;
+  const bool combine = a.cnt != nullptr && gridDim.y > 1;
+  const int mb = m0 + wm * 64, nbase = n0 + wn * 64;
+  if (gridDim.y > 1) {
+    if (combine) {
+      lds_barrier();  // every wave is done with the operand stages (the ticket word lives there)
+      const int tile = blockIdx.z * a.tiles_x + blockIdx.x;
+      if (!splitk_combine<4, 4, NW * 64>(acc, a.ws, a.cnt, tile, gridDim.y, blockIdx.y, smem)) return;
+    } else if (a.ws != nullptr) {
+      // wgrad, and small-M fwd / stride-1 dgrad: this slice's fp32 partial tile into
+      // its own slab; a separate chip-wide kernel sums the slabs (slab_sum_kernel /
+      // conv_slab_epilogue_kernel with the bias / ReLU epilogue) -- deterministic, no
+      // atomics, and no single workgroup re-reading every slice of its tile
+      GemmParams p{};
+      p.C = a.ws + (size_t)blockIdx.y * a.M * a.N;
+      p.M = g.M;
+      p.N = a.N;
+      p.ldc = a.N;
+      epilogue<EPI_NONE, true, 4, 4>(p, acc, mb, nbase, lane);
+      return;
+    } else {
+      if constexpr (OUT_F32 && EPI == EPI_NONE) {  // fp32 atomics into the (cleared / accumulated) output
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int n = nbase + j * 16 + 4 * (lane >> 4);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int m = mb + i * 16 + (lane & 15);
+            if (n < a.N && m < g.M) {
+              float* c = reinterpret_cast<float*>(a.out) + (size_t)m * a.N + n;
+#pragma unroll
+              for (int r = 0; r < 4; ++r) atomicAdd(c + r, acc[j][i][r]);
+            }
+          }
+        }
+      }
+      return;
+    }
+  }
+  if constexpr (DGRAD && !OUT_F32) {
+    if (g.hmul == 2) {
+      store_remapped(a, g, acc, mb, nbase, lane);
+      return;
+    }
+  }
+  GemmParams p{};
+  p.C = a.out;
+  p.M = g.M;
+  p.N = a.N;
+  p.ldc = a.N;
+  p.bias = a.bias;
+  p.beta = a.beta;
+  epilogue<EPI, OUT_F32, 4, 4>(p, acc, mb, nbase, lane);
+  if constexpr (!DGRAD && !OUT_F32 && EPI == EPI_NONE) {
+    if (a.bn_stats) bn_stats_epilogue<WM, WN>(a, g, acc, mb, n0, wm, wn, lane, blockIdx.x, smem, lds_floats);
+  }
+}
+
 // NS = LDS stages in the ring.  NS = 2: two workgroups per CU, the DMA of K-tile
 // kt+1 in flight while kt is multiplied.  NS = 3 / 4 (grids of at most one
 // workgroup per CU): K-tiles kt+1 .. kt+NS-1 in flight, a counted vmcnt (never 0
@@ -589,60 +654,161 @@ __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void conv_lds_kernel(LArgs a,
     }
   }
 
-  const int mb = m0 + wm * 64, nbase = n0 + wn * 64;
-  if (gridDim.y > 1) {
-    if (combine) {
-      lds_barrier();  // every wave is done with the operand stages (the ticket word lives there)
-      const int tile = blockIdx.z * a.tiles_x + blockIdx.x;
-      if (!splitk_combine<4, 4, NW * 64>(acc, a.ws, a.cnt, tile, gridDim.y, blockIdx.y, smem)) return;
-    } else if (a.ws != nullptr) {
-      // wgrad, and small-M fwd / stride-1 dgrad: this slice's fp32 partial tile into
-      // its own slab; a separate chip-wide kernel sums the slabs (slab_sum_kernel /
-      // conv_slab_epilogue_kernel with the bias / ReLU epilogue) -- deterministic, no
-      // atomics, and no single workgroup re-reading every slice of its tile
-      GemmParams p{};
-      p.C = a.ws + (size_t)blockIdx.y * a.M * a.N;
-      p.M = g.M;
-      p.N = a.N;
-      p.ldc = a.N;
-      epilogue<EPI_NONE, true, 4, 4>(p, acc, mb, nbase, lane);
-      return;
-    } else {
-      if constexpr (OUT_F32 && EPI == EPI_NONE) {  // fp32 atomics into the (cleared / accumulated) output
+  conv_tail<WM, WN, EPI, OUT_F32, DGRAD>(a, g, acc, m0, n0, wm, wn, lane, smem, NS * STAGE / 4);
+}
+
+// ---- halo path: 3x3 stride-1 pad-1 fwd / dgrad with the A operand staged ONCE --
+// The gather kernel above DMAs a fresh 64-channel A tile for every filter tap, so
+// each activation row crosses the L1 / texture path 9 times per channel block --
+// and that fill rate, not the MFMA, bounds it (11-15 % MFMA busy, profiles/).  For
+// a stride-1 3x3 convolution the 9 taps of a tile read ONE contiguous run of
+// flattened pixels: rows m0 - (W+1) .. m0 + BM + W of the NHWC activation.  This
+// kernel DMAs that halo (BM + 2W + 2 rows x 64 channels, 128-B rows, XOR-swizzled
+// like every KC image) once per channel block and reads each tap's A fragments
+// from it at a row offset dr*W + ds; a lane whose tap falls outside the image
+// (top / bottom / left / right edge, or a row past M) reads a zero row instead.
+// The B operand (weights) streams per K-tile through a 2-stage ring as before.
+// K-tile order is taps fastest inside a channel block; the halo buffer is reloaded
+// at each channel block (two workgroups per CU cover that reload's latency).
+// fwd: rows = output pixels, tap (r, s) reads x at (p + r - 1, q + s - 1);
+// dgrad: rows = input pixels, tap (r, s) reads dy at (h + 1 - r, w + 1 - s).
+constexpr int kHaloExtra = 120;  // 2W + 2 rows of halo, rounded up to 8, at most (W <= 59)
+
+template <int WM, int WN, class OB, int EPI, bool DGRAD>
+__global__ __launch_bounds__(256, 2) void conv_halo_kernel(LArgs a, const bf16_t* pa, uint32_t bytes_a,
+                                                           const bf16_t* pb, uint32_t bytes_b) {
+  constexpr int NW = WM * WN, BM = WM * 64, BN = WN * 64;
+  static_assert(NW == 4 && OB::kRows == BN && OB::kPieces == BN / 8 / NW, "operand policy geometry");
+  constexpr int HR = BM + kHaloExtra;            // halo image rows (max)
+  constexpr int H_BYTES = HR * 128, Z_BYTES = 128, B_BYTES = BN * 128;
+  // B ring depth: 2 = K-tile kt+1 in flight (measured faster than 3 on the ResNet-18
+  // shapes: the 3-stage ring's counted waits did not pay for its extra LDS)
+  constexpr int NSB = 2;
+  constexpr int LDS = H_BYTES + Z_BYTES + NSB * B_BYTES;
+  static_assert(2 * LDS <= 160 * 1024, "two workgroups per CU");
+  constexpr int PPB = OB::kPieces;
+  __shared__ __attribute__((aligned(1024))) char smem[LDS];
+  char* const halo = smem;
+  char* const zrow = smem + H_BYTES;  // 128 zero bytes: the A fragment of a tap outside the image
+  char* const bst = smem + H_BYTES + Z_BYTES;
+
+  const Geo g = make_geo(a, DGRAD);
+  const int tiles_m = (g.M + BM - 1) / BM, tiles_n = (a.N + BN - 1) / BN;
+  if ((int)blockIdx.x >= tiles_m * tiles_n) return;
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+  int m0, n0;
+  tile_coords(g.M, a.N, BM, BN, m0, n0);
+  const int kt0 = blockIdx.y * a.nk_split;
+  const int nk = max(0, min(g.nk - kt0, a.nk_split));
+
+  floatx4 acc[4][4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int n = nbase + j * 16 + 4 * (lane >> 4);
+  for (int j = 0; j < 4; ++j)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int m = mb + i * 16 + (lane & 15);
-            if (n < a.N && m < g.M) {
-              float* c = reinterpret_cast<float*>(a.out) + (size_t)m * a.N + n;
+    for (int i = 0; i < 4; ++i) acc[j][i] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  if (nk > 0) {
+    const int W = g.rows_w, P = g.rows_h;
+    const int cin = DGRAD ? a.s.K : a.s.C;            // channels of the A tensor
+    const int hrows = (BM + 2 * W + 2 + 7) & ~7;      // halo rows of this shape (<= HR)
+    const int hbase = m0 - (W + 1);                   // flattened pixel of halo row 0
+    // per row-tile: this lane's halo row at tap offset 0, and its edge flags
+    int lrow[4], edge[4];
 #pragma unroll
-              for (int r = 0; r < 4; ++r) atomicAdd(c + r, acc[j][i][r]);
-            }
-          }
+    for (int i = 0; i < 4; ++i) {
+      const int r = wm * 64 + i * 16 + (lane & 15);
+      const int m = m0 + r;
+      const int t = fdiv(m, g.f_rw), q = m - t * W, n = fdiv(t, g.f_rh), p = t - n * P;
+      lrow[i] = r + W + 1;
+      edge[i] = (p == 0 ? 1 : 0) | (p == P - 1 ? 2 : 0) | (q == 0 ? 4 : 0) | (q == W - 1 ? 8 : 0) | (m >= g.M ? 16 : 0);
+    }
+    if (threadIdx.x < 8) *reinterpret_cast<floatx4*>(zrow + threadIdx.x * 16) = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    OB ob;
+    ob.init(a, g, n0, wid, lane, kt0);
+    Rsrc ra, rb;
+    ra.r = __builtin_amdgcn_make_buffer_rsrc((void*)pa, (short)0, (int)bytes_a, 0x00020000);
+    rb.r = __builtin_amdgcn_make_buffer_rsrc((void*)pb, (short)0, (int)bytes_b, 0x00020000);
+    KS ks = ks_init(a, g, kt0);   // K-tile whose B is issued next
+    KS kc = ks;                   // K-tile being multiplied
+
+    // halo of channel block cb: 1-KiB pieces, 8 rows each, spread over the 4 waves
+    auto load_halo = [&](int cb) {
+      const int npieces = hrows >> 3;
+      for (int pc = wid; pc < npieces; pc += NW) {
+        const int j = pc * 8 + (lane >> 3);
+        const int k = ((lane & 7) ^ (j & 7)) * 8;
+        const int gp = hbase + j;
+        const int o = gp >= 0 ? (int)(((unsigned)gp * (unsigned)cin + (unsigned)(cb * 64 + k)) * 2u) : (int)kOOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(ra.r, (lds_void*)(halo + pc * 1024), 16, o, 0, 0, 0);
+      }
+    };
+
+    // prologue: B of K-tiles 0 .. NSB-2
+#pragma unroll
+    for (int t = 0; t < NSB - 1; ++t) {
+      if (t < nk) {
+        if (t > 0) {
+          ks_next(a, g, ks);
+          ob.advance(a);
+        }
+        LDNN_DMA_TILE(ob, PPB, rb, bst + t * B_BYTES, ks);
+      }
+    }
+    int cur = 0;
+    for (int kt = 0; kt < nk; ++kt) {
+      const int tap = kc.r * 3 + kc.s;
+      if (kt == 0 || tap == 0) {
+        if (kt > 0) lds_barrier();  // every wave is done reading the previous block's halo
+        load_halo(kc.cb);
+        wait_vm<0>();               // the halo (issued last) and with it every B in flight
+      } else if (NSB > 2 && kt + 1 < nk) {
+        wait_vm<PPB * (NSB - 2)>();  // B(kt) landed; later tiles may stay in flight
+      } else {
+        wait_vm<0>();
+      }
+      lds_barrier();  // publishes them; every wave is done with B(kt-1)'s stage
+      if (kt + NSB - 1 < nk) {  // B(kt+NSB-1) into the stage B(kt-1) used
+        ks_next(a, g, ks);
+        ob.advance(a);
+        LDNN_DMA_TILE(ob, PPB, rb, bst + (cur == 0 ? NSB - 1 : cur - 1) * B_BYTES, ks);
+      }
+      const int dr = DGRAD ? 1 - kc.r : kc.r - 1, ds = DGRAD ? 1 - kc.s : kc.s - 1;
+      const int toff = dr * W + ds;
+      const int emask = 16 | (dr < 0 ? 1 : 0) | (dr > 0 ? 2 : 0) | (ds < 0 ? 4 : 0) | (ds > 0 ? 8 : 0);
+      const char* lb = bst + cur * B_BYTES;
+      __builtin_amdgcn_s_setprio(1);
+      bf16x8 fa[2][4], fb[2][4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int hr = lrow[i] + toff;
+        const bool zero = (edge[i] & emask) != 0;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          const int chunk = kk * 4 + (lane >> 4);
+          const char* src = zero ? zrow + (chunk << 4) : halo + hr * 128 + ((chunk ^ (hr & 7)) << 4);
+          fa[kk][i] = *reinterpret_cast<const bf16x8*>(src);
         }
       }
-      return;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) fb[kk][j] = read_frag<OB::KC, BN>(lb, wn * 4 + j, kk, lane);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[kk][j], fa[kk][i], acc[j][i], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      cur = cur == NSB - 1 ? 0 : cur + 1;
+      ks_next(a, g, kc);
     }
   }
-  if constexpr (DGRAD && !OUT_F32) {
-    if (g.hmul == 2) {
-      store_remapped(a, g, acc, mb, nbase, lane);
-      return;
-    }
-  }
-  GemmParams p{};
-  p.C = a.out;
-  p.M = g.M;
-  p.N = a.N;
-  p.ldc = a.N;
-  p.bias = a.bias;
-  p.beta = a.beta;
-  epilogue<EPI, OUT_F32, 4, 4>(p, acc, mb, nbase, lane);
-  if constexpr (!DGRAD && !OUT_F32 && EPI == EPI_NONE) {
-    if (a.bn_stats) bn_stats_epilogue<WM, WN>(a, g, acc, mb, n0, wm, wn, lane, blockIdx.x, smem, NS * STAGE / 4);
-  }
+  conv_tail<WM, WN, EPI, false, DGRAD>(a, g, acc, m0, n0, wm, wn, lane, smem, LDS / 4);
 }
 
 // ---- big-tile path: 256 x BN tiles, one wave per SIMD (conv_q) ---------------
@@ -1022,6 +1188,38 @@ hipError_t launch(LArgs a, int epi, int splits, const bf16_t* pa, size_t ba, con
   return launch_ns<WM, WN, OA, OB, OUT_F32, DGRAD, 2>(a, epi, splits, pa, ba, pb, bb, st);
 }
 
+// Halo path (conv_halo_kernel) for 3x3 stride-1 pad-1 fwd / dgrad; LDNN_CONV_HALO=0
+// turns it off, =2 also takes the 128x128 tiles (A/B knobs).  By default only the
+// 256x64 tiles of 64-channel layers take it: there the activation tile is 4/5 of the
+// gather kernel's fill; on 128x128 tiles the weight tile dominates and the per-block
+// halo reload stalls (profiles/conv_halo_micro_r2.txt).
+int g_conv_halo = -2;  // -2: not read yet
+int halo_env() {
+  if (g_conv_halo == -2) g_conv_halo = env_int("LDNN_CONV_HALO", 1);
+  return g_conv_halo;
+}
+bool halo_ok(const ConvShape& s) {
+  return halo_env() != 0 && s.R == 3 && s.S == 3 && s.stride == 1 && s.pad == 1 && s.P == s.H && s.Q == s.W &&
+         ((2 * s.W + 2 + 7) & ~7) <= kHaloExtra;
+}
+
+template <int WM, int WN, class OB, bool DGRAD>
+hipError_t launch_halo(LArgs a, int epi, int splits, const bf16_t* pa, size_t ba, const bf16_t* pb, size_t bb,
+                       hipStream_t st) {
+  a.tap_major = 1;  // taps fastest inside a channel block: one halo per block
+  dim3 grid(a.tiles_x, splits, 1), block(256);
+#define LDNN_CONV_HALO(E) \
+  conv_halo_kernel<WM, WN, OB, E, DGRAD><<<grid, block, 0, st>>>(a, pa, (uint32_t)ba, pb, (uint32_t)bb)
+  switch (epi) {
+    case EPI_NONE: LDNN_CONV_HALO(EPI_NONE); break;
+    case EPI_BIAS: LDNN_CONV_HALO(EPI_BIAS); break;
+    case EPI_BIAS_RELU: LDNN_CONV_HALO(EPI_BIAS_RELU); break;
+    default: return hipErrorInvalidValue;
+  }
+#undef LDNN_CONV_HALO
+  return hipGetLastError();
+}
+
 // LDNN_CONV_SLAB=0: small-M fwd / dgrad use the in-launch combine (A/B knob)
 bool slab_env_off() {
   static const bool v = [] {
@@ -1250,6 +1448,8 @@ ConvWorkspace ws_of_q(const QPlan& p, int M, int N) {
 using namespace convlds;
 
 void set_conv_q(int mode) { g_conv_q = mode; }
+void set_conv_halo(int mode) { g_conv_halo = mode; }
+int get_conv_halo() { return halo_env(); }
 int get_conv_q() { return q_mode(); }
 
 ConvWorkspace conv2d_lds_workspace(const ConvShape& s, int op) {
@@ -1351,8 +1551,16 @@ hipError_t conv2d_fwd_lds(const ConvShape& s, const uint16_t* x, const uint16_t*
   }
   const size_t bx = (size_t)s.N * s.H * s.W * s.C * 2, bw = (size_t)s.K * a.rsc * 2;
   hipError_t e;
-  if (pl.wm == 4) e = launch<4, 1, FwdA<256, 8, 4>, WeightKC<64, 2, 4>, false, false>(a, epi, pl.splits, x, bx, w, bw, st);
-  else e = launch<2, 2, FwdA<128, 4, 4>, WeightKC<128, 4, 4>, false, false>(a, epi, pl.splits, x, bx, w, bw, st);
+  if (halo_ok(s) && !deep_ring(0) && (pl.wm == 4 || halo_env() == 2)) {
+    // fwd: the halo wins on the 256x64 tiles of 64-filter layers (C64 H56: 53.7 -> 35-37 us)
+    // and loses on 128x128 ones (C128 H28 25.8 -> 27.7, C512 H7 34.9 -> 40.0 us)
+    if (pl.wm == 4) e = launch_halo<4, 1, WeightKC<64, 2, 4>, false>(a, epi, pl.splits, x, bx, w, bw, st);
+    else e = launch_halo<2, 2, WeightKC<128, 4, 4>, false>(a, epi, pl.splits, x, bx, w, bw, st);
+  } else if (pl.wm == 4) {
+    e = launch<4, 1, FwdA<256, 8, 4>, WeightKC<64, 2, 4>, false, false>(a, epi, pl.splits, x, bx, w, bw, st);
+  } else {
+    e = launch<2, 2, FwdA<128, 4, 4>, WeightKC<128, 4, 4>, false, false>(a, epi, pl.splits, x, bx, w, bw, st);
+  }
   if (e != hipSuccess || !slab) return e;
   return conv_slab_epilogue(ws, y, a.M, a.N, pl.splits, bias, epi, st);
 }
@@ -1386,8 +1594,16 @@ hipError_t conv2d_dgrad_lds(const ConvShape& s, const uint16_t* dy, const uint16
   }
   const size_t bdy = (size_t)s.N * s.P * s.Q * s.K * 2, bw = (size_t)s.K * a.rsc * 2;
   hipError_t e;
-  if (pl.wm == 4) e = launch<4, 1, DgradA<256, 8, 4>, DgradB<64, 2, 4>, false, true>(a, EPI_NONE, pl.splits, dy, bdy, w, bw, st);
-  else e = launch<2, 2, DgradA<128, 4, 4>, DgradB<128, 4, 4>, false, true>(a, EPI_NONE, pl.splits, dy, bdy, w, bw, st);
+  if (halo_ok(s) && !deep_ring(0) && (pl.wm == 4 || halo_env() == 2)) {
+    // dgrad likewise: C64 H56 38.9 -> 36.5 us; on 128x128 tiles neutral to 1 us slower
+    // (ResNet-18 C128-C512) and up to 2.6 us slower on the EnhancedCNN 16x16 .. 2x2 stages
+    if (pl.wm == 4) e = launch_halo<4, 1, DgradB<64, 2, 4>, true>(a, EPI_NONE, pl.splits, dy, bdy, w, bw, st);
+    else e = launch_halo<2, 2, DgradB<128, 4, 4>, true>(a, EPI_NONE, pl.splits, dy, bdy, w, bw, st);
+  } else if (pl.wm == 4) {
+    e = launch<4, 1, DgradA<256, 8, 4>, DgradB<64, 2, 4>, false, true>(a, EPI_NONE, pl.splits, dy, bdy, w, bw, st);
+  } else {
+    e = launch<2, 2, DgradA<128, 4, 4>, DgradB<128, 4, 4>, false, true>(a, EPI_NONE, pl.splits, dy, bdy, w, bw, st);
+  }
   if (e != hipSuccess || !slab) return e;
   return conv_slab_epilogue(ws, dx, a.M, a.N, pl.splits, nullptr, EPI_NONE, st);
 }

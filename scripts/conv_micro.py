@@ -17,6 +17,8 @@ from ldnn.ops import _ext  # noqa: E402
 # ResNet-18 @224 conv shapes (C, H, K, R, stride, pad); batch from --batch
 SHAPES = [(64, 56, 64, 3, 1, 1), (64, 56, 128, 3, 2, 1), (128, 28, 128, 3, 1, 1), (128, 28, 256, 3, 2, 1),
           (256, 14, 256, 3, 1, 1), (256, 14, 512, 3, 2, 1), (512, 7, 512, 3, 1, 1), (64, 56, 128, 1, 2, 0)]
+# EnhancedCNN @32 stride-1 3x3 convs (--model enhanced_cnn)
+SHAPES_ECNN = [(128, 16, 128, 3, 1, 1), (256, 8, 256, 3, 1, 1), (512, 4, 512, 3, 1, 1), (1024, 2, 1024, 3, 1, 1)]
 
 
 def timeit(fn, iters):
@@ -37,12 +39,13 @@ def main():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--no-stock", action="store_true")
+    ap.add_argument("--model", choices=["resnet18", "enhanced_cnn"], default="resnet18")
     a = ap.parse_args()
     C_ = _ext._C
     assert C_ is not None, "ldnn extension not loaded"
     N = a.batch
     tot = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0}
-    for (C, H, K, R, st, pad) in SHAPES:
+    for (C, H, K, R, st, pad) in (SHAPES if a.model == "resnet18" else SHAPES_ECNN):
         P = (H + 2 * pad - R) // st + 1
         x = torch.randn(N, H, H, C, device="cuda").bfloat16()
         w = (torch.randn(K, R, R, C, device="cuda") * 0.05).bfloat16()

@@ -26,6 +26,11 @@ SHAPES = [
     (4, 512, 4, 4, 1024, 3, 2, 1),    # EnhancedCNN layer4 first conv (split-K combine)
     (4, 1024, 2, 2, 1024, 3, 1, 1),   # EnhancedCNN tail (split-K combine, huge K)
     (2, 64, 9, 9, 128, 5, 1, 2),      # 5x5 taps on the fast path
+    # halo path (3x3 stride 1): channel-block reloads, in-launch split-K, the widest halo
+    (2, 256, 14, 14, 256, 3, 1, 1),   # 4 row tiles x 2: split-K slices start mid-block
+    (3, 128, 28, 28, 64, 3, 1, 1),    # 256x64 fwd tiles spanning images, 2 channel blocks
+    (1, 64, 59, 59, 128, 3, 1, 1),    # W = 59: 2W + 2 = 120 halo rows (the limit)
+    (1, 64, 60, 60, 64, 3, 1, 1),     # W = 60: past the halo limit, gather kernel
 ]
 
 
@@ -159,3 +164,31 @@ def test_nchw_to_nhwc_pad(dtype, C, cp):
     ref = torch.zeros(3, 13, 17, cp, device="cuda", dtype=torch.bfloat16)
     ref[..., :C] = x.permute(0, 2, 3, 1).to(torch.bfloat16)
     assert torch.equal(out, ref)
+
+
+@pytest.mark.parametrize("N,C,H,W,K", [(2, 64, 56, 56, 64), (2, 128, 28, 28, 128), (3, 256, 14, 14, 256),
+                                       (2, 512, 7, 7, 512), (2, 128, 20, 20, 64), (1, 64, 59, 59, 128)])
+def test_halo_conv_matches_gather_kernel(N, C, H, W, K):
+    """The halo-staged 3x3 stride-1 kernels (set_conv_halo 2: every eligible fwd tile and
+    dgrad) == the per-tap gather kernels (set_conv_halo 0), bias+ReLU fwd epilogue,
+    split-K slices and channel-block reloads included."""
+    torch.manual_seed(3)
+    Cc = _ext.C()
+    x = torch.randn(N, H, W, C, device="cuda").bfloat16()
+    w = (torch.randn(K, 3, 3, C, device="cuda") * (1.0 / (C * 9) ** 0.5)).bfloat16()
+    gy = torch.randn(N, H, W, K, device="cuda").bfloat16()
+    bias = torch.randn(K, device="cuda")
+    outs = {}
+    try:
+        for mode in (0, 2):
+            Cc.set_conv_halo(mode)
+            y = torch.empty(N, H, W, K, device="cuda", dtype=torch.bfloat16)
+            Cc.conv_fwd(x, w, y, 1, 1, bias, Cc.EPI_BIAS_RELU)
+            dx = torch.empty(N, H, W, C, device="cuda", dtype=torch.bfloat16)
+            Cc.conv_dgrad(gy, w, dx, 1, 1)
+            outs[mode] = (y.float(), dx.float())
+    finally:
+        Cc.set_conv_halo(1)
+    (y0, dx0), (y2, dx2) = outs[0], outs[2]
+    torch.testing.assert_close(y2, y0, rtol=2e-2, atol=2e-2 * y0.abs().max().item())
+    torch.testing.assert_close(dx2, dx0, rtol=2e-2, atol=2e-2 * dx0.abs().max().item())
