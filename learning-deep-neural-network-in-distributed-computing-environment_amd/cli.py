@@ -75,6 +75,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--bucket_mb", type=float, default=32.0)
     p.add_argument("--grad_comm_dtype", choices=["fp32", "bf16"], default="fp32",
                    help="dtype of the per-step gradient all-reduce (bf16 halves the xGMI bytes)")
+    p.add_argument("--oneshot_bytes", type=int, default=0,
+                   help="RCCL runs: SUM all-reduces of at most this many bytes use the one-shot IPC kernel that "
+                        "reads every peer's copy over its own xGMI link (parallel/ipc.py); 0 = off")
     p.add_argument("--augment", nargs="?", const="autoaugment", default="none",
                    choices=["none", "autoaugment", "flipcrop", "autoaugment+flipcrop"],
                    help="training-set augmentation in the native input kernel (augment.hip); bare --augment = "
@@ -152,7 +155,7 @@ def main(argv=None):
     rank, world = ctx.rank, ctx.world_size
     dev = ctx.device
     torch.manual_seed(args.seed)
-    comm = default_comm()
+    comm = default_comm(args.oneshot_bytes)
 
     dataset = args.dataset or dataset_for(args.model)
     model = build_model(args.model)

@@ -6,6 +6,8 @@
 #include <torch/extension.h>
 #include <pybind11/stl.h>
 #include <vector>
+#include <cstring>
+#include <string>
 #include <mutex>
 #include <map>
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
@@ -984,6 +986,94 @@ struct GraphEvent {
   }
 };
 
+
+// One-shot all-reduce communicator (ipc.hip): this rank's staging + signal regions,
+// exported as IPC handles, and the peers' regions opened from theirs.
+struct OneShotComm {
+  int rank, world, dev;
+  size_t half_bytes;
+  char* data = nullptr;      // own staging region, 2 halves
+  uint32_t* sig = nullptr;   // own signal region (uncached)
+  int* err = nullptr;        // own error word (uncached)
+  ldnn::IpcPeers peers{};
+  std::vector<void*> opened;
+  uint32_t epoch = 0;
+  int blocks;
+
+  OneShotComm(int rank_, int world_, int64_t max_bytes, int device, int blocks_)
+      : rank(rank_), world(world_), dev(device), blocks(blocks_) {
+    TORCH_CHECK(world >= 1 && world <= ldnn::kIpcMaxRanks && rank >= 0 && rank < world, "bad rank / world");
+    TORCH_CHECK(blocks >= 1 && blocks <= ldnn::kIpcMaxBlocks, "blocks must be in [1, ", ldnn::kIpcMaxBlocks, "]");
+    half_bytes = (size_t)((max_bytes + 255) / 256 * 256);
+    check(hipSetDevice(dev), "hipSetDevice");
+    check(hipMalloc(reinterpret_cast<void**>(&data), 2 * half_bytes), "hipMalloc(staging)");
+    const size_t sbytes = sizeof(uint32_t) * ldnn::kIpcMaxBlocks * ldnn::kIpcMaxRanks;
+    check(hipExtMallocWithFlags(reinterpret_cast<void**>(&sig), sbytes, hipDeviceMallocUncached), "hipExtMalloc(signals)");
+    check(hipMemset(sig, 0, sbytes), "hipMemset(signals)");
+    check(hipExtMallocWithFlags(reinterpret_cast<void**>(&err), 256, hipDeviceMallocUncached), "hipExtMalloc(err)");
+    check(hipMemset(err, 0, 256), "hipMemset(err)");
+    check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+    peers.half_bytes = half_bytes;
+    peers.err = err;
+  }
+  ~OneShotComm() {
+    for (void* q : opened) (void)hipIpcCloseMemHandle(q);
+    if (data) (void)hipFree(data);
+    if (sig) (void)hipFree(sig);
+    if (err) (void)hipFree(err);
+  }
+  static py::bytes handle_of(void* p) {
+    hipIpcMemHandle_t h;
+    check(hipIpcGetMemHandle(&h, p), "hipIpcGetMemHandle");
+    return py::bytes(reinterpret_cast<const char*>(&h), sizeof(h));
+  }
+  py::tuple handles() const { return py::make_tuple(handle_of(data), handle_of(sig)); }
+  // handles[j] = (staging handle, signal handle) of rank j (this rank's own entry is ignored)
+  void connect(const std::vector<std::pair<std::string, std::string>>& hs) {
+    TORCH_CHECK((int)hs.size() == world, "need one handle pair per rank");
+    check(hipSetDevice(dev), "hipSetDevice");
+    for (int j = 0; j < world; ++j) {
+      if (j == rank) {
+        peers.data[j] = data;
+        peers.sig[j] = sig;
+        continue;
+      }
+      void* ptrs[2];
+      for (int k = 0; k < 2; ++k) {
+        const std::string& b = k == 0 ? hs[j].first : hs[j].second;
+        TORCH_CHECK(b.size() == sizeof(hipIpcMemHandle_t), "bad IPC handle size");
+        hipIpcMemHandle_t h;
+        std::memcpy(&h, b.data(), sizeof(h));
+        check(hipIpcOpenMemHandle(&ptrs[k], h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
+        opened.push_back(ptrs[k]);
+      }
+      peers.data[j] = reinterpret_cast<const char*>(ptrs[0]);
+      peers.sig[j] = reinterpret_cast<uint32_t*>(ptrs[1]);
+    }
+  }
+  // t <- sum over ranks of t (in place); fp32 or bf16, numel % 8 == 0, <= max_bytes
+  void all_reduce(at::Tensor t) {
+    TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "all_reduce needs a contiguous GPU tensor");
+    const bool bf16 = t.scalar_type() == at::kBFloat16;
+    TORCH_CHECK(bf16 || t.scalar_type() == at::kFloat, "fp32 or bf16 only");
+    TORCH_CHECK(t.numel() % 8 == 0, "numel must be a multiple of 8");
+    const size_t bytes = (size_t)t.numel() * t.element_size();
+    TORCH_CHECK(bytes <= half_bytes, "tensor larger than the staging buffer");
+    hipStream_t s = cur_stream(t);
+    ++epoch;
+    const int half = epoch & 1;
+    check(hipMemcpyAsync(data + (size_t)half * half_bytes, t.data_ptr(), bytes, hipMemcpyDeviceToDevice, s),
+          "hipMemcpyAsync(staging)");
+    check(ldnn::oneshot_all_reduce(peers, rank, world, epoch, half, t.numel(), bf16, t.data_ptr(), blocks, s),
+          "oneshot_all_reduce");
+  }
+  int error() const {
+    int v = 0;
+    check(hipMemcpy(&v, err, sizeof(int), hipMemcpyDeviceToHost), "hipMemcpy(err)");
+    return v;
+  }
+};
+
 PYBIND11_MODULE(_C, m) {
   py::class_<GraphEvent>(m, "GraphEvent")
       .def(py::init<>())
@@ -992,6 +1082,15 @@ PYBIND11_MODULE(_C, m) {
       .def("record", &GraphEvent::record, py::arg("stream"))
       .def("wait", &GraphEvent::wait, py::arg("stream"), "make the raw hipStream_t wait for the last record")
       .def("query", &GraphEvent::query);
+  py::class_<OneShotComm>(m, "OneShotComm")
+      .def(py::init<int, int, int64_t, int, int>(), py::arg("rank"), py::arg("world"), py::arg("max_bytes"),
+           py::arg("device"), py::arg("blocks") = 64)
+      .def("handles", &OneShotComm::handles, "(staging, signal) IPC handles of this rank")
+      .def("connect", &OneShotComm::connect, py::arg("handles"))
+      .def("all_reduce", &OneShotComm::all_reduce, py::arg("t"), "in-place sum over ranks (one kernel, one barrier)")
+      .def("error", &OneShotComm::error)
+      .def_readonly("epoch", &OneShotComm::epoch)
+      .def_readonly("half_bytes", &OneShotComm::half_bytes);
   m.doc() = "ldnn: hand-written gfx950 (MI355X / CDNA4) HIP kernels";
   m.attr("EPI_NONE") = (int)ldnn::EPI_NONE;
   m.attr("EPI_BIAS") = (int)ldnn::EPI_BIAS;

@@ -332,4 +332,17 @@ struct AugParams {
 constexpr int kAugMaxPixels = 28 * 1024;
 hipError_t augment_batch(const AugParams& p, bool out_f32, hipStream_t s);
 
+
+// ---- one-shot intra-node all-reduce over IPC-mapped peer buffers (ipc.hip) ----
+constexpr int kIpcMaxRanks = 8;     // one MI355X node
+constexpr int kIpcMaxBlocks = 256;  // signal slots per rank: [block][rank]
+struct IpcPeers {
+  const char* data[kIpcMaxRanks];   // every rank's staging region (2 halves of half_bytes)
+  uint32_t* sig[kIpcMaxRanks];      // every rank's signal region [kIpcMaxBlocks][kIpcMaxRanks]
+  int* err;                         // this rank's error word (1: a peer never arrived)
+  size_t half_bytes;
+};
+hipError_t oneshot_all_reduce(const IpcPeers& p, int rank, int world, uint32_t epoch, int half, int64_t n, bool bf16,
+                              void* out, int blocks, hipStream_t s);
+
 }  // namespace ldnn

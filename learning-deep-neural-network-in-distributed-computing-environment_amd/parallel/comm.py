@@ -19,6 +19,7 @@ schedule checker can hash the op sequence and detect rank divergence.
 from __future__ import annotations
 
 import hashlib
+import os
 import threading
 
 import torch
@@ -128,8 +129,21 @@ class TorchComm(Comm):
     def _global(self, r: int) -> int:
         return r if self.group is None else dist.get_global_rank(self.group, r)
 
+    def enable_oneshot(self, max_bytes: int, device=None):
+        """Route SUM all-reduces of at most ``max_bytes`` (fp32 / bf16 device tensors)
+        through the one-shot IPC path (parallel/ipc.py).  Collective: every rank calls it."""
+        from .ipc import OneShotAllReduce
+
+        self.oneshot = OneShotAllReduce(max_bytes, group=self.group, device=device)
+        return self.oneshot
+
+    oneshot = None
+
     def all_reduce(self, t, op=SUM, async_op=False):
         self.record("all_reduce", t)
+        if op == SUM and self.oneshot is not None and self.oneshot.eligible(t):
+            self.oneshot.all_reduce(t)  # stream-ordered: nothing to wait for on the host
+            return _Done() if async_op else None
         return dist.all_reduce(t, op=_TORCH_OPS[op], group=self.group, async_op=async_op)
 
     def broadcast(self, t, src=0):
@@ -254,7 +268,15 @@ class FakeComm(Comm):
             rt.copy_(merged[(src, self.rank)])
 
 
-def default_comm() -> Comm:
+def default_comm(oneshot_bytes: int | None = None) -> Comm:
+    """TorchComm over the default group (LocalComm for a world of one).  oneshot_bytes
+    (or env LDNN_ONESHOT_BYTES) > 0 enables the one-shot IPC all-reduce for messages up
+    to that size when the backend is RCCL (collective: every rank must pass the same)."""
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-        return TorchComm()
+        c = TorchComm()
+        if oneshot_bytes is None:
+            oneshot_bytes = int(os.environ.get("LDNN_ONESHOT_BYTES", "0"))
+        if oneshot_bytes > 0 and c.backend == "nccl" and torch.cuda.is_available():
+            c.enable_oneshot(oneshot_bytes)
+        return c
     return LocalComm()
