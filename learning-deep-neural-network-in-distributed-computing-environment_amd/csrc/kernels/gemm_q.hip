@@ -86,7 +86,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_at(const Op& op, int k0, 
   return __builtin_amdgcn_make_buffer_rsrc((void*)(op.base + shift), (short)0, past ? 0 : (int)(op.bytes - shift),
                                            0x00020000);
 }
+template <int XF = 0>
 __device__ __forceinline__ void dma1(__amdgpu_buffer_rsrc_t rs, char* dst, const Op& op, int i, bool kill, int wid) {
+  if constexpr (XF & 32) kill = true;  // experiment: issue the DMA, read nothing (out of range)
   __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(dst + (i * 4 + wid) * 1024), 16, kill ? kOOB : op.voff[i],
                                            0, 0, 0);
 }
@@ -290,7 +292,8 @@ __device__ __forceinline__ void epilogue_q(const GemmParams& p, floatx4 (&acc)[8
   }
 }
 
-// XF: experiment flags (0 in production): bit0 no in-loop DMA, bit1 no DMA wait, bit2 no in-loop ds_reads
+// XF: experiment flags (0 in production): bit0 no in-loop DMA, bit1 no DMA wait, bit2 no in-loop ds_reads,
+// bits 3 / 4: alternative DMA / read placements in sub-step 1 (see there), bit5 in-loop DMAs read nothing
 template <bool A_KC, bool B_KC, int EPI, bool OUT_F32, int XF = 0>
 __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(GemmParams p) {
   constexpr bool kDma = !(XF & 1), kWait = !(XF & 2), kRead = !(XF & 4);
@@ -371,17 +374,41 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(GemmParams p) {
     const int k2 = kbase + (t + 2) * BK;
     const __amdgpu_buffer_rsrc_t ra = rsrc_at<A_KC>(oa, k2, kend), rb = rsrc_at<B_KC>(ob, k2, kend);
     const bool killa = A_KC && (k2 + oa.kslot >= p.K), killb = B_KC && (k2 + ob.kslot >= p.K);
-    // (DMA every 4th MFMA, reads every 2nd from MFMA 1 on)
+    // (DMA every 4th MFMA, reads every 2nd from MFMA 1 on; experiment schedules:
+    // XF bit3 = reads in MFMA gaps 0..31, DMAs in gaps 32..63 every 2nd;
+    // XF bit4 = DMAs in gaps 0..31 every 2nd, reads in gaps 32..63)
     mma(acc, fa1, fb1, [&](int q) {
-      const int r = q >> 2;
-      if (kDma && !(q & 3)) {
-        if (r < 8) dma1(ra, cur, oa, r, killa, wid);
-        else dma1(rb, cur + kTile, ob, r - 8, killb, wid);
-      }
-      const int rr = q >> 1;
-      if (kRead && (q & 1) && rr < 16) {
-        if (rr < 8) fa0[rr] = frag<A_KC, kAsm>(nxt, wm * 8 + rr, 0, lane);
-        else fb0[rr - 8] = frag<B_KC, kAsm>(nxt + kTile, wn * 8 + rr - 8, 0, lane);
+      if constexpr (XF & 8) {
+        const int rr = q >> 1, r = (q - 32) >> 1;
+        if (kRead && q < 32 && (q & 1)) {
+          if (rr < 8) fa0[rr] = frag<A_KC, kAsm>(nxt, wm * 8 + rr, 0, lane);
+          else fb0[rr - 8] = frag<B_KC, kAsm>(nxt + kTile, wn * 8 + rr - 8, 0, lane);
+        }
+        if (kDma && q >= 32 && !(q & 1)) {
+          if (r < 8) dma1<XF>(ra, cur, oa, r, killa, wid);
+          else dma1<XF>(rb, cur + kTile, ob, r - 8, killb, wid);
+        }
+      } else if constexpr (XF & 16) {
+        const int r = q >> 1, rr = (q - 32) >> 1;
+        if (kDma && q < 32 && !(q & 1)) {
+          if (r < 8) dma1<XF>(ra, cur, oa, r, killa, wid);
+          else dma1<XF>(rb, cur + kTile, ob, r - 8, killb, wid);
+        }
+        if (kRead && q >= 32 && (q & 1)) {
+          if (rr < 8) fa0[rr] = frag<A_KC, kAsm>(nxt, wm * 8 + rr, 0, lane);
+          else fb0[rr - 8] = frag<B_KC, kAsm>(nxt + kTile, wn * 8 + rr - 8, 0, lane);
+        }
+      } else {
+        const int r = q >> 2;
+        if (kDma && !(q & 3)) {
+          if (r < 8) dma1<XF>(ra, cur, oa, r, killa, wid);
+          else dma1<XF>(rb, cur + kTile, ob, r - 8, killb, wid);
+        }
+        const int rr = q >> 1;
+        if (kRead && (q & 1) && rr < 16) {
+          if (rr < 8) fa0[rr] = frag<A_KC, kAsm>(nxt, wm * 8 + rr, 0, lane);
+          else fb0[rr - 8] = frag<B_KC, kAsm>(nxt + kTile, wn * 8 + rr - 8, 0, lane);
+        }
       }
     });
   }
@@ -415,6 +442,9 @@ hipError_t dispatch_epi(const GemmParams& p, int epi, hipStream_t s) {
         case 2: gemm_kernel<true, true, EPI_BIAS_RELU, false, 2><<<grid, block, 0, s>>>(p); break;
         case 4: gemm_kernel<true, true, EPI_BIAS_RELU, false, 4><<<grid, block, 0, s>>>(p); break;
         case 5: gemm_kernel<true, true, EPI_BIAS_RELU, false, 5><<<grid, block, 0, s>>>(p); break;
+        case 8: gemm_kernel<true, true, EPI_BIAS_RELU, false, 8><<<grid, block, 0, s>>>(p); break;
+        case 16: gemm_kernel<true, true, EPI_BIAS_RELU, false, 16><<<grid, block, 0, s>>>(p); break;
+        case 32: gemm_kernel<true, true, EPI_BIAS_RELU, false, 32><<<grid, block, 0, s>>>(p); break;
         default: return hipErrorInvalidValue;
       }
       return hipGetLastError();
