@@ -811,6 +811,113 @@ __global__ __launch_bounds__(256, 2) void conv_halo_kernel(LArgs a, const bf16_t
   conv_tail<WM, WN, EPI, false, DGRAD>(a, g, acc, m0, n0, wm, wn, lane, smem, LDS / 4);
 }
 
+// ---- patch path: small-C stems (C = 8: 3 / 1 real channels) -------------------
+// FwdASmallC gathers one 16-B (tap, 8-channel) chunk per lane per tap: every input
+// pixel crosses the L1 / texture path once per filter tap that covers it (49x for
+// the 7x7 ResNet stem, ~12x per output at stride 2), each chunk its own address --
+// the stem ran at ~75 TFLOP/s (profiles/).  Here a 256-pixel output tile (one
+// image, P*Q % 256 == 0) DMAs its whole input patch ONCE: input rows
+// stride*p_lo - pad ... , every column -pad .. W+pad-1, 16 B per pixel, zero-filled
+// outside the image by the buffer range check.  The A fragment of tap t for output
+// pixel (p, q) is the 16-B patch cell (stride*(p - p_lo) + r, stride*q + s): one
+// ds_read_b128 at a per-lane base plus a per-(k-step, lane-group) tap offset.
+// B (the [K][R*S*8] weights, a few tens of KB, L2-resident) is read straight from
+// global memory into registers, one k-step ahead.  4 waves x 64 output pixels x
+// 64 filters, v_mfma_f32_16x16x32_bf16 (a k-step = 4 taps x 8 channels).
+constexpr int kPatchBytes = 48 * 1024;
+
+template <int KS, int STR, int EPI>
+__global__ __launch_bounds__(256, 2) void conv_patch_kernel(LArgs a, const bf16_t* px, uint32_t bytes_x,
+                                                            const bf16_t* pw) {
+  constexpr int WM = 4, WN = 1, BM = 256, BN = 64;
+  __shared__ __attribute__((aligned(1024))) char smem[kPatchBytes];
+  const ConvShape& sh = a.s;
+  const Geo g = make_geo(a, false);
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wid, wn = 0;
+  int m0, n0;
+  tile_coords(g.M, a.N, BM, BN, m0, n0);
+  const int PQ = sh.P * sh.Q;
+  const int n_img = m0 / PQ, mi0 = m0 - n_img * PQ;  // tiles never straddle images (PQ % 256 == 0)
+  const int p_lo = mi0 / sh.Q;
+  const int PW = sh.W + 2 * sh.pad;                   // patch columns
+  const int PH = ((mi0 + BM - 1) / sh.Q - p_lo) * STR + sh.R;
+  const int cells = PH * PW;
+
+  // ---- patch DMA: cell e = (i, j) -> input (STR*p_lo - pad + i, j - pad)
+  {
+    Rsrc rx;
+    rx.r = __builtin_amdgcn_make_buffer_rsrc((void*)px, (short)0, (int)bytes_x, 0x00020000);
+    const int ih0 = STR * p_lo - sh.pad;
+    const int npieces = (cells + 63) >> 6;
+    for (int pc = wid; pc < npieces; pc += 4) {
+      const int e = pc * 64 + lane;
+      const int i = fdiv(e, a.f_w), j = e - i * PW;   // f_w: division by PW (host)
+      const int ih = ih0 + i, iw = j - sh.pad;
+      const bool ok = e < cells && (unsigned)ih < (unsigned)sh.H && (unsigned)iw < (unsigned)sh.W;
+      const int o = ok ? (int)((((unsigned)n_img * sh.H + ih) * (unsigned)sh.W + iw) * 16u) : (int)kOOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx.r, (lds_void*)(smem + pc * 1024), 16, o, 0, 0, 0);
+    }
+  }
+  // ---- per-lane geometry: patch cell of tap (0, 0) for each of the wave's 4 row tiles,
+  // and this lane group's tap offsets for each k-step (-1: a padding tap past R*S)
+  int base[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int mi = mi0 + wm * 64 + i * 16 + (lane & 15);
+    const int p = mi / sh.Q, q = mi - p * sh.Q;
+    base[i] = (STR * (p - p_lo)) * PW + STR * q;
+  }
+  int toff[KS];
+  const int RS = sh.R * sh.S;
+#pragma unroll
+  for (int k = 0; k < KS; ++k) {
+    const int t = k * 4 + (lane >> 4);
+    const int r = t / sh.S;
+    toff[k] = t < RS ? r * PW + (t - r * sh.S) : -1;
+  }
+  // B fragment of k-step k, filter tile j: filter n0 + j*16 + (lane & 15), k = 8 * tap
+  const int rsc = a.rsc;
+  auto bfrag = [&](int k, int j) -> bf16x8 {
+    const int t = k * 4 + (lane >> 4);
+    const int n = n0 + j * 16 + (lane & 15);
+    if (t >= RS || n >= a.N) return bf16x8{};
+    return *reinterpret_cast<const bf16x8*>(pw + (size_t)n * rsc + t * 8);
+  };
+
+  floatx4 acc[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[j][i] = floatx4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 fb[2][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) fb[0][j] = bfrag(0, j);
+  wait_vm<0>();
+  lds_barrier();  // the patch landed
+#pragma unroll
+  for (int k = 0; k < KS; ++k) {
+    if (k + 1 < KS) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[(k + 1) & 1][j] = bfrag(k + 1, j);
+    }
+    bf16x8 fa[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int cell = base[i] + toff[k];
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(smem + (toff[k] >= 0 ? cell : 0) * 16);
+      fa[i] = toff[k] >= 0 ? v : bf16x8{};
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[k & 1][j], fa[i], acc[j][i], 0, 0, 0);
+  }
+  conv_tail<WM, WN, EPI, false, false>(a, g, acc, m0, n0, wm, wn, lane, smem, kPatchBytes / 4);
+}
+
 // ---- big-tile path: 256 x BN tiles, one wave per SIMD (conv_q) ---------------
 // The 128x128 / 2-workgroup kernel above is bound by the operand fill rate, not
 // by the MFMAs: a 128x128x64 step needs 32 KiB through the vector L1 / texture
@@ -1477,6 +1584,50 @@ hipError_t slab_sum(const float* ws, float* out, int64_t n4, int splits, float b
   return hipGetLastError();
 }
 
+// Patch path for C = 8 stems (conv_patch_kernel): 3x3 / 5x5 / 7x7 taps, stride 1 or 2,
+// P*Q % 256 == 0 (tiles inside one image), K % 64 == 0, the patch within 48 KiB.
+// LDNN_CONV_PATCH=0 turns it off (A/B knob).
+int patch_env() {
+  static const int v = env_int("LDNN_CONV_PATCH", 1);
+  return v;
+}
+int patch_ks(const ConvShape& s) {
+  const int rs = s.R * s.S;
+  return rs == 9 ? 3 : rs == 25 ? 7 : rs == 49 ? 13 : 0;
+}
+bool patch_ok(const ConvShape& s) {
+  if (patch_env() == 0 || s.C != 8 || s.K % 64 != 0 || patch_ks(s) == 0 || (s.stride != 1 && s.stride != 2)) return false;
+  const int pq = s.P * s.Q;
+  if (pq % 256 != 0) return false;
+  const int rows_out = (255 + s.Q - 1) / s.Q + 1;  // output rows a 256-pixel tile can touch
+  const int ph = (rows_out - 1) * s.stride + s.R;
+  return (size_t)ph * (s.W + 2 * s.pad) * 16 <= (size_t)kPatchBytes;
+}
+template <int KS, int STR>
+hipError_t launch_patch_e(const LArgs& a, int epi, const bf16_t* x, size_t bx, const bf16_t* w, hipStream_t st) {
+  const dim3 grid(a.tiles_x), block(256);
+  switch (epi) {
+    case EPI_NONE: conv_patch_kernel<KS, STR, EPI_NONE><<<grid, block, 0, st>>>(a, x, (uint32_t)bx, w); break;
+    case EPI_BIAS: conv_patch_kernel<KS, STR, EPI_BIAS><<<grid, block, 0, st>>>(a, x, (uint32_t)bx, w); break;
+    case EPI_BIAS_RELU: conv_patch_kernel<KS, STR, EPI_BIAS_RELU><<<grid, block, 0, st>>>(a, x, (uint32_t)bx, w); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+hipError_t launch_patch(LArgs a, int epi, const bf16_t* x, size_t bx, const bf16_t* w, hipStream_t st) {
+  a.f_w = make_fastdiv(a.s.W + 2 * a.s.pad);  // patch row length (cell -> row, column)
+  a.tiles_x = (a.M / 256) * (a.N / 64);
+  const int ks = patch_ks(a.s);
+  if (a.s.stride == 1) {
+    if (ks == 3) return launch_patch_e<3, 1>(a, epi, x, bx, w, st);
+    if (ks == 7) return launch_patch_e<7, 1>(a, epi, x, bx, w, st);
+    return launch_patch_e<13, 1>(a, epi, x, bx, w, st);
+  }
+  if (ks == 3) return launch_patch_e<3, 2>(a, epi, x, bx, w, st);
+  if (ks == 7) return launch_patch_e<7, 2>(a, epi, x, bx, w, st);
+  return launch_patch_e<13, 2>(a, epi, x, bx, w, st);
+}
+
 // Each returns hipErrorNotSupported when the shape is outside the fast path
 // (conv.hip then runs its generic register-staged kernel).
 // Stems and other small-C convolutions (C in {8, 16, 32}, e.g. the 7x7 ResNet stem
@@ -1500,6 +1651,7 @@ hipError_t conv2d_fwd_lds_small_c(const ConvShape& s, const uint16_t* x, const u
   const bool narrow = s.K <= 64;
   a.tiles_x = ((a.M + (narrow ? 255 : 127)) / (narrow ? 256 : 128)) * ((s.K + (narrow ? 63 : 127)) / (narrow ? 64 : 128));
   const size_t bx = (size_t)s.N * s.H * s.W * s.C * 2, bw = (size_t)s.K * a.rsc * 2;
+  if (patch_ok(s)) return launch_patch(a, epi, x, bx, w, st);
   if (narrow) return launch<4, 1, FwdASmallC<256, 8, 4>, WeightKC<64, 2, 4>, false, false>(a, epi, 1, x, bx, w, bw, st);
   return launch<2, 2, FwdASmallC<128, 4, 4>, WeightKC<128, 4, 4>, false, false>(a, epi, 1, x, bx, w, bw, st);
 }

@@ -31,6 +31,10 @@ SHAPES = [
     (3, 128, 28, 28, 64, 3, 1, 1),    # 256x64 fwd tiles spanning images, 2 channel blocks
     (1, 64, 59, 59, 128, 3, 1, 1),    # W = 59: 2W + 2 = 120 halo rows (the limit)
     (1, 64, 60, 60, 64, 3, 1, 1),     # W = 60: past the halo limit, gather kernel
+    # patch path (C = 8 stems, P*Q % 256 == 0): the full ResNet stem, 2 filter tiles, 5x5 taps
+    (2, 3, 224, 224, 64, 7, 2, 3),
+    (2, 3, 32, 32, 128, 3, 1, 1),
+    (2, 8, 32, 32, 64, 5, 1, 2),
 ]
 
 
@@ -87,7 +91,8 @@ def test_conv_fwd_dgrad_wgrad(N, C, H, W, K, R, st, pad):
 @pytest.mark.parametrize("N,C,H,W,K,R,st,pad", [(2, 64, 17, 17, 128, 3, 2, 1), (4, 512, 4, 4, 1024, 3, 2, 1),
                                                 (2, 128, 16, 16, 64, 3, 1, 1), (4, 1024, 2, 2, 1024, 3, 1, 1),
                                                 (2, 8, 40, 40, 64, 7, 2, 3), (3, 16, 9, 9, 32, 3, 1, 1),
-                                                (2, 32, 12, 12, 128, 5, 1, 2)])
+                                                (2, 32, 12, 12, 128, 5, 1, 2), (2, 8, 64, 64, 64, 7, 2, 3),
+                                                (3, 8, 32, 32, 128, 3, 1, 1)])
 def test_lds_fast_path_matches_generic_kernel(N, C, H, W, K, R, st, pad):
     """The LDS-DMA kernels (set_conv_impl(0)) agree with the generic register-staged
     kernels (set_conv_impl(1)) on every output, and repeated launches of the
