@@ -360,18 +360,35 @@ void mix3(const at::Tensor& out, const at::Tensor& x, const c10::optional<at::Te
         "mix3");
 }
 
+// Self-cleaning [acc0, acc1, counter] of the finalizing softmax-xent, one per
+// (device, stream): the kernels leave it zero, so it is zeroed once at creation.
+int* xent_fin_ws(const at::Tensor& like) {
+  static std::mutex mu;
+  static std::map<std::pair<int, int64_t>, at::Tensor> pools;
+  const auto key = std::make_pair((int)like.get_device(), (int64_t)cur_stream(like));
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = pools.find(key);
+  if (it == pools.end()) it = pools.emplace(key, at::zeros({4}, like.options().dtype(at::kInt))).first;
+  return it->second.data_ptr<int>();
+}
+
 void softmax_xent(const at::Tensor& logits, const at::Tensor& labels, const at::Tensor& dlogits,
-                  const at::Tensor& stats, const c10::optional<at::Tensor>& dbias, int64_t num_classes,
-                  double grad_scale) {
+                  const c10::optional<at::Tensor>& stats, const c10::optional<at::Tensor>& dbias, int64_t num_classes,
+                  double grad_scale, const c10::optional<at::Tensor>& loss_out, double loss_scale) {
   check_dev(logits, at::kBFloat16, "logits");
   check_dev(dlogits, at::kBFloat16, "dlogits");
   check_dev(labels, at::kLong, "labels");
-  check_dev(stats, at::kFloat, "stats");
+  float* st = nullptr;
+  if (stats.has_value()) {
+    check_dev(*stats, at::kFloat, "stats");
+    TORCH_CHECK(stats->numel() >= 2, "xent: stats needs 2 floats");
+    st = stats->data_ptr<float>();
+  }
+  TORCH_CHECK(st != nullptr || loss_out.has_value(), "xent: give stats and/or loss_out");
   TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1 && dlogits.sizes() == logits.sizes() &&
                   dlogits.strides() == logits.strides(),
               "xent: logits/dlogits layout mismatch");
   TORCH_CHECK(labels.is_contiguous() && labels.numel() == logits.size(0), "xent: bad labels");
-  TORCH_CHECK(stats.numel() >= 2, "xent: stats needs 2 floats");
   // logits may be a [B][C] view of a zero-padded [B][ld] buffer (ld % 8 == 0):
   // the kernel reads C columns and writes all ld columns of dlogits (pad = 0).
   const int64_t ld = logits.stride(0);
@@ -384,9 +401,19 @@ void softmax_xent(const at::Tensor& logits, const at::Tensor& labels, const at::
     TORCH_CHECK(dbias->numel() >= ld, "xent: bad dbias");
     db = dbias->data_ptr<float>();
   }
-  check(ldnn::softmax_xent(bf16_ptr(logits), labels.data_ptr<int64_t>(), bf16_mut(dlogits),
-                           stats.data_ptr<float>(), db, (int)logits.size(0), (int)num_classes, (int)ld,
-                           (float)grad_scale, cur_stream(logits)),
+  ldnn::XentFin fin;
+  if (loss_out.has_value()) {
+    check_dev(*loss_out, at::kFloat, "loss_out");
+    TORCH_CHECK(loss_out->numel() >= 2 && loss_out->is_contiguous(), "xent: loss_out needs 2 dense floats");
+    int* ws = xent_fin_ws(logits);
+    fin.out = loss_out->data_ptr<float>();
+    fin.acc = reinterpret_cast<float*>(ws);
+    fin.cnt = reinterpret_cast<unsigned*>(ws + 2);
+    fin.scale = (float)loss_scale;
+  }
+  check(ldnn::softmax_xent(bf16_ptr(logits), labels.data_ptr<int64_t>(), bf16_mut(dlogits), st, db,
+                           (int)logits.size(0), (int)num_classes, (int)ld, (float)grad_scale, cur_stream(logits),
+                           loss_out.has_value() ? &fin : nullptr),
         "softmax_xent");
 }
 
@@ -869,7 +896,7 @@ void bn_bwd(const at::Tensor& x, const at::Tensor& y, const at::Tensor& dy, cons
             const c10::optional<at::Tensor>& dres, const c10::optional<at::Tensor>& gamma,
             const at::Tensor& save_mean, const at::Tensor& save_invstd, const at::Tensor& ws,
             const c10::optional<at::Tensor>& dgamma, const c10::optional<at::Tensor>& dbeta, bool relu,
-            const c10::optional<at::Tensor>& mask, bool grad_assign) {
+            const c10::optional<at::Tensor>& mask, bool grad_assign, const c10::optional<at::Tensor>& dy2) {
   check_dev(x, at::kBFloat16, "x");
   check_dev(dy, at::kBFloat16, "dy");
   check_dev(dx, at::kBFloat16, "dx");
@@ -891,6 +918,11 @@ void bn_bwd(const at::Tensor& x, const at::Tensor& y, const at::Tensor& dy, cons
     check_dev(*mask, at::kByte, "mask");
     TORCH_CHECK(relu && mask->is_contiguous() && mask->numel() == M * C / 8, "bn_bwd: mask needs relu, [M][C/8]");
     a.mask = mask->data_ptr<uint8_t>();
+  }
+  if (dy2.has_value()) {
+    check_dev(*dy2, at::kBFloat16, "dy2");
+    TORCH_CHECK(dy2->sizes() == x.sizes() && dy2->is_contiguous(), "bn_bwd: dy2 layout");
+    a.dy2 = bf16_ptr(*dy2);
   }
   uint16_t* dr = nullptr;
   if (dres.has_value()) {
@@ -914,6 +946,7 @@ void pool_fwd(const at::Tensor& x, const at::Tensor& y, const c10::optional<at::
     TORCH_CHECK(argmax.has_value() && argmax->scalar_type() == at::kByte && argmax->numel() == y.numel(),
                 "pool: max pooling needs a uint8 argmax tensor");
     am = argmax->data_ptr<uint8_t>();
+    TORCH_CHECK(argmax->is_contiguous() && ((uintptr_t)am & 7) == 0, "pool: argmax must be dense and 8-B aligned");
   }
   check(ldnn::pool2d_fwd(bf16_ptr(x), bf16_mut(y), am, (int)x.size(0), (int)x.size(1), (int)x.size(2),
                          (int)x.size(3), (int)y.size(1), (int)y.size(2), (int)R, (int)S, (int)stride, (int)pad, is_max,
@@ -922,7 +955,7 @@ void pool_fwd(const at::Tensor& x, const at::Tensor& y, const c10::optional<at::
 }
 
 void pool_bwd(const at::Tensor& dy, const c10::optional<at::Tensor>& argmax, const at::Tensor& dx, int64_t R,
-              int64_t S, int64_t stride, int64_t pad, bool is_max) {
+              int64_t S, int64_t stride, int64_t pad, bool is_max, const c10::optional<at::Tensor>& dy2) {
   check_dev(dy, at::kBFloat16, "dy");
   check_dev(dx, at::kBFloat16, "dx");
   TORCH_CHECK(dy.is_contiguous() && dx.is_contiguous(), "pool_bwd: dense NHWC");
@@ -930,10 +963,17 @@ void pool_bwd(const at::Tensor& dy, const c10::optional<at::Tensor>& argmax, con
   if (is_max) {
     TORCH_CHECK(argmax.has_value() && argmax->numel() == dy.numel(), "pool_bwd: argmax");
     am = argmax->data_ptr<uint8_t>();
+    TORCH_CHECK(argmax->is_contiguous() && ((uintptr_t)am & 7) == 0, "pool: argmax must be dense and 8-B aligned");
+  }
+  const uint16_t* d2 = nullptr;
+  if (dy2.has_value()) {
+    check_dev(*dy2, at::kBFloat16, "dy2");
+    TORCH_CHECK(dy2->sizes() == dy.sizes() && dy2->is_contiguous(), "pool_bwd: dy2 layout");
+    d2 = bf16_ptr(*dy2);
   }
   check(ldnn::pool2d_bwd(bf16_ptr(dy), am, bf16_mut(dx), (int)dx.size(0), (int)dx.size(1), (int)dx.size(2),
                          (int)dx.size(3), (int)dy.size(1), (int)dy.size(2), (int)R, (int)S, (int)stride, (int)pad,
-                         is_max, cur_stream(dy)),
+                         is_max, cur_stream(dy), d2),
         "pool2d_bwd");
 }
 
@@ -1198,7 +1238,20 @@ PYBIND11_MODULE(_C, m) {
   m.def("mix3", &mix3, py::arg("out"), py::arg("x"), py::arg("y1") = py::none(), py::arg("y2") = py::none(),
         py::arg("a") = 1.0, py::arg("b") = 0.0, py::arg("c") = 0.0, py::arg("shadow") = py::none());
   m.def("softmax_xent", &softmax_xent, py::arg("logits"), py::arg("labels"), py::arg("dlogits"),
-        py::arg("stats"), py::arg("dbias") = py::none(), py::arg("num_classes"), py::arg("grad_scale"));
+        py::arg("stats"), py::arg("dbias") = py::none(), py::arg("num_classes"), py::arg("grad_scale"),
+        py::arg("loss_out") = py::none(), py::arg("loss_scale") = 1.0,
+        "fused softmax-xent + argmax; loss_out: the last block writes [loss_sum * loss_scale, #correct] there "
+        "(and adds both into stats if given)");
+  m.def("scale_bf16", [](const at::Tensor& src, const at::Tensor& scale, const at::Tensor& out) {
+    check_dev(src, at::kBFloat16, "src");
+    check_dev(out, at::kBFloat16, "out");
+    check_dev(scale, at::kFloat, "scale");
+    TORCH_CHECK(src.is_contiguous() && out.is_contiguous() && src.numel() == out.numel() && scale.numel() >= 1,
+                "scale_bf16: dense tensors of one size");
+    c10::hip::HIPGuardMasqueradingAsCUDA g(src.device());
+    check(ldnn::scale_bf16_dev(bf16_ptr(src), scale.data_ptr<float>(), bf16_mut(out), src.numel(), cur_stream(src)),
+          "scale_bf16");
+  }, py::arg("src"), py::arg("scale"), py::arg("out"), "out = src * scale[0] (device scalar)");
   // roctx ranges (rocprofv3 --marker-trace shows them on the timeline)
   m.def("trace_push", [](const std::string& s) { return roctxRangePushA(s.c_str()); }, py::arg("name"));
   m.def("trace_pop", []() { return roctxRangePop(); });
@@ -1241,9 +1294,11 @@ PYBIND11_MODULE(_C, m) {
         py::arg("C"));
   m.def("bn_bwd", &bn_bwd, py::arg("x"), py::arg("y"), py::arg("dy"), py::arg("dx"), py::arg("dres"),
         py::arg("gamma"), py::arg("save_mean"), py::arg("save_invstd"), py::arg("ws"), py::arg("dgamma"),
-        py::arg("dbeta"), py::arg("relu"), py::arg("mask") = py::none(), py::arg("grad_assign") = false);
+        py::arg("dbeta"), py::arg("relu"), py::arg("mask") = py::none(), py::arg("grad_assign") = false,
+        py::arg("dy2") = py::none());
   m.def("pool_fwd", &pool_fwd);
-  m.def("pool_bwd", &pool_bwd);
+  m.def("pool_bwd", &pool_bwd, py::arg("dy"), py::arg("argmax"), py::arg("dx"), py::arg("R"), py::arg("S"),
+        py::arg("stride"), py::arg("pad"), py::arg("is_max"), py::arg("dy2") = py::none());
   m.def("gap_fwd", &gap_fwd);
   m.def("gap_bwd", &gap_bwd);
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("stride"), py::arg("pad"),

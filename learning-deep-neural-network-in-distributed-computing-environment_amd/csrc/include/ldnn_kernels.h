@@ -159,6 +159,8 @@ struct BnArgs {
   int64_t* num_batches;       // optional BatchNorm2d.num_batches_tracked, += 1 per training forward
   uint8_t* mask;              // optional [M][C/8] ReLU bits: written by a relu forward, read by the
                               // backward instead of y (1/16 of y's bytes per read)
+  const uint16_t* dy2;        // backward: optional second gradient of y, summed with dy on the fly
+                              // (a residual block's shortcut-branch gradient: no separate add pass)
 };
 int bn_workspace_floats(int C);
 hipError_t bn_forward(const BnArgs& a, hipStream_t s);
@@ -191,7 +193,8 @@ hipError_t bn_backward(const BnArgs& a, const uint16_t* dy, uint16_t* dx, uint16
 hipError_t pool2d_fwd(const uint16_t* x, uint16_t* y, uint8_t* argmax, int N, int H, int W, int C, int P, int Q,
                       int R, int S, int stride, int pad, bool is_max, hipStream_t s);
 hipError_t pool2d_bwd(const uint16_t* dy, const uint8_t* argmax, uint16_t* dx, int N, int H, int W, int C, int P,
-                      int Q, int R, int S, int stride, int pad, bool is_max, hipStream_t s);
+                      int Q, int R, int S, int stride, int pad, bool is_max, hipStream_t s,
+                      const uint16_t* dy2 = nullptr);
 hipError_t global_avgpool_fwd(const uint16_t* x, uint16_t* y, int N, int HW, int C, hipStream_t s);
 hipError_t global_avgpool_bwd(const uint16_t* dy, uint16_t* dx, int N, int HW, int C, hipStream_t s);
 
@@ -226,8 +229,21 @@ hipError_t scale_f32(float* x, float scale, int64_t n, uint16_t* shadow, hipStre
 // Writes dlogits [B][ld] bf16 = (softmax - onehot) * grad_scale (padded columns 0),
 // accumulates sum of per-row loss into stats[0] and #correct into stats[1]
 // (fp32), optionally column sums of dlogits into dbias[ld].
+// With fin.out set the per-row sums go to fin.acc (2 floats + an arrival counter,
+// zero at entry and left zero: a persistent workspace) and the last block writes
+// fin.out = [loss_sum * fin.scale, #correct], adds both into `stats` if given --
+// the loss scalar and the running statistics with no fill / divide / add launches.
+struct XentFin {
+  float* out = nullptr;
+  float* acc = nullptr;
+  unsigned* cnt = nullptr;
+  float scale = 1.f;
+};
 hipError_t softmax_xent(const uint16_t* logits, const int64_t* labels, uint16_t* dlogits, float* stats,
-                        float* dbias, int B, int C, int ld, float grad_scale, hipStream_t s);
+                        float* dbias, int B, int C, int ld, float grad_scale, hipStream_t s,
+                        const XentFin* fin = nullptr);
+// out[i] = src[i] * (*scale) over n bf16 (the loss backward's grad_output, read on the device)
+hipError_t scale_bf16_dev(const uint16_t* src, const float* scale, uint16_t* out, int64_t n, hipStream_t s);
 
 // ---- fused optimizers over flat fp32 buffers -------------------------------
 // hp (device fp32): [0]=lr [1]=step (already incremented for Adam) ; grad_scale multiplies g

@@ -85,21 +85,25 @@ RedGeo red_geo(int M, int C, bool reduce = false) {
 }
 
 // RELU: g = dy * relu'(y); MASK: relu'(y) from the forward's bit mask (mask + o / 8)
+// dy2 (nullable, wave-uniform): a second gradient of the same output, added to dy
 template <bool BWD, bool RELU, bool MASK = false>
 __device__ __forceinline__ void red_row(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
                                         const bf16_t* __restrict__ y, size_t o, const float (&mu)[8],
                                         const float (&is)[8], float (&s0)[8], float (&s1)[8],
-                                        const uint8_t* __restrict__ mask = nullptr) {
+                                        const uint8_t* __restrict__ mask = nullptr,
+                                        const bf16_t* __restrict__ dy2 = nullptr) {
   const u16x8 xv = *reinterpret_cast<const u16x8*>(x + o);
   if constexpr (BWD) {
     const u16x8 gv = *reinterpret_cast<const u16x8*>(dy + o);
+    u16x8 g2v = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (dy2) g2v = *reinterpret_cast<const u16x8*>(dy2 + o);
     u16x8 yv;
     uint32_t mb = 0;
     if constexpr (RELU && MASK) mb = mask[o >> 3];
     else if constexpr (RELU) yv = *reinterpret_cast<const u16x8*>(y + o);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      float g = bf2f(gv[j]);
+      float g = bf2f(gv[j]) + bf2f(g2v[j]);
       if constexpr (RELU && MASK) g = ((mb >> j) & 1u) ? g : 0.f;
       else if constexpr (RELU) g = bf2f(yv[j]) > 0.f ? g : 0.f;
       s0[j] += g;
@@ -120,7 +124,8 @@ __global__ __launch_bounds__(256) void bn_reduce_kernel(const bf16_t* __restrict
                                                         const bf16_t* __restrict__ y, const float* __restrict__ mean,
                                                         const float* __restrict__ invstd, float* __restrict__ acc,
                                                         int M, int C, int rpb, int lanes, int rl, BnFin fin,
-                                                        const uint8_t* __restrict__ mask, int ncop) {
+                                                        const uint8_t* __restrict__ mask, int ncop,
+                                                        const bf16_t* __restrict__ dy2 = nullptr) {
   __shared__ float red[2][256 * 8];
   const int tid = threadIdx.x, lane = tid % lanes, rlane = tid / lanes;
   const int cv0 = blockIdx.x * 256 + lane;
@@ -147,9 +152,9 @@ __global__ __launch_bounds__(256) void bn_reduce_kernel(const bf16_t* __restrict
     for (; r + 3 * rl < r_end; r += 4 * rl) {
 #pragma unroll
       for (int u = 0; u < 4; ++u)
-        red_row<BWD, RELU, MASK>(x, dy, y, (size_t)(r + u * rl) * C + c0, mu, is, s0, s1, mask);
+        red_row<BWD, RELU, MASK>(x, dy, y, (size_t)(r + u * rl) * C + c0, mu, is, s0, s1, mask, dy2);
     }
-    for (; r < r_end; r += rl) red_row<BWD, RELU, MASK>(x, dy, y, (size_t)r * C + c0, mu, is, s0, s1, mask);
+    for (; r < r_end; r += rl) red_row<BWD, RELU, MASK>(x, dy, y, (size_t)r * C + c0, mu, is, s0, s1, mask, dy2);
   }
   const int row = lanes * 8;
   if (rlane < rl) {
@@ -239,7 +244,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16_t* __restr
                                                            const bf16_t* __restrict__ y,
                                                            const float* __restrict__ coef, bf16_t* __restrict__ dx,
                                                            bf16_t* __restrict__ dres, int M, int C, int rpb,
-                                                           int lanes, int rl, const uint8_t* __restrict__ mask = nullptr) {
+                                                           int lanes, int rl, const uint8_t* __restrict__ mask = nullptr,
+                                                           const bf16_t* __restrict__ dy2 = nullptr) {
   const int tid = threadIdx.x, lane = tid % lanes, rlane = tid / lanes;
   const int c0 = (blockIdx.x * 256 + lane) * 8;
   if (rlane >= rl || c0 >= C) return;
@@ -253,6 +259,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16_t* __restr
     const size_t o = (size_t)r * C + c0;
     const u16x8 xv = *reinterpret_cast<const u16x8*>(x + o);
     const u16x8 gv = *reinterpret_cast<const u16x8*>(dy + o);
+    u16x8 g2v = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (dy2) g2v = *reinterpret_cast<const u16x8*>(dy2 + o);
     u16x8 yv;
     uint32_t mb = 0;
     if constexpr (RELU && MASK) mb = mask[o >> 3];
@@ -260,7 +268,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16_t* __restr
     u16x8 out, og;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      float g = bf2f(gv[j]);
+      float g = bf2f(gv[j]) + bf2f(g2v[j]);
       if constexpr (RELU && MASK) g = ((mb >> j) & 1u) ? g : 0.f;
       else if constexpr (RELU) g = bf2f(yv[j]) > 0.f ? g : 0.f;
       out[j] = f2bf(A[j] * g + B[j] * bf2f(xv[j]) + D[j]);
@@ -272,102 +280,122 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16_t* __restr
 }
 
 // ---- pooling (NHWC): one thread per 8 channels of one output pixel ----------
-template <bool MAX>
-__global__ void pool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, uint8_t* __restrict__ arg,
-                                int N, int H, int W, int C, int P, int Q, int R, int S, int st, int pad) {
+// Grid: blockIdx.y = one output row (n, p) [bwd: one input row (n, h)], threads over
+// (column, 8-channel group) of that row -- one division per element instead of
+// three.  KS > 0: a compile-time KS x KS window with stride ST (the ResNet stem's
+// 3x3/2 max-pool: every tap's load issued up front, predicated); KS = 0: runtime
+// window.  The 8 per-channel argmax bytes move as one 8-B load / store.
+template <bool MAX, int KS, int ST>
+__global__ __launch_bounds__(256) void pool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                                       uint8_t* __restrict__ arg, int N, int H, int W, int C, int P,
+                                                       int Q, int R_, int S_, int st_, int pad) {
+  const int R = KS ? KS : R_, S = KS ? KS : S_, st = KS ? ST : st_;
   const int cv = C / 8;
-  const int64_t total = (int64_t)N * P * Q * cv;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += stride) {
-    const int c8 = (int)(i % cv);
-    int64_t t = i / cv;
-    const int q = (int)(t % Q);
-    t /= Q;
-    const int p = (int)(t % P);
-    const int n = (int)(t / P);
-    float best[8];
-    int bidx[8];
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= Q * cv) return;
+  const int c8 = j % cv, q = j / cv;
+  for (int row = blockIdx.y; row < N * P; row += gridDim.y) {
+  const int n = row / P, p = row - n * P;
+  const size_t img = (size_t)n * H;
+  float best[8];
+  int bidx[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      best[j] = MAX ? -INFINITY : 0.f;
-      bidx[j] = 0;
-    }
-    int cnt = 0;
-    for (int r = 0; r < R; ++r) {
-      const int h = p * st - pad + r;
-      if (h < 0 || h >= H) continue;
-      for (int s = 0; s < S; ++s) {
-        const int w = q * st - pad + s;
-        if (w < 0 || w >= W) continue;
-        const u16x8 v = *reinterpret_cast<const u16x8*>(x + (((size_t)n * H + h) * W + w) * C + c8 * 8);
-        ++cnt;
+  for (int t = 0; t < 8; ++t) {
+    best[t] = MAX ? -INFINITY : 0.f;
+    bidx[t] = 0;
+  }
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float f = bf2f(v[j]);
-          if (MAX) {
-            if (f > best[j]) { best[j] = f; bidx[j] = r * S + s; }
-          } else {
-            best[j] += f;
+  for (int r = 0; r < (KS ? KS : 1); ++r) {
+    for (int rr = (KS ? r : 0); rr < (KS ? r + 1 : R); ++rr) {
+      const int h = p * st - pad + rr;
+      const bool hok = h >= 0 && h < H;
+#pragma unroll
+      for (int s0 = 0; s0 < (KS ? KS : 1); ++s0) {
+        for (int ss = (KS ? s0 : 0); ss < (KS ? s0 + 1 : S); ++ss) {
+          const int w = q * st - pad + ss;
+          if (!hok || w < 0 || w >= W) continue;
+          const u16x8 v = *reinterpret_cast<const u16x8*>(x + ((img + h) * W + w) * C + c8 * 8);
+#pragma unroll
+          for (int t = 0; t < 8; ++t) {
+            const float f = bf2f(v[t]);
+            if (MAX) {
+              if (f > best[t]) { best[t] = f; bidx[t] = rr * S + ss; }
+            } else {
+              best[t] += f;
+            }
           }
         }
       }
     }
-    u16x8 o;
-    const float inv = MAX ? 1.f : 1.f / (float)(R * S);  // count_include_pad=True (torch default)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = f2bf(best[j] * inv);
-    (void)cnt;
-    reinterpret_cast<u16x8*>(y)[i] = o;
-    if (MAX) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) arg[i * 8 + j] = (uint8_t)bidx[j];
-    }
   }
+  u16x8 o;
+  const float inv = MAX ? 1.f : 1.f / (float)(R * S);  // count_include_pad=True (torch default)
+#pragma unroll
+  for (int t = 0; t < 8; ++t) o[t] = f2bf(best[t] * inv);
+  const size_t oi = ((size_t)row * Q + q) * cv + c8;
+  reinterpret_cast<u16x8*>(y)[oi] = o;
+  if (MAX) {
+    uint2 a;
+    a.x = (uint32_t)bidx[0] | ((uint32_t)bidx[1] << 8) | ((uint32_t)bidx[2] << 16) | ((uint32_t)bidx[3] << 24);
+    a.y = (uint32_t)bidx[4] | ((uint32_t)bidx[5] << 8) | ((uint32_t)bidx[6] << 16) | ((uint32_t)bidx[7] << 24);
+    reinterpret_cast<uint2*>(arg)[oi] = a;
+  }
+  }  // rows
 }
 
 // gather form (no atomics): each input pixel sums the outputs whose window holds it
-template <bool MAX>
-__global__ void pool_bwd_kernel(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ arg,
-                                bf16_t* __restrict__ dx, int N, int H, int W, int C, int P, int Q, int R, int S,
-                                int st, int pad) {
+// (KS > 0: at most ceil(KS / ST)^2 candidate outputs, unrolled)
+template <bool MAX, int KS, int ST>
+__global__ __launch_bounds__(256) void pool_bwd_kernel(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ arg,
+                                                       bf16_t* __restrict__ dx, int N, int H, int W, int C, int P,
+                                                       int Q, int R_, int S_, int st_, int pad,
+                                                       const bf16_t* __restrict__ dy2) {
+  const int R = KS ? KS : R_, S = KS ? KS : S_, st = KS ? ST : st_;
+  constexpr int kSpan = KS ? (KS + ST - 1) / ST : 1;
   const int cv = C / 8;
-  const int64_t total = (int64_t)N * H * W * cv;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += stride) {
-    const int c8 = (int)(i % cv);
-    int64_t t = i / cv;
-    const int w = (int)(t % W);
-    t /= W;
-    const int h = (int)(t % H);
-    const int n = (int)(t / H);
-    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    // outputs p with p*st - pad <= h <= p*st - pad + R - 1
-    const int p_lo = max(0, (h + pad - R + st) / st), p_hi = min(P - 1, (h + pad) / st);
-    const int q_lo = max(0, (w + pad - S + st) / st), q_hi = min(Q - 1, (w + pad) / st);
-    for (int p = p_lo; p <= p_hi; ++p) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= W * cv) return;
+  const int c8 = j % cv, w = j / cv;
+  for (int row = blockIdx.y; row < N * H; row += gridDim.y) {
+  const int n = row / H, h = row - n * H;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  // outputs p with p*st - pad <= h <= p*st - pad + R - 1
+  const int p_lo = max(0, (h + pad - R + st) / st), p_hi = min(P - 1, (h + pad) / st);
+  const int q_lo = max(0, (w + pad - S + st) / st), q_hi = min(Q - 1, (w + pad) / st);
+#pragma unroll
+  for (int i = 0; i < kSpan; ++i) {
+    for (int p = (KS ? p_lo + i : p_lo); p <= (KS ? min(p_lo + i, p_hi) : p_hi); ++p) {
       const int r = h - (p * st - pad);
       if (r < 0 || r >= R) continue;
-      for (int q = q_lo; q <= q_hi; ++q) {
-        const int s = w - (q * st - pad);
-        if (s < 0 || s >= S) continue;
-        const size_t o = (((size_t)n * P + p) * Q + q) * cv + c8;
-        const u16x8 g = reinterpret_cast<const u16x8*>(dy)[o];
-        if (MAX) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j)
-            if (arg[o * 8 + j] == (uint8_t)(r * S + s)) acc[j] += bf2f(g[j]);
-        } else {
+      for (int k = 0; k < kSpan; ++k) {
+        for (int q = (KS ? q_lo + k : q_lo); q <= (KS ? min(q_lo + k, q_hi) : q_hi); ++q) {
+          const int s = w - (q * st - pad);
+          if (s < 0 || s >= S) continue;
+          const size_t o = (((size_t)n * P + p) * Q + q) * cv + c8;
+          const u16x8 g = reinterpret_cast<const u16x8*>(dy)[o];
+          u16x8 g2 = {0, 0, 0, 0, 0, 0, 0, 0};  // a second gradient of the same output (a residual
+          if (dy2) g2 = reinterpret_cast<const u16x8*>(dy2)[o];  // block's input), summed here
+          if (MAX) {
+            const uint2 a = reinterpret_cast<const uint2*>(arg)[o];
+            const uint32_t want = (uint32_t)(r * S + s);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) acc[j] += bf2f(g[j]);
+            for (int t = 0; t < 8; ++t)
+              if ((((t < 4 ? a.x : a.y) >> (8 * (t & 3))) & 0xffu) == want) acc[t] += bf2f(g[t]) + bf2f(g2[t]);
+          } else {
+#pragma unroll
+            for (int t = 0; t < 8; ++t) acc[t] += bf2f(g[t]) + bf2f(g2[t]);
+          }
         }
       }
     }
-    u16x8 out;
-    const float inv = MAX ? 1.f : 1.f / (float)(R * S);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) out[j] = f2bf(acc[j] * inv);
-    reinterpret_cast<u16x8*>(dx)[i] = out;
   }
+  u16x8 out;
+  const float inv = MAX ? 1.f : 1.f / (float)(R * S);
+#pragma unroll
+  for (int t = 0; t < 8; ++t) out[t] = f2bf(acc[t] * inv);
+  reinterpret_cast<u16x8*>(dx)[((size_t)row * W + w) * cv + c8] = out;
+  }  // rows
 }
 
 // global average pool [N][HW][C] -> [N][C] (fp32 accumulate), and its backward
@@ -500,38 +528,51 @@ hipError_t bn_backward(const BnArgs& a, const uint16_t* dy, uint16_t* dx, uint16
   f.grad_assign = grad_assign ? 1 : 0;
   if (a.relu && a.mask)
     bn_reduce_kernel<true, true, true><<<grid_r, 256, 0, s>>>(a.x, dy, nullptr, a.save_mean, a.save_invstd, f.acc, M,
-                                                            C, gr.rpb, gr.lanes, gr.rl, f, a.mask, bn_ncop(true, gr.gx * gr.gy));
+                                                            C, gr.rpb, gr.lanes, gr.rl, f, a.mask,
+                                                            bn_ncop(true, gr.gx * gr.gy), a.dy2);
   else if (a.relu)
     bn_reduce_kernel<true, true><<<grid_r, 256, 0, s>>>(a.x, dy, a.y, a.save_mean, a.save_invstd, f.acc, M, C, gr.rpb,
-                                                      gr.lanes, gr.rl, f, nullptr, bn_ncop(true, gr.gx * gr.gy));
+                                                      gr.lanes, gr.rl, f, nullptr, bn_ncop(true, gr.gx * gr.gy), a.dy2);
   else
     bn_reduce_kernel<true, false><<<grid_r, 256, 0, s>>>(a.x, dy, nullptr, a.save_mean, a.save_invstd, f.acc, M, C,
-                                                       gr.rpb, gr.lanes, gr.rl, f, nullptr, bn_ncop(true, gr.gx * gr.gy));
+                                                       gr.rpb, gr.lanes, gr.rl, f, nullptr, bn_ncop(true, gr.gx * gr.gy),
+                                                       a.dy2);
   if (a.relu && a.mask)
     bn_bwd_apply_kernel<true, true><<<grid, 256, 0, s>>>(a.x, dy, nullptr, f.coef, dx, dres, M, C, g.rpb, g.lanes,
-                                                         g.rl, a.mask);
+                                                         g.rl, a.mask, a.dy2);
   else if (a.relu)
-    bn_bwd_apply_kernel<true><<<grid, 256, 0, s>>>(a.x, dy, a.y, f.coef, dx, dres, M, C, g.rpb, g.lanes, g.rl);
+    bn_bwd_apply_kernel<true><<<grid, 256, 0, s>>>(a.x, dy, a.y, f.coef, dx, dres, M, C, g.rpb, g.lanes, g.rl, nullptr,
+                                                   a.dy2);
   else
-    bn_bwd_apply_kernel<false><<<grid, 256, 0, s>>>(a.x, dy, nullptr, f.coef, dx, dres, M, C, g.rpb, g.lanes, g.rl);
+    bn_bwd_apply_kernel<false><<<grid, 256, 0, s>>>(a.x, dy, nullptr, f.coef, dx, dres, M, C, g.rpb, g.lanes, g.rl,
+                                                    nullptr, a.dy2);
   return hipGetLastError();
 }
 
 hipError_t pool2d_fwd(const uint16_t* x, uint16_t* y, uint8_t* argmax, int N, int H, int W, int C, int P, int Q,
                       int R, int S, int stride, int pad, bool is_max, hipStream_t s) {
   if (C % 8) return hipErrorInvalidValue;
-  const int g = grid_for((int64_t)N * P * Q * C / 8);
-  if (is_max) pool_fwd_kernel<true><<<g, kBlock, 0, s>>>(x, y, argmax, N, H, W, C, P, Q, R, S, stride, pad);
-  else pool_fwd_kernel<false><<<g, kBlock, 0, s>>>(x, y, argmax, N, H, W, C, P, Q, R, S, stride, pad);
+  if ((int64_t)N * P >= (1ll << 31) || (int64_t)Q * (C / 8) > (1 << 30)) return hipErrorInvalidValue;
+  const dim3 g((Q * (C / 8) + kBlock - 1) / kBlock, std::min(N * P, 65535));
+  const bool k3 = R == 3 && S == 3 && stride == 2;
+  if (is_max && k3) pool_fwd_kernel<true, 3, 2><<<g, kBlock, 0, s>>>(x, y, argmax, N, H, W, C, P, Q, R, S, stride, pad);
+  else if (is_max) pool_fwd_kernel<true, 0, 1><<<g, kBlock, 0, s>>>(x, y, argmax, N, H, W, C, P, Q, R, S, stride, pad);
+  else pool_fwd_kernel<false, 0, 1><<<g, kBlock, 0, s>>>(x, y, argmax, N, H, W, C, P, Q, R, S, stride, pad);
   return hipGetLastError();
 }
 
 hipError_t pool2d_bwd(const uint16_t* dy, const uint8_t* argmax, uint16_t* dx, int N, int H, int W, int C, int P,
-                      int Q, int R, int S, int stride, int pad, bool is_max, hipStream_t s) {
+                      int Q, int R, int S, int stride, int pad, bool is_max, hipStream_t s, const uint16_t* dy2) {
   if (C % 8) return hipErrorInvalidValue;
-  const int g = grid_for((int64_t)N * H * W * C / 8);
-  if (is_max) pool_bwd_kernel<true><<<g, kBlock, 0, s>>>(dy, argmax, dx, N, H, W, C, P, Q, R, S, stride, pad);
-  else pool_bwd_kernel<false><<<g, kBlock, 0, s>>>(dy, argmax, dx, N, H, W, C, P, Q, R, S, stride, pad);
+  if ((int64_t)N * H >= (1ll << 31) || (int64_t)W * (C / 8) > (1 << 30)) return hipErrorInvalidValue;
+  const dim3 g((W * (C / 8) + kBlock - 1) / kBlock, std::min(N * H, 65535));
+  const bool k3 = R == 3 && S == 3 && stride == 2;
+  if (is_max && k3)
+    pool_bwd_kernel<true, 3, 2><<<g, kBlock, 0, s>>>(dy, argmax, dx, N, H, W, C, P, Q, R, S, stride, pad, dy2);
+  else if (is_max)
+    pool_bwd_kernel<true, 0, 1><<<g, kBlock, 0, s>>>(dy, argmax, dx, N, H, W, C, P, Q, R, S, stride, pad, dy2);
+  else
+    pool_bwd_kernel<false, 0, 1><<<g, kBlock, 0, s>>>(dy, argmax, dx, N, H, W, C, P, Q, R, S, stride, pad, dy2);
   return hipGetLastError();
 }
 

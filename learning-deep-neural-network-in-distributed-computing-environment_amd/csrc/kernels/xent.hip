@@ -8,6 +8,8 @@
 // One wave per row (lanes stride over classes), 4 waves per block, 16 rows per
 // block; per-block partials are combined in LDS and added with one atomic per
 // statistic / bias column.
+#include <algorithm>
+
 #include "ldnn_common.h"
 #include "ldnn_kernels.h"
 
@@ -18,11 +20,47 @@ namespace {
 constexpr int kRowsPerBlock = 16;  // 4 rows per wave: B = 4096 -> 256 blocks fill the chip
 constexpr int kMaxColsPerLane = 16;  // C <= 1024
 
+// Last-block finalize (fin.out set): every block's statistic atomics are made
+// device-visible before its arrival is counted; the last arrival swaps the sums
+// out of the accumulator (leaving it zero), writes [loss_sum * scale, #correct]
+// and adds both into the running stats.
+__device__ __forceinline__ void xent_finish(const XentFin& fin, float* stats) {
+  if (fin.out == nullptr) return;
+  __threadfence();
+  __syncthreads();
+  __shared__ int last;
+  if (threadIdx.x == 0) last = atomicAdd(fin.cnt, 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (!last || threadIdx.x != 0) return;
+  __threadfence();
+  const float l = atomicExch(fin.acc, 0.f), c = atomicExch(fin.acc + 1, 0.f);
+  fin.out[0] = l * fin.scale;
+  fin.out[1] = c;
+  if (stats) {
+    atomicAdd(stats, l);
+    atomicAdd(stats + 1, c);
+  }
+  atomicExch(fin.cnt, 0u);
+}
+
+__global__ __launch_bounds__(256) void scale_bf16_kernel(const bf16_t* __restrict__ src, const float* __restrict__ scale,
+                                                         bf16_t* __restrict__ out, int64_t n8) {
+  const float k = *scale;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8; i += stride) {
+    const u16x8 v = reinterpret_cast<const u16x8*>(src)[i];
+    u16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = f2bf(bf2f(v[j]) * k);
+    reinterpret_cast<u16x8*>(out)[i] = o;
+  }
+}
+
 __global__ __launch_bounds__(256) void xent_kernel(const bf16_t* __restrict__ logits,
                                                    const int64_t* __restrict__ labels,
                                                    bf16_t* __restrict__ dlogits, float* __restrict__ stats,
                                                    float* __restrict__ dbias, int B, int C, int ld,
-                                                   float grad_scale) {
+                                                   float grad_scale, int rows_per_block, XentFin fin) {
   __shared__ float sdb[4][kMaxColsPerLane * 64];
   __shared__ float sstat[4][2];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -32,8 +70,8 @@ __global__ __launch_bounds__(256) void xent_kernel(const bf16_t* __restrict__ lo
   for (int t = 0; t < kMaxColsPerLane; ++t) dacc[t] = 0.f;
   float loss_sum = 0.f, correct = 0.f;
 
-  const int r_end = min(B, (blockIdx.x + 1) * kRowsPerBlock);
-  for (int r = blockIdx.x * kRowsPerBlock + w; r < r_end; r += 4) {
+  const int r_end = min(B, (blockIdx.x + 1) * rows_per_block);
+  for (int r = blockIdx.x * rows_per_block + w; r < r_end; r += 4) {
     const bf16_t* row = logits + (size_t)r * ld;
     const int lab = (int)labels[r];
     float xv[kMaxColsPerLane];
@@ -94,13 +132,15 @@ __global__ __launch_bounds__(256) void xent_kernel(const bf16_t* __restrict__ lo
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    atomicAdd(stats + 0, sstat[0][0] + sstat[1][0] + sstat[2][0] + sstat[3][0]);
-    atomicAdd(stats + 1, sstat[0][1] + sstat[1][1] + sstat[2][1] + sstat[3][1]);
+    float* st = fin.out ? fin.acc : stats;
+    atomicAdd(st + 0, sstat[0][0] + sstat[1][0] + sstat[2][0] + sstat[3][0]);
+    atomicAdd(st + 1, sstat[0][1] + sstat[1][1] + sstat[2][1] + sstat[3][1]);
   }
   if (dbias) {
     for (int c = threadIdx.x; c < ld; c += blockDim.x)
       atomicAdd(dbias + c, sdb[0][c] + sdb[1][c] + sdb[2][c] + sdb[3][c]);
   }
+  xent_finish(fin, stats);
 }
 
 
@@ -114,7 +154,7 @@ __global__ __launch_bounds__(256) void xent_rows_kernel(const bf16_t* __restrict
                                                         const int64_t* __restrict__ labels,
                                                         bf16_t* __restrict__ dlogits, float* __restrict__ stats,
                                                         float* __restrict__ dbias, int B, int C, int ld,
-                                                        float grad_scale) {
+                                                        float grad_scale, XentFin fin) {
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
   const bool ok = r < B;
   float x[LD];
@@ -184,33 +224,46 @@ __global__ __launch_bounds__(256) void xent_rows_kernel(const bf16_t* __restrict
   const int t = threadIdx.x;
   if (t < LD + 2 && (dbias || t >= LD)) {
     const float v = part[0][t] + part[1][t] + part[2][t] + part[3][t];
-    atomicAdd(t < LD ? dbias + t : stats + (t - LD), v);
+    atomicAdd(t < LD ? dbias + t : (fin.out ? fin.acc : stats) + (t - LD), v);
   }
+  xent_finish(fin, stats);
 }
 
 }  // namespace
 
 hipError_t softmax_xent(const uint16_t* logits, const int64_t* labels, uint16_t* dlogits, float* stats,
-                        float* dbias, int B, int C, int ld, float grad_scale, hipStream_t s) {
+                        float* dbias, int B, int C, int ld, float grad_scale, hipStream_t s, const XentFin* finp) {
   if (ld > kMaxColsPerLane * 64 || C > ld) return hipErrorInvalidValue;
+  const XentFin fin = finp ? *finp : XentFin{};
+  if (fin.out && (fin.acc == nullptr || fin.cnt == nullptr)) return hipErrorInvalidValue;
+  if (!fin.out && stats == nullptr) return hipErrorInvalidValue;
   if (B <= 0) return hipSuccess;
   const bool vec_ok = (ld % 8 == 0) && ((reinterpret_cast<uintptr_t>(logits) | reinterpret_cast<uintptr_t>(dlogits)) & 15) == 0;
   if (vec_ok && ld <= 64) {
     const int g = (B + 255) / 256;
     switch (ld) {
-      case 8: xent_rows_kernel<8><<<g, 256, 0, s>>>(logits, labels, dlogits, stats, dbias, B, C, ld, grad_scale); break;
-      case 16: xent_rows_kernel<16><<<g, 256, 0, s>>>(logits, labels, dlogits, stats, dbias, B, C, ld, grad_scale); break;
-      case 24: xent_rows_kernel<24><<<g, 256, 0, s>>>(logits, labels, dlogits, stats, dbias, B, C, ld, grad_scale); break;
-      case 32: xent_rows_kernel<32><<<g, 256, 0, s>>>(logits, labels, dlogits, stats, dbias, B, C, ld, grad_scale); break;
-      case 40: xent_rows_kernel<40><<<g, 256, 0, s>>>(logits, labels, dlogits, stats, dbias, B, C, ld, grad_scale); break;
-      case 48: xent_rows_kernel<48><<<g, 256, 0, s>>>(logits, labels, dlogits, stats, dbias, B, C, ld, grad_scale); break;
-      case 56: xent_rows_kernel<56><<<g, 256, 0, s>>>(logits, labels, dlogits, stats, dbias, B, C, ld, grad_scale); break;
-      default: xent_rows_kernel<64><<<g, 256, 0, s>>>(logits, labels, dlogits, stats, dbias, B, C, ld, grad_scale); break;
+#define LDNN_XR(L) \
+      case L: xent_rows_kernel<L><<<g, 256, 0, s>>>(logits, labels, dlogits, stats, dbias, B, C, ld, grad_scale, fin); break;
+      LDNN_XR(8) LDNN_XR(16) LDNN_XR(24) LDNN_XR(32) LDNN_XR(40) LDNN_XR(48) LDNN_XR(56)
+#undef LDNN_XR
+      default: xent_rows_kernel<64><<<g, 256, 0, s>>>(logits, labels, dlogits, stats, dbias, B, C, ld, grad_scale, fin); break;
     }
     return hipGetLastError();
   }
-  const int g = (B + kRowsPerBlock - 1) / kRowsPerBlock;
-  xent_kernel<<<g, 256, 0, s>>>(logits, labels, dlogits, stats, dbias, B, C, ld, grad_scale);
+  // one row per wave while that still leaves < 256 blocks (a 64-row batch: 16 blocks
+  // instead of 4 waves walking 16 rows each), 16 rows per block beyond
+  const int rpb = B <= 4 * 256 ? 4 : kRowsPerBlock;
+  const int g = (B + rpb - 1) / rpb;
+  xent_kernel<<<g, 256, 0, s>>>(logits, labels, dlogits, stats, dbias, B, C, ld, grad_scale, rpb, fin);
+  return hipGetLastError();
+}
+
+hipError_t scale_bf16_dev(const uint16_t* src, const float* scale, uint16_t* out, int64_t n, hipStream_t s) {
+  if (n % 8 || ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(out)) & 15)) return hipErrorInvalidValue;
+  if (n == 0) return hipSuccess;
+  const int64_t n8 = n / 8;
+  const int g = (int)std::min<int64_t>((n8 + 255) / 256, 1024);
+  scale_bf16_kernel<<<g, 256, 0, s>>>(src, scale, out, n8);
   return hipGetLastError();
 }
 

@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import torch.nn as nn
 
+from ..ops import functional as LF
 from .layers import AdaptiveAvgPool2d, AvgPool2d, BatchNorm2d, Conv2d, Linear, MaxPool2d, ReLU, pair_conv_bn
 
 
@@ -51,9 +52,11 @@ class ResBlock(nn.Module):
             pair_conv_bn(self.shortcut[0], self.shortcut[1])
 
     def forward(self, x):
-        # BAR/model.py:67-72 with BN+ReLU and BN+residual-add+ReLU each fused into one pass
+        # BAR/model.py:67-72 with BN+ReLU and BN+residual-add+ReLU each fused into one pass;
+        # the shortcut reads x's twin (LF.shortcut_input), so the producer of x sums the two
+        # branch gradients in its own backward kernels instead of a separate add
         out = self.bn1.act(self.conv1(x), relu=True)
-        return self.bn2.act(self.conv2(out), residual=self.shortcut(x), relu=True)
+        return self.bn2.act(self.conv2(out), residual=self.shortcut(LF.shortcut_input(x)), relu=True)
 
 
 class EnhancedCNNModel(nn.Module):

@@ -6,6 +6,7 @@ from __future__ import annotations
 
 import torch.nn as nn
 
+from ..ops import functional as LF
 from .layers import AdaptiveAvgPool2d, BatchNorm2d, Conv2d, Linear, MaxPool2d, ReLU, pair_conv_bn
 
 
@@ -26,7 +27,8 @@ class BasicBlock(nn.Module):
             pair_conv_bn(downsample[0], downsample[1])
 
     def forward(self, x):
-        idt = x if self.downsample is None else self.downsample(x)
+        xs = LF.shortcut_input(x)   # (x's twin: see models/cnn.py ResBlock)
+        idt = xs if self.downsample is None else self.downsample(xs)
         out = self.bn1.act(self.conv1(x), relu=True)
         return self.bn2.act(self.conv2(out), residual=idt, relu=True)
 

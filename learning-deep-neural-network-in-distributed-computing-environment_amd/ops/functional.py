@@ -174,19 +174,23 @@ class _SoftmaxXentNative(torch.autograd.Function):
         lg = logits if (logits.dtype == torch.bfloat16 and logits.stride(1) == 1) else logits.to(torch.bfloat16).contiguous()
         ld = lg.stride(0)
         dfull = torch.empty(B * ld, dtype=torch.bfloat16, device=lg.device).view(B, ld)
-        local = torch.zeros(2, dtype=torch.float32, device=lg.device)
-        C.softmax_xent(lg, labels, dfull[:, :n], local, None, n, 1.0 / B)
-        if stats is not None:
-            stats[:2].add_(local)
+        # one launch: the kernel's last block writes [mean loss, #correct] into `out`
+        # and adds [loss sum, #correct] into `stats` (no fill / divide / add kernels)
+        out = torch.empty(2, dtype=torch.float32, device=lg.device)
+        C.softmax_xent(lg, labels, dfull[:, :n], stats, None, n, 1.0 / B, loss_out=out, loss_scale=1.0 / B)
         ctx.save_for_backward(dfull)
         ctx.n, ctx.in_dtype = n, logits.dtype
-        return local[0] / B
+        return out[0]
 
     @staticmethod
     def backward(ctx, go):
         (dfull,) = ctx.saved_tensors
+        if ctx.in_dtype == torch.bfloat16 and go.dtype == torch.float32 and go.is_cuda and dfull.numel() % 8 == 0:
+            # d = dlogits * grad_output in one pass over the padded rows (pad stays 0)
+            full = torch.empty_like(dfull)
+            _ext.C().scale_bf16(dfull, go.reshape(1), full)
+            return full[:, : ctx.n], None, None
         d = dfull[:, : ctx.n]
-        # grad_output is the scalar d(loss); keep the zero padding of the stored rows
         d = (d.float() * go).to(torch.bfloat16) if ctx.in_dtype == torch.bfloat16 else d.float() * go
         if ctx.in_dtype == torch.bfloat16 and dfull.stride(0) != ctx.n:
             full = torch.zeros_like(dfull)
@@ -363,6 +367,22 @@ def _bn_workspace(mod, C: int, dev, C_) -> torch.Tensor:
     return ws
 
 
+def _with_twin(y: torch.Tensor, twin: torch.Tensor) -> torch.Tensor:
+    """Native BN / pool outputs come with a twin: a second autograd output over the
+    same storage.  A residual block reads its shortcut through the twin
+    (``shortcut_input``), so the producer's backward receives the two branch
+    gradients separately and sums them inside its own kernels -- no separate
+    elementwise add of the gradients (autograd's accumulation of a tensor used twice)."""
+    y._ldnn_twin = twin
+    return y
+
+
+def shortcut_input(x: torch.Tensor) -> torch.Tensor:
+    """The tensor a residual block's shortcut branch should read (x's twin if it has one)."""
+    t = getattr(x, "_ldnn_twin", None)
+    return x if t is None else t
+
+
 class _BatchNormNative(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, residual, mod, flat, relu):
@@ -400,15 +420,24 @@ class _BatchNormNative(torch.autograd.Function):
         ctx.mask = mask
         ctx.save_for_backward(x2, y if mask is None else x2.new_empty(0), smean, sinv)
         ctx.meta = (flat, weight, bias, relu, residual is not None, ws, (N, C, H, W), x.dtype)
-        return nchw_view(y, C)
+        ctx.set_materialize_grads(False)
+        return nchw_view(y, C), nchw_view(y, C)
 
     @staticmethod
-    def backward(ctx, gy):
+    def backward(ctx, gy, gy_twin):
         C_ = _ext.C()
         x2, y, smean, sinv = ctx.saved_tensors
         flat, weight, bias, relu, has_res, ws, (N, C, H, W), in_dtype = ctx.meta
+        if gy is None:
+            gy, gy_twin = gy_twin, None
+        if gy is None:
+            return None, None, None, None, None, None, None
         g2 = as_nhwc(gy if gy.dtype == torch.bfloat16 else gy.to(torch.bfloat16), C, zero_pad=False)
         g2 = g2.contiguous().view(-1, C)
+        gt = None
+        if gy_twin is not None:   # the shortcut branch's gradient of the same output: summed in the kernels
+            gt = as_nhwc(gy_twin if gy_twin.dtype == torch.bfloat16 else gy_twin.to(torch.bfloat16), C,
+                         zero_pad=False).contiguous().view(-1, C)
         dx = torch.empty(N, H, W, C, dtype=torch.bfloat16, device=x2.device)
         dres = torch.empty_like(dx) if has_res and ctx.needs_input_grad[3] else None
         gamma = flat.master_storage(weight)[:C] if weight is not None else None
@@ -424,7 +453,7 @@ class _BatchNormNative(torch.autograd.Function):
         mask = ctx.mask
         yv = y.view(-1, C) if mask is None else x2   # (y is not read when the mask is given)
         C_.bn_bwd(x2, yv, g2, dx.view(-1, C), dres.view(-1, C) if dres is not None else None, gamma,
-                  smean, sinv, ws, dg, db, relu, mask=mask, grad_assign=assign)
+                  smean, sinv, ws, dg, db, relu, mask=mask, grad_assign=assign, dy2=gt)
         flat.notify(weight, bias)
         dxv = nchw_view(dx, C)
         dresv = nchw_view(dres, C) if dres is not None else None
@@ -443,7 +472,7 @@ def batch_norm_act(x, mod, residual=None, relu: bool = False):
     (fp32 statistics over NHWC bf16); the CPU path is the fp32 reference."""
     flat = getattr(mod, "_ldnn_flat", None)
     if _ext.use_native(x) and flat is not None and x.shape[1] % 8 == 0 and mod.affine:
-        return _BatchNormNative.apply(x, mod.weight, mod.bias, residual, mod, flat, relu)
+        return _with_twin(*_BatchNormNative.apply(x, mod.weight, mod.bias, residual, mod, flat, relu))
     y = batch_norm2d(x, mod)
     if residual is not None:
         y = y + residual
@@ -479,16 +508,24 @@ class _PoolNative(torch.autograd.Function):
         C_.pool_fwd(xb.contiguous(), y, am, k, k, stride, pad, is_max)
         ctx.save_for_backward(am) if is_max else None
         ctx.meta = (k, stride, pad, is_max, (N, C, H, W, cp), x.dtype)
-        return nchw_view(y, C)
+        ctx.set_materialize_grads(False)
+        return nchw_view(y, C), nchw_view(y, C)
 
     @staticmethod
-    def backward(ctx, gy):
+    def backward(ctx, gy, gy_twin):
         C_ = _ext.C()
         k, stride, pad, is_max, (N, C, H, W, cp), in_dtype = ctx.meta
+        if gy is None:
+            gy, gy_twin = gy_twin, None
+        if gy is None:
+            return None, None, None, None, None
         am = ctx.saved_tensors[0] if is_max else None
         g = as_nhwc(gy if gy.dtype == torch.bfloat16 else gy.to(torch.bfloat16), cp).contiguous()
+        gt = None
+        if gy_twin is not None:
+            gt = as_nhwc(gy_twin if gy_twin.dtype == torch.bfloat16 else gy_twin.to(torch.bfloat16), cp).contiguous()
         dx = torch.empty(N, H, W, cp, dtype=torch.bfloat16, device=gy.device)
-        C_.pool_bwd(g, am, dx, k, k, stride, pad, is_max)
+        C_.pool_bwd(g, am, dx, k, k, stride, pad, is_max, dy2=gt)
         out = nchw_view(dx, C)
         return (out if in_dtype == torch.bfloat16 else out.to(in_dtype)), None, None, None, None
 
@@ -503,7 +540,7 @@ def pool2d(x, mod, is_max: bool):
               and (not is_max or _sq(mod.dilation) == 1) and (is_max or getattr(mod, "count_include_pad", True))
               and k * k <= 255)
     if _ext.use_native(x) and simple and x.dim() == 4:
-        return _PoolNative.apply(x, k, st, pad, is_max)
+        return _with_twin(*_PoolNative.apply(x, k, st, pad, is_max))
     if is_max:
         return F.max_pool2d(x, mod.kernel_size, mod.stride, mod.padding, mod.dilation, mod.ceil_mode)
     return F.avg_pool2d(x, mod.kernel_size, mod.stride, mod.padding, mod.ceil_mode, mod.count_include_pad)
@@ -525,8 +562,12 @@ class _GapNative(torch.autograd.Function):
     def backward(ctx, gy):
         C_ = _ext.C()
         N, C, H, W, cp, in_dtype = ctx.meta
-        g = torch.zeros(N, cp, dtype=torch.bfloat16, device=gy.device)
-        g[:, :C] = gy.reshape(N, C)
+        g2 = gy.reshape(N, C)
+        if cp == C and g2.dtype == torch.bfloat16 and g2.is_contiguous():
+            g = g2   # (the Linear dgrad's dense output: no zero-pad copy)
+        else:
+            g = torch.zeros(N, cp, dtype=torch.bfloat16, device=gy.device)
+            g[:, :C] = g2
         dx = torch.empty(N, H, W, cp, dtype=torch.bfloat16, device=gy.device)
         C_.gap_bwd(g, dx.view(N, H * W, cp))
         out = nchw_view(dx, C)

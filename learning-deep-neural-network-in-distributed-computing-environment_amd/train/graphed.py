@@ -46,6 +46,8 @@ class GraphedStep:
         self.y = y_example.detach().clone()
         self.stats = stats if stats is not None else torch.zeros(2, dtype=torch.float32, device=self.x.device)
         self._lrs = None
+        # persistent d(loss)/d(loss) = 1: the captured backward needs no seed fill launch
+        self._one = torch.ones((), dtype=torch.float32, device=self.x.device)
         s = torch.cuda.Stream(device=self.x.device)
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
@@ -57,7 +59,9 @@ class GraphedStep:
         self.graph = torch.cuda.CUDAGraph()
         self._set_capture(True)
         try:
-            with no_gc(), torch.cuda.graph(self.graph):
+            # captured on the warmup stream: the per-stream native workspaces (conv
+            # split-K counters, xent accumulators) exist already, so no fill lands in the graph
+            with no_gc(), torch.cuda.graph(self.graph, stream=s):
                 self.loss = self._eager()
         finally:
             self._set_capture(False)
@@ -78,7 +82,7 @@ class GraphedStep:
             loss = self.criterion(out, self.y, self.stats)
         except TypeError:  # a stock criterion without the stats argument
             loss = self.criterion(out.float(), self.y)
-        loss.backward()
+        loss.backward(self._one if loss.dtype == torch.float32 and loss.dim() == 0 else None)
         self.optimizer.step()
         return loss
 

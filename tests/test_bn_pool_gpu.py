@@ -119,3 +119,40 @@ def test_bn_relu_mask_matches_reading_y(residual, monkeypatch):
     for a, b in zip(*outs):
         if a is not None:
             torch.testing.assert_close(a, b, rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("op", ["bn_relu", "bn_res_relu", "maxpool", "avgpool"])
+def test_twin_output_sums_branch_gradients(op):
+    """A native BN / pool output read by two branches through its twin
+    (LF.shortcut_input): the producer's backward sums both branch gradients in its
+    kernels == the fp32 reference with autograd's accumulation."""
+    torch.manual_seed(9)
+    N, C, H, W = 8, 64, 18, 18
+    x = torch.randn(N, C, H, W, device="cuda") * 1.5 + 0.3
+    r = torch.randn(N, C, H, W, device="cuda")
+    xb = _cl(x).requires_grad_(True)
+    # contiguous NCHW reference (torch-ROCm's channels_last avg_pool2d backward: see test_pools)
+    xf = xb.detach().float().contiguous().requires_grad_(True)
+    if op.startswith("bn"):
+        bn = BatchNorm2d(C)
+        with torch.no_grad():
+            bn.weight.uniform_(0.5, 1.5)
+            bn.bias.uniform_(-0.5, 0.5)
+        ref = torch.nn.BatchNorm2d(C).cuda()
+        ref.load_state_dict(bn.state_dict())
+        ldnn.prepare(bn, "cuda")
+        res = op == "bn_res_relu"
+        rb = _cl(r) if res else None
+        y = bn.act(xb, rb, True)
+        yr = (ref(xf) + (rb.float() if res else 0.0)).relu()
+    else:
+        mod = MaxPool2d(3, 2, 1) if op == "maxpool" else AvgPool2d(3, 2, 1)
+        y = mod(xb)
+        yr = F.max_pool2d(xf, 3, 2, 1) if op == "maxpool" else F.avg_pool2d(xf, 3, 2, 1)
+    twin = LF.shortcut_input(y)
+    assert twin is not y and twin.data_ptr() == y.data_ptr()
+    g1 = torch.randn_like(yr).bfloat16().float()
+    g2 = torch.randn_like(yr).bfloat16().float()
+    ((y.float() * g1).sum() + (twin.float() * g2).sum()).backward()
+    ((yr * g1).sum() + (yr * g2).sum()).backward()
+    torch.testing.assert_close(xb.grad.float(), xf.grad, rtol=3e-2, atol=3e-2 * xf.grad.abs().max().item())

@@ -146,6 +146,49 @@ def test_softmax_xent_matches_torch():
     torch.testing.assert_close(db[:Cc], dl[:, :Cc].float().sum(0), rtol=1e-3, atol=1e-5)
 
 
+@pytest.mark.parametrize("B,Cc,ld", [(64, 10, 16), (300, 10, 16), (64, 1000, 1000), (5000, 100, 104)])
+def test_softmax_xent_finalize(B, Cc, ld):
+    """loss_out: the last block writes [mean loss, #correct] and adds the sums into
+    stats; its accumulator workspace is left zero (second call sees only its own batch)."""
+    torch.manual_seed(7)
+    full = torch.randn(B, ld, device="cuda").bfloat16()
+    logits = full[:, :Cc]
+    labels = torch.randint(0, Cc, (B,), device="cuda")
+    dl = torch.empty(B, ld, device="cuda", dtype=torch.bfloat16)
+    stats = torch.tensor([1.0, 2.0], device="cuda")
+    ref = torch.nn.functional.cross_entropy(logits.float(), labels)
+    correct = (logits.float().argmax(1) == labels).sum().item()
+    for rep in range(2):
+        out = torch.full((2,), -5.0, device="cuda")
+        C().softmax_xent(logits, labels, dl[:, :Cc], stats if rep == 0 else None, None, Cc, 1.0 / B,
+                         loss_out=out, loss_scale=1.0 / B)
+        torch.testing.assert_close(out[0], ref, rtol=1e-4, atol=1e-4)
+        assert out[1].item() == correct
+    torch.testing.assert_close(stats, torch.tensor([1.0 + ref.item() * B, 2.0 + correct], device="cuda"),
+                               rtol=1e-4, atol=1e-3)
+    lf = logits.float().requires_grad_(True)
+    torch.nn.functional.cross_entropy(lf, labels).backward()
+    torch.testing.assert_close(dl[:, :Cc].float(), lf.grad, rtol=2e-2, atol=1e-4)
+
+
+def test_scale_bf16_and_loss_backward():
+    """The native loss backward (grad_output read on the device) == autograd of the fp32 loss."""
+    from ldnn.ops import functional as LF
+
+    torch.manual_seed(8)
+    x = torch.randn(96, 16, device="cuda").bfloat16()
+    src = torch.randn(96, 16, device="cuda").bfloat16()
+    out = torch.empty_like(src)
+    C().scale_bf16(src, torch.tensor([-2.5], device="cuda"), out)
+    torch.testing.assert_close(out.float(), (src.float() * -2.5).bfloat16().float(), rtol=0, atol=0)
+    logits = x[:, :10].clone().requires_grad_(True)
+    labels = torch.randint(0, 10, (96,), device="cuda")
+    (3.0 * LF.cross_entropy(logits, labels)).backward()
+    lf = x[:, :10].float().requires_grad_(True)
+    (3.0 * torch.nn.functional.cross_entropy(lf, labels)).backward()
+    torch.testing.assert_close(logits.grad.float(), lf.grad, rtol=2e-2, atol=2e-4)
+
+
 def test_sgd_momentum_matches_torch():
     torch.manual_seed(5)
     n = 10_003
