@@ -213,11 +213,13 @@ def test_train_global_with_graphs_matches_eager():
     assert abs(h0[4][-1] - h1[4][-1]) < 1e-2 and abs(h0[5][-1] - h1[5][-1]) < 0.5
 
 
-@pytest.mark.parametrize("name,shape", [("enhanced_cnn_small", (32, 3, 32, 32)), ("resnet18", (8, 3, 96, 96))])
+@pytest.mark.parametrize("name,shape", [("enhanced_cnn_small", (32, 3, 32, 32)), ("resnet18", (8, 3, 96, 96)),
+                                        ("enhanced_cnn", (64, 3, 32, 32))])
 def test_conv_epilogue_bn_statistics_match_separate_pass(name, shape, monkeypatch):
     """Training-mode BN whose statistics the producing conv's epilogue accumulated and
     finalized (conv_lds.hip bn_stats_epilogue) == the BN's own reduce pass: outputs,
-    running statistics, num_batches_tracked and gradients."""
+    running statistics, num_batches_tracked and gradients.  (Full EnhancedCNN at batch
+    64: its 4x4 / 2x2 slab split-K stages keep the separate statistics pass.)"""
     import ldnn.models.layers as layers_mod
     from ldnn.models.layers import Conv2d
 
