@@ -1274,6 +1274,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("eps"), py::arg("weight_decay"), py::arg("decoupled"),
         py::arg("zero_ranges") = std::vector<std::pair<int64_t, int64_t>>{});
   m.def("bump_step", &bump_step);
+  m.def("set_opt_max_blocks", &ldnn::set_opt_max_blocks, py::arg("n"),
+        "grid cap of optimizer launches from now on (0 = default)");
   m.def("head_fwd_xent", &head_fwd_xent, "fused narrow Linear + softmax-xent + argmax (per-16-row stats slots)",
         py::arg("h"), py::arg("W"), py::arg("bias"), py::arg("labels"), py::arg("logits"), py::arg("dlogits"),
         py::arg("stats"), py::arg("num_classes"), py::arg("grad_scale"), py::arg("dh") = py::none(), py::arg("dbias") = py::none(),

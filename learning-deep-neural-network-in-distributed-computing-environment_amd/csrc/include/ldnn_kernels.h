@@ -259,6 +259,8 @@ struct SgdParams {
   int first_step;  // momentum buffer initialised from g (torch semantics)
   GradZero zero;
 };
+// grid cap of the optimizer kernels launched from now on (0 = default 2048 blocks)
+void set_opt_max_blocks(int n);
 hipError_t sgd_step(float* param, float* grad, float* mom, uint16_t* shadow, const float* hp,
                     float grad_scale, SgdParams sp, int64_t n, hipStream_t s);
 struct AdamParams {

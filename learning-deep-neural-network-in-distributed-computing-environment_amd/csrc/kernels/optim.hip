@@ -125,12 +125,16 @@ __global__ void adam_kernel(float* __restrict__ param, float* __restrict__ grad,
 
 __global__ void bump_kernel(float* hp) { hp[1] += 1.f; }
 
+int g_opt_max_blocks = 2048;  // optimizer grid cap (set_opt_max_blocks: a narrow side-stream update)
+
 inline int grid_for(int64_t n4) {
   int64_t g = (n4 + kBlock - 1) / kBlock;
-  return (int)(g < 1 ? 1 : (g > 2048 ? 2048 : g));
+  return (int)(g < 1 ? 1 : (g > g_opt_max_blocks ? g_opt_max_blocks : g));
 }
 
 }  // namespace
+
+void set_opt_max_blocks(int n) { g_opt_max_blocks = n > 0 ? n : 2048; }
 
 hipError_t sgd_step(float* param, float* grad, float* mom, uint16_t* shadow, const float* hp,
                     float grad_scale, SgdParams sp, int64_t n, hipStream_t s) {

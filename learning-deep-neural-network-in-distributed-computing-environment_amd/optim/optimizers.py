@@ -88,6 +88,30 @@ class _FlatOptimizer(torch.optim.Optimizer):
             st[name] = b
         return b
 
+    # ---- range updates (optimizer overlapped with the backward, train/graphed.py) ----
+    def range_updater(self):
+        """A ``_RangeUpdate`` for ONE step of a single flat-buffer group on the GPU
+        (None when the optimizer cannot update by ranges: several groups, no
+        FlatParams, CPU).  ``update(lo, hi)`` runs the fused kernel on flat elements
+        [lo, hi) on the current stream; ``end()`` closes the step.  Every element must
+        be covered exactly once per step."""
+        if not self.supports_ranges():
+            return None
+        group = self.param_groups[0]
+        return _RangeUpdate(self, self._flat_for_group(group), group)
+
+    def supports_ranges(self) -> bool:
+        if len(self.param_groups) != 1 or type(self)._update_range is _FlatOptimizer._update_range:
+            return False
+        f = self._flat_for_group(self.param_groups[0])
+        return f is not None and _ext.use_native(f.master)
+
+    def _begin_ranges(self, f, group):  # per-step setup on the current stream (subclasses)
+        return {}
+
+    def _update_range(self, f, group, ctx, lo, hi):
+        raise NotImplementedError
+
     def zero_grad(self, set_to_none: bool = True):
         for group in self.param_groups:
             f = self._flat_for_group(group)
@@ -143,6 +167,17 @@ class SGD(_FlatOptimizer):
                         ps["momentum_buffer"] = torch.zeros_like(p)
                     self._sgd_torch(p.data, p.grad, ps.get("momentum_buffer"), lr, mu, damp, wd, nest, first)
         return loss
+
+    def _begin_ranges(self, f, group):
+        mu = group["momentum"]
+        return dict(hp=self._hp(f, group["lr"]), first=self._ls().get("step", 0) == 0,
+                    mom=self._buf("momentum", f.master) if mu != 0 else f.master)
+
+    def _update_range(self, f, group, ctx, lo, hi):
+        sh = f.shadow[lo:hi] if f.shadow is not None else None
+        _ext.C().sgd_step(f.master[lo:hi], f.grad[lo:hi], ctx["mom"][lo:hi], sh, ctx["hp"], f.grad_scale,
+                          group["momentum"], group["dampening"], group["weight_decay"], group["nesterov"],
+                          ctx["first"])
 
     @staticmethod
     def _sgd_torch(p, g, buf, lr, mu, damp, wd, nest, first):
@@ -201,6 +236,17 @@ class Adam(_FlatOptimizer):
                                      wd)
         return loss
 
+    def _begin_ranges(self, f, group):
+        hp = self._hp(f, group["lr"])
+        _ext.C().bump_step(hp)   # once per step, before any range reads the step count
+        return dict(hp=hp, m=self._buf("exp_avg", f.master), v=self._buf("exp_avg_sq", f.master))
+
+    def _update_range(self, f, group, ctx, lo, hi):
+        b1, b2 = group["betas"]
+        sh = f.shadow[lo:hi] if f.shadow is not None else None
+        _ext.C().adam_step(f.master[lo:hi], f.grad[lo:hi], ctx["m"][lo:hi], ctx["v"][lo:hi], sh, ctx["hp"],
+                           f.grad_scale, b1, b2, group["eps"], group["weight_decay"], self.decoupled)
+
     def _adam_torch(self, p, g, m, v, t, lr, b1, b2, eps, wd):
         if wd != 0:
             if self.decoupled:
@@ -231,3 +277,25 @@ def build_optimizer(name: str, params, lr: float, momentum: float = 0.9, weight_
     if name == "adamw":
         return AdamW(params, lr=lr, weight_decay=weight_decay)
     raise ValueError(f"unknown optimizer {name!r}")
+
+
+class _RangeUpdate:
+    """One optimizer step applied as several flat-range launches (see
+    ``_FlatOptimizer.range_updater``)."""
+
+    def __init__(self, opt, flat, group):
+        self.opt, self.flat, self.group = opt, flat, group
+        self.ctx = opt._begin_ranges(flat, group)
+        self.done = 0
+
+    @torch.no_grad()
+    def update(self, lo: int, hi: int):
+        if hi > lo:
+            self.opt._update_range(self.flat, self.group, self.ctx, lo, hi)
+            self.done += hi - lo
+
+    def end(self):
+        if self.done != self.flat.numel:
+            raise RuntimeError(f"range updates covered {self.done} of {self.flat.numel} flat elements")
+        st = self.opt._ls()
+        st["step"] = st.get("step", 0) + 1

@@ -36,12 +36,77 @@ from ..optim.optimizers import _FlatOptimizer
 from .static_mlp import no_gc
 
 
+# Optimizer overlapped with the backward (GraphedStep overlap_optimizer): the flat
+# buffer is laid out in gradient-ready order, so the parameters whose gradients are
+# final form a growing prefix of it.  When an op notifies new gradients, every
+# parameter that became ready BEFORE it is past its last backward read (its own dgrad
+# / BN backward ran earlier on the main stream), so that prefix is updated on a side
+# stream -- forked from the main stream at that point -- while the backward goes on;
+# the rest is updated on the main stream after the backward and the side stream joins.
+# OFF by default: measured on MI355X (profiles/overlap_optimizer_ab_r2.jsonl, same box,
+# alternated) EnhancedCNN b64 2.21-2.24 ms without it vs 2.32-2.44 ms with it, and
+# 3.27 ms with a 32-block side grid -- the side-stream branch of the replayed graph does
+# not run beside the backward kernels here, it adds to them (as in
+# profiles/graph_branch_concurrency_r2.jsonl).  LDNN_OVERLAP_OPT=1 turns it on,
+# LDNN_OVERLAP_OPT_ELEMS sets the launch granularity, LDNN_OVERLAP_OPT_BLOCKS the side grid.
+# (Assumes every parameter's gradient is written by one op per step -- true of the
+# models here; tied / shared weights need overlap_optimizer=False.)
+_OVERLAP_OPT = __import__("os").environ.get("LDNN_OVERLAP_OPT", "0") != "0"
+_OVERLAP_ELEMS = int(__import__("os").environ.get("LDNN_OVERLAP_OPT_ELEMS", str(4 << 20)))
+_OVERLAP_BLOCKS = int(__import__("os").environ.get("LDNN_OVERLAP_OPT_BLOCKS", "0"))  # side launches' grid cap
+
+
+class _OverlapUpdate:
+    def __init__(self, upd, flat, side: torch.cuda.Stream, min_elems: int):
+        self.upd, self.flat, self.side, self.min_elems = upd, flat, side, min_elems
+        self.segs = flat.segments          # buffer (gradient-ready) order
+        self.idx, self.lo = 0, 0           # [0, lo) updated / launched
+        self.ready: set = set()
+
+    def on_ready(self, params):
+        # (a native op notifies its parameters while its backward still runs; autograd's
+        # AccumulateGrad then re-notifies each one after the op returned -- a repeat is
+        # that echo.  Each parameter's gradient must come from ONE op per step: shared
+        # weights need overlap_optimizer=False.)
+        j = self.idx
+        while j < len(self.segs) and id(self.segs[j].param) in self.ready:
+            j += 1
+        self.ready.update(id(p) for p in params)
+        hi = self.segs[j].offset if j < len(self.segs) else self.flat.numel
+        if j > self.idx and hi - self.lo >= self.min_elems:
+            cur = torch.cuda.current_stream()
+            self.side.wait_stream(cur)     # everything issued so far (the readers of [lo, hi))
+            with torch.cuda.stream(self.side):
+                if _OVERLAP_BLOCKS:
+                    from ..ops import _ext
+                    _ext.C().set_opt_max_blocks(_OVERLAP_BLOCKS)
+                try:
+                    self.upd.update(self.lo, hi)
+                finally:
+                    if _OVERLAP_BLOCKS:
+                        _ext.C().set_opt_max_blocks(0)
+            self.lo, self.idx = hi, j
+
+    def finish(self):
+        self.flat.finalize_grads()         # gradients no op wrote this step (outside [0, lo))
+        self.upd.update(self.lo, self.flat.numel)
+        torch.cuda.current_stream().wait_stream(self.side)
+        self.upd.end()
+
+
 class GraphedStep:
     def __init__(self, model, criterion, optimizer, x_example: torch.Tensor, y_example: torch.Tensor,
-                 warmup: int = 3, stats: torch.Tensor | None = None):
+                 warmup: int = 3, stats: torch.Tensor | None = None, overlap_optimizer: bool | None = None):
         if not x_example.is_cuda:
             raise ValueError("GraphedStep needs GPU tensors")
         self.model, self.criterion, self.optimizer = model, criterion, optimizer
+        if overlap_optimizer is None:
+            overlap_optimizer = _OVERLAP_OPT
+        self._ov_side, self._ov = None, None
+        if overlap_optimizer and isinstance(optimizer, _FlatOptimizer) and optimizer.supports_ranges():
+            self._ov_flat = optimizer._flat_for_group(optimizer.param_groups[0])
+            self._ov_side = torch.cuda.Stream(device=x_example.device)
+            self._ov_flat.add_ready_group_hook(self._on_ready)
         self.x = x_example.detach().clone()
         self.y = y_example.detach().clone()
         self.stats = stats if stats is not None else torch.zeros(2, dtype=torch.float32, device=self.x.device)
@@ -82,9 +147,22 @@ class GraphedStep:
             loss = self.criterion(out, self.y, self.stats)
         except TypeError:  # a stock criterion without the stats argument
             loss = self.criterion(out.float(), self.y)
-        loss.backward(self._one if loss.dtype == torch.float32 and loss.dim() == 0 else None)
-        self.optimizer.step()
+        seed = self._one if loss.dtype == torch.float32 and loss.dim() == 0 else None
+        if self._ov_side is not None:
+            self._ov = _OverlapUpdate(self.optimizer.range_updater(), self._ov_flat, self._ov_side, _OVERLAP_ELEMS)
+            try:
+                loss.backward(seed)
+                self._ov.finish()
+            finally:
+                self._ov = None
+        else:
+            loss.backward(seed)
+            self.optimizer.step()
         return loss
+
+    def _on_ready(self, params):
+        if self._ov is not None:
+            self._ov.on_ready(params)
 
     def _sync_lr(self, force: bool = False):
         lrs = [g["lr"] for g in self.optimizer.param_groups]

@@ -123,6 +123,7 @@ class FlatParams:
         # gradient-readiness notification: native ops call notify() after writing a
         # weight gradient; params handled by stock torch ops signal through autograd.
         self._ready_hooks: list = []
+        self._ready_group_hooks: list = []
         # first-write gradients: native ops ask grad_beta() before writing a gradient;
         # after a lazy zero_grad the first writer overwrites (beta 0) instead of
         # accumulating onto a zero-filled buffer -- no fill pass, and the fp32 wgrad
@@ -142,12 +143,19 @@ class FlatParams:
     def add_ready_hook(self, fn):
         self._ready_hooks.append(fn)
 
+    def add_ready_group_hook(self, fn):
+        """fn(params): called once per notify() with every parameter it names (the
+        gradients one op wrote together; the op may still read those weights after)."""
+        self._ready_group_hooks.append(fn)
+
     def notify(self, *params):
-        for p in params:
-            if p is None:
-                continue
+        ps = [p for p in params if p is not None]
+        for p in ps:
             for fn in self._ready_hooks:
                 fn(p)
+        if ps:
+            for fn in self._ready_group_hooks:
+                fn(ps)
 
     # ---- views ---------------------------------------------------------------
     @staticmethod

@@ -131,15 +131,25 @@ def test_cnn_native_matches_cpu_fp32(name, shape):
         assert cos > 0.98, (n, cos)
 
 
-@pytest.mark.parametrize("name,shape,opt_name", [("lenet5", (256, 1, 28, 28), "sgd"),
-                                                 ("enhanced_cnn_small", (32, 3, 32, 32), "sgd"),
-                                                 ("lenet5", (256, 1, 28, 28), "adam")])
-def test_graphed_step_matches_eager(name, shape, opt_name):
+@pytest.mark.parametrize("name,shape,opt_name,ov_elems", [("lenet5", (256, 1, 28, 28), "sgd", None),
+                                                          ("enhanced_cnn_small", (32, 3, 32, 32), "sgd", None),
+                                                          ("lenet5", (256, 1, 28, 28), "adam", None),
+                                                          ("enhanced_cnn_small", (32, 3, 32, 32), "sgd", 4096),
+                                                          ("enhanced_cnn_small", (32, 3, 32, 32), "adam", 4096),
+                                                          ("lenet5", (256, 1, 28, 28), "sgd", 0)])
+def test_graphed_step_matches_eager(name, shape, opt_name, ov_elems, monkeypatch):
     """A training step replayed from one hipGraph (train.graphed.GraphedStep) gives the
     same parameters as the same steps run eagerly, including an lr change between
-    replays (the graph reads lr from the optimizer's device tensor)."""
+    replays (the graph reads lr from the optimizer's device tensor).  ov_elems: the
+    optimizer overlapped with the backward in ranges of >= ov_elems flat elements
+    (4096: many side-stream launches; 0: overlap off)."""
+    import ldnn.train.graphed as graphed_mod
     from ldnn.optim import SGD, Adam
     from ldnn.train.graphed import GraphedStep
+
+    if ov_elems is not None:
+        monkeypatch.setattr(graphed_mod, "_OVERLAP_ELEMS", max(ov_elems, 1))
+        monkeypatch.setattr(graphed_mod, "_OVERLAP_OPT", ov_elems > 0)
 
     torch.manual_seed(0)
     m1, m2, m3 = build_model(name), build_model(name), build_model(name)
@@ -180,7 +190,9 @@ def test_graphed_step_matches_eager(name, shape, opt_name):
         eg, ee = (d1 - d2).norm().item(), (d3 - d2).norm().item()
         assert eg <= 3.0 * ee + 2e-3 * d2.norm().item(), (n, eg, ee, d2.norm().item())
         cos = torch.nn.functional.cosine_similarity(d1, d2, dim=0).item()
-        assert cos > 0.9, (n, cos)
+        # (Adam normalises each element's update: on BN parameters at batch 32 the
+        # arrival-order noise alone turns the update direction by up to ~25 degrees)
+        assert cos > (0.8 if opt_name == "adam" and "bn" in n else 0.9), (n, cos)
     for (n, b), (_, c), (_, e) in zip(m1.named_buffers(), m2.named_buffers(), m3.named_buffers()):
         b, c, e = b.double(), c.double(), e.double()
         assert (b - c).norm().item() <= 3.0 * (e - c).norm().item() + 1e-3 * c.norm().item() + 1e-6, n
@@ -313,3 +325,42 @@ def test_lazy_zero_grad_first_write_matches_filled_buffer():
     crit(nets[0](x), y).backward()
     for p, a in zip(nets[0].parameters(), g[0]):
         torch.testing.assert_close(p.grad, 2 * a, rtol=1e-3, atol=1e-5)
+
+
+@pytest.mark.parametrize("opt_name", ["sgd", "adam"])
+def test_optimizer_range_updates_equal_full_step(opt_name):
+    """The flat optimizer applied as range launches (the overlapped-optimizer path)
+    == one full-buffer step, bit for bit, over two steps (momentum / moments / step count)."""
+    from ldnn.optim import SGD, Adam
+
+    torch.manual_seed(3)
+    m1, m2 = build_model("enhanced_cnn_small"), build_model("enhanced_cnn_small")
+    m2.load_state_dict(m1.state_dict())
+    ldnn.prepare(m1, "cuda")
+    ldnn.prepare(m2, "cuda")
+    mk = (lambda p: SGD(p, lr=0.05, momentum=0.9, weight_decay=1e-4)) if opt_name == "sgd" else (lambda p: Adam(p, lr=1e-3))
+    o1, o2 = mk(m1.parameters()), mk(m2.parameters())
+    f1, f2 = o1._flat_for_group(o1.param_groups[0]), o2._flat_for_group(o2.param_groups[0])
+    assert o2.supports_ranges()
+    n = f1.numel
+    for step in range(2):
+        g = torch.randn(n, device="cuda")
+        f1.grad.copy_(g)
+        f2.grad.copy_(g)
+        o1.step()
+        upd = o2.range_updater()
+        cuts = sorted(set(torch.randint(1, n, (7,)).tolist())) + [n]
+        lo = 0
+        for hi in cuts:
+            upd.update(lo, hi)
+            lo = hi
+        upd.end()
+    torch.cuda.synchronize()
+    assert torch.equal(f1.master, f2.master)
+    assert torch.equal(f1.shadow, f2.shadow)
+    for k in ("momentum", "exp_avg", "exp_avg_sq"):
+        a, b = o1._ls().get(k), o2._ls().get(k)
+        if a is not None:
+            assert torch.equal(a, b), k
+    assert o1._ls()["step"] == o2._ls()["step"] == 2
+
