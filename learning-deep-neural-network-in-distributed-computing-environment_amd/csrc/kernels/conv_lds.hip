@@ -71,6 +71,7 @@ struct LArgs {
   int bn_stats;      // fwd: accumulate + finalize the next BatchNorm's statistics (bn)
   BnFin bn;
   int tap_major;     // fwd / dgrad K-tile order: 0 = channel block fastest, 1 = filter tap fastest
+  int f32_rows;      // fp32 outputs (wgrad, split-K slabs) through the row-coalesced LDS epilogue
 };
 
 // Per-workgroup geometry: which rows its class covers and which taps it sums.
@@ -482,6 +483,38 @@ __device__ __forceinline__ void store_remapped(const LArgs& a, const Geo& g, flo
   }
 }
 
+// Row-coalesced fp32 store of a wave's 64 x 64 tile (wgrad outputs, split-K slabs):
+// the accumulators go to the wave's 16 KiB LDS slice ([64][64] fp32, 16-B chunks
+// XOR-swizzled by row), then 16 lanes write each 256-B row run -- 4 full rows per
+// instruction instead of 16 rows x 64 B straight from the MFMA layout.  The caller
+// has barriered the operand stages away.  out = acc (+ beta * out).
+__device__ __forceinline__ void store_f32_rows(const GemmParams& p, floatx4 (&acc)[4][4], char* wsm, int mbase,
+                                               int nbase, int lane) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int row = i * 16 + (lane & 15);
+      const int chunk = j * 4 + (lane >> 4);
+      *reinterpret_cast<floatx4*>(wsm + row * 256 + ((chunk ^ (row & 15)) << 4)) = acc[j][i];
+    }
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's staging writes landed (private slice)
+  __builtin_amdgcn_wave_barrier();
+  const int c = lane & 15;
+  const int n = nbase + c * 4;
+#pragma unroll 4
+  for (int it = 0; it < 16; ++it) {
+    const int row = it * 4 + (lane >> 4);
+    const int m = mbase + row;
+    floatx4 v = *reinterpret_cast<const floatx4*>(wsm + row * 256 + ((c ^ (row & 15)) << 4));
+    if (m < p.M && n < p.N) {
+      float* o = reinterpret_cast<float*>(p.C) + (size_t)m * p.ldc + n;
+      if (p.beta != 0.f) v = v + p.beta * *reinterpret_cast<const floatx4*>(o);
+      *reinterpret_cast<floatx4*>(o) = v;
+    }
+  }
+}
+
 template <int N>
 __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -512,6 +545,11 @@ __device__ __forceinline__ void conv_tail(const LArgs& a, const Geo& g, floatx4 
       p.M = g.M;
       p.N = a.N;
       p.ldc = a.N;
+      if (a.f32_rows && lds_floats >= NW * 4096) {
+        lds_barrier();  // every wave is done with the operand stages
+        store_f32_rows(p, acc, smem + (size_t)(wm * WN + wn) * 16384, mb, nbase, lane);
+        return;
+      }
       epilogue<EPI_NONE, true, 4, 4>(p, acc, mb, nbase, lane);
       return;
     } else {
@@ -546,6 +584,13 @@ __device__ __forceinline__ void conv_tail(const LArgs& a, const Geo& g, floatx4 
   p.ldc = a.N;
   p.bias = a.bias;
   p.beta = a.beta;
+  if constexpr (OUT_F32 && EPI == EPI_NONE) {
+    if (a.f32_rows && lds_floats >= NW * 4096 && !combine) {
+      lds_barrier();  // every wave is done with the operand stages
+      store_f32_rows(p, acc, smem + (size_t)(wm * WN + wn) * 16384, mb, nbase, lane);
+      return;
+    }
+  }
   epilogue<EPI, OUT_F32, 4, 4>(p, acc, mb, nbase, lane);
   if constexpr (!DGRAD && !OUT_F32 && EPI == EPI_NONE) {
     if (a.bn_stats) bn_stats_epilogue<WM, WN>(a, g, acc, mb, n0, wm, wn, lane, blockIdx.x, smem, lds_floats);
@@ -1218,9 +1263,16 @@ int tap_major_env() {
   return v;
 }
 
+// A/B knob: LDNN_CONV_F32_ROWS=0 stores fp32 conv outputs straight from the MFMA layout
+int f32_rows_env() {
+  static const int v = env_int("LDNN_CONV_F32_ROWS", 1);
+  return v;
+}
+
 LArgs base_args(const ConvShape& s) {
   LArgs a{};
   a.tap_major = tap_major_env();
+  a.f32_rows = f32_rows_env();
   a.s = s;
   a.rsc = s.R * s.S * s.C;
   a.pq = s.P * s.Q;
