@@ -72,6 +72,7 @@ struct LArgs {
   BnFin bn;
   int tap_major;     // fwd / dgrad K-tile order: 0 = channel block fastest, 1 = filter tap fastest
   int f32_rows;      // fp32 outputs (wgrad, split-K slabs) through the row-coalesced LDS epilogue
+  int bf16_rows;     // bf16 outputs (fwd y, stride-1 dgrad dx) through the row-coalesced LDS epilogue
 };
 
 // Per-workgroup geometry: which rows its class covers and which taps it sums.
@@ -515,6 +516,48 @@ __device__ __forceinline__ void store_f32_rows(const GemmParams& p, floatx4 (&ac
   }
 }
 
+// The same staging for bf16 outputs with the bias / ReLU epilogue: 8 lanes write each
+// 128-B row run (8 rows per instruction instead of 16 rows x 32 B).
+template <int EPI>
+__device__ __forceinline__ void store_bf16_rows(const GemmParams& p, floatx4 (&acc)[4][4], char* wsm, int mbase,
+                                                int nbase, int lane) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int row = i * 16 + (lane & 15);
+      const int chunk = j * 4 + (lane >> 4);
+      *reinterpret_cast<floatx4*>(wsm + row * 256 + ((chunk ^ (row & 15)) << 4)) = acc[j][i];
+    }
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's staging writes landed (private slice)
+  __builtin_amdgcn_wave_barrier();
+  const int c8 = lane & 7;
+  const int n = nbase + c8 * 8;
+  const bool nok = n < p.N;
+  float bias[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_RELU) {
+    if (nok) {
+      const floatx4 b0 = *reinterpret_cast<const floatx4*>(p.bias + n);
+      const floatx4 b1 = *reinterpret_cast<const floatx4*>(p.bias + n + 4);
+      bias[0] = b0[0]; bias[1] = b0[1]; bias[2] = b0[2]; bias[3] = b0[3];
+      bias[4] = b1[0]; bias[5] = b1[1]; bias[6] = b1[2]; bias[7] = b1[3];
+    }
+  }
+#pragma unroll 4
+  for (int it = 0; it < 8; ++it) {
+    const int row = it * 8 + (lane >> 3);
+    const int m = mbase + row;
+    const char* rb = wsm + row * 256;
+    const floatx4 v0 = *reinterpret_cast<const floatx4*>(rb + (((2 * c8) ^ (row & 15)) << 4));
+    const floatx4 v1 = *reinterpret_cast<const floatx4*>(rb + (((2 * c8 + 1) ^ (row & 15)) << 4));
+    if (!(nok && m < p.M)) continue;
+    u16x8 o;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) o[q] = f2bf(apply_epi<EPI>(q < 4 ? v0[q] : v1[q - 4], bias[q], 0.f));
+    *reinterpret_cast<u16x8*>(reinterpret_cast<bf16_t*>(p.C) + (size_t)m * p.ldc + n) = o;
+  }
+}
+
 template <int N>
 __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -588,6 +631,16 @@ __device__ __forceinline__ void conv_tail(const LArgs& a, const Geo& g, floatx4 
     if (a.f32_rows && lds_floats >= NW * 4096 && !combine) {
       lds_barrier();  // every wave is done with the operand stages
       store_f32_rows(p, acc, smem + (size_t)(wm * WN + wn) * 16384, mb, nbase, lane);
+      return;
+    }
+  }
+  if constexpr (!OUT_F32 && (EPI == EPI_NONE || EPI == EPI_BIAS || EPI == EPI_BIAS_RELU)) {
+    if (a.bf16_rows && lds_floats >= NW * 4096 && !combine) {
+      lds_barrier();  // every wave is done with the operand stages
+      store_bf16_rows<EPI>(p, acc, smem + (size_t)(wm * WN + wn) * 16384, mb, nbase, lane);
+      if constexpr (!DGRAD && EPI == EPI_NONE) {
+        if (a.bn_stats) bn_stats_epilogue<WM, WN>(a, g, acc, mb, n0, wm, wn, lane, blockIdx.x, smem, lds_floats);
+      }
       return;
     }
   }
@@ -1269,10 +1322,17 @@ int f32_rows_env() {
   return v;
 }
 
+// A/B knob: LDNN_CONV_BF16_ROWS=0 stores bf16 conv outputs straight from the MFMA layout
+int bf16_rows_env() {
+  static const int v = env_int("LDNN_CONV_BF16_ROWS", 1);
+  return v;
+}
+
 LArgs base_args(const ConvShape& s) {
   LArgs a{};
   a.tap_major = tap_major_env();
   a.f32_rows = f32_rows_env();
+  a.bf16_rows = bf16_rows_env();
   a.s = s;
   a.rsc = s.R * s.S * s.C;
   a.pq = s.P * s.Q;
