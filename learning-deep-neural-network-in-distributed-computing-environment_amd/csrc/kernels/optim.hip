@@ -10,6 +10,8 @@
 // Hyper-parameters that change between steps (lr, Adam step count) are read
 // from a device buffer `hp`, so a captured hipGraph replays with the current
 // schedule value and no host sync.
+#include <cstdlib>
+
 #include "ldnn_common.h"
 #include "ldnn_kernels.h"
 
@@ -18,6 +20,20 @@ namespace ldnn {
 namespace {
 
 constexpr int kBlock = 256;
+
+// NT: streaming (nontemporal) loads / stores -- every optimizer byte is touched once
+// per step, so it need not displace the L2 / Infinity Cache lines the next kernels
+// read (A/B knob LDNN_OPT_NT)
+template <bool NT>
+__device__ __forceinline__ floatx4 ld4(const float* p, int64_t i) {
+  if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(p) + i);
+  else return reinterpret_cast<const floatx4*>(p)[i];
+}
+template <bool NT>
+__device__ __forceinline__ void st4(float* p, int64_t i, floatx4 v) {
+  if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<floatx4*>(p) + i);
+  else reinterpret_cast<floatx4*>(p)[i] = v;
+}
 
 __device__ __forceinline__ bool in_zero(const GradZero& z, int64_t i) {
   return (i >= z.zb[0] && i < z.ze[0]) || (i >= z.zb[1] && i < z.ze[1]);
@@ -35,6 +51,7 @@ __device__ __forceinline__ void clear4(const GradZero& z, float* grad, int64_t i
   }
 }
 
+template <bool NT>
 __global__ void sgd_kernel(float* __restrict__ param, float* __restrict__ grad, float* __restrict__ mom,
                            bf16_t* __restrict__ shadow, const float* __restrict__ hp, float grad_scale,
                            SgdParams sp, int64_t n) {
@@ -42,19 +59,19 @@ __global__ void sgd_kernel(float* __restrict__ param, float* __restrict__ grad, 
   const int64_t nv = n / 4;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nv; i += stride) {
-    floatx4 p = reinterpret_cast<floatx4*>(param)[i];
-    floatx4 g = reinterpret_cast<const floatx4*>(grad)[i] * grad_scale;
+    floatx4 p = ld4<NT>(param, i);
+    floatx4 g = ld4<NT>(grad, i) * grad_scale;
     clear4(sp.zero, grad, i);
     if (sp.weight_decay != 0.f) g += sp.weight_decay * p;
     if (sp.momentum != 0.f) {
       floatx4 b;
       if (sp.first_step) b = g;
-      else b = sp.momentum * reinterpret_cast<floatx4*>(mom)[i] + (1.f - sp.dampening) * g;
-      reinterpret_cast<floatx4*>(mom)[i] = b;
+      else b = sp.momentum * ld4<NT>(mom, i) + (1.f - sp.dampening) * g;
+      st4<NT>(mom, i, b);
       g = sp.nesterov ? g + sp.momentum * b : b;
     }
     p -= lr * g;
-    reinterpret_cast<floatx4*>(param)[i] = p;
+    st4<NT>(param, i, p);
     if (shadow) reinterpret_cast<u16x4*>(shadow)[i] = u16x4{f2bf(p[0]), f2bf(p[1]), f2bf(p[2]), f2bf(p[3])};
   }
   for (int64_t i = nv * 4 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride) {
@@ -85,6 +102,7 @@ __device__ __forceinline__ float adam_elem(float p, float g, float& m, float& v,
   return p - (lr / bc1) * m / denom;
 }
 
+template <bool NT>
 __global__ void adam_kernel(float* __restrict__ param, float* __restrict__ grad, float* __restrict__ mm,
                             float* __restrict__ vv, bf16_t* __restrict__ shadow, const float* __restrict__ hp,
                             float grad_scale, AdamParams ap, int64_t n) {
@@ -95,11 +113,11 @@ __global__ void adam_kernel(float* __restrict__ param, float* __restrict__ grad,
   const int64_t nv = n / 4;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nv; i += stride) {
-    floatx4 p = reinterpret_cast<floatx4*>(param)[i];
-    const floatx4 g = reinterpret_cast<const floatx4*>(grad)[i] * grad_scale;
+    floatx4 p = ld4<NT>(param, i);
+    const floatx4 g = ld4<NT>(grad, i) * grad_scale;
     clear4(ap.zero, grad, i);
-    floatx4 m = reinterpret_cast<floatx4*>(mm)[i];
-    floatx4 v = reinterpret_cast<floatx4*>(vv)[i];
+    floatx4 m = ld4<NT>(mm, i);
+    floatx4 v = ld4<NT>(vv, i);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       float mj = m[j], vj = v[j];
@@ -107,9 +125,9 @@ __global__ void adam_kernel(float* __restrict__ param, float* __restrict__ grad,
       m[j] = mj;
       v[j] = vj;
     }
-    reinterpret_cast<floatx4*>(param)[i] = p;
-    reinterpret_cast<floatx4*>(mm)[i] = m;
-    reinterpret_cast<floatx4*>(vv)[i] = v;
+    st4<NT>(param, i, p);
+    st4<NT>(mm, i, m);
+    st4<NT>(vv, i, v);
     if (shadow) reinterpret_cast<u16x4*>(shadow)[i] = u16x4{f2bf(p[0]), f2bf(p[1]), f2bf(p[2]), f2bf(p[3])};
   }
   for (int64_t i = nv * 4 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride) {
@@ -134,19 +152,29 @@ inline int grid_for(int64_t n4) {
 
 }  // namespace
 
+int opt_nt_env() {
+  static const int v = [] {
+    const char* e = std::getenv("LDNN_OPT_NT");
+    return e ? std::atoi(e) : 1;
+  }();
+  return v;
+}
+
 void set_opt_max_blocks(int n) { g_opt_max_blocks = n > 0 ? n : 2048; }
 
 hipError_t sgd_step(float* param, float* grad, float* mom, uint16_t* shadow, const float* hp,
                     float grad_scale, SgdParams sp, int64_t n, hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  sgd_kernel<<<grid_for((n + 3) / 4), kBlock, 0, s>>>(param, grad, mom, shadow, hp, grad_scale, sp, n);
+  if (opt_nt_env()) sgd_kernel<true><<<grid_for((n + 3) / 4), kBlock, 0, s>>>(param, grad, mom, shadow, hp, grad_scale, sp, n);
+  else sgd_kernel<false><<<grid_for((n + 3) / 4), kBlock, 0, s>>>(param, grad, mom, shadow, hp, grad_scale, sp, n);
   return hipGetLastError();
 }
 
 hipError_t adam_step(float* param, float* grad, float* m, float* v, uint16_t* shadow, const float* hp,
                      float grad_scale, AdamParams ap, int64_t n, hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  adam_kernel<<<grid_for((n + 3) / 4), kBlock, 0, s>>>(param, grad, m, v, shadow, hp, grad_scale, ap, n);
+  if (opt_nt_env()) adam_kernel<true><<<grid_for((n + 3) / 4), kBlock, 0, s>>>(param, grad, m, v, shadow, hp, grad_scale, ap, n);
+  else adam_kernel<false><<<grid_for((n + 3) / 4), kBlock, 0, s>>>(param, grad, m, v, shadow, hp, grad_scale, ap, n);
   return hipGetLastError();
 }
 
