@@ -1204,10 +1204,25 @@ __global__ __launch_bounds__(256, 1) void conv_q_kernel(LArgs a, const bf16_t* p
   epilogue<EPI, false, MT, NT>(p, acc, mb, nbase, lane);
 }
 
+int slab_nt_env() {
+  static const int v = [] {
+    const char* e = std::getenv("LDNN_SLAB_NT");
+    return e ? std::atoi(e) : 1;
+  }();
+  return v;
+}
+
+// NT: the slabs are read for the last time -- streaming (nontemporal) loads (A/B knob LDNN_SLAB_NT)
+template <bool NT>
+__device__ __forceinline__ floatx4 slab_ld(const floatx4* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+
 // bf16 out[m][n] = epi(sum_s ws[s][m][n] (+ bias[n])): the split-K reduction of the
 // small-M fwd / dgrad slabs, 8 consecutive outputs per thread (two float4 per slab,
 // one 16-B store), all CUs.
-template <int EPI>
+template <int EPI, bool NT>
 __global__ __launch_bounds__(256) void conv_slab_epilogue_kernel(const float* __restrict__ ws, bf16_t* __restrict__ out,
                                                                  int64_t n8, int N, int splits,
                                                                  const float* __restrict__ bias) {
@@ -1215,10 +1230,10 @@ __global__ __launch_bounds__(256) void conv_slab_epilogue_kernel(const float* __
   if (i >= n8) return;
   const floatx4* w = reinterpret_cast<const floatx4*>(ws) + 2 * i;
   const int64_t stride4 = 2 * n8;
-  floatx4 v0 = w[0], v1 = w[1];
+  floatx4 v0 = slab_ld<NT>(w), v1 = slab_ld<NT>(w + 1);
   for (int sp = 1; sp < splits; ++sp) {
-    v0 += w[sp * stride4];
-    v1 += w[sp * stride4 + 1];
+    v0 += slab_ld<NT>(w + sp * stride4);
+    v1 += slab_ld<NT>(w + sp * stride4 + 1);
   }
   const int n = (int)((i * 8) % N);
   u16x8 o;
@@ -1235,12 +1250,17 @@ hipError_t conv_slab_epilogue(const float* ws, uint16_t* out, int M, int N, int 
   const int64_t n8 = (int64_t)M * N / 8;
   if (n8 <= 0) return hipSuccess;
   const unsigned g = (unsigned)((n8 + 255) / 256);
+  const bool nt = slab_nt_env();
   switch (epi) {
-    case EPI_NONE: conv_slab_epilogue_kernel<EPI_NONE><<<g, 256, 0, st>>>(ws, out, n8, N, splits, bias); break;
-    case EPI_BIAS: conv_slab_epilogue_kernel<EPI_BIAS><<<g, 256, 0, st>>>(ws, out, n8, N, splits, bias); break;
-    case EPI_BIAS_RELU:
-      conv_slab_epilogue_kernel<EPI_BIAS_RELU><<<g, 256, 0, st>>>(ws, out, n8, N, splits, bias);
-      break;
+#define LDNN_SLAB_EPI(E)                                                                                 \
+  case E:                                                                                                \
+    if (nt) conv_slab_epilogue_kernel<E, true><<<g, 256, 0, st>>>(ws, out, n8, N, splits, bias);       \
+    else conv_slab_epilogue_kernel<E, false><<<g, 256, 0, st>>>(ws, out, n8, N, splits, bias);         \
+    break;
+    LDNN_SLAB_EPI(EPI_NONE)
+    LDNN_SLAB_EPI(EPI_BIAS)
+    LDNN_SLAB_EPI(EPI_BIAS_RELU)
+#undef LDNN_SLAB_EPI
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -1250,6 +1270,7 @@ hipError_t conv_slab_epilogue(const float* ws, uint16_t* out, int M, int N, int 
 // A block is 32 float4 columns x 8 split lanes (each lane sums every 8th slab,
 // 4 loads in flight), reduced through LDS: enough blocks to cover the chip even
 // for a 64 x 576 weight, and a fixed summation order (deterministic).
+template <bool NT>
 __global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__ ws, float* __restrict__ out,
                                                        int64_t n4, int splits, float beta) {
   __shared__ floatx4 part[8][32];
@@ -1260,11 +1281,11 @@ __global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__
     const floatx4* w = reinterpret_cast<const floatx4*>(ws) + i;
     int sp = sl;
     for (; sp + 24 < splits; sp += 32) {
-      const floatx4 a = w[(int64_t)sp * n4], b = w[(int64_t)(sp + 8) * n4];
-      const floatx4 c = w[(int64_t)(sp + 16) * n4], d = w[(int64_t)(sp + 24) * n4];
+      const floatx4 a = slab_ld<NT>(w + (int64_t)sp * n4), b = slab_ld<NT>(w + (int64_t)(sp + 8) * n4);
+      const floatx4 c = slab_ld<NT>(w + (int64_t)(sp + 16) * n4), d = slab_ld<NT>(w + (int64_t)(sp + 24) * n4);
       v += (a + b) + (c + d);
     }
-    for (; sp < splits; sp += 8) v += w[(int64_t)sp * n4];
+    for (; sp < splits; sp += 8) v += slab_ld<NT>(w + (int64_t)sp * n4);
   }
   part[sl][col] = v;
   __syncthreads();
@@ -1692,7 +1713,8 @@ ConvWorkspace conv2d_lds_workspace(const ConvShape& s, int op) {
 
 hipError_t slab_sum(const float* ws, float* out, int64_t n4, int splits, float beta, hipStream_t st) {
   if (n4 <= 0) return hipSuccess;
-  slab_sum_kernel<<<(unsigned)((n4 + 31) / 32), 256, 0, st>>>(ws, out, n4, splits, beta);
+  if (slab_nt_env()) slab_sum_kernel<true><<<(unsigned)((n4 + 31) / 32), 256, 0, st>>>(ws, out, n4, splits, beta);
+  else slab_sum_kernel<false><<<(unsigned)((n4 + 31) / 32), 256, 0, st>>>(ws, out, n4, splits, beta);
   return hipGetLastError();
 }
 
@@ -1912,7 +1934,8 @@ hipError_t conv2d_wgrad_lds(const ConvShape& s, const uint16_t* dy, const uint16
     e = launch<2, 2, WgradA<128, 4, 4>, WgradB<128, 4, 4>, true, false>(a, EPI_NONE, splits, dy, bdy, x, bx, st);
   if (e != hipSuccess || splits == 1 || ws == nullptr) return e;
   const int64_t n4 = (int64_t)a.M * a.N / 4;
-  slab_sum_kernel<<<(unsigned)((n4 + 31) / 32), 256, 0, st>>>(ws, dw, n4, splits, beta);
+  if (slab_nt_env()) slab_sum_kernel<true><<<(unsigned)((n4 + 31) / 32), 256, 0, st>>>(ws, dw, n4, splits, beta);
+  else slab_sum_kernel<false><<<(unsigned)((n4 + 31) / 32), 256, 0, st>>>(ws, dw, n4, splits, beta);
   return hipGetLastError();
 }
 
