@@ -190,9 +190,9 @@ def test_graphed_step_matches_eager(name, shape, opt_name, ov_elems, monkeypatch
         eg, ee = (d1 - d2).norm().item(), (d3 - d2).norm().item()
         assert eg <= 3.0 * ee + 2e-3 * d2.norm().item(), (n, eg, ee, d2.norm().item())
         cos = torch.nn.functional.cosine_similarity(d1, d2, dim=0).item()
-        # (Adam normalises each element's update: on BN parameters at batch 32 the
-        # arrival-order noise alone turns the update direction by up to ~25 degrees)
-        assert cos > (0.8 if opt_name == "adam" and "bn" in n else 0.9), (n, cos)
+        # (Adam normalises each element's update: on the 1-D BatchNorm / bias parameters at
+        # batch 32 the arrival-order noise alone turns the update direction by up to ~25 degrees)
+        assert cos > (0.8 if opt_name == "adam" and p.dim() == 1 else 0.9), (n, cos)
     for (n, b), (_, c), (_, e) in zip(m1.named_buffers(), m2.named_buffers(), m3.named_buffers()):
         b, c, e = b.double(), c.double(), e.double()
         assert (b - c).norm().item() <= 3.0 * (e - c).norm().item() + 1e-3 * c.norm().item() + 1e-6, n
