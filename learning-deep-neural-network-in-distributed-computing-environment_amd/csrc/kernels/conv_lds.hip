@@ -73,6 +73,7 @@ struct LArgs {
   int tap_major;     // fwd / dgrad K-tile order: 0 = channel block fastest, 1 = filter tap fastest
   int f32_rows;      // fp32 outputs (wgrad, split-K slabs) through the row-coalesced LDS epilogue
   int bf16_rows;     // bf16 outputs (fwd y, stride-1 dgrad dx) through the row-coalesced LDS epilogue
+  int remap_rows;    // stride-2 dgrad dx (class row remap) through the row-coalesced LDS epilogue
 };
 
 // Per-workgroup geometry: which rows its class covers and which taps it sums.
@@ -558,6 +559,41 @@ __device__ __forceinline__ void store_bf16_rows(const GemmParams& p, floatx4 (&a
   }
 }
 
+// store_remapped through the wave's LDS slice: each GEMM row (one dx pixel's
+// channels) leaves as 128-B runs, 8 lanes a row, instead of 16 rows x 32 B.
+__device__ __forceinline__ void store_remapped_rows(const LArgs& a, const Geo& g, floatx4 (&acc)[4][4], char* wsm,
+                                                    int mbase, int nbase, int lane) {
+  const ConvShape& s = a.s;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int row = i * 16 + (lane & 15);
+      const int chunk = j * 4 + (lane >> 4);
+      *reinterpret_cast<floatx4*>(wsm + row * 256 + ((chunk ^ (row & 15)) << 4)) = acc[j][i];
+    }
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's staging writes landed (private slice)
+  __builtin_amdgcn_wave_barrier();
+  const int c8 = lane & 7;
+  const int c = nbase + c8 * 8;
+  const bool cok = c < a.N;
+#pragma unroll 4
+  for (int it = 0; it < 8; ++it) {
+    const int row = it * 8 + (lane >> 3);
+    const int m = mbase + row;
+    const char* rb = wsm + row * 256;
+    const floatx4 v0 = *reinterpret_cast<const floatx4*>(rb + (((2 * c8) ^ (row & 15)) << 4));
+    const floatx4 v1 = *reinterpret_cast<const floatx4*>(rb + (((2 * c8 + 1) ^ (row & 15)) << 4));
+    if (!(cok && m < g.M)) continue;
+    const int t = fdiv(m, g.f_rw), w2 = m - t * g.rows_w, n = fdiv(t, g.f_rh), h2 = t - n * g.rows_h;
+    const size_t px = ((size_t)n * s.H + g.hmul * h2 + g.hoff) * s.W + g.hmul * w2 + g.woff;
+    u16x8 o;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) o[q] = f2bf(q < 4 ? v0[q] : v1[q - 4]);
+    *reinterpret_cast<u16x8*>(reinterpret_cast<bf16_t*>(a.out) + px * a.N + c) = o;
+  }
+}
+
 template <int N>
 __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -616,6 +652,11 @@ __device__ __forceinline__ void conv_tail(const LArgs& a, const Geo& g, floatx4 
   }
   if constexpr (DGRAD && !OUT_F32) {
     if (g.hmul == 2) {
+      if (a.remap_rows && lds_floats >= NW * 4096 && !combine) {
+        lds_barrier();  // every wave is done with the operand stages
+        store_remapped_rows(a, g, acc, smem + (size_t)(wm * WN + wn) * 16384, mb, nbase, lane);
+        return;
+      }
       store_remapped(a, g, acc, mb, nbase, lane);
       return;
     }
@@ -1349,11 +1390,18 @@ int bf16_rows_env() {
   return v;
 }
 
+// A/B knob: LDNN_CONV_REMAP_ROWS=0 keeps the direct remapped store of stride-2 dgrads
+int remap_rows_env() {
+  static const int v = env_int("LDNN_CONV_REMAP_ROWS", 0);
+  return v;
+}
+
 LArgs base_args(const ConvShape& s) {
   LArgs a{};
   a.tap_major = tap_major_env();
   a.f32_rows = f32_rows_env();
   a.bf16_rows = bf16_rows_env();
+  a.remap_rows = remap_rows_env();
   a.s = s;
   a.rsc = s.R * s.S * s.C;
   a.pq = s.P * s.Q;
