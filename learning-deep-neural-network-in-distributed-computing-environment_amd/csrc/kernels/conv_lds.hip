@@ -1392,7 +1392,7 @@ int bf16_rows_env() {
 
 // A/B knob: LDNN_CONV_REMAP_ROWS=0 keeps the direct remapped store of stride-2 dgrads
 int remap_rows_env() {
-  static const int v = env_int("LDNN_CONV_REMAP_ROWS", 0);
+  static const int v = env_int("LDNN_CONV_REMAP_ROWS", 1);
   return v;
 }
 
