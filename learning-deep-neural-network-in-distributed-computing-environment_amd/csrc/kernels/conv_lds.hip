@@ -518,20 +518,13 @@ __device__ __forceinline__ void store_f32_rows(const GemmParams& p, floatx4 (&ac
 }
 
 // The same staging for bf16 outputs with the bias / ReLU epilogue: 8 lanes write each
-// 128-B row run (8 rows per instruction instead of 16 rows x 32 B).
-template <int EPI>
+// 128-B row run (8 rows per instruction instead of 16 rows x 32 B).  HALVES = 2 stages
+// the 64 rows as two 32-row halves (8 KiB per wave) for kernels with less LDS (the
+// C = 8 stem's patch kernel).
+template <int EPI, int HALVES = 1>
 __device__ __forceinline__ void store_bf16_rows(const GemmParams& p, floatx4 (&acc)[4][4], char* wsm, int mbase,
                                                 int nbase, int lane) {
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int row = i * 16 + (lane & 15);
-      const int chunk = j * 4 + (lane >> 4);
-      *reinterpret_cast<floatx4*>(wsm + row * 256 + ((chunk ^ (row & 15)) << 4)) = acc[j][i];
-    }
-  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's staging writes landed (private slice)
-  __builtin_amdgcn_wave_barrier();
+  constexpr int RH = 64 / HALVES;  // rows staged per pass
   const int c8 = lane & 7;
   const int n = nbase + c8 * 8;
   const bool nok = n < p.N;
@@ -544,18 +537,32 @@ __device__ __forceinline__ void store_bf16_rows(const GemmParams& p, floatx4 (&a
       bias[4] = b1[0]; bias[5] = b1[1]; bias[6] = b1[2]; bias[7] = b1[3];
     }
   }
-#pragma unroll 4
-  for (int it = 0; it < 8; ++it) {
-    const int row = it * 8 + (lane >> 3);
-    const int m = mbase + row;
-    const char* rb = wsm + row * 256;
-    const floatx4 v0 = *reinterpret_cast<const floatx4*>(rb + (((2 * c8) ^ (row & 15)) << 4));
-    const floatx4 v1 = *reinterpret_cast<const floatx4*>(rb + (((2 * c8 + 1) ^ (row & 15)) << 4));
-    if (!(nok && m < p.M)) continue;
-    u16x8 o;
 #pragma unroll
-    for (int q = 0; q < 8; ++q) o[q] = f2bf(apply_epi<EPI>(q < 4 ? v0[q] : v1[q - 4], bias[q], 0.f));
-    *reinterpret_cast<u16x8*>(reinterpret_cast<bf16_t*>(p.C) + (size_t)m * p.ldc + n) = o;
+  for (int h = 0; h < HALVES; ++h) {
+#pragma unroll
+    for (int i = 0; i < 4 / HALVES; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = i * 16 + (lane & 15);
+        const int chunk = j * 4 + (lane >> 4);
+        *reinterpret_cast<floatx4*>(wsm + row * 256 + ((chunk ^ (row & 15)) << 4)) = acc[j][h * (4 / HALVES) + i];
+      }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's staging writes landed (private slice)
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll 4
+    for (int it = 0; it < RH / 8; ++it) {
+      const int row = it * 8 + (lane >> 3);
+      const int m = mbase + h * RH + row;
+      const char* rb = wsm + row * 256;
+      const floatx4 v0 = *reinterpret_cast<const floatx4*>(rb + (((2 * c8) ^ (row & 15)) << 4));
+      const floatx4 v1 = *reinterpret_cast<const floatx4*>(rb + (((2 * c8 + 1) ^ (row & 15)) << 4));
+      if (!(nok && m < p.M)) continue;
+      u16x8 o;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) o[q] = f2bf(apply_epi<EPI>(q < 4 ? v0[q] : v1[q - 4], bias[q], 0.f));
+      *reinterpret_cast<u16x8*>(reinterpret_cast<bf16_t*>(p.C) + (size_t)m * p.ldc + n) = o;
+    }
+    __builtin_amdgcn_wave_barrier();  // the slice is re-staged by the next half
   }
 }
 
@@ -676,9 +683,12 @@ __device__ __forceinline__ void conv_tail(const LArgs& a, const Geo& g, floatx4 
     }
   }
   if constexpr (!OUT_F32 && (EPI == EPI_NONE || EPI == EPI_BIAS || EPI == EPI_BIAS_RELU)) {
-    if (a.bf16_rows && lds_floats >= NW * 4096 && !combine) {
+    if (a.bf16_rows && lds_floats >= NW * (a.bf16_rows >= 2 ? 2048 : 4096) && !combine) {
       lds_barrier();  // every wave is done with the operand stages
-      store_bf16_rows<EPI>(p, acc, smem + (size_t)(wm * WN + wn) * 16384, mb, nbase, lane);
+      if (lds_floats >= NW * 4096)
+        store_bf16_rows<EPI>(p, acc, smem + (size_t)(wm * WN + wn) * 16384, mb, nbase, lane);
+      else
+        store_bf16_rows<EPI, 2>(p, acc, smem + (size_t)(wm * WN + wn) * 8192, mb, nbase, lane);
       if constexpr (!DGRAD && EPI == EPI_NONE) {
         if (a.bn_stats) bn_stats_epilogue<WM, WN>(a, g, acc, mb, n0, wm, wn, lane, blockIdx.x, smem, lds_floats);
       }
@@ -1384,7 +1394,8 @@ int f32_rows_env() {
   return v;
 }
 
-// A/B knob: LDNN_CONV_BF16_ROWS=0 stores bf16 conv outputs straight from the MFMA layout
+// A/B knob: LDNN_CONV_BF16_ROWS=0 stores bf16 conv outputs straight from the MFMA layout,
+// 1 (default) stages only in kernels with a 16 KiB LDS slice per wave, 2 also in halves
 int bf16_rows_env() {
   static const int v = env_int("LDNN_CONV_BF16_ROWS", 1);
   return v;
