@@ -1395,9 +1395,9 @@ int f32_rows_env() {
 }
 
 // A/B knob: LDNN_CONV_BF16_ROWS=0 stores bf16 conv outputs straight from the MFMA layout,
-// 1 (default) stages only in kernels with a 16 KiB LDS slice per wave, 2 also in halves
+// 1 stages only in kernels with a 16 KiB LDS slice per wave, 2 (default) also in halves
 int bf16_rows_env() {
-  static const int v = env_int("LDNN_CONV_BF16_ROWS", 1);
+  static const int v = env_int("LDNN_CONV_BF16_ROWS", 2);
   return v;
 }
 
