@@ -18,17 +18,33 @@ at 1/2/4/8 MI355X".  Config (weak scaling, fixed per-GPU work):
              random-init (Xavier) weights; no dataset download exists here
 
 Single GPU:  python bench.py [--steps K --warmup W]
-N GPUs:      python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
+N GPUs:      python bench.py --gpus N            (spawns `torch.distributed.run` itself, as a
+                                                  child process, before any GPU call)
+         or  python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
                  --master-port P bench.py --gpus N
+Under a launcher the world size must equal --gpus (checked); with RCCL every rank
+must own a distinct GPU (checked: RCCL refuses two ranks on one device).
+
 Rank 0 prints ONE JSON line; `value` is the whole-job samples/sec (max step time
-over ranks).  `--compare-stock` also times a stock PyTorch-ROCm eager
-implementation (nn.Linear + DDP + torch.optim.SGD) of the same config.
+over ranks).  Besides the headline it reports, per rank and maxed over ranks:
+  per_gpu_local_ms     the same engine's comm-free step (world 1, no collectives)
+  scaling_efficiency   per_gpu_local_ms / ms_per_step  (1.0 at N = 1)
+  comm_us              standalone per-bucket reduce-scatter / all-gather times (N > 1)
+  configs              BASELINE configs #4/#5 through the same DP path at this N:
+                       LeNet-5 28x28 b256 and ResNet-18 224x224 b64 / b256 per GPU, each
+                       a graph-replayed step (GraphedDPStep: bucket all-reduces issued
+                       between the links of the backward graph chain) with its own
+                       comm-free local time and scaling efficiency (--no-configs skips)
+`--compare-stock` also times a stock PyTorch-ROCm eager implementation
+(nn.Linear + DDP + torch.optim.SGD) of the headline config.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -95,10 +111,8 @@ def run_ldnn(ctx, args):
                           device=ctx.device, world_size=ctx.world_size, use_graphs=not args.no_graphs,
                           bucket_cap_elems=args.bucket_elems, shard_optimizer=False if args.no_shard else None,
                           library_gemms=args.gemms == "library",
-                          early_optimizer={"on": True, "off": False, "auto": None}[args.early_opt],
                           fuse_head_dgrad=False if args.no_fuse_head_dgrad else None,
-                          concurrent_wgrad=args.concurrent_wgrad, overlap_optimizer=args.overlap_opt,
-                          pad_input=args.pad_input, head_dgrad_mode=args.head_dgrad_mode)
+                          head_dgrad_mode=args.head_dgrad_mode)
     if ctx.distributed:
         dist.broadcast(eng.flat.master, src=0)
         eng.flat.refresh_shadow()
@@ -111,8 +125,117 @@ def run_ldnn(ctx, args):
 
     el = timed(ctx, step, args.steps, args.warmup)
     loss, acc = eng.read_stats(args.batch * (args.steps + args.warmup))
-    return el, dict(train_loss=round(loss, 4), n_params=sum(p.numel() for p in model.parameters()),
-                    in_pad=eng.in_pad, gemm_kernels=eng.describe())
+    extra = dict(train_loss=round(loss, 4), n_params=sum(p.numel() for p in model.parameters()),
+                 buckets=len(eng.buckets), gemm_kernels=eng.describe())
+    if ctx.world_size > 1:
+        extra["comm_us"] = comm_micro(ctx, eng)
+        # the same engine without any collective: this rank's comm-free step time
+        torch.manual_seed(1234)
+        m1 = mlp3(args.in_features, args.hidden, args.classes)
+        xavier_init(m1)
+        loc = StaticMLPEngine(m1, args.batch, OptimConfig("sgd", lr=args.lr, momentum=0.9), device=ctx.device,
+                              world_size=1, use_graphs=not args.no_graphs)
+
+        def lstep(i):
+            j = i % len(xs)
+            loc.load_batch(xs[j], ys[j])
+            loc.step()
+
+        extra["local_s"] = timed(ctx, lstep, args.steps, args.warmup)
+        del loc
+    return el, extra
+
+
+def comm_micro(ctx, eng, iters: int = 10) -> dict:
+    """Standalone RCCL time of each bucket's fp32 reduce-scatter and bf16 all-gather
+    (the sharded engine's two collectives), max over ranks, in microseconds."""
+    out = {}
+    for i, (b, e, _) in enumerate(eng.buckets):
+        g = torch.empty(e - b, dtype=torch.float32, device=ctx.device)
+        gs = torch.empty((e - b) // ctx.world_size, dtype=torch.float32, device=ctx.device)
+        w = torch.empty(e - b, dtype=torch.bfloat16, device=ctx.device)
+        ws = torch.empty((e - b) // ctx.world_size, dtype=torch.bfloat16, device=ctx.device)
+        res = []
+        if ctx.backend != "nccl":   # gloo rehearsal: no device reduce-scatter / in-place gather
+            fns = (lambda: dist.all_reduce(g), lambda: dist.all_reduce(w.float()))
+        else:
+            fns = (lambda: dist.reduce_scatter_tensor(gs, g), lambda: dist.all_gather_into_tensor(w, ws))
+        for fn in fns:
+            fn()
+            dist.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(iters):
+                fn()
+            torch.cuda.synchronize()
+            t = torch.tensor([(time.perf_counter() - t0) / iters * 1e6], device=ctx.device, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            res.append(round(t.item(), 1))
+        out[f"bucket{i}"] = {"mb_fp32": round((e - b) * 4 / 2**20, 2), "reduce_scatter_fp32_us": res[0],
+                             "all_gather_bf16_us": res[1]}
+    return out
+
+
+CNN_CONFIGS = (("lenet5", 256, 50), ("resnet18", 64, 20), ("resnet18", 256, 8))
+
+
+def run_cnn(ctx, name: str, batch: int, steps: int, warmup: int = 3) -> dict:
+    """One BASELINE CNN config (#4 LeNet-5 28x28, #5 ResNet-18 224x224) at this world
+    size: SGD momentum 0.9, bf16 native kernels, synthetic data, random-init weights;
+    per-step DP = GraphedDPStep (fp32 bucket all-reduce on RCCL between the links of
+    the backward graph chain), N = 1 = the single-process graphed step."""
+    import ldnn
+    from ldnn.data.datasets import SHAPES
+    from ldnn.models import CrossEntropyLoss, build_model, dataset_for, xavier_init as xinit
+    from ldnn.optim import SGD
+    from ldnn.parallel.comm import TorchComm
+    from ldnn.parallel.ddp import DataParallel
+    from ldnn.train.graphed import GraphedDPStep, GraphedStep
+
+    shape = SHAPES[dataset_for(name)]
+    nc = 1000 if name == "resnet18" else 10
+    g = torch.Generator(device=ctx.device).manual_seed(100 + ctx.rank)
+    xs = [torch.randn(batch, *shape, device=ctx.device, generator=g).bfloat16() for _ in range(2)]
+    ys = [torch.randint(0, nc, (batch,), device=ctx.device, generator=g) for _ in range(2)]
+    crit = CrossEntropyLoss()
+
+    def make(dp_on: bool):
+        torch.manual_seed(0)
+        m = build_model(name)
+        xinit(m)
+        ldnn.prepare(m, ctx.device)
+        opt = SGD(m.parameters(), lr=0.01, momentum=0.9)
+        dp = DataParallel(m, TorchComm(), bucket_cap_mb=32.0) if dp_on else None
+        net = dp if dp is not None else m
+        opt.zero_grad()
+        crit(net(xs[0]), ys[0]).backward()
+        if dp is not None:
+            dp.finish_gradient_sync()
+        opt.step()
+        if dp is not None:
+            return GraphedDPStep(dp, crit, opt, xs[0], ys[0]), m
+        return GraphedStep(m, crit, opt, xs[0], ys[0], warmup=0), m
+
+    gs, m = make(ctx.world_size > 1)
+    el = timed(ctx, lambda i: gs(xs[i % 2], ys[i % 2]), steps, warmup)
+    ms = el / steps * 1e3
+    rec = {"model": name, "per_gpu_batch": batch, "global_batch": batch * ctx.world_size, "steps": steps,
+           "ms_per_step": round(ms, 4), "samples_per_s": round(batch * ctx.world_size / el * steps, 1),
+           "n_params": sum(p.numel() for p in m.parameters())}
+    if ctx.world_size > 1:
+        rec["buckets"] = len(gs.bk.buckets)
+        rec["graph_segments"] = gs.n_segments
+        del gs
+        gl, _ = make(False)
+        ell = timed(ctx, lambda i: gl(xs[i % 2], ys[i % 2]), steps, warmup)
+        rec["per_gpu_local_ms"] = round(ell / steps * 1e3, 4)
+        rec["scaling_efficiency"] = round(ell / el, 4)
+        del gl
+    else:
+        rec["per_gpu_local_ms"] = rec["ms_per_step"]
+        rec["scaling_efficiency"] = 1.0
+    torch.cuda.empty_cache()
+    return rec
 
 
 def run_stock(ctx, args):
@@ -142,6 +265,31 @@ def run_stock(ctx, args):
     return timed(ctx, step, args.steps, args.warmup)
 
 
+def _free_port() -> int:
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    return port
+
+
+def self_launch(args) -> int:
+    """--gpus N > 1 without a launcher: run `torch.distributed.run` as a CHILD process
+    (never exec: nothing here has touched the GPU yet) and return its exit code.
+    Rank 0's JSON line reaches our stdout through the inherited file descriptor."""
+    if args.backend in ("auto", "nccl"):
+        ndev = torch.cuda.device_count()   # does not initialise the GPU runtime
+        if ndev < args.gpus:
+            print(f"bench.py: --gpus {args.gpus} with RCCL needs {args.gpus} GPUs, this node has {ndev} "
+                  f"(RCCL refuses two ranks on one GPU; use --backend gloo to rehearse)", file=sys.stderr)
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -160,25 +308,36 @@ def main():
     ap.add_argument("--gemms", choices=["ldnn", "library"], default="ldnn",
                     help="ldnn: every GEMM on ldnn's own MFMA kernels (default); library: the plain GEMMs "
                          "(fp32 wgrads, bias+ReLU forwards, hidden dgrad) on hipBLASLt, as an A/B baseline")
-    ap.add_argument("--pad-input", action="store_true",
-                    help="with --gemms library: pad the 784-wide first layer to K = 832 (measured slightly slower)")
-    ap.add_argument("--overlap-opt", action="store_true",
-                    help="1 GPU: optimizer update of all weights but W_0 on a side stream beside wgrad(0)")
-    ap.add_argument("--concurrent-wgrad", action="store_true",
-                    help="1 GPU: wgrad(1) on a side stream beside dgrad(1) + wgrad(0)")
     ap.add_argument("--no-fuse-head-dgrad", action="store_true",
                     help="separate head dgrad GEMM instead of the head kernel's fused dgrad (dReLU + dbias)")
     ap.add_argument("--head-dgrad-mode", type=int, default=-1,
                     help="-1 auto (streaming dh kernel for <= 16 classes), 1 fused (h re-read), 2 fused (h in LDS)")
-    ap.add_argument("--early-opt", choices=["auto", "on", "off"], default="auto",
-                    help="1 GPU: update W_{L-1}..W_1 on a side stream beside the last dgrad GEMM")
     ap.add_argument("--compare-stock", action="store_true")
     ap.add_argument("--backend", default="auto", help="auto (nccl = RCCL on GPUs) | gloo (testing only)")
+    ap.add_argument("--no-configs", action="store_true", help="skip the LeNet-5 / ResNet-18 config timings")
     args = ap.parse_args()
 
+    if args.gpus > 1 and D.launch_env()[1] == 1:
+        sys.exit(self_launch(args))
+    if D.launch_env()[1] != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but the launcher started {D.launch_env()[1]} ranks", file=sys.stderr)
+        sys.exit(2)
+    if args.backend in ("auto", "nccl") and args.gpus > torch.cuda.device_count():
+        print(f"bench.py: --gpus {args.gpus} with RCCL needs one GPU per rank, this node has "
+              f"{torch.cuda.device_count()}", file=sys.stderr)
+        sys.exit(2)
     ctx = D.setup(None if args.backend == "auto" else args.backend)
     n = ctx.world_size
+    assert n == args.gpus, (n, args.gpus)
+    comm_info = {"backend": "RCCL" if ctx.backend == "nccl" else ctx.backend, "ranks": n}
+    if n > 1:
+        devs = [torch.zeros(1, dtype=torch.int64, device=ctx.device) for _ in range(n)]
+        dist.all_gather(devs, torch.tensor([ctx.device.index or 0], device=ctx.device))
+        comm_info["devices"] = [int(d.item()) for d in devs]
+        if ctx.backend == "nccl" and len(set(comm_info["devices"])) != n:
+            raise SystemExit(f"bench.py: RCCL ranks share a GPU: {comm_info['devices']}")
     el, extra = run_ldnn(ctx, args)
+    local_s = extra.pop("local_s", el)
     comm = "RCCL" if ctx.backend == "nccl" else ctx.backend
     ms = el / args.steps * 1e3
     value = args.batch * n * args.steps / el
@@ -207,12 +366,18 @@ def main():
                       "head dgrad), SGD" if args.gemms == "ldnn" else
                       "hipBLASLt: fp32 wgrads, bias/ReLU fwd, hidden dgrad; ldnn: fused dReLU+dbias pass, "
                       "classifier head (Linear + softmax-xent + argmax + head dgrad), SGD"),
+            "comm": comm_info,
             "grad_sync": ("none (1 GPU)" if n == 1 else
                           f"fp32 {comm} all-reduce, bucketed, overlapped" if args.no_shard else
                           f"fp32 {comm} reduce-scatter (bucketed, overlapped) + sharded SGD + bf16 weight all-gather"),
         },
     }
+    rec["per_gpu_local_ms"] = round(local_s / args.steps * 1e3, 4)
+    rec["scaling_efficiency"] = round(local_s / el, 4)
+    rec["rccl_ranks"] = n if ctx.backend == "nccl" else 0
     rec.update(extra)
+    if not args.no_configs:
+        rec["configs"] = {f"{name}_b{b}": run_cnn(ctx, name, b, st) for name, b, st in CNN_CONFIGS}
     if args.compare_stock:
         el_s = run_stock(ctx, args)
         stock = args.batch * n * args.steps / el_s

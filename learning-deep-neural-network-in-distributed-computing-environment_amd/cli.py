@@ -75,9 +75,10 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--bucket_mb", type=float, default=32.0)
     p.add_argument("--grad_comm_dtype", choices=["fp32", "bf16"], default="fp32",
                    help="dtype of the per-step gradient all-reduce (bf16 halves the xGMI bytes)")
-    p.add_argument("--oneshot_bytes", type=int, default=0,
+    p.add_argument("--oneshot_bytes", type=int, default=None,
                    help="RCCL runs: SUM all-reduces of at most this many bytes use the one-shot IPC kernel that "
-                        "reads every peer's copy over its own xGMI link (parallel/ipc.py); 0 = off")
+                        "reads every peer's copy over its own xGMI link (parallel/ipc.py); default 4 MiB "
+                        "(env LDNN_ONESHOT_BYTES), 0 = off")
     p.add_argument("--augment", nargs="?", const="autoaugment", default="none",
                    choices=["none", "autoaugment", "flipcrop", "autoaugment+flipcrop"],
                    help="training-set augmentation in the native input kernel (augment.hip); bare --augment = "
@@ -185,7 +186,8 @@ def main(argv=None):
         D.broadcast_module(model)
         flat.refresh_shadow()
     elif args.sync_every == "step" and args.topology == "allreduce" and world > 1:
-        dp = DataParallel(model, comm, bucket_cap_mb=args.bucket_mb, average=args.aggregation_type == "equal",
+        dp = DataParallel(model, comm, bucket_cap_mb=args.bucket_mb,
+                          local_weight=args.local_weight if args.aggregation_type == "weighted" else None,
                           comm_dtype=torch.bfloat16 if args.grad_comm_dtype == "bf16" else None)
     else:  # reference A6: broadcast every state_dict entry from rank 0
         D.broadcast_module(model)

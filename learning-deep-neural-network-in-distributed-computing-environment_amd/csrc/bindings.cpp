@@ -1035,9 +1035,10 @@ struct OneShotComm {
   char* data = nullptr;      // own staging region, 2 halves
   uint32_t* sig = nullptr;   // own signal region (uncached)
   int* err = nullptr;        // own error word (uncached)
+  uint32_t* ctr = nullptr;   // own per-block epoch counters (device memory: graph-replay safe)
   ldnn::IpcPeers peers{};
   std::vector<void*> opened;
-  uint32_t epoch = 0;
+  uint64_t calls = 0;        // host-side count of launches (diagnostics only)
   int blocks;
 
   OneShotComm(int rank_, int world_, int64_t max_bytes, int device, int blocks_)
@@ -1052,15 +1053,20 @@ struct OneShotComm {
     check(hipMemset(sig, 0, sbytes), "hipMemset(signals)");
     check(hipExtMallocWithFlags(reinterpret_cast<void**>(&err), 256, hipDeviceMallocUncached), "hipExtMalloc(err)");
     check(hipMemset(err, 0, 256), "hipMemset(err)");
+    check(hipMalloc(reinterpret_cast<void**>(&ctr), sizeof(uint32_t) * ldnn::kIpcMaxBlocks), "hipMalloc(ctr)");
+    check(hipMemset(ctr, 0, sizeof(uint32_t) * ldnn::kIpcMaxBlocks), "hipMemset(ctr)");
     check(hipDeviceSynchronize(), "hipDeviceSynchronize");
     peers.half_bytes = half_bytes;
     peers.err = err;
+    peers.mine = data;
+    peers.ctr = ctr;
   }
   ~OneShotComm() {
     for (void* q : opened) (void)hipIpcCloseMemHandle(q);
     if (data) (void)hipFree(data);
     if (sig) (void)hipFree(sig);
     if (err) (void)hipFree(err);
+    if (ctr) (void)hipFree(ctr);
   }
   static py::bytes handle_of(void* p) {
     hipIpcMemHandle_t h;
@@ -1100,15 +1106,15 @@ struct OneShotComm {
     const size_t bytes = (size_t)t.numel() * t.element_size();
     TORCH_CHECK(bytes <= half_bytes, "tensor larger than the staging buffer");
     hipStream_t s = cur_stream(t);
-    ++epoch;
-    const int half = epoch & 1;
-    check(hipMemcpyAsync(data + (size_t)half * half_bytes, t.data_ptr(), bytes, hipMemcpyDeviceToDevice, s),
-          "hipMemcpyAsync(staging)");
-    check(ldnn::oneshot_all_reduce(peers, rank, world, epoch, half, t.numel(), bf16, t.data_ptr(), blocks, s),
+    ++calls;
+    check(ldnn::oneshot_all_reduce(peers, rank, world, t.numel(), bf16, t.data_ptr(), blocks, s),
           "oneshot_all_reduce");
   }
+  // sticky error word (1: some call timed out waiting for a peer; every later call
+  // leaves its tensor unsummed).  Synchronises the device.
   int error() const {
     int v = 0;
+    check(hipDeviceSynchronize(), "hipDeviceSynchronize");
     check(hipMemcpy(&v, err, sizeof(int), hipMemcpyDeviceToHost), "hipMemcpy(err)");
     return v;
   }
@@ -1129,7 +1135,7 @@ PYBIND11_MODULE(_C, m) {
       .def("connect", &OneShotComm::connect, py::arg("handles"))
       .def("all_reduce", &OneShotComm::all_reduce, py::arg("t"), "in-place sum over ranks (one kernel, one barrier)")
       .def("error", &OneShotComm::error)
-      .def_readonly("epoch", &OneShotComm::epoch)
+      .def_readonly("calls", &OneShotComm::calls)
       .def_readonly("half_bytes", &OneShotComm::half_bytes);
   m.doc() = "ldnn: hand-written gfx950 (MI355X / CDNA4) HIP kernels";
   m.attr("EPI_NONE") = (int)ldnn::EPI_NONE;

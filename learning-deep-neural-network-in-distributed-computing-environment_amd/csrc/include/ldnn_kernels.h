@@ -357,10 +357,13 @@ constexpr int kIpcMaxBlocks = 256;  // signal slots per rank: [block][rank]
 struct IpcPeers {
   const char* data[kIpcMaxRanks];   // every rank's staging region (2 halves of half_bytes)
   uint32_t* sig[kIpcMaxRanks];      // every rank's signal region [kIpcMaxBlocks][kIpcMaxRanks]
-  int* err;                         // this rank's error word (1: a peer never arrived)
+  char* mine;                       // this rank's staging region (= data[rank], writable)
+  uint32_t* ctr;                    // this rank's per-block epoch counters [kIpcMaxBlocks]
+  int* err;                         // this rank's error word (1: a peer never arrived; sticky)
   size_t half_bytes;
 };
-hipError_t oneshot_all_reduce(const IpcPeers& p, int rank, int world, uint32_t epoch, int half, int64_t n, bool bf16,
-                              void* out, int blocks, hipStream_t s);
+// buf <- sum over ranks of buf (in place), one kernel: stage, barrier, sum
+hipError_t oneshot_all_reduce(const IpcPeers& p, int rank, int world, int64_t n, bool bf16, void* buf, int blocks,
+                              hipStream_t s);
 
 }  // namespace ldnn

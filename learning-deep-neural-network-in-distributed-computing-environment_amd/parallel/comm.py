@@ -63,6 +63,7 @@ class Comm:
         the reference's dead time-limit break would cause."""
         if self.world_size <= 1:
             return
+        self.check_errors()
         n, h = self.schedule_digest()
         v = torch.tensor([n, int(h[:15], 16)], dtype=torch.int64,
                          device=device if device is not None else "cpu")
@@ -70,6 +71,9 @@ class Comm:
         if any(not torch.equal(got[0], g) for g in got):
             desc = ", ".join(f"rank {r}: {int(g[0])} ops #{int(g[1]):015x}" for r, g in enumerate(got))
             raise RankDivergenceError(f"collective schedules diverged{' at ' + where if where else ''}: {desc}")
+
+    def check_errors(self):
+        """Raise if a device-side collective path recorded a failure (one-shot IPC timeout)."""
 
     # -- API (implemented by subclasses)
     def all_reduce(self, t: torch.Tensor, op: str = SUM, async_op: bool = False):
@@ -129,15 +133,37 @@ class TorchComm(Comm):
     def _global(self, r: int) -> int:
         return r if self.group is None else dist.get_global_rank(self.group, r)
 
-    def enable_oneshot(self, max_bytes: int, device=None):
+    def enable_oneshot(self, max_bytes: int, device=None, self_test: bool = True):
         """Route SUM all-reduces of at most ``max_bytes`` (fp32 / bf16 device tensors)
-        through the one-shot IPC path (parallel/ipc.py).  Collective: every rank calls it."""
+        through the one-shot IPC path (parallel/ipc.py).  Collective: every rank calls it.
+        With ``self_test`` the path is verified against RCCL first and left off (on
+        every rank, with a warning) if it fails anywhere -- e.g. a node whose GPUs
+        cannot map each other's memory."""
         from .ipc import OneShotAllReduce
 
-        self.oneshot = OneShotAllReduce(max_bytes, group=self.group, device=device)
-        return self.oneshot
+        try:
+            os_ = OneShotAllReduce(max_bytes, group=self.group, device=device)
+            ok = os_.self_test() if self_test else True
+        except Exception as e:  # noqa: BLE001 -- IPC mapping refused: keep RCCL
+            import warnings
+
+            warnings.warn(f"one-shot IPC all-reduce unavailable ({e!r}); using RCCL for every message")
+            flag = torch.zeros(1, device=device or torch.device("cuda", torch.cuda.current_device()))
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)   # (matches self_test's collective)
+            return None
+        if not ok:
+            import warnings
+
+            warnings.warn("one-shot IPC all-reduce failed its self-test on some rank; using RCCL for every message")
+            return None
+        self.oneshot = os_
+        return os_
 
     oneshot = None
+
+    def check_errors(self):
+        if self.oneshot is not None:
+            self.oneshot.check()
 
     def all_reduce(self, t, op=SUM, async_op=False):
         self.record("all_reduce", t)
@@ -268,14 +294,20 @@ class FakeComm(Comm):
             rt.copy_(merged[(src, self.rank)])
 
 
+ONESHOT_DEFAULT_BYTES = 4 << 20
+
+
 def default_comm(oneshot_bytes: int | None = None) -> Comm:
-    """TorchComm over the default group (LocalComm for a world of one).  oneshot_bytes
-    (or env LDNN_ONESHOT_BYTES) > 0 enables the one-shot IPC all-reduce for messages up
-    to that size when the backend is RCCL (collective: every rank must pass the same)."""
+    """TorchComm over the default group (LocalComm for a world of one).  With RCCL,
+    SUM all-reduces of at most ``oneshot_bytes`` (default 4 MiB, env
+    LDNN_ONESHOT_BYTES; 0 = off) use the one-shot IPC kernel that reads every peer's
+    copy over its own xGMI link (SURVEY §5 small-message path: metric vectors, small
+    gradient buckets such as LeNet-5's whole 0.25 MB gradient).  Collective: every
+    rank must pass the same value."""
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
         c = TorchComm()
         if oneshot_bytes is None:
-            oneshot_bytes = int(os.environ.get("LDNN_ONESHOT_BYTES", "0"))
+            oneshot_bytes = int(os.environ.get("LDNN_ONESHOT_BYTES", str(ONESHOT_DEFAULT_BYTES)))
         if oneshot_bytes > 0 and c.backend == "nccl" and torch.cuda.is_available():
             c.enable_oneshot(oneshot_bytes)
         return c

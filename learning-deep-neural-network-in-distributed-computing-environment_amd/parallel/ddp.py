@@ -43,8 +43,18 @@ def ensure_flat(module: nn.Module, device=None) -> FlatParams:
 
 
 class GradBucketer:
+    """Flat gradient buckets, each all-reduced (SUM) once its last gradient is written.
+
+    ``local_weight`` (None = equal averaging, folded into the optimizer's 1/N
+    ``grad_scale``) selects the reference's self-weighted all-reduce
+    (BAR/communication.py:4-10): ``g <- w g_own + (1-w) (sum - g_own) / (N-1)``.
+    Each bucket's own gradient is kept in an fp32 copy taken right before its
+    collective, and after the wait ONE fused mix3 pass (elementwise.hip, K18)
+    evaluates ``(w - o) g_own + o sum`` with ``o = (1-w)/(N-1)`` in place.
+    A world of one keeps its gradient (Q4: no division by N-1 = 0)."""
+
     def __init__(self, flat: FlatParams, comm: Comm, bucket_cap_elems: int = 8 << 20,
-                 comm_dtype: torch.dtype | None = None):
+                 comm_dtype: torch.dtype | None = None, local_weight: float | None = None):
         self.flat, self.comm = flat, comm
         self.comm_dtype = None if comm_dtype in (None, torch.float32) else comm_dtype
         self.buckets: list[dict] = []
@@ -66,11 +76,49 @@ class GradBucketer:
                 self.of_param[id(p)] = i
         self._stage = ([torch.empty(b["end"] - b["begin"], dtype=self.comm_dtype, device=flat.grad.device)
                         for b in self.buckets] if self.comm_dtype is not None else None)
+        N = comm.world_size
+        self.weighted = local_weight is not None and N > 1
+        self._own = None
+        if self.weighted:
+            w = float(local_weight)
+            other = (1.0 - w) / (N - 1)
+            self._mix_ab = (w - other, other)
+            self._own = [torch.empty(b["end"] - b["begin"], dtype=torch.float32, device=flat.grad.device)
+                         for b in self.buckets]
         self.works: list = []
         self._pending: list[int] = []
         self._launched: list[bool] = []
         self.active = False
         flat.add_ready_hook(self._on_ready)
+
+    def grad_view(self, i):
+        b = self.buckets[i]
+        return self.flat.grad[b["begin"]: b["end"]]
+
+    def comm_buffer(self, i):
+        """The buffer bucket i's collective runs on (bf16 stage or the fp32 gradient)."""
+        return self._stage[i] if self._stage is not None else self.grad_view(i)
+
+    def pre_collective(self, i):
+        """Stream-ordered work right before bucket i's collective: keep the own
+        gradient (weighted), cast into the bf16 stage (comm_dtype)."""
+        g = self.grad_view(i)
+        if self._own is not None:
+            self._own[i].copy_(g)
+        if self._stage is not None:
+            self._stage[i].copy_(g)
+
+    def post_collective(self, i):
+        """Stream-ordered work after bucket i's collective landed: widen the stage
+        back into the fp32 gradient, apply the weighted mix."""
+        g = self.grad_view(i)
+        if self._stage is not None:
+            g.copy_(self._stage[i])
+        if self._own is not None:
+            from .aggregation import _mix
+
+            a, b = self._mix_ab
+            _mix(g, self._own[i], g, a=a, b=b)
 
     def prepare(self):
         self._pending = [len(b["params"]) for b in self.buckets]
@@ -80,15 +128,9 @@ class GradBucketer:
         self.active = True
 
     def _launch(self, i):
-        b = self.buckets[i]
         self._launched[i] = True
-        g = self.flat.grad[b["begin"]: b["end"]]
-        if self._stage is not None:
-            st = self._stage[i]
-            st.copy_(g)
-            self.works.append((self.comm.all_reduce(st, SUM, async_op=True), i))
-        else:
-            self.works.append((self.comm.all_reduce(g, SUM, async_op=True), None))
+        self.pre_collective(i)
+        self.works.append((self.comm.all_reduce(self.comm_buffer(i), SUM, async_op=True), i))
 
     def _on_ready(self, p):
         if not self.active or id(p) in self._seen:
@@ -110,18 +152,21 @@ class GradBucketer:
         for w, i in self.works:
             if w is not None:
                 w.wait()
-            if i is not None:
-                b = self.buckets[i]
-                self.flat.grad[b["begin"]: b["end"]].copy_(self._stage[i])
+            self.post_collective(i)
         self.works = []
         self.active = False
 
 
 class DataParallel(nn.Module):
-    """Wrap a model for synchronous per-step DP (SURVEY P1 done per step)."""
+    """Wrap a model for synchronous per-step DP (SURVEY P1 done per step).
+
+    ``local_weight`` = w turns the per-step all-reduce into the reference's
+    weighted average (``--aggregation_type weighted``, BAR/communication.py:4-10);
+    None (default) is the equal average (BAR/communication.py:21-25)."""
 
     def __init__(self, module: nn.Module, comm: Comm | None = None, bucket_cap_mb: float = 32.0,
-                 broadcast_init: bool = True, average: bool = True, comm_dtype: torch.dtype | None = None):
+                 broadcast_init: bool = True, average: bool = True, comm_dtype: torch.dtype | None = None,
+                 local_weight: float | None = None):
         super().__init__()
         self.module = module
         self.comm = comm or default_comm()
@@ -132,8 +177,11 @@ class DataParallel(nn.Module):
                 for b in module.buffers():
                     self.comm.broadcast(b, 0)
             self.flat.refresh_shadow()
-        self.flat.grad_scale = (1.0 / self.comm.world_size) if average else 1.0
-        self.bucketer = GradBucketer(self.flat, self.comm, int(bucket_cap_mb * (1 << 20) / 4), comm_dtype=comm_dtype)
+        # equal averaging folds 1/N into the fused optimizer; the weighted mix (and a
+        # plain sum, average=False) leave the gradient at scale 1
+        self.flat.grad_scale = (1.0 / self.comm.world_size) if (average and local_weight is None) else 1.0
+        self.bucketer = GradBucketer(self.flat, self.comm, int(bucket_cap_mb * (1 << 20) / 4), comm_dtype=comm_dtype,
+                                     local_weight=local_weight)
 
     def forward(self, *args, **kwargs):
         if self.training and torch.is_grad_enabled() and self.comm.world_size > 1:

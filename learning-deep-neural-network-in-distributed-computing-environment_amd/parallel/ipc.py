@@ -6,15 +6,23 @@ node every GPU has its own xGMI link to each peer, so for small messages (metric
 vectors, the schedule digest, small gradient buckets, the MLP configs' gradients)
 one kernel that reads every peer's copy at once over all links is latency-optimal.
 The native side (``csrc/kernels/ipc.hip``, ``OneShotComm`` in the bindings) owns
-this rank's staging and signal regions; their IPC handles are exchanged once
-through the process group, after which a call is one stream-ordered device copy
-plus one kernel with a single cross-rank barrier -- no host synchronisation.
+this rank's staging, signal and per-block epoch-counter regions; their IPC handles
+are exchanged once through the process group, after which a call is ONE
+stream-ordered kernel (stage, one cross-rank barrier, sum) -- no host
+synchronisation, and no host-side call number in its arguments, so a call
+captured into a hipGraph is a correct call on every replay.
 
 Requirements: every rank of the group on one node, one GPU per rank (a rank may
 map a peer on the same device too: that is how the one-GPU test box runs it),
 fp32 or bf16 tensors with numel % 8 == 0.  Anything else falls back to the
 process group's all-reduce.  Every wait in the kernel has a 5 s wall-clock limit;
-``check()`` raises if a peer never arrived.
+a timed-out call sets a sticky error word and leaves its tensor (and every later
+call's) unsummed: ``check()`` raises then, and ``Comm.check_schedule`` -- run every
+global epoch and every few hundred per-step-DP steps -- calls it.
+
+``self_test()`` (run when the communicator is enabled) sums a rank-dependent
+vector through the kernel and compares with the process group's all-reduce; any
+mismatch or timeout on any rank disables the path on every rank.
 """
 from __future__ import annotations
 
@@ -37,7 +45,11 @@ class OneShotAllReduce:
         mine = tuple(bytes(h) for h in self._c.handles())
         allh: list = [None] * self.world_size
         dist.all_gather_object(allh, mine, group=group)  # the one host exchange: IPC handles
-        self._c.connect([(a, b) for a, b in allh])
+        self.connect_error = None
+        try:
+            self._c.connect([(a, b) for a, b in allh])
+        except Exception as e:  # noqa: BLE001 -- reported by self_test on every rank
+            self.connect_error = e
         dist.barrier(group=group)  # every rank mapped every peer before the first kernel
 
     def eligible(self, t: torch.Tensor) -> bool:
@@ -51,4 +63,22 @@ class OneShotAllReduce:
 
     def check(self) -> None:
         if self._c.error():
-            raise RuntimeError("one-shot all-reduce: a peer rank never reached the barrier (5 s limit)")
+            raise RuntimeError("one-shot all-reduce: a peer rank never reached the barrier (5 s limit); the "
+                               "tensors of that call and of every later one-shot call were left unsummed")
+
+    def self_test(self) -> bool:
+        """Collective: True on every rank iff the kernel summed correctly on every rank."""
+        ok = self.connect_error is None
+        for dt in (torch.float32, torch.bfloat16):
+            n = 4096
+            t = (torch.arange(n, device=self.device, dtype=torch.float32) % 7 + self.rank + 1).to(dt)
+            ref = t.float().clone()
+            dist.all_reduce(ref, group=self.group)
+            for _ in range(3 if ok else 0):   # consecutive calls: both staging halves, epoch counters advance
+                u = t.clone()
+                self.all_reduce(u)
+                torch.cuda.synchronize(self.device)
+                ok = ok and not self._c.error() and torch.allclose(u.float(), ref, rtol=1e-2 if dt != torch.float32 else 0)
+        flag = torch.tensor([1.0 if ok else 0.0], device=self.device)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)
+        return bool(flag.item() == 1.0)

@@ -22,8 +22,12 @@ and steps a fixed batch shape.  Two adapters let the unchanged driver run it:
 ``train_local_epoch`` recognises an ``EngineModule`` and runs ``engine_local_epoch``:
 one ``load_batch`` + ``step`` per full batch, the per-batch losses read from the
 engine's on-device statistics (one small reduction per step, one host read per
-epoch).  A trailing partial batch is skipped (the engine's shapes are static;
-the count is reported as ``engine_local_epoch.last_skipped``).
+epoch).  A trailing partial batch is trained too, as the reference does
+(BAR/trainer.py:202-216): the engine's shapes are static, so it runs
+``StaticMLPEngine.eager_step`` (autograd on the same flat parameters + the fused
+update).  A data-parallel engine instead runs the same number of full steps on
+every rank (collective schedules must match); what it leaves out is reported as
+``engine_local_epoch.last_skipped``.
 """
 from __future__ import annotations
 
@@ -127,20 +131,29 @@ def engine_local_epoch(model: EngineModule, trainloader, optimizer, scheduler=No
     nb = model.full_batches(trainloader)
     if max_steps is not None:
         nb = min(nb, max_steps)
+    partial = not eng.distributed
     # cum[i] = running (loss sum, #correct) after step i -- one tiny reduction per step
-    cum = torch.zeros(max(nb, 1) + 1, 2, dtype=torch.float64, device=dev)
+    cum = torch.zeros(max(nb, 1) + 2, 2, dtype=torch.float64, device=dev)
+    sizes = []
     eng.reset_stats()
     done, skipped = 0, 0
     try:
         for i, (x, y) in enumerate(trainloader):
-            if done >= nb:
-                skipped += y.numel() if y.numel() != eng.B else 0
-                break
-            if y.numel() != eng.B:   # static shapes: a partial batch cannot run
+            if done >= nb + (1 if partial else 0):
                 skipped += y.numel()
-                continue
-            eng.load_batch(x, y)
-            eng.step()
+                break
+            if y.numel() != eng.B:
+                if not partial or done >= nb + 1:
+                    skipped += y.numel()
+                    continue
+                eng.eager_step(x, y)   # the trailing partial batch (single-process engine)
+            else:
+                if done >= nb:
+                    skipped += y.numel()
+                    break
+                eng.load_batch(x, y)
+                eng.step()
+            sizes.append(y.numel())
             torch.sum(eng.stats, 0, dtype=torch.float64, out=cum[done + 1])
             done += 1
             if cutoff is not None:
@@ -152,26 +165,26 @@ def engine_local_epoch(model: EngineModule, trainloader, optimizer, scheduler=No
             optimizer.step()   # a no-op; keeps torch's scheduler-order check quiet
         if step_scheduler and scheduler is not None:
             scheduler.step()
-        _finish(model, done, skipped)
+        _finish(model, done, skipped, sizes)
         raise
-    if done and isinstance(optimizer, EngineOptimizer):
-        optimizer.step()
+    if isinstance(optimizer, EngineOptimizer):
+        optimizer.step()   # a no-op (the engine's fused update ran): keeps the scheduler-order contract
     if step_scheduler and scheduler is not None:
         scheduler.step()
-    return _finish(model, done, skipped, cum)
+    return _finish(model, done, skipped, sizes, cum)
 
 
-def _finish(model, done, skipped, cum=None):
+def _finish(model, done, skipped, sizes, cum=None):
     engine_local_epoch.last_skipped = skipped
-    engine_local_epoch.last_samples = done * model.engine.B
+    engine_local_epoch.last_samples = sum(sizes)
     if cum is None or done == 0:
         return 0.0, 0.0, []
     c = cum[: done + 1].cpu()   # the one host sync of the epoch
     model.engine.sync()
-    per = (c[1:, 0] - c[:-1, 0]) / model.engine.B
+    per = (c[1:, 0] - c[:-1, 0]) / torch.tensor(sizes, dtype=torch.float64)
     losses = per.tolist()
     correct = float(c[done, 1])
-    return float(per.mean()), 100.0 * correct / (done * model.engine.B), losses
+    return float(per.mean()), 100.0 * correct / max(sum(sizes), 1), losses
 
 
 engine_local_epoch.last_skipped = 0

@@ -23,10 +23,9 @@ What makes the ldnn step capturable:
 * every native op writes into caller-provided / caching-allocator tensors
   (graph-pool allocations during capture).
 
-Limitations (checked): one process (no per-step gradient collectives inside
-the graph -- those are issued from Python between graph segments, see
-train/static_mlp.py), static shapes (the last, smaller batch of an epoch runs
-eagerly), CUDA tensors only.
+Limitations (checked): one process (per-step gradient collectives are issued
+from Python between the graphs of a chain: GraphedDPStep below), static shapes
+(the last, smaller batch of an epoch runs eagerly), CUDA tensors only.
 """
 from __future__ import annotations
 
@@ -36,77 +35,18 @@ from ..optim.optimizers import _FlatOptimizer
 from .static_mlp import no_gc
 
 
-# Optimizer overlapped with the backward (GraphedStep overlap_optimizer): the flat
-# buffer is laid out in gradient-ready order, so the parameters whose gradients are
-# final form a growing prefix of it.  When an op notifies new gradients, every
-# parameter that became ready BEFORE it is past its last backward read (its own dgrad
-# / BN backward ran earlier on the main stream), so that prefix is updated on a side
-# stream -- forked from the main stream at that point -- while the backward goes on;
-# the rest is updated on the main stream after the backward and the side stream joins.
-# OFF by default: measured on MI355X (profiles/overlap_optimizer_ab_r2.jsonl, same box,
-# alternated) EnhancedCNN b64 2.21-2.24 ms without it vs 2.32-2.44 ms with it, and
-# 3.27 ms with a 32-block side grid -- the side-stream branch of the replayed graph does
-# not run beside the backward kernels here, it adds to them (as in
-# profiles/graph_branch_concurrency_r2.jsonl).  LDNN_OVERLAP_OPT=1 turns it on,
-# LDNN_OVERLAP_OPT_ELEMS sets the launch granularity, LDNN_OVERLAP_OPT_BLOCKS the side grid.
-# (Assumes every parameter's gradient is written by one op per step -- true of the
-# models here; tied / shared weights need overlap_optimizer=False.)
-_OVERLAP_OPT = __import__("os").environ.get("LDNN_OVERLAP_OPT", "0") != "0"
-_OVERLAP_ELEMS = int(__import__("os").environ.get("LDNN_OVERLAP_OPT_ELEMS", str(4 << 20)))
-_OVERLAP_BLOCKS = int(__import__("os").environ.get("LDNN_OVERLAP_OPT_BLOCKS", "0"))  # side launches' grid cap
-
-
-class _OverlapUpdate:
-    def __init__(self, upd, flat, side: torch.cuda.Stream, min_elems: int):
-        self.upd, self.flat, self.side, self.min_elems = upd, flat, side, min_elems
-        self.segs = flat.segments          # buffer (gradient-ready) order
-        self.idx, self.lo = 0, 0           # [0, lo) updated / launched
-        self.ready: set = set()
-
-    def on_ready(self, params):
-        # (a native op notifies its parameters while its backward still runs; autograd's
-        # AccumulateGrad then re-notifies each one after the op returned -- a repeat is
-        # that echo.  Each parameter's gradient must come from ONE op per step: shared
-        # weights need overlap_optimizer=False.)
-        j = self.idx
-        while j < len(self.segs) and id(self.segs[j].param) in self.ready:
-            j += 1
-        self.ready.update(id(p) for p in params)
-        hi = self.segs[j].offset if j < len(self.segs) else self.flat.numel
-        if j > self.idx and hi - self.lo >= self.min_elems:
-            cur = torch.cuda.current_stream()
-            self.side.wait_stream(cur)     # everything issued so far (the readers of [lo, hi))
-            with torch.cuda.stream(self.side):
-                if _OVERLAP_BLOCKS:
-                    from ..ops import _ext
-                    _ext.C().set_opt_max_blocks(_OVERLAP_BLOCKS)
-                try:
-                    self.upd.update(self.lo, hi)
-                finally:
-                    if _OVERLAP_BLOCKS:
-                        _ext.C().set_opt_max_blocks(0)
-            self.lo, self.idx = hi, j
-
-    def finish(self):
-        self.flat.finalize_grads()         # gradients no op wrote this step (outside [0, lo))
-        self.upd.update(self.lo, self.flat.numel)
-        torch.cuda.current_stream().wait_stream(self.side)
-        self.upd.end()
+# (An optimizer overlapped with the backward on a side-stream branch of the step
+# graph was built in round 2 and measured slower -- EnhancedCNN b64 2.21-2.24 vs
+# 2.32-2.44 ms, profiles/overlap_optimizer_ab_r2.jsonl: a replayed graph's branches
+# run one after the other on this stack -- and removed.)
 
 
 class GraphedStep:
     def __init__(self, model, criterion, optimizer, x_example: torch.Tensor, y_example: torch.Tensor,
-                 warmup: int = 3, stats: torch.Tensor | None = None, overlap_optimizer: bool | None = None):
+                 warmup: int = 3, stats: torch.Tensor | None = None):
         if not x_example.is_cuda:
             raise ValueError("GraphedStep needs GPU tensors")
         self.model, self.criterion, self.optimizer = model, criterion, optimizer
-        if overlap_optimizer is None:
-            overlap_optimizer = _OVERLAP_OPT
-        self._ov_side, self._ov = None, None
-        if overlap_optimizer and isinstance(optimizer, _FlatOptimizer) and optimizer.supports_ranges():
-            self._ov_flat = optimizer._flat_for_group(optimizer.param_groups[0])
-            self._ov_side = torch.cuda.Stream(device=x_example.device)
-            self._ov_flat.add_ready_group_hook(self._on_ready)
         self.x = x_example.detach().clone()
         self.y = y_example.detach().clone()
         self.stats = stats if stats is not None else torch.zeros(2, dtype=torch.float32, device=self.x.device)
@@ -148,21 +88,9 @@ class GraphedStep:
         except TypeError:  # a stock criterion without the stats argument
             loss = self.criterion(out.float(), self.y)
         seed = self._one if loss.dtype == torch.float32 and loss.dim() == 0 else None
-        if self._ov_side is not None:
-            self._ov = _OverlapUpdate(self.optimizer.range_updater(), self._ov_flat, self._ov_side, _OVERLAP_ELEMS)
-            try:
-                loss.backward(seed)
-                self._ov.finish()
-            finally:
-                self._ov = None
-        else:
-            loss.backward(seed)
-            self.optimizer.step()
+        loss.backward(seed)
+        self.optimizer.step()
         return loss
-
-    def _on_ready(self, params):
-        if self._ov is not None:
-            self._ov.on_ready(params)
 
     def _sync_lr(self, force: bool = False):
         lrs = [g["lr"] for g in self.optimizer.param_groups]
@@ -209,19 +137,31 @@ class GraphedDPStep:
     (parallel/ddp.py) already buckets the flat gradient and launches each bucket's
     all-reduce from backward hooks -- but eagerly, one Python launch per kernel.
 
-    mode "in_graph" (default with RCCL): ONE graph per step.  The bucket-readiness
-    hooks fire once during capture; at each the capture forks onto a side stream
-    and captures that bucket's RCCL all-reduce there (after the bucket's bf16
-    staging copy when comm_dtype is bf16), so in every replay bucket i travels over
-    xGMI while the backward nodes of buckets i+1.. still run; the capture joins the
-    side stream before the (widen +) fused optimizer nodes.  1/N averaging is
-    folded into the optimizer (flat.grad_scale).
-    mode "after" (host-staged backends such as gloo, or on request): graph G1 =
-    zero_grad + forward + backward, then the bucket collectives from Python, then
-    graph G2 = (widen +) optimizer.
+    mode "segmented" (default with RCCL): the step is captured as a CHAIN of
+    graphs cut at the bucket-ready points of the backward -- G_0 = zero_grad +
+    forward + loss + backward up to the moment bucket b_0's last gradient is
+    written, G_1 = the backward on to b_1's, ... -- plus G_opt = (widen / mix +)
+    fused optimizer.  A replay launches G_0, issues b_0's RCCL all-reduce from the
+    host (RCCL's own stream waits on an event behind G_0), launches G_1 at once,
+    and so on; the host then makes the compute stream wait for every collective
+    (no host sync) and launches G_opt.  So bucket i travels over xGMI on its own
+    HIP stream / hardware queue while G_{i+1}.. run on the compute stream.
+    (Putting the collectives on a side-stream branch INSIDE one graph does not
+    overlap on this stack: a replayed graph's branches execute one after the
+    other, profiles/graph_branch_concurrency_r2.jsonl -- separate streams do.)
+    mode "after" (host-staged backends such as gloo, or on request): one backward
+    graph, then the bucket collectives from Python, then G_opt.
 
-    ``comm_fn(i, buf)`` (tests) replaces the collective of bucket i and is issued
-    exactly where the collective would be.
+    1/N averaging is folded into the optimizer (flat.grad_scale); the weighted
+    all-reduce's mix and the bf16 stage widen run in G_opt (GradBucketer
+    post_collective).  Every replay issues its collectives through ``comm`` -- the
+    same ops, in the same order, as the eager fallback for an odd-shaped batch --
+    so the runtime schedule check (Comm.check_schedule) sees identical sequences
+    on ranks whose last batch is short and on ranks whose is not.
+
+    ``comm_fn(i, buf)`` (tests, overlap probes) replaces the collective of bucket i;
+    it is called on the host where the collective would be issued and may return
+    an object with ``wait()`` (called before G_opt, e.g. a cross-stream join).
     """
 
     def __init__(self, dp, criterion, optimizer, x_example: torch.Tensor, y_example: torch.Tensor,
@@ -238,24 +178,29 @@ class GraphedDPStep:
         self.y = y_example.detach().clone()
         self.stats = stats if stats is not None else torch.zeros(2, dtype=torch.float32, device=self.x.device)
         self._lrs = None
+        self.device_collectives = bool(getattr(self.comm, "device_collectives", False))
         if mode is None:
-            mode = "in_graph" if (getattr(self.comm, "device_collectives", False) or comm_fn is not None) else "after"
-        if mode not in ("in_graph", "after"):
+            mode = "segmented" if (self.device_collectives or comm_fn is not None) else "after"
+        if mode not in ("segmented", "after"):
             raise ValueError(f"unknown GraphedDPStep mode {mode!r}")
         self.mode = mode
         nb = len(self.bk.buckets)
-        self.side = torch.cuda.Stream(device=self.x.device) if mode == "in_graph" else None
         self._cap = None
-        self.flat.add_ready_hook(self._on_ready)
+        self.flat.add_ready_group_hook(self._on_ready)
         torch.cuda.synchronize(self.x.device)
         self.stats.zero_()
-        self.g1 = torch.cuda.CUDAGraph()
-        self.g2 = torch.cuda.CUDAGraph() if mode == "after" else None
+        self.graphs: list = []     # the backward chain G_0 .. G_k
+        self.issue: list = []      # buckets whose collective is issued after G_j
+        self._empty: list = []     # G_j captured no work (not replayed)
+        self._pool = torch.cuda.graph_pool_handle()
+        self._stream = torch.cuda.Stream(device=self.x.device)
+        self._stream.wait_stream(torch.cuda.current_stream())
         self._set_capture(True)
         try:
             self._cap = {"pending": [len(b["params"]) for b in self.bk.buckets], "fired": [False] * nb,
-                         "seen": set(), "works": []}
-            with no_gc(), torch.cuda.graph(self.g1):
+                         "seen": set()}
+            with no_gc(), torch.cuda.stream(self._stream):
+                self._begin()
                 self.optimizer.zero_grad()
                 out = self.model(self.x)
                 try:
@@ -263,23 +208,21 @@ class GraphedDPStep:
                 except TypeError:
                     loss = self.criterion(out.float(), self.y)
                 loss.backward()
-                for i in range(nb):  # buckets whose parameters got no gradient
-                    if not self._cap["fired"][i]:
-                        self._fire(i)
-                if mode == "in_graph":
-                    for w in self._cap["works"]:
-                        if w is not None:
-                            w.wait()
-                    torch.cuda.current_stream().wait_stream(self.side)
-                    self._widen_and_step()
-            self._cap = None
+                rest = [i for i in range(nb) if not self._cap["fired"][i]]   # params with no gradient
+                if rest:
+                    self._fire(rest)
+                self._end()
+                if self.mode == "after":
+                    self.issue[-1] = list(range(nb))
+                self.g_opt = torch.cuda.CUDAGraph()
+                self.g_opt.capture_begin(pool=self._pool, capture_error_mode="thread_local")
+                self._widen_and_step()
+                self.g_opt.capture_end()
             self.loss = loss
-            if mode == "after":
-                with no_gc(), torch.cuda.graph(self.g2, pool=self.g1.pool()):
-                    self._widen_and_step()
         finally:
             self._cap = None
             self._set_capture(False)
+        torch.cuda.current_stream().wait_stream(self._stream)
         self._sync_lr(force=True)
 
     # ---------------------------------------------------------------- capture
@@ -287,34 +230,60 @@ class GraphedDPStep:
         if isinstance(self.optimizer, _FlatOptimizer):
             self.optimizer._ldnn_capturing = on
 
+    def _begin(self):
+        # thread_local: RCCL's watchdog / gloo's progress threads keep querying the HIP
+        # runtime while the (main or autograd) thread captures
+        g = torch.cuda.CUDAGraph()
+        g.capture_begin(pool=self._pool, capture_error_mode="thread_local")
+        self._cur = g
+
+    def _end(self):
+        import warnings
+
+        with warnings.catch_warnings(record=True) as ws:
+            warnings.simplefilter("always")
+            self._cur.capture_end()
+        self.graphs.append(self._cur)
+        self.issue.append([])
+        self._empty.append(any("empty" in str(w.message).lower() for w in ws))
+        self._cur = None
+
     def _widen_and_step(self):
-        if self.bk._stage is not None:
-            for i, b in enumerate(self.bk.buckets):
-                self.flat.grad[b["begin"]: b["end"]].copy_(self.bk._stage[i])
+        for i in range(len(self.bk.buckets)):
+            self.bk.post_collective(i)
         self.optimizer.step()
 
-    def _fire(self, i):
-        """(capture) bucket i's gradients are complete at this point of the graph."""
-        self._cap["fired"][i] = True
-        if self.bk._stage is not None:
-            b = self.bk.buckets[i]
-            self.bk._stage[i].copy_(self.flat.grad[b["begin"]: b["end"]])
-        if self.mode == "in_graph":
-            self.side.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(self.side):
-                self._cap["works"].append(self._collective(i, async_op=True))
+    def _fire(self, idx):
+        """(capture) buckets ``idx``'s gradients are complete at this point of the backward."""
+        for i in idx:
+            self._cap["fired"][i] = True
+            self.bk.pre_collective(i)   # own-gradient copy / bf16 stage: captured before the cut
+        if self.mode == "segmented":
+            # cut the chain here: the autograd thread runs this hook with the forward's
+            # (= capture) stream current, so the next backward kernels land in G_{j+1}
+            if torch.cuda.current_stream() != self._stream:
+                raise RuntimeError("GraphedDPStep: a gradient-ready hook ran off the capture stream")
+            self._end()
+            self.issue[-1].extend(idx)
+            self._begin()
 
-    def _on_ready(self, p):
+    def _on_ready(self, params):
         c = self._cap
-        if c is None or id(p) in c["seen"]:
+        if c is None:
             return
-        c["seen"].add(id(p))
-        i = self.bk.of_param.get(id(p))
-        if i is None:
-            return
-        c["pending"][i] -= 1
-        if c["pending"][i] == 0 and not c["fired"][i]:
-            self._fire(i)
+        done = []
+        for p in params:
+            if id(p) in c["seen"]:
+                continue
+            c["seen"].add(id(p))
+            i = self.bk.of_param.get(id(p))
+            if i is None:
+                continue
+            c["pending"][i] -= 1
+            if c["pending"][i] == 0 and not c["fired"][i]:
+                done.append(i)
+        if done:
+            self._fire(done)
 
     def _sync_lr(self, force: bool = False):
         lrs = [g["lr"] for g in self.optimizer.param_groups]
@@ -323,18 +292,15 @@ class GraphedDPStep:
                 self.optimizer.sync_hyperparams()
             self._lrs = lrs
 
-    def _buf(self, i):
-        if self.bk._stage is not None:
-            return self.bk._stage[i]
-        b = self.bk.buckets[i]
-        return self.flat.grad[b["begin"]: b["end"]]
-
-    def _collective(self, i, async_op=False):
-        buf = self._buf(i)
+    def _collective(self, i):
+        buf = self.bk.comm_buffer(i)
         if self.comm_fn is not None:
-            self.comm_fn(i, buf)
-            return None
-        return self.comm.all_reduce(buf, self._SUM, async_op=async_op)
+            return self.comm_fn(i, buf)
+        return self.comm.all_reduce(buf, self._SUM, async_op=True)
+
+    @property
+    def n_segments(self) -> int:
+        return len(self.graphs)
 
     # -------------------------------------------------------------------- API
     def flush_stats(self, into: torch.Tensor):
@@ -347,15 +313,19 @@ class GraphedDPStep:
         self.x.copy_(x, non_blocking=True)
         self.y.copy_(y, non_blocking=True)
         self._sync_lr()
-        self.g1.replay()
-        if self.mode == "after":
-            if not getattr(self.comm, "device_collectives", False):
+        works = []
+        for j, g in enumerate(self.graphs):
+            if not self._empty[j]:
+                g.replay()
+            issue = self.issue[j]
+            if issue and not self.device_collectives and self.comm_fn is None:
                 torch.cuda.current_stream().synchronize()  # a host-staged backend reads the buffers
-            works = [self._collective(i, async_op=True) for i in range(len(self.bk.buckets))]
-            for w in works:
-                if w is not None:
-                    w.wait()
-            self.g2.replay()
+            for i in issue:
+                works.append(self._collective(i))
+        for w in works:
+            if w is not None:
+                w.wait()
+        self.g_opt.replay()
         return self.loss
 
     def _eager_step(self, x, y):

@@ -96,12 +96,9 @@ class StaticMLPEngine:
     def __init__(self, model, batch_size: int, optim: OptimConfig | None = None, *, device=None,
                  process_group=None, world_size: int | None = None, bucket_cap_elems: int = 8 << 20,
                  use_graphs: bool = True, average_grads: bool = True, use_head_kernels: bool = True,
-                 shard_optimizer: bool | None = None, overlap_optimizer: bool = False, wgrad_combine: bool = True,
-                 fuse_optimizer: bool | None = None, library_gemms: bool | None = None,
-                 fuse_head_dgrad: bool | None = None, early_optimizer: bool | None = None,
-                 library_dgrad: bool | None = None, concurrent_wgrad: bool = False, pad_input: bool = False,
-                 head_dgrad_mode: int = -1, relu_masks: bool = True, wgrad_slabs: bool = True,
-                 transposed_dgrad: bool = True, bias_ones_column: bool = True, fuse_head_wgrad: bool = False):
+                 shard_optimizer: bool | None = None, wgrad_combine: bool = True, library_gemms: bool | None = None,
+                 fuse_head_dgrad: bool | None = None, library_dgrad: bool | None = None, head_dgrad_mode: int = -1,
+                 relu_masks: bool = True, transposed_dgrad: bool = True, bias_ones_column: bool = True):
         from ..models.mlp import MLP
 
         if not isinstance(model, MLP):
@@ -208,18 +205,6 @@ class StaticMLPEngine:
                                 or self.layers[-1].in_features <= self.C.head_dgrad_max_k()))
         self._head_db_ws = (torch.empty(self.C.head_dgrad_ws_floats(B, self.layers[-1].in_features),
                                         dtype=torch.float32, device=self.device) if self.head_dgrad else None)
-        # fuse_head_wgrad (streaming head dgrad, <= 16 classes): the dgrad stream also
-        # produces the head's dW / db from the same pass over h_{L-1} (head.hip mode 3):
-        # one read of the 128 MB activation instead of two (dgrad stream + head_wgrad).
-        # Off by default: measured on MI355X at batch 16384 it is VALU-bound (2 x 16 fp32
-        # FMAs per element on the vector ALUs): 135 us vs 61 + 26 us for the dgrad stream
-        # plus the MFMA head_wgrad (1.740 vs 1.710 ms/step)
-        self.head_dw = (fuse_head_wgrad and self.head_dgrad and npad[-1] == 16 and self.head_dgrad_mode in (-1, 0, 3)
-                        and self.layers[-1].in_features % 4 == 0)
-        if self.head_dw:
-            self.head_dgrad_mode = 3
-            self._head_dw_ws = torch.empty(self.C.head_dw_splits(B) * 16 * self.layers[-1].in_features,
-                                           dtype=torch.float32, device=self.device)
         # [loss_sum, correct] -- one pair per 16-row workgroup of the head kernel
         nslots = (B + 15) // 16 if self.use_head else 1
         self.stats = torch.zeros(nslots, 2, dtype=torch.float32, device=dev)
@@ -268,28 +253,6 @@ class StaticMLPEngine:
                            for l in range(L)]
         self._act_code = [None] + [{"relu": self.C.ACT_RELU, "sigmoid": self.C.ACT_SIGMOID}.get(
             self.layers[l - 1].activation) for l in range(1, L)]
-        # pad_input: with both first-layer GEMMs on hipBLASLt, the input width is padded
-        # to a multiple of 64 with zero columns (784 -> 832): measured on MI355X at batch
-        # 16384 (scripts/bench_k_pad.py, profiles/first_layer_kpad_b16384_r1.jsonl) the
-        # fwd goes 108 -> 92 us and the wgrad 173 -> 155 us.  The forward reads a padded
-        # bf16 copy of W_0 refreshed right before it (6.4 MB), the wgrad writes a padded
-        # fp32 scratch whose real columns are copied into the flat gradient.  Off by
-        # default: in the step it measured slightly SLOWER (batch 16384: 1.863/1.861 vs
-        # 1.859/1.853 ms; batch 4096: 0.583 vs 0.571) -- the in-step wgrad kept its
-        # 128x128 hipBLASLt solution (194 us) and the two copies ate the forward's gain.
-        K0 = self.layers[0].in_features
-        self.in_pad = 0
-        if pad_input and not (K0 % 64 and self._lib_fwd[0] and self._lib_wgrad[0]):
-            raise ValueError("pad_input applies only when both first-layer GEMMs run on hipBLASLt "
-                             "(library_gemms=True) and the input width is not a multiple of 64")
-        if pad_input:
-            Kp = (K0 + 63) // 64 * 64
-            self.in_pad = Kp
-            self.xp = torch.zeros(B, Kp, dtype=bf, device=dev)
-            self.x = self.xp[:, :K0]
-            self.h[0] = self.xp
-            self.W0p = torch.zeros(self.W[0].shape[0], Kp, dtype=bf, device=dev)
-            self.dW0p = torch.zeros(self.W[0].shape[0], Kp, dtype=torch.float32, device=dev)
         self.bias_bf16 = [f.shadow_storage(l.bias) for l in self.layers]
         # relu_masks: a ReLU hidden layer's forward (four-wave kernel) also writes a bit
         # mask of its output (1 bit per activation, 1/16 of the bf16 bytes), and the dgrad
@@ -313,8 +276,8 @@ class StaticMLPEngine:
             M, N = self.dW[l].shape
             self._wgrad_ws.append(None)
             self._wgrad_slab.append(None)
-            if self.use_head and l == L - 1:   # (the fused head stream overwrites dW: no clearing)
-                self._wgrad_splitk.append(1 if self.head_dw else self.C.head_wgrad_splits(B, N))
+            if self.use_head and l == L - 1:
+                self._wgrad_splitk.append(self.C.head_wgrad_splits(B, N))
                 continue
             if self._lib_wgrad[l]:   # overwrites the gradient: no clearing, no split-K
                 self._wgrad_splitk.append(1)
@@ -323,35 +286,28 @@ class StaticMLPEngine:
             if B >= 4096 and t256 < 192:
                 # long-K wgrad whose 256-tile grid leaves CUs idle (the 4096 x 784 first
                 # layer: 64 tiles): the four-wave kernel splits the batch reduction over
-                # gridDim.y and combines the slices in the launch (deterministic, overwrites)
+                # gridDim.y into separate fp32 slabs and one chip-wide slab_sum adds them
+                # (measured on MI355X, 4096 x 784 x 16384: an in-launch combine, where the
+                # last-arriving workgroup of a tile re-reads every split's 256 KiB alone,
+                # cost ~90 of the kernel's 177 us)
                 sk = max(2, min(8, round(256 / t256)))
-                if wgrad_slabs:
-                    # the splits write separate fp32 slabs and one chip-wide slab_sum adds them:
-                    # measured on MI355X (4096 x 784 x 16384) the in-launch combine, where the
-                    # last-arriving workgroup of a tile re-reads every split's 256 KiB alone,
-                    # cost ~90 of the kernel's 177 us
-                    Nw = N
-                    if (l == 0 and bias_ones_column and not pad_input and L >= 2 and self.mask[1] is not None
-                            and self.layers[0].bias is not None and (N + 255) // 256 == (N + 8 + 255) // 256):
-                        # bias_ones_column: the input buffer carries a ones column after its K0
-                        # features, so this wgrad's product has one more column = sum over the
-                        # batch of dz_1 = the first layer's bias gradient, in the free part of the
-                        # last 256-wide tile; dgrad(1) then needs no bias-gradient sums (measured
-                        # on MI355X: the dgrad epilogue's column sums + atomics cost 13-30 us)
-                        # (rows padded to a multiple of 64 elements: every row starts on a 128-B line)
-                        Nw = N + 8
-                        self.xp_full = torch.zeros(B, (Nw + 63) // 64 * 64, dtype=bf, device=dev)
-                        self.xp = self.xp_full[:, :Nw]
-                        self.xp[:, N] = 1.0
-                        self.x = self.xp[:, :N]
-                        self.h[0] = self.x
-                        self._db0_from_wgrad = True
-                    self._wgrad_slab[l] = torch.empty(sk, M, Nw, dtype=torch.float32, device=self.device)
-                    self._wgrad_splitk.append(sk)
-                    continue
-                ne, nc = self.C.gemm_pp_ws(M, N, sk)
-                self._wgrad_ws[l] = (torch.empty(ne, dtype=torch.float32, device=self.device),
-                                     torch.zeros(nc, dtype=torch.int32, device=self.device), 256)
+                Nw = N
+                if (l == 0 and bias_ones_column and L >= 2 and self.mask[1] is not None
+                        and self.layers[0].bias is not None and (N + 255) // 256 == (N + 8 + 255) // 256):
+                    # bias_ones_column: the input buffer carries a ones column after its K0
+                    # features, so this wgrad's product has one more column = sum over the
+                    # batch of dz_1 = the first layer's bias gradient, in the free part of the
+                    # last 256-wide tile; dgrad(1) then needs no bias-gradient sums (measured
+                    # on MI355X: the dgrad epilogue's column sums + atomics cost 13-30 us)
+                    # (rows padded to a multiple of 64 elements: every row starts on a 128-B line)
+                    Nw = N + 8
+                    self.xp_full = torch.zeros(B, (Nw + 63) // 64 * 64, dtype=bf, device=dev)
+                    self.xp = self.xp_full[:, :Nw]
+                    self.xp[:, N] = 1.0
+                    self.x = self.xp[:, :N]
+                    self.h[0] = self.x
+                    self._db0_from_wgrad = True
+                self._wgrad_slab[l] = torch.empty(sk, M, Nw, dtype=torch.float32, device=self.device)
                 self._wgrad_splitk.append(sk)
                 continue
             tile, sk = self.C.gemm_plan(M, N, B, True)
@@ -382,55 +338,7 @@ class StaticMLPEngine:
         else:
             self._opt_zero, self._fill_zero = merged[:2], merged[2:]
 
-        # fuse_optimizer (single process): the optimizer update of every big weight
-        # runs IN its wgrad GEMM's epilogue (gemm_opt): the fp32 gradient never goes
-        # to HBM and the separate optimizer pass shrinks to the head + biases.  Needs
-        # dgrad(l) before wgrad(l) (dgrad reads the old W_l) and a wgrad that is not
-        # an atomic split-K.  Off by default: measured on MI355X (mlp3 4096, batch
-        # 4096) the step is SLOWER, 0.674 vs 0.616 ms -- all 256 output tiles finish
-        # together, so the 18 B/weight read-modify-write runs as an uncovered tail
-        # with fragment-shaped (16 rows x 64 B) accesses, instead of the separate
-        # optimizer's fully coalesced stream.
-        if fuse_optimizer is None:
-            fuse_optimizer = False
-        if overlap_optimizer:
-            fuse_optimizer = False  # the side-stream variant updates whole ranges itself
-        self._fused = [bool(fuse_optimizer) and not self.distributed and not (self.use_head and l == L - 1)
-                       and not self._lib_wgrad[l]
-                       and (self._wgrad_splitk[l] == 1 or (self._wgrad_ws[l] is not None
-                                                           and self._wgrad_ws[l][2] == 128)) for l in range(L)]
         self.rank = dist.get_rank(process_group) if self.distributed else 0
-        self.overlap_optimizer = overlap_optimizer
-        # early_optimizer (single process, L >= 2): the update of W_{L-1} .. W_1 runs on
-        # a side stream as soon as wgrad(1) has produced the last of their gradients,
-        # BESIDE dgrad(1) -- a 256-workgroup MFMA GEMM holding one workgroup per CU with
-        # ~100 VGPRs/lane, so the bandwidth-bound update's waves fit next to it.  dgrad(1)
-        # still reads the old bf16 W_1, so W_1's new shadow goes to a scratch copy that
-        # the main stream moves into place after the join; W_0 and the biases update
-        # on the main stream after the last wgrad, as before.
-        # Off by default: measured on MI355X (profiles/mlp3_early_optimizer_timeline_r1.txt)
-        # the co-resident update slows dgrad(1) from ~134 to ~210 us, more than the
-        # 60 us it hides (0.641 vs 0.599 ms/step).
-        if early_optimizer is None:
-            early_optimizer = False
-        self.early_optimizer = (bool(early_optimizer) and not self.distributed and L >= 2
-                                and not overlap_optimizer and not any(self._fused))
-        self._w1_span = None
-        if self.early_optimizer:
-            s1 = f.seg(self.layers[1].weight)
-            self._w1_span = (s1.offset, s1.offset + s1.storage_numel)
-            self._w0_begin = f.seg(self.layers[0].weight).offset
-            self._early_scratch = torch.empty(s1.storage_numel, dtype=torch.bfloat16, device=self.device)
-        # concurrent_wgrad (single process, L >= 2, plain schedule): wgrad(1) runs on a
-        # side stream BESIDE dgrad(1) -> act pass -> wgrad(0) (they share only reads of
-        # dz_2 / h_1), so the 784-wide wgrad(0), whose grid covers < 256 CUs, fills in
-        # next to the full-grid wgrad(1) instead of running alone.  Off by default:
-        # measured neutral on MI355X (batch 16384: 1.785/1.787 vs 1.789/1.782 ms/step;
-        # batch 4096: 0.559 vs 0.566) -- the two hipBLASLt GEMMs do not co-run usefully.
-        self.concurrent_wgrad = (bool(concurrent_wgrad) and not self.distributed and L >= 2
-                                 and not overlap_optimizer and not self.early_optimizer and not any(self._fused))
-        self.side = (torch.cuda.Stream(device=self.device)
-                     if (overlap_optimizer or self.early_optimizer or self.concurrent_wgrad) else None)
         self._pending_gather = {}
         self._master_whole = True
         if self.shard:
@@ -450,11 +358,10 @@ class StaticMLPEngine:
         L = len(self.layers)
         if self.use_head:   # last Linear + softmax-xent + argmax (+ the head's dgrad) in one launch
             if self.head_dgrad:
-                hw = dict(dw=self.dW[L - 1], db_head=self.db[L - 1], dw_ws=self._head_dw_ws) if self.head_dw else {}
                 self.C.head_fwd_xent(self.h[L - 1], self.W[L - 1], self.bias[L - 1], self.labels, self.h[L],
                                      self.dz[L], self.stats, self.num_classes, 1.0 / self.B, dh=self.dz[L - 1],
                                      dbias=self.db[L - 2], dgrad_epi=self._dgrad_epi[L - 1],
-                                     dbias_ws=self._head_db_ws, dgrad_mode=self.head_dgrad_mode, **hw)
+                                     dbias_ws=self._head_db_ws, dgrad_mode=self.head_dgrad_mode)
                 return
             self.C.head_fwd_xent(self.h[L - 1], self.W[L - 1], self.bias[L - 1], self.labels, self.h[L], self.dz[L],
                                  self.stats, self.num_classes, 1.0 / self.B)
@@ -466,15 +373,9 @@ class StaticMLPEngine:
     def _wgrad(self, l):
         sk = self._wgrad_splitk[l]
         if self.use_head and l == len(self.layers) - 1:   # also emits the head's bias gradient
-            if self.head_dw:   # already produced by the head's fused dgrad + wgrad stream
-                return
             self.C.head_wgrad(self.dz[l + 1], self.h[l], self.dW[l], self.db[l], sk)
             return
         if self._lib_wgrad[l]:   # plain GEMM, fp32 out: hipBLASLt straight into the flat grad buffer
-            if l == 0 and self.in_pad:
-                torch.mm(self.dz[1].t(), self.xp, out_dtype=torch.float32, out=self.dW0p)
-                self.dW[0].copy_(self.dW0p[:, : self.layers[0].in_features])
-                return
             torch.mm(self.dz[l + 1].t(), self.h[l], out_dtype=torch.float32, out=self.dW[l])
             return
         if self._wgrad_slab[l] is not None:   # split-K into slabs + one summing pass, overwrites
@@ -487,45 +388,11 @@ class StaticMLPEngine:
             return
         if self._wgrad_ws[l] is not None:   # in-launch split-K combine, overwrites the gradient
             ws, cnt, tile = self._wgrad_ws[l]
-            self.C.gemm(self.dz[l + 1], self.h[l], self.dW[l], False, False, tile=tile, splitk=sk, ws=ws, cnt=cnt,
-                        variant=32 if tile == 256 else 0)
+            self.C.gemm(self.dz[l + 1], self.h[l], self.dW[l], False, False, tile=tile, splitk=sk, ws=ws, cnt=cnt)
         elif sk > 1:   # accumulates into the grad the previous optimizer launch cleared
             self.C.gemm(self.dz[l + 1], self.h[l], self.dW[l], False, False, beta=1.0, tile=128, splitk=sk)
         else:
             self.C.gemm(self.dz[l + 1], self.h[l], self.dW[l], False, False)
-
-    def _wgrad_opt(self, l):
-        """wgrad of layer l with the optimizer update fused into the epilogue."""
-        f, o = self.flat, self.optim
-        w = self.layers[l].weight
-        seg = f.seg(w)
-        view = lambda t: f.storage_view(seg, t)  # noqa: E731
-        m = v = None
-        if o.name == "sgd":
-            m = view(self.mom) if self.mom is not None else None
-        else:
-            m, v = view(self.exp_avg), view(self.exp_avg_sq)
-        sk = self._wgrad_splitk[l]
-        ws, cnt, _ = self._wgrad_ws[l] if self._wgrad_ws[l] is not None else (None, None, None)
-        self.C.gemm_opt(self.dz[l + 1], self.h[l], view(f.master), False, False, o.name, m=m, v=v,
-                        shadow=view(f.shadow), hp=self.hp, grad_scale=self._grad_scale, momentum=o.momentum,
-                        dampening=o.dampening, weight_decay=o.weight_decay, nesterov=o.nesterov,
-                        beta1=o.betas[0], beta2=o.betas[1], eps=o.eps, tile=128 if ws is not None else 0,
-                        splitk=sk if ws is not None else 0, ws=ws, cnt=cnt)
-
-    def _unfused_ranges(self):
-        """Flat ranges the standalone optimizer launch still updates (unfused weights + biases)."""
-        f = self.flat
-        rs = [(f.seg(l.weight).offset, f.seg(l.weight).offset + f.seg(l.weight).storage_numel)
-              for i, l in enumerate(self.layers) if not self._fused[i]]
-        rs.append((self._bias_begin, f.numel))
-        merged = []
-        for b, e in sorted(rs):
-            if merged and b <= merged[-1][1]:
-                merged[-1] = (merged[-1][0], max(merged[-1][1], e))
-            else:
-                merged.append((b, e))
-        return merged
 
     def _dgrad(self, l):
         # dz_l(prev layer output) = (dz_{l+1} W_l) * act'(h_l), bias grad of layer l-1 fused
@@ -547,40 +414,10 @@ class StaticMLPEngine:
         self.C.gemm(self.dz[l + 1], self.W[l], self.dz[l], True, False, self._dgrad_epi[l], aux=self.h[l],
                     dbias=self.db[l - 1])
 
-    def _fork_opt(self, ranges):
-        self.side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(self.side):
-            for b, e in ranges:
-                if e > b:
-                    self._opt(b, e)
-
-    def _fork_wgrad(self, l):
-        self.side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(self.side):
-            self._wgrad(l)
-
-    def _join(self):
-        torch.cuda.current_stream().wait_stream(self.side)
-
     def _shard_range(self, i):
         b, e, _ = self.buckets[i]
         s = (e - b) // self.world
         return b + self.rank * s, b + (self.rank + 1) * s
-
-    def _early_opt(self):
-        """Side stream (see early_optimizer): update W_{L-1} .. W_1 beside dgrad(1)."""
-        s1b, s1e = self._w1_span
-        self.side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(self.side):
-            if s1b > 0:
-                self._opt(0, s1b)   # shadows no later kernel of this step reads
-            self._opt(s1b, s1e, shadow=self._early_scratch)
-
-    def _early_join(self):
-        s1b, s1e = self._w1_span
-        self._join()
-        self.flat.shadow[s1b:s1e].copy_(self._early_scratch)
-        self._opt(s1e, self.flat.numel)
 
     def _opt(self, b, e, grad=None, shadow=None):
         f, o, C = self.flat, self.optim, self.C
@@ -611,11 +448,6 @@ class StaticMLPEngine:
         pieces[0].append(self._loss)
         self._cut_buckets = []
         for l in reversed(range(L)):
-            if self._fused[l]:  # dgrad reads the old W_l, then the fused wgrad updates it
-                if l > 0:
-                    pieces[-1].append(lambda l=l: self._dgrad(l))
-                pieces[-1].append(lambda l=l: self._wgrad_opt(l))
-                continue
             wg = lambda l=l: self._wgrad(l)  # noqa: E731
             wg._ldnn_wgrad = l
             pieces[-1].append(wg)
@@ -633,37 +465,7 @@ class StaticMLPEngine:
             return f
 
         if not self.distributed:
-            if L >= 2 and self.overlap_optimizer:
-                # Once the last dgrad (layer 1) has run, every gradient except W_0's is
-                # final and no later kernel reads those weights: their optimizer update
-                # runs on a side stream beside the last wgrad (a 224-tile GEMM that
-                # leaves CUs and HBM bandwidth idle); W_0's update follows on the
-                # main stream.  Fork/join are stream-event edges inside the graph.
-                # Off by default: measured on MI355X the bandwidth-bound SGD slows the
-                # latency-bound wgrad from 68 to 119 us, a net loss (0.654 vs 0.624 ms).
-                w0 = self.flat.seg(self.layers[0].weight).offset
-                side = [(0, w0), (self._bias_begin, self.flat.numel)]
-                fns = []
-                for p in pieces:
-                    for fn in p:
-                        fns.append(fn)
-                fns.insert(len(fns) - 1, lambda: self._fork_opt(side))   # before wgrad(0)
-                fns += [lambda: self._opt(w0, self._bias_begin), self._join]
-            elif self.early_optimizer:
-                fns = [fn for p in pieces for fn in p]
-                i1 = next(i for i, fn in enumerate(fns) if getattr(fn, "_ldnn_wgrad", None) == 1)
-                fns.insert(i1 + 1, self._early_opt)   # fork right after wgrad(1)
-                fns.append(self._early_join)          # after wgrad(0)
-            elif any(self._fused):
-                fns = [fn for p in pieces for fn in p] + [lambda b=b, e=e: self._opt(b, e)
-                                                          for b, e in self._unfused_ranges()]
-            elif self.concurrent_wgrad:
-                fns = [fn for p in pieces for fn in p]
-                i1 = next(i for i, fn in enumerate(fns) if getattr(fn, "_ldnn_wgrad", None) == 1)
-                fns[i1] = lambda: self._fork_wgrad(1)
-                fns += [self._join, lambda: self._opt(0, self.flat.numel)]
-            else:
-                fns = [fn for p in pieces for fn in p] + [lambda: self._opt(0, self.flat.numel)]
+            fns = [fn for p in pieces for fn in p] + [lambda: self._opt(0, self.flat.numel)]
             self.segments = [_Segment(run(fns), self.use_graphs)]
             self.opt_segments = []
         elif self.shard:
@@ -720,9 +522,6 @@ class StaticMLPEngine:
         C = self.C
         if self._lib_fwd[l]:
             W = self.W[l]
-            if l == 0 and self.in_pad:   # padded copy of the current (possibly just all-gathered) W_0
-                self.W0p[:, : self.layers[0].in_features].copy_(W)
-                W = self.W0p
             if self.layers[l].activation == "relu":
                 torch._addmm_activation(self.bias_bf16[l], self.h[l], W.t(), out=self.h[l + 1])
             else:
@@ -741,6 +540,31 @@ class StaticMLPEngine:
     def load_batch(self, x: torch.Tensor, y: torch.Tensor):
         self.x.copy_(x.reshape(self.B, -1))
         self.labels.copy_(y)
+
+    def eager_step(self, x: torch.Tensor, y: torch.Tensor):
+        """One training step on a batch of ANOTHER size (the trailing partial batch of an
+        epoch, BAR/trainer.py:202-216 trains it): the MLP's autograd path on the same
+        flat parameters (ldnn native Linear / softmax-xent kernels; its CE adds
+        [loss_sum, #correct] into ``stats[0]``), then the engine's fused update.
+        Single-process engines only: per-step data parallelism needs the same
+        collectives on every rank, so the driver runs the same number of full steps
+        everywhere instead."""
+        if self.distributed:
+            raise RuntimeError("eager_step: a data-parallel engine steps full batches only")
+        from ..models.layers import CrossEntropyLoss
+
+        f = self.flat
+        f.grad.zero_()   # the engine's wgrads overwrite: their ranges hold the last step's values
+        f._stale.clear()
+        with torch.enable_grad():
+            self.model.train()
+            out = self.model(x.reshape(x.shape[0], -1).to(self.x.dtype))
+            loss = CrossEntropyLoss()(out, y, self.stats[0])
+            loss.backward()
+        if self.optim.name in ("adam", "adamw"):
+            self.C.bump_step(self.hp)
+        self._opt(0, f.numel)
+        return loss.detach()
 
     # ------------------------------------------------------------ collectives
     def _reduce_scatter(self, i):
@@ -857,10 +681,7 @@ class StaticMLPEngine:
             if self.use_head and l == L - 1:
                 d[f"fwd{l}"] = "ldnn head_fwd_xent (Linear + softmax-xent + argmax)"
                 d[f"wgrad{l}"] = "ldnn head_wgrad"
-                if self.head_dw:
-                    d[f"wgrad{l}"] = d[f"dgrad{l}"] = ("ldnn head_stream_dw (dgrad + dReLU + bias sums + the head's "
-                                                       "dW / db in one pass over h)")
-                elif self.head_dgrad:
+                if self.head_dgrad:
                     d[f"dgrad{l}"] = ("ldnn head_dgrad_stream (dReLU + bias-gradient sums)" if self.head_dgrad_mode in
                                       (-1, 0) else "ldnn head_fwd_xent fused dgrad")
                 continue

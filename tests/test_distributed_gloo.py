@@ -207,3 +207,58 @@ def test_schedule_divergence_is_detected():
     for r in range(world):
         assert "collective schedules diverged at after divergence" in res[r], res
         assert "rank 0: 3 ops" in res[r] and "rank 1: 2 ops" in res[r], res
+
+
+def _weighted_dp_worker(rank, world, port, q, w):
+    _init(rank, world, port)
+    import ldnn
+    from ldnn.models.mlp import mlp2
+    from ldnn.optim import SGD
+    from ldnn.parallel.comm import TorchComm
+    from ldnn.parallel.ddp import DataParallel
+
+    torch.manual_seed(11)
+    m = mlp2(64, 16, 10)
+    ldnn.prepare(m, "cpu")
+    p0 = [p.detach().clone() for p in m.parameters()]
+    dp = DataParallel(m, TorchComm(), bucket_cap_mb=0.002, local_weight=w)   # several buckets
+    assert len(dp.bucketer.buckets) > 1 and dp.bucketer.weighted
+    assert dp.flat.grad_scale == 1.0
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(4 * world, 64, generator=g)
+    y = torch.randint(0, 10, (4 * world,), generator=g)
+    # every rank's own gradient, computed locally on a private replica (the expected value)
+    own = []
+    for r in range(world):
+        ref = mlp2(64, 16, 10)
+        ref.load_state_dict(m.state_dict())
+        torch.nn.functional.cross_entropy(ref(x[4 * r:4 * r + 4]), y[4 * r:4 * r + 4]).backward()
+        own.append([p.grad.detach().clone() for p in ref.parameters()])
+    opt = SGD(m.parameters(), lr=0.5, momentum=0.0)
+    opt.zero_grad()
+    torch.nn.functional.cross_entropy(dp(x[4 * rank:4 * rank + 4]), y[4 * rank:4 * rank + 4]).backward()
+    dp.finish_gradient_sync()
+    got_g = [p.grad.detach().clone() for p in m.parameters()]
+    opt.step()
+    err_g, err_p = 0.0, 0.0
+    for k, p in enumerate(m.parameters()):
+        total = sum(o[k] for o in own)
+        exp = w * own[rank][k] + (1 - w) * (total - own[rank][k]) / (world - 1)   # BAR/communication.py:4-10
+        err_g = max(err_g, ((got_g[k] - exp).abs().max() / exp.abs().max().clamp_min(1e-12)).item())
+        err_p = max(err_p, ((p.detach() - (p0[k] - 0.5 * exp)).abs().max()).item())
+    q.put((rank, err_g, err_p))
+    dist.destroy_process_group()
+
+
+def test_per_step_weighted_allreduce_three_ranks():
+    """--sync_every step --aggregation_type weighted --local_weight 0.8 (cli.py ->
+    DataParallel(local_weight=0.8)): every rank's consumed gradient is the reference's
+    w g_own + (1-w)(sum - g_own)/(N-1), and the optimizer applies it at scale 1."""
+    world, port = 3, _port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    mp.spawn(_weighted_dp_worker, args=(world, port, q, 0.8), nprocs=world, join=True)
+    res = sorted(q.get(timeout=30) for _ in range(world))
+    for r, err_g, err_p in res:
+        assert err_g < 1e-5, res
+        assert err_p < 1e-6, res

@@ -37,6 +37,11 @@ class FakeEngine:
         self.stats[self.steps % 3, 0] += float(self.x.float().mean()) * self.B
         self.stats[0, 1] += float((self.y == 0).sum())
 
+    def eager_step(self, x, y):   # the partial batch: same stats contract
+        self.eager = getattr(self, "eager", 0) + 1
+        self.stats[0, 0] += float(x.float().mean()) * y.numel()
+        self.stats[0, 1] += float((y == 0).sum())
+
     def sync(self):
         self.synced += 1
 
@@ -62,17 +67,25 @@ def _loader(B, n_full, tail):
     return L(batches)
 
 
-def test_engine_local_epoch_per_batch_losses_and_partial_skip():
+@pytest.mark.filterwarnings("ignore:Detected call of `lr_scheduler.step\(\)`")
+def test_engine_local_epoch_per_batch_losses_and_partial_batch_trained():
+    """Every batch is trained, the trailing partial one too (BAR/trainer.py:202-216):
+    it runs the engine's eager_step; per-batch losses are per-batch means."""
     B = 8
     m = EA.EngineModule(_Model(), FakeEngine(B))
     opt = torch.optim.SGD(m.module.parameters(), lr=0.25)
     sch = torch.optim.lr_scheduler.StepLR(opt, 1, gamma=0.5)
     loss, acc, bl = EA.engine_local_epoch(m, _loader(B, 4, 3), opt, sch)
     assert m.engine.lr == 0.25 and opt.param_groups[0]["lr"] == 0.125   # synced before, stepped after
-    assert bl == pytest.approx([1.0, 2.0, 3.0, 4.0]) and loss == pytest.approx(2.5)
-    assert acc == pytest.approx(50.0)
-    assert EA.engine_local_epoch.last_skipped == 3 and EA.engine_local_epoch.last_samples == 4 * B
-    assert m.engine.steps == 4
+    assert bl == pytest.approx([1.0, 2.0, 3.0, 4.0, 99.0]) and loss == pytest.approx(109.0 / 5)
+    assert acc == pytest.approx(100.0 * (4 * 4 + 3) / (4 * B + 3))
+    assert EA.engine_local_epoch.last_skipped == 0 and EA.engine_local_epoch.last_samples == 4 * B + 3
+    assert m.engine.steps == 4 and m.engine.eager == 1
+    # a data-parallel engine steps full batches only (same collectives on every rank)
+    md = EA.EngineModule(_Model(), FakeEngine(B))
+    md.engine.distributed = True
+    _, _, bld = EA.engine_local_epoch(md, _loader(B, 4, 3), opt, None)
+    assert bld == pytest.approx([1.0, 2.0, 3.0, 4.0]) and EA.engine_local_epoch.last_skipped == 3
     # max_steps caps the steps (per-step DP keeps ranks aligned)
     m2 = EA.EngineModule(_Model(), FakeEngine(B))
     _, _, bl2 = EA.engine_local_epoch(m2, _loader(B, 4, 0), opt, None, max_steps=2)

@@ -1,6 +1,7 @@
-"""Graph-captured data-parallel steps (train/graphed.py GraphedDPStep): the bucket
-collectives run on a side-stream branch of the step graph while the backward
-still runs (in_graph), or between a backward graph and an optimizer graph (after)."""
+"""Graph-captured data-parallel steps (train/graphed.py GraphedDPStep): the backward is
+a chain of graphs cut at the bucket-ready points with each bucket's collective issued
+between two links of the chain (segmented), or one backward graph followed by every
+collective (after); then the optimizer graph."""
 import os
 import socket
 import subprocess
@@ -37,11 +38,11 @@ def _close_updates(pa, pb, p0, rel=2e-2):
         assert (da - db).norm().item() <= rel * db.norm().item() + 1e-6, ((da - db).norm().item(), db.norm().item())
 
 
-@pytest.mark.parametrize("mode", ["in_graph", "after"])
+@pytest.mark.parametrize("mode", ["segmented", "after"])
 @pytest.mark.parametrize("comm_dtype", [None, torch.bfloat16])
 def test_side_stream_collective_waits_for_its_bucket(comm_dtype, mode):
     """Ordering check without a second rank: the 'collective' doubles each bucket where
-    the all-reduce would run (a side-stream branch of the graph for in_graph).  Only if
+    the all-reduce would run (between two graphs of the chain for segmented).  Only if
     it runs after the bucket's gradients were written and before the optimizer is the
     result == plain SGD at twice the lr."""
     shape = (512, 1, 28, 28)
@@ -61,6 +62,9 @@ def test_side_stream_collective_waits_for_its_bucket(comm_dtype, mode):
         m._ldnn_flat.grad.mul_(k)
         o.step()
     gd = GraphedDPStep(dp, crit, o1, xs[0], ys[0], mode=mode, comm_fn=lambda i, buf: buf.mul_(2.0))
+    if mode == "segmented":   # one cut per bucket (+ the trailing piece of the backward)
+        assert gd.n_segments >= len(dp.bucketer.buckets)
+        assert sorted(i for iss in gd.issue for i in iss) == list(range(len(dp.bucketer.buckets)))
     gs = GraphedStep(m2, crit, o2, xs[0], ys[0], warmup=0)
     for i in range(1, 4):
         gd(xs[i], ys[i])
@@ -71,8 +75,8 @@ def test_side_stream_collective_waits_for_its_bucket(comm_dtype, mode):
 
 def test_rccl_world1_overlap_path(tmp_path):
     """The real RCCL path (TorchComm on a 1-rank communicator: the bucket all-reduces
-    captured into the step graph on a side-stream branch) trains like the
-    single-process graphed step."""
+    issued between the links of the backward chain) trains like the single-process
+    graphed step, and records the same collective schedule as the eager fallback."""
     import torch.distributed as dist
 
     from ldnn.parallel.comm import TorchComm
@@ -96,13 +100,21 @@ def test_rccl_world1_overlap_path(tmp_path):
             crit(m(xs[0]), ys[0]).backward()
             o.step()
         gd = GraphedDPStep(dp, crit, o1, xs[0], ys[0])
-        assert gd.mode == "in_graph"
+        assert gd.mode == "segmented"
         gs = GraphedStep(m2, crit, o2, xs[0], ys[0], warmup=0)
-        for i in range(1, 5):
+        n0 = comm.schedule_digest()[0]
+        gd(xs[1], ys[1])
+        gs(xs[1], ys[1])
+        n_graphed = comm.schedule_digest()[0] - n0
+        assert n_graphed == len(dp.bucketer.buckets)
+        for i in range(2, 5):
             gd(xs[i], ys[i])
             gs(xs[i], ys[i])
-        # the odd-shaped last batch of an epoch falls back to the eager bucketed step
+        # the odd-shaped last batch of an epoch falls back to the eager bucketed step,
+        # which issues the same collectives (count) as a replay
+        n1 = comm.schedule_digest()[0]
         gd(xs[0][:100], ys[0][:100])
+        assert comm.schedule_digest()[0] - n1 == n_graphed
         gs(xs[0][:100], ys[0][:100])
         torch.cuda.synchronize()
         _close_updates(list(m1.parameters()), list(m2.parameters()), p0)
@@ -122,3 +134,40 @@ def test_graphed_dp_two_ranks_gloo_equals_big_batch():
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     assert "GRAPHED_DP_OK" in r.stdout, r.stdout[-3000:]
+
+
+def test_segmented_weighted_allreduce_world1_identity():
+    """--aggregation_type weighted on a world of one keeps the own gradient (Q4)."""
+    shape = (128, 1, 28, 28)
+    m1, m2 = _models("lenet5", 2)
+    crit = CrossEntropyLoss()
+    dp = DataParallel(m1, LocalComm(), bucket_cap_mb=0.05, broadcast_init=False, local_weight=0.8)
+    assert not dp.bucketer.weighted
+    o1, o2 = SGD(m1.parameters(), lr=0.02, momentum=0.9), SGD(m2.parameters(), lr=0.02, momentum=0.9)
+    g = torch.Generator(device="cuda").manual_seed(3)
+    xs = [torch.randn(*shape, device="cuda", generator=g).bfloat16() for _ in range(3)]
+    ys = [torch.randint(0, 10, (shape[0],), device="cuda", generator=g) for _ in range(3)]
+    p0 = [p.detach().clone() for p in m2.parameters()]
+    for m, o in ((m1, o1), (m2, o2)):
+        o.zero_grad()
+        crit(m(xs[0]), ys[0]).backward()
+        o.step()
+    gd = GraphedDPStep(dp, crit, o1, xs[0], ys[0], mode="segmented", comm_fn=lambda i, buf: None)
+    gs = GraphedStep(m2, crit, o2, xs[0], ys[0], warmup=0)
+    for i in range(1, 3):
+        gd(xs[i], ys[i])
+        gs(xs[i], ys[i])
+    torch.cuda.synchronize()
+    _close_updates(list(m1.parameters()), list(m2.parameters()), p0)
+
+
+def test_segmented_comm_stream_standin_overlaps():
+    """A bandwidth-bound stand-in for each bucket's collective on its own HIP stream
+    (parallel/overlap_probe.py) runs beside the remaining backward graphs: the step
+    with the stand-in costs less than the step without it plus the stand-in's
+    standalone time (no overlap at all would make them equal)."""
+    from ldnn.parallel.overlap_probe import measure_overlap
+
+    r = measure_overlap("lenet5", batch=1024, bucket_mb=0.05, reps=4, steps=20)
+    assert r["segments"] >= 3
+    assert r["with_standin_ms"] < r["single_ms"] + r["standin_alone_ms"], r

@@ -150,32 +150,6 @@ def test_wgrad_inlaunch_splitk_combine_matches_unsplit():
     torch.testing.assert_close(e1.flat.master, e2.flat.master, rtol=1e-4, atol=1e-5)
 
 
-@pytest.mark.parametrize("opt", ["sgd", "adam"])
-def test_fused_optimizer_epilogue_matches_separate_launch(opt):
-    """Single-GPU engine with the optimizer fused into the wgrad epilogues (256-tile
-    4096 x 4096 layer, 128-tile first layer) == the engine with one separate fused
-    optimizer launch over the flat buffers."""
-    torch.manual_seed(0)
-    B = 512
-    m1, m2 = mlp3(784, 4096, 10), mlp3(784, 4096, 10)
-    m2.load_state_dict(m1.state_dict())
-    cfg = OptimConfig(opt, lr=0.05 if opt == "sgd" else 1e-3, momentum=0.9, weight_decay=1e-4)
-    e1 = StaticMLPEngine(m1, B, cfg, use_graphs=True, fuse_optimizer=True, library_gemms=False)
-    e2 = StaticMLPEngine(m2, B, cfg, use_graphs=True, fuse_optimizer=False, library_gemms=False)
-    assert any(e1._fused) and not any(e2._fused)
-    g = torch.Generator(device="cuda").manual_seed(9)
-    for i in range(5):
-        x = torch.randn(B, 784, device="cuda", generator=g).bfloat16()
-        y = torch.randint(0, 10, (B,), device="cuda", generator=g)
-        for e in (e1, e2):
-            e.load_batch(x, y)
-            e.step()
-    torch.cuda.synchronize()
-    # same arithmetic; only FMA contraction differs between the two kernels
-    torch.testing.assert_close(e1.flat.master, e2.flat.master, rtol=1e-4, atol=2e-5)
-    assert torch.equal(e1.flat.shadow, e1.flat.master.bfloat16())
-
-
 @pytest.mark.parametrize("B", [1024, 4096])
 def test_library_gemm_engine_matches_native_engine(B):
     """hipBLASLt plain GEMMs (fp32 wgrads, bias+ReLU forwards,
@@ -226,34 +200,6 @@ def test_fused_head_dgrad_engine_matches_separate_dgrad():
     torch.testing.assert_close(e1.flat.master, e2.flat.master, rtol=1e-3, atol=1e-4)
 
 
-@pytest.mark.parametrize("opt,dims", [("sgd", (784, 1024, 10)), ("adam", (784, 1024, 10)),
-                                      ("sgd", (784, 512, 512, 10))])
-def test_early_optimizer_side_stream_matches_serial(opt, dims):
-    """early_optimizer=True (W_{L-1}..W_1 updated on a side stream beside dgrad(1),
-    W_1's new shadow parked in a scratch copy) trains like the serial step, and the
-    bf16 shadow is the rounded master after every step."""
-    from ldnn.models.mlp import MLP
-    torch.manual_seed(0)
-    B = 512
-    mk = lambda: MLP(dims[0], dims[1:-1], dims[-1])  # noqa: E731
-    m1, m2 = mk(), mk()
-    m2.load_state_dict(m1.state_dict())
-    cfg = OptimConfig(opt, lr=0.05 if opt == "sgd" else 1e-3, momentum=0.9)
-    e1 = StaticMLPEngine(m1, B, cfg, use_graphs=True, early_optimizer=True)
-    e2 = StaticMLPEngine(m2, B, cfg, use_graphs=True, early_optimizer=False)
-    assert e1.early_optimizer and not e2.early_optimizer
-    g = torch.Generator(device="cuda").manual_seed(7)
-    for i in range(5):
-        x = torch.randn(B, dims[0], device="cuda", generator=g).bfloat16()
-        y = torch.randint(0, dims[-1], (B,), device="cuda", generator=g)
-        for e in (e1, e2):
-            e.load_batch(x, y)
-            e.step()
-    torch.cuda.synchronize()
-    torch.testing.assert_close(e1.flat.master, e2.flat.master, rtol=1e-3, atol=1e-4)
-    assert torch.equal(e1.flat.shadow, e1.flat.master.bfloat16())
-
-
 @pytest.mark.parametrize("act", ["relu", "sigmoid"])
 def test_library_dgrad_matches_fused_dgrad(act):
     """hipBLASLt dgrad + fused act'/bias-grad pass (library_dgrad) == ldnn's dgrad with
@@ -281,73 +227,6 @@ def test_library_dgrad_matches_fused_dgrad(act):
     for a, b in zip(l1, l2):
         assert abs(a - b) < 1e-2 * max(1.0, abs(b)), (l1, l2)
     torch.testing.assert_close(e1.flat.master, e2.flat.master, rtol=2e-2, atol=2e-3)
-
-
-@pytest.mark.parametrize("graphs", [False, True])
-def test_concurrent_wgrad_side_stream_matches_serial(graphs):
-    """wgrad(1) on a side stream beside dgrad(1) + wgrad(0) == the serial schedule."""
-    torch.manual_seed(0)
-    B = 2048
-    m1, m2 = mlp3(784, 1024, 10), mlp3(784, 1024, 10)
-    m2.load_state_dict(m1.state_dict())
-    cfg = OptimConfig("sgd", lr=0.05, momentum=0.9)
-    e1 = StaticMLPEngine(m1, B, cfg, use_graphs=graphs, concurrent_wgrad=True)
-    e2 = StaticMLPEngine(m2, B, cfg, use_graphs=graphs, concurrent_wgrad=False)
-    assert e1.concurrent_wgrad and not e2.concurrent_wgrad
-    g = torch.Generator(device="cuda").manual_seed(3)
-    l1, l2 = [], []
-    for i in range(6):
-        x = torch.randn(B, 784, device="cuda", generator=g).bfloat16()
-        y = torch.randint(0, 10, (B,), device="cuda", generator=g)
-        for e, ls in ((e1, l1), (e2, l2)):
-            e.reset_stats()
-            e.load_batch(x, y)
-            e.step()
-            ls.append(e.read_stats(B)[0])
-    torch.cuda.synchronize()
-    for a, b in zip(l1, l2):
-        assert abs(a - b) < 1e-2 * max(1.0, abs(b)), (l1, l2)
-    torch.testing.assert_close(e1.flat.master, e2.flat.master, rtol=2e-2, atol=2e-3)
-
-
-def test_padded_input_matches_unpadded():
-    """784 -> 832 zero-padded first layer (pad_input, hipBLASLt path) == the unpadded
-    GEMMs: after ONE step the first layer's activations and weight gradient match at
-    tight tolerances (a wrong dW_0 column copy or a stale padded W_0 fails here), then
-    six plain-SGD steps keep the masters together."""
-    torch.manual_seed(0)
-    B = 1024
-    m1, m2 = mlp3(784, 1024, 10), mlp3(784, 1024, 10)
-    m2.load_state_dict(m1.state_dict())
-    cfg = OptimConfig("sgd", lr=0.05, momentum=0.0)
-    e1 = StaticMLPEngine(m1, B, cfg, use_graphs=True, pad_input=True, library_gemms=True)
-    e2 = StaticMLPEngine(m2, B, cfg, use_graphs=True, pad_input=False, library_gemms=True)
-    assert e1.in_pad == 832 and e2.in_pad == 0
-    g = torch.Generator(device="cuda").manual_seed(9)
-    l1, l2 = [], []
-    for i in range(6):
-        x = torch.randn(B, 784, device="cuda", generator=g).bfloat16()
-        y = torch.randint(0, 10, (B,), device="cuda", generator=g)
-        for e, ls in ((e1, l1), (e2, l2)):
-            e.reset_stats()
-            e.load_batch(x, y)
-            e.step()
-            ls.append(e.read_stats(B)[0])
-        if i == 0:
-            torch.cuda.synchronize()
-            torch.testing.assert_close(e1.h[1].float(), e2.h[1].float(), rtol=1e-2, atol=1e-2)
-            scale = e2.dW[0].abs().max().item()
-            assert (e1.dW[0] - e2.dW[0]).abs().max().item() <= 1e-3 * scale + 1e-6
-    torch.cuda.synchronize()
-    for a, b in zip(l1, l2):
-        assert abs(a - b) < 2e-3 * max(1.0, abs(b)), (l1, l2)
-    torch.testing.assert_close(e1.flat.master, e2.flat.master, rtol=1e-3, atol=1e-4)
-    assert e1.xp[:, 784:].abs().max().item() == 0 and e1.W0p[:, 784:].abs().max().item() == 0
-
-
-def test_pad_input_rejected_without_library_gemms():
-    with pytest.raises(ValueError):
-        StaticMLPEngine(mlp3(784, 256, 10), 256, OptimConfig("sgd", lr=0.05), pad_input=True, library_gemms=False)
 
 
 def test_wgrad_q_splitk_matches_library_gemms():
@@ -386,21 +265,20 @@ def test_wgrad_q_splitk_matches_library_gemms():
 
 @pytest.mark.parametrize("opt", ["sgd", "adam"])
 def test_relu_masks_and_wgrad_slabs_match_plain_engine(opt):
-    """The engine with ReLU bit masks (fwd writes, dgrad reads), the split-slab wgrad, the
-    transposed-W dgrad and the first-layer bias gradient from the wgrad's ones column
-    equals the engine reading the bf16 activations, k-strided W, in-launch split-K combine
-    and dgrad-epilogue bias sums."""
+    """The engine with ReLU bit masks (fwd writes, dgrad reads), the transposed-W dgrad
+    and the first-layer bias gradient from the wgrad's ones column equals the engine
+    reading the bf16 activations, k-strided W and dgrad-epilogue bias sums."""
     torch.manual_seed(0)
     B = 4096
     m1, m2 = mlp3(784, 1024, 10), mlp3(784, 1024, 10)
     m2.load_state_dict(m1.state_dict())
     cfg = OptimConfig(opt, lr=0.05 if opt == "sgd" else 1e-3, momentum=0.9)
     e1 = StaticMLPEngine(m1, B, cfg, use_graphs=True)
-    e2 = StaticMLPEngine(m2, B, cfg, use_graphs=True, relu_masks=False, wgrad_slabs=False, transposed_dgrad=False,
+    e2 = StaticMLPEngine(m2, B, cfg, use_graphs=True, relu_masks=False, transposed_dgrad=False,
                          bias_ones_column=False)
     assert e1.mask[1] is not None and e1._wgrad_slab[0] is not None and e1.Wt[1] is not None
     assert e1._db0_from_wgrad and e1.xp.shape[1] == 792 and not e2._db0_from_wgrad
-    assert e2.mask[1] is None and e2._wgrad_slab[0] is None
+    assert e2.mask[1] is None and e2.Wt[1] is None
     g = torch.Generator(device="cuda").manual_seed(8)
     for _ in range(5):
         x = torch.randn(B, 784, device="cuda", generator=g).bfloat16()
@@ -417,30 +295,35 @@ def test_relu_masks_and_wgrad_slabs_match_plain_engine(opt):
         torch.testing.assert_close(p.detach(), q.detach(), rtol=1e-4, atol=atol)
 
 
-@pytest.mark.parametrize("B", [4096, 1000])
-def test_fused_head_stream_dw_matches_separate_head_wgrad(B):
-    """Head mode 3 (one pass over h: dgrad + dReLU + bias sums + the head's dW / db) equals
-    the separate dgrad stream + head_wgrad kernels (B = 1000: a partial row slice)."""
+
+
+@pytest.mark.parametrize("opt", ["sgd", "adam"])
+def test_eager_partial_batch_step_matches_reference(opt):
+    """The trailing partial batch (StaticMLPEngine.eager_step: autograd on the engine's
+    flat parameters + the fused update) == an fp32 torch step on that batch, and the
+    next full engine step still matches (its accumulating gradients were left clean)."""
     torch.manual_seed(0)
-    m1, m2 = mlp3(784, 1024, 10), mlp3(784, 1024, 10)
-    m2.load_state_dict(m1.state_dict())
-    cfg = OptimConfig("sgd", lr=0.05, momentum=0.9)
-    e1 = StaticMLPEngine(m1, B, cfg, use_graphs=True, fuse_head_wgrad=True)
-    e2 = StaticMLPEngine(m2, B, cfg, use_graphs=True, fuse_head_wgrad=False)
-    assert e1.head_dw and e1.head_dgrad_mode == 3 and not e2.head_dw
-    g = torch.Generator(device="cuda").manual_seed(3)
-    x = torch.randn(B, 784, device="cuda", generator=g).bfloat16()
-    y = torch.randint(0, 10, (B,), device="cuda", generator=g)
-    for e in (e1, e2):
-        e.load_batch(x, y)
-        e._forward(train=True)
-        e._loss()
-        if not e.head_dw:
-            e._wgrad(2)
+    B, b = 512, 200
+    m = mlp3(784, 256, 10)
+    ref = mlp3(784, 256, 10)
+    ref.load_state_dict(m.state_dict())
+    ref = ref.cuda().float()
+    cfg = OptimConfig(opt, lr=0.05 if opt == "sgd" else 1e-3, momentum=0.9)
+    e = StaticMLPEngine(m, B, cfg, use_graphs=True)
+    ropt = (torch.optim.SGD(ref.parameters(), lr=0.05, momentum=0.9) if opt == "sgd" else
+            torch.optim.Adam(ref.parameters(), lr=1e-3))
+    g = torch.Generator(device="cuda").manual_seed(4)
+    for n in (B, b, B, B, b):
+        x = torch.randn(n, 784, device="cuda", generator=g).bfloat16()
+        y = torch.randint(0, 10, (n,), device="cuda", generator=g)
+        if n == B:
+            e.load_batch(x, y)
+            e.step()
+        else:
+            e.eager_step(x, y)
+        ropt.zero_grad()
+        torch.nn.functional.cross_entropy(ref(x.float()), y).backward()
+        ropt.step()
     torch.cuda.synchronize()
-    torch.testing.assert_close(e1.dz[2], e2.dz[2], rtol=0, atol=0)
-    torch.testing.assert_close(e1.dW[2], e2.dW[2], rtol=1e-4, atol=1e-6)
-    torch.testing.assert_close(e1.db[2], e2.db[2], rtol=1e-4, atol=1e-6)
-    torch.testing.assert_close(e1.db[1], e2.db[1], rtol=1e-4, atol=1e-5)
-    ref = e2.dz[3].float().t() @ e2.h[2].float()
-    torch.testing.assert_close(e1.dW[2][:10], ref[:10], rtol=1e-3, atol=1e-5)
+    for p, q in zip(m.parameters(), ref.parameters()):
+        torch.testing.assert_close(p.detach().float(), q.detach(), rtol=5e-2, atol=5e-3 if opt == "sgd" else 2e-3)
