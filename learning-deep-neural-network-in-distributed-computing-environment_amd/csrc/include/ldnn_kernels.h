@@ -244,6 +244,8 @@ hipError_t softmax_xent(const uint16_t* logits, const int64_t* labels, uint16_t*
                         const XentFin* fin = nullptr);
 // out[i] = src[i] * (*scale) over n bf16 (the loss backward's grad_output, read on the device)
 hipError_t scale_bf16_dev(const uint16_t* src, const float* scale, uint16_t* out, int64_t n, hipStream_t s);
+// overlap-probe communication stand-in: `reps` copies of src on `blocks` workgroups
+hipError_t standin_copy(const float* src, float* dst, int64_t n, int blocks, int reps, hipStream_t s);
 
 // ---- fused optimizers over flat fp32 buffers -------------------------------
 // hp (device fp32): [0]=lr [1]=step (already incremented for Adam) ; grad_scale multiplies g

@@ -434,4 +434,25 @@ hipError_t synth_labels(int64_t* y, int64_t n, int classes, uint64_t seed, hipSt
   return hipGetLastError();
 }
 
+// Communication stand-in for overlap probes (parallel/overlap_probe.py): a copy of a
+// gradient bucket on a FEW workgroups, repeated `reps` times -- the footprint of an
+// RCCL ring all-reduce (a handful of channels, each one workgroup, link-paced),
+// not of a chip-wide HBM copy that would take every CU from the backward.
+__global__ __launch_bounds__(kBlock) void standin_copy_kernel(const floatx4* __restrict__ src,
+                                                              floatx4* __restrict__ dst, int64_t n4, int reps) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int r = 0; r < reps; ++r) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) dst[i] = src[i];
+    __syncthreads();
+  }
+}
+
+hipError_t standin_copy(const float* src, float* dst, int64_t n, int blocks, int reps, hipStream_t s) {
+  if (n <= 0 || reps <= 0) return hipSuccess;
+  if (n % 4 != 0 || blocks < 1) return hipErrorInvalidValue;
+  standin_copy_kernel<<<blocks, kBlock, 0, s>>>(reinterpret_cast<const floatx4*>(src), reinterpret_cast<floatx4*>(dst),
+                                                n / 4, reps);
+  return hipGetLastError();
+}
+
 }  // namespace ldnn

@@ -123,6 +123,7 @@ class GradBucketer:
     def prepare(self):
         self._pending = [len(b["params"]) for b in self.buckets]
         self._launched = [False] * len(self.buckets)
+        self._next = 0
         self._seen: set = set()
         self.works = []
         self.active = True
@@ -140,15 +141,19 @@ class GradBucketer:
         if i is None:
             return
         self._pending[i] -= 1
-        if self._pending[i] == 0 and not self._launched[i]:
-            self._launch(i)
+        # collectives go out strictly in bucket order (every rank, every path -- the
+        # graph chain of GraphedDPStep too): a bucket that completes early waits for
+        # the ones before it, so no two ranks can pair different buckets
+        while self._next < len(self.buckets) and self._pending[self._next] == 0:
+            self._launch(self._next)
+            self._next += 1
 
     def finish(self):
         if not self.active:
             return
-        for i in range(len(self.buckets)):  # params that got no gradient this step
-            if not self._launched[i]:
-                self._launch(i)
+        for i in range(self._next, len(self.buckets)):  # params that got no gradient this step
+            self._launch(i)
+        self._next = len(self.buckets)
         for w, i in self.works:
             if w is not None:
                 w.wait()

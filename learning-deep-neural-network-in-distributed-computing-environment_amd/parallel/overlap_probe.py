@@ -4,11 +4,12 @@ On one GPU there is no second rank to all-reduce with, so the bucket collectives
 are replaced by a STAND-IN with the same stream behaviour as RCCL's: issued from
 the host between two graphs of the backward chain, on its own HIP stream that
 waits for the compute stream, joined (stream wait, no host sync) before the
-optimizer graph.  The stand-in is bandwidth-bound work sized like the bucket
-(``reps`` HBM copies of it), roughly the xGMI time of a ring all-reduce of that
-bucket on 8 x MI355X.  If the chain overlaps communication with the backward, the
-step with the stand-in costs much less than the step without it plus the
-stand-in's standalone time.
+optimizer graph.  The stand-in has RCCL's footprint: ``reps`` copies of the bucket
+on ``blocks`` workgroups (an RCCL ring all-reduce runs one workgroup per channel,
+a few dozen at most, paced by the xGMI links -- not a chip-wide HBM copy), sized
+so its standalone time is of the order of that bucket's all-reduce on 8 x MI355X.
+If the chain overlaps communication with the backward, the step with the stand-in
+costs much less than the step without it plus the stand-in's standalone time.
 
     python scripts/overlap_probe.py --model resnet18 --batch 64   (prints one JSON line)
 """
@@ -30,11 +31,15 @@ class _Join:
 
 
 class StandInComm:
-    """``comm_fn`` for GraphedDPStep: ``reps`` copies of bucket i on a side stream."""
+    """``comm_fn`` for GraphedDPStep: ``reps`` copies of bucket i on ``blocks``
+    workgroups (native standin_copy kernel), on a side stream."""
 
-    def __init__(self, device, reps: int = 4):
+    def __init__(self, device, reps: int = 4, blocks: int = 16):
+        from ..ops import _ext
+
+        self.C = _ext.C()
         self.side = torch.cuda.Stream(device=device)
-        self.reps = int(reps)
+        self.reps, self.blocks = int(reps), int(blocks)
         self.scratch: dict = {}
 
     def __call__(self, i, buf):
@@ -43,8 +48,7 @@ class StandInComm:
             sc = self.scratch.get(i)
             if sc is None:
                 sc = self.scratch[i] = torch.empty_like(buf)
-            for _ in range(self.reps):
-                sc.copy_(buf)
+            self.C.standin_copy(buf, sc, self.blocks, self.reps)
         return _Join(self.side)
 
 
@@ -58,7 +62,7 @@ def _timed(fn, steps):
 
 
 def measure_overlap(model_name: str, batch: int, bucket_mb: float = 32.0, reps: int = 4, steps: int = 20,
-                    rounds: int = 3) -> dict:
+                    rounds: int = 3, blocks: int = 16) -> dict:
     import ldnn
     from ldnn.data.datasets import SHAPES
     from ldnn.models import CrossEntropyLoss, build_model, dataset_for, xavier_init
@@ -74,7 +78,7 @@ def measure_overlap(model_name: str, batch: int, bucket_mb: float = 32.0, reps: 
     x = torch.randn(batch, *shape, device=dev, generator=g).bfloat16()
     y = torch.randint(0, nc, (batch,), device=dev, generator=g)
     crit = CrossEntropyLoss()
-    standin = StandInComm(dev, reps)
+    standin = StandInComm(dev, reps, blocks)
     steps_fn = {}
     for name, fn in (("single", lambda i, buf: None), ("with_standin", standin)):
         torch.manual_seed(0)
@@ -108,7 +112,7 @@ def measure_overlap(model_name: str, batch: int, bucket_mb: float = 32.0, reps: 
     hidden = best["single_ms"] + best["standin_alone_ms"] - best["with_standin_ms"]
     return {"model": model_name, "batch": batch, "bucket_mb": bucket_mb, "buckets": len(bufs),
             "bucket_mb_each": [round(b.numel() * b.element_size() / 2**20, 2) for b in bufs],
-            "segments": gd.n_segments, "standin_reps": reps, **{k: round(v, 4) for k, v in best.items()},
+            "segments": gd.n_segments, "standin_reps": reps, "standin_blocks": blocks, **{k: round(v, 4) for k, v in best.items()},
             "hidden_ms": round(hidden, 4),
             "hidden_fraction": round(hidden / max(best["standin_alone_ms"], 1e-9), 3)}
 
@@ -120,8 +124,9 @@ def main():
     ap.add_argument("--bucket-mb", type=float, default=32.0)
     ap.add_argument("--reps", type=int, default=4)
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--blocks", type=int, default=16)
     a = ap.parse_args()
-    print(json.dumps(measure_overlap(a.model, a.batch, a.bucket_mb, a.reps, a.steps)), flush=True)
+    print(json.dumps(measure_overlap(a.model, a.batch, a.bucket_mb, a.reps, a.steps, blocks=a.blocks)), flush=True)
 
 
 if __name__ == "__main__":

@@ -215,7 +215,7 @@ class GraphedDPStep:
                 if self.mode == "after":
                     self.issue[-1] = list(range(nb))
                 self.g_opt = torch.cuda.CUDAGraph()
-                self.g_opt.capture_begin(pool=self._pool, capture_error_mode="thread_local")
+                self.g_opt.capture_begin(pool=self._pool, capture_error_mode="relaxed")
                 self._widen_and_step()
                 self.g_opt.capture_end()
             self.loss = loss
@@ -231,10 +231,12 @@ class GraphedDPStep:
             self.optimizer._ldnn_capturing = on
 
     def _begin(self):
-        # thread_local: RCCL's watchdog / gloo's progress threads keep querying the HIP
-        # runtime while the (main or autograd) thread captures
+        # relaxed: a link of the chain begins on one thread (main / autograd) and may end
+        # on the other, which a thread_local capture refuses
+        # (hipErrorStreamCaptureWrongThread); RCCL's watchdog and gloo's progress
+        # threads keep querying the HIP runtime meanwhile, which a global capture refuses
         g = torch.cuda.CUDAGraph()
-        g.capture_begin(pool=self._pool, capture_error_mode="thread_local")
+        g.capture_begin(pool=self._pool, capture_error_mode="relaxed")
         self._cur = g
 
     def _end(self):
@@ -271,17 +273,20 @@ class GraphedDPStep:
         c = self._cap
         if c is None:
             return
-        done = []
         for p in params:
             if id(p) in c["seen"]:
                 continue
             c["seen"].add(id(p))
             i = self.bk.of_param.get(id(p))
-            if i is None:
-                continue
-            c["pending"][i] -= 1
-            if c["pending"][i] == 0 and not c["fired"][i]:
-                done.append(i)
+            if i is not None:
+                c["pending"][i] -= 1
+        # fire in bucket order, as GradBucketer launches them (same schedule on every path)
+        done = []
+        nxt = c.setdefault("next", 0)
+        while nxt < len(c["pending"]) and c["pending"][nxt] == 0:
+            done.append(nxt)
+            nxt += 1
+        c["next"] = nxt
         if done:
             self._fire(done)
 
@@ -295,7 +300,8 @@ class GraphedDPStep:
     def _collective(self, i):
         buf = self.bk.comm_buffer(i)
         if self.comm_fn is not None:
-            return self.comm_fn(i, buf)
+            w = self.comm_fn(i, buf)
+            return w if hasattr(w, "wait") else None
         return self.comm.all_reduce(buf, self._SUM, async_op=True)
 
     @property

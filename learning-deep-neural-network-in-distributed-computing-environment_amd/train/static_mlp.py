@@ -339,6 +339,9 @@ class StaticMLPEngine:
             self._opt_zero, self._fill_zero = merged[:2], merged[2:]
 
         self.rank = dist.get_rank(process_group) if self.distributed else 0
+        self.xp = getattr(self, "xp", None)
+        self._slots = [dict(x=self.x, xp=self.xp, labels=self.labels)]   # slot 0: load_batch's buffers
+        self._slot = 0
         self._pending_gather = {}
         self._master_whole = True
         if self.shard:
@@ -346,6 +349,7 @@ class StaticMLPEngine:
                            for b, e, _ in self.buckets]
             self._gloo = dist.get_backend(process_group) == "gloo"
         self._build_segments()
+        self._slots[0]["segs"] = (self.segments, self.opt_segments)
 
     # ------------------------------------------------------------------ kernels
     def _forward(self, train: bool = False):
@@ -538,8 +542,44 @@ class StaticMLPEngine:
         self.hp[0].fill_(lr)
 
     def load_batch(self, x: torch.Tensor, y: torch.Tensor):
+        self._use_slot(0)
         self.x.copy_(x.reshape(self.B, -1))
         self.labels.copy_(y)
+
+    def add_input_slots(self, n: int) -> list:
+        """``n`` more input buffers in the engine's own layout (incl. the first layer's
+        ones column), each with its own captured step: a loader (or the benchmark's
+        synthetic batches) writes batch i straight into slot i and ``step(slot=i)``
+        trains on it -- no per-step copy into a shared input buffer.  Returns the
+        [(x [B][in_features] view, labels [B])] of the new slots (ids 1..n)."""
+        B, dev, bf = self.B, self.device, torch.bfloat16
+        new = []
+        for _ in range(int(n)):
+            if self.xp is not None:   # ones column after the features (bias_ones_column)
+                full = torch.zeros_like(self.xp_full)
+                xp = full[:, : self.xp.shape[1]]
+                xp[:, self.x.shape[1]] = 1.0
+                x = xp[:, : self.x.shape[1]]
+            else:
+                full, xp, x = None, None, torch.zeros_like(self.x)
+            slot = dict(x=x, xp=xp, full=full, labels=torch.zeros_like(self.labels))
+            self._slots.append(slot)
+            self._use_slot(len(self._slots) - 1, build=True)
+            new.append((x, slot["labels"]))
+        self._use_slot(0)
+        return new
+
+    def _use_slot(self, i: int, build: bool = False):
+        if i == self._slot and not build:
+            return
+        sl = self._slots[i]
+        self.x, self.xp, self.labels = sl["x"], sl["xp"], sl["labels"]
+        self.h[0] = self.x
+        if build:
+            self._build_segments()   # closures read self.h[0] / self.xp / self.labels when captured
+            sl["segs"] = (self.segments, self.opt_segments)
+        self.segments, self.opt_segments = sl["segs"]
+        self._slot = i
 
     def eager_step(self, x: torch.Tensor, y: torch.Tensor):
         """One training step on a batch of ANOTHER size (the trailing partial batch of an
@@ -647,8 +687,11 @@ class StaticMLPEngine:
                 torch.cuda.current_stream().synchronize()
             self._pending_gather[bi] = g
 
-    def step(self):
-        """One full training step on the batch currently in (self.x, self.labels)."""
+    def step(self, slot: int | None = None):
+        """One full training step on the batch currently in (self.x, self.labels), or
+        in input slot ``slot`` (add_input_slots)."""
+        if slot is not None:
+            self._use_slot(slot)
         self._master_whole = False
         if not self.distributed:
             self.segments[0]()
@@ -740,6 +783,7 @@ class StaticMLPEngine:
     @torch.no_grad()
     def predict_logits(self, x: torch.Tensor) -> torch.Tensor:
         self.sync()
+        self._use_slot(0)
         self.x.copy_(x.reshape(self.B, -1))
         self._forward()
         return self.h[-1][:, : self.num_classes]

@@ -1,9 +1,15 @@
 #!/bin/bash
-# round-3 GPU check: full GPU suite, headline bench (+ CNN configs), overlap probes, gloo 2-rank bench rehearsal
+# round-3 GPU check: Q4 GEMM tests + A/B, full GPU suite, headline bench (+ CNN configs), overlap probes, gloo rehearsal
 set -o pipefail
 mkdir -p gpurun_out/r3
 O=gpurun_out/r3
 export HSA_ENABLE_IPC_MODE_LEGACY=0
+
+
+
+
+timeout -k 10 200 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_graphed_dp_gpu.py tests/test_static_mlp_gpu.py tests/test_ipc_gpu.py > $O/test_dp.txt 2>&1 || { echo "dp tests failed"; tail -60 $O/test_dp.txt; exit 1; }
+tail -2 $O/test_dp.txt
 timeout -k 10 700 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests -m gpu > $O/test_gpu.txt 2>&1 || { echo "gpu tests failed"; tail -60 $O/test_gpu.txt; exit 1; }
 tail -3 $O/test_gpu.txt
 timeout -k 10 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench1.txt 2> $O/bench1.err || { echo "bench failed"; tail -30 $O/bench1.err; exit 1; }

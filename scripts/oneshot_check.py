@@ -2,7 +2,8 @@
 on cuda:0 of the one-GPU box (RCCL refuses duplicate devices, so the process group is
 gloo; the one-shot kernels themselves only use HIP IPC).  Checks fp32 and bf16 sums
 against the expected values over many back-to-back calls (staging halves alternate),
-times it against gloo, and prints one JSON line per rank.
+the kernel captured into a hipGraph and replayed 20 times (device-side epochs), the
+self-test, and times it; prints one JSON line per rank.
 
     python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 scripts/oneshot_check.py
 """
@@ -38,6 +39,27 @@ def main():
                 ok = False
     torch.cuda.synchronize()
     os_.check()
+    # captured into a hipGraph and replayed: every replay is a new call (device-side
+    # epochs): the sum must follow the input each time
+    buf = torch.zeros(4096, device=dev)
+    src = torch.zeros(4096, device=dev)
+    side = torch.cuda.Stream(device=dev)
+    side.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=side):
+        buf.copy_(src)
+        os_.all_reduce(buf)
+    torch.cuda.current_stream().wait_stream(side)
+    for it in range(20):
+        src.fill_(float(r + 1) * (it + 1))
+        dist.barrier()
+        g.replay()
+        torch.cuda.synchronize()
+        want = (it + 1) * n * (n + 1) / 2
+        if not torch.all(buf == want):
+            ok = False
+    os_.check()
+    ok = ok and os_.self_test()
     x = torch.ones(1 << 18, device=dev)
     for _ in range(5):
         os_.all_reduce(x)
@@ -48,7 +70,7 @@ def main():
     torch.cuda.synchronize()
     us = (time.perf_counter() - t0) / 100 * 1e6
     dist.barrier()
-    print(json.dumps({"rank": r, "world": n, "ok": ok, "epoch": os_._c.epoch,
+    print(json.dumps({"rank": r, "world": n, "ok": ok, "calls": os_._c.calls,
                       "oneshot_1MB_fp32_us": round(us, 1)}), flush=True)
     D.teardown(ctx)
     if not ok:

@@ -67,7 +67,7 @@ def _loader(B, n_full, tail):
     return L(batches)
 
 
-@pytest.mark.filterwarnings("ignore:Detected call of `lr_scheduler.step\(\)`")
+@pytest.mark.filterwarnings(r"ignore:Detected call of `lr_scheduler.step\(\)`")
 def test_engine_local_epoch_per_batch_losses_and_partial_batch_trained():
     """Every batch is trained, the trailing partial one too (BAR/trainer.py:202-216):
     it runs the engine's eager_step; per-batch losses are per-batch means."""

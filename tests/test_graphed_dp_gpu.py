@@ -110,11 +110,8 @@ def test_rccl_world1_overlap_path(tmp_path):
         for i in range(2, 5):
             gd(xs[i], ys[i])
             gs(xs[i], ys[i])
-        # the odd-shaped last batch of an epoch falls back to the eager bucketed step,
-        # which issues the same collectives (count) as a replay
-        n1 = comm.schedule_digest()[0]
+        # the odd-shaped last batch of an epoch falls back to the eager bucketed step
         gd(xs[0][:100], ys[0][:100])
-        assert comm.schedule_digest()[0] - n1 == n_graphed
         gs(xs[0][:100], ys[0][:100])
         torch.cuda.synchronize()
         _close_updates(list(m1.parameters()), list(m2.parameters()), p0)
@@ -168,6 +165,39 @@ def test_segmented_comm_stream_standin_overlaps():
     standalone time (no overlap at all would make them equal)."""
     from ldnn.parallel.overlap_probe import measure_overlap
 
-    r = measure_overlap("lenet5", batch=1024, bucket_mb=0.05, reps=4, steps=20)
+    r = measure_overlap("lenet5", batch=1024, bucket_mb=0.05, reps=64, steps=20, blocks=8)
     assert r["segments"] >= 3
     assert r["with_standin_ms"] < r["single_ms"] + r["standin_alone_ms"], r
+
+
+def test_eager_fallback_and_replay_record_the_same_schedule():
+    """A rank whose last batch is short runs the eager bucketed step while its peers
+    replay the graph chain: both must record the same collectives, or
+    Comm.check_schedule raises a false RankDivergenceError.  A 2-rank stand-in comm
+    (identity collectives) keeps the bookkeeping of a real world > 1."""
+    import hashlib
+
+    class TwoRankEcho(LocalComm):
+        world_size = 2
+
+    shape = (128, 1, 28, 28)
+    m1, = _models("lenet5", 1)
+    crit = CrossEntropyLoss()
+    comms = [TwoRankEcho(), TwoRankEcho()]
+    dp = DataParallel(m1, comms[0], bucket_cap_mb=0.05, broadcast_init=False)
+    o1 = SGD(m1.parameters(), lr=0.01, momentum=0.0)
+    x = torch.randn(*shape, device="cuda").bfloat16()
+    y = torch.randint(0, 10, (shape[0],), device="cuda")
+    o1.zero_grad()
+    crit(dp(x), y).backward()
+    dp.finish_gradient_sync()
+    o1.step()
+    gd = GraphedDPStep(dp, crit, o1, x, y)
+    digests = []
+    for c, xb, yb in ((comms[0], x, y), (comms[1], x[:50], y[:50])):
+        dp.comm = dp.bucketer.comm = gd.comm = c
+        c._sched, c._nops = hashlib.sha1(), 0
+        gd(xb, yb)    # full batch: graph chain; short batch: eager fallback
+        digests.append(c.schedule_digest())
+    torch.cuda.synchronize()
+    assert digests[0] == digests[1] and digests[0][0] == len(dp.bucketer.buckets), digests
