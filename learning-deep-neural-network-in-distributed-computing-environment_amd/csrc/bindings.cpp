@@ -1220,9 +1220,6 @@ PYBIND11_MODULE(_C, m) {
       py::arg("N"), py::arg("splitk"));
   m.def("set_conv_impl", &ldnn::set_conv_impl, "0 = LDS-DMA fast path where it applies, 1 = generic kernel only",
         py::arg("impl"));
-  m.def("set_conv_q", &ldnn::set_conv_q, "big-tile conv path: 0 off (default), 1 every eligible shape",
-        py::arg("mode"));
-  m.def("get_conv_q", &ldnn::get_conv_q);
   m.def("set_conv_halo", &ldnn::set_conv_halo,
         "halo-staged 3x3 stride-1 conv: 0 off, 1 default (dgrad + 256x64 fwd tiles), 2 every eligible shape",
         py::arg("mode"));

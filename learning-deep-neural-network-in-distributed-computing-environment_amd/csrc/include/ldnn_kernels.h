@@ -130,9 +130,6 @@ ConvWorkspace conv2d_lds_workspace(const ConvShape& s, int op);
 // 0 = LDS-DMA fast path where it applies (default), 1 = generic kernel only (A/B and tests)
 void set_conv_impl(int impl);
 int get_conv_impl();
-// big-tile conv_q path (conv_lds.hip): 0 = off (default, measured slower), 1 = every eligible shape
-void set_conv_q(int mode);
-int get_conv_q();
 // halo-staged 3x3 stride-1 conv path (conv_lds.hip): 0 = off, 1 = default dispatch
 // (dgrad + 256x64 fwd tiles), 2 = also the 128x128 fwd tiles
 void set_conv_halo(int mode);

@@ -60,6 +60,13 @@ int bn_red_rows() {
   static const int v = std::max(1, env_int_or("LDNN_BN_RED_ROWS", 8));
   return v;
 }
+// rows per row lane of the apply passes (A/B knob LDNN_BN_APPLY_ROWS): 1 = the most blocks,
+// one row per thread -- measured on MI355X (profiles/r3/bn_apply_rows_ab_r3.jsonl, alternated)
+// EnhancedCNN b64 2.145 -> 2.076 ms vs 8 rows, ResNet-18 b64 / b256 unchanged
+int bn_apply_rows() {
+  static const int v = std::max(1, env_int_or("LDNN_BN_APPLY_ROWS", 1));
+  return v;
+}
 
 // accumulator copies the reduce blocks spread over (A/B: LDNN_BN_NCOP_FWD / _BWD)
 // (1 or kBnCopies: copies only pay when many blocks contend for the same addresses)
@@ -77,7 +84,7 @@ RedGeo red_geo(int M, int C, bool reduce = false) {
   g.rl = 256 / g.lanes;
   g.gx = (cv + 255) / 256;
   int gy = std::max(1, (reduce ? bn_red_blocks() : 1024) / g.gx);   // ~4 blocks per CU in total
-  const int min_rows = (reduce ? bn_red_rows() : 8) * g.rl;          // >= 8 rows per row lane
+  const int min_rows = (reduce ? bn_red_rows() : bn_apply_rows()) * g.rl;  // >= 8 rows per row lane
   gy = std::min(gy, std::max(1, (M + min_rows - 1) / min_rows));
   g.rpb = (M + gy - 1) / gy;
   g.gy = (M + g.rpb - 1) / g.rpb;

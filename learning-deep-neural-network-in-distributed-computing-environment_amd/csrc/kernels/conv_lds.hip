@@ -1067,194 +1067,6 @@ __global__ __launch_bounds__(256, 2) void conv_patch_kernel(LArgs a, const bf16_
   conv_tail<WM, WN, EPI, false, false>(a, g, acc, m0, n0, wm, wn, lane, smem, kPatchBytes / 4);
 }
 
-// ---- big-tile path: 256 x BN tiles, one wave per SIMD (conv_q) ---------------
-// The 128x128 / 2-workgroup kernel above is bound by the operand fill rate, not
-// by the MFMAs: a 128x128x64 step needs 32 KiB through the vector L1 / texture
-// path (64 B/clk/CU) for 2 MFLOP, i.e. 64 FLOP/B -- exactly the CU's MFMA rate
-// per L1 byte -- and the im2col gathers add latency on top (PMC: 11-15 % MFMA
-// busy on the ResNet-18 @224 step, profiles/pmc_rn64_r2.txt).  A 256 x 256
-// tile halves the bytes per FLOP (128 FLOP/B; 256 x 128: 85).  The pipeline is
-// gemm_q.hip's: 4 waves in a 2x2 grid, each owning 128 x BN/2 of C in AGPRs
-// (v_mfma_f32_16x16x32_bf16, 8 x BN/32 accumulator tiles), two 32-deep
-// sub-steps per K-tile whose fragment reads for the next sub-step, and (in
-// sub-step 1) the LDS-DMA of K-tile t+2, trickle out between the MFMAs; one
-// barrier per K-tile.  The operand gathers are the policies above (row = pixel,
-// k = (tap, channel block)), their offsets computed lane-wise right before each
-// DMA instruction.  Small-M shapes split the reduction into fp32 slabs summed by
-// conv_slab_epilogue_kernel.
-namespace q {
-
-__device__ __forceinline__ uint32_t lds_addr(const char* p) {
-  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
-}
-
-// fragment read (read_frag's image / lane map); asm when any operand is k-strided,
-// so the compiler does not drain the in-flight DMA before each ds_read (gemm_q.hip)
-template <bool KC, int ROWS, bool ASM>
-__device__ __forceinline__ bf16x8 frag(const char* lds, int rt, int kk, int lane) {
-  if constexpr (!ASM) {
-    return read_frag<KC, ROWS>(lds, rt, kk, lane);
-  } else if constexpr (KC) {
-    const int row = rt * 16 + (lane & 15);
-    const int chunk = kk * 4 + (lane >> 4);
-    bf16x8 v;
-    asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(lds_addr(lds) + (uint32_t)(row * 128 + ((chunk ^ (row & 7)) << 4)))
-                 : "memory");
-    return v;
-  } else {
-    const int g = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
-    const int kb = kk * 4 + g;
-    const int sw = (kb & 1) << 2;
-    const uint32_t blk = lds_addr(lds) + (uint32_t)((kb * (ROWS / 16) + rt) * 256);
-    bf16x4 lo, hi;
-    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(blk + ((qq ^ sw) * 32) + pp * 8) : "memory");
-    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(hi) : "v"(blk + (((4 + qq) ^ sw) * 32) + pp * 8) : "memory");
-    return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  }
-}
-__device__ __forceinline__ void lgkm_all() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
-__device__ __forceinline__ void mfma1(floatx4& acc, const bf16x8& b, const bf16x8& a) {
-  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(b), "v"(a) : "memory");
-}
-__device__ __forceinline__ void mma_fence() { asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory"); }
-template <int NT, typename F>
-__device__ __forceinline__ void mma(floatx4 (&acc)[NT][8], const bf16x8 (&fa)[8], const bf16x8 (&fb)[NT], F&& extra) {
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < NT; ++j) {
-      extra(i * NT + j);
-      mfma1(acc[j][i], fb[j], fa[i]);
-    }
-}
-
-}  // namespace q
-
-template <int BN, int NS, class OA, class OB, int EPI, bool DGRAD>
-__global__ __launch_bounds__(256, 1) void conv_q_kernel(LArgs a, const bf16_t* pa, uint32_t bytes_a, const bf16_t* pb,
-                                                        uint32_t bytes_b) {
-  constexpr int BM = 256, NW = 4, MT = 8, NT = BN / 32;
-  constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128, STAGE = A_BYTES + B_BYTES;
-  constexpr int PPA = OA::kPieces, PPB = OB::kPieces, PIECES = PPA + PPB;
-  static_assert(OA::kRows == BM && OB::kRows == BN && PPA == BM / 32 && PPB == BN / 32, "operand policy geometry");
-  constexpr int NMMA = MT * NT;                 // MFMAs per 32-deep sub-step
-  constexpr int DSTEP = NMMA / PIECES;          // a DMA instruction every DSTEP MFMAs
-  static_assert(DSTEP >= 1 && 2 * (MT + NT) <= NMMA, "interleave slots");
-  constexpr bool kAsm = !(OA::KC && OB::KC);
-  static_assert(NS >= 2 && NS * STAGE <= 160 * 1024, "LDS ring");
-  __shared__ __attribute__((aligned(1024))) char smem[NS * STAGE];
-
-  const Geo g = make_geo(a, DGRAD);
-  const int lane = threadIdx.x & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = wid >> 1, wn = wid & 1;
-  int m0, n0;
-  tile_coords(g.M, a.N, BM, BN, m0, n0);
-  const int kt0 = blockIdx.y * a.nk_split;
-  const int nk = max(0, min(g.nk - kt0, a.nk_split));
-
-  floatx4 acc[NT][MT];
-#pragma unroll
-  for (int j = 0; j < NT; ++j)
-#pragma unroll
-    for (int i = 0; i < MT; ++i) acc[j][i] = floatx4{0.f, 0.f, 0.f, 0.f};
-
-  OA oa;
-  OB ob;
-  oa.init(a, g, m0, wid, lane, kt0);
-  ob.init(a, g, n0, wid, lane, kt0);
-  Rsrc ra, rb;
-  ra.r = __builtin_amdgcn_make_buffer_rsrc((void*)pa, (short)0, (int)bytes_a, 0x00020000);
-  rb.r = __builtin_amdgcn_make_buffer_rsrc((void*)pb, (short)0, (int)bytes_b, 0x00020000);
-  KS ks = ks_init(a, g, kt0);  // K-tile of the next DMA
-  // DMA instruction r (< PIECES) of the K-tile at `ks` into stage `dst`
-  auto dma = [&](char* dst, int r) {
-    if (r < PPA) {
-      const int o = (int)oa.off(a, r, ks);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra.r, (lds_void*)(dst + (r * NW + wid) * 1024), 16, o, 0, 0, 0);
-    } else {
-      const int o = (int)ob.off(a, r - PPA, ks);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb.r, (lds_void*)(dst + A_BYTES + ((r - PPA) * NW + wid) * 1024), 16,
-                                               o, 0, 0, 0);
-    }
-  };
-  auto next_tile = [&]() {
-    ks_next(a, g, ks);
-    oa.advance(a);
-    ob.advance(a);
-  };
-
-  bf16x8 fa0[MT], fb0[NT], fa1[MT], fb1[NT];
-  q::mma_fence();
-  if (nk > 0) {
-    // prologue: K-tiles 0 .. NS-1 into stages 0 .. NS-1 (ks ends on the last one issued)
-#pragma unroll
-    for (int r = 0; r < PIECES; ++r) dma(smem, r);
-#pragma unroll
-    for (int t = 1; t < NS; ++t) {
-      if (t < nk) {
-        next_tile();
-#pragma unroll
-        for (int r = 0; r < PIECES; ++r) dma(smem + t * STAGE, r);
-      }
-    }
-    if (nk >= NS) wait_vm<PIECES * (NS - 1)>();  // tile 0 landed, tiles 1 .. NS-1 in flight
-    else wait_vm<0>();
-    lds_barrier();
-#pragma unroll
-    for (int i = 0; i < MT; ++i) fa0[i] = q::frag<OA::KC, BM, kAsm>(smem, wm * MT + i, 0, lane);
-#pragma unroll
-    for (int j = 0; j < NT; ++j) fb0[j] = q::frag<OB::KC, BN, kAsm>(smem + A_BYTES, wn * NT + j, 0, lane);
-  }
-  int cur_s = 0;  // stage of K-tile t
-  for (int t = 0; t < nk; ++t) {
-    const int nxt_s = cur_s == NS - 1 ? 0 : cur_s + 1;
-    char* const cur = smem + cur_s * STAGE;
-    char* const nxt = smem + nxt_s * STAGE;
-    // sub-step 0: sub-step 1's fragments stream in between the MFMAs (every 2nd)
-    q::lgkm_all();
-    q::mma<NT>(acc, fa0, fb0, [&](int qi) {
-      const int r = qi >> 1;
-      if (!(qi & 1) && r < MT + NT) {
-        if (r < MT) fa1[r] = q::frag<OA::KC, BM, kAsm>(cur, wm * MT + r, 1, lane);
-        else fb1[r - MT] = q::frag<OB::KC, BN, kAsm>(cur + A_BYTES, wn * NT + r - MT, 1, lane);
-      }
-    });
-    // one barrier per K-tile: every wave is done reading `cur`; tile t+1 (own DMA waited,
-    // tiles t+2 .. t+NS-1 may stay in flight) published
-    if (t + NS - 1 < nk) wait_vm<PIECES * (NS - 2)>();
-    else wait_vm<0>();
-    lds_barrier();
-    const bool more = t + NS < nk, have_next = t + 1 < nk;
-    if (more) next_tile();
-    // sub-step 1: tile t+NS's DMA into `cur`, tile t+1's first fragments (odd MFMAs)
-    q::mma<NT>(acc, fa1, fb1, [&](int qi) {
-      if (more && qi % DSTEP == 0 && qi / DSTEP < PIECES) dma(cur, qi / DSTEP);
-      const int r = qi >> 1;
-      if (have_next && (qi & 1) && r < MT + NT) {
-        if (r < MT) fa0[r] = q::frag<OA::KC, BM, kAsm>(nxt, wm * MT + r, 0, lane);
-        else fb0[r - MT] = q::frag<OB::KC, BN, kAsm>(nxt + A_BYTES, wn * NT + r - MT, 0, lane);
-      }
-    });
-    cur_s = nxt_s;
-  }
-  q::mma_fence();
-
-  const int mb = m0 + wm * 128, nbase = n0 + wn * (BN / 2);
-  GemmParams p{};
-  p.M = g.M;
-  p.N = a.N;
-  p.ldc = a.N;
-  if (gridDim.y > 1) {  // this slice's fp32 partial tile into its slab (conv_slab_epilogue sums them)
-    p.C = a.ws + (size_t)blockIdx.y * a.M * a.N;
-    epilogue<EPI_NONE, true, MT, NT>(p, acc, mb, nbase, lane);
-    return;
-  }
-  p.C = a.out;
-  p.bias = a.bias;
-  epilogue<EPI, false, MT, NT>(p, acc, mb, nbase, lane);
-}
-
 int slab_nt_env() {
   static const int v = [] {
     const char* e = std::getenv("LDNN_SLAB_NT");
@@ -1624,143 +1436,17 @@ ConvWorkspace ws_of(const Plan& p) {
   return w;
 }
 
-// ---- conv_q plan (big tiles) ------------------------------------------------
-// LDNN_CONV_Q: unset / 0 = never (default), 1 = every eligible shape.
-// LDNN_CONV_Q_BN / LDNN_CONV_Q_SPLITS override the tile width / slab split (A/B).
-// Measured on MI355X over the ResNet-18 @224 shapes (scripts/conv_micro.py,
-// profiles/conv_q_ab_r2.txt) the big tiles LOSE to the 128x128 two-workgroup
-// kernel on every shape (e.g. C128 H28 fwd 28.0 vs 23.4 us, C256 H14 32.3 vs 39.6
-// at 256x256): kept as an opt-in experiment, not dispatched by default.
-int q_env(const char* name, int dflt) {
-  const char* e = std::getenv(name);
-  return e ? std::atoi(e) : dflt;
-}
-int g_conv_q = -2;  // -2: not read yet
-int q_mode() {
-  if (g_conv_q == -2) g_conv_q = q_env("LDNN_CONV_Q", 0);
-  return g_conv_q;
-}
-
-struct QPlan {
-  bool on;
-  int bn, tiles, splits, nk_all, nk_split;
-};
-
-QPlan plan_q(int M, int N, int nk_all, bool eligible) {
-  QPlan p{};
-  if (!eligible || q_mode() <= 0 || N % 128 != 0 || M <= 0) return p;
-  static const int env_bn = q_env("LDNN_CONV_Q_BN", 0), env_sp = q_env("LDNN_CONV_Q_SPLITS", 0);
-  // 256 x 128 with a 3-deep ring (144 KiB) by default: two K-tiles of MFMAs to hide a
-  // gather's latency; 256 x 256 fits only 2 stages (A/B knob)
-  p.bn = env_bn == 256 && N % 256 == 0 ? 256 : 128;
-  p.tiles = ((M + 255) / 256) * (N / p.bn);
-  p.nk_all = nk_all;
-  // ~1 workgroup per CU at least: split the reduction into fp32 slabs, >= 8 K-tiles a slice
-  int sp = 1;
-  if (p.tiles < 128) sp = std::max(1, std::min((256 + p.tiles - 1) / p.tiles, nk_all / 8));
-  if (env_sp > 0) sp = std::min(env_sp, nk_all);
-  p.nk_split = (nk_all + sp - 1) / sp;
-  p.splits = (nk_all + p.nk_split - 1) / p.nk_split;
-  p.on = true;
-  return p;
-}
-
-QPlan plan_q_fwd(const ConvShape& s) {
-  return plan_q(s.N * s.P * s.Q, s.K, s.R * s.S * s.C / 64, s.C % 64 == 0 && s.K % 128 == 0);
-}
-QPlan plan_q_dgrad(const ConvShape& s) {
-  return plan_q(s.N * s.H * s.W, s.C, s.R * s.S * s.K / 64, s.stride == 1 && s.K % 64 == 0 && s.C % 128 == 0);
-}
-
-template <int BN, int NS, class OA, class OB, bool DGRAD>
-hipError_t launch_q(LArgs a, const QPlan& pl, int epi, const bf16_t* pa, size_t ba, const bf16_t* pb, size_t bb,
-                    hipStream_t st) {
-  const dim3 grid(pl.tiles, pl.splits), block(256);
-  if (pl.splits > 1) epi = EPI_NONE;  // the slab epilogue kernel applies it
-  switch (epi) {
-    case EPI_NONE:
-      conv_q_kernel<BN, NS, OA, OB, EPI_NONE, DGRAD><<<grid, block, 0, st>>>(a, pa, (uint32_t)ba, pb, (uint32_t)bb);
-      break;
-    case EPI_BIAS:
-      if constexpr (DGRAD) return hipErrorInvalidValue;
-      else conv_q_kernel<BN, NS, OA, OB, EPI_BIAS, DGRAD><<<grid, block, 0, st>>>(a, pa, (uint32_t)ba, pb, (uint32_t)bb);
-      break;
-    case EPI_BIAS_RELU:
-      if constexpr (DGRAD) return hipErrorInvalidValue;
-      else conv_q_kernel<BN, NS, OA, OB, EPI_BIAS_RELU, DGRAD><<<grid, block, 0, st>>>(a, pa, (uint32_t)ba, pb, (uint32_t)bb);
-      break;
-    default:
-      return hipErrorInvalidValue;
-  }
-  return hipGetLastError();
-}
-
-hipError_t conv2d_fwd_q(const ConvShape& s, const QPlan& pl, const uint16_t* x, const uint16_t* w, uint16_t* y,
-                        const float* bias, int epi, hipStream_t st, float* ws) {
-  if (pl.splits > 1 && ws == nullptr) return hipErrorNotSupported;
-  LArgs a = base_args(s);
-  a.out = y;
-  a.bias = bias;
-  a.M = s.N * s.P * s.Q;
-  a.N = s.K;
-  a.nb = s.C / 64;
-  a.tiles_x = pl.tiles;
-  a.nk_all = pl.nk_all;
-  a.nk_split = pl.nk_split;
-  a.ws = pl.splits > 1 ? ws : nullptr;
-  const size_t bx = (size_t)s.N * s.H * s.W * s.C * 2, bw = (size_t)s.K * a.rsc * 2;
-  const hipError_t e =
-      pl.bn == 256 ? launch_q<256, 2, FwdA<256, 8, 4>, WeightKC<256, 8, 4>, false>(a, pl, epi, x, bx, w, bw, st)
-                   : launch_q<128, 3, FwdA<256, 8, 4>, WeightKC<128, 4, 4>, false>(a, pl, epi, x, bx, w, bw, st);
-  if (e != hipSuccess || pl.splits == 1) return e;
-  return conv_slab_epilogue(ws, y, a.M, a.N, pl.splits, bias, epi, st);
-}
-
-hipError_t conv2d_dgrad_q(const ConvShape& s, const QPlan& pl, const uint16_t* dy, const uint16_t* w, uint16_t* dx,
-                          hipStream_t st, float* ws) {
-  if (pl.splits > 1 && ws == nullptr) return hipErrorNotSupported;
-  LArgs a = base_args(s);
-  a.out = dx;
-  a.M = s.N * s.H * s.W;
-  a.N = s.C;
-  a.nb = s.K / 64;
-  a.tiles_x = pl.tiles;
-  a.nk_all = pl.nk_all;
-  a.nk_split = pl.nk_split;
-  a.ws = pl.splits > 1 ? ws : nullptr;
-  const size_t bdy = (size_t)s.N * s.P * s.Q * s.K * 2, bw = (size_t)s.K * a.rsc * 2;
-  const hipError_t e =
-      pl.bn == 256 ? launch_q<256, 2, DgradA<256, 8, 4>, DgradB<256, 8, 4>, true>(a, pl, EPI_NONE, dy, bdy, w, bw, st)
-                   : launch_q<128, 3, DgradA<256, 8, 4>, DgradB<128, 4, 4>, true>(a, pl, EPI_NONE, dy, bdy, w, bw, st);
-  if (e != hipSuccess || pl.splits == 1) return e;
-  return conv_slab_epilogue(ws, dx, a.M, a.N, pl.splits, nullptr, EPI_NONE, st);
-}
-
-ConvWorkspace ws_of_q(const QPlan& p, int M, int N) {
-  ConvWorkspace w{};
-  if (p.on && p.splits > 1) w.slab_bytes = (size_t)p.splits * M * N * 4;
-  return w;
-}
-
 }  // namespace convlds
 
 using namespace convlds;
 
-void set_conv_q(int mode) { g_conv_q = mode; }
 void set_conv_halo(int mode) { g_conv_halo = mode; }
 int get_conv_halo() { return halo_env(); }
-int get_conv_q() { return q_mode(); }
 
 ConvWorkspace conv2d_lds_workspace(const ConvShape& s, int op) {
   if (!shape_ok(s)) return ConvWorkspace{};
-  if (op == 0 && s.C % 64 == 0) {
-    const QPlan q = plan_q_fwd(s);
-    return q.on ? ws_of_q(q, s.N * s.P * s.Q, s.K) : ws_of(plan_fwd(s));
-  }
-  if (op == 1 && s.K % 64 == 0) {
-    const QPlan q = plan_q_dgrad(s);
-    return q.on ? ws_of_q(q, s.N * s.H * s.W, s.C) : ws_of(plan_dgrad(s));
-  }
+  if (op == 0 && s.C % 64 == 0) return ws_of(plan_fwd(s));
+  if (op == 1 && s.K % 64 == 0) return ws_of(plan_dgrad(s));
   if (op == 2 && s.C % 8 == 0 && s.K % 8 == 0) {
     const WgradPlan p = plan_wgrad(s);
     ConvWorkspace w{};
@@ -1860,11 +1546,6 @@ hipError_t conv2d_fwd_lds(const ConvShape& s, const uint16_t* x, const uint16_t*
   }
   if (s.C % 64 != 0) return hipErrorNotSupported;
   if (s.N * s.P * s.Q <= 0) return bn != nullptr ? hipErrorNotSupported : hipSuccess;
-  const QPlan qp = plan_q_fwd(s);
-  if (qp.on) {  // big tiles; the next BN runs its own statistics pass
-    if (bn_used) *bn_used = false;
-    return conv2d_fwd_q(s, qp, x, w, y, bias, epi, st, ws);
-  }
   Plan pl = plan_fwd(s);
   LArgs a = base_args(s);
   if (bn != nullptr && pl.slab) {  // slab split-K: the next BN runs its own statistics pass
@@ -1914,8 +1595,6 @@ hipError_t conv2d_dgrad_lds(const ConvShape& s, const uint16_t* dy, const uint16
                             float* ws, int* cnt) {
   if (s.K % 64 != 0 || !shape_ok(s)) return hipErrorNotSupported;
   if (s.N * s.H * s.W <= 0) return hipSuccess;
-  const QPlan qp = plan_q_dgrad(s);
-  if (qp.on) return conv2d_dgrad_q(s, qp, dy, w, dx, st, ws);
   Plan pl = plan_dgrad(s);
   LArgs a = base_args(s);
   a.out = dx;

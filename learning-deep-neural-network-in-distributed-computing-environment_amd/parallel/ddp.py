@@ -54,13 +54,31 @@ class GradBucketer:
     A world of one keeps its gradient (Q4: no division by N-1 = 0)."""
 
     def __init__(self, flat: FlatParams, comm: Comm, bucket_cap_elems: int = 8 << 20,
-                 comm_dtype: torch.dtype | None = None, local_weight: float | None = None):
+                 comm_dtype: torch.dtype | None = None, local_weight: float | None = None,
+                 last_bucket_cap_elems: int | None = 1 << 20):
         self.flat, self.comm = flat, comm
         self.comm_dtype = None if comm_dtype in (None, torch.float32) else comm_dtype
         self.buckets: list[dict] = []
+        segs = list(flat.segments)
+        # The LAST bucket holds the first layers' gradients, ready only when the whole
+        # backward is done: nothing is left to hide its collective behind, so it is cut
+        # small (default 1 M elements = 4 MiB fp32, the one-shot IPC path's size) and the
+        # big buckets take everything that becomes ready earlier.
+        tail = []
+        if last_bucket_cap_elems and len(segs) > 1 and flat.numel > bucket_cap_elems:
+            last_cap = min(int(last_bucket_cap_elems), int(bucket_cap_elems))
+            n = 0
+            while len(segs) > 1 and n + segs[-1].storage_numel <= last_cap:
+                n += segs[-1].storage_numel
+                tail.insert(0, segs.pop())
         cur = None
-        for seg in flat.segments:
-            if cur is None or (seg.offset + seg.storage_numel - cur["begin"]) > bucket_cap_elems and cur["params"]:
+        for seg in segs:
+            # close the bucket when the next tensor would overflow it -- unless the bucket
+            # is still small (< cap / 4: e.g. a classifier + a BatchNorm in front of a
+            # 36 MB conv weight), which then rides along instead of costing a collective
+            size = seg.offset + seg.storage_numel - (cur["begin"] if cur is not None else 0)
+            if cur is None or (size > bucket_cap_elems and cur["params"]
+                               and cur["end"] - cur["begin"] >= bucket_cap_elems // 4):
                 if cur is not None:
                     self.buckets.append(cur)
                 cur = {"begin": seg.offset, "end": seg.offset, "params": []}
@@ -68,6 +86,10 @@ class GradBucketer:
             cur["params"].append(seg.param)
         if cur is not None:
             self.buckets.append(cur)
+        if tail:
+            self.buckets.append({"begin": tail[0].offset, "end": tail[-1].offset + tail[-1].storage_numel,
+                                 "params": [t.param for t in tail]})
+            self.buckets[-2]["end"] = tail[0].offset
         if self.buckets:
             self.buckets[-1]["end"] = flat.numel
         self.of_param = {}

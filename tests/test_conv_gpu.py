@@ -126,39 +126,6 @@ def test_lds_fast_path_matches_generic_kernel(N, C, H, W, K, R, st, pad):
     assert torch.equal(y0, y1) and torch.equal(dx0, dx1)
 
 
-@pytest.mark.parametrize("N,C,H,W,K,R,st,pad", [
-    (2, 128, 28, 28, 128, 3, 1, 1),    # 256x128 tiles, ragged last row tile
-    (4, 256, 14, 14, 256, 3, 1, 1),    # 256x256 tiles, slab split-K
-    (2, 256, 14, 14, 512, 3, 2, 1),    # stride-2 fwd (dgrad stays on the 128x128 kernel)
-    (3, 512, 7, 7, 512, 3, 1, 1),      # deep reduction, many slabs
-    (2, 64, 56, 56, 128, 1, 2, 0),     # 1x1 stride-2 shortcut
-])
-def test_big_tile_conv_matches_small_tile_kernel(N, C, H, W, K, R, st, pad):
-    """conv_q (256 x 256 / 256 x 128 tiles, one wave per SIMD) == the 128x128 LDS-DMA
-    kernel on fwd (bias+ReLU epilogue) and stride-1 dgrad, slab split-K included."""
-    torch.manual_seed(2)
-    Cc = _ext.C()
-    P = (H + 2 * pad - R) // st + 1
-    x = torch.randn(N, H, W, C, device="cuda").bfloat16()
-    w = (torch.randn(K, R, R, C, device="cuda") * (1.0 / (C * R * R) ** 0.5)).bfloat16()
-    gy = torch.randn(N, P, P, K, device="cuda").bfloat16()
-    bias = torch.randn(K, device="cuda")
-    outs = {}
-    try:
-        for mode in (0, 1):
-            Cc.set_conv_q(mode)
-            y = torch.empty(N, P, P, K, device="cuda", dtype=torch.bfloat16)
-            Cc.conv_fwd(x, w, y, st, pad, bias, Cc.EPI_BIAS_RELU)
-            dx = torch.empty(N, H, W, C, device="cuda", dtype=torch.bfloat16)
-            Cc.conv_dgrad(gy, w, dx, st, pad)
-            outs[mode] = (y.float(), dx.float())
-    finally:
-        Cc.set_conv_q(0)
-    (y0, dx0), (y1, dx1) = outs[0], outs[1]
-    torch.testing.assert_close(y1, y0, rtol=2e-2, atol=2e-2 * y0.abs().max().item())
-    torch.testing.assert_close(dx1, dx0, rtol=2e-2, atol=2e-2 * dx0.abs().max().item())
-
-
 @pytest.mark.parametrize("dtype,C,cp", [(torch.float32, 3, 8), (torch.bfloat16, 3, 8), (torch.float32, 16, 16),
                                         (torch.bfloat16, 20, 32)])
 def test_nchw_to_nhwc_pad(dtype, C, cp):

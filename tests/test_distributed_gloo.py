@@ -41,7 +41,7 @@ def _dp_worker(rank, world, port, out, comm_dtype=None):
     torch.manual_seed(123 + rank)  # different init on purpose: DataParallel must broadcast rank 0's
     m = mlp2(784, 32, 10)
     ldnn.prepare(m, "cpu")
-    dp = DataParallel(m, TorchComm(), bucket_cap_mb=0.01, comm_dtype=comm_dtype)  # tiny buckets -> several messages
+    dp = DataParallel(m, TorchComm(), bucket_cap_mb=0.001, comm_dtype=comm_dtype)  # tiny buckets -> several messages
     assert len(dp.bucketer.buckets) > 1
     opt = SGD(m.parameters(), lr=0.1, momentum=0.9)
     g = torch.Generator().manual_seed(7)
