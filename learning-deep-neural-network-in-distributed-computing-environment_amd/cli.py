@@ -93,9 +93,11 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--timeout", type=float, default=600.0, help="collective timeout (s): failure detection")
     p.add_argument("--no_eval", action="store_true")
     p.add_argument("--quiet", action="store_true")
-    p.add_argument("--graphs", action="store_true",
-                   help="replay each training step from hipGraphs; with --sync_every step the bucket "
-                        "all-reduces are captured into the step graph beside the backward (RCCL)")
+    p.add_argument("--graphs", dest="graphs", action="store_true", default=True,
+                   help="(default) on a GPU, replay each training step from hipGraphs; with --sync_every step the "
+                        "backward is a chain of graphs cut at the gradient buckets, each bucket's RCCL all-reduce "
+                        "issued between two links (train/graphed.py GraphedDPStep).  CPU runs are always eager")
+    p.add_argument("--no_graphs", dest="graphs", action="store_false", help="eager steps (one launch per kernel)")
     p.add_argument("--engine", choices=["auto", "autograd", "static"], default="auto",
                    help="static: MLP models run on the graph-captured static engine (train/static_mlp.py: native "
                         "kernels, fused loss + optimizer, per-step DP = its own RCCL reduce-scatter / sharded update "

@@ -488,8 +488,7 @@ void head_fwd_xent(const at::Tensor& h, const at::Tensor& W, const at::Tensor& b
                    int64_t num_classes, double grad_scale, const c10::optional<at::Tensor>& dh,
                    const c10::optional<at::Tensor>& dbias, int64_t dgrad_epi,
                    const c10::optional<at::Tensor>& dbias_ws, int64_t dgrad_mode,
-                   const c10::optional<at::Tensor>& dw, const c10::optional<at::Tensor>& db_head,
-                   const c10::optional<at::Tensor>& dw_ws) {
+                   const c10::optional<at::Tensor>& dgrad_mask) {
   check_dev(h, at::kBFloat16, "h");
   check_dev(W, at::kBFloat16, "W");
   check_dev(bias, at::kFloat, "bias");
@@ -534,26 +533,17 @@ void head_fwd_xent(const at::Tensor& h, const at::Tensor& W, const at::Tensor& b
                     dh->stride(0) % 8 == 0 && aligned16(dh->data_ptr()),
                 "head: dh must be [B][K] with 16-B aligned rows");
     if (dgrad_mode < 0) dgrad_mode = ld == 16 ? 0 : 1;  // auto: the streaming dgrad where it applies
-    TORCH_CHECK(dgrad_mode >= 0 && dgrad_mode <= 3, "head: dgrad_mode must be -1 (auto), 0, 1, 2 or 3");
-    TORCH_CHECK((dgrad_mode != 0 && dgrad_mode != 3) || ld == 16, "head: the streaming dgrad (mode 0 / 3) needs ld == 16");
-    TORCH_CHECK(dgrad_mode == 0 || dgrad_mode == 3 || K <= ldnn::head_dgrad_max_k(), "head: fused dgrad needs K <= ",
+    TORCH_CHECK(dgrad_mode >= 0 && dgrad_mode <= 2, "head: dgrad_mode must be -1 (auto), 0, 1 or 2");
+    TORCH_CHECK(dgrad_mode != 0 || ld == 16, "head: the streaming dgrad (mode 0) needs ld == 16");
+    TORCH_CHECK(dgrad_mode == 0 || K <= ldnn::head_dgrad_max_k(), "head: fused dgrad needs K <= ",
                 ldnn::head_dgrad_max_k());
-    if (dgrad_mode == 3) {  // + the head's own weight / bias gradients from the same pass over h
-      TORCH_CHECK(dw.has_value() && dw_ws.has_value(), "head: mode 3 needs dw and dw_ws");
-      check_dev(*dw, at::kFloat, "dw");
-      check_dev(*dw_ws, at::kFloat, "dw_ws");
-      TORCH_CHECK(dw->dim() == 2 && dw->is_contiguous() && dw->size(1) == K && dw->size(0) == W.size(0) &&
-                      aligned16(dw->data_ptr()), "head: dw must be a dense [W rows][K] fp32 tensor");
-      TORCH_CHECK(dw_ws->is_contiguous() && dw_ws->numel() >= (int64_t)ldnn::head_dw_splits((int)B) * 16 * K &&
-                      aligned16(dw_ws->data_ptr()), "head: dw_ws too small (head_dw_splits(B) x 16 x K)");
-      p.dw = dw->data_ptr<float>();
-      p.dw_ws = dw_ws->data_ptr<float>();
-      p.lddw = (int)K;
-      if (db_head.has_value()) {
-        check_dev(*db_head, at::kFloat, "db_head");
-        TORCH_CHECK(db_head->is_contiguous() && db_head->numel() >= W.size(0), "head: bad db_head");
-        p.db_head = db_head->data_ptr<float>();
-      }
+    if (dgrad_mask.has_value()) {  // relu'(h) from the forward's bit mask (streaming mode, EPI_DRELU)
+      check_dev(*dgrad_mask, at::kByte, "dgrad_mask");
+      TORCH_CHECK(dgrad_mode == 0 && dgrad_epi == ldnn::EPI_DRELU && dgrad_mask->dim() == 2 &&
+                      dgrad_mask->size(0) == B && dgrad_mask->size(1) * 8 >= K && dgrad_mask->stride(1) == 1,
+                  "head: dgrad_mask needs the streaming mode, EPI_DRELU and a [B][>= K/8] byte mask");
+      p.mask = dgrad_mask->data_ptr<uint8_t>();
+      p.ldmask = (int)dgrad_mask->stride(0);
     }
     p.dgrad_mode = (int)dgrad_mode;
     TORCH_CHECK(dgrad_epi == ldnn::EPI_NONE || dgrad_epi == ldnn::EPI_DRELU || dgrad_epi == ldnn::EPI_DSIGMOID,
@@ -1295,10 +1285,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("h"), py::arg("W"), py::arg("bias"), py::arg("labels"), py::arg("logits"), py::arg("dlogits"),
         py::arg("stats"), py::arg("num_classes"), py::arg("grad_scale"), py::arg("dh") = py::none(), py::arg("dbias") = py::none(),
         py::arg("dgrad_epi") = (int64_t)ldnn::EPI_DRELU, py::arg("dbias_ws") = py::none(),
-        py::arg("dgrad_mode") = (int64_t)-1, py::arg("dw") = py::none(), py::arg("db_head") = py::none(),
-        py::arg("dw_ws") = py::none());
+        py::arg("dgrad_mode") = (int64_t)-1, py::arg("dgrad_mask") = py::none());
   m.def("head_dgrad_ws_floats", &ldnn::head_dgrad_ws_floats, py::arg("B"), py::arg("K"));
-  m.def("head_dw_splits", &ldnn::head_dw_splits, py::arg("B"));
   m.def("head_wgrad", &head_wgrad, "dW = dz^T h (+ db = colsum dz); splits > 1 accumulate atomically",
         py::arg("dz"), py::arg("h"), py::arg("dW"), py::arg("db") = py::none(), py::arg("splits") = 0);
   m.def("head_dgrad_max_k", &ldnn::head_dgrad_max_k);

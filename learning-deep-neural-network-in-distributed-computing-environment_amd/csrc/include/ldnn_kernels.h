@@ -294,16 +294,12 @@ struct HeadParams {
   //    global memory; 2: fused, h staged in LDS (1 / 2 need K <= head_dgrad_max_k()
   //    and dbias_ws for dbias)
   int dgrad_mode;
-  // mode 3: the streaming dgrad ALSO produces the head's weight / bias gradients from the
-  // same pass over h: per-workgroup partial dW slabs dw_ws [head_dw_splits(B)][ld][K] fp32,
-  // summed into dw [ld][lddw] (overwritten), db_head [ld] (+= column sums of dlogits)
-  float* dw_ws;
-  float* dw;
-  float* db_head;
-  int lddw;
+  // mode 0 with dgrad_epi EPI_DRELU: relu'(h) from the forward's bit mask (mask [B][ldmask]
+  // bytes, bit j of byte (r, c/8) = h[r][c] > 0) instead of re-reading h -- 1/16 of the bytes
+  const uint8_t* mask;
+  int ldmask;
 };
 hipError_t head_fwd_xent(const HeadParams& p, hipStream_t s);
-int head_dw_splits(int B);
 int head_dgrad_max_k();
 size_t head_dgrad_ws_floats(int B, int K);
 // out[i] = sum_s ws[s][i] (+ beta * out[i]) over n4 float4 columns and `splits` slabs

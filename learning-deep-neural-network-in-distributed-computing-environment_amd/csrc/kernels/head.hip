@@ -411,7 +411,9 @@ __global__ __launch_bounds__(kWgWaves * 64) void head_wgrad_kernel(HeadWgradPara
 // The column sums are reduced over the workgroup's 8 row lanes in LDS and added
 // with one atomic per column per workgroup.  Two rows per iteration keep 4 loads in
 // flight per lane.
-template <int DEPI>
+// MASK (EPI_DRELU only): relu'(h) from the forward's bit mask instead of h -- the stream
+// then reads 8 MB instead of 128 MB at batch 16384 x 4096 (the dh write is the cost left)
+template <int DEPI, bool MASK = false>
 __global__ __launch_bounds__(256) void head_dgrad_stream_kernel(HeadParams p, int rows_per_block) {
   __shared__ float part[8][256];
   const int cg = threadIdx.x & 31, ty = threadIdx.x >> 5;
@@ -428,7 +430,7 @@ __global__ __launch_bounds__(256) void head_dgrad_stream_kernel(HeadParams p, in
     for (int i = 0; i < 8; ++i) wf[c][i] = bf2f(w[i]);
   }
   float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  auto row_out = [&](const u16x8& g0, const u16x8& g1, const u16x8& hv, int r) {
+  auto row_out = [&](const u16x8& g0, const u16x8& g1, const u16x8& hv, uint32_t mb, int r) {
     float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int c = 0; c < 16; ++c) {
@@ -441,12 +443,21 @@ __global__ __launch_bounds__(256) void head_dgrad_stream_kernel(HeadParams p, in
     for (int i = 0; i < 8; ++i) {
       const float hf = bf2f(hv[i]);
       float x = v[i];
-      if constexpr (DEPI == EPI_DRELU) x = hf > 0.f ? x : 0.f;
+      if constexpr (MASK) x = ((mb >> i) & 1u) ? x : 0.f;
+      else if constexpr (DEPI == EPI_DRELU) x = hf > 0.f ? x : 0.f;
       else if constexpr (DEPI == EPI_DSIGMOID) x *= hf * (1.f - hf);
       o[i] = f2bf(x);
       s[i] += bf2f(o[i]);
     }
     *reinterpret_cast<u16x8*>(p.dh + (size_t)r * p.lddh + c0) = o;
+  };
+  auto hrow = [&](int r) -> u16x8 {
+    if constexpr (MASK) return u16x8{};
+    else return *reinterpret_cast<const u16x8*>(p.h + (size_t)r * p.ldh + c0);
+  };
+  auto mrow = [&](int r) -> uint32_t {
+    if constexpr (MASK) return (uint32_t)p.mask[(size_t)r * p.ldmask + (c0 >> 3)];
+    else return 0u;
   };
   if (cok) {
     int r = r_begin + ty;
@@ -454,14 +465,14 @@ __global__ __launch_bounds__(256) void head_dgrad_stream_kernel(HeadParams p, in
       const u16x8* gp0 = reinterpret_cast<const u16x8*>(p.dlogits + (size_t)r * p.ld);
       const u16x8* gp1 = reinterpret_cast<const u16x8*>(p.dlogits + (size_t)(r + 8) * p.ld);
       const u16x8 a0 = gp0[0], a1 = gp0[1], b0 = gp1[0], b1 = gp1[1];
-      const u16x8 h0 = *reinterpret_cast<const u16x8*>(p.h + (size_t)r * p.ldh + c0);
-      const u16x8 h1 = *reinterpret_cast<const u16x8*>(p.h + (size_t)(r + 8) * p.ldh + c0);
-      row_out(a0, a1, h0, r);
-      row_out(b0, b1, h1, r + 8);
+      const u16x8 h0 = hrow(r), h1 = hrow(r + 8);
+      const uint32_t m0 = mrow(r), m1 = mrow(r + 8);
+      row_out(a0, a1, h0, m0, r);
+      row_out(b0, b1, h1, m1, r + 8);
     }
     for (; r < r_end; r += 8) {
       const u16x8* gp0 = reinterpret_cast<const u16x8*>(p.dlogits + (size_t)r * p.ld);
-      row_out(gp0[0], gp0[1], *reinterpret_cast<const u16x8*>(p.h + (size_t)r * p.ldh + c0), r);
+      row_out(gp0[0], gp0[1], hrow(r), mrow(r), r);
     }
   }
   if (p.dbias == nullptr) return;
@@ -479,121 +490,18 @@ __global__ __launch_bounds__(256) void head_dgrad_stream_kernel(HeadParams p, in
   }
 }
 
-// Mode 3: the streaming dgrad fused with the head's wgrad -- ONE pass over h produces
-// dh = (dlogits W) * act'(h) (+ its column sums = the previous layer's bias gradient) AND
-// the head's dW = dlogits^T h (+ db_head = column sums of dlogits), instead of the dgrad
-// stream and head_wgrad each reading h (128 MB at batch 16384 x 4096).  A thread owns 4
-// columns and walks rows 4 apart (a wave = one 512-B row run): per row 16 x 4 FMAs for
-// dh and 16 x 4 for dW, both accumulated in registers; the workgroup's four waves fold
-// their dW partials with LDS float atomics and write one [16][256] fp32 slab per
-// workgroup row-slice, summed by slab_sum into dW (deterministic, no global atomics).
-constexpr int kDwSplits = 32;
-
-template <int DEPI>
-__global__ __launch_bounds__(256) void head_stream_dw_kernel(HeadParams p, int rows_per_block) {
-  __shared__ float pdw[16][256];
-  __shared__ float pdb[4][256];
-  __shared__ float pdl[16];
-  const int cg = threadIdx.x & 63, ty = threadIdx.x >> 6;
-  const int c0 = (blockIdx.x * 64 + cg) * 4;
-  const int r_begin = blockIdx.y * rows_per_block;
-  const int r_end = min(p.B, r_begin + rows_per_block);
-  const bool cok = c0 < p.K;
-  for (int i = threadIdx.x; i < 16 * 256; i += 256) (&pdw[0][0])[i] = 0.f;
-  if (threadIdx.x < 16) pdl[threadIdx.x] = 0.f;
-  float wf[16][4], acc[16][4], dls[16];
-#pragma unroll
-  for (int c = 0; c < 16; ++c) {
-    u16x4 w = {};
-    if (cok && c < p.ldw_rows) w = *reinterpret_cast<const u16x4*>(p.W + (size_t)c * p.ldw + c0);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      wf[c][i] = bf2f(w[i]);
-      acc[c][i] = 0.f;
-    }
-    dls[c] = 0.f;
-  }
-  float s[4] = {0.f, 0.f, 0.f, 0.f};
-  __syncthreads();
-  if (cok) {
-#pragma unroll 2
-    for (int r = r_begin + ty; r < r_end; r += 4) {
-      const u16x8* gp = reinterpret_cast<const u16x8*>(p.dlogits + (size_t)r * p.ld);
-      const u16x8 g0 = gp[0], g1 = gp[1];
-      const u16x4 hv = *reinterpret_cast<const u16x4*>(p.h + (size_t)r * p.ldh + c0);
-      float hf[4], v[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int i = 0; i < 4; ++i) hf[i] = bf2f(hv[i]);
-#pragma unroll
-      for (int c = 0; c < 16; ++c) {
-        const float gc = bf2f(c < 8 ? g0[c] : g1[c - 8]);  // padded classes hold 0
-        dls[c] += gc;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          v[i] = fmaf(gc, wf[c][i], v[i]);
-          acc[c][i] = fmaf(gc, hf[i], acc[c][i]);
-        }
-      }
-      u16x4 o;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        float x = v[i];
-        if constexpr (DEPI == EPI_DRELU) x = hf[i] > 0.f ? x : 0.f;
-        else if constexpr (DEPI == EPI_DSIGMOID) x *= hf[i] * (1.f - hf[i]);
-        o[i] = f2bf(x);
-        s[i] += bf2f(o[i]);
-      }
-      *reinterpret_cast<u16x4*>(p.dh + (size_t)r * p.lddh + c0) = o;
-    }
-  }
-  // fold the 4 waves' partials
-#pragma unroll
-  for (int c = 0; c < 16; ++c)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) atomicAdd(&pdw[c][cg * 4 + i], acc[c][i]);
-#pragma unroll
-  for (int i = 0; i < 4; ++i) pdb[ty][cg * 4 + i] = s[i];
-  if (blockIdx.x == 0 && cg == 0) {
-#pragma unroll
-    for (int c = 0; c < 16; ++c) atomicAdd(&pdl[c], dls[c]);
-  }
-  __syncthreads();
-  // slab [blockIdx.y][16][K]: row c of this workgroup's 256 columns
-  float* slab = p.dw_ws + (size_t)blockIdx.y * 16 * p.K;
-  for (int q = threadIdx.x; q < 16 * 64; q += 256) {
-    const int c = q >> 6, col = (q & 63) * 4;
-    if (blockIdx.x * 256 + col < p.K)
-      *reinterpret_cast<floatx4*>(slab + (size_t)c * p.K + blockIdx.x * 256 + col) =
-          *reinterpret_cast<const floatx4*>(&pdw[c][col]);
-  }
-  if (p.dbias != nullptr) {
-    const int col = threadIdx.x;
-    if (blockIdx.x * 256 + col < p.K)
-      atomicAdd(p.dbias + blockIdx.x * 256 + col, pdb[0][col] + pdb[1][col] + pdb[2][col] + pdb[3][col]);
-  }
-  if (p.db_head != nullptr && blockIdx.x == 0 && threadIdx.x < 16 && threadIdx.x < p.ldw_rows)
-    atomicAdd(p.db_head + threadIdx.x, pdl[threadIdx.x]);
-}
-
-template <int DEPI>
-hipError_t launch_head_stream_dw(const HeadParams& p, hipStream_t s) {
-  const int gx = (p.K + 255) / 256;
-  const int gy = head_dw_splits(p.B);
-  const int rpb = (p.B + gy - 1) / gy;
-  head_stream_dw_kernel<DEPI><<<dim3(gx, gy), 256, 0, s>>>(p, rpb);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  // dW rows (16 padded classes) = sum of the gy slabs
-  if (p.lddw == p.K) return slab_sum(p.dw_ws, p.dw, (int64_t)p.ldw_rows * p.K / 4, gy, 0.f, s);
-  return hipErrorInvalidValue;
-}
-
 template <int DEPI>
 hipError_t launch_head_dgrad_stream(const HeadParams& p, hipStream_t s) {
   const int gx = (p.K + 255) / 256;
   int gy = (p.B + 255) / 256;
   if (gy > 256) gy = 256;
   const int rpb = (p.B + gy - 1) / gy;
+  if constexpr (DEPI == EPI_DRELU) {
+    if (p.mask != nullptr) {
+      head_dgrad_stream_kernel<DEPI, true><<<dim3(gx, gy), 256, 0, s>>>(p, rpb);
+      return hipGetLastError();
+    }
+  }
   head_dgrad_stream_kernel<DEPI><<<dim3(gx, gy), 256, 0, s>>>(p, rpb);
   return hipGetLastError();
 }
@@ -617,11 +525,6 @@ hipError_t launch_head_fwd_dg(const HeadParams& p, hipStream_t s) {
 
 template <int DEPI>
 hipError_t head_dgrad_dispatch(const HeadParams& p, hipStream_t s) {
-  if (p.dgrad_mode == 3) {  // forward-only head kernel, then the fused dgrad + wgrad stream
-    hipError_t e = launch_head_fwd<-1, false>(p, s);
-    if (e != hipSuccess) return e;
-    return launch_head_stream_dw<DEPI>(p, s);
-  }
   if (p.dgrad_mode == 0) {  // streaming: forward-only head kernel, then the dgrad stream
     hipError_t e = launch_head_fwd<-1, false>(p, s);
     if (e != hipSuccess) return e;
@@ -641,10 +544,8 @@ hipError_t head_fwd_xent(const HeadParams& p, hipStream_t s) {
   if (p.ld > 64 || p.ld % 16 != 0 || p.C > p.ld || p.ldw_rows > p.ld || p.K % 8 != 0) return hipErrorInvalidValue;
   if (p.dh == nullptr) return launch_head_fwd<-1, false>(p, s);
   if (p.lddh % 8 != 0) return hipErrorInvalidValue;
-  if (p.dgrad_mode < 0 || p.dgrad_mode > 3 || ((p.dgrad_mode == 0 || p.dgrad_mode == 3) && p.ld != 16))
-    return hipErrorInvalidValue;
-  if (p.dgrad_mode == 3 && (p.dw_ws == nullptr || p.dw == nullptr || p.lddw != p.K || p.K % 4 != 0 ||
-                            p.ldw_rows > 16 || p.ldw % 4 != 0 || p.ldh % 4 != 0 || p.lddh % 4 != 0))
+  if (p.dgrad_mode < 0 || p.dgrad_mode > 2 || (p.dgrad_mode == 0 && p.ld != 16)) return hipErrorInvalidValue;
+  if (p.mask != nullptr && (p.dgrad_mode != 0 || p.dgrad_epi != EPI_DRELU || p.ldmask * 8 < p.K))
     return hipErrorInvalidValue;
   if ((p.dgrad_mode == 1 || p.dgrad_mode == 2) &&
       (p.K > kHeadDgradMaxK || (p.dbias != nullptr && p.dbias_ws == nullptr)))
@@ -658,8 +559,6 @@ hipError_t head_fwd_xent(const HeadParams& p, hipStream_t s) {
 }
 
 size_t head_dgrad_ws_floats(int B, int K) { return (size_t)((B + 15) / 16) * K; }
-
-int head_dw_splits(int B) { return std::max(1, std::min(kDwSplits, (B + 127) / 128)); }
 
 int head_dgrad_max_k() { return kHeadDgradMaxK; }
 

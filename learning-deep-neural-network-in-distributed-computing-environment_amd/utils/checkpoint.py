@@ -121,6 +121,19 @@ def load_checkpoint(path: str, model, optimizer=None, scheduler=None, map_locati
         xp = os.path.join(os.path.dirname(path), f"xtra_ge{int(sd['global_epoch']):04d}_rank{rank}.pt")
         if os.path.exists(xp):
             sd["extra"] = torch.load(xp, map_location=map_location, weights_only=True)["extra"]
+        else:
+            # rank 0's shard indices / partition RNG are NOT this rank's: drop them (the
+            # caller re-partitions from its own seed) instead of resuming every rank on
+            # rank 0's shard with rank 0's draws (e.g. a non-shared filesystem, or a
+            # checkpoint written before per-rank extras existed)
+            import warnings
+
+            warnings.warn(f"{xp} not found: rank {rank} resumes without its saved shard / partition RNG "
+                          "(re-partitioned from the seed)")
+            ex = dict(sd.get("extra") or {})
+            for k in ("indices_train", "indices_val", "rng_state"):
+                ex.pop(k, None)
+            sd["extra"] = ex
     with torch.no_grad():
         model.load_state_dict(sd["model"])
     for m in model.modules():

@@ -9,9 +9,14 @@
 # with the reference's default (gradients) the exchange is a no-op and the
 # six variants would differ only by noise.
 # 5 ranks share the one GPU over gloo (RCCL needs a GPU per rank).
-#   bash scripts/experiment_matrix.sh [variant ...]     -> gpurun_out/matrix/<variant>/
+# AGG=gradients (the reference's default: SURVEY Q1 no-op) | weights (default here); SYNC=step runs
+# per-step data parallelism instead of the reference's once-per-global-epoch exchange.
+#   bash scripts/experiment_matrix.sh     -> gpurun_out/matrix${TAG}/<variant>/
 cd "${GRAFT_REPO_ROOT:-.}"
-mkdir -p gpurun_out/matrix
+AGG=${AGG:-weights}
+SYNC=${SYNC:-global_epoch}
+M=gpurun_out/matrix${TAG}
+mkdir -p $M
 N=${N:-5}
 port=29711
 specs=("BAR allreduce balanced" "BR ring balanced" "BDR double_ring balanced"
@@ -20,17 +25,17 @@ for spec in "${specs[@]}"; do
   set -- $spec
   name=$1; topo=$2; part=$3
   if [ -n "$ONLY" ] && [[ " $ONLY " != *" $name "* ]]; then continue; fi
-  out=gpurun_out/matrix/$name
+  out=$M/$name
   rm -rf $out && mkdir -p $out
   t0=$(date +%s.%N)
   timeout -k 10 ${LIMIT:-420} python -m torch.distributed.run --nproc-per-node $N --master-addr 127.0.0.1 \
     --master-port $port train.py --backend gloo --model enhanced_cnn --dataset cifar10-hard --n_train ${NTRAIN:-10000} \
     --n_test 2000 --epochs_global ${EG:-20} --epochs_local ${EL:-5} --batch_size 64 --lr 1e-3 --topology $topo \
-    --partition $part --aggregation_by weights --augment autoaugment --graphs --quiet --time_limit 0 \
+    --partition $part --aggregation_by $AGG --sync_every $SYNC --augment autoaugment --graphs --quiet --time_limit 0 \
     --plots $out/Graphs --out_dir $out > $out/train.log 2>&1
   rc=$?
   t1=$(date +%s.%N)
-  echo "$name topology=$topo partition=$part rc=$rc wall_s=$(python3 -c "print(round($t1-$t0,1))")" | tee -a gpurun_out/matrix/summary.txt
+  echo "$name topology=$topo partition=$part rc=$rc wall_s=$(python3 -c "print(round($t1-$t0,1))")" | tee -a $M/summary.txt
   [ $rc -eq 0 ] || exit $rc
   port=$((port + 1))
 done

@@ -121,3 +121,23 @@ def test_replace_follows_reference_variant():
     assert resolve_replace("auto", None, "double_ring") is True
     assert resolve_replace("auto", 0.5, "allreduce") is True
     assert resolve_replace("off", 0.5, "ring") is False and resolve_replace("on", None, "ring") is True
+
+
+def test_rank_without_its_extra_drops_rank0_shard(tmp_path):
+    """A rank > 0 resuming a rank-0 checkpoint whose per-rank extra file is missing must
+    not silently take rank 0's shard indices / partition RNG."""
+    import numpy as np
+    import pytest
+
+    m = mlp2(784, 32, 10)
+    ldnn.prepare(m, "cpu")
+    opt = Adam(m.parameters(), lr=1e-2)
+    p = Checkpointer(str(tmp_path), rank=0).save(2, m, opt, None, histories={},
+                                                 extra={"indices_train": np.arange(5), "indices_val": np.arange(3),
+                                                        "rng_state": {"a": 1}, "fixed_classes": [0, 1]})
+    with pytest.warns(UserWarning, match="re-partitioned"):
+        sd = load_checkpoint(p, m, opt, rank=1)
+    assert "indices_train" not in sd["extra"] and "rng_state" not in sd["extra"]
+    assert list(sd["extra"]["fixed_classes"]) == [0, 1]
+    sd0 = load_checkpoint(p, m, opt, rank=0)
+    assert "indices_train" in sd0["extra"]
