@@ -129,7 +129,7 @@ def run_ldnn(ctx, args):
                           bucket_cap_elems=args.bucket_elems, shard_optimizer=False if args.no_shard else None,
                           library_gemms=args.gemms == "library",
                           fuse_head_dgrad=False if args.no_fuse_head_dgrad else None,
-                          head_dgrad_mode=args.head_dgrad_mode, head_relu_mask=not args.no_head_mask)
+                          head_dgrad_mode=args.head_dgrad_mode)
     if ctx.distributed:
         dist.broadcast(eng.flat.master, src=0)
         eng.flat.refresh_shadow()
@@ -329,8 +329,6 @@ def main():
                     help="separate head dgrad GEMM instead of the head kernel's fused dgrad (dReLU + dbias)")
     ap.add_argument("--head-dgrad-mode", type=int, default=-1,
                     help="-1 auto (streaming dh kernel for <= 16 classes), 1 fused (h re-read), 2 fused (h in LDS)")
-    ap.add_argument("--no-head-mask", action="store_true",
-                    help="A/B: the head's streaming dgrad re-reads h instead of the forward's ReLU bit mask")
     ap.add_argument("--compare-stock", action="store_true")
     ap.add_argument("--backend", default="auto", help="auto (nccl = RCCL on GPUs) | gloo (testing only)")
     ap.add_argument("--no-configs", action="store_true", help="skip the LeNet-5 / ResNet-18 config timings")

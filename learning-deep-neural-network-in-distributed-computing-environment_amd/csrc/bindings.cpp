@@ -487,8 +487,7 @@ void head_fwd_xent(const at::Tensor& h, const at::Tensor& W, const at::Tensor& b
                    const c10::optional<at::Tensor>& logits, const at::Tensor& dlogits, const at::Tensor& stats,
                    int64_t num_classes, double grad_scale, const c10::optional<at::Tensor>& dh,
                    const c10::optional<at::Tensor>& dbias, int64_t dgrad_epi,
-                   const c10::optional<at::Tensor>& dbias_ws, int64_t dgrad_mode,
-                   const c10::optional<at::Tensor>& dgrad_mask) {
+                   const c10::optional<at::Tensor>& dbias_ws, int64_t dgrad_mode) {
   check_dev(h, at::kBFloat16, "h");
   check_dev(W, at::kBFloat16, "W");
   check_dev(bias, at::kFloat, "bias");
@@ -537,14 +536,6 @@ void head_fwd_xent(const at::Tensor& h, const at::Tensor& W, const at::Tensor& b
     TORCH_CHECK(dgrad_mode != 0 || ld == 16, "head: the streaming dgrad (mode 0) needs ld == 16");
     TORCH_CHECK(dgrad_mode == 0 || K <= ldnn::head_dgrad_max_k(), "head: fused dgrad needs K <= ",
                 ldnn::head_dgrad_max_k());
-    if (dgrad_mask.has_value()) {  // relu'(h) from the forward's bit mask (streaming mode, EPI_DRELU)
-      check_dev(*dgrad_mask, at::kByte, "dgrad_mask");
-      TORCH_CHECK(dgrad_mode == 0 && dgrad_epi == ldnn::EPI_DRELU && dgrad_mask->dim() == 2 &&
-                      dgrad_mask->size(0) == B && dgrad_mask->size(1) * 8 >= K && dgrad_mask->stride(1) == 1,
-                  "head: dgrad_mask needs the streaming mode, EPI_DRELU and a [B][>= K/8] byte mask");
-      p.mask = dgrad_mask->data_ptr<uint8_t>();
-      p.ldmask = (int)dgrad_mask->stride(0);
-    }
     p.dgrad_mode = (int)dgrad_mode;
     TORCH_CHECK(dgrad_epi == ldnn::EPI_NONE || dgrad_epi == ldnn::EPI_DRELU || dgrad_epi == ldnn::EPI_DSIGMOID,
                 "head: dgrad_epi must be EPI_NONE / EPI_DRELU / EPI_DSIGMOID");
@@ -1285,7 +1276,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("h"), py::arg("W"), py::arg("bias"), py::arg("labels"), py::arg("logits"), py::arg("dlogits"),
         py::arg("stats"), py::arg("num_classes"), py::arg("grad_scale"), py::arg("dh") = py::none(), py::arg("dbias") = py::none(),
         py::arg("dgrad_epi") = (int64_t)ldnn::EPI_DRELU, py::arg("dbias_ws") = py::none(),
-        py::arg("dgrad_mode") = (int64_t)-1, py::arg("dgrad_mask") = py::none());
+        py::arg("dgrad_mode") = (int64_t)-1);
   m.def("head_dgrad_ws_floats", &ldnn::head_dgrad_ws_floats, py::arg("B"), py::arg("K"));
   m.def("head_wgrad", &head_wgrad, "dW = dz^T h (+ db = colsum dz); splits > 1 accumulate atomically",
         py::arg("dz"), py::arg("h"), py::arg("dW"), py::arg("db") = py::none(), py::arg("splits") = 0);

@@ -294,10 +294,6 @@ struct HeadParams {
   //    global memory; 2: fused, h staged in LDS (1 / 2 need K <= head_dgrad_max_k()
   //    and dbias_ws for dbias)
   int dgrad_mode;
-  // mode 0 with dgrad_epi EPI_DRELU: relu'(h) from the forward's bit mask (mask [B][ldmask]
-  // bytes, bit j of byte (r, c/8) = h[r][c] > 0) instead of re-reading h -- 1/16 of the bytes
-  const uint8_t* mask;
-  int ldmask;
 };
 hipError_t head_fwd_xent(const HeadParams& p, hipStream_t s);
 int head_dgrad_max_k();

@@ -411,9 +411,7 @@ __global__ __launch_bounds__(kWgWaves * 64) void head_wgrad_kernel(HeadWgradPara
 // The column sums are reduced over the workgroup's 8 row lanes in LDS and added
 // with one atomic per column per workgroup.  Two rows per iteration keep 4 loads in
 // flight per lane.
-// MASK (EPI_DRELU only): relu'(h) from the forward's bit mask instead of h -- the stream
-// then reads 8 MB instead of 128 MB at batch 16384 x 4096 (the dh write is the cost left)
-template <int DEPI, bool MASK = false>
+template <int DEPI>
 __global__ __launch_bounds__(256) void head_dgrad_stream_kernel(HeadParams p, int rows_per_block) {
   __shared__ float part[8][256];
   const int cg = threadIdx.x & 31, ty = threadIdx.x >> 5;
@@ -430,7 +428,7 @@ __global__ __launch_bounds__(256) void head_dgrad_stream_kernel(HeadParams p, in
     for (int i = 0; i < 8; ++i) wf[c][i] = bf2f(w[i]);
   }
   float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  auto row_out = [&](const u16x8& g0, const u16x8& g1, const u16x8& hv, uint32_t mb, int r) {
+  auto row_out = [&](const u16x8& g0, const u16x8& g1, const u16x8& hv, int r) {
     float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int c = 0; c < 16; ++c) {
@@ -443,22 +441,14 @@ __global__ __launch_bounds__(256) void head_dgrad_stream_kernel(HeadParams p, in
     for (int i = 0; i < 8; ++i) {
       const float hf = bf2f(hv[i]);
       float x = v[i];
-      if constexpr (MASK) x = ((mb >> i) & 1u) ? x : 0.f;
-      else if constexpr (DEPI == EPI_DRELU) x = hf > 0.f ? x : 0.f;
+      if constexpr (DEPI == EPI_DRELU) x = hf > 0.f ? x : 0.f;
       else if constexpr (DEPI == EPI_DSIGMOID) x *= hf * (1.f - hf);
       o[i] = f2bf(x);
       s[i] += bf2f(o[i]);
     }
     *reinterpret_cast<u16x8*>(p.dh + (size_t)r * p.lddh + c0) = o;
   };
-  auto hrow = [&](int r) -> u16x8 {
-    if constexpr (MASK) return u16x8{};
-    else return *reinterpret_cast<const u16x8*>(p.h + (size_t)r * p.ldh + c0);
-  };
-  auto mrow = [&](int r) -> uint32_t {
-    if constexpr (MASK) return (uint32_t)p.mask[(size_t)r * p.ldmask + (c0 >> 3)];
-    else return 0u;
-  };
+  auto hrow = [&](int r) -> u16x8 { return *reinterpret_cast<const u16x8*>(p.h + (size_t)r * p.ldh + c0); };
   if (cok) {
     int r = r_begin + ty;
     for (; r + 8 < r_end; r += 16) {
@@ -466,13 +456,12 @@ __global__ __launch_bounds__(256) void head_dgrad_stream_kernel(HeadParams p, in
       const u16x8* gp1 = reinterpret_cast<const u16x8*>(p.dlogits + (size_t)(r + 8) * p.ld);
       const u16x8 a0 = gp0[0], a1 = gp0[1], b0 = gp1[0], b1 = gp1[1];
       const u16x8 h0 = hrow(r), h1 = hrow(r + 8);
-      const uint32_t m0 = mrow(r), m1 = mrow(r + 8);
-      row_out(a0, a1, h0, m0, r);
-      row_out(b0, b1, h1, m1, r + 8);
+      row_out(a0, a1, h0, r);
+      row_out(b0, b1, h1, r + 8);
     }
     for (; r < r_end; r += 8) {
       const u16x8* gp0 = reinterpret_cast<const u16x8*>(p.dlogits + (size_t)r * p.ld);
-      row_out(gp0[0], gp0[1], hrow(r), mrow(r), r);
+      row_out(gp0[0], gp0[1], hrow(r), r);
     }
   }
   if (p.dbias == nullptr) return;
@@ -496,12 +485,6 @@ hipError_t launch_head_dgrad_stream(const HeadParams& p, hipStream_t s) {
   int gy = (p.B + 255) / 256;
   if (gy > 256) gy = 256;
   const int rpb = (p.B + gy - 1) / gy;
-  if constexpr (DEPI == EPI_DRELU) {
-    if (p.mask != nullptr) {
-      head_dgrad_stream_kernel<DEPI, true><<<dim3(gx, gy), 256, 0, s>>>(p, rpb);
-      return hipGetLastError();
-    }
-  }
   head_dgrad_stream_kernel<DEPI><<<dim3(gx, gy), 256, 0, s>>>(p, rpb);
   return hipGetLastError();
 }
@@ -545,8 +528,6 @@ hipError_t head_fwd_xent(const HeadParams& p, hipStream_t s) {
   if (p.dh == nullptr) return launch_head_fwd<-1, false>(p, s);
   if (p.lddh % 8 != 0) return hipErrorInvalidValue;
   if (p.dgrad_mode < 0 || p.dgrad_mode > 2 || (p.dgrad_mode == 0 && p.ld != 16)) return hipErrorInvalidValue;
-  if (p.mask != nullptr && (p.dgrad_mode != 0 || p.dgrad_epi != EPI_DRELU || p.ldmask * 8 < p.K))
-    return hipErrorInvalidValue;
   if ((p.dgrad_mode == 1 || p.dgrad_mode == 2) &&
       (p.K > kHeadDgradMaxK || (p.dbias != nullptr && p.dbias_ws == nullptr)))
     return hipErrorInvalidValue;

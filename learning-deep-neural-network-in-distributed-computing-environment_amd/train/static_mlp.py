@@ -98,8 +98,7 @@ class StaticMLPEngine:
                  use_graphs: bool = True, average_grads: bool = True, use_head_kernels: bool = True,
                  shard_optimizer: bool | None = None, wgrad_combine: bool = True, library_gemms: bool | None = None,
                  fuse_head_dgrad: bool | None = None, library_dgrad: bool | None = None, head_dgrad_mode: int = -1,
-                 relu_masks: bool = True, transposed_dgrad: bool = True, bias_ones_column: bool = True,
-                 head_relu_mask: bool = True):
+                 relu_masks: bool = True, transposed_dgrad: bool = True, bias_ones_column: bool = True):
         from ..models.mlp import MLP
 
         if not isinstance(model, MLP):
@@ -204,11 +203,11 @@ class StaticMLPEngine:
         self.head_dgrad = (bool(fuse_head_dgrad) and self.use_head and L >= 2
                            and (npad[-1] == 16 and self.head_dgrad_mode in (-1, 0, 3)
                                 or self.layers[-1].in_features <= self.C.head_dgrad_max_k()))
-        # the streaming head dgrad (<= 16 classes) takes relu'(h_{L-1}) from the forward's bit
-        # mask: it streams 8 MB of mask instead of re-reading the 128 MB activation
-        # (batch 16384 x 4096); the fused modes 1 / 2 keep reading h
+        # (the streaming head dgrad re-reads h_{L-1} for relu': reading a bit mask written by
+        # the previous forward GEMM instead measured ~14 us SLOWER per step at batch 16384 --
+        # the GEMM's byte-wise mask stores cost more than the stream saves,
+        # profiles/r3/head_dgrad_mask_ab_r3.jsonl)
         self._head_stream = self.head_dgrad and npad[-1] == 16 and self.head_dgrad_mode in (-1, 0)
-        self._head_mask = bool(head_relu_mask)
         self._head_db_ws = (torch.empty(self.C.head_dgrad_ws_floats(B, self.layers[-1].in_features),
                                         dtype=torch.float32, device=self.device) if self.head_dgrad else None)
         # [loss_sum, correct] -- one pair per 16-row workgroup of the head kernel
@@ -267,8 +266,7 @@ class StaticMLPEngine:
         self.mask = [None] * (L + 1)
         for l in range(1, L):
             if (relu_masks and self.layers[l - 1].activation == "relu" and not self._lib_fwd[l - 1]
-                    and not self._lib_dgrad[l] and not (self.use_head and l == L - 1 and fuse_head_dgrad
-                                                         and not (self._head_stream and self._head_mask))):
+                    and not self._lib_dgrad[l] and not (self.use_head and l == L - 1 and fuse_head_dgrad)):
                 self.mask[l] = torch.zeros(B, (npad[l - 1] + 7) // 8, dtype=torch.uint8, device=dev)
         self._db0_from_wgrad = False
         # transposed_dgrad: dgrad(l) reads a transposed bf16 copy of W_l, refreshed by one
@@ -369,11 +367,10 @@ class StaticMLPEngine:
         L = len(self.layers)
         if self.use_head:   # last Linear + softmax-xent + argmax (+ the head's dgrad) in one launch
             if self.head_dgrad:
-                mk = self.mask[L - 1] if (self._head_stream and self._dgrad_epi[L - 1] == self.C.EPI_DRELU) else None
                 self.C.head_fwd_xent(self.h[L - 1], self.W[L - 1], self.bias[L - 1], self.labels, self.h[L],
                                      self.dz[L], self.stats, self.num_classes, 1.0 / self.B, dh=self.dz[L - 1],
                                      dbias=self.db[L - 2], dgrad_epi=self._dgrad_epi[L - 1],
-                                     dbias_ws=self._head_db_ws, dgrad_mode=self.head_dgrad_mode, dgrad_mask=mk)
+                                     dbias_ws=self._head_db_ws, dgrad_mode=self.head_dgrad_mode)
                 return
             self.C.head_fwd_xent(self.h[L - 1], self.W[L - 1], self.bias[L - 1], self.labels, self.h[L], self.dz[L],
                                  self.stats, self.num_classes, 1.0 / self.B)
@@ -733,9 +730,7 @@ class StaticMLPEngine:
                 d[f"fwd{l}"] = "ldnn head_fwd_xent (Linear + softmax-xent + argmax)"
                 d[f"wgrad{l}"] = "ldnn head_wgrad"
                 if self.head_dgrad:
-                    d[f"dgrad{l}"] = (("ldnn head_dgrad_stream (dReLU from bit mask + bias-gradient sums)"
-                                       if self.mask[l] is not None else
-                                       "ldnn head_dgrad_stream (dReLU + bias-gradient sums)") if self._head_stream
+                    d[f"dgrad{l}"] = ("ldnn head_dgrad_stream (dReLU + bias-gradient sums)" if self._head_stream
                                       else "ldnn head_fwd_xent fused dgrad")
                 continue
             d[f"fwd{l}"] = ("hipBLASLt" if self._lib_fwd[l] else

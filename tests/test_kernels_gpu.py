@@ -444,31 +444,3 @@ def test_act_bwd_colsum_matches_fp32(act, inplace, accumulate, rows, cols):
     ref_out = ref_dx.sum(0) + (base if accumulate else 0)
     torch.testing.assert_close(out, ref_out, rtol=1e-3, atol=1e-3 * (rows ** 0.5))
 
-
-@pytest.mark.parametrize("B,K", [(4096, 4096), (1000, 784), (70, 520)])
-def test_head_dgrad_stream_from_relu_bit_mask(B, K):
-    """The streaming head dgrad reading relu'(h) from the forward's bit mask (1 bit per
-    activation) == the same kernel reading h: bit-identical dh and bias gradient."""
-    torch.manual_seed(5)
-    h = torch.randn(B, K, device="cuda").relu().bfloat16()
-    ncls, ld = 10, 16
-    W = torch.zeros(ld, K, device="cuda")
-    W[:ncls] = torch.randn(ncls, K, device="cuda") * K ** -0.5
-    W = W.bfloat16()
-    bias = torch.zeros(ld, device="cuda")
-    y = torch.randint(0, ncls, (B,), device="cuda")
-    bits = (h.float() > 0).to(torch.uint8).view(B, K // 8, 8)
-    mask = (bits << torch.arange(8, device="cuda", dtype=torch.uint8)).sum(-1).to(torch.uint8).contiguous()
-    cc = C()
-    outs = []
-    for mk in (None, mask):
-        dl = torch.empty(B, ld, device="cuda", dtype=torch.bfloat16)
-        st = torch.zeros((B + 15) // 16, 2, device="cuda")
-        dh = torch.full((B, K), 7.0, device="cuda").bfloat16()
-        db = torch.zeros(K, device="cuda")
-        cc.head_fwd_xent(h, W, bias, y, None, dl, st, ncls, 1.0 / B, dh=dh, dbias=db, dgrad_epi=cc.EPI_DRELU,
-                         dgrad_mode=0, dgrad_mask=mk)
-        outs.append((dh, db))
-    torch.cuda.synchronize()
-    assert torch.equal(outs[0][0], outs[1][0])
-    torch.testing.assert_close(outs[0][1], outs[1][1], rtol=1e-5, atol=1e-6)
