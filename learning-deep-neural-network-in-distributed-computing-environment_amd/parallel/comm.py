@@ -141,20 +141,13 @@ class TorchComm(Comm):
         cannot map each other's memory."""
         from .ipc import OneShotAllReduce
 
-        try:
-            os_ = OneShotAllReduce(max_bytes, group=self.group, device=device)
-            ok = os_.self_test() if self_test else True
-        except Exception as e:  # noqa: BLE001 -- IPC mapping refused: keep RCCL
-            import warnings
-
-            warnings.warn(f"one-shot IPC all-reduce unavailable ({e!r}); using RCCL for every message")
-            flag = torch.zeros(1, device=device or torch.device("cuda", torch.cuda.current_device()))
-            dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)   # (matches self_test's collective)
-            return None
+        os_ = OneShotAllReduce(max_bytes, group=self.group, device=device)   # never raises; collective
+        ok = os_.self_test() if self_test else os_.connect_error is None
         if not ok:
             import warnings
 
-            warnings.warn("one-shot IPC all-reduce failed its self-test on some rank; using RCCL for every message")
+            warnings.warn(f"one-shot IPC all-reduce unavailable or failed its self-test on some rank "
+                          f"({os_.connect_error!r} here); using RCCL for every message")
             return None
         self.oneshot = os_
         return os_

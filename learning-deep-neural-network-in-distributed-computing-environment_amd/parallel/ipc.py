@@ -34,6 +34,10 @@ from ..ops import _ext
 
 class OneShotAllReduce:
     def __init__(self, max_bytes: int = 4 << 20, group=None, device: torch.device | None = None, blocks: int = 64):
+        """Collective.  Every rank runs the same collective sequence whatever fails
+        locally (allocation, IPC export / import): one all_gather_object + one barrier
+        here, then self_test()'s three all-reduces -- a rank whose setup failed takes
+        part with ok = False and the path is then off on every rank."""
         self.group = group
         self.rank = dist.get_rank(group)
         self.world_size = dist.get_world_size(group)
@@ -41,15 +45,22 @@ class OneShotAllReduce:
             device = torch.device("cuda", torch.cuda.current_device())
         self.device = device
         self.max_bytes = int(max_bytes)
-        self._c = _ext.C().OneShotComm(self.rank, self.world_size, self.max_bytes, device.index, blocks)
-        mine = tuple(bytes(h) for h in self._c.handles())
-        allh: list = [None] * self.world_size
-        dist.all_gather_object(allh, mine, group=group)  # the one host exchange: IPC handles
         self.connect_error = None
+        self._c, mine = None, None
         try:
-            self._c.connect([(a, b) for a, b in allh])
+            self._c = _ext.C().OneShotComm(self.rank, self.world_size, self.max_bytes, device.index, blocks)
+            mine = tuple(bytes(h) for h in self._c.handles())
         except Exception as e:  # noqa: BLE001 -- reported by self_test on every rank
             self.connect_error = e
+        allh: list = [None] * self.world_size
+        dist.all_gather_object(allh, mine, group=group)  # the one host exchange: IPC handles
+        if self.connect_error is None and any(h is None for h in allh):
+            self.connect_error = RuntimeError("a peer rank could not export its IPC buffers")
+        if self.connect_error is None:
+            try:
+                self._c.connect([(a, b) for a, b in allh])
+            except Exception as e:  # noqa: BLE001
+                self.connect_error = e
         dist.barrier(group=group)  # every rank mapped every peer before the first kernel
 
     def eligible(self, t: torch.Tensor) -> bool:
@@ -68,7 +79,7 @@ class OneShotAllReduce:
 
     def self_test(self) -> bool:
         """Collective: True on every rank iff the kernel summed correctly on every rank."""
-        ok = self.connect_error is None
+        ok = self._agree(self.connect_error is None)   # no kernel waits on a peer that failed to map
         for dt in (torch.float32, torch.bfloat16):
             n = 4096
             t = (torch.arange(n, device=self.device, dtype=torch.float32) % 7 + self.rank + 1).to(dt)
@@ -79,6 +90,9 @@ class OneShotAllReduce:
                 self.all_reduce(u)
                 torch.cuda.synchronize(self.device)
                 ok = ok and not self._c.error() and torch.allclose(u.float(), ref, rtol=1e-2 if dt != torch.float32 else 0)
+        return self._agree(ok)
+
+    def _agree(self, ok: bool) -> bool:
         flag = torch.tensor([1.0 if ok else 0.0], device=self.device)
         dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)
         return bool(flag.item() == 1.0)

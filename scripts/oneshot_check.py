@@ -27,6 +27,8 @@ def main():
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     os_ = OneShotAllReduce(1 << 20, device=dev, blocks=32)
+    if os_.connect_error is not None:
+        raise os_.connect_error
     ok = True
     for it in range(50):
         for dt, numel in ((torch.float32, 1 << 16), (torch.bfloat16, 4096 + 8), (torch.float32, 8)):

@@ -262,3 +262,44 @@ def test_per_step_weighted_allreduce_three_ranks():
     for r, err_g, err_p in res:
         assert err_g < 1e-5, res
         assert err_p < 1e-6, res
+
+
+def _oneshot_setup_worker(rank, world, port, q):
+    _init(rank, world, port, timeout=30)
+    import ldnn  # noqa: F401
+    from ldnn.parallel import ipc
+    from ldnn.parallel.comm import TorchComm
+
+    class _Fake:
+        def __init__(self, r, *a):
+            if r == 1:   # this rank's allocation / export fails
+                raise RuntimeError("hipExtMallocWithFlags failed")
+
+        def handles(self):
+            return (b"s", b"g")
+
+        def connect(self, h):
+            pass
+
+    class _C:
+        OneShotComm = _Fake
+
+    ipc._ext.C = lambda: _C()
+    import warnings
+
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        got = TorchComm().enable_oneshot(1 << 20, device=torch.device("cpu"))
+    q.put((rank, got is None, any("one-shot" in str(x.message) for x in w)))
+    dist.destroy_process_group()
+
+
+def test_oneshot_setup_failure_on_one_rank_disables_everywhere_without_hanging():
+    """a rank whose one-shot setup fails must take part in the same
+    collective sequence as the others (no mismatched collectives, no hang); the path
+    ends up off on every rank with a warning."""
+    world, port = 2, _port()
+    q = mp.get_context("spawn").SimpleQueue()
+    mp.spawn(_oneshot_setup_worker, args=(world, port, q), nprocs=world, join=True)
+    res = sorted(q.get() for _ in range(world))
+    assert res == [(0, True, True), (1, True, True)]
