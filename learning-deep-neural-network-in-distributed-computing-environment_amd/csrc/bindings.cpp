@@ -50,7 +50,8 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c_in, bool
           int64_t epi, const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& aux,
           const c10::optional<at::Tensor>& dbias, double beta, int64_t tile, int64_t splitk, bool direct_epi,
           int64_t variant, const c10::optional<at::Tensor>& ws, const c10::optional<at::Tensor>& cnt,
-          const c10::optional<at::Tensor>& mask_out, const c10::optional<at::Tensor>& mask_in) {
+          const c10::optional<at::Tensor>& mask_out, const c10::optional<at::Tensor>& mask_in,
+          const c10::optional<at::Tensor>& head_w, const c10::optional<at::Tensor>& head_part) {
   check_dev(a, at::kBFloat16, "a");
   check_dev(b, at::kBFloat16, "b");
   TORCH_CHECK(c_in.is_cuda() && (c_in.scalar_type() == at::kBFloat16 || c_in.scalar_type() == at::kFloat),
@@ -118,6 +119,26 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c_in, bool
     }
     force_q = true;
   }
+  if (head_w.has_value() || head_part.has_value()) {
+    // bias + ReLU forward with the classifier head's partial logits (EPI_BIAS_RELU_HEAD)
+    TORCH_CHECK(head_w.has_value() && head_part.has_value(), "gemm: head_w and head_part go together");
+    TORCH_CHECK(epi == ldnn::EPI_BIAS_RELU && !out_f32 && a_kcontig && b_kcontig && !slabs && !dbias.has_value() &&
+                    !mask_out.has_value() && !mask_in.has_value() && splitk <= 1 && beta == 0.0,
+                "gemm: head partials need EPI_BIAS_RELU, bf16 out, k-contiguous operands, no split-K / masks / dbias");
+    check_dev(*head_w, at::kBFloat16, "head_w");
+    check_dev(*head_part, at::kFloat, "head_part");
+    TORCH_CHECK(head_w->dim() == 2 && head_w->size(0) == 16 && head_w->size(1) >= N && head_w->stride(1) == 1 &&
+                    head_w->stride(0) % 4 == 0 && ((uintptr_t)head_w->data_ptr() & 7) == 0,
+                "gemm: head_w must be [16][>= N] bf16 (classes zero-padded to 16), 8-B aligned rows");
+    TORCH_CHECK(head_part->is_contiguous() && head_part->dim() == 3 && head_part->size(0) == (N + 255) / 256 &&
+                    head_part->size(1) == M && head_part->size(2) == 16 && aligned16(head_part->data_ptr()),
+                "gemm: head_part must be a dense [ceil(N / 256)][M][16] fp32 tensor");
+    p.head_w = bf16_ptr(*head_w);
+    p.ldhw = (int)head_w->stride(0);
+    p.head_part = head_part->data_ptr<float>();
+    epi = ldnn::EPI_BIAS_RELU_HEAD;
+    force_q = true;
+  }
   if (epi == ldnn::EPI_DRELU || epi == ldnn::EPI_DSIGMOID) {
     TORCH_CHECK(aux.has_value(), "gemm: derivative epilogue needs the saved activation");
     check_dev(*aux, at::kBFloat16, "aux");
@@ -129,6 +150,9 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c_in, bool
   if (dbias.has_value()) {
     check_dev(*dbias, at::kFloat, "dbias");
     TORCH_CHECK(dbias->is_contiguous() && dbias->numel() >= N, "gemm: bad dbias");
+    TORCH_CHECK(!(epi == ldnn::EPI_BIAS || epi == ldnn::EPI_BIAS_RELU || epi == ldnn::EPI_BIAS_SIGMOID ||
+                  epi == ldnn::EPI_BIAS_RELU_MASK),
+                "gemm: dbias (output column sums) goes with the dgrad / plain epilogues, not a bias forward");
     p.dbias = dbias->data_ptr<float>();
   }
   const bool skinny_ok = a_kcontig && b_kcontig && !out_f32 && N <= 64 && !dbias.has_value() && beta == 0.0 &&
@@ -560,6 +584,84 @@ void head_fwd_xent(const at::Tensor& h, const at::Tensor& W, const at::Tensor& b
   }
   c10::hip::HIPGuardMasqueradingAsCUDA g(h.device());
   check(ldnn::head_fwd_xent(p, cur_stream(h)), "head_fwd_xent");
+}
+
+// Softmax-xent from the partial logits of an EPI_BIAS_RELU_HEAD forward (gemm head_part)
+void head_xent_parts(const at::Tensor& parts, const at::Tensor& bias, const at::Tensor& labels,
+                     const c10::optional<at::Tensor>& logits, const at::Tensor& dlogits, const at::Tensor& stats,
+                     int64_t num_classes, double grad_scale) {
+  check_dev(parts, at::kFloat, "parts");
+  check_dev(bias, at::kFloat, "bias");
+  check_dev(labels, at::kLong, "labels");
+  check_dev(dlogits, at::kBFloat16, "dlogits");
+  check_dev(stats, at::kFloat, "stats");
+  TORCH_CHECK(parts.dim() == 3 && parts.is_contiguous() && parts.size(2) == 16 && aligned16(parts.data_ptr()),
+              "head_xent_parts: parts must be a dense [nparts][B][16] fp32 tensor");
+  const int64_t B = parts.size(1);
+  TORCH_CHECK(dlogits.is_contiguous() && dlogits.dim() == 2 && dlogits.size(0) == B && dlogits.size(1) == 16,
+              "head_xent_parts: dlogits must be a contiguous [B][16] buffer");
+  TORCH_CHECK(num_classes >= 1 && num_classes <= 16, "head_xent_parts: 1..16 classes");
+  TORCH_CHECK(bias.is_contiguous() && bias.numel() >= 16 && aligned16(bias.data_ptr()), "head_xent_parts: bias padded to 16");
+  TORCH_CHECK(labels.is_contiguous() && labels.numel() == B, "head_xent_parts: bad labels");
+  TORCH_CHECK(stats.is_contiguous() && stats.numel() >= 2 * ((B + 15) / 16), "head_xent_parts: stats needs 2 floats per 16 rows");
+  ldnn::HeadParams p{};
+  p.bias = bias.data_ptr<float>();
+  p.labels = labels.data_ptr<int64_t>();
+  if (logits.has_value()) {
+    check_dev(*logits, at::kBFloat16, "logits");
+    TORCH_CHECK(logits->is_contiguous() && logits->sizes() == dlogits.sizes(), "head_xent_parts: logits like dlogits");
+    p.logits = bf16_mut(*logits);
+  }
+  p.dlogits = bf16_mut(dlogits);
+  p.stats = stats.data_ptr<float>();
+  p.B = (int)B;
+  p.C = (int)num_classes;
+  p.ld = 16;
+  p.grad_scale = (float)grad_scale;
+  c10::hip::HIPGuardMasqueradingAsCUDA g(parts.device());
+  check(ldnn::head_xent_parts(p, parts.data_ptr<float>(), (int)parts.size(0), cur_stream(parts)), "head_xent_parts");
+}
+
+// dh = (dlogits W) * act'(h) and dbias += column sums of dh (the streaming head dgrad alone)
+void head_dgrad_stream(const at::Tensor& h, const at::Tensor& W, const at::Tensor& dlogits, const at::Tensor& dh,
+                       const c10::optional<at::Tensor>& dbias, int64_t dgrad_epi) {
+  check_dev(h, at::kBFloat16, "h");
+  check_dev(W, at::kBFloat16, "W");
+  check_dev(dlogits, at::kBFloat16, "dlogits");
+  check_dev(dh, at::kBFloat16, "dh");
+  const int64_t B = h.size(0), K = h.size(1);
+  TORCH_CHECK(h.dim() == 2 && h.stride(1) == 1 && h.stride(0) % 8 == 0 && K % 8 == 0 && aligned16(h.data_ptr()),
+              "head_dgrad_stream: h must be [B][K] with 16-B aligned rows");
+  TORCH_CHECK(W.dim() == 2 && W.size(0) <= 16 && W.size(1) == K && W.stride(1) == 1 && W.stride(0) % 8 == 0 &&
+                  aligned16(W.data_ptr()),
+              "head_dgrad_stream: W must be [<= 16][K] with 16-B aligned rows");
+  TORCH_CHECK(dlogits.is_contiguous() && dlogits.dim() == 2 && dlogits.size(0) == B && dlogits.size(1) == 16,
+              "head_dgrad_stream: dlogits must be a contiguous [B][16] buffer");
+  TORCH_CHECK(dh.dim() == 2 && dh.size(0) == B && dh.size(1) == K && dh.stride(1) == 1 && dh.stride(0) % 8 == 0 &&
+                  aligned16(dh.data_ptr()),
+              "head_dgrad_stream: dh must be [B][K] with 16-B aligned rows");
+  TORCH_CHECK(dgrad_epi == ldnn::EPI_NONE || dgrad_epi == ldnn::EPI_DRELU || dgrad_epi == ldnn::EPI_DSIGMOID,
+              "head_dgrad_stream: dgrad_epi must be EPI_NONE / EPI_DRELU / EPI_DSIGMOID");
+  ldnn::HeadParams p{};
+  p.h = bf16_ptr(h);
+  p.W = bf16_ptr(W);
+  p.dlogits = bf16_mut(dlogits);
+  p.B = (int)B;
+  p.K = (int)K;
+  p.ld = 16;
+  p.ldh = (int)h.stride(0);
+  p.ldw = (int)W.stride(0);
+  p.ldw_rows = (int)W.size(0);
+  p.dh = bf16_mut(dh);
+  p.lddh = (int)dh.stride(0);
+  p.dgrad_epi = (int)dgrad_epi;
+  if (dbias.has_value()) {
+    check_dev(*dbias, at::kFloat, "dbias");
+    TORCH_CHECK(dbias->is_contiguous() && dbias->numel() >= K, "head_dgrad_stream: bad dbias");
+    p.dbias = dbias->data_ptr<float>();
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA g(h.device());
+  check(ldnn::head_dgrad_stream(p, cur_stream(h)), "head_dgrad_stream");
 }
 
 void head_wgrad(const at::Tensor& dz, const at::Tensor& h, const at::Tensor& dW, const c10::optional<at::Tensor>& db,
@@ -1132,7 +1234,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("aux") = py::none(), py::arg("dbias") = py::none(), py::arg("beta") = 0.0,
         py::arg("tile") = 0, py::arg("splitk") = 0, py::arg("direct_epi") = false, py::arg("variant") = 0,
         py::arg("ws") = py::none(), py::arg("cnt") = py::none(), py::arg("mask_out") = py::none(),
-        py::arg("mask_in") = py::none());
+        py::arg("mask_in") = py::none(), py::arg("head_w") = py::none(), py::arg("head_part") = py::none());
   m.def("nchw_to_nhwc", [](const at::Tensor& src, const at::Tensor& dst) {
         TORCH_CHECK(src.is_cuda() && src.dim() == 4 && src.is_contiguous() &&
                         (src.scalar_type() == at::kFloat || src.scalar_type() == at::kBFloat16),
@@ -1278,6 +1380,12 @@ PYBIND11_MODULE(_C, m) {
         py::arg("dgrad_epi") = (int64_t)ldnn::EPI_DRELU, py::arg("dbias_ws") = py::none(),
         py::arg("dgrad_mode") = (int64_t)-1);
   m.def("head_dgrad_ws_floats", &ldnn::head_dgrad_ws_floats, py::arg("B"), py::arg("K"));
+  m.def("head_xent_parts", &head_xent_parts, "softmax-xent + argmax from EPI_BIAS_RELU_HEAD partial logits",
+        py::arg("parts"), py::arg("bias"), py::arg("labels"), py::arg("logits"), py::arg("dlogits"), py::arg("stats"),
+        py::arg("num_classes"), py::arg("grad_scale"));
+  m.def("head_dgrad_stream", &head_dgrad_stream, "streaming head dgrad: dh = (dlogits W) * act'(h), dbias += colsums",
+        py::arg("h"), py::arg("W"), py::arg("dlogits"), py::arg("dh"), py::arg("dbias") = py::none(),
+        py::arg("dgrad_epi") = (int64_t)ldnn::EPI_DRELU);
   m.def("head_wgrad", &head_wgrad, "dW = dz^T h (+ db = colsum dz); splits > 1 accumulate atomically",
         py::arg("dz"), py::arg("h"), py::arg("dW"), py::arg("db") = py::none(), py::arg("splits") = 0);
   m.def("head_dgrad_max_k", &ldnn::head_dgrad_max_k);

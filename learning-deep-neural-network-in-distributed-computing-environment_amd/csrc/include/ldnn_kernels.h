@@ -23,6 +23,11 @@ enum Epilogue : int {
   // beside the activation; the dgrad reads mask_in instead of 16 B of aux per 8 columns
   EPI_BIAS_RELU_MASK = 8,
   EPI_DRELU_MASK = 9,
+  // four-wave kernel only, bf16 out, no split-K: bias + ReLU forward of the last hidden
+  // layer that also multiplies its output tile by the classifier head's weight
+  // (head_w, <= 16 classes) on the MFMA pipe: head_part[n0 / 256][m][0..15] = the
+  // tile's partial logits (summed by head_xent_parts)
+  EPI_BIAS_RELU_HEAD = 10,
 };
 
 // Fused optimizer epilogue: gradient element (m, n) updates master[m*ldc + n].
@@ -58,6 +63,9 @@ struct GemmParams {
   uint8_t* mask_out;       // EPI_BIAS_RELU_MASK: [M][ldmask] ReLU bits
   const uint8_t* mask_in;  // EPI_DRELU_MASK: [M][ldmask] ReLU bits of the saved activation
   int ldmask;              // bytes per mask row (>= N / 8)
+  const uint16_t* head_w;  // EPI_BIAS_RELU_HEAD: [16][ldhw] bf16 head weight (rows >= classes zero)
+  float* head_part;        // EPI_BIAS_RELU_HEAD: [ceil(N / 256)][M][16] fp32 partial logits
+  int ldhw;
 };
 // Workspace of the in-launch split-K combine of a 128-tile GEMM (bytes; counters = tiles).
 size_t gemm_splitk_ws_bytes(int M, int N, int splitk);
@@ -296,6 +304,13 @@ struct HeadParams {
   int dgrad_mode;
 };
 hipError_t head_fwd_xent(const HeadParams& p, hipStream_t s);
+// Softmax-xent + argmax of logits = bias + sum_s parts[s][b][0..15] (the partial logits
+// of an EPI_BIAS_RELU_HEAD forward, ld == 16): writes logits / dlogits / stats exactly
+// like head_fwd_xent (p.h / p.W unused).
+hipError_t head_xent_parts(const HeadParams& p, const float* parts, int nparts, hipStream_t s);
+// The streaming head dgrad alone (head_fwd_xent's dgrad_mode 0 second launch):
+// dh = (dlogits W) * act'(h), dbias += column sums of dh; needs ld == 16.
+hipError_t head_dgrad_stream(const HeadParams& p, hipStream_t s);
 int head_dgrad_max_k();
 size_t head_dgrad_ws_floats(int B, int K);
 // out[i] = sum_s ws[s][i] (+ beta * out[i]) over n4 float4 columns and `splits` slabs

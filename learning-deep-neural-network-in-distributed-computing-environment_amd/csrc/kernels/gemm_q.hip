@@ -199,6 +199,8 @@ __device__ __forceinline__ void epilogue_q(const GemmParams& p, floatx4 (&acc)[8
       }
     }
   }
+  // bias-gradient column sums: dgrad / plain epilogues only (a forward never has a dbias)
+  constexpr bool kSums = !kBias && EPI != EPI_BIAS_RELU_HEAD;
   float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
@@ -252,17 +254,19 @@ __device__ __forceinline__ void epilogue_q(const GemmParams& p, floatx4 (&acc)[8
         }
         *reinterpret_cast<floatx4*>(c) = w0;
         *reinterpret_cast<floatx4*>(c + 4) = w1;
+        if constexpr (kSums) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          cs[q] += w0[q];
-          cs[q + 4] += w1[q];
+          for (int q = 0; q < 4; ++q) {
+            cs[q] += w0[q];
+            cs[q + 4] += w1[q];
+          }
         }
       } else {
         u16x8 ob;
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
           ob[q] = f2bf(o[q]);
-          cs[q] += bf2f(ob[q]);
+          if constexpr (kSums) cs[q] += bf2f(ob[q]);
         }
         u16x8* dst = reinterpret_cast<u16x8*>(reinterpret_cast<bf16_t*>(p.C) + (size_t)m * p.ldc + n);
         if (p.variant & 4096) __builtin_nontemporal_store(ob, dst);
@@ -277,7 +281,7 @@ __device__ __forceinline__ void epilogue_q(const GemmParams& p, floatx4 (&acc)[8
     }
     __builtin_amdgcn_wave_barrier();
   }
-  if (p.dbias != nullptr) {
+  if (kSums && p.dbias != nullptr) {
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       float t = cs[q];
@@ -288,6 +292,114 @@ __device__ __forceinline__ void epilogue_q(const GemmParams& p, floatx4 (&acc)[8
     if (lane < 16 && nok) {
 #pragma unroll
       for (int q = 0; q < 8; ++q) atomicAdd(p.dbias + n + q, cs[q]);
+    }
+  }
+}
+
+// EPI_BIAS_RELU_HEAD epilogue: the activation is finished in the MFMA accumulator
+// layout and the wave's 128 x 128 block of it is multiplied by the classifier head's
+// weight on the MFMA pipe (32 MFMAs: 16 classes x 128 rows) before it is stored.
+//  * bias + ReLU + bf16: one packed add per 2 values, one v_cvt_pk_bf16_f32 per 2,
+//    ReLU as a packed int16 max on the bf16 bits (negative bf16 <=> negative int16;
+//    rounding is monotone, so max(bf16(v), 0) == bf16(max(v, 0))).
+//  * The accumulator layout is fed to the MFMA as is: lane (g = l >> 4, r16 = l & 15)
+//    of m-tile i holds row i*16 + r16 at columns 32t + 4g + {0..3} (n-tile 2t) and
+//    32t + 16 + 4g + {0..3} (n-tile 2t+1), so k-slot 8g + e of k-step t means exactly
+//    those columns, and the head weight fragment is loaded with the same permutation
+//    (two 8-B pieces per class row).
+//  * The two column halves of the workgroup (wn = 0, 1) combine their partial
+//    logits in the wn = 0 wave's LDS slice; wn = 0 stores head_part[n0 / 256][m][c].
+//  * The bf16 tile is staged in the wave's own 32 KiB slice (all 128 rows at once,
+//    16-B chunks XOR-swizzled by row) and re-read row-wise for full 256-B row stores:
+//    no VALU work left in the store phase.
+__device__ __forceinline__ void epilogue_head(const GemmParams& p, floatx4 (&acc)[8][8], char* smem, int wid, int mbase,
+                                              int nbase, int lane) {
+  typedef short s16x2 __attribute__((ext_vector_type(2)));
+  const int g = lane >> 4, r16 = lane & 15;
+  floatx4 bias[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int n = nbase + j * 16 + 4 * g;
+    bias[j] = n < p.N ? *reinterpret_cast<const floatx4*>(p.bias + n) : floatx4{0.f, 0.f, 0.f, 0.f};
+  }
+  bf16x8 wf[4];
+  const bf16_t* wrow = p.head_w + (size_t)r16 * p.ldhw;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int nlo = nbase + 32 * t + 4 * g, nhi = nlo + 16;
+    const bf16x4 zero = {};
+    const bf16x4 lo = nlo < p.N ? *reinterpret_cast<const bf16x4*>(wrow + nlo) : zero;
+    const bf16x4 hi = nhi < p.N ? *reinterpret_cast<const bf16x4*>(wrow + nhi) : zero;
+    wf[t] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  }
+  // packed bf16 activations, [n-tile j][m-tile i]: 4 values = 2 dwords
+  uint32_t hq[8][8][2];
+  const s16x2 zero2 = {0, 0};
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const floatx4 v = acc[j][i] + bias[j];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+        const bf16x2 pb = {(__bf16)v[2 * h], (__bf16)v[2 * h + 1]};
+        const s16x2 r = __builtin_elementwise_max(__builtin_bit_cast(s16x2, pb), zero2);
+        hq[j][i][h] = __builtin_bit_cast(uint32_t, r);
+      }
+    }
+  floatx4 d[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    d[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const u32x4 q = {hq[2 * t][i][0], hq[2 * t][i][1], hq[2 * t + 1][i][0], hq[2 * t + 1][i][1]};
+      d[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[t], __builtin_bit_cast(bf16x8, q), d[i], 0, 0, 0);
+    }
+  }
+  const int wm = wid >> 1, wn = wid & 1;
+  floatx4* xch = reinterpret_cast<floatx4*>(smem + (2 * wm) * 32768);  // the wn = 0 wave's slice
+  if (wn == 1) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) xch[i * 64 + lane] = d[i];
+  }
+  barrier();
+  if (wn == 0) {
+    float* part = p.head_part + (size_t)(nbase / 256) * p.M * 16;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int m = mbase + i * 16 + r16;
+      const floatx4 v = d[i] + xch[i * 64 + lane];
+      if (m < p.M) *reinterpret_cast<floatx4*>(part + (size_t)m * 16 + 4 * g) = v;
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // reads of the slice done before this wave stages into it
+  }
+  // stage: row i*16 + r16 (256 B), 8-B piece (j*16 + 4g) * 2 B within 16-B chunk 2j + (g >> 1)
+  char* wbuf = smem + wid * 32768;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int row = i * 16 + r16;
+      const int chunk = 2 * j + (g >> 1);
+      *reinterpret_cast<uint2*>(wbuf + row * 256 + ((chunk ^ (row & 15)) << 4) + (g & 1) * 8) =
+          uint2{hq[j][i][0], hq[j][i][1]};
+    }
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
+  const int c8 = lane & 15;
+  const int n = nbase + c8 * 8;
+  if (n >= p.N) return;
+#pragma unroll
+  for (int it = 0; it < 32; ++it) {
+    const int row = it * 4 + (lane >> 4);
+    const int m = mbase + row;
+    const u16x8 v = *reinterpret_cast<const u16x8*>(wbuf + row * 256 + ((c8 ^ (row & 15)) << 4));
+    if (m < p.M) {
+      u16x8* dst = reinterpret_cast<u16x8*>(reinterpret_cast<bf16_t*>(p.C) + (size_t)m * p.ldc + n);
+      if (p.variant & 4096) __builtin_nontemporal_store(v, dst);
+      else *dst = v;
     }
   }
 }
@@ -424,7 +536,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(GemmParams p) {
   }
   if constexpr (EPI != EPI_OPT_SGD && EPI != EPI_OPT_ADAM) {
     barrier();  // every wave is done with the operand stages: LDS belongs to the epilogue
-    epilogue_q<EPI, OUT_F32>(pe, acc, smem, wid, m0 + wm * 128, n0 + wn * 128, lane);
+    if constexpr (EPI == EPI_BIAS_RELU_HEAD) epilogue_head(pe, acc, smem, wid, m0 + wm * 128, n0 + wn * 128, lane);
+    else epilogue_q<EPI, OUT_F32>(pe, acc, smem, wid, m0 + wm * 128, n0 + wn * 128, lane);
   } else {
     epilogue<EPI, OUT_F32, 8, 8>(p, acc, m0 + wm * 128, n0 + wn * 128, lane);
   }
@@ -473,6 +586,12 @@ hipError_t dispatch_epi(const GemmParams& p, int epi, hipStream_t s) {
         break;
       }
       return hipErrorInvalidValue;
+    case EPI_BIAS_RELU_HEAD:
+      if constexpr (A_KC && B_KC && !OUT_F32) {
+        gemm_kernel<true, true, EPI_BIAS_RELU_HEAD, false><<<grid, block, 0, s>>>(p);
+        break;
+      }
+      return hipErrorInvalidValue;
     case EPI_OPT_SGD:
       if constexpr (OUT_F32) {
         gemm_kernel<A_KC, B_KC, EPI_OPT_SGD, true><<<grid, block, 0, s>>>(p);
@@ -507,6 +626,10 @@ hipError_t gemm_q(const GemmParams& p, bool a_kc, bool b_kc, int epi, bool out_f
   if (p.splitk > 1 && p.c_split_stride == 0 && (p.ws == nullptr || p.cnt == nullptr)) return hipErrorInvalidValue;
   if ((epi == EPI_BIAS_RELU_MASK && p.mask_out == nullptr) || (epi == EPI_DRELU_MASK && p.mask_in == nullptr) ||
       ((epi == EPI_BIAS_RELU_MASK || epi == EPI_DRELU_MASK) && (p.ldmask * 8 < p.N || p.N % 8 != 0)))
+    return hipErrorInvalidValue;
+  if (epi == EPI_BIAS_RELU_HEAD &&
+      (p.head_w == nullptr || p.head_part == nullptr || p.bias == nullptr || p.splitk > 1 || p.ldhw < p.N ||
+       p.ldhw % 4 != 0 || p.N % 8 != 0 || ((uintptr_t)p.head_w & 7) != 0 || ((uintptr_t)p.head_part & 15) != 0))
     return hipErrorInvalidValue;
   if (a_kc) {
     if (b_kc) return out_f32 ? kq::dispatch_epi<true, true, true>(p, epi, s) : kq::dispatch_epi<true, true, false>(p, epi, s);

@@ -63,13 +63,14 @@ __device__ __forceinline__ int hs_off(int r, int q, int K) {
   return r * ((K + 127) & ~127) * 2 + ((q ^ (r & 15)) << 4);
 }
 
+// (acc: this wave's logits before the bias; red: nred more partial sums to add first;
+// slot: the [loss, correct] pair of these 16 rows)
 template <int NT, bool DG>
 __device__ __forceinline__ void head_softmax_xent(const HeadParams& p, floatx4 (&acc)[NT], floatx4 (*red)[NT][64],
-                                                  float* dls, int lane, int row, int m0) {
+                                                  int nred, float* dls, int lane, int row, int slot) {
 #pragma unroll
   for (int j = 0; j < NT; ++j)
-#pragma unroll
-    for (int q = 0; q < kFwdWaves - 1; ++q) acc[j] += red[q][j][lane];
+    for (int q = 0; q < nred; ++q) acc[j] += red[q][j][lane];
 
   // lane: row m0 + (lane & 15), classes c = j*16 + 4*(lane >> 4) + r
   const bool rok = row < p.B;
@@ -155,8 +156,8 @@ __device__ __forceinline__ void head_softmax_xent(const HeadParams& p, floatx4 (
     corr += __shfl_xor(corr, o, 64);
   }
   if (lane == 0) {  // this workgroup's own slot: plain read-modify-write, replay-safe
-    p.stats[2 * blockIdx.x] += loss;
-    p.stats[2 * blockIdx.x + 1] += corr;
+    p.stats[2 * slot] += loss;
+    p.stats[2 * slot + 1] += corr;
   }
 }
 
@@ -255,11 +256,40 @@ __global__ __launch_bounds__(kFwdWaves * 64) void head_fwd_xent_kernel(HeadParam
     for (int j = 0; j < NT; ++j) red[w - 1][j][lane] = acc[j];
   }
   __syncthreads();
-  if (w == 0) head_softmax_xent<NT, DG>(p, acc, red, dls, lane, row, m0);
+  if (w == 0) head_softmax_xent<NT, DG>(p, acc, red, kFwdWaves - 1, dls, lane, row, blockIdx.x);
   if constexpr (DG) {
     __syncthreads();  // dlogits of the 16 rows in LDS, h staged
     head_dgrad_rows<DEPI, HS>(p, hs, dls, m0);
   }
+}
+
+// Loss from partial logits (EPI_BIAS_RELU_HEAD forward, gemm_q.hip): one wave per 16
+// rows sums the nparts [B][16] fp32 slabs in the head kernel's accumulator layout
+// (lane: row l & 15, classes 4 (l >> 4) + r) -- 16 KiB per wave, the whole pass reads
+// nparts x 64 B per row instead of the K x 2 B of h -- then the same softmax-xent.
+constexpr int kPartWaves = 4;
+__global__ __launch_bounds__(kPartWaves * 64) void head_xent_parts_kernel(HeadParams p, const float* parts,
+                                                                          int nparts) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int slot = blockIdx.x * kPartWaves + w;
+  const int m0 = slot * 16;
+  if (m0 >= p.B) return;
+  const int row = m0 + (lane & 15);
+  floatx4 acc[1] = {floatx4{0.f, 0.f, 0.f, 0.f}};
+  if (row < p.B) {
+    const float* src = parts + (size_t)row * 16 + 4 * (lane >> 4);
+    const size_t stride = (size_t)p.B * 16;
+    int s = 0;
+    for (; s + 4 <= nparts; s += 4) {  // four 16-B loads in flight per lane
+      const floatx4 a = *reinterpret_cast<const floatx4*>(src + (s + 0) * stride);
+      const floatx4 b = *reinterpret_cast<const floatx4*>(src + (s + 1) * stride);
+      const floatx4 c = *reinterpret_cast<const floatx4*>(src + (s + 2) * stride);
+      const floatx4 d = *reinterpret_cast<const floatx4*>(src + (s + 3) * stride);
+      acc[0] += (a + b) + (c + d);
+    }
+    for (; s < nparts; ++s) acc[0] += *reinterpret_cast<const floatx4*>(src + s * stride);
+  }
+  head_softmax_xent<1, false>(p, acc, nullptr, 0, nullptr, lane, row, slot);
 }
 
 // ---------------------------------------------------------------------------
@@ -535,6 +565,25 @@ hipError_t head_fwd_xent(const HeadParams& p, hipStream_t s) {
     case EPI_NONE: return head_dgrad_dispatch<EPI_NONE>(p, s);
     case EPI_DRELU: return head_dgrad_dispatch<EPI_DRELU>(p, s);
     case EPI_DSIGMOID: return head_dgrad_dispatch<EPI_DSIGMOID>(p, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t head_xent_parts(const HeadParams& p, const float* parts, int nparts, hipStream_t s) {
+  if (p.B <= 0) return hipSuccess;
+  if (p.ld != 16 || p.C > 16 || nparts < 1 || parts == nullptr) return hipErrorInvalidValue;
+  const int slots = (p.B + 15) / 16;
+  head_xent_parts_kernel<<<(slots + kPartWaves - 1) / kPartWaves, kPartWaves * 64, 0, s>>>(p, parts, nparts);
+  return hipGetLastError();
+}
+
+hipError_t head_dgrad_stream(const HeadParams& p, hipStream_t s) {
+  if (p.B <= 0) return hipSuccess;
+  if (p.ld != 16 || p.dh == nullptr || p.lddh % 8 != 0 || p.K % 8 != 0 || p.ldw_rows > 16) return hipErrorInvalidValue;
+  switch (p.dgrad_epi) {
+    case EPI_NONE: return launch_head_dgrad_stream<EPI_NONE>(p, s);
+    case EPI_DRELU: return launch_head_dgrad_stream<EPI_DRELU>(p, s);
+    case EPI_DSIGMOID: return launch_head_dgrad_stream<EPI_DSIGMOID>(p, s);
     default: return hipErrorInvalidValue;
   }
 }

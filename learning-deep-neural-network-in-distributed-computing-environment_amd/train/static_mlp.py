@@ -98,7 +98,8 @@ class StaticMLPEngine:
                  use_graphs: bool = True, average_grads: bool = True, use_head_kernels: bool = True,
                  shard_optimizer: bool | None = None, wgrad_combine: bool = True, library_gemms: bool | None = None,
                  fuse_head_dgrad: bool | None = None, library_dgrad: bool | None = None, head_dgrad_mode: int = -1,
-                 relu_masks: bool = True, transposed_dgrad: bool = True, bias_ones_column: bool = True):
+                 relu_masks: bool = True, transposed_dgrad: bool = True, bias_ones_column: bool = True,
+                 fuse_head_fwd: bool = True):
         from ..models.mlp import MLP
 
         if not isinstance(model, MLP):
@@ -208,6 +209,16 @@ class StaticMLPEngine:
         # the GEMM's byte-wise mask stores cost more than the stream saves,
         # profiles/r3/head_dgrad_mask_ab_r3.jsonl)
         self._head_stream = self.head_dgrad and npad[-1] == 16 and self.head_dgrad_mode in (-1, 0)
+        # fuse_head_fwd: the last hidden layer's forward GEMM (four-wave kernel,
+        # EPI_BIAS_RELU_HEAD) also multiplies each 256-column tile of its ReLU output by
+        # the head weight on the MFMA pipe and stores the partial logits; the loss kernel
+        # (head_xent_parts) then sums 16 x 64 B per row instead of streaming the 128 MB
+        # h_{L-1} again for a K = 4096, N = 16 product (gemm_q.hip head_partial).
+        self._head_part = None
+        if (fuse_head_fwd and self._head_stream and L >= 2 and self.layers[L - 2].activation == "relu"
+                and self.layers[L - 1].in_features % 8 == 0 and npad[-1] == 16):
+            self._head_part = torch.empty((self.layers[L - 1].in_features + 255) // 256, B, 16,
+                                          dtype=torch.float32, device=dev)
         self._head_db_ws = (torch.empty(self.C.head_dgrad_ws_floats(B, self.layers[-1].in_features),
                                         dtype=torch.float32, device=self.device) if self.head_dgrad else None)
         # [loss_sum, correct] -- one pair per 16-row workgroup of the head kernel
@@ -268,6 +279,8 @@ class StaticMLPEngine:
             if (relu_masks and self.layers[l - 1].activation == "relu" and not self._lib_fwd[l - 1]
                     and not self._lib_dgrad[l] and not (self.use_head and l == L - 1 and fuse_head_dgrad)):
                 self.mask[l] = torch.zeros(B, (npad[l - 1] + 7) // 8, dtype=torch.uint8, device=dev)
+        if self._head_part is not None and (self._lib_fwd[L - 2] or self.mask[L - 1] is not None):
+            self._head_part = None
         self._db0_from_wgrad = False
         # transposed_dgrad: dgrad(l) reads a transposed bf16 copy of W_l, refreshed by one
         # transpose pass right before it, so both GEMM operands are k-contiguous (measured
@@ -343,6 +356,9 @@ class StaticMLPEngine:
         else:
             self._opt_zero, self._fill_zero = merged[:2], merged[2:]
 
+        if (self._head_part is not None and self.shard
+                and self._bucket_of(self.layers[L - 1].weight) != self._bucket_of(self.layers[L - 2].weight)):
+            self._head_part = None   # the fused forward would read two buckets' all-gathered weights
         self.rank = dist.get_rank(process_group) if self.distributed else 0
         self.xp = getattr(self, "xp", None)
         self._slots = [dict(x=self.x, xp=self.xp, labels=self.labels)]   # slot 0: load_batch's buffers
@@ -361,10 +377,16 @@ class StaticMLPEngine:
         C = self.C
         L = len(self.layers)
         for l in range(L - 1 if (train and self.use_head) else L):
-            self._forward_layer(l)
+            self._forward_layer(l, train)
 
     def _loss(self):
         L = len(self.layers)
+        if self._head_part is not None:   # logits from the last hidden forward's partial products
+            self.C.head_xent_parts(self._head_part, self.bias[L - 1], self.labels, self.h[L], self.dz[L], self.stats,
+                                   self.num_classes, 1.0 / self.B)
+            self.C.head_dgrad_stream(self.h[L - 1], self.W[L - 1], self.dz[L], self.dz[L - 1], self.db[L - 2],
+                                     self._dgrad_epi[L - 1])
+            return
         if self.use_head:   # last Linear + softmax-xent + argmax (+ the head's dgrad) in one launch
             if self.head_dgrad:
                 self.C.head_fwd_xent(self.h[L - 1], self.W[L - 1], self.bias[L - 1], self.labels, self.h[L],
@@ -505,7 +527,7 @@ class StaticMLPEngine:
         assert i_loss == i_fwd + 1
         prologue, tail = p0[:i_fwd], p0[i_loss + 1:]
         # forward ops in layer order with the bucket each one reads
-        ops = [(lambda l=l: self._forward_layer(l), self._bucket_of(self.layers[l].weight)) for l in range(n_fwd)]
+        ops = [(lambda l=l: self._forward_layer(l, True), self._bucket_of(self.layers[l].weight)) for l in range(n_fwd)]
         ops.append((self._loss, self._bucket_of(self.layers[L - 1].weight)))
         bias_bucket = self._bucket_of(self.layers[0].bias)
         groups, waits = [], []
@@ -527,8 +549,12 @@ class StaticMLPEngine:
         self.opt_segments = [_Segment(run([lambda i=i: self._opt(*self._shard_range(i), grad=self.gshard[i])]),
                                       self.use_graphs) for i in range(len(self.buckets))]
 
-    def _forward_layer(self, l):
+    def _forward_layer(self, l, train: bool = False):
         C = self.C
+        if train and self._head_part is not None and l == len(self.layers) - 2:
+            C.gemm(self.h[l], self.W[l], self.h[l + 1], True, True, C.EPI_BIAS_RELU, bias=self.bias[l],
+                   head_w=self.W[l + 1], head_part=self._head_part)
+            return
         if self._lib_fwd[l]:
             W = self.W[l]
             if self.layers[l].activation == "relu":
@@ -727,7 +753,9 @@ class StaticMLPEngine:
         L, d = len(self.layers), {}
         for l in range(L):
             if self.use_head and l == L - 1:
-                d[f"fwd{l}"] = "ldnn head_fwd_xent (Linear + softmax-xent + argmax)"
+                d[f"fwd{l}"] = ("ldnn head_xent_parts (softmax-xent + argmax of the logits the previous forward "
+                                "GEMM's epilogue computed on the MFMA pipe)" if self._head_part is not None
+                                else "ldnn head_fwd_xent (Linear + softmax-xent + argmax)")
                 d[f"wgrad{l}"] = "ldnn head_wgrad"
                 if self.head_dgrad:
                     d[f"dgrad{l}"] = ("ldnn head_dgrad_stream (dReLU + bias-gradient sums)" if self._head_stream
@@ -735,6 +763,7 @@ class StaticMLPEngine:
                 continue
             d[f"fwd{l}"] = ("hipBLASLt" if self._lib_fwd[l] else
                             "ldnn gemm_q (bias+ReLU" + (" + ReLU bit mask" if self.mask[l + 1] is not None else "")
+                            + (" + head partial logits" if self._head_part is not None and l == L - 2 else "")
                             + " epilogue)")
             if self._lib_wgrad[l]:
                 d[f"wgrad{l}"] = "hipBLASLt"
