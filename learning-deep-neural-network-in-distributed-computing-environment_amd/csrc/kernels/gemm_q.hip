@@ -24,6 +24,8 @@
 //    operand; a K tail (K % 64 != 0) of a k-contiguous operand is masked per slot.
 //  * LDS images, fragment reads, XCD-aware tile order and the fused epilogues are
 //    shared with gemm.hip (ldnn_gemm_tile.h).
+#include <type_traits>
+
 #include "ldnn_common.h"
 #include "ldnn_gemm_tile.h"
 #include "ldnn_kernels.h"
@@ -177,10 +179,11 @@ __device__ __forceinline__ void barrier() {
 // the staging writes, so their latency overlaps it instead of serialising.
 // Bias-gradient column sums stay per lane (8 fixed columns) and are reduced
 // across the 4 row lanes once, then one atomic per column per wave.
-template <int EPI, bool OUT_F32>
+template <int EPI, bool OUT_F32, int XF = 0>
 __device__ __forceinline__ void epilogue_q(const GemmParams& p, floatx4 (&acc)[8][8], char* smem, int wid, int mbase,
                                            int nbase, int lane) {
   char* wbuf = smem + wid * 32768;
+  uint32_t xsum = 0;  // XF bit 7 (experiment): no global stores, a checksum keeps the work live
   const int c8 = lane & 15;  // this lane's 8 columns
   const int n = nbase + c8 * 8;
   const bool nok = n < p.N;  // N % 8 == 0
@@ -269,8 +272,13 @@ __device__ __forceinline__ void epilogue_q(const GemmParams& p, floatx4 (&acc)[8
           if constexpr (kSums) cs[q] += bf2f(ob[q]);
         }
         u16x8* dst = reinterpret_cast<u16x8*>(reinterpret_cast<bf16_t*>(p.C) + (size_t)m * p.ldc + n);
-        if (p.variant & 4096) __builtin_nontemporal_store(ob, dst);
-        else *dst = ob;
+        if constexpr ((XF & 128) != 0) {
+          xsum ^= (uint32_t)ob[0] | ((uint32_t)ob[7] << 16);
+        } else if (p.variant & 4096) {
+          __builtin_nontemporal_store(ob, dst);
+        } else {
+          *dst = ob;
+        }
         if constexpr (kMaskOut) {
           uint32_t bits = 0;
 #pragma unroll
@@ -281,6 +289,7 @@ __device__ __forceinline__ void epilogue_q(const GemmParams& p, floatx4 (&acc)[8
     }
     __builtin_amdgcn_wave_barrier();
   }
+  if constexpr ((XF & 128) != 0) reinterpret_cast<uint32_t*>(p.C)[(size_t)blockIdx.x * kThreads + wid * 64 + lane] = xsum;
   if (kSums && p.dbias != nullptr) {
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
@@ -296,84 +305,105 @@ __device__ __forceinline__ void epilogue_q(const GemmParams& p, floatx4 (&acc)[8
   }
 }
 
-// EPI_BIAS_RELU_HEAD epilogue: the activation is finished in the MFMA accumulator
-// layout and the wave's 128 x 128 block of it is multiplied by the classifier head's
-// weight on the MFMA pipe (32 MFMAs: 16 classes x 128 rows) before it is stored.
-//  * bias + ReLU + bf16: one packed add per 2 values, one v_cvt_pk_bf16_f32 per 2,
-//    ReLU as a packed int16 max on the bf16 bits (negative bf16 <=> negative int16;
-//    rounding is monotone, so max(bf16(v), 0) == bf16(max(v, 0))).
-//  * The accumulator layout is fed to the MFMA as is: lane (g = l >> 4, r16 = l & 15)
-//    of m-tile i holds row i*16 + r16 at columns 32t + 4g + {0..3} (n-tile 2t) and
+// bf16-output epilogue with the activation finished in the MFMA accumulator layout
+// (EPI_NONE / EPI_BIAS / EPI_BIAS_RELU / EPI_BIAS_RELU_MASK / EPI_BIAS_RELU_HEAD /
+// EPI_DRELU_MASK).  Measured on MI355X (scripts/bench_epi_share.py): the fp32-staged
+// row epilogue (epilogue_q) costs ~20 us of VALU + LDS work per 16384 x 4096 output
+// on top of its ~10 us of stores; this one moves half the LDS bytes and leaves the
+// store phase almost free of VALU work.
+//  * bias (+ ReLU) + bf16 in registers: one packed add per 2 values, one
+//    v_cvt_pk_bf16_f32 per 2, ReLU as a packed int16 max on the bf16 bits (negative
+//    bf16 <=> negative int16; rounding is monotone, so max(bf16(v), 0) == bf16(max(v, 0))).
+//  * EPI_BIAS_RELU_HEAD: the wave's 128 x 128 block of the activation times the
+//    classifier head's weight on the MFMA pipe (32 MFMAs: 16 classes x 128 rows).  The
+//    accumulator layout is fed to the MFMA as is: lane (g = l >> 4, r16 = l & 15) of
+//    m-tile i holds row i*16 + r16 at columns 32t + 4g + {0..3} (n-tile 2t) and
 //    32t + 16 + 4g + {0..3} (n-tile 2t+1), so k-slot 8g + e of k-step t means exactly
 //    those columns, and the head weight fragment is loaded with the same permutation
-//    (two 8-B pieces per class row).
-//  * The two column halves of the workgroup (wn = 0, 1) combine their partial
-//    logits in the wn = 0 wave's LDS slice; wn = 0 stores head_part[n0 / 256][m][c].
+//    (two 8-B pieces per class row).  The two column halves of the workgroup
+//    (wn = 0, 1) combine their partial logits in the wn = 0 wave's LDS slice; wn = 0
+//    stores head_part[n0 / 256][m][c].
 //  * The bf16 tile is staged in the wave's own 32 KiB slice (all 128 rows at once,
-//    16-B chunks XOR-swizzled by row) and re-read row-wise for full 256-B row stores:
-//    no VALU work left in the store phase.
-__device__ __forceinline__ void epilogue_head(const GemmParams& p, floatx4 (&acc)[8][8], char* smem, int wid, int mbase,
+//    16-B chunks XOR-swizzled by row) and re-read row-wise -- 16 lanes per 256-B row,
+//    4 rows per instruction -- for full-row stores; the ReLU bit masks (read for the
+//    dgrad, written by the forward) and the bias-gradient column sums work on those
+//    8-column row pieces.
+template <int EPI>
+__device__ __forceinline__ void epilogue_bf16(const GemmParams& p, floatx4 (&acc)[8][8], char* smem, int wid, int mbase,
                                               int nbase, int lane) {
   typedef short s16x2 __attribute__((ext_vector_type(2)));
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+  constexpr bool kHead = EPI == EPI_BIAS_RELU_HEAD;
+  constexpr bool kRelu = EPI == EPI_BIAS_RELU || EPI == EPI_BIAS_RELU_MASK || kHead;
+  constexpr bool kBias = kRelu || EPI == EPI_BIAS;
+  constexpr bool kMaskIn = EPI == EPI_DRELU_MASK, kMaskOut = EPI == EPI_BIAS_RELU_MASK;
+  constexpr bool kSums = EPI == EPI_NONE || kMaskIn;
   const int g = lane >> 4, r16 = lane & 15;
   floatx4 bias[8];
+  if constexpr (kBias) {
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int n = nbase + j * 16 + 4 * g;
-    bias[j] = n < p.N ? *reinterpret_cast<const floatx4*>(p.bias + n) : floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < 8; ++j) {
+      const int n = nbase + j * 16 + 4 * g;
+      bias[j] = n < p.N ? *reinterpret_cast<const floatx4*>(p.bias + n) : floatx4{0.f, 0.f, 0.f, 0.f};
+    }
   }
   bf16x8 wf[4];
-  const bf16_t* wrow = p.head_w + (size_t)r16 * p.ldhw;
+  if constexpr (kHead) {
+    const bf16_t* wrow = p.head_w + (size_t)r16 * p.ldhw;
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const int nlo = nbase + 32 * t + 4 * g, nhi = nlo + 16;
-    const bf16x4 zero = {};
-    const bf16x4 lo = nlo < p.N ? *reinterpret_cast<const bf16x4*>(wrow + nlo) : zero;
-    const bf16x4 hi = nhi < p.N ? *reinterpret_cast<const bf16x4*>(wrow + nhi) : zero;
-    wf[t] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    for (int t = 0; t < 4; ++t) {
+      const int nlo = nbase + 32 * t + 4 * g, nhi = nlo + 16;
+      const bf16x4 zero = {};
+      const bf16x4 lo = nlo < p.N ? *reinterpret_cast<const bf16x4*>(wrow + nlo) : zero;
+      const bf16x4 hi = nhi < p.N ? *reinterpret_cast<const bf16x4*>(wrow + nhi) : zero;
+      wf[t] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    }
   }
-  // packed bf16 activations, [n-tile j][m-tile i]: 4 values = 2 dwords
+  // packed bf16 results, [n-tile j][m-tile i]: 4 values = 2 dwords
   uint32_t hq[8][8][2];
   const s16x2 zero2 = {0, 0};
 #pragma unroll
   for (int j = 0; j < 8; ++j)
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const floatx4 v = acc[j][i] + bias[j];
+      floatx4 v = acc[j][i];
+      if constexpr (kBias) v += bias[j];
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
         const bf16x2 pb = {(__bf16)v[2 * h], (__bf16)v[2 * h + 1]};
-        const s16x2 r = __builtin_elementwise_max(__builtin_bit_cast(s16x2, pb), zero2);
+        s16x2 r = __builtin_bit_cast(s16x2, pb);
+        if constexpr (kRelu) r = __builtin_elementwise_max(r, zero2);
         hq[j][i][h] = __builtin_bit_cast(uint32_t, r);
       }
     }
-  floatx4 d[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    d[i] = floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const u32x4 q = {hq[2 * t][i][0], hq[2 * t][i][1], hq[2 * t + 1][i][0], hq[2 * t + 1][i][1]};
-      d[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[t], __builtin_bit_cast(bf16x8, q), d[i], 0, 0, 0);
-    }
-  }
-  const int wm = wid >> 1, wn = wid & 1;
-  floatx4* xch = reinterpret_cast<floatx4*>(smem + (2 * wm) * 32768);  // the wn = 0 wave's slice
-  if (wn == 1) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) xch[i * 64 + lane] = d[i];
-  }
-  barrier();
-  if (wn == 0) {
-    float* part = p.head_part + (size_t)(nbase / 256) * p.M * 16;
+  if constexpr (kHead) {
+    floatx4 d[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const int m = mbase + i * 16 + r16;
-      const floatx4 v = d[i] + xch[i * 64 + lane];
-      if (m < p.M) *reinterpret_cast<floatx4*>(part + (size_t)m * 16 + 4 * g) = v;
+      d[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const u32x4 q = {hq[2 * t][i][0], hq[2 * t][i][1], hq[2 * t + 1][i][0], hq[2 * t + 1][i][1]};
+        d[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[t], __builtin_bit_cast(bf16x8, q), d[i], 0, 0, 0);
+      }
     }
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // reads of the slice done before this wave stages into it
+    const int wm = wid >> 1, wn = wid & 1;
+    floatx4* xch = reinterpret_cast<floatx4*>(smem + (2 * wm) * 32768);  // the wn = 0 wave's slice
+    if (wn == 1) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) xch[i * 64 + lane] = d[i];
+    }
+    barrier();
+    if (wn == 0) {
+      float* part = p.head_part + (size_t)(nbase / 256) * p.M * 16;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int m = mbase + i * 16 + r16;
+        const floatx4 v = d[i] + xch[i * 64 + lane];
+        if (m < p.M) *reinterpret_cast<floatx4*>(part + (size_t)m * 16 + 4 * g) = v;
+      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // reads of the slice done before this wave stages into it
+    }
   }
   // stage: row i*16 + r16 (256 B), 8-B piece (j*16 + 4g) * 2 B within 16-B chunk 2j + (g >> 1)
   char* wbuf = smem + wid * 32768;
@@ -386,26 +416,79 @@ __device__ __forceinline__ void epilogue_head(const GemmParams& p, floatx4 (&acc
       *reinterpret_cast<uint2*>(wbuf + row * 256 + ((chunk ^ (row & 15)) << 4) + (g & 1) * 8) =
           uint2{hq[j][i][0], hq[j][i][1]};
     }
-  __builtin_amdgcn_s_waitcnt(0xc07f);
-  __builtin_amdgcn_wave_barrier();
   const int c8 = lane & 15;
   const int n = nbase + c8 * 8;
-  if (n >= p.N) return;
+  const bool nok = n < p.N;  // N % 8 == 0
+  uint32_t mk[32];
+  if constexpr (kMaskIn) {  // one byte per row and 8 columns, all 32 in flight during the staging
 #pragma unroll
-  for (int it = 0; it < 32; ++it) {
-    const int row = it * 4 + (lane >> 4);
-    const int m = mbase + row;
-    const u16x8 v = *reinterpret_cast<const u16x8*>(wbuf + row * 256 + ((c8 ^ (row & 15)) << 4));
-    if (m < p.M) {
-      u16x8* dst = reinterpret_cast<u16x8*>(reinterpret_cast<bf16_t*>(p.C) + (size_t)m * p.ldc + n);
+    for (int it = 0; it < 32; ++it) {
+      const int m = mbase + it * 4 + (lane >> 4);
+      mk[it] = (nok && m < p.M) ? (uint32_t)p.mask_in[(size_t)m * p.ldmask + (n >> 3)] : 0u;
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): own staging writes landed (wave-private slice)
+  __builtin_amdgcn_wave_barrier();
+  auto rows = [&](auto sums) {
+    constexpr bool kS = decltype(sums)::value;
+    float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int it = 0; it < 32; ++it) {
+      const int row = it * 4 + (lane >> 4);
+      const int m = mbase + row;
+      u32x4 v = *reinterpret_cast<const u32x4*>(wbuf + row * 256 + ((c8 ^ (row & 15)) << 4));
+      if (!(nok && m < p.M)) continue;
+      if constexpr (kMaskIn) {  // relu'(h) from the bit mask: zero the 16-bit halves whose bit is 0
+        const uint32_t b = mk[it];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          v[k] &= (((b >> (2 * k)) & 1u) ? 0x0000ffffu : 0u) | (((b >> (2 * k + 1)) & 1u) ? 0xffff0000u : 0u);
+      }
+      if constexpr (kS) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          cs[2 * k] += __uint_as_float(v[k] << 16);
+          cs[2 * k + 1] += __uint_as_float(v[k] & 0xffff0000u);
+        }
+      }
+      u32x4* dst = reinterpret_cast<u32x4*>(reinterpret_cast<bf16_t*>(p.C) + (size_t)m * p.ldc + n);
       if (p.variant & 4096) __builtin_nontemporal_store(v, dst);
       else *dst = v;
+      if constexpr (kMaskOut) {  // bit q = output (m, n + q) > 0 (ReLU output: sign clear, nonzero)
+        uint32_t bits = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          bits |= ((v[k] & 0xffffu) != 0u ? 1u : 0u) << (2 * k);
+          bits |= ((v[k] >> 16) != 0u ? 1u : 0u) << (2 * k + 1);
+        }
+        p.mask_out[(size_t)m * p.ldmask + (n >> 3)] = (uint8_t)bits;
+      }
     }
+    if constexpr (kS) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        float t = cs[q];
+        t += __shfl_xor(t, 16, 64);
+        t += __shfl_xor(t, 32, 64);
+        cs[q] = t;
+      }
+      if (lane < 16 && nok) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) atomicAdd(p.dbias + n + q, cs[q]);
+      }
+    }
+  };
+  if constexpr (kSums) {
+    if (p.dbias != nullptr) rows(std::true_type{});
+    else rows(std::false_type{});
+  } else {
+    rows(std::false_type{});
   }
 }
 
 // XF: experiment flags (0 in production): bit0 no in-loop DMA, bit1 no DMA wait, bit2 no in-loop ds_reads,
-// bits 3 / 4: alternative DMA / read placements in sub-step 1 (see there), bit5 in-loop DMAs read nothing
+// bits 3 / 4: alternative DMA / read placements in sub-step 1 (see there), bit5 in-loop DMAs read nothing,
+// bit6 no epilogue (measures the epilogue's share of the kernel), bit7 epilogue without its global stores
 template <bool A_KC, bool B_KC, int EPI, bool OUT_F32, int XF = 0>
 __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(GemmParams p) {
   constexpr bool kDma = !(XF & 1), kWait = !(XF & 2), kRead = !(XF & 4);
@@ -534,10 +617,30 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(GemmParams p) {
       return;
     }
   }
+  if constexpr ((XF & 64) != 0) {  // experiment: no epilogue (one float per lane keeps the MFMAs live)
+    float t = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) t += acc[j][i][0] + acc[j][i][3];
+    reinterpret_cast<float*>(p.C)[(size_t)blockIdx.x * kThreads + tid] = t;
+    return;
+  }
   if constexpr (EPI != EPI_OPT_SGD && EPI != EPI_OPT_ADAM) {
     barrier();  // every wave is done with the operand stages: LDS belongs to the epilogue
-    if constexpr (EPI == EPI_BIAS_RELU_HEAD) epilogue_head(pe, acc, smem, wid, m0 + wm * 128, n0 + wn * 128, lane);
-    else epilogue_q<EPI, OUT_F32>(pe, acc, smem, wid, m0 + wm * 128, n0 + wn * 128, lane);
+    // bf16 outputs whose activation is exact on the bf16 value: the register-side epilogue
+    // (variant bit 13 selects the fp32-staged one, an A/B knob)
+    constexpr bool kBf16Epi = !OUT_F32 && (EPI == EPI_NONE || EPI == EPI_BIAS || EPI == EPI_BIAS_RELU ||
+                                           EPI == EPI_BIAS_RELU_MASK || EPI == EPI_BIAS_RELU_HEAD ||
+                                           EPI == EPI_DRELU_MASK) && (XF & 128) == 0;
+    if constexpr (EPI == EPI_BIAS_RELU_HEAD) {
+      epilogue_bf16<EPI>(pe, acc, smem, wid, m0 + wm * 128, n0 + wn * 128, lane);
+    } else if constexpr (kBf16Epi) {
+      if (p.variant & 8192) epilogue_q<EPI, OUT_F32, XF>(pe, acc, smem, wid, m0 + wm * 128, n0 + wn * 128, lane);
+      else epilogue_bf16<EPI>(pe, acc, smem, wid, m0 + wm * 128, n0 + wn * 128, lane);
+    } else {
+      epilogue_q<EPI, OUT_F32, XF>(pe, acc, smem, wid, m0 + wm * 128, n0 + wn * 128, lane);
+    }
   } else {
     epilogue<EPI, OUT_F32, 8, 8>(p, acc, m0 + wm * 128, n0 + wn * 128, lane);
   }
@@ -558,6 +661,8 @@ hipError_t dispatch_epi(const GemmParams& p, int epi, hipStream_t s) {
         case 8: gemm_kernel<true, true, EPI_BIAS_RELU, false, 8><<<grid, block, 0, s>>>(p); break;
         case 16: gemm_kernel<true, true, EPI_BIAS_RELU, false, 16><<<grid, block, 0, s>>>(p); break;
         case 32: gemm_kernel<true, true, EPI_BIAS_RELU, false, 32><<<grid, block, 0, s>>>(p); break;
+        case 64: gemm_kernel<true, true, EPI_BIAS_RELU, false, 64><<<grid, block, 0, s>>>(p); break;
+        case 128: gemm_kernel<true, true, EPI_BIAS_RELU, false, 128><<<grid, block, 0, s>>>(p); break;
         default: return hipErrorInvalidValue;
       }
       return hipGetLastError();
