@@ -38,6 +38,9 @@ def main():
     ap.add_argument("--model", default="lenet5")
     ap.add_argument("--batch", type=int, default=128, help="per rank")
     ap.add_argument("--steps", type=int, default=6)
+    ap.add_argument("--oneshot", action="store_true",
+                    help="also train with the one-shot IPC all-reduce on (buckets <= 4 MiB) and require "
+                         "the same parameters as with it off")
     a = ap.parse_args()
     ctx = D.setup(a.backend)
     N, r, dev = ctx.world_size, ctx.rank, ctx.device
@@ -70,6 +73,19 @@ def main():
     got = torch.cat([p.detach().flatten().cpu() for p in m.parameters()])
     print(f"rank {r}: batch losses {[round(v, 4) for v in bl]}", flush=True)
     ok = True
+    if a.oneshot:
+        c1 = TorchComm()
+        os_ = c1.enable_oneshot(4 << 20, device=dev)
+        assert os_ is not None, "one-shot self-test failed"
+        calls0 = os_._c.calls
+        m1, _ = run(N, r, c1)
+        c1.check_errors()
+        used = os_._c.calls - calls0
+        got1 = torch.cat([p.detach().flatten().cpu() for p in m1.parameters()])
+        diff = (got1 - got).abs().max().item()
+        scale = got.abs().max().item()
+        print(f"rank {r}: one-shot calls {used}, max |params(one-shot) - params(gloo)| {diff:.3e}", flush=True)
+        ok = ok and used > 0 and diff <= 1e-6 * max(scale, 1.0)
     if r == 0:
         ref_m, ref_bl = run(1, 0, None)
         ref = torch.cat([p.detach().flatten().cpu() for p in ref_m.parameters()])
@@ -80,7 +96,7 @@ def main():
         du, dr = (got - p0).double(), (ref - p0).double()
         err = (du - dr).norm().item() / max(dr.norm().item(), 1e-12)
         print(f"relative update difference vs single rank: {err:.3e}", flush=True)
-        ok = err < 2e-2
+        ok = ok and err < 2e-2
     t = torch.tensor([1.0 if ok else 0.0])
     dist.all_reduce(t, op=dist.ReduceOp.MIN)
     others = [torch.zeros_like(got) for _ in range(N)]
