@@ -360,6 +360,7 @@ class StaticMLPEngine:
                 and self._bucket_of(self.layers[L - 1].weight) != self._bucket_of(self.layers[L - 2].weight)):
             self._head_part = None   # the fused forward would read two buckets' all-gathered weights
         self.rank = dist.get_rank(process_group) if self.distributed else 0
+        self._bias_bucket = self._bucket_of(self.layers[0].bias)
         self.xp = getattr(self, "xp", None)
         self._slots = [dict(x=self.x, xp=self.xp, labels=self.labels)]   # slot 0: load_batch's buffers
         self._slot = 0
@@ -666,6 +667,37 @@ class StaticMLPEngine:
             if w is not None:
                 w.wait()
         self._pending_gather = {}
+        self._wait_bias_bcast()
+
+    def _wait_bias_bcast(self):
+        for w in getattr(self, "_pending_bias", ()):
+            if w is not None:
+                w.wait()
+        self._pending_bias = []
+
+    def _broadcast_biases(self, bi, capturing):
+        """Sharded step: the forward GEMM epilogues and the loss read the fp32 MASTER
+        biases, but each rank updates only its shard of the master -- so the owner(s) of
+        the bias range send the updated fp32 biases to every rank (a few KB; the
+        momentum / Adam state stays with its owner, the only rank that reads it)."""
+        b, e, _ = self.buckets[bi]
+        sz = (e - b) // self.world
+        bb = self._bias_begin
+        be = self.flat.seg(self.layers[-1].bias).offset + self.flat.seg(self.layers[-1].bias).storage_numel
+        works = []
+        for k in range(self.world):
+            lo, hi = max(bb, b + k * sz), min(be, b + (k + 1) * sz)
+            if lo >= hi:
+                continue
+            src = k if self.pg is None else dist.get_global_rank(self.pg, k)
+            sync = self._gloo or capturing
+            w = dist.broadcast(self.flat.master[lo:hi], src=src, group=self.pg, async_op=not sync)
+            if sync:
+                if capturing:
+                    torch.cuda.current_stream().synchronize()
+                w = None
+            works.append(w)
+        self._pending_bias = getattr(self, "_pending_bias", []) + works
 
     @torch.no_grad()
     def gather_master(self):
@@ -688,6 +720,7 @@ class StaticMLPEngine:
     def _step_sharded(self, capturing):
         pend = self._pending_gather   # bucket -> the previous step's weight all-gather
         self._pending_gather = {}
+        self._wait_bias_bcast()       # the previous step's fp32 bias refresh (the forward reads it)
         works = []
         for i, seg in enumerate(self.segments):
             for bi in self._seg_waits[i]:
@@ -712,6 +745,8 @@ class StaticMLPEngine:
             if w is not None:
                 w.wait()
             self.opt_segments[bi]()
+            if bi == self._bias_bucket:
+                self._broadcast_biases(bi, capturing)
             g = self._all_gather(bi)
             if capturing and g is not None:
                 g.wait()

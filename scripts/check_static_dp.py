@@ -51,6 +51,18 @@ def main():
         torch.cuda.synchronize()
         print(f"rank {r} step {i} loss {eng.read_stats(B)[0]:.5f} finite={bool(torch.isfinite(eng.flat.shadow).all())}",
               flush=True)
+    # the forward reads the fp32 master biases: they must agree on every rank after
+    # sharded updates too (each rank updates only its shard of the master)
+    eng.sync()
+    bm = torch.cat([eng.bias[l].detach().float().flatten() for l in range(len(eng.bias))])
+    bmx, bmn = bm.clone(), bm.clone()
+    if N > 1:
+        dist.all_reduce(bmx, op=dist.ReduceOp.MAX)
+        dist.all_reduce(bmn, op=dist.ReduceOp.MIN)
+    bias_ok = bool(torch.equal(bmx, bmn))
+    if r == 0:
+        print("BIASES_CONSISTENT" if bias_ok else
+              f"BIASES_STALE max spread {(bmx - bmn).abs().max().item():.3e}", flush=True)
     eng.gather_master()   # sharded optimizer: make the fp32 master whole on every rank
     torch.cuda.synchronize()
     got = eng.flat.master.detach().cpu().clone()
@@ -73,6 +85,7 @@ def main():
             scale = p2.detach().abs().max().item() + 1e-6
             print(f"{n1}: max|diff| = {d:.3e} (scale {scale:.3e})")
             ok &= d <= 2e-2 * scale + 1e-3
+        ok &= bias_ok
         print("STATIC_DP_OK" if ok else "STATIC_DP_MISMATCH", flush=True)
     # every rank holds identical parameters
     t = got.to(ctx.device)

@@ -28,13 +28,19 @@ def main():
     ends = [i for i, r in enumerate(rows) if a.marker in r["Kernel_Name"]]
     lo = ends[a.step - 1] + 1
     hi = ends[a.step]
-    tot = 0.0
+    tot = gaps = 0.0
+    prev_end = None
     for r in rows[lo:hi + 1]:
-        us = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+        t0, t1 = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        us = (t1 - t0) / 1e3
         tot += us
+        if prev_end is not None and t0 > prev_end:
+            gaps += (t0 - prev_end) / 1e3
+        prev_end = t1 if prev_end is None else max(prev_end, t1)
         g = int(r["Grid_Size_X"]) // max(1, int(r["Workgroup_Size_X"]))
         print(f"{us:8.1f} {g:6d}x{r['Grid_Size_Y']:>4s}  {short(r['Kernel_Name'])}")
-    print(f"{tot:8.1f} total ({hi - lo + 1} kernels)")
+    span = (int(rows[hi]["End_Timestamp"]) - int(rows[lo]["Start_Timestamp"])) / 1e3
+    print(f"{tot:8.1f} total ({hi - lo + 1} kernels); step span {span:.1f} us, idle gaps between kernels {gaps:.1f} us")
 
 
 if __name__ == "__main__":

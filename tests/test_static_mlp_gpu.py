@@ -72,9 +72,12 @@ def test_graph_replay_matches_eager_with_splitk():
     torch.testing.assert_close(e1.flat.master, e2.flat.master, rtol=1e-6, atol=1e-8)
 
 
-def test_multirank_static_engine_gloo_two_ranks_one_gpu():
-    """The bucketed multi-rank step (async all-reduce between graph segments)
-    equals one rank on the concatenated batch (2 ranks share the GPU via gloo)."""
+@pytest.mark.parametrize("nproc", [2, 3])
+def test_multirank_static_engine_gloo_two_ranks_one_gpu(nproc):
+    """The bucketed multi-rank step (sharded optimizer: reduce-scatter between graph
+    segments, shard update, weight all-gather, fp32 bias refresh from the shard
+    owners) equals one rank on the concatenated batch, and every rank's forward reads
+    the same fp32 biases (2 / 3 ranks share the GPU via gloo)."""
     import os
     import socket
     import subprocess
@@ -85,11 +88,12 @@ def test_multirank_static_engine_gloo_two_ranks_one_gpu():
     port = s.getsockname()[1]
     s.close()
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", str(nproc), "--master-addr", "127.0.0.1",
            "--master-port", str(port), os.path.join(root, "scripts", "check_static_dp.py"), "--backend", "gloo",
            "--hidden", "512", "--batch", "1024", "--steps", "7"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
+    assert "BIASES_CONSISTENT" in r.stdout, r.stdout[-3000:]
     assert "STATIC_DP_OK" in r.stdout and "REPLICAS_IDENTICAL" in r.stdout, r.stdout[-3000:]
 
 
