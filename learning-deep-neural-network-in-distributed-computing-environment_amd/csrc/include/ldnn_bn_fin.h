@@ -33,7 +33,11 @@ __device__ __forceinline__ void bn_acc_add(float* p, float v) { atomicAdd(p, v);
 template <bool BWD, int NCOP>
 __device__ __forceinline__ void bn_finalize_last(const BnFin& f, int M, int C, int nblk, float* tot, int cap,
                                                  int ncop = NCOP) {
-  __shared__ int last;
+  // the "last block" flag lives in the caller's scratch (its last float): a second
+  // __shared__ object would add 4 bytes to the kernels that inline this (the trap of
+  // cdna_hip_programming.md, and an 80-KiB kernel would lose its second workgroup)
+  int& last = *reinterpret_cast<int*>(tot + cap - 1);
+  cap -= 1;
   __syncthreads();
   if (threadIdx.x == 0) {
     const int t = __hip_atomic_fetch_add(f.ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

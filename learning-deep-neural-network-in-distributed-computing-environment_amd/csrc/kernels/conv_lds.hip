@@ -34,6 +34,7 @@
 // and fragment reads are those of gemm.hip (ldnn_gemm_tile.h).
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "ldnn_common.h"
 #include "ldnn_fastdiv.h"
@@ -404,8 +405,9 @@ __device__ __forceinline__ int tiles_of(const LArgs& a) { return a.tiles_x; }
 // The following training-mode BatchNorm's statistics from this tile's bf16 outputs
 // (exactly the values BN reads): per channel sum and sum of squares over the
 // tile's valid rows -- 16 row lanes by shuffles, the WM wave rows through LDS --
-// then ONE pair of fp32 atomics per channel per tile, into one of kBnCopies
-// accumulator copies (tile % kBnCopies: 8x less same-address serialisation).  The
+// then ONE pair of fp32 atomics per channel per tile, into one of bn_ncop
+// accumulator copies (tile % kBnCopies: 8x less same-address serialisation; 64 copies
+// measured no faster, profiles/r3/bn_copies_ab_r3.txt).  The
 // last of the grid's `tiles` workgroups sums the copies and finalizes (mean,
 // invstd, running-stat EMA, apply coefficients), so the BN needs no reduce pass.
 template <int WM, int WN>
@@ -705,7 +707,9 @@ __device__ __forceinline__ void conv_tail(const LArgs& a, const Geo& g, floatx4 
 // kt+1 in flight while kt is multiplied.  NS = 3 / 4 (grids of at most one
 // workgroup per CU): K-tiles kt+1 .. kt+NS-1 in flight, a counted vmcnt (never 0
 // in the steady state) retires only tile kt before the barrier that publishes it.
-template <int WM, int WN, class OA, class OB, int EPI, bool OUT_F32, bool DGRAD, int NS>
+// XF (experiment builds only, LDNN_CONV_XF): bit0 no in-loop DMA, bit1 the A operand DMAs
+// contiguous 16-KiB-aligned chunks instead of the im2col gather, bit2 no fragment reads / MFMAs
+template <int WM, int WN, class OA, class OB, int EPI, bool OUT_F32, bool DGRAD, int NS, int XF = 0>
 __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void conv_lds_kernel(LArgs a, const bf16_t* pa, uint32_t bytes_a,
                                                                        const bf16_t* pb, uint32_t bytes_b) {
   constexpr int NW = WM * WN, BM = WM * 64, BN = WN * 64;
@@ -770,16 +774,29 @@ __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void conv_lds_kernel(LArgs a,
         wait_vm<PER_TILE * (NS - 2)>();
       }
       lds_barrier();  // publishes tile kt; every wave is done reading tile kt-1's stage
-      if (kt + NS - 1 < nk) {
+      if (!(XF & 1) && kt + NS - 1 < nk) {
         ks_next(a, g, ks);
         oa.advance(a);
         ob.advance(a);
         char* nxt = smem + (cur == 0 ? NS - 1 : cur - 1) * STAGE;  // stage of tile kt-1
-        LDNN_DMA_TILE(oa, PPA, ra, nxt, ks);
+        if constexpr ((XF & 2) != 0) {  // contiguous A chunks: the fill without the gather
+          const uint32_t span = (bytes_a >> 1) & ~16383u;
+          const uint32_t tb = (uint32_t)(blockIdx.x * 9 + ks.kt) * (uint32_t)A_BYTES % span;
+#pragma unroll
+          for (int i_ = 0; i_ < PPA; ++i_)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(ra.r, (lds_void*)(nxt + (i_ * NW + wid) * 1024), 16,
+                                                     (int)(tb + (i_ * NW + wid) * 1024 + lane * 16), 0, 0, 0);
+        } else {
+          LDNN_DMA_TILE(oa, PPA, ra, nxt, ks);
+        }
         LDNN_DMA_TILE(ob, PPB, rb, nxt + A_BYTES, ks);
       }
       const char* la = smem + cur * STAGE;
       const char* lb = la + A_BYTES;
+      if constexpr ((XF & 4) != 0) {
+        cur = cur == NS - 1 ? 0 : cur + 1;
+        continue;
+      }
       __builtin_amdgcn_s_setprio(1);
       // all 16 fragments of the K-tile first (64 VGPRs): the reads of the second
       // K-half are in flight while the first half's 16 MFMAs run
@@ -823,6 +840,11 @@ __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void conv_lds_kernel(LArgs a,
 // dgrad: rows = input pixels, tap (r, s) reads dy at (h + 1 - r, w + 1 - s).
 constexpr int kHaloExtra = 120;  // 2W + 2 rows of halo, rounded up to 8, at most (W <= 59)
 
+// (Measured negative, removed: a double-buffered variant for the 128x128 tiles -- the next
+// channel block's halo DMAd into a second buffer over taps 0..7 -- cuts the fill per
+// K-tile from 32 to ~19 KiB, yet ran slower than the gather kernel on every ResNet-18 /
+// EnhancedCNN shape, e.g. C256 H14 b256 fwd 75 -> 106 us, dgrad 101 -> 112 us;
+// profiles/r3/conv_fill_knockout_r3.txt.)
 template <int WM, int WN, class OB, int EPI, bool DGRAD>
 __global__ __launch_bounds__(256, 2) void conv_halo_kernel(LArgs a, const bf16_t* pa, uint32_t bytes_a,
                                                            const bf16_t* pb, uint32_t bytes_b) {
@@ -1262,11 +1284,29 @@ int ring_env() {
 bool deep_ring(int) { return ring_env() >= 3; }
 
 // OA / OB = Policy<rows, DMA pieces per wave (= rows / 8 / 4 waves), 4 waves>.
+int conv_xf_env() {
+  static const int v = env_int("LDNN_CONV_XF", 0);
+  return v;
+}
+
 template <int WM, int WN, class OA, class OB, bool OUT_F32, bool DGRAD, int NS>
 hipError_t launch_ns(LArgs a, int epi, int splits, const bf16_t* pa, size_t ba, const bf16_t* pb, size_t bb,
                      hipStream_t st) {
   constexpr int NW = WM * WN;
   dim3 grid(a.tiles_x, splits, a.classes), block(NW * 64);
+  if constexpr (std::is_same_v<OA, FwdA<128, 4, 4>> && NS == 2) {
+    const int xf = conv_xf_env();
+    if (xf != 0 && epi == EPI_NONE) {
+      switch (xf) {
+        case 1: conv_lds_kernel<WM, WN, OA, OB, EPI_NONE, OUT_F32, DGRAD, NS, 1><<<grid, block, 0, st>>>(a, pa, (uint32_t)ba, pb, (uint32_t)bb); break;
+        case 2: conv_lds_kernel<WM, WN, OA, OB, EPI_NONE, OUT_F32, DGRAD, NS, 2><<<grid, block, 0, st>>>(a, pa, (uint32_t)ba, pb, (uint32_t)bb); break;
+        case 4: conv_lds_kernel<WM, WN, OA, OB, EPI_NONE, OUT_F32, DGRAD, NS, 4><<<grid, block, 0, st>>>(a, pa, (uint32_t)ba, pb, (uint32_t)bb); break;
+        case 6: conv_lds_kernel<WM, WN, OA, OB, EPI_NONE, OUT_F32, DGRAD, NS, 6><<<grid, block, 0, st>>>(a, pa, (uint32_t)ba, pb, (uint32_t)bb); break;
+        default: return hipErrorInvalidValue;
+      }
+      return hipGetLastError();
+    }
+  }
 #define LDNN_CONV_LDS(E)                                                                                      \
   conv_lds_kernel<WM, WN, OA, OB, E, OUT_F32, DGRAD, NS><<<grid, block, 0, st>>>(a, pa, (uint32_t)ba, pb, \
                                                                                   (uint32_t)bb)
@@ -1299,11 +1339,11 @@ hipError_t launch(LArgs a, int epi, int splits, const bf16_t* pa, size_t ba, con
   return launch_ns<WM, WN, OA, OB, OUT_F32, DGRAD, 2>(a, epi, splits, pa, ba, pb, bb, st);
 }
 
-// Halo path (conv_halo_kernel) for 3x3 stride-1 pad-1 fwd / dgrad; LDNN_CONV_HALO=0
-// turns it off, =2 also takes the 128x128 tiles (A/B knobs).  By default only the
-// 256x64 tiles of 64-channel layers take it: there the activation tile is 4/5 of the
-// gather kernel's fill; on 128x128 tiles the weight tile dominates and the per-block
-// halo reload stalls (profiles/conv_halo_micro_r2.txt).
+// Halo path (conv_halo_kernel) for 3x3 stride-1 pad-1 fwd / dgrad.  LDNN_CONV_HALO
+// (A/B knob): 0 off; 1 (default) the 256x64 tiles of 64-channel layers only (there the
+// activation tile is 4/5 of the gather kernel's fill and one channel block is loaded
+// once); 2 the 128x128 tiles too (slower: there the weight tile dominates the fill and
+// the per-block halo reload stalls, profiles/conv_halo_micro_r2.txt).
 int g_conv_halo = -2;  // -2: not read yet
 int halo_env() {
   if (g_conv_halo == -2) g_conv_halo = env_int("LDNN_CONV_HALO", 1);
@@ -1312,6 +1352,13 @@ int halo_env() {
 bool halo_ok(const ConvShape& s) {
   return halo_env() != 0 && s.R == 3 && s.S == 3 && s.stride == 1 && s.pad == 1 && s.P == s.H && s.Q == s.W &&
          ((2 * s.W + 2 + 7) & ~7) <= kHaloExtra;
+}
+// the halo path takes this plan (wm: its wave rows, 4 = 256x64 tiles, 2 = 128x128)
+bool halo_takes(const ConvShape& s, int wm) {
+  if (!halo_ok(s) || deep_ring(0)) return false;
+  const int m = halo_env();
+  if (wm == 4) return m != 0;
+  return m == 2;
 }
 
 template <int WM, int WN, class OB, bool DGRAD>
@@ -1577,9 +1624,9 @@ hipError_t conv2d_fwd_lds(const ConvShape& s, const uint16_t* x, const uint16_t*
   }
   const size_t bx = (size_t)s.N * s.H * s.W * s.C * 2, bw = (size_t)s.K * a.rsc * 2;
   hipError_t e;
-  if (halo_ok(s) && !deep_ring(0) && (pl.wm == 4 || halo_env() == 2)) {
-    // fwd: the halo wins on the 256x64 tiles of 64-filter layers (C64 H56: 53.7 -> 35-37 us)
-    // and loses on 128x128 ones (C128 H28 25.8 -> 27.7, C512 H7 34.9 -> 40.0 us)
+  if (halo_takes(s, pl.wm)) {
+    // fwd: the halo wins on the 256x64 tiles of 64-filter layers (C64 H56: 53.7 -> 35-37 us);
+    // on 128x128 ones only double-buffered (single: C128 H28 25.8 -> 27.7, C512 H7 34.9 -> 40.0 us)
     if (pl.wm == 4) e = launch_halo<4, 1, WeightKC<64, 2, 4>, false>(a, epi, pl.splits, x, bx, w, bw, st);
     else e = launch_halo<2, 2, WeightKC<128, 4, 4>, false>(a, epi, pl.splits, x, bx, w, bw, st);
   } else if (pl.wm == 4) {
@@ -1618,9 +1665,9 @@ hipError_t conv2d_dgrad_lds(const ConvShape& s, const uint16_t* dy, const uint16
   }
   const size_t bdy = (size_t)s.N * s.P * s.Q * s.K * 2, bw = (size_t)s.K * a.rsc * 2;
   hipError_t e;
-  if (halo_ok(s) && !deep_ring(0) && (pl.wm == 4 || halo_env() == 2)) {
-    // dgrad likewise: C64 H56 38.9 -> 36.5 us; on 128x128 tiles neutral to 1 us slower
-    // (ResNet-18 C128-C512) and up to 2.6 us slower on the EnhancedCNN 16x16 .. 2x2 stages
+  if (halo_takes(s, pl.wm)) {
+    // dgrad likewise: C64 H56 38.9 -> 36.5 us; single-buffered on 128x128 tiles neutral to 1 us
+    // slower (ResNet-18 C128-C512), up to 2.6 us slower on the EnhancedCNN 16x16 .. 2x2 stages
     if (pl.wm == 4) e = launch_halo<4, 1, DgradB<64, 2, 4>, true>(a, EPI_NONE, pl.splits, dy, bdy, w, bw, st);
     else e = launch_halo<2, 2, DgradB<128, 4, 4>, true>(a, EPI_NONE, pl.splits, dy, bdy, w, bw, st);
   } else if (pl.wm == 4) {

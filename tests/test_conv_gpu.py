@@ -139,11 +139,13 @@ def test_nchw_to_nhwc_pad(dtype, C, cp):
 
 
 @pytest.mark.parametrize("N,C,H,W,K", [(2, 64, 56, 56, 64), (2, 128, 28, 28, 128), (3, 256, 14, 14, 256),
-                                       (2, 512, 7, 7, 512), (2, 128, 20, 20, 64), (1, 64, 59, 59, 128)])
+                                       (2, 512, 7, 7, 512), (2, 128, 20, 20, 64), (1, 64, 59, 59, 128),
+                                       (8, 128, 31, 31, 128), (4, 1024, 2, 2, 1024), (4, 512, 4, 4, 512),
+                                       (16, 256, 8, 8, 256), (5, 384, 9, 9, 128)])
 def test_halo_conv_matches_gather_kernel(N, C, H, W, K):
-    """The halo-staged 3x3 stride-1 kernels (set_conv_halo 2: every eligible fwd tile and
-    dgrad) == the per-tap gather kernels (set_conv_halo 0), bias+ReLU fwd epilogue,
-    split-K slices and channel-block reloads included."""
+    """The halo-staged 3x3 stride-1 kernels == the per-tap gather kernels (set_conv_halo 0),
+    bias+ReLU fwd epilogue, split-K slices (in-launch combine and slabs) and channel-block
+    reloads included: mode 1 (default: 256x64 tiles) and mode 2 (128x128 tiles too)."""
     torch.manual_seed(3)
     Cc = _ext.C()
     x = torch.randn(N, H, W, C, device="cuda").bfloat16()
@@ -152,7 +154,7 @@ def test_halo_conv_matches_gather_kernel(N, C, H, W, K):
     bias = torch.randn(K, device="cuda")
     outs = {}
     try:
-        for mode in (0, 2):
+        for mode in (0, 1, 2):
             Cc.set_conv_halo(mode)
             y = torch.empty(N, H, W, K, device="cuda", dtype=torch.bfloat16)
             Cc.conv_fwd(x, w, y, 1, 1, bias, Cc.EPI_BIAS_RELU)
@@ -161,6 +163,8 @@ def test_halo_conv_matches_gather_kernel(N, C, H, W, K):
             outs[mode] = (y.float(), dx.float())
     finally:
         Cc.set_conv_halo(1)
-    (y0, dx0), (y2, dx2) = outs[0], outs[2]
-    torch.testing.assert_close(y2, y0, rtol=2e-2, atol=2e-2 * y0.abs().max().item())
-    torch.testing.assert_close(dx2, dx0, rtol=2e-2, atol=2e-2 * dx0.abs().max().item())
+    (y0, dx0) = outs[0]
+    for mode in (1, 2):
+        y2, dx2 = outs[mode]
+        torch.testing.assert_close(y2, y0, rtol=2e-2, atol=2e-2 * y0.abs().max().item())
+        torch.testing.assert_close(dx2, dx0, rtol=2e-2, atol=2e-2 * dx0.abs().max().item())
