@@ -129,7 +129,8 @@ def run_ldnn(ctx, args):
                           bucket_cap_elems=args.bucket_elems, shard_optimizer=False if args.no_shard else None,
                           library_gemms=args.gemms == "library",
                           fuse_head_dgrad=False if args.no_fuse_head_dgrad else None,
-                          head_dgrad_mode=args.head_dgrad_mode, fuse_head_fwd=not args.no_fuse_head_fwd)
+                          head_dgrad_mode=args.head_dgrad_mode, fuse_head_fwd=not args.no_fuse_head_fwd,
+                          fuse_head_bwd=not args.no_fuse_head_bwd)
     if ctx.distributed:
         dist.broadcast(eng.flat.master, src=0)
         eng.flat.refresh_shadow()
@@ -327,6 +328,8 @@ def main():
                          "(fp32 wgrads, bias+ReLU forwards, hidden dgrad) on hipBLASLt, as an A/B baseline")
     ap.add_argument("--no-fuse-head-fwd", action="store_true",
                     help="A/B: separate head kernel instead of the logits in the last hidden forward's epilogue")
+    ap.add_argument("--no-fuse-head-bwd", action="store_true",
+                    help="A/B: head dgrad stream + separate head wgrad instead of the fused MFMA head backward")
     ap.add_argument("--no-fuse-head-dgrad", action="store_true",
                     help="separate head dgrad GEMM instead of the head kernel's fused dgrad (dReLU + dbias)")
     ap.add_argument("--head-dgrad-mode", type=int, default=-1,

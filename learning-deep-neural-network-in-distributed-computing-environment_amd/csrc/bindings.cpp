@@ -664,6 +664,57 @@ void head_dgrad_stream(const at::Tensor& h, const at::Tensor& W, const at::Tenso
   check(ldnn::head_dgrad_stream(p, cur_stream(h)), "head_dgrad_stream");
 }
 
+// the head's dgrad (as head_dgrad_stream) and wgrad (dW / db accumulated, pre-cleared) in one pass
+void head_bwd(const at::Tensor& h, const at::Tensor& W, const at::Tensor& dlogits, const at::Tensor& dh,
+              const at::Tensor& dW, const c10::optional<at::Tensor>& dbias, int64_t dgrad_epi,
+              const c10::optional<at::Tensor>& db) {
+  check_dev(h, at::kBFloat16, "h");
+  check_dev(W, at::kBFloat16, "W");
+  check_dev(dlogits, at::kBFloat16, "dlogits");
+  check_dev(dh, at::kBFloat16, "dh");
+  check_dev(dW, at::kFloat, "dW");
+  const int64_t B = h.size(0), K = h.size(1);
+  TORCH_CHECK(h.dim() == 2 && h.stride(1) == 1 && h.stride(0) % 8 == 0 && K % 64 == 0 && aligned16(h.data_ptr()),
+              "head_bwd: h must be [B][K] with K % 64 == 0 and 16-B aligned rows");
+  TORCH_CHECK(W.dim() == 2 && W.size(0) <= 16 && W.size(1) == K && W.stride(1) == 1, "head_bwd: W must be [<= 16][K]");
+  TORCH_CHECK(dlogits.is_contiguous() && dlogits.dim() == 2 && dlogits.size(0) == B && dlogits.size(1) == 16 &&
+                  aligned16(dlogits.data_ptr()),
+              "head_bwd: dlogits must be a contiguous [B][16] buffer");
+  TORCH_CHECK(dh.dim() == 2 && dh.size(0) == B && dh.size(1) == K && dh.stride(1) == 1 && dh.stride(0) % 8 == 0 &&
+                  aligned16(dh.data_ptr()),
+              "head_bwd: dh must be [B][K] with 16-B aligned rows");
+  TORCH_CHECK(dgrad_epi == ldnn::EPI_NONE || dgrad_epi == ldnn::EPI_DRELU, "head_bwd: dgrad_epi must be EPI_NONE / EPI_DRELU");
+  TORCH_CHECK(dW.dim() == 2 && dW.size(1) == K && dW.size(0) <= 16 && dW.stride(1) == 1, "head_bwd: dW must be [<= 16][K]");
+  ldnn::HeadParams p{};
+  p.h = bf16_ptr(h);
+  p.W = bf16_ptr(W);
+  p.dlogits = bf16_mut(dlogits);
+  p.B = (int)B;
+  p.K = (int)K;
+  p.ld = 16;
+  p.ldh = (int)h.stride(0);
+  p.ldw = (int)W.stride(0);
+  p.ldw_rows = (int)W.size(0);
+  p.dh = bf16_mut(dh);
+  p.lddh = (int)dh.stride(0);
+  p.dgrad_epi = (int)dgrad_epi;
+  p.dW = dW.data_ptr<float>();
+  p.lddw = (int)dW.stride(0);
+  p.nrows_w = (int)dW.size(0);
+  if (dbias.has_value()) {
+    check_dev(*dbias, at::kFloat, "dbias");
+    TORCH_CHECK(dbias->is_contiguous() && dbias->numel() >= K, "head_bwd: bad dbias");
+    p.dbias = dbias->data_ptr<float>();
+  }
+  if (db.has_value()) {
+    check_dev(*db, at::kFloat, "db");
+    TORCH_CHECK(db->is_contiguous() && db->numel() >= dW.size(0), "head_bwd: bad db");
+    p.db = db->data_ptr<float>();
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA g(h.device());
+  check(ldnn::head_bwd(p, cur_stream(h)), "head_bwd");
+}
+
 void head_wgrad(const at::Tensor& dz, const at::Tensor& h, const at::Tensor& dW, const c10::optional<at::Tensor>& db,
                 int64_t splits) {
   check_dev(dz, at::kBFloat16, "dz");
@@ -1386,6 +1437,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("head_dgrad_stream", &head_dgrad_stream, "streaming head dgrad: dh = (dlogits W) * act'(h), dbias += colsums",
         py::arg("h"), py::arg("W"), py::arg("dlogits"), py::arg("dh"), py::arg("dbias") = py::none(),
         py::arg("dgrad_epi") = (int64_t)ldnn::EPI_DRELU);
+  m.def("head_bwd", &head_bwd, "fused head dgrad + wgrad (dW / db / dbias accumulated: pre-cleared)", py::arg("h"),
+        py::arg("W"), py::arg("dlogits"), py::arg("dh"), py::arg("dW"), py::arg("dbias") = py::none(),
+        py::arg("dgrad_epi") = (int64_t)ldnn::EPI_DRELU, py::arg("db") = py::none());
   m.def("head_wgrad", &head_wgrad, "dW = dz^T h (+ db = colsum dz); splits > 1 accumulate atomically",
         py::arg("dz"), py::arg("h"), py::arg("dW"), py::arg("db") = py::none(), py::arg("splits") = 0);
   m.def("head_dgrad_max_k", &ldnn::head_dgrad_max_k);

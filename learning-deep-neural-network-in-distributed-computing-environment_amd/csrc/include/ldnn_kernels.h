@@ -302,6 +302,10 @@ struct HeadParams {
   //    global memory; 2: fused, h staged in LDS (1 / 2 need K <= head_dgrad_max_k()
   //    and dbias_ws for dbias)
   int dgrad_mode;
+  // head_bwd only: dW [nrows_w][lddw] fp32 += dlogits^T h, db [nrows_w] += column sums of dlogits
+  float* dW;
+  float* db;
+  int lddw, nrows_w;
 };
 hipError_t head_fwd_xent(const HeadParams& p, hipStream_t s);
 // Softmax-xent + argmax of logits = bias + sum_s parts[s][b][0..15] (the partial logits
@@ -311,6 +315,10 @@ hipError_t head_xent_parts(const HeadParams& p, const float* parts, int nparts, 
 // The streaming head dgrad alone (head_fwd_xent's dgrad_mode 0 second launch):
 // dh = (dlogits W) * act'(h), dbias += column sums of dh; needs ld == 16.
 hipError_t head_dgrad_stream(const HeadParams& p, hipStream_t s);
+// The head's dgrad (head_dgrad_stream's outputs) AND wgrad (head_wgrad's, accumulated into a
+// pre-cleared dW / db by fp32 atomics) in one pass over h, both products on the MFMA pipe;
+// needs ld == 16, K % 64 == 0, dgrad_epi EPI_NONE / EPI_DRELU, dbias (if any) pre-cleared.
+hipError_t head_bwd(const HeadParams& p, hipStream_t s);
 int head_dgrad_max_k();
 size_t head_dgrad_ws_floats(int B, int K);
 // out[i] = sum_s ws[s][i] (+ beta * out[i]) over n4 float4 columns and `splits` slabs

@@ -588,6 +588,208 @@ hipError_t head_dgrad_stream(const HeadParams& p, hipStream_t s) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// fused head backward: the head's dgrad AND wgrad in one pass over h (ld == 16)
+// ---------------------------------------------------------------------------
+//   dh[m][n] = act'(h[m][n]) * sum_c dlogits[m][c] W[c][n]      (bf16, dbias += column sums)
+//   dW[c][n] += sum_m dlogits[m][c] h[m][n]                      (fp32 atomics, pre-cleared)
+//   db[c]    += sum_m dlogits[m][c]
+// Both products are rank-16 and run on v_mfma_f32_16x16x16_bf16 (the VALU form of
+// head_dgrad_stream spends ~128 FMAs per 8 outputs: VALU-bound at ~62 us for a
+// 16384 x 4096 h on MI355X, and head_wgrad re-read the same 128 MB of h for another
+// ~34 us).  A wave owns a 64-column strip and walks 16-row blocks:
+//  * dgrad: 4 MFMAs (one per 4-column group t), operand A = W^T with its rows mapped to
+//    columns so that lane (g = l/16, r16 = l%16) ends up holding dh[m0 + r16][n0 + 8g ..
+//    8g+7] and [n0 + 32 + 8g .. 32 + 8g + 7] -- the same columns it loaded from h for the
+//    ReLU: two 16-B loads and two 16-B stores per lane, each instruction covering 64
+//    contiguous bytes of 16 rows (measured +x % over 32-B lane pieces).
+//  * wgrad: the block (h 16 x 64, dlogits 16 x 16) is staged in the wave's LDS slice and
+//    read back k-major with ds_read_b64_tr_b16 as the MFMA operands (k = the 16 rows):
+//    4 MFMAs per block accumulate dW^T[n][c] in 16 registers per lane.
+// The 4 waves of a workgroup take the same strip, interleaved 16-row blocks, and combine
+// their dW / dbias / db partials in LDS before one atomic per output per workgroup;
+// gridDim.y row groups (~2 workgroups per CU) add up by fp32 atomics.
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+constexpr int kHbUnroll = 4;  // 16-row blocks whose loads are in flight together per wave
+
+template <bool RELU>
+__global__ __launch_bounds__(256) void head_bwd_kernel(HeadParams p, int rows_per_wg) {
+  constexpr int kH = 16 * 128, kD = 16 * 32, kSt = kH + kD;  // one 16-row block: h + dlogits
+  constexpr int kWave = kHbUnroll * kSt;                      // a wave's staging slice
+  __shared__ __attribute__((aligned(16))) char smem[4 * kWave];  // staging, then the cross-wave partials
+  static_assert(4 * kWave >= 4 * 64 * 17 * 4, "the reduction scratch fits");
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int g = lane >> 4, r16 = lane & 15;
+  const int n0 = blockIdx.x * 64;
+  const int r_begin = blockIdx.y * rows_per_wg, r_end = min(p.B, r_begin + rows_per_wg);
+  char* const st = smem + wid * kWave;
+  typedef __attribute__((address_space(3))) bf16x4 lds_b4;
+
+  // lane (g, r16) owns row r16 of a block and columns n0 + hcol(k), k = 0..15: 8g..8g+7 and
+  // 32+8g..32+8g+7 (hcol(k) = 32*(k/8) + 8g + k%8), so each 16-B load / store instruction
+  // covers 64 contiguous bytes of a row
+  s16x4 wa[4];  // dgrad operand A_t: row i = r16 <-> column n0 + 32*(t/2) + 8*(i/4) + 4*(t%2) + i%4, k = classes 4g..4g+3
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int n = n0 + (t >> 1) * 32 + 8 * (r16 >> 2) + (t & 1) * 4 + (r16 & 3);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int c = 4 * g + q;
+      wa[t][q] = (c < p.ldw_rows && n < p.K) ? (short)p.W[(size_t)c * p.ldw + n] : (short)0;
+    }
+  }
+  floatx4 acc2[4];  // dW^T partial: [nt][r] <-> column n0 + 16nt + 4g + r, class r16
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc2[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+  float cs[16];  // dh column sums over this lane's rows: columns hcol(k)
+#pragma unroll
+  for (int k = 0; k < 16; ++k) cs[k] = 0.f;
+  float dbs[4] = {0.f, 0.f, 0.f, 0.f};  // db partial: classes 4g..4g+3
+  const int q = r16 >> 2, pp = r16 & 3;  // tr-read: lane 4q+p addresses row 4g+q, elements 4p..4p+3
+
+  for (int mb = r_begin + wid * 16; mb < r_end; mb += 64 * kHbUnroll) {
+    u16x8 hv[kHbUnroll][2];
+    uint2 dl[kHbUnroll];
+#pragma unroll
+    for (int u = 0; u < kHbUnroll; ++u) {
+      const int m = mb + u * 64 + r16;
+      hv[u][0] = hv[u][1] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      dl[u] = uint2{0u, 0u};
+      if (m < r_end) {
+        const bf16_t* hr = p.h + (size_t)m * p.ldh + n0 + 8 * g;
+        hv[u][0] = *reinterpret_cast<const u16x8*>(hr);
+        hv[u][1] = *reinterpret_cast<const u16x8*>(hr + 32);
+        dl[u] = *reinterpret_cast<const uint2*>(p.dlogits + (size_t)m * 16 + 4 * g);
+      }
+    }
+    // stage every block first (h rows of 128 B, dlogits rows of 32 B): one LDS wait per
+    // kHbUnroll blocks instead of two per block
+#pragma unroll
+    for (int u = 0; u < kHbUnroll; ++u) {
+      char* sb = st + u * kSt;
+      *reinterpret_cast<u16x8*>(sb + r16 * 128 + g * 16) = hv[u][0];
+      *reinterpret_cast<u16x8*>(sb + r16 * 128 + 64 + g * 16) = hv[u][1];
+      *reinterpret_cast<uint2*>(sb + kH + r16 * 32 + g * 8) = dl[u];
+    }
+#pragma unroll
+    for (int u = 0; u < kHbUnroll; ++u) {
+      const int m = mb + u * 64 + r16;
+      // ---- dgrad: lane holds dh[m][n0 + hcol(4t + r)] = d[t][r]
+      const s16x4 bl = __builtin_bit_cast(s16x4, dl[u]);
+      floatx4 d[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        d[t] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(wa[t], bl, floatx4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      u16x8 o[2];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const uint16_t hb = hv[u][k >> 3][k & 7];
+        float v = d[k >> 2][k & 3];
+        if constexpr (RELU) v = (short)hb > 0 ? v : 0.f;  // bf16 > 0 <=> sign clear and nonzero
+        const uint16_t ob = f2bf(v);
+        o[k >> 3][k & 7] = ob;
+        cs[k] += bf2f(ob);
+      }
+      if (m < r_end) {
+        bf16_t* dst = p.dh + (size_t)m * p.lddh + n0 + 8 * g;
+        *reinterpret_cast<u16x8*>(dst) = o[0];
+        *reinterpret_cast<u16x8*>(dst + 32) = o[1];
+      }
+#pragma unroll
+      for (int c = 0; c < 4; ++c) dbs[c] += bf2f((uint16_t)((c < 2 ? dl[u].x : dl[u].y) >> (16 * (c & 1))));
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's own staging writes landed
+    __builtin_amdgcn_wave_barrier();
+    // ---- wgrad: the staged blocks read back k-major (k = row) as MFMA operands; the next
+    // iteration's staging writes follow these reads in the wave's in-order LDS queue
+#pragma unroll
+    for (int u = 0; u < kHbUnroll; ++u) {
+      const char* sb = st + u * kSt;
+      const bf16x4 bd = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_b4*)(sb + kH + (4 * g + q) * 32 + pp * 8));
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const bf16x4 ah =
+            __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_b4*)(sb + (4 * g + q) * 128 + (16 * nt + 4 * pp) * 2));
+        acc2[nt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_bit_cast(s16x4, ah),
+                                                             __builtin_bit_cast(s16x4, bd), acc2[nt], 0, 0, 0);
+      }
+    }
+  }
+
+  // ---- reductions: over the 16 row lanes, then over the 4 waves (LDS), one atomic per output
+#pragma unroll
+  for (int k = 0; k < 16; ++k)
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) cs[k] += __shfl_xor(cs[k], o, 64);
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) dbs[q] += __shfl_xor(dbs[q], o, 64);
+  __syncthreads();  // every wave is done with its staging slice
+  float* red = reinterpret_cast<float*>(smem);  // [4 waves][64 lanes][17]: 16 dW values, then cs / dbs
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[(wid * 64 + lane) * 17 + nt * 4 + r] = acc2[nt][r];
+  __syncthreads();
+  if (wid == 0) {
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float t = 0.f;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) t += red[(w * 64 + lane) * 17 + nt * 4 + r];
+        const int n = n0 + 16 * nt + 4 * g + r;
+        if (r16 < p.nrows_w && n < p.K) atomicAdd(p.dW + (size_t)r16 * p.lddw + n, t);
+      }
+  }
+  __syncthreads();
+  // column sums: lanes r16 == 0 hold columns n0 + hcol(k); db: classes 4g + q
+  if (r16 == 0) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) red[(wid * 4 + g) * 17 + k] = cs[k];
+    red[(wid * 4 + g) * 17 + 16] = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) red[16 * 17 + (wid * 4 + g) * 4 + q] = dbs[q];
+  }
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const int gg = threadIdx.x >> 4, k = threadIdx.x & 15;
+    const int n = n0 + (k >> 3) * 32 + 8 * gg + (k & 7);
+    if (p.dbias != nullptr && n < p.K) {
+      float t = 0.f;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) t += red[(w * 4 + gg) * 17 + k];
+      atomicAdd(p.dbias + n, t);
+    }
+  } else if (threadIdx.x < 80 && blockIdx.x == 0 && p.db != nullptr) {
+    const int c = threadIdx.x - 64, gg = c >> 2, q = c & 3;
+    if (c < p.nrows_w) {
+      float t = 0.f;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) t += red[16 * 17 + (w * 4 + gg) * 4 + q];
+      atomicAdd(p.db + c, t);
+    }
+  }
+}
+
+hipError_t head_bwd(const HeadParams& p, hipStream_t s) {
+  if (p.B <= 0) return hipSuccess;
+  if (p.ld != 16 || p.dh == nullptr || p.dW == nullptr || p.lddh % 8 != 0 || p.ldh % 8 != 0 || p.K % 64 != 0 ||
+      p.ldw_rows > 16 || p.nrows_w > 16 || (p.dgrad_epi != EPI_NONE && p.dgrad_epi != EPI_DRELU))
+    return hipErrorInvalidValue;
+  const int gx = p.K / 64;
+  int gy = std::max(1, std::min(64, 768 / gx));  // ~3 workgroups per CU (the register-bound occupancy)
+  int rpw = (p.B + gy - 1) / gy;
+  rpw = (rpw + 63) & ~63;
+  gy = (p.B + rpw - 1) / rpw;
+  const dim3 grid(gx, gy);
+  if (p.dgrad_epi == EPI_DRELU) head_bwd_kernel<true><<<grid, 256, 0, s>>>(p, rpw);
+  else head_bwd_kernel<false><<<grid, 256, 0, s>>>(p, rpw);
+  return hipGetLastError();
+}
+
 size_t head_dgrad_ws_floats(int B, int K) { return (size_t)((B + 15) / 16) * K; }
 
 int head_dgrad_max_k() { return kHeadDgradMaxK; }

@@ -99,7 +99,7 @@ class StaticMLPEngine:
                  shard_optimizer: bool | None = None, wgrad_combine: bool = True, library_gemms: bool | None = None,
                  fuse_head_dgrad: bool | None = None, library_dgrad: bool | None = None, head_dgrad_mode: int = -1,
                  relu_masks: bool = True, transposed_dgrad: bool = True, bias_ones_column: bool = True,
-                 fuse_head_fwd: bool = True):
+                 fuse_head_fwd: bool = True, fuse_head_bwd: bool = True):
         from ..models.mlp import MLP
 
         if not isinstance(model, MLP):
@@ -370,6 +370,11 @@ class StaticMLPEngine:
             self.gshard = [torch.zeros((e - b) // self.world, dtype=torch.float32, device=dev)
                            for b, e, _ in self.buckets]
             self._gloo = dist.get_backend(process_group) == "gloo"
+        # fuse_head_bwd: the head's dgrad and wgrad in one pass over h_{L-1}, both on the MFMA
+        # pipe (head.hip head_bwd; the wgrad accumulates into the gradient the optimizer cleared)
+        self._fuse_head_bwd = bool(fuse_head_bwd and self._head_part is not None and L >= 2
+                                   and self._dgrad_epi[L - 1] in (self.C.EPI_NONE, self.C.EPI_DRELU)
+                                   and self.layers[L - 1].in_features % 64 == 0 and self._wgrad_splitk[L - 1] > 1)
         self._build_segments()
         self._slots[0]["segs"] = (self.segments, self.opt_segments)
 
@@ -385,6 +390,10 @@ class StaticMLPEngine:
         if self._head_part is not None:   # logits from the last hidden forward's partial products
             self.C.head_xent_parts(self._head_part, self.bias[L - 1], self.labels, self.h[L], self.dz[L], self.stats,
                                    self.num_classes, 1.0 / self.B)
+            if self._fuse_head_bwd:   # + the head's wgrad (dW, db) in the same pass over h
+                self.C.head_bwd(self.h[L - 1], self.W[L - 1], self.dz[L], self.dz[L - 1], self.dW[L - 1],
+                                self.db[L - 2], self._dgrad_epi[L - 1], self.db[L - 1])
+                return
             self.C.head_dgrad_stream(self.h[L - 1], self.W[L - 1], self.dz[L], self.dz[L - 1], self.db[L - 2],
                                      self._dgrad_epi[L - 1])
             return
@@ -405,7 +414,8 @@ class StaticMLPEngine:
     def _wgrad(self, l):
         sk = self._wgrad_splitk[l]
         if self.use_head and l == len(self.layers) - 1:   # also emits the head's bias gradient
-            self.C.head_wgrad(self.dz[l + 1], self.h[l], self.dW[l], self.db[l], sk)
+            if not self._fuse_head_bwd:   # (else done by head_bwd in _loss)
+                self.C.head_wgrad(self.dz[l + 1], self.h[l], self.dW[l], self.db[l], sk)
             return
         if self._lib_wgrad[l]:   # plain GEMM, fp32 out: hipBLASLt straight into the flat grad buffer
             torch.mm(self.dz[l + 1].t(), self.h[l], out_dtype=torch.float32, out=self.dW[l])
@@ -795,6 +805,9 @@ class StaticMLPEngine:
                 if self.head_dgrad:
                     d[f"dgrad{l}"] = ("ldnn head_dgrad_stream (dReLU + bias-gradient sums)" if self._head_stream
                                       else "ldnn head_fwd_xent fused dgrad")
+                if self._fuse_head_bwd:
+                    d[f"wgrad{l}"] = "ldnn head_bwd (with the dgrad: one pass over h, both on MFMA)"
+                    d[f"dgrad{l}"] = "ldnn head_bwd (dReLU + bias-gradient sums, MFMA)"
                 continue
             d[f"fwd{l}"] = ("hipBLASLt" if self._lib_fwd[l] else
                             "ldnn gemm_q (bias+ReLU" + (" + ReLU bit mask" if self.mask[l + 1] is not None else "")

@@ -98,6 +98,79 @@ def test_engine_fused_head_matches_separate_head(opt):
     for a, b in zip(l1, l2):
         assert abs(a[0] - b[0]) < 1e-3 * max(1.0, abs(b[0])), (l1, l2)
         assert abs(a[1] - b[1]) <= 0.5, (l1, l2)   # accuracy, percent
-    atol = 1e-4 if opt == "sgd" else 2e-3
+    # Adam: a gradient element near zero can flip sign between two summation orders (the
+    # GPU atomics' arrival order differs run to run), moving its weight by 2 lr per step
+    atol = 1e-4 if opt == "sgd" else 5 * cfg.lr
     for p, q in zip(m1.parameters(), m2.parameters()):
         torch.testing.assert_close(p.detach(), q.detach(), rtol=1e-3, atol=atol)
+
+
+@pytest.mark.parametrize("opt", ["sgd", "adam"])
+def test_engine_fused_head_bwd_matches_separate(opt):
+    """The engine's fused MFMA head backward (head_bwd: dgrad + wgrad in one pass) trains
+    like the head dgrad stream + head wgrad pair (hidden 1024, batch 4000)."""
+    from ldnn.models.mlp import mlp3
+    from ldnn.train.static_mlp import OptimConfig, StaticMLPEngine
+
+    torch.manual_seed(0)
+    B = 4000
+    m1, m2 = mlp3(784, 1024, 10), mlp3(784, 1024, 10)
+    m2.load_state_dict(m1.state_dict())
+    cfg = OptimConfig(opt, lr=0.05 if opt == "sgd" else 1e-3, momentum=0.9)
+    e1 = StaticMLPEngine(m1, B, cfg, use_graphs=True)
+    e2 = StaticMLPEngine(m2, B, cfg, use_graphs=True, fuse_head_bwd=False)
+    assert e1._fuse_head_bwd and not e2._fuse_head_bwd
+    g = torch.Generator(device="cuda").manual_seed(5)
+    for _ in range(5):
+        x = torch.randn(B, 784, device="cuda", generator=g).bfloat16()
+        y = torch.randint(0, 10, (B,), device="cuda", generator=g)
+        st = []
+        for e in (e1, e2):
+            e.reset_stats()
+            e.load_batch(x, y)
+            e.step()
+            st.append(e.read_stats(B))
+        assert abs(st[0][0] - st[1][0]) < 1e-3 * max(1.0, abs(st[1][0])), st
+    atol = 1e-4 if opt == "sgd" else 5 * cfg.lr
+    for p, q in zip(m1.parameters(), m2.parameters()):
+        torch.testing.assert_close(p.detach(), q.detach(), rtol=1e-3, atol=atol)
+
+
+@pytest.mark.parametrize("B,K,ncls,relu", [(1000, 512, 10, True), (16384, 4096, 10, True), (333, 128, 16, False),
+                                           (64, 64, 3, True)])
+def test_head_bwd_matches_fp32_and_stream_kernels(B, K, ncls, relu):
+    """head_bwd (fused head dgrad + wgrad on MFMA) == fp32 references of dh, its column sums, dW and db,
+    and agrees with the head_dgrad_stream + head_wgrad pair it replaces."""
+    C = _ext.C()
+    g = torch.Generator(device="cuda").manual_seed(7)
+    h = torch.randn(B, K, device="cuda", generator=g).bfloat16()
+    if relu:
+        h = torch.relu(h)
+    W = torch.zeros(16, K, device="cuda", dtype=torch.bfloat16)
+    W[:ncls] = (torch.randn(ncls, K, device="cuda", generator=g) / K ** 0.5).bfloat16()
+    dl = torch.zeros(B, 16, device="cuda", dtype=torch.bfloat16)
+    dl[:, :ncls] = (torch.randn(B, ncls, device="cuda", generator=g) / B).bfloat16()
+    epi = C.EPI_DRELU if relu else C.EPI_NONE
+    dh = torch.full((B, K), float("nan"), device="cuda", dtype=torch.bfloat16)
+    dbias = torch.zeros(K, device="cuda")
+    dW = torch.zeros(16, K, device="cuda")
+    db = torch.zeros(16, device="cuda")
+    C.head_bwd(h, W, dl, dh, dW, dbias, epi, db)
+    ref = dl.float() @ W.float()
+    if relu:
+        ref = ref * (h.float() > 0)
+    torch.testing.assert_close(dh.float(), ref, rtol=1e-2, atol=1e-2 * ref.abs().max().item())
+    torch.testing.assert_close(dbias, dh.float().sum(0), rtol=1e-3, atol=1e-3 * dbias.abs().max().item())
+    dW_ref = dl.float().t() @ h.float()
+    torch.testing.assert_close(dW, dW_ref, rtol=1e-3, atol=1e-3 * dW_ref.abs().max().item())
+    torch.testing.assert_close(db, dl.float().sum(0), rtol=1e-3, atol=1e-6)
+    # the kernels it replaces
+    dh2 = torch.empty_like(dh)
+    dbias2 = torch.zeros(K, device="cuda")
+    C.head_dgrad_stream(h, W, dl, dh2, dbias2, epi)
+    dW2 = torch.zeros(16, K, device="cuda")
+    db2 = torch.zeros(16, device="cuda")
+    C.head_wgrad(dl, h, dW2, db2, 4)
+    diff = (dh.float() - dh2.float()).abs().max().item()
+    assert diff <= 1e-2 * ref.abs().max().item(), diff
+    torch.testing.assert_close(dW, dW2, rtol=1e-4, atol=1e-4 * dW2.abs().max().item())
