@@ -75,7 +75,23 @@ struct LArgs {
   int f32_rows;      // fp32 outputs (wgrad, split-K slabs) through the row-coalesced LDS epilogue
   int bf16_rows;     // bf16 outputs (fwd y, stride-1 dgrad dx) through the row-coalesced LDS epilogue
   int remap_rows;    // stride-2 dgrad dx (class row remap) through the row-coalesced LDS epilogue
+  int xcd_split;     // split-K grids: the tiles of one K slice share an XCD (see split_coords)
 };
+
+// (tile, K slice) of this workgroup.  Default: tile = blockIdx.x, slice = blockIdx.y.  With
+// xcd_split the linear workgroup id goes through the XCD remap first, so the gridDim.x tiles
+// of one slice -- which read the same activation rows (a wgrad's filter-tap / channel tiles
+// over one npq range) -- are dispatched to ONE XCD and share its L2 instead of each of 8
+// XCDs fetching those rows from the Infinity Cache / HBM.
+__device__ __forceinline__ void split_coords(const LArgs& a, int& bx, int& by) {
+  bx = blockIdx.x;
+  by = blockIdx.y;
+  if (a.xcd_split && gridDim.y > 1) {
+    const int id = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
+    bx = id % gridDim.x;
+    by = id / gridDim.x;
+  }
+}
 
 // Per-workgroup geometry: which rows its class covers and which taps it sums.
 struct Geo {
@@ -614,22 +630,22 @@ __device__ __forceinline__ void wait_vm() {
 // (lds_floats floats), free once every wave is past its operand reads.
 template <int WM, int WN, int EPI, bool OUT_F32, bool DGRAD>
 __device__ __forceinline__ void conv_tail(const LArgs& a, const Geo& g, floatx4 (&acc)[4][4], int m0, int n0, int wm,
-                                          int wn, int lane, char* smem, int lds_floats) {
+                                          int wn, int lane, char* smem, int lds_floats, int bx, int by) {
   constexpr int NW = WM * WN;
   const bool combine = a.cnt != nullptr && gridDim.y > 1;
   const int mb = m0 + wm * 64, nbase = n0 + wn * 64;
   if (gridDim.y > 1) {
     if (combine) {
       lds_barrier();  // every wave is done with the operand stages (the ticket word lives there)
-      const int tile = blockIdx.z * a.tiles_x + blockIdx.x;
-      if (!splitk_combine<4, 4, NW * 64>(acc, a.ws, a.cnt, tile, gridDim.y, blockIdx.y, smem)) return;
+      const int tile = blockIdx.z * a.tiles_x + bx;
+      if (!splitk_combine<4, 4, NW * 64>(acc, a.ws, a.cnt, tile, gridDim.y, by, smem)) return;
     } else if (a.ws != nullptr) {
       // wgrad, and small-M fwd / stride-1 dgrad: this slice's fp32 partial tile into
       // its own slab; a separate chip-wide kernel sums the slabs (slab_sum_kernel /
       // conv_slab_epilogue_kernel with the bias / ReLU epilogue) -- deterministic, no
       // atomics, and no single workgroup re-reading every slice of its tile
       GemmParams p{};
-      p.C = a.ws + (size_t)blockIdx.y * a.M * a.N;
+      p.C = a.ws + (size_t)by * a.M * a.N;
       p.M = g.M;
       p.N = a.N;
       p.ldc = a.N;
@@ -692,14 +708,14 @@ __device__ __forceinline__ void conv_tail(const LArgs& a, const Geo& g, floatx4 
       else
         store_bf16_rows<EPI, 2>(p, acc, smem + (size_t)(wm * WN + wn) * 8192, mb, nbase, lane);
       if constexpr (!DGRAD && EPI == EPI_NONE) {
-        if (a.bn_stats) bn_stats_epilogue<WM, WN>(a, g, acc, mb, n0, wm, wn, lane, blockIdx.x, smem, lds_floats);
+        if (a.bn_stats) bn_stats_epilogue<WM, WN>(a, g, acc, mb, n0, wm, wn, lane, bx, smem, lds_floats);
       }
       return;
     }
   }
   epilogue<EPI, OUT_F32, 4, 4>(p, acc, mb, nbase, lane);
   if constexpr (!DGRAD && !OUT_F32 && EPI == EPI_NONE) {
-    if (a.bn_stats) bn_stats_epilogue<WM, WN>(a, g, acc, mb, n0, wm, wn, lane, blockIdx.x, smem, lds_floats);
+    if (a.bn_stats) bn_stats_epilogue<WM, WN>(a, g, acc, mb, n0, wm, wn, lane, bx, smem, lds_floats);
   }
 }
 
@@ -707,8 +723,9 @@ __device__ __forceinline__ void conv_tail(const LArgs& a, const Geo& g, floatx4 
 // kt+1 in flight while kt is multiplied.  NS = 3 / 4 (grids of at most one
 // workgroup per CU): K-tiles kt+1 .. kt+NS-1 in flight, a counted vmcnt (never 0
 // in the steady state) retires only tile kt before the barrier that publishes it.
-// XF (experiment builds only, LDNN_CONV_XF): bit0 no in-loop DMA, bit1 the A operand DMAs
-// contiguous 16-KiB-aligned chunks instead of the im2col gather, bit2 no fragment reads / MFMAs
+// XF (experiment builds only, LDNN_CONV_XF, on the 128x128 fwd / dgrad / wgrad and the narrow
+// wgrad kernels): bit0 no in-loop DMA, bit1 (fwd only) the A operand DMAs contiguous
+// 16-KiB-aligned chunks instead of the im2col gather, bit2 no fragment reads / MFMAs
 template <int WM, int WN, class OA, class OB, int EPI, bool OUT_F32, bool DGRAD, int NS, int XF = 0>
 __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void conv_lds_kernel(LArgs a, const bf16_t* pa, uint32_t bytes_a,
                                                                        const bf16_t* pb, uint32_t bytes_b) {
@@ -725,13 +742,20 @@ __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void conv_lds_kernel(LArgs a,
 
   const Geo g = make_geo(a, DGRAD);
   const int tiles_m = (g.M + BM - 1) / BM, tiles_n = (a.N + BN - 1) / BN;
-  if ((int)blockIdx.x >= tiles_m * tiles_n) return;  // a smaller parity class: whole workgroup exits
+  int bx, by;
+  split_coords(a, bx, by);
+  if (bx >= tiles_m * tiles_n) return;  // a smaller parity class: whole workgroup exits
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wid / WN, wn = wid % WN;
   int m0, n0;
-  tile_coords(g.M, a.N, BM, BN, m0, n0);
-  const int kt0 = blockIdx.y * a.nk_split;
+  if (a.xcd_split && gridDim.y > 1) {  // the XCD placement is split_coords'; tiles in row-major order
+    m0 = (bx / tiles_n) * BM;
+    n0 = (bx % tiles_n) * BN;
+  } else {
+    tile_coords(g.M, a.N, BM, BN, m0, n0);
+  }
+  const int kt0 = by * a.nk_split;
   const int nk = max(0, min(g.nk - kt0, a.nk_split));
   const bool combine = a.cnt != nullptr && gridDim.y > 1;
   if (nk == 0 && gridDim.y > 1 && !combine && a.ws == nullptr) return;  // an empty atomic slice adds nothing
@@ -781,7 +805,7 @@ __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void conv_lds_kernel(LArgs a,
         char* nxt = smem + (cur == 0 ? NS - 1 : cur - 1) * STAGE;  // stage of tile kt-1
         if constexpr ((XF & 2) != 0) {  // contiguous A chunks: the fill without the gather
           const uint32_t span = (bytes_a >> 1) & ~16383u;
-          const uint32_t tb = (uint32_t)(blockIdx.x * 9 + ks.kt) * (uint32_t)A_BYTES % span;
+          const uint32_t tb = (uint32_t)(bx * 9 + ks.kt) * (uint32_t)A_BYTES % span;
 #pragma unroll
           for (int i_ = 0; i_ < PPA; ++i_)
             __builtin_amdgcn_raw_ptr_buffer_load_lds(ra.r, (lds_void*)(nxt + (i_ * NW + wid) * 1024), 16,
@@ -820,7 +844,7 @@ __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void conv_lds_kernel(LArgs a,
     }
   }
 
-  conv_tail<WM, WN, EPI, OUT_F32, DGRAD>(a, g, acc, m0, n0, wm, wn, lane, smem, NS * STAGE / 4);
+  conv_tail<WM, WN, EPI, OUT_F32, DGRAD>(a, g, acc, m0, n0, wm, wn, lane, smem, NS * STAGE / 4, bx, by);
 }
 
 // ---- halo path: 3x3 stride-1 pad-1 fwd / dgrad with the A operand staged ONCE --
@@ -979,7 +1003,7 @@ __global__ __launch_bounds__(256, 2) void conv_halo_kernel(LArgs a, const bf16_t
       ks_next(a, g, kc);
     }
   }
-  conv_tail<WM, WN, EPI, false, DGRAD>(a, g, acc, m0, n0, wm, wn, lane, smem, LDS / 4);
+  conv_tail<WM, WN, EPI, false, DGRAD>(a, g, acc, m0, n0, wm, wn, lane, smem, LDS / 4, blockIdx.x, blockIdx.y);
 }
 
 // ---- patch path: small-C stems (C = 8: 3 / 1 real channels) -------------------
@@ -1086,7 +1110,8 @@ __global__ __launch_bounds__(256, 2) void conv_patch_kernel(LArgs a, const bf16_
       for (int i = 0; i < 4; ++i)
         acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[k & 1][j], fa[i], acc[j][i], 0, 0, 0);
   }
-  conv_tail<WM, WN, EPI, false, false>(a, g, acc, m0, n0, wm, wn, lane, smem, kPatchBytes / 4);
+  conv_tail<WM, WN, EPI, false, false>(a, g, acc, m0, n0, wm, wn, lane, smem, kPatchBytes / 4, blockIdx.x,
+                                       blockIdx.y);
 }
 
 int slab_nt_env() {
@@ -1194,6 +1219,13 @@ struct WgradPlan {
   int tiles, splits, nk_all, nk_split;
 };
 
+// LDNN_CONV_WGRAD_XCD (A/B knob, default 1): a split-K wgrad's tiles of one npq slice on
+// one XCD (split_coords)
+int wgrad_xcd_env() {
+  static const int v = env_int("LDNN_CONV_WGRAD_XCD", 1);
+  return v;
+}
+
 WgradPlan plan_wgrad(const ConvShape& s) {
   WgradPlan p;
   p.narrow = s.K <= 64;
@@ -1294,14 +1326,21 @@ hipError_t launch_ns(LArgs a, int epi, int splits, const bf16_t* pa, size_t ba, 
                      hipStream_t st) {
   constexpr int NW = WM * WN;
   dim3 grid(a.tiles_x, splits, a.classes), block(NW * 64);
-  if constexpr (std::is_same_v<OA, FwdA<128, 4, 4>> && NS == 2) {
+  if constexpr ((std::is_same_v<OA, FwdA<128, 4, 4>> || std::is_same_v<OA, WgradA<64, 2, 4>> ||
+                 std::is_same_v<OA, WgradA<128, 4, 4>> || std::is_same_v<OA, DgradA<128, 4, 4>>) && NS == 2) {
     const int xf = conv_xf_env();
     if (xf != 0 && epi == EPI_NONE) {
       switch (xf) {
         case 1: conv_lds_kernel<WM, WN, OA, OB, EPI_NONE, OUT_F32, DGRAD, NS, 1><<<grid, block, 0, st>>>(a, pa, (uint32_t)ba, pb, (uint32_t)bb); break;
-        case 2: conv_lds_kernel<WM, WN, OA, OB, EPI_NONE, OUT_F32, DGRAD, NS, 2><<<grid, block, 0, st>>>(a, pa, (uint32_t)ba, pb, (uint32_t)bb); break;
+        case 2:
+          if constexpr (!std::is_same_v<OA, FwdA<128, 4, 4>>) return hipErrorInvalidValue;
+          else conv_lds_kernel<WM, WN, OA, OB, EPI_NONE, OUT_F32, DGRAD, NS, 2><<<grid, block, 0, st>>>(a, pa, (uint32_t)ba, pb, (uint32_t)bb);
+          break;
         case 4: conv_lds_kernel<WM, WN, OA, OB, EPI_NONE, OUT_F32, DGRAD, NS, 4><<<grid, block, 0, st>>>(a, pa, (uint32_t)ba, pb, (uint32_t)bb); break;
-        case 6: conv_lds_kernel<WM, WN, OA, OB, EPI_NONE, OUT_F32, DGRAD, NS, 6><<<grid, block, 0, st>>>(a, pa, (uint32_t)ba, pb, (uint32_t)bb); break;
+        case 6:
+          if constexpr (!std::is_same_v<OA, FwdA<128, 4, 4>>) return hipErrorInvalidValue;
+          else conv_lds_kernel<WM, WN, OA, OB, EPI_NONE, OUT_F32, DGRAD, NS, 6><<<grid, block, 0, st>>>(a, pa, (uint32_t)ba, pb, (uint32_t)bb);
+          break;
         default: return hipErrorInvalidValue;
       }
       return hipGetLastError();
@@ -1703,6 +1742,7 @@ hipError_t conv2d_wgrad_lds(const ConvShape& s, const uint16_t* dy, const uint16
   a.f_c = make_fastdiv(s.C);
   a.f_s = make_fastdiv(s.S);
   const int splits = pl.splits;
+  a.xcd_split = splits > 1 ? wgrad_xcd_env() : 0;
   if (splits > 1) {
     if (ws != nullptr) {
       a.ws = ws;  // partial slabs + slab_sum_kernel
