@@ -1354,6 +1354,8 @@ PYBIND11_MODULE(_C, m) {
       py::arg("N"), py::arg("splitk"));
   m.def("set_conv_impl", &ldnn::set_conv_impl, "0 = LDS-DMA fast path where it applies, 1 = generic kernel only",
         py::arg("impl"));
+  m.def("set_conv_wgrad_ring", &ldnn::set_conv_wgrad_ring, "A/B: ring wgrad for 3x3 stride-1 convs: 1 = 64x64 layers (default), 2 = every eligible shape, 0 = off",
+        py::arg("mode"));
   m.def("set_conv_halo", &ldnn::set_conv_halo,
         "halo-staged 3x3 stride-1 conv: 0 off, 1 default (dgrad + 256x64 fwd tiles), 2 every eligible shape",
         py::arg("mode"));

@@ -140,6 +140,7 @@ void set_conv_impl(int impl);
 int get_conv_impl();
 // halo-staged 3x3 stride-1 conv path (conv_lds.hip): 0 = off, 1 = default dispatch
 // (dgrad + 256x64 fwd tiles), 2 = also the 128x128 fwd tiles
+void set_conv_wgrad_ring(int mode);  // 0: split-K wgrad everywhere, 1: the ring wgrad for 3x3 stride-1 convs
 void set_conv_halo(int mode);
 int get_conv_halo();
 

@@ -1006,6 +1006,173 @@ __global__ __launch_bounds__(256, 2) void conv_halo_kernel(LArgs a, const bf16_t
   conv_tail<WM, WN, EPI, false, DGRAD>(a, g, acc, m0, n0, wm, wn, lane, smem, LDS / 4, blockIdx.x, blockIdx.y);
 }
 
+// ---- ring wgrad: 3x3 stride-1 pad-1 weight gradient, activation rows staged once ----
+// The split-K wgrad above re-gathers x for every filter tap: a 128x128 tile's K-tile
+// moves 32 KiB through the LDS-DMA path for 2 MFLOP, and the pass is fill-bound (its
+// DMA alone takes 100-122 of 113-131 us at ResNet-18 C128 H28 b256,
+// profiles/r3/conv_fill_knockout_r3.txt).  Here ONE workgroup computes the whole
+// 64 x (9 taps x 64 channels) gradient block of a (64-filter, 64-channel) pair over a
+// slice of npq: per K-tile of 64 output pixels it DMAs the 64 x 64 dy tile (8 KiB) and
+// only the 64 NEW activation rows of a 256-row LDS ring (8 KiB: the 9 taps of
+// consecutive pixels read overlapping row windows, flattened pixel npq + (r-1) W +
+// (s-1)) -- 16 KiB per 4.7 MFLOP instead of 120 KiB.  Both operands are read k-major
+// (k = npq) with ds_read_b64_tr_b16 from 128-B rows (16-B chunks XOR-swizzled by row);
+// a tap that leaves the image (row / column edge) zeroes its activation element by a
+// per-lane mask (dy rows past the end read as zeros, so they need none).  Wave w owns
+// channels 16w.. of the block for all 9 taps (taps unrolled: every mask / offset choice
+// is compile-time): 9 x 4 MFMA accumulator tiles per wave; partial blocks go to fp32
+// slabs summed by slab_sum_kernel.  The tiles of one npq slice run on one XCD.
+namespace wr {
+constexpr int kRingRows = 256, kRingBytes = kRingRows * 128, kDyBytes = 64 * 128;
+}
+
+struct WRArgs {
+  int N, H, W, C, K, M;  // M = N*H*W output pixels (stride 1: = input pixels)
+  int nk, nk_split;      // K-tiles of 64 pixels, per slice
+  int kbn, cbn;          // 64-filter / 64-channel blocks
+  int HE;                // halo rows beyond a K-tile's 64: (2W + 2) rounded up to 8 (<= 128)
+  FastDiv f_w, f_h;
+  float* out;            // [slices][K][9C] fp32 slabs, or dw itself with one slice
+  float beta;            // one slice: out = acc + beta * out
+};
+
+__global__ __launch_bounds__(256, 2) void wgrad_ring_kernel(WRArgs a, const bf16_t* pdy, uint32_t bytes_dy,
+                                                            const bf16_t* px, uint32_t bytes_x) {
+  using namespace wr;
+  __shared__ __attribute__((aligned(1024))) char smem[2 * kDyBytes + kRingBytes];  // 48 KiB
+  char* const dyst = smem;
+  char* const ring = smem + 2 * kDyBytes;
+  typedef __attribute__((address_space(3))) bf16x4 lds_b4;
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4, r16 = lane & 15, qq = r16 >> 2, pp = r16 & 3;
+  const int ntiles = a.kbn * a.cbn;
+  const int id = xcd_remap(blockIdx.x, gridDim.x);  // the tiles of one slice on one XCD
+  const int slice = id / ntiles, tile = id - (id / ntiles) * ntiles;
+  const int kb = tile / a.cbn, cb = tile - (tile / a.cbn) * a.cbn;
+  const int kt0 = slice * a.nk_split;
+  const int nk = min(a.nk - kt0, a.nk_split);
+
+  floatx4 acc[9][4];
+#pragma unroll
+  for (int j = 0; j < 9; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[j][i] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  if (nk > 0) {
+    Rsrc rdy, rx;
+    rdy.r = __builtin_amdgcn_make_buffer_rsrc((void*)pdy, (short)0, (int)bytes_dy, 0x00020000);
+    rx.r = __builtin_amdgcn_make_buffer_rsrc((void*)px, (short)0, (int)bytes_x, 0x00020000);
+    const int hb = kt0 * 64 - (a.W + 1);  // pixel of ring slot 0
+    const int jrow = lane >> 3, jslot = lane & 7;
+    // dy K-tile kt into stage `st`: 8 pieces of 8 rows, pieces wid and wid + 4
+    auto load_dy = [&](int kt, int st) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int pc = wid + 4 * h;
+        const int j = pc * 8 + jrow;
+        const int k = jslot ^ (j & 7);
+        const uint32_t o = ((uint32_t)(kt * 64 + j) * (uint32_t)a.K + (uint32_t)(kb * 64 + k * 8)) * 2u;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rdy.r, (lds_void*)(dyst + st * kDyBytes + pc * 1024), 16, (int)o, 0,
+                                                 0, 0);
+      }
+    };
+    // ring rows [p0, p0 + n): n % 8 == 0, (p0 - hb) % 8 == 0; piece i issued by wave i % 4
+    auto load_rows = [&](int p0, int n) {
+      for (int pc = wid; pc < (n >> 3); pc += 4) {
+        const int pix0 = p0 + pc * 8;
+        const int slot0 = (pix0 - hb) & (kRingRows - 1);
+        const int pix = pix0 + jrow;
+        const int k = jslot ^ jrow;
+        const int o = pix >= 0 ? (int)(((uint32_t)pix * (uint32_t)a.C + (uint32_t)(cb * 64 + k * 8)) * 2u) : (int)kOOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rx.r, (lds_void*)(ring + slot0 * 128), 16, o, 0, 0, 0);
+      }
+    };
+    load_dy(kt0, 0);
+    load_rows(hb, 64 + a.HE);
+    const int cc = 2 * wid + (pp >> 1);  // this wave's 16 channels cb*64 + 16 wid ..: 16-B chunk of the tr reads
+    for (int t = 0; t < nk; ++t) {
+      wait_vm<0>();
+      lds_barrier();  // publishes K-tile t; every wave is done with K-tile t-1's dy stage
+      if (t + 1 < nk) {
+        load_dy(kt0 + t + 1, (t + 1) & 1);
+        load_rows(hb + 64 * (t + 1) + a.HE, 64);
+      }
+      const char* dys = dyst + (t & 1) * kDyBytes;
+      const int npq0 = (kt0 + t) * 64;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        // this lane's 8 pixels b + e (b = npq0 + 32kk + 8g) cross at most one image row (W >= 8):
+        // elements e >= ew are in the next row.  Edge masks (bit e = tap element valid):
+        const int b = npq0 + 32 * kk + 8 * g;
+        const int t1 = fdiv(b, a.f_w), q0 = b - t1 * a.W;
+        const int p0 = t1 - fdiv(t1, a.f_h) * a.H;
+        const int ew = a.W - q0;                                  // >= 1
+        const uint32_t low = ew >= 8 ? 0xffu : (1u << ew) - 1u;  // elements in row p0
+        const uint32_t row0 = (p0 == 0 ? ~low : 0xffu) & (p0 + 1 == a.H ? low : 0xffu) & 0xffu;  // tap row r = 0
+        const uint32_t row2 = (p0 + 1 == a.H ? ~low : 0xffu) & (p0 + 2 == a.H ? low : 0xffu) & 0xffu;  // r = 2
+        const uint32_t col0 = 0xffu & ~(q0 == 0 ? 1u : 0u) & ~(ew < 8 ? 1u << ew : 0u);        // s = 0: q >= 1
+        const uint32_t col2 = 0xffu & ~(ew - 1 < 8 ? 1u << (ew - 1) : 0u);                      // s = 2: q <= W-2
+        auto words = [](uint32_t m, u32x4& w) {
+#pragma unroll
+          for (int h = 0; h < 4; ++h)
+            w[h] = ((0u - ((m >> (2 * h)) & 1u)) & 0xffffu) | ((0u - ((m >> (2 * h + 1)) & 1u)) << 16);
+        };
+        u32x4 wr0, wr2, wc0, wc2;
+        words(row0, wr0);
+        words(row2, wr2);
+        words(col0, wc0);
+        words(col2, wc2);
+        // dy fragments (A: rows = filters i*16 + r16, k = pixels)
+        bf16x8 fa[4];
+        const int rl = 32 * kk + 8 * g + qq;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int c = 2 * i + (pp >> 1);
+          const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+              (lds_b4*)(dys + rl * 128 + ((c ^ (rl & 7)) << 4) + 8 * (pp & 1)));
+          const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+              (lds_b4*)(dys + (rl + 4) * 128 + ((c ^ ((rl + 4) & 7)) << 4) + 8 * (pp & 1)));
+          fa[i] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        }
+        const int sb = npq0 + rl - hb;  // ring position of this lane's row at tap offset 0
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) {
+          const int r = tap / 3, sc = tap % 3;  // compile-time
+          const int s0 = (sb + (r - 1) * a.W + (sc - 1)) & (kRingRows - 1);
+          const int s1 = (s0 + 4) & (kRingRows - 1);
+          const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+              (lds_b4*)(ring + s0 * 128 + ((cc ^ (s0 & 7)) << 4) + 8 * (pp & 1)));
+          const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+              (lds_b4*)(ring + s1 * 128 + ((cc ^ (s1 & 7)) << 4) + 8 * (pp & 1)));
+          u32x4 w = __builtin_bit_cast(u32x4, bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]});
+          if (r == 0) w &= wr0;
+          if (r == 2) w &= wr2;
+          if (sc == 0) w &= wc0;
+          if (sc == 2) w &= wc2;
+          const bf16x8 fb = __builtin_bit_cast(bf16x8, w);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) acc[tap][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb, fa[i], acc[tap][i], 0, 0, 0);
+        }
+      }
+    }
+  }
+  // lane holds out[filter kb*64 + 16i + r16][tap * C + cb*64 + 16*wid + 4g + 0..3]
+  float* outp = a.out + (gridDim.x > (unsigned)ntiles ? (size_t)slice * a.K * 9 * a.C : 0);
+  const int ldo = 9 * a.C;
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap) {
+    const int col = tap * a.C + cb * 64 + 16 * wid + 4 * g;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float* o = outp + (size_t)(kb * 64 + 16 * i + r16) * ldo + col;
+      floatx4 v = acc[tap][i];
+      if (gridDim.x == (unsigned)ntiles && a.beta != 0.f) v += a.beta * *reinterpret_cast<const floatx4*>(o);
+      *reinterpret_cast<floatx4*>(o) = v;
+    }
+  }
+}
+
 // ---- patch path: small-C stems (C = 8: 3 / 1 real channels) -------------------
 // FwdASmallC gathers one 16-B (tap, 8-channel) chunk per lane per tap: every input
 // pixel crosses the L1 / texture path once per filter tap that covers it (49x for
@@ -1216,8 +1383,26 @@ int env_int(const char* name, int dflt) {
 
 struct WgradPlan {
   bool narrow;
+  bool ring;  // wgrad_ring_kernel (3x3 s1 p1, C % 64 == K % 64 == 0, 8 <= W <= 63)
   int tiles, splits, nk_all, nk_split;
 };
+
+// LDNN_CONV_WGRAD_RING (A/B knob): 1 (default) the ring wgrad for the 64-filter x 64-channel
+// 3x3 stride-1 convs (ResNet-18 layer 1: 56 -> 43 us at b64, 178 -> 117 us at b256, where the
+// split-K kernel's 64x256 tiles re-read dy 3x and waste a quarter of their MFMAs); 2 also
+// for wider layers (measured equal at ResNet-18 28x28 / 14x14, slower at EnhancedCNN's 16x16
+// / 8x8 b64, whose ~20 K-tiles per block leave too few workgroups:
+// profiles/r3/wgrad_ring_ab_r3.txt); 0 off
+int g_wgrad_ring = -2;  // -2: not read yet
+int wgrad_ring_env() {
+  if (g_wgrad_ring == -2) g_wgrad_ring = env_int("LDNN_CONV_WGRAD_RING", 1);
+  return g_wgrad_ring;
+}
+bool wgrad_ring_ok(const ConvShape& s) {
+  const int m = wgrad_ring_env();
+  return m != 0 && s.R == 3 && s.S == 3 && s.stride == 1 && s.pad == 1 && s.P == s.H && s.Q == s.W &&
+         s.C % 64 == 0 && s.K % 64 == 0 && s.W >= 8 && s.W <= 63 && (m == 2 || (s.C == 64 && s.K == 64));
+}
 
 // LDNN_CONV_WGRAD_XCD (A/B knob, default 1): a split-K wgrad's tiles of one npq slice on
 // one XCD (split_coords)
@@ -1228,6 +1413,17 @@ int wgrad_xcd_env() {
 
 WgradPlan plan_wgrad(const ConvShape& s) {
   WgradPlan p;
+  p.ring = wgrad_ring_ok(s);
+  if (p.ring) {  // (64 filters x 576 tap-channels) blocks x npq slices of >= 12 K-tiles, ~384 workgroups
+    static const int target = env_int("LDNN_CONV_RING_TARGET", 384);
+    p.narrow = false;
+    p.tiles = (s.K / 64) * (s.C / 64);
+    p.nk_all = (s.N * s.P * s.Q + 63) / 64;
+    int splits = std::max(1, std::min(target / p.tiles, p.nk_all / 12));
+    p.nk_split = (p.nk_all + splits - 1) / splits;
+    p.splits = (p.nk_all + p.nk_split - 1) / p.nk_split;
+    return p;
+  }
   p.narrow = s.K <= 64;
   const int BM = p.narrow ? 64 : 128, BN = p.narrow ? 256 : 128;
   const int M = s.K, N = s.R * s.S * s.C;
@@ -1527,6 +1723,7 @@ ConvWorkspace ws_of(const Plan& p) {
 using namespace convlds;
 
 void set_conv_halo(int mode) { g_conv_halo = mode; }
+void set_conv_wgrad_ring(int mode) { g_wgrad_ring = mode; }
 int get_conv_halo() { return halo_env(); }
 
 ConvWorkspace conv2d_lds_workspace(const ConvShape& s, int op) {
@@ -1723,6 +1920,30 @@ hipError_t conv2d_wgrad_lds(const ConvShape& s, const uint16_t* dy, const uint16
   if (!shape_ok(s) || s.C % 8 != 0 || s.K % 8 != 0) return hipErrorNotSupported;
   if (beta != 0.f && beta != 1.f) return hipErrorNotSupported;
   const WgradPlan pl = plan_wgrad(s);
+  if (pl.ring) {
+    WRArgs r{};
+    r.N = s.N; r.H = s.H; r.W = s.W; r.C = s.C; r.K = s.K;
+    r.M = s.N * s.H * s.W;
+    r.nk = pl.nk_all;
+    r.nk_split = pl.nk_split;
+    r.kbn = s.K / 64;
+    r.cbn = s.C / 64;
+    r.HE = (2 * s.W + 2 + 7) & ~7;
+    r.f_w = make_fastdiv(s.W);
+    r.f_h = make_fastdiv(s.H);
+    r.beta = beta;
+    const bool slab = pl.splits > 1;
+    if (slab && ws == nullptr) return hipErrorNotSupported;  // (conv2d_lds_workspace sizes the slabs)
+    r.out = slab ? ws : dw;
+    const size_t bdy = (size_t)s.N * s.P * s.Q * s.K * 2, bx = (size_t)s.N * s.H * s.W * s.C * 2;
+    wgrad_ring_kernel<<<pl.splits * pl.tiles, 256, 0, st>>>(r, dy, (uint32_t)bdy, x, (uint32_t)bx);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || !slab) return e;
+    const int64_t n4 = (int64_t)s.K * 9 * s.C / 4;
+    if (slab_nt_env()) slab_sum_kernel<true><<<(unsigned)((n4 + 31) / 32), 256, 0, st>>>(ws, dw, n4, pl.splits, beta);
+    else slab_sum_kernel<false><<<(unsigned)((n4 + 31) / 32), 256, 0, st>>>(ws, dw, n4, pl.splits, beta);
+    return hipGetLastError();
+  }
   LArgs a = base_args(s);
   a.out = dw;
   a.beta = beta;

@@ -168,3 +168,35 @@ def test_halo_conv_matches_gather_kernel(N, C, H, W, K):
         y2, dx2 = outs[mode]
         torch.testing.assert_close(y2, y0, rtol=2e-2, atol=2e-2 * y0.abs().max().item())
         torch.testing.assert_close(dx2, dx0, rtol=2e-2, atol=2e-2 * dx0.abs().max().item())
+
+
+@pytest.mark.parametrize("N,C,H,W,K", [(2, 64, 56, 56, 64), (3, 128, 28, 28, 128), (2, 256, 14, 14, 512),
+                                       (4, 512, 7, 7, 512), (5, 64, 9, 9, 128), (2, 128, 16, 16, 256),
+                                       (1, 64, 63, 63, 64), (7, 192, 4, 4, 64), (3, 64, 5, 5, 64), (2, 64, 8, 8, 128), (3, 128, 9, 11, 64)])
+def test_ring_wgrad_matches_fp32_and_split_k(N, C, H, W, K):
+    """The ring wgrad (3x3 stride 1: 64 x 576 blocks, activation rows staged once in an LDS
+    ring, edge taps masked) == the fp32 reference and == the split-K gather wgrad, with beta
+    0 (slab sum overwrites) and beta 1 (accumulates)."""
+    torch.manual_seed(5)
+    Cc = _ext.C()
+    x = torch.randn(N, H, W, C, device="cuda").bfloat16()
+    gy = torch.randn(N, H, W, K, device="cuda").bfloat16()
+    ref = torch.nn.grad.conv2d_weight(x.float().permute(0, 3, 1, 2), (K, C, 3, 3), gy.float().permute(0, 3, 1, 2),
+                                      stride=1, padding=1).permute(0, 2, 3, 1)
+    outs = {}
+    try:
+        for mode in (2, 0):   # 2: the ring wgrad on every eligible shape (default 1: 64 x 64 layers)
+            Cc.set_conv_wgrad_ring(mode)
+            dw = torch.full((K, 3, 3, C), float("nan"), device="cuda")
+            Cc.conv_wgrad(gy, x, dw, 1, 1)
+            base = torch.randn(K, 3, 3, C, device="cuda")
+            acc = base.clone()
+            Cc.conv_wgrad(gy, x, acc, 1, 1, 1.0)
+            outs[mode] = (dw, acc - base)
+    finally:
+        Cc.set_conv_wgrad_ring(1)
+    for mode in (2, 0):
+        dw, dacc = outs[mode]
+        torch.testing.assert_close(dw, ref, rtol=1e-3, atol=1e-3 * ref.abs().max().item())
+        torch.testing.assert_close(dacc, ref, rtol=1e-3, atol=2e-3 * ref.abs().max().item())
+    torch.testing.assert_close(outs[2][0], outs[0][0], rtol=1e-4, atol=1e-4 * ref.abs().max().item())
