@@ -949,7 +949,7 @@ void conv_dgrad(const at::Tensor& dy, const at::Tensor& w, const at::Tensor& dx,
 }
 
 void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& dw, int64_t stride, int64_t pad,
-                double beta) {
+                double beta, int64_t real_channels) {
   check_dev(dy, at::kBFloat16, "dy");
   check_dev(x, at::kBFloat16, "x");
   check_dev(dw, at::kFloat, "dw");
@@ -960,6 +960,7 @@ void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& dw,
   s.K = (int)dw.size(0); s.R = (int)dw.size(1); s.S = (int)dw.size(2);
   s.P = (int)dy.size(1); s.Q = (int)dy.size(2);
   s.stride = (int)stride; s.pad = (int)pad;
+  s.c_real = real_channels > 0 && real_channels < s.C ? (int)real_channels : 0;
   TORCH_CHECK(dw.size(3) == s.C && dy.size(3) == s.K && dy.size(0) == s.N, "conv_wgrad: shape mismatch");
   TORCH_CHECK(s.C % 8 == 0 && s.K % 8 == 0, "conv_wgrad: channels must be multiples of 8");
   c10::hip::HIPGuardMasqueradingAsCUDA g(dy.device());
@@ -1354,6 +1355,8 @@ PYBIND11_MODULE(_C, m) {
       py::arg("N"), py::arg("splitk"));
   m.def("set_conv_impl", &ldnn::set_conv_impl, "0 = LDS-DMA fast path where it applies, 1 = generic kernel only",
         py::arg("impl"));
+  m.def("set_conv_stem_s2d", &ldnn::set_conv_stem_s2d, "A/B: 1 = space-to-depth stem wgrad (default), 0 = off",
+        py::arg("mode"));
   m.def("set_conv_wgrad_ring", &ldnn::set_conv_wgrad_ring, "A/B: ring wgrad for 3x3 stride-1 convs: 1 = 64x64 layers (default), 2 = every eligible shape, 0 = off",
         py::arg("mode"));
   m.def("set_conv_halo", &ldnn::set_conv_halo,
@@ -1469,7 +1472,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("bn_num_batches") = py::none());
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("stride"), py::arg("pad"));
   m.def("conv_wgrad", &conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("dw"), py::arg("stride"), py::arg("pad"),
-        py::arg("beta") = 0.0);
+        py::arg("beta") = 0.0, py::arg("real_channels") = 0,
+        "real_channels: channels of x that carry data (the rest zero padding, e.g. 3 of a stem's 8); 0 = all");
   m.def("synth_normal", &synth_normal);
   m.def("synth_labels", &synth_labels);
   m.def("augment_batch", &augment_batch, "gather + AutoAugment / flip+crop + normalise (augment.hip)");

@@ -105,6 +105,7 @@ struct ConvShape {
   int K, R, S;      // output channels (padded to a multiple of 8), filter
   int P, Q;         // output spatial size
   int stride, pad;
+  int c_real;       // channels of C that carry data (the rest are zero padding); 0 = all C
 };
 // ws / cnt: optional in-launch split-K workspace for small-M shapes (conv2d_lds_workspace);
 // without it those shapes run unsplit.
@@ -140,6 +141,7 @@ void set_conv_impl(int impl);
 int get_conv_impl();
 // halo-staged 3x3 stride-1 conv path (conv_lds.hip): 0 = off, 1 = default dispatch
 // (dgrad + 256x64 fwd tiles), 2 = also the 128x128 fwd tiles
+void set_conv_stem_s2d(int mode);   // 0: split-K stem wgrad, 1: space-to-depth stem wgrad (default)
 void set_conv_wgrad_ring(int mode);  // 0: split-K wgrad everywhere, 1: the ring wgrad for 3x3 stride-1 convs
 void set_conv_halo(int mode);
 int get_conv_halo();

@@ -1173,6 +1173,163 @@ __global__ __launch_bounds__(256, 2) void wgrad_ring_kernel(WRArgs a, const bf16
   }
 }
 
+// ---- stem wgrad via space-to-depth (7x7 stride-2 pad-3, C = 8 with <= 4 real channels) ----
+// The split-K wgrad gathers the C = 8 stem's activation as one 16-B pixel per (tap, pixel)
+// element: 40 KiB of 16-B pieces per K-tile, ~300 TFLOP/s, the largest kernel of the
+// ResNet-18 b64 step (131 us).  Rewritten on the 2x2 space-to-depth image
+//   xs[n][i][j][(dh*2 + dw)*4 + c] = x[n][2(i-2) + dh][2(j-2) + dw][c]   (zero outside),
+// the stem is a 4x4 stride-1 unpadded conv with 16 channels:
+//   y[p][q] = sum_{a,b<4} w'[a][b][.] . xs[p+a][q+b][.],  w'[a][b][dh,dw,c] = w[2a+dh-1][2b+dw-1][c]
+// so its weight gradient dW'[k][a][b][16] = sum_pq dy[p][q][k] xs[p+a][q+b][.] needs no
+// gather and no masks: per K-step (32 output pixels of one row) a workgroup DMAs the dy rows
+// (4 KiB) and 4 activation row segments of 36 s2d pixels (4 x 1.1 KiB), wave a multiplies
+// taps (a, 0..3) -- 16 MFMAs; 256 x 64 fp32 partial blocks per slice, summed and scattered
+// back to dW[k][r][s][c] by stem_s2d_sum_kernel.
+namespace s2d {
+constexpr int kDy = 32 * 128, kSeg = 2048, kStage = kDy + 4 * kSeg;  // 12 KiB per stage
+constexpr int kStages = 4;  // K-steps t+1 .. t+2 in flight while t is multiplied (t+3 issued after its barrier)
+}
+
+__global__ __launch_bounds__(256) void stem_s2d_pack_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ xs,
+                                                            int N, int H, int W, int Hs, int Ws) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // s2d pixel
+  if (i >= (int64_t)N * Hs * Ws) return;
+  const int jj = (int)(i % Ws);
+  const int64_t t = i / Ws;
+  const int ii = (int)(t % Hs), n = (int)(t / Hs);
+  u16x8 o[2];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {  // d = dh*2 + dw
+    const int h = 2 * (ii - 2) + (d >> 1), w = 2 * (jj - 2) + (d & 1);
+    u16x4 v = {0, 0, 0, 0};
+    if (h >= 0 && h < H && w >= 0 && w < W)
+      v = *reinterpret_cast<const u16x4*>(x + (((size_t)n * H + h) * W + w) * 8);  // channels 0..3
+#pragma unroll
+    for (int c = 0; c < 4; ++c) o[d >> 1][(d & 1) * 4 + c] = v[c];
+  }
+  u16x8* dst = reinterpret_cast<u16x8*>(xs + i * 16);
+  dst[0] = o[0];
+  dst[1] = o[1];
+}
+
+struct S2dArgs {
+  int N, P, Q, Hs, Ws, K;   // output P x Q, s2d image Hs x Ws (= P + 3, Q + 3), filters K (= 64)
+  int nchunk, steps, steps_per;  // 32-pixel chunks per output row; total K-steps; per slice
+  float* slab;              // [slices][64][256]
+};
+
+__global__ __launch_bounds__(256, 2) void stem_s2d_wgrad_kernel(S2dArgs a, const bf16_t* pdy, uint32_t bytes_dy,
+                                                                const bf16_t* pxs, uint32_t bytes_xs) {
+  using namespace s2d;
+  __shared__ __attribute__((aligned(1024))) char smem[kStages * kStage];  // 48 KiB
+  typedef __attribute__((address_space(3))) bf16x4 lds_b4;
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // = filter-row tap a
+  const int g = lane >> 4, r16 = lane & 15, qq = r16 >> 2, pp = r16 & 3;
+  const int st0 = blockIdx.x * a.steps_per;
+  const int nst = min(a.steps - st0, a.steps_per);
+  floatx4 acc[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[j][i] = floatx4{0.f, 0.f, 0.f, 0.f};
+  if (nst > 0) {
+    Rsrc rdy, rxs;
+    rdy.r = __builtin_amdgcn_make_buffer_rsrc((void*)pdy, (short)0, (int)bytes_dy, 0x00020000);
+    rxs.r = __builtin_amdgcn_make_buffer_rsrc((void*)pxs, (short)0, (int)bytes_xs, 0x00020000);
+    // K-step st = (n * P + p) * nchunk + chunk: dy rows of pixels (n, p, 32 chunk ..), the 4 s2d
+    // row segments (n, p + a, 32 chunk .. + 35); wave `wid` DMAs dy piece wid and segment a = wid
+    auto load = [&](int st, char* dst) {
+      const int chunk = st % a.nchunk, row = st / a.nchunk;  // row = n * P + p
+      const int p = row % a.P, n = row / a.P;
+      const int q0 = chunk * 32;
+      {
+        const int j = wid * 8 + (lane >> 3);
+        const int k = (lane & 7) ^ (j & 7);
+        const int o = q0 + j < a.Q ? (int)(((uint32_t)(row * a.Q + q0 + j) * (uint32_t)a.K + (uint32_t)(k * 8)) * 2u)
+                                   : (int)kOOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rdy.r, (lds_void*)(dst + wid * 1024), 16, o, 0, 0, 0);
+      }
+      const uint32_t pix0 = ((uint32_t)(n * a.Hs + p + wid) * (uint32_t)a.Ws + (uint32_t)q0);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {  // 64 s2d pixels x 32 B from q0 (only 35 are read)
+        const uint32_t o = (pix0 + (uint32_t)(h * 32 + (lane >> 1))) * 32u + (uint32_t)(lane & 1) * 16u;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rxs.r, (lds_void*)(dst + kDy + wid * kSeg + h * 1024), 16, (int)o, 0,
+                                                 0, 0);
+      }
+    };
+    // three DMA instructions per wave per K-step; steps 0..2 in the prologue, step t+3 after
+    // the barrier of step t (into the stage of step t-1), a counted wait keeps two in flight
+#pragma unroll
+    for (int t = 0; t < kStages - 1; ++t)
+      if (t < nst) load(st0 + t, smem + t * kStage);
+    for (int t = 0; t < nst; ++t) {
+      const int ahead = min(nst, t + kStages - 1) - t - 1;  // steps issued after t
+      if (ahead >= 2) wait_vm<6>();
+      else if (ahead == 1) wait_vm<3>();
+      else wait_vm<0>();
+      lds_barrier();  // publishes step t; every wave is done with step t-1's stage
+      if (t + kStages - 1 < nst) load(st0 + t + kStages - 1, smem + ((t + kStages - 1) % kStages) * kStage);
+      const char* stg = smem + (t % kStages) * kStage;
+      const int rl = 8 * g + qq;
+      bf16x8 fa[4];  // dy: rows = filters 16i + r16, k = the step's 32 pixels
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int c = 2 * i + (pp >> 1);
+        const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+            (lds_b4*)(stg + rl * 128 + ((c ^ (rl & 7)) << 4) + 8 * (pp & 1)));
+        const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+            (lds_b4*)(stg + (rl + 4) * 128 + ((c ^ ((rl + 4) & 7)) << 4) + 8 * (pp & 1)));
+        fa[i] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+      const char* seg = stg + kDy + wid * kSeg;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {  // tap (a = wid, b): s2d pixel q + b, 16 channels
+        const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_b4*)(seg + (rl + b) * 32 + 8 * pp));
+        const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_b4*)(seg + (rl + 4 + b) * 32 + 8 * pp));
+        const bf16x8 fb = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[b][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb, fa[i], acc[b][i], 0, 0, 0);
+      }
+    }
+  }
+  // lane holds dW'[filter 16i + r16][tap (wid, b) * 16 + 4g + 0..3]
+  float* o = a.slab + (size_t)blockIdx.x * 64 * 256;
+#pragma unroll
+  for (int b = 0; b < 4; ++b)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      *reinterpret_cast<floatx4*>(o + (size_t)(16 * i + r16) * 256 + (wid * 4 + b) * 16 + 4 * g) = acc[b][i];
+}
+
+// dW[k][r][s][c] (7 x 7 x 8) = sum over slices of dW'[k][a][b][(dh,dw,c)], r = 2a+dh-1, s = 2b+dw-1
+// (channels 4..7 of the padded C = 8 carry no activation: their gradient is 0) (+ beta * dW)
+__global__ __launch_bounds__(256) void stem_s2d_sum_kernel(const float* __restrict__ slab, float* __restrict__ dw,
+                                                           int slices, float beta) {
+  const int e = blockIdx.x * 256 + threadIdx.x;  // dW element
+  if (e >= 64 * 49 * 8) return;
+  const int c = e & 7, rs = (e >> 3) % 49, k = e / (49 * 8);
+  float v = 0.f;
+  if (c < 4) {
+    const int r = rs / 7, sx = rs % 7;
+    const int aa = (r + 1) >> 1, dh = (r + 1) & 1, bb = (sx + 1) >> 1, dwv = (sx + 1) & 1;
+    const int j = (aa * 4 + bb) * 16 + (dh * 2 + dwv) * 4 + c;
+    const float* p = slab + (size_t)k * 256 + j;
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    int sl = 0;
+    for (; sl + 3 < slices; sl += 4) {
+      s0 += p[(size_t)sl * 64 * 256];
+      s1 += p[(size_t)(sl + 1) * 64 * 256];
+      s2 += p[(size_t)(sl + 2) * 64 * 256];
+      s3 += p[(size_t)(sl + 3) * 64 * 256];
+    }
+    for (; sl < slices; ++sl) s0 += p[(size_t)sl * 64 * 256];
+    v = (s0 + s1) + (s2 + s3);
+  }
+  dw[e] = beta != 0.f ? v + beta * dw[e] : v;
+}
+
+
 // ---- patch path: small-C stems (C = 8: 3 / 1 real channels) -------------------
 // FwdASmallC gathers one 16-B (tap, 8-channel) chunk per lane per tap: every input
 // pixel crosses the L1 / texture path once per filter tap that covers it (49x for
@@ -1726,8 +1883,44 @@ void set_conv_halo(int mode) { g_conv_halo = mode; }
 void set_conv_wgrad_ring(int mode) { g_wgrad_ring = mode; }
 int get_conv_halo() { return halo_env(); }
 
+// Space-to-depth stem wgrad (stem_s2d_*): the 7x7 / 2 / pad-3 C = 8 stem with <= 4 data
+// channels (ResNet-18's 3), even H and W.  LDNN_CONV_STEM_S2D=0 turns it off (A/B knob).
+int g_stem_s2d = -2;
+void set_conv_stem_s2d(int mode) { g_stem_s2d = mode; }
+bool stem_s2d_ok(const ConvShape& s) {
+  if (g_stem_s2d == -2) g_stem_s2d = env_int("LDNN_CONV_STEM_S2D", 1);
+  return g_stem_s2d != 0 && s.C == 8 && s.c_real > 0 && s.c_real <= 4 && s.K == 64 && s.R == 7 && s.S == 7 &&
+         s.stride == 2 && s.pad == 3 && s.H % 2 == 0 && s.W % 2 == 0 && s.P == s.H / 2 && s.Q == s.W / 2 &&
+         (size_t)s.N * (s.P + 3) * (s.Q + 3) * 32 < kOOBLimit;
+}
+struct S2dPlan {
+  int Hs, Ws, nchunk, steps, slices, steps_per;
+  size_t slab_floats, tmp_floats, xs_floats;
+};
+S2dPlan plan_s2d(const ConvShape& s) {
+  S2dPlan p;
+  p.Hs = s.P + 3;
+  p.Ws = s.Q + 3;
+  p.nchunk = (s.Q + 31) / 32;
+  p.steps = s.N * s.P * p.nchunk;
+  static const int target = env_int("LDNN_CONV_S2D_TARGET", 512);
+  int slices = std::max(1, std::min(target, p.steps / 8));
+  p.steps_per = (p.steps + slices - 1) / slices;
+  p.slices = (p.steps + p.steps_per - 1) / p.steps_per;
+  p.slab_floats = (size_t)p.slices * 64 * 256;
+  p.tmp_floats = 64 * 256;
+  p.xs_floats = (size_t)s.N * p.Hs * p.Ws * 8;  // bf16 x 16 channels
+  return p;
+}
+
 ConvWorkspace conv2d_lds_workspace(const ConvShape& s, int op) {
   if (!shape_ok(s)) return ConvWorkspace{};
+  if (op == 2 && stem_s2d_ok(s)) {
+    const S2dPlan p = plan_s2d(s);
+    ConvWorkspace w{};
+    w.slab_bytes = (p.slab_floats + p.tmp_floats + p.xs_floats) * 4;
+    return w;
+  }
   if (op == 0 && s.C % 64 == 0) return ws_of(plan_fwd(s));
   if (op == 1 && s.K % 64 == 0) return ws_of(plan_dgrad(s));
   if (op == 2 && s.C % 8 == 0 && s.K % 8 == 0) {
@@ -1919,6 +2112,26 @@ hipError_t conv2d_wgrad_lds(const ConvShape& s, const uint16_t* dy, const uint16
                             hipStream_t st, float* ws) {
   if (!shape_ok(s) || s.C % 8 != 0 || s.K % 8 != 0) return hipErrorNotSupported;
   if (beta != 0.f && beta != 1.f) return hipErrorNotSupported;
+  if (stem_s2d_ok(s) && ws != nullptr) {
+    const S2dPlan p = plan_s2d(s);
+    float* slab = ws;
+    float* tmp = ws + p.slab_floats;
+    bf16_t* xs = reinterpret_cast<bf16_t*>(tmp + p.tmp_floats);
+    const int64_t npix = (int64_t)s.N * p.Hs * p.Ws;
+    stem_s2d_pack_kernel<<<(unsigned)((npix + 255) / 256), 256, 0, st>>>(x, xs, s.N, s.H, s.W, p.Hs, p.Ws);
+    S2dArgs a{};
+    a.N = s.N; a.P = s.P; a.Q = s.Q; a.Hs = p.Hs; a.Ws = p.Ws; a.K = s.K;
+    a.nchunk = p.nchunk;
+    a.steps = p.steps;
+    a.steps_per = p.steps_per;
+    a.slab = slab;
+    const size_t bdy = (size_t)s.N * s.P * s.Q * s.K * 2, bxs = (size_t)npix * 32;
+    stem_s2d_wgrad_kernel<<<p.slices, 256, 0, st>>>(a, dy, (uint32_t)bdy, xs, (uint32_t)bxs);
+    const int64_t n4 = 64 * 256 / 4;
+    slab_sum_kernel<false><<<(unsigned)((n4 + 31) / 32), 256, 0, st>>>(slab, tmp, n4, p.slices, 0.f);
+    stem_s2d_sum_kernel<<<(64 * 49 * 8 + 255) / 256, 256, 0, st>>>(tmp, dw, 1, beta);
+    return hipGetLastError();
+  }
   const WgradPlan pl = plan_wgrad(s);
   if (pl.ring) {
     WRArgs r{};

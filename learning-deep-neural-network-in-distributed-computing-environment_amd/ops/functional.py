@@ -325,7 +325,7 @@ class _Conv2dNative(torch.autograd.Function):
             gz = torch.empty_like(g)
             C.act_bwd(g.contiguous(), y, gz, 0)
             g = gz
-        C.conv_wgrad(g, xb, flat.grad_storage(weight), stride, pad, flat.grad_beta(weight))
+        C.conv_wgrad(g, xb, flat.grad_storage(weight), stride, pad, flat.grad_beta(weight), real_channels=Cin)
         if bias is not None:
             C.colsum(g.view(-1, kp), flat.grad_storage(bias), flat.grad_beta(bias) != 0.0)
         flat.notify(weight, bias)

@@ -200,3 +200,36 @@ def test_ring_wgrad_matches_fp32_and_split_k(N, C, H, W, K):
         torch.testing.assert_close(dw, ref, rtol=1e-3, atol=1e-3 * ref.abs().max().item())
         torch.testing.assert_close(dacc, ref, rtol=1e-3, atol=2e-3 * ref.abs().max().item())
     torch.testing.assert_close(outs[2][0], outs[0][0], rtol=1e-4, atol=1e-4 * ref.abs().max().item())
+
+
+@pytest.mark.parametrize("N,Cin,H,W", [(2, 3, 224, 224), (3, 3, 64, 64), (2, 1, 32, 48), (1, 4, 70, 38)])
+def test_stem_s2d_wgrad_matches_fp32_and_split_k(N, Cin, H, W):
+    """The space-to-depth stem wgrad (7x7 / 2 / pad 3, C padded to 8 with <= 4 data channels,
+    real_channels given) == the fp32 reference and == the split-K gather wgrad; beta 0 and 1."""
+    torch.manual_seed(9)
+    Cc = _ext.C()
+    K = 64
+    x = torch.zeros(N, H, W, 8, device="cuda", dtype=torch.bfloat16)
+    x[..., :Cin] = torch.randn(N, H, W, Cin, device="cuda").bfloat16()
+    P, Q = H // 2, W // 2
+    gy = torch.randn(N, P, Q, K, device="cuda").bfloat16()
+    ref = torch.nn.grad.conv2d_weight(x.float().permute(0, 3, 1, 2), (K, 8, 7, 7), gy.float().permute(0, 3, 1, 2),
+                                      stride=2, padding=3).permute(0, 2, 3, 1)
+    outs = {}
+    try:
+        for mode in (1, 0):
+            Cc.set_conv_stem_s2d(mode)
+            dw = torch.full((K, 7, 7, 8), float("nan"), device="cuda")
+            Cc.conv_wgrad(gy, x, dw, 2, 3, 0.0, real_channels=Cin)
+            base = torch.randn(K, 7, 7, 8, device="cuda")
+            acc = base.clone()
+            Cc.conv_wgrad(gy, x, acc, 2, 3, 1.0, real_channels=Cin)
+            outs[mode] = (dw, acc - base)
+    finally:
+        Cc.set_conv_stem_s2d(1)
+    scale = ref.abs().max().item()
+    for mode in (1, 0):
+        dw, dacc = outs[mode]
+        torch.testing.assert_close(dw, ref, rtol=1e-3, atol=1e-3 * scale)
+        torch.testing.assert_close(dacc, ref, rtol=1e-3, atol=2e-3 * scale)
+    assert (outs[1][0][..., 4:] == 0).all()
