@@ -2054,8 +2054,8 @@ hipError_t conv2d_fwd_lds(const ConvShape& s, const uint16_t* x, const uint16_t*
   const size_t bx = (size_t)s.N * s.H * s.W * s.C * 2, bw = (size_t)s.K * a.rsc * 2;
   hipError_t e;
   if (halo_takes(s, pl.wm)) {
-    // fwd: the halo wins on the 256x64 tiles of 64-filter layers (C64 H56: 53.7 -> 35-37 us);
-    // on 128x128 ones only double-buffered (single: C128 H28 25.8 -> 27.7, C512 H7 34.9 -> 40.0 us)
+    // fwd: the halo wins on the 256x64 tiles of 64-filter layers (C64 H56: 53.7 -> 35-37 us) and
+    // loses on 128x128 ones (C128 H28 25.8 -> 27.7, C512 H7 34.9 -> 40.0 us; double-buffered too)
     if (pl.wm == 4) e = launch_halo<4, 1, WeightKC<64, 2, 4>, false>(a, epi, pl.splits, x, bx, w, bw, st);
     else e = launch_halo<2, 2, WeightKC<128, 4, 4>, false>(a, epi, pl.splits, x, bx, w, bw, st);
   } else if (pl.wm == 4) {
