@@ -1112,6 +1112,82 @@ void pool_bwd(const at::Tensor& dy, const c10::optional<at::Tensor>& argmax, con
         "pool2d_bwd");
 }
 
+// relu(BN(x)) -> 3x3/2 max-pool in one pass: x [N][H][W][C] (pre-BN), y / argmax [N][P][Q][C]
+bool bn_pool_fwd(const at::Tensor& x, const at::Tensor& y, const at::Tensor& argmax,
+                 const c10::optional<at::Tensor>& gamma, const c10::optional<at::Tensor>& beta,
+                 const c10::optional<at::Tensor>& running_mean, const c10::optional<at::Tensor>& running_var,
+                 const at::Tensor& save_mean, const at::Tensor& save_invstd, const at::Tensor& ws, double eps,
+                 double momentum, const c10::optional<at::Tensor>& num_batches, bool stats_ready, int64_t pad) {
+  check_dev(x, at::kBFloat16, "x");
+  check_dev(y, at::kBFloat16, "y");
+  check_dev(argmax, at::kByte, "argmax");
+  TORCH_CHECK(x.dim() == 4 && y.dim() == 4 && x.is_contiguous() && y.is_contiguous() && argmax.is_contiguous() &&
+                  argmax.sizes() == y.sizes() && y.size(0) == x.size(0) && y.size(3) == x.size(3),
+              "bn_pool_fwd: dense NHWC x / y / argmax");
+  const int64_t N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  ldnn::BnArgs a{};
+  a.x = bf16_ptr(x);
+  a.gamma = fptr_opt(gamma, C, "gamma");
+  a.beta = fptr_opt(beta, C, "beta");
+  a.running_mean = fptr_opt(running_mean, C, "running_mean");
+  a.running_var = fptr_opt(running_var, C, "running_var");
+  a.save_mean = fptr_opt(save_mean, C, "save_mean");
+  a.save_invstd = fptr_opt(save_invstd, C, "save_invstd");
+  a.ws = fptr_opt(ws, ldnn::bn_workspace_floats((int)C), "ws");
+  a.M = (int)(N * H * W);
+  a.C = (int)C;
+  a.eps = (float)eps;
+  a.momentum = (float)momentum;
+  a.training = 1;
+  a.relu = 1;
+  if (num_batches.has_value()) {
+    check_dev(*num_batches, at::kLong, "num_batches");
+    a.num_batches = num_batches->data_ptr<int64_t>();
+  }
+  uint8_t* am = argmax.data_ptr<uint8_t>();
+  TORCH_CHECK(((uintptr_t)am & 7) == 0, "bn_pool_fwd: argmax must be 8-B aligned");
+  check(ldnn::bn_maxpool_forward(a, (int)N, (int)H, (int)W, (int)y.size(1), (int)y.size(2), (int)pad, bf16_mut(y),
+                                 am, stats_ready, cur_stream(x)),
+        "bn_maxpool_forward (3x3/2 window, C/8 dividing 256)");
+  return true;
+}
+
+void bn_pool_bwd(const at::Tensor& x, const at::Tensor& dy, const at::Tensor& argmax, const at::Tensor& dx,
+                 const c10::optional<at::Tensor>& gamma, const at::Tensor& save_mean, const at::Tensor& save_invstd,
+                 const at::Tensor& ws, const c10::optional<at::Tensor>& dgamma,
+                 const c10::optional<at::Tensor>& dbeta, bool grad_assign, const c10::optional<at::Tensor>& dy2,
+                 int64_t pad) {
+  check_dev(x, at::kBFloat16, "x");
+  check_dev(dy, at::kBFloat16, "dy");
+  check_dev(dx, at::kBFloat16, "dx");
+  check_dev(argmax, at::kByte, "argmax");
+  TORCH_CHECK(x.dim() == 4 && dy.dim() == 4 && x.is_contiguous() && dy.is_contiguous() && dx.is_contiguous() &&
+                  dx.sizes() == x.sizes() && argmax.sizes() == dy.sizes() && argmax.is_contiguous() &&
+                  dy.size(0) == x.size(0) && dy.size(3) == x.size(3),
+              "bn_pool_bwd: dense NHWC tensors");
+  const int64_t N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  ldnn::BnArgs a{};
+  a.x = bf16_ptr(x);
+  a.gamma = fptr_opt(gamma, C, "gamma");
+  a.save_mean = fptr_opt(save_mean, C, "save_mean");
+  a.save_invstd = fptr_opt(save_invstd, C, "save_invstd");
+  a.ws = fptr_opt(ws, ldnn::bn_workspace_floats((int)C), "ws");
+  a.M = (int)(N * H * W);
+  a.C = (int)C;
+  a.relu = 1;
+  if (dy2.has_value()) {
+    check_dev(*dy2, at::kBFloat16, "dy2");
+    TORCH_CHECK(dy2->sizes() == dy.sizes() && dy2->is_contiguous(), "bn_pool_bwd: dy2 layout");
+    a.dy2 = bf16_ptr(*dy2);
+  }
+  const uint8_t* am = argmax.data_ptr<uint8_t>();
+  TORCH_CHECK(((uintptr_t)am & 7) == 0, "bn_pool_bwd: argmax must be 8-B aligned");
+  check(ldnn::bn_maxpool_backward(a, (int)N, (int)H, (int)W, (int)dy.size(1), (int)dy.size(2), (int)pad,
+                                  bf16_ptr(dy), am, bf16_mut(dx), fptr_opt(dgamma, C, "dgamma"),
+                                  fptr_opt(dbeta, C, "dbeta"), cur_stream(x), grad_assign),
+        "bn_maxpool_backward");
+}
+
 void gap_fwd(const at::Tensor& x, const at::Tensor& y) {  // x [N][HW][C], y [N][C]
   check_dev(x, at::kBFloat16, "x");
   check_dev(y, at::kBFloat16, "y");
@@ -1462,6 +1538,15 @@ PYBIND11_MODULE(_C, m) {
   m.def("pool_fwd", &pool_fwd);
   m.def("pool_bwd", &pool_bwd, py::arg("dy"), py::arg("argmax"), py::arg("dx"), py::arg("R"), py::arg("S"),
         py::arg("stride"), py::arg("pad"), py::arg("is_max"), py::arg("dy2") = py::none());
+  m.def("bn_pool_fwd", &bn_pool_fwd, "relu(BN(x)) -> 3x3/2 max-pool in one pass (pooled output + argmax)",
+        py::arg("x"), py::arg("y"), py::arg("argmax"), py::arg("gamma"), py::arg("beta"), py::arg("running_mean"),
+        py::arg("running_var"), py::arg("save_mean"), py::arg("save_invstd"), py::arg("ws"), py::arg("eps"),
+        py::arg("momentum"), py::arg("num_batches") = py::none(), py::arg("stats_ready") = false,
+        py::arg("pad") = 1);
+  m.def("bn_pool_bwd", &bn_pool_bwd, "backward of bn_pool_fwd: dx, dgamma / dbeta", py::arg("x"), py::arg("dy"),
+        py::arg("argmax"), py::arg("dx"), py::arg("gamma"), py::arg("save_mean"), py::arg("save_invstd"),
+        py::arg("ws"), py::arg("dgamma"), py::arg("dbeta"), py::arg("grad_assign") = false,
+        py::arg("dy2") = py::none(), py::arg("pad") = 1);
   m.def("gap_fwd", &gap_fwd);
   m.def("gap_bwd", &gap_bwd);
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("stride"), py::arg("pad"),

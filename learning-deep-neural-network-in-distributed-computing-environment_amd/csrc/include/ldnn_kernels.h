@@ -198,6 +198,16 @@ hipError_t bn_forward_apply(const BnArgs& a, hipStream_t s);
 // branch); dgamma / dbeta are ACCUMULATED (flat gradient buffer)
 hipError_t bn_backward(const BnArgs& a, const uint16_t* dy, uint16_t* dx, uint16_t* dres, float* dgamma,
                        float* dbeta, hipStream_t s, bool grad_assign = false);
+// relu(BN(x)) -> 3x3/2 max-pool in one pass (a.x = [N][H][W][C] pre-BN, a.M = N*H*W, a.relu = 1):
+// y [N][P][Q][C] pooled, arg [N][P][Q][C] window argmax (0xff: the max was clamped by the ReLU).
+// stats_ready: scale / shift already in a.ws (the producing conv's epilogue finalized them).
+// Needs C / 8 to divide 256.
+hipError_t bn_maxpool_forward(const BnArgs& a, int N, int H, int W, int P, int Q, int pad, uint16_t* y,
+                              uint8_t* arg, bool stats_ready, hipStream_t s);
+// its backward: dx [N][H][W][C] from the pooled gradient dy (+ a.dy2), dgamma / dbeta as bn_backward
+hipError_t bn_maxpool_backward(const BnArgs& a, int N, int H, int W, int P, int Q, int pad, const uint16_t* dy,
+                               const uint8_t* arg, uint16_t* dx, float* dgamma, float* dbeta, hipStream_t s,
+                               bool grad_assign = false);
 hipError_t pool2d_fwd(const uint16_t* x, uint16_t* y, uint8_t* argmax, int N, int H, int W, int C, int P, int Q,
                       int R, int S, int stride, int pad, bool is_max, hipStream_t s);
 hipError_t pool2d_bwd(const uint16_t* dy, const uint8_t* argmax, uint16_t* dx, int N, int H, int W, int C, int P,

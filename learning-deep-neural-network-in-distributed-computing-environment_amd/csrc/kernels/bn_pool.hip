@@ -405,6 +405,245 @@ __global__ __launch_bounds__(256) void pool_bwd_kernel(const bf16_t* __restrict_
   }  // rows
 }
 
+// ---- BatchNorm + ReLU + 3x3/2 max-pool in one pass (the ResNet stem) ----------
+// The BN output is never stored: the forward applies scale / shift + ReLU to every
+// tap of the window on the fly (same bf16 rounding as bn_apply_kernel, so the same
+// maxima and argmax as the unfused BN -> pool pair) and writes only the pooled
+// output + argmax.  relu'(bn(x)) at a window's argmax is (pooled max > 0), so the
+// argmax byte doubles as the ReLU mask: kNoGrad when the max was clamped to 0.  The
+// backward gathers the pool gradient of each input pixel from its candidate windows
+// and feeds it straight into the BN statistics (reduce) and into dx = A g + B x + D
+// (apply): the 4x larger pre-pool gradient is never written or re-read.  Traffic at the ResNet-18 stem, b64: forward 142 MB instead of
+// 206 (apply) + 135 (pool); backward 387 MB instead of 135 + 206 + 309.
+constexpr uint32_t kNoGrad = 0xffu;
+
+// Branch-free address arithmetic throughout (out-of-range window taps / candidates are
+// loaded from a clamped address and masked), so every load of a thread is independent
+// and in flight together.  PAD (0 or 1) is compile-time: the tap of a window that holds
+// a given input pixel is then a constant.
+//
+// The backward works on 2x2 input blocks (2a..2a+1) x (2b..2b+1): with a 3x3 / 2 window
+// every pixel of the block lies in windows {a-1+PAD, a+PAD} x {b-1+PAD, b+PAD} (row 2a+di
+// at tap di + 2 - PAD - 2i of window a-1+PAD+i), so a thread loads those 4 windows' argmax
+// and gradient once and produces 4 pixels (1 window load per pixel instead of 2.25).
+template <int PAD>
+__device__ __forceinline__ void block_grads(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ dy2,
+                                            const uint8_t* __restrict__ arg, int n, int a, int b, int c8, int cv,
+                                            int P, int Q, float (&g)[2][2][8]) {
+  uint2 am[2][2];
+  u16x8 gv[2][2], g2[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int p = a - 1 + PAD + i, q = b - 1 + PAD + k;
+      const bool ok = p >= 0 && p < P && q >= 0 && q < Q;
+      const int pc = min(max(p, 0), P - 1), qc = min(max(q, 0), Q - 1);
+      const size_t o = (((size_t)n * P + pc) * Q + qc) * cv + c8;
+      am[i][k] = reinterpret_cast<const uint2*>(arg)[o];
+      gv[i][k] = reinterpret_cast<const u16x8*>(dy)[o];
+      g2[i][k] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      if (dy2) g2[i][k] = reinterpret_cast<const u16x8*>(dy2)[o];
+      if (!ok) am[i][k] = uint2{0xffffffffu, 0xffffffffu};   // kNoGrad bytes never match a tap
+    }
+#pragma unroll
+  for (int di = 0; di < 2; ++di)
+#pragma unroll
+    for (int dj = 0; dj < 2; ++dj) {
+#pragma unroll
+      for (int t = 0; t < 8; ++t) g[di][dj][t] = 0.f;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int r = di + 2 - PAD - 2 * i;
+        if (r < 0 || r > 2) continue;   // compile-time
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          const int sc = dj + 2 - PAD - 2 * k;
+          if (sc < 0 || sc > 2) continue;
+          const uint32_t want = (uint32_t)(r * 3 + sc);
+#pragma unroll
+          for (int t = 0; t < 8; ++t) {
+            const uint32_t bt = ((t < 4 ? am[i][k].x : am[i][k].y) >> (8 * (t & 3))) & 0xffu;
+            g[di][dj][t] += bt == want ? bf2f(gv[i][k][t]) + bf2f(g2[i][k][t]) : 0.f;
+          }
+        }
+      }
+    }
+}
+
+// forward: one thread per (output column, 8-channel group) of an output row
+template <int PAD>
+__global__ __launch_bounds__(256) void bn_maxpool_fwd_kernel(const bf16_t* __restrict__ x,
+                                                             const float* __restrict__ scale,
+                                                             const float* __restrict__ shift, bf16_t* __restrict__ y,
+                                                             uint8_t* __restrict__ arg, int N, int H, int W, int C,
+                                                             int P, int Q) {
+  const int cv = C / 8;
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= Q * cv) return;
+  const int c8 = j % cv, q = j / cv;
+  float sc[8], sh[8];
+  load8(scale + c8 * 8, sc);
+  load8(shift + c8 * 8, sh);
+  for (int row = blockIdx.y; row < N * P; row += gridDim.y) {
+    const int n = row / P, p = row - n * P;
+    u16x8 v[3][3];
+    bool ok[3][3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int s = 0; s < 3; ++s) {
+        const int h = p * 2 - PAD + r, w = q * 2 - PAD + s;
+        ok[r][s] = h >= 0 && h < H && w >= 0 && w < W;
+        const int hc = min(max(h, 0), H - 1), wc = min(max(w, 0), W - 1);
+        v[r][s] = *reinterpret_cast<const u16x8*>(x + (((size_t)n * H + hc) * W + wc) * C + c8 * 8);
+      }
+    float best[8];
+    uint32_t bidx[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      best[t] = -INFINITY;
+      bidx[t] = 0;
+    }
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int s = 0; s < 3; ++s)
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          // the unfused BN apply's bf16 output, then the pool's first-max scan
+          const float f = bf2f(f2bf(fmaxf(bf2f(v[r][s][t]) * sc[t] + sh[t], 0.f)));
+          if (ok[r][s] && f > best[t]) {
+            best[t] = f;
+            bidx[t] = (uint32_t)(r * 3 + s);
+          }
+        }
+    u16x8 o;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      o[t] = f2bf(best[t]);
+      if (!(best[t] > 0.f)) bidx[t] = kNoGrad;   // relu'(bn) = 0 at the argmax: no gradient
+    }
+    const size_t oi = ((size_t)row * Q + q) * cv + c8;
+    reinterpret_cast<u16x8*>(y)[oi] = o;
+    uint2 am;
+    am.x = bidx[0] | (bidx[1] << 8) | (bidx[2] << 16) | (bidx[3] << 24);
+    am.y = bidx[4] | (bidx[5] << 8) | (bidx[6] << 16) | (bidx[7] << 24);
+    reinterpret_cast<uint2*>(arg)[oi] = am;
+  }
+}
+
+// backward statistics: acc += (sum g, sum g xhat) per channel; one thread per (2x2 input
+// block column, 8-channel group) -- the channel group is fixed per thread (256 % cv == 0)
+template <int PAD>
+__global__ __launch_bounds__(256) void bn_maxpool_bwd_reduce_kernel(
+    const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy, const bf16_t* __restrict__ dy2,
+    const uint8_t* __restrict__ arg, const float* __restrict__ mean, const float* __restrict__ invstd,
+    float* __restrict__ acc, int N, int H, int W, int C, int P, int Q, BnFin fin, int ncop) {
+  __shared__ float red[2][256 * 8];
+  const int cv = C / 8;
+  const int tid = threadIdx.x;
+  const int j = blockIdx.x * blockDim.x + tid;
+  const int c8 = tid % cv, b = j / cv;
+  const int Hb = (H + 1) / 2, Wb = (W + 1) / 2;
+  float s0[8], s1[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    s0[t] = 0.f;
+    s1[t] = 0.f;
+  }
+  if (b < Wb) {
+    float mu[8], is[8];
+    load8(mean + c8 * 8, mu);
+    load8(invstd + c8 * 8, is);
+    for (int rb = blockIdx.y; rb < N * Hb; rb += gridDim.y) {
+      const int n = rb / Hb, a = rb - n * Hb;
+      u16x8 xv[2][2];
+      bool in[2][2];
+#pragma unroll
+      for (int di = 0; di < 2; ++di)
+#pragma unroll
+        for (int dj = 0; dj < 2; ++dj) {
+          const int h = 2 * a + di, w = 2 * b + dj;
+          in[di][dj] = h < H && w < W;
+          xv[di][dj] = *reinterpret_cast<const u16x8*>(
+              x + (((size_t)n * H + min(h, H - 1)) * W + min(w, W - 1)) * C + c8 * 8);
+        }
+      float g[2][2][8];
+      block_grads<PAD>(dy, dy2, arg, n, a, b, c8, cv, P, Q, g);
+#pragma unroll
+      for (int di = 0; di < 2; ++di)
+#pragma unroll
+        for (int dj = 0; dj < 2; ++dj)
+#pragma unroll
+          for (int t = 0; t < 8; ++t) {
+            const float gg = in[di][dj] ? g[di][dj][t] : 0.f;
+            s0[t] += gg;
+            s1[t] += gg * (bf2f(xv[di][dj][t]) - mu[t]) * is[t];
+          }
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    red[0][tid * 8 + t] = s0[t];
+    red[1][tid * 8 + t] = s1[t];
+  }
+  __syncthreads();
+  float* accc = acc + (size_t)((blockIdx.x + gridDim.x * blockIdx.y) % ncop) * 2 * C;
+  for (int ch = tid; ch < C; ch += 256) {   // ch = c8 * 8 + t; threads c8, c8 + cv, ... hold it
+    const int g8 = ch >> 3, t = ch & 7;
+    float t0 = 0.f, t1 = 0.f;
+    for (int k = g8; k < 256; k += cv) {
+      t0 += red[0][k * 8 + t];
+      t1 += red[1][k * 8 + t];
+    }
+    bn_acc_add(accc + ch, t0);
+    bn_acc_add(accc + C + ch, t1);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's atomics have completed
+  bn_finalize_last<true, kBnCopies>(fin, N * H * W, C, gridDim.x * gridDim.y, &red[0][0], 2 * 256 * 8, ncop);
+}
+
+// backward apply: dx = A g + B x + D, same 2x2-block threads
+template <int PAD>
+__global__ __launch_bounds__(256) void bn_maxpool_bwd_apply_kernel(
+    const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy, const bf16_t* __restrict__ dy2,
+    const uint8_t* __restrict__ arg, const float* __restrict__ coef, bf16_t* __restrict__ dx, int N, int H, int W,
+    int C, int P, int Q) {
+  const int cv = C / 8;
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c8 = j % cv, b = j / cv;
+  const int Hb = (H + 1) / 2, Wb = (W + 1) / 2;
+  if (b >= Wb) return;
+  float A[8], B[8], D[8];
+  load8(coef + c8 * 8, A);
+  load8(coef + C + c8 * 8, B);
+  load8(coef + 2 * C + c8 * 8, D);
+  for (int rb = blockIdx.y; rb < N * Hb; rb += gridDim.y) {
+    const int n = rb / Hb, a = rb - n * Hb;
+    u16x8 xv[2][2];
+#pragma unroll
+    for (int di = 0; di < 2; ++di)
+#pragma unroll
+      for (int dj = 0; dj < 2; ++dj)
+        xv[di][dj] = *reinterpret_cast<const u16x8*>(
+            x + (((size_t)n * H + min(2 * a + di, H - 1)) * W + min(2 * b + dj, W - 1)) * C + c8 * 8);
+    float g[2][2][8];
+    block_grads<PAD>(dy, dy2, arg, n, a, b, c8, cv, P, Q, g);
+#pragma unroll
+    for (int di = 0; di < 2; ++di)
+#pragma unroll
+      for (int dj = 0; dj < 2; ++dj) {
+        const int h = 2 * a + di, w = 2 * b + dj;
+        if (h >= H || w >= W) continue;
+        u16x8 out;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) out[t] = f2bf(A[t] * g[di][dj][t] + B[t] * bf2f(xv[di][dj][t]) + D[t]);
+        *reinterpret_cast<u16x8*>(dx + (((size_t)n * H + h) * W + w) * C + c8 * 8) = out;
+      }
+  }
+}
+
 // global average pool [N][HW][C] -> [N][C] (fp32 accumulate), and its backward
 __global__ void gap_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int N, int HW, int C) {
   const int cv = C / 8;
@@ -497,10 +736,10 @@ hipError_t bn_forward_apply(const BnArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t bn_forward(const BnArgs& a, hipStream_t s) {
+// the statistics half of the forward: batch statistics (training) or the running ones (eval)
+// -> scale / shift in a.ws
+static void bn_forward_stats(const BnArgs& a, hipStream_t s) {
   const int M = a.M, C = a.C;
-  if (C % 8) return hipErrorInvalidValue;
-  if (M <= 0) return hipSuccess;
   const RedGeo g = red_geo(M, C, true);
   const dim3 grid(g.gx, g.gy);
   if (a.training) {
@@ -511,7 +750,70 @@ hipError_t bn_forward(const BnArgs& a, hipStream_t s) {
     bn_eval_coeff_kernel<<<(C + 255) / 256, 256, 0, s>>>(a.gamma, a.beta, a.running_mean, a.running_var, a.ws,
                                                          a.ws + C, C, a.eps);
   }
+}
+
+hipError_t bn_forward(const BnArgs& a, hipStream_t s) {
+  const int M = a.M, C = a.C;
+  if (C % 8) return hipErrorInvalidValue;
+  if (M <= 0) return hipSuccess;
+  bn_forward_stats(a, s);
   return bn_forward_apply(a, s);
+}
+
+// BN + ReLU + 3x3/2 max-pool (kernels above); grid knob LDNN_BNPOOL_BLOCKS (workgroups of the
+// backward statistics pass)
+namespace {
+int bnpool_blocks() {
+  static const int v = std::max(64, env_int_or("LDNN_BNPOOL_BLOCKS", 2048));
+  return v;
+}
+bool bnpool_ok(const BnArgs& a, int N, int H, int W, int P, int Q, int pad) {
+  const int cv = a.C / 8;
+  return a.C % 8 == 0 && cv <= 256 && 256 % cv == 0 && N > 0 && pad >= 0 && pad <= 1 &&
+         P == (H + 2 * pad - 3) / 2 + 1 && Q == (W + 2 * pad - 3) / 2 + 1 && (int64_t)N * H * W == a.M &&
+         (int64_t)N * H < (1ll << 31);
+}
+}  // namespace
+
+hipError_t bn_maxpool_forward(const BnArgs& a, int N, int H, int W, int P, int Q, int pad, uint16_t* y,
+                              uint8_t* arg, bool stats_ready, hipStream_t s) {
+  if (!bnpool_ok(a, N, H, W, P, Q, pad) || !a.relu || !y || !arg) return hipErrorInvalidValue;
+  if (!stats_ready) bn_forward_stats(a, s);
+  const int cv = a.C / 8;
+  const dim3 g((Q * cv + kBlock - 1) / kBlock, std::min(N * P, 65535));   // one output row per workgroup
+  if (pad) bn_maxpool_fwd_kernel<1><<<g, kBlock, 0, s>>>(a.x, a.ws, a.ws + a.C, y, arg, N, H, W, a.C, P, Q);
+  else bn_maxpool_fwd_kernel<0><<<g, kBlock, 0, s>>>(a.x, a.ws, a.ws + a.C, y, arg, N, H, W, a.C, P, Q);
+  return hipGetLastError();
+}
+
+hipError_t bn_maxpool_backward(const BnArgs& a, int N, int H, int W, int P, int Q, int pad, const uint16_t* dy,
+                               const uint8_t* arg, uint16_t* dx, float* dgamma, float* dbeta, hipStream_t s,
+                               bool grad_assign) {
+  if (!bnpool_ok(a, N, H, W, P, Q, pad) || !dy || !arg || !dx) return hipErrorInvalidValue;
+  const int C = a.C, cv = C / 8;
+  BnFin f{};
+  f.acc = a.ws + 10 * C + 32 + kBnCopies * 2 * C;
+  f.ticket = reinterpret_cast<int*>(a.ws + 10 * C + 16);
+  f.gamma = a.gamma;
+  f.save_mean = a.save_mean;
+  f.save_invstd = a.save_invstd;
+  f.coef = a.ws + 6 * C;
+  f.dgamma = dgamma;
+  f.dbeta = dbeta;
+  f.grad_assign = grad_assign ? 1 : 0;
+  const int gx = ((W + 1) / 2 * cv + kBlock - 1) / kBlock, rows = N * ((H + 1) / 2);
+  const dim3 gr(gx, std::min(rows, std::max(1, bnpool_blocks() / gx)));   // reduce: bounded atomics
+  const dim3 ga(gx, std::min(rows, 65535));                                // apply: one block row per workgroup
+  if (pad) {
+    bn_maxpool_bwd_reduce_kernel<1><<<gr, kBlock, 0, s>>>(a.x, dy, a.dy2, arg, a.save_mean, a.save_invstd, f.acc, N,
+                                                          H, W, C, P, Q, f, bn_ncop(true, gr.x * gr.y));
+    bn_maxpool_bwd_apply_kernel<1><<<ga, kBlock, 0, s>>>(a.x, dy, a.dy2, arg, f.coef, dx, N, H, W, C, P, Q);
+  } else {
+    bn_maxpool_bwd_reduce_kernel<0><<<gr, kBlock, 0, s>>>(a.x, dy, a.dy2, arg, a.save_mean, a.save_invstd, f.acc, N,
+                                                          H, W, C, P, Q, f, bn_ncop(true, gr.x * gr.y));
+    bn_maxpool_bwd_apply_kernel<0><<<ga, kBlock, 0, s>>>(a.x, dy, a.dy2, arg, f.coef, dx, N, H, W, C, P, Q);
+  }
+  return hipGetLastError();
 }
 
 hipError_t bn_backward(const BnArgs& a, const uint16_t* dy, uint16_t* dx, uint16_t* dres, float* dgamma,

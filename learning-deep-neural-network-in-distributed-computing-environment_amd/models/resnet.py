@@ -65,7 +65,7 @@ class ResNet(nn.Module):
         return nn.Sequential(*layers)
 
     def forward(self, x):
-        x = self.maxpool(self.bn1.act(self.conv1(x), relu=True))
+        x = LF.bn_relu_maxpool(self.conv1(x), self.bn1, self.maxpool)   # maxpool(relu(bn1(conv1 x)))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         x = self.avgpool(x).flatten(1)
         return self.fc(x)

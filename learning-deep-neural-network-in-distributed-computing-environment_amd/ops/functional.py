@@ -530,6 +530,88 @@ class _PoolNative(torch.autograd.Function):
         return (out if in_dtype == torch.bfloat16 else out.to(in_dtype)), None, None, None, None
 
 
+class _BnReluMaxPoolNative(torch.autograd.Function):
+    """maxpool3x3/2(relu(BatchNorm2d(x))) in one native pass each way (bn_pool.hip
+    bn_maxpool_*): the BN output is never stored, the pool's argmax doubles as the
+    ReLU mask and the backward turns the pooled gradient straight into dx."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, mod, flat, pad):
+        C_ = _ext.C()
+        N, C, H, W = x.shape
+        xb = as_nhwc(x if x.dtype == torch.bfloat16 else x.to(torch.bfloat16), C, zero_pad=False).contiguous()
+        P, Q = (H + 2 * pad - 3) // 2 + 1, (W + 2 * pad - 3) // 2 + 1
+        dev = x.device
+        y = torch.empty(N, P, Q, C, dtype=torch.bfloat16, device=dev)
+        am = torch.empty(N, P, Q, C, dtype=torch.uint8, device=dev)
+        ws = _bn_workspace(mod, C, dev, C_)
+        gamma = flat.master_storage(weight)[:C] if weight is not None else None
+        beta = flat.master_storage(bias)[:C] if bias is not None else None
+        pre = mod.__dict__.pop("_ldnn_pre", None)
+        if pre is not None and pre[0] == xb.data_ptr():
+            # statistics already accumulated + finalized by the producing conv's epilogue
+            smean, sinv = pre[1], pre[2]
+            C_.bn_pool_fwd(xb, y, am, gamma, beta, None, None, smean, sinv, ws, mod.eps, 0.0, None, True, pad)
+        else:
+            smean = torch.empty(C, dtype=torch.float32, device=dev)
+            sinv = torch.empty(C, dtype=torch.float32, device=dev)
+            rm, rv, mom, nbt = _bn_train_state(mod, dev)
+            C_.bn_pool_fwd(xb, y, am, gamma, beta, rm, rv, smean, sinv, ws, mod.eps, mom or 0.0, nbt, False, pad)
+        ctx.save_for_backward(xb, am, smean, sinv)
+        ctx.meta = (flat, weight, bias, ws, pad, C, x.dtype)
+        ctx.set_materialize_grads(False)
+        return nchw_view(y, C), nchw_view(y, C)
+
+    @staticmethod
+    def backward(ctx, gy, gy_twin):
+        C_ = _ext.C()
+        xb, am, smean, sinv = ctx.saved_tensors
+        flat, weight, bias, ws, pad, C, in_dtype = ctx.meta
+        if gy is None:
+            gy, gy_twin = gy_twin, None
+        if gy is None:
+            return None, None, None, None, None, None
+        g = as_nhwc(gy if gy.dtype == torch.bfloat16 else gy.to(torch.bfloat16), C, zero_pad=False).contiguous()
+        gt = None
+        if gy_twin is not None:
+            gt = as_nhwc(gy_twin if gy_twin.dtype == torch.bfloat16 else gy_twin.to(torch.bfloat16), C,
+                         zero_pad=False).contiguous()
+        dx = torch.empty_like(xb)
+        gamma = flat.master_storage(weight)[:C] if weight is not None else None
+        dg = flat.grad_storage(weight)[:C] if weight is not None else None
+        db = flat.grad_storage(bias)[:C] if bias is not None else None
+        fresh = [(t, flat.grad_beta(p) == 0.0) for t, p in ((dg, weight), (db, bias)) if p is not None]
+        assign = all(f for _, f in fresh)
+        if not assign:
+            for t, f in fresh:
+                if f:
+                    t.zero_()
+        C_.bn_pool_bwd(xb, g, am, dx, gamma, smean, sinv, ws, dg, db, assign, gt, pad)
+        flat.notify(weight, bias)
+        dxv = nchw_view(dx, C)
+        return (dxv if in_dtype == torch.bfloat16 else dxv.to(in_dtype)), None, None, None, None, None
+
+
+# BN + ReLU + max-pool fused (LDNN_BN_POOL=0: the separate BN-apply and pool passes)
+BN_POOL_FUSED = __import__("os").environ.get("LDNN_BN_POOL", "1") != "0"
+
+
+def bn_relu_maxpool(x, bn, pool):
+    """pool(relu(bn(x))) for a 3x3 / stride-2 max-pool: one native pass each way on the
+    GPU in training mode (C / 8 dividing 256), else the separate layers."""
+    flat = getattr(bn, "_ldnn_flat", None)
+    k, st, pad = _sq(pool.kernel_size), _sq(pool.stride if pool.stride is not None else pool.kernel_size), \
+        _sq(pool.padding)
+    C = x.shape[1] if x.dim() == 4 else 0
+    ok = (BN_POOL_FUSED and _ext.use_native(x) and flat is not None and bn.training and bn.affine
+          and x.dim() == 4 and C % 8 == 0 and 256 % (C // 8 or 1) == 0 and C // 8 <= 256
+          and k == 3 and st == 2 and pad is not None and 0 <= pad <= 1 and _sq(pool.dilation) == 1
+          and not getattr(pool, "ceil_mode", False) and not getattr(pool, "return_indices", False))
+    if ok:
+        return _with_twin(*_BnReluMaxPoolNative.apply(x, bn.weight, bn.bias, bn, flat, pad))
+    return pool(bn.act(x, relu=True))
+
+
 def _sq(v):
     return v if isinstance(v, int) else (v[0] if v[0] == v[1] else None)
 

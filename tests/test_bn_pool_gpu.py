@@ -156,3 +156,88 @@ def test_twin_output_sums_branch_gradients(op):
     ((y.float() * g1).sum() + (twin.float() * g2).sum()).backward()
     ((yr * g1).sum() + (yr * g2).sum()).backward()
     torch.testing.assert_close(xb.grad.float(), xf.grad, rtol=3e-2, atol=3e-2 * xf.grad.abs().max().item())
+
+
+def _stem_pair(C, pad, seed=4):
+    torch.manual_seed(seed)
+    bn = BatchNorm2d(C)
+    with torch.no_grad():
+        bn.weight.uniform_(-1.0, 1.5)   # negative gammas too: max(relu(a x + b)) is not a monotone map of x
+        bn.bias.uniform_(-0.5, 0.5)
+    ref = torch.nn.BatchNorm2d(C).cuda()
+    ref.load_state_dict(bn.state_dict())
+    ldnn.prepare(bn, "cuda")
+    return bn, ref, MaxPool2d(3, 2, pad)
+
+
+@pytest.mark.parametrize("N,C,H,W,pad", [(4, 64, 20, 18, 1), (2, 16, 11, 13, 1), (3, 32, 12, 12, 0),
+                                         (2, 8, 9, 7, 0)])
+@pytest.mark.parametrize("twin", [False, True])
+def test_bn_relu_maxpool_fused(N, C, H, W, pad, twin, monkeypatch):
+    """maxpool3x3/2(relu(BN(x))) in one native pass each way (bn_maxpool_*) == the separate
+    native BN-apply + pool pair (identical outputs; gradients up to the fp32 summation order
+    of the statistics) and == the fp32 PyTorch reference."""
+    x = torch.randn(N, C, H, W, device="cuda") * 2 + 0.3
+    g1 = torch.randn(N, C, (H + 2 * pad - 3) // 2 + 1, (W + 2 * pad - 3) // 2 + 1, device="cuda").bfloat16().float()
+    g2 = torch.randn_like(g1).bfloat16().float()
+    res = []
+    for fused in (True, False):
+        monkeypatch.setattr(LF, "BN_POOL_FUSED", fused)
+        bn, ref, pool = _stem_pair(C, pad)
+        xb = _cl(x).requires_grad_(True)
+        y = LF.bn_relu_maxpool(xb, bn, pool)
+        assert (getattr(y, "_ldnn_twin", None) is not None)
+        loss = (y.float() * g1).sum()
+        if twin:
+            loss = loss + (LF.shortcut_input(y).float() * g2).sum()
+        loss.backward()
+        res.append((y.detach().float(), xb.grad.float(), bn.weight.grad.clone(), bn.bias.grad.clone(),
+                    bn.running_mean.clone(), bn.running_var.clone(), int(bn.num_batches_tracked)))
+    (yf, dxf, dgf, dbf, rmf, rvf, nbf), (yu, dxu, dgu, dbu, rmu, rvu, nbu) = res
+    assert torch.equal(yf, yu)
+    assert nbf == nbu == 1
+    torch.testing.assert_close(rmf, rmu, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(rvf, rvu, rtol=1e-5, atol=1e-6)
+    # (the separate pool pass rounds the pre-BN gradient to bf16 where windows overlap; the
+    # fused pass keeps it fp32)
+    torch.testing.assert_close(dgf, dgu, rtol=2e-2, atol=5e-3 * dgu.abs().max().item())
+    torch.testing.assert_close(dbf, dbu, rtol=2e-2, atol=5e-3 * dbu.abs().max().item())
+    torch.testing.assert_close(dxf, dxu, rtol=2e-2, atol=1e-2 * dxu.abs().max().item())
+    # fp32 reference (argmax ties within bf16 rounding may route a gradient to a neighbour:
+    # compare dx as a whole)
+    bn, ref, pool = _stem_pair(C, pad)
+    xf = _cl(x).float().contiguous().requires_grad_(True)
+    yr = F.max_pool2d(ref(xf).relu(), 3, 2, pad)
+    torch.testing.assert_close(yf, yr, rtol=2e-2, atol=3e-2)
+    ((yr * g1).sum() + ((yr * g2).sum() if twin else 0.0)).backward()
+    assert ((dxf - xf.grad).norm() / xf.grad.norm()).item() < 3e-2
+    assert ((dgf - ref.weight.grad).norm() / ref.weight.grad.norm()).item() < 3e-2
+    assert ((dbf - ref.bias.grad).norm() / ref.bias.grad.norm()).item() < 3e-2
+    torch.testing.assert_close(rmf, ref.running_mean, rtol=1e-3, atol=1e-4)
+    torch.testing.assert_close(rvf, ref.running_var, rtol=1e-3, atol=1e-3)
+
+
+def test_resnet_stem_fused_bn_pool_matches_separate(monkeypatch):
+    """ResNet-18 (stem statistics from the conv epilogue, then the fused BN + ReLU + max-pool)
+    trains like the separate BN-apply + pool passes."""
+    from ldnn.models import CrossEntropyLoss, build_model, xavier_init
+
+    x = torch.randn(4, 3, 64, 64, device="cuda").bfloat16()
+    yl = torch.randint(0, 10, (4,), device="cuda")
+    outs = []
+    for fused in (True, False):
+        monkeypatch.setattr(LF, "BN_POOL_FUSED", fused)
+        torch.manual_seed(0)
+        m = build_model("resnet18")
+        xavier_init(m)
+        ldnn.prepare(m, "cuda")
+        m.train()
+        out = m(x)
+        CrossEntropyLoss()(out, yl).backward()
+        outs.append((out.detach().float(), m.conv1.weight.grad.clone(), m.bn1.weight.grad.clone(),
+                     m.bn1.running_var.clone()))
+    (o1, w1, g1, v1), (o2, w2, g2, v2) = outs
+    assert ((o1 - o2).norm() / o2.norm()).item() < 1e-2
+    torch.testing.assert_close(v1, v2, rtol=1e-5, atol=1e-6)
+    assert ((g1 - g2).norm() / g2.norm()).item() < 5e-2
+    assert ((w1 - w2).norm() / w2.norm()).item() < 5e-2
