@@ -9,6 +9,8 @@
 // all-reduce), BR/communication.py:30,62 (ring), BDR/communication.py:39-40,77
 // (double ring) -- is  out = a*x + b*y1 + c*y2  for suitable (a, b, c), done in
 // one pass, in place, with the bf16 compute shadow refreshed in the same pass.
+#include <algorithm>
+
 #include "ldnn_common.h"
 #include "ldnn_kernels.h"
 
@@ -68,99 +70,78 @@ __global__ void act_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __re
     dx[i] = f2bf(act_b<ACT>(bf2f(dy[i]), bf2f(y[i])));
 }
 
-// Column sums of a [rows][cols] bf16 matrix: a block is 32 column-groups of 8
-// columns (16-B loads) x 8 row lanes; rows are split over gridDim.y.
-__global__ void colsum_kernel(const bf16_t* __restrict__ x, float* __restrict__ out, int rows, int cols,
-                              int rows_per_block) {
-  __shared__ float part[8][32 * 8];
-  const int cg = threadIdx.x & 31, ty = threadIdx.x >> 5;
-  const int c0 = (blockIdx.x * 32 + cg) * 8;
-  const int r_begin = blockIdx.y * rows_per_block;
-  const int r_end = min(rows, r_begin + rows_per_block);
-  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  if (c0 < cols) {
-    for (int r = r_begin + ty; r < r_end; r += 8) {
-      const u16x8 v = *reinterpret_cast<const u16x8*>(x + (size_t)r * cols + c0);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) s[j] += bf2f(v[j]);
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < 8; ++j) part[ty][cg * 8 + j] = s[j];
-  __syncthreads();
-  if (ty == 0 && c0 < cols) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float t = 0.f;
-#pragma unroll
-      for (int q = 0; q < 8; ++q) t += part[q][cg * 8 + j];
-      atomicAdd(out + c0 + j, t);
-    }
-  }
+// Column sums of a [rows][cols] bf16 matrix (bias gradients), optionally fused with an
+// activation backward (BWD: dx = act'(y) * dy, the sums taken from the fp32
+// derivative before rounding; dy may alias dx).  A block is `lanes` 8-column groups
+// (16-B accesses) x `rl` = 256 / lanes row lanes, lanes = min(cols / 8, 32): narrow
+// matrices keep every thread busy (a conv bias of 8 channels was 8 active threads
+// per block: 44 us for a 200704 x 8 colsum).  Rows split over gridDim.y, two rows
+// in flight per lane.  STORE (a single row block, first write): the block stores its
+// sums instead of adding them -- no zeroing launch.
+struct CsGeo {
+  int lanes, rl, gx, gy, rpb;
+};
+inline CsGeo cs_geo(int rows, int cols) {
+  CsGeo g;
+  const int cv = cols / 8;
+  g.lanes = cv < 32 ? cv : 32;
+  g.rl = 256 / g.lanes;
+  g.gx = (cv + g.lanes - 1) / g.lanes;
+  int gy = std::max(1, 1024 / g.gx);
+  gy = std::min(gy, std::max(1, (rows + 16 * g.rl - 1) / (16 * g.rl)));   // >= 16 rows per row lane
+  g.rpb = (rows + gy - 1) / gy;
+  g.gy = (rows + g.rpb - 1) / g.rpb;
+  return g;
 }
 
-// Activation backward fused with the bias-gradient column sums:
-//   dx = act'(y) * dy,   out[c] (+)= sum_r dx[r][c]
-// The dgrad GEMM of a library (hipBLASLt) step writes dy = dz_{l+1} W_l; this
-// one pass applies layer l-1's activation derivative and emits its bias
-// gradient (3 bf16 streams, no re-read of dx for a separate colsum).  dy may
-// alias dx (in place).  Same block shape as colsum_kernel: 32 column groups of
-// 8 columns (16-B accesses) x 8 row lanes; rows split over gridDim.y; the
-// column sums are taken from the fp32 derivative before rounding.
-template <int ACT>
-__global__ void act_bwd_colsum_kernel(const bf16_t* dy, const bf16_t* __restrict__ y, bf16_t* dx,
-                                      float* __restrict__ out, int rows, int cols, int rows_per_block) {
-  __shared__ float part[8][32 * 8];
-  const int cg = threadIdx.x & 31, ty = threadIdx.x >> 5;
-  const int c0 = (blockIdx.x * 32 + cg) * 8;
-  const int r_begin = blockIdx.y * rows_per_block;
-  const int r_end = min(rows, r_begin + rows_per_block);
+template <int ACT, bool BWD>
+__global__ __launch_bounds__(256) void colsum_geo_kernel(const bf16_t* dy, const bf16_t* __restrict__ y, bf16_t* dx,
+                                                         float* __restrict__ out, int rows, int cols, int rpb,
+                                                         int lanes, int rl, int store) {
+  __shared__ float part[256 * 8];
+  const int tid = threadIdx.x, lane = tid % lanes, ty = tid / lanes;
+  const int c0 = (blockIdx.x * lanes + lane) * 8;
+  const int r_begin = blockIdx.y * rpb;
+  const int r_end = min(rows, r_begin + rpb);
   float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  if (c0 < cols) {
-    int r = r_begin + ty;
-    for (; r + 8 < r_end; r += 16) {   // two rows in flight per lane
-      const size_t o0 = (size_t)r * cols + c0, o1 = o0 + (size_t)8 * cols;
-      const u16x8 g0 = *reinterpret_cast<const u16x8*>(dy + o0);
-      const u16x8 v0 = *reinterpret_cast<const u16x8*>(y + o0);
-      const u16x8 g1 = *reinterpret_cast<const u16x8*>(dy + o1);
-      const u16x8 v1 = *reinterpret_cast<const u16x8*>(y + o1);
-      u16x8 d0, d1;
+  auto row = [&](size_t o) {
+    const u16x8 g = *reinterpret_cast<const u16x8*>(dy + o);
+    if constexpr (BWD) {
+      const u16x8 v = *reinterpret_cast<const u16x8*>(y + o);
+      u16x8 d;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const float a = act_b<ACT>(bf2f(g0[j]), bf2f(v0[j]));
-        const float b = act_b<ACT>(bf2f(g1[j]), bf2f(v1[j]));
-        s[j] += a + b;
-        d0[j] = f2bf(a);
-        d1[j] = f2bf(b);
-      }
-      *reinterpret_cast<u16x8*>(dx + o0) = d0;
-      *reinterpret_cast<u16x8*>(dx + o1) = d1;
-    }
-    for (; r < r_end; r += 8) {
-      const size_t o0 = (size_t)r * cols + c0;
-      const u16x8 g0 = *reinterpret_cast<const u16x8*>(dy + o0);
-      const u16x8 v0 = *reinterpret_cast<const u16x8*>(y + o0);
-      u16x8 d0;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float a = act_b<ACT>(bf2f(g0[j]), bf2f(v0[j]));
+        const float a = act_b<ACT>(bf2f(g[j]), bf2f(v[j]));
         s[j] += a;
-        d0[j] = f2bf(a);
+        d[j] = f2bf(a);
       }
-      *reinterpret_cast<u16x8*>(dx + o0) = d0;
+      *reinterpret_cast<u16x8*>(dx + o) = d;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s[j] += bf2f(g[j]);
     }
+  };
+  if (ty < rl && c0 < cols) {
+    int r = r_begin + ty;
+    for (; r + rl < r_end; r += 2 * rl) {
+      row((size_t)r * cols + c0);
+      row((size_t)(r + rl) * cols + c0);
+    }
+    for (; r < r_end; r += rl) row((size_t)r * cols + c0);
   }
+  const int w = lanes * 8;
+  if (ty < rl) {
 #pragma unroll
-  for (int j = 0; j < 8; ++j) part[ty][cg * 8 + j] = s[j];
+    for (int j = 0; j < 8; ++j) part[ty * w + lane * 8 + j] = s[j];
+  }
   __syncthreads();
-  if (ty == 0 && c0 < cols) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float t = 0.f;
-#pragma unroll
-      for (int q = 0; q < 8; ++q) t += part[q][cg * 8 + j];
-      atomicAdd(out + c0 + j, t);
-    }
+  for (int ch = tid; ch < w; ch += 256) {
+    const int c = blockIdx.x * w + ch;
+    if (c >= cols) continue;
+    float t = 0.f;
+    for (int q = 0; q < rl; ++q) t += part[q * w + ch];
+    if (store) out[c] = t;
+    else atomicAdd(out + c, t);
   }
 }
 
@@ -365,34 +346,36 @@ hipError_t zero2d_f32(float* p, int rows, int cols, int ld, hipStream_t s) {
 }
 
 hipError_t colsum_bf16(const uint16_t* x, float* out, int rows, int cols, bool accumulate, hipStream_t s) {
-  if (!accumulate) {
+  if (cols <= 0) return hipSuccess;
+  if (cols % 8) return hipErrorInvalidValue;
+  const CsGeo g = cs_geo(std::max(rows, 1), cols);
+  const bool store = !accumulate && g.gy == 1;
+  if (!accumulate && !store) {
     hipError_t e = zero2d_f32(out, 1, cols, cols, s);
     if (e != hipSuccess) return e;
   }
-  if (rows <= 0 || cols <= 0) return hipSuccess;
-  const int gx = (cols + 255) / 256;
-  int gy = (rows + 255) / 256;
-  if (gy > 256) gy = 256;
-  const int rpb = (rows + gy - 1) / gy;
-  colsum_kernel<<<dim3(gx, gy), kBlock, 0, s>>>(x, out, rows, cols, rpb);
+  colsum_geo_kernel<ACT_RELU, false><<<dim3(g.gx, g.gy), kBlock, 0, s>>>(x, nullptr, nullptr, out, rows, cols, g.rpb,
+                                                                      g.lanes, g.rl, store ? 1 : 0);
   return hipGetLastError();
 }
 
 hipError_t act_bwd_colsum(const uint16_t* dy, const uint16_t* y, uint16_t* dx, float* out, int rows, int cols,
                           int act, bool accumulate, hipStream_t s) {
-  if (!accumulate) {
+  if (cols <= 0) return hipSuccess;
+  if (cols % 8) return hipErrorInvalidValue;
+  const CsGeo g = cs_geo(std::max(rows, 1), cols);
+  const bool store = !accumulate && g.gy == 1;
+  if (!accumulate && !store) {
     hipError_t e = zero2d_f32(out, 1, cols, cols, s);
     if (e != hipSuccess) return e;
   }
-  if (rows <= 0 || cols <= 0) return hipSuccess;
-  const int gx = (cols + 255) / 256;
-  int gy = (rows + 255) / 256;
-  if (gy > 256) gy = 256;
-  const int rpb = (rows + gy - 1) / gy;
+  const dim3 grid(g.gx, g.gy);
   if (act == ACT_RELU)
-    act_bwd_colsum_kernel<ACT_RELU><<<dim3(gx, gy), kBlock, 0, s>>>(dy, y, dx, out, rows, cols, rpb);
+    colsum_geo_kernel<ACT_RELU, true><<<grid, kBlock, 0, s>>>(dy, y, dx, out, rows, cols, g.rpb, g.lanes, g.rl,
+                                                              store ? 1 : 0);
   else
-    act_bwd_colsum_kernel<ACT_SIGMOID><<<dim3(gx, gy), kBlock, 0, s>>>(dy, y, dx, out, rows, cols, rpb);
+    colsum_geo_kernel<ACT_SIGMOID, true><<<grid, kBlock, 0, s>>>(dy, y, dx, out, rows, cols, g.rpb, g.lanes, g.rl,
+                                                                 store ? 1 : 0);
   return hipGetLastError();
 }
 

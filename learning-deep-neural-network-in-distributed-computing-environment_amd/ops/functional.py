@@ -84,14 +84,18 @@ class _LinearActNative(torch.autograd.Function):
         g = _padded_rows_view(_to_bf16(gy.reshape(-1, gy.shape[-1])), npad)
         if ctx.act is not None:
             gz = torch.empty_like(y)
-            C.act_bwd(g.contiguous(), y, gz, ctx.act)
+            if bias is not None:   # activation backward + the bias gradient's column sums in one pass
+                C.act_bwd_colsum(g.contiguous(), y, gz, flat.grad_storage(bias), ctx.act,
+                                 flat.grad_beta(bias) != 0.0)
+            else:
+                C.act_bwd(g.contiguous(), y, gz, ctx.act)
         else:
             gz = g.contiguous()
+            if bias is not None:
+                C.colsum(gz, flat.grad_storage(bias), flat.grad_beta(bias) != 0.0)
         # weight grad straight into the flat fp32 gradient buffer (accumulate, or
         # overwrite as the step's first write: FlatParams.grad_beta)
         C.gemm(gz, x2, flat.grad_storage(weight), False, False, beta=flat.grad_beta(weight))
-        if bias is not None:
-            C.colsum(gz, flat.grad_storage(bias), flat.grad_beta(bias) != 0.0)
         flat.notify(weight, bias)
         dx = None
         if ctx.needs_input_grad[0]:
@@ -228,7 +232,7 @@ def as_nhwc(t: torch.Tensor, cp: int, zero_pad: bool = True) -> torch.Tensor:
     if (t.dtype == torch.bfloat16 and t.stride(1) == 1 and t.stride(3) == cp and t.stride(2) == W * cp
             and t.stride(0) == H * W * cp):
         buf = t.as_strided((N, H, W, cp), (H * W * cp, W * cp, cp, 1), t.storage_offset())
-        if zero_pad and cp > C:
+        if zero_pad and cp > C and not getattr(t, "_ldnn_zpad", False):
             buf.data[..., C:].zero_()
         return buf
     if (cp % 8 == 0 and t.is_contiguous() and t.dtype in (torch.float32, torch.bfloat16)
@@ -246,6 +250,14 @@ def as_nhwc(t: torch.Tensor, cp: int, zero_pad: bool = True) -> torch.Tensor:
 def nchw_view(buf: torch.Tensor, c: int) -> torch.Tensor:
     """Dense NHWC buffer -> logical [N, c, H, W] view (channels_last strides)."""
     return buf[..., :c].permute(0, 3, 1, 2)
+
+
+def _zpad(t: torch.Tensor) -> torch.Tensor:
+    """Mark a native op's NHWC output whose pad channels (c .. cp-1) are exactly zero by
+    construction (zero weight rows / bias entries, pooling or gradients of zero pads), so
+    its consumer's as_nhwc skips the pad-clearing launch."""
+    t._ldnn_zpad = True
+    return t
 
 
 def _bn_train_state(mod, dev):
@@ -322,18 +334,22 @@ class _Conv2dNative(torch.autograd.Function):
         kp = y.shape[3]
         g = as_nhwc(gy if gy.dtype == torch.bfloat16 else gy.to(torch.bfloat16), kp)
         if relu:
-            gz = torch.empty_like(g)
-            C.act_bwd(g.contiguous(), y, gz, 0)
+            gz = torch.empty_like(y)
+            if bias is not None:   # ReLU backward + the bias gradient's column sums in one pass
+                C.act_bwd_colsum(g.contiguous().view(-1, kp), y.view(-1, kp), gz.view(-1, kp),
+                                 flat.grad_storage(bias), 0, flat.grad_beta(bias) != 0.0)
+            else:
+                C.act_bwd(g.contiguous(), y, gz, 0)
             g = gz
+        elif bias is not None:
+            C.colsum(g.contiguous().view(-1, kp), flat.grad_storage(bias), flat.grad_beta(bias) != 0.0)
         C.conv_wgrad(g, xb, flat.grad_storage(weight), stride, pad, flat.grad_beta(weight), real_channels=Cin)
-        if bias is not None:
-            C.colsum(g.view(-1, kp), flat.grad_storage(bias), flat.grad_beta(bias) != 0.0)
         flat.notify(weight, bias)
         dx = None
         if ctx.needs_input_grad[0]:
             dxb = torch.empty_like(xb)
             C.conv_dgrad(g, flat.shadow_storage(weight), dxb, stride, pad)
-            dx = nchw_view(dxb, Cin)
+            dx = _zpad(nchw_view(dxb, Cin))   # (weight pad channels are zero)
             if in_dtype != torch.bfloat16:
                 dx = dx.to(in_dtype)
         return dx, None, None, None, None, None, None, None
@@ -351,7 +367,8 @@ def conv2d(x, mod, relu: bool = False, bn=None):
         if not ok:
             raise RuntimeError("native conv needs groups=1, dilation=1, square stride/padding and "
                                "the model attached to FlatParams (ldnn.prepare(model))")
-        return _Conv2dNative.apply(x, mod.weight, mod.bias, mod.stride[0], mod.padding[0], flat, relu, bn)
+        # output pad channels: zero weight rows and bias entries -> exactly 0 (also after ReLU)
+        return _zpad(_Conv2dNative.apply(x, mod.weight, mod.bias, mod.stride[0], mod.padding[0], flat, relu, bn))
     y = F.conv2d(x.float(), mod.weight, mod.bias, mod.stride, mod.padding, mod.dilation, mod.groups)
     return F.relu(y) if relu else y
 
@@ -526,7 +543,7 @@ class _PoolNative(torch.autograd.Function):
             gt = as_nhwc(gy_twin if gy_twin.dtype == torch.bfloat16 else gy_twin.to(torch.bfloat16), cp).contiguous()
         dx = torch.empty(N, H, W, cp, dtype=torch.bfloat16, device=gy.device)
         C_.pool_bwd(g, am, dx, k, k, stride, pad, is_max, dy2=gt)
-        out = nchw_view(dx, C)
+        out = _zpad(nchw_view(dx, C))   # (pooled gradient of zero pad channels)
         return (out if in_dtype == torch.bfloat16 else out.to(in_dtype)), None, None, None, None
 
 
@@ -622,7 +639,8 @@ def pool2d(x, mod, is_max: bool):
               and (not is_max or _sq(mod.dilation) == 1) and (is_max or getattr(mod, "count_include_pad", True))
               and k * k <= 255)
     if _ext.use_native(x) and simple and x.dim() == 4:
-        return _with_twin(*_PoolNative.apply(x, k, st, pad, is_max))
+        y, twin = _PoolNative.apply(x, k, st, pad, is_max)   # (the input's pad was zeroed / zero)
+        return _with_twin(_zpad(y), _zpad(twin))
     if is_max:
         return F.max_pool2d(x, mod.kernel_size, mod.stride, mod.padding, mod.dilation, mod.ceil_mode)
     return F.avg_pool2d(x, mod.kernel_size, mod.stride, mod.padding, mod.ceil_mode, mod.count_include_pad)

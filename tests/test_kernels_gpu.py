@@ -425,7 +425,7 @@ def test_gemm_splitk_inlaunch_combine(splitk, case):
 @pytest.mark.parametrize("act", ["relu", "sigmoid"])
 @pytest.mark.parametrize("inplace", [False, True])
 @pytest.mark.parametrize("accumulate", [False, True])
-@pytest.mark.parametrize("rows,cols", [(1003, 264), (4096, 512), (7, 8)])
+@pytest.mark.parametrize("rows,cols", [(1003, 264), (4096, 512), (7, 8), (200704, 8), (50021, 48)])
 def test_act_bwd_colsum_matches_fp32(act, inplace, accumulate, rows, cols):
     """elementwise.hip act_bwd_colsum: dx = act'(y) * dy and out (+)= colsum(dx), vs torch fp32."""
     torch.manual_seed(rows + cols)
@@ -444,3 +444,17 @@ def test_act_bwd_colsum_matches_fp32(act, inplace, accumulate, rows, cols):
     ref_out = ref_dx.sum(0) + (base if accumulate else 0)
     torch.testing.assert_close(out, ref_out, rtol=1e-3, atol=1e-3 * (rows ** 0.5))
 
+
+
+@pytest.mark.parametrize("accumulate", [False, True])
+@pytest.mark.parametrize("rows,cols", [(200704, 8), (12345, 48), (256, 128), (3, 4096), (40000, 2056), (0, 16)])
+def test_colsum_geometries(rows, cols, accumulate):
+    """elementwise.hip colsum over narrow (conv-bias) and wide matrices, single-block stores and
+    multi-block atomics, vs torch fp32."""
+    torch.manual_seed(cols)
+    x = torch.randn(rows, cols, device="cuda").bfloat16()
+    base = torch.randn(cols, device="cuda")
+    out = base.clone()
+    C().colsum(x, out, accumulate)
+    ref = x.float().sum(0) + (base if accumulate else 0)
+    torch.testing.assert_close(out, ref, rtol=1e-3, atol=1e-3 * max(1.0, rows ** 0.5))
