@@ -784,8 +784,8 @@ __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void conv_lds_kernel(LArgs a,
           oa.advance(a);
           ob.advance(a);
         }
-        LDNN_DMA_TILE(oa, PPA, ra, smem + t * STAGE, ks);
-        LDNN_DMA_TILE(ob, PPB, rb, smem + t * STAGE + A_BYTES, ks);
+        if constexpr (!(XF & 16)) LDNN_DMA_TILE(oa, PPA, ra, smem + t * STAGE, ks);
+        if constexpr (!(XF & 8)) LDNN_DMA_TILE(ob, PPB, rb, smem + t * STAGE + A_BYTES, ks);
       }
     }
 
@@ -810,10 +810,10 @@ __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void conv_lds_kernel(LArgs a,
           for (int i_ = 0; i_ < PPA; ++i_)
             __builtin_amdgcn_raw_ptr_buffer_load_lds(ra.r, (lds_void*)(nxt + (i_ * NW + wid) * 1024), 16,
                                                      (int)(tb + (i_ * NW + wid) * 1024 + lane * 16), 0, 0, 0);
-        } else {
+        } else if constexpr (!(XF & 16)) {
           LDNN_DMA_TILE(oa, PPA, ra, nxt, ks);
         }
-        LDNN_DMA_TILE(ob, PPB, rb, nxt + A_BYTES, ks);
+        if constexpr (!(XF & 8)) LDNN_DMA_TILE(ob, PPB, rb, nxt + A_BYTES, ks);  // XF 8 / 16: no B / A fill
       }
       const char* la = smem + cur * STAGE;
       const char* lb = la + A_BYTES;
@@ -1694,6 +1694,8 @@ hipError_t launch_ns(LArgs a, int epi, int splits, const bf16_t* pa, size_t ba, 
           if constexpr (!std::is_same_v<OA, FwdA<128, 4, 4>>) return hipErrorInvalidValue;
           else conv_lds_kernel<WM, WN, OA, OB, EPI_NONE, OUT_F32, DGRAD, NS, 6><<<grid, block, 0, st>>>(a, pa, (uint32_t)ba, pb, (uint32_t)bb);
           break;
+        case 8: conv_lds_kernel<WM, WN, OA, OB, EPI_NONE, OUT_F32, DGRAD, NS, 8><<<grid, block, 0, st>>>(a, pa, (uint32_t)ba, pb, (uint32_t)bb); break;
+        case 16: conv_lds_kernel<WM, WN, OA, OB, EPI_NONE, OUT_F32, DGRAD, NS, 16><<<grid, block, 0, st>>>(a, pa, (uint32_t)ba, pb, (uint32_t)bb); break;
         default: return hipErrorInvalidValue;
       }
       return hipGetLastError();
