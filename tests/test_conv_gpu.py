@@ -17,6 +17,7 @@ SHAPES = [
     (8, 1, 28, 28, 6, 5, 1, 2),       # LeNet conv1 (C 1 -> 8, K 6 -> 8)
     (8, 6, 14, 14, 16, 5, 1, 0),      # LeNet conv2
     (2, 3, 64, 64, 64, 7, 2, 3),      # ResNet stem
+    (3, 5, 17, 17, 24, 3, 2, 1),      # small-channel VALU dgrad, stride 2
     # LDS-DMA fast path (C / K multiples of 64): 64-channel tiles, ragged rows,
     # stride-2 parity-class dgrad, split-K combine of the small-M tail stages
     (2, 64, 56, 56, 64, 3, 1, 1),     # ResNet layer1 (256x64 tiles)
@@ -92,7 +93,8 @@ def test_conv_fwd_dgrad_wgrad(N, C, H, W, K, R, st, pad):
                                                 (2, 128, 16, 16, 64, 3, 1, 1), (4, 1024, 2, 2, 1024, 3, 1, 1),
                                                 (2, 8, 40, 40, 64, 7, 2, 3), (3, 16, 9, 9, 32, 3, 1, 1),
                                                 (2, 32, 12, 12, 128, 5, 1, 2), (2, 8, 64, 64, 64, 7, 2, 3),
-                                                (3, 8, 32, 32, 128, 3, 1, 1)])
+                                                (3, 8, 32, 32, 128, 3, 1, 1), (3, 8, 17, 17, 24, 3, 2, 1),
+                                                (4, 8, 14, 14, 16, 5, 1, 0)])
 def test_lds_fast_path_matches_generic_kernel(N, C, H, W, K, R, st, pad):
     """The LDS-DMA kernels (set_conv_impl(0)) agree with the generic register-staged
     kernels (set_conv_impl(1)) on every output, and repeated launches of the
