@@ -1112,6 +1112,99 @@ void pool_bwd(const at::Tensor& dy, const c10::optional<at::Tensor>& argmax, con
         "pool2d_bwd");
 }
 
+// y = relu(bn_a(x) + bn_b(r)): residual block tail whose shortcut carries its own BatchNorm
+// (the shortcut BN's output is never stored).  x, r, y: [M][C] dense bf16.
+ldnn::BnArgs dual_args(const at::Tensor& x, const c10::optional<at::Tensor>& gamma,
+                       const c10::optional<at::Tensor>& beta, const c10::optional<at::Tensor>& running_mean,
+                       const c10::optional<at::Tensor>& running_var, const at::Tensor& save_mean,
+                       const at::Tensor& save_invstd, const at::Tensor& ws, double eps, double momentum,
+                       const c10::optional<at::Tensor>& num_batches) {
+  const int64_t M = x.size(0), C = x.size(1);
+  ldnn::BnArgs a{};
+  a.x = bf16_ptr(x);
+  a.gamma = fptr_opt(gamma, C, "gamma");
+  a.beta = fptr_opt(beta, C, "beta");
+  a.running_mean = fptr_opt(running_mean, C, "running_mean");
+  a.running_var = fptr_opt(running_var, C, "running_var");
+  a.save_mean = fptr_opt(save_mean, C, "save_mean");
+  a.save_invstd = fptr_opt(save_invstd, C, "save_invstd");
+  a.ws = fptr_opt(ws, ldnn::bn_workspace_floats((int)C), "ws");
+  a.M = (int)M;
+  a.C = (int)C;
+  a.eps = (float)eps;
+  a.momentum = (float)momentum;
+  a.training = 1;
+  if (num_batches.has_value()) {
+    check_dev(*num_batches, at::kLong, "num_batches");
+    a.num_batches = num_batches->data_ptr<int64_t>();
+  }
+  return a;
+}
+
+void bn_dual_fwd(const at::Tensor& x, const at::Tensor& r, const at::Tensor& y, const c10::optional<at::Tensor>& mask,
+                 const c10::optional<at::Tensor>& gamma_a, const c10::optional<at::Tensor>& beta_a,
+                 const c10::optional<at::Tensor>& rm_a, const c10::optional<at::Tensor>& rv_a,
+                 const at::Tensor& mean_a, const at::Tensor& invstd_a, const at::Tensor& ws_a, double eps_a,
+                 double mom_a, const c10::optional<at::Tensor>& nb_a, bool ready_a,
+                 const c10::optional<at::Tensor>& gamma_b, const c10::optional<at::Tensor>& beta_b,
+                 const c10::optional<at::Tensor>& rm_b, const c10::optional<at::Tensor>& rv_b,
+                 const at::Tensor& mean_b, const at::Tensor& invstd_b, const at::Tensor& ws_b, double eps_b,
+                 double mom_b, const c10::optional<at::Tensor>& nb_b, bool ready_b) {
+  for (const at::Tensor* t : {&x, &r, &y}) {
+    check_dev(*t, at::kBFloat16, "bn_dual_fwd tensor");
+    TORCH_CHECK(t->dim() == 2 && t->is_contiguous() && t->sizes() == x.sizes(), "bn_dual_fwd: [M][C] dense");
+  }
+  TORCH_CHECK(x.size(1) % 8 == 0, "bn_dual_fwd: C % 8");
+  ldnn::BnArgs a = dual_args(x, gamma_a, beta_a, rm_a, rv_a, mean_a, invstd_a, ws_a, eps_a, mom_a, nb_a);
+  ldnn::BnArgs b = dual_args(r, gamma_b, beta_b, rm_b, rv_b, mean_b, invstd_b, ws_b, eps_b, mom_b, nb_b);
+  a.y = bf16_mut(y);
+  a.relu = 1;
+  if (mask.has_value()) {
+    check_dev(*mask, at::kByte, "mask");
+    TORCH_CHECK(mask->is_contiguous() && mask->numel() == x.numel() / 8, "bn_dual_fwd: mask [M][C/8]");
+    a.mask = mask->data_ptr<uint8_t>();
+  }
+  check(ldnn::bn_dual_forward(a, b, ready_a, ready_b, cur_stream(x)), "bn_dual_forward");
+}
+
+void bn_dual_bwd(const at::Tensor& x, const at::Tensor& r, const at::Tensor& y, const c10::optional<at::Tensor>& mask,
+                 const at::Tensor& dy, const c10::optional<at::Tensor>& dy2, const at::Tensor& dx,
+                 const at::Tensor& dr, const c10::optional<at::Tensor>& gamma_a, const at::Tensor& mean_a,
+                 const at::Tensor& invstd_a, const at::Tensor& ws_a, const c10::optional<at::Tensor>& dgamma_a,
+                 const c10::optional<at::Tensor>& dbeta_a, bool assign_a, const c10::optional<at::Tensor>& gamma_b,
+                 const at::Tensor& mean_b, const at::Tensor& invstd_b, const at::Tensor& ws_b,
+                 const c10::optional<at::Tensor>& dgamma_b, const c10::optional<at::Tensor>& dbeta_b,
+                 bool assign_b) {
+  for (const at::Tensor* t : {&x, &r, &dy, &dx, &dr}) {
+    check_dev(*t, at::kBFloat16, "bn_dual_bwd tensor");
+    TORCH_CHECK(t->dim() == 2 && t->is_contiguous() && t->sizes() == x.sizes(), "bn_dual_bwd: [M][C] dense");
+  }
+  const int64_t C = x.size(1);
+  ldnn::BnArgs a = dual_args(x, gamma_a, c10::nullopt, c10::nullopt, c10::nullopt, mean_a, invstd_a, ws_a, 0.0, 0.0,
+                             c10::nullopt);
+  ldnn::BnArgs b = dual_args(r, gamma_b, c10::nullopt, c10::nullopt, c10::nullopt, mean_b, invstd_b, ws_b, 0.0, 0.0,
+                             c10::nullopt);
+  a.relu = 1;
+  if (mask.has_value()) {
+    check_dev(*mask, at::kByte, "mask");
+    TORCH_CHECK(mask->is_contiguous() && mask->numel() == x.numel() / 8, "bn_dual_bwd: mask [M][C/8]");
+    a.mask = mask->data_ptr<uint8_t>();
+  } else {
+    check_dev(y, at::kBFloat16, "y");
+    TORCH_CHECK(y.sizes() == x.sizes() && y.is_contiguous(), "bn_dual_bwd: y layout");
+    a.y = bf16_mut(y);
+  }
+  if (dy2.has_value()) {
+    check_dev(*dy2, at::kBFloat16, "dy2");
+    TORCH_CHECK(dy2->sizes() == x.sizes() && dy2->is_contiguous(), "bn_dual_bwd: dy2 layout");
+    a.dy2 = bf16_ptr(*dy2);
+  }
+  check(ldnn::bn_dual_backward(a, b, bf16_ptr(dy), bf16_mut(dx), bf16_mut(dr), fptr_opt(dgamma_a, C, "dgamma_a"),
+                               fptr_opt(dbeta_a, C, "dbeta_a"), fptr_opt(dgamma_b, C, "dgamma_b"),
+                               fptr_opt(dbeta_b, C, "dbeta_b"), assign_a, assign_b, cur_stream(x)),
+        "bn_dual_backward");
+}
+
 // relu(BN(x)) -> 3x3/2 max-pool in one pass: x [N][H][W][C] (pre-BN), y / argmax [N][P][Q][C]
 bool bn_pool_fwd(const at::Tensor& x, const at::Tensor& y, const at::Tensor& argmax,
                  const c10::optional<at::Tensor>& gamma, const c10::optional<at::Tensor>& beta,
@@ -1538,6 +1631,17 @@ PYBIND11_MODULE(_C, m) {
   m.def("pool_fwd", &pool_fwd);
   m.def("pool_bwd", &pool_bwd, py::arg("dy"), py::arg("argmax"), py::arg("dx"), py::arg("R"), py::arg("S"),
         py::arg("stride"), py::arg("pad"), py::arg("is_max"), py::arg("dy2") = py::none());
+  m.def("bn_dual_fwd", &bn_dual_fwd, "y = relu(bn_a(x) + bn_b(r)) in one pass (the shortcut BN output never stored)",
+        py::arg("x"), py::arg("r"), py::arg("y"), py::arg("mask"), py::arg("gamma_a"), py::arg("beta_a"),
+        py::arg("rm_a"), py::arg("rv_a"), py::arg("mean_a"), py::arg("invstd_a"), py::arg("ws_a"), py::arg("eps_a"),
+        py::arg("mom_a"), py::arg("nb_a"), py::arg("ready_a"), py::arg("gamma_b"), py::arg("beta_b"),
+        py::arg("rm_b"), py::arg("rv_b"), py::arg("mean_b"), py::arg("invstd_b"), py::arg("ws_b"), py::arg("eps_b"),
+        py::arg("mom_b"), py::arg("nb_b"), py::arg("ready_b"));
+  m.def("bn_dual_bwd", &bn_dual_bwd, "backward of bn_dual_fwd: dx, dr and both BNs' dgamma / dbeta",
+        py::arg("x"), py::arg("r"), py::arg("y"), py::arg("mask"), py::arg("dy"), py::arg("dy2"), py::arg("dx"),
+        py::arg("dr"), py::arg("gamma_a"), py::arg("mean_a"), py::arg("invstd_a"), py::arg("ws_a"),
+        py::arg("dgamma_a"), py::arg("dbeta_a"), py::arg("assign_a"), py::arg("gamma_b"), py::arg("mean_b"),
+        py::arg("invstd_b"), py::arg("ws_b"), py::arg("dgamma_b"), py::arg("dbeta_b"), py::arg("assign_b"));
   m.def("bn_pool_fwd", &bn_pool_fwd, "relu(BN(x)) -> 3x3/2 max-pool in one pass (pooled output + argmax)",
         py::arg("x"), py::arg("y"), py::arg("argmax"), py::arg("gamma"), py::arg("beta"), py::arg("running_mean"),
         py::arg("running_var"), py::arg("save_mean"), py::arg("save_invstd"), py::arg("ws"), py::arg("eps"),

@@ -198,6 +198,14 @@ hipError_t bn_forward_apply(const BnArgs& a, hipStream_t s);
 // branch); dgamma / dbeta are ACCUMULATED (flat gradient buffer)
 hipError_t bn_backward(const BnArgs& a, const uint16_t* dy, uint16_t* dx, uint16_t* dres, float* dgamma,
                        float* dbeta, hipStream_t s, bool grad_assign = false);
+// Residual block tail with a BatchNorm on both branches: y = relu(bn_a(a.x) + bn_b(b.x)), the
+// shortcut BN's output never stored (a.relu, both training mode; ready_*: statistics already
+// finalized into the ws by the producing convs).  a.y / a.mask: the output and its ReLU bits.
+hipError_t bn_dual_forward(const BnArgs& a, const BnArgs& b, bool ready_a, bool ready_b, hipStream_t s);
+// its backward: dx = d/d a.x, dr = d/d b.x from dy (+ a.dy2); dgamma / dbeta as bn_backward
+hipError_t bn_dual_backward(const BnArgs& a, const BnArgs& b, const uint16_t* dy, uint16_t* dx, uint16_t* dr,
+                            float* dgamma_a, float* dbeta_a, float* dgamma_b, float* dbeta_b, bool assign_a,
+                            bool assign_b, hipStream_t s);
 // relu(BN(x)) -> 3x3/2 max-pool in one pass (a.x = [N][H][W][C] pre-BN, a.M = N*H*W, a.relu = 1):
 // y [N][P][Q][C] pooled, arg [N][P][Q][C] window argmax (0xff: the max was clamped by the ReLU).
 // stats_ready: scale / shift already in a.ws (the producing conv's epilogue finalized them).

@@ -207,18 +207,28 @@ __device__ __forceinline__ void load8(const float* p, float (&v)[8]) {
 }
 
 // y = relu?( x * scale[c] + shift[c] (+ res) ) -- same fixed-channel geometry
-template <bool RES, bool RELU, bool MASK = false>
+// RA: the residual is itself a BatchNorm's INPUT (the pre-BN shortcut conv output):
+// y = relu?( x * scale + shift + res * scale2 + shift2 ) -- the shortcut BN's output is never stored
+template <bool RES, bool RELU, bool MASK = false, bool RA = false>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
                                                        const float* __restrict__ scale,
                                                        const float* __restrict__ shift, bf16_t* __restrict__ y,
                                                        int M, int C, int rpb, int lanes, int rl,
-                                                       uint8_t* __restrict__ mask = nullptr) {
+                                                       uint8_t* __restrict__ mask = nullptr,
+                                                       const float* __restrict__ scale2 = nullptr,
+                                                       const float* __restrict__ shift2 = nullptr) {
   const int tid = threadIdx.x, lane = tid % lanes, rlane = tid / lanes;
   const int c0 = (blockIdx.x * 256 + lane) * 8;
   if (rlane >= rl || c0 >= C) return;
-  float sc[8], sh[8];
+  float sc[8], sh[8], sc2[8], sh2[8];
   load8(scale + c0, sc);
   load8(shift + c0, sh);
+  if constexpr (RA) {
+    load8(scale2 + c0, sc2);
+    load8(shift2 + c0, sh2);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sh[j] += sh2[j];
+  }
   const int r_end = min(M, (int)(blockIdx.y + 1) * rpb);
 #pragma unroll 4
   for (int r = blockIdx.y * rpb + rlane; r < r_end; r += rl) {
@@ -230,7 +240,8 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict_
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float v = bf2f(xv[j]) * sc[j] + sh[j];
-      if constexpr (RES) v += bf2f(rv[j]);
+      if constexpr (RA) v += bf2f(rv[j]) * sc2[j];
+      else if constexpr (RES) v += bf2f(rv[j]);
       if constexpr (RELU) v = fmaxf(v, 0.f);
       out[j] = f2bf(v);
     }
@@ -283,6 +294,142 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16_t* __restr
     }
     *reinterpret_cast<u16x8*>(dx + o) = out;
     if (dres) *reinterpret_cast<u16x8*>(dres + o) = og;
+  }
+}
+
+// ---- residual block tail with a BN on both branches: y = relu(bn1(x) + bn2(r)) ------
+// Both BNs see the same post-ReLU gradient g = dy (+ dy2) * relu'(y), so one pass
+// accumulates sum g (shared), sum g * xhat and sum g * rhat, and its last block
+// finalizes both BNs' coefficients; one apply pass writes dx and dr.  (The separate
+// path: bn1 reduce + apply writing dx AND the residual gradient g, then the shortcut BN's
+// reduce + apply reading g back.)
+template <bool MASK>
+__global__ __launch_bounds__(256) void bn_reduce_dual_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ r,
+                                                             const bf16_t* __restrict__ dy,
+                                                             const bf16_t* __restrict__ dy2,
+                                                             const bf16_t* __restrict__ y,
+                                                             const uint8_t* __restrict__ mask, int M, int C, int rpb,
+                                                             int lanes, int rl, BnFin fin1, BnFin fin2, int ncop) {
+  __shared__ float red[3][256 * 8];
+  const int tid = threadIdx.x, lane = tid % lanes, rlane = tid / lanes;
+  const int c0 = (blockIdx.x * 256 + lane) * 8;
+  const bool active = rlane < rl && c0 < C;
+  float s0[8], s1[8], s2[8], mu1[8], is1[8], mu2[8], is2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    s0[j] = s1[j] = s2[j] = 0.f;
+    mu1[j] = is1[j] = mu2[j] = is2[j] = 0.f;
+  }
+  if (active) {
+    load8(fin1.save_mean + c0, mu1);
+    load8(fin1.save_invstd + c0, is1);
+    load8(fin2.save_mean + c0, mu2);
+    load8(fin2.save_invstd + c0, is2);
+    const int r_end = min(M, (int)(blockIdx.y + 1) * rpb);
+#pragma unroll 2
+    for (int row = blockIdx.y * rpb + rlane; row < r_end; row += rl) {
+      const size_t o = (size_t)row * C + c0;
+      const u16x8 xv = *reinterpret_cast<const u16x8*>(x + o);
+      const u16x8 rv = *reinterpret_cast<const u16x8*>(r + o);
+      const u16x8 gv = *reinterpret_cast<const u16x8*>(dy + o);
+      u16x8 g2v = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (dy2) g2v = *reinterpret_cast<const u16x8*>(dy2 + o);
+      u16x8 yv;
+      uint32_t mb = 0;
+      if constexpr (MASK) mb = mask[o >> 3];
+      else yv = *reinterpret_cast<const u16x8*>(y + o);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float g = bf2f(gv[j]) + bf2f(g2v[j]);
+        if constexpr (MASK) g = ((mb >> j) & 1u) ? g : 0.f;
+        else g = bf2f(yv[j]) > 0.f ? g : 0.f;
+        s0[j] += g;
+        s1[j] += g * (bf2f(xv[j]) - mu1[j]) * is1[j];
+        s2[j] += g * (bf2f(rv[j]) - mu2[j]) * is2[j];
+      }
+    }
+  }
+  const int wrow = lanes * 8;
+  if (rlane < rl) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      red[0][rlane * wrow + lane * 8 + j] = s0[j];
+      red[1][rlane * wrow + lane * 8 + j] = s1[j];
+      red[2][rlane * wrow + lane * 8 + j] = s2[j];
+    }
+  }
+  __syncthreads();
+  const int cp = (blockIdx.x + gridDim.x * blockIdx.y) % ncop;
+  float* acc1 = fin1.acc + (size_t)cp * 2 * C;
+  float* acc2 = fin2.acc + (size_t)cp * 2 * C;
+  for (int ch = tid; ch < wrow; ch += 256) {
+    float t0 = 0.f, t1 = 0.f, t2 = 0.f;
+    for (int q = 0; q < rl; ++q) {
+      t0 += red[0][q * wrow + ch];
+      t1 += red[1][q * wrow + ch];
+      t2 += red[2][q * wrow + ch];
+    }
+    const int c = blockIdx.x * 2048 + ch;
+    if (c < C) {
+      bn_acc_add(acc1 + c, t0);
+      bn_acc_add(acc1 + C + c, t1);
+      bn_acc_add(acc2 + c, t0);
+      bn_acc_add(acc2 + C + c, t2);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's atomics have completed
+  const int nblk = gridDim.x * gridDim.y;
+  bn_finalize_last<true, kBnCopies>(fin1, M, C, nblk, &red[0][0], 3 * 256 * 8, ncop);
+  __syncthreads();
+  bn_finalize_last<true, kBnCopies>(fin2, M, C, nblk, &red[0][0], 3 * 256 * 8, ncop);
+}
+
+// dx = A1 g + B1 x + D1, dr = A2 g + B2 r + D2
+template <bool MASK>
+__global__ __launch_bounds__(256) void bn_bwd_apply_dual_kernel(const bf16_t* __restrict__ x,
+                                                                const bf16_t* __restrict__ r,
+                                                                const bf16_t* __restrict__ dy,
+                                                                const bf16_t* __restrict__ dy2,
+                                                                const bf16_t* __restrict__ y,
+                                                                const uint8_t* __restrict__ mask,
+                                                                const float* __restrict__ coef1,
+                                                                const float* __restrict__ coef2, bf16_t* __restrict__ dx,
+                                                                bf16_t* __restrict__ dr, int M, int C, int rpb,
+                                                                int lanes, int rl) {
+  const int tid = threadIdx.x, lane = tid % lanes, rlane = tid / lanes;
+  const int c0 = (blockIdx.x * 256 + lane) * 8;
+  if (rlane >= rl || c0 >= C) return;
+  float A1[8], B1[8], D1[8], A2[8], B2[8], D2[8];
+  load8(coef1 + c0, A1);
+  load8(coef1 + C + c0, B1);
+  load8(coef1 + 2 * C + c0, D1);
+  load8(coef2 + c0, A2);
+  load8(coef2 + C + c0, B2);
+  load8(coef2 + 2 * C + c0, D2);
+  const int r_end = min(M, (int)(blockIdx.y + 1) * rpb);
+#pragma unroll 2
+  for (int row = blockIdx.y * rpb + rlane; row < r_end; row += rl) {
+    const size_t o = (size_t)row * C + c0;
+    const u16x8 xv = *reinterpret_cast<const u16x8*>(x + o);
+    const u16x8 rv = *reinterpret_cast<const u16x8*>(r + o);
+    const u16x8 gv = *reinterpret_cast<const u16x8*>(dy + o);
+    u16x8 g2v = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (dy2) g2v = *reinterpret_cast<const u16x8*>(dy2 + o);
+    u16x8 yv;
+    uint32_t mb = 0;
+    if constexpr (MASK) mb = mask[o >> 3];
+    else yv = *reinterpret_cast<const u16x8*>(y + o);
+    u16x8 ox, orr;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float g = bf2f(gv[j]) + bf2f(g2v[j]);
+      if constexpr (MASK) g = ((mb >> j) & 1u) ? g : 0.f;
+      else g = bf2f(yv[j]) > 0.f ? g : 0.f;
+      ox[j] = f2bf(A1[j] * g + B1[j] * bf2f(xv[j]) + D1[j]);
+      orr[j] = f2bf(A2[j] * g + B2[j] * bf2f(rv[j]) + D2[j]);
+    }
+    *reinterpret_cast<u16x8*>(dx + o) = ox;
+    *reinterpret_cast<u16x8*>(dr + o) = orr;
   }
 }
 
@@ -855,6 +1002,67 @@ hipError_t bn_backward(const BnArgs& a, const uint16_t* dy, uint16_t* dx, uint16
   else
     bn_bwd_apply_kernel<false><<<grid, 256, 0, s>>>(a.x, dy, nullptr, f.coef, dx, dres, M, C, g.rpb, g.lanes, g.rl,
                                                     nullptr, a.dy2);
+  return hipGetLastError();
+}
+
+hipError_t bn_dual_forward(const BnArgs& a, const BnArgs& b, bool ready_a, bool ready_b, hipStream_t s) {
+  const int M = a.M, C = a.C;
+  if (C % 8 || b.C != C || b.M != M || !a.relu || !a.training || !b.training) return hipErrorInvalidValue;
+  if (M <= 0) return hipSuccess;
+  if (!ready_a) bn_forward_stats(a, s);
+  if (!ready_b) bn_forward_stats(b, s);
+  const RedGeo g = red_geo(M, C);
+  const dim3 grid(g.gx, g.gy);
+  if (a.mask)
+    bn_apply_kernel<true, true, true, true><<<grid, 256, 0, s>>>(a.x, b.x, a.ws, a.ws + C, a.y, M, C, g.rpb, g.lanes,
+                                                                 g.rl, a.mask, b.ws, b.ws + C);
+  else
+    bn_apply_kernel<true, true, false, true><<<grid, 256, 0, s>>>(a.x, b.x, a.ws, a.ws + C, a.y, M, C, g.rpb, g.lanes,
+                                                                  g.rl, nullptr, b.ws, b.ws + C);
+  return hipGetLastError();
+}
+
+namespace {
+BnFin bn_backward_fin(const BnArgs& a, float* dgamma, float* dbeta, bool grad_assign) {
+  const int C = a.C;
+  BnFin f{};
+  f.acc = a.ws + 10 * C + 32 + kBnCopies * 2 * C;
+  f.ticket = reinterpret_cast<int*>(a.ws + 10 * C + 16);
+  f.gamma = a.gamma;
+  f.save_mean = a.save_mean;
+  f.save_invstd = a.save_invstd;
+  f.coef = a.ws + 6 * C;
+  f.dgamma = dgamma;
+  f.dbeta = dbeta;
+  f.grad_assign = grad_assign ? 1 : 0;
+  return f;
+}
+}  // namespace
+
+hipError_t bn_dual_backward(const BnArgs& a, const BnArgs& b, const uint16_t* dy, uint16_t* dx, uint16_t* dr,
+                            float* dgamma_a, float* dbeta_a, float* dgamma_b, float* dbeta_b, bool assign_a,
+                            bool assign_b, hipStream_t s) {
+  const int M = a.M, C = a.C;
+  if (C % 8 || b.C != C || b.M != M || !a.relu) return hipErrorInvalidValue;
+  if (M <= 0) return hipSuccess;
+  const BnFin fa = bn_backward_fin(a, dgamma_a, dbeta_a, assign_a);
+  const BnFin fb = bn_backward_fin(b, dgamma_b, dbeta_b, assign_b);
+  const RedGeo gr = red_geo(M, C, true);
+  const dim3 grid_r(gr.gx, gr.gy);
+  const int ncop = bn_ncop(true, gr.gx * gr.gy);
+  const RedGeo g = red_geo(M, C);
+  const dim3 grid(g.gx, g.gy);
+  if (a.mask) {
+    bn_reduce_dual_kernel<true><<<grid_r, 256, 0, s>>>(a.x, b.x, dy, a.dy2, nullptr, a.mask, M, C, gr.rpb, gr.lanes,
+                                                       gr.rl, fa, fb, ncop);
+    bn_bwd_apply_dual_kernel<true><<<grid, 256, 0, s>>>(a.x, b.x, dy, a.dy2, nullptr, a.mask, fa.coef, fb.coef, dx, dr,
+                                                        M, C, g.rpb, g.lanes, g.rl);
+  } else {
+    bn_reduce_dual_kernel<false><<<grid_r, 256, 0, s>>>(a.x, b.x, dy, a.dy2, a.y, nullptr, M, C, gr.rpb, gr.lanes,
+                                                        gr.rl, fa, fb, ncop);
+    bn_bwd_apply_dual_kernel<false><<<grid, 256, 0, s>>>(a.x, b.x, dy, a.dy2, a.y, nullptr, fa.coef, fb.coef, dx, dr,
+                                                         M, C, g.rpb, g.lanes, g.rl);
+  }
   return hipGetLastError();
 }
 

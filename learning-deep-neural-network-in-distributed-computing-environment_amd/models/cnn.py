@@ -56,7 +56,10 @@ class ResBlock(nn.Module):
         # the shortcut reads x's twin (LF.shortcut_input), so the producer of x sums the two
         # branch gradients in its own backward kernels instead of a separate add
         out = self.bn1.act(self.conv1(x), relu=True)
-        return self.bn2.act(self.conv2(out), residual=self.shortcut(LF.shortcut_input(x)), relu=True)
+        if len(self.shortcut):   # conv1x1 + BN shortcut: both BNs, the add and the ReLU in one pass
+            c2 = self.conv2(out)
+            return LF.batch_norm_dual_act(c2, self.bn2, self.shortcut[0](LF.shortcut_input(x)), self.shortcut[1])
+        return self.bn2.act(self.conv2(out), residual=LF.shortcut_input(x), relu=True)
 
 
 class EnhancedCNNModel(nn.Module):

@@ -28,9 +28,11 @@ class BasicBlock(nn.Module):
 
     def forward(self, x):
         xs = LF.shortcut_input(x)   # (x's twin: see models/cnn.py ResBlock)
-        idt = xs if self.downsample is None else self.downsample(xs)
         out = self.bn1.act(self.conv1(x), relu=True)
-        return self.bn2.act(self.conv2(out), residual=idt, relu=True)
+        if self.downsample is not None:   # conv1x1 + BN shortcut: both BNs, the add and the ReLU in one pass
+            c2 = self.conv2(out)
+            return LF.batch_norm_dual_act(c2, self.bn2, self.downsample[0](xs), self.downsample[1])
+        return self.bn2.act(self.conv2(out), residual=xs, relu=True)
 
 
 class ResNet(nn.Module):

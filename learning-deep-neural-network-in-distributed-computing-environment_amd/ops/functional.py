@@ -479,6 +479,108 @@ class _BatchNormNative(torch.autograd.Function):
         return dxv, None, None, dresv, None, None, None
 
 
+class _BatchNormDualNative(torch.autograd.Function):
+    """relu(bn_a(x) + bn_b(r)) -- a residual block whose shortcut carries its own BatchNorm
+    (1x1 downsample conv + BN) -- as one native pass each way (bn_pool.hip bn_dual_*): the
+    shortcut BN's output is never stored, both BNs' backward statistics come from one
+    reduce pass over the shared post-ReLU gradient, and one apply pass writes dx and dr."""
+
+    @staticmethod
+    def forward(ctx, x, r, wa, ba, wb, bb, mod_a, mod_b, flat):
+        C_ = _ext.C()
+        N, C, H, W = x.shape
+        dev = x.device
+        x2 = as_nhwc(x if x.dtype == torch.bfloat16 else x.to(torch.bfloat16), C, zero_pad=False).reshape(-1, C)
+        r2 = as_nhwc(r if r.dtype == torch.bfloat16 else r.to(torch.bfloat16), C, zero_pad=False).reshape(-1, C)
+        y = torch.empty(N, H, W, C, dtype=torch.bfloat16, device=dev)
+        mask = (torch.empty(x2.shape[0] * C // 8, dtype=torch.uint8, device=dev)
+                if any(ctx.needs_input_grad) and BN_RELU_MASK else None)
+
+        def state(mod, t2, w, b):
+            st = dict(ws=_bn_workspace(mod, C, dev, C_), gamma=flat.master_storage(w)[:C],
+                      beta=flat.master_storage(b)[:C])
+            pre = mod.__dict__.pop("_ldnn_pre", None)
+            if pre is not None and pre[0] == t2.data_ptr():
+                # statistics already accumulated + finalized by the producing conv's epilogue
+                st.update(rm=None, rv=None, mom=0.0, nb=None, mean=pre[1], invstd=pre[2], ready=True)
+            else:
+                rm, rv, mom, nbt = _bn_train_state(mod, dev)
+                st.update(rm=rm, rv=rv, mom=mom or 0.0, nb=nbt, mean=torch.empty(C, dtype=torch.float32, device=dev),
+                          invstd=torch.empty(C, dtype=torch.float32, device=dev), ready=False)
+            return st
+
+        sa, sb = state(mod_a, x2, wa, ba), state(mod_b, r2, wb, bb)
+        C_.bn_dual_fwd(x2, r2, y.view(-1, C), mask,
+                       sa["gamma"], sa["beta"], sa["rm"], sa["rv"], sa["mean"], sa["invstd"], sa["ws"], mod_a.eps,
+                       sa["mom"], sa["nb"], sa["ready"],
+                       sb["gamma"], sb["beta"], sb["rm"], sb["rv"], sb["mean"], sb["invstd"], sb["ws"], mod_b.eps,
+                       sb["mom"], sb["nb"], sb["ready"])
+        ctx.mask = mask
+        ctx.save_for_backward(x2, r2, y.view(-1, C) if mask is None else x2.new_empty(0), sa["mean"], sa["invstd"],
+                              sb["mean"], sb["invstd"])
+        ctx.meta = (flat, (wa, ba, sa["ws"]), (wb, bb, sb["ws"]), (N, C, H, W), x.dtype, r.dtype)
+        ctx.set_materialize_grads(False)
+        return nchw_view(y, C), nchw_view(y, C)
+
+    @staticmethod
+    def backward(ctx, gy, gy_twin):
+        C_ = _ext.C()
+        x2, r2, y2, mean_a, inv_a, mean_b, inv_b = ctx.saved_tensors
+        flat, (wa, ba, ws_a), (wb, bb, ws_b), (N, C, H, W), x_dtype, r_dtype = ctx.meta
+        if gy is None:
+            gy, gy_twin = gy_twin, None
+        if gy is None:
+            return (None,) * 9
+
+        def nhwc2(t):
+            return as_nhwc(t if t.dtype == torch.bfloat16 else t.to(torch.bfloat16), C,
+                           zero_pad=False).contiguous().view(-1, C)
+
+        g2 = nhwc2(gy)
+        gt = nhwc2(gy_twin) if gy_twin is not None else None
+        dx = torch.empty(N, H, W, C, dtype=torch.bfloat16, device=x2.device)
+        dr = torch.empty_like(dx)
+
+        def grads(w, b):
+            dg, db = flat.grad_storage(w)[:C], flat.grad_storage(b)[:C]
+            fresh = [(dg, flat.grad_beta(w) == 0.0), (db, flat.grad_beta(b) == 0.0)]
+            assign = all(f for _, f in fresh)
+            if not assign:   # mixed (only if a caller accumulated one of them): clear the fresh ones
+                for t, f in fresh:
+                    if f:
+                        t.zero_()
+            return flat.master_storage(w)[:C], dg, db, assign
+
+        ga, dga, dba, asa = grads(wa, ba)
+        gb, dgb, dbb, asb = grads(wb, bb)
+        C_.bn_dual_bwd(x2, r2, y2 if ctx.mask is None else x2, ctx.mask, g2, gt, dx.view(-1, C), dr.view(-1, C),
+                       ga, mean_a, inv_a, ws_a, dga, dba, asa, gb, mean_b, inv_b, ws_b, dgb, dbb, asb)
+        flat.notify(wa, ba)
+        flat.notify(wb, bb)
+        dxv, drv = nchw_view(dx, C), nchw_view(dr, C)
+        if x_dtype != torch.bfloat16:
+            dxv = dxv.to(x_dtype)
+        if r_dtype != torch.bfloat16:
+            drv = drv.to(r_dtype)
+        return dxv, drv, None, None, None, None, None, None, None
+
+
+# y = relu(bn_a(x) + bn_b(r)) in one pass (LDNN_BN_DUAL=0: bn_b's apply + bn_a's residual pass)
+BN_DUAL_FUSED = __import__("os").environ.get("LDNN_BN_DUAL", "1") != "0"
+
+
+def batch_norm_dual_act(x, mod_a, r, mod_b):
+    """relu(mod_a(x) + mod_b(r)): the tail of a residual block whose shortcut is conv + BN."""
+    fa, fb = getattr(mod_a, "_ldnn_flat", None), getattr(mod_b, "_ldnn_flat", None)
+    ok = (BN_DUAL_FUSED and _ext.use_native(x) and fa is not None and fa is fb and mod_a.training
+          and mod_b.training and mod_a.affine and mod_b.affine and x.dim() == 4 and x.shape == r.shape
+          and x.shape[1] % 8 == 0)
+    if ok:
+        return _with_twin(*_BatchNormDualNative.apply(x, r, mod_a.weight, mod_a.bias, mod_b.weight, mod_b.bias,
+                                                      mod_a, mod_b, fa))
+    return mod_a.act(x, residual=mod_b(r), relu=True)
+
+
 # BatchNorm + ReLU keeps a bit mask of the output for its backward (measured A/B in
 # profiles/, LDNN_BN_RELU_MASK=0 reads the bf16 output instead)
 BN_RELU_MASK = __import__("os").environ.get("LDNN_BN_RELU_MASK", "1") != "0"
