@@ -41,6 +41,8 @@
 //                  fp32 atomics into the (pre-cleared) gradient.
 #include <algorithm>
 
+#include <cstdlib>
+
 #include "ldnn_common.h"
 #include "ldnn_gemm_tile.h"
 #include "ldnn_kernels.h"
@@ -780,7 +782,12 @@ hipError_t head_bwd(const HeadParams& p, hipStream_t s) {
       p.ldw_rows > 16 || p.nrows_w > 16 || (p.dgrad_epi != EPI_NONE && p.dgrad_epi != EPI_DRELU))
     return hipErrorInvalidValue;
   const int gx = p.K / 64;
-  int gy = std::max(1, std::min(64, 768 / gx));  // ~3 workgroups per CU (the register-bound occupancy)
+  // ~3 workgroups per CU (the register-bound occupancy); A/B knob LDNN_HEAD_BWD_WGS (total workgroups)
+  static const int target = [] {
+    const char* e = std::getenv("LDNN_HEAD_BWD_WGS");
+    return e ? std::max(64, std::atoi(e)) : 768;
+  }();
+  int gy = std::max(1, std::min(256, target / gx));
   int rpw = (p.B + gy - 1) / gy;
   rpw = (rpw + 63) & ~63;
   gy = (p.B + rpw - 1) / rpw;

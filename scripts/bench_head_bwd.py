@@ -40,8 +40,9 @@ def main():
     t_f = timeit(lambda: C.head_bwd(h, W, dl, dh, dW, dbias, C.EPI_DRELU, db))
     t_s = timeit(lambda: C.head_dgrad_stream(h, W, dl, dh, dbias, C.EPI_DRELU))
     t_w = timeit(lambda: C.head_wgrad(dl, h, dW, db, 4))
+    t_c = timeit(lambda: dh.copy_(h))   # the same bytes moved by a plain copy (read h, write dh)
     print(json.dumps({"B": B, "K": K, "head_bwd_us": round(t_f, 2), "head_dgrad_stream_us": round(t_s, 2),
-                      "head_wgrad_us": round(t_w, 2), "gbps_fused": round(2 * B * K * 2 / t_f / 1e3, 1)}))
+                      "head_wgrad_us": round(t_w, 2), "copy_us": round(t_c, 2), "gbps_fused": round(2 * B * K * 2 / t_f / 1e3, 1)}))
 
 
 if __name__ == "__main__":
