@@ -33,17 +33,20 @@ def _run_rank(comm, El=2, Eg=2, fixed_ratio=None, topology="allreduce", by="grad
         tr = DeviceLoader(trainset, ti, 32, "cpu")
     crit = CrossEntropyLoss()
     opt = Adam(model.parameters(), lr=1e-3)
-    sch = StepLR(opt, step_size=25)
     if slow_rank is not None and comm.rank == slow_rank:
         orig = opt.step
 
-        def slow_step(*a, **k):
+        def slow_step(self, *a, **k):
             import time
 
             time.sleep(0.05)
             return orig(*a, **k)
 
-        opt.step = slow_step
+        import types
+
+        # a bound method, set before the scheduler wraps step (no scheduler-order warning)
+        opt.step = types.MethodType(slow_step, opt)
+    sch = StepLR(opt, step_size=25)
     H = train_global(model, tr, va, trainset, valset, ti, vi, crit, opt, sch, "cpu", comm.rank, comm.world_size, El,
                      Eg, timelimit, 32, 0.5, 0.5, 0.5, agg, by, comm=comm, topology=topology, fixed_classes=fixed,
                      fixed_ratio=fixed_ratio, sync_every=sync_every, progress=False, verbose=False,
