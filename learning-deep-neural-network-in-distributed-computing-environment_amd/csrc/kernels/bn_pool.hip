@@ -811,6 +811,40 @@ __global__ void gap_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict_
   }
 }
 
+// Split-HW global average pool: one block per (image, L-lane channel chunk); the
+// block's 256 threads split the H*W positions over G = 256 / L row groups (each
+// group reads L x 16 B contiguous) and the partial sums meet in LDS.  The one-
+// thread-per-channel-octet kernel above walks all H*W positions serially: with
+// ResNet-18's 64 x 7 x 7 x 512 input that is 16 workgroups doing 49 dependent
+// loads each (16.8 us per step, profiles/r3s2/resnet18_b64_step_timeline.txt).
+__global__ __launch_bounds__(256) void gap_fwd_split_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                                            int HW, int C, int L) {
+  __shared__ float part[8][256];
+  const int cv = C / 8, chunks = cv / L;
+  const int n = blockIdx.x / chunks, ch = blockIdx.x - n * chunks;
+  const int l = threadIdx.x % L, g = threadIdx.x / L, G = blockDim.x / L;
+  const int c8 = ch * L + l;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const bf16_t* base = x + (size_t)n * HW * C + c8 * 8;
+  for (int k = g; k < HW; k += G) {
+    const u16x8 v = *reinterpret_cast<const u16x8*>(base + (size_t)k * C);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += bf2f(v[j]);
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) part[j][threadIdx.x] = acc[j];
+  __syncthreads();
+  if (g != 0) return;
+  u16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float t = 0.f;
+    for (int q = 0; q < G; ++q) t += part[j][q * L + l];
+    o[j] = f2bf(t / (float)HW);
+  }
+  reinterpret_cast<u16x8*>(y)[(size_t)n * cv + c8] = o;
+}
+
 __global__ void gap_bwd_kernel(const bf16_t* __restrict__ dy, bf16_t* __restrict__ dx, int N, int HW, int C) {
   const int cv = C / 8;
   const int64_t total = (int64_t)N * HW * cv;
@@ -1095,6 +1129,13 @@ hipError_t pool2d_bwd(const uint16_t* dy, const uint8_t* argmax, uint16_t* dx, i
 
 hipError_t global_avgpool_fwd(const uint16_t* x, uint16_t* y, int N, int HW, int C, hipStream_t s) {
   if (C % 8) return hipErrorInvalidValue;
+  const int cv = C / 8;
+  int L = 16;  // 16 lanes x 16 B = 256 contiguous bytes per row group
+  while (L > 1 && cv % L) L >>= 1;
+  if (HW >= 8 && (int64_t)N * (cv / L) <= INT32_MAX) {
+    gap_fwd_split_kernel<<<(unsigned)((int64_t)N * (cv / L)), 256, 0, s>>>(x, y, HW, C, L);
+    return hipGetLastError();
+  }
   gap_fwd_kernel<<<grid_for((int64_t)N * C / 8), kBlock, 0, s>>>(x, y, N, HW, C);
   return hipGetLastError();
 }

@@ -85,9 +85,11 @@ def test_pools(kind, k, st, pad, C):
     torch.testing.assert_close(xb.grad.float(), xf.grad, rtol=2e-2, atol=2e-2)
 
 
-def test_global_avgpool():
+@pytest.mark.parametrize("shape", [(4, 72, 7, 7), (64, 512, 7, 7), (8, 1024, 4, 4), (2, 64, 2, 2),
+                                   (3, 136, 14, 14), (5, 256, 3, 3)])
+def test_global_avgpool(shape):
     torch.manual_seed(3)
-    x = torch.randn(4, 72, 7, 7, device="cuda")
+    x = torch.randn(*shape, device="cuda")
     xb = _cl(x).requires_grad_(True)
     y = AdaptiveAvgPool2d(1)(xb)
     xf = xb.detach().float().requires_grad_(True)
