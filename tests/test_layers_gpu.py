@@ -39,7 +39,8 @@ def test_native_linear_autograd(act, fin, fout, batch):
     # weight grads: the kernel sums bf16-rounded output gradients; compare relative to the scale
     scale = ref.weight.grad.abs().max()
     assert ((lin.weight.grad - ref.weight.grad).abs().max() / scale).item() < 2e-2
-    torch.testing.assert_close(lin.bias.grad, ref.bias.grad, rtol=3e-2, atol=5e-2)
+    # column sums of bf16-rounded gradients: the rounding noise grows like sqrt(batch)
+    torch.testing.assert_close(lin.bias.grad, ref.bias.grad, rtol=3e-2, atol=5e-2 * max(1.0, (batch / 96) ** 0.5))
     torch.testing.assert_close(xb.grad.float(), xr.grad, rtol=3e-2, atol=3e-2)
     pad = flat.grad_storage(lin.weight)[fout:]
     assert pad.numel() == 0 or pad.abs().max().item() == 0.0
