@@ -47,8 +47,9 @@ def _padded_rows_view(g: torch.Tensor, npad: int, zero_pad_guaranteed: bool = Tr
 # Split-K with the in-launch combine for Linear forwards whose 128-tile grid is tiny
 # and whose K loop is long, e.g. ResNet-18's 64 x 512 -> 1000 classifier (8 tiles of
 # 8 K-steps each).  The workspace and the (self-resetting) arrival counters persist
-# per (device, M, N, split) so graph replays reuse them.  Opt-in (LDNN_FC_SPLITK=1)
-# until its step-time A/B has run on the GPU (numerics: tests/test_layers_gpu.py).
+# per (device, M, N, split) so graph replays reuse them.  Opt-in (LDNN_FC_SPLITK=1):
+# measured slower standalone (11.5 -> 12.0-15.2 us) and neutral in the ResNet-18 b64
+# step (profiles/r3s3/head_micro.jsonl); numerics: tests/test_layers_gpu.py.
 FC_SPLITK = __import__("os").environ.get("LDNN_FC_SPLITK", "0") != "0"
 _SPLITK_BUFS: dict = {}
 
