@@ -97,6 +97,7 @@ def fill_slots(eng, args, seed):
     for _ in range(3):
         for i in range(len(slots)):
             eng.step(slot=1 + i)
+    eng.reset_stats()   # the statistics then cover exactly the warmup + timed steps
     return slots
 
 

@@ -76,9 +76,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--grad_comm_dtype", choices=["fp32", "bf16"], default="fp32",
                    help="dtype of the per-step gradient all-reduce (bf16 halves the xGMI bytes)")
     p.add_argument("--oneshot_bytes", type=int, default=None,
-                   help="RCCL runs: SUM all-reduces of at most this many bytes use the one-shot IPC kernel that "
-                        "reads every peer's copy over its own xGMI link (parallel/ipc.py); default 4 MiB "
-                        "(env LDNN_ONESHOT_BYTES), 0 = off")
+                   help="RCCL runs on one node: SUM all-reduces of at most this many bytes use the one-shot IPC "
+                        "kernel that reads every peer's copy over its own xGMI link (parallel/ipc.py); opt-in, "
+                        "default 0 = off (env LDNN_ONESHOT_BYTES); 4194304 covers LeNet-5's whole gradient")
     p.add_argument("--augment", nargs="?", const="autoaugment", default="none",
                    choices=["none", "autoaugment", "flipcrop", "autoaugment+flipcrop"],
                    help="training-set augmentation in the native input kernel (augment.hip); bare --augment = "

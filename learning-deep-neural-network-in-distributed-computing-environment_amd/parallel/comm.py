@@ -57,23 +57,39 @@ class Comm:
 
     def check_schedule(self, where: str = "", device=None):
         """Cross-check every rank's collective schedule (op count + running hash of
-        op / shape / dtype) with one small all-gather; raise RankDivergenceError on
-        the first mismatch.  The training driver calls it once per global epoch and
-        every ``check_every`` steps of per-step synchronisation -- the class of bug
-        the reference's dead time-limit break would cause."""
+        op / shape / dtype) AND every rank's device-side error flag (one-shot IPC
+        timeout) with one small all-gather; raise on EVERY rank at the same point:
+        RankDivergenceError on the first schedule mismatch, RuntimeError if any rank
+        recorded a collective failure.  The error is usually set on the rank(s) that
+        timed out only, so a local check would leave the others waiting in the next
+        collective.  The training driver calls it once per global epoch and every
+        ``check_every`` steps of per-step synchronisation -- the class of bug the
+        reference's dead time-limit break would cause."""
         if self.world_size <= 1:
             return
-        self.check_errors()
         n, h = self.schedule_digest()
-        v = torch.tensor([n, int(h[:15], 16)], dtype=torch.int64,
+        err = self.local_error()
+        v = torch.tensor([n, int(h[:15], 16), 1 if err else 0], dtype=torch.int64,
                          device=device if device is not None else "cpu")
         got = [t.cpu() for t in self.all_gather(v)]
-        if any(not torch.equal(got[0], g) for g in got):
+        bad = [r for r, g in enumerate(got) if int(g[2]) != 0]
+        if bad:
+            raise RuntimeError(f"collective failure on rank(s) {bad}{' at ' + where if where else ''}"
+                               f"{': ' + err if err else ''}")
+        if any(not torch.equal(got[0][:2], g[:2]) for g in got):
             desc = ", ".join(f"rank {r}: {int(g[0])} ops #{int(g[1]):015x}" for r, g in enumerate(got))
             raise RankDivergenceError(f"collective schedules diverged{' at ' + where if where else ''}: {desc}")
 
+    def local_error(self) -> str | None:
+        """Description of a failure a device-side collective path recorded on THIS rank
+        (one-shot IPC timeout), else None.  Never raises, never communicates."""
+        return None
+
     def check_errors(self):
-        """Raise if a device-side collective path recorded a failure (one-shot IPC timeout)."""
+        """Raise (locally) if this rank's device-side collective path recorded a failure."""
+        err = self.local_error()
+        if err:
+            raise RuntimeError(err)
 
     # -- API (implemented by subclasses)
     def all_reduce(self, t: torch.Tensor, op: str = SUM, async_op: bool = False):
@@ -135,14 +151,19 @@ class TorchComm(Comm):
 
     def enable_oneshot(self, max_bytes: int, device=None, self_test: bool = True):
         """Route SUM all-reduces of at most ``max_bytes`` (fp32 / bf16 device tensors)
-        through the one-shot IPC path (parallel/ipc.py).  Collective: every rank calls it.
-        With ``self_test`` the path is verified against RCCL first and left off (on
-        every rank, with a warning) if it fails anywhere -- e.g. a node whose GPUs
-        cannot map each other's memory."""
+        through the one-shot IPC path (parallel/ipc.py).  Collective: every rank calls it
+        and every rank reaches the same decision (the path is on everywhere or nowhere:
+        a rank routing a bucket through IPC while a peer uses RCCL would hang).  With
+        ``self_test`` the path is verified against RCCL first and left off (on every
+        rank, with a warning) if it fails anywhere -- e.g. a node whose GPUs cannot map
+        each other's memory.  Only for groups inside one node (IPC handles do not cross
+        hosts): a multi-node world leaves it off without any setup."""
         from .ipc import OneShotAllReduce
 
+        if not single_node():
+            return None
         os_ = OneShotAllReduce(max_bytes, group=self.group, device=device)   # never raises; collective
-        ok = os_.self_test() if self_test else os_.connect_error is None
+        ok = os_.self_test() if self_test else os_._agree(os_.connect_error is None)
         if not ok:
             import warnings
 
@@ -154,9 +175,10 @@ class TorchComm(Comm):
 
     oneshot = None
 
-    def check_errors(self):
+    def local_error(self):
         if self.oneshot is not None:
-            self.oneshot.check()
+            return self.oneshot.error()
+        return None
 
     def all_reduce(self, t, op=SUM, async_op=False):
         self.record("all_reduce", t)
@@ -290,17 +312,30 @@ class FakeComm(Comm):
 ONESHOT_DEFAULT_BYTES = 4 << 20
 
 
+def single_node() -> bool:
+    """Every rank of the default world on this host (torchrun / mpirun local-size env)."""
+    world = os.environ.get("WORLD_SIZE") or os.environ.get("OMPI_COMM_WORLD_SIZE") or os.environ.get("PMI_SIZE")
+    local = (os.environ.get("LOCAL_WORLD_SIZE") or os.environ.get("OMPI_COMM_WORLD_LOCAL_SIZE")
+             or os.environ.get("MPI_LOCALNRANKS"))
+    if world is None or local is None:
+        return False
+    return int(local) == int(world)
+
+
 def default_comm(oneshot_bytes: int | None = None) -> Comm:
-    """TorchComm over the default group (LocalComm for a world of one).  With RCCL,
-    SUM all-reduces of at most ``oneshot_bytes`` (default 4 MiB, env
-    LDNN_ONESHOT_BYTES; 0 = off) use the one-shot IPC kernel that reads every peer's
-    copy over its own xGMI link (SURVEY §5 small-message path: metric vectors, small
-    gradient buckets such as LeNet-5's whole 0.25 MB gradient).  Collective: every
-    rank must pass the same value."""
+    """TorchComm over the default group (LocalComm for a world of one).  With RCCL on
+    one node, SUM all-reduces of at most ``oneshot_bytes`` use the one-shot IPC kernel
+    that reads every peer's copy over its own xGMI link (SURVEY §5 small-message path:
+    metric vectors, small gradient buckets such as LeNet-5's whole 0.25 MB gradient).
+    Opt-in (default 0 = off, env LDNN_ONESHOT_BYTES): its device-side barrier gives up
+    after a fixed wall-clock limit, so ranks skewed by more than that (a rank-0
+    checkpoint write, unequal validation shards) would fail the call where RCCL just
+    waits; lock-step loops (bench.py, per-step DP) turn it on.  Collective: every rank
+    must pass the same value."""
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
         c = TorchComm()
         if oneshot_bytes is None:
-            oneshot_bytes = int(os.environ.get("LDNN_ONESHOT_BYTES", str(ONESHOT_DEFAULT_BYTES)))
+            oneshot_bytes = int(os.environ.get("LDNN_ONESHOT_BYTES", "0"))
         if oneshot_bytes > 0 and c.backend == "nccl" and torch.cuda.is_available():
             c.enable_oneshot(oneshot_bytes)
         return c

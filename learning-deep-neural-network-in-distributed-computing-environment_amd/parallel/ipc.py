@@ -18,7 +18,9 @@ fp32 or bf16 tensors with numel % 8 == 0.  Anything else falls back to the
 process group's all-reduce.  Every wait in the kernel has a 5 s wall-clock limit;
 a timed-out call sets a sticky error word and leaves its tensor (and every later
 call's) unsummed: ``check()`` raises then, and ``Comm.check_schedule`` -- run every
-global epoch and every few hundred per-step-DP steps -- calls it.
+global epoch and every few hundred per-step-DP steps -- gathers every rank's flag and
+raises on all of them.  Because of that limit the path is opt-in for training
+(``default_comm``), on for lock-step loops such as bench.py.
 
 ``self_test()`` (run when the communicator is enabled) sums a rank-dependent
 vector through the kernel and compares with the process group's all-reduce; any
@@ -72,10 +74,16 @@ class OneShotAllReduce:
         """In-place sum over the group's ranks, ordered on the current stream."""
         self._c.all_reduce(t)
 
+    def error(self) -> str | None:
+        if self._c is not None and self._c.error():
+            return ("one-shot all-reduce: a peer rank never reached the barrier (5 s limit); the tensors of "
+                    "that call and of every later one-shot call were left unsummed")
+        return None
+
     def check(self) -> None:
-        if self._c.error():
-            raise RuntimeError("one-shot all-reduce: a peer rank never reached the barrier (5 s limit); the "
-                               "tensors of that call and of every later one-shot call were left unsummed")
+        err = self.error()
+        if err:
+            raise RuntimeError(err)
 
     def self_test(self) -> bool:
         """Collective: True on every rank iff the kernel summed correctly on every rank."""

@@ -1,0 +1,33 @@
+#!/bin/bash
+# One gpurun call = a chain of named steps, each under its own time limit, chained so that a
+# crash / abort / timeout ends the call (a plain test FAILURE, rc 1, lets later steps run).
+#   bash scripts/gpu_run.sh <outdir> suite smoke bench iso prof ...
+# Outputs land in gpurun_out/<outdir>/.
+cd "${GRAFT_REPO_ROOT:-.}"
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+O=gpurun_out/$1; shift
+mkdir -p "$O"
+T="timeout -k 10"
+PYT="python -u -m pytest -v --timeout 120 --timeout-method thread"
+fatal() { [ "$1" -ne 0 ] && [ "$1" -ne 1 ]; }
+for step in "$@"; do
+  case $step in
+    suite) $T 900 $PYT tests -m gpu > $O/suite.txt 2>&1 ;;
+    suitex) $T 900 $PYT -x tests -m gpu > $O/suite.txt 2>&1 ;;
+    tests:*) $T 600 $PYT -m gpu ${step#tests:} > $O/tests_$(basename ${step#tests:} .py).txt 2>&1 ;;
+    smoke) $T 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 ;;
+    bench) $T 600 python -u bench.py > $O/bench.json 2> $O/bench.err ;;
+    iso) $T 300 python -u scripts/debug/stem_isolation.py > $O/stem_isolation.jsonl 2>&1 ;;
+    cnn:*) a=${step#cnn:}; $T 300 python -u scripts/bench_cnn.py --model ${a%%@*} --batch ${a##*@} --graph --no-stock \
+             >> $O/cnn.jsonl 2>> $O/cnn.err ;;
+    prof:*) a=${step#prof:}; $T 400 rocprofv3 --kernel-trace --stats -d $O/prof_$a -o run -- \
+             python -u scripts/bench_cnn.py --model ${a%%@*} --batch ${a##*@} --graph --no-stock --steps 20 --warmup 5 \
+             > $O/prof_$a.txt 2>&1 ;;
+    profmlp) $T 400 rocprofv3 --kernel-trace --stats -d $O/prof_mlp -o run -- python -u bench.py --steps 20 --warmup 5 \
+             > $O/prof_mlp.txt 2>&1 ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+  rc=$?
+  echo "step $step rc=$rc" | tee -a $O/steps.txt
+  if fatal $rc; then echo "fatal rc=$rc at $step: stopping"; exit $rc; fi
+done

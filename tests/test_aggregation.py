@@ -117,3 +117,32 @@ def test_reference_named_functions():
     torch.testing.assert_close(out[0][0], 0.8 * xs[0] + 0.2 * xs[1])
     # N=2: the 2-hop neighbour is the rank itself
     torch.testing.assert_close(out[0][1], (xs[0] + xs[1] + xs[0]) / 3)
+
+
+def test_check_schedule_raises_on_every_rank_when_one_rank_reports_a_collective_error():
+    """a one-shot IPC timeout is usually recorded on the late rank only.
+    check_schedule gathers every rank's error flag with the schedule digest, so EVERY
+    rank raises the same RuntimeError at the same point (none is left waiting in the
+    next collective until the process-group timeout)."""
+    from ldnn.parallel.comm import FakeComm, RankDivergenceError
+
+    class _ErrComm(FakeComm):
+        def local_error(self):
+            return "one-shot all-reduce timed out" if self.rank == 1 else None
+
+    world = FakeWorld(3, timeout=10)
+
+    def body(c):
+        c.__class__ = _ErrComm
+        c.all_reduce(torch.ones(4))
+        try:
+            c.check_schedule("step 7")
+        except RankDivergenceError:
+            return "divergence"
+        except RuntimeError as e:
+            return str(e)
+        return "ok"
+
+    got = world.run(body)
+    assert all(g.startswith("collective failure on rank(s) [1] at step 7") for g in got), got
+    assert "timed out" in got[1]

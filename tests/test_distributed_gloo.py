@@ -266,6 +266,7 @@ def test_per_step_weighted_allreduce_three_ranks():
 
 def _oneshot_setup_worker(rank, world, port, q):
     _init(rank, world, port, timeout=30)
+    os.environ.update(WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world))   # one node: the path is eligible
     import ldnn  # noqa: F401
     from ldnn.parallel import ipc
     from ldnn.parallel.comm import TorchComm
