@@ -30,10 +30,12 @@ over ranks).  Besides the headline it reports, per rank and maxed over ranks:
   per_gpu_local_ms     the same engine's comm-free step (world 1, no collectives)
   scaling_efficiency   per_gpu_local_ms / ms_per_step  (1.0 at N = 1)
   comm_us              standalone per-bucket reduce-scatter / all-gather times (N > 1)
-  configs              BASELINE configs #4/#5 through the same DP path at this N:
-                       LeNet-5 28x28 b256 and ResNet-18 224x224 b64 / b256 per GPU, each
-                       a graph-replayed step (GraphedDPStep: bucket all-reduces issued
-                       between the links of the backward graph chain) with its own
+  configs              BASELINE configs #4/#5 and the reference's own workload at this N:
+                       LeNet-5 28x28 b256, ResNet-18 224x224 b64 / b256 (SGD momentum) and
+                       EnhancedCNNModel 32x32 b64 with Adam lr 1e-3 per GPU, each a
+                       graph-replayed step (N > 1: GraphedDPStep over the sharded DP --
+                       bucket reduce-scatters issued between the links of the backward
+                       graph chain, sharded optimizer, bf16 weight all-gathers) with its own
                        comm-free local time and scaling efficiency (--no-configs skips)
 `--compare-stock` also times a stock PyTorch-ROCm eager implementation
 (nn.Linear + DDP + torch.optim.SGD) of the headline config.
@@ -195,19 +197,24 @@ def comm_micro(ctx, eng, iters: int = 10) -> dict:
     return out
 
 
-CNN_CONFIGS = (("lenet5", 256, 50), ("resnet18", 64, 20), ("resnet18", 256, 8))
+# (model, per-GPU batch, timed steps, optimizer): BASELINE configs #4 / #5 and the
+# reference's own workload (EnhancedCNNModel, batch 64, Adam lr 1e-3: BAR/main.py:52-54)
+CNN_CONFIGS = (("lenet5", 256, 50, "sgd"), ("resnet18", 64, 20, "sgd"), ("resnet18", 256, 8, "sgd"),
+               ("enhanced_cnn", 64, 30, "adam"))
 
 
-def run_cnn(ctx, name: str, batch: int, steps: int, warmup: int = 3) -> dict:
-    """One BASELINE CNN config (#4 LeNet-5 28x28, #5 ResNet-18 224x224) at this world
-    size: SGD momentum 0.9, bf16 native kernels, synthetic data, random-init weights;
-    per-step DP = GraphedDPStep (fp32 bucket all-reduce on RCCL between the links of
-    the backward graph chain), N = 1 = the single-process graphed step."""
+def run_cnn(ctx, name: str, batch: int, steps: int, optimizer: str = "sgd", warmup: int = 3) -> dict:
+    """One CNN config at this world size: bf16 native kernels, synthetic data,
+    random-init weights; SGD momentum 0.9 (lr 0.01) or Adam (lr 1e-3).  N = 1: the
+    single-process graphed step.  N > 1: GraphedDPStep over DataParallel(shard_optimizer=
+    True) -- each gradient bucket's fp32 RCCL reduce-scatter issued between the links of
+    the backward graph chain, the fused optimizer on this rank's 1/N shard, the bf16
+    weights all-gathered in place -- with the one-shot IPC path for buckets <= 4 MiB."""
     import ldnn
     from ldnn.data.datasets import SHAPES
     from ldnn.models import CrossEntropyLoss, build_model, dataset_for, xavier_init as xinit
-    from ldnn.optim import SGD
-    from ldnn.parallel.comm import TorchComm
+    from ldnn.optim import SGD, Adam
+    from ldnn.parallel.comm import ONESHOT_DEFAULT_BYTES, default_comm
     from ldnn.parallel.ddp import DataParallel
     from ldnn.train.graphed import GraphedDPStep, GraphedStep
 
@@ -217,14 +224,16 @@ def run_cnn(ctx, name: str, batch: int, steps: int, warmup: int = 3) -> dict:
     xs = [torch.randn(batch, *shape, device=ctx.device, generator=g).bfloat16() for _ in range(2)]
     ys = [torch.randint(0, nc, (batch,), device=ctx.device, generator=g) for _ in range(2)]
     crit = CrossEntropyLoss()
+    comm = default_comm(ONESHOT_DEFAULT_BYTES) if ctx.world_size > 1 else None
 
     def make(dp_on: bool):
         torch.manual_seed(0)
         m = build_model(name)
         xinit(m)
         ldnn.prepare(m, ctx.device)
-        opt = SGD(m.parameters(), lr=0.01, momentum=0.9)
-        dp = DataParallel(m, TorchComm(), bucket_cap_mb=32.0) if dp_on else None
+        dp = DataParallel(m, comm, bucket_cap_mb=32.0, shard_optimizer=True) if dp_on else None
+        # (the optimizer after the wrapper: sharding re-lays the flat buffers out)
+        opt = SGD(m.parameters(), lr=0.01, momentum=0.9) if optimizer == "sgd" else Adam(m.parameters(), lr=1e-3)
         net = dp if dp is not None else m
         opt.zero_grad()
         crit(net(xs[0]), ys[0]).backward()
@@ -232,6 +241,7 @@ def run_cnn(ctx, name: str, batch: int, steps: int, warmup: int = 3) -> dict:
             dp.finish_gradient_sync()
         opt.step()
         if dp is not None:
+            dp.wait_gathers()
             return GraphedDPStep(dp, crit, opt, xs[0], ys[0]), m
         return GraphedStep(m, crit, opt, xs[0], ys[0], warmup=0), m
 
@@ -239,10 +249,17 @@ def run_cnn(ctx, name: str, batch: int, steps: int, warmup: int = 3) -> dict:
     el = timed(ctx, lambda i: gs(xs[i % 2], ys[i % 2]), steps, warmup)
     ms = el / steps * 1e3
     rec = {"model": name, "per_gpu_batch": batch, "global_batch": batch * ctx.world_size, "steps": steps,
+           "optimizer": "sgd momentum 0.9 lr 0.01" if optimizer == "sgd" else "adam lr 1e-3",
            "ms_per_step": round(ms, 4), "samples_per_s": round(batch * ctx.world_size / el * steps, 1),
            "n_params": sum(p.numel() for p in m.parameters())}
     if ctx.world_size > 1:
-        rec["buckets"] = len(gs.bk.buckets)
+        bk = gs.bk
+        rec["grad_sync"] = ("fp32 reduce-scatter per bucket (between backward graph links) + sharded "
+                            f"{optimizer} + bf16 weight all-gather; 1-D params all-reduced")
+        rec["comm_dtype"] = "fp32 gradients / bf16 weights"
+        rec["oneshot_ipc"] = bool(getattr(comm, "oneshot", None) is not None)
+        rec["buckets"] = len(bk.buckets)
+        rec["sharded_buckets"] = sum(1 for b in bk.buckets if b["sharded"])
         rec["graph_segments"] = gs.n_segments
         del gs
         gl, _ = make(False)
@@ -400,7 +417,8 @@ def main():
     rec["rccl_ranks"] = n if ctx.backend == "nccl" else 0
     rec.update(extra)
     if not args.no_configs:
-        rec["configs"] = {f"{name}_b{b}": run_cnn(ctx, name, b, st) for name, b, st in CNN_CONFIGS}
+        rec["configs"] = {f"{name}_b{b}" + ("_adam" if o == "adam" else ""): run_cnn(ctx, name, b, st, o)
+                          for name, b, st, o in CNN_CONFIGS}
     if args.compare_stock:
         el_s = run_stock(ctx, args)
         stock = args.batch * n * args.steps / el_s

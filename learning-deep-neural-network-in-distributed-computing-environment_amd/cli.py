@@ -75,6 +75,10 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--bucket_mb", type=float, default=32.0)
     p.add_argument("--grad_comm_dtype", choices=["fp32", "bf16"], default="fp32",
                    help="dtype of the per-step gradient all-reduce (bf16 halves the xGMI bytes)")
+    p.add_argument("--shard_optimizer", choices=["auto", "on", "off"], default="auto",
+                   help="per-step all-reduce DP of autograd models: reduce-scatter each gradient bucket, run the "
+                        "fused optimizer on this rank's 1/N shard, all-gather the bf16 weights (ZeRO-1 style, "
+                        "parallel/ddp.py); auto = on for GPU runs with --aggregation_type equal")
     p.add_argument("--oneshot_bytes", type=int, default=None,
                    help="RCCL runs on one node: SUM all-reduces of at most this many bytes use the one-shot IPC "
                         "kernel that reads every peer's copy over its own xGMI link (parallel/ipc.py); opt-in, "
@@ -188,9 +192,17 @@ def main(argv=None):
         D.broadcast_module(model)
         flat.refresh_shadow()
     elif args.sync_every == "step" and args.topology == "allreduce" and world > 1:
+        weighted = args.aggregation_type == "weighted"
+        if args.shard_optimizer == "on" and weighted:
+            raise SystemExit("--shard_optimizer on needs --aggregation_type equal (the weighted mix gives every "
+                             "rank its own update)")
+        shard = not weighted and (args.shard_optimizer == "on" or (args.shard_optimizer == "auto"
+                                                                    and dev.type == "cuda"))
         dp = DataParallel(model, comm, bucket_cap_mb=args.bucket_mb,
-                          local_weight=args.local_weight if args.aggregation_type == "weighted" else None,
-                          comm_dtype=torch.bfloat16 if args.grad_comm_dtype == "bf16" else None)
+                          local_weight=args.local_weight if weighted else None,
+                          comm_dtype=torch.bfloat16 if args.grad_comm_dtype == "bf16" else None,
+                          shard_optimizer=shard)
+        flat = dp.flat   # (sharding re-lays the flat buffers out)
     else:  # reference A6: broadcast every state_dict entry from rank 0
         D.broadcast_module(model)
         flat.refresh_shadow()

@@ -171,7 +171,11 @@ def estimate_epoch_duration(trainloader, world_size, model, device, num_batches:
     device is synchronised so GPU time is actually measured."""
     from ..parallel.comm import default_comm
 
+    from ..parallel.ddp import DataParallel
+
     comm = comm or default_comm()
+    if isinstance(model, DataParallel):   # time the replica's own step: no gradient collectives
+        model = model.module
     dev = torch.device(device)
     bn_state = {k: v.clone() for k, v in model.state_dict().items() if "running" in k or "num_batches" in k}
     was_training = model.training

@@ -112,6 +112,23 @@ class _FlatOptimizer(torch.optim.Optimizer):
     def _update_range(self, f, group, ctx, lo, hi):
         raise NotImplementedError
 
+    def _sharded_step(self, f, group) -> bool:
+        """DataParallel(shard_optimizer=True) owns ``f``: update only this rank's flat
+        ranges (its shard of every reduce-scattered bucket + the replicated tail), then
+        let the data-parallel wrapper start the weight all-gathers.  False otherwise."""
+        sh = getattr(f, "shard_sync", None)
+        if sh is None or len(self.param_groups) != 1:
+            return False
+        f.finalize_grads()
+        ctx = self._begin_ranges(f, group)
+        for lo, hi in sh.update_ranges():
+            if hi > lo:
+                self._update_range(f, group, ctx, lo, hi)
+        st = self._ls()
+        st["step"] = st.get("step", 0) + 1
+        sh.after_update()
+        return True
+
     def zero_grad(self, set_to_none: bool = True):
         for group in self.param_groups:
             f = self._flat_for_group(group)
@@ -141,6 +158,8 @@ class SGD(_FlatOptimizer):
         for group in self.param_groups:
             lr, mu, damp, wd, nest = (group[k] for k in ("lr", "momentum", "dampening", "weight_decay", "nesterov"))
             f = self._flat_for_group(group)
+            if f is not None and self._sharded_step(f, group):
+                continue
             if f is not None:
                 f.finalize_grads()
                 st = self._ls()
@@ -170,11 +189,19 @@ class SGD(_FlatOptimizer):
 
     def _begin_ranges(self, f, group):
         mu = group["momentum"]
-        return dict(hp=self._hp(f, group["lr"]), first=self._ls().get("step", 0) == 0,
+        hp = self._hp(f, group["lr"]) if _ext.use_native(f.master) else None
+        return dict(hp=hp, first=self._ls().get("step", 0) == 0,
                     mom=self._buf("momentum", f.master) if mu != 0 else f.master)
 
     def _update_range(self, f, group, ctx, lo, hi):
         sh = f.shadow[lo:hi] if f.shadow is not None else None
+        if not _ext.use_native(f.master):
+            mu = group["momentum"]
+            self._sgd_torch(f.master[lo:hi], f.grad[lo:hi] * f.grad_scale, ctx["mom"][lo:hi] if mu != 0 else None,
+                            group["lr"], mu, group["dampening"], group["weight_decay"], group["nesterov"], ctx["first"])
+            if sh is not None:
+                sh.copy_(f.master[lo:hi])
+            return
         _ext.C().sgd_step(f.master[lo:hi], f.grad[lo:hi], ctx["mom"][lo:hi], sh, ctx["hp"], f.grad_scale,
                           group["momentum"], group["dampening"], group["weight_decay"], group["nesterov"],
                           ctx["first"])
@@ -205,6 +232,8 @@ class Adam(_FlatOptimizer):
         for group in self.param_groups:
             lr, (b1, b2), eps, wd = group["lr"], group["betas"], group["eps"], group["weight_decay"]
             f = self._flat_for_group(group)
+            if f is not None and self._sharded_step(f, group):
+                continue
             if f is not None:
                 f.finalize_grads()
                 st = self._ls()
@@ -237,13 +266,22 @@ class Adam(_FlatOptimizer):
         return loss
 
     def _begin_ranges(self, f, group):
-        hp = self._hp(f, group["lr"])
-        _ext.C().bump_step(hp)   # once per step, before any range reads the step count
-        return dict(hp=hp, m=self._buf("exp_avg", f.master), v=self._buf("exp_avg_sq", f.master))
+        hp = None
+        if _ext.use_native(f.master):
+            hp = self._hp(f, group["lr"])
+            _ext.C().bump_step(hp)   # once per step, before any range reads the step count
+        return dict(hp=hp, m=self._buf("exp_avg", f.master), v=self._buf("exp_avg_sq", f.master),
+                    t=self._ls().get("step", 0) + 1)
 
     def _update_range(self, f, group, ctx, lo, hi):
         b1, b2 = group["betas"]
         sh = f.shadow[lo:hi] if f.shadow is not None else None
+        if not _ext.use_native(f.master):
+            self._adam_torch(f.master[lo:hi], f.grad[lo:hi] * f.grad_scale, ctx["m"][lo:hi], ctx["v"][lo:hi],
+                             ctx["t"], group["lr"], b1, b2, group["eps"], group["weight_decay"])
+            if sh is not None:
+                sh.copy_(f.master[lo:hi])
+            return
         _ext.C().adam_step(f.master[lo:hi], f.grad[lo:hi], ctx["m"][lo:hi], ctx["v"][lo:hi], sh, ctx["hp"],
                            f.grad_scale, b1, b2, group["eps"], group["weight_decay"], self.decoupled)
 

@@ -108,6 +108,16 @@ class Comm:
         """Grouped point-to-point: post every send and receive, wait for all."""
         raise NotImplementedError
 
+    def reduce_scatter(self, out: torch.Tensor, inp: torch.Tensor, async_op: bool = False):
+        """SUM-reduce ``inp`` (world_size * out.numel() elements) over the ranks; rank r
+        receives slice r into ``out``.  ``inp`` may be clobbered."""
+        raise NotImplementedError
+
+    def all_gather_into(self, out: torch.Tensor, inp: torch.Tensor, async_op: bool = False):
+        """``out`` (world_size * inp.numel() elements) <- every rank's ``inp``, in rank order.
+        ``inp`` may be ``out``'s own slot (in place)."""
+        raise NotImplementedError
+
 
 class _Done:
     def wait(self):
@@ -135,6 +145,17 @@ class LocalComm(Comm):
         self.record("sendrecv")
         for (rt, src), (st, dst) in zip(recvs, sends):
             rt.copy_(st)
+
+    def reduce_scatter(self, out, inp, async_op=False):
+        self.record("reduce_scatter", inp)
+        out.copy_(inp)
+        return _Done() if async_op else None
+
+    def all_gather_into(self, out, inp, async_op=False):
+        self.record("all_gather_into", out)
+        if out.data_ptr() != inp.data_ptr():
+            out.copy_(inp)
+        return _Done() if async_op else None
 
 
 class TorchComm(Comm):
@@ -220,6 +241,24 @@ class TorchComm(Comm):
         if stage:
             for (t, _), (c, _) in zip(dev_recvs, recvs):
                 t.copy_(c)
+
+    def reduce_scatter(self, out, inp, async_op=False):
+        self.record("reduce_scatter", inp)
+        if self.backend == "nccl":
+            return dist.reduce_scatter_tensor(out, inp, group=self.group, async_op=async_op)
+        # gloo has no reduce-scatter of device tensors: all-reduce, keep this rank's slice
+        dist.all_reduce(inp, group=self.group)
+        n = out.numel()
+        out.copy_(inp[self.rank * n: (self.rank + 1) * n])
+        return _Done() if async_op else None
+
+    def all_gather_into(self, out, inp, async_op=False):
+        self.record("all_gather_into", out)
+        if self.backend == "nccl":   # in place when inp is out's slot r (the RCCL convention)
+            return dist.all_gather_into_tensor(out, inp, group=self.group, async_op=async_op)
+        src = inp.clone()
+        dist.all_gather(list(out.chunk(self.world_size)), src, group=self.group)
+        return _Done() if async_op else None
 
 
 # ------------------------------------------------------------------ fake world
@@ -307,6 +346,19 @@ class FakeComm(Comm):
             merged.update(m)
         for rt, src in recvs:
             rt.copy_(merged[(src, self.rank)])
+
+    def reduce_scatter(self, out, inp, async_op=False):
+        self.record("reduce_scatter", inp)
+        tot = torch.stack(self._exchange(inp.detach().clone())).sum(0)
+        n = out.numel()
+        out.copy_(tot[self.rank * n: (self.rank + 1) * n].to(out.dtype))
+        return _Done() if async_op else None
+
+    def all_gather_into(self, out, inp, async_op=False):
+        self.record("all_gather_into", out)
+        vals = self._exchange(inp.detach().clone())
+        out.copy_(torch.cat(vals).to(out.dtype))
+        return _Done() if async_op else None
 
 
 ONESHOT_DEFAULT_BYTES = 4 << 20

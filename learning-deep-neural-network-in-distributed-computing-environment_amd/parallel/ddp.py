@@ -22,6 +22,17 @@ BAR/trainer.py:141-150 vs :205,210).  This is the real thing, MI355X-style:
   bucket is cast into a persistent bf16 staging buffer on the compute stream,
   all-reduced in bf16, and widened back into the fp32 gradient after the wait.
   The optimizer still runs on fp32 master weights.
+* ``shard_optimizer=True`` (ZeRO-1 style, the static MLP engine's design carried
+  over to autograd models): each bucket is REDUCE-SCATTERED instead of
+  all-reduced, the fused optimizer updates only this rank's 1/N of it (master,
+  momentum / Adam moments and the bf16 shadow), and the updated bf16 weights are
+  ALL-GATHERED in place -- (N-1)/N of a bucket each way instead of twice that for
+  an all-reduce + full update, and 1/N of the optimizer's HBM traffic.  The
+  forward reads convolution / Linear weights from the gathered bf16 shadow but
+  BatchNorm affine parameters and biases from the fp32 master, so the 1-D
+  parameters form one small REPLICATED tail bucket (all-reduced, every rank
+  updates it whole).  Sharded buckets are laid out N x 64-element aligned (the
+  flat buffers are rebuilt once, before the optimizer exists).
 """
 from __future__ import annotations
 
@@ -42,6 +53,35 @@ def ensure_flat(module: nn.Module, device=None) -> FlatParams:
     return f
 
 
+def plan_groups(segs, bucket_cap_elems: int, last_bucket_cap_elems: int | None = None) -> list[list]:
+    """Cut flat segments (gradient-ready order) into bucket parameter groups of about
+    ``bucket_cap_elems``; the last group (the first layers' gradients, ready only when
+    the backward ends) is capped at ``last_bucket_cap_elems``."""
+    segs = list(segs)
+    tail = []
+    if last_bucket_cap_elems and len(segs) > 1:
+        last_cap = min(int(last_bucket_cap_elems), int(bucket_cap_elems))
+        n = 0
+        while len(segs) > 1 and n + segs[-1].storage_numel <= last_cap:
+            n += segs[-1].storage_numel
+            tail.insert(0, segs.pop())
+    groups, cur, size = [], [], 0
+    for seg in segs:
+        # close the group when the next tensor would overflow it -- unless it is still
+        # small (< cap / 4: e.g. a classifier + a BatchNorm in front of a 36 MB conv
+        # weight), which then rides along instead of costing a collective
+        if cur and size + seg.storage_numel > bucket_cap_elems and size >= bucket_cap_elems // 4:
+            groups.append(cur)
+            cur, size = [], 0
+        cur.append(seg.param)
+        size += seg.storage_numel
+    if cur:
+        groups.append(cur)
+    if tail:
+        groups.append([t.param for t in tail])
+    return groups
+
+
 class GradBucketer:
     """Flat gradient buckets, each all-reduced (SUM) once its last gradient is written.
 
@@ -55,92 +95,190 @@ class GradBucketer:
 
     def __init__(self, flat: FlatParams, comm: Comm, bucket_cap_elems: int = 8 << 20,
                  comm_dtype: torch.dtype | None = None, local_weight: float | None = None,
-                 last_bucket_cap_elems: int | None = 1 << 20):
+                 last_bucket_cap_elems: int | None = 1 << 20, groups: list | None = None):
+        """``groups`` (sharded mode, DataParallel(shard_optimizer=True)): the bucket plan as
+        lists of parameters -- every group but the last is reduce-scattered (its flat range
+        already N x 64 aligned), the last one (the 1-D parameters) is all-reduced."""
         self.flat, self.comm = flat, comm
         self.comm_dtype = None if comm_dtype in (None, torch.float32) else comm_dtype
         self.buckets: list[dict] = []
-        segs = list(flat.segments)
-        # The LAST bucket holds the first layers' gradients, ready only when the whole
-        # backward is done: nothing is left to hide its collective behind, so it is cut
-        # small (default 1 M elements = 4 MiB fp32, the one-shot IPC path's size) and the
-        # big buckets take everything that becomes ready earlier.
-        tail = []
-        if last_bucket_cap_elems and len(segs) > 1 and flat.numel > bucket_cap_elems:
-            last_cap = min(int(last_bucket_cap_elems), int(bucket_cap_elems))
-            n = 0
-            while len(segs) > 1 and n + segs[-1].storage_numel <= last_cap:
-                n += segs[-1].storage_numel
-                tail.insert(0, segs.pop())
-        cur = None
-        for seg in segs:
-            # close the bucket when the next tensor would overflow it -- unless the bucket
-            # is still small (< cap / 4: e.g. a classifier + a BatchNorm in front of a
-            # 36 MB conv weight), which then rides along instead of costing a collective
-            size = seg.offset + seg.storage_numel - (cur["begin"] if cur is not None else 0)
-            if cur is None or (size > bucket_cap_elems and cur["params"]
-                               and cur["end"] - cur["begin"] >= bucket_cap_elems // 4):
-                if cur is not None:
-                    self.buckets.append(cur)
-                cur = {"begin": seg.offset, "end": seg.offset, "params": []}
-            cur["end"] = seg.offset + seg.storage_numel
-            cur["params"].append(seg.param)
-        if cur is not None:
-            self.buckets.append(cur)
-        if tail:
-            self.buckets.append({"begin": tail[0].offset, "end": tail[-1].offset + tail[-1].storage_numel,
-                                 "params": [t.param for t in tail]})
-            self.buckets[-2]["end"] = tail[0].offset
-        if self.buckets:
-            self.buckets[-1]["end"] = flat.numel
+        N = comm.world_size
+        self.shard = groups is not None
+        if self.shard:
+            for gi, ps in enumerate(groups):
+                if not ps:
+                    continue
+                segs = [flat.seg(p) for p in ps]
+                b = segs[0].offset
+                e = flat.numel if gi == len(groups) - 1 else segs[-1].offset + segs[-1].storage_numel
+                sharded = gi < len(groups) - 1
+                if sharded:
+                    a = N * 64
+                    e = (e + a - 1) // a * a
+                self.buckets.append({"begin": b, "end": e, "params": list(ps), "sharded": sharded})
+            for x, y in zip(self.buckets, self.buckets[1:]):
+                assert x["end"] == y["begin"], "sharded bucket plan does not tile the flat buffer"
+        else:
+            self._plan(list(flat.segments), bucket_cap_elems, last_bucket_cap_elems)
         self.of_param = {}
         for i, b in enumerate(self.buckets):
+            b.setdefault("sharded", False)
             for p in b["params"]:
                 self.of_param[id(p)] = i
-        self._stage = ([torch.empty(b["end"] - b["begin"], dtype=self.comm_dtype, device=flat.grad.device)
+        self.rank = comm.rank
+        dev = flat.grad.device
+        self._stage = ([torch.zeros(b["end"] - b["begin"], dtype=self.comm_dtype, device=dev)
                         for b in self.buckets] if self.comm_dtype is not None else None)
-        N = comm.world_size
+        # sharded buckets: reduce-scatter output (comm dtype), this rank's flat range
+        self._gshard = [torch.zeros((b["end"] - b["begin"]) // N, dtype=self.comm_dtype or torch.float32, device=dev)
+                        if b["sharded"] else None for b in self.buckets]
         self.weighted = local_weight is not None and N > 1
         self._own = None
         if self.weighted:
             w = float(local_weight)
             other = (1.0 - w) / (N - 1)
             self._mix_ab = (w - other, other)
-            self._own = [torch.empty(b["end"] - b["begin"], dtype=torch.float32, device=flat.grad.device)
-                         for b in self.buckets]
+            self._own = [torch.empty(self._own_len(i), dtype=torch.float32, device=dev)
+                         for i in range(len(self.buckets))]
         self.works: list = []
         self._pending: list[int] = []
         self._launched: list[bool] = []
+        self._gathers: list = []
         self.active = False
+        self.master_whole = True
         flat.add_ready_hook(self._on_ready)
+        if self.shard:
+            flat.shard_sync = self
+
+    def _plan(self, segs, bucket_cap_elems, last_bucket_cap_elems):
+        # The LAST bucket holds the first layers' gradients, ready only when the whole
+        # backward is done: nothing is left to hide its collective behind, so it is cut
+        # small (default 1 M elements = 4 MiB fp32, the one-shot IPC path's size) and the
+        # big buckets take everything that becomes ready earlier.
+        flat = self.flat
+        for ps in plan_groups(segs, bucket_cap_elems, last_bucket_cap_elems if flat.numel > bucket_cap_elems else None):
+            sg = [flat.seg(p) for p in ps]
+            self.buckets.append({"begin": sg[0].offset, "end": sg[-1].offset + sg[-1].storage_numel, "params": ps})
+        for x, y in zip(self.buckets, self.buckets[1:]):
+            x["end"] = y["begin"]
+        if self.buckets:
+            self.buckets[-1]["end"] = flat.numel
+
+    # ---- sharded-bucket geometry
+    def shard_range(self, i) -> tuple[int, int]:
+        """[lo, hi) of the flat buffers this rank owns in sharded bucket i."""
+        b = self.buckets[i]
+        S = (b["end"] - b["begin"]) // self.comm.world_size
+        lo = b["begin"] + self.rank * S
+        return lo, lo + S
+
+    def _own_len(self, i):
+        b = self.buckets[i]
+        return (b["end"] - b["begin"]) // self.comm.world_size if b["sharded"] else b["end"] - b["begin"]
 
     def grad_view(self, i):
         b = self.buckets[i]
         return self.flat.grad[b["begin"]: b["end"]]
 
     def comm_buffer(self, i):
-        """The buffer bucket i's collective runs on (bf16 stage or the fp32 gradient)."""
+        """The buffer bucket i's collective reads (bf16 stage or the fp32 gradient)."""
         return self._stage[i] if self._stage is not None else self.grad_view(i)
 
     def pre_collective(self, i):
         """Stream-ordered work right before bucket i's collective: keep the own
-        gradient (weighted), cast into the bf16 stage (comm_dtype)."""
+        gradient (weighted; this rank's shard of it when sharded), cast into the bf16
+        stage (comm_dtype)."""
         g = self.grad_view(i)
         if self._own is not None:
-            self._own[i].copy_(g)
+            if self.buckets[i]["sharded"]:
+                lo, hi = self.shard_range(i)
+                self._own[i].copy_(self.flat.grad[lo:hi])
+            else:
+                self._own[i].copy_(g)
         if self._stage is not None:
             self._stage[i].copy_(g)
 
+    def collective(self, i):
+        """Issue bucket i's collective (async): reduce-scatter into this rank's shard
+        buffer for a sharded bucket, else an in-place SUM all-reduce."""
+        if self.buckets[i]["sharded"]:
+            return self.comm.reduce_scatter(self._gshard[i], self.comm_buffer(i), async_op=True)
+        return self.comm.all_reduce(self.comm_buffer(i), SUM, async_op=True)
+
     def post_collective(self, i):
-        """Stream-ordered work after bucket i's collective landed: widen the stage
-        back into the fp32 gradient, apply the weighted mix."""
-        g = self.grad_view(i)
-        if self._stage is not None:
-            g.copy_(self._stage[i])
+        """Stream-ordered work after bucket i's collective landed: widen the stage /
+        the reduce-scattered shard back into the fp32 gradient, apply the weighted mix."""
+        if self.buckets[i]["sharded"]:
+            lo, hi = self.shard_range(i)
+            g = self.flat.grad[lo:hi]
+            g.copy_(self._gshard[i])
+        else:
+            g = self.grad_view(i)
+            if self._stage is not None:
+                g.copy_(self._stage[i])
         if self._own is not None:
             from .aggregation import _mix
 
             a, b = self._mix_ab
             _mix(g, self._own[i], g, a=a, b=b)
+
+    # ---- sharded optimizer step (called by _FlatOptimizer.step through flat.shard_sync)
+    def update_ranges(self) -> list[tuple[int, int]]:
+        """Flat ranges this rank's optimizer updates: its shard of every sharded bucket
+        and the whole replicated tail."""
+        out = []
+        for i, b in enumerate(self.buckets):
+            out.append(self.shard_range(i) if b["sharded"] else (b["begin"], b["end"]))
+        return out
+
+    def after_update(self):
+        """The sharded update of this step is done: start the weight all-gathers (not
+        while a graph is being captured -- GraphedDPStep issues them after its replay)."""
+        self.master_whole = False
+        if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+            return
+        self.issue_gathers()
+
+    def gather_target(self) -> torch.Tensor:
+        """The buffer the forward reads weights from: the bf16 shadow (GPU), else the master."""
+        return self.flat.shadow if self.flat.shadow is not None else self.flat.master
+
+    def issue_gathers(self):
+        """All-gather every sharded bucket's updated weights, in place, in FORWARD order
+        (the last bucket -- the first layers -- first)."""
+        t = self.gather_target()
+        for i in reversed(range(len(self.buckets))):
+            b = self.buckets[i]
+            if b["sharded"]:
+                lo, hi = self.shard_range(i)
+                self._gathers.append(self.comm.all_gather_into(t[b["begin"]: b["end"]], t[lo:hi], async_op=True))
+
+    def wait_gathers(self):
+        """Order the current stream after the weight all-gathers (no host sync with RCCL)."""
+        for w in self._gathers:
+            if w is not None:
+                w.wait()
+        self._gathers = []
+
+    @torch.no_grad()
+    def gather_master(self, optimizer=None):
+        """Make the fp32 master (and ``optimizer``'s flat state: momentum / Adam moments)
+        whole on every rank after sharded steps -- before a checkpoint, weight averaging
+        or any reader of ``model.parameters()``.  Collective; a no-op until the next step."""
+        self.wait_gathers()
+        if not self.shard or self.master_whole:
+            return
+        bufs = [self.flat.master]
+        if optimizer is not None:
+            bufs += [v for k, v in optimizer._ls().items() if torch.is_tensor(v) and v.shape == self.flat.master.shape]
+        for i, b in enumerate(self.buckets):
+            if b["sharded"]:
+                lo, hi = self.shard_range(i)
+                for t in bufs:
+                    self.comm.all_gather_into(t[b["begin"]: b["end"]], t[lo:hi])
+        self.master_whole = True
+        if self.flat.shadow is not None:
+            self.flat.refresh_shadow()
 
     def prepare(self):
         self._pending = [len(b["params"]) for b in self.buckets]
@@ -153,7 +291,7 @@ class GradBucketer:
     def _launch(self, i):
         self._launched[i] = True
         self.pre_collective(i)
-        self.works.append((self.comm.all_reduce(self.comm_buffer(i), SUM, async_op=True), i))
+        self.works.append((self.collective(i), i))
 
     def _on_ready(self, p):
         if not self.active or id(p) in self._seen:
@@ -189,15 +327,30 @@ class DataParallel(nn.Module):
 
     ``local_weight`` = w turns the per-step all-reduce into the reference's
     weighted average (``--aggregation_type weighted``, BAR/communication.py:4-10);
-    None (default) is the equal average (BAR/communication.py:21-25)."""
+    None (default) is the equal average (BAR/communication.py:21-25).
+
+    ``shard_optimizer`` (world > 1, equal averaging): reduce-scatter + sharded fused
+    optimizer + bf16 weight all-gather (module docstring).  Build the optimizer AFTER this
+    wrapper: sharding re-lays the flat buffers out once.  ``optimizer.step()`` then
+    updates only this rank's shards and starts the all-gathers; the next forward
+    (or ``wait_gathers``) orders itself after them.  Call ``gather_master(opt)``
+    (collective) before reading ``model.parameters()`` / a checkpoint."""
 
     def __init__(self, module: nn.Module, comm: Comm | None = None, bucket_cap_mb: float = 32.0,
                  broadcast_init: bool = True, average: bool = True, comm_dtype: torch.dtype | None = None,
-                 local_weight: float | None = None):
+                 local_weight: float | None = None, shard_optimizer: bool = False):
         super().__init__()
         self.module = module
         self.comm = comm or default_comm()
         self.flat = ensure_flat(module)
+        cap = int(bucket_cap_mb * (1 << 20) / 4)
+        groups = None
+        if shard_optimizer and local_weight is not None:
+            # the weighted mix gives every rank its OWN gradient (replicas drift apart, as the
+            # reference's weighted averaging does): no rank can own a shard of the others' update
+            raise ValueError("shard_optimizer needs equal averaging (local_weight=None)")
+        if shard_optimizer and self.comm.world_size > 1:
+            self.flat, groups = _shard_layout(module, self.flat, self.comm.world_size, cap)
         if broadcast_init and self.comm.world_size > 1:
             with torch.no_grad():
                 self.comm.broadcast(self.flat.master, 0)
@@ -207,23 +360,60 @@ class DataParallel(nn.Module):
         # equal averaging folds 1/N into the fused optimizer; the weighted mix (and a
         # plain sum, average=False) leave the gradient at scale 1
         self.flat.grad_scale = (1.0 / self.comm.world_size) if (average and local_weight is None) else 1.0
-        self.bucketer = GradBucketer(self.flat, self.comm, int(bucket_cap_mb * (1 << 20) / 4), comm_dtype=comm_dtype,
-                                     local_weight=local_weight)
+        self.bucketer = GradBucketer(self.flat, self.comm, cap, comm_dtype=comm_dtype, local_weight=local_weight,
+                                     groups=groups)
+
+    @property
+    def sharded(self) -> bool:
+        return self.bucketer.shard
 
     def forward(self, *args, **kwargs):
+        self.bucketer.wait_gathers()   # the previous sharded step's weight all-gathers
         if self.training and torch.is_grad_enabled() and self.comm.world_size > 1:
             self.bucketer.prepare()
         return self.module(*args, **kwargs)
 
     def finish_gradient_sync(self):
-        """Wait for every bucket's all-reduce (call between backward and optimizer.step)."""
+        """Wait for every bucket's collective (call between backward and optimizer.step)."""
         if self.comm.world_size > 1:
             self.bucketer.finish()
 
+    def wait_gathers(self):
+        self.bucketer.wait_gathers()
+
+    def gather_master(self, optimizer=None):
+        """Collective: whole fp32 master (+ the optimizer's flat state) on every rank."""
+        self.bucketer.gather_master(optimizer)
+
     def state_dict(self, *a, **k):
+        if self.sharded and not self.bucketer.master_whole:
+            raise RuntimeError("DataParallel(shard_optimizer=True): call gather_master() on every rank "
+                               "before state_dict()")
         return self.module.state_dict(*a, **k)
 
     def load_state_dict(self, *a, **k):
         r = self.module.load_state_dict(*a, **k)
         self.flat.refresh_shadow()
         return r
+
+
+def _shard_layout(module: nn.Module, flat: FlatParams, world: int, cap: int):
+    """Re-lay ``module``'s flat buffers out for the sharded step: the >= 2-D weights in
+    gradient-ready order, cut into bucket groups whose flat ranges are padded to
+    world x 64 elements (every rank's shard 256-B aligned), then every 1-D parameter
+    (BatchNorm affine, biases: read from the fp32 master by the forward) as the
+    replicated tail.  Returns (new FlatParams, groups)."""
+    segs = list(flat.segments)
+    big = [s for s in segs if s.param.dim() >= 2]
+    small = [s.param for s in segs if s.param.dim() < 2]
+    groups = plan_groups(big, cap, 1 << 20 if sum(s.storage_numel for s in big) > cap else None)
+    align_after = {id(g[-1]): world * 64 for g in groups}
+    if not small:   # keep a (possibly empty-ranged) replicated tail group
+        small = []
+    order = [s.param for s in big] + small
+    new = FlatParams(module, flat.device, order=order, align_after=align_after)
+    module._ldnn_flat = new
+    # the old buffers are unreferenced now (every param / grad views the new ones)
+    flat.master = flat.grad = torch.empty(0, device=flat.device)
+    flat.shadow = None
+    return new, groups + [small]

@@ -152,6 +152,11 @@ class GraphedDPStep:
     mode "after" (host-staged backends such as gloo, or on request): one backward
     graph, then the bucket collectives from Python, then G_opt.
 
+    With ``DataParallel(shard_optimizer=True)`` a bucket's collective is a
+    reduce-scatter, G_opt widens + updates only this rank's shards (and the
+    replicated 1-D tail), and after G_opt the host issues the in-place bf16 weight
+    all-gathers in forward order; the next replay's stream waits for them first.
+
     1/N averaging is folded into the optimizer (flat.grad_scale); the weighted
     all-reduce's mix and the bf16 stage widen run in G_opt (GradBucketer
     post_collective).  Every replay issues its collectives through ``comm`` -- the
@@ -298,11 +303,10 @@ class GraphedDPStep:
             self._lrs = lrs
 
     def _collective(self, i):
-        buf = self.bk.comm_buffer(i)
         if self.comm_fn is not None:
-            w = self.comm_fn(i, buf)
+            w = self.comm_fn(i, self.bk.comm_buffer(i))
             return w if hasattr(w, "wait") else None
-        return self.comm.all_reduce(buf, self._SUM, async_op=True)
+        return self.bk.collective(i)   # reduce-scatter (sharded bucket) or all-reduce
 
     @property
     def n_segments(self) -> int:
@@ -316,6 +320,7 @@ class GraphedDPStep:
     def __call__(self, x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
         if x.shape != self.x.shape or y.shape != self.y.shape:
             return self._eager_step(x, y)
+        self.bk.wait_gathers()   # the previous sharded step's weight all-gathers (stream waits)
         self.x.copy_(x, non_blocking=True)
         self.y.copy_(y, non_blocking=True)
         self._sync_lr()
@@ -332,6 +337,11 @@ class GraphedDPStep:
             if w is not None:
                 w.wait()
         self.g_opt.replay()
+        if self.bk.shard:
+            self.bk.master_whole = False
+            if not self.device_collectives and self.comm_fn is None:
+                torch.cuda.current_stream().synchronize()   # a host-staged backend reads the shadow
+            self.bk.issue_gathers()   # updated bf16 weight shards, in forward order
         return self.loss
 
     def _eager_step(self, x, y):

@@ -129,9 +129,13 @@ def train_local_epoch(model, trainloader, criterion, optimizer, device, schedule
     except StopLocalTraining:
         if step_scheduler and scheduler is not None:
             scheduler.step()
+        if dp is not None:
+            dp.wait_gathers()
         raise
     if step_scheduler and scheduler is not None:
         scheduler.step()
+    if dp is not None:
+        dp.wait_gathers()   # sharded DP: the last step's weight all-gathers land before any reader
     gs = getattr(model, "_ldnn_graphed", None) if use_graph else None
     if gs is not None:
         gs.flush_stats(stats)
@@ -291,6 +295,8 @@ def train_global(model, trainloader, val_loader, trainset, valset, indices_train
                 print(f"Worker {rank}, Global Epoch {global_epoch + 1}, Validation Loss: {val_loss:.4f}, "
                       f"Validation Accuracy: {val_acc:.2f}%")
         cutoff.finish()
+        if dp is not None and getattr(dp, "sharded", False):
+            dp.gather_master(optimizer)   # sharded DP: whole master for aggregation / checkpoint / eval
 
         # ---- one metric exchange per global epoch (replaces C3-C6 per local epoch)
         lt = torch.tensor([float(max([len(b) for b in batch_losses] + [0]))], device=dev)

@@ -119,15 +119,18 @@ def test_rccl_world1_overlap_path(tmp_path):
         dist.destroy_process_group()
 
 
-def test_graphed_dp_two_ranks_gloo_equals_big_batch():
+@pytest.mark.parametrize("extra", [[], ["--shard"], ["--shard", "--optimizer", "adam"],
+                                   ["--shard", "--comm-dtype", "bf16"]])
+def test_graphed_dp_two_ranks_gloo_equals_big_batch(extra):
     """2 ranks (gloo, sharing the GPU) through train_local_epoch(graphs=True, dp=...)
-    end with the parameters of ONE graphed rank on the concatenated batches."""
+    end with the parameters of ONE graphed rank on the concatenated batches -- also
+    with the sharded step (reduce-scatter + sharded SGD / Adam + weight all-gather)."""
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
-           "--master-port", str(port), os.path.join(ROOT, "scripts", "check_graphed_dp.py")]
+           "--master-port", str(port), os.path.join(ROOT, "scripts", "check_graphed_dp.py")] + extra
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     assert "GRAPHED_DP_OK" in r.stdout, r.stdout[-3000:]
