@@ -132,10 +132,6 @@ def resolve_engine(args, model, dev, world: int) -> bool:
         why = f"--model {args.model} is not an MLP"
     elif dev.type != "cuda" or not _ext.use_native(torch.empty(0, device=dev)):
         why = "the static engine needs the native extension on a GPU"
-    elif args.sync_every == "step" and world > 1 and args.topology != "allreduce":
-        why = "per-step gossip (--topology ring/double_ring with --sync_every step) runs on the autograd path"
-    elif args.sync_every == "step" and world > 1 and args.aggregation_type != "equal":
-        why = "per-step weighted all-reduce runs on the autograd path"
     elif args.grad_comm_dtype != "fp32":
         why = "--grad_comm_dtype bf16 runs on the autograd path"
     if args.engine == "static" and why is not None:
@@ -172,10 +168,13 @@ def main(argv=None):
         from .train.engine_adapter import build_engine
 
         step_dp = args.sync_every == "step" and world > 1
+        hops = {"allreduce": 0, "ring": 1, "double_ring": 2}[args.topology]
+        lw = args.local_weight if args.aggregation_type == "weighted" else None
         net, optimizer = build_engine(model.to(dev), args.batch_size, args.optimizer, args.lr, dev,
                                       momentum=args.momentum, weight_decay=args.weight_decay,
                                       world_size=world if step_dp else 1, use_graphs=True,
-                                      bucket_cap_elems=int(args.bucket_mb * (1 << 20)) // 4)
+                                      bucket_cap_elems=int(args.bucket_mb * (1 << 20)) // 4,
+                                      grad_mix=(hops, lw) if step_dp else None)
         flat = net.engine.flat
     else:
         flat = prepare(model, dev)

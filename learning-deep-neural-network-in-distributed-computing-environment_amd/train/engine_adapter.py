@@ -25,9 +25,12 @@ engine's on-device statistics (one small reduction per step, one host read per
 epoch).  A trailing partial batch is trained too, as the reference does
 (BAR/trainer.py:202-216): the engine's shapes are static, so it runs
 ``StaticMLPEngine.eager_step`` (autograd on the same flat parameters + the fused
-update).  A data-parallel engine instead runs the same number of full steps on
-every rank (collective schedules must match); what it leaves out is reported as
-``engine_local_epoch.last_skipped``.
+update).  A data-parallel engine runs the same number of full steps on every rank
+(the minimum over the ranks), then ONE tail step on every rank
+(``StaticMLPEngine.dp_tail_step``: each rank's next batch of any size -- its
+partial batch, or none -- weighted by its sample count, so the update is the mean
+over all ranks' samples).  Batches beyond that (shards of unequal length) are
+reported as ``engine_local_epoch.last_skipped``.
 """
 from __future__ import annotations
 
@@ -104,16 +107,18 @@ class EngineOptimizer(torch.optim.Optimizer):
 
 def build_engine(model, batch_size: int, optimizer: str, lr: float, device, *, momentum: float = 0.9,
                  weight_decay: float = 0.0, world_size: int = 1, process_group=None, use_graphs: bool = True,
-                 bucket_cap_elems: int = 8 << 20):
+                 bucket_cap_elems: int = 8 << 20, grad_mix: tuple | None = None):
     """(EngineModule, EngineOptimizer) for an ldnn MLP.  ``world_size`` > 1 = per-step
     data parallelism inside the engine (reduce-scatter + sharded update + all-gather
     over RCCL); 1 = an independent replica (the reference's global-epoch schedule
-    aggregates it through the Aggregator like any other model)."""
+    aggregates it through the Aggregator like any other model).  ``grad_mix`` =
+    (hops, local_weight): per-step ring / double-ring gossip or the self-weighted
+    all-reduce inside the engine (StaticMLPEngine)."""
     name = optimizer.lower()
     oc = (OptimConfig("sgd", lr=lr, momentum=momentum, weight_decay=weight_decay) if name == "sgd"
           else OptimConfig(name, lr=lr, weight_decay=weight_decay))
     eng = StaticMLPEngine(model, batch_size, oc, device=device, world_size=world_size, process_group=process_group,
-                          use_graphs=use_graphs, bucket_cap_elems=bucket_cap_elems)
+                          use_graphs=use_graphs, bucket_cap_elems=bucket_cap_elems, grad_mix=grad_mix)
     return EngineModule(model, eng), EngineOptimizer(eng, model.parameters())
 
 
@@ -131,35 +136,58 @@ def engine_local_epoch(model: EngineModule, trainloader, optimizer, scheduler=No
     nb = model.full_batches(trainloader)
     if max_steps is not None:
         nb = min(nb, max_steps)
-    partial = not eng.distributed
+    dist_ = eng.distributed
     # cum[i] = running (loss sum, #correct) after step i -- one tiny reduction per step
     cum = torch.zeros(max(nb, 1) + 2, 2, dtype=torch.float64, device=dev)
     sizes = []
     eng.reset_stats()
-    done, skipped = 0, 0
+    done, skipped, tail, steps = 0, 0, False, 0
+
+    def record(n):
+        nonlocal done
+        sizes.append(n)
+        torch.sum(eng.stats, 0, dtype=torch.float64, out=cum[len(sizes)])
+        done += 1
+
+    def after_step():
+        # (counts every step incl. a sample-less tail step: the collective checks stay aligned)
+        nonlocal steps
+        steps += 1
+        if cutoff is not None:
+            cutoff.step(steps - 1)
+        if check_comm is not None and steps % check_every == 0:
+            check_comm.check_schedule(f"step {steps}", dev if check_comm.device_collectives else None)
+
+    total = int(trainloader.num_samples) if hasattr(trainloader, "num_samples") else None
+    seen = 0
     try:
-        for i, (x, y) in enumerate(trainloader):
-            if done >= nb + (1 if partial else 0):
-                skipped += y.numel()
-                break
-            if y.numel() != eng.B:
-                if not partial or done >= nb + 1:
-                    skipped += y.numel()
-                    continue
-                eng.eager_step(x, y)   # the trailing partial batch (single-process engine)
-            else:
-                if done >= nb:
-                    skipped += y.numel()
-                    break
+        for x, y in trainloader:
+            seen += y.numel()
+            if done < nb and y.numel() == eng.B:
                 eng.load_batch(x, y)
                 eng.step()
-            sizes.append(y.numel())
-            torch.sum(eng.stats, 0, dtype=torch.float64, out=cum[done + 1])
-            done += 1
-            if cutoff is not None:
-                cutoff.step(done - 1)
-            if check_comm is not None and done % check_every == 0:
-                check_comm.check_schedule(f"step {done}", dev if check_comm.device_collectives else None)
+                record(y.numel())
+                after_step()
+                continue
+            # the first batch past the full steps: the trailing partial batch (or, under
+            # data parallelism, this rank's next batch of any size) -- at most one tail step
+            tail = True
+            if dist_:
+                eng.dp_tail_step(x, y)   # collective: every rank runs exactly one
+                record(y.numel())
+                after_step()
+            elif y.numel() != eng.B:
+                eng.eager_step(x, y)
+                record(y.numel())
+                after_step()
+            else:
+                seen -= y.numel()
+            break
+        if dist_ and not tail:   # this rank's shard ran out: take part in the tail step with no samples
+            tail = True
+            eng.dp_tail_step(None, None)
+            after_step()
+        skipped = (total - sum(sizes)) if total is not None else max(seen - sum(sizes), 0)
     except StopLocalTraining:
         if isinstance(optimizer, EngineOptimizer):
             optimizer.step()   # a no-op; keeps torch's scheduler-order check quiet

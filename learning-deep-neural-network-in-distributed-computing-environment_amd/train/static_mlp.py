@@ -99,7 +99,16 @@ class StaticMLPEngine:
                  shard_optimizer: bool | None = None, wgrad_combine: bool = True, library_gemms: bool | None = None,
                  fuse_head_dgrad: bool | None = None, library_dgrad: bool | None = None, head_dgrad_mode: int = -1,
                  relu_masks: bool = True, transposed_dgrad: bool = True, bias_ones_column: bool = True,
-                 fuse_head_fwd: bool = True, fuse_head_bwd: bool = True):
+                 fuse_head_fwd: bool = True, fuse_head_bwd: bool = True, grad_mix: tuple | None = None):
+        """``grad_mix`` = (hops, local_weight): per-step gradient exchange other than the
+        equal all-reduce (world > 1) -- hops 0 with a weight = the reference's
+        self-weighted all-reduce (BAR/communication.py:4-10), hops 1 / 2 = ring /
+        double-ring gossip (BR/communication.py:5-62, BDR/communication.py:5-77), equal
+        (local_weight None) or weighted.  Each bucket is exchanged between the backward's
+        graph segments (grouped send/recv or all-reduce on RCCL's stream) and combined in
+        place by the fused mix kernel (K18) before its optimizer segment.  Every rank
+        then applies its OWN mixed gradient (decentralised SGD: replicas differ), so
+        these modes run the replicated optimizer."""
         from ..models.mlp import MLP
 
         if not isinstance(model, MLP):
@@ -136,6 +145,13 @@ class StaticMLPEngine:
         # the new bf16 weights are all-gathered -- 3/4 of an fp32 all-reduce's bytes
         # on xGMI and 1/N of the optimizer's HBM traffic per rank.
         # (shard_optimizer=True also forces the collective path at world 1: a test hook for RCCL)
+        if grad_mix is not None and (grad_mix[0] == 0 and grad_mix[1] is None):
+            grad_mix = None   # equal all-reduce: the default path
+        self._mix_cfg = grad_mix if world_size > 1 else None
+        if self._mix_cfg is not None and shard_optimizer:
+            raise ValueError("grad_mix modes give every rank its own update: no sharded optimizer")
+        if self._mix_cfg is not None:
+            shard_optimizer = False
         self.shard = (self.world > 1) if shard_optimizer is None else bool(shard_optimizer)
         self.distributed = self.world > 1 or self.shard
         # ---- bucket plan: close a bucket after wgrad_l once it holds >= cap elements.
@@ -230,7 +246,7 @@ class StaticMLPEngine:
         if o.name in ("adam", "adamw"):
             self.exp_avg = torch.zeros_like(f.master)
             self.exp_avg_sq = torch.zeros_like(f.master)
-        self._grad_scale = 1.0 / self.world if average_grads else 1.0
+        self._grad_scale = 1.0 / self.world if (average_grads and self._mix_cfg is None) else 1.0
 
         # Gradients produced by accumulation (split-K wgrad atomics, bias-gradient
         # atomics of the xent / dgrad epilogues) must start each step at zero.  The
@@ -648,6 +664,154 @@ class StaticMLPEngine:
         self._opt(0, f.numel)
         return loss.detach()
 
+    def dp_tail_step(self, x: torch.Tensor | None = None, y: torch.Tensor | None = None):
+        """Collective (every rank, the same number of times): one data-parallel step on
+        batches of ANY size -- the ranks' trailing partial batches, or nothing on a rank
+        whose shard ran out (BAR/trainer.py:202-216 trains the short last batch).
+        Each rank's gradient is the mean over its own samples (autograd on the flat
+        parameters, as eager_step); it is weighted by n_rank * N / n_total before the
+        engine's usual collectives, so after the 1/N averaging the update is the mean
+        over every rank's samples -- what one process on the concatenated batch does.
+        The collectives are a full step's (same buckets, same order), preceded by one
+        tiny all-reduce of the sample counts.  Returns the local loss (or None)."""
+        if not self.distributed:
+            raise RuntimeError("dp_tail_step: single-process engines use eager_step")
+        from ..models.layers import CrossEntropyLoss
+
+        n = 0 if y is None else int(y.numel())
+        cnt = torch.tensor([float(n)], dtype=torch.float32, device=self.device)
+        dist.all_reduce(cnt, group=self.pg)
+        n_tot = float(cnt.item())
+        if n_tot == 0:
+            return None
+        self.sync()   # the previous step's weight all-gathers / bias refresh
+        self._master_whole = False
+        f = self.flat
+        f.grad.zero_()
+        f._stale.clear()
+        if self.optim.name in ("adam", "adamw"):
+            self.C.bump_step(self.hp)
+        loss = None
+        if n > 0:
+            with torch.enable_grad():
+                self.model.train()
+                out = self.model(x.reshape(n, -1).to(self.x.dtype))
+                loss = CrossEntropyLoss()(out, y, self.stats[0])
+                loss.backward()
+            f.finalize_grads()
+        if self._mix_cfg is None:   # (gossip / weighted modes: each rank keeps its own gradient's scale)
+            f.grad.mul_(n * self.world / n_tot)
+        capturing = any(s.will_capture for s in self.opt_segments)
+        if self.shard:
+            works = []
+            for bi in self._cut_buckets:
+                w = self._reduce_scatter(bi)
+                if capturing and w is not None:
+                    w.wait()
+                    torch.cuda.current_stream().synchronize()
+                works.append((bi, w))
+            for bi, w in sorted(works, key=lambda t: -t[0]):
+                if w is not None:
+                    w.wait()
+                self.opt_segments[bi]()
+                if bi == self._bias_bucket:
+                    self._broadcast_biases(bi, capturing)
+                g = self._all_gather(bi)
+                if capturing and g is not None:
+                    g.wait()
+                    torch.cuda.current_stream().synchronize()
+                self._pending_gather[bi] = g
+        else:
+            works = []
+            for bi in self._cut_buckets:
+                w = self._exchange(bi)
+                if capturing:
+                    self._wait(w)
+                    torch.cuda.current_stream().synchronize()
+                works.append((bi, w))
+            for bi, w in works:
+                self._combine(bi, w)
+                self.opt_segments[bi]()
+        return None if loss is None else loss.detach()
+
+    # ------------------------------------------------- per-bucket gradient exchange
+    def _exchange(self, bi):
+        """Start bucket bi's gradient exchange (non-sharded step): the equal / weighted
+        all-reduce, or the ring / double-ring neighbour exchange (grad_mix)."""
+        b, e, _ = self.buckets[bi]
+        g = self.flat.grad[b:e]
+        if self._mix_cfg is None:
+            return dist.all_reduce(g, group=self.pg, async_op=True)
+        hops, w = self._mix_cfg
+        bufs = self._mix_bufs(bi)
+        if hops == 0:
+            bufs[0].copy_(g)   # the own gradient, for the self-weighted mix
+            return dist.all_reduce(g, group=self.pg, async_op=True)
+        r, N = self.rank, self.world
+        sends, recvs = [], []
+        for h in range(1, hops + 1):
+            src, dst = (r - h) % N, (r + h) % N
+            if src == r:   # double ring on 2 ranks: the 2-hop neighbour is this rank
+                bufs[h - 1].copy_(g)
+                continue
+            recvs.append((bufs[h - 1], src))
+            sends.append((g, dst))
+        if not recvs:
+            return None
+        glob = (lambda q: q) if self.pg is None else (lambda q: dist.get_global_rank(self.pg, q))
+        if self._gloo_backend():
+            # gloo: host-staged point-to-point (its device P2P path is slow), synchronous
+            from ..parallel.comm import TorchComm
+
+            TorchComm(self.pg).sendrecv(sends, recvs)
+            return None
+        ops = [dist.P2POp(dist.irecv, t, glob(q), self.pg) for t, q in recvs]
+        ops += [dist.P2POp(dist.isend, t, glob(q), self.pg) for t, q in sends]
+        return dist.batch_isend_irecv(ops)
+
+    @staticmethod
+    def _wait(w):
+        for x in (w if isinstance(w, list) else [w]):
+            if x is not None:
+                x.wait()
+
+    def _combine(self, bi, w):
+        """Wait for bucket bi's exchange and mix it in place (fused mix kernel, K18)."""
+        self._wait(w)
+        if self._mix_cfg is None:
+            return
+        from ..parallel.aggregation import _mix
+
+        b, e, _ = self.buckets[bi]
+        g = self.flat.grad[b:e]
+        hops, lw = self._mix_cfg
+        bufs = self._mix_bufs(bi)
+        N = self.world
+        if hops == 0:   # w g + (1-w)(sum - g)/(N-1) = (w - o) g + o sum
+            o = (1.0 - lw) / (N - 1)
+            _mix(g, bufs[0], g, a=lw - o, b=o)
+        elif hops == 1:
+            a, c = (0.5, 0.5) if lw is None else (lw, 1.0 - lw)
+            _mix(g, g, bufs[0], a=a, b=c)
+        else:
+            a, c = (1.0 / 3.0, 1.0 / 3.0) if lw is None else (lw, (1.0 - lw) / 2.0)
+            _mix(g, g, bufs[0], bufs[1], a=a, b=c, c=c)
+
+    def _mix_bufs(self, bi):
+        bufs = self.__dict__.setdefault("_mixb", {})
+        if bi not in bufs:
+            b, e, _ = self.buckets[bi]
+            n = max(1, self._mix_cfg[0])
+            bufs[bi] = [torch.empty(e - b, dtype=torch.float32, device=self.device) for _ in range(n)]
+        return bufs[bi]
+
+    def _gloo_backend(self) -> bool:
+        g = self.__dict__.get("_is_gloo")
+        if g is None:
+            g = dist.get_backend(self.pg) == "gloo"
+            self._is_gloo = g
+        return g
+
     # ------------------------------------------------------------ collectives
     def _reduce_scatter(self, i):
         b, e, _ = self.buckets[i]
@@ -783,15 +947,15 @@ class StaticMLPEngine:
         works = []
         for i, seg in enumerate(self.segments):
             seg()
-            b, e, _ = self.buckets[self._cut_buckets[i]]
-            w = dist.all_reduce(self.flat.grad[b:e], group=self.pg, async_op=True)
+            bi = self._cut_buckets[i]
+            w = self._exchange(bi)
             if capturing:
-                w.wait()
+                self._wait(w)
                 torch.cuda.current_stream().synchronize()
-            works.append(w)
-        for w, oseg in zip(works, self.opt_segments):
-            w.wait()
-            oseg()
+            works.append((bi, w))
+        for bi, w in works:
+            self._combine(bi, w)
+            self.opt_segments[bi]()
 
     def describe(self) -> dict:
         """Which kernel runs each GEMM of the step (bench.py reports it)."""

@@ -28,6 +28,11 @@ def main():
     ap.add_argument("--cap", type=int, default=1 << 17)
     ap.add_argument("--steps", type=int, default=6)
     ap.add_argument("--shard", type=int, default=-1, help="-1 auto (on for N > 1), 0 off, 1 on")
+    ap.add_argument("--tail", type=str, default="",
+                    help="comma-separated per-rank sample counts of one final dp_tail_step (e.g. '2,0': rank 0's "
+                         "partial batch of 2, rank 1 without data); the reference then trains the concatenated "
+                         "tail with eager_step")
+    ap.add_argument("--optimizer", choices=["sgd", "adam"], default="sgd")
     a = ap.parse_args()
     ctx = D.setup(a.backend)
     N, r = ctx.world_size, ctx.rank
@@ -35,7 +40,8 @@ def main():
     torch.manual_seed(0)
     model = mlp3(784, H, 10)
     # small bucket cap -> several buckets / segments on the multi-rank path
-    eng = StaticMLPEngine(model, B, OptimConfig("sgd", lr=0.05, momentum=0.9), device=ctx.device, world_size=N,
+    cfg = OptimConfig("sgd", lr=0.05, momentum=0.9) if a.optimizer == "sgd" else OptimConfig("adam", lr=1e-3)
+    eng = StaticMLPEngine(model, B, cfg, device=ctx.device, world_size=N,
                           bucket_cap_elems=a.cap, use_graphs=bool(a.graphs),
                           shard_optimizer=None if a.shard < 0 else bool(a.shard))
     print(f"rank {r}: shard={eng.shard}", flush=True)
@@ -51,6 +57,16 @@ def main():
         torch.cuda.synchronize()
         print(f"rank {r} step {i} loss {eng.read_stats(B)[0]:.5f} finite={bool(torch.isfinite(eng.flat.shadow).all())}",
               flush=True)
+    tails = [int(v) for v in a.tail.split(",")] if a.tail else []
+    if tails:
+        assert len(tails) == N
+        gt = torch.Generator(device="cpu").manual_seed(6)
+        xt = torch.randn(sum(tails), 784, generator=gt)
+        yt = torch.randint(0, 10, (sum(tails),), generator=gt)
+        o = sum(tails[:r])
+        n = tails[r]
+        eng.dp_tail_step(xt[o:o + n].to(ctx.device).bfloat16() if n else None, yt[o:o + n].to(ctx.device) if n else None)
+        torch.cuda.synchronize()
     # the forward reads the fp32 master biases: they must agree on every rank after
     # sharded updates too (each rank updates only its shard of the master)
     eng.sync()
@@ -72,11 +88,12 @@ def main():
     if r == 0:
         # single-rank reference on the concatenated batch (same kernels, no graphs)
         torch.manual_seed(0)
-        ref = StaticMLPEngine(mlp3(784, H, 10), N * B, OptimConfig("sgd", lr=0.05, momentum=0.9),
-                              device=ctx.device, world_size=1, use_graphs=False)
+        ref = StaticMLPEngine(mlp3(784, H, 10), N * B, cfg, device=ctx.device, world_size=1, use_graphs=False)
         for i in range(S):
             ref.load_batch(xs[i].to(ctx.device).bfloat16(), ys[i].to(ctx.device))
             ref.step()
+        if tails and sum(tails):
+            ref.eager_step(xt.to(ctx.device).bfloat16(), yt.to(ctx.device))
         torch.cuda.synchronize()
         # map the two flat layouts through the named parameters
         ok = True

@@ -42,8 +42,14 @@ def grads(m):
 
 
 def zero(m):
-    for p in m.parameters():
-        p.grad = None
+    f = getattr(m, "_ldnn_flat", None)
+    if f is None:   # the torch.nn oracle
+        for p in m.parameters():
+            p.grad = None
+        return
+    f.reattach_grads()   # ldnn: gradients are views of the flat buffer
+    f.grad.zero_()
+    f._stale.clear()
 
 
 def run(N, H, seed=0):

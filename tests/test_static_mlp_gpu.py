@@ -72,12 +72,17 @@ def test_graph_replay_matches_eager_with_splitk():
     torch.testing.assert_close(e1.flat.master, e2.flat.master, rtol=1e-6, atol=1e-8)
 
 
-@pytest.mark.parametrize("nproc", [2, 3])
-def test_multirank_static_engine_gloo_two_ranks_one_gpu(nproc):
+@pytest.mark.parametrize("nproc,extra", [(2, []), (3, []), (2, ["--tail", "2,0"]), (3, ["--tail", "5,256,0"]),
+                                         (2, ["--tail", "7,3", "--optimizer", "adam"]),
+                                         (2, ["--tail", "7,3", "--shard", "0"])])
+def test_multirank_static_engine_gloo_two_ranks_one_gpu(nproc, extra):
     """The bucketed multi-rank step (sharded optimizer: reduce-scatter between graph
     segments, shard update, weight all-gather, fp32 bias refresh from the shard
     owners) equals one rank on the concatenated batch, and every rank's forward reads
-    the same fp32 biases (2 / 3 ranks share the GPU via gloo)."""
+    the same fp32 biases (2 / 3 ranks share the GPU via gloo).  ``--tail``: then one
+    dp_tail_step with per-rank batches of any size (partial, full, none) == the single
+    rank's eager_step on the concatenated tail (the DP engine trains the
+    trailing partial batch)."""
     import os
     import socket
     import subprocess
@@ -90,7 +95,7 @@ def test_multirank_static_engine_gloo_two_ranks_one_gpu(nproc):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", str(nproc), "--master-addr", "127.0.0.1",
            "--master-port", str(port), os.path.join(root, "scripts", "check_static_dp.py"), "--backend", "gloo",
-           "--hidden", "512", "--batch", "1024", "--steps", "7"]
+           "--hidden", "512", "--batch", "1024" if not extra else "256", "--steps", "7"] + extra
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     assert "BIASES_CONSISTENT" in r.stdout, r.stdout[-3000:]
@@ -337,3 +342,30 @@ def test_eager_partial_batch_step_matches_reference(opt):
     for l, r in zip(lin, [ref[0], ref[2], ref[4]]):
         for p, q in ((l.weight, r.weight), (l.bias, r.bias)):
             torch.testing.assert_close(p.detach().float(), q.detach(), rtol=5e-2, atol=5e-3 if opt == "sgd" else 1e-2)  # Adam: sign-amplified bf16 noise near 0
+
+
+@pytest.mark.parametrize("nproc,hops,weight", [(3, 1, None), (3, 1, 0.7), (3, 2, None), (3, 2, 0.6), (2, 2, None),
+                                               (3, 0, 0.8), (4, 2, 0.5)])
+def test_static_engine_per_step_gossip_and_weighted_match_reference_formulas(nproc, hops, weight):
+    """--sync_every step --topology ring / double_ring (equal / weighted) and the weighted
+    all-reduce on the static engine (grad_mix: per-bucket neighbour exchange between the
+    backward's graph segments + the fused mix kernel) == the reference formulas
+    (parallel.aggregation on FakeWorld, fp32) applied to the ranks' own gradients, step
+    after step while the replicas drift apart (gloo ranks sharing the GPU)."""
+    import os
+    import socket
+    import subprocess
+    import sys
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", str(nproc), "--master-addr", "127.0.0.1",
+           "--master-port", str(port), os.path.join(root, "scripts", "check_engine_gossip.py"), "--hops", str(hops)]
+    if weight is not None:
+        cmd += ["--weight", str(weight)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "ENGINE_GOSSIP_OK" in r.stdout, r.stdout[-3000:]
