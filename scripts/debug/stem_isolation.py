@@ -82,6 +82,7 @@ def run(N, H, seed=0):
     yr = ref.stem(xf)
     (yr * G).sum().backward()
     gref = {"bn1.weight": ref.bn1.weight.grad, "bn1.bias": ref.bn1.bias.grad, "conv1.weight": ref.conv1.weight.grad}
+    gref_a = {k: v.clone() for k, v in gref.items()}
     out.append({"cfg": tag, "part": "A_injected_G", "q": "stem_out",
                 "fused_vs_sep_maxabs": (res["fused"][0] - res["sep"][0]).abs().max().item(),
                 "fused_vs_fp32": rel(res["fused"][0], yr), "sep_vs_fp32": rel(res["sep"][0], yr)})
@@ -134,6 +135,39 @@ def run(N, H, seed=0):
     for k in gref:
         out.append({"cfg": tag, "part": "C_true_G", "q": k,
                     "fused_vs_fp32": rel(full["fused"][k], gref[k]), "sep_vs_fp32": rel(full["sep"][k], gref[k])})
+    # part D: the fp32 oracle with ONLY the conv1-output gradient rounded to bf16 (what
+    # ldnn's BN backward stores): how much of the stem wgrad gap that rounding explains
+    zero(ref)
+    c = ref.conv1(xf)
+    c.register_hook(lambda gr: gr.bfloat16().float())
+    yr2 = ref.maxpool(torch.relu(ref.bn1(c)))
+    (yr2 * G).sum().backward()
+    out.append({"cfg": tag, "part": "D_fp32_bf16_dx", "q": "conv1.weight",
+                "vs_fp32": rel(ref.conv1.weight.grad, gref_a["conv1.weight"])})
+    # D2: ... and the conv output itself stored in bf16 (what the BN reads in ldnn)
+    zero(ref)
+    c = ref.conv1(xf)
+    c.register_hook(lambda gr: gr.bfloat16().float())
+    cb = c + (c.detach().bfloat16().float() - c.detach())   # bf16 value, identity gradient
+    yr3 = ref.maxpool(torch.relu(ref.bn1(cb)))
+    (yr3 * G).sum().backward()
+    out.append({"cfg": tag, "part": "D2_fp32_bf16_conv_out_and_dx", "q": "conv1.weight",
+                "vs_fp32": rel(ref.conv1.weight.grad, gref_a["conv1.weight"]),
+                "bn1.weight_vs_fp32": rel(ref.bn1.weight.grad, gref_a["bn1.weight"])})
+    # part E: stock PyTorch bf16 autocast (MIOpen / hipBLASLt) on the same model: its
+    # gradient at the stem output vs fp32, twice (its own run-to-run spread)
+    if DEV == "cuda":
+        gs = []
+        for _ in range(2):
+            zero(ref)
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                yb = ref.stem(xf)
+                ybd = yb.detach().requires_grad_(True)
+                lb = ref.trunk(ybd)
+            torch.nn.functional.cross_entropy(lb.float(), yl).backward()
+            gs.append(ybd.grad.detach().float().clone())
+        out.append({"cfg": tag, "part": "E_stock_autocast_bf16", "q": "grad_at_stem_out",
+                    "vs_fp32": rel(gs[0], g_true), "run_to_run": rel(gs[1], gs[0])})
     LF.BN_POOL_FUSED = True
     return out
 

@@ -18,6 +18,7 @@ for step in "$@"; do
     smoke) $T 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 ;;
     bench) $T 600 python -u bench.py > $O/bench.json 2> $O/bench.err ;;
     iso) $T 300 python -u scripts/debug/stem_isolation.py > $O/stem_isolation.jsonl 2>&1 ;;
+    det:*) a=${step#det:}; $T 300 python -u scripts/debug/determinism_probe.py --model ${a%%@*} --hw ${a##*@} >> $O/determinism.jsonl 2>&1 ;;
     cnn:*) a=${step#cnn:}; $T 300 python -u scripts/bench_cnn.py --model ${a%%@*} --batch ${a##*@} --graph --no-stock \
              >> $O/cnn.jsonl 2>> $O/cnn.err ;;
     prof:*) a=${step#prof:}; $T 400 rocprofv3 --kernel-trace --stats -d $O/prof_$a -o run -- \

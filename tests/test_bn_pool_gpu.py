@@ -219,34 +219,74 @@ def test_bn_relu_maxpool_fused(N, C, H, W, pad, twin, monkeypatch):
     torch.testing.assert_close(rvf, ref.running_var, rtol=1e-3, atol=1e-3)
 
 
-def test_resnet_stem_fused_bn_pool_matches_separate(monkeypatch):
-    """ResNet-18 (stem statistics from the conv epilogue, then the fused BN + ReLU + max-pool)
-    trains like the separate BN-apply + pool passes: same logits / running statistics, and
-    stem gradients within the spread of two runs of the separate path (at batch 4 bf16
-    rounding flips from the fp32 summation order are amplified through 17 layers, see
-    tests/test_layers_gpu.py::test_conv_epilogue_bn_statistics_match_separate_pass; the
-    fused backward itself is pinned against fp32 by test_bn_relu_maxpool_fused)."""
-    from ldnn.models import CrossEntropyLoss, build_model, xavier_init
+@pytest.mark.parametrize("N,H", [(16, 112), (16, 224)])
+def test_resnet_stem_fused_bn_pool_vs_fp32_oracle(N, H, monkeypatch):
+    """ResNet-18's stem -- conv1 7x7/2 (BN statistics from its epilogue) -> bn1 -> ReLU ->
+    max-pool 3x3/2 -- with ONE seeded upstream gradient injected at the pool output, in
+    three implementations: the fused bn_maxpool pass, the separate BN-apply + pool
+    passes, and a plain torch.nn fp32 oracle with the same weights (tests/ref_models.py).
 
-    x = torch.randn(4, 3, 64, 64, device="cuda").bfloat16()
-    yl = torch.randint(0, 10, (4,), device="cuda")
-    outs = []
-    for fused in (True, False, False):
+    Why this replaces the round-3 model-level check: at model level the
+    gradient reaching the stem is ill-conditioned in ANY bf16 implementation -- stock
+    PyTorch-ROCm bf16 autocast differs from fp32 there by 39-42 % and from itself
+    run-to-run by 12-14 %, ldnn by 37-40 % / ~20 % (profiles/r4/stem_bn_pool_isolation.txt)
+    -- so it cannot separate a kernel bug from rounding.  With the upstream gradient
+    fixed the comparison is well conditioned.  Tolerances (bf16 unit roundoff
+    u = 2^-9): measured fused-vs-fp32 0.17-0.6 % on dgamma / dbeta, fused-vs-separate
+    0.15 %; the conv1 wgrad sits 7.3-7.9 % from fp32 in BOTH paths, and an fp32 oracle
+    that only stores the conv output and its gradient in bf16 (what any bf16 pipeline
+    stores) reproduces 6.1-6.7 % of it: sum(dx * c) = 0 per channel after a BN, so the
+    wgrad is a small difference of large terms -- it is compared against that oracle."""
+    from ldnn.models import build_model, xavier_init
+    from ref_models import oracle_for, rel
+
+    torch.manual_seed(0)
+    m = build_model("resnet18")
+    xavier_init(m)
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    ldnn.prepare(m, "cuda")
+    m.train()
+    f = m._ldnn_flat
+    g = torch.Generator(device="cuda").manual_seed(1234)
+    x = torch.randn(N, 3, H, H, device="cuda", generator=g).bfloat16()
+    P = ((H + 1) // 2 + 1) // 2
+    G = torch.randn(N, 64, P, P, device="cuda", generator=g).bfloat16().float()
+    res = {}
+    for fused in (True, False):
         monkeypatch.setattr(LF, "BN_POOL_FUSED", fused)
-        torch.manual_seed(0)
-        m = build_model("resnet18")
-        xavier_init(m)
-        ldnn.prepare(m, "cuda")
-        m.train()
-        out = m(x)
-        CrossEntropyLoss()(out, yl).backward()
-        outs.append((out.detach().float(), m.conv1.weight.grad.clone(), m.bn1.weight.grad.clone(),
-                     m.bn1.running_var.clone()))
-    (o1, w1, g1, v1), (o2, w2, g2, v2), (_, w3, g3, _) = outs
-    assert ((o1 - o2).norm() / o2.norm()).item() < 3e-2
-    torch.testing.assert_close(v1, v2, rtol=1e-5, atol=1e-6)
-    for a, b, c in ((g1, g2, g3), (w1, w2, w3)):
-        assert (a - b).norm().item() <= 3.0 * (c - b).norm().item() + 0.3 * b.norm().item()
+        m.load_state_dict(sd)
+        f.refresh_shadow()
+        f.reattach_grads()
+        f.grad.zero_()
+        f._stale.clear()
+        y = LF.bn_relu_maxpool(m.conv1(x), m.bn1, m.maxpool)
+        (y.float() * G).sum().backward()
+        res[fused] = (y.detach().float(), m.bn1.weight.grad.clone(), m.bn1.bias.grad.clone(),
+                      m.conv1.weight.grad.clone(), m.bn1.running_mean.clone(), m.bn1.running_var.clone())
+    ref = oracle_for("resnet18", sd)
+    ref.train()
+    xf = x.float()
+    yr = ref.stem(xf)
+    (yr * G).sum().backward()
+    # the bf16-storage oracle: conv output and its gradient rounded to bf16, all math fp32
+    emu = oracle_for("resnet18", sd)
+    emu.train()
+    c = emu.conv1(xf)
+    c.register_hook(lambda gr: gr.bfloat16().float())
+    cb = c + (c.detach().bfloat16().float() - c.detach())
+    (emu.maxpool(torch.relu(emu.bn1(cb))) * G).sum().backward()
+    (yf, dgf, dbf, dwf, rmf, rvf), (ys, dgs, dbs, dws, rms, rvs) = res[True], res[False]
+    assert rel(yf, ys) < 1e-3                       # same statistics, same bf16 outputs (rare rounding flips)
+    assert rel(yf, yr) < 1e-2                       # measured 2.6e-3
+    for a, b, what in ((dgf, dgs, "dgamma"), (dbf, dbs, "dbeta"), (dwf, dws, "dW")):
+        assert rel(a, b) < 1e-2, (what, rel(a, b))   # fused vs separate: measured <= 2.2e-3
+    assert rel(dgf, ref.bn1.weight.grad) < 2e-2, rel(dgf, ref.bn1.weight.grad)   # measured <= 2.3e-3
+    assert rel(dbf, ref.bn1.bias.grad) < 3e-2, rel(dbf, ref.bn1.bias.grad)       # measured <= 6.2e-3
+    assert rel(dwf, emu.conv1.weight.grad) < 4e-2, rel(dwf, emu.conv1.weight.grad)
+    assert rel(dwf, ref.conv1.weight.grad) < 0.15, rel(dwf, ref.conv1.weight.grad)  # measured 7.3-7.9 %
+    torch.testing.assert_close(rmf, ref.bn1.running_mean, rtol=1e-2, atol=1e-3 * ref.bn1.running_var.sqrt().max().item())
+    torch.testing.assert_close(rvf, ref.bn1.running_var, rtol=1e-2, atol=1e-4)
+    torch.testing.assert_close(rmf, rms, rtol=1e-4, atol=1e-6)
 
 
 @pytest.mark.parametrize("N,C,H,W", [(8, 64, 16, 16), (4, 128, 7, 9), (2, 24, 5, 5)])

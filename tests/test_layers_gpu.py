@@ -226,60 +226,119 @@ def test_train_global_with_graphs_matches_eager():
     assert abs(h0[4][-1] - h1[4][-1]) < 1e-2 and abs(h0[5][-1] - h1[5][-1]) < 0.5
 
 
-@pytest.mark.parametrize("name,shape", [("enhanced_cnn_small", (32, 3, 32, 32)), ("resnet18", (8, 3, 96, 96)),
-                                        ("enhanced_cnn", (64, 3, 32, 32))])
-def test_conv_epilogue_bn_statistics_match_separate_pass(name, shape, monkeypatch):
-    """Training-mode BN whose statistics the producing conv's epilogue accumulated and
-    finalized (conv_lds.hip bn_stats_epilogue) == the BN's own reduce pass: outputs,
-    running statistics, num_batches_tracked and gradients.  (Full EnhancedCNN at batch
-    64: its 4x4 / 2x2 slab split-K stages keep the separate statistics pass.)"""
+@pytest.mark.parametrize("N,Cin,H,Cout,stride", [(16, 64, 56, 64, 1), (16, 128, 28, 256, 2), (64, 64, 32, 128, 2),
+                                                  (64, 256, 8, 256, 1)])
+def test_conv_epilogue_bn_statistics_layer_vs_fp32(N, Cin, H, Cout, stride, monkeypatch):
+    """A conv whose epilogue accumulates + finalizes the next BatchNorm's statistics
+    (conv_lds.hip bn_stats_epilogue; ResNet-18 layer1 / a stride-2 stage entry, two
+    EnhancedCNN stages) == the same conv + the BN's own reduce pass == a plain fp32
+    torch conv + BN, on ONE seeded upstream gradient injected at relu(bn(conv x)):
+    running statistics, outputs, dgamma / dbeta / dx, and dW against an fp32 oracle
+    that stores the conv output and its gradient in bf16 (as every bf16 pipeline does;
+    see tests/test_bn_pool_gpu.py::test_resnet_stem_fused_bn_pool_vs_fp32_oracle for
+    why dW is compared against that oracle).  Layer-level and seeded: well
+    conditioned, unlike the model-level gradients of round 3."""
     import ldnn.models.layers as layers_mod
-    from ldnn.models.layers import Conv2d
+    from ldnn.models.layers import BatchNorm2d, Conv2d
+    from ref_models import rel
 
     monkeypatch.setattr(layers_mod, "FUSE_BN_STATS", True)
+    torch.manual_seed(5)
+    conv0 = torch.nn.Conv2d(Cin, Cout, 3, stride, 1, bias=False)
+    bn0 = torch.nn.BatchNorm2d(Cout)
+    with torch.no_grad():
+        bn0.weight.uniform_(0.5, 1.5)
+        bn0.bias.uniform_(-0.3, 0.3)
+        conv0.weight.copy_(conv0.weight.bfloat16().float())   # the weights the MFMA kernels read
+    g = torch.Generator(device="cuda").manual_seed(6)
+    x = torch.randn(N, Cin, H, H, device="cuda", generator=g).bfloat16()
+    res = {}
+    for paired in (True, False):
+        conv, bn = Conv2d(Cin, Cout, 3, stride, 1, bias=False), BatchNorm2d(Cout)
+        conv.load_state_dict(conv0.state_dict())
+        bn.load_state_dict(bn0.state_dict())
+        if paired:
+            layers_mod.pair_conv_bn(conv, bn)
+        net = torch.nn.Sequential(conv, bn)
+        ldnn.prepare(net, "cuda")
+        net.train()
+        xb = x.clone().requires_grad_(True)
+        y = bn.act(conv(xb), relu=True)
+        if "G" not in res:
+            res["G"] = torch.randn(y.shape, device="cuda", generator=g).bfloat16().float()
+        (y.float() * res["G"]).sum().backward()
+        res[paired] = (y.detach().float(), bn.weight.grad.clone(), bn.bias.grad.clone(), xb.grad.float(),
+                       conv.weight.grad.clone(), bn.running_mean.clone(), bn.running_var.clone(),
+                       int(bn.num_batches_tracked))
+    G = res["G"]
+    # fp32 oracle, and the bf16-storage oracle (conv output + its gradient rounded to bf16)
+    outs = []
+    for emulate in (False, True):
+        c0, b0 = torch.nn.Conv2d(Cin, Cout, 3, stride, 1, bias=False).cuda(), torch.nn.BatchNorm2d(Cout).cuda()
+        c0.load_state_dict(conv0.state_dict())
+        b0.load_state_dict(bn0.state_dict())
+        xf = x.float().requires_grad_(True)
+        c = c0(xf)
+        if emulate:
+            c.register_hook(lambda gr: gr.bfloat16().float())
+            c = c + (c.detach().bfloat16().float() - c.detach())
+        yr = torch.relu(b0(c))
+        (yr * G).sum().backward()
+        outs.append((yr.detach(), b0.weight.grad, b0.bias.grad, xf.grad, c0.weight.grad, b0.running_mean,
+                     b0.running_var))
+    (yr, dgr, dbr, dxr, dwr, rmr, rvr), (_, _, _, _, dwe, _, _) = outs
+    (yp, dgp, dbp, dxp, dwp, rmp, rvp, nbp), (yu, dgu, dbu, dxu, dwu, rmu, rvu, nbu) = res[True], res[False]
+    assert nbp == nbu == 1
+    # paired (epilogue statistics) vs separate reduce: the same statistics up to fp32 summation order
+    torch.testing.assert_close(rmp, rmu, rtol=1e-4, atol=1e-6)
+    torch.testing.assert_close(rvp, rvu, rtol=1e-4, atol=1e-6)
+    assert rel(yp, yu) < 2e-3
+    for a, b, what in ((dgp, dgu, "dgamma"), (dbp, dbu, "dbeta"), (dxp, dxu, "dx"), (dwp, dwu, "dW")):
+        assert rel(a, b) < 1e-2, (what, rel(a, b))
+    # vs fp32 (statistics of the bf16-rounded conv output vs of the fp32 one)
+    sd = rvr.sqrt().max().item()
+    torch.testing.assert_close(rmp, rmr, rtol=1e-2, atol=2e-3 * sd)
+    torch.testing.assert_close(rvp, rvr, rtol=1e-2, atol=1e-4)
+    assert rel(yp, yr) < 1e-2, rel(yp, yr)
+    assert rel(dgp, dgr) < 3e-2, rel(dgp, dgr)
+    assert rel(dbp, dbr) < 3e-2, rel(dbp, dbr)
+    assert rel(dxp, dxr) < 3e-2, rel(dxp, dxr)
+    assert rel(dwp, dwe) < 4e-2, rel(dwp, dwe)
+
+
+@pytest.mark.parametrize("name,shape", [("resnet18", (16, 3, 112, 112)), ("enhanced_cnn", (64, 3, 32, 32))])
+def test_cnn_forward_and_head_gradients_vs_fp32_oracle(name, shape):
+    """Whole model, default (fused) paths vs a plain torch.nn fp32 twin with the same
+    weights (tests/ref_models.py), seeded: logits, the first BatchNorm's running
+    statistics and the classifier's gradients -- the quantities that stay well
+    conditioned at model level (the deep trunk's gradients do not, in any bf16
+    implementation: see test_resnet_stem_fused_bn_pool_vs_fp32_oracle)."""
+    from ref_models import oracle_for, rel
 
     torch.manual_seed(0)
-    m1, m2, m3 = build_model(name), build_model(name), build_model(name)
-    xavier_init(m1)
-    for mm in (m2, m3):
-        mm.load_state_dict(m1.state_dict())
-        for m in mm.modules():  # m2, m3: unpaired -> separate BN statistics pass
-            if isinstance(m, Conv2d):
-                m.__dict__["_ldnn_stats_bn"] = None
-    for mm in (m1, m2, m3):
-        ldnn.prepare(mm, "cuda")
-    assert any(getattr(m, "_ldnn_stats_bn", None) is not None for m in m1.modules())
-    x = torch.randn(*shape, device="cuda").bfloat16()
-    y = torch.randint(0, 10, (shape[0],), device="cuda")
-    crit = CrossEntropyLoss()
-    outs = []
-    for m in (m1, m2, m3):
-        m.train()
-        for _ in range(2):
-            out = m(x)
-            crit(out, y).backward()
-        outs.append(out.float())
-    torch.cuda.synchronize()
-    # (batch statistics over as few as 16 values per channel in the last stage:
-    # compare the logits as a whole, fp32 summation order differs between the paths)
-    rel = ((outs[0] - outs[1]).norm() / outs[1].norm()).item()
-    assert rel < 2e-2, rel
-    for (n, b1), (_, b2) in zip(m1.named_buffers(), m2.named_buffers()):
-        if "num_batches" in n:
-            assert torch.equal(b1.cpu(), b2.cpu()), n
-        else:
-            torch.testing.assert_close(b1, b2, rtol=1e-2, atol=1e-3, msg=n)
-    # gradients: within the spread of two runs of the SAME (separate-pass) path, whose
-    # fp32 atomics already differ in arrival order.  Only the last quarter of the
-    # parameters (nearest the loss): at these tiny batches (BN over 72 values in the
-    # last ResNet stage) bf16 rounding flips from any fp32 summation order are
-    # amplified layer by layer -- two separate-pass runs differ by up to ~25 % at the
-    # stem (measured, scripts/debug/bn_fused_diff.py) -- so the deep layers' gradients
-    # carry no signal about the statistics path; the forward checks above pin it.
-    named = list(zip(m1.named_parameters(), m2.named_parameters(), m3.named_parameters()))
-    for (n, p1), (_, p2), (_, p3) in named[-max(2, len(named) // 4):]:
-        g1, g2, g3 = (p.grad.flatten().double() for p in (p1, p2, p3))
-        assert (g1 - g2).norm().item() <= 3.0 * (g3 - g2).norm().item() + 5e-2 * g2.norm().item(), n
+    m = build_model(name)
+    xavier_init(m)
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    ldnn.prepare(m, "cuda")
+    m.train()
+    ref = oracle_for(name, sd)
+    ref.train()
+    g = torch.Generator(device="cuda").manual_seed(7)
+    x = torch.randn(*shape, device="cuda", generator=g).bfloat16()
+    nc = 1000 if name == "resnet18" else 10
+    y = torch.randint(0, nc, (shape[0],), device="cuda", generator=g)
+    out = m(x)
+    CrossEntropyLoss()(out, y).backward()
+    outr = ref(x.float())
+    torch.nn.functional.cross_entropy(outr, y).backward()
+    assert rel(out.float(), outr) < 4e-2, rel(out.float(), outr)
+    bn_name = "bn1" if name == "resnet18" else "prep.1"
+    mb, rb = m.get_submodule(bn_name), ref.get_submodule(bn_name)
+    torch.testing.assert_close(mb.running_mean, rb.running_mean, rtol=1e-2,
+                               atol=2e-3 * rb.running_var.sqrt().max().item())
+    torch.testing.assert_close(mb.running_var, rb.running_var, rtol=1e-2, atol=1e-4)
+    assert rel(m.fc.weight.grad, ref.fc.weight.grad) < 6e-2, rel(m.fc.weight.grad, ref.fc.weight.grad)
+    assert rel(m.fc.bias.grad, ref.fc.bias.grad) < 2e-2, rel(m.fc.bias.grad, ref.fc.bias.grad)
 
 
 def test_lazy_zero_grad_first_write_matches_filled_buffer():
