@@ -178,29 +178,25 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c_in, bool
     return;
   }
   // variant (low byte): 0 = auto (the four-wave gemm_q kernel where it wins, else k256),
-  // 1 = gemm.hip k256, 2/3 = k256 ring experiments, 4.. = gemm_pp, 32.. = gemm_q
+  // 1 = gemm.hip k256, 2/3 = k256 ring experiments, 32.. = gemm_q
   if (tile == 256 && (variant & 255) == 0 && ldnn::gemm_q_preferred(p.M, p.N, p.K)) {
     variant |= 32;
     p.variant = (int)variant;
   }
-  if (tile == 256 && (variant & 255) >= 4) {  // ping-pong kernel (gemm_pp.hip) / four-wave kernel (gemm_q.hip, variant 32)
-    const bool q = (variant & 255) >= 32;
+  TORCH_CHECK(!(tile == 256 && (variant & 255) >= 4 && (variant & 255) < 32), "gemm: unknown variant");
+  if (tile == 256 && (variant & 255) >= 32) {  // four-wave kernel (gemm_q.hip)
     if (splitk > 1 && !slabs) {
-      TORCH_CHECK(ws.has_value() && cnt.has_value(), "gemm: the pp kernel's split-K needs ws and cnt");
+      TORCH_CHECK(ws.has_value() && cnt.has_value(), "gemm: gemm_q's in-launch split-K needs ws and cnt");
       check_dev(*ws, at::kFloat, "ws");
       check_dev(*cnt, at::kInt, "cnt");
-      TORCH_CHECK(ws->is_contiguous() && (size_t)ws->numel() * 4 >= (q ? ldnn::gemm_q_ws_bytes(p.M, p.N, (int)splitk)
-                                                                       : ldnn::gemm_pp_ws_bytes(p.M, p.N, (int)splitk)),
+      TORCH_CHECK(ws->is_contiguous() && (size_t)ws->numel() * 4 >= ldnn::gemm_q_ws_bytes(p.M, p.N, (int)splitk),
                   "gemm: split-K workspace too small");
-      TORCH_CHECK(cnt->is_contiguous() && cnt->numel() >= ldnn::gemm_pp_tiles(p.M, p.N), "gemm: too few counters");
+      TORCH_CHECK(cnt->is_contiguous() && cnt->numel() >= ldnn::gemm_q_tiles(p.M, p.N), "gemm: too few counters");
       p.splitk = (int)splitk;
       p.ws = ws->data_ptr<float>();
       p.cnt = cnt->data_ptr<int>();
     }
-    if (q)
-      check(ldnn::gemm_q(p, a_kcontig, b_kcontig, (int)epi, out_f32, cur_stream(a)), "gemm_q");
-    else
-      check(ldnn::gemm_pp(p, a_kcontig, b_kcontig, (int)epi, out_f32, cur_stream(a)), "gemm_pp");
+    check(ldnn::gemm_q(p, a_kcontig, b_kcontig, (int)epi, out_f32, cur_stream(a)), "gemm_q");
     return;
   }
   if (ws.has_value() || cnt.has_value()) {
@@ -1517,9 +1513,9 @@ PYBIND11_MODULE(_C, m) {
                               (int64_t)ldnn::gemm_tiles128((int)M, (int)N));
       }, "(fp32 workspace elements, int32 counters) of a 128-tile split-K combine", py::arg("M"), py::arg("N"),
       py::arg("splitk"));
-  m.def("gemm_pp_ws", [](int64_t M, int64_t N, int64_t splitk) {
-        return std::make_pair((int64_t)(ldnn::gemm_pp_ws_bytes((int)M, (int)N, (int)splitk) / 4),
-                              (int64_t)ldnn::gemm_pp_tiles((int)M, (int)N));
+  m.def("gemm_q_ws", [](int64_t M, int64_t N, int64_t splitk) {
+        return std::make_pair((int64_t)(ldnn::gemm_q_ws_bytes((int)M, (int)N, (int)splitk) / 4),
+                              (int64_t)ldnn::gemm_q_tiles((int)M, (int)N));
       }, "(fp32 workspace elements, int32 counters) of a ping-pong 256-tile split-K combine", py::arg("M"),
       py::arg("N"), py::arg("splitk"));
   m.def("set_conv_impl", &ldnn::set_conv_impl, "0 = LDS-DMA fast path where it applies, 1 = generic kernel only",

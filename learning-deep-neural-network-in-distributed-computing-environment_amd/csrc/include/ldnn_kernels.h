@@ -78,16 +78,13 @@ hipError_t gemm_bf16(const GemmParams& p, bool a_kcontig, bool b_kcontig, int ep
 hipError_t gemm_bf16_tile(const GemmParams& p, bool a_kcontig, bool b_kcontig, int epi, bool out_f32, int tile,
                           hipStream_t s);
 int gemm_pick_tile(int M, int N, int K, bool out_f32);
-// Ping-pong 256x256 kernel (gemm_pp.hip): same contract; p.splitk > 1 needs the
-// in-launch combine workspace p.ws (gemm_pp_ws_bytes) and p.cnt (gemm_pp_tiles
-// zeroed counters).  Operands must each be < 2 GiB.
-hipError_t gemm_pp(const GemmParams& p, bool a_kcontig, bool b_kcontig, int epi, bool out_f32, hipStream_t s);
-size_t gemm_pp_ws_bytes(int M, int N, int splitk);
-int gemm_pp_tiles(int M, int N);
-// Four-wave 256x256 kernel (gemm_q.hip, 128x128 per wave): same contract as gemm_pp
-// (tiles = gemm_pp_tiles, split-K workspace gemm_q_ws_bytes).
+// Four-wave 256x256 kernel (gemm_q.hip, 128x128 per wave): same contract as
+// gemm_bf16; p.splitk > 1 needs the in-launch combine workspace p.ws
+// (gemm_q_ws_bytes) and p.cnt (gemm_q_tiles zeroed counters).  Operands must each
+// be < 2 GiB.
 hipError_t gemm_q(const GemmParams& p, bool a_kcontig, bool b_kcontig, int epi, bool out_f32, hipStream_t s);
 size_t gemm_q_ws_bytes(int M, int N, int splitk);
+int gemm_q_tiles(int M, int N);
 // Whether gemm_q beats gemm.hip's k256 on a 256-tile shape (measured on MI355X,
 // profiles/gemm_q_r2.txt: it loses at short K, where its one-wave-per-SIMD
 // prologue/epilogue is not amortised).

@@ -722,6 +722,7 @@ size_t gemm_q_ws_bytes(int M, int N, int splitk) {
   const size_t tiles = (size_t)((M + kq::BM - 1) / kq::BM) * ((N + kq::BN - 1) / kq::BN);
   return tiles * (size_t)splitk * (size_t)(64 * kq::kThreads * 16);
 }
+int gemm_q_tiles(int M, int N) { return ((M + kq::BM - 1) / kq::BM) * ((N + kq::BN - 1) / kq::BN); }
 
 hipError_t gemm_q(const GemmParams& p, bool a_kc, bool b_kc, int epi, bool out_f32, hipStream_t s) {
   if (p.M <= 0 || p.N <= 0) return hipSuccess;

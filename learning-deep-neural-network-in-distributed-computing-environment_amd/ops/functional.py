@@ -44,35 +44,6 @@ def _padded_rows_view(g: torch.Tensor, npad: int, zero_pad_guaranteed: bool = Tr
     return out
 
 
-# Split-K with the in-launch combine for Linear forwards whose 128-tile grid is tiny
-# and whose K loop is long, e.g. ResNet-18's 64 x 512 -> 1000 classifier (8 tiles of
-# 8 K-steps each).  The workspace and the (self-resetting) arrival counters persist
-# per (device, M, N, split) so graph replays reuse them.  Opt-in (LDNN_FC_SPLITK=1):
-# measured slower standalone (11.5 -> 12.0-15.2 us) and neutral in the ResNet-18 b64
-# step (profiles/r3s3/head_micro.jsonl); numerics: tests/test_layers_gpu.py.
-FC_SPLITK = __import__("os").environ.get("LDNN_FC_SPLITK", "0") != "0"
-_SPLITK_BUFS: dict = {}
-
-
-def _fc_splitk(M: int, N: int, K: int) -> int:
-    if not FC_SPLITK:
-        return 1
-    tiles = ((M + 127) // 128) * ((N + 127) // 128)
-    if tiles >= 64 or K < 256 or K % 64 or N <= 64:   # N <= 64: the skinny-N kernel's shapes
-        return 1
-    return max(1, min(K // 128, 64 // tiles, 8))
-
-
-def _splitk_buffers(C, dev, M: int, N: int, sk: int):
-    key = (dev, M, N, sk)
-    buf = _SPLITK_BUFS.get(key)
-    if buf is None:
-        ne, nc = C.gemm_splitk_ws(M, N, sk)
-        buf = (torch.empty(ne, dtype=torch.float32, device=dev), torch.zeros(nc, dtype=torch.int32, device=dev))
-        _SPLITK_BUFS[key] = buf
-    return buf
-
-
 class _LinearActNative(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, act, flat):
@@ -96,12 +67,10 @@ class _LinearActNative(torch.autograd.Function):
         else:
             b = torch.zeros(npad, dtype=torch.float32, device=x.device)
         epi = {None: C.EPI_BIAS, 0: C.EPI_BIAS_RELU, 1: C.EPI_BIAS_SIGMOID}[act]
-        sk = _fc_splitk(x2.shape[0], npad, kpad)
-        if sk > 1:
-            ws, cnt = _splitk_buffers(C, x.device, x2.shape[0], npad, sk)
-            C.gemm(x2, w, y, True, True, epi, bias=b, tile=128, splitk=sk, ws=ws, cnt=cnt)
-        else:
-            C.gemm(x2, w, y, True, True, epi, bias=b)
+        # (a split-K forward with the in-launch combine for the 64 x 512 -> 1000 classifier
+        # measured slower standalone and neutral in the ResNet-18 step: removed in round 4,
+        # profiles/r3s3/head_micro.jsonl)
+        C.gemm(x2, w, y, True, True, epi, bias=b)
         ctx.save_for_backward(x2, y)
         ctx.act, ctx.flat, ctx.weight, ctx.bias = act, flat, weight, bias
         ctx.xshape = x.shape

@@ -13,15 +13,10 @@ pytestmark = pytest.mark.gpu
 @pytest.mark.parametrize("act,fin,fout,batch", [("relu", 200, 84, 96), ("sigmoid", 200, 84, 96), ("none", 200, 84, 96),
                                                 ("none", 512, 1000, 64), ("relu", 512, 1000, 64),
                                                 ("none", 512, 1000, 256)])
-def test_native_linear_autograd(act, fin, fout, batch, monkeypatch):
-    """84 outputs: padded rows, 200 in; 512 -> 1000 at batch 64 / 256: the tiny-grid
-    split-K forward with the in-launch combine (ResNet-18's classifier)."""
+def test_native_linear_autograd(act, fin, fout, batch):
+    """84 outputs: padded rows, 200 in; 512 -> 1000 at batch 64 / 256: ResNet-18's
+    classifier."""
     from ldnn.models.layers import Linear
-    from ldnn.ops import functional as LF
-
-    monkeypatch.setattr(LF, "FC_SPLITK", True)
-    if fout == 1000:
-        assert LF._fc_splitk(batch, fout, fin) > 1
 
     torch.manual_seed(0)
     lin = Linear(fin, fout, activation=act)
