@@ -133,7 +133,11 @@ __global__ __launch_bounds__(256) void bn_reduce_kernel(const bf16_t* __restrict
                                                         int M, int C, int rpb, int lanes, int rl, BnFin fin,
                                                         const uint8_t* __restrict__ mask, int ncop,
                                                         const bf16_t* __restrict__ dy2 = nullptr) {
-  __shared__ float red[2][256 * 8];
+  // partials channel-major: element j of thread tid at red[k][j * (256 + lanes) + tid] --
+  // conflict-free stores (consecutive threads, consecutive words) and, with the
+  // (256 + lanes) stride, conflict-free per-channel reads for every lanes value
+  // (the thread-major [tid][8] image was an 8-way bank conflict on every store)
+  __shared__ float red[2][8 * 512];
   const int tid = threadIdx.x, lane = tid % lanes, rlane = tid / lanes;
   const int cv0 = blockIdx.x * 256 + lane;
   const int c0 = cv0 * 8;
@@ -163,22 +167,23 @@ __global__ __launch_bounds__(256) void bn_reduce_kernel(const bf16_t* __restrict
     }
     for (; r < r_end; r += rl) red_row<BWD, RELU, MASK>(x, dy, y, (size_t)r * C + c0, mu, is, s0, s1, mask, dy2);
   }
-  const int row = lanes * 8;
+  const int row = lanes * 8, js = 256 + lanes;
   if (rlane < rl) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      red[0][rlane * row + lane * 8 + j] = s0[j];
-      red[1][rlane * row + lane * 8 + j] = s1[j];
+      red[0][j * js + tid] = s0[j];
+      red[1][j * js + tid] = s1[j];
     }
   }
   __syncthreads();
-  for (int ch = tid; ch < row; ch += 256) {
+  for (int idx = tid; idx < row; idx += 256) {
+    const int j = idx / lanes, ln = idx - j * lanes;   // channel ln * 8 + j of this block
     float t0 = 0.f, t1 = 0.f;
     for (int q = 0; q < rl; ++q) {
-      t0 += red[0][q * row + ch];
-      t1 += red[1][q * row + ch];
+      t0 += red[0][j * js + q * lanes + ln];
+      t1 += red[1][j * js + q * lanes + ln];
     }
-    const int c = blockIdx.x * 2048 + ch;
+    const int c = blockIdx.x * 2048 + ln * 8 + j;
     float* accc = acc + (size_t)((blockIdx.x + gridDim.x * blockIdx.y) % ncop) * 2 * C;
     if (c < C) {
       bn_acc_add(accc + c, t0);
@@ -186,7 +191,7 @@ __global__ __launch_bounds__(256) void bn_reduce_kernel(const bf16_t* __restrict
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's atomics have completed
-  bn_finalize_last<BWD, kBnCopies>(fin, M, C, gridDim.x * gridDim.y, &red[0][0], 2 * 256 * 8, ncop);
+  bn_finalize_last<BWD, kBnCopies>(fin, M, C, gridDim.x * gridDim.y, &red[0][0], 2 * 8 * 512, ncop);
 }
 
 __global__ void bn_eval_coeff_kernel(const float* __restrict__ gamma, const float* __restrict__ beta,
@@ -310,7 +315,7 @@ __global__ __launch_bounds__(256) void bn_reduce_dual_kernel(const bf16_t* __res
                                                              const bf16_t* __restrict__ y,
                                                              const uint8_t* __restrict__ mask, int M, int C, int rpb,
                                                              int lanes, int rl, BnFin fin1, BnFin fin2, int ncop) {
-  __shared__ float red[3][256 * 8];
+  __shared__ float red[3][8 * 512];   // channel-major partials, see bn_reduce_kernel
   const int tid = threadIdx.x, lane = tid % lanes, rlane = tid / lanes;
   const int c0 = (blockIdx.x * 256 + lane) * 8;
   const bool active = rlane < rl && c0 < C;
@@ -349,27 +354,28 @@ __global__ __launch_bounds__(256) void bn_reduce_dual_kernel(const bf16_t* __res
       }
     }
   }
-  const int wrow = lanes * 8;
+  const int wrow = lanes * 8, js = 256 + lanes;
   if (rlane < rl) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      red[0][rlane * wrow + lane * 8 + j] = s0[j];
-      red[1][rlane * wrow + lane * 8 + j] = s1[j];
-      red[2][rlane * wrow + lane * 8 + j] = s2[j];
+      red[0][j * js + tid] = s0[j];
+      red[1][j * js + tid] = s1[j];
+      red[2][j * js + tid] = s2[j];
     }
   }
   __syncthreads();
   const int cp = (blockIdx.x + gridDim.x * blockIdx.y) % ncop;
   float* acc1 = fin1.acc + (size_t)cp * 2 * C;
   float* acc2 = fin2.acc + (size_t)cp * 2 * C;
-  for (int ch = tid; ch < wrow; ch += 256) {
+  for (int idx = tid; idx < wrow; idx += 256) {
+    const int j = idx / lanes, ln = idx - j * lanes;
     float t0 = 0.f, t1 = 0.f, t2 = 0.f;
     for (int q = 0; q < rl; ++q) {
-      t0 += red[0][q * wrow + ch];
-      t1 += red[1][q * wrow + ch];
-      t2 += red[2][q * wrow + ch];
+      t0 += red[0][j * js + q * lanes + ln];
+      t1 += red[1][j * js + q * lanes + ln];
+      t2 += red[2][j * js + q * lanes + ln];
     }
-    const int c = blockIdx.x * 2048 + ch;
+    const int c = blockIdx.x * 2048 + ln * 8 + j;
     if (c < C) {
       bn_acc_add(acc1 + c, t0);
       bn_acc_add(acc1 + C + c, t1);
@@ -379,9 +385,9 @@ __global__ __launch_bounds__(256) void bn_reduce_dual_kernel(const bf16_t* __res
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's atomics have completed
   const int nblk = gridDim.x * gridDim.y;
-  bn_finalize_last<true, kBnCopies>(fin1, M, C, nblk, &red[0][0], 3 * 256 * 8, ncop);
+  bn_finalize_last<true, kBnCopies>(fin1, M, C, nblk, &red[0][0], 3 * 8 * 512, ncop);
   __syncthreads();
-  bn_finalize_last<true, kBnCopies>(fin2, M, C, nblk, &red[0][0], 3 * 256 * 8, ncop);
+  bn_finalize_last<true, kBnCopies>(fin2, M, C, nblk, &red[0][0], 3 * 8 * 512, ncop);
 }
 
 // dx = A1 g + B1 x + D1, dr = A2 g + B2 r + D2
@@ -687,7 +693,10 @@ __global__ __launch_bounds__(256) void bn_maxpool_bwd_reduce_kernel(
     const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy, const bf16_t* __restrict__ dy2,
     const uint8_t* __restrict__ arg, const float* __restrict__ mean, const float* __restrict__ invstd,
     float* __restrict__ acc, int N, int H, int W, int C, int P, int Q, BnFin fin, int ncop) {
-  __shared__ float red[2][256 * 8];
+  // channel-major partials: element t of thread tid at red[k][t * 264 + tid] (consecutive
+  // threads store consecutive words; the 264 = 8 mod 64 stride keeps the reads conflict-free)
+  constexpr int kS = 264;
+  __shared__ float red[2][8 * kS];
   const int cv = C / 8;
   const int tid = threadIdx.x;
   const int j = blockIdx.x * blockDim.x + tid;
@@ -732,8 +741,8 @@ __global__ __launch_bounds__(256) void bn_maxpool_bwd_reduce_kernel(
   }
 #pragma unroll
   for (int t = 0; t < 8; ++t) {
-    red[0][tid * 8 + t] = s0[t];
-    red[1][tid * 8 + t] = s1[t];
+    red[0][t * kS + tid] = s0[t];
+    red[1][t * kS + tid] = s1[t];
   }
   __syncthreads();
   float* accc = acc + (size_t)((blockIdx.x + gridDim.x * blockIdx.y) % ncop) * 2 * C;
@@ -741,14 +750,14 @@ __global__ __launch_bounds__(256) void bn_maxpool_bwd_reduce_kernel(
     const int g8 = ch >> 3, t = ch & 7;
     float t0 = 0.f, t1 = 0.f;
     for (int k = g8; k < 256; k += cv) {
-      t0 += red[0][k * 8 + t];
-      t1 += red[1][k * 8 + t];
+      t0 += red[0][t * kS + k];
+      t1 += red[1][t * kS + k];
     }
     bn_acc_add(accc + ch, t0);
     bn_acc_add(accc + C + ch, t1);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's atomics have completed
-  bn_finalize_last<true, kBnCopies>(fin, N * H * W, C, gridDim.x * gridDim.y, &red[0][0], 2 * 256 * 8, ncop);
+  bn_finalize_last<true, kBnCopies>(fin, N * H * W, C, gridDim.x * gridDim.y, &red[0][0], 2 * 8 * kS, ncop);
 }
 
 // backward apply: dx = A g + B x + D, same 2x2-block threads

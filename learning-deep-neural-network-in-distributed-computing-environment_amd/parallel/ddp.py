@@ -143,7 +143,7 @@ class GradBucketer:
         self.works: list = []
         self._pending: list[int] = []
         self._launched: list[bool] = []
-        self._gathers: list = []
+        self._gathers: dict = {}   # sharded bucket -> its in-flight weight all-gather
         self.active = False
         self.master_whole = True
         flat.add_ready_hook(self._on_ready)
@@ -251,14 +251,24 @@ class GradBucketer:
             b = self.buckets[i]
             if b["sharded"]:
                 lo, hi = self.shard_range(i)
-                self._gathers.append(self.comm.all_gather_into(t[b["begin"]: b["end"]], t[lo:hi], async_op=True))
+                self._gathers[i] = self.comm.all_gather_into(t[b["begin"]: b["end"]], t[lo:hi], async_op=True)
 
-    def wait_gathers(self):
-        """Order the current stream after the weight all-gathers (no host sync with RCCL)."""
-        for w in self._gathers:
+    def wait_gathers(self, buckets=None):
+        """Order the current stream after the weight all-gathers of ``buckets`` (default:
+        all in flight) -- a stream wait with RCCL, no host sync."""
+        for i in (list(self._gathers) if buckets is None else buckets):
+            w = self._gathers.pop(i, None)
             if w is not None:
                 w.wait()
-        self._gathers = []
+
+    def buckets_of(self, params) -> list[int]:
+        """Sharded bucket indices holding any of ``params``."""
+        out = []
+        for p in params:
+            i = self.of_param.get(id(p))
+            if i is not None and self.buckets[i]["sharded"] and i not in out:
+                out.append(i)
+        return out
 
     @torch.no_grad()
     def gather_master(self, optimizer=None):

@@ -52,6 +52,52 @@ class StandInComm:
         return _Join(self.side)
 
 
+class ShardProbeComm:
+    """A world-of-``world`` stand-in communicator on ONE GPU for the sharded step
+    (DataParallel(shard_optimizer=True)): the bucket layout, shard ranges and every
+    collective call site are the real ones, but each reduce-scatter / all-gather is
+    the stand-in copy (RCCL's stream behaviour and footprint) of the bytes that
+    collective moves over xGMI, (N-1)/N of its full buffer.  Numerics are not
+    meaningful (nothing is summed); the timing is."""
+
+    device_collectives = True
+
+    def __init__(self, device, world: int = 8, reps: int = 4, blocks: int = 16):
+        from .comm import Comm
+
+        self._rec = Comm()
+        self.rank, self.world_size = 0, int(world)
+        self.standin = StandInComm(device, reps, blocks)
+        self._k = 0
+
+    def record(self, *a, **k):
+        return self._rec.record(*a, **k)
+
+    def schedule_digest(self):
+        return self._rec.schedule_digest()
+
+    def _moved(self, t):
+        n = t.numel() * (self.world_size - 1) // self.world_size // 8 * 8
+        v = t.view(-1)[:max(n, 8)]
+        return v if v.dtype == torch.float32 else v.view(torch.float32)   # (bf16 weights: same bytes)
+
+    def reduce_scatter(self, out, inp, async_op=False):
+        self._k += 1
+        return self.standin(("rs", inp.data_ptr()), self._moved(inp))
+
+    def all_gather_into(self, out, inp, async_op=False):
+        return self.standin(("ag", out.data_ptr()), self._moved(out))
+
+    def all_reduce(self, t, op="sum", async_op=False):
+        return self.standin(("ar", t.data_ptr()), t if t.dtype == torch.float32 else t.view(torch.float32))
+
+    def broadcast(self, t, src=0):
+        return None
+
+    def barrier(self):
+        return None
+
+
 def _timed(fn, steps):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -62,7 +108,13 @@ def _timed(fn, steps):
 
 
 def measure_overlap(model_name: str, batch: int, bucket_mb: float = 32.0, reps: int = 4, steps: int = 20,
-                    rounds: int = 3, blocks: int = 16) -> dict:
+                    rounds: int = 3, blocks: int = 16, shard_world: int = 0, optimizer: str = "sgd") -> dict:
+    """shard_world > 0: the sharded step (reduce-scatter between backward links, sharded
+    optimizer, bf16 weight all-gathers waited by the forward links) on a
+    ShardProbeComm of that world size; the stand-ins then cover the reduce-scatter
+    AND the all-gather bytes of each bucket."""
+    if shard_world:
+        return _measure_sharded(model_name, batch, bucket_mb, reps, steps, rounds, blocks, shard_world, optimizer)
     import ldnn
     from ldnn.data.datasets import SHAPES
     from ldnn.models import CrossEntropyLoss, build_model, dataset_for, xavier_init
@@ -117,6 +169,79 @@ def measure_overlap(model_name: str, batch: int, bucket_mb: float = 32.0, reps: 
             "hidden_fraction": round(hidden / max(best["standin_alone_ms"], 1e-9), 3)}
 
 
+def _measure_sharded(model_name, batch, bucket_mb, reps, steps, rounds, blocks, world, optimizer):
+    import ldnn
+    from ldnn.data.datasets import SHAPES
+    from ldnn.models import CrossEntropyLoss, build_model, dataset_for, xavier_init
+    from ldnn.optim import SGD, Adam
+    from ldnn.parallel.ddp import DataParallel
+    from ldnn.train.graphed import GraphedDPStep, GraphedStep
+
+    dev = torch.device("cuda", torch.cuda.current_device())
+    shape = SHAPES[dataset_for(model_name)]
+    nc = 1000 if model_name == "resnet18" else 10
+    g = torch.Generator(device=dev).manual_seed(0)
+    x = torch.randn(batch, *shape, device=dev, generator=g).bfloat16()
+    y = torch.randint(0, nc, (batch,), device=dev, generator=g)
+    crit = CrossEntropyLoss()
+
+    def opt_for(m):
+        return SGD(m.parameters(), lr=0.01, momentum=0.9) if optimizer == "sgd" else Adam(m.parameters(), lr=1e-3)
+
+    # the comm-free single-process step
+    torch.manual_seed(0)
+    m1 = build_model(model_name)
+    xavier_init(m1)
+    ldnn.prepare(m1, dev)
+    o1 = opt_for(m1)
+    o1.zero_grad()
+    crit(m1(x), y).backward()
+    o1.step()
+    single = GraphedStep(m1, crit, o1, x, y, warmup=0)
+    # the sharded step with stand-in collectives
+    torch.manual_seed(0)
+    m = build_model(model_name)
+    xavier_init(m)
+    ldnn.prepare(m, dev)
+    comm = ShardProbeComm(dev, world, reps, blocks)
+    dp = DataParallel(m, comm, bucket_cap_mb=bucket_mb, broadcast_init=False, shard_optimizer=True)
+    o = opt_for(m)
+    o.zero_grad()
+    crit(dp(x), y).backward()
+    dp.finish_gradient_sync()
+    o.step()
+    dp.wait_gathers()
+    gd = GraphedDPStep(dp, crit, o, x, y)
+    bk = dp.bucketer
+
+    def standin_alone():   # every collective of one step, back to back on the side stream
+        joins = []
+        for i, b in enumerate(bk.buckets):
+            joins.append(bk.collective(i))
+        bk.issue_gathers()
+        for j in joins:
+            if j is not None:
+                j.wait()
+        bk.wait_gathers()
+
+    fns = {"single_ms": lambda: single(x, y), "with_standin_ms": lambda: gd(x, y), "standin_alone_ms": standin_alone}
+    for f in fns.values():
+        for _ in range(3):
+            f()
+    best = {k: 1e9 for k in fns}
+    for _ in range(rounds):
+        for k, f in fns.items():
+            best[k] = min(best[k], _timed(f, steps))
+    hidden = best["single_ms"] + best["standin_alone_ms"] - best["with_standin_ms"]
+    return {"model": model_name, "batch": batch, "mode": f"sharded (world {world} stand-in)", "optimizer": optimizer,
+            "bucket_mb": bucket_mb, "buckets": len(bk.buckets),
+            "sharded_buckets": sum(1 for b in bk.buckets if b["sharded"]),
+            "bucket_mb_each": [round((b["end"] - b["begin"]) * 4 / 2**20, 2) for b in bk.buckets],
+            "segments": gd.n_segments, "forward_waits": sum(1 for w in gd.waits if w), "standin_reps": reps,
+            "standin_blocks": blocks, **{k: round(v, 4) for k, v in best.items()}, "hidden_ms": round(hidden, 4),
+            "hidden_fraction": round(hidden / max(best["standin_alone_ms"], 1e-9), 3)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="resnet18")
@@ -125,8 +250,11 @@ def main():
     ap.add_argument("--reps", type=int, default=4)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--blocks", type=int, default=16)
+    ap.add_argument("--shard", type=int, default=0, help="world size of the sharded-step probe (0 = all-reduce step)")
+    ap.add_argument("--optimizer", choices=["sgd", "adam"], default="sgd")
     a = ap.parse_args()
-    print(json.dumps(measure_overlap(a.model, a.batch, a.bucket_mb, a.reps, a.steps, blocks=a.blocks)), flush=True)
+    print(json.dumps(measure_overlap(a.model, a.batch, a.bucket_mb, a.reps, a.steps, blocks=a.blocks,
+                                     shard_world=a.shard, optimizer=a.optimizer)), flush=True)
 
 
 if __name__ == "__main__":

@@ -200,6 +200,18 @@ class GraphedDPStep:
         self._pool = torch.cuda.graph_pool_handle()
         self._stream = torch.cuda.Stream(device=self.x.device)
         self._stream.wait_stream(torch.cuda.current_stream())
+        # sharded DP: the forward is cut too, right before the first module that reads a
+        # sharded bucket's weights; a replay waits for that bucket's all-gather (issued
+        # after the previous step's optimizer, in forward order) only there, so the
+        # gathers of the deep layers' big weights run beside the shallow layers' forward
+        self.waits: list = []      # buckets whose weight all-gather graph G_j waits for
+        self._fwd_hooks = []
+        self._fwd_seen: set = set()
+        if self.bk.shard:
+            for mod in self.model.modules():
+                own = [p for p in mod.parameters(recurse=False)]
+                if own and self.bk.buckets_of(own):
+                    self._fwd_hooks.append(mod.register_forward_pre_hook(self._on_forward))
         self._set_capture(True)
         try:
             self._cap = {"pending": [len(b["params"]) for b in self.bk.buckets], "fired": [False] * nb,
@@ -227,6 +239,9 @@ class GraphedDPStep:
         finally:
             self._cap = None
             self._set_capture(False)
+            for h in self._fwd_hooks:
+                h.remove()
+            self._fwd_hooks = []
         torch.cuda.current_stream().wait_stream(self._stream)
         self._sync_lr(force=True)
 
@@ -234,6 +249,19 @@ class GraphedDPStep:
     def _set_capture(self, on: bool):
         if isinstance(self.optimizer, _FlatOptimizer):
             self.optimizer._ldnn_capturing = on
+
+    def _on_forward(self, mod, args):
+        """(capture) module ``mod`` is about to read its weights: cut the chain before it
+        when one of its sharded buckets has not been waited for in this forward yet."""
+        if self._cap is None:
+            return
+        need = [b for b in self.bk.buckets_of(mod.parameters(recurse=False)) if b not in self._fwd_seen]
+        if not need:
+            return
+        self._fwd_seen.update(need)
+        self._end()
+        self._begin()
+        self.waits[-1] = need   # waited before the link that starts here
 
     def _begin(self):
         # relaxed: a link of the chain begins on one thread (main / autograd) and may end
@@ -243,6 +271,7 @@ class GraphedDPStep:
         g = torch.cuda.CUDAGraph()
         g.capture_begin(pool=self._pool, capture_error_mode="relaxed")
         self._cur = g
+        self.waits.append([])
 
     def _end(self):
         import warnings
@@ -320,12 +349,13 @@ class GraphedDPStep:
     def __call__(self, x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
         if x.shape != self.x.shape or y.shape != self.y.shape:
             return self._eager_step(x, y)
-        self.bk.wait_gathers()   # the previous sharded step's weight all-gathers (stream waits)
         self.x.copy_(x, non_blocking=True)
         self.y.copy_(y, non_blocking=True)
         self._sync_lr()
         works = []
         for j, g in enumerate(self.graphs):
+            if self.waits[j]:
+                self.bk.wait_gathers(self.waits[j])   # this link's first reads of those buckets' weights
             if not self._empty[j]:
                 g.replay()
             issue = self.issue[j]
@@ -336,6 +366,7 @@ class GraphedDPStep:
         for w in works:
             if w is not None:
                 w.wait()
+        self.bk.wait_gathers()   # (any gather no forward link waited for) before the optimizer writes
         self.g_opt.replay()
         if self.bk.shard:
             self.bk.master_whole = False
