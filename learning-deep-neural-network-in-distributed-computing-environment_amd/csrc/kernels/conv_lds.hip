@@ -1807,8 +1807,10 @@ int small_m_splits(int tiles, int nk) {
 // per slice, at most 32 slices.
 int slab_splits(int tiles, int nk) {
   if (tiles >= 160 || nk < 8) return 1;
-  int sp = (512 + tiles - 1) / tiles;
-  sp = std::min(sp, nk / 3);
+  static const int target = env_int("LDNN_CONV_SLAB_TARGET", 512);     // workgroups to aim for (A/B knob)
+  static const int min_kt = env_int("LDNN_CONV_SLAB_MIN_KT", 3);        // K-tiles per slice at least (A/B knob)
+  int sp = (target + tiles - 1) / tiles;
+  sp = std::min(sp, nk / std::max(1, min_kt));
   sp = std::min(sp, 32);
   return sp < 2 ? 1 : sp;
 }

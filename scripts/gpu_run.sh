@@ -19,6 +19,16 @@ for step in "$@"; do
     bench) $T 600 python -u bench.py > $O/bench.json 2> $O/bench.err ;;
     iso) $T 300 python -u scripts/debug/stem_isolation.py > $O/stem_isolation.jsonl 2>&1 ;;
     det:*) a=${step#det:}; $T 300 python -u scripts/debug/determinism_probe.py --model ${a%%@*} --hw ${a##*@} >> $O/determinism.jsonl 2>&1 ;;
+    probe:*) a=${step#probe:}; m=${a%%@*}; r=${a#*@}; b=${r%%@*}; sh=${r#*@}; [ "$sh" = "$r" ] && sh=0
+             $T 300 python -u scripts/overlap_probe.py --model $m --batch $b --shard $sh ${PROBE_ARGS:-} \
+             >> $O/overlap_probe.jsonl 2>> $O/overlap_probe.err ;;
+    micro:*) m=${step#micro:}; rc=0
+             for e in ${MICRO_ENVS:-X=0}; do
+               echo "{\"env\": \"$e\"}" >> $O/micro_$m.jsonl
+               env $e $T 300 python -u scripts/conv_micro.py --model $m --no-stock >> $O/micro_$m.jsonl 2>> $O/micro.err || { rc=$?; break; }
+             done; (exit $rc) ;;
+    ab:*) a=${step#ab:}; rm -f gpurun_out/ab_cnn.jsonl; $T 900 bash scripts/ab_cnn.sh "${a//,/ }" ${AB_ENVS:-X=0} > $O/ab.txt 2>&1
+          rc=$?; cp -f gpurun_out/ab_cnn.jsonl $O/ 2>/dev/null; (exit $rc) ;;
     cnn:*) a=${step#cnn:}; $T 300 python -u scripts/bench_cnn.py --model ${a%%@*} --batch ${a##*@} --graph --no-stock \
              >> $O/cnn.jsonl 2>> $O/cnn.err ;;
     prof:*) a=${step#prof:}; $T 400 rocprofv3 --kernel-trace --stats -d $O/prof_$a -o run -- \
