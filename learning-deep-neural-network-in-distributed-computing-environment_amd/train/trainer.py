@@ -55,7 +55,7 @@ def _progress(it, enabled, desc):
 def train_local_epoch(model, trainloader, criterion, optimizer, device, scheduler=None, *, dp=None,
                       step_aggregator=None, cutoff: StragglerCutoff | None = None, max_steps: int | None = None,
                       step_scheduler: bool = True, timer: PhaseTimer | None = None, graphs: bool = False,
-                      check_comm=None, check_every: int = 50):
+                      check_comm=None, check_every: int = 50, dp_tail: bool = False):
     """One pass over the rank's shard.  Returns (mean loss, accuracy %, per-batch losses).
 
     ``timer`` (utils.tracing.PhaseTimer) brackets forward / backward / grad_sync /
@@ -66,6 +66,11 @@ def train_local_epoch(model, trainloader, criterion, optimizer, device, schedule
     (GraphedDPStep).
     ``check_comm``: with per-step synchronisation, cross-check the ranks' collective
     schedules every ``check_every`` steps (Comm.check_schedule).
+    ``dp_tail`` (per-step DP, shards of unequal batch counts): after the ``max_steps``
+    common steps every rank runs ONE more sample-count-weighted step on its next batch,
+    or -- its shard exhausted -- a zero-weight step that only takes part in the
+    collectives, so no rank's samples are dropped beyond one batch (the reference trains
+    every batch of its shard, BAR/trainer.py:202-216).
     """
     from .engine_adapter import EngineModule, engine_local_epoch
 
@@ -83,11 +88,33 @@ def train_local_epoch(model, trainloader, criterion, optimizer, device, schedule
     total, done = 0, 0
     ldnn_ce = isinstance(criterion, LdnnCE)
     use_graph = (graphs and dev.type == "cuda" and step_aggregator is None and ldnn_ce and timer is None)
+    # equal-average per-step DP: the epoch's LAST step may be short on some ranks (shards of
+    # unequal length, the trailing partial batch).  Every rank exchanges its sample count
+    # there and scales its loss by n_rank * N / n_total, so the 1/N-averaged gradient is the
+    # mean over all ranks' samples -- what one process on the concatenated batch computes
+    # (static-engine twin: StaticMLPEngine.dp_tail_step).
+    weigh_last = (dp is not None and dp.comm.world_size > 1 and step_aggregator is None
+                  and not getattr(dp.bucketer, "weighted", False))
+
+    def weight_of(n):
+        cnt = torch.tensor([float(n)], dtype=torch.float32, device=dev)
+        dp.comm.all_reduce(cnt, SUM)
+        return n * dp.comm.world_size / max(float(cnt.item()), 1.0)
+
+    dp_tail = dp_tail and weigh_last
+    it = iter(trainloader)
+    batches = ((i, b) for i, b in enumerate(it))
+    last = pending = None
     try:
-        for i, (x, y) in enumerate(trainloader):
+        for i, (x, y) in batches:
             if i >= nb:
+                pending = (x, y)   # (the tail step's batch, already drawn from the iterator)
                 break
-            if use_graph and (i > 0 or getattr(model, "_ldnn_graphed", None) is not None):
+            last = (x, y)
+            scale = 1.0
+            if weigh_last and i == nb - 1:
+                scale = weight_of(y.numel())
+            if use_graph and scale == 1.0 and (i > 0 or getattr(model, "_ldnn_graphed", None) is not None):
                 # the first batch ran eagerly (momentum / optimizer state exist), so the
                 # capture needs no extra warmup steps and training semantics are unchanged
                 gs = _graphed_step(model, criterion, optimizer, x, y, dp)
@@ -110,7 +137,7 @@ def train_local_epoch(model, trainloader, criterion, optimizer, device, schedule
                     with torch.no_grad():
                         stats[1] += (out.argmax(1) == y).sum()
             with tm.phase("backward"):
-                loss.backward()
+                (loss if scale == 1.0 else loss * scale).backward()
             if dp is not None or step_aggregator is not None:
                 with tm.phase("grad_sync"):
                     if dp is not None:
@@ -126,6 +153,25 @@ def train_local_epoch(model, trainloader, criterion, optimizer, device, schedule
                 cutoff.step(i)
             if check_comm is not None and (i + 1) % check_every == 0:
                 check_comm.check_schedule(f"step {i + 1}", dev if check_comm.device_collectives else None)
+        if dp_tail and last is not None:
+            nxt = pending if pending is not None else next(it, None)
+            x, y = nxt if nxt is not None else last
+            n = y.numel() if nxt is not None else 0
+            scale = weight_of(n)
+            optimizer.zero_grad()
+            out = model(x)
+            st = stats if n else torch.zeros_like(stats)   # a zero-weight step adds no statistics
+            loss = criterion(out, y, st) if ldnn_ce else criterion(out.float(), y)
+            if n and not ldnn_ce:
+                with torch.no_grad():
+                    stats[1] += (out.argmax(1) == y).sum()
+            (loss * scale).backward()
+            dp.finish_gradient_sync()
+            optimizer.step()
+            if n:
+                losses = torch.cat([losses[:done], loss.detach().float().reshape(1)])
+                total += n
+                done += 1
     except StopLocalTraining:
         if step_scheduler and scheduler is not None:
             scheduler.step()
@@ -264,12 +310,14 @@ def train_global(model, trainloader, val_loader, trainset, valset, indices_train
         t_start = time.perf_counter()
         cutoff.reset()
         max_steps = None
+        dp_tail = False
         if sync_every == "step" and N > 1 or getattr(model, "engine", None) is not None and model.engine.distributed:
             # per-step collectives need the same number of steps on every rank
             nsteps = model.full_batches(trainloader) if hasattr(model, "full_batches") else len(trainloader)
-            t = torch.tensor([float(nsteps)], device=dev)
+            t = torch.tensor([float(nsteps), -float(nsteps)], device=dev)
             comm.all_reduce(t, MIN)
-            max_steps = int(t.item())
+            max_steps = int(t[0].item())
+            dp_tail = -int(t[1].item()) > max_steps   # a rank holds more batches: one weighted tail step
         records, batch_losses, samples = [], [], 0
         for local_epoch in range(num_local_epochs):
             try:
@@ -277,7 +325,7 @@ def train_global(model, trainloader, val_loader, trainset, valset, indices_train
                                                   step_aggregator=step_aggregator, cutoff=cutoff,
                                                   max_steps=max_steps, timer=timer, graphs=graphs,
                                                   check_comm=comm if (sync_every == "step" and N > 1) else None,
-                                                  check_every=max(check_every, 1) * 5)
+                                                  check_every=max(check_every, 1) * 5, dp_tail=dp_tail)
             except StopLocalTraining:
                 # cut by the collective time limit: keep LR schedules aligned across ranks
                 for _ in range(num_local_epochs - local_epoch - 1):

@@ -29,6 +29,13 @@ for step in "$@"; do
              done; (exit $rc) ;;
     ab:*) a=${step#ab:}; rm -f gpurun_out/ab_cnn.jsonl; $T 900 bash scripts/ab_cnn.sh "${a//,/ }" ${AB_ENVS:-X=0} > $O/ab.txt 2>&1
           rc=$?; cp -f gpurun_out/ab_cnn.jsonl $O/ 2>/dev/null; (exit $rc) ;;
+    microprof:*) m=${step#microprof:}; (cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+             $T 400 rocprofv3 --kernel-trace --stats -d $O/microprof_$m -o run -- \
+             python -u scripts/conv_micro.py --model $m --no-stock --iters 20 > $O/microprof_$m.txt 2>&1) ;;
+    micropmc:*) m=${step#micropmc:}; (cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+             timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
+               SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d $O/micropmc_$m -o run -- \
+             python -u scripts/conv_micro.py --model $m --no-stock --iters 5 > $O/micropmc_$m.txt 2>&1) ;;
     cnn:*) a=${step#cnn:}; $T 300 python -u scripts/bench_cnn.py --model ${a%%@*} --batch ${a##*@} --graph --no-stock \
              >> $O/cnn.jsonl 2>> $O/cnn.err ;;
     prof:*) a=${step#prof:}; $T 400 rocprofv3 --kernel-trace --stats -d $O/prof_$a -o run -- \

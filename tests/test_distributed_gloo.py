@@ -304,3 +304,64 @@ def test_oneshot_setup_failure_on_one_rank_disables_everywhere_without_hanging()
     mp.spawn(_oneshot_setup_worker, args=(world, port, q), nprocs=world, join=True)
     res = sorted(q.get() for _ in range(world))
     assert res == [(0, True, True), (1, True, True)]
+
+
+def _tail_worker(rank, world, port, out, shard):
+    _init(rank, world, port)
+    import ldnn
+    from ldnn.models.layers import CrossEntropyLoss
+    from ldnn.models.mlp import mlp2
+    from ldnn.optim import SGD
+    from ldnn.parallel.comm import TorchComm
+    from ldnn.parallel.ddp import DataParallel
+    from ldnn.train.trainer import train_local_epoch
+
+    torch.manual_seed(5)
+    m = mlp2(784, 32, 10)
+    ldnn.prepare(m, "cpu")
+    dp = DataParallel(m, TorchComm(), bucket_cap_mb=0.001, shard_optimizer=shard)
+    opt = SGD(m.parameters(), lr=0.1, momentum=0.9)
+    g = torch.Generator().manual_seed(9)
+    x, y = torch.randn(258, 784, generator=g), torch.randint(0, 10, (258,), generator=g)
+    lo, hi = (0, 130) if rank == 0 else (130, 258)
+    xs, ys = x[lo:hi], y[lo:hi]
+    batches = [(xs[i:i + 64], ys[i:i + 64]) for i in range(0, hi - lo, 64)]
+    n = torch.tensor([float(len(batches)), -float(len(batches))])
+    dist.all_reduce(n, op=dist.ReduceOp.MIN)
+    steps, tail = int(n[0]), -int(n[1]) > int(n[0])
+    _, _, bl = train_local_epoch(dp, batches, CrossEntropyLoss(), opt, "cpu", dp=dp, max_steps=steps, dp_tail=tail)
+    dp.gather_master(opt)
+    if rank == 0:
+        torch.save({"sd": {k: v.clone() for k, v in m.state_dict().items()}, "n_losses": len(bl),
+                    "samples": train_local_epoch.last_samples}, out)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("shard", [False, True])
+def test_per_step_dp_trains_the_partial_batch_weighted(tmp_path, shard):
+    """VERDICT r3 #7, autograd path: shards of 130 and 128 samples at batch 64 on 2 gloo
+    ranks -- two common steps, then ONE sample-count-weighted tail step (rank 0's 2
+    leftover samples; rank 1, exhausted, takes part with weight 0) -- end with exactly
+    the parameters of one process on the 258 samples at batch 128 (3 steps, the last
+    one on the 2 leftover samples).  Nothing is dropped."""
+    world, port, out = 2, _port(), str(tmp_path / "tail.pt")
+    mp.spawn(_tail_worker, args=(world, port, out, shard), nprocs=world, join=True)
+    sys.path.insert(0, ROOT)
+    import ldnn
+    from ldnn.models.mlp import mlp2
+    from ldnn.optim import SGD
+
+    torch.manual_seed(5)
+    m = mlp2(784, 32, 10)
+    ldnn.prepare(m, "cpu")
+    opt = SGD(m.parameters(), lr=0.1, momentum=0.9)
+    g = torch.Generator().manual_seed(9)
+    x, y = torch.randn(258, 784, generator=g), torch.randint(0, 10, (258,), generator=g)
+    for idx in ([*range(0, 64), *range(130, 194)], [*range(64, 128), *range(194, 258)], [128, 129]):
+        opt.zero_grad()
+        torch.nn.functional.cross_entropy(m(x[idx]), y[idx]).backward()
+        opt.step()
+    got = torch.load(out, weights_only=True)
+    assert got["n_losses"] == 3 and got["samples"] == 130
+    for k, v in m.state_dict().items():
+        torch.testing.assert_close(got["sd"][k], v, rtol=1e-5, atol=1e-6)
