@@ -417,8 +417,16 @@ def main():
     rec["rccl_ranks"] = n if ctx.backend == "nccl" else 0
     rec.update(extra)
     if not args.no_configs:
-        rec["configs"] = {f"{name}_b{b}" + ("_adam" if o == "adam" else ""): run_cnn(ctx, name, b, st, o)
-                          for name, b, st, o in CNN_CONFIGS}
+        rec["configs"] = {}
+        for name, b, st, o in CNN_CONFIGS:
+            key = f"{name}_b{b}" + ("_adam" if o == "adam" else "")
+            try:
+                rec["configs"][key] = run_cnn(ctx, name, b, st, o)
+            except Exception as e:  # noqa: BLE001 -- a secondary config must not cost the headline record
+                if ctx.world_size > 1:   # every rank fails the same config together (or the job aborts)
+                    dist.barrier()
+                rec["configs"][key] = {"error": f"{type(e).__name__}: {e}"[:500]}
+                torch.cuda.empty_cache()
     if args.compare_stock:
         el_s = run_stock(ctx, args)
         stock = args.batch * n * args.steps / el_s

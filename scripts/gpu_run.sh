@@ -17,6 +17,7 @@ for step in "$@"; do
     tests:*) $T 600 $PYT -m gpu ${step#tests:} > $O/tests_$(basename ${step#tests:} .py).txt 2>&1 ;;
     smoke) $T 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 ;;
     bench) $T 600 python -u bench.py > $O/bench.json 2> $O/bench.err ;;
+    benchgloo) $T 600 python -u bench.py --gpus 2 --backend gloo --steps 5 --warmup 2 > $O/bench_gloo2.json 2> $O/bench_gloo2.err ;;
     iso) $T 300 python -u scripts/debug/stem_isolation.py > $O/stem_isolation.jsonl 2>&1 ;;
     det:*) a=${step#det:}; $T 300 python -u scripts/debug/determinism_probe.py --model ${a%%@*} --hw ${a##*@} >> $O/determinism.jsonl 2>&1 ;;
     probe:*) a=${step#probe:}; m=${a%%@*}; r=${a#*@}; b=${r%%@*}; sh=${r#*@}; [ "$sh" = "$r" ] && sh=0
