@@ -231,7 +231,7 @@ def test_conv_epilogue_bn_statistics_layer_vs_fp32(N, Cin, H, Cout, stride, monk
     running statistics, outputs, dgamma / dbeta / dx, and dW against an fp32 oracle
     that stores the conv output and its gradient in bf16 (as every bf16 pipeline does;
     see tests/test_bn_pool_gpu.py::test_resnet_stem_fused_bn_pool_vs_fp32_oracle for
-    why dW is compared against that oracle).  Layer-level and seeded: well
+    why dW is held to that oracle's error).  Layer-level and seeded: well
     conditioned, unlike the model-level gradients of round 3."""
     import ldnn.models.layers as layers_mod
     from ldnn.models.layers import BatchNorm2d, Conv2d
@@ -298,7 +298,9 @@ def test_conv_epilogue_bn_statistics_layer_vs_fp32(N, Cin, H, Cout, stride, monk
     assert rel(dgp, dgr) < 3e-2, rel(dgp, dgr)
     assert rel(dbp, dbr) < 3e-2, rel(dbp, dbr)
     assert rel(dxp, dxr) < 3e-2, rel(dxp, dxr)
-    assert rel(dwp, dwe) < 4e-2, rel(dwp, dwe)
+    # dW: a small difference of large terms after the BN (sum(dx * c) = 0 per channel) --
+    # within twice the error of an fp32 pipeline that only stores in bf16
+    assert rel(dwp, dwr) < 2.0 * rel(dwe, dwr) + 1e-2, (rel(dwp, dwr), rel(dwe, dwr))
 
 
 @pytest.mark.parametrize("name,shape", [("resnet18", (16, 3, 112, 112)), ("enhanced_cnn", (64, 3, 32, 32))])
