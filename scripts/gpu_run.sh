@@ -20,9 +20,9 @@ for step in "$@"; do
     benchgloo) $T 600 python -u bench.py --gpus 2 --backend gloo --steps 5 --warmup 2 > $O/bench_gloo2.json 2> $O/bench_gloo2.err ;;
     iso) $T 300 python -u scripts/debug/stem_isolation.py > $O/stem_isolation.jsonl 2>&1 ;;
     det:*) a=${step#det:}; $T 300 python -u scripts/debug/determinism_probe.py --model ${a%%@*} --hw ${a##*@} >> $O/determinism.jsonl 2>&1 ;;
-    probe:*) a=${step#probe:}; m=${a%%@*}; r=${a#*@}; b=${r%%@*}; sh=${r#*@}; [ "$sh" = "$r" ] && sh=0
-             $T 300 python -u scripts/overlap_probe.py --model $m --batch $b --shard $sh ${PROBE_ARGS:-} \
-             >> $O/overlap_probe.jsonl 2>> $O/overlap_probe.err ;;
+    probe:*) IFS=@ read -r m b sh reps opt <<< "${step#probe:}"
+             $T 300 python -u scripts/overlap_probe.py --model $m --batch $b --shard ${sh:-0} --reps ${reps:-4} \
+               --optimizer ${opt:-sgd} ${PROBE_ARGS:-} >> $O/overlap_probe.jsonl 2>> $O/overlap_probe.err ;;
     micro:*) m=${step#micro:}; rc=0
              for e in ${MICRO_ENVS:-X=0}; do
                echo "{\"env\": \"$e\"}" >> $O/micro_$m.jsonl
