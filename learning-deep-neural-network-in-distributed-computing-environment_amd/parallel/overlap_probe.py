@@ -69,6 +69,7 @@ class ShardProbeComm:
         self.rank, self.world_size = 0, int(world)
         self.standin = StandInComm(device, reps, blocks)
         self._k = 0
+        self.enabled = True   # False: every collective is a no-op (the chain's own cost)
 
     def record(self, *a, **k):
         return self._rec.record(*a, **k)
@@ -83,12 +84,14 @@ class ShardProbeComm:
 
     def reduce_scatter(self, out, inp, async_op=False):
         self._k += 1
-        return self.standin(("rs", inp.data_ptr()), self._moved(inp))
+        return self.standin(("rs", inp.data_ptr()), self._moved(inp)) if self.enabled else None
 
     def all_gather_into(self, out, inp, async_op=False):
-        return self.standin(("ag", out.data_ptr()), self._moved(out))
+        return self.standin(("ag", out.data_ptr()), self._moved(out)) if self.enabled else None
 
     def all_reduce(self, t, op="sum", async_op=False):
+        if not self.enabled:
+            return None
         return self.standin(("ar", t.data_ptr()), t if t.dtype == torch.float32 else t.view(torch.float32))
 
     def broadcast(self, t, src=0):
@@ -214,6 +217,13 @@ def _measure_sharded(model_name, batch, bucket_mb, reps, steps, rounds, blocks, 
     gd = GraphedDPStep(dp, crit, o, x, y)
     bk = dp.bucketer
 
+    def chain_only():   # the same graph chain with every collective a no-op
+        comm.enabled = False
+        try:
+            gd(x, y)
+        finally:
+            comm.enabled = True
+
     def standin_alone():   # every collective of one step, back to back on the side stream
         joins = []
         for i, b in enumerate(bk.buckets):
@@ -224,7 +234,8 @@ def _measure_sharded(model_name, batch, bucket_mb, reps, steps, rounds, blocks, 
                 j.wait()
         bk.wait_gathers()
 
-    fns = {"single_ms": lambda: single(x, y), "with_standin_ms": lambda: gd(x, y), "standin_alone_ms": standin_alone}
+    fns = {"single_graph_ms": lambda: single(x, y), "single_ms": chain_only, "with_standin_ms": lambda: gd(x, y),
+           "standin_alone_ms": standin_alone}
     for f in fns.values():
         for _ in range(3):
             f()
@@ -232,6 +243,8 @@ def _measure_sharded(model_name, batch, bucket_mb, reps, steps, rounds, blocks, 
     for _ in range(rounds):
         for k, f in fns.items():
             best[k] = min(best[k], _timed(f, steps))
+    # single_ms: the sharded chain with no-op collectives (its cut points included);
+    # single_graph_ms: the one-graph step without data parallelism (the chain's own cost)
     hidden = best["single_ms"] + best["standin_alone_ms"] - best["with_standin_ms"]
     return {"model": model_name, "batch": batch, "mode": f"sharded (world {world} stand-in)", "optimizer": optimizer,
             "bucket_mb": bucket_mb, "buckets": len(bk.buckets),
