@@ -218,6 +218,54 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c_in, bool
   check(ldnn::gemm_bf16_tile(p, a_kcontig, b_kcontig, (int)epi, out_f32, (int)tile, cur_stream(a)), "gemm");
 }
 
+// The fused-optimizer state of a weight block `master` (fp32 storage; m / v / shadow in
+// the same layout) -> OptEpi; returns the EPI_OPT_* epilogue of `kind` ("sgd" | "adam" | "adamw").
+int opt_epi_of(ldnn::OptEpi& o, const at::Tensor& master, const std::string& kind,
+               const c10::optional<at::Tensor>& m, const c10::optional<at::Tensor>& v,
+               const c10::optional<at::Tensor>& shadow, const at::Tensor& hp, double grad_scale, double momentum,
+               double dampening, double weight_decay, bool nesterov, double beta1, double beta2, double eps,
+               const char* who) {
+  check_dev(master, at::kFloat, "master");
+  check_dev(hp, at::kFloat, "hp");
+  auto same = [&](const c10::optional<at::Tensor>& t, const char* name) -> float* {
+    if (!t.has_value()) return nullptr;
+    check_dev(*t, at::kFloat, name);
+    TORCH_CHECK(t->sizes() == master.sizes() && t->strides() == master.strides(), who, ": ", name, " layout");
+    TORCH_CHECK(aligned16(t->data_ptr()), who, ": ", name, " alignment");
+    return t->data_ptr<float>();
+  };
+  o = ldnn::OptEpi{};
+  o.master = master.data_ptr<float>();
+  o.m = same(m, "m");
+  o.v = same(v, "v");
+  if (shadow.has_value()) {
+    check_dev(*shadow, at::kBFloat16, "shadow");
+    TORCH_CHECK(shadow->sizes() == master.sizes() && shadow->strides() == master.strides(), who, ": shadow layout");
+    TORCH_CHECK(((uintptr_t)shadow->data_ptr() & 7) == 0, who, ": shadow alignment");
+    o.shadow = bf16_mut(*shadow);
+  }
+  o.hp = hp.data_ptr<float>();
+  o.grad_scale = (float)grad_scale;
+  o.momentum = (float)momentum;
+  o.dampening = (float)dampening;
+  o.weight_decay = (float)weight_decay;
+  o.nesterov = nesterov ? 1 : 0;
+  o.beta1 = (float)beta1;
+  o.beta2 = (float)beta2;
+  o.eps = (float)eps;
+  if (kind == "sgd") {
+    TORCH_CHECK(momentum == 0.0 || o.m, who, ": SGD momentum needs its buffer");
+    return ldnn::EPI_OPT_SGD;
+  }
+  if (kind == "adam" || kind == "adamw") {
+    o.decoupled = kind == "adamw" ? 1 : 0;
+    TORCH_CHECK(o.m && o.v, who, ": Adam needs exp_avg and exp_avg_sq");
+    return ldnn::EPI_OPT_ADAM;
+  }
+  TORCH_CHECK(false, who, ": unknown optimizer ", kind);
+  return -1;
+}
+
 // Weight-gradient GEMM whose epilogue applies SGD / Adam to `master` (fp32
 // [M][N] storage, the layout of the gradient it replaces) and refreshes the bf16
 // shadow: the gradient never goes to HBM.  kind: "sgd" | "adam" | "adamw".
@@ -229,8 +277,6 @@ void gemm_opt(const at::Tensor& a, const at::Tensor& b, const at::Tensor& master
               const c10::optional<at::Tensor>& cnt) {
   check_dev(a, at::kBFloat16, "a");
   check_dev(b, at::kBFloat16, "b");
-  check_dev(master, at::kFloat, "master");
-  check_dev(hp, at::kFloat, "hp");
   const int64_t lda = ld_of(a, "a"), ldb = ld_of(b, "b"), ldc = ld_of(master, "master");
   const int64_t M = a_kcontig ? a.size(0) : a.size(1);
   const int64_t K = a_kcontig ? a.size(1) : a.size(0);
@@ -239,12 +285,6 @@ void gemm_opt(const at::Tensor& a, const at::Tensor& b, const at::Tensor& master
   TORCH_CHECK(master.size(0) == M && master.size(1) == N, "gemm_opt: master shape mismatch");
   TORCH_CHECK(lda % 8 == 0 && ldb % 8 == 0 && ldc % 4 == 0 && N % 8 == 0, "gemm_opt: leading dims");
   TORCH_CHECK(a_kcontig || M % 8 == 0, "gemm_opt: M must be a multiple of 8 for a k-strided A");
-  auto same = [&](const c10::optional<at::Tensor>& t, const char* name) -> float* {
-    if (!t.has_value()) return nullptr;
-    check_dev(*t, at::kFloat, name);
-    TORCH_CHECK(t->sizes() == master.sizes() && t->strides() == master.strides(), "gemm_opt: ", name, " layout");
-    return t->data_ptr<float>();
-  };
   ldnn::GemmParams p{};
   p.A = bf16_ptr(a);
   p.B = bf16_ptr(b);
@@ -255,36 +295,16 @@ void gemm_opt(const at::Tensor& a, const at::Tensor& b, const at::Tensor& master
   p.lda = (int)lda;
   p.ldb = (int)ldb;
   p.ldc = (int)ldc;
-  p.opt.master = master.data_ptr<float>();
-  p.opt.m = same(m, "m");
-  p.opt.v = same(v, "v");
-  if (shadow.has_value()) {
-    check_dev(*shadow, at::kBFloat16, "shadow");
-    TORCH_CHECK(shadow->sizes() == master.sizes() && shadow->strides() == master.strides(), "gemm_opt: shadow layout");
-    p.opt.shadow = bf16_mut(*shadow);
-  }
-  p.opt.hp = hp.data_ptr<float>();
-  p.opt.grad_scale = (float)grad_scale;
-  p.opt.momentum = (float)momentum;
-  p.opt.dampening = (float)dampening;
-  p.opt.weight_decay = (float)weight_decay;
-  p.opt.nesterov = nesterov ? 1 : 0;
-  p.opt.beta1 = (float)beta1;
-  p.opt.beta2 = (float)beta2;
-  p.opt.eps = (float)eps;
-  int epi;
-  if (kind == "sgd") {
-    epi = ldnn::EPI_OPT_SGD;
-    TORCH_CHECK(momentum == 0.0 || p.opt.m, "gemm_opt: SGD momentum needs its buffer");
-  } else if (kind == "adam" || kind == "adamw") {
-    epi = ldnn::EPI_OPT_ADAM;
-    p.opt.decoupled = kind == "adamw" ? 1 : 0;
-    TORCH_CHECK(p.opt.m && p.opt.v, "gemm_opt: Adam needs exp_avg and exp_avg_sq");
-  } else {
-    TORCH_CHECK(false, "gemm_opt: unknown optimizer ", kind);
-  }
+  const int epi = opt_epi_of(p.opt, master, kind, m, v, shadow, hp, grad_scale, momentum, dampening, weight_decay,
+                             nesterov, beta1, beta2, eps, "gemm_opt");
   TORCH_CHECK(aligned16(a.data_ptr()) && aligned16(b.data_ptr()) && aligned16(master.data_ptr()), "gemm_opt: alignment");
   if (tile == 0) tile = ldnn::gemm_pick_tile(p.M, p.N, p.K, true);
+  if (tile == 256 && splitk <= 1 && ldnn::gemm_q_preferred(p.M, p.N, p.K)) {
+    // the four-wave kernel (the one the plain wgrad of this shape runs), row-staged update epilogue
+    c10::hip::HIPGuardMasqueradingAsCUDA g(a.device());
+    check(ldnn::gemm_q(p, a_kcontig, b_kcontig, epi, true, cur_stream(a)), "gemm_opt (gemm_q)");
+    return;
+  }
   if (splitk > 1) {
     TORCH_CHECK(tile == 128 && ws.has_value() && cnt.has_value(), "gemm_opt: split-K needs the in-launch combine");
     check_dev(*ws, at::kFloat, "ws");
@@ -298,6 +318,33 @@ void gemm_opt(const at::Tensor& a, const at::Tensor& b, const at::Tensor& master
   }
   c10::hip::HIPGuardMasqueradingAsCUDA g(a.device());
   check(ldnn::gemm_bf16_tile(p, a_kcontig, b_kcontig, epi, true, (int)tile, cur_stream(a)), "gemm_opt");
+}
+
+// Split-K slabs of a weight gradient summed straight into the fused optimizer update of
+// `master` ([rows][ncols] fp32 storage view; m / v / shadow in the same layout); extra[r]
+// (optional) = column ncols of the sum (the ones-column bias gradient).
+void slab_sum_opt(const at::Tensor& ws, const at::Tensor& master, const c10::optional<at::Tensor>& extra,
+                  const std::string& kind, const c10::optional<at::Tensor>& m, const c10::optional<at::Tensor>& v,
+                  const c10::optional<at::Tensor>& shadow, const at::Tensor& hp, double grad_scale, double momentum,
+                  double dampening, double weight_decay, bool nesterov, double beta1, double beta2, double eps) {
+  check_dev(ws, at::kFloat, "ws");
+  TORCH_CHECK(ws.dim() == 3 && ws.is_contiguous() && aligned16(ws.data_ptr()), "slab_sum_opt: ws must be [splits][rows][ldw]");
+  TORCH_CHECK(master.dim() == 2 && master.size(0) == ws.size(1) && master.stride(1) == 1 &&
+                  aligned16(master.data_ptr()) && master.stride(0) % 4 == 0 && master.size(1) % 4 == 0,
+              "slab_sum_opt: master must be a 16-B aligned [rows][ncols % 4 == 0] view");
+  ldnn::OptEpi o;
+  const int epi = opt_epi_of(o, master, kind, m, v, shadow, hp, grad_scale, momentum, dampening, weight_decay,
+                             nesterov, beta1, beta2, eps, "slab_sum_opt");
+  float* ex = nullptr;
+  if (extra.has_value()) {
+    check_dev(*extra, at::kFloat, "extra");
+    TORCH_CHECK(extra->is_contiguous() && extra->numel() >= ws.size(1), "slab_sum_opt: bad extra");
+    ex = extra->data_ptr<float>();
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA g(ws.device());
+  check(ldnn::slab_sum_opt(ws.data_ptr<float>(), (int)ws.size(0), (int)ws.size(1), (int)ws.size(2),
+                           (int)master.stride(0), (int)master.size(1), ex, o, epi, cur_stream(ws)),
+        "slab_sum_opt");
 }
 
 void act_fwd(const at::Tensor& x, const at::Tensor& y, int64_t act) {
@@ -1536,6 +1583,12 @@ PYBIND11_MODULE(_C, m) {
         py::arg("weight_decay") = 0.0, py::arg("nesterov") = false, py::arg("beta1") = 0.9, py::arg("beta2") = 0.999,
         py::arg("eps") = 1e-8, py::arg("tile") = 0, py::arg("splitk") = 0, py::arg("ws") = py::none(),
         py::arg("cnt") = py::none());
+  m.def("slab_sum_opt", &slab_sum_opt, "split-K weight-gradient slabs summed into the fused optimizer update",
+        py::arg("ws"), py::arg("master"), py::arg("extra") = py::none(), py::arg("kind") = "sgd",
+        py::arg("m") = py::none(), py::arg("v") = py::none(), py::arg("shadow") = py::none(), py::arg("hp"),
+        py::arg("grad_scale") = 1.0, py::arg("momentum") = 0.0, py::arg("dampening") = 0.0,
+        py::arg("weight_decay") = 0.0, py::arg("nesterov") = false, py::arg("beta1") = 0.9, py::arg("beta2") = 0.999,
+        py::arg("eps") = 1e-8);
   m.def("act_fwd", &act_fwd);
   m.def("act_bwd", &act_bwd);
   m.def("colsum", &colsum, py::arg("x"), py::arg("out"), py::arg("accumulate") = false);

@@ -122,21 +122,19 @@ __device__ __forceinline__ OptConst opt_const(const OptEpi& o) {
   return c;
 }
 
+// The update arithmetic on registers: p (weights), m (momentum / exp_avg), v (exp_avg_sq).
 template <int EPI>
-__device__ __forceinline__ void opt_update4(const OptEpi& o, const OptConst& k, size_t off, floatx4 g) {
-  floatx4 p = *reinterpret_cast<const floatx4*>(o.master + off);
+__device__ __forceinline__ void opt_math(const OptEpi& o, const OptConst& k, floatx4& p, floatx4& m, floatx4& v,
+                                         floatx4 g) {
   g = g * o.grad_scale;
   if constexpr (EPI == EPI_OPT_SGD) {
     if (o.weight_decay != 0.f) g += o.weight_decay * p;
     if (o.m != nullptr) {
-      floatx4 b = o.momentum * *reinterpret_cast<const floatx4*>(o.m + off) + (1.f - o.dampening) * g;
-      *reinterpret_cast<floatx4*>(o.m + off) = b;
-      g = o.nesterov ? g + o.momentum * b : b;
+      m = o.momentum * m + (1.f - o.dampening) * g;
+      g = o.nesterov ? g + o.momentum * m : m;
     }
     p -= k.lr * g;
   } else {
-    floatx4 m = *reinterpret_cast<const floatx4*>(o.m + off);
-    floatx4 v = *reinterpret_cast<const floatx4*>(o.v + off);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       float gr = g[r], pr = p[r];
@@ -148,11 +146,56 @@ __device__ __forceinline__ void opt_update4(const OptEpi& o, const OptConst& k, 
       v[r] = o.beta2 * v[r] + (1.f - o.beta2) * gr * gr;
       p[r] = pr - (k.lr / k.bc1) * m[r] / (sqrtf(v[r]) / k.bc2s + o.eps);
     }
-    *reinterpret_cast<floatx4*>(o.m + off) = m;
-    *reinterpret_cast<floatx4*>(o.v + off) = v;
   }
-  *reinterpret_cast<floatx4*>(o.master + off) = p;
+}
+
+template <int EPI>
+__device__ __forceinline__ void opt_load4(const OptEpi& o, size_t off, floatx4& p, floatx4& m, floatx4& v) {
+  // (streaming accesses: every optimizer byte is touched once per step, as in optim.hip)
+  p = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(o.master + off));
+  m = floatx4{0.f, 0.f, 0.f, 0.f};
+  v = m;
+  if (o.m != nullptr) m = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(o.m + off));
+  if constexpr (EPI == EPI_OPT_ADAM) v = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(o.v + off));
+}
+
+template <int EPI>
+__device__ __forceinline__ void opt_store4(const OptEpi& o, size_t off, const floatx4& p, const floatx4& m,
+                                           const floatx4& v) {
+  if (o.m != nullptr) __builtin_nontemporal_store(m, reinterpret_cast<floatx4*>(o.m + off));
+  if constexpr (EPI == EPI_OPT_ADAM) __builtin_nontemporal_store(v, reinterpret_cast<floatx4*>(o.v + off));
+  __builtin_nontemporal_store(p, reinterpret_cast<floatx4*>(o.master + off));
   if (o.shadow) *reinterpret_cast<u16x4*>(o.shadow + off) = u16x4{f2bf(p[0]), f2bf(p[1]), f2bf(p[2]), f2bf(p[3])};
+}
+
+template <int EPI>
+__device__ __forceinline__ void opt_update4(const OptEpi& o, const OptConst& k, size_t off, floatx4 g) {
+  floatx4 p, m, v;
+  opt_load4<EPI>(o, off, p, m, v);
+  opt_math<EPI>(o, k, p, m, v, g);
+  opt_store4<EPI>(o, off, p, m, v);
+}
+
+// U independent 8-weight runs (two floatx4 each, at off[u] and off[u] + 4): every
+// state load of the batch is issued before its first store, so a lane keeps up to
+// 6 U 16-B loads in flight instead of one load -> store round trip per run.
+template <int EPI, int U>
+__device__ __forceinline__ void opt_update8_batch(const OptEpi& o, const OptConst& k, const size_t (&off)[U],
+                                                  const bool (&ok)[U], const floatx4 (&g)[U][2]) {
+  floatx4 p[U][2], m[U][2], v[U][2];
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      if (ok[u]) opt_load4<EPI>(o, off[u] + 4 * h, p[u][h], m[u][h], v[u][h]);
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      if (ok[u]) {
+        opt_math<EPI>(o, k, p[u][h], m[u][h], v[u][h], g[u][h]);
+        opt_store4<EPI>(o, off[u] + 4 * h, p[u][h], m[u][h], v[u][h]);
+      }
 }
 
 // ---- shared epilogue: acc[j][i] is the 16x16 tile (n-tile j, m-tile i) -----

@@ -297,6 +297,11 @@ hipError_t adam_step(float* param, float* grad, float* m, float* v, uint16_t* sh
                      float grad_scale, AdamParams ap, int64_t n, hipStream_t s);
 // hp[1] += 1 (graph-capturable step counter)
 hipError_t bump_step(float* hp, hipStream_t s);
+// Split-K weight-gradient slabs [splits][rows][ldw] summed straight into the fused
+// optimizer update of o.master[rows][ncols] (row stride ldo; epi EPI_OPT_SGD / _ADAM);
+// extra[r] (optional) = column ncols of the sum (a ones-column bias gradient).  ncols % 4 == 0.
+hipError_t slab_sum_opt(const float* ws, int splits, int rows, int ldw, int ldo, int ncols, float* extra,
+                        const OptEpi& o, int epi, hipStream_t s);
 
 // ---- classifier head (<= 64 classes): fused Linear + softmax-xent, and its wgrad
 struct HeadParams {

@@ -202,11 +202,49 @@ __device__ __forceinline__ void epilogue_q(const GemmParams& p, floatx4 (&acc)[8
       }
     }
   }
+  // fused optimizer (weight-gradient GEMMs): the 8-column row runs update master / state /
+  // shadow in place of storing the gradient -- 512-B fp32 runs per row, like the stores
+  constexpr bool kOpt = EPI == EPI_OPT_SGD || EPI == EPI_OPT_ADAM;
   // bias-gradient column sums: dgrad / plain epilogues only (a forward never has a dbias)
-  constexpr bool kSums = !kBias && EPI != EPI_BIAS_RELU_HEAD;
+  constexpr bool kSums = !kBias && !kOpt && EPI != EPI_BIAS_RELU_HEAD;
   float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  OptConst okc{};
+  if constexpr (kOpt) okc = opt_const<EPI>(p.opt);
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
+    if constexpr (kOpt) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int row = i * 16 + (lane & 15);
+          const int chunk = j * 4 + (lane >> 4);
+          *reinterpret_cast<floatx4*>(wbuf + row * 512 + ((chunk ^ (row & 31)) << 4)) = acc[j][h * 4 + i];
+        }
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): own staging writes landed (wave-private slice)
+      __builtin_amdgcn_wave_barrier();
+      constexpr int U = EPI == EPI_OPT_SGD ? 8 : 4;  // row runs per batch: all their state loads in flight
+      // together (SGD 2 state arrays: 8 x 2 x (g, p, m) floatx4 = 192 VGPRs; Adam 3 arrays: 4)
+#pragma unroll
+      for (int it0 = 0; it0 < 16; it0 += U) {
+        size_t off[U];
+        bool ok[U];
+        floatx4 g[U][2];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int row = (it0 + u) * 4 + (lane >> 4);
+          const int m = mbase + h * 64 + row;
+          const char* rb = wbuf + row * 512;
+          g[u][0] = *reinterpret_cast<const floatx4*>(rb + (((2 * c8) ^ (row & 31)) << 4));
+          g[u][1] = *reinterpret_cast<const floatx4*>(rb + (((2 * c8 + 1) ^ (row & 31)) << 4));
+          ok[u] = nok && m < p.M;
+          off[u] = (size_t)m * p.ldc + n;
+        }
+        opt_update8_batch<EPI, U>(p.opt, okc, off, ok, g);
+      }
+      __builtin_amdgcn_wave_barrier();
+      continue;
+    }
     u16x8 a8[16];
     uint32_t mk[16];
     if constexpr (kAux) {
@@ -642,7 +680,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(GemmParams p) {
       epilogue_q<EPI, OUT_F32, XF>(pe, acc, smem, wid, m0 + wm * 128, n0 + wn * 128, lane);
     }
   } else {
-    epilogue<EPI, OUT_F32, 8, 8>(p, acc, m0 + wm * 128, n0 + wn * 128, lane);
+    barrier();  // every wave is done with the operand stages: LDS belongs to the epilogue
+    epilogue_q<EPI, OUT_F32, XF>(pe, acc, smem, wid, m0 + wm * 128, n0 + wn * 128, lane);
   }
 }
 

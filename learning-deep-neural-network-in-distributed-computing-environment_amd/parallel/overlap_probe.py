@@ -111,13 +111,15 @@ def _timed(fn, steps):
 
 
 def measure_overlap(model_name: str, batch: int, bucket_mb: float = 32.0, reps: int = 4, steps: int = 20,
-                    rounds: int = 3, blocks: int = 16, shard_world: int = 0, optimizer: str = "sgd") -> dict:
+                    rounds: int = 3, blocks: int = 16, shard_world: int = 0, optimizer: str = "sgd",
+                    tail_steps: int = 0) -> dict:
     """shard_world > 0: the sharded step (reduce-scatter between backward links, sharded
     optimizer, bf16 weight all-gathers waited by the forward links) on a
     ShardProbeComm of that world size; the stand-ins then cover the reduce-scatter
     AND the all-gather bytes of each bucket."""
     if shard_world:
-        return _measure_sharded(model_name, batch, bucket_mb, reps, steps, rounds, blocks, shard_world, optimizer)
+        return _measure_sharded(model_name, batch, bucket_mb, reps, steps, rounds, blocks, shard_world, optimizer,
+                                tail_steps)
     import ldnn
     from ldnn.data.datasets import SHAPES
     from ldnn.models import CrossEntropyLoss, build_model, dataset_for, xavier_init
@@ -165,6 +167,7 @@ def measure_overlap(model_name: str, batch: int, bucket_mb: float = 32.0, reps: 
         for k, f in fns.items():
             best[k] = min(best[k], _timed(f, steps))
     hidden = best["single_ms"] + best["standin_alone_ms"] - best["with_standin_ms"]
+    _tail(fns["with_standin_ms"], tail_steps)
     return {"model": model_name, "batch": batch, "bucket_mb": bucket_mb, "buckets": len(bufs),
             "bucket_mb_each": [round(b.numel() * b.element_size() / 2**20, 2) for b in bufs],
             "segments": gd.n_segments, "standin_reps": reps, "standin_blocks": blocks, **{k: round(v, 4) for k, v in best.items()},
@@ -172,7 +175,19 @@ def measure_overlap(model_name: str, batch: int, bucket_mb: float = 32.0, reps: 
             "hidden_fraction": round(hidden / max(best["standin_alone_ms"], 1e-9), 3)}
 
 
-def _measure_sharded(model_name, batch, bucket_mb, reps, steps, rounds, blocks, world, optimizer):
+def _tail(fn, n):
+    """n more steps of the overlapped step after a 20 ms idle gap: the last stretch of a
+    kernel trace is then that phase alone (scripts/probe_timeline.py)."""
+    if n <= 0:
+        return
+    torch.cuda.synchronize()
+    time.sleep(0.02)
+    for _ in range(n):
+        fn()
+    torch.cuda.synchronize()
+
+
+def _measure_sharded(model_name, batch, bucket_mb, reps, steps, rounds, blocks, world, optimizer, tail_steps=0):
     import ldnn
     from ldnn.data.datasets import SHAPES
     from ldnn.models import CrossEntropyLoss, build_model, dataset_for, xavier_init
@@ -246,6 +261,7 @@ def _measure_sharded(model_name, batch, bucket_mb, reps, steps, rounds, blocks, 
     # single_ms: the sharded chain with no-op collectives (its cut points included);
     # single_graph_ms: the one-graph step without data parallelism (the chain's own cost)
     hidden = best["single_ms"] + best["standin_alone_ms"] - best["with_standin_ms"]
+    _tail(lambda: gd(x, y), tail_steps)
     return {"model": model_name, "batch": batch, "mode": f"sharded (world {world} stand-in)", "optimizer": optimizer,
             "bucket_mb": bucket_mb, "buckets": len(bk.buckets),
             "sharded_buckets": sum(1 for b in bk.buckets if b["sharded"]),
@@ -265,9 +281,12 @@ def main():
     ap.add_argument("--blocks", type=int, default=16)
     ap.add_argument("--shard", type=int, default=0, help="world size of the sharded-step probe (0 = all-reduce step)")
     ap.add_argument("--optimizer", choices=["sgd", "adam"], default="sgd")
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--tail-steps", type=int, default=0, help="then this many overlapped steps after an idle gap "
+                    "(kernel-trace timelines: scripts/probe_timeline.py)")
     a = ap.parse_args()
-    print(json.dumps(measure_overlap(a.model, a.batch, a.bucket_mb, a.reps, a.steps, blocks=a.blocks,
-                                     shard_world=a.shard, optimizer=a.optimizer)), flush=True)
+    print(json.dumps(measure_overlap(a.model, a.batch, a.bucket_mb, a.reps, a.steps, rounds=a.rounds, blocks=a.blocks,
+                                     shard_world=a.shard, optimizer=a.optimizer, tail_steps=a.tail_steps)), flush=True)
 
 
 if __name__ == "__main__":

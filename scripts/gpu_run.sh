@@ -23,6 +23,11 @@ for step in "$@"; do
     probe:*) IFS=@ read -r m b sh reps opt <<< "${step#probe:}"
              $T 300 python -u scripts/overlap_probe.py --model $m --batch $b --shard ${sh:-0} --reps ${reps:-4} \
                --optimizer ${opt:-sgd} ${PROBE_ARGS:-} >> $O/overlap_probe.jsonl 2>> $O/overlap_probe.err ;;
+    probetrace:*) IFS=@ read -r m b sh reps opt <<< "${step#probetrace:}"
+             (cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+             $T 400 rocprofv3 --kernel-trace -d $O/probetrace_${m}_$sh -o run -- python -u scripts/overlap_probe.py \
+               --model $m --batch $b --shard ${sh:-0} --reps ${reps:-1} --optimizer ${opt:-sgd} --rounds 1 --steps 5 --tail-steps 3 \
+               > $O/probetrace_${m}_$sh.txt 2>&1) ;;
     micro:*) m=${step#micro:}; rc=0
              for e in ${MICRO_ENVS:-X=0}; do
                echo "{\"env\": \"$e\"}" >> $O/micro_$m.jsonl
