@@ -1575,6 +1575,15 @@ PYBIND11_MODULE(_C, m) {
         "halo-staged 3x3 stride-1 conv: 0 off, 1 default (dgrad + 256x64 fwd tiles), 2 every eligible shape",
         py::arg("mode"));
   m.def("get_conv_halo", &ldnn::get_conv_halo);
+  m.def("set_conv_trace", [](const c10::optional<at::Tensor>& buf) {
+        if (!buf.has_value()) {
+          ldnn::set_conv_trace(nullptr);
+          return;
+        }
+        TORCH_CHECK(buf->is_cuda() && buf->scalar_type() == at::kLong && buf->is_contiguous(), "set_conv_trace: int64 cuda");
+        ldnn::set_conv_trace(reinterpret_cast<uint64_t*>(buf->data_ptr<int64_t>()));
+      }, "phase-trace buffer of the LDNN_CONV_XF=32 diagnostic conv build ([>= workgroups][4] int64; None = off)",
+      py::arg("buf"));
   m.def("get_conv_impl", &ldnn::get_conv_impl);
   m.def("gemm_opt", &gemm_opt, "weight-gradient GEMM with the optimizer update fused into its epilogue",
         py::arg("a"), py::arg("b"), py::arg("master"), py::arg("a_kcontig"), py::arg("b_kcontig"), py::arg("kind"),

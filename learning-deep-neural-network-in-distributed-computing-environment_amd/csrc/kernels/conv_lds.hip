@@ -76,6 +76,7 @@ struct LArgs {
   int bf16_rows;     // bf16 outputs (fwd y, stride-1 dgrad dx) through the row-coalesced LDS epilogue
   int remap_rows;    // stride-2 dgrad dx (class row remap) through the row-coalesced LDS epilogue
   int xcd_split;     // split-K grids: the tiles of one K slice share an XCD (see split_coords)
+  uint64_t* trace;   // XF bit 5 (phase-trace builds): [workgroup][4] s_memrealtime stamps
 };
 
 // (tile, K slice) of this workgroup.  Default: tile = blockIdx.x, slice = blockIdx.y.  With
@@ -725,7 +726,9 @@ __device__ __forceinline__ void conv_tail(const LArgs& a, const Geo& g, floatx4 
 // in the steady state) retires only tile kt before the barrier that publishes it.
 // XF (experiment builds only, LDNN_CONV_XF, on the 128x128 fwd / dgrad / wgrad and the narrow
 // wgrad kernels): bit0 no in-loop DMA, bit1 (fwd only) the A operand DMAs contiguous
-// 16-KiB-aligned chunks instead of the im2col gather, bit2 no fragment reads / MFMAs
+// 16-KiB-aligned chunks instead of the im2col gather, bit2 no fragment reads / MFMAs, bit5 phase
+// trace: wave 0 stamps s_memrealtime (100 MHz) at entry, after the first K-tile landed, after
+// the main loop and at exit into a.trace[workgroup][4] (scripts/conv_phase_trace.py)
 template <int WM, int WN, class OA, class OB, int EPI, bool OUT_F32, bool DGRAD, int NS, int XF = 0>
 __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void conv_lds_kernel(LArgs a, const bf16_t* pa, uint32_t bytes_a,
                                                                        const bf16_t* pb, uint32_t bytes_b) {
@@ -742,6 +745,13 @@ __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void conv_lds_kernel(LArgs a,
 
   const Geo g = make_geo(a, DGRAD);
   const int tiles_m = (g.M + BM - 1) / BM, tiles_n = (a.N + BN - 1) / BN;
+  uint64_t* trace = nullptr;
+  if constexpr ((XF & 32) != 0) {
+    if (threadIdx.x == 0 && a.trace != nullptr) {
+      trace = a.trace + 4 * (size_t)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z));
+      trace[0] = __builtin_amdgcn_s_memrealtime();
+    }
+  }
   int bx, by;
   split_coords(a, bx, by);
   if (bx >= tiles_m * tiles_n) return;  // a smaller parity class: whole workgroup exits
@@ -798,6 +808,9 @@ __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void conv_lds_kernel(LArgs a,
         wait_vm<PER_TILE * (NS - 2)>();
       }
       lds_barrier();  // publishes tile kt; every wave is done reading tile kt-1's stage
+      if constexpr ((XF & 32) != 0) {
+        if (kt == 0 && trace != nullptr) trace[1] = __builtin_amdgcn_s_memrealtime();
+      }
       if (!(XF & 1) && kt + NS - 1 < nk) {
         ks_next(a, g, ks);
         oa.advance(a);
@@ -844,7 +857,13 @@ __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void conv_lds_kernel(LArgs a,
     }
   }
 
+  if constexpr ((XF & 32) != 0) {
+    if (trace != nullptr) trace[2] = __builtin_amdgcn_s_memrealtime();
+  }
   conv_tail<WM, WN, EPI, OUT_F32, DGRAD>(a, g, acc, m0, n0, wm, wn, lane, smem, NS * STAGE / 4, bx, by);
+  if constexpr ((XF & 32) != 0) {
+    if (trace != nullptr) trace[3] = __builtin_amdgcn_s_memrealtime();
+  }
 }
 
 // ---- halo path: 3x3 stride-1 pad-1 fwd / dgrad with the A operand staged ONCE --
@@ -1626,8 +1645,11 @@ int remap_rows_env() {
   return v;
 }
 
+uint64_t* g_conv_trace = nullptr;  // phase-trace buffer of LDNN_CONV_XF=32 builds (set_conv_trace)
+
 LArgs base_args(const ConvShape& s) {
   LArgs a{};
+  a.trace = g_conv_trace;
   a.tap_major = tap_major_env();
   a.f32_rows = f32_rows_env();
   a.bf16_rows = bf16_rows_env();
@@ -1696,6 +1718,7 @@ hipError_t launch_ns(LArgs a, int epi, int splits, const bf16_t* pa, size_t ba, 
           break;
         case 8: conv_lds_kernel<WM, WN, OA, OB, EPI_NONE, OUT_F32, DGRAD, NS, 8><<<grid, block, 0, st>>>(a, pa, (uint32_t)ba, pb, (uint32_t)bb); break;
         case 16: conv_lds_kernel<WM, WN, OA, OB, EPI_NONE, OUT_F32, DGRAD, NS, 16><<<grid, block, 0, st>>>(a, pa, (uint32_t)ba, pb, (uint32_t)bb); break;
+        case 32: conv_lds_kernel<WM, WN, OA, OB, EPI_NONE, OUT_F32, DGRAD, NS, 32><<<grid, block, 0, st>>>(a, pa, (uint32_t)ba, pb, (uint32_t)bb); break;
         default: return hipErrorInvalidValue;
       }
       return hipGetLastError();
@@ -1884,6 +1907,7 @@ ConvWorkspace ws_of(const Plan& p) {
 using namespace convlds;
 
 void set_conv_halo(int mode) { g_conv_halo = mode; }
+void set_conv_trace(uint64_t* buf) { g_conv_trace = buf; }
 void set_conv_wgrad_ring(int mode) { g_wgrad_ring = mode; }
 int get_conv_halo() { return halo_env(); }
 

@@ -121,9 +121,13 @@ class _FlatOptimizer(torch.optim.Optimizer):
             return False
         f.finalize_grads()
         ctx = self._begin_ranges(f, group)
-        for lo, hi in sh.update_ranges():
-            if hi > lo:
-                self._update_range(f, group, ctx, lo, hi)
+        parts = getattr(sh, "step_parts", None)
+        if parts is not None:   # the caller interleaves its own work per bucket (GraphedDPStep capture)
+            parts(lambda lo, hi: self._update_range(f, group, ctx, lo, hi) if hi > lo else None)
+        else:
+            for lo, hi in sh.update_ranges():
+                if hi > lo:
+                    self._update_range(f, group, ctx, lo, hi)
         st = self._ls()
         st["step"] = st.get("step", 0) + 1
         sh.after_update()

@@ -146,6 +146,9 @@ class GradBucketer:
         self._gathers: dict = {}   # sharded bucket -> its in-flight weight all-gather
         self.active = False
         self.master_whole = True
+        # step_parts(update): set by a caller that interleaves its own work between the
+        # buckets' optimizer updates (GraphedDPStep's per-bucket optimizer graphs)
+        self.step_parts = None
         flat.add_ready_hook(self._on_ready)
         if self.shard:
             flat.shard_sync = self
@@ -243,15 +246,31 @@ class GradBucketer:
         """The buffer the forward reads weights from: the bf16 shadow (GPU), else the master."""
         return self.flat.shadow if self.flat.shadow is not None else self.flat.master
 
+    def update_range(self, i) -> tuple[int, int]:
+        """The flat range this rank's optimizer updates in bucket i."""
+        b = self.buckets[i]
+        return self.shard_range(i) if b["sharded"] else (b["begin"], b["end"])
+
+    def opt_order(self) -> list[int]:
+        """Bucket order of a per-bucket optimizer: the replicated tail(s), then the sharded
+        buckets in FORWARD order (the last bucket -- the first layers -- first), so each
+        one's weight all-gather can start as soon as its own update is done."""
+        rep = [i for i, b in enumerate(self.buckets) if not b["sharded"]]
+        return rep + [i for i in reversed(range(len(self.buckets))) if self.buckets[i]["sharded"]]
+
+    def issue_gather(self, i):
+        """All-gather sharded bucket i's updated weights, in place (async)."""
+        b = self.buckets[i]
+        if b["sharded"]:
+            t = self.gather_target()
+            lo, hi = self.shard_range(i)
+            self._gathers[i] = self.comm.all_gather_into(t[b["begin"]: b["end"]], t[lo:hi], async_op=True)
+
     def issue_gathers(self):
         """All-gather every sharded bucket's updated weights, in place, in FORWARD order
         (the last bucket -- the first layers -- first)."""
-        t = self.gather_target()
         for i in reversed(range(len(self.buckets))):
-            b = self.buckets[i]
-            if b["sharded"]:
-                lo, hi = self.shard_range(i)
-                self._gathers[i] = self.comm.all_gather_into(t[b["begin"]: b["end"]], t[lo:hi], async_op=True)
+            self.issue_gather(i)
 
     def wait_gathers(self, buckets=None):
         """Order the current stream after the weight all-gathers of ``buckets`` (default:

@@ -23,11 +23,17 @@ import torch
 
 
 class _Join:
+    """The stand-in's work handle: like an RCCL work, ``wait()`` orders the current stream
+    after THIS collective (an event recorded when it was issued) -- not after everything
+    queued on the side stream since (a weight all-gather waited by the forward must not
+    also wait for the all-gathers issued after it)."""
+
     def __init__(self, side):
-        self.side = side
+        self.ev = torch.cuda.Event()
+        self.ev.record(side)
 
     def wait(self):
-        torch.cuda.current_stream().wait_stream(self.side)
+        torch.cuda.current_stream().wait_event(self.ev)
 
 
 class StandInComm:

@@ -231,10 +231,7 @@ class GraphedDPStep:
                 self._end()
                 if self.mode == "after":
                     self.issue[-1] = list(range(nb))
-                self.g_opt = torch.cuda.CUDAGraph()
-                self.g_opt.capture_begin(pool=self._pool, capture_error_mode="relaxed")
-                self._widen_and_step()
-                self.g_opt.capture_end()
+                self._capture_opt()
             self.loss = loss
         finally:
             self._cap = None
@@ -284,10 +281,45 @@ class GraphedDPStep:
         self._empty.append(any("empty" in str(w.message).lower() for w in ws))
         self._cur = None
 
-    def _widen_and_step(self):
-        for i in range(len(self.bk.buckets)):
-            self.bk.post_collective(i)
-        self.optimizer.step()
+    def _capture_opt(self):
+        """G_opt = widen / mix + the fused optimizer.  Sharded: one graph PER BUCKET in
+        GradBucketer.opt_order (replicated tail, then the sharded buckets in forward
+        order), so a replay issues bucket i's weight all-gather right after its own
+        update -- the first layers' gathers run beside the deep buckets' updates instead
+        of after all of them.  (self.g_opts: [(graph, bucket or None)])"""
+        self.g_opts = []
+        order = self.bk.opt_order() if (self.bk.shard and isinstance(self.optimizer, _FlatOptimizer)) else None
+
+        def begin(i):
+            g = torch.cuda.CUDAGraph()
+            g.capture_begin(pool=self._pool, capture_error_mode="relaxed")
+            self.g_opts.append((g, i))
+
+        if order is None:
+            begin(None)
+            for i in range(len(self.bk.buckets)):
+                self.bk.post_collective(i)
+            self.optimizer.step()
+            self.g_opts[-1][0].capture_end()
+            return
+
+        def parts(update):
+            for k, i in enumerate(order):
+                if k > 0:
+                    self.g_opts[-1][0].capture_end()
+                    begin(i)
+                else:
+                    self.g_opts[-1] = (self.g_opts[-1][0], i)
+                self.bk.post_collective(i)
+                update(*self.bk.update_range(i))
+
+        begin(None)   # (the optimizer's per-step prologue, e.g. Adam's step count, lands in the first)
+        self.bk.step_parts = parts
+        try:
+            self.optimizer.step()
+        finally:
+            self.bk.step_parts = None
+        self.g_opts[-1][0].capture_end()
 
     def _fire(self, idx):
         """(capture) buckets ``idx``'s gradients are complete at this point of the backward."""
@@ -367,12 +399,16 @@ class GraphedDPStep:
             if w is not None:
                 w.wait()
         self.bk.wait_gathers()   # (any gather no forward link waited for) before the optimizer writes
-        self.g_opt.replay()
+        host_staged = not self.device_collectives and self.comm_fn is None
+        for g, i in self.g_opts:
+            g.replay()
+            if i is not None:   # bucket i's updated bf16 weight shard -> its all-gather (forward order)
+                self.bk.master_whole = False
+                if host_staged:
+                    torch.cuda.current_stream().synchronize()   # a host-staged backend reads the shadow
+                self.bk.issue_gather(i)
         if self.bk.shard:
             self.bk.master_whole = False
-            if not self.device_collectives and self.comm_fn is None:
-                torch.cuda.current_stream().synchronize()   # a host-staged backend reads the shadow
-            self.bk.issue_gathers()   # updated bf16 weight shards, in forward order
         return self.loss
 
     def _eager_step(self, x, y):

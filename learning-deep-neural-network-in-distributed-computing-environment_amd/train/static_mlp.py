@@ -28,6 +28,7 @@ messages (BAR/communication.py:4-31).
 from __future__ import annotations
 
 import contextlib
+import os
 import gc
 from dataclasses import dataclass
 
@@ -100,7 +101,7 @@ class StaticMLPEngine:
                  fuse_head_dgrad: bool | None = None, library_dgrad: bool | None = None, head_dgrad_mode: int = -1,
                  relu_masks: bool = True, transposed_dgrad: bool = True, bias_ones_column: bool = True,
                  fuse_head_fwd: bool = True, fuse_head_bwd: bool = True, grad_mix: tuple | None = None,
-                 fuse_optimizer: bool = True):
+                 fuse_optimizer: bool | None = None):
         """``grad_mix`` = (hops, local_weight): per-step gradient exchange other than the
         equal all-reduce (world > 1) -- hops 0 with a weight = the reference's
         self-weighted all-reduce (BAR/communication.py:4-10), hops 1 / 2 = ring /
@@ -399,6 +400,9 @@ class StaticMLPEngine:
         # slab wgrad, the pass that sums the slabs (slab_sum_opt).  dgrad(l) then runs
         # BEFORE wgrad(l): it reads the weights that epilogue overwrites.  The step's
         # separate optimizer launches cover only the rest (head weight, biases).
+        # (None: on unless LDNN_FUSE_OPT=0, an A/B knob)
+        if fuse_optimizer is None:
+            fuse_optimizer = os.environ.get("LDNN_FUSE_OPT", "1") != "0"
         self._fused_opt = [False] * L
         if fuse_optimizer and not self.distributed and self.optim.name in ("sgd", "adam", "adamw"):
             for l in range(L):

@@ -28,6 +28,14 @@ for step in "$@"; do
              $T 400 rocprofv3 --kernel-trace -d $O/probetrace_${m}_$sh -o run -- python -u scripts/overlap_probe.py \
                --model $m --batch $b --shard ${sh:-0} --reps ${reps:-1} --optimizer ${opt:-sgd} --rounds 1 --steps 5 --tail-steps 3 \
                > $O/probetrace_${m}_$sh.txt 2>&1) ;;
+    phase:*) m=${step#phase:}; LDNN_CONV_XF=32 $T 300 python -u scripts/conv_phase_trace.py --model $m >> $O/phase_$m.jsonl 2>> $O/phase.err ;;
+    mlpab) rc=0   # same-box A/B of MLP_AB_ENVS on the headline bench (MLP only), alternated 3x
+           for r in 1 2 3; do for e in ${MLP_AB_ENVS:-X=0}; do
+             echo "{\"rep\": $r, \"env\": \"$e\"}" >> $O/mlpab.jsonl
+             env $e $T 200 python -u bench.py --no-configs >> $O/mlpab.jsonl 2>> $O/mlpab.err || { rc=$?; break 2; }
+           done; done; (exit $rc) ;;
+    gemmxf:*) $T 300 python -u scripts/gemm_q_xf.py --K ${step#gemmxf:} --variants ${XF_VARIANTS:-32,33,37,96,160} \
+               >> $O/gemmxf.jsonl 2>> $O/gemmxf.err ;;
     micro:*) m=${step#micro:}; rc=0
              for e in ${MICRO_ENVS:-X=0}; do
                echo "{\"env\": \"$e\"}" >> $O/micro_$m.jsonl

@@ -46,7 +46,7 @@ def main():
         print("no stand-in kernels in the trace")
         return
     # the probe's --tail-steps phase: everything after the last idle gap > 10 ms
-    t_end = max(e for _, e in rows)
+    t_end = max(r[2] for r in rows)
     t0 = rows[0][1]
     prev_end = rows[0][2]
     for n, s, e in rows[1:]:
