@@ -402,8 +402,8 @@ def main():
             "parallelism": f"dp{n}",
             "optimizer": "sgd momentum 0.9, fp32 master",
             "gemms": ("ldnn MFMA kernels only: bias+ReLU fwd (ReLU bit masks), dReLU dgrad on a transposed W, "
-                      "hidden wgrads with the SGD momentum update fused into their epilogues (1 GPU; split-K slabs for "
-                      "the 784-wide one), classifier head (Linear + softmax-xent + argmax + head dgrad), SGD"
+                      "fp32 wgrads (the 784-wide one split-K into slabs, summed by the pass that also applies its SGD "
+                      "update on 1 GPU), classifier head (Linear + softmax-xent + argmax + head dgrad), fused SGD"
                       if args.gemms == "ldnn" else
                       "hipBLASLt: fp32 wgrads, bias/ReLU fwd, hidden dgrad; ldnn: fused dReLU+dbias pass, "
                       "classifier head (Linear + softmax-xent + argmax + head dgrad), SGD"),

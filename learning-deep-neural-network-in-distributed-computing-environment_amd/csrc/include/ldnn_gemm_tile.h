@@ -403,15 +403,36 @@ __device__ __forceinline__ bool splitk_combine(floatx4 (&acc)[NT][MT], float* ws
   for (int j = 0; j < NT; ++j)
 #pragma unroll
     for (int i = 0; i < MT; ++i) acc[j][i] = floatx4{0.f, 0.f, 0.f, 0.f};
-  for (int s = 0; s < splits; ++s) {
+  auto load = [&](int s, int j, int i) {
     const uint32_t o = (uint32_t)s * kSlab + (uint32_t)tid * 16u;
+    return __builtin_bit_cast(
+        floatx4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(o + (uint32_t)((j * MT + i) * NTHREADS * 16)), 0,
+                                                       kSc1));
+  };
+  int s = 0;
+  if constexpr (NT * MT <= 16) {
+    // two slabs per round trip (the summing workgroup's combine is latency-bound: one
+    // split's 64 KiB per round trip left a 4-way split's last arrival ~20 us in its tail)
+    for (; s + 1 < splits; s += 2) {
+      floatx4 t0[NT][MT], t1[NT][MT];
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int i = 0; i < MT; ++i) {
+          t0[j][i] = load(s, j, i);
+          t1[j][i] = load(s + 1, j, i);
+        }
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int i = 0; i < MT; ++i) acc[j][i] += t0[j][i] + t1[j][i];
+    }
+  }
+  for (; s < splits; ++s) {
 #pragma unroll
     for (int j = 0; j < NT; ++j)
 #pragma unroll
-      for (int i = 0; i < MT; ++i)
-        acc[j][i] += __builtin_bit_cast(
-            floatx4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(o + (uint32_t)((j * MT + i) * NTHREADS * 16)),
-                                                           0, kSc1));
+      for (int i = 0; i < MT; ++i) acc[j][i] += load(s, j, i);
   }
   return true;
 }

@@ -101,7 +101,7 @@ class StaticMLPEngine:
                  fuse_head_dgrad: bool | None = None, library_dgrad: bool | None = None, head_dgrad_mode: int = -1,
                  relu_masks: bool = True, transposed_dgrad: bool = True, bias_ones_column: bool = True,
                  fuse_head_fwd: bool = True, fuse_head_bwd: bool = True, grad_mix: tuple | None = None,
-                 fuse_optimizer: bool | None = None):
+                 fuse_optimizer: bool | str | None = None):
         """``grad_mix`` = (hops, local_weight): per-step gradient exchange other than the
         equal all-reduce (world > 1) -- hops 0 with a weight = the reference's
         self-weighted all-reduce (BAR/communication.py:4-10), hops 1 / 2 = ring /
@@ -395,22 +395,29 @@ class StaticMLPEngine:
                                    and self.layers[L - 1].in_features % 64 == 0 and self._wgrad_splitk[L - 1] > 1)
         # fuse_optimizer (single-process engines): a hidden layer's weight gradient never
         # reaches HBM -- the optimizer update of its weights (fp32 master, momentum / Adam
-        # moments, bf16 shadow) runs in the epilogue of the kernel that produces it: the
-        # four-wave wgrad GEMM (gemm_q EPI_OPT_*, row-staged 512-B runs) or, for a split-K
-        # slab wgrad, the pass that sums the slabs (slab_sum_opt).  dgrad(l) then runs
-        # BEFORE wgrad(l): it reads the weights that epilogue overwrites.  The step's
-        # separate optimizer launches cover only the rest (head weight, biases).
-        # (None: on unless LDNN_FUSE_OPT=0, an A/B knob)
+        # moments, bf16 shadow) runs in the epilogue of the kernel that produces it:
+        # "slab" = the pass that sums a split-K slab wgrad's slabs (slab_sum_opt), "all" /
+        # True = also the four-wave wgrad GEMM's epilogue (gemm_q EPI_OPT_*, row-staged).
+        # dgrad(l) then runs BEFORE wgrad(l): it reads the weights that epilogue overwrites;
+        # the step's separate optimizer launches cover only the rest.  Measured on MI355X
+        # (same box, alternated, profiles/r4/mlp_fused_opt_ab.jsonl): the gemm_q epilogue
+        # update is SLOWER in the headline step (1.628 vs 1.599 ms: its 256 workgroups all
+        # reach the 288 MB read-modify-write at once, +84 us on a 415 us GEMM, more than the
+        # separate 71 us update costs), so the default fuses the slab pass only.
+        # (None: LDNN_FUSE_OPT = 0 | slab | all, default slab -- an A/B knob)
         if fuse_optimizer is None:
-            fuse_optimizer = os.environ.get("LDNN_FUSE_OPT", "1") != "0"
+            fuse_optimizer = os.environ.get("LDNN_FUSE_OPT", "slab")
+        mode = {True: "all", False: "0", "1": "all"}.get(fuse_optimizer, fuse_optimizer)
+        if mode not in ("0", "slab", "all"):
+            raise ValueError(f"fuse_optimizer must be 0 / slab / all, got {fuse_optimizer!r}")
         self._fused_opt = [False] * L
-        if fuse_optimizer and not self.distributed and self.optim.name in ("sgd", "adam", "adamw"):
+        if mode != "0" and not self.distributed and self.optim.name in ("sgd", "adam", "adamw"):
             for l in range(L):
                 if (self.use_head and l == L - 1) or self._lib_wgrad[l]:
                     continue
                 if self._wgrad_slab[l] is not None:
                     self._fused_opt[l] = self.W[l].shape[1] % 4 == 0
-                elif self._wgrad_ws[l] is None and self._wgrad_splitk[l] <= 1:
+                elif mode == "all" and self._wgrad_ws[l] is None and self._wgrad_splitk[l] <= 1:
                     self._fused_opt[l] = True
         fused = sorted((f.seg(self.layers[l].weight).offset,
                         f.seg(self.layers[l].weight).offset + f.seg(self.layers[l].weight).storage_numel)

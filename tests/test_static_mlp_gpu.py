@@ -387,7 +387,7 @@ def test_fused_optimizer_epilogues_match_separate_update(opt, B, H):
     m2.load_state_dict(m1.state_dict())
     cfg = OptimConfig(opt, lr=0.05 if opt == "sgd" else 1e-3, momentum=0.9,
                       weight_decay=1e-2 if opt == "adamw" else 0.0)
-    e1 = StaticMLPEngine(m1, B, cfg, use_graphs=True)
+    e1 = StaticMLPEngine(m1, B, cfg, use_graphs=True, fuse_optimizer="all")
     e2 = StaticMLPEngine(m2, B, cfg, use_graphs=True, fuse_optimizer=False)
     assert e1._fused_opt[:2] == [True, True] and not any(e2._fused_opt)
     assert (e1._wgrad_slab[1] is None) == (H == 4096)   # the gemm_q epilogue path at 4096 x 4096
