@@ -320,33 +320,6 @@ void gemm_opt(const at::Tensor& a, const at::Tensor& b, const at::Tensor& master
   check(ldnn::gemm_bf16_tile(p, a_kcontig, b_kcontig, epi, true, (int)tile, cur_stream(a)), "gemm_opt");
 }
 
-// Split-K slabs of a weight gradient summed straight into the fused optimizer update of
-// `master` ([rows][ncols] fp32 storage view; m / v / shadow in the same layout); extra[r]
-// (optional) = column ncols of the sum (the ones-column bias gradient).
-void slab_sum_opt(const at::Tensor& ws, const at::Tensor& master, const c10::optional<at::Tensor>& extra,
-                  const std::string& kind, const c10::optional<at::Tensor>& m, const c10::optional<at::Tensor>& v,
-                  const c10::optional<at::Tensor>& shadow, const at::Tensor& hp, double grad_scale, double momentum,
-                  double dampening, double weight_decay, bool nesterov, double beta1, double beta2, double eps) {
-  check_dev(ws, at::kFloat, "ws");
-  TORCH_CHECK(ws.dim() == 3 && ws.is_contiguous() && aligned16(ws.data_ptr()), "slab_sum_opt: ws must be [splits][rows][ldw]");
-  TORCH_CHECK(master.dim() == 2 && master.size(0) == ws.size(1) && master.stride(1) == 1 &&
-                  aligned16(master.data_ptr()) && master.stride(0) % 4 == 0 && master.size(1) % 4 == 0,
-              "slab_sum_opt: master must be a 16-B aligned [rows][ncols % 4 == 0] view");
-  ldnn::OptEpi o;
-  const int epi = opt_epi_of(o, master, kind, m, v, shadow, hp, grad_scale, momentum, dampening, weight_decay,
-                             nesterov, beta1, beta2, eps, "slab_sum_opt");
-  float* ex = nullptr;
-  if (extra.has_value()) {
-    check_dev(*extra, at::kFloat, "extra");
-    TORCH_CHECK(extra->is_contiguous() && extra->numel() >= ws.size(1), "slab_sum_opt: bad extra");
-    ex = extra->data_ptr<float>();
-  }
-  c10::hip::HIPGuardMasqueradingAsCUDA g(ws.device());
-  check(ldnn::slab_sum_opt(ws.data_ptr<float>(), (int)ws.size(0), (int)ws.size(1), (int)ws.size(2),
-                           (int)master.stride(0), (int)master.size(1), ex, o, epi, cur_stream(ws)),
-        "slab_sum_opt");
-}
-
 void act_fwd(const at::Tensor& x, const at::Tensor& y, int64_t act) {
   check_dev(x, at::kBFloat16, "x");
   check_dev(y, at::kBFloat16, "y");
@@ -980,15 +953,52 @@ bool conv_fwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& y, int
   return done;
 }
 
-void conv_dgrad(const at::Tensor& dy, const at::Tensor& w, const at::Tensor& dx, int64_t stride, int64_t pad) {
+// bn_*: fuse the backward statistics of the BatchNorm + ReLU that produced this conv's input
+// (dx = that BN output's gradient, this conv its only consumer): bn_x = the BN's input [M][C],
+// bn_mask its ReLU bits, save_mean / save_invstd its batch statistics, bn_ws its workspace.
+// Returns whether the epilogue did it (then the BN backward runs with stats_ready=True).
+bool conv_dgrad(const at::Tensor& dy, const at::Tensor& w, const at::Tensor& dx, int64_t stride, int64_t pad,
+                const c10::optional<at::Tensor>& bn_x, const c10::optional<at::Tensor>& bn_mask,
+                const c10::optional<at::Tensor>& bn_gamma, const c10::optional<at::Tensor>& bn_save_mean,
+                const c10::optional<at::Tensor>& bn_save_invstd, const c10::optional<at::Tensor>& bn_ws,
+                const c10::optional<at::Tensor>& bn_dgamma, const c10::optional<at::Tensor>& bn_dbeta,
+                bool bn_grad_assign) {
   check_dev(dy, at::kBFloat16, "dy");
   check_dev(w, at::kBFloat16, "w");
   check_dev(dx, at::kBFloat16, "dx");
   ldnn::ConvShape s = conv_shape(dx, w, dy, stride, pad);
   c10::hip::HIPGuardMasqueradingAsCUDA g(dy.device());
   const ConvWs ws = conv_ws(s, 1, dy);
-  check(ldnn::conv2d_dgrad(s, bf16_ptr(dy), bf16_ptr(w), bf16_mut(dx), cur_stream(dy), ws.ws(), ws.c()),
+  ldnn::BnBwdFuse fuse{};
+  const ldnn::BnBwdFuse* fp = nullptr;
+  if (bn_x.has_value()) {
+    const int C = s.C;
+    const int64_t M = (int64_t)s.N * s.H * s.W;
+    check_dev(*bn_x, at::kBFloat16, "bn_x");
+    TORCH_CHECK(bn_x->is_contiguous() && bn_x->numel() == M * C, "conv_dgrad: bn_x must be the BN input [M][C]");
+    TORCH_CHECK(bn_mask.has_value() && bn_mask->is_contiguous() && bn_mask->numel() == M * C / 8,
+                "conv_dgrad: bn_mask must be the BN's ReLU bits [M][C/8]");
+    check_dev(*bn_mask, at::kByte, "bn_mask");
+    ldnn::BnArgs a{};
+    a.M = (int)M;
+    a.C = C;
+    a.gamma = fptr_opt(bn_gamma, C, "bn_gamma");
+    a.save_mean = fptr_opt(bn_save_mean, C, "bn_save_mean");
+    a.save_invstd = fptr_opt(bn_save_invstd, C, "bn_save_invstd");
+    TORCH_CHECK(a.save_mean && a.save_invstd && aligned16(a.save_mean) && aligned16(a.save_invstd),
+                "conv_dgrad: fused BN statistics need 16-B aligned save_mean / save_invstd");
+    a.ws = fptr_opt(bn_ws, ldnn::bn_workspace_floats(C), "bn_ws");
+    TORCH_CHECK(a.ws, "conv_dgrad: fused BN statistics need the BN workspace");
+    fuse.fin = ldnn::bn_backward_fin_conv(a, fptr_opt(bn_dgamma, C, "bn_dgamma"), fptr_opt(bn_dbeta, C, "bn_dbeta"),
+                                          bn_grad_assign);
+    fuse.x = bf16_ptr(*bn_x);
+    fuse.mask = bn_mask->data_ptr<uint8_t>();
+    fp = &fuse;
+  }
+  bool done = false;
+  check(ldnn::conv2d_dgrad(s, bf16_ptr(dy), bf16_ptr(w), bf16_mut(dx), cur_stream(dy), ws.ws(), ws.c(), fp, &done),
         "conv2d_dgrad");
+  return done;
 }
 
 void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& dw, int64_t stride, int64_t pad,
@@ -1074,7 +1084,8 @@ void bn_bwd(const at::Tensor& x, const at::Tensor& y, const at::Tensor& dy, cons
             const c10::optional<at::Tensor>& dres, const c10::optional<at::Tensor>& gamma,
             const at::Tensor& save_mean, const at::Tensor& save_invstd, const at::Tensor& ws,
             const c10::optional<at::Tensor>& dgamma, const c10::optional<at::Tensor>& dbeta, bool relu,
-            const c10::optional<at::Tensor>& mask, bool grad_assign, const c10::optional<at::Tensor>& dy2) {
+            const c10::optional<at::Tensor>& mask, bool grad_assign, const c10::optional<at::Tensor>& dy2,
+            bool stats_ready) {
   check_dev(x, at::kBFloat16, "x");
   check_dev(dy, at::kBFloat16, "dy");
   check_dev(dx, at::kBFloat16, "dx");
@@ -1107,6 +1118,10 @@ void bn_bwd(const at::Tensor& x, const at::Tensor& y, const at::Tensor& dy, cons
     check_dev(*dres, at::kBFloat16, "dres");
     TORCH_CHECK(dres->sizes() == x.sizes() && dres->is_contiguous(), "bn_bwd: dres layout");
     dr = bf16_mut(*dres);
+  }
+  if (stats_ready) {   // coefficients + dgamma / dbeta already finalized (conv_dgrad's fused statistics)
+    check(ldnn::bn_backward_apply(a, bf16_ptr(dy), bf16_mut(dx), dr, cur_stream(x)), "bn_backward_apply");
+    return;
   }
   check(ldnn::bn_backward(a, bf16_ptr(dy), bf16_mut(dx), dr, fptr_opt(dgamma, C, "dgamma"),
                           fptr_opt(dbeta, C, "dbeta"), cur_stream(x), grad_assign),
@@ -1592,12 +1607,6 @@ PYBIND11_MODULE(_C, m) {
         py::arg("weight_decay") = 0.0, py::arg("nesterov") = false, py::arg("beta1") = 0.9, py::arg("beta2") = 0.999,
         py::arg("eps") = 1e-8, py::arg("tile") = 0, py::arg("splitk") = 0, py::arg("ws") = py::none(),
         py::arg("cnt") = py::none());
-  m.def("slab_sum_opt", &slab_sum_opt, "split-K weight-gradient slabs summed into the fused optimizer update",
-        py::arg("ws"), py::arg("master"), py::arg("extra") = py::none(), py::arg("kind") = "sgd",
-        py::arg("m") = py::none(), py::arg("v") = py::none(), py::arg("shadow") = py::none(), py::arg("hp"),
-        py::arg("grad_scale") = 1.0, py::arg("momentum") = 0.0, py::arg("dampening") = 0.0,
-        py::arg("weight_decay") = 0.0, py::arg("nesterov") = false, py::arg("beta1") = 0.9, py::arg("beta2") = 0.999,
-        py::arg("eps") = 1e-8);
   m.def("act_fwd", &act_fwd);
   m.def("act_bwd", &act_bwd);
   m.def("colsum", &colsum, py::arg("x"), py::arg("out"), py::arg("accumulate") = false);
@@ -1685,7 +1694,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_bwd", &bn_bwd, py::arg("x"), py::arg("y"), py::arg("dy"), py::arg("dx"), py::arg("dres"),
         py::arg("gamma"), py::arg("save_mean"), py::arg("save_invstd"), py::arg("ws"), py::arg("dgamma"),
         py::arg("dbeta"), py::arg("relu"), py::arg("mask") = py::none(), py::arg("grad_assign") = false,
-        py::arg("dy2") = py::none());
+        py::arg("dy2") = py::none(), py::arg("stats_ready") = false);
   m.def("pool_fwd", &pool_fwd);
   m.def("pool_bwd", &pool_bwd, py::arg("dy"), py::arg("argmax"), py::arg("dx"), py::arg("R"), py::arg("S"),
         py::arg("stride"), py::arg("pad"), py::arg("is_max"), py::arg("dy2") = py::none());
@@ -1717,7 +1726,12 @@ PYBIND11_MODULE(_C, m) {
         py::arg("bn_running_var") = py::none(), py::arg("bn_save_mean") = py::none(),
         py::arg("bn_save_invstd") = py::none(), py::arg("bn_eps") = 1e-5, py::arg("bn_momentum") = 0.1,
         py::arg("bn_num_batches") = py::none());
-  m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("stride"), py::arg("pad"));
+  m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("stride"), py::arg("pad"),
+        py::arg("bn_x") = py::none(), py::arg("bn_mask") = py::none(), py::arg("bn_gamma") = py::none(),
+        py::arg("bn_save_mean") = py::none(), py::arg("bn_save_invstd") = py::none(), py::arg("bn_ws") = py::none(),
+        py::arg("bn_dgamma") = py::none(), py::arg("bn_dbeta") = py::none(), py::arg("bn_grad_assign") = false,
+        "dgrad; with bn_*: also the backward statistics of the BN + ReLU whose output this conv read "
+        "(returns whether they were fused)");
   m.def("conv_wgrad", &conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("dw"), py::arg("stride"), py::arg("pad"),
         py::arg("beta") = 0.0, py::arg("real_channels") = 0,
         "real_channels: channels of x that carry data (the rest zero padding, e.g. 3 of a stem's 8); 0 = all");

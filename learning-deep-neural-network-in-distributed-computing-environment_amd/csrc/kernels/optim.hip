@@ -13,7 +13,6 @@
 #include <cstdlib>
 
 #include "ldnn_common.h"
-#include "ldnn_gemm_tile.h"
 #include "ldnn_kernels.h"
 
 namespace ldnn {
@@ -144,28 +143,6 @@ __global__ void adam_kernel(float* __restrict__ param, float* __restrict__ grad,
 
 __global__ void bump_kernel(float* hp) { hp[1] += 1.f; }
 
-// Split-K weight-gradient slabs ws[s][r][0 .. ldw) -> the fused optimizer update of the
-// weights they sum to (the gradient is never stored): columns [0, ncols) update
-// master[r * ldo + c] (+ state / shadow, OptEpi layout); column ncols, when extra is set,
-// is the bias gradient a ones column of the GEMM's B operand produced -> extra[r].
-template <int EPI>
-__global__ __launch_bounds__(256) void slab_sum_opt_kernel(const float* __restrict__ ws, int splits, int rows,
-                                                           int ldw, int ldo, int ncols, float* __restrict__ extra,
-                                                           OptEpi o) {
-  const int g4 = ncols / 4 + (extra != nullptr ? 1 : 0);
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= (int64_t)rows * g4) return;
-  const int r = (int)(i / g4), c = (int)(i % g4) * 4;
-  const size_t slab = (size_t)rows * ldw;
-  floatx4 v = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(ws + (size_t)r * ldw + c));
-  for (int sp = 1; sp < splits; ++sp)
-    v += __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(ws + sp * slab + (size_t)r * ldw + c));
-  if (c >= ncols) {
-    extra[r] = v[0];
-    return;
-  }
-  opt_update4<EPI>(o, opt_const<EPI>(o), (size_t)r * ldo + c, v);
-}
 
 int g_opt_max_blocks = 2048;  // optimizer grid cap (set_opt_max_blocks: a narrow side-stream update)
 
@@ -199,18 +176,6 @@ hipError_t adam_step(float* param, float* grad, float* m, float* v, uint16_t* sh
   if (n <= 0) return hipSuccess;
   if (opt_nt_env()) adam_kernel<true><<<grid_for((n + 3) / 4), kBlock, 0, s>>>(param, grad, m, v, shadow, hp, grad_scale, ap, n);
   else adam_kernel<false><<<grid_for((n + 3) / 4), kBlock, 0, s>>>(param, grad, m, v, shadow, hp, grad_scale, ap, n);
-  return hipGetLastError();
-}
-
-hipError_t slab_sum_opt(const float* ws, int splits, int rows, int ldw, int ldo, int ncols, float* extra,
-                        const OptEpi& o, int epi, hipStream_t s) {
-  if (rows <= 0 || ncols <= 0) return hipSuccess;
-  if (ncols % 4 || ldo % 4 || ldw % 4 || ncols + (extra ? 1 : 0) > ldw || splits < 1) return hipErrorInvalidValue;
-  const int64_t n = (int64_t)rows * (ncols / 4 + (extra ? 1 : 0));
-  const unsigned g = (unsigned)((n + 255) / 256);
-  if (epi == EPI_OPT_SGD) slab_sum_opt_kernel<EPI_OPT_SGD><<<g, 256, 0, s>>>(ws, splits, rows, ldw, ldo, ncols, extra, o);
-  else if (epi == EPI_OPT_ADAM) slab_sum_opt_kernel<EPI_OPT_ADAM><<<g, 256, 0, s>>>(ws, splits, rows, ldw, ldo, ncols, extra, o);
-  else return hipErrorInvalidValue;
   return hipGetLastError();
 }
 

@@ -28,7 +28,6 @@ messages (BAR/communication.py:4-31).
 from __future__ import annotations
 
 import contextlib
-import os
 import gc
 from dataclasses import dataclass
 
@@ -100,8 +99,7 @@ class StaticMLPEngine:
                  shard_optimizer: bool | None = None, wgrad_combine: bool = True, library_gemms: bool | None = None,
                  fuse_head_dgrad: bool | None = None, library_dgrad: bool | None = None, head_dgrad_mode: int = -1,
                  relu_masks: bool = True, transposed_dgrad: bool = True, bias_ones_column: bool = True,
-                 fuse_head_fwd: bool = True, fuse_head_bwd: bool = True, grad_mix: tuple | None = None,
-                 fuse_optimizer: bool | str | None = None):
+                 fuse_head_fwd: bool = True, fuse_head_bwd: bool = True, grad_mix: tuple | None = None):
         """``grad_mix`` = (hops, local_weight): per-step gradient exchange other than the
         equal all-reduce (world > 1) -- hops 0 with a weight = the reference's
         self-weighted all-reduce (BAR/communication.py:4-10), hops 1 / 2 = ring /
@@ -393,42 +391,6 @@ class StaticMLPEngine:
         self._fuse_head_bwd = bool(fuse_head_bwd and self._head_part is not None and L >= 2
                                    and self._dgrad_epi[L - 1] in (self.C.EPI_NONE, self.C.EPI_DRELU)
                                    and self.layers[L - 1].in_features % 64 == 0 and self._wgrad_splitk[L - 1] > 1)
-        # fuse_optimizer (single-process engines): a hidden layer's weight gradient never
-        # reaches HBM -- the optimizer update of its weights (fp32 master, momentum / Adam
-        # moments, bf16 shadow) runs in the epilogue of the kernel that produces it:
-        # "slab" = the pass that sums a split-K slab wgrad's slabs (slab_sum_opt), "all" /
-        # True = also the four-wave wgrad GEMM's epilogue (gemm_q EPI_OPT_*, row-staged).
-        # dgrad(l) then runs BEFORE wgrad(l): it reads the weights that epilogue overwrites;
-        # the step's separate optimizer launches cover only the rest.  Measured on MI355X
-        # (same box, alternated, profiles/r4/mlp_fused_opt_ab.jsonl): the gemm_q epilogue
-        # update is SLOWER in the headline step (1.628 vs 1.599 ms: its 256 workgroups all
-        # reach the 288 MB read-modify-write at once, +84 us on a 415 us GEMM, more than the
-        # separate 71 us update costs), so the default fuses the slab pass only.
-        # (None: LDNN_FUSE_OPT = 0 | slab | all, default slab -- an A/B knob)
-        if fuse_optimizer is None:
-            fuse_optimizer = os.environ.get("LDNN_FUSE_OPT", "slab")
-        mode = {True: "all", False: "0", "1": "all"}.get(fuse_optimizer, fuse_optimizer)
-        if mode not in ("0", "slab", "all"):
-            raise ValueError(f"fuse_optimizer must be 0 / slab / all, got {fuse_optimizer!r}")
-        self._fused_opt = [False] * L
-        if mode != "0" and not self.distributed and self.optim.name in ("sgd", "adam", "adamw"):
-            for l in range(L):
-                if (self.use_head and l == L - 1) or self._lib_wgrad[l]:
-                    continue
-                if self._wgrad_slab[l] is not None:
-                    self._fused_opt[l] = self.W[l].shape[1] % 4 == 0
-                elif mode == "all" and self._wgrad_ws[l] is None and self._wgrad_splitk[l] <= 1:
-                    self._fused_opt[l] = True
-        fused = sorted((f.seg(self.layers[l].weight).offset,
-                        f.seg(self.layers[l].weight).offset + f.seg(self.layers[l].weight).storage_numel)
-                       for l in range(L) if self._fused_opt[l])
-        self._opt_ranges, pos = [], 0   # what the step's optimizer launches still update
-        for b, e in fused:
-            if b > pos:
-                self._opt_ranges.append((pos, b))
-            pos = e
-        if pos < f.numel:
-            self._opt_ranges.append((pos, f.numel))
         self._build_segments()
         self._slots[0]["segs"] = (self.segments, self.opt_segments)
 
@@ -465,34 +427,8 @@ class StaticMLPEngine:
         self.C.softmax_xent(logits, self.labels, self.dz[L][:, : self.num_classes], self.stats,
                             dbias=self.db[L - 1], num_classes=self.num_classes, grad_scale=1.0 / self.B)
 
-    def _opt_kwargs(self, l) -> dict:
-        """The fused optimizer's state views of layer l's weight (storage layout)."""
-        f, o, seg = self.flat, self.optim, self.flat.seg(self.layers[l].weight)
-        kw = dict(kind=o.name, shadow=self.W[l], hp=self.hp, grad_scale=self._grad_scale,
-                  weight_decay=o.weight_decay)
-        if o.name == "sgd":
-            kw.update(m=f.storage_view(seg, self.mom) if self.mom is not None else None, momentum=o.momentum,
-                      dampening=o.dampening, nesterov=o.nesterov)
-        else:
-            kw.update(m=f.storage_view(seg, self.exp_avg), v=f.storage_view(seg, self.exp_avg_sq),
-                      beta1=o.betas[0], beta2=o.betas[1], eps=o.eps)
-        return kw
-
     def _wgrad(self, l):
         sk = self._wgrad_splitk[l]
-        if self._fused_opt[l]:   # gradient -> optimizer update in the producing kernel
-            master = self.flat.master_storage(self.layers[l].weight)
-            if self._wgrad_slab[l] is not None:
-                extra = None
-                if l == 0 and self._db0_from_wgrad:
-                    self.C.gemm(self.dz[1], self.xp, self._wgrad_slab[0], False, False, tile=256, splitk=sk)
-                    extra = self.db[0]
-                else:
-                    self.C.gemm(self.dz[l + 1], self.h[l], self._wgrad_slab[l], False, False, tile=256, splitk=sk)
-                self.C.slab_sum_opt(self._wgrad_slab[l], master, extra, **self._opt_kwargs(l))
-                return
-            self.C.gemm_opt(self.dz[l + 1], self.h[l], master, False, False, **self._opt_kwargs(l))
-            return
         if self.use_head and l == len(self.layers) - 1:   # also emits the head's bias gradient
             if not self._fuse_head_bwd:   # (else done by head_bwd in _loss)
                 self.C.head_wgrad(self.dz[l + 1], self.h[l], self.dW[l], self.db[l], sk)
@@ -572,17 +508,11 @@ class StaticMLPEngine:
         for l in reversed(range(L)):
             wg = lambda l=l: self._wgrad(l)  # noqa: E731
             wg._ldnn_wgrad = l
-            dg = l > 0 and not (self.head_dgrad and l == L - 1)   # (else done by the head kernel)
-            if self._fused_opt[l]:   # (single process: one segment) the dgrad reads W_l before the update
-                if dg:
-                    pieces[-1].append(lambda l=l: self._dgrad(l))
-                pieces[-1].append(wg)
-                continue
             pieces[-1].append(wg)
             if l in triggers:
                 self._cut_buckets.append(triggers[l])
                 pieces.append([])
-            if dg:
+            if l > 0 and not (self.head_dgrad and l == L - 1):   # (else done by the head kernel)
                 pieces[-1].append(lambda l=l: self._dgrad(l))
         self._cut_buckets.append(len(self.buckets) - 1)
 
@@ -593,7 +523,7 @@ class StaticMLPEngine:
             return f
 
         if not self.distributed:
-            fns = [fn for p in pieces for fn in p] + [lambda b=b, e=e: self._opt(b, e) for b, e in self._opt_ranges]
+            fns = [fn for p in pieces for fn in p] + [lambda: self._opt(0, self.flat.numel)]
             self.segments = [_Segment(run(fns), self.use_graphs)]
             self.opt_segments = []
         elif self.shard:
@@ -1049,12 +979,6 @@ class StaticMLPEngine:
                             + " epilogue)")
             if self._lib_wgrad[l]:
                 d[f"wgrad{l}"] = "hipBLASLt"
-            elif self._fused_opt[l] and self._wgrad_slab[l] is not None:
-                d[f"wgrad{l}"] = (f"ldnn gemm_q split-K x{self._wgrad_splitk[l]} slabs + slab_sum_opt (the "
-                                  f"{self.optim.name} update of W{l} in the slab-summing pass"
-                                  + (", bias grad from a ones column)" if l == 0 and self._db0_from_wgrad else ")"))
-            elif self._fused_opt[l]:
-                d[f"wgrad{l}"] = f"ldnn gemm_opt (gemm_q with the {self.optim.name} update of W{l} as its epilogue)"
             elif self._wgrad_slab[l] is not None:
                 d[f"wgrad{l}"] = (f"ldnn gemm_q split-K x{self._wgrad_splitk[l]} slabs + slab_sum"
                                   + (" (+ bias grad from a ones column)" if l == 0 and self._db0_from_wgrad else ""))
@@ -1065,8 +989,7 @@ class StaticMLPEngine:
                 d[f"dgrad{l}"] = ("hipBLASLt + act_bwd_colsum" if self._lib_dgrad[l] else
                                   "ldnn gemm_q" + (" on transposed W" if self.Wt[l] is not None else "")
                                   + (" (dReLU from bit mask)" if self.mask[l] is not None else " (fused derivative)"))
-        d["optimizer"] = (f"ldnn fused {self.optim.name} (flat fp32 master + bf16 shadow)"
-                          + ("; hidden weights updated in their wgrad epilogues" if any(self._fused_opt) else ""))
+        d["optimizer"] = f"ldnn fused {self.optim.name} (flat fp32 master + bf16 shadow)"
         d["library_gemms"] = sum(v.startswith("hipBLASLt") for v in d.values())
         return d
 

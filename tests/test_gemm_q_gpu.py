@@ -231,3 +231,43 @@ def test_transpose_and_slab_sum_cols():
     tot = ws.sum(0)
     torch.testing.assert_close(dst, tot[:, :784], rtol=1e-6, atol=1e-5)
     torch.testing.assert_close(extra, tot[:, 784], rtol=1e-6, atol=1e-5)
+
+
+@pytest.mark.parametrize("kind", ["sgd", "adam", "adamw"])
+@pytest.mark.parametrize("M,N,K", [(4096, 4096, 4096), (512, 784, 2048)])
+def test_gemm_opt_epilogue_equals_gemm_then_optimizer(kind, M, N, K):
+    """gemm_opt: a weight-gradient GEMM whose epilogue applies SGD (momentum, weight decay) /
+    Adam / AdamW to the fp32 master and refreshes the bf16 shadow -- the four-wave kernel's
+    row-staged update at 4096 x 4096 x 4096 (gemm_q EPI_OPT_*), gemm.hip's at the smaller
+    shape -- == the plain fp32-out GEMM followed by the separate fused optimizer launch."""
+    torch.manual_seed(0)
+    C = _ext.C()
+    dz = (torch.randn(K, M, device="cuda") * 0.1).bfloat16()   # [batch][out]
+    h = torch.randn(K, N, device="cuda").bfloat16()            # [batch][in]
+    master0 = torch.randn(M, N, device="cuda") * 0.05
+    hp = torch.tensor([1e-2 if kind == "sgd" else 1e-3, 3.0], device="cuda")   # lr, Adam step (already bumped)
+    wd = 1e-2
+    # reference: gradient GEMM, then the flat optimizer kernel
+    g = torch.empty(M, N, device="cuda")
+    C.gemm(dz, h, g, False, False)
+    torch.testing.assert_close(g, dz.float().t() @ h.float(), rtol=2e-3, atol=2e-3)
+    mr, m1, v1 = master0.clone(), torch.randn(M, N, device="cuda") * 1e-3, torch.rand(M, N, device="cuda") * 1e-5
+    sr = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+    mf, m2, v2 = master0.clone(), m1.clone(), v1.clone()
+    sf = torch.empty_like(sr)
+    if kind == "sgd":
+        C.sgd_step(mr.view(-1), g.view(-1), m1.view(-1), sr.view(-1), hp, 0.5, 0.9, 0.0, wd, False, False)
+        C.gemm_opt(dz, h, mf, False, False, "sgd", m=m2, shadow=sf, hp=hp, grad_scale=0.5, momentum=0.9,
+                   weight_decay=wd)
+        states = ((m2, m1),)
+    else:
+        C.adam_step(mr.view(-1), g.view(-1), m1.view(-1), v1.view(-1), sr.view(-1), hp, 0.5, 0.9, 0.999, 1e-8, wd,
+                    kind == "adamw")
+        C.gemm_opt(dz, h, mf, False, False, kind, m=m2, v=v2, shadow=sf, hp=hp, grad_scale=0.5, weight_decay=wd)
+        states = ((m2, m1), (v2, v1))
+    torch.cuda.synchronize()
+    # the same gradient (fp32 accumulate, tile order identical), the same update arithmetic
+    torch.testing.assert_close(mf, mr, rtol=1e-5, atol=1e-7)
+    for a, b in states:
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-9)
+    assert (sf.float() - sr.float()).abs().max().item() <= 2 ** -7 * mr.abs().max().item()
