@@ -1541,8 +1541,10 @@ PYBIND11_MODULE(_C, m) {
         check(ldnn::transpose_bf16(bf16_ptr(in), bf16_mut(out), (int)in.size(0), (int)in.size(1), (int)ldi, (int)ldo,
                                    cur_stream(in)), "transpose_bf16");
       }, "out = in^T (bf16)", py::arg("in"), py::arg("out"));
-  m.def("slab_sum_cols", [](const at::Tensor& ws, const at::Tensor& out, const c10::optional<at::Tensor>& extra) {
-        // ws [splits][rows][ldw] fp32 -> out [rows][ncols] (+ extra[rows] = column ncols of the sum)
+  m.def("slab_sum_cols", [](const at::Tensor& ws, const at::Tensor& out, const c10::optional<at::Tensor>& extra,
+                            const c10::optional<at::Tensor>& tail) {
+        // ws [splits][rows][ldw] fp32 -> out [rows][ncols] (+ extra[rows] = column ncols of the sum);
+        // tail [rows][tw] fp32: columns ldw .. of the sum (the slabs cover only the first ldw)
         check_dev(ws, at::kFloat, "ws");
         check_dev(out, at::kFloat, "out");
         TORCH_CHECK(ws.dim() == 3 && ws.is_contiguous() && out.dim() == 2 && out.size(0) == ws.size(1) &&
@@ -1553,12 +1555,22 @@ PYBIND11_MODULE(_C, m) {
           TORCH_CHECK(extra->is_contiguous() && extra->numel() >= ws.size(1), "slab_sum_cols: bad extra");
           ex = extra->data_ptr<float>();
         }
+        const float* tp = nullptr;
+        int tw = 0;
+        if (tail.has_value()) {
+          check_dev(*tail, at::kFloat, "tail");
+          TORCH_CHECK(tail->dim() == 2 && tail->is_contiguous() && tail->size(0) == ws.size(1) &&
+                          aligned16(tail->data_ptr()), "slab_sum_cols: tail must be a dense [rows][tw] fp32 tensor");
+          tp = tail->data_ptr<float>();
+          tw = (int)tail->size(1);
+        }
         c10::hip::HIPGuardMasqueradingAsCUDA g(ws.device());
         check(ldnn::slab_sum_cols(ws.data_ptr<float>(), (int)ws.size(0), (int)ws.size(1), (int)ws.size(2),
-                                  out.data_ptr<float>(), (int)out.stride(0), (int)out.size(1), ex, cur_stream(ws)),
+                                  out.data_ptr<float>(), (int)out.stride(0), (int)out.size(1), ex, cur_stream(ws), tp,
+                                  tw),
               "slab_sum_cols");
-      }, "sum split-K slabs into out (and one extra column)", py::arg("ws"), py::arg("out"),
-      py::arg("extra") = py::none());
+      }, "sum split-K slabs into out (and one extra column; columns past the slabs from a tail product)",
+      py::arg("ws"), py::arg("out"), py::arg("extra") = py::none(), py::arg("tail") = py::none());
   m.def("slab_sum", [](const at::Tensor& ws, const at::Tensor& out, double beta) {
         // out = sum over the leading dim of ws (+ beta * out); fp32, dense, same trailing size
         check_dev(ws, at::kFloat, "ws");

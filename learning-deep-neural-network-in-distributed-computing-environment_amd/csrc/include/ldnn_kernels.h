@@ -257,9 +257,10 @@ hipError_t zero2d_f32(float* p, int rows, int cols, int ld, hipStream_t s);
 hipError_t transpose_bf16(const uint16_t* in, uint16_t* out, int rows, int cols, int ldi, int ldo, hipStream_t s);
 // NCHW (fp32 / bf16) -> NHWC bf16 [N][HW][cp], pad channels zeroed (cp % 8 == 0)
 hipError_t nchw_to_nhwc(const void* src, bool src_f32, uint16_t* dst, int N, int C, int HW, int cp, hipStream_t s);
-// sum split-K slabs [splits][rows][ldw] into out[rows][ncols] (stride ldo); extra[r] = column ncols
+// sum split-K slabs [splits][rows][ldw] into out[rows][ncols] (stride ldo); extra[r] = column ncols;
+// tail (optional, [rows][tw]): columns ldw .. ncols (and extra) taken from it instead
 hipError_t slab_sum_cols(const float* ws, int splits, int rows, int ldw, float* out, int ldo, int ncols, float* extra,
-                         hipStream_t s);
+                         hipStream_t s, const float* tail = nullptr, int tw = 0);
 hipError_t cast_bf16_f32(const uint16_t* x, float* y, int64_t n, hipStream_t s);
 // y = a*x + b*y1 + c*y2 (fp32, in place on x allowed); optional bf16 shadow of y
 hipError_t mix3_f32(float* out, const float* x, const float* y1, const float* y2, float a, float b, float c,

@@ -36,6 +36,7 @@ for step in "$@"; do
            done; done; (exit $rc) ;;
     gemmxf:*) $T 300 python -u scripts/gemm_q_xf.py --K ${step#gemmxf:} --variants ${XF_VARIANTS:-32,33,37,96,160} \
                >> $O/gemmxf.jsonl 2>> $O/gemmxf.err ;;
+    script:*) f=${step#script:}; $T 300 python -u scripts/$f >> $O/${f%.py}.jsonl 2>> $O/${f%.py}.err ;;
     micro:*) m=${step#micro:}; rc=0
              for e in ${MICRO_ENVS:-X=0}; do
                echo "{\"env\": \"$e\"}" >> $O/micro_$m.jsonl
