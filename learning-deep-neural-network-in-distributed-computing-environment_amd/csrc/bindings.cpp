@@ -953,52 +953,15 @@ bool conv_fwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& y, int
   return done;
 }
 
-// bn_*: fuse the backward statistics of the BatchNorm + ReLU that produced this conv's input
-// (dx = that BN output's gradient, this conv its only consumer): bn_x = the BN's input [M][C],
-// bn_mask its ReLU bits, save_mean / save_invstd its batch statistics, bn_ws its workspace.
-// Returns whether the epilogue did it (then the BN backward runs with stats_ready=True).
-bool conv_dgrad(const at::Tensor& dy, const at::Tensor& w, const at::Tensor& dx, int64_t stride, int64_t pad,
-                const c10::optional<at::Tensor>& bn_x, const c10::optional<at::Tensor>& bn_mask,
-                const c10::optional<at::Tensor>& bn_gamma, const c10::optional<at::Tensor>& bn_save_mean,
-                const c10::optional<at::Tensor>& bn_save_invstd, const c10::optional<at::Tensor>& bn_ws,
-                const c10::optional<at::Tensor>& bn_dgamma, const c10::optional<at::Tensor>& bn_dbeta,
-                bool bn_grad_assign) {
+void conv_dgrad(const at::Tensor& dy, const at::Tensor& w, const at::Tensor& dx, int64_t stride, int64_t pad) {
   check_dev(dy, at::kBFloat16, "dy");
   check_dev(w, at::kBFloat16, "w");
   check_dev(dx, at::kBFloat16, "dx");
   ldnn::ConvShape s = conv_shape(dx, w, dy, stride, pad);
   c10::hip::HIPGuardMasqueradingAsCUDA g(dy.device());
   const ConvWs ws = conv_ws(s, 1, dy);
-  ldnn::BnBwdFuse fuse{};
-  const ldnn::BnBwdFuse* fp = nullptr;
-  if (bn_x.has_value()) {
-    const int C = s.C;
-    const int64_t M = (int64_t)s.N * s.H * s.W;
-    check_dev(*bn_x, at::kBFloat16, "bn_x");
-    TORCH_CHECK(bn_x->is_contiguous() && bn_x->numel() == M * C, "conv_dgrad: bn_x must be the BN input [M][C]");
-    TORCH_CHECK(bn_mask.has_value() && bn_mask->is_contiguous() && bn_mask->numel() == M * C / 8,
-                "conv_dgrad: bn_mask must be the BN's ReLU bits [M][C/8]");
-    check_dev(*bn_mask, at::kByte, "bn_mask");
-    ldnn::BnArgs a{};
-    a.M = (int)M;
-    a.C = C;
-    a.gamma = fptr_opt(bn_gamma, C, "bn_gamma");
-    a.save_mean = fptr_opt(bn_save_mean, C, "bn_save_mean");
-    a.save_invstd = fptr_opt(bn_save_invstd, C, "bn_save_invstd");
-    TORCH_CHECK(a.save_mean && a.save_invstd && aligned16(a.save_mean) && aligned16(a.save_invstd),
-                "conv_dgrad: fused BN statistics need 16-B aligned save_mean / save_invstd");
-    a.ws = fptr_opt(bn_ws, ldnn::bn_workspace_floats(C), "bn_ws");
-    TORCH_CHECK(a.ws, "conv_dgrad: fused BN statistics need the BN workspace");
-    fuse.fin = ldnn::bn_backward_fin_conv(a, fptr_opt(bn_dgamma, C, "bn_dgamma"), fptr_opt(bn_dbeta, C, "bn_dbeta"),
-                                          bn_grad_assign);
-    fuse.x = bf16_ptr(*bn_x);
-    fuse.mask = bn_mask->data_ptr<uint8_t>();
-    fp = &fuse;
-  }
-  bool done = false;
-  check(ldnn::conv2d_dgrad(s, bf16_ptr(dy), bf16_ptr(w), bf16_mut(dx), cur_stream(dy), ws.ws(), ws.c(), fp, &done),
+  check(ldnn::conv2d_dgrad(s, bf16_ptr(dy), bf16_ptr(w), bf16_mut(dx), cur_stream(dy), ws.ws(), ws.c()),
         "conv2d_dgrad");
-  return done;
 }
 
 void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& dw, int64_t stride, int64_t pad,
@@ -1084,8 +1047,7 @@ void bn_bwd(const at::Tensor& x, const at::Tensor& y, const at::Tensor& dy, cons
             const c10::optional<at::Tensor>& dres, const c10::optional<at::Tensor>& gamma,
             const at::Tensor& save_mean, const at::Tensor& save_invstd, const at::Tensor& ws,
             const c10::optional<at::Tensor>& dgamma, const c10::optional<at::Tensor>& dbeta, bool relu,
-            const c10::optional<at::Tensor>& mask, bool grad_assign, const c10::optional<at::Tensor>& dy2,
-            bool stats_ready) {
+            const c10::optional<at::Tensor>& mask, bool grad_assign, const c10::optional<at::Tensor>& dy2) {
   check_dev(x, at::kBFloat16, "x");
   check_dev(dy, at::kBFloat16, "dy");
   check_dev(dx, at::kBFloat16, "dx");
@@ -1118,10 +1080,6 @@ void bn_bwd(const at::Tensor& x, const at::Tensor& y, const at::Tensor& dy, cons
     check_dev(*dres, at::kBFloat16, "dres");
     TORCH_CHECK(dres->sizes() == x.sizes() && dres->is_contiguous(), "bn_bwd: dres layout");
     dr = bf16_mut(*dres);
-  }
-  if (stats_ready) {   // coefficients + dgamma / dbeta already finalized (conv_dgrad's fused statistics)
-    check(ldnn::bn_backward_apply(a, bf16_ptr(dy), bf16_mut(dx), dr, cur_stream(x)), "bn_backward_apply");
-    return;
   }
   check(ldnn::bn_backward(a, bf16_ptr(dy), bf16_mut(dx), dr, fptr_opt(dgamma, C, "dgamma"),
                           fptr_opt(dbeta, C, "dbeta"), cur_stream(x), grad_assign),
@@ -1541,10 +1499,8 @@ PYBIND11_MODULE(_C, m) {
         check(ldnn::transpose_bf16(bf16_ptr(in), bf16_mut(out), (int)in.size(0), (int)in.size(1), (int)ldi, (int)ldo,
                                    cur_stream(in)), "transpose_bf16");
       }, "out = in^T (bf16)", py::arg("in"), py::arg("out"));
-  m.def("slab_sum_cols", [](const at::Tensor& ws, const at::Tensor& out, const c10::optional<at::Tensor>& extra,
-                            const c10::optional<at::Tensor>& tail) {
-        // ws [splits][rows][ldw] fp32 -> out [rows][ncols] (+ extra[rows] = column ncols of the sum);
-        // tail [rows][tw] fp32: columns ldw .. of the sum (the slabs cover only the first ldw)
+  m.def("slab_sum_cols", [](const at::Tensor& ws, const at::Tensor& out, const c10::optional<at::Tensor>& extra) {
+        // ws [splits][rows][ldw] fp32 -> out [rows][ncols] (+ extra[rows] = column ncols of the sum)
         check_dev(ws, at::kFloat, "ws");
         check_dev(out, at::kFloat, "out");
         TORCH_CHECK(ws.dim() == 3 && ws.is_contiguous() && out.dim() == 2 && out.size(0) == ws.size(1) &&
@@ -1555,22 +1511,12 @@ PYBIND11_MODULE(_C, m) {
           TORCH_CHECK(extra->is_contiguous() && extra->numel() >= ws.size(1), "slab_sum_cols: bad extra");
           ex = extra->data_ptr<float>();
         }
-        const float* tp = nullptr;
-        int tw = 0;
-        if (tail.has_value()) {
-          check_dev(*tail, at::kFloat, "tail");
-          TORCH_CHECK(tail->dim() == 2 && tail->is_contiguous() && tail->size(0) == ws.size(1) &&
-                          aligned16(tail->data_ptr()), "slab_sum_cols: tail must be a dense [rows][tw] fp32 tensor");
-          tp = tail->data_ptr<float>();
-          tw = (int)tail->size(1);
-        }
         c10::hip::HIPGuardMasqueradingAsCUDA g(ws.device());
         check(ldnn::slab_sum_cols(ws.data_ptr<float>(), (int)ws.size(0), (int)ws.size(1), (int)ws.size(2),
-                                  out.data_ptr<float>(), (int)out.stride(0), (int)out.size(1), ex, cur_stream(ws), tp,
-                                  tw),
+                                  out.data_ptr<float>(), (int)out.stride(0), (int)out.size(1), ex, cur_stream(ws)),
               "slab_sum_cols");
-      }, "sum split-K slabs into out (and one extra column; columns past the slabs from a tail product)",
-      py::arg("ws"), py::arg("out"), py::arg("extra") = py::none(), py::arg("tail") = py::none());
+      }, "sum split-K slabs into out (and one extra column)", py::arg("ws"), py::arg("out"),
+      py::arg("extra") = py::none());
   m.def("slab_sum", [](const at::Tensor& ws, const at::Tensor& out, double beta) {
         // out = sum over the leading dim of ws (+ beta * out); fp32, dense, same trailing size
         check_dev(ws, at::kFloat, "ws");
@@ -1706,7 +1652,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_bwd", &bn_bwd, py::arg("x"), py::arg("y"), py::arg("dy"), py::arg("dx"), py::arg("dres"),
         py::arg("gamma"), py::arg("save_mean"), py::arg("save_invstd"), py::arg("ws"), py::arg("dgamma"),
         py::arg("dbeta"), py::arg("relu"), py::arg("mask") = py::none(), py::arg("grad_assign") = false,
-        py::arg("dy2") = py::none(), py::arg("stats_ready") = false);
+        py::arg("dy2") = py::none());
   m.def("pool_fwd", &pool_fwd);
   m.def("pool_bwd", &pool_bwd, py::arg("dy"), py::arg("argmax"), py::arg("dx"), py::arg("R"), py::arg("S"),
         py::arg("stride"), py::arg("pad"), py::arg("is_max"), py::arg("dy2") = py::none());
@@ -1738,12 +1684,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("bn_running_var") = py::none(), py::arg("bn_save_mean") = py::none(),
         py::arg("bn_save_invstd") = py::none(), py::arg("bn_eps") = 1e-5, py::arg("bn_momentum") = 0.1,
         py::arg("bn_num_batches") = py::none());
-  m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("stride"), py::arg("pad"),
-        py::arg("bn_x") = py::none(), py::arg("bn_mask") = py::none(), py::arg("bn_gamma") = py::none(),
-        py::arg("bn_save_mean") = py::none(), py::arg("bn_save_invstd") = py::none(), py::arg("bn_ws") = py::none(),
-        py::arg("bn_dgamma") = py::none(), py::arg("bn_dbeta") = py::none(), py::arg("bn_grad_assign") = false,
-        "dgrad; with bn_*: also the backward statistics of the BN + ReLU whose output this conv read "
-        "(returns whether they were fused)");
+  m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("stride"), py::arg("pad"));
   m.def("conv_wgrad", &conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("dw"), py::arg("stride"), py::arg("pad"),
         py::arg("beta") = 0.0, py::arg("real_channels") = 0,
         "real_channels: channels of x that carry data (the rest zero padding, e.g. 3 of a stem's 8); 0 = all");

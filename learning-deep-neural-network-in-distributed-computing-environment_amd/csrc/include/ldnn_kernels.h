@@ -113,12 +113,8 @@ struct BnFin;  // (BatchNorm finalize state, below)
 hipError_t conv2d_fwd(const ConvShape& s, const uint16_t* x, const uint16_t* w, uint16_t* y, const float* bias,
                       int epi, hipStream_t st, float* ws = nullptr, int* cnt = nullptr, const BnFin* bn = nullptr,
                       bool* bn_done = nullptr);
-struct BnBwdFuse;
-// bnb (optional): fuse the backward statistics of the BN + ReLU that produced this conv's input
-// (LDS-DMA path, stride 1, no slab split-K); *bnb_done reports whether that happened.
 hipError_t conv2d_dgrad(const ConvShape& s, const uint16_t* dy, const uint16_t* w, uint16_t* dx, hipStream_t st,
-                        float* ws = nullptr, int* cnt = nullptr, const BnBwdFuse* bnb = nullptr,
-                        bool* bnb_done = nullptr);
+                        float* ws = nullptr, int* cnt = nullptr);
 hipError_t conv2d_wgrad(const ConvShape& s, const uint16_t* dy, const uint16_t* x, float* dw, float beta,
                         hipStream_t st, float* ws = nullptr);
 // LDS-DMA fast path (conv_lds.hip): hipErrorNotSupported outside its shape set
@@ -127,9 +123,8 @@ hipError_t conv2d_wgrad(const ConvShape& s, const uint16_t* dy, const uint16_t* 
 hipError_t conv2d_fwd_lds(const ConvShape& s, const uint16_t* x, const uint16_t* w, uint16_t* y, const float* bias,
                           int epi, hipStream_t st, float* ws, int* cnt, const BnFin* bn = nullptr,
                           bool* bn_used = nullptr);
-struct BnBwdFuse;  // (below, after BnFin)
 hipError_t conv2d_dgrad_lds(const ConvShape& s, const uint16_t* dy, const uint16_t* w, uint16_t* dx, hipStream_t st,
-                            float* ws, int* cnt, const BnBwdFuse* bnb = nullptr, bool* bnb_used = nullptr);
+                            float* ws, int* cnt);
 hipError_t conv2d_wgrad_lds(const ConvShape& s, const uint16_t* dy, const uint16_t* x, float* dw, float beta,
                             hipStream_t st, float* ws);
 struct ConvWorkspace {
@@ -192,14 +187,6 @@ struct BnFin {
   int64_t* num_batches;       // fwd: += 1 (BatchNorm2d.num_batches_tracked), nullable
   float eps, momentum;
 };
-// Fused backward statistics of the BatchNorm + ReLU whose output a stride-1 conv read (its
-// only consumer): the dgrad epilogue sums dx * relu' and dx * relu' * x^ per channel and the
-// last tile finalizes (fin = that BN's backward BnFin: coefficients, dgamma / dbeta).
-struct BnBwdFuse {
-  BnFin fin;
-  const uint16_t* x;     // the BN's input [M][C]
-  const uint8_t* mask;   // its ReLU bit mask [M][C / 8]
-};
 // Training-mode forward finalize state of a BN (its ws accumulators / ticket / coef).
 BnFin bn_forward_fin(const BnArgs& a);
 // ... for a producing conv's epilogue (its kBnCopies accumulator copies in ws).
@@ -210,11 +197,6 @@ hipError_t bn_forward_apply(const BnArgs& a, hipStream_t s);
 // branch); dgamma / dbeta are ACCUMULATED (flat gradient buffer)
 hipError_t bn_backward(const BnArgs& a, const uint16_t* dy, uint16_t* dx, uint16_t* dres, float* dgamma,
                        float* dbeta, hipStream_t s, bool grad_assign = false);
-// The apply pass alone, with the coefficients a fused statistics pass (a dgrad epilogue,
-// conv2d_dgrad's bnb) left in a.ws
-hipError_t bn_backward_apply(const BnArgs& a, const uint16_t* dy, uint16_t* dx, uint16_t* dres, hipStream_t s);
-// That BN's backward finalize state (its ws accumulators / ticket / coefficients).
-BnFin bn_backward_fin_conv(const BnArgs& a, float* dgamma, float* dbeta, bool grad_assign);
 // Residual block tail with a BatchNorm on both branches: y = relu(bn_a(a.x) + bn_b(b.x)), the
 // shortcut BN's output never stored (a.relu, both training mode; ready_*: statistics already
 // finalized into the ws by the producing convs).  a.y / a.mask: the output and its ReLU bits.
@@ -257,10 +239,9 @@ hipError_t zero2d_f32(float* p, int rows, int cols, int ld, hipStream_t s);
 hipError_t transpose_bf16(const uint16_t* in, uint16_t* out, int rows, int cols, int ldi, int ldo, hipStream_t s);
 // NCHW (fp32 / bf16) -> NHWC bf16 [N][HW][cp], pad channels zeroed (cp % 8 == 0)
 hipError_t nchw_to_nhwc(const void* src, bool src_f32, uint16_t* dst, int N, int C, int HW, int cp, hipStream_t s);
-// sum split-K slabs [splits][rows][ldw] into out[rows][ncols] (stride ldo); extra[r] = column ncols;
-// tail (optional, [rows][tw]): columns ldw .. ncols (and extra) taken from it instead
+// sum split-K slabs [splits][rows][ldw] into out[rows][ncols] (stride ldo); extra[r] = column ncols
 hipError_t slab_sum_cols(const float* ws, int splits, int rows, int ldw, float* out, int ldo, int ncols, float* extra,
-                         hipStream_t s, const float* tail = nullptr, int tw = 0);
+                         hipStream_t s);
 hipError_t cast_bf16_f32(const uint16_t* x, float* y, int64_t n, hipStream_t s);
 // y = a*x + b*y1 + c*y2 (fp32, in place on x allowed); optional bf16 shadow of y
 hipError_t mix3_f32(float* out, const float* x, const float* y1, const float* y2, float a, float b, float c,

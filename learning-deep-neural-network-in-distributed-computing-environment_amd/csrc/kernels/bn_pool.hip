@@ -1082,29 +1082,6 @@ BnFin bn_backward_fin(const BnArgs& a, float* dgamma, float* dbeta, bool grad_as
 }
 }  // namespace
 
-BnFin bn_backward_fin_conv(const BnArgs& a, float* dgamma, float* dbeta, bool grad_assign) {
-  return bn_backward_fin(a, dgamma, dbeta, grad_assign);
-}
-
-hipError_t bn_backward_apply(const BnArgs& a, const uint16_t* dy, uint16_t* dx, uint16_t* dres, hipStream_t s) {
-  const int M = a.M, C = a.C;
-  if (C % 8) return hipErrorInvalidValue;
-  if (M <= 0) return hipSuccess;
-  const RedGeo g = red_geo(M, C);
-  const dim3 grid(g.gx, g.gy);
-  const float* coef = a.ws + 6 * C;
-  if (a.relu && a.mask)
-    bn_bwd_apply_kernel<true, true><<<grid, 256, 0, s>>>(a.x, dy, nullptr, coef, dx, dres, M, C, g.rpb, g.lanes,
-                                                         g.rl, a.mask, a.dy2);
-  else if (a.relu)
-    bn_bwd_apply_kernel<true><<<grid, 256, 0, s>>>(a.x, dy, a.y, coef, dx, dres, M, C, g.rpb, g.lanes, g.rl, nullptr,
-                                                   a.dy2);
-  else
-    bn_bwd_apply_kernel<false><<<grid, 256, 0, s>>>(a.x, dy, nullptr, coef, dx, dres, M, C, g.rpb, g.lanes, g.rl,
-                                                    nullptr, a.dy2);
-  return hipGetLastError();
-}
-
 hipError_t bn_dual_backward(const BnArgs& a, const BnArgs& b, const uint16_t* dy, uint16_t* dx, uint16_t* dr,
                             float* dgamma_a, float* dbeta_a, float* dgamma_b, float* dbeta_b, bool assign_a,
                             bool assign_b, hipStream_t s) {

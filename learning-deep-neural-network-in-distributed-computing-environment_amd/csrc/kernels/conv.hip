@@ -341,10 +341,9 @@ hipError_t conv2d_fwd(const ConvShape& s, const uint16_t* x, const uint16_t* w, 
 }
 
 hipError_t conv2d_dgrad(const ConvShape& s, const uint16_t* dy, const uint16_t* w, uint16_t* dx, hipStream_t st,
-                        float* ws, int* cnt, const BnBwdFuse* bnb, bool* bnb_done) {
-  if (bnb_done) *bnb_done = false;
+                        float* ws, int* cnt) {
   if (g_conv_impl == 0) {
-    const hipError_t e = conv2d_dgrad_lds(s, dy, w, dx, st, ws, cnt, bnb, bnb_done);
+    const hipError_t e = conv2d_dgrad_lds(s, dy, w, dx, st, ws, cnt);
     if (e != hipErrorNotSupported) return e;
   }
   if (g_conv_impl == 0 && s.C == 8 && s.K % 8 == 0 && s.K * s.R * s.S * 8 <= kDgradC8MaxW && s.stride >= 1) {

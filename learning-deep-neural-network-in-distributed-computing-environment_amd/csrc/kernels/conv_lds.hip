@@ -69,12 +69,8 @@ struct LArgs {
   FastDiv f_cw[2], f_ch[2];      // stride-2 dgrad class rows: (W - pw + 1) / 2, (H - ph + 1) / 2
   float* ws;         // split-K: combine slabs (with cnt) or wgrad partial slabs [split][M][N] (without)
   int* cnt;          // split-K arrival counters of the in-launch combine
-  int bn_stats;      // 1 (fwd): accumulate + finalize the next BatchNorm's statistics (bn);
-                     // 2 (stride-1 dgrad): the backward statistics of the BatchNorm + ReLU whose output
-                     // this conv read -- sum dy' and sum dy' x^ (dy' = dx masked by the ReLU bits)
+  int bn_stats;      // fwd: accumulate + finalize the next BatchNorm's statistics (bn)
   BnFin bn;
-  const bf16_t* bnb_x;     // bn_stats 2: that BatchNorm's input [M][C]
-  const uint8_t* bnb_mask; // bn_stats 2: its ReLU bit mask [M][C / 8]
   int tap_major;     // fwd / dgrad K-tile order: 0 = channel block fastest, 1 = filter tap fastest
   int f32_rows;      // fp32 outputs (wgrad, split-K slabs) through the row-coalesced LDS epilogue
   int bf16_rows;     // bf16 outputs (fwd y, stride-1 dgrad dx) through the row-coalesced LDS epilogue
@@ -486,84 +482,6 @@ __device__ __forceinline__ void bn_stats_epilogue(const LArgs& a, const Geo& g, 
   bn_finalize_last<false, kBnCopies>(a.bn, g.M, a.N, tiles_of(a), red, lds_floats);
 }
 
-// The backward twin of bn_stats_epilogue, for a stride-1 dgrad whose output dx is the
-// gradient of a BatchNorm + ReLU output (the BN's only consumer is this conv): from the
-// tile's bf16 dx values (exactly what the BN backward reads), per channel
-//   S0 = sum dx * relu'    S1 = sum dx * relu' * (x - mean) * invstd
-// over the tile's valid rows (relu' from the BN's bit mask, x its input), reduced like
-// the forward statistics, then the last tile finalizes the backward coefficients and
-// dgamma / dbeta (bn_finalize_last<true>): the BN backward runs only its apply pass.
-template <int WM, int WN>
-__device__ __forceinline__ void bnb_stats_epilogue(const LArgs& a, const Geo& g, floatx4 (&acc)[4][4], int mbase,
-                                                   int n0, int wm, int wn, int lane, int tile, char* smem,
-                                                   int lds_floats) {
-  constexpr int BN = WN * 64;
-  float* red = reinterpret_cast<float*>(smem);  // [WM][BN][2]
-  __syncthreads();  // every wave is done with the operand stages / its store staging
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int nc = n0 + wn * 64 + j * 16 + 4 * (lane >> 4);  // channels nc .. nc + 3
-    const bool cok = nc < a.N;
-    float mu[4] = {0.f, 0.f, 0.f, 0.f}, is[4] = {0.f, 0.f, 0.f, 0.f};
-    if (cok) {
-      const floatx4 m4 = *reinterpret_cast<const floatx4*>(a.bn.save_mean + nc);
-      const floatx4 i4 = *reinterpret_cast<const floatx4*>(a.bn.save_invstd + nc);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        mu[r] = m4[r];
-        is[r] = i4[r];
-      }
-    }
-    float s0[4] = {0.f, 0.f, 0.f, 0.f}, s1[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int m = mbase + i * 16 + (lane & 15);
-      if (!cok || m >= g.M) continue;
-      const size_t o = (size_t)m * a.N + nc;
-      const u16x4 xv = *reinterpret_cast<const u16x4*>(a.bnb_x + o);
-      const uint32_t mb = (uint32_t)a.bnb_mask[o >> 3] >> (nc & 7);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float v = ((mb >> r) & 1u) ? bf2f(f2bf(acc[j][i][r])) : 0.f;
-        s0[r] += v;
-        s1[r] += v * (bf2f(xv[r]) - mu[r]) * is[r];
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) {
-        s0[r] += __shfl_xor(s0[r], o, 64);
-        s1[r] += __shfl_xor(s1[r], o, 64);
-      }
-    }
-    if ((lane & 15) == 0) {
-      const int lc = wn * 64 + j * 16 + 4 * (lane >> 4);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        red[(wm * BN + lc + r) * 2] = s0[r];
-        red[(wm * BN + lc + r) * 2 + 1] = s1[r];
-      }
-    }
-  }
-  __syncthreads();
-  float* accc = a.bn.acc + (size_t)(tile % kBnCopies) * 2 * a.N;
-  for (int t = threadIdx.x; t < BN; t += blockDim.x) {
-    const int c = n0 + t;
-    if (c >= a.N) continue;
-    float s0 = 0.f, s1 = 0.f;
-#pragma unroll
-    for (int q = 0; q < WM; ++q) {
-      s0 += red[(q * BN + t) * 2];
-      s1 += red[(q * BN + t) * 2 + 1];
-    }
-    bn_acc_add(accc + c, s0);
-    bn_acc_add(accc + a.N + c, s1);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's atomics have completed
-  bn_finalize_last<true, kBnCopies>(a.bn, g.M, a.N, tiles_of(a), red, lds_floats);
-}
-
 // Direct epilogue with the class row remap: GEMM row m of a stride-2 dgrad
 // class is pixel (n, 2*h2 + hoff, 2*w2 + woff) of dx.
 __device__ __forceinline__ void store_remapped(const LArgs& a, const Geo& g, floatx4 (&acc)[4][4], int mbase,
@@ -793,18 +711,12 @@ __device__ __forceinline__ void conv_tail(const LArgs& a, const Geo& g, floatx4 
       if constexpr (!DGRAD && EPI == EPI_NONE) {
         if (a.bn_stats) bn_stats_epilogue<WM, WN>(a, g, acc, mb, n0, wm, wn, lane, bx, smem, lds_floats);
       }
-      if constexpr (DGRAD && EPI == EPI_NONE) {
-        if (a.bn_stats == 2) bnb_stats_epilogue<WM, WN>(a, g, acc, mb, n0, wm, wn, lane, bx, smem, lds_floats);
-      }
       return;
     }
   }
   epilogue<EPI, OUT_F32, 4, 4>(p, acc, mb, nbase, lane);
   if constexpr (!DGRAD && !OUT_F32 && EPI == EPI_NONE) {
     if (a.bn_stats) bn_stats_epilogue<WM, WN>(a, g, acc, mb, n0, wm, wn, lane, bx, smem, lds_floats);
-  }
-  if constexpr (DGRAD && !OUT_F32 && EPI == EPI_NONE) {
-    if (a.bn_stats == 2) bnb_stats_epilogue<WM, WN>(a, g, acc, mb, n0, wm, wn, lane, bx, smem, lds_floats);
   }
 }
 
@@ -2184,21 +2096,11 @@ hipError_t conv2d_fwd_lds(const ConvShape& s, const uint16_t* x, const uint16_t*
 }
 
 hipError_t conv2d_dgrad_lds(const ConvShape& s, const uint16_t* dy, const uint16_t* w, uint16_t* dx, hipStream_t st,
-                            float* ws, int* cnt, const BnBwdFuse* bnb, bool* bnb_used) {
-  if (bnb_used) *bnb_used = false;
+                            float* ws, int* cnt) {
   if (s.K % 64 != 0 || !shape_ok(s)) return hipErrorNotSupported;
   if (s.N * s.H * s.W <= 0) return hipSuccess;
   Plan pl = plan_dgrad(s);
   LArgs a = base_args(s);
-  // the fused BN-backward statistics need every output tile finished in this launch (no slab
-  // split-K: its sums happen in a second kernel) and stride-1 rows (pixel = GEMM row)
-  if (bnb != nullptr && s.stride == 1 && !(pl.splits > 1 && pl.slab) && s.C % 8 == 0) {
-    a.bn_stats = 2;
-    a.bn = bnb->fin;
-    a.bnb_x = reinterpret_cast<const bf16_t*>(bnb->x);
-    a.bnb_mask = bnb->mask;
-    if (bnb_used) *bnb_used = true;
-  }
   a.out = dx;
   a.M = s.N * s.H * s.W;
   a.N = s.C;

@@ -212,25 +212,18 @@ __global__ __launch_bounds__(256) void transpose_bf16_kernel(const bf16_t* __res
 
 // split-K slabs ws[s][r][0 .. ldw) -> out[r][0 .. ncols) (row stride ldo) and, when
 // extra != nullptr, extra[r] = column ncols (a GEMM whose B operand carries a ones
-// column: the bias gradient comes out of the weight-gradient GEMM).  With a tail
-// ([rows][tw] fp32, its own GEMM's finished product), columns ldw .. of the sum come from
-// tail[r][c - ldw] instead: the slabs cover only the full 256-wide column tiles.
+// column: the bias gradient comes out of the weight-gradient GEMM)
 __global__ __launch_bounds__(256) void slab_sum_cols_kernel(const float* __restrict__ ws, int splits, int rows, int ldw,
                                                             float* __restrict__ out, int ldo, int ncols,
-                                                            float* __restrict__ extra, const float* __restrict__ tail,
-                                                            int tw) {
+                                                            float* __restrict__ extra) {
   const int g4 = (ncols + 4) / 4;  // float4 groups per row, incl. the one holding column ncols
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= (int64_t)rows * g4) return;
   const int r = (int)(i / g4), c = (int)(i % g4) * 4;
   const size_t slab = (size_t)rows * ldw;
-  floatx4 v;
-  if (tail != nullptr && c >= ldw) {
-    v = *reinterpret_cast<const floatx4*>(tail + (size_t)r * tw + (c - ldw));
-  } else {
-    v = *reinterpret_cast<const floatx4*>(ws + (size_t)r * ldw + c);
-    for (int sp = 1; sp < splits; ++sp) v += *reinterpret_cast<const floatx4*>(ws + sp * slab + (size_t)r * ldw + c);
-  }
+  const floatx4* w = reinterpret_cast<const floatx4*>(ws + (size_t)r * ldw + c);
+  floatx4 v = w[0];
+  for (int sp = 1; sp < splits; ++sp) v += *reinterpret_cast<const floatx4*>(ws + sp * slab + (size_t)r * ldw + c);
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     if (c + q < ncols) out[(size_t)r * ldo + c + q] = v[q];
@@ -338,18 +331,11 @@ hipError_t transpose_bf16(const uint16_t* in, uint16_t* out, int rows, int cols,
 }
 
 hipError_t slab_sum_cols(const float* ws, int splits, int rows, int ldw, float* out, int ldo, int ncols, float* extra,
-                         hipStream_t s, const float* tail, int tw) {
+                         hipStream_t s) {
   if (rows <= 0 || ncols <= 0) return hipSuccess;
-  const int span = ((ncols + 4) / 4) * 4;   // columns the float4 groups touch
-  if (ldw % 4) return hipErrorInvalidValue;
-  if (tail != nullptr) {
-    if (tw % 4 || span - ldw > tw || ldw > ncols) return hipErrorInvalidValue;
-  } else if (ncols + (extra ? 1 : 0) > ldw || span > ldw) {
-    return hipErrorInvalidValue;
-  }
+  if (ldw % 4 || ncols + (extra ? 1 : 0) > ldw || ((ncols + 4) / 4) * 4 > ldw) return hipErrorInvalidValue;
   const int64_t n = (int64_t)rows * ((ncols + 4) / 4);
-  slab_sum_cols_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(ws, splits, rows, ldw, out, ldo, ncols, extra,
-                                                                   tail, tw);
+  slab_sum_cols_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(ws, splits, rows, ldw, out, ldo, ncols, extra);
   return hipGetLastError();
 }
 

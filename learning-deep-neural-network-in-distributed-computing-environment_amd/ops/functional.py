@@ -325,10 +325,6 @@ class _Conv2dNative(torch.autograd.Function):
                     bn.num_batches_tracked.copy_(snap[1])
         else:
             C.conv_fwd(xb, w, y, stride, pad, b, epi)
-        link = getattr(x, "_ldnn_bnb", None)
-        if link is not None:
-            link["readers"] += 1
-        ctx.bnb = link if (link is not None and stride == 1 and link["C"] == cp) else None
         ctx.save_for_backward(xb, y)
         ctx.meta = (stride, pad, flat, weight, bias, relu, Cin, x.dtype)
         return nchw_view(y, K)
@@ -355,29 +351,7 @@ class _Conv2dNative(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0]:
             dxb = torch.empty_like(xb)
-            link = ctx.bnb
-            bflat = link["flat"] if link is not None else None
-            if (link is not None and link["readers"] == 1 and not link["twin_used"]
-                    and id(link["weight"]) in bflat._stale and id(link["bias"]) in bflat._stale):
-                # this conv is the only reader of a BN + ReLU output whose dgamma / dbeta are
-                # unwritten this step: the dgrad epilogue sums that BN's backward statistics,
-                # finalizes its coefficients and assigns dgamma / dbeta (bn_bwd then applies only)
-                Cb = link["C"]
-                bflat.grad_beta(link["weight"])
-                bflat.grad_beta(link["bias"])
-                done = C.conv_dgrad(g, flat.shadow_storage(weight), dxb, stride, pad, bn_x=link["x2"],
-                                    bn_mask=link["mask"], bn_gamma=link["gamma"], bn_save_mean=link["smean"],
-                                    bn_save_invstd=link["sinv"], bn_ws=link["ws"],
-                                    bn_dgamma=bflat.grad_storage(link["weight"])[:Cb],
-                                    bn_dbeta=bflat.grad_storage(link["bias"])[:Cb], bn_grad_assign=True)
-                if done:
-                    link["dx_ptr"] = dxb.data_ptr()
-                    BN_BWD_FUSED[0] += 1
-                else:   # not on the fused path (shape): the BN backward writes them itself
-                    bflat._stale.add(id(link["weight"]))
-                    bflat._stale.add(id(link["bias"]))
-            else:
-                C.conv_dgrad(g, flat.shadow_storage(weight), dxb, stride, pad)
+            C.conv_dgrad(g, flat.shadow_storage(weight), dxb, stride, pad)
             dx = _zpad(nchw_view(dxb, Cin))   # (weight pad channels are zero)
             if in_dtype != torch.bfloat16:
                 dx = dx.to(in_dtype)
@@ -426,9 +400,6 @@ def _with_twin(y: torch.Tensor, twin: torch.Tensor) -> torch.Tensor:
 def shortcut_input(x: torch.Tensor) -> torch.Tensor:
     """The tensor a residual block's shortcut branch should read (x's twin if it has one)."""
     t = getattr(x, "_ldnn_twin", None)
-    link = getattr(x, "_ldnn_bnb", None)
-    if link is not None:   # a second consumer: its gradient joins the BN's (no fused statistics)
-        link["twin_used"] = True
     return x if t is None else t
 
 
@@ -467,15 +438,6 @@ class _BatchNormNative(torch.autograd.Function):
                       rv if (training and mod.training) or not training else None, smean, sinv, ws, mod.eps,
                       mom or 0.0, training, relu, nbt, mask=mask)
         ctx.mask = mask
-        # the BN + ReLU output's gradient may arrive with its backward statistics already
-        # summed by the consuming conv's dgrad epilogue (BN_BWD_FUSE; _Conv2dNative.backward)
-        link = None
-        if (BN_BWD_FUSE and relu and mask is not None and residual is None and mod.training and training
-                and weight is not None and bias is not None):
-            link = {"x2": x2, "mask": mask, "smean": smean, "sinv": sinv, "ws": ws, "gamma": gamma, "flat": flat,
-                    "weight": weight, "bias": bias, "C": C, "readers": 0, "twin_used": False, "dx_ptr": None}
-            mod.__dict__["_ldnn_bnb_last"] = link
-        ctx.link = link
         ctx.save_for_backward(x2, y if mask is None else x2.new_empty(0), smean, sinv)
         ctx.meta = (flat, weight, bias, relu, residual is not None, ws, (N, C, H, W), x.dtype)
         ctx.set_materialize_grads(False)
@@ -501,27 +463,17 @@ class _BatchNormNative(torch.autograd.Function):
         gamma = flat.master_storage(weight)[:C] if weight is not None else None
         dg = flat.grad_storage(weight)[:C] if weight is not None else None
         db = flat.grad_storage(bias)[:C] if bias is not None else None
-        link = ctx.link
-        ready = False
-        if link is not None and link["dx_ptr"] is not None:
-            # the consuming conv's dgrad epilogue finalized this BN's backward statistics (and
-            # assigned dgamma / dbeta) -- valid only if gy IS that dgrad output: no second
-            # consumer's gradient was summed in (else redo them from scratch, assigning again)
-            ready = gt is None and g2.data_ptr() == link["dx_ptr"]
-            link["dx_ptr"] = None
-            assign = True
-        else:
-            # first write of the step: the finalize stores dgamma / dbeta instead of adding
-            fresh = [(t, flat.grad_beta(p) == 0.0) for t, p in ((dg, weight), (db, bias)) if p is not None]
-            assign = all(f for _, f in fresh)
-            if not assign:  # mixed (only if a caller accumulated one of them): clear the fresh ones
-                for t, f in fresh:
-                    if f:
-                        t.zero_()
+        # first write of the step: the finalize stores dgamma / dbeta instead of adding
+        fresh = [(t, flat.grad_beta(p) == 0.0) for t, p in ((dg, weight), (db, bias)) if p is not None]
+        assign = all(f for _, f in fresh)
+        if not assign:  # mixed (only if a caller accumulated one of them): clear the fresh ones
+            for t, f in fresh:
+                if f:
+                    t.zero_()
         mask = ctx.mask
         yv = y.view(-1, C) if mask is None else x2   # (y is not read when the mask is given)
         C_.bn_bwd(x2, yv, g2, dx.view(-1, C), dres.view(-1, C) if dres is not None else None, gamma,
-                  smean, sinv, ws, dg, db, relu, mask=mask, grad_assign=assign, dy2=gt, stats_ready=ready)
+                  smean, sinv, ws, dg, db, relu, mask=mask, grad_assign=assign, dy2=gt)
         flat.notify(weight, bias)
         dxv = nchw_view(dx, C)
         dresv = nchw_view(dres, C) if dres is not None else None
@@ -635,11 +587,6 @@ def batch_norm_dual_act(x, mod_a, r, mod_b):
 # BatchNorm + ReLU keeps a bit mask of the output for its backward (measured A/B in
 # profiles/, LDNN_BN_RELU_MASK=0 reads the bf16 output instead)
 BN_RELU_MASK = __import__("os").environ.get("LDNN_BN_RELU_MASK", "1") != "0"
-# The backward statistics of a BN + ReLU whose output only one stride-1 native conv reads are
-# summed in that conv's dgrad epilogue (its BN backward then runs the apply pass alone);
-# LDNN_BN_BWD_FUSE=0 keeps the separate statistics pass (A/B knob)
-BN_BWD_FUSE = __import__("os").environ.get("LDNN_BN_BWD_FUSE", "1") != "0"
-BN_BWD_FUSED = [0]   # how many dgrads took that path (tests)
 
 
 def batch_norm_act(x, mod, residual=None, relu: bool = False):
@@ -647,11 +594,7 @@ def batch_norm_act(x, mod, residual=None, relu: bool = False):
     (fp32 statistics over NHWC bf16); the CPU path is the fp32 reference."""
     flat = getattr(mod, "_ldnn_flat", None)
     if _ext.use_native(x) and flat is not None and x.shape[1] % 8 == 0 and mod.affine:
-        y = _with_twin(*_BatchNormNative.apply(x, mod.weight, mod.bias, residual, mod, flat, relu))
-        link = mod.__dict__.pop("_ldnn_bnb_last", None)
-        if link is not None:
-            y._ldnn_bnb = link
-        return y
+        return _with_twin(*_BatchNormNative.apply(x, mod.weight, mod.bias, residual, mod, flat, relu))
     y = batch_norm2d(x, mod)
     if residual is not None:
         y = y + residual

@@ -101,7 +101,7 @@ class StaticMLPEngine:
                  fuse_head_dgrad: bool | None = None, library_dgrad: bool | None = None, head_dgrad_mode: int = -1,
                  relu_masks: bool = True, transposed_dgrad: bool = True, bias_ones_column: bool = True,
                  fuse_head_fwd: bool = True, fuse_head_bwd: bool = True, grad_mix: tuple | None = None,
-                 wgrad_tail_split: bool | None = None, overlap_optimizer: bool | None = None):
+                 overlap_optimizer: bool | None = None):
         """``grad_mix`` = (hops, local_weight): per-step gradient exchange other than the
         equal all-reduce (world > 1) -- hops 0 with a weight = the reference's
         self-weighted all-reduce (BAR/communication.py:4-10), hops 1 / 2 = ring /
@@ -308,7 +308,6 @@ class StaticMLPEngine:
             if transposed_dgrad and not self._lib_dgrad[l] and not (self.use_head and l == L - 1 and self.head_dgrad):
                 self.Wt[l] = torch.zeros(self.W[l].shape[1], self.W[l].shape[0], dtype=bf, device=dev)
         self._wgrad_splitk, self._wgrad_ws, self._wgrad_slab = [], [], []
-        self._wgrad_tail = None
         for l, layer in enumerate(self.layers):
             M, N = self.dW[l].shape
             self._wgrad_ws.append(None)
@@ -344,27 +343,6 @@ class StaticMLPEngine:
                     self.x = self.xp[:, :N]
                     self.h[0] = self.x
                     self._db0_from_wgrad = True
-                # wgrad_tail_split: a width that is not a multiple of 256 (784 + the ones column)
-                # leaves the last 256-column tile of the four-wave kernel 9 % full; the full tiles
-                # run split-K into slabs, the narrow tail (<= 64 columns) on the 128-tile kernel
-                # with the in-launch combine, and the slab sum takes the tail's columns from its
-                # product (A/B knob LDNN_WGRAD_TAIL_SPLIT; scripts/bench_wgrad0.py)
-                split = (os.environ.get("LDNN_WGRAD_TAIL_SPLIT", "1") != "0" if wgrad_tail_split is None
-                         else bool(wgrad_tail_split))
-                main = Nw // 256 * 256
-                if split and l == 0 and self._db0_from_wgrad and main > 0 and 0 < Nw - main <= 64:
-                    t256m = ((M + 255) // 256) * (main // 256)
-                    skm = max(2, min(8, round(256 / t256m)))
-                    tw = (Nw - main + 7) // 8 * 8
-                    skt = 16
-                    ne, nc = self.C.gemm_splitk_ws(M, tw, skt)
-                    self._wgrad_tail = dict(main=main, tw=tw, sk=skt,
-                                            out=torch.empty(M, tw, dtype=torch.float32, device=self.device),
-                                            ws=torch.empty(ne, dtype=torch.float32, device=self.device),
-                                            cnt=torch.zeros(nc, dtype=torch.int32, device=self.device))
-                    self._wgrad_slab[l] = torch.empty(skm, M, main, dtype=torch.float32, device=self.device)
-                    self._wgrad_splitk.append(skm)
-                    continue
                 self._wgrad_slab[l] = torch.empty(sk, M, Nw, dtype=torch.float32, device=self.device)
                 self._wgrad_splitk.append(sk)
                 continue
@@ -473,14 +451,6 @@ class StaticMLPEngine:
             return
         if self._wgrad_slab[l] is not None:   # split-K into slabs + one summing pass, overwrites
             if l == 0 and self._db0_from_wgrad:   # + the ones column: dW_0 and the bias gradient
-                t = self._wgrad_tail
-                if t is not None:   # full column tiles split-K into slabs + the narrow tail on its own
-                    mn = t["main"]
-                    self.C.gemm(self.dz[1], self.xp[:, :mn], self._wgrad_slab[0], False, False, tile=256, splitk=sk)
-                    self.C.gemm(self.dz[1], self.xp[:, mn:mn + t["tw"]], t["out"], False, False, tile=128,
-                                splitk=t["sk"], ws=t["ws"], cnt=t["cnt"])
-                    self.C.slab_sum_cols(self._wgrad_slab[0], self.dW[0], self.db[0], tail=t["out"])
-                    return
                 self.C.gemm(self.dz[1], self.xp, self._wgrad_slab[0], False, False, tile=256, splitk=sk)
                 self.C.slab_sum_cols(self._wgrad_slab[0], self.dW[0], self.db[0])
                 return
@@ -1068,10 +1038,7 @@ class StaticMLPEngine:
                 d[f"wgrad{l}"] = "hipBLASLt"
             elif self._wgrad_slab[l] is not None:
                 d[f"wgrad{l}"] = (f"ldnn gemm_q split-K x{self._wgrad_splitk[l]} slabs + slab_sum"
-                                  + (" (+ bias grad from a ones column)" if l == 0 and self._db0_from_wgrad else "")
-                                  + (f"; the {self._wgrad_tail['tw']}-column tail on the 128-tile kernel "
-                                     f"(split-K x{self._wgrad_tail['sk']}, in-launch combine)"
-                                     if l == 0 and self._wgrad_tail is not None else ""))
+                                  + (" (+ bias grad from a ones column)" if l == 0 and self._db0_from_wgrad else ""))
             else:
                 d[f"wgrad{l}"] = ("ldnn gemm (auto: gemm_q four-wave 256x256 where gemm_q_preferred, else k256)"
                                   + (f" split-K x{self._wgrad_splitk[l]}" if self._wgrad_splitk[l] > 1 else ""))

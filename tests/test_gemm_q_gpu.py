@@ -249,7 +249,8 @@ def test_gemm_opt_epilogue_equals_gemm_then_optimizer(kind, M, N, K):
     wd = 1e-2
     # reference: gradient GEMM, then the flat optimizer kernel
     g = torch.empty(M, N, device="cuda")
-    C.gemm(dz, h, g, False, False)
+    # (the tiling gemm_opt takes, unsplit: the same fp32 accumulation order)
+    C.gemm(dz, h, g, False, False, tile=256 if M * N >= 192 * 65536 else 128, splitk=1)
     torch.testing.assert_close(g, dz.float().t() @ h.float(), rtol=2e-3, atol=2e-3)
     mr, m1, v1 = master0.clone(), torch.randn(M, N, device="cuda") * 1e-3, torch.rand(M, N, device="cuda") * 1e-5
     sr = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
