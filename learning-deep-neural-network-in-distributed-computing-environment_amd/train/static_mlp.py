@@ -29,7 +29,6 @@ from __future__ import annotations
 
 import contextlib
 import gc
-import os
 from dataclasses import dataclass
 
 import torch
@@ -100,8 +99,7 @@ class StaticMLPEngine:
                  shard_optimizer: bool | None = None, wgrad_combine: bool = True, library_gemms: bool | None = None,
                  fuse_head_dgrad: bool | None = None, library_dgrad: bool | None = None, head_dgrad_mode: int = -1,
                  relu_masks: bool = True, transposed_dgrad: bool = True, bias_ones_column: bool = True,
-                 fuse_head_fwd: bool = True, fuse_head_bwd: bool = True, grad_mix: tuple | None = None,
-                 overlap_optimizer: bool | None = None):
+                 fuse_head_fwd: bool = True, fuse_head_bwd: bool = True, grad_mix: tuple | None = None):
         """``grad_mix`` = (hops, local_weight): per-step gradient exchange other than the
         equal all-reduce (world > 1) -- hops 0 with a weight = the reference's
         self-weighted all-reduce (BAR/communication.py:4-10), hops 1 / 2 = ring /
@@ -393,17 +391,6 @@ class StaticMLPEngine:
         self._fuse_head_bwd = bool(fuse_head_bwd and self._head_part is not None and L >= 2
                                    and self._dgrad_epi[L - 1] in (self.C.EPI_NONE, self.C.EPI_DRELU)
                                    and self.layers[L - 1].in_features % 64 == 0 and self._wgrad_splitk[L - 1] > 1)
-        # overlap_optimizer (single-process engines): the fused update of every weight but the
-        # first layer's runs on a side HIP stream beside the first layer's wgrad GEMM (the
-        # memory-bound pass hides under the compute-bound one); the step joins before it
-        # returns.  (None: on unless LDNN_MLP_OPT_OVERLAP=0, an A/B knob)
-        if overlap_optimizer is None:
-            overlap_optimizer = os.environ.get("LDNN_MLP_OPT_OVERLAP", "1") != "0"
-        self._opt_overlap = bool(overlap_optimizer) and not self.distributed and self.device.type == "cuda"
-        if self._opt_overlap:
-            self._side = torch.cuda.Stream(device=self.device)
-            self._ev_bwd = torch.cuda.Event()
-            self._ev_opt = torch.cuda.Event()
         self._build_segments()
         self._slots[0]["segs"] = (self.segments, self.opt_segments)
 
@@ -536,48 +523,15 @@ class StaticMLPEngine:
             return f
 
         if not self.distributed:
-            fns = [fn for p in pieces for fn in p]
-            cut = next((i for i, fn in enumerate(fns) if getattr(fn, "_ldnn_wgrad", None) == 0), None)
-            if self._opt_overlap and cut is not None and L >= 2:
-                # G_1 = everything up to the first layer's wgrad; then the update of every weight
-                # but the first layer's (a memory-bound pass) on a side stream BESIDE G_2 = the
-                # first layer's wgrad (compute-bound) + its own update; the step ends joined
-                a, b = self._first_layer_ranges()
-                self._rest_ranges = self._complement(a, b)
-                self.segments = [_Segment(run(fns[:cut]), self.use_graphs),
-                                 _Segment(run(fns[cut:] + [lambda: self._opt(a[0], a[1]),
-                                                           lambda: self._opt(b[0], b[1])]), self.use_graphs)]
-                self.opt_segments = [_Segment(run([lambda r=r: self._opt(*r) for r in self._rest_ranges]),
-                                              self.use_graphs)]
-            else:
-                self.segments = [_Segment(run(fns + [lambda: self._opt(0, self.flat.numel)]), self.use_graphs)]
-                self.opt_segments = []
+            fns = [fn for p in pieces for fn in p] + [lambda: self._opt(0, self.flat.numel)]
+            self.segments = [_Segment(run(fns), self.use_graphs)]
+            self.opt_segments = []
         elif self.shard:
             self._build_sharded_segments(pieces, run)
         else:
             self.segments = [_Segment(run(p), self.use_graphs) for p in pieces]
             self.opt_segments = [_Segment(run([lambda b=b, e=e: self._opt(b, e)]), self.use_graphs)
                                  for (b, e, _) in self.buckets]
-
-    def _first_layer_ranges(self):
-        """Flat ranges of the first layer's weight and bias storage."""
-        f = self.flat
-        out = []
-        for p in (self.layers[0].weight, self.layers[0].bias):
-            sg = f.seg(p)
-            out.append((sg.offset, sg.offset + sg.storage_numel))
-        return out
-
-    def _complement(self, *ranges):
-        """[0, numel) minus ``ranges`` (sorted, disjoint)."""
-        out, pos = [], 0
-        for b, e in sorted(ranges):
-            if b > pos:
-                out.append((pos, b))
-            pos = max(pos, e)
-        if pos < self.flat.numel:
-            out.append((pos, self.flat.numel))
-        return out
 
     def _bucket_of(self, t) -> int:
         off = self.flat.seg(t).offset
@@ -980,17 +934,6 @@ class StaticMLPEngine:
             self._use_slot(slot)
         self._master_whole = False
         if not self.distributed:
-            if self.opt_segments:   # the update of the later layers overlaps the first layer's wgrad
-                main = torch.cuda.current_stream()
-                self.segments[0]()
-                self._ev_bwd.record(main)
-                with torch.cuda.stream(self._side):
-                    self._side.wait_event(self._ev_bwd)
-                    self.opt_segments[0]()
-                    self._ev_opt.record(self._side)
-                self.segments[1]()
-                main.wait_event(self._ev_opt)
-                return
             self.segments[0]()
             return
         if self.shard:
@@ -1046,9 +989,7 @@ class StaticMLPEngine:
                 d[f"dgrad{l}"] = ("hipBLASLt + act_bwd_colsum" if self._lib_dgrad[l] else
                                   "ldnn gemm_q" + (" on transposed W" if self.Wt[l] is not None else "")
                                   + (" (dReLU from bit mask)" if self.mask[l] is not None else " (fused derivative)"))
-        d["optimizer"] = (f"ldnn fused {self.optim.name} (flat fp32 master + bf16 shadow)"
-                          + ("; every layer but the first updated on a side stream beside the first layer's wgrad"
-                             if self.opt_segments and not self.distributed else ""))
+        d["optimizer"] = f"ldnn fused {self.optim.name} (flat fp32 master + bf16 shadow)"
         d["library_gemms"] = sum(v.startswith("hipBLASLt") for v in d.values())
         return d
 
