@@ -226,25 +226,11 @@ def run_cnn(ctx, name: str, batch: int, steps: int, optimizer: str = "sgd", warm
     crit = CrossEntropyLoss()
     comm = default_comm(ONESHOT_DEFAULT_BYTES) if ctx.world_size > 1 else None
 
-    # N = 1: the per-bucket updates on a side stream beside the rest of the backward
-    # (GraphedDPStep side_optimizer over a world-1 DataParallel; LDNN_CNN_SIDE_OPT=0: one graph)
-    side = ctx.world_size == 1 and os.environ.get("LDNN_CNN_SIDE_OPT", "1") != "0"
-
     def make(dp_on: bool):
         torch.manual_seed(0)
         m = build_model(name)
         xinit(m)
         ldnn.prepare(m, ctx.device)
-        if side:
-            from ldnn.parallel.comm import LocalComm
-
-            dp = DataParallel(m, LocalComm(), bucket_cap_mb=32.0, broadcast_init=False)
-            opt = SGD(m.parameters(), lr=0.01, momentum=0.9) if optimizer == "sgd" else Adam(m.parameters(), lr=1e-3)
-            opt.zero_grad()
-            crit(dp(xs[0]), ys[0]).backward()
-            dp.finish_gradient_sync()
-            opt.step()
-            return GraphedDPStep(dp, crit, opt, xs[0], ys[0], side_optimizer=True), m
         dp = DataParallel(m, comm, bucket_cap_mb=32.0, shard_optimizer=True) if dp_on else None
         # (the optimizer after the wrapper: sharding re-lays the flat buffers out)
         opt = SGD(m.parameters(), lr=0.01, momentum=0.9) if optimizer == "sgd" else Adam(m.parameters(), lr=1e-3)
@@ -266,9 +252,6 @@ def run_cnn(ctx, name: str, batch: int, steps: int, optimizer: str = "sgd", warm
            "optimizer": "sgd momentum 0.9 lr 0.01" if optimizer == "sgd" else "adam lr 1e-3",
            "ms_per_step": round(ms, 4), "samples_per_s": round(batch * ctx.world_size / el * steps, 1),
            "n_params": sum(p.numel() for p in m.parameters())}
-    if side:
-        rec["optimizer_overlap"] = (f"per-bucket fused {optimizer} graphs ({len(gs.bk.buckets)} buckets) on a side "
-                                    "stream beside the rest of the backward")
     if ctx.world_size > 1:
         bk = gs.bk
         rec["grad_sync"] = ("fp32 reduce-scatter per bucket (between backward graph links) + sharded "

@@ -170,8 +170,7 @@ class GraphedDPStep:
     """
 
     def __init__(self, dp, criterion, optimizer, x_example: torch.Tensor, y_example: torch.Tensor,
-                 stats: torch.Tensor | None = None, mode: str | None = None, comm_fn=None,
-                 side_optimizer: bool = False):
+                 stats: torch.Tensor | None = None, mode: str | None = None, comm_fn=None):
         from ..parallel.comm import SUM
 
         if not x_example.is_cuda:
@@ -185,18 +184,6 @@ class GraphedDPStep:
         self.stats = stats if stats is not None else torch.zeros(2, dtype=torch.float32, device=self.x.device)
         self._lrs = None
         self.device_collectives = bool(getattr(self.comm, "device_collectives", False))
-        # side_optimizer (one process, world-1 DataParallel): each bucket's fused update is its
-        # own graph, replayed on a side HIP stream once the backward is past the bucket's last
-        # reader -- the link after the one that completed its gradients (a layer's dgrad, which
-        # reads its weights, directly follows its wgrad) -- so the memory-bound update runs
-        # beside the rest of the (latency-bound) backward; the step joins before returning
-        self.side_opt = bool(side_optimizer)
-        if self.side_opt:
-            if self.bk.shard or getattr(self.comm, "world_size", 1) != 1 or not isinstance(optimizer, _FlatOptimizer):
-                raise ValueError("side_optimizer needs a single-process (world 1), non-sharded DataParallel and an "
-                                 "ldnn optimizer")
-            mode = "segmented"
-            self._side = torch.cuda.Stream(device=self.x.device)
         if mode is None:
             mode = "segmented" if (self.device_collectives or comm_fn is not None) else "after"
         if mode not in ("segmented", "after"):
@@ -302,8 +289,6 @@ class GraphedDPStep:
         of after all of them.  (self.g_opts: [(graph, bucket or None)])"""
         self.g_opts = []
         order = self.bk.opt_order() if (self.bk.shard and isinstance(self.optimizer, _FlatOptimizer)) else None
-        if self.side_opt:   # bucket order: the order their gradients complete in
-            order = list(range(len(self.bk.buckets)))
 
         def begin(i):
             g = torch.cuda.CUDAGraph()
@@ -330,15 +315,10 @@ class GraphedDPStep:
 
         begin(None)   # (the optimizer's per-step prologue, e.g. Adam's step count, lands in the first)
         self.bk.step_parts = parts
-        if self.side_opt:   # (the per-range optimizer path: _FlatOptimizer._sharded_step)
-            self.flat.shard_sync = self.bk
         try:
             self.optimizer.step()
         finally:
             self.bk.step_parts = None
-            if self.side_opt:
-                self.flat.shard_sync = None
-                self.bk.master_whole = True
         self.g_opts[-1][0].capture_end()
 
     def _fire(self, idx):
@@ -404,8 +384,6 @@ class GraphedDPStep:
         self.x.copy_(x, non_blocking=True)
         self.y.copy_(y, non_blocking=True)
         self._sync_lr()
-        if self.side_opt:
-            return self._replay_side()
         works = []
         for j, g in enumerate(self.graphs):
             if self.waits[j]:
@@ -431,34 +409,6 @@ class GraphedDPStep:
                 self.bk.issue_gather(i)
         if self.bk.shard:
             self.bk.master_whole = False
-        return self.loss
-
-    def _replay_side(self):
-        """side_optimizer replay: link j on the compute stream; the update graphs of the buckets
-        completed by link j-1 on the side stream after link j (their weights' last reader)."""
-        main = torch.cuda.current_stream()
-        opt_of = {i: g for g, i in self.g_opts}
-        if not hasattr(self, "_evs"):
-            self._evs = [torch.cuda.Event() for _ in self.graphs]
-        pending: list = []
-
-        def launch(buckets, ev):
-            if not buckets:
-                return
-            self._side.wait_event(ev)
-            with torch.cuda.stream(self._side):
-                for i in buckets:
-                    opt_of[i].replay()
-
-        for j, g in enumerate(self.graphs):
-            if not self._empty[j]:
-                g.replay()
-            self._evs[j].record(main)
-            launch(pending, self._evs[j])
-            pending = list(self.issue[j])
-        launch(pending, self._evs[-1])
-        # (the first update graph holds the optimizer's per-step prologue: bucket 0 goes first)
-        main.wait_stream(self._side)
         return self.loss
 
     def _eager_step(self, x, y):

@@ -63,22 +63,7 @@ def main():
         crit(m(xb), y).backward()
         opt.step()
 
-    if a.graph and os.environ.get("LDNN_CNN_SIDE_OPT", "1") != "0":
-        # per-bucket updates on a side stream beside the rest of the backward (bench.py's N = 1 path)
-        from ldnn.parallel.comm import LocalComm
-        from ldnn.parallel.ddp import DataParallel
-        from ldnn.train.graphed import GraphedDPStep
-
-        dp = DataParallel(m, LocalComm(), bucket_cap_mb=32.0, broadcast_init=False)
-        opt.zero_grad()
-        crit(dp(xb), y).backward()
-        dp.finish_gradient_sync()
-        opt.step()
-        gs = GraphedDPStep(dp, crit, opt, xb, y, side_optimizer=True)
-
-        def step_ldnn():  # noqa: F811
-            gs(xb, y)
-    elif a.graph:
+    if a.graph:
         from ldnn.train.graphed import GraphedStep
 
         gs = GraphedStep(m, crit, opt, xb, y)

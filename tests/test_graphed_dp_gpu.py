@@ -204,51 +204,3 @@ def test_eager_fallback_and_replay_record_the_same_schedule():
         digests.append(c.schedule_digest())
     torch.cuda.synchronize()
     assert digests[0] == digests[1] and digests[0][0] == len(dp.bucketer.buckets), digests
-
-
-@pytest.mark.parametrize("name,batch,shape,optname", [("enhanced_cnn", 64, (3, 32, 32), "sgd"),
-                                                       ("enhanced_cnn", 64, (3, 32, 32), "adam"),
-                                                       ("lenet5", 256, (1, 28, 28), "sgd")])
-def test_side_stream_optimizer_matches_single_graph_step(name, batch, shape, optname):
-    """GraphedDPStep(side_optimizer=True) over a world-1 DataParallel -- each bucket's update a
-    graph of its own, replayed on a side stream once the backward is past the bucket's last
-    reader -- trains exactly like the one-graph GraphedStep (same kernels, the update split
-    into per-bucket ranges), loss bookkeeping included."""
-    from ldnn.optim import Adam
-
-    torch.manual_seed(0)
-    g = torch.Generator(device="cuda").manual_seed(3)
-    nc = 10
-    xs = [torch.randn(batch, *shape, device="cuda", generator=g).bfloat16() for _ in range(3)]
-    ys = [torch.randint(0, nc, (batch,), device="cuda", generator=g) for _ in range(3)]
-
-    def make(side):
-        torch.manual_seed(0)
-        m = build_model(name)
-        xavier_init(m)
-        ldnn.prepare(m, "cuda")
-        crit = CrossEntropyLoss()
-        net = DataParallel(m, LocalComm(), bucket_cap_mb=8.0, broadcast_init=False) if side else m
-        opt = SGD(m.parameters(), lr=0.01, momentum=0.9) if optname == "sgd" else Adam(m.parameters(), lr=1e-3)
-        opt.zero_grad()
-        crit(net(xs[0]), ys[0]).backward()
-        if side:
-            net.finish_gradient_sync()
-        opt.step()
-        if side:
-            gs = GraphedDPStep(net, crit, opt, xs[0], ys[0], side_optimizer=True)
-            assert len(gs.g_opts) == len(net.bucketer.buckets) >= 3
-            return gs, m
-        return GraphedStep(m, crit, opt, xs[0], ys[0], warmup=0), m
-
-    (g1, m1), (g2, m2) = make(True), make(False)
-    l1, l2 = [], []
-    for i in range(6):
-        l1.append(g1(xs[i % 3], ys[i % 3]).item())
-        l2.append(g2(xs[i % 3], ys[i % 3]).item())
-    torch.cuda.synchronize()
-    for a, b in zip(l1, l2):
-        assert abs(a - b) < 2e-3 * max(1.0, abs(b)), (l1, l2)
-    f1, f2 = m1._ldnn_flat, m2._ldnn_flat
-    err = ((f1.master - f2.master).norm() / f2.master.norm()).item()
-    assert err < 1e-4, err
