@@ -1548,6 +1548,10 @@ PYBIND11_MODULE(_C, m) {
         "halo-staged 3x3 stride-1 conv: 0 off, 1 default (dgrad + 256x64 fwd tiles), 2 every eligible shape",
         py::arg("mode"));
   m.def("get_conv_halo", &ldnn::get_conv_halo);
+  m.def("set_conv_ws", &ldnn::set_conv_ws,
+        "weight-stationary 64 -> 64 channel 3x3 stride-1 conv (fwd without bias, dgrad): 0 off, 1 on (default)",
+        py::arg("mode"));
+  m.def("get_conv_ws", &ldnn::get_conv_ws);
   m.def("set_conv_trace", [](const c10::optional<at::Tensor>& buf) {
         if (!buf.has_value()) {
           ldnn::set_conv_trace(nullptr);

@@ -888,7 +888,8 @@ constexpr int kHaloExtra = 120;  // 2W + 2 rows of halo, rounded up to 8, at mos
 // K-tile from 32 to ~19 KiB, yet ran slower than the gather kernel on every ResNet-18 /
 // EnhancedCNN shape, e.g. C256 H14 b256 fwd 75 -> 106 us, dgrad 101 -> 112 us;
 // profiles/r3/conv_fill_knockout_r3.txt.)
-template <int WM, int WN, class OB, int EPI, bool DGRAD>
+// XF bit5: the phase trace of conv_lds_kernel (entry / first K-tile landed / loop end / exit)
+template <int WM, int WN, class OB, int EPI, bool DGRAD, int XF = 0>
 __global__ __launch_bounds__(256, 2) void conv_halo_kernel(LArgs a, const bf16_t* pa, uint32_t bytes_a,
                                                            const bf16_t* pb, uint32_t bytes_b) {
   constexpr int NW = WM * WN, BM = WM * 64, BN = WN * 64;
@@ -908,6 +909,13 @@ __global__ __launch_bounds__(256, 2) void conv_halo_kernel(LArgs a, const bf16_t
 
   const Geo g = make_geo(a, DGRAD);
   const int tiles_m = (g.M + BM - 1) / BM, tiles_n = (a.N + BN - 1) / BN;
+  uint64_t* trace = nullptr;
+  if constexpr ((XF & 32) != 0) {
+    if (threadIdx.x == 0 && a.trace != nullptr) {
+      trace = a.trace + 4 * (size_t)(blockIdx.x + gridDim.x * blockIdx.y);
+      trace[0] = __builtin_amdgcn_s_memrealtime();
+    }
+  }
   if ((int)blockIdx.x >= tiles_m * tiles_n) return;
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -984,6 +992,9 @@ __global__ __launch_bounds__(256, 2) void conv_halo_kernel(LArgs a, const bf16_t
         wait_vm<0>();
       }
       lds_barrier();  // publishes them; every wave is done with B(kt-1)'s stage
+      if constexpr ((XF & 32) != 0) {
+        if (kt == 0 && trace != nullptr) trace[1] = __builtin_amdgcn_s_memrealtime();
+      }
       if (kt + NSB - 1 < nk) {  // B(kt+NSB-1) into the stage B(kt-1) used
         ks_next(a, g, ks);
         ob.advance(a);
@@ -1022,7 +1033,293 @@ __global__ __launch_bounds__(256, 2) void conv_halo_kernel(LArgs a, const bf16_t
       ks_next(a, g, kc);
     }
   }
+  if constexpr ((XF & 32) != 0) {
+    if (trace != nullptr) trace[2] = __builtin_amdgcn_s_memrealtime();
+  }
   conv_tail<WM, WN, EPI, false, DGRAD>(a, g, acc, m0, n0, wm, wn, lane, smem, LDS / 4, blockIdx.x, blockIdx.y);
+  if constexpr ((XF & 32) != 0) {
+    if (trace != nullptr) trace[3] = __builtin_amdgcn_s_memrealtime();
+  }
+}
+
+// ---- weight-stationary persistent halo conv: 64 -> 64 channels, 3x3 stride 1 pad 1 ----
+// conv_halo_kernel above streams the 8-KiB weight tile of every filter tap through a 2-stage
+// LDS ring, and each tap waits for a DMA issued one tap earlier: at ResNet-18 layer 1 (C64 H56
+// b256) its K loop takes 10.3 us for 9 taps -- 1.14 us per tap, the LDS-DMA issue -> landed
+// latency (~1.1 us, MI355X_MICROARCH.md ldsdma-fill), against ~0.2 us of MFMA work
+// (profiles/r4/conv_phase_trace_rn256.jsonl).  Here the whole 64 x 576 weight matrix lives in
+// REGISTERS: a persistent grid (one 4-wave workgroup per CU, 512 registers per lane) stages it
+// through LDS once, each wave keeps the B fragments of its 32 output channels for all 9 taps
+// (144 VGPRs), and the loop over the workgroup's contiguous run of BM-row tiles only moves
+// activations: one halo image per tile (BM + 128 rows of 64 channels, DMA'd into a double buffer
+// one tile ahead), 9 taps x 2 x 2 x RT MFMAs per wave per tile with no wait inside the tile (the
+// A fragments of step s+1 are read while step s multiplies).  Waves: 2 row strips of RT x 16
+// rows x 2 column halves.  fwd: rows = output pixels, B[n][c] = w[n][r][s][c], tap shift (r-1,
+// s-1); dgrad: rows = input pixels, B[c][k] = w[k][r][s][c], shift (1-r, 1-s).  Same MFMA order
+// per accumulator as conv_halo_kernel (taps r-major, then kk), so the two agree bit for bit.  The
+// fwd epilogue accumulates the next BatchNorm's statistics per lane over all of the workgroup's
+// tiles and adds them once per workgroup.
+__device__ __forceinline__ uint32_t lds_off(const void* p) { return (uint32_t)(uintptr_t)(lds_void*)p; }
+namespace ws64 {
+constexpr int kPitch = 1152 + 16;      // LDS row pitch of the staged weights (16-B aligned, rows spread over banks)
+constexpr int kHPitch = 160;           // LDS row pitch of the halo: 8 chunks + 2 pad slots -- no swizzle, so a
+                                       // tap shift is a plain address offset, and no bank conflict for any row
+                                       // offset (144 B: 2-way, 4.1 extra LDS cycles per read measured)
+constexpr int kSlots = kHPitch / 16;
+constexpr int kWBytes = 64 * kPitch;   // 74,752 B
+}  // namespace ws64
+
+// XF (LDNN_CONV_XF experiment builds): bit0 no halo DMA after the first two tiles, bit1 no
+// epilogue stores, bit2 no A fragment reads, bit3 no waits on the fragment reads (results wrong
+// by construction), bit5 phase trace.
+template <int RT, bool DGRAD, int XF = 0>
+__global__ __launch_bounds__(256, 1) void conv_ws64_kernel(LArgs a, const bf16_t* pa, uint32_t bytes_a,
+                                                           const bf16_t* pw) {
+  constexpr int NW = 4, NT = 256, BM = 2 * RT * 16;
+  constexpr int HROWS = BM + 128;         // halo rows DMA'd per tile (>= BM + 2W + 2 for W <= 63)
+  constexpr int HB = HROWS * ws64::kHPitch; // one halo buffer: rows of 8 16-B chunks + pad slots
+  constexpr int PPW = HB / 1024 / NW;     // 1-KiB DMA pieces per wave per tile
+  static_assert(PPW * NW * 1024 == HB && PPW < 64, "halo pieces");
+  constexpr int REGION = 2 * HB + ws64::kWBytes;  // halo double buffer, then the staged weights
+  constexpr int LDS = REGION + 128;
+  static_assert(LDS <= 160 * 1024 && RT == 4, "LDS / tile rows (RT 8 spills, see launch_ws64)");
+  __shared__ __attribute__((aligned(1024))) char smem[LDS];
+  char* const wst = smem + 2 * HB;        // weight image (prologue only)
+  char* const zrow = smem + REGION;       // 128 zero bytes: the A fragment of a tap outside the image
+
+  uint64_t* trace = nullptr;
+  if constexpr ((XF & 32) != 0) {
+    if (threadIdx.x == 0 && a.trace != nullptr) {
+      trace = a.trace + 4 * (size_t)blockIdx.x;
+      trace[0] = __builtin_amdgcn_s_memrealtime();
+    }
+  }
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  const Geo g = make_geo(a, DGRAD);
+  const int W = g.rows_w, P = g.rows_h;
+  const int T = (g.M + BM - 1) / BM;
+  const int t0 = (int)((int64_t)blockIdx.x * T / gridDim.x);
+  const int t1 = (int)((int64_t)(blockIdx.x + 1) * T / gridDim.x);
+
+  Rsrc ra;
+  ra.r = __builtin_amdgcn_make_buffer_rsrc((void*)pa, (short)0, (int)bytes_a, 0x00020000);
+  // the halo of tile t into buffer b, lane-linear 16-B slots of kHPitch-B rows (slots 8.. of a
+  // row are padding: zero reads); rows outside the tensor read as zeros
+  auto dma = [&](int t, int b) {
+    const int hbase = t * BM - (W + 1);
+    char* const dst = smem + b * HB;
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const int pc = i * NW + wid;
+      const int slot = pc * 64 + lane;
+      const int j = slot / ws64::kSlots, c = slot - j * ws64::kSlots;
+      const int gp = hbase + j;
+      const int o = gp >= 0 && c < 8 ? (int)(((unsigned)gp * 64u + (unsigned)c * 8u) * 2u) : (int)kOOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra.r, (lds_void*)(dst + pc * 1024), 16, o, 0, 0, 0);
+    }
+  };
+
+  float bs0[2][4], bs1[2][4];  // fwd: the next BN's per-channel sums over this workgroup's rows
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bs0[j][r] = bs1[j][r] = 0.f;
+
+  // the first two tiles' halos DMA while the weights are staged (separate LDS regions)
+  if (t0 < t1) {
+    dma(t0, 0);
+    if (t0 + 1 < t1) dma(t0 + 1, 1);
+  }
+  // weights -> LDS ([64][1152 B] at pitch kPitch) -> this wave's B fragments
+  {
+    constexpr int NQ = 64 * 72 / NT;  // 16-B pieces per thread, all loads in flight together
+    static_assert(NQ * NT == 64 * 72, "weight pieces");
+    uint4 wv[NQ];
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) {
+      const int q = threadIdx.x + k * NT, n = q / 72, c16 = q - n * 72;
+      wv[k] = *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(pw) + (size_t)n * 1152 + c16 * 16);
+    }
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) {
+      const int q = threadIdx.x + k * NT, n = q / 72, c16 = q - n * 72;
+      *reinterpret_cast<uint4*>(wst + n * ws64::kPitch + c16 * 16) = wv[k];
+    }
+  }
+  if (threadIdx.x < 8) *reinterpret_cast<floatx4*>(zrow + threadIdx.x * 16) = floatx4{0.f, 0.f, 0.f, 0.f};
+  __syncthreads();
+  bf16x8 fb[9][2][2];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int n = wn * 32 + j * 16 + (lane & 15), k0 = kk * 32 + (lane >> 4) * 8;
+        if constexpr (!DGRAD) {
+          fb[t][kk][j] = *reinterpret_cast<const bf16x8*>(wst + n * ws64::kPitch + t * 128 + k0 * 2);
+        } else {
+          u16x8 v;
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            v[e] = *reinterpret_cast<const uint16_t*>(wst + (k0 + e) * ws64::kPitch + t * 128 + n * 2);
+          fb[t][kk][j] = __builtin_bit_cast(bf16x8, v);
+        }
+      }
+
+  if (t0 < t1) {
+    if (t0 + 1 < t1) wait_vm<PPW>();  // tile t0's pieces landed (loads retire in order)
+    else wait_vm<0>();
+  }
+  if constexpr ((XF & 32) != 0) {
+    if (trace != nullptr) trace[1] = __builtin_amdgcn_s_memrealtime();
+  }
+  bf16_t* const out = reinterpret_cast<bf16_t*>(a.out);
+  for (int t = t0; t < t1; ++t) {
+    const uint32_t halo = lds_off(smem + ((t - t0) & 1) * HB + (lane >> 4) * 16);
+    const uint32_t zr = lds_off(zrow + (lane >> 4) * 16);
+    // per (row tile, tap): this lane's A row address (the zero row for a tap outside the image);
+    // a step's fragment is then one ds_read_b128 at that address + kk * 64, no address math
+    uint32_t ab[RT][9];
+#pragma unroll
+    for (int i = 0; i < RT; ++i) {
+      const int r = wm * RT * 16 + i * 16 + (lane & 15);
+      const int m = t * BM + r;
+      const int tq = fdiv(m, g.f_rw), q = m - tq * W, n = fdiv(tq, g.f_rh), p = tq - n * P;
+      const int edge = (p == 0 ? 1 : 0) | (p == P - 1 ? 2 : 0) | (q == 0 ? 4 : 0) | (q == W - 1 ? 8 : 0) | (m >= g.M ? 16 : 0);
+      const uint32_t rowp = halo + (r + W + 1) * ws64::kHPitch;
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int dr = DGRAD ? 1 - tap / 3 : tap / 3 - 1, ds = DGRAD ? 1 - tap % 3 : tap % 3 - 1;
+        const int emask = 16 | (dr < 0 ? 1 : 0) | (dr > 0 ? 2 : 0) | (ds < 0 ? 4 : 0) | (ds > 0 ? 8 : 0);
+        ab[i][tap] = (edge & emask) != 0 ? zr : rowp + (dr * W + ds) * ws64::kHPitch;
+      }
+    }
+    // the fragment reads are asm (the compiler would otherwise sink each read next to its MFMAs
+    // and wait on it there); their waits are the counted lgkmcnt below, tied to the registers
+    auto read_step = [&](int st, bf16x8 (&f)[RT]) {
+#pragma unroll
+      for (int i = 0; i < RT; ++i) {
+        if constexpr ((XF & 4) != 0) {
+          f[i] = fb[st >> 1][st & 1][i & 1];  // knockout: no A fragment reads
+        } else if ((st & 1) == 0) {
+          asm volatile("ds_read_b128 %0, %1" : "=v"(f[i]) : "v"(ab[i][st >> 1]));
+        } else {
+          asm volatile("ds_read_b128 %0, %1 offset:64" : "=v"(f[i]) : "v"(ab[i][st >> 1]));
+        }
+      }
+    };
+    floatx4 acc[2][RT];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int i = 0; i < RT; ++i) acc[j][i] = floatx4{0.f, 0.f, 0.f, 0.f};
+    lds_barrier();  // every wave waited for its own pieces of tile t: the whole halo is visible
+    __builtin_amdgcn_s_setprio(1);
+    // step st = tap * 2 + kk: its RT fragment reads are issued two steps ahead
+    static_assert(RT == 4, "the counted waits below name 4 fragments");
+    bf16x8 fa[3][RT];
+    read_step(0, fa[0]);
+    read_step(1, fa[1]);
+#pragma unroll
+    for (int st = 0; st < 18; ++st) {
+      bf16x8 (&f)[RT] = fa[st % 3];
+      if (st + 2 < 18) read_step(st + 2, fa[(st + 2) % 3]);
+      if constexpr ((XF & 12) == 0) {  // step st's reads landed; steps st+1, st+2 (<= 2 RT reads) may be in flight
+        if (st + 2 < 18) asm volatile("s_waitcnt lgkmcnt(8)" : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]));
+        else if (st + 1 < 18) asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]));
+        else asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]));
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int i = 0; i < RT; ++i)
+          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[st >> 1][st & 1][j], f[i], acc[j][i], 0, 0, 0);
+    }
+    if constexpr ((XF & 8) != 0) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_setprio(0);
+    lds_barrier();  // every wave is done reading this buffer
+    if (t + 2 < t1 && (XF & 1) == 0) dma(t + 2, (t - t0) & 1);
+    if (t + 1 < t1) {
+      // tile t+1's pieces: issued a whole tile ago, followed only by the stores of tile t-1 and
+      // tile t+2's pieces -- vmcnt(PPW) holds whether or not stores retire in order with loads
+      if (t + 2 < t1 && (XF & 1) == 0) wait_vm<PPW>();
+      else wait_vm<0>();
+    }
+    if constexpr ((XF & 2) != 0) {  // knockout: no epilogue stores (keep the accumulators live)
+      float z = 0.f;
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int i = 0; i < RT; ++i) z += acc[j][i][0] + acc[j][i][1] + acc[j][i][2] + acc[j][i][3];
+      if (z == 12345.f) out[lane] = 0;
+      continue;
+    }
+    // epilogue: bf16 rows (8 B = 4 channels per lane), the BN sums of the rounded values
+#pragma unroll
+    for (int i = 0; i < RT; ++i) {
+      const int m = t * BM + wm * RT * 16 + i * 16 + (lane & 15);
+      if (m >= g.M) continue;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int c = wn * 32 + j * 16 + 4 * (lane >> 4);
+        const floatx4 v = acc[j][i];
+        const u16x4 o = u16x4{f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+        *reinterpret_cast<u16x4*>(out + (size_t)m * 64 + c) = o;
+        if constexpr (!DGRAD) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float b = bf2f(o[r]);
+            bs0[j][r] += b;
+            bs1[j][r] += b * b;
+          }
+        }
+      }
+    }
+  }
+  if constexpr ((XF & 32) != 0) {
+    if (trace != nullptr) trace[2] = __builtin_amdgcn_s_memrealtime();
+  }
+  if constexpr (!DGRAD) {
+    if (a.bn_stats) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int o = 1; o < 16; o <<= 1) {
+            bs0[j][r] += __shfl_xor(bs0[j][r], o, 64);
+            bs1[j][r] += __shfl_xor(bs1[j][r], o, 64);
+          }
+      float* red = reinterpret_cast<float*>(smem);  // [2][64][2]
+      __syncthreads();  // (the last tile's barrier already retired every halo read)
+      if ((lane & 15) == 0) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int c = wn * 32 + j * 16 + 4 * (lane >> 4) + r;
+            red[(wm * 64 + c) * 2] = bs0[j][r];
+            red[(wm * 64 + c) * 2 + 1] = bs1[j][r];
+          }
+      }
+      __syncthreads();
+      float* accc = a.bn.acc + (size_t)(blockIdx.x % kBnCopies) * 2 * 64;
+      if (threadIdx.x < 64) {
+        const float s0 = red[threadIdx.x * 2] + red[(64 + threadIdx.x) * 2];
+        const float s1 = red[threadIdx.x * 2 + 1] + red[(64 + threadIdx.x) * 2 + 1];
+        bn_acc_add(accc + threadIdx.x, s0);
+        bn_acc_add(accc + 64 + threadIdx.x, s1);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's atomics have completed
+      bn_finalize_last<false, kBnCopies>(a.bn, g.M, 64, gridDim.x, red, LDS / 4);
+    }
+  }
+  if constexpr ((XF & 32) != 0) {
+    if (trace != nullptr) trace[3] = __builtin_amdgcn_s_memrealtime();
+  }
 }
 
 // ---- ring wgrad: 3x3 stride-1 pad-1 weight gradient, activation rows staged once ----
@@ -1778,11 +2075,63 @@ bool halo_takes(const ConvShape& s, int wm) {
   return m == 2;
 }
 
+// Weight-stationary path (conv_ws64_kernel) for 64 -> 64 channel 3x3 stride-1 pad-1 fwd
+// (no bias) and dgrad.  LDNN_CONV_WS=0 (A/B knob) turns it off (conv_halo_kernel).
+int g_conv_ws = -2;  // -2: not read yet
+int ws_env() {
+  if (g_conv_ws == -2) g_conv_ws = env_int("LDNN_CONV_WS", 1);
+  return g_conv_ws;
+}
+bool ws64_takes(const ConvShape& s, int epi) {
+  return ws_env() != 0 && epi == EPI_NONE && s.C == 64 && s.K == 64 && s.R == 3 && s.S == 3 && s.stride == 1 &&
+         s.pad == 1 && s.P == s.H && s.Q == s.W && s.W <= 63;
+}
+int cu_count() {
+  static int n[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+  if (n[dev] == 0) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+    n[dev] = v;
+  }
+  return n[dev];
+}
+template <int RT, bool DGRAD>
+hipError_t launch_ws64_m(LArgs a, int grid, const bf16_t* pa, size_t ba, const bf16_t* pw, hipStream_t st) {
+  a.tiles_x = grid;
+  const int xf = conv_xf_env();
+  if (xf == 32) {
+    conv_ws64_kernel<RT, DGRAD, 32><<<grid, 256, 0, st>>>(a, pa, (uint32_t)ba, pw);
+  } else if (xf == 1 || xf == 2 || xf == 4 || xf == 7 || xf == 8 || xf == 10) {  // knockouts (fwd timing only)
+    if constexpr (DGRAD) return hipErrorInvalidValue;
+    else if (xf == 1) conv_ws64_kernel<RT, false, 1><<<grid, 256, 0, st>>>(a, pa, (uint32_t)ba, pw);
+    else if (xf == 2) conv_ws64_kernel<RT, false, 2><<<grid, 256, 0, st>>>(a, pa, (uint32_t)ba, pw);
+    else if (xf == 4) conv_ws64_kernel<RT, false, 4><<<grid, 256, 0, st>>>(a, pa, (uint32_t)ba, pw);
+    else if (xf == 8) conv_ws64_kernel<RT, false, 8><<<grid, 256, 0, st>>>(a, pa, (uint32_t)ba, pw);
+    else if (xf == 10) conv_ws64_kernel<RT, false, 10><<<grid, 256, 0, st>>>(a, pa, (uint32_t)ba, pw);
+    else conv_ws64_kernel<RT, false, 7><<<grid, 256, 0, st>>>(a, pa, (uint32_t)ba, pw);
+  } else
+    conv_ws64_kernel<RT, DGRAD><<<grid, 256, 0, st>>>(a, pa, (uint32_t)ba, pw);
+  return hipGetLastError();
+}
+// 128-row tiles (RT 4).  (256-row tiles, RT 8, need ~290 live registers per lane; hipcc spilled
+// them and the dgrad variant read corrupted B fragments -- removed.)
+template <bool DGRAD>
+hipError_t launch_ws64(const LArgs& a, const bf16_t* pa, size_t ba, const bf16_t* pw, hipStream_t st) {
+  const int64_t tiles = (a.M + 127) / 128;
+  return launch_ws64_m<4, DGRAD>(a, (int)std::min<int64_t>(tiles, cu_count()), pa, ba, pw, st);
+}
+
 template <int WM, int WN, class OB, bool DGRAD>
 hipError_t launch_halo(LArgs a, int epi, int splits, const bf16_t* pa, size_t ba, const bf16_t* pb, size_t bb,
                        hipStream_t st) {
   a.tap_major = 1;  // taps fastest inside a channel block: one halo per block
   dim3 grid(a.tiles_x, splits, 1), block(256);
+  if (conv_xf_env() == 32 && epi == EPI_NONE) {
+    conv_halo_kernel<WM, WN, OB, EPI_NONE, DGRAD, 32><<<grid, block, 0, st>>>(a, pa, (uint32_t)ba, pb, (uint32_t)bb);
+    return hipGetLastError();
+  }
 #define LDNN_CONV_HALO(E) \
   conv_halo_kernel<WM, WN, OB, E, DGRAD><<<grid, block, 0, st>>>(a, pa, (uint32_t)ba, pb, (uint32_t)bb)
   switch (epi) {
@@ -1907,6 +2256,8 @@ ConvWorkspace ws_of(const Plan& p) {
 using namespace convlds;
 
 void set_conv_halo(int mode) { g_conv_halo = mode; }
+void set_conv_ws(int mode) { g_conv_ws = mode; }
+int get_conv_ws() { return ws_env(); }
 void set_conv_trace(uint64_t* buf) { g_conv_trace = buf; }
 void set_conv_wgrad_ring(int mode) { g_wgrad_ring = mode; }
 int get_conv_halo() { return halo_env(); }
@@ -2080,6 +2431,12 @@ hipError_t conv2d_fwd_lds(const ConvShape& s, const uint16_t* x, const uint16_t*
     a.nk_split = pl.nk_all;
   }
   const size_t bx = (size_t)s.N * s.H * s.W * s.C * 2, bw = (size_t)s.K * a.rsc * 2;
+  if (ws64_takes(s, epi)) {  // persistent grid, no split-K: the plan's slab / combine is not used
+    a.ws = nullptr;
+    a.cnt = nullptr;
+    a.nk_split = a.nk_all;
+    return launch_ws64<false>(a, x, bx, w, st);
+  }
   hipError_t e;
   if (halo_takes(s, pl.wm)) {
     // fwd: the halo wins on the 256x64 tiles of 64-filter layers (C64 H56: 53.7 -> 35-37 us) and
@@ -2121,6 +2478,12 @@ hipError_t conv2d_dgrad_lds(const ConvShape& s, const uint16_t* dy, const uint16
     a.nk_split = pl.nk_all;
   }
   const size_t bdy = (size_t)s.N * s.P * s.Q * s.K * 2, bw = (size_t)s.K * a.rsc * 2;
+  if (ws64_takes(s, EPI_NONE)) {
+    a.ws = nullptr;
+    a.cnt = nullptr;
+    a.nk_split = a.nk_all;
+    return launch_ws64<true>(a, dy, bdy, w, st);
+  }
   hipError_t e;
   if (halo_takes(s, pl.wm)) {
     // dgrad likewise: C64 H56 38.9 -> 36.5 us; single-buffered on 128x128 tiles neutral to 1 us

@@ -19,7 +19,8 @@ import ldnn  # noqa: E402,F401
 from ldnn.ops import _ext  # noqa: E402
 
 SHAPES = {"enhanced_cnn": [(128, 16, 128, 3, 1, 1), (256, 8, 256, 3, 1, 1), (512, 4, 512, 3, 1, 1)],
-          "resnet18": [(128, 28, 128, 3, 1, 1), (256, 14, 256, 3, 1, 1), (512, 7, 512, 3, 1, 1)]}
+          "resnet18_l1": [(64, 56, 64, 3, 1, 1)],
+          "resnet18": [(64, 56, 64, 3, 1, 1), (128, 28, 128, 3, 1, 1), (256, 14, 256, 3, 1, 1), (512, 7, 512, 3, 1, 1)]}
 
 
 def med(v):

@@ -58,6 +58,17 @@ for step in "$@"; do
              > $O/prof_$a.txt 2>&1 ;;
     profmlp) $T 400 rocprofv3 --kernel-trace --stats -d $O/prof_mlp -o run -- python -u bench.py --steps 20 --warmup 5 \
              > $O/prof_mlp.txt 2>&1 ;;
+    wsbench) $T 200 python -u scripts/bench_ws64.py >> $O/bench_ws64.jsonl 2>> $O/bench_ws64.err ;;
+    wsko) rc=0   # knockout builds of the weight-stationary conv (fwd, b256): XF bits, see conv_ws64_kernel
+          for xf in ${WS_XF:-1 2 4 8}; do LDNN_CONV_XF=$xf $T 100 python -u scripts/bench_ws64.py --modes 1 --fwd-only \
+            --batches 256 >> $O/ws_knockouts.jsonl 2>> $O/bench_ws64.err || { rc=$?; break; }; done; (exit $rc) ;;
+    wspmc) (cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+           timeout -s KILL 90 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_LDS \
+             SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_WAVES GRBM_GUI_ACTIVE --output-format csv -d $O/wspmc/p1 -o run -- \
+             python3 scripts/bench_ws64.py --modes 0,1 --batches 256 > $O/wspmc_p1.log 2>&1 &&
+           timeout -s KILL 90 rocprofv3 --pmc SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_INSTS_MFMA SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
+             GRBM_GUI_ACTIVE --output-format csv -d $O/wspmc/p2 -o run -- \
+             python3 scripts/bench_ws64.py --modes 0,1 --batches 256 > $O/wspmc_p2.log 2>&1) ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
   rc=$?

@@ -172,6 +172,42 @@ def test_halo_conv_matches_gather_kernel(N, C, H, W, K):
         torch.testing.assert_close(dx2, dx0, rtol=2e-2, atol=2e-2 * dx0.abs().max().item())
 
 
+@pytest.mark.parametrize("N,H,W", [(64, 56, 56), (2, 56, 56), (3, 9, 11), (1, 63, 63), (5, 5, 5), (24, 28, 28)])
+def test_weight_stationary_conv64_matches_halo_and_fp32(N, H, W):
+    """The weight-stationary persistent 64 -> 64 channel 3x3 kernels (conv_ws64_kernel: all
+    9 taps' weights in registers, one halo per 128-row tile double-buffered a tile ahead) == the
+    halo kernel (set_conv_ws 0)
+    bit for bit (same MFMA order; to rounding where the halo kernel splits K) for fwd and dgrad,
+    and == the fp32 reference.  N 64 at 56 x 56
+    gives every workgroup several tiles (the DMA-ahead path); 3 x 9 x 11 a ragged last tile."""
+    torch.manual_seed(11)
+    Cc = _ext.C()
+    x = torch.randn(N, H, W, 64, device="cuda").bfloat16()
+    w = (torch.randn(64, 3, 3, 64, device="cuda") * (1.0 / 576 ** 0.5)).bfloat16()
+    gy = torch.randn(N, H, W, 64, device="cuda").bfloat16()
+    outs, mode = {}, 1
+    try:
+        for m in (0, mode):
+            Cc.set_conv_ws(m)
+            y = torch.full((N, H, W, 64), 7.0, device="cuda", dtype=torch.bfloat16)
+            Cc.conv_fwd(x, w, y, 1, 1)
+            dx = torch.full((N, H, W, 64), 7.0, device="cuda", dtype=torch.bfloat16)
+            Cc.conv_dgrad(gy, w, dx, 1, 1)
+            outs[m] = (y, dx)
+    finally:
+        Cc.set_conv_ws(1)
+    if N * H * W >= 65536:  # the halo kernel runs unsplit there: same MFMA order, same bits
+        assert torch.equal(outs[mode][0], outs[0][0])
+        assert torch.equal(outs[mode][1], outs[0][1])
+    for a, b in zip(outs[mode], outs[0]):  # small M: the halo kernel splits K (another summation order)
+        torch.testing.assert_close(a.float(), b.float(), rtol=1e-2, atol=1e-2 * b.float().abs().max().item())
+    xf, wf, gyf = x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), gy.float().permute(0, 3, 1, 2)
+    yr = torch.nn.functional.conv2d(xf, wf, padding=1).permute(0, 2, 3, 1)
+    dxr = torch.nn.grad.conv2d_input(xf.shape, wf, gyf, padding=1).permute(0, 2, 3, 1)
+    torch.testing.assert_close(outs[mode][0].float(), yr, rtol=1e-2, atol=1e-2 * yr.abs().max().item())
+    torch.testing.assert_close(outs[mode][1].float(), dxr, rtol=1e-2, atol=1e-2 * dxr.abs().max().item())
+
+
 @pytest.mark.parametrize("N,C,H,W,K", [(2, 64, 56, 56, 64), (3, 128, 28, 28, 128), (2, 256, 14, 14, 512),
                                        (4, 512, 7, 7, 512), (5, 64, 9, 9, 128), (2, 128, 16, 16, 256),
                                        (1, 64, 63, 63, 64), (7, 192, 4, 4, 64), (3, 64, 5, 5, 64), (2, 64, 8, 8, 128), (3, 128, 9, 11, 64)])
