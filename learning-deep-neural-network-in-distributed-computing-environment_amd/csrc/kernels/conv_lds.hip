@@ -1071,7 +1071,7 @@ constexpr int kWBytes = 64 * kPitch;   // 74,752 B
 
 // XF (LDNN_CONV_XF experiment builds): bit0 no halo DMA after the first two tiles, bit1 no
 // epilogue stores, bit2 no A fragment reads, bit3 no waits on the fragment reads (results wrong
-// by construction), bit5 phase trace.
+// by construction), bit4 reads kept but the MFMAs take register operands, bit5 phase trace.
 template <int RT, bool DGRAD, int XF = 0>
 __global__ __launch_bounds__(256, 1) void conv_ws64_kernel(LArgs a, const bf16_t* pa, uint32_t bytes_a,
                                                            const bf16_t* pw) {
@@ -1218,6 +1218,7 @@ __global__ __launch_bounds__(256, 1) void conv_ws64_kernel(LArgs a, const bf16_t
       for (int i = 0; i < RT; ++i) acc[j][i] = floatx4{0.f, 0.f, 0.f, 0.f};
     lds_barrier();  // every wave waited for its own pieces of tile t: the whole halo is visible
     __builtin_amdgcn_s_setprio(1);
+    uint32_t sink = 0;
     // step st = tap * 2 + kk: its RT fragment reads are issued two steps ahead
     static_assert(RT == 4, "the counted waits below name 4 fragments");
     bf16x8 fa[3][RT];
@@ -1236,10 +1237,18 @@ __global__ __launch_bounds__(256, 1) void conv_ws64_kernel(LArgs a, const bf16_t
       for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int i = 0; i < RT; ++i)
-          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[st >> 1][st & 1][j], f[i], acc[j][i], 0, 0, 0);
+          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[st >> 1][st & 1][j],
+                                                              (XF & 16) != 0 ? fb[st >> 1][st & 1][i & 1] : f[i], acc[j][i], 0, 0, 0);
+      if constexpr ((XF & 16) != 0) {  // knockout: reads kept (consumed by a VALU xor), MFMAs on registers
+#pragma unroll
+        for (int i = 0; i < RT; ++i) sink ^= __builtin_bit_cast(uint4, f[i]).x;
+      }
     }
     if constexpr ((XF & 8) != 0) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_setprio(0);
+    if constexpr ((XF & 16) != 0) {
+      if (sink == 0x12345679u) out[lane] = 0;
+    }
     lds_barrier();  // every wave is done reading this buffer
     if (t + 2 < t1 && (XF & 1) == 0) dma(t + 2, (t - t0) & 1);
     if (t + 1 < t1) {
@@ -1754,6 +1763,200 @@ __global__ __launch_bounds__(256, 2) void conv_patch_kernel(LArgs a, const bf16_
                                        blockIdx.y);
 }
 
+// Persistent weight-stationary variant of conv_patch_kernel for 64-filter stems (the ResNet-18
+// 7x7 / 2 stem: 384 us of the b256 step, ~15 us per 256-pixel tile-pair per CU, its B fragments
+// streamed from L2 one k-step ahead).  One 4-wave workgroup per CU keeps the whole [64][R*S*8]
+// weight matrix in registers (each wave: 64 rows x all 64 filters, KS x 4 fragments), walks a
+// contiguous run of 256-pixel tiles, DMAs each tile's input patch into a double buffer one tile
+// ahead (a fixed 48 pieces per tile: rows below the patch load harmlessly), and reads the A
+// fragments two k-steps ahead (asm + counted lgkmcnt, as conv_ws64_kernel).  Padding taps
+// (t >= R*S) read cell 0: their weights are zero.  The next BN's statistics stay in registers
+// over all tiles.  EPI_NONE, K = 64.
+template <int KS, int STR, int XF = 0>
+__global__ __launch_bounds__(256, 1) void conv_patch_ws_kernel(LArgs a, const bf16_t* px, uint32_t bytes_x,
+                                                               const bf16_t* pw) {
+  constexpr int BM = 256, NW = 4;
+  constexpr int PIECES = kPatchBytes / 1024, PPW = PIECES / NW;
+  static_assert(PPW * NW == PIECES && KS >= 3, "patch pieces / k-steps");
+  constexpr int LDS = 2 * kPatchBytes + 16;
+  __shared__ __attribute__((aligned(1024))) char smem[LDS];
+  const ConvShape& sh = a.s;
+  const Geo g = make_geo(a, false);
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int PQ = sh.P * sh.Q, PW = sh.W + 2 * sh.pad, RS = sh.R * sh.S;
+  const int T = g.M / BM;
+  const int t0 = (int)((int64_t)blockIdx.x * T / gridDim.x);
+  const int t1 = (int)((int64_t)(blockIdx.x + 1) * T / gridDim.x);
+  uint64_t* trace = nullptr;
+  if constexpr ((XF & 32) != 0) {
+    if (threadIdx.x == 0 && a.trace != nullptr) {
+      trace = a.trace + 4 * (size_t)blockIdx.x;
+      trace[0] = __builtin_amdgcn_s_memrealtime();
+    }
+  }
+
+  Rsrc rx;
+  rx.r = __builtin_amdgcn_make_buffer_rsrc((void*)px, (short)0, (int)bytes_x, 0x00020000);
+  // patch of tile t into buffer b: cell e = (i, j) -> input (STR*p_lo - pad + i, j - pad)
+  auto dma = [&](int t, int b) {
+    const int m0 = t * BM, n_img = m0 / PQ, p_lo = (m0 - n_img * PQ) / sh.Q;
+    const int ih0 = STR * p_lo - sh.pad;
+    char* const dst = smem + b * kPatchBytes;
+#pragma unroll
+    for (int q = 0; q < PPW; ++q) {
+      const int pc = q * NW + wid;
+      const int e = pc * 64 + lane;
+      const int i = fdiv(e, a.f_w), j = e - i * PW;
+      const int ih = ih0 + i, iw = j - sh.pad;
+      const bool ok = (unsigned)ih < (unsigned)sh.H && (unsigned)iw < (unsigned)sh.W;
+      const int o = ok ? (int)((((unsigned)n_img * sh.H + ih) * (unsigned)sh.W + iw) * 16u) : (int)kOOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx.r, (lds_void*)(dst + pc * 1024), 16, o, 0, 0, 0);
+    }
+  };
+  if (t0 < t1) {
+    dma(t0, 0);
+    if (t0 + 1 < t1) dma(t0 + 1, 1);
+  }
+  // B fragments of every k-step (filter j*16 + (lane & 15), taps 4k + lane/16): registers for the launch
+  bf16x8 fb[KS][4];
+#pragma unroll
+  for (int k = 0; k < KS; ++k)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int t = k * 4 + (lane >> 4);
+      fb[k][j] = t < RS ? *reinterpret_cast<const bf16x8*>(pw + (size_t)(j * 16 + (lane & 15)) * a.rsc + t * 8)
+                        : bf16x8{};
+    }
+  // this lane group's tap offset (in patch cells) per k-step; padding taps read cell 0 (zero weights)
+  int toff[KS];
+#pragma unroll
+  for (int k = 0; k < KS; ++k) {
+    const int t = k * 4 + (lane >> 4);
+    const int r = t / sh.S;
+    toff[k] = t < RS ? r * PW + (t - r * sh.S) : 0;
+  }
+  if (t0 < t1) {
+    if (t0 + 1 < t1) wait_vm<PPW>();  // tile t0's patch landed (loads retire in order)
+    else wait_vm<0>();
+  }
+  if constexpr ((XF & 32) != 0) {
+    if (trace != nullptr) trace[1] = __builtin_amdgcn_s_memrealtime();
+  }
+  float bs0[4][4], bs1[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bs0[j][r] = bs1[j][r] = 0.f;
+  bf16_t* const out = reinterpret_cast<bf16_t*>(a.out);
+  for (int t = t0; t < t1; ++t) {
+    const int m0 = t * BM, n_img = m0 / PQ, mi0 = m0 - n_img * PQ, p_lo = mi0 / sh.Q;
+    const uint32_t patch = lds_off(smem + ((t - t0) & 1) * kPatchBytes);
+    uint32_t base[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int mi = mi0 + wid * 64 + i * 16 + (lane & 15);
+      const int p = fdiv(mi, a.f_q), q = mi - p * sh.Q;
+      base[i] = patch + (uint32_t)((STR * (p - p_lo)) * PW + STR * q) * 16u;
+    }
+    auto read_step = [&](int k, bf16x8 (&f)[4]) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t ad = base[i] + (uint32_t)toff[k] * 16u;
+        asm volatile("ds_read_b128 %0, %1" : "=v"(f[i]) : "v"(ad));
+      }
+    };
+    floatx4 acc[4][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[j][i] = floatx4{0.f, 0.f, 0.f, 0.f};
+    lds_barrier();  // every wave waited for its own pieces of tile t: the whole patch is visible
+    bf16x8 fa[3][4];
+    read_step(0, fa[0]);
+    read_step(1, fa[1]);
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+      bf16x8 (&f)[4] = fa[k % 3];
+      if (k + 2 < KS) read_step(k + 2, fa[(k + 2) % 3]);
+      if (k + 2 < KS) asm volatile("s_waitcnt lgkmcnt(8)" : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]));
+      else if (k + 1 < KS) asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]));
+      else asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]));
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[k][j], f[i], acc[j][i], 0, 0, 0);
+    }
+    lds_barrier();  // every wave is done reading this buffer
+    if (t + 2 < t1) dma(t + 2, (t - t0) & 1);
+    if (t + 1 < t1) {  // tile t+1's patch (issued a tile ago; see conv_ws64_kernel for why vmcnt(PPW) holds)
+      if (t + 2 < t1) wait_vm<PPW>();
+      else wait_vm<0>();
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = m0 + wid * 64 + i * 16 + (lane & 15);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = j * 16 + 4 * (lane >> 4);
+        const floatx4 v = acc[j][i];
+        const u16x4 o = u16x4{f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+        *reinterpret_cast<u16x4*>(out + (size_t)m * 64 + c) = o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float bv = bf2f(o[r]);
+          bs0[j][r] += bv;
+          bs1[j][r] += bv * bv;
+        }
+      }
+    }
+  }
+  if constexpr ((XF & 32) != 0) {
+    if (trace != nullptr) trace[2] = __builtin_amdgcn_s_memrealtime();
+  }
+  if (a.bn_stats) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          bs0[j][r] += __shfl_xor(bs0[j][r], o, 64);
+          bs1[j][r] += __shfl_xor(bs1[j][r], o, 64);
+        }
+    float* red = reinterpret_cast<float*>(smem);  // [4][64][2]
+    __syncthreads();
+    if ((lane & 15) == 0) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int c = j * 16 + 4 * (lane >> 4) + r;
+          red[(wid * 64 + c) * 2] = bs0[j][r];
+          red[(wid * 64 + c) * 2 + 1] = bs1[j][r];
+        }
+    }
+    __syncthreads();
+    float* accc = a.bn.acc + (size_t)(blockIdx.x % kBnCopies) * 2 * 64;
+    if (threadIdx.x < 64) {
+      float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+      for (int q = 0; q < NW; ++q) {
+        s0 += red[(q * 64 + threadIdx.x) * 2];
+        s1 += red[(q * 64 + threadIdx.x) * 2 + 1];
+      }
+      bn_acc_add(accc + threadIdx.x, s0);
+      bn_acc_add(accc + 64 + threadIdx.x, s1);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's atomics have completed
+    bn_finalize_last<false, kBnCopies>(a.bn, g.M, 64, gridDim.x, red, LDS / 4);
+  }
+  if constexpr ((XF & 32) != 0) {
+    if (trace != nullptr) trace[3] = __builtin_amdgcn_s_memrealtime();
+  }
+}
+
 int slab_nt_env() {
   static const int v = [] {
     const char* e = std::getenv("LDNN_SLAB_NT");
@@ -2076,7 +2279,8 @@ bool halo_takes(const ConvShape& s, int wm) {
 }
 
 // Weight-stationary path (conv_ws64_kernel) for 64 -> 64 channel 3x3 stride-1 pad-1 fwd
-// (no bias) and dgrad.  LDNN_CONV_WS=0 (A/B knob) turns it off (conv_halo_kernel).
+// (no bias) and dgrad, and conv_patch_ws_kernel for the 64-filter 7x7 / 2 stem.  LDNN_CONV_WS=0
+// (A/B knob) turns both off (conv_halo_kernel / conv_patch_kernel).
 int g_conv_ws = -2;  // -2: not read yet
 int ws_env() {
   if (g_conv_ws == -2) g_conv_ws = env_int("LDNN_CONV_WS", 1);
@@ -2103,13 +2307,14 @@ hipError_t launch_ws64_m(LArgs a, int grid, const bf16_t* pa, size_t ba, const b
   const int xf = conv_xf_env();
   if (xf == 32) {
     conv_ws64_kernel<RT, DGRAD, 32><<<grid, 256, 0, st>>>(a, pa, (uint32_t)ba, pw);
-  } else if (xf == 1 || xf == 2 || xf == 4 || xf == 7 || xf == 8 || xf == 10) {  // knockouts (fwd timing only)
+  } else if (xf == 1 || xf == 2 || xf == 4 || xf == 7 || xf == 8 || xf == 10 || xf == 16) {  // knockouts (fwd timing only)
     if constexpr (DGRAD) return hipErrorInvalidValue;
     else if (xf == 1) conv_ws64_kernel<RT, false, 1><<<grid, 256, 0, st>>>(a, pa, (uint32_t)ba, pw);
     else if (xf == 2) conv_ws64_kernel<RT, false, 2><<<grid, 256, 0, st>>>(a, pa, (uint32_t)ba, pw);
     else if (xf == 4) conv_ws64_kernel<RT, false, 4><<<grid, 256, 0, st>>>(a, pa, (uint32_t)ba, pw);
     else if (xf == 8) conv_ws64_kernel<RT, false, 8><<<grid, 256, 0, st>>>(a, pa, (uint32_t)ba, pw);
     else if (xf == 10) conv_ws64_kernel<RT, false, 10><<<grid, 256, 0, st>>>(a, pa, (uint32_t)ba, pw);
+    else if (xf == 16) conv_ws64_kernel<RT, false, 16><<<grid, 256, 0, st>>>(a, pa, (uint32_t)ba, pw);
     else conv_ws64_kernel<RT, false, 7><<<grid, 256, 0, st>>>(a, pa, (uint32_t)ba, pw);
   } else
     conv_ws64_kernel<RT, DGRAD><<<grid, 256, 0, st>>>(a, pa, (uint32_t)ba, pw);
@@ -2348,10 +2553,23 @@ hipError_t launch_patch_e(const LArgs& a, int epi, const bf16_t* x, size_t bx, c
   }
   return hipGetLastError();
 }
+template <int KS, int STR>
+hipError_t launch_patch_ws_e(LArgs a, const bf16_t* x, size_t bx, const bf16_t* w, hipStream_t st) {
+  const int grid = std::max(1, std::min(a.M / 256, cu_count()));
+  a.tiles_x = grid;
+  if (conv_xf_env() == 32)
+    conv_patch_ws_kernel<KS, STR, 32><<<grid, 256, 0, st>>>(a, x, (uint32_t)bx, w);
+  else
+    conv_patch_ws_kernel<KS, STR><<<grid, 256, 0, st>>>(a, x, (uint32_t)bx, w);
+  return hipGetLastError();
+}
+
 hipError_t launch_patch(LArgs a, int epi, const bf16_t* x, size_t bx, const bf16_t* w, hipStream_t st) {
   a.f_w = make_fastdiv(a.s.W + 2 * a.s.pad);  // patch row length (cell -> row, column)
   a.tiles_x = (a.M / 256) * (a.N / 64);
   const int ks = patch_ks(a.s);
+  if (ws_env() != 0 && epi == EPI_NONE && a.N == 64 && ks == 13 && a.s.stride == 2)  // (LDNN_CONV_WS, as ws64)
+    return launch_patch_ws_e<13, 2>(a, x, bx, w, st);
   if (a.s.stride == 1) {
     if (ks == 3) return launch_patch_e<3, 1>(a, epi, x, bx, w, st);
     if (ks == 7) return launch_patch_e<7, 1>(a, epi, x, bx, w, st);

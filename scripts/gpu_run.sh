@@ -60,7 +60,7 @@ for step in "$@"; do
              > $O/prof_mlp.txt 2>&1 ;;
     wsbench) $T 200 python -u scripts/bench_ws64.py >> $O/bench_ws64.jsonl 2>> $O/bench_ws64.err ;;
     wsko) rc=0   # knockout builds of the weight-stationary conv (fwd, b256): XF bits, see conv_ws64_kernel
-          for xf in ${WS_XF:-1 2 4 8}; do LDNN_CONV_XF=$xf $T 100 python -u scripts/bench_ws64.py --modes 1 --fwd-only \
+          for xf in ${WS_XF:-1 2 4 8}; do LDNN_CONV_XF=$xf $T 100 python -u scripts/bench_ws64.py --modes 1 --fwd-only --no-stem \
             --batches 256 >> $O/ws_knockouts.jsonl 2>> $O/bench_ws64.err || { rc=$?; break; }; done; (exit $rc) ;;
     wspmc) (cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
            timeout -s KILL 90 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_LDS \

@@ -172,6 +172,42 @@ def test_halo_conv_matches_gather_kernel(N, C, H, W, K):
         torch.testing.assert_close(dx2, dx0, rtol=2e-2, atol=2e-2 * dx0.abs().max().item())
 
 
+@pytest.mark.parametrize("N", [24, 3])
+def test_weight_stationary_stem_matches_patch_kernel_and_fp32(N):
+    """The persistent weight-stationary 7x7 / 2 stem (conv_patch_ws_kernel: weights in registers,
+    input patches double-buffered a tile ahead; N 24 gives every workgroup several tiles) == the
+    per-tile patch kernel (set_conv_ws 0) bit for bit, == the fp32 conv, and its fused BatchNorm
+    statistics (kept in registers over a workgroup's tiles) == the patch kernel's."""
+    torch.manual_seed(13)
+    Cc = _ext.C()
+    x = torch.zeros(N, 224, 224, 8, device="cuda", dtype=torch.bfloat16)
+    x[..., :3] = torch.randn(N, 224, 224, 3, device="cuda").bfloat16()
+    w = torch.zeros(64, 7, 7, 8, device="cuda", dtype=torch.bfloat16)
+    w[..., :3] = (torch.randn(64, 7, 7, 3, device="cuda") * 0.08).bfloat16()
+    res = {}
+    try:
+        for m in (0, 1):
+            Cc.set_conv_ws(m)
+            y = torch.full((N, 112, 112, 64), 7.0, device="cuda", dtype=torch.bfloat16)
+            ws = torch.zeros(Cc.bn_workspace_floats(64), device="cuda")
+            sm, si = torch.zeros(64, device="cuda"), torch.zeros(64, device="cuda")
+            rm, rv = torch.zeros(64, device="cuda"), torch.ones(64, device="cuda")
+            Cc.conv_fwd(x, w, y, 2, 3, bn_ws=ws, bn_running_mean=rm, bn_running_var=rv, bn_save_mean=sm,
+                        bn_save_invstd=si)
+            res[m] = (y, sm, si, rm, rv)
+    finally:
+        Cc.set_conv_ws(1)
+    assert torch.equal(res[1][0], res[0][0])
+    for a, b in zip(res[1][1:], res[0][1:]):  # statistics: fp32 sums in another order
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5)
+    ref = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), stride=2,
+                                     padding=3).permute(0, 2, 3, 1)
+    torch.testing.assert_close(res[1][0].float(), ref, rtol=1e-2, atol=1e-2 * ref.abs().max().item())
+    yb = res[1][0].float().reshape(-1, 64)
+    torch.testing.assert_close(res[1][1], yb.mean(0), rtol=1e-3, atol=1e-4)
+    torch.testing.assert_close(res[1][2], torch.rsqrt(yb.var(0, unbiased=False) + 1e-5), rtol=1e-3, atol=1e-4)
+
+
 @pytest.mark.parametrize("N,H,W", [(64, 56, 56), (2, 56, 56), (3, 9, 11), (1, 63, 63), (5, 5, 5), (24, 28, 28)])
 def test_weight_stationary_conv64_matches_halo_and_fp32(N, H, W):
     """The weight-stationary persistent 64 -> 64 channel 3x3 kernels (conv_ws64_kernel: all
