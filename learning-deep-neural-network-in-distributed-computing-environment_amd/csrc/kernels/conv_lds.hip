@@ -2090,8 +2090,10 @@ int wgrad_xcd_env() {
 WgradPlan plan_wgrad(const ConvShape& s) {
   WgradPlan p;
   p.ring = wgrad_ring_ok(s);
-  if (p.ring) {  // (64 filters x 576 tap-channels) blocks x npq slices of >= 12 K-tiles, ~384 workgroups
-    static const int target = env_int("LDNN_CONV_RING_TARGET", 384);
+  if (p.ring) {  // (64 filters x 576 tap-channels) blocks x npq slices of >= 12 K-tiles, ~512 workgroups
+    // (two per CU: ResNet-18 b256 7.652 vs 7.705-7.711 ms at 384, 7.70 at 256, 7.78 at 1024; b64 capped by
+    // the 12-K-tile floor either way, profiles/r4/ring_wgrad_target_ab.jsonl)
+    static const int target = env_int("LDNN_CONV_RING_TARGET", 512);
     p.narrow = false;
     p.tiles = (s.K / 64) * (s.C / 64);
     p.nk_all = (s.N * s.P * s.Q + 63) / 64;
