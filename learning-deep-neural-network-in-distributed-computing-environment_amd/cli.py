@@ -134,6 +134,9 @@ def resolve_engine(args, model, dev, world: int) -> bool:
         why = "the static engine needs the native extension on a GPU"
     elif args.grad_comm_dtype != "fp32":
         why = "--grad_comm_dtype bf16 runs on the autograd path"
+    elif args.legacy_gossip and args.sync_every == "step" and args.topology != "allreduce" and world > 1:
+        # the static engine's grad_mix always applies the combine (no reference-Q2 mode)
+        why = "--legacy_gossip runs on the autograd path"
     if args.engine == "static" and why is not None:
         raise SystemExit(f"--engine static: {why}")
     return args.engine != "autograd" and why is None
@@ -190,17 +193,20 @@ def main(argv=None):
     if use_engine:   # the engine synchronises its own gradients (per-step DP) or is a plain replica
         D.broadcast_module(model)
         flat.refresh_shadow()
-    elif args.sync_every == "step" and args.topology == "allreduce" and world > 1:
+    elif args.sync_every == "step" and world > 1:
         weighted = args.aggregation_type == "weighted"
-        if args.shard_optimizer == "on" and weighted:
-            raise SystemExit("--shard_optimizer on needs --aggregation_type equal (the weighted mix gives every "
-                             "rank its own update)")
-        shard = not weighted and (args.shard_optimizer == "on" or (args.shard_optimizer == "auto"
-                                                                    and dev.type == "cuda"))
+        gossip = {"allreduce": 0, "ring": 1, "double_ring": 2}[args.topology]
+        if args.shard_optimizer == "on" and (weighted or gossip):
+            raise SystemExit("--shard_optimizer on needs --topology allreduce --aggregation_type equal (the "
+                             "weighted mix and gossip give every rank its own update)")
+        if gossip and args.grad_comm_dtype != "fp32":
+            raise SystemExit("per-step gossip exchanges fp32 gradient buckets (--grad_comm_dtype fp32)")
+        shard = not weighted and not gossip and (args.shard_optimizer == "on" or (args.shard_optimizer == "auto"
+                                                                                   and dev.type == "cuda"))
         dp = DataParallel(model, comm, bucket_cap_mb=args.bucket_mb,
                           local_weight=args.local_weight if weighted else None,
                           comm_dtype=torch.bfloat16 if args.grad_comm_dtype == "bf16" else None,
-                          shard_optimizer=shard)
+                          shard_optimizer=shard, gossip=gossip, legacy_gossip=args.legacy_gossip)
         flat = dp.flat   # (sharding re-lays the flat buffers out)
     else:  # reference A6: broadcast every state_dict entry from rank 0
         D.broadcast_module(model)

@@ -23,6 +23,18 @@ from ..utils.flat_params import owner_of
 _LAZY_ZERO = __import__("os").environ.get("LDNN_LAZY_ZERO", "1") != "0"
 
 
+def _refuse_partial_sharded(params):
+    """A param group that does not map onto one whole FlatParams would take the per-tensor
+    update path; on a sharded DataParallel buffer (only this rank's shard of flat.grad is
+    reduced, and nothing all-gathers the result) that silently diverges the replicas."""
+    for p in params:
+        f = owner_of(p)
+        if f is not None and getattr(f, "shard_sync", None) is not None:
+            raise RuntimeError("DataParallel(shard_optimizer=True): the optimizer's param group must hold "
+                               "every parameter of the model's flat buffer (one group, built AFTER the "
+                               "DataParallel wrapper)")
+
+
 class _FlatOptimizer(torch.optim.Optimizer):
     def _ls(self) -> dict:
         """Fused (flat-buffer) optimizer state: momentum / moments / step / hp."""
@@ -55,6 +67,7 @@ class _FlatOptimizer(torch.optim.Optimizer):
             return None
         f = owner_of(ps[0])
         if f is None or any(owner_of(p) is not f for p in ps) or len(ps) != len(f.segments):
+            _refuse_partial_sharded(ps)
             return None
         return f
 
@@ -117,8 +130,14 @@ class _FlatOptimizer(torch.optim.Optimizer):
         ranges (its shard of every reduce-scattered bucket + the replicated tail), then
         let the data-parallel wrapper start the weight all-gathers.  False otherwise."""
         sh = getattr(f, "shard_sync", None)
-        if sh is None or len(self.param_groups) != 1:
+        if sh is None:
             return False
+        if len(self.param_groups) != 1:
+            # the full-replica update below would read flat.grad, of which only this rank's
+            # shards hold reduced values, and no weight all-gather would follow: replicas
+            # would silently diverge
+            raise RuntimeError("DataParallel(shard_optimizer=True) needs ONE param group holding the whole "
+                               f"flat buffer; this optimizer has {len(self.param_groups)}")
         f.finalize_grads()
         ctx = self._begin_ranges(f, group)
         parts = getattr(sh, "step_parts", None)

@@ -104,8 +104,11 @@ class Comm:
     def barrier(self):
         raise NotImplementedError
 
-    def sendrecv(self, sends: list[tuple[torch.Tensor, int]], recvs: list[tuple[torch.Tensor, int]]):
-        """Grouped point-to-point: post every send and receive, wait for all."""
+    def sendrecv(self, sends: list[tuple[torch.Tensor, int]], recvs: list[tuple[torch.Tensor, int]],
+                 async_op: bool = False):
+        """Grouped point-to-point: post every send and receive, wait for all.  ``async_op``:
+        return a handle whose ``wait()`` orders the current stream after them (RCCL) --
+        the sends' buffers must not change before it."""
         raise NotImplementedError
 
     def reduce_scatter(self, out: torch.Tensor, inp: torch.Tensor, async_op: bool = False):
@@ -122,6 +125,17 @@ class Comm:
 class _Done:
     def wait(self):
         return None
+
+
+class _Works:
+    """Several in-flight c10d works behind one ``wait()`` (a grouped send/recv)."""
+
+    def __init__(self, works):
+        self.works = list(works)
+
+    def wait(self):
+        for w in self.works:
+            w.wait()
 
 
 class LocalComm(Comm):
@@ -141,10 +155,11 @@ class LocalComm(Comm):
     def barrier(self):
         self.record("barrier")
 
-    def sendrecv(self, sends, recvs):
+    def sendrecv(self, sends, recvs, async_op=False):
         self.record("sendrecv")
         for (rt, src), (st, dst) in zip(recvs, sends):
             rt.copy_(st)
+        return _Done() if async_op else None
 
     def reduce_scatter(self, out, inp, async_op=False):
         self.record("reduce_scatter", inp)
@@ -225,7 +240,7 @@ class TorchComm(Comm):
         else:
             dist.barrier(group=self.group)
 
-    def sendrecv(self, sends, recvs):
+    def sendrecv(self, sends, recvs, async_op=False):
         self.record("sendrecv")
         # gloo moves GPU tensors point-to-point through a slow per-op path (measured: a
         # 178 MB ring exchange ~10 s vs 0.1 s for the same bytes from host memory), so the
@@ -236,11 +251,15 @@ class TorchComm(Comm):
             dev_recvs, recvs = recvs, [(torch.empty(t.shape, dtype=t.dtype), src) for t, src in recvs]
         ops = [dist.P2POp(dist.irecv, t, self._global(src), self.group) for t, src in recvs]
         ops += [dist.P2POp(dist.isend, t, self._global(dst), self.group) for t, dst in sends]
-        for w in dist.batch_isend_irecv(ops):
+        works = dist.batch_isend_irecv(ops)
+        if async_op and not stage:
+            return _Works(works)   # RCCL: wait() = stream waits, no host sync
+        for w in works:
             w.wait()
         if stage:
             for (t, _), (c, _) in zip(dev_recvs, recvs):
                 t.copy_(c)
+        return _Done() if async_op else None
 
     def reduce_scatter(self, out, inp, async_op=False):
         self.record("reduce_scatter", inp)
@@ -337,7 +356,7 @@ class FakeComm(Comm):
         self.record("barrier")
         self._exchange(None)
 
-    def sendrecv(self, sends, recvs):
+    def sendrecv(self, sends, recvs, async_op=False):
         self.record("sendrecv")
         msgs = {(self.rank, dst): st.detach().clone() for st, dst in sends}
         allm = self._exchange(msgs)
@@ -346,6 +365,7 @@ class FakeComm(Comm):
             merged.update(m)
         for rt, src in recvs:
             rt.copy_(merged[(src, self.rank)])
+        return _Done() if async_op else None
 
     def reduce_scatter(self, out, inp, async_op=False):
         self.record("reduce_scatter", inp)

@@ -95,12 +95,25 @@ class GradBucketer:
 
     def __init__(self, flat: FlatParams, comm: Comm, bucket_cap_elems: int = 8 << 20,
                  comm_dtype: torch.dtype | None = None, local_weight: float | None = None,
-                 last_bucket_cap_elems: int | None = 1 << 20, groups: list | None = None):
+                 last_bucket_cap_elems: int | None = 1 << 20, groups: list | None = None,
+                 gossip: int = 0, legacy_gossip: bool = False):
         """``groups`` (sharded mode, DataParallel(shard_optimizer=True)): the bucket plan as
         lists of parameters -- every group but the last is reduce-scattered (its flat range
-        already N x 64 aligned), the last one (the 1-D parameters) is all-reduced."""
+        already N x 64 aligned), the last one (the 1-D parameters) is all-reduced.
+
+        ``gossip`` = 1 (ring) / 2 (double ring): per-step decentralised SGD instead of an
+        all-reduce -- each bucket goes to the next ``gossip`` ranks and comes from the
+        previous ones in ONE grouped send/recv (each neighbour pair on its own xGMI link),
+        and after the wait one fused mix3 pass evaluates the reference's combine in place:
+        (g + y1)/2 or w g + (1-w) y1 (BR/communication.py:5-62), (g + y1 + y2)/3 or
+        w g + (1-w)/2 (y1 + y2) (BDR/communication.py:5-77); ``local_weight`` None = equal.
+        ``legacy_gossip``: the reference's GPU behaviour -- the exchange runs,
+        the update is lost (except the double-ring weighted op, which works there too)."""
         self.flat, self.comm = flat, comm
         self.comm_dtype = None if comm_dtype in (None, torch.float32) else comm_dtype
+        self.gossip = int(gossip)
+        if self.gossip and (groups is not None or self.comm_dtype is not None):
+            raise ValueError("per-step gossip exchanges whole fp32 buckets (no sharding, no bf16 stage)")
         self.buckets: list[dict] = []
         N = comm.world_size
         self.shard = groups is not None
@@ -134,12 +147,30 @@ class GradBucketer:
                         if b["sharded"] else None for b in self.buckets]
         self.weighted = local_weight is not None and N > 1
         self._own = None
-        if self.weighted:
+        self._recv = None
+        if self.gossip:
+            w = 0.5 if local_weight is None else float(local_weight)
+            if self.gossip == 1:
+                self._mix_abc = (0.5, 0.5, 0.0) if local_weight is None else (w, 1.0 - w, 0.0)
+            else:
+                self._mix_abc = (1 / 3, 1 / 3, 1 / 3) if local_weight is None else (w, (1 - w) / 2, (1 - w) / 2)
+            self._apply_mix = not (legacy_gossip and dev.type == "cuda" and not (self.gossip == 2 and
+                                                                                 local_weight is not None))
+            # hop h: from (r - h), to (r + h); the 2-hop neighbour of a 2-rank world is this
+            # rank itself (its own gradient stands in, as parallel.aggregation.gossip_mix)
+            self._hops = [((self.rank - h) % N, (self.rank + h) % N) for h in range(1, self.gossip + 1)]
+            self._recv = [[torch.zeros(b["end"] - b["begin"], dtype=torch.float32, device=dev)
+                           if src != self.rank else None for src, _ in self._hops] for b in self.buckets]
+            self.weighted = False   # (the all-reduce's self-weighted mix is not used)
+        elif self.weighted:
             w = float(local_weight)
             other = (1.0 - w) / (N - 1)
             self._mix_ab = (w - other, other)
             self._own = [torch.empty(self._own_len(i), dtype=torch.float32, device=dev)
                          for i in range(len(self.buckets))]
+        # equal all-reduce average (1/N folded into the optimizer): the step a weighted tail
+        # batch can be re-scaled for (train_local_epoch's dp_tail)
+        self.averaging = not self.gossip and not self.weighted
         self.works: list = []
         self._pending: list[int] = []
         self._launched: list[bool] = []
@@ -204,13 +235,28 @@ class GradBucketer:
     def collective(self, i):
         """Issue bucket i's collective (async): reduce-scatter into this rank's shard
         buffer for a sharded bucket, else an in-place SUM all-reduce."""
+        if self.gossip:
+            g = self.grad_view(i)
+            recvs = [(rb, src) for rb, (src, _) in zip(self._recv[i], self._hops) if rb is not None]
+            sends = [(g, dst) for rb, (_, dst) in zip(self._recv[i], self._hops) if rb is not None]
+            return self.comm.sendrecv(sends, recvs, async_op=True) if recvs else None
         if self.buckets[i]["sharded"]:
             return self.comm.reduce_scatter(self._gshard[i], self.comm_buffer(i), async_op=True)
         return self.comm.all_reduce(self.comm_buffer(i), SUM, async_op=True)
 
     def post_collective(self, i):
         """Stream-ordered work after bucket i's collective landed: widen the stage /
-        the reduce-scattered shard back into the fp32 gradient, apply the weighted mix."""
+        the reduce-scattered shard back into the fp32 gradient, apply the weighted mix
+        (all-reduce) or the neighbour combine (gossip)."""
+        if self.gossip:
+            if self._apply_mix and self.comm.world_size > 1:
+                from .aggregation import _mix
+
+                g = self.grad_view(i)
+                ys = [rb if rb is not None else g for rb in self._recv[i]]
+                a, b, c = self._mix_abc
+                _mix(g, g, ys[0], ys[1] if len(ys) > 1 else None, a=a, b=b, c=c)
+            return
         if self.buckets[i]["sharded"]:
             lo, hi = self.shard_range(i)
             g = self.flat.grad[lo:hi]
@@ -252,11 +298,12 @@ class GradBucketer:
         return self.shard_range(i) if b["sharded"] else (b["begin"], b["end"])
 
     def opt_order(self) -> list[int]:
-        """Bucket order of a per-bucket optimizer: the replicated tail(s), then the sharded
-        buckets in FORWARD order (the last bucket -- the first layers -- first), so each
-        one's weight all-gather can start as soon as its own update is done."""
-        rep = [i for i, b in enumerate(self.buckets) if not b["sharded"]]
-        return rep + [i for i in reversed(range(len(self.buckets))) if self.buckets[i]["sharded"]]
+        """Bucket order of a per-bucket optimizer (GraphedDPStep): the sharded buckets in the
+        order their reduce-scatters complete (bucket order: the deep layers first), then the
+        replicated tail(s), whose all-reduce goes out last.  Each update waits only for its
+        own bucket's collective; the weight all-gathers follow in forward order."""
+        sh = [i for i, b in enumerate(self.buckets) if b["sharded"]]
+        return sh + [i for i, b in enumerate(self.buckets) if not b["sharded"]]
 
     def issue_gather(self, i):
         """All-gather sharded bucket i's updated weights, in place (async)."""
@@ -358,6 +405,10 @@ class DataParallel(nn.Module):
     weighted average (``--aggregation_type weighted``, BAR/communication.py:4-10);
     None (default) is the equal average (BAR/communication.py:21-25).
 
+    ``gossip`` = 1 / 2: per-step ring / double-ring gossip of the gradient buckets
+    (``--topology ring|double_ring --sync_every step``; GradBucketer), bucketed and
+    overlapped with the backward like the all-reduce, graph-replayed by GraphedDPStep.
+
     ``shard_optimizer`` (world > 1, equal averaging): reduce-scatter + sharded fused
     optimizer + bf16 weight all-gather (module docstring).  Build the optimizer AFTER this
     wrapper: sharding re-lays the flat buffers out once.  ``optimizer.step()`` then
@@ -367,7 +418,8 @@ class DataParallel(nn.Module):
 
     def __init__(self, module: nn.Module, comm: Comm | None = None, bucket_cap_mb: float = 32.0,
                  broadcast_init: bool = True, average: bool = True, comm_dtype: torch.dtype | None = None,
-                 local_weight: float | None = None, shard_optimizer: bool = False):
+                 local_weight: float | None = None, shard_optimizer: bool = False, gossip: int = 0,
+                 legacy_gossip: bool = False):
         super().__init__()
         self.module = module
         self.comm = comm or default_comm()
@@ -378,6 +430,8 @@ class DataParallel(nn.Module):
             # the weighted mix gives every rank its OWN gradient (replicas drift apart, as the
             # reference's weighted averaging does): no rank can own a shard of the others' update
             raise ValueError("shard_optimizer needs equal averaging (local_weight=None)")
+        if shard_optimizer and gossip:
+            raise ValueError("shard_optimizer needs the all-reduce topology (gossip gives every rank its own update)")
         if shard_optimizer and self.comm.world_size > 1:
             self.flat, groups = _shard_layout(module, self.flat, self.comm.world_size, cap)
         if broadcast_init and self.comm.world_size > 1:
@@ -388,9 +442,10 @@ class DataParallel(nn.Module):
             self.flat.refresh_shadow()
         # equal averaging folds 1/N into the fused optimizer; the weighted mix (and a
         # plain sum, average=False) leave the gradient at scale 1
-        self.flat.grad_scale = (1.0 / self.comm.world_size) if (average and local_weight is None) else 1.0
+        self.flat.grad_scale = (1.0 / self.comm.world_size) if (average and local_weight is None
+                                                                and not gossip) else 1.0
         self.bucketer = GradBucketer(self.flat, self.comm, cap, comm_dtype=comm_dtype, local_weight=local_weight,
-                                     groups=groups)
+                                     groups=groups, gossip=gossip, legacy_gossip=legacy_gossip)
 
     @property
     def sharded(self) -> bool:

@@ -277,6 +277,112 @@ def _measure_sharded(model_name, batch, bucket_mb, reps, steps, rounds, blocks, 
             "hidden_fraction": round(hidden / max(best["standin_alone_ms"], 1e-9), 3)}
 
 
+def measure_mlp_sharded(world: int = 8, batch: int = 16384, hidden: int = 4096, in_features: int = 784,
+                        classes: int = 10, bucket_elems: int = 8 << 20, reps: int = 4, blocks: int = 16,
+                        steps: int = 20, rounds: int = 3, tail_steps: int = 0) -> dict:
+    """The headline engine's sharded data-parallel step (train/static_mlp.py
+    StaticMLPEngine at world ``world``, rank 0: bench.py's mlp3 784-4096-4096-10 at
+    16384 samples per GPU, SGD momentum) on ONE GPU, every reduce-scatter / all-gather
+    replaced by the stand-in copy of the bytes it moves over xGMI ((N-1)/N of the fp32
+    gradient bucket, resp. of the bf16 weight bucket).  The engine's own schedule runs:
+    reduce-scatters issued between the backward's graph segments, shard updates and
+    weight all-gathers in forward order, the next step's forward waiting for each
+    bucket's gather right before its first GEMM.  Needs a (world-1) RCCL group for the
+    engine's rank bookkeeping; nothing goes over it in the timed steps."""
+    import os
+
+    import torch.distributed as dist
+
+    from ldnn.models.mlp import mlp3
+    from ldnn.train.static_mlp import OptimConfig, StaticMLPEngine
+
+    dev = torch.device("cuda", torch.cuda.current_device())
+    if not dist.is_initialized():
+        import socket
+
+        s_ = socket.socket()
+        s_.bind(("127.0.0.1", 0))
+        port = s_.getsockname()[1]
+        s_.close()
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                                device_id=dev)
+
+    def engine(w):
+        torch.manual_seed(1234)
+        m = mlp3(in_features, hidden, classes)
+        for mod in m.modules():
+            if isinstance(mod, torch.nn.Linear):
+                torch.nn.init.xavier_uniform_(mod.weight)
+                torch.nn.init.zeros_(mod.bias)
+        e = StaticMLPEngine(m, batch, OptimConfig("sgd", lr=0.01, momentum=0.9), device=dev, world_size=w,
+                            bucket_cap_elems=bucket_elems, shard_optimizer=True if w > 1 else None)
+        g = torch.Generator(device=dev).manual_seed(3)
+        e.load_batch(torch.randn(batch, in_features, device=dev, generator=g).bfloat16(),
+                     torch.randint(0, classes, (batch,), device=dev, generator=g))
+        return e
+
+    single = engine(1)
+    eng = engine(world)
+    standin = StandInComm(dev, reps, blocks)
+    state = {"on": True}
+
+    def moved(t):
+        n = t.numel() * (world - 1) // world // 8 * 8
+        v = t.view(-1)[:max(n, 8)]
+        return v if v.dtype == torch.float32 else v.view(torch.float32)
+
+    def rs(i):
+        b, e_, _ = eng.buckets[i]
+        return standin(("rs", i), moved(eng.flat.grad[b:e_])) if state["on"] else None
+
+    def ag(i):
+        b, e_, _ = eng.buckets[i]
+        return standin(("ag", i), moved(eng.flat.shadow[b:e_])) if state["on"] else None
+
+    eng._reduce_scatter, eng._all_gather = rs, ag
+    eng._broadcast_biases = lambda bi, capturing: None   # (a few KB: not a bandwidth term)
+
+    def chain_only():
+        state["on"] = False
+        try:
+            eng.step()
+        finally:
+            state["on"] = True
+
+    def standin_alone():
+        js = [rs(i) for i in range(len(eng.buckets))] + [ag(i) for i in reversed(range(len(eng.buckets)))]
+        for j in js:
+            j.wait()
+
+    def overlapped():
+        eng.step()
+
+    # prime (eager warm-up calls + the graph captures) before any timing
+    for _ in range(4):
+        single.step()
+        chain_only()
+        overlapped()
+    eng.sync()
+    fns = {"single_ms": single.step, "chain_ms": chain_only, "with_standin_ms": overlapped,
+           "standin_alone_ms": standin_alone}
+    best = {k: 1e9 for k in fns}
+    for _ in range(rounds):
+        for k, f in fns.items():
+            best[k] = min(best[k], _timed(lambda: (f(), eng.sync()) if f in (chain_only, overlapped) else f(), steps))
+    exposed = best["with_standin_ms"] - best["chain_ms"]
+    hid = best["standin_alone_ms"] - exposed
+    _tail(overlapped, tail_steps)
+    eng.sync()
+    return {"model": f"mlp3 {in_features}-{hidden}-{hidden}-{classes}", "batch": batch,
+            "mode": f"static engine, sharded (world {world} stand-in)", "optimizer": "sgd momentum 0.9",
+            "buckets": len(eng.buckets), "bucket_mb_fp32": [round((e_ - b) * 4 / 2**20, 2) for b, e_, _ in eng.buckets],
+            "segments": len(eng.segments), "standin_reps": reps, "standin_blocks": blocks,
+            **{k: round(v, 4) for k, v in best.items()}, "exposed_ms": round(exposed, 4),
+            "exposed_fraction_of_step": round(exposed / max(best["chain_ms"], 1e-9), 4),
+            "hidden_ms": round(hid, 4), "hidden_fraction": round(hid / max(best["standin_alone_ms"], 1e-9), 3)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="resnet18")
@@ -291,6 +397,11 @@ def main():
     ap.add_argument("--tail-steps", type=int, default=0, help="then this many overlapped steps after an idle gap "
                     "(kernel-trace timelines: scripts/probe_timeline.py)")
     a = ap.parse_args()
+    if a.model == "mlp3":   # the headline engine (StaticMLPEngine), sharded at world --shard (default 8)
+        print(json.dumps(measure_mlp_sharded(a.shard or 8, a.batch if a.batch != 64 else 16384, reps=a.reps,
+                                             blocks=a.blocks, steps=a.steps, rounds=a.rounds,
+                                             tail_steps=a.tail_steps)), flush=True)
+        return
     print(json.dumps(measure_overlap(a.model, a.batch, a.bucket_mb, a.reps, a.steps, rounds=a.rounds, blocks=a.blocks,
                                      shard_world=a.shard, optimizer=a.optimizer, tail_steps=a.tail_steps)), flush=True)
 

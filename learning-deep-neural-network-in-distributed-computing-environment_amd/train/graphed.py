@@ -283,10 +283,10 @@ class GraphedDPStep:
 
     def _capture_opt(self):
         """G_opt = widen / mix + the fused optimizer.  Sharded: one graph PER BUCKET in
-        GradBucketer.opt_order (replicated tail, then the sharded buckets in forward
-        order), so a replay issues bucket i's weight all-gather right after its own
-        update -- the first layers' gathers run beside the deep buckets' updates instead
-        of after all of them.  (self.g_opts: [(graph, bucket or None)])"""
+        GradBucketer.opt_order (the sharded buckets in the order their reduce-scatters
+        complete, then the replicated tail), so a replay waits for each bucket's own
+        collective right before its update: the deep buckets update while the last
+        bucket's reduce-scatter is still in flight.  (self.g_opts: [(graph, bucket or None)])"""
         self.g_opts = []
         order = self.bk.opt_order() if (self.bk.shard and isinstance(self.optimizer, _FlatOptimizer)) else None
 
@@ -384,7 +384,7 @@ class GraphedDPStep:
         self.x.copy_(x, non_blocking=True)
         self.y.copy_(y, non_blocking=True)
         self._sync_lr()
-        works = []
+        works = {}
         for j, g in enumerate(self.graphs):
             if self.waits[j]:
                 self.bk.wait_gathers(self.waits[j])   # this link's first reads of those buckets' weights
@@ -394,21 +394,27 @@ class GraphedDPStep:
             if issue and not self.device_collectives and self.comm_fn is None:
                 torch.cuda.current_stream().synchronize()  # a host-staged backend reads the buffers
             for i in issue:
-                works.append(self._collective(i))
-        for w in works:
-            if w is not None:
-                w.wait()
+                works[i] = self._collective(i)
         self.bk.wait_gathers()   # (any gather no forward link waited for) before the optimizer writes
         host_staged = not self.device_collectives and self.comm_fn is None
+        # each optimizer graph waits only for ITS bucket's collective (a stream wait): the deep
+        # buckets, reduced first, update while the last bucket's reduce-scatter is still on
+        # the wire; the weight all-gathers then go out in forward order
         for g, i in self.g_opts:
+            for k in (list(works) if i is None else [i]):
+                w = works.pop(k, None)
+                if w is not None:
+                    w.wait()
             g.replay()
-            if i is not None:   # bucket i's updated bf16 weight shard -> its all-gather (forward order)
-                self.bk.master_whole = False
-                if host_staged:
-                    torch.cuda.current_stream().synchronize()   # a host-staged backend reads the shadow
-                self.bk.issue_gather(i)
+        for w in works.values():   # (buckets without an optimizer graph of their own)
+            if w is not None:
+                w.wait()
         if self.bk.shard:
             self.bk.master_whole = False
+            if any(i is not None for _, i in self.g_opts):
+                if host_staged:
+                    torch.cuda.current_stream().synchronize()   # a host-staged backend reads the shadow
+                self.bk.issue_gathers()
         return self.loss
 
     def _eager_step(self, x, y):

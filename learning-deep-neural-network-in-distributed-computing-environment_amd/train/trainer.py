@@ -94,7 +94,7 @@ def train_local_epoch(model, trainloader, criterion, optimizer, device, schedule
     # mean over all ranks' samples -- what one process on the concatenated batch computes
     # (static-engine twin: StaticMLPEngine.dp_tail_step).
     weigh_last = (dp is not None and dp.comm.world_size > 1 and step_aggregator is None
-                  and not getattr(dp.bucketer, "weighted", False))
+                  and getattr(dp.bucketer, "averaging", False))
 
     def weight_of(n):
         cnt = torch.tensor([float(n)], dtype=torch.float32, device=dev)
@@ -158,14 +158,22 @@ def train_local_epoch(model, trainloader, criterion, optimizer, device, schedule
             x, y = nxt if nxt is not None else last
             n = y.numel() if nxt is not None else 0
             scale = weight_of(n)
-            optimizer.zero_grad()
-            out = model(x)
-            st = stats if n else torch.zeros_like(stats)   # a zero-weight step adds no statistics
-            loss = criterion(out, y, st) if ldnn_ce else criterion(out.float(), y)
-            if n and not ldnn_ce:
-                with torch.no_grad():
-                    stats[1] += (out.argmax(1) == y).sum()
-            (loss * scale).backward()
+            if n:
+                optimizer.zero_grad()
+                out = model(x)
+                loss = criterion(out, y, stats) if ldnn_ce else criterion(out.float(), y)
+                if not ldnn_ce:
+                    with torch.no_grad():
+                        stats[1] += (out.argmax(1) == y).sum()
+                (loss * scale).backward()
+            else:
+                # shard exhausted: a zero-weight step that only joins the collectives -- no
+                # forward (BatchNorm running statistics would see a duplicate batch) and no
+                # loss * 0 backward (a non-finite loss would put NaN into every rank's sum)
+                optimizer.zero_grad(set_to_none=False)
+                dp.flat.zero_grad(lazy=False)
+                dp.wait_gathers()
+                dp.bucketer.prepare()
             dp.finish_gradient_sync()
             optimizer.step()
             if n:
@@ -301,7 +309,8 @@ def train_global(model, trainloader, val_loader, trainset, valset, indices_train
                             average_buffers)
     step_aggregator = None
     if sync_every == "step" and dp is None:
-        # per-step decentralised SGD: gossip (or all-reduce) the gradients every step
+        # per-step decentralised SGD without a DataParallel wrapper (CPU / legacy_gossip
+        # runs): gossip (or all-reduce) the whole gradient every step, eagerly
         step_aggregator = Aggregator(topology, aggregation_type, "gradients", local_weight, comm, legacy_gossip)
     cutoff = StragglerCutoff(comm, timelimit, check_every, dev)
 

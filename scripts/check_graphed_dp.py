@@ -45,6 +45,9 @@ def main():
                     help="DataParallel(shard_optimizer=True): reduce-scatter + sharded optimizer + weight all-gather")
     ap.add_argument("--optimizer", choices=["sgd", "adam"], default="sgd")
     ap.add_argument("--comm-dtype", choices=["fp32", "bf16"], default="fp32")
+    ap.add_argument("--gossip", type=int, default=0,
+                    help="1 / 2: per-step ring / double-ring gossip (DataParallel(gossip=...)): the graphed chain "
+                         "must give the parameters of the eager bucketed gossip step (replicas differ by design)")
     a = ap.parse_args()
     ctx = D.setup(a.backend)
     N, r, dev = ctx.world_size, ctx.rank, ctx.device
@@ -57,13 +60,14 @@ def main():
     xs.append(xs[0][: N * (B // 2)])
     ys.append(ys[0][: N * (B // 2)])
 
-    def run(world, rank, comm):
+    def run(world, rank, comm, graphs=True):
         torch.manual_seed(0)
         m = build_model(a.model)
         xavier_init(m)
         ldnn.prepare(m, dev)
         cd = torch.bfloat16 if a.comm_dtype == "bf16" else None
-        dp = (DataParallel(m, comm, bucket_cap_mb=0.05, shard_optimizer=a.shard, comm_dtype=cd)
+        dp = (DataParallel(m, comm, bucket_cap_mb=0.05, shard_optimizer=a.shard, comm_dtype=cd, gossip=a.gossip,
+                           local_weight=0.7 if a.gossip == 2 else None)
               if comm is not None else None)
         # (built after the wrapper: sharding re-lays the flat buffers out)
         opt = SGD(m.parameters(), lr=0.02, momentum=0.9) if a.optimizer == "sgd" else Adam(m.parameters(), lr=1e-3)
@@ -72,7 +76,8 @@ def main():
             b = x.shape[0] // world
             batches.append((x[rank * b:(rank + 1) * b].to(dev).bfloat16(), y[rank * b:(rank + 1) * b].to(dev)))
         net = dp if dp is not None else m
-        loss, acc, bl = train_local_epoch(net, ListLoader(batches), CrossEntropyLoss(), opt, dev, graphs=True, dp=dp)
+        loss, acc, bl = train_local_epoch(net, ListLoader(batches), CrossEntropyLoss(), opt, dev, graphs=graphs,
+                                          dp=dp)
         if dp is not None:
             if a.shard:
                 assert dp.sharded and any(b["sharded"] for b in dp.bucketer.buckets)
@@ -84,6 +89,22 @@ def main():
     got = torch.cat([p.detach().flatten().cpu() for p in m.parameters()])
     print(f"rank {r}: batch losses {[round(v, 4) for v in bl]}", flush=True)
     ok = True
+    if a.gossip:
+        me, _ = run(N, r, TorchComm(), graphs=False)
+        ref = torch.cat([p.detach().flatten().cpu() for p in me.parameters()])
+        torch.manual_seed(0)
+        m0 = build_model(a.model)
+        xavier_init(m0)
+        p0 = torch.cat([p.detach().flatten() for p in m0.parameters()])
+        du, dr = (got - p0).double(), (ref - p0).double()
+        err = (du - dr).norm().item() / max(dr.norm().item(), 1e-12)
+        print(f"rank {r}: gossip graphed vs eager relative update difference {err:.3e}", flush=True)
+        t = torch.tensor([1.0 if err < 1e-2 else 0.0])
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        if r == 0 and t.item() == 1.0:
+            print("GRAPHED_DP_OK", flush=True)
+        D.teardown(ctx)
+        return
     if a.oneshot:
         c1 = TorchComm()
         os_ = c1.enable_oneshot(4 << 20, device=dev)

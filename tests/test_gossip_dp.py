@@ -1,0 +1,118 @@
+"""Per-step ring / double-ring gossip on the DataParallel path (parallel/ddp.py
+GradBucketer(gossip=...)): bucketed grouped send/recv + one fused combine per bucket,
+the same formulas as parallel.aggregation.gossip_mix (BR/communication.py:5-62,
+BDR/communication.py:5-77) -- checked step by step on FakeWorld (several buckets, the
+2-rank double ring whose 2-hop neighbour is the rank itself) and on 3 gloo processes."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import ldnn
+from ldnn.models import CrossEntropyLoss, build_model, xavier_init
+from ldnn.optim import SGD
+from ldnn.parallel.aggregation import gossip_mix
+from ldnn.parallel.comm import FakeWorld
+from ldnn.parallel.ddp import DataParallel
+
+torch.manual_seed(0)
+_M = build_model("lenet5")
+xavier_init(_M)
+INIT = _M.state_dict()
+
+
+def _run(comm, hops, lw, steps=3):
+    """Train with DataParallel(gossip) and, beside it, a replica that computes the same
+    step with the reference formula on the whole flat gradient (gossip_mix)."""
+    m, ref = build_model("lenet5"), build_model("lenet5")
+    m.load_state_dict(INIT)
+    ref.load_state_dict(INIT)
+    ldnn.prepare(m, "cpu")
+    ldnn.prepare(ref, "cpu")
+    dp = DataParallel(m, comm, bucket_cap_mb=0.05, gossip=hops, local_weight=lw)
+    assert len(dp.bucketer.buckets) >= 3 and dp.flat.grad_scale == 1.0 and not dp.bucketer.averaging
+    opt = SGD(m.parameters(), lr=0.1, momentum=0.9)
+    ropt = SGD(ref.parameters(), lr=0.1, momentum=0.9)
+    crit = CrossEntropyLoss()
+    g = torch.Generator().manual_seed(5 + comm.rank)
+    errs = []
+    for _ in range(steps):
+        x = torch.randn(4, 1, 28, 28, generator=g)
+        y = torch.randint(0, 10, (4,), generator=g)
+        opt.zero_grad()
+        crit(dp(x), y).backward()
+        dp.finish_gradient_sync()
+        opt.step()
+        ropt.zero_grad()
+        crit(ref(x), y).backward()
+        rf = ref._ldnn_flat
+        rf.finalize_grads()
+        gossip_mix(rf.grad, comm, hops, lw is not None, 0.5 if lw is None else lw)
+        ropt.step()
+        errs.append((m._ldnn_flat.master - rf.master).abs().max().item())
+    return errs
+
+
+@pytest.mark.parametrize("N,hops,lw", [(3, 1, None), (3, 1, 0.7), (4, 2, None), (3, 2, 0.6), (2, 2, None)])
+def test_bucketed_gossip_equals_reference_formula(N, hops, lw):
+    res = FakeWorld(N).run(_run, hops, lw)
+    for errs in res:
+        assert max(errs) < 1e-6, res
+
+
+def _replicas_differ(comm):
+    m = build_model("lenet5")
+    m.load_state_dict(INIT)
+    ldnn.prepare(m, "cpu")
+    dp = DataParallel(m, comm, bucket_cap_mb=0.05, gossip=1)
+    opt = SGD(m.parameters(), lr=0.1)
+    g = torch.Generator().manual_seed(comm.rank)
+    opt.zero_grad()
+    CrossEntropyLoss()(dp(torch.randn(4, 1, 28, 28, generator=g)), torch.randint(0, 10, (4,), generator=g)).backward()
+    dp.finish_gradient_sync()
+    opt.step()
+    return m._ldnn_flat.master.clone()
+
+
+def test_gossip_replicas_drift_apart_unlike_allreduce():
+    """Gossip mixes only neighbours: after one step the replicas differ (an all-reduce
+    would keep them identical)."""
+    a, b, c = FakeWorld(3).run(_replicas_differ)
+    assert (a - b).abs().max() > 1e-6 and (b - c).abs().max() > 1e-6
+
+
+def test_gossip_refuses_sharding_and_bf16_stage():
+    with pytest.raises(ValueError):
+        FakeWorld(2).run(lambda comm: DataParallel(build_model("lenet5"), comm, gossip=1, shard_optimizer=True))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _gloo_worker(rank, world, port, q, hops, lw):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from ldnn.parallel.comm import TorchComm
+
+    try:
+        q.put((rank, _run(TorchComm(), hops, lw)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("hops,lw", [(1, None), (2, 0.6)])
+def test_gossip_three_gloo_ranks_step_by_step(hops, lw):
+    world = 3
+    q = mp.get_context("spawn").Queue()
+    mp.spawn(_gloo_worker, args=(world, _port(), q, hops, lw), nprocs=world, join=True)
+    res = [q.get(timeout=60) for _ in range(world)]
+    for r, errs in res:
+        assert max(errs) < 1e-6, res

@@ -145,3 +145,31 @@ def test_cli_sharded_per_step_dp_two_ranks(tmp_path):
     assert ck, list(tmp_path.iterdir())
     sd = torch.load(ck[-1], weights_only=True)
     assert "features.0.weight" in sd["model"] and sd["global_epoch"] == 2
+
+
+def _two_groups(comm):
+    m = build_model("lenet5")
+    m.load_state_dict(INIT["lenet5"])
+    ldnn.prepare(m, "cpu")
+    dp = DataParallel(m, comm, bucket_cap_mb=0.05, shard_optimizer=True)
+    ps = list(m.parameters())
+    opt = SGD([{"params": ps[:2]}, {"params": ps[2:]}], lr=0.05)
+    x = torch.randn(4, *SHAPES["lenet5"])
+    y = torch.randint(0, 10, (4,))
+    CrossEntropyLoss()(dp(x), y).backward()
+    dp.finish_gradient_sync()
+    try:
+        opt.step()
+    except RuntimeError as e:
+        return str(e)
+    return "no error"
+
+
+def test_sharded_refuses_an_optimizer_that_cannot_update_by_shards():
+    """A sharded DataParallel holds reduced values only in this rank's shard of flat.grad and
+    relies on the optimizer to start the weight all-gathers: an optimizer whose param groups
+    do not map onto the one flat buffer must raise, not fall back to a full-replica update
+    (which would silently diverge the replicas)."""
+    res = FakeWorld(2).run(_two_groups)
+    for r in res:
+        assert "shard_optimizer=True" in r and "param group" in r, res
