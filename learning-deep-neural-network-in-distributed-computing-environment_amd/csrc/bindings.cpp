@@ -1548,6 +1548,10 @@ PYBIND11_MODULE(_C, m) {
         "halo-staged 3x3 stride-1 conv: 0 off, 1 default (dgrad + 256x64 fwd tiles), 2 every eligible shape",
         py::arg("mode"));
   m.def("get_conv_halo", &ldnn::get_conv_halo);
+  m.def("set_conv_hb", &ldnn::set_conv_hb,
+        "big-tile (256x128, 8-wave) halo 3x3 stride-1 conv for 128-multiple output channels: 0 off, 1 on (default)",
+        py::arg("mode"));
+  m.def("get_conv_hb", &ldnn::get_conv_hb);
   m.def("set_conv_ws", &ldnn::set_conv_ws,
         "weight-stationary 64 -> 64 channel 3x3 stride-1 conv (fwd without bias, dgrad): 0 off, 1 on (default)",
         py::arg("mode"));

@@ -141,6 +141,8 @@ int get_conv_impl();
 void set_conv_stem_s2d(int mode);   // 0: split-K stem wgrad, 1: space-to-depth stem wgrad (default)
 void set_conv_wgrad_ring(int mode);  // 0: split-K wgrad everywhere, 1: the ring wgrad for 3x3 stride-1 convs
 void set_conv_halo(int mode);
+void set_conv_hb(int mode);
+int get_conv_hb();
 // weight-stationary 64 -> 64 channel 3x3 conv: 0 off, 1 on (default)
 void set_conv_ws(int mode);  // see conv_lds.hip ws_env
 int get_conv_ws();

@@ -1042,6 +1042,187 @@ __global__ __launch_bounds__(256, 2) void conv_halo_kernel(LArgs a, const bf16_t
   }
 }
 
+// ---- big-tile halo conv: 3x3 stride-1 pad-1 fwd / dgrad, 256 x 128 tiles, 8 waves ----------
+// The 128x128 gather kernel above moves 32 KiB through the LDS-DMA path per 2.1 MFLOP K-tile and
+// runs at 18.5-19 % MFMA busy on ResNet-18's 128..512-channel stages (fill-bound: its per-CU
+// LDS-DMA rate, not the MFMA pipe, sets the K-tile time, profiles/r3/conv_fill_knockout_r3.txt).
+// Here one 8-wave workgroup per CU owns a 256-row x 128-column tile and cuts the bytes per MAC
+// three ways: (a) the activation operand is a HALO -- the BM + 2W + 2 flattened pixels a tile's 9
+// taps read, one 64-channel block of them, DMA'd ONCE per channel block (not once per tap) into
+// rows of 160 B (8 data + 2 pad slots: a tap shift is a plain address offset and no shift
+// conflicts, the conv_ws64_kernel layout); (b) the tile is 2x the gather kernel's, so each weight
+// K-tile (16 KiB, the only per-K-tile stream left) feeds 4.2 MFLOP; (c) the weight stream runs 2
+// K-tiles ahead in a 3-stage LDS ring and the next channel block's halo fills a second halo
+// buffer during the current block's taps (counted vmcnt waits, raw barriers: nothing drains the
+// DMA queue inside the loop).  Per K-tile ~20.5 KiB for 4.2 MFLOP against 32 KiB for 2.1.
+// Waves: 4 row strips x 2 column halves, 64 x 64 each (the gather kernel's fragment map and
+// MFMA order, so the shared epilogue / split-K / BN-statistics tail applies unchanged).  K-tile
+// order: channel blocks, taps fastest (r-major); a split-K slice holds whole channel blocks.
+// fwd: rows = output pixels, tap (r, s) reads x at (p + r - 1, q + s - 1); dgrad: rows = input
+// pixels, tap (r, s) reads dy at (h + 1 - r, w + 1 - s).  W <= 32.
+namespace hb {
+constexpr int kBM = 256, kBN = 128, kNW = 8, kNT = 512;
+constexpr int kPitch = 160;                   // halo row pitch: 8 data chunks + 2 zero pad slots
+constexpr int kSlots = kPitch / 16;
+constexpr int kMaxW = 32;                     // 2W + 2 rounded up to 8 <= 72 halo rows past the tile
+constexpr int kHaloBytes = ((kBM + 72) * kPitch + 1023) / 1024 * 1024;   // 52 KiB (whole 1-KiB DMA pieces)
+constexpr int kNSB = 3;                       // weight ring: K-tiles kt+1, kt+2 in flight
+constexpr int kBBytes = kBN * 128;
+constexpr int kLds = 2 * kHaloBytes + kNSB * kBBytes + 128;
+static_assert(kLds <= 160 * 1024, "LDS");
+}  // namespace hb
+
+// s_waitcnt vmcnt(n) for a wave-uniform n (a scalar branch to the immediate)
+__device__ __forceinline__ void wait_vm_n(int n) {
+  switch (n) {
+    case 0: wait_vm<0>(); break;
+    case 1: wait_vm<1>(); break;
+    case 2: wait_vm<2>(); break;
+    case 3: wait_vm<3>(); break;
+    case 4: wait_vm<4>(); break;
+    case 5: wait_vm<5>(); break;
+    case 6: wait_vm<6>(); break;
+    case 7: wait_vm<7>(); break;
+    case 8: wait_vm<8>(); break;
+    case 9: wait_vm<9>(); break;
+    case 10: wait_vm<10>(); break;
+    case 11: wait_vm<11>(); break;
+    default: wait_vm<0>(); break;
+  }
+}
+
+template <class OB, int EPI, bool DGRAD>
+__global__ __launch_bounds__(512, 1) void conv_hb_kernel(LArgs a, const bf16_t* pa, uint32_t bytes_a,
+                                                         const bf16_t* pb, uint32_t bytes_b) {
+  using namespace hb;
+  constexpr int NW = kNW, WM = 4, WN = 2, BM = kBM, BN = kBN;
+  constexpr int PPB = OB::kPieces;
+  static_assert(OB::kRows == BN && PPB * NW * 8 == BN, "weight policy geometry");
+  __shared__ __attribute__((aligned(1024))) char smem[kLds];
+  char* const bst = smem + 2 * kHaloBytes;
+  char* const zrow = bst + kNSB * kBBytes;  // 128 zero bytes: the A fragment of a tap outside the image
+
+  const Geo g = make_geo(a, DGRAD);
+  const int tiles_m = (g.M + BM - 1) / BM, tiles_n = (a.N + BN - 1) / BN;
+  const int bx = blockIdx.x, by = blockIdx.y;
+  if (bx >= tiles_m * tiles_n) return;
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+  int m0, n0;
+  tile_coords(g.M, a.N, BM, BN, m0, n0);
+  const int kt0 = by * a.nk_split;  // a multiple of 9: slices hold whole channel blocks
+  const int nk = max(0, min(g.nk - kt0, a.nk_split));
+
+  floatx4 acc[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[j][i] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  if (nk > 0) {
+    const int W = g.rows_w, P = g.rows_h;
+    const int cin = DGRAD ? a.s.K : a.s.C;             // channels of the A tensor
+    const int hrows = BM + ((2 * W + 2 + 7) & ~7);     // halo rows of this shape
+    const int npieces = (hrows * kSlots + 63) / 64;    // 1-KiB DMA pieces per halo
+    const int hp = (npieces - wid + NW - 1) / NW;      // ... issued by this wave
+    const int hbase = m0 - (W + 1);                    // flattened pixel of halo row 0
+    const int cb0 = kt0 / 9, nblk = nk / 9;
+    // per row tile: this lane's halo row offset at tap shift 0, and its image-edge flags
+    int rowoff[4], edge[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = wm * 64 + i * 16 + (lane & 15);
+      const int m = m0 + r;
+      const int t = fdiv(m, g.f_rw), q = m - t * W, n = fdiv(t, g.f_rh), p = t - n * P;
+      rowoff[i] = (r + W + 1) * kPitch + (lane >> 4) * 16;
+      edge[i] = (p == 0 ? 1 : 0) | (p == P - 1 ? 2 : 0) | (q == 0 ? 4 : 0) | (q == W - 1 ? 8 : 0) | (m >= g.M ? 16 : 0);
+    }
+    if (threadIdx.x < 8) *reinterpret_cast<floatx4*>(zrow + threadIdx.x * 16) = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    Rsrc ra, rb;
+    ra.r = __builtin_amdgcn_make_buffer_rsrc((void*)pa, (short)0, (int)bytes_a, 0x00020000);
+    rb.r = __builtin_amdgcn_make_buffer_rsrc((void*)pb, (short)0, (int)bytes_b, 0x00020000);
+    OB ob;
+    ob.init(a, g, n0, wid, lane, kt0);
+    KS ks = ks_init(a, g, kt0);  // K-tile whose weights are issued next
+
+    // halo of channel block cb into buffer buf: lane-linear 16-B slots of kPitch-B rows (slots
+    // 8, 9 of a row are padding and read as zeros, like rows outside the tensor)
+    auto load_halo = [&](int cb, int buf) {
+      char* const dst = smem + buf * kHaloBytes;
+      for (int pc = wid; pc < npieces; pc += NW) {
+        const int slot = pc * 64 + lane;
+        const int j = slot / kSlots, c = slot - j * kSlots;
+        const int gp = hbase + j;
+        const int o = gp >= 0 && c < 8 ? (int)(((unsigned)gp * (unsigned)cin + (unsigned)(cb * 64 + c * 8)) * 2u)
+                                       : (int)kOOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(ra.r, (lds_void*)(dst + pc * 1024), 16, o, 0, 0, 0);
+      }
+    };
+
+    // prologue: the first block's halo, weights of K-tiles 0 and 1
+    load_halo(cb0, 0);
+    LDNN_DMA_TILE(ob, PPB, rb, bst, ks);
+    if (nk > 1) {
+      ks_next(a, g, ks);
+      ob.advance(a);
+      LDNN_DMA_TILE(ob, PPB, rb, bst + kBBytes, ks);
+      wait_vm<PPB>();  // halo + weights(0) landed (loads retire in order)
+    } else {
+      wait_vm<0>();
+    }
+    lds_barrier();
+
+    int kt = 0;
+    for (int blk = 0; blk < nblk; ++blk) {
+      const char* const hbuf = smem + (blk & 1) * kHaloBytes;
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap, ++kt) {
+        if (kt > 0) {
+          // weights(kt) landed: what may stay in flight is what was issued after them --
+          // weights(kt+1), and at taps 1 / 2 the next block's halo (issued at tap 0 after
+          // weights(kt+2)); from tap 3 on that halo has to have landed too (it is read 6+ K-tiles later)
+          const bool halo_after = (tap == 1 || tap == 2) && blk + 1 < nblk;
+          wait_vm_n((kt + 1 < nk ? PPB : 0) + (halo_after ? hp : 0));
+          lds_barrier();  // publishes weights(kt); every wave is done with K-tile kt-1
+        }
+        if (kt + 2 < nk) {  // weights(kt+2) into the stage K-tile kt-1 used
+          ks_next(a, g, ks);
+          ob.advance(a);
+          LDNN_DMA_TILE(ob, PPB, rb, bst + ((kt + 2) % kNSB) * kBBytes, ks);
+        }
+        if (tap == 0 && blk + 1 < nblk) load_halo(cb0 + blk + 1, (blk + 1) & 1);  // its buffer's last reader was K-tile kt-1
+        const int dr = DGRAD ? 1 - tap / 3 : tap / 3 - 1, ds = DGRAD ? 1 - tap % 3 : tap % 3 - 1;
+        const int emask = 16 | (dr < 0 ? 1 : 0) | (dr > 0 ? 2 : 0) | (ds < 0 ? 4 : 0) | (ds > 0 ? 8 : 0);
+        const int toff = (dr * W + ds) * kPitch;
+        const char* lb = bst + (kt % kNSB) * kBBytes;
+        __builtin_amdgcn_s_setprio(1);
+        bf16x8 fa[2][4], fb[2][4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const char* src = (edge[i] & emask) != 0 ? zrow + (lane >> 4) * 16 : hbuf + rowoff[i] + toff;
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk) fa[kk][i] = *reinterpret_cast<const bf16x8*>(src + kk * 64);
+        }
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) fb[kk][j] = read_frag<OB::KC, BN>(lb, wn * 4 + j, kk, lane);
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+              acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[kk][j], fa[kk][i], acc[j][i], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+      }
+    }
+  }
+  conv_tail<WM, WN, EPI, false, DGRAD>(a, g, acc, m0, n0, wm, wn, lane, smem, hb::kLds / 4, bx, by);
+}
+
 // ---- weight-stationary persistent halo conv: 64 -> 64 channels, 3x3 stride 1 pad 1 ----
 // conv_halo_kernel above streams the 8-KiB weight tile of every filter tap through a 2-stage
 // LDS ring, and each tap waits for a DMA issued one tap earlier: at ResNet-18 layer 1 (C64 H56
@@ -2351,6 +2532,51 @@ hipError_t launch_halo(LArgs a, int epi, int splits, const bf16_t* pa, size_t ba
   return hipGetLastError();
 }
 
+// Big-tile halo path (conv_hb_kernel) for 3x3 stride-1 pad-1 fwd / dgrad with 64-multiple input
+// and 128-multiple output channels, W <= 32 (ResNet-18 layers 2-4, EnhancedCNN's stages).
+// LDNN_CONV_HB (A/B knob): 0 off; 1 (default) dgrad grids of >= 96 tiles; 2 fwd too; 3 every
+// eligible shape.  Measured (scripts/conv_micro.py, profiles/r5/conv_hb_micro.jsonl): the dgrad
+// wins at ResNet-18 b256 (C128 H28 108 -> 102 us, C256 H14 100 -> 93, C512 H7 104 -> 94) and
+// b64 C128 H28 (28.6 -> 26.5); the fwd loses to the gather kernel (C128 H28 b256 79 -> 94 us) and
+// the small split-K grids (EnhancedCNN b64) lose both ways.
+int g_conv_hb = -2;  // -2: not read yet
+int hb_env() {
+  if (g_conv_hb == -2) g_conv_hb = env_int("LDNN_CONV_HB", 1);
+  return g_conv_hb;
+}
+bool hb_takes(const ConvShape& s, bool dgrad) {
+  const int m = hb_env();
+  const int cin = dgrad ? s.K : s.C, cout = dgrad ? s.C : s.K;
+  if (m == 0 || (m == 1 && !dgrad)) return false;
+  if (!(s.R == 3 && s.S == 3 && s.stride == 1 && s.pad == 1 && s.P == s.H && s.Q == s.W && s.W <= hb::kMaxW &&
+        cin % 64 == 0 && cout % 128 == 0))
+    return false;
+  const int64_t tiles = ((int64_t)s.N * s.H * s.W + hb::kBM - 1) / hb::kBM * (cout / hb::kBN);
+  return m == 3 || tiles >= 96;
+}
+
+template <class OB, bool DGRAD>
+hipError_t launch_hb(LArgs a, int epi, int splits, const bf16_t* pa, size_t ba, const bf16_t* pb, size_t bb,
+                     hipStream_t st) {
+  a.tap_major = 1;  // taps fastest inside a channel block: one halo per block
+  dim3 grid(a.tiles_x, splits, 1), block(hb::kNT);
+#define LDNN_CONV_HB(E) conv_hb_kernel<OB, E, DGRAD><<<grid, block, 0, st>>>(a, pa, (uint32_t)ba, pb, (uint32_t)bb)
+  switch (epi) {
+    case EPI_NONE: LDNN_CONV_HB(EPI_NONE); break;
+    case EPI_BIAS:
+      if constexpr (DGRAD) return hipErrorInvalidValue;
+      else LDNN_CONV_HB(EPI_BIAS);
+      break;
+    case EPI_BIAS_RELU:
+      if constexpr (DGRAD) return hipErrorInvalidValue;
+      else LDNN_CONV_HB(EPI_BIAS_RELU);
+      break;
+    default: return hipErrorInvalidValue;
+  }
+#undef LDNN_CONV_HB
+  return hipGetLastError();
+}
+
 // LDNN_CONV_SLAB=0: small-M fwd / dgrad use the in-launch combine (A/B knob)
 bool slab_env_off() {
   static const bool v = [] {
@@ -2447,12 +2673,37 @@ Plan plan_dgrad(const ConvShape& s) {
   return p;
 }
 
+// conv_hb_kernel: 256 x 128 tiles (4 x 2 waves); a split-K slice holds whole channel blocks.
+// Split only grids below ~3/4 of a workgroup per CU, to ~one workgroup per CU.
+Plan plan_hb(const ConvShape& s, bool dgrad) {
+  Plan p{};
+  p.wm = 4;
+  p.wn = 2;
+  p.classes = 1;
+  const int cin = dgrad ? s.K : s.C, cout = dgrad ? s.C : s.K;
+  p.M = s.N * s.H * s.W;
+  p.N = cout;
+  p.tiles_x = ((p.M + hb::kBM - 1) / hb::kBM) * (cout / hb::kBN);
+  const int nblk = cin / 64;
+  p.nk_all = 9 * nblk;
+  static const int target = env_int("LDNN_CONV_HB_TARGET", 256);  // workgroups to aim for (A/B knob)
+  int sp = 1;
+  if (p.tiles_x < 192) sp = std::min(nblk, std::max(1, (target + p.tiles_x - 1) / p.tiles_x));
+  const int bps = (nblk + sp - 1) / sp;  // channel blocks per slice
+  p.nk_split = 9 * bps;
+  p.splits = (nblk + bps - 1) / bps;
+  p.slab = p.splits > 1 && p.tiles_x < 48 && !slab_env_off();
+  return p;
+}
+
+constexpr int kSlabBytes8 = 16 * 512 * 16;  // one 8-wave workgroup's fp32 accumulators
+
 ConvWorkspace ws_of(const Plan& p) {
   ConvWorkspace w{};
   if (p.splits > 1 && p.slab) {
     w.slab_bytes = (size_t)p.splits * p.M * p.N * 4;
   } else if (p.splits > 1) {
-    w.slab_bytes = (size_t)p.tiles_x * p.classes * p.splits * kSlabBytes4;
+    w.slab_bytes = (size_t)p.tiles_x * p.classes * p.splits * (p.wm * p.wn == 8 ? kSlabBytes8 : kSlabBytes4);
     w.counters = p.tiles_x * p.classes;
   }
   return w;
@@ -2463,6 +2714,8 @@ ConvWorkspace ws_of(const Plan& p) {
 using namespace convlds;
 
 void set_conv_halo(int mode) { g_conv_halo = mode; }
+void set_conv_hb(int mode) { g_conv_hb = mode; }
+int get_conv_hb() { return hb_env(); }
 void set_conv_ws(int mode) { g_conv_ws = mode; }
 int get_conv_ws() { return ws_env(); }
 void set_conv_trace(uint64_t* buf) { g_conv_trace = buf; }
@@ -2507,8 +2760,8 @@ ConvWorkspace conv2d_lds_workspace(const ConvShape& s, int op) {
     w.slab_bytes = (p.slab_floats + p.tmp_floats + p.xs_floats) * 4;
     return w;
   }
-  if (op == 0 && s.C % 64 == 0) return ws_of(plan_fwd(s));
-  if (op == 1 && s.K % 64 == 0) return ws_of(plan_dgrad(s));
+  if (op == 0 && s.C % 64 == 0) return ws_of(hb_takes(s, false) ? plan_hb(s, false) : plan_fwd(s));
+  if (op == 1 && s.K % 64 == 0) return ws_of(hb_takes(s, true) ? plan_hb(s, true) : plan_dgrad(s));
   if (op == 2 && s.C % 8 == 0 && s.K % 8 == 0) {
     const WgradPlan p = plan_wgrad(s);
     ConvWorkspace w{};
@@ -2621,7 +2874,8 @@ hipError_t conv2d_fwd_lds(const ConvShape& s, const uint16_t* x, const uint16_t*
   }
   if (s.C % 64 != 0) return hipErrorNotSupported;
   if (s.N * s.P * s.Q <= 0) return bn != nullptr ? hipErrorNotSupported : hipSuccess;
-  Plan pl = plan_fwd(s);
+  const bool hbp = hb_takes(s, false);
+  Plan pl = hbp ? plan_hb(s, false) : plan_fwd(s);
   LArgs a = base_args(s);
   if (bn != nullptr && pl.slab) {  // slab split-K: the next BN runs its own statistics pass
     bn = nullptr;
@@ -2658,7 +2912,9 @@ hipError_t conv2d_fwd_lds(const ConvShape& s, const uint16_t* x, const uint16_t*
     return launch_ws64<false>(a, x, bx, w, st);
   }
   hipError_t e;
-  if (halo_takes(s, pl.wm)) {
+  if (hbp) {
+    e = launch_hb<WeightKC<128, 2, 8>, false>(a, epi, pl.splits, x, bx, w, bw, st);
+  } else if (halo_takes(s, pl.wm)) {
     // fwd: the halo wins on the 256x64 tiles of 64-filter layers (C64 H56: 53.7 -> 35-37 us) and
     // loses on 128x128 ones (C128 H28 25.8 -> 27.7, C512 H7 34.9 -> 40.0 us; double-buffered too)
     if (pl.wm == 4) e = launch_halo<4, 1, WeightKC<64, 2, 4>, false>(a, epi, pl.splits, x, bx, w, bw, st);
@@ -2676,7 +2932,8 @@ hipError_t conv2d_dgrad_lds(const ConvShape& s, const uint16_t* dy, const uint16
                             float* ws, int* cnt) {
   if (s.K % 64 != 0 || !shape_ok(s)) return hipErrorNotSupported;
   if (s.N * s.H * s.W <= 0) return hipSuccess;
-  Plan pl = plan_dgrad(s);
+  const bool hbp = hb_takes(s, true);
+  Plan pl = hbp ? plan_hb(s, true) : plan_dgrad(s);
   LArgs a = base_args(s);
   a.out = dx;
   a.M = s.N * s.H * s.W;
@@ -2705,7 +2962,9 @@ hipError_t conv2d_dgrad_lds(const ConvShape& s, const uint16_t* dy, const uint16
     return launch_ws64<true>(a, dy, bdy, w, st);
   }
   hipError_t e;
-  if (halo_takes(s, pl.wm)) {
+  if (hbp) {
+    e = launch_hb<DgradB<128, 2, 8>, true>(a, EPI_NONE, pl.splits, dy, bdy, w, bw, st);
+  } else if (halo_takes(s, pl.wm)) {
     // dgrad likewise: C64 H56 38.9 -> 36.5 us; single-buffered on 128x128 tiles neutral to 1 us
     // slower (ResNet-18 C128-C512), up to 2.6 us slower on the EnhancedCNN 16x16 .. 2x2 stages
     if (pl.wm == 4) e = launch_halo<4, 1, DgradB<64, 2, 4>, true>(a, EPI_NONE, pl.splits, dy, bdy, w, bw, st);

@@ -38,15 +38,47 @@ class _Join:
 
 class StandInComm:
     """``comm_fn`` for GraphedDPStep: ``reps`` copies of bucket i on ``blocks``
-    workgroups (native standin_copy kernel), on a side stream."""
+    workgroups (native standin_copy kernel), on a side stream.  ``blocks`` = 0:
+    calibrate -- the fewest workgroups whose single copy moves bytes at least at
+    ``gbps`` (the xGMI bus bandwidth the stand-in impersonates, see calibrate())."""
 
-    def __init__(self, device, reps: int = 4, blocks: int = 16):
+    def __init__(self, device, reps: int = 4, blocks: int = 16, gbps: float = 300.0):
         from ..ops import _ext
 
+        import os
+
         self.C = _ext.C()
-        self.side = torch.cuda.Stream(device=device)
+        # (a high-priority stream, as RCCL's with utils.distributed.setup: LDNN_RCCL_HIGH_PRIO)
+        self.priority = -1 if os.environ.get("LDNN_RCCL_HIGH_PRIO", "1") != "0" else 0
+        self.side = torch.cuda.Stream(device=device, priority=self.priority)
         self.reps, self.blocks = int(reps), int(blocks)
         self.scratch: dict = {}
+        self.calibration = None
+        if self.blocks <= 0:
+            self.calibrate(device, gbps)
+
+    def calibrate(self, device, gbps: float, mb: int = 32):
+        """Pick ``blocks`` (reps = 1) so the stand-in moves a buffer at >= ``gbps`` GB/s: an
+        8-GPU RCCL reduce-scatter / all-gather of S bytes moves (N-1)/N S per rank, at
+        roughly 300 GB/s bus bandwidth over MI355X xGMI (7 links x ~150 GB/s, ring
+        channels); the stand-in is handed exactly those moved bytes."""
+        src = torch.empty(mb << 18, dtype=torch.float32, device=device)
+        dst = torch.empty_like(src)
+        rates = {}
+        for b in (4, 8, 12, 16, 24, 32, 48, 64, 96, 128):
+            self.C.standin_copy(src, dst, b, 1)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(5):
+                self.C.standin_copy(src, dst, b, 1)
+            torch.cuda.synchronize()
+            rates[b] = src.numel() * 4 * 5 / (time.perf_counter() - t0) / 1e9
+            if rates[b] >= gbps:
+                break
+        self.blocks = next((b for b, r in rates.items() if r >= gbps), max(rates))
+        self.reps = 1
+        self.calibration = {"target_gbps": gbps, "blocks": self.blocks,
+                            "gbps": round(rates[self.blocks], 1), "stream_priority": self.priority}
 
     def __call__(self, i, buf):
         self.side.wait_stream(torch.cuda.current_stream())
@@ -68,12 +100,12 @@ class ShardProbeComm:
 
     device_collectives = True
 
-    def __init__(self, device, world: int = 8, reps: int = 4, blocks: int = 16):
+    def __init__(self, device, world: int = 8, reps: int = 4, blocks: int = 16, gbps: float = 300.0):
         from .comm import Comm
 
         self._rec = Comm()
         self.rank, self.world_size = 0, int(world)
-        self.standin = StandInComm(device, reps, blocks)
+        self.standin = StandInComm(device, reps, blocks, gbps)
         self._k = 0
         self.enabled = True   # False: every collective is a no-op (the chain's own cost)
 
@@ -118,14 +150,14 @@ def _timed(fn, steps):
 
 def measure_overlap(model_name: str, batch: int, bucket_mb: float = 32.0, reps: int = 4, steps: int = 20,
                     rounds: int = 3, blocks: int = 16, shard_world: int = 0, optimizer: str = "sgd",
-                    tail_steps: int = 0) -> dict:
+                    tail_steps: int = 0, gbps: float = 300.0) -> dict:
     """shard_world > 0: the sharded step (reduce-scatter between backward links, sharded
     optimizer, bf16 weight all-gathers waited by the forward links) on a
     ShardProbeComm of that world size; the stand-ins then cover the reduce-scatter
     AND the all-gather bytes of each bucket."""
     if shard_world:
         return _measure_sharded(model_name, batch, bucket_mb, reps, steps, rounds, blocks, shard_world, optimizer,
-                                tail_steps)
+                                tail_steps, gbps)
     import ldnn
     from ldnn.data.datasets import SHAPES
     from ldnn.models import CrossEntropyLoss, build_model, dataset_for, xavier_init
@@ -141,7 +173,7 @@ def measure_overlap(model_name: str, batch: int, bucket_mb: float = 32.0, reps: 
     x = torch.randn(batch, *shape, device=dev, generator=g).bfloat16()
     y = torch.randint(0, nc, (batch,), device=dev, generator=g)
     crit = CrossEntropyLoss()
-    standin = StandInComm(dev, reps, blocks)
+    standin = StandInComm(dev, reps, blocks, gbps)
     steps_fn = {}
     for name, fn in (("single", lambda i, buf: None), ("with_standin", standin)):
         torch.manual_seed(0)
@@ -176,7 +208,8 @@ def measure_overlap(model_name: str, batch: int, bucket_mb: float = 32.0, reps: 
     _tail(fns["with_standin_ms"], tail_steps)
     return {"model": model_name, "batch": batch, "bucket_mb": bucket_mb, "buckets": len(bufs),
             "bucket_mb_each": [round(b.numel() * b.element_size() / 2**20, 2) for b in bufs],
-            "segments": gd.n_segments, "standin_reps": reps, "standin_blocks": blocks, **{k: round(v, 4) for k, v in best.items()},
+            "segments": gd.n_segments, "standin_reps": standin.reps, "standin_blocks": standin.blocks,
+            "standin_calibration": standin.calibration, **{k: round(v, 4) for k, v in best.items()},
             "hidden_ms": round(hidden, 4),
             "hidden_fraction": round(hidden / max(best["standin_alone_ms"], 1e-9), 3)}
 
@@ -193,7 +226,14 @@ def _tail(fn, n):
     torch.cuda.synchronize()
 
 
-def _measure_sharded(model_name, batch, bucket_mb, reps, steps, rounds, blocks, world, optimizer, tail_steps=0):
+def _opt_order():
+    from . import ddp
+
+    return ddp._OPT_ORDER
+
+
+def _measure_sharded(model_name, batch, bucket_mb, reps, steps, rounds, blocks, world, optimizer, tail_steps=0,
+                     gbps=300.0):
     import ldnn
     from ldnn.data.datasets import SHAPES
     from ldnn.models import CrossEntropyLoss, build_model, dataset_for, xavier_init
@@ -227,7 +267,7 @@ def _measure_sharded(model_name, batch, bucket_mb, reps, steps, rounds, blocks, 
     m = build_model(model_name)
     xavier_init(m)
     ldnn.prepare(m, dev)
-    comm = ShardProbeComm(dev, world, reps, blocks)
+    comm = ShardProbeComm(dev, world, reps, blocks, gbps)
     dp = DataParallel(m, comm, bucket_cap_mb=bucket_mb, broadcast_init=False, shard_optimizer=True)
     o = opt_for(m)
     o.zero_grad()
@@ -272,14 +312,17 @@ def _measure_sharded(model_name, batch, bucket_mb, reps, steps, rounds, blocks, 
             "bucket_mb": bucket_mb, "buckets": len(bk.buckets),
             "sharded_buckets": sum(1 for b in bk.buckets if b["sharded"]),
             "bucket_mb_each": [round((b["end"] - b["begin"]) * 4 / 2**20, 2) for b in bk.buckets],
-            "segments": gd.n_segments, "forward_waits": sum(1 for w in gd.waits if w), "standin_reps": reps,
-            "standin_blocks": blocks, **{k: round(v, 4) for k, v in best.items()}, "hidden_ms": round(hidden, 4),
+            "segments": gd.n_segments, "forward_waits": sum(1 for w in gd.waits if w),
+            "standin_reps": comm.standin.reps, "standin_blocks": comm.standin.blocks,
+            "standin_calibration": comm.standin.calibration, "opt_order": _opt_order(),
+            **{k: round(v, 4) for k, v in best.items()}, "hidden_ms": round(hidden, 4),
+            "exposed_ms": round(best["with_standin_ms"] - best["single_ms"], 4),
             "hidden_fraction": round(hidden / max(best["standin_alone_ms"], 1e-9), 3)}
 
 
 def measure_mlp_sharded(world: int = 8, batch: int = 16384, hidden: int = 4096, in_features: int = 784,
-                        classes: int = 10, bucket_elems: int = 8 << 20, reps: int = 4, blocks: int = 16,
-                        steps: int = 20, rounds: int = 3, tail_steps: int = 0) -> dict:
+                        classes: int = 10, bucket_elems: int = 8 << 20, reps: int = 1, blocks: int = 0,
+                        steps: int = 20, rounds: int = 3, tail_steps: int = 0, gbps: float = 300.0) -> dict:
     """The headline engine's sharded data-parallel step (train/static_mlp.py
     StaticMLPEngine at world ``world``, rank 0: bench.py's mlp3 784-4096-4096-10 at
     16384 samples per GPU, SGD momentum) on ONE GPU, every reduce-scatter / all-gather
@@ -324,7 +367,7 @@ def measure_mlp_sharded(world: int = 8, batch: int = 16384, hidden: int = 4096, 
 
     single = engine(1)
     eng = engine(world)
-    standin = StandInComm(dev, reps, blocks)
+    standin = StandInComm(dev, reps, blocks, gbps)
     state = {"on": True}
 
     def moved(t):
@@ -369,7 +412,7 @@ def measure_mlp_sharded(world: int = 8, batch: int = 16384, hidden: int = 4096, 
     best = {k: 1e9 for k in fns}
     for _ in range(rounds):
         for k, f in fns.items():
-            best[k] = min(best[k], _timed(lambda: (f(), eng.sync()) if f in (chain_only, overlapped) else f(), steps))
+            best[k] = min(best[k], _timed(f, steps))   # (device-wide sync at both ends)
     exposed = best["with_standin_ms"] - best["chain_ms"]
     hid = best["standin_alone_ms"] - exposed
     _tail(overlapped, tail_steps)
@@ -377,7 +420,8 @@ def measure_mlp_sharded(world: int = 8, batch: int = 16384, hidden: int = 4096, 
     return {"model": f"mlp3 {in_features}-{hidden}-{hidden}-{classes}", "batch": batch,
             "mode": f"static engine, sharded (world {world} stand-in)", "optimizer": "sgd momentum 0.9",
             "buckets": len(eng.buckets), "bucket_mb_fp32": [round((e_ - b) * 4 / 2**20, 2) for b, e_, _ in eng.buckets],
-            "segments": len(eng.segments), "standin_reps": reps, "standin_blocks": blocks,
+            "segments": len(eng.segments), "standin_reps": standin.reps, "standin_blocks": standin.blocks,
+            "standin_calibration": standin.calibration,
             **{k: round(v, 4) for k, v in best.items()}, "exposed_ms": round(exposed, 4),
             "exposed_fraction_of_step": round(exposed / max(best["chain_ms"], 1e-9), 4),
             "hidden_ms": round(hid, 4), "hidden_fraction": round(hid / max(best["standin_alone_ms"], 1e-9), 3)}
@@ -388,9 +432,12 @@ def main():
     ap.add_argument("--model", default="resnet18")
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--bucket-mb", type=float, default=32.0)
-    ap.add_argument("--reps", type=int, default=4)
+    ap.add_argument("--reps", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--blocks", type=int, default=16)
+    ap.add_argument("--blocks", type=int, default=0,
+                    help="stand-in workgroups; 0 = calibrate to --gbps (reps 1)")
+    ap.add_argument("--gbps", type=float, default=300.0,
+                    help="xGMI bus bandwidth the calibrated stand-in moves a collective's bytes at")
     ap.add_argument("--shard", type=int, default=0, help="world size of the sharded-step probe (0 = all-reduce step)")
     ap.add_argument("--optimizer", choices=["sgd", "adam"], default="sgd")
     ap.add_argument("--rounds", type=int, default=3)
@@ -400,10 +447,11 @@ def main():
     if a.model == "mlp3":   # the headline engine (StaticMLPEngine), sharded at world --shard (default 8)
         print(json.dumps(measure_mlp_sharded(a.shard or 8, a.batch if a.batch != 64 else 16384, reps=a.reps,
                                              blocks=a.blocks, steps=a.steps, rounds=a.rounds,
-                                             tail_steps=a.tail_steps)), flush=True)
+                                             tail_steps=a.tail_steps, gbps=a.gbps)), flush=True)
         return
     print(json.dumps(measure_overlap(a.model, a.batch, a.bucket_mb, a.reps, a.steps, rounds=a.rounds, blocks=a.blocks,
-                                     shard_world=a.shard, optimizer=a.optimizer, tail_steps=a.tail_steps)), flush=True)
+                                     shard_world=a.shard, optimizer=a.optimizer, tail_steps=a.tail_steps,
+                                     gbps=a.gbps)), flush=True)
 
 
 if __name__ == "__main__":

@@ -102,6 +102,14 @@ def setup(backend: str | None = None, timeout_s: float = 600.0, device: str | No
         kw = dict(backend=backend, timeout=datetime.timedelta(seconds=timeout_s))
         if backend == "nccl":
             kw["device_id"] = dev
+            # RCCL's kernels on a HIGH-priority stream: the compute stream's GEMM / conv grids
+            # fill every CU, and a freed CU then goes to the collective's waiting workgroups
+            # first instead of the next compute tile (without it a bucket's reduce-scatter
+            # waits for the whole overlapping GEMM: profiles/r5/overlap_probe.jsonl)
+            if os.environ.get("LDNN_RCCL_HIGH_PRIO", "1") != "0":
+                opts = dist.ProcessGroupNCCL.Options()
+                opts.is_high_priority_stream = True
+                kw["pg_options"] = opts
         dist.init_process_group(**kw)
         ctx.initialized_here = True
     if dist.is_initialized():

@@ -21,7 +21,7 @@ for step in "$@"; do
     iso) $T 300 python -u scripts/debug/stem_isolation.py > $O/stem_isolation.jsonl 2>&1 ;;
     det:*) a=${step#det:}; $T 300 python -u scripts/debug/determinism_probe.py --model ${a%%@*} --hw ${a##*@} >> $O/determinism.jsonl 2>&1 ;;
     probe:*) IFS=@ read -r m b sh reps opt <<< "${step#probe:}"
-             $T 300 python -u scripts/overlap_probe.py --model $m --batch $b --shard ${sh:-0} --reps ${reps:-4} \
+             $T 300 python -u scripts/overlap_probe.py --model $m --batch $b --shard ${sh:-0} --reps ${reps:-1} \
                --optimizer ${opt:-sgd} ${PROBE_ARGS:-} >> $O/overlap_probe.jsonl 2>> $O/overlap_probe.err ;;
     probetrace:*) IFS=@ read -r m b sh reps opt <<< "${step#probetrace:}"
              (cd /tmp && export TMPDIR=/tmp && cd - > /dev/null

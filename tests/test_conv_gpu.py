@@ -307,3 +307,81 @@ def test_stem_s2d_wgrad_matches_fp32_and_split_k(N, Cin, H, W):
         torch.testing.assert_close(dw, ref, rtol=1e-3, atol=1e-3 * scale)
         torch.testing.assert_close(dacc, ref, rtol=1e-3, atol=2e-3 * scale)
     assert (outs[1][0][..., 4:] == 0).all()
+
+
+@pytest.mark.parametrize("N,C,H,W,K", [(2, 128, 28, 28, 128), (8, 128, 31, 31, 128), (64, 128, 16, 16, 128),
+                                       (16, 256, 14, 14, 256), (4, 512, 7, 7, 512), (4, 1024, 2, 2, 1024),
+                                       (5, 384, 9, 9, 128), (64, 256, 8, 8, 256), (64, 128, 28, 28, 128),
+                                       (3, 128, 14, 14, 256), (2, 256, 12, 12, 128), (2, 128, 33, 33, 128)])
+def test_big_tile_halo_conv_matches_gather_and_fp32(N, C, H, W, K):
+    """The 8-wave 256x128 halo kernel (conv_hb_kernel: one halo per channel block, the next
+    block's halo and 2 weight K-tiles in flight) == the per-tap gather kernel (set_conv_hb 0,
+    set_conv_halo 0) and == fp32 for fwd (plain and bias+ReLU) and dgrad, unsplit, in-launch
+    split-K combine and slab split-K grids, ragged last tiles and W = 31 (33: past the halo
+    limit, the gather kernel runs either way)."""
+    torch.manual_seed(17)
+    Cc = _ext.C()
+    x = torch.randn(N, H, W, C, device="cuda").bfloat16()
+    w = (torch.randn(K, 3, 3, C, device="cuda") * (1.0 / (C * 9) ** 0.5)).bfloat16()
+    gy = torch.randn(N, H, W, K, device="cuda").bfloat16()
+    bias = torch.randn(K, device="cuda")
+    outs = {}
+    halo0 = Cc.get_conv_halo()
+    try:
+        Cc.set_conv_halo(0)
+        for mode in (0, 3, 3):   # 3: every eligible shape (the default, 1, takes large dgrad grids only)
+            Cc.set_conv_hb(mode)
+            y = torch.full((N, H, W, K), 7.0, device="cuda", dtype=torch.bfloat16)
+            Cc.conv_fwd(x, w, y, 1, 1)
+            yb = torch.full((N, H, W, K), 7.0, device="cuda", dtype=torch.bfloat16)
+            Cc.conv_fwd(x, w, yb, 1, 1, bias, Cc.EPI_BIAS_RELU)
+            dx = torch.full((N, H, W, C), 7.0, device="cuda", dtype=torch.bfloat16)
+            Cc.conv_dgrad(gy, w, dx, 1, 1)
+            outs.setdefault(mode, []).append((y.float(), yb.float(), dx.float()))
+    finally:
+        Cc.set_conv_hb(1)
+        Cc.set_conv_halo(halo0)
+    ref = outs[0][0]
+    outs[1] = outs[3]
+    for a, b in zip(outs[1][0], outs[1][1]):   # repeated launches (split-K counters reset): same bits
+        assert torch.equal(a, b)
+    for a, b in zip(outs[1][0], ref):
+        torch.testing.assert_close(a, b, rtol=1e-2, atol=1e-2 * b.abs().max().item())
+    xf, wf, gyf = x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), gy.float().permute(0, 3, 1, 2)
+    yr = torch.nn.functional.conv2d(xf, wf, padding=1).permute(0, 2, 3, 1)
+    dxr = torch.nn.grad.conv2d_input(xf.shape, wf, gyf, padding=1).permute(0, 2, 3, 1)
+    y1, yb1, dx1 = outs[1][0]
+    torch.testing.assert_close(y1, yr, rtol=1e-2, atol=1e-2 * yr.abs().max().item())
+    torch.testing.assert_close(yb1, torch.relu(yr + bias), rtol=1e-2, atol=1e-2 * yr.abs().max().item())
+    torch.testing.assert_close(dx1, dxr, rtol=1e-2, atol=1e-2 * dxr.abs().max().item())
+
+
+@pytest.mark.parametrize("N,C,H,W", [(64, 128, 28, 28), (64, 128, 16, 16), (8, 256, 14, 14)])
+def test_big_tile_halo_conv_fused_bn_statistics(N, C, H, W):
+    """The next BatchNorm's statistics accumulated in the conv_hb_kernel epilogue (unsplit and
+    in-launch split-K grids) == those of the output it stores, as the gather kernel's do."""
+    torch.manual_seed(19)
+    Cc = _ext.C()
+    x = torch.randn(N, H, W, C, device="cuda").bfloat16()
+    w = (torch.randn(C, 3, 3, C, device="cuda") * (1.0 / (C * 9) ** 0.5)).bfloat16()
+    res = {}
+    try:
+        for m in (0, 3):
+            Cc.set_conv_hb(m)
+            y = torch.full((N, H, W, C), 7.0, device="cuda", dtype=torch.bfloat16)
+            ws = torch.zeros(Cc.bn_workspace_floats(C), device="cuda")
+            sm, si = torch.zeros(C, device="cuda"), torch.zeros(C, device="cuda")
+            rm, rv = torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")
+            used = Cc.conv_fwd(x, w, y, 1, 1, bn_ws=ws, bn_running_mean=rm, bn_running_var=rv, bn_save_mean=sm,
+                               bn_save_invstd=si)
+            if not used:   # (a slab split-K grid: the BN runs its own statistics pass)
+                pytest.skip("fused statistics not taken on this grid")
+            res[m] = (y.float(), sm, si, rm, rv)
+    finally:
+        Cc.set_conv_hb(1)
+    res[1] = res[3]
+    yb = res[1][0].reshape(-1, C)
+    torch.testing.assert_close(res[1][1], yb.mean(0), rtol=1e-3, atol=1e-4)
+    torch.testing.assert_close(res[1][2], torch.rsqrt(yb.var(0, unbiased=False) + 1e-5), rtol=1e-3, atol=1e-4)
+    for a, b in zip(res[1][1:], res[0][1:]):
+        torch.testing.assert_close(a, b, rtol=1e-3, atol=1e-4)
