@@ -30,6 +30,38 @@ constexpr int kBnCopies = 8;  // accumulator copies of the BN statistics (conv e
 // that inline this occupancy.)
 __device__ __forceinline__ void bn_acc_add(float* p, float v) { atomicAdd(p, v); }
 
+// Channel c's totals (forward: sum x, sum x^2; backward: sum g, sum g * xhat) -> saved
+// statistics, running-stat EMA and apply coefficients (forward), or the backward
+// coefficients and dgamma / dbeta.
+template <bool BWD>
+__device__ __forceinline__ void bn_finalize_channel(const BnFin& f, int M, int C, int c, float S0, float S1,
+                                                    float invM) {
+  const float gm = f.gamma ? f.gamma[c] : 1.f;
+  if constexpr (!BWD) {
+    const float m = S0 * invM;
+    const float var = fmaxf(S1 * invM - m * m, 0.f);
+    const float is = rsqrtf(var + f.eps);
+    f.save_mean[c] = m;
+    f.save_invstd[c] = is;
+    const float b = f.beta ? f.beta[c] : 0.f;
+    f.coef[c] = gm * is;
+    f.coef[C + c] = b - m * gm * is;
+    if (f.running_mean) {
+      f.running_mean[c] = (1.f - f.momentum) * f.running_mean[c] + f.momentum * m;
+      const float unb = M > 1 ? var * (float)M / (float)(M - 1) : var;
+      f.running_var[c] = (1.f - f.momentum) * f.running_var[c] + f.momentum * unb;
+    }
+  } else {
+    const float is = f.save_invstd[c];
+    const float A = gm * is, B = -gm * is * is * S1 * invM;
+    f.coef[c] = A;
+    f.coef[C + c] = B;
+    f.coef[2 * C + c] = -gm * is * S0 * invM - B * f.save_mean[c];
+    if (f.dgamma) f.dgamma[c] = f.grad_assign ? S1 : f.dgamma[c] + S1;
+    if (f.dbeta) f.dbeta[c] = f.grad_assign ? S0 : f.dbeta[c] + S0;
+  }
+}
+
 template <bool BWD, int NCOP>
 __device__ __forceinline__ void bn_finalize_last(const BnFin& f, int M, int C, int nblk, float* tot, int cap,
                                                  int ncop = NCOP) {
@@ -91,30 +123,7 @@ __device__ __forceinline__ void bn_finalize_last(const BnFin& f, int M, int C, i
         S1 += atomicExch(f.acc + (size_t)k * 2 * C + C + c, 0.f);
       }
     }
-    const float gm = f.gamma ? f.gamma[c] : 1.f;
-    if constexpr (!BWD) {
-      const float m = S0 * invM;
-      const float var = fmaxf(S1 * invM - m * m, 0.f);
-      const float is = rsqrtf(var + f.eps);
-      f.save_mean[c] = m;
-      f.save_invstd[c] = is;
-      const float b = f.beta ? f.beta[c] : 0.f;
-      f.coef[c] = gm * is;
-      f.coef[C + c] = b - m * gm * is;
-      if (f.running_mean) {
-        f.running_mean[c] = (1.f - f.momentum) * f.running_mean[c] + f.momentum * m;
-        const float unb = M > 1 ? var * (float)M / (float)(M - 1) : var;
-        f.running_var[c] = (1.f - f.momentum) * f.running_var[c] + f.momentum * unb;
-      }
-    } else {
-      const float is = f.save_invstd[c];
-      const float A = gm * is, B = -gm * is * is * S1 * invM;
-      f.coef[c] = A;
-      f.coef[C + c] = B;
-      f.coef[2 * C + c] = -gm * is * S0 * invM - B * f.save_mean[c];
-      if (f.dgamma) f.dgamma[c] = f.grad_assign ? S1 : f.dgamma[c] + S1;
-      if (f.dbeta) f.dbeta[c] = f.grad_assign ? S0 : f.dbeta[c] + S0;
-    }
+    bn_finalize_channel<BWD>(f, M, C, c, S0, S1, invM);
   }
   if (!BWD && threadIdx.x == 0 && f.num_batches) f.num_batches[0] += 1;
 }

@@ -194,6 +194,67 @@ __global__ __launch_bounds__(256) void bn_reduce_kernel(const bf16_t* __restrict
   bn_finalize_last<BWD, kBnCopies>(fin, M, C, gridDim.x * gridDim.y, &red[0][0], 2 * 8 * 512, ncop);
 }
 
+// Small-M statistics (the 4x4 / 2x2 stages of EnhancedCNN at batch 64: M = 1024 / 256 rows):
+// the reduce above is a chain of dependent round trips there -- block partials, fp32 atomics,
+// a ticket, then the last block's exchange-and-finalize -- ~11-15 us for a 0.5-2 MB tensor
+// (profiles/r5/pmc_enhanced_cnn_b64_mem.txt).  Here ONE workgroup per 64-channel group reads
+// every row of its channels (8 row-parallel loads in flight per thread) and finalizes them
+// itself: no accumulator, no atomics, no ticket.
+template <bool BWD, bool RELU, bool MASK = false>
+__global__ __launch_bounds__(256) void bn_reduce_small_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
+                                                              const bf16_t* __restrict__ y, const float* __restrict__ mean,
+                                                              const float* __restrict__ invstd, int M, int C, BnFin fin,
+                                                              const uint8_t* __restrict__ mask,
+                                                              const bf16_t* __restrict__ dy2 = nullptr) {
+  constexpr int kLanes = 8, kRl = 32, kJs = 256 + kLanes;
+  __shared__ float red[2][8 * kJs];
+  const int tid = threadIdx.x, lane = tid % kLanes, rlane = tid / kLanes;
+  const int c0 = blockIdx.x * 64 + lane * 8;
+  const bool active = c0 < C;
+  float s0[8], s1[8], mu[8], is[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    s0[j] = 0.f;
+    s1[j] = 0.f;
+    mu[j] = 0.f;
+    is[j] = 0.f;
+  }
+  if (active) {
+    if constexpr (BWD) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        mu[j] = mean[c0 + j];
+        is[j] = invstd[c0 + j];
+      }
+    }
+    int r = rlane;
+    for (; r + 7 * kRl < M; r += 8 * kRl) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        red_row<BWD, RELU, MASK>(x, dy, y, (size_t)(r + u * kRl) * C + c0, mu, is, s0, s1, mask, dy2);
+    }
+    for (; r < M; r += kRl) red_row<BWD, RELU, MASK>(x, dy, y, (size_t)r * C + c0, mu, is, s0, s1, mask, dy2);
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    red[0][j * kJs + tid] = s0[j];
+    red[1][j * kJs + tid] = s1[j];
+  }
+  __syncthreads();
+  if (tid < 64) {
+    const int j = tid / kLanes, ln = tid - j * kLanes;   // channel ln * 8 + j of this group
+    float t0 = 0.f, t1 = 0.f;
+#pragma unroll 8
+    for (int q = 0; q < kRl; ++q) {
+      t0 += red[0][j * kJs + q * kLanes + ln];
+      t1 += red[1][j * kJs + q * kLanes + ln];
+    }
+    const int c = blockIdx.x * 64 + ln * 8 + j;
+    if (c < C) bn_finalize_channel<BWD>(fin, M, C, c, t0, t1, 1.f / (float)M);
+  }
+  if (!BWD && blockIdx.x == 0 && tid == 0 && fin.num_batches) fin.num_batches[0] += 1;
+}
+
 __global__ void bn_eval_coeff_kernel(const float* __restrict__ gamma, const float* __restrict__ beta,
                                      const float* __restrict__ rm, const float* __restrict__ rv,
                                      float* __restrict__ scale, float* __restrict__ shift, int C, float eps) {
@@ -926,12 +987,24 @@ hipError_t bn_forward_apply(const BnArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+// the small-M reduce (bn_reduce_small_kernel) below this many rows; LDNN_BN_SMALL_ROWS (A/B
+// knob, 0 = off)
+int bn_small_rows() {
+  static const int v = env_int_or("LDNN_BN_SMALL_ROWS", 2048);
+  return v;
+}
+
 // the statistics half of the forward: batch statistics (training) or the running ones (eval)
 // -> scale / shift in a.ws
 static void bn_forward_stats(const BnArgs& a, hipStream_t s) {
   const int M = a.M, C = a.C;
   const RedGeo g = red_geo(M, C, true);
   const dim3 grid(g.gx, g.gy);
+  if (a.training && M <= bn_small_rows()) {
+    bn_reduce_small_kernel<false, false><<<(C + 63) / 64, 256, 0, s>>>(a.x, nullptr, nullptr, nullptr, nullptr, M, C,
+                                                                       bn_forward_fin(a), nullptr);
+    return;
+  }
   if (a.training) {
     const BnFin f = bn_forward_fin(a);
     bn_reduce_kernel<false, false><<<grid, 256, 0, s>>>(a.x, nullptr, nullptr, nullptr, nullptr, f.acc, M, C, g.rpb,
@@ -1025,7 +1098,18 @@ hipError_t bn_backward(const BnArgs& a, const uint16_t* dy, uint16_t* dx, uint16
   f.dgamma = dgamma;
   f.dbeta = dbeta;
   f.grad_assign = grad_assign ? 1 : 0;
-  if (a.relu && a.mask)
+  const int gs = (C + 63) / 64;
+  if (M <= bn_small_rows()) {
+    if (a.relu && a.mask)
+      bn_reduce_small_kernel<true, true, true><<<gs, 256, 0, s>>>(a.x, dy, nullptr, a.save_mean, a.save_invstd, M, C,
+                                                                  f, a.mask, a.dy2);
+    else if (a.relu)
+      bn_reduce_small_kernel<true, true><<<gs, 256, 0, s>>>(a.x, dy, a.y, a.save_mean, a.save_invstd, M, C, f, nullptr,
+                                                            a.dy2);
+    else
+      bn_reduce_small_kernel<true, false><<<gs, 256, 0, s>>>(a.x, dy, nullptr, a.save_mean, a.save_invstd, M, C, f,
+                                                             nullptr, a.dy2);
+  } else if (a.relu && a.mask)
     bn_reduce_kernel<true, true, true><<<grid_r, 256, 0, s>>>(a.x, dy, nullptr, a.save_mean, a.save_invstd, f.acc, M,
                                                             C, gr.rpb, gr.lanes, gr.rl, f, a.mask,
                                                             bn_ncop(true, gr.gx * gr.gy), a.dy2);

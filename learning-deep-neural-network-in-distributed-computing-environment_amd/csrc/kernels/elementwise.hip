@@ -187,25 +187,49 @@ __global__ __launch_bounds__(256) void nchw_to_nhwc_kernel(const T* __restrict__
   reinterpret_cast<u16x8*>(dst)[i] = o;
 }
 
+// out[c][r] = in[r][c], 64 x 64 tiles.  The tile goes to LDS as whole 128-B rows (16-B chunks
+// XOR-swizzled by row, rows 8 apart shifted by 4 more chunks) and comes back COLUMN-wise through
+// ds_read_b64_tr_b16 (per 16-lane group: 4 rows x 16 columns, lane i receives column i):
+// wave w owns output rows c0 + 16w .. +15 (lane i of each group one of them), group gq the input
+// rows 8gq + 32h .. +7 of pass h, so each lane stores 8 consecutive outputs (16 B) per pass --
+// no 2-byte LDS accesses and no bank conflicts (the element-wise tile was 12.4 extra LDS cycles
+// per instruction, profiles/r5/pmc_mlp3.txt).  Needs a full 256-thread block (EXEC all ones for
+// the transposing read: out-of-range rows / columns are loaded as zeros and not stored).
+__device__ __forceinline__ int tr_sw(int row) { return (row & 7) ^ (((row >> 3) & 1) << 2); }
+
 __global__ __launch_bounds__(256) void transpose_bf16_kernel(const bf16_t* __restrict__ in, bf16_t* __restrict__ out,
                                                              int rows, int cols, int ldi, int ldo) {
-  __shared__ uint16_t t[64][72];
+  typedef __attribute__((address_space(3))) bf16x4 lds_b4;
+  __shared__ __attribute__((aligned(16))) char t[64 * 128];
   const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
-  for (int p = threadIdx.x; p < 512; p += 256) {
-    const int r = p >> 3, c8 = (p & 7) * 8;
-    u16x8 v = {};
-    if (r0 + r < rows && c0 + c8 < cols) v = *reinterpret_cast<const u16x8*>(in + (size_t)(r0 + r) * ldi + c0 + c8);
 #pragma unroll
-    for (int q = 0; q < 8; ++q) t[r][c8 + q] = v[q];
+  for (int it = 0; it < 2; ++it) {
+    const int p = threadIdx.x + it * 256;
+    const int r = p >> 3, ch = p & 7;
+    u16x8 v = {};
+    if (r0 + r < rows && c0 + ch * 8 < cols) v = *reinterpret_cast<const u16x8*>(in + (size_t)(r0 + r) * ldi + c0 + ch * 8);
+    *reinterpret_cast<u16x8*>(t + r * 128 + ((ch ^ tr_sw(r)) << 4)) = v;
   }
   __syncthreads();
-  for (int p = threadIdx.x; p < 512; p += 256) {
-    const int c = p >> 3, r8 = (p & 7) * 8;
-    if (c0 + c < cols && r0 + r8 < rows) {
-      u16x8 o;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int gq = lane >> 4, i = lane & 15, q = i >> 2, pp = i & 3;
+  const int ch = 2 * w + (pp >> 1);  // the 16-B chunk of columns 16w + 4pp .. +3
 #pragma unroll
-      for (int q = 0; q < 8; ++q) o[q] = t[r8 + q][c];
-      *reinterpret_cast<u16x8*>(out + (size_t)(c0 + c) * ldo + r0 + r8) = o;
+  for (int h = 0; h < 2; ++h) {
+    const int rb = 32 * h + 8 * gq;  // input rows rb .. rb + 7 -> this lane's 8 outputs
+    bf16x4 lo, hi;
+    {
+      const int r = rb + q;
+      lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_b4*)(t + r * 128 + ((ch ^ tr_sw(r)) << 4) + (pp & 1) * 8));
+    }
+    {
+      const int r = rb + 4 + q;
+      hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_b4*)(t + r * 128 + ((ch ^ tr_sw(r)) << 4) + (pp & 1) * 8));
+    }
+    const int c = c0 + 16 * w + i;
+    if (c < cols && r0 + rb < rows) {
+      const bf16x8 o = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      *reinterpret_cast<bf16x8*>(out + (size_t)c * ldo + r0 + rb) = o;
     }
   }
 }

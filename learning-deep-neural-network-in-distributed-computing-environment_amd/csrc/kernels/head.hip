@@ -666,12 +666,15 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(HeadParams p, int rows_pe
     }
     // stage every block first (h rows of 128 B, dlogits rows of 32 B): one LDS wait per
     // kHbUnroll blocks instead of two per block
+    // (16-B chunks of an h row XOR-swizzled by row, 8-B slots of a dlogits row by row / 4: the
+    // 16 rows of a store instruction hit distinct banks -- straight 128-B / 32-B rows were an 8-way /
+    // 4-way conflict, 12.3 extra LDS cycles per instruction, profiles/r5/pmc_mlp3.txt)
 #pragma unroll
     for (int u = 0; u < kHbUnroll; ++u) {
       char* sb = st + u * kSt;
-      *reinterpret_cast<u16x8*>(sb + r16 * 128 + g * 16) = hv[u][0];
-      *reinterpret_cast<u16x8*>(sb + r16 * 128 + 64 + g * 16) = hv[u][1];
-      *reinterpret_cast<uint2*>(sb + kH + r16 * 32 + g * 8) = dl[u];
+      *reinterpret_cast<u16x8*>(sb + r16 * 128 + ((g ^ (r16 & 7)) << 4)) = hv[u][0];
+      *reinterpret_cast<u16x8*>(sb + r16 * 128 + (((4 + g) ^ (r16 & 7)) << 4)) = hv[u][1];
+      *reinterpret_cast<uint2*>(sb + kH + r16 * 32 + ((g ^ ((r16 >> 2) & 3)) << 3)) = dl[u];
     }
 #pragma unroll
     for (int u = 0; u < kHbUnroll; ++u) {
@@ -707,11 +710,12 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(HeadParams p, int rows_pe
 #pragma unroll
     for (int u = 0; u < kHbUnroll; ++u) {
       const char* sb = st + u * kSt;
-      const bf16x4 bd = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_b4*)(sb + kH + (4 * g + q) * 32 + pp * 8));
+      const int row = 4 * g + q;  // (row >> 2) == g
+      const bf16x4 bd = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_b4*)(sb + kH + row * 32 + ((pp ^ g) << 3)));
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) {
-        const bf16x4 ah =
-            __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_b4*)(sb + (4 * g + q) * 128 + (16 * nt + 4 * pp) * 2));
+        const bf16x4 ah = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+            (lds_b4*)(sb + row * 128 + (((2 * nt + (pp >> 1)) ^ (row & 7)) << 4) + (pp & 1) * 8));
         acc2[nt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_bit_cast(s16x4, ah),
                                                              __builtin_bit_cast(s16x4, bd), acc2[nt], 0, 0, 0);
       }

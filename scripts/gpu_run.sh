@@ -42,8 +42,8 @@ for step in "$@"; do
                echo "{\"env\": \"$e\"}" >> $O/micro_$m.jsonl
                env $e $T 300 python -u scripts/conv_micro.py --model $m --no-stock >> $O/micro_$m.jsonl 2>> $O/micro.err || { rc=$?; break; }
              done; (exit $rc) ;;
-    ab:*) a=${step#ab:}; rm -f gpurun_out/ab_cnn.jsonl; $T 900 bash scripts/ab_cnn.sh "${a//,/ }" ${AB_ENVS:-X=0} > $O/ab.txt 2>&1
-          rc=$?; cp -f gpurun_out/ab_cnn.jsonl $O/ 2>/dev/null; (exit $rc) ;;
+    ab:*) a=${step#ab:}; rm -f gpurun_out/ab_cnn.jsonl; $T 900 bash scripts/ab_cnn.sh "${a//,/ }" ${AB_ENVS:-X=0} >> $O/ab.txt 2>&1
+          rc=$?; cat gpurun_out/ab_cnn.jsonl >> $O/ab_cnn.jsonl 2>/dev/null; (exit $rc) ;;
     microprof:*) m=${step#microprof:}; (cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
              $T 400 rocprofv3 --kernel-trace --stats -d $O/microprof_$m -o run -- \
              python -u scripts/conv_micro.py --model $m --no-stock --iters 20 > $O/microprof_$m.txt 2>&1) ;;
@@ -53,11 +53,15 @@ for step in "$@"; do
              python -u scripts/conv_micro.py --model $m --no-stock --iters 5 > $O/micropmc_$m.txt 2>&1) ;;
     cnn:*) a=${step#cnn:}; $T 300 python -u scripts/bench_cnn.py --model ${a%%@*} --batch ${a##*@} --graph --no-stock \
              >> $O/cnn.jsonl 2>> $O/cnn.err ;;
-    prof:*) a=${step#prof:}; $T 400 rocprofv3 --kernel-trace --stats -d $O/prof_$a -o run -- \
+    prof:*) a=${step#prof:}; $T 400 rocprofv3 --kernel-trace --stats -d $O/prof_$a -o prof_${a%%@*}_${a##*@} -- \
              python -u scripts/bench_cnn.py --model ${a%%@*} --batch ${a##*@} --graph --no-stock --steps 20 --warmup 5 \
              > $O/prof_$a.txt 2>&1 ;;
-    profmlp) $T 400 rocprofv3 --kernel-trace --stats -d $O/prof_mlp -o run -- python -u bench.py --steps 20 --warmup 5 \
-             > $O/prof_mlp.txt 2>&1 ;;
+    profmlp) $T 400 rocprofv3 --kernel-trace --stats -d $O/prof_mlp -o prof_mlp -- python -u bench.py --steps 20 --warmup 5 \
+             --no-configs > $O/prof_mlp.txt 2>&1 ;;
+    pmc:*) IFS=@ read -r tg m b <<< "${step#pmc:}"
+           if [ "$m" = mlp3 ]; then $T 400 bash scripts/pmc_step.sh $tg python3 bench.py --steps 4 --warmup 3 --no-configs > $O/pmc_$tg.txt 2>&1
+           else $T 400 bash scripts/pmc_step.sh $tg python3 scripts/bench_cnn.py --model $m --batch $b --steps 3 --warmup 2 --no-stock > $O/pmc_$tg.txt 2>&1; fi
+           rc=$?; cp -f gpurun_out/pmc_$tg/table.txt $O/pmc_${tg}_table.txt 2>/dev/null; (exit $rc) ;;
     wsbench) $T 200 python -u scripts/bench_ws64.py >> $O/bench_ws64.jsonl 2>> $O/bench_ws64.err ;;
     wsko) rc=0   # knockout builds of the weight-stationary conv (fwd, b256): XF bits, see conv_ws64_kernel
           for xf in ${WS_XF:-1 2 4 8}; do LDNN_CONV_XF=$xf $T 100 python -u scripts/bench_ws64.py --modes 1 --fwd-only --no-stem \

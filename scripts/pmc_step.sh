@@ -13,5 +13,9 @@ d=gpurun_out/pmc_$tag
 rm -rf $d && mkdir -p $d
 timeout -s KILL 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_WAVES GRBM_GUI_ACTIVE --output-format csv -d $d/p1 -o run -- "${cmd[@]}" > $d/p1.log 2>&1
 timeout -s KILL 120 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE --output-format csv -d $d/p2 -o run -- "${cmd[@]}" > $d/p2.log 2>&1
+if [ -n "$MEM" ]; then   # HBM-side bytes (FETCH_SIZE reads 1/2 of 16-B-per-lane loads: doubled in the table)
+  timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE GRBM_GUI_ACTIVE --output-format csv -d $d/p3 -o run -- "${cmd[@]}" > $d/p3.log 2>&1
+  timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE GRBM_GUI_ACTIVE --output-format csv -d $d/p4 -o run -- "${cmd[@]}" > $d/p4.log 2>&1
+fi
 python3 scripts/pmc_util.py $d > $d/table.txt
 cat $d/table.txt

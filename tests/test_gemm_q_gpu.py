@@ -224,6 +224,11 @@ def test_transpose_and_slab_sum_cols():
     out = torch.empty(776, 520, device="cuda", dtype=torch.bfloat16)
     c.transpose_bf16(x, out)
     assert torch.equal(out, x.t())
+    for r, cc in ((4096, 4096), (64, 64), (8, 1032), (1032, 8)):   # whole / single / ragged tiles
+        x = torch.randn(r, cc, device="cuda").bfloat16()
+        out = torch.empty(cc, r, device="cuda", dtype=torch.bfloat16)
+        c.transpose_bf16(x, out)
+        assert torch.equal(out, x.t()), (r, cc)
     ws = torch.randn(3, 264, 792, device="cuda")
     dst = torch.full((264, 784), float("nan"), device="cuda")
     extra = torch.full((264,), float("nan"), device="cuda")
