@@ -98,7 +98,7 @@ __device__ __forceinline__ void red_row(const bf16_t* __restrict__ x, const bf16
                                         const bf16_t* __restrict__ y, size_t o, const float (&mu)[8],
                                         const float (&is)[8], float (&s0)[8], float (&s1)[8],
                                         const uint8_t* __restrict__ mask = nullptr,
-                                        const bf16_t* __restrict__ dy2 = nullptr) {
+                                        const bf16_t* __restrict__ dy2 = nullptr, float w = 1.f) {
   const u16x8 xv = *reinterpret_cast<const u16x8*>(x + o);
   if constexpr (BWD) {
     const u16x8 gv = *reinterpret_cast<const u16x8*>(dy + o);
@@ -110,7 +110,7 @@ __device__ __forceinline__ void red_row(const bf16_t* __restrict__ x, const bf16
     else if constexpr (RELU) yv = *reinterpret_cast<const u16x8*>(y + o);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      float g = bf2f(gv[j]) + bf2f(g2v[j]);
+      float g = (bf2f(gv[j]) + bf2f(g2v[j])) * w;
       if constexpr (RELU && MASK) g = ((mb >> j) & 1u) ? g : 0.f;
       else if constexpr (RELU) g = bf2f(yv[j]) > 0.f ? g : 0.f;
       s0[j] += g;
@@ -119,7 +119,7 @@ __device__ __forceinline__ void red_row(const bf16_t* __restrict__ x, const bf16
   } else {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const float v = bf2f(xv[j]);
+      const float v = bf2f(xv[j]) * w;
       s0[j] += v;
       s1[j] += v * v;
     }
@@ -200,12 +200,55 @@ __global__ __launch_bounds__(256) void bn_reduce_kernel(const bf16_t* __restrict
 // (profiles/r5/pmc_enhanced_cnn_b64_mem.txt).  Here ONE workgroup per 64-channel group reads
 // every row of its channels (8 row-parallel loads in flight per thread) and finalizes them
 // itself: no accumulator, no atomics, no ticket.
+//
+// Mid-size M (EnhancedCNN 8x8 / 16x16, ResNet-18 7x7 / 14x14 at b64): the same workgroups split
+// the rows too (grid.y = row groups, `rpb` rows each).  Each publishes its 64 channels' partial
+// sums to `part` ([grid.y][2][C]); the LAST of a column's grid.y workgroups (per-column ticket)
+// sums them and finalizes those 64 channels -- a short chain per column, all columns in parallel,
+// instead of the big reduce's fp32 atomics + one block exchanging every channel's copies.
+__device__ __forceinline__ void grp_store(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float grp_load(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// After wave 0 stored this workgroup's partials: true in every thread of the workgroup that
+// draws the column's last ticket (it resets the ticket).  As in bn_finalize_last, no fences: the
+// partials are agent-scope atomic stores (coherent at the memory side), wave 0 waits for their
+// completion before its ticket, and the finalizer reads them with agent-scope atomic loads.
+__device__ __forceinline__ bool grp_ticket(int* ticket, int n, int& flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (threadIdx.x == 0) {
+    const int t = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    flag = t == n - 1;
+    if (flag) __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  return flag;
+}
+// the finalizer's column totals: thread (q = tid / 64, channel tid % 64) sums every 4th row
+// group's partial k into tot[k][q][64]; the caller reads tot after a barrier
+__device__ __forceinline__ void grp_sum(const float* part, int C, int c, int k, int ny, float* tot) {
+  const int q = threadIdx.x >> 6;
+  float v = 0.f;
+  if (c < C)
+    for (int y0 = q; y0 < ny; y0 += 32) {   // 8 loads in flight (atomic loads are not batched for us)
+      float t[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) t[u] = y0 + 4 * u < ny ? grp_load(part + ((size_t)(y0 + 4 * u) * 2 + k) * C + c) : 0.f;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v += t[u];
+    }
+  tot[(k * 4 + q) * 64 + (threadIdx.x & 63)] = v;
+}
+
 template <bool BWD, bool RELU, bool MASK = false>
 __global__ __launch_bounds__(256) void bn_reduce_small_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
                                                               const bf16_t* __restrict__ y, const float* __restrict__ mean,
                                                               const float* __restrict__ invstd, int M, int C, BnFin fin,
                                                               const uint8_t* __restrict__ mask,
-                                                              const bf16_t* __restrict__ dy2 = nullptr) {
+                                                              const bf16_t* __restrict__ dy2, float* __restrict__ part,
+                                                              int* __restrict__ tickets, int rpb) {
   constexpr int kLanes = 8, kRl = 32, kJs = 256 + kLanes;
   __shared__ float red[2][8 * kJs];
   const int tid = threadIdx.x, lane = tid % kLanes, rlane = tid / kLanes;
@@ -227,13 +270,17 @@ __global__ __launch_bounds__(256) void bn_reduce_small_kernel(const bf16_t* __re
         is[j] = invstd[c0 + j];
       }
     }
-    int r = rlane;
-    for (; r + 7 * kRl < M; r += 8 * kRl) {
+    // batches of 8 rows per lane, all loads in flight together; a short batch re-reads the
+    // group's last row with weight 0 instead of a one-row-per-round-trip tail loop
+    const int r_end = min(M, (int)(blockIdx.y + 1) * rpb);
+    for (int r = blockIdx.y * rpb + rlane; r < r_end; r += 8 * kRl) {
 #pragma unroll
-      for (int u = 0; u < 8; ++u)
-        red_row<BWD, RELU, MASK>(x, dy, y, (size_t)(r + u * kRl) * C + c0, mu, is, s0, s1, mask, dy2);
+      for (int u = 0; u < 8; ++u) {
+        const int rr = r + u * kRl;
+        red_row<BWD, RELU, MASK>(x, dy, y, (size_t)min(rr, r_end - 1) * C + c0, mu, is, s0, s1, mask, dy2,
+                                 rr < r_end ? 1.f : 0.f);
+      }
     }
-    for (; r < M; r += kRl) red_row<BWD, RELU, MASK>(x, dy, y, (size_t)r * C + c0, mu, is, s0, s1, mask, dy2);
   }
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -250,9 +297,27 @@ __global__ __launch_bounds__(256) void bn_reduce_small_kernel(const bf16_t* __re
       t1 += red[1][j * kJs + q * kLanes + ln];
     }
     const int c = blockIdx.x * 64 + ln * 8 + j;
-    if (c < C) bn_finalize_channel<BWD>(fin, M, C, c, t0, t1, 1.f / (float)M);
+    if (gridDim.y == 1) {
+      if (c < C) bn_finalize_channel<BWD>(fin, M, C, c, t0, t1, 1.f / (float)M);
+    } else if (c < C) {
+      grp_store(part + (size_t)blockIdx.y * 2 * C + c, t0);
+      grp_store(part + ((size_t)blockIdx.y * 2 + 1) * C + c, t1);
+    }
   }
-  if (!BWD && blockIdx.x == 0 && tid == 0 && fin.num_batches) fin.num_batches[0] += 1;
+  if (!BWD && blockIdx.x == 0 && blockIdx.y == 0 && tid == 0 && fin.num_batches) fin.num_batches[0] += 1;
+  if (gridDim.y == 1) return;
+  __shared__ int last;
+  if (!grp_ticket(tickets + blockIdx.x, gridDim.y, last)) return;
+  float* tot = &red[0][0];
+  const int cc = blockIdx.x * 64 + (tid & 63);
+  grp_sum(part, C, cc, 0, gridDim.y, tot);
+  grp_sum(part, C, cc, 1, gridDim.y, tot);
+  __syncthreads();
+  if (tid < 64 && cc < C) {
+    const float S0 = tot[tid] + tot[64 + tid] + tot[128 + tid] + tot[192 + tid];
+    const float S1 = tot[256 + tid] + tot[320 + tid] + tot[384 + tid] + tot[448 + tid];
+    bn_finalize_channel<BWD>(fin, M, C, cc, S0, S1, 1.f / (float)M);
+  }
 }
 
 __global__ void bn_eval_coeff_kernel(const float* __restrict__ gamma, const float* __restrict__ beta,
@@ -449,6 +514,100 @@ __global__ __launch_bounds__(256) void bn_reduce_dual_kernel(const bf16_t* __res
   bn_finalize_last<true, kBnCopies>(fin1, M, C, nblk, &red[0][0], 3 * 8 * 512, ncop);
   __syncthreads();
   bn_finalize_last<true, kBnCopies>(fin2, M, C, nblk, &red[0][0], 3 * 8 * 512, ncop);
+}
+
+// The same statistics for small M (see bn_reduce_small_kernel): one workgroup per 64-channel
+// group reads all rows and finalizes both BNs' coefficients itself.
+template <bool MASK>
+__global__ __launch_bounds__(256) void bn_reduce_dual_small_kernel(
+    const bf16_t* __restrict__ x, const bf16_t* __restrict__ r, const bf16_t* __restrict__ dy,
+    const bf16_t* __restrict__ dy2, const bf16_t* __restrict__ y, const uint8_t* __restrict__ mask, int M, int C,
+    BnFin fin1, BnFin fin2, float* __restrict__ part1, float* __restrict__ part2, int* __restrict__ tickets, int rpb) {
+  constexpr int kLanes = 8, kRl = 32, kJs = 256 + kLanes;
+  __shared__ float red[3][8 * kJs];
+  const int tid = threadIdx.x, lane = tid % kLanes, rlane = tid / kLanes;
+  const int c0 = blockIdx.x * 64 + lane * 8;
+  float s0[8], s1[8], s2[8], mu1[8], is1[8], mu2[8], is2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    s0[j] = s1[j] = s2[j] = 0.f;
+    mu1[j] = is1[j] = mu2[j] = is2[j] = 0.f;
+  }
+  if (c0 < C) {
+    load8(fin1.save_mean + c0, mu1);
+    load8(fin1.save_invstd + c0, is1);
+    load8(fin2.save_mean + c0, mu2);
+    load8(fin2.save_invstd + c0, is2);
+    const int r_end = min(M, (int)(blockIdx.y + 1) * rpb);
+    for (int r0 = blockIdx.y * rpb + rlane; r0 < r_end; r0 += 4 * kRl)   // batches of 4 rows (see above)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float w = r0 + u * kRl < r_end ? 1.f : 0.f;
+      const size_t o = (size_t)min(r0 + u * kRl, r_end - 1) * C + c0;
+      const u16x8 xv = *reinterpret_cast<const u16x8*>(x + o);
+      const u16x8 rv = *reinterpret_cast<const u16x8*>(r + o);
+      const u16x8 gv = *reinterpret_cast<const u16x8*>(dy + o);
+      u16x8 g2v = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (dy2) g2v = *reinterpret_cast<const u16x8*>(dy2 + o);
+      u16x8 yv;
+      uint32_t mb = 0;
+      if constexpr (MASK) mb = mask[o >> 3];
+      else yv = *reinterpret_cast<const u16x8*>(y + o);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float g = (bf2f(gv[j]) + bf2f(g2v[j])) * w;
+        if constexpr (MASK) g = ((mb >> j) & 1u) ? g : 0.f;
+        else g = bf2f(yv[j]) > 0.f ? g : 0.f;
+        s0[j] += g;
+        s1[j] += g * (bf2f(xv[j]) - mu1[j]) * is1[j];
+        s2[j] += g * (bf2f(rv[j]) - mu2[j]) * is2[j];
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    red[0][j * kJs + tid] = s0[j];
+    red[1][j * kJs + tid] = s1[j];
+    red[2][j * kJs + tid] = s2[j];
+  }
+  __syncthreads();
+  if (tid < 64) {
+    const int j = tid / kLanes, ln = tid - j * kLanes;
+    float t0 = 0.f, t1 = 0.f, t2 = 0.f;
+#pragma unroll 8
+    for (int q = 0; q < kRl; ++q) {
+      t0 += red[0][j * kJs + q * kLanes + ln];
+      t1 += red[1][j * kJs + q * kLanes + ln];
+      t2 += red[2][j * kJs + q * kLanes + ln];
+    }
+    const int c = blockIdx.x * 64 + ln * 8 + j;
+    if (gridDim.y == 1) {
+      if (c < C) {
+        bn_finalize_channel<true>(fin1, M, C, c, t0, t1, 1.f / (float)M);
+        bn_finalize_channel<true>(fin2, M, C, c, t0, t2, 1.f / (float)M);
+      }
+    } else if (c < C) {
+      grp_store(part1 + (size_t)blockIdx.y * 2 * C + c, t0);
+      grp_store(part1 + ((size_t)blockIdx.y * 2 + 1) * C + c, t1);
+      grp_store(part2 + ((size_t)blockIdx.y * 2 + 1) * C + c, t2);
+    }
+  }
+  if (gridDim.y == 1) return;
+  __shared__ int last;
+  if (!grp_ticket(tickets + blockIdx.x, gridDim.y, last)) return;
+  float* tot = &red[0][0];
+  const int cc = blockIdx.x * 64 + (tid & 63);
+  grp_sum(part1, C, cc, 0, gridDim.y, tot);
+  grp_sum(part1, C, cc, 1, gridDim.y, tot);
+  grp_sum(part2, C, cc, 1, gridDim.y, tot + 512);
+  __syncthreads();
+  if (tid < 64 && cc < C) {
+    const float S0 = tot[tid] + tot[64 + tid] + tot[128 + tid] + tot[192 + tid];
+    const float S1 = tot[256 + tid] + tot[320 + tid] + tot[384 + tid] + tot[448 + tid];
+    const float S2 = tot[768 + tid] + tot[832 + tid] + tot[896 + tid] + tot[960 + tid];
+    bn_finalize_channel<true>(fin1, M, C, cc, S0, S1, 1.f / (float)M);
+    bn_finalize_channel<true>(fin2, M, C, cc, S0, S2, 1.f / (float)M);
+  }
 }
 
 // dx = A1 g + B1 x + D1, dr = A2 g + B2 r + D2
@@ -938,9 +1097,17 @@ __global__ void gap_bwd_kernel(const bf16_t* __restrict__ dy, bf16_t* __restrict
 //   [10C + 32, 26C + 32) kBnCopies x [2C] forward accumulators, shared by the BN
 //   reduce and the conv-epilogue statistics path (one BN's statistics come from
 //   exactly one of the two) |
-//   [26C + 32, 42C + 32) kBnCopies x [2C] backward accumulators.
+//   [26C + 32, 42C + 32) kBnCopies x [2C] backward accumulators |
+//   [42C + 32, ...) kGrpMax x [2C] row-group partials of the mid-M reduce (bn_reduce_small_kernel),
+//   then its ceil(C / 64) per-column tickets.
 // Accumulators and tickets are left zero by the finalizing block.
-int bn_workspace_floats(int C) { return 10 * C + 32 + 2 * kBnCopies * 2 * C; }
+constexpr int kGrpMax = 128;   // row groups of the mid-M reduce, at most
+int bn_workspace_floats(int C) { return 42 * C + 32 + kGrpMax * 2 * C + ((C + 63) / 64 + 3) / 4 * 4; }
+
+namespace {
+float* grp_part(const BnArgs& a) { return a.ws + 42 * a.C + 32; }
+int* grp_tickets(const BnArgs& a) { return reinterpret_cast<int*>(a.ws + 42 * a.C + 32 + kGrpMax * 2 * a.C); }
+}  // namespace
 
 BnFin bn_forward_fin(const BnArgs& a) {
   const int C = a.C;
@@ -987,11 +1154,30 @@ hipError_t bn_forward_apply(const BnArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-// the small-M reduce (bn_reduce_small_kernel) below this many rows; LDNN_BN_SMALL_ROWS (A/B
-// knob, 0 = off)
+// the small-M reduce (bn_reduce_small_kernel, one workgroup per 64 channels) below this many
+// rows; LDNN_BN_SMALL_ROWS (A/B knob, 0 = off)
 int bn_small_rows() {
   static const int v = env_int_or("LDNN_BN_SMALL_ROWS", 2048);
   return v;
+}
+// the same kernel with row groups up to this many rows (LDNN_BN_GRP_ROWS, A/B knob; 0 = off),
+// aiming at LDNN_BN_GRP_TARGET workgroups with >= LDNN_BN_GRP_MIN rows each
+struct Grp {
+  int ny, rpb;
+  bool on;
+};
+Grp grp_geo(int M, int C) {
+  static const int rows = env_int_or("LDNN_BN_GRP_ROWS", 65536);
+  static const int target = std::max(1, env_int_or("LDNN_BN_GRP_TARGET", 512));
+  static const int min_rows = std::max(32, env_int_or("LDNN_BN_GRP_MIN", 256));
+  if (M > rows && M > bn_small_rows()) return {0, 0, false};
+  if (M > rows) return {1, M, true};
+  const int G = (C + 63) / 64;
+  int ny = (target + G - 1) / G;
+  ny = std::min(ny, std::max(1, M / min_rows));
+  ny = std::max(1, std::min(ny, kGrpMax));
+  const int rpb = (M + ny - 1) / ny;
+  return {(M + rpb - 1) / rpb, rpb, true};
 }
 
 // the statistics half of the forward: batch statistics (training) or the running ones (eval)
@@ -1000,9 +1186,12 @@ static void bn_forward_stats(const BnArgs& a, hipStream_t s) {
   const int M = a.M, C = a.C;
   const RedGeo g = red_geo(M, C, true);
   const dim3 grid(g.gx, g.gy);
-  if (a.training && M <= bn_small_rows()) {
-    bn_reduce_small_kernel<false, false><<<(C + 63) / 64, 256, 0, s>>>(a.x, nullptr, nullptr, nullptr, nullptr, M, C,
-                                                                       bn_forward_fin(a), nullptr);
+  const Grp gg = grp_geo(M, C);
+  if (a.training && gg.on) {
+    const dim3 gs((C + 63) / 64, gg.ny);
+    bn_reduce_small_kernel<false, false><<<gs, 256, 0, s>>>(a.x, nullptr, nullptr, nullptr, nullptr, M, C,
+                                                            bn_forward_fin(a), nullptr, nullptr, grp_part(a),
+                                                            grp_tickets(a), gg.rpb);
     return;
   }
   if (a.training) {
@@ -1098,17 +1287,20 @@ hipError_t bn_backward(const BnArgs& a, const uint16_t* dy, uint16_t* dx, uint16
   f.dgamma = dgamma;
   f.dbeta = dbeta;
   f.grad_assign = grad_assign ? 1 : 0;
-  const int gs = (C + 63) / 64;
-  if (M <= bn_small_rows()) {
+  const Grp gg = grp_geo(M, C);
+  const dim3 gs((C + 63) / 64, gg.ny);
+  float* part = grp_part(a);
+  int* tk = grp_tickets(a);
+  if (gg.on) {
     if (a.relu && a.mask)
       bn_reduce_small_kernel<true, true, true><<<gs, 256, 0, s>>>(a.x, dy, nullptr, a.save_mean, a.save_invstd, M, C,
-                                                                  f, a.mask, a.dy2);
+                                                                  f, a.mask, a.dy2, part, tk, gg.rpb);
     else if (a.relu)
       bn_reduce_small_kernel<true, true><<<gs, 256, 0, s>>>(a.x, dy, a.y, a.save_mean, a.save_invstd, M, C, f, nullptr,
-                                                            a.dy2);
+                                                            a.dy2, part, tk, gg.rpb);
     else
       bn_reduce_small_kernel<true, false><<<gs, 256, 0, s>>>(a.x, dy, nullptr, a.save_mean, a.save_invstd, M, C, f,
-                                                             nullptr, a.dy2);
+                                                             nullptr, a.dy2, part, tk, gg.rpb);
   } else if (a.relu && a.mask)
     bn_reduce_kernel<true, true, true><<<grid_r, 256, 0, s>>>(a.x, dy, nullptr, a.save_mean, a.save_invstd, f.acc, M,
                                                             C, gr.rpb, gr.lanes, gr.rl, f, a.mask,
@@ -1179,14 +1371,25 @@ hipError_t bn_dual_backward(const BnArgs& a, const BnArgs& b, const uint16_t* dy
   const int ncop = bn_ncop(true, gr.gx * gr.gy);
   const RedGeo g = red_geo(M, C);
   const dim3 grid(g.gx, g.gy);
+  const Grp gg = grp_geo(M, C);
+  const bool small = gg.on;
+  const dim3 gs((C + 63) / 64, gg.ny);
+  if (small && a.mask)
+    bn_reduce_dual_small_kernel<true><<<gs, 256, 0, s>>>(a.x, b.x, dy, a.dy2, nullptr, a.mask, M, C, fa, fb,
+                                                         grp_part(a), grp_part(b), grp_tickets(a), gg.rpb);
+  else if (small)
+    bn_reduce_dual_small_kernel<false><<<gs, 256, 0, s>>>(a.x, b.x, dy, a.dy2, a.y, nullptr, M, C, fa, fb,
+                                                          grp_part(a), grp_part(b), grp_tickets(a), gg.rpb);
   if (a.mask) {
-    bn_reduce_dual_kernel<true><<<grid_r, 256, 0, s>>>(a.x, b.x, dy, a.dy2, nullptr, a.mask, M, C, gr.rpb, gr.lanes,
-                                                       gr.rl, fa, fb, ncop);
+    if (!small)
+      bn_reduce_dual_kernel<true><<<grid_r, 256, 0, s>>>(a.x, b.x, dy, a.dy2, nullptr, a.mask, M, C, gr.rpb, gr.lanes,
+                                                         gr.rl, fa, fb, ncop);
     bn_bwd_apply_dual_kernel<true><<<grid, 256, 0, s>>>(a.x, b.x, dy, a.dy2, nullptr, a.mask, fa.coef, fb.coef, dx, dr,
                                                         M, C, g.rpb, g.lanes, g.rl);
   } else {
-    bn_reduce_dual_kernel<false><<<grid_r, 256, 0, s>>>(a.x, b.x, dy, a.dy2, a.y, nullptr, M, C, gr.rpb, gr.lanes,
-                                                        gr.rl, fa, fb, ncop);
+    if (!small)
+      bn_reduce_dual_kernel<false><<<grid_r, 256, 0, s>>>(a.x, b.x, dy, a.dy2, a.y, nullptr, M, C, gr.rpb, gr.lanes,
+                                                          gr.rl, fa, fb, ncop);
     bn_bwd_apply_dual_kernel<false><<<grid, 256, 0, s>>>(a.x, b.x, dy, a.dy2, a.y, nullptr, fa.coef, fb.coef, dx, dr,
                                                          M, C, g.rpb, g.lanes, g.rl);
   }

@@ -14,11 +14,14 @@ def _cl(x):  # bf16 channels_last copy of a fp32 NCHW tensor
     return x.bfloat16().contiguous(memory_format=torch.channels_last)
 
 
-@pytest.mark.parametrize("shape", [(8, 64, 16, 16), (8, 64, 24, 24), (64, 1024, 2, 2), (16, 40, 4, 4)])
+@pytest.mark.parametrize("shape", [(8, 64, 16, 16), (8, 64, 24, 24), (10, 200, 32, 32), (64, 1024, 2, 2),
+                                   (16, 40, 4, 4), (17, 64, 64, 64)])
 @pytest.mark.parametrize("residual,relu", [(False, False), (False, True), (True, True)])
 def test_batchnorm_train_fused(residual, relu, shape):
-    """(M = N*H*W <= 2048 rows runs the one-pass small-M statistics kernel, 8 x 64 x 24 x 24 the
-    multi-block reduce with atomics + last-block finalize; C = 40: a partial 64-channel group)"""
+    """(M = N*H*W <= 2048 rows runs the one-pass small-M statistics kernel; up to 65536 rows the
+    same kernel over row groups with per-column tickets (8 x 64 x 24 x 24; 10 x 200 x 32 x 32: a
+    partial last column); 17 x 64 x 64 x 64 the multi-block reduce with atomics + last-block
+    finalize; C = 40: a partial 64-channel group)"""
     torch.manual_seed(0)
     N, C, H, W = shape
     bn = BatchNorm2d(C)
@@ -295,7 +298,7 @@ def test_resnet_stem_fused_bn_pool_vs_fp32_oracle(N, H, monkeypatch):
     torch.testing.assert_close(rmf, rms, rtol=1e-4, atol=1e-6)
 
 
-@pytest.mark.parametrize("N,C,H,W", [(8, 64, 16, 16), (4, 128, 7, 9), (2, 24, 5, 5)])
+@pytest.mark.parametrize("N,C,H,W", [(8, 64, 16, 16), (4, 128, 7, 9), (2, 24, 5, 5), (16, 64, 24, 24), (17, 64, 64, 64)])
 @pytest.mark.parametrize("twin", [False, True])
 @pytest.mark.parametrize("use_mask", [True, False])
 def test_bn_dual_act_matches_separate_and_fp32(N, C, H, W, twin, use_mask, monkeypatch):
