@@ -10,6 +10,7 @@
 namespace ldnn {
 
 constexpr int kBnCopies = 8;  // accumulator copies of the BN statistics (conv epilogue and BN reduce)
+constexpr int kGrpMax = 128;  // row groups of the grouped statistics passes (BnFin::part rows), at most
 
 // Totals of every block are complete in `acc` when the last block draws its
 // ticket: the fp32 atomics execute at the memory side and every block waits
@@ -126,6 +127,47 @@ __device__ __forceinline__ void bn_finalize_last(const BnFin& f, int M, int C, i
     bn_finalize_channel<BWD>(f, M, C, c, S0, S1, invM);
   }
   if (!BWD && threadIdx.x == 0 && f.num_batches) f.num_batches[0] += 1;
+}
+
+// ---- grouped statistics (bn_reduce_small_kernel in bn_pool.hip, the conv slab epilogue in
+// conv_lds.hip): a grid of (64-channel columns) x (row groups); every workgroup publishes its
+// columns' partial sums to BnFin::part ([row group][2][C]) and the LAST workgroup of a column
+// (per-column ticket) sums them and finalizes those 64 channels -- a short chain per column,
+// all columns in parallel.
+__device__ __forceinline__ void grp_store(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float grp_load(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// After wave 0 stored this workgroup's partials: true in every thread of the workgroup that
+// draws the column's last ticket (it resets the ticket).  As in bn_finalize_last, no fences: the
+// partials are agent-scope atomic stores (coherent at the memory side), wave 0 waits for their
+// completion before its ticket, and the finalizer reads them with agent-scope atomic loads.
+__device__ __forceinline__ bool grp_ticket(int* ticket, int n, int& flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (threadIdx.x == 0) {
+    const int t = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    flag = t == n - 1;
+    if (flag) __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  return flag;
+}
+// the finalizer's column totals: thread (q = tid / 64, channel tid % 64) sums every 4th row
+// group's partial k into tot[k][q][64]; the caller reads tot after a barrier
+__device__ __forceinline__ void grp_sum(const float* part, int C, int c, int k, int ny, float* tot) {
+  const int q = threadIdx.x >> 6;
+  float v = 0.f;
+  if (c < C)
+    for (int y0 = q; y0 < ny; y0 += 32) {   // 8 loads in flight (atomic loads are not batched for us)
+      float t[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) t[u] = y0 + 4 * u < ny ? grp_load(part + ((size_t)(y0 + 4 * u) * 2 + k) * C + c) : 0.f;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v += t[u];
+    }
+  tot[(k * 4 + q) * 64 + (threadIdx.x & 63)] = v;
 }
 
 }  // namespace ldnn

@@ -191,6 +191,8 @@ struct BnFin {
   int grad_assign;            // bwd: 1 = dgamma / dbeta = the totals (first write of the step)
   int64_t* num_batches;       // fwd: += 1 (BatchNorm2d.num_batches_tracked), nullable
   float eps, momentum;
+  float* part;                // [kGrpMax][2C] row-group partials of the grouped reduce (ldnn_bn_fin.h)
+  int* tickets;               // its per-64-channel-column tickets (left zero)
 };
 // Training-mode forward finalize state of a BN (its ws accumulators / ticket / coef).
 BnFin bn_forward_fin(const BnArgs& a);

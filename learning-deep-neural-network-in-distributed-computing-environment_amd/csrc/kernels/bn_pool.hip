@@ -206,42 +206,6 @@ __global__ __launch_bounds__(256) void bn_reduce_kernel(const bf16_t* __restrict
 // sums to `part` ([grid.y][2][C]); the LAST of a column's grid.y workgroups (per-column ticket)
 // sums them and finalizes those 64 channels -- a short chain per column, all columns in parallel,
 // instead of the big reduce's fp32 atomics + one block exchanging every channel's copies.
-__device__ __forceinline__ void grp_store(float* p, float v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ float grp_load(const float* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// After wave 0 stored this workgroup's partials: true in every thread of the workgroup that
-// draws the column's last ticket (it resets the ticket).  As in bn_finalize_last, no fences: the
-// partials are agent-scope atomic stores (coherent at the memory side), wave 0 waits for their
-// completion before its ticket, and the finalizer reads them with agent-scope atomic loads.
-__device__ __forceinline__ bool grp_ticket(int* ticket, int n, int& flag) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (threadIdx.x == 0) {
-    const int t = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    flag = t == n - 1;
-    if (flag) __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __syncthreads();
-  return flag;
-}
-// the finalizer's column totals: thread (q = tid / 64, channel tid % 64) sums every 4th row
-// group's partial k into tot[k][q][64]; the caller reads tot after a barrier
-__device__ __forceinline__ void grp_sum(const float* part, int C, int c, int k, int ny, float* tot) {
-  const int q = threadIdx.x >> 6;
-  float v = 0.f;
-  if (c < C)
-    for (int y0 = q; y0 < ny; y0 += 32) {   // 8 loads in flight (atomic loads are not batched for us)
-      float t[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) t[u] = y0 + 4 * u < ny ? grp_load(part + ((size_t)(y0 + 4 * u) * 2 + k) * C + c) : 0.f;
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v += t[u];
-    }
-  tot[(k * 4 + q) * 64 + (threadIdx.x & 63)] = v;
-}
-
 template <bool BWD, bool RELU, bool MASK = false>
 __global__ __launch_bounds__(256) void bn_reduce_small_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
                                                               const bf16_t* __restrict__ y, const float* __restrict__ mean,
@@ -1101,7 +1065,6 @@ __global__ void gap_bwd_kernel(const bf16_t* __restrict__ dy, bf16_t* __restrict
 //   [42C + 32, ...) kGrpMax x [2C] row-group partials of the mid-M reduce (bn_reduce_small_kernel),
 //   then its ceil(C / 64) per-column tickets.
 // Accumulators and tickets are left zero by the finalizing block.
-constexpr int kGrpMax = 128;   // row groups of the mid-M reduce, at most
 int bn_workspace_floats(int C) { return 42 * C + 32 + kGrpMax * 2 * C + ((C + 63) / 64 + 3) / 4 * 4; }
 
 namespace {
@@ -1124,6 +1087,8 @@ BnFin bn_forward_fin(const BnArgs& a) {
   f.num_batches = a.num_batches;
   f.eps = a.eps;
   f.momentum = a.momentum;
+  f.part = grp_part(a);
+  f.tickets = grp_tickets(a);
   return f;
 }
 
@@ -1354,6 +1319,8 @@ BnFin bn_backward_fin(const BnArgs& a, float* dgamma, float* dbeta, bool grad_as
   f.dgamma = dgamma;
   f.dbeta = dbeta;
   f.grad_assign = grad_assign ? 1 : 0;
+  f.part = grp_part(a);
+  f.tickets = grp_tickets(a);
   return f;
 }
 }  // namespace

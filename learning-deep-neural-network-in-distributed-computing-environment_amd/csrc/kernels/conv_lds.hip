@@ -2153,6 +2153,29 @@ __device__ __forceinline__ floatx4 slab_ld(const floatx4* p) {
   else return *p;
 }
 
+// sum over `splits` slabs (stride4 floatx4 apart) of the two floatx4 at w: 4 slabs' loads in
+// flight per step (a plain loop waits on every load before the next add)
+template <bool NT>
+__device__ __forceinline__ void slab_sum8(const floatx4* w, int64_t stride4, int splits, floatx4& v0, floatx4& v1) {
+  v0 = slab_ld<NT>(w);
+  v1 = slab_ld<NT>(w + 1);
+  int sp = 1;
+  for (; sp + 3 < splits; sp += 4) {
+    floatx4 a[4], b[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      a[u] = slab_ld<NT>(w + (sp + u) * stride4);
+      b[u] = slab_ld<NT>(w + (sp + u) * stride4 + 1);
+    }
+    v0 += (a[0] + a[1]) + (a[2] + a[3]);
+    v1 += (b[0] + b[1]) + (b[2] + b[3]);
+  }
+  for (; sp < splits; ++sp) {
+    v0 += slab_ld<NT>(w + sp * stride4);
+    v1 += slab_ld<NT>(w + sp * stride4 + 1);
+  }
+}
+
 // bf16 out[m][n] = epi(sum_s ws[s][m][n] (+ bias[n])): the split-K reduction of the
 // small-M fwd / dgrad slabs, 8 consecutive outputs per thread (two float4 per slab,
 // one 16-B store), all CUs.
@@ -2163,12 +2186,8 @@ __global__ __launch_bounds__(256) void conv_slab_epilogue_kernel(const float* __
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= n8) return;
   const floatx4* w = reinterpret_cast<const floatx4*>(ws) + 2 * i;
-  const int64_t stride4 = 2 * n8;
-  floatx4 v0 = slab_ld<NT>(w), v1 = slab_ld<NT>(w + 1);
-  for (int sp = 1; sp < splits; ++sp) {
-    v0 += slab_ld<NT>(w + sp * stride4);
-    v1 += slab_ld<NT>(w + sp * stride4 + 1);
-  }
+  floatx4 v0, v1;
+  slab_sum8<NT>(w, 2 * n8, splits, v0, v1);
   const int n = (int)((i * 8) % N);
   u16x8 o;
 #pragma unroll
@@ -2197,6 +2216,98 @@ hipError_t conv_slab_epilogue(const float* ws, uint16_t* out, int M, int N, int 
 #undef LDNN_SLAB_EPI
     default: return hipErrorInvalidValue;
   }
+  return hipGetLastError();
+}
+
+// The slab split-K sum of a small-M forward conv AND the following training BatchNorm's
+// statistics in one pass (the slab epilogue + a separate statistics pass otherwise): the grouped
+// geometry of bn_reduce_small_kernel -- workgroup = 64 channels x rpb rows, 8 channel lanes x 32
+// row lanes, every slab's loads of a row in flight together -- summing the statistics of the
+// bf16-rounded outputs, then the per-column ticket finalize (ldnn_bn_fin.h).  (A round-2 variant
+// with 8-copy atomics and one finalizing block was slower than the pair, profiles/cnn_slab_bn_ab_r2.jsonl.)
+template <bool NT>
+__global__ __launch_bounds__(256) void conv_slab_bn_kernel(const float* __restrict__ ws, bf16_t* __restrict__ out,
+                                                           int M, int N, int splits, BnFin fin, int rpb) {
+  constexpr int kLanes = 8, kRl = 32, kJs = 256 + kLanes;
+  __shared__ float red[2][8 * kJs];
+  __shared__ int last;
+  const int tid = threadIdx.x, lane = tid % kLanes, rlane = tid / kLanes;
+  const int c0 = blockIdx.x * 64 + lane * 8;
+  float s0[8], s1[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s0[j] = s1[j] = 0.f;
+  if (c0 < N) {
+    const int r_end = min(M, (int)(blockIdx.y + 1) * rpb);
+    const size_t sstride = (size_t)M * N / 4;
+    for (int r = blockIdx.y * rpb + rlane; r < r_end; r += kRl) {
+      const size_t o = (size_t)r * N + c0;
+      floatx4 v0, v1;
+      slab_sum8<NT>(reinterpret_cast<const floatx4*>(ws + o), (int64_t)sstride, splits, v0, v1);
+      u16x8 ob;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        ob[j] = f2bf(j < 4 ? v0[j] : v1[j - 4]);
+        const float v = bf2f(ob[j]);
+        s0[j] += v;
+        s1[j] += v * v;
+      }
+      *reinterpret_cast<u16x8*>(out + o) = ob;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    red[0][j * kJs + tid] = s0[j];
+    red[1][j * kJs + tid] = s1[j];
+  }
+  __syncthreads();
+  if (tid < 64) {
+    const int j = tid / kLanes, ln = tid - j * kLanes;
+    float t0 = 0.f, t1 = 0.f;
+#pragma unroll 8
+    for (int q = 0; q < kRl; ++q) {
+      t0 += red[0][j * kJs + q * kLanes + ln];
+      t1 += red[1][j * kJs + q * kLanes + ln];
+    }
+    const int c = blockIdx.x * 64 + ln * 8 + j;
+    if (gridDim.y == 1) {
+      if (c < N) bn_finalize_channel<false>(fin, M, N, c, t0, t1, 1.f / (float)M);
+    } else if (c < N) {
+      grp_store(fin.part + (size_t)blockIdx.y * 2 * N + c, t0);
+      grp_store(fin.part + ((size_t)blockIdx.y * 2 + 1) * N + c, t1);
+    }
+  }
+  if (blockIdx.x == 0 && blockIdx.y == 0 && tid == 0 && fin.num_batches) fin.num_batches[0] += 1;
+  if (gridDim.y == 1) return;
+  if (!grp_ticket(fin.tickets + blockIdx.x, gridDim.y, last)) return;
+  float* tot = &red[0][0];
+  const int cc = blockIdx.x * 64 + (tid & 63);
+  grp_sum(fin.part, N, cc, 0, gridDim.y, tot);
+  grp_sum(fin.part, N, cc, 1, gridDim.y, tot);
+  __syncthreads();
+  if (tid < 64 && cc < N) {
+    const float S0 = tot[tid] + tot[64 + tid] + tot[128 + tid] + tot[192 + tid];
+    const float S1 = tot[256 + tid] + tot[320 + tid] + tot[384 + tid] + tot[448 + tid];
+    bn_finalize_channel<false>(fin, M, N, cc, S0, S1, 1.f / (float)M);
+  }
+}
+
+int env_int(const char* name, int dflt);
+// LDNN_CONV_SLAB_BN (A/B knob, default 1): slab-split forward convs followed by a training BN
+// take the BN statistics in conv_slab_bn_kernel; LDNN_CONV_SLAB_BN_TARGET workgroups aimed at
+int slab_bn_env() {
+  static const int v = env_int("LDNN_CONV_SLAB_BN", 1);
+  return v;
+}
+hipError_t conv_slab_bn(const float* ws, uint16_t* out, int M, int N, int splits, const BnFin& fin, hipStream_t st) {
+  if (M <= 0) return hipSuccess;
+  static const int target = std::max(1, env_int("LDNN_CONV_SLAB_BN_TARGET", 512));
+  const int G = (N + 63) / 64;
+  int ny = std::max(1, std::min({(target + G - 1) / G, (M + 31) / 32, kGrpMax}));
+  const int rpb = (M + ny - 1) / ny;
+  ny = (M + rpb - 1) / rpb;
+  const dim3 g(G, ny);
+  if (slab_nt_env()) conv_slab_bn_kernel<true><<<g, 256, 0, st>>>(ws, out, M, N, splits, fin, rpb);
+  else conv_slab_bn_kernel<false><<<g, 256, 0, st>>>(ws, out, M, N, splits, fin, rpb);
   return hipGetLastError();
 }
 
@@ -2877,9 +2988,13 @@ hipError_t conv2d_fwd_lds(const ConvShape& s, const uint16_t* x, const uint16_t*
   const bool hbp = hb_takes(s, false);
   Plan pl = hbp ? plan_hb(s, false) : plan_fwd(s);
   LArgs a = base_args(s);
-  if (bn != nullptr && pl.slab) {  // slab split-K: the next BN runs its own statistics pass
+  // slab split-K: the slab pass takes the next BN's statistics (conv_slab_bn), or with
+  // LDNN_CONV_SLAB_BN=0 the BN runs its own statistics pass
+  const BnFin* slab_fin = nullptr;
+  if (bn != nullptr && pl.slab) {
+    if (slab_bn_env() && bn->part != nullptr && bn->tickets != nullptr && s.K % 8 == 0) slab_fin = bn;
+    else if (bn_used) *bn_used = false;
     bn = nullptr;
-    if (bn_used) *bn_used = false;
   }
   if (bn != nullptr) {
     a.bn_stats = 1;
@@ -2925,6 +3040,7 @@ hipError_t conv2d_fwd_lds(const ConvShape& s, const uint16_t* x, const uint16_t*
     e = launch<2, 2, FwdA<128, 4, 4>, WeightKC<128, 4, 4>, false, false>(a, epi, pl.splits, x, bx, w, bw, st);
   }
   if (e != hipSuccess || !slab) return e;
+  if (slab_fin != nullptr) return conv_slab_bn(ws, y, a.M, a.N, pl.splits, *slab_fin, st);
   return conv_slab_epilogue(ws, y, a.M, a.N, pl.splits, bias, epi, st);
 }
 

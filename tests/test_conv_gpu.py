@@ -385,3 +385,39 @@ def test_big_tile_halo_conv_fused_bn_statistics(N, C, H, W):
     torch.testing.assert_close(res[1][2], torch.rsqrt(yb.var(0, unbiased=False) + 1e-5), rtol=1e-3, atol=1e-4)
     for a, b in zip(res[1][1:], res[0][1:]):
         torch.testing.assert_close(a, b, rtol=1e-3, atol=1e-4)
+
+
+@pytest.mark.parametrize("N,C,H,K", [(64, 512, 4, 512), (64, 1024, 2, 1024), (64, 256, 4, 512), (3, 128, 5, 200)])
+def test_slab_split_conv_fused_bn_statistics(N, C, H, K):
+    """Slab split-K forward convs (EnhancedCNN's 4x4 / 2x2 tails) followed by a training BN: the
+    slab pass (conv_slab_bn_kernel) writes the bf16 output AND finalizes the BN statistics over
+    row groups with per-column tickets -- output == fp32 conv, saved mean / invstd == those of the
+    stored output, running stats == the EMA, and a repeat (tickets left zero) gives the same bits."""
+    torch.manual_seed(23)
+    Cc = _ext.C()
+    x = torch.randn(N, H, H, C, device="cuda").bfloat16()
+    w = (torch.randn(K, 3, 3, C, device="cuda") * (1.0 / (C * 9) ** 0.5)).bfloat16()
+    ws = torch.zeros(Cc.bn_workspace_floats(K), device="cuda")
+    nb = torch.zeros(1, dtype=torch.long, device="cuda")
+    outs = []
+    for _ in range(2):
+        y = torch.full((N, H, H, K), 7.0, device="cuda", dtype=torch.bfloat16)
+        sm, si = torch.zeros(K, device="cuda"), torch.zeros(K, device="cuda")
+        rm, rv = torch.zeros(K, device="cuda"), torch.ones(K, device="cuda")
+        used = Cc.conv_fwd(x, w, y, 1, 1, bn_ws=ws, bn_running_mean=rm, bn_running_var=rv, bn_save_mean=sm,
+                           bn_save_invstd=si, bn_num_batches=nb)
+        assert used
+        outs.append((y.float(), sm, si, rm, rv))
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b)
+    assert nb.item() == 2
+    y, sm, si, rm, rv = outs[0]
+    xf, wf = x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2)
+    yr = torch.nn.functional.conv2d(xf, wf, padding=1).permute(0, 2, 3, 1)
+    torch.testing.assert_close(y, yr, rtol=1e-2, atol=1e-2 * yr.abs().max().item())
+    yb = y.reshape(-1, K)
+    mean, var = yb.mean(0), yb.var(0, unbiased=False)
+    torch.testing.assert_close(sm, mean, rtol=1e-3, atol=1e-4)
+    torch.testing.assert_close(si, torch.rsqrt(var + 1e-5), rtol=1e-3, atol=1e-4)
+    torch.testing.assert_close(rm, 0.1 * mean, rtol=1e-3, atol=1e-5)
+    torch.testing.assert_close(rv, 0.9 + 0.1 * yb.var(0, unbiased=True), rtol=1e-3, atol=1e-5)
