@@ -1315,6 +1315,59 @@ void gap_bwd(const at::Tensor& dy, const at::Tensor& dx) {
         "gap_bwd");
 }
 
+
+// x [N][HW][C] bf16, w [>= ncls][ldw] bf16, b [>= ncls] fp32 (optional) -> pooled [N][C], logits [N][>= ncls]
+void gap_linear_fwd(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& b,
+                    const at::Tensor& pooled, const at::Tensor& logits, int64_t ncls) {
+  check_dev(x, at::kBFloat16, "x");
+  check_dev(w, at::kBFloat16, "w");
+  check_dev(pooled, at::kBFloat16, "pooled");
+  check_dev(logits, at::kBFloat16, "logits");
+  TORCH_CHECK(x.dim() == 3 && x.is_contiguous(), "gap_linear_fwd: x must be a dense [N][HW][C]");
+  const int64_t N = x.size(0), HW = x.size(1), C = x.size(2);
+  TORCH_CHECK(pooled.is_contiguous() && pooled.numel() == N * C, "gap_linear_fwd: pooled must be a dense [N][C]");
+  TORCH_CHECK(w.dim() == 2 && w.stride(1) == 1 && w.size(0) >= ncls && w.size(1) >= C, "gap_linear_fwd: bad w");
+  TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1 && logits.size(0) == N && logits.size(1) >= ncls,
+              "gap_linear_fwd: bad logits");
+  TORCH_CHECK(ldnn::gap_linear_ok((int)N, (int)HW, (int)C, (int)ncls), "gap_linear_fwd: unsupported shape");
+  const float* bp = nullptr;
+  if (b.has_value()) {
+    check_dev(*b, at::kFloat, "b");
+    TORCH_CHECK(b->is_contiguous() && b->numel() >= ncls, "gap_linear_fwd: bad b");
+    bp = b->data_ptr<float>();
+  }
+  check(ldnn::gap_linear_fwd(bf16_ptr(x), bf16_ptr(w), bp, bf16_mut(pooled), bf16_mut(logits), (int)N, (int)HW,
+                             (int)C, (int)w.stride(0), (int)ncls, (int)logits.stride(0), cur_stream(x)),
+        "gap_linear_fwd");
+}
+
+// g [N][>= ncls] bf16, pooled [N][C], w [>= ncls][ldw] -> dw [>= ncls][lddw] fp32 (beta_w), db (beta_b), dx [N][HW][C]
+void gap_linear_bwd(const at::Tensor& g, const at::Tensor& pooled, const at::Tensor& w, const at::Tensor& dw,
+                    const c10::optional<at::Tensor>& db, const at::Tensor& dx, int64_t ncls, double beta_w,
+                    double beta_b) {
+  check_dev(g, at::kBFloat16, "g");
+  check_dev(pooled, at::kBFloat16, "pooled");
+  check_dev(w, at::kBFloat16, "w");
+  check_dev(dw, at::kFloat, "dw");
+  check_dev(dx, at::kBFloat16, "dx");
+  TORCH_CHECK(dx.dim() == 3 && dx.is_contiguous(), "gap_linear_bwd: dx must be a dense [N][HW][C]");
+  const int64_t N = dx.size(0), HW = dx.size(1), C = dx.size(2);
+  TORCH_CHECK(pooled.is_contiguous() && pooled.numel() == N * C, "gap_linear_bwd: pooled must be a dense [N][C]");
+  TORCH_CHECK(g.dim() == 2 && g.stride(1) == 1 && g.size(0) == N && g.size(1) >= ncls, "gap_linear_bwd: bad g");
+  TORCH_CHECK(w.dim() == 2 && w.stride(1) == 1 && w.size(0) >= ncls && w.size(1) >= C, "gap_linear_bwd: bad w");
+  TORCH_CHECK(dw.dim() == 2 && dw.stride(1) == 1 && dw.size(0) >= ncls && dw.size(1) >= C, "gap_linear_bwd: bad dw");
+  TORCH_CHECK(ldnn::gap_linear_ok((int)N, (int)HW, (int)C, (int)ncls), "gap_linear_bwd: unsupported shape");
+  float* dbp = nullptr;
+  if (db.has_value()) {
+    check_dev(*db, at::kFloat, "db");
+    TORCH_CHECK(db->is_contiguous() && db->numel() >= ncls, "gap_linear_bwd: bad db");
+    dbp = db->data_ptr<float>();
+  }
+  check(ldnn::gap_linear_bwd(bf16_ptr(g), bf16_ptr(pooled), bf16_ptr(w), dw.data_ptr<float>(), dbp, bf16_mut(dx),
+                             (int)N, (int)HW, (int)C, (int)g.stride(0), (int)w.stride(0), (int)dw.stride(0), (int)ncls,
+                             (float)beta_w, (float)beta_b, cur_stream(g)),
+        "gap_linear_bwd");
+}
 }  // namespace
 
 // A HIP event whose record inside a stream capture becomes an EXTERNAL event-record
@@ -1686,6 +1739,13 @@ PYBIND11_MODULE(_C, m) {
         py::arg("dy2") = py::none(), py::arg("pad") = 1);
   m.def("gap_fwd", &gap_fwd);
   m.def("gap_bwd", &gap_bwd);
+  m.def("gap_linear_ok", &ldnn::gap_linear_ok, "shapes the fused pooled classifier head takes", py::arg("N"),
+        py::arg("HW"), py::arg("C"), py::arg("ncls"));
+  m.def("gap_linear_fwd", &gap_linear_fwd, "global average pool + Linear (<= 16 classes) in one launch", py::arg("x"),
+        py::arg("w"), py::arg("b"), py::arg("pooled"), py::arg("logits"), py::arg("ncls"));
+  m.def("gap_linear_bwd", &gap_linear_bwd, "its backward: dW, db and the input gradient in one launch", py::arg("g"),
+        py::arg("pooled"), py::arg("w"), py::arg("dw"), py::arg("db"), py::arg("dx"), py::arg("ncls"),
+        py::arg("beta_w") = 0.0, py::arg("beta_b") = 0.0);
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("stride"), py::arg("pad"),
         py::arg("bias") = py::none(), py::arg("epi") = 0, py::arg("bn_ws") = py::none(),
         py::arg("bn_gamma") = py::none(), py::arg("bn_beta") = py::none(), py::arg("bn_running_mean") = py::none(),

@@ -279,6 +279,14 @@ hipError_t scale_bf16_dev(const uint16_t* src, const float* scale, uint16_t* out
 // overlap-probe communication stand-in: `reps` copies of src on `blocks` workgroups
 hipError_t standin_copy(const float* src, float* dst, int64_t n, int blocks, int reps, hipStream_t s);
 
+// ---- pooled classifier head (gap_head.hip): global average pool + Linear (<= 16 classes)
+bool gap_linear_ok(int N, int HW, int C, int ncls);
+hipError_t gap_linear_fwd(const uint16_t* x, const uint16_t* W, const float* b, uint16_t* pooled, uint16_t* logits,
+                          int N, int HW, int C, int ldw, int ncls, int ldl, hipStream_t s);
+hipError_t gap_linear_bwd(const uint16_t* g, const uint16_t* pooled, const uint16_t* W, float* dW, float* db,
+                          uint16_t* dx, int N, int HW, int C, int ldg, int ldw, int lddw, int ncls, float beta_w,
+                          float beta_b, hipStream_t s);
+
 // ---- fused optimizers over flat fp32 buffers -------------------------------
 // hp (device fp32): [0]=lr [1]=step (already incremented for Adam) ; grad_scale multiplies g
 // Gradient ranges [zb[i], ze[i]) (element offsets into this launch's range) are

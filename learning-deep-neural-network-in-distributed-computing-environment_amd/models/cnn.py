@@ -83,9 +83,7 @@ class EnhancedCNNModel(nn.Module):
         x = self.layer2(x)
         x = self.layer3(x)
         x = self.layer4(x)
-        x = self.pool(x)
-        x = x.view(x.size(0), -1)
-        return self.fc(x)
+        return LF.gap_linear(x, self.pool, self.fc)   # pool -> view -> fc (one fused launch each way on the GPU)
 
 
 class EnhancedCNNSmall(nn.Module):
@@ -107,8 +105,7 @@ class EnhancedCNNSmall(nn.Module):
     def forward(self, x):
         x = self.prep(x)
         x = self.layer3(self.layer2(self.layer1(x)))
-        x = self.pool(x)
-        return self.fc(x.view(x.size(0), -1))
+        return LF.gap_linear(x, self.pool, self.fc)
 
 
 class LeNet5(nn.Module):

@@ -13,6 +13,8 @@ bookkeeping (K14, K15; BAR/trainer.py:207-216).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
 
@@ -784,3 +786,60 @@ def adaptive_avg_pool2d(x, output_size):
     if _ext.use_native(x) and os_ == 1 and x.dim() == 4:
         return _GapNative.apply(x)
     return F.adaptive_avg_pool2d(x, output_size)
+
+
+class _GapLinearNative(torch.autograd.Function):
+    """AdaptiveAvgPool2d(1) -> flatten -> Linear (<= 16 classes) in one launch each way
+    (gap_head.hip): the CNN classifier heads at small batch are pure launch latency."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, flat):
+        C_ = _ext.C()
+        N, C, H, W = x.shape
+        w = flat.shadow_storage(weight)
+        npad = w.shape[0]
+        xb = as_nhwc(x if x.dtype == torch.bfloat16 else x.to(torch.bfloat16), C).contiguous()
+        pooled = torch.empty(N, C, dtype=torch.bfloat16, device=x.device)
+        logits = torch.empty(N, npad, dtype=torch.bfloat16, device=x.device)
+        b = flat.master_storage(bias) if bias is not None else None
+        ncls = weight.shape[0]
+        C_.gap_linear_fwd(xb.view(N, H * W, C), w, b, pooled, logits, ncls)
+        ctx.save_for_backward(pooled)
+        ctx.meta = (N, C, H, W, ncls, x.dtype)
+        ctx.flat, ctx.weight, ctx.bias = flat, weight, bias
+        return logits[:, :ncls]
+
+    @staticmethod
+    def backward(ctx, gy):
+        C_ = _ext.C()
+        (pooled,) = ctx.saved_tensors
+        N, C, H, W, ncls, in_dtype = ctx.meta
+        flat, weight, bias = ctx.flat, ctx.weight, ctx.bias
+        g = gy if (gy.dtype == torch.bfloat16 and gy.stride(1) == 1) else gy.to(torch.bfloat16).contiguous()
+        dx = torch.empty(N, H, W, C, dtype=torch.bfloat16, device=gy.device)
+        C_.gap_linear_bwd(g, pooled, flat.shadow_storage(weight), flat.grad_storage(weight),
+                          flat.grad_storage(bias) if bias is not None else None, dx.view(N, H * W, C), ncls,
+                          beta_w=flat.grad_beta(weight), beta_b=flat.grad_beta(bias) if bias is not None else 0.0)
+        flat.notify(weight, bias)
+        out = nchw_view(dx, C)
+        return (out if in_dtype == torch.bfloat16 else out.to(in_dtype)), None, None, None
+
+
+# LDNN_GAP_LINEAR=0: the pooled classifier head runs as separate pool + Linear ops (A/B knob)
+GAP_LINEAR = os.environ.get("LDNN_GAP_LINEAR", "1") == "1"
+
+
+def gap_linear(x, pool, fc):
+    """fc(flatten(pool(x))) for a global average pool `pool` and an ldnn Linear `fc`; one fused
+    launch each way when the shapes allow (<= 16 classes, unpadded features), else the two ops."""
+    flat = getattr(fc, "_ldnn_flat", None)
+    os_ = pool.output_size if isinstance(pool.output_size, int) else (
+        pool.output_size[0] if pool.output_size[0] == pool.output_size[1] else None)
+    if (GAP_LINEAR and _ext.use_native(x) and x.dim() == 4 and os_ == 1 and flat is not None
+            and flat.shadow is not None and getattr(fc, "activation", "none") == "none"):
+        N, C, H, W = x.shape
+        w = flat.shadow_storage(fc.weight)
+        if w.shape[1] == C and C == fc.in_features and _ext.C().gap_linear_ok(N, H * W, C, fc.out_features):
+            return _GapLinearNative.apply(x, fc.weight, fc.bias, flat)
+    y = pool(x)
+    return fc(y.reshape(y.size(0), -1))
