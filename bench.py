@@ -274,6 +274,47 @@ def run_cnn(ctx, name: str, batch: int, steps: int, optimizer: str = "sgd", warm
     return rec
 
 
+def run_configs(ctx, configs, run_fn) -> dict:
+    """The secondary CNN configs, each guarded: a failing config records its error instead of
+    costing the headline record.  After each config every rank learns whether any rank failed
+    (0 ok, 1 failed, 2 device fault) with one small all_reduce(MAX), so a rank that failed alone
+    never leaves its peers inside collectives it does not join; a device fault (or, with peers,
+    any failure) ends the loop.
+    The flag travels on a side gloo group, so it can never pair up with a collective of the
+    config itself: peers still waiting inside the failed config's collectives leave them at the
+    process group's timeout (an error of their own) and then meet the failed rank there."""
+    out = {}
+    side = dist.new_group(backend="gloo") if ctx.world_size > 1 else None
+    for name, b, st, o in configs:
+        key = f"{name}_b{b}" + ("_adam" if o == "adam" else "")
+        err = None
+        try:
+            out[key] = run_fn(ctx, name, b, st, o)
+        except Exception as e:  # noqa: BLE001 -- a secondary config must not cost the headline record
+            err = e
+            out[key] = {"error": f"{type(e).__name__}: {e}"[:500]}
+        fault = err is not None and any(t in str(err) for t in ("HIP error", "hipError", "illegal", "fault"))
+        code = 2 if fault else (1 if err is not None else 0)
+        if ctx.world_size > 1:
+            try:
+                flag = torch.tensor([code], dtype=torch.int32)
+                dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=side)
+                code = int(flag.item())
+            except Exception:  # noqa: BLE001
+                code = 2
+        if code and err is None:
+            out[key] = {"error": "failed on another rank"}
+        # a device fault, or any failure with peers (their process group may be left broken or
+        # mid-collective): no further configs
+        if code == 2 or (code and ctx.world_size > 1):
+            for n2, b2, _, o2 in configs[len(out):]:
+                out[f"{n2}_b{b2}" + ("_adam" if o2 == "adam" else "")] = {"skipped": "an earlier config failed"}
+            break
+        if torch.cuda.is_available():
+            torch.cuda.empty_cache()
+    return out
+
+
 def run_stock(ctx, args):
     """Stock PyTorch-ROCm eager baseline of the same config (hipBLASLt GEMMs,
     MIOpen/ATen elementwise, RCCL DDP, torch.optim.SGD foreach), bf16 autocast."""
@@ -402,8 +443,9 @@ def main():
             "parallelism": f"dp{n}",
             "optimizer": "sgd momentum 0.9, fp32 master",
             "gemms": ("ldnn MFMA kernels only: bias+ReLU fwd (ReLU bit masks), dReLU dgrad on a transposed W, "
-                      "fp32 wgrads (the 784-wide one split-K into slabs, summed by the pass that also applies its SGD "
-                      "update on 1 GPU), classifier head (Linear + softmax-xent + argmax + head dgrad), fused SGD"
+                      "fp32 wgrads (the 784-wide one split-K into slabs + one summing pass that also emits the bias "
+                      "gradient from a ones column), classifier head (logits in the last hidden forward's epilogue, "
+                      "softmax-xent + argmax, fused MFMA head backward), fused SGD"
                       if args.gemms == "ldnn" else
                       "hipBLASLt: fp32 wgrads, bias/ReLU fwd, hidden dgrad; ldnn: fused dReLU+dbias pass, "
                       "classifier head (Linear + softmax-xent + argmax + head dgrad), SGD"),
@@ -418,16 +460,7 @@ def main():
     rec["rccl_ranks"] = n if ctx.backend == "nccl" else 0
     rec.update(extra)
     if not args.no_configs:
-        rec["configs"] = {}
-        for name, b, st, o in CNN_CONFIGS:
-            key = f"{name}_b{b}" + ("_adam" if o == "adam" else "")
-            try:
-                rec["configs"][key] = run_cnn(ctx, name, b, st, o)
-            except Exception as e:  # noqa: BLE001 -- a secondary config must not cost the headline record
-                if ctx.world_size > 1:   # every rank fails the same config together (or the job aborts)
-                    dist.barrier()
-                rec["configs"][key] = {"error": f"{type(e).__name__}: {e}"[:500]}
-                torch.cuda.empty_cache()
+        rec["configs"] = run_configs(ctx, CNN_CONFIGS, run_cnn)
     if args.compare_stock:
         el_s = run_stock(ctx, args)
         stock = args.batch * n * args.steps / el_s
