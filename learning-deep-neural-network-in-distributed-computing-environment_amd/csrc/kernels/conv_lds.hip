@@ -2743,7 +2743,8 @@ void finish_plan(Plan& p) {
   // tiles (EnhancedCNN 8x8 / 16x16 stages, ResNet-18 7x7) the slab traffic cost what
   // the in-launch combine does (ResNet-18 b64 3.94 vs 3.89 ms), at 16 / 32 tiles the
   // slabs win (EnhancedCNN 4x4 / 2x2 convs 28 / 38 -> 25 / 28 us)
-  p.slab = p.classes == 1 && p.tiles_x < 48 && !slab_env_off();
+  static const int slab_tiles = env_int("LDNN_CONV_SLAB_TILES", 48);   // (A/B knob)
+  p.slab = p.classes == 1 && p.tiles_x < slab_tiles && !slab_env_off();
   p.splits = p.slab ? slab_splits(p.tiles_x, p.nk_all) : small_m_splits(p.tiles_x * p.classes, p.nk_all);
   p.nk_split = (p.nk_all + p.splits - 1) / p.splits;
   p.splits = (p.nk_all + p.nk_split - 1) / p.nk_split;
