@@ -1,6 +1,6 @@
 // Pooled classifier head of the CNNs: global average pool + Linear (<= 16 classes), forward
 // and backward in one launch each (EnhancedCNN: AdaptiveAvgPool2d(1) -> Linear(1024, 10),
-// BAR/model.py:85-87; SURVEY §2 K12 + K13).
+// BAR/model.py:99-100,108-110; SURVEY §2 K12 + K13).
 //
 // At batch 64 the head is 64 x 4 x 1024 activations and a 10 x 1024 weight: pure latency.  The
 // separate path runs gap_fwd + the skinny GEMM forward and colsum + two small GEMMs + gap_bwd
