@@ -1739,6 +1739,9 @@ PYBIND11_MODULE(_C, m) {
         py::arg("dy2") = py::none(), py::arg("pad") = 1);
   m.def("gap_fwd", &gap_fwd);
   m.def("gap_bwd", &gap_bwd);
+  m.def("set_conv_combine_last", &ldnn::set_conv_combine_last,
+        "split-K combine summer: 1 = the tile's last K slice, 0 = the last workgroup to arrive", py::arg("on"));
+  m.def("get_conv_combine_last", &ldnn::get_conv_combine_last);
   m.def("gap_linear_ok", &ldnn::gap_linear_ok, "shapes the fused pooled classifier head takes", py::arg("N"),
         py::arg("HW"), py::arg("C"), py::arg("ncls"));
   m.def("gap_linear_fwd", &gap_linear_fwd, "global average pool + Linear (<= 16 classes) in one launch", py::arg("x"),

@@ -371,7 +371,8 @@ constexpr int kSc1 = 16;  // buffer cache-policy bit: sc1 (write-through / L1 by
 
 template <int NT, int MT, int NTHREADS>
 __device__ __forceinline__ bool splitk_combine(floatx4 (&acc)[NT][MT], float* ws, int* cnt, int tile, int splits,
-                                               int split, char* smem) {
+                                               int split, char* smem, uint64_t* tr = nullptr) {
+  // tr (phase-trace builds, thread 0 only): [4] slab stores drained, [5] ticket drawn, [6] slabs summed
   constexpr uint32_t kSlab = (uint32_t)(NT * MT) * NTHREADS * 16u;
   const int tid = threadIdx.x;
   const uint32_t tile_bytes = kSlab * (uint32_t)splits;
@@ -386,6 +387,7 @@ __device__ __forceinline__ bool splitk_combine(floatx4 (&acc)[NT][MT], float* ws
                                              (int)(own + (uint32_t)((j * MT + i) * NTHREADS * 16)), 0, kSc1);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // EVERY storing wave drains its slab stores
   __syncthreads();
+  if (tr != nullptr) tr[4] = __builtin_amdgcn_s_memrealtime();
   int* flag = reinterpret_cast<int*>(smem);
   if (tid == 0) {
     const int t = __hip_atomic_fetch_add(cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -398,6 +400,7 @@ __device__ __forceinline__ bool splitk_combine(floatx4 (&acc)[NT][MT], float* ws
     *flag = last;
   }
   __syncthreads();
+  if (tr != nullptr) tr[5] = __builtin_amdgcn_s_memrealtime();
   if (*flag == 0) return false;
 #pragma unroll
   for (int j = 0; j < NT; ++j)
@@ -433,6 +436,93 @@ __device__ __forceinline__ bool splitk_combine(floatx4 (&acc)[NT][MT], float* ws
     for (int j = 0; j < NT; ++j)
 #pragma unroll
       for (int i = 0; i < MT; ++i) acc[j][i] += load(s, j, i);
+  }
+  if (tr != nullptr) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    tr[6] = __builtin_amdgcn_s_memrealtime();
+  }
+  return true;
+}
+
+// The same hand-off with a FIXED summer: the tile's last K slice (split == splits - 1).  The
+// other slices deposit their slabs (write-through, drained) and count themselves in; the summer
+// never stores its own partial -- it waits until all the others are in, then adds their slabs to
+// its registers in slice order (deterministic: own + s_0 + s_1 + ...).  That removes the
+// summer's 64 KiB store drain, its ticket and the re-read of its own slab: EnhancedCNN's 16x16 /
+// 8x8 convs measured the last arriver at 2.5 us store drain + 0.7 ticket + 1.3 waiting for the
+// last + 2.5-3.4 summing + 1.4 epilogue (profiles/r5/conv_phase_trace_combine.jsonl).
+// Progress: the summer waits only for workgroups of LOWER linear id (same tile, lower slice) --
+// the dispatcher issues a kernel's workgroups to each XCD in id order, so every workgroup the
+// summer waits for was dispatched before it and waits for nothing itself; a capped spin keeps
+// even a broken assumption from hanging the GPU.  Callers must not remap (tile, slice) to
+// workgroup ids (xcd_split).
+template <int NT, int MT, int NTHREADS>
+__device__ __forceinline__ bool splitk_combine_last(floatx4 (&acc)[NT][MT], float* ws, int* cnt, int tile, int splits,
+                                                    int split, char* smem, uint64_t* tr = nullptr) {
+  constexpr uint32_t kSlab = (uint32_t)(NT * MT) * NTHREADS * 16u;
+  const int tid = threadIdx.x;
+  const uint32_t tile_bytes = kSlab * (uint32_t)(splits - 1);
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      reinterpret_cast<char*>(ws) + (size_t)tile * kSlab * (uint32_t)splits, (short)0, (int)tile_bytes, 0x00020000);
+  if (split != splits - 1) {
+    const uint32_t own = (uint32_t)split * kSlab + (uint32_t)tid * 16u;
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[j][i]), rs,
+                                               (int)(own + (uint32_t)((j * MT + i) * NTHREADS * 16)), 0, kSc1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // EVERY storing wave drains its slab stores
+    __syncthreads();
+    if (tr != nullptr) tr[4] = __builtin_amdgcn_s_memrealtime();
+    if (tid == 0) __hip_atomic_fetch_add(cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return false;
+  }
+  if (tid == 0) {
+    if (tr != nullptr) tr[4] = __builtin_amdgcn_s_memrealtime();
+    for (int spin = 0; spin < (1 << 22); ++spin) {
+      if (__hip_atomic_load(cnt + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= splits - 1) break;
+      __builtin_amdgcn_s_sleep(2);
+    }
+    __hip_atomic_store(cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  if (tr != nullptr) tr[5] = __builtin_amdgcn_s_memrealtime();
+  auto load = [&](int s, int j, int i) {
+    const uint32_t o = (uint32_t)s * kSlab + (uint32_t)tid * 16u;
+    return __builtin_bit_cast(
+        floatx4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(o + (uint32_t)((j * MT + i) * NTHREADS * 16)), 0,
+                                                       kSc1));
+  };
+  const int nother = splits - 1;
+  int s = 0;
+  if constexpr (NT * MT <= 16) {
+    for (; s + 1 < nother; s += 2) {
+      floatx4 t0[NT][MT], t1[NT][MT];
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int i = 0; i < MT; ++i) {
+          t0[j][i] = load(s, j, i);
+          t1[j][i] = load(s + 1, j, i);
+        }
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int i = 0; i < MT; ++i) acc[j][i] += t0[j][i] + t1[j][i];
+    }
+  }
+  for (; s < nother; ++s) {
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int i = 0; i < MT; ++i) acc[j][i] += load(s, j, i);
+  }
+  if (tr != nullptr) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    tr[6] = __builtin_amdgcn_s_memrealtime();
   }
   return true;
 }

@@ -147,6 +147,9 @@ int get_conv_hb();
 void set_conv_ws(int mode);  // see conv_lds.hip ws_env
 int get_conv_ws();
 // phase-trace buffer ([workgroup][4] uint64) of the LDNN_CONV_XF=32 diagnostic build (nullptr: off)
+// in-launch split-K combine of the LDS-DMA convs: 1 = the tile's last K slice sums, 0 = the last arrival
+void set_conv_combine_last(int on);
+int get_conv_combine_last();
 void set_conv_trace(uint64_t* buf);
 int get_conv_halo();
 

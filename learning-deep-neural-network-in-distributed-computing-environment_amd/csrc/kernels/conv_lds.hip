@@ -76,7 +76,8 @@ struct LArgs {
   int bf16_rows;     // bf16 outputs (fwd y, stride-1 dgrad dx) through the row-coalesced LDS epilogue
   int remap_rows;    // stride-2 dgrad dx (class row remap) through the row-coalesced LDS epilogue
   int xcd_split;     // split-K grids: the tiles of one K slice share an XCD (see split_coords)
-  uint64_t* trace;   // XF bit 5 (phase-trace builds): [workgroup][4] s_memrealtime stamps
+  uint64_t* trace;   // XF bit 5 (phase-trace builds): [workgroup][8] s_memrealtime stamps
+  int combine_last;  // in-launch split-K: the last K slice sums (splitk_combine_last), else the last arrival
 };
 
 // (tile, K slice) of this workgroup.  Default: tile = blockIdx.x, slice = blockIdx.y.  With
@@ -639,7 +640,15 @@ __device__ __forceinline__ void conv_tail(const LArgs& a, const Geo& g, floatx4 
     if (combine) {
       lds_barrier();  // every wave is done with the operand stages (the ticket word lives there)
       const int tile = blockIdx.z * a.tiles_x + bx;
-      if (!splitk_combine<4, 4, NW * 64>(acc, a.ws, a.cnt, tile, gridDim.y, by, smem)) return;
+      // (phase-trace builds: stamps 4..6 of this workgroup's trace row, see splitk_combine)
+      uint64_t* tr = (a.trace != nullptr && threadIdx.x == 0)
+                         ? a.trace + 8 * (size_t)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z))
+                         : nullptr;
+      if (a.xcd_split || !a.combine_last) {
+        if (!splitk_combine<4, 4, NW * 64>(acc, a.ws, a.cnt, tile, gridDim.y, by, smem, tr)) return;
+      } else if (!splitk_combine_last<4, 4, NW * 64>(acc, a.ws, a.cnt, tile, gridDim.y, by, smem, tr)) {
+        return;
+      }
     } else if (a.ws != nullptr) {
       // wgrad, and small-M fwd / stride-1 dgrad: this slice's fp32 partial tile into
       // its own slab; a separate chip-wide kernel sums the slabs (slab_sum_kernel /
@@ -748,7 +757,7 @@ __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void conv_lds_kernel(LArgs a,
   uint64_t* trace = nullptr;
   if constexpr ((XF & 32) != 0) {
     if (threadIdx.x == 0 && a.trace != nullptr) {
-      trace = a.trace + 4 * (size_t)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z));
+      trace = a.trace + 8 * (size_t)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z));
       trace[0] = __builtin_amdgcn_s_memrealtime();
     }
   }
@@ -912,7 +921,7 @@ __global__ __launch_bounds__(256, 2) void conv_halo_kernel(LArgs a, const bf16_t
   uint64_t* trace = nullptr;
   if constexpr ((XF & 32) != 0) {
     if (threadIdx.x == 0 && a.trace != nullptr) {
-      trace = a.trace + 4 * (size_t)(blockIdx.x + gridDim.x * blockIdx.y);
+      trace = a.trace + 8 * (size_t)(blockIdx.x + gridDim.x * blockIdx.y);
       trace[0] = __builtin_amdgcn_s_memrealtime();
     }
   }
@@ -1271,7 +1280,7 @@ __global__ __launch_bounds__(256, 1) void conv_ws64_kernel(LArgs a, const bf16_t
   uint64_t* trace = nullptr;
   if constexpr ((XF & 32) != 0) {
     if (threadIdx.x == 0 && a.trace != nullptr) {
-      trace = a.trace + 4 * (size_t)blockIdx.x;
+      trace = a.trace + 8 * (size_t)blockIdx.x;
       trace[0] = __builtin_amdgcn_s_memrealtime();
     }
   }
@@ -1972,7 +1981,7 @@ __global__ __launch_bounds__(256, 1) void conv_patch_ws_kernel(LArgs a, const bf
   uint64_t* trace = nullptr;
   if constexpr ((XF & 32) != 0) {
     if (threadIdx.x == 0 && a.trace != nullptr) {
-      trace = a.trace + 4 * (size_t)blockIdx.x;
+      trace = a.trace + 8 * (size_t)blockIdx.x;
       trace[0] = __builtin_amdgcn_s_memrealtime();
     }
   }
@@ -2441,9 +2450,18 @@ int remap_rows_env() {
 
 uint64_t* g_conv_trace = nullptr;  // phase-trace buffer of LDNN_CONV_XF=32 builds (set_conv_trace)
 
+// LDNN_CONV_COMBINE_LAST (A/B knob, default 1): the in-launch split-K combine's summer is the
+// tile's last K slice (splitk_combine_last) instead of the last workgroup to arrive
+int g_combine_last = -1;   // set_conv_combine_last (tests), else LDNN_CONV_COMBINE_LAST
+int combine_last_env() {
+  if (g_combine_last < 0) g_combine_last = env_int("LDNN_CONV_COMBINE_LAST", 1);
+  return g_combine_last;
+}
+
 LArgs base_args(const ConvShape& s) {
   LArgs a{};
   a.trace = g_conv_trace;
+  a.combine_last = combine_last_env();
   a.tap_major = tap_major_env();
   a.f32_rows = f32_rows_env();
   a.bf16_rows = bf16_rows_env();
@@ -2831,6 +2849,8 @@ int get_conv_hb() { return hb_env(); }
 void set_conv_ws(int mode) { g_conv_ws = mode; }
 int get_conv_ws() { return ws_env(); }
 void set_conv_trace(uint64_t* buf) { g_conv_trace = buf; }
+void set_conv_combine_last(int on) { g_combine_last = on; }
+int get_conv_combine_last() { return combine_last_env(); }
 void set_conv_wgrad_ring(int mode) { g_wgrad_ring = mode; }
 int get_conv_halo() { return halo_env(); }
 

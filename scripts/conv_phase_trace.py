@@ -40,7 +40,7 @@ def main():
     a = ap.parse_args()
     C = _ext._C
     assert C is not None and os.environ.get("LDNN_CONV_XF") == "32"
-    tr = torch.zeros(1 << 16, 4, dtype=torch.int64, device="cuda")
+    tr = torch.zeros(1 << 16, 8, dtype=torch.int64, device="cuda")
     C.set_conv_trace(tr)
     N = a.batch
     for (Ci, H, K, R, st, pad) in SHAPES[a.model]:
@@ -82,6 +82,17 @@ def main():
                    # tail spread: a split-K hand-off's last-arriving workgroup also sums the slabs
                    "tail_p10_p90": [pct((t[ok, 3] - t[ok, 2]).tolist(), 0.1), pct((t[ok, 3] - t[ok, 2]).tolist(), 0.9)],
                    "loop_p10_p90": [pct((t[ok, 2] - t[ok, 1]).tolist(), 0.1), pct((t[ok, 2] - t[ok, 1]).tolist(), 0.9)]}
+            # split-K combine phases (stamps 4..6): slab stores drained, ticket drawn, slabs summed (summer)
+            cb = ok & (t[:, 4] > 0)
+            if cb.any():
+                sm = cb & (t[:, 6] > 0)
+                rec["combine"] = {"store_drain_us": round(med((t[cb, 4] - t[cb, 2]).tolist()), 2),
+                                  "ticket_us": round(med((t[cb, 5] - t[cb, 4]).tolist()), 2),
+                                  "summers": int(sm.sum().item()),
+                                  "sum_loads_us": round(med((t[sm, 6] - t[sm, 5]).tolist()), 2) if sm.any() else None,
+                                  "epilogue_us": round(med((t[sm, 3] - t[sm, 6]).tolist()), 2) if sm.any() else None,
+                                  "summer_tail_us": round(med((t[sm, 3] - t[sm, 2]).tolist()), 2) if sm.any() else None,
+                                  "summer_wait_for_last_us": round(med((t[sm, 5] - t[sm, 4]).tolist()), 2) if sm.any() else None}
             print(json.dumps(rec), flush=True)
     C.set_conv_trace(None)
 

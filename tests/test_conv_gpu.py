@@ -421,3 +421,47 @@ def test_slab_split_conv_fused_bn_statistics(N, C, H, K):
     torch.testing.assert_close(si, torch.rsqrt(var + 1e-5), rtol=1e-3, atol=1e-4)
     torch.testing.assert_close(rm, 0.1 * mean, rtol=1e-3, atol=1e-5)
     torch.testing.assert_close(rv, 0.9 + 0.1 * yb.var(0, unbiased=True), rtol=1e-3, atol=1e-5)
+
+
+@pytest.mark.parametrize("N,C,H,K,stride", [(64, 128, 16, 128, 1), (64, 256, 8, 256, 1), (64, 128, 16, 256, 2),
+                                            (8, 512, 7, 512, 1), (5, 192, 9, 320, 1)])
+def test_fixed_summer_split_k_combine_matches_last_arrival(N, C, H, K, stride):
+    """In-launch split-K hand-off with the tile's LAST K slice as the summer (it never stores or
+    re-reads its own partial) == the last-arrival summer and the fp32 reference, fwd (with the
+    next BN's statistics) and dgrad (stride-2: parity classes); repeated launches give the same
+    output bits (the counters are left zero)."""
+    torch.manual_seed(29)
+    Cc = _ext.C()
+    x = torch.randn(N, H, H, C, device="cuda").bfloat16()
+    w = (torch.randn(K, 3, 3, C, device="cuda") * (1.0 / (C * 9) ** 0.5)).bfloat16()
+    P = (H + 2 - 3) // stride + 1
+    gy = torch.randn(N, P, P, K, device="cuda").bfloat16()
+    res = {}
+    old = Cc.get_conv_combine_last()
+    try:
+        for mode in (0, 1, 1):
+            Cc.set_conv_combine_last(mode)
+            y = torch.empty(N, P, P, K, device="cuda", dtype=torch.bfloat16)
+            ws = torch.zeros(Cc.bn_workspace_floats(K), device="cuda")
+            sm, si = torch.zeros(K, device="cuda"), torch.zeros(K, device="cuda")
+            Cc.conv_fwd(x, w, y, stride, 1, bn_ws=ws, bn_save_mean=sm, bn_save_invstd=si)
+            dx = torch.empty_like(x)
+            Cc.conv_dgrad(gy, w, dx, stride, 1)
+            torch.cuda.synchronize()
+            res.setdefault(mode, []).append((y.float(), sm, si, dx.float()))
+    finally:
+        Cc.set_conv_combine_last(old)
+    for k in (0, 3):   # fixed summer: the same output bits launch to launch
+        assert torch.equal(res[1][0][k], res[1][1][k])
+    for k in (1, 2):   # (the BN statistics' fp32 atomics: arrival order)
+        torch.testing.assert_close(res[1][0][k], res[1][1][k], rtol=1e-5, atol=1e-6)
+    for a, b in zip(res[1][0], res[0][0]):   # vs the last-arrival summer: same sums, another order
+        torch.testing.assert_close(a, b, rtol=2e-2, atol=1e-2 * b.abs().max().item())
+    xf, wf, gyf = x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), gy.float().permute(0, 3, 1, 2)
+    yr = torch.nn.functional.conv2d(xf, wf, stride=stride, padding=1).permute(0, 2, 3, 1)
+    dxr = torch.nn.grad.conv2d_input(xf.shape, wf, gyf, stride=stride, padding=1).permute(0, 2, 3, 1)
+    y1, sm1, si1, dx1 = res[1][0]
+    torch.testing.assert_close(y1, yr, rtol=1e-2, atol=1e-2 * yr.abs().max().item())
+    torch.testing.assert_close(dx1, dxr, rtol=1e-2, atol=1e-2 * dxr.abs().max().item())
+    yb = y1.reshape(-1, K)
+    torch.testing.assert_close(sm1, yb.mean(0), rtol=1e-3, atol=1e-4)
