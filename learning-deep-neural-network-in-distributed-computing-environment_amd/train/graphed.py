@@ -29,10 +29,49 @@ from Python between the graphs of a chain: GraphedDPStep below), static shapes
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from ..optim.optimizers import _FlatOptimizer
 from .static_mlp import no_gc
+
+# LDNN_NHWC_INPUT=0: the graph's static input stays an NCHW copy of the batch (A/B knob)
+NHWC_INPUT = os.environ.get("LDNN_NHWC_INPUT", "1") == "1"
+
+
+def static_input(model, x_example: torch.Tensor):
+    """The graph's static input buffer and its per-step staging function.
+
+    For a conv net whose first layer is an ldnn Conv2d (it reads dense NHWC bf16 with the
+    channels padded to 8), the buffer IS that padded NHWC image, seen as a logical NCHW view:
+    the per-step staging is one native pass from the caller's NCHW batch (layout + cast +
+    zeroed pad channels) and the replayed graph starts at the first conv -- no device copy
+    of the batch and no layout pass inside the graph (ResNet-18 b256: a 77 MB copy and a
+    56 us conversion became one pass).  Anything else: a plain copy into a clone."""
+    from ..models.layers import Conv2d
+    from ..ops import _ext
+    from ..ops import functional as LF
+
+    x = x_example
+    first = next((m for m in model.modules() if next(m.children(), None) is None), None)
+    if (NHWC_INPUT and x.dim() == 4 and x.is_contiguous() and x.dtype in (torch.float32, torch.bfloat16)
+            and isinstance(first, Conv2d) and _ext.use_native(x)):
+        N, C, H, W = x.shape
+        fl = getattr(first, "_ldnn_flat", None)   # the channel padding the conv's weight shadow uses
+        cp = fl.shadow_storage(first.weight).shape[3] if fl is not None and fl.shadow is not None else LF._up8(C)
+        buf = torch.empty(N, H, W, cp, dtype=torch.bfloat16, device=x.device)
+        C_ = _ext.C()
+        C_.nchw_to_nhwc(x, buf)
+        xs = LF.nchw_view(buf, C)
+        xs._ldnn_zpad = True   # the staging pass writes the pad channels' zeros
+
+        def stage(xn: torch.Tensor):
+            C_.nchw_to_nhwc(xn if xn.is_contiguous() else xn.contiguous(), buf)
+        return xs, stage
+
+    xs = x.detach().clone()
+    return xs, lambda xn: xs.copy_(xn, non_blocking=True)
 
 
 # (An optimizer overlapped with the backward on a side-stream branch of the step
@@ -47,7 +86,7 @@ class GraphedStep:
         if not x_example.is_cuda:
             raise ValueError("GraphedStep needs GPU tensors")
         self.model, self.criterion, self.optimizer = model, criterion, optimizer
-        self.x = x_example.detach().clone()
+        self.x, self._stage_x = static_input(model, x_example)
         self.y = y_example.detach().clone()
         self.stats = stats if stats is not None else torch.zeros(2, dtype=torch.float32, device=self.x.device)
         self._lrs = None
@@ -109,7 +148,7 @@ class GraphedStep:
         """One training step on (x, y); returns the (device) loss tensor of this step."""
         if x.shape != self.x.shape or y.shape != self.y.shape:
             return self._eager_step(x, y)
-        self.x.copy_(x, non_blocking=True)
+        self._stage_x(x)
         self.y.copy_(y, non_blocking=True)
         self._sync_lr()
         self.graph.replay()
@@ -179,7 +218,7 @@ class GraphedDPStep:
         self.bk, self.flat, self.comm = dp.bucketer, dp.flat, dp.comm
         self._SUM = SUM
         self.comm_fn = comm_fn
-        self.x = x_example.detach().clone()
+        self.x, self._stage_x = static_input(self.model, x_example)
         self.y = y_example.detach().clone()
         self.stats = stats if stats is not None else torch.zeros(2, dtype=torch.float32, device=self.x.device)
         self._lrs = None
@@ -381,7 +420,7 @@ class GraphedDPStep:
     def __call__(self, x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
         if x.shape != self.x.shape or y.shape != self.y.shape:
             return self._eager_step(x, y)
-        self.x.copy_(x, non_blocking=True)
+        self._stage_x(x)
         self.y.copy_(y, non_blocking=True)
         self._sync_lr()
         works = {}
