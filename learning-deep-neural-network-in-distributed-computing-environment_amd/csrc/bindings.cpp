@@ -1525,7 +1525,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("tile") = 0, py::arg("splitk") = 0, py::arg("direct_epi") = false, py::arg("variant") = 0,
         py::arg("ws") = py::none(), py::arg("cnt") = py::none(), py::arg("mask_out") = py::none(),
         py::arg("mask_in") = py::none(), py::arg("head_w") = py::none(), py::arg("head_part") = py::none());
-  m.def("nchw_to_nhwc", [](const at::Tensor& src, const at::Tensor& dst) {
+  m.def("nchw_to_nhwc", [](const at::Tensor& src, const at::Tensor& dst, const c10::optional<at::Tensor>& extra_src,
+                           const c10::optional<at::Tensor>& extra_dst) {
         TORCH_CHECK(src.is_cuda() && src.dim() == 4 && src.is_contiguous() &&
                         (src.scalar_type() == at::kFloat || src.scalar_type() == at::kBFloat16),
                     "nchw_to_nhwc: src must be a contiguous NCHW fp32 / bf16 CUDA tensor");
@@ -1534,11 +1535,25 @@ PYBIND11_MODULE(_C, m) {
         TORCH_CHECK(dst.dim() == 4 && dst.is_contiguous() && dst.size(0) == N && dst.size(1) == H && dst.size(2) == W &&
                         dst.size(3) >= C && dst.size(3) % 8 == 0 && aligned16(dst.data_ptr()),
                     "nchw_to_nhwc: dst must be contiguous [N][H][W][cp], cp >= C, cp % 8 == 0");
+        const void* es = nullptr;
+        void* ed = nullptr;
+        int64_t eb = 0;
+        if (extra_src.has_value() || extra_dst.has_value()) {   // e.g. the batch's labels, copied in the same launch
+          TORCH_CHECK(extra_src.has_value() && extra_dst.has_value() && extra_src->is_cuda() && extra_dst->is_cuda() &&
+                          extra_src->is_contiguous() && extra_dst->is_contiguous() &&
+                          extra_src->nbytes() == extra_dst->nbytes() && extra_src->nbytes() % 8 == 0 &&
+                          ((uintptr_t)extra_src->data_ptr() & 7) == 0 && ((uintptr_t)extra_dst->data_ptr() & 7) == 0,
+                      "nchw_to_nhwc: extra_src / extra_dst must be contiguous GPU tensors of the same size, 8-B multiples");
+          es = extra_src->data_ptr();
+          ed = extra_dst->data_ptr();
+          eb = (int64_t)extra_src->nbytes();
+        }
         c10::hip::HIPGuardMasqueradingAsCUDA g(src.device());
         check(ldnn::nchw_to_nhwc(src.data_ptr(), src.scalar_type() == at::kFloat, bf16_mut(dst), (int)N, (int)C,
-                                 (int)(H * W), (int)dst.size(3), cur_stream(src)),
+                                 (int)(H * W), (int)dst.size(3), cur_stream(src), es, ed, eb),
               "nchw_to_nhwc");
-      }, "NCHW fp32/bf16 -> NHWC bf16 with zeroed pad channels", py::arg("src"), py::arg("dst"));
+      }, "NCHW fp32/bf16 -> NHWC bf16 with zeroed pad channels (+ an extra same-launch copy, e.g. labels)",
+      py::arg("src"), py::arg("dst"), py::arg("extra_src") = py::none(), py::arg("extra_dst") = py::none());
   m.def("transpose_bf16", [](const at::Tensor& in, const at::Tensor& out) {
         check_dev(in, at::kBFloat16, "in");
         check_dev(out, at::kBFloat16, "out");

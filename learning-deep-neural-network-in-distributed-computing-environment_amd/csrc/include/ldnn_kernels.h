@@ -248,7 +248,8 @@ hipError_t zero2d_f32(float* p, int rows, int cols, int ld, hipStream_t s);
 // out[c][r] = in[r][c], bf16, rows / cols / strides multiples of 8
 hipError_t transpose_bf16(const uint16_t* in, uint16_t* out, int rows, int cols, int ldi, int ldo, hipStream_t s);
 // NCHW (fp32 / bf16) -> NHWC bf16 [N][HW][cp], pad channels zeroed (cp % 8 == 0)
-hipError_t nchw_to_nhwc(const void* src, bool src_f32, uint16_t* dst, int N, int C, int HW, int cp, hipStream_t s);
+hipError_t nchw_to_nhwc(const void* src, bool src_f32, uint16_t* dst, int N, int C, int HW, int cp, hipStream_t s,
+                        const void* extra_src = nullptr, void* extra_dst = nullptr, int64_t extra_bytes = 0);
 // sum split-K slabs [splits][rows][ldw] into out[rows][ncols] (stride ldo); extra[r] = column ncols
 hipError_t slab_sum_cols(const float* ws, int splits, int rows, int ldw, float* out, int ldo, int ncols, float* extra,
                          hipStream_t s);

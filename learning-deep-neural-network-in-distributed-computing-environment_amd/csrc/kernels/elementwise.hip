@@ -165,8 +165,11 @@ __global__ void zero2d_kernel(float* __restrict__ p, int rows, int cols, int ld)
 // zero fill + permute copy (two ATen launches, ~3x the bytes) at every CNN input.
 template <typename T>
 __global__ __launch_bounds__(256) void nchw_to_nhwc_kernel(const T* __restrict__ src, bf16_t* __restrict__ dst,
-                                                           int64_t total, int C, int HW, int groups) {
+                                                           int64_t total, int C, int HW, int groups,
+                                                           const uint2* __restrict__ esrc, uint2* __restrict__ edst,
+                                                           int64_t e8) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < e8) edst[i] = esrc[i];   // a batch's labels staged in the same launch (8-B pieces)
   if (i >= total) return;
   const int g = (int)(i % groups);
   const int64_t pix = i / groups;
@@ -334,16 +337,21 @@ hipError_t act_bwd(const uint16_t* dy, const uint16_t* y, uint16_t* dx, int64_t 
   return hipGetLastError();
 }
 
-hipError_t nchw_to_nhwc(const void* src, bool src_f32, uint16_t* dst, int N, int C, int HW, int cp, hipStream_t s) {
+hipError_t nchw_to_nhwc(const void* src, bool src_f32, uint16_t* dst, int N, int C, int HW, int cp, hipStream_t s,
+                        const void* extra_src, void* extra_dst, int64_t extra_bytes) {
   if (N <= 0 || HW <= 0) return hipSuccess;
   if (cp % 8 || cp < C || C <= 0) return hipErrorInvalidValue;
+  if (extra_bytes % 8 || ((uintptr_t)extra_src & 7) || ((uintptr_t)extra_dst & 7)) return hipErrorInvalidValue;
   const int groups = cp / 8;
   const int64_t total = (int64_t)N * HW * groups;
-  const unsigned g = (unsigned)((total + 255) / 256);
+  const int64_t e8 = extra_bytes / 8;
+  const unsigned g = (unsigned)((std::max(total, e8) + 255) / 256);
+  const uint2* es = static_cast<const uint2*>(extra_src);
+  uint2* ed = static_cast<uint2*>(extra_dst);
   if (src_f32)
-    nchw_to_nhwc_kernel<float><<<g, 256, 0, s>>>(static_cast<const float*>(src), dst, total, C, HW, groups);
+    nchw_to_nhwc_kernel<float><<<g, 256, 0, s>>>(static_cast<const float*>(src), dst, total, C, HW, groups, es, ed, e8);
   else
-    nchw_to_nhwc_kernel<bf16_t><<<g, 256, 0, s>>>(static_cast<const bf16_t*>(src), dst, total, C, HW, groups);
+    nchw_to_nhwc_kernel<bf16_t><<<g, 256, 0, s>>>(static_cast<const bf16_t*>(src), dst, total, C, HW, groups, es, ed, e8);
   return hipGetLastError();
 }
 

@@ -40,15 +40,24 @@ from .static_mlp import no_gc
 NHWC_INPUT = os.environ.get("LDNN_NHWC_INPUT", "1") == "1"
 
 
+def unit_seed(device) -> torch.Tensor:
+    """A persistent fp32 scalar 1 for ``loss.backward(seed)``: no fill launch for the seed, and
+    marked so the native loss backward skips multiplying its gradient by it."""
+    one = torch.ones((), dtype=torch.float32, device=device)
+    one._ldnn_unit = True
+    return one
+
+
 def static_input(model, x_example: torch.Tensor):
     """The graph's static input buffer and its per-step staging function.
 
     For a conv net whose first layer is an ldnn Conv2d (it reads dense NHWC bf16 with the
     channels padded to 8), the buffer IS that padded NHWC image, seen as a logical NCHW view:
     the per-step staging is one native pass from the caller's NCHW batch (layout + cast +
-    zeroed pad channels) and the replayed graph starts at the first conv -- no device copy
-    of the batch and no layout pass inside the graph (ResNet-18 b256: a 77 MB copy and a
-    56 us conversion became one pass).  Anything else: a plain copy into a clone."""
+    zeroed pad channels, the labels copied in the same launch) and the replayed graph starts at
+    the first conv -- no device copy of the batch and no layout pass inside the graph (ResNet-18
+    b256: a 77 MB copy and a 56 us conversion became one pass).  Anything else: plain copies
+    into a clone.  The staging function takes (x, y, y_static)."""
     from ..models.layers import Conv2d
     from ..ops import _ext
     from ..ops import functional as LF
@@ -66,12 +75,22 @@ def static_input(model, x_example: torch.Tensor):
         xs = LF.nchw_view(buf, C)
         xs._ldnn_zpad = True   # the staging pass writes the pad channels' zeros
 
-        def stage(xn: torch.Tensor):
-            C_.nchw_to_nhwc(xn if xn.is_contiguous() else xn.contiguous(), buf)
+        def stage(xn: torch.Tensor, yn: torch.Tensor, ys: torch.Tensor):
+            xn = xn if xn.is_contiguous() else xn.contiguous()
+            if (yn.is_cuda and yn.is_contiguous() and yn.dtype == ys.dtype and yn.nbytes % 8 == 0
+                    and yn.data_ptr() % 8 == 0):   # the labels ride along in the same launch
+                C_.nchw_to_nhwc(xn, buf, yn, ys)
+            else:
+                C_.nchw_to_nhwc(xn, buf)
+                ys.copy_(yn, non_blocking=True)
         return xs, stage
 
     xs = x.detach().clone()
-    return xs, lambda xn: xs.copy_(xn, non_blocking=True)
+
+    def copy(xn: torch.Tensor, yn: torch.Tensor, ys: torch.Tensor):
+        xs.copy_(xn, non_blocking=True)
+        ys.copy_(yn, non_blocking=True)
+    return xs, copy
 
 
 # (An optimizer overlapped with the backward on a side-stream branch of the step
@@ -90,8 +109,9 @@ class GraphedStep:
         self.y = y_example.detach().clone()
         self.stats = stats if stats is not None else torch.zeros(2, dtype=torch.float32, device=self.x.device)
         self._lrs = None
-        # persistent d(loss)/d(loss) = 1: the captured backward needs no seed fill launch
-        self._one = torch.ones((), dtype=torch.float32, device=self.x.device)
+        # persistent d(loss)/d(loss) = 1: the captured backward needs no seed fill launch, and
+        # the loss backward knows it scales by exactly 1 (no scaling pass: _SoftmaxXentNative)
+        self._one = unit_seed(self.x.device)
         s = torch.cuda.Stream(device=self.x.device)
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
@@ -148,8 +168,7 @@ class GraphedStep:
         """One training step on (x, y); returns the (device) loss tensor of this step."""
         if x.shape != self.x.shape or y.shape != self.y.shape:
             return self._eager_step(x, y)
-        self._stage_x(x)
-        self.y.copy_(y, non_blocking=True)
+        self._stage_x(x, y, self.y)
         self._sync_lr()
         self.graph.replay()
         return self.loss
@@ -220,6 +239,7 @@ class GraphedDPStep:
         self.comm_fn = comm_fn
         self.x, self._stage_x = static_input(self.model, x_example)
         self.y = y_example.detach().clone()
+        self._one = unit_seed(self.x.device)
         self.stats = stats if stats is not None else torch.zeros(2, dtype=torch.float32, device=self.x.device)
         self._lrs = None
         self.device_collectives = bool(getattr(self.comm, "device_collectives", False))
@@ -263,7 +283,7 @@ class GraphedDPStep:
                     loss = self.criterion(out, self.y, self.stats)
                 except TypeError:
                     loss = self.criterion(out.float(), self.y)
-                loss.backward()
+                loss.backward(self._one if loss.dtype == torch.float32 and loss.dim() == 0 else None)
                 rest = [i for i in range(nb) if not self._cap["fired"][i]]   # params with no gradient
                 if rest:
                     self._fire(rest)
@@ -420,8 +440,7 @@ class GraphedDPStep:
     def __call__(self, x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
         if x.shape != self.x.shape or y.shape != self.y.shape:
             return self._eager_step(x, y)
-        self._stage_x(x)
-        self.y.copy_(y, non_blocking=True)
+        self._stage_x(x, y, self.y)
         self._sync_lr()
         works = {}
         for j, g in enumerate(self.graphs):
