@@ -1088,31 +1088,43 @@ void bn_bwd(const at::Tensor& x, const at::Tensor& y, const at::Tensor& dy, cons
 
 // x [N][H][W][C], y [N][P][Q][C] dense bf16; argmax uint8 [N][P][Q][C] for max pooling
 void pool_fwd(const at::Tensor& x, const at::Tensor& y, const c10::optional<at::Tensor>& argmax, int64_t R,
-              int64_t S, int64_t stride, int64_t pad, bool is_max) {
+              int64_t S, int64_t stride, int64_t pad, bool is_max, bool nchw_out) {
   check_dev(x, at::kBFloat16, "x");
   check_dev(y, at::kBFloat16, "y");
   TORCH_CHECK(x.dim() == 4 && y.dim() == 4 && x.is_contiguous() && y.is_contiguous(), "pool: dense NHWC");
+  // nchw_out: y is [N][Cl][P][Q] (Cl <= C logical channels), argmax keeps the NHWC [N][P][Q][C] layout
+  const int64_t P = nchw_out ? y.size(2) : y.size(1), Q = nchw_out ? y.size(3) : y.size(2);
+  const int64_t cl = nchw_out ? y.size(1) : 0;
+  TORCH_CHECK(y.size(0) == x.size(0) && (nchw_out ? cl <= x.size(3) : y.size(3) == x.size(3)), "pool: y shape");
   uint8_t* am = nullptr;
   if (is_max) {
-    TORCH_CHECK(argmax.has_value() && argmax->scalar_type() == at::kByte && argmax->numel() == y.numel(),
+    TORCH_CHECK(argmax.has_value() && argmax->scalar_type() == at::kByte &&
+                    argmax->numel() == x.size(0) * P * Q * x.size(3),
                 "pool: max pooling needs a uint8 argmax tensor");
     am = argmax->data_ptr<uint8_t>();
     TORCH_CHECK(argmax->is_contiguous() && ((uintptr_t)am & 7) == 0, "pool: argmax must be dense and 8-B aligned");
   }
   check(ldnn::pool2d_fwd(bf16_ptr(x), bf16_mut(y), am, (int)x.size(0), (int)x.size(1), (int)x.size(2),
-                         (int)x.size(3), (int)y.size(1), (int)y.size(2), (int)R, (int)S, (int)stride, (int)pad, is_max,
-                         cur_stream(x)),
+                         (int)x.size(3), (int)P, (int)Q, (int)R, (int)S, (int)stride, (int)pad, is_max,
+                         cur_stream(x), (int)cl),
         "pool2d_fwd");
 }
 
 void pool_bwd(const at::Tensor& dy, const c10::optional<at::Tensor>& argmax, const at::Tensor& dx, int64_t R,
-              int64_t S, int64_t stride, int64_t pad, bool is_max, const c10::optional<at::Tensor>& dy2) {
+              int64_t S, int64_t stride, int64_t pad, bool is_max, const c10::optional<at::Tensor>& dy2,
+              bool nchw_dy) {
   check_dev(dy, at::kBFloat16, "dy");
   check_dev(dx, at::kBFloat16, "dx");
-  TORCH_CHECK(dy.is_contiguous() && dx.is_contiguous(), "pool_bwd: dense NHWC");
+  TORCH_CHECK(dy.dim() == 4 && dx.dim() == 4 && dy.is_contiguous() && dx.is_contiguous(), "pool_bwd: dense NHWC");
+  // nchw_dy: dy is [N][Cl][P][Q] (the NCHW output of pool_fwd(nchw_out=True))
+  const int64_t P = nchw_dy ? dy.size(2) : dy.size(1), Q = nchw_dy ? dy.size(3) : dy.size(2);
+  const int64_t cl = nchw_dy ? dy.size(1) : 0;
+  TORCH_CHECK(dy.size(0) == dx.size(0) && (nchw_dy ? cl <= dx.size(3) : dy.size(3) == dx.size(3)),
+              "pool_bwd: dy shape");
+  TORCH_CHECK(!(nchw_dy && dy2.has_value()), "pool_bwd: dy2 needs the NHWC gradient");
   const uint8_t* am = nullptr;
   if (is_max) {
-    TORCH_CHECK(argmax.has_value() && argmax->numel() == dy.numel(), "pool_bwd: argmax");
+    TORCH_CHECK(argmax.has_value() && argmax->numel() == dx.size(0) * P * Q * dx.size(3), "pool_bwd: argmax");
     am = argmax->data_ptr<uint8_t>();
     TORCH_CHECK(argmax->is_contiguous() && ((uintptr_t)am & 7) == 0, "pool: argmax must be dense and 8-B aligned");
   }
@@ -1123,8 +1135,8 @@ void pool_bwd(const at::Tensor& dy, const c10::optional<at::Tensor>& argmax, con
     d2 = bf16_ptr(*dy2);
   }
   check(ldnn::pool2d_bwd(bf16_ptr(dy), am, bf16_mut(dx), (int)dx.size(0), (int)dx.size(1), (int)dx.size(2),
-                         (int)dx.size(3), (int)dy.size(1), (int)dy.size(2), (int)R, (int)S, (int)stride, (int)pad,
-                         is_max, cur_stream(dy), d2),
+                         (int)dx.size(3), (int)P, (int)Q, (int)R, (int)S, (int)stride, (int)pad,
+                         is_max, cur_stream(dy), d2, (int)cl),
         "pool2d_bwd");
 }
 
@@ -1729,9 +1741,11 @@ PYBIND11_MODULE(_C, m) {
         py::arg("gamma"), py::arg("save_mean"), py::arg("save_invstd"), py::arg("ws"), py::arg("dgamma"),
         py::arg("dbeta"), py::arg("relu"), py::arg("mask") = py::none(), py::arg("grad_assign") = false,
         py::arg("dy2") = py::none());
-  m.def("pool_fwd", &pool_fwd);
+  m.def("pool_fwd", &pool_fwd, py::arg("x"), py::arg("y"), py::arg("argmax"), py::arg("R"), py::arg("S"),
+        py::arg("stride"), py::arg("pad"), py::arg("is_max"), py::arg("nchw_out") = false);
   m.def("pool_bwd", &pool_bwd, py::arg("dy"), py::arg("argmax"), py::arg("dx"), py::arg("R"), py::arg("S"),
-        py::arg("stride"), py::arg("pad"), py::arg("is_max"), py::arg("dy2") = py::none());
+        py::arg("stride"), py::arg("pad"), py::arg("is_max"), py::arg("dy2") = py::none(),
+        py::arg("nchw_dy") = false);
   m.def("bn_dual_fwd", &bn_dual_fwd, "y = relu(bn_a(x) + bn_b(r)) in one pass (the shortcut BN output never stored)",
         py::arg("x"), py::arg("r"), py::arg("y"), py::arg("mask"), py::arg("gamma_a"), py::arg("beta_a"),
         py::arg("rm_a"), py::arg("rv_a"), py::arg("mean_a"), py::arg("invstd_a"), py::arg("ws_a"), py::arg("eps_a"),

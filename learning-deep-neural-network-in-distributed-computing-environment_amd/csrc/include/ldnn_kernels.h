@@ -226,10 +226,11 @@ hipError_t bn_maxpool_backward(const BnArgs& a, int N, int H, int W, int P, int 
                                const uint8_t* arg, uint16_t* dx, float* dgamma, float* dbeta, hipStream_t s,
                                bool grad_assign = false);
 hipError_t pool2d_fwd(const uint16_t* x, uint16_t* y, uint8_t* argmax, int N, int H, int W, int C, int P, int Q,
-                      int R, int S, int stride, int pad, bool is_max, hipStream_t s);
+                      int R, int S, int stride, int pad, bool is_max, hipStream_t s, int nchw_c = 0);
+// nchw_c > 0: y (fwd) / dy (bwd) is a dense NCHW tensor of the first nchw_c channels (argmax stays NHWC)
 hipError_t pool2d_bwd(const uint16_t* dy, const uint8_t* argmax, uint16_t* dx, int N, int H, int W, int C, int P,
                       int Q, int R, int S, int stride, int pad, bool is_max, hipStream_t s,
-                      const uint16_t* dy2 = nullptr);
+                      const uint16_t* dy2 = nullptr, int nchw_c = 0);
 hipError_t global_avgpool_fwd(const uint16_t* x, uint16_t* y, int N, int HW, int C, hipStream_t s);
 hipError_t global_avgpool_bwd(const uint16_t* dy, uint16_t* dx, int N, int HW, int C, hipStream_t s);
 

@@ -632,7 +632,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_dual_kernel(const bf16_t* __
 template <bool MAX, int KS, int ST>
 __global__ __launch_bounds__(256) void pool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
                                                        uint8_t* __restrict__ arg, int N, int H, int W, int C, int P,
-                                                       int Q, int R_, int S_, int st_, int pad) {
+                                                       int Q, int R_, int S_, int st_, int pad, int cl) {
   const int R = KS ? KS : R_, S = KS ? KS : S_, st = KS ? ST : st_;
   const int cv = C / 8;
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
@@ -677,7 +677,13 @@ __global__ __launch_bounds__(256) void pool_fwd_kernel(const bf16_t* __restrict_
 #pragma unroll
   for (int t = 0; t < 8; ++t) o[t] = f2bf(best[t] * inv);
   const size_t oi = ((size_t)row * Q + q) * cv + c8;
-  reinterpret_cast<u16x8*>(y)[oi] = o;
+  if (cl) {  // NCHW output of the cl logical channels (a flatten consumer reads it as is)
+#pragma unroll
+    for (int t = 0; t < 8; ++t)
+      if (c8 * 8 + t < cl) y[(((size_t)n * cl + c8 * 8 + t) * P + p) * Q + q] = o[t];
+  } else {
+    reinterpret_cast<u16x8*>(y)[oi] = o;
+  }
   if (MAX) {
     uint2 a;
     a.x = (uint32_t)bidx[0] | ((uint32_t)bidx[1] << 8) | ((uint32_t)bidx[2] << 16) | ((uint32_t)bidx[3] << 24);
@@ -693,7 +699,7 @@ template <bool MAX, int KS, int ST>
 __global__ __launch_bounds__(256) void pool_bwd_kernel(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ arg,
                                                        bf16_t* __restrict__ dx, int N, int H, int W, int C, int P,
                                                        int Q, int R_, int S_, int st_, int pad,
-                                                       const bf16_t* __restrict__ dy2) {
+                                                       const bf16_t* __restrict__ dy2, int cl) {
   const int R = KS ? KS : R_, S = KS ? KS : S_, st = KS ? ST : st_;
   constexpr int kSpan = KS ? (KS + ST - 1) / ST : 1;
   const int cv = C / 8;
@@ -717,7 +723,14 @@ __global__ __launch_bounds__(256) void pool_bwd_kernel(const bf16_t* __restrict_
           const int s = w - (q * st - pad);
           if (s < 0 || s >= S) continue;
           const size_t o = (((size_t)n * P + p) * Q + q) * cv + c8;
-          const u16x8 g = reinterpret_cast<const u16x8*>(dy)[o];
+          u16x8 g;
+          if (cl) {  // NCHW gradient of the cl logical channels (zero for the pad channels)
+#pragma unroll
+            for (int t = 0; t < 8; ++t)
+              g[t] = c8 * 8 + t < cl ? dy[(((size_t)n * cl + c8 * 8 + t) * P + p) * Q + q] : (uint16_t)0;
+          } else {
+            g = reinterpret_cast<const u16x8*>(dy)[o];
+          }
           u16x8 g2 = {0, 0, 0, 0, 0, 0, 0, 0};  // a second gradient of the same output (a residual
           if (dy2) g2 = reinterpret_cast<const u16x8*>(dy2)[o];  // block's input), summed here
           if (MAX) {
@@ -1364,29 +1377,36 @@ hipError_t bn_dual_backward(const BnArgs& a, const BnArgs& b, const uint16_t* dy
 }
 
 hipError_t pool2d_fwd(const uint16_t* x, uint16_t* y, uint8_t* argmax, int N, int H, int W, int C, int P, int Q,
-                      int R, int S, int stride, int pad, bool is_max, hipStream_t s) {
-  if (C % 8) return hipErrorInvalidValue;
+                      int R, int S, int stride, int pad, bool is_max, hipStream_t s, int nchw_c) {
+  if (C % 8 || nchw_c < 0 || nchw_c > C) return hipErrorInvalidValue;
   if ((int64_t)N * P >= (1ll << 31) || (int64_t)Q * (C / 8) > (1 << 30)) return hipErrorInvalidValue;
   const dim3 g((Q * (C / 8) + kBlock - 1) / kBlock, std::min(N * P, 65535));
   const bool k3 = R == 3 && S == 3 && stride == 2;
-  if (is_max && k3) pool_fwd_kernel<true, 3, 2><<<g, kBlock, 0, s>>>(x, y, argmax, N, H, W, C, P, Q, R, S, stride, pad);
-  else if (is_max) pool_fwd_kernel<true, 0, 1><<<g, kBlock, 0, s>>>(x, y, argmax, N, H, W, C, P, Q, R, S, stride, pad);
-  else pool_fwd_kernel<false, 0, 1><<<g, kBlock, 0, s>>>(x, y, argmax, N, H, W, C, P, Q, R, S, stride, pad);
+  if (is_max && k3) pool_fwd_kernel<true, 3, 2><<<g, kBlock, 0, s>>>(x, y, argmax, N, H, W, C, P, Q, R, S, stride,
+                                                                pad, nchw_c);
+  else if (is_max) pool_fwd_kernel<true, 0, 1><<<g, kBlock, 0, s>>>(x, y, argmax, N, H, W, C, P, Q, R, S, stride,
+                                                                pad, nchw_c);
+  else pool_fwd_kernel<false, 0, 1><<<g, kBlock, 0, s>>>(x, y, argmax, N, H, W, C, P, Q, R, S, stride,
+                                                                pad, nchw_c);
   return hipGetLastError();
 }
 
 hipError_t pool2d_bwd(const uint16_t* dy, const uint8_t* argmax, uint16_t* dx, int N, int H, int W, int C, int P,
-                      int Q, int R, int S, int stride, int pad, bool is_max, hipStream_t s, const uint16_t* dy2) {
-  if (C % 8) return hipErrorInvalidValue;
+                      int Q, int R, int S, int stride, int pad, bool is_max, hipStream_t s, const uint16_t* dy2,
+                      int nchw_c) {
+  if (C % 8 || nchw_c < 0 || nchw_c > C || (nchw_c && dy2)) return hipErrorInvalidValue;
   if ((int64_t)N * H >= (1ll << 31) || (int64_t)W * (C / 8) > (1 << 30)) return hipErrorInvalidValue;
   const dim3 g((W * (C / 8) + kBlock - 1) / kBlock, std::min(N * H, 65535));
   const bool k3 = R == 3 && S == 3 && stride == 2;
   if (is_max && k3)
-    pool_bwd_kernel<true, 3, 2><<<g, kBlock, 0, s>>>(dy, argmax, dx, N, H, W, C, P, Q, R, S, stride, pad, dy2);
+    pool_bwd_kernel<true, 3, 2><<<g, kBlock, 0, s>>>(dy, argmax, dx, N, H, W, C, P, Q, R, S, stride, pad, dy2,
+                                                   nchw_c);
   else if (is_max)
-    pool_bwd_kernel<true, 0, 1><<<g, kBlock, 0, s>>>(dy, argmax, dx, N, H, W, C, P, Q, R, S, stride, pad, dy2);
+    pool_bwd_kernel<true, 0, 1><<<g, kBlock, 0, s>>>(dy, argmax, dx, N, H, W, C, P, Q, R, S, stride, pad, dy2,
+                                                   nchw_c);
   else
-    pool_bwd_kernel<false, 0, 1><<<g, kBlock, 0, s>>>(dy, argmax, dx, N, H, W, C, P, Q, R, S, stride, pad, dy2);
+    pool_bwd_kernel<false, 0, 1><<<g, kBlock, 0, s>>>(dy, argmax, dx, N, H, W, C, P, Q, R, S, stride, pad, dy2,
+                                                   nchw_c);
   return hipGetLastError();
 }
 

@@ -122,6 +122,7 @@ class LeNet5(nn.Module):
         # the ReLUs are fused into the conv epilogues; the modules stay for the reference layout
         self.features[1] = nn.Identity()
         self.features[4] = nn.Identity()
+        self.features[5].flatten_out = True   # native pool writes NCHW: the flatten below is a view
         self.fc1 = Linear(16 * 5 * 5, 120, activation="relu")
         self.fc2 = Linear(120, 84, activation="relu")
         self.fc3 = Linear(84, num_classes)

@@ -59,10 +59,12 @@ class _LinearActNative(torch.autograd.Function):
         if kpad != K:
             # pad columns must be 0 so the weight-gradient pad columns stay exactly 0
             # (the producer's pad may hold e.g. sigmoid(0) = 0.5)
+            zp = getattr(x, "_ldnn_zpad", False)
             x2 = _padded_rows_view(x2, kpad)
-            # through .data: the producer saved this buffer for its own backward and
-            # its pad columns never influence that backward (their gradient is 0)
-            x2.data[:, K:].zero_()
+            if not zp:
+                # through .data: the producer saved this buffer for its own backward and
+                # its pad columns never influence that backward (their gradient is 0)
+                x2.data[:, K:].zero_()
         y = torch.empty(x2.shape[0], npad, dtype=torch.bfloat16, device=x.device)
         if bias is not None:
             b = flat.master_storage(bias)
@@ -78,7 +80,12 @@ class _LinearActNative(torch.autograd.Function):
         ctx.xshape = x.shape
         n = weight.shape[0]
         out = y if n == npad else y[:, :n]
-        return out.reshape(*x.shape[:-1], n)
+        out = out.reshape(*x.shape[:-1], n)
+        if act != 1 and n != npad and out.dim() == 2:
+            # pad rows of W and pad entries of b are exactly 0 (their gradients are), so the
+            # pad columns hold act(0) = 0: a padded consumer skips re-zeroing them
+            out._ldnn_zpad = True
+        return out
 
     @staticmethod
     def backward(ctx, gy):
@@ -744,11 +751,47 @@ def _sq(v):
     return v if isinstance(v, int) else (v[0] if v[0] == v[1] else None)
 
 
+class _PoolFlatNative(torch.autograd.Function):
+    """A pool whose only consumer flattens it (LeNet-5's last pool -> fc1): the kernel
+    writes the dense NCHW output itself, so ``flatten(1)`` is a free view instead of an
+    NHWC -> NCHW copy, and the backward reads the flattened gradient in place
+    (bn_pool.hip pool_fwd_kernel / pool_bwd_kernel with ``cl`` > 0)."""
+
+    @staticmethod
+    def forward(ctx, x, k, stride, pad, is_max):
+        C_ = _ext.C()
+        N, C, H, W = x.shape
+        cp = _up8(C)
+        xb = as_nhwc(x if x.dtype == torch.bfloat16 else x.to(torch.bfloat16), cp)
+        P, Q = (H + 2 * pad - k) // stride + 1, (W + 2 * pad - k) // stride + 1
+        y = torch.empty(N, C, P, Q, dtype=torch.bfloat16, device=x.device)
+        am = torch.empty(N, P, Q, cp, dtype=torch.uint8, device=x.device) if is_max else None
+        C_.pool_fwd(xb.contiguous(), y, am, k, k, stride, pad, is_max, nchw_out=True)
+        ctx.save_for_backward(am) if is_max else None
+        ctx.meta = (k, stride, pad, is_max, (N, C, H, W, cp), x.dtype)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        C_ = _ext.C()
+        k, stride, pad, is_max, (N, C, H, W, cp), in_dtype = ctx.meta
+        am = ctx.saved_tensors[0] if is_max else None
+        g = (gy if gy.dtype == torch.bfloat16 else gy.to(torch.bfloat16)).contiguous()
+        dx = torch.empty(N, H, W, cp, dtype=torch.bfloat16, device=gy.device)
+        C_.pool_bwd(g, am, dx, k, k, stride, pad, is_max, nchw_dy=True)
+        out = _zpad(nchw_view(dx, C))
+        return (out if in_dtype == torch.bfloat16 else out.to(in_dtype)), None, None, None, None
+
+
 def pool2d(x, mod, is_max: bool):
+    """Max / average pooling.  ``mod.flatten_out`` (set by a model whose pool feeds a
+    flatten, e.g. LeNet-5) makes the native path return a dense NCHW tensor."""
     k, st, pad = _sq(mod.kernel_size), _sq(mod.stride if mod.stride is not None else mod.kernel_size), _sq(mod.padding)
     simple = (None not in (k, st, pad) and not getattr(mod, "ceil_mode", False)
               and (not is_max or _sq(mod.dilation) == 1) and (is_max or getattr(mod, "count_include_pad", True))
               and k * k <= 255)
+    if _ext.use_native(x) and simple and x.dim() == 4 and getattr(mod, "flatten_out", False):
+        return _PoolFlatNative.apply(x, k, st, pad, is_max)
     if _ext.use_native(x) and simple and x.dim() == 4:
         y, twin = _PoolNative.apply(x, k, st, pad, is_max)   # (the input's pad was zeroed / zero)
         return _with_twin(_zpad(y), _zpad(twin))

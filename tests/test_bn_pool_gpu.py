@@ -74,12 +74,19 @@ def test_batchnorm_eval_uses_running_stats():
 
 @pytest.mark.parametrize("kind,k,st,pad", [("max", 2, 2, 0), ("max", 3, 2, 1), ("avg", 2, 2, 0), ("avg", 3, 1, 1)])
 @pytest.mark.parametrize("C", [6, 64])
-def test_pools(kind, k, st, pad, C):
+@pytest.mark.parametrize("flat", [False, True])
+def test_pools(kind, k, st, pad, C, flat):
+    """(flat: ``flatten_out`` -- the kernel writes a dense NCHW output and its backward reads
+    the flattened NCHW gradient, LeNet-5's pool -> fc1 hand-off)"""
     torch.manual_seed(2)
     mod = MaxPool2d(k, st, pad) if kind == "max" else AvgPool2d(k, st, pad)
+    mod.flatten_out = flat
     x = torch.randn(4, C, 14, 14, device="cuda")
     xb = _cl(x).requires_grad_(True)
     y = mod(xb)
+    if flat:
+        assert y.is_contiguous()
+        y = y.flatten(1).view(y.shape)
     # reference on a contiguous NCHW copy: torch-ROCm's avg_pool2d backward on a
     # channels_last input returned wrong (asymmetric) gradients for k3/s1/p1 here
     xf = xb.detach().float().contiguous().requires_grad_(True)
