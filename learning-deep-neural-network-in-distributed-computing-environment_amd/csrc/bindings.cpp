@@ -953,15 +953,51 @@ bool conv_fwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& y, int
   return done;
 }
 
-void conv_dgrad(const at::Tensor& dy, const at::Tensor& w, const at::Tensor& dx, int64_t stride, int64_t pad) {
+// bn_x given: dx is the gradient of a training BatchNorm(+ReLU)'s output (bn_x = that BN's
+// input, bn_mask its ReLU bits); returns whether the dgrad's epilogue also accumulated and
+// finalized that BN's backward statistics (then bn_bwd(..., stats_ready=True) applies them).
+bool conv_dgrad(const at::Tensor& dy, const at::Tensor& w, const at::Tensor& dx, int64_t stride, int64_t pad,
+                const c10::optional<at::Tensor>& bn_x, const c10::optional<at::Tensor>& bn_mask,
+                const c10::optional<at::Tensor>& bn_ws, const c10::optional<at::Tensor>& bn_gamma,
+                const c10::optional<at::Tensor>& bn_save_mean, const c10::optional<at::Tensor>& bn_save_invstd,
+                const c10::optional<at::Tensor>& bn_dgamma, const c10::optional<at::Tensor>& bn_dbeta,
+                bool bn_assign) {
   check_dev(dy, at::kBFloat16, "dy");
   check_dev(w, at::kBFloat16, "w");
   check_dev(dx, at::kBFloat16, "dx");
   ldnn::ConvShape s = conv_shape(dx, w, dy, stride, pad);
   c10::hip::HIPGuardMasqueradingAsCUDA g(dy.device());
   const ConvWs ws = conv_ws(s, 1, dy);
-  check(ldnn::conv2d_dgrad(s, bf16_ptr(dy), bf16_ptr(w), bf16_mut(dx), cur_stream(dy), ws.ws(), ws.c()),
+  ldnn::BnBwdFuse fuse{};
+  const ldnn::BnBwdFuse* fp = nullptr;
+  if (bn_x.has_value()) {
+    const int C = s.C;
+    const int64_t M = (int64_t)s.N * s.H * s.W;
+    check_dev(*bn_x, at::kBFloat16, "bn_x");
+    TORCH_CHECK(bn_x->is_contiguous() && bn_x->numel() == M * C, "conv_dgrad: bn_x must be dense [M][C] like dx");
+    ldnn::BnArgs a{};
+    a.M = (int)M;
+    a.C = C;
+    a.gamma = fptr_opt(bn_gamma, C, "bn_gamma");
+    a.save_mean = fptr_opt(bn_save_mean, C, "bn_save_mean");
+    a.save_invstd = fptr_opt(bn_save_invstd, C, "bn_save_invstd");
+    TORCH_CHECK(a.save_mean && a.save_invstd, "conv_dgrad: the BN statistics need save_mean / save_invstd");
+    a.ws = fptr_opt(bn_ws, ldnn::bn_workspace_floats(C), "bn_ws");
+    TORCH_CHECK(a.ws != nullptr, "conv_dgrad: bn_ws");
+    fuse.fin = ldnn::bn_backward_fin_conv(a, fptr_opt(bn_dgamma, C, "bn_dgamma"), fptr_opt(bn_dbeta, C, "bn_dbeta"),
+                                          bn_assign);
+    fuse.x = bf16_ptr(*bn_x);
+    if (bn_mask.has_value()) {
+      check_dev(*bn_mask, at::kByte, "bn_mask");
+      TORCH_CHECK(bn_mask->is_contiguous() && bn_mask->numel() == M * C / 8, "conv_dgrad: bn_mask [M][C/8]");
+      fuse.mask = bn_mask->data_ptr<uint8_t>();
+    }
+    fp = &fuse;
+  }
+  bool done = false;
+  check(ldnn::conv2d_dgrad(s, bf16_ptr(dy), bf16_ptr(w), bf16_mut(dx), cur_stream(dy), ws.ws(), ws.c(), fp, &done),
         "conv2d_dgrad");
+  return done;
 }
 
 void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& dw, int64_t stride, int64_t pad,
@@ -1047,10 +1083,12 @@ void bn_bwd(const at::Tensor& x, const at::Tensor& y, const at::Tensor& dy, cons
             const c10::optional<at::Tensor>& dres, const c10::optional<at::Tensor>& gamma,
             const at::Tensor& save_mean, const at::Tensor& save_invstd, const at::Tensor& ws,
             const c10::optional<at::Tensor>& dgamma, const c10::optional<at::Tensor>& dbeta, bool relu,
-            const c10::optional<at::Tensor>& mask, bool grad_assign, const c10::optional<at::Tensor>& dy2) {
+            const c10::optional<at::Tensor>& mask, bool grad_assign, const c10::optional<at::Tensor>& dy2,
+            bool stats_ready) {
   check_dev(x, at::kBFloat16, "x");
   check_dev(dy, at::kBFloat16, "dy");
   check_dev(dx, at::kBFloat16, "dx");
+  TORCH_CHECK(!(stats_ready && dy2.has_value()), "bn_bwd: stats_ready covers dy alone");
   TORCH_CHECK(x.dim() == 2 && x.is_contiguous() && dy.sizes() == x.sizes() && dy.is_contiguous() &&
                   dx.sizes() == x.sizes() && dx.is_contiguous(),
               "bn_bwd: [M][C] dense tensors");
@@ -1082,7 +1120,7 @@ void bn_bwd(const at::Tensor& x, const at::Tensor& y, const at::Tensor& dy, cons
     dr = bf16_mut(*dres);
   }
   check(ldnn::bn_backward(a, bf16_ptr(dy), bf16_mut(dx), dr, fptr_opt(dgamma, C, "dgamma"),
-                          fptr_opt(dbeta, C, "dbeta"), cur_stream(x), grad_assign),
+                          fptr_opt(dbeta, C, "dbeta"), cur_stream(x), grad_assign, stats_ready),
         "bn_backward");
 }
 
@@ -1740,7 +1778,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_bwd", &bn_bwd, py::arg("x"), py::arg("y"), py::arg("dy"), py::arg("dx"), py::arg("dres"),
         py::arg("gamma"), py::arg("save_mean"), py::arg("save_invstd"), py::arg("ws"), py::arg("dgamma"),
         py::arg("dbeta"), py::arg("relu"), py::arg("mask") = py::none(), py::arg("grad_assign") = false,
-        py::arg("dy2") = py::none());
+        py::arg("dy2") = py::none(), py::arg("stats_ready") = false);
   m.def("pool_fwd", &pool_fwd, py::arg("x"), py::arg("y"), py::arg("argmax"), py::arg("R"), py::arg("S"),
         py::arg("stride"), py::arg("pad"), py::arg("is_max"), py::arg("nchw_out") = false);
   m.def("pool_bwd", &pool_bwd, py::arg("dy"), py::arg("argmax"), py::arg("dx"), py::arg("R"), py::arg("S"),
@@ -1771,6 +1809,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("set_conv_combine_last", &ldnn::set_conv_combine_last,
         "split-K combine summer: 1 = the tile's last K slice, 0 = the last workgroup to arrive", py::arg("on"));
   m.def("get_conv_combine_last", &ldnn::get_conv_combine_last);
+  m.def("set_conv_bn_bwd", &ldnn::set_conv_bn_bwd,
+        "dgrad-side BN backward statistics: 0 off, 1 slab sum only (default), 2 also the dgrad epilogue");
+  m.def("get_conv_bn_bwd", &ldnn::get_conv_bn_bwd);
   m.def("gap_linear_ok", &ldnn::gap_linear_ok, "shapes the fused pooled classifier head takes", py::arg("N"),
         py::arg("HW"), py::arg("C"), py::arg("ncls"));
   m.def("gap_linear_fwd", &gap_linear_fwd, "global average pool + Linear (<= 16 classes) in one launch", py::arg("x"),
@@ -1784,7 +1825,11 @@ PYBIND11_MODULE(_C, m) {
         py::arg("bn_running_var") = py::none(), py::arg("bn_save_mean") = py::none(),
         py::arg("bn_save_invstd") = py::none(), py::arg("bn_eps") = 1e-5, py::arg("bn_momentum") = 0.1,
         py::arg("bn_num_batches") = py::none());
-  m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("stride"), py::arg("pad"));
+  m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("stride"), py::arg("pad"),
+        py::arg("bn_x") = py::none(), py::arg("bn_mask") = py::none(), py::arg("bn_ws") = py::none(),
+        py::arg("bn_gamma") = py::none(), py::arg("bn_save_mean") = py::none(),
+        py::arg("bn_save_invstd") = py::none(), py::arg("bn_dgamma") = py::none(), py::arg("bn_dbeta") = py::none(),
+        py::arg("bn_assign") = false);
   m.def("conv_wgrad", &conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("dw"), py::arg("stride"), py::arg("pad"),
         py::arg("beta") = 0.0, py::arg("real_channels") = 0,
         "real_channels: channels of x that carry data (the rest zero padding, e.g. 3 of a stem's 8); 0 = all");

@@ -113,8 +113,12 @@ struct BnFin;  // (BatchNorm finalize state, below)
 hipError_t conv2d_fwd(const ConvShape& s, const uint16_t* x, const uint16_t* w, uint16_t* y, const float* bias,
                       int epi, hipStream_t st, float* ws = nullptr, int* cnt = nullptr, const BnFin* bn = nullptr,
                       bool* bn_done = nullptr);
+struct BnBwdFuse;  // (a BatchNorm backward whose statistics a dgrad epilogue takes, below)
+// bnb (optional): dx is the gradient of a training BatchNorm(+ReLU)'s output; also accumulate
+// that BN's backward statistics over the bf16 dx and finalize them (*bn_done: whether it did)
 hipError_t conv2d_dgrad(const ConvShape& s, const uint16_t* dy, const uint16_t* w, uint16_t* dx, hipStream_t st,
-                        float* ws = nullptr, int* cnt = nullptr);
+                        float* ws = nullptr, int* cnt = nullptr, const BnBwdFuse* bnb = nullptr,
+                        bool* bn_done = nullptr);
 hipError_t conv2d_wgrad(const ConvShape& s, const uint16_t* dy, const uint16_t* x, float* dw, float beta,
                         hipStream_t st, float* ws = nullptr);
 // LDS-DMA fast path (conv_lds.hip): hipErrorNotSupported outside its shape set
@@ -124,7 +128,7 @@ hipError_t conv2d_fwd_lds(const ConvShape& s, const uint16_t* x, const uint16_t*
                           int epi, hipStream_t st, float* ws, int* cnt, const BnFin* bn = nullptr,
                           bool* bn_used = nullptr);
 hipError_t conv2d_dgrad_lds(const ConvShape& s, const uint16_t* dy, const uint16_t* w, uint16_t* dx, hipStream_t st,
-                            float* ws, int* cnt);
+                            float* ws, int* cnt, const BnBwdFuse* bnb = nullptr, bool* bn_used = nullptr);
 hipError_t conv2d_wgrad_lds(const ConvShape& s, const uint16_t* dy, const uint16_t* x, float* dw, float beta,
                             hipStream_t st, float* ws);
 struct ConvWorkspace {
@@ -150,6 +154,10 @@ int get_conv_ws();
 // in-launch split-K combine of the LDS-DMA convs: 1 = the tile's last K slice sums, 0 = the last arrival
 void set_conv_combine_last(int on);
 int get_conv_combine_last();
+// dgrad-side BN backward statistics: 0 off, 1 slab split-K sum only, 2 also the direct / combine
+// epilogue (LDNN_CONV_BN_BWD; the setter is for tests)
+void set_conv_bn_bwd(int mode);
+int get_conv_bn_bwd();
 void set_conv_trace(uint64_t* buf);
 int get_conv_halo();
 
@@ -197,6 +205,13 @@ struct BnFin {
   float* part;                // [kGrpMax][2C] row-group partials of the grouped reduce (ldnn_bn_fin.h)
   int* tickets;               // its per-64-channel-column tickets (left zero)
 };
+// The backward statistics of a BN(+ReLU) taken by the epilogue of the dgrad that produces the
+// gradient of its output: sum g and sum g * (x - mean) * invstd, g = dy * relu'(y) (mask bits)
+struct BnBwdFuse {
+  BnFin fin;                  // bn_backward_fin_conv: the BN's backward finalize state
+  const uint16_t* x;          // [M][C] the BN's input
+  const uint8_t* mask;        // [M][C/8] its ReLU bits (nullptr: no ReLU)
+};
 // Training-mode forward finalize state of a BN (its ws accumulators / ticket / coef).
 BnFin bn_forward_fin(const BnArgs& a);
 // ... for a producing conv's epilogue (its kBnCopies accumulator copies in ws).
@@ -205,8 +220,12 @@ BnFin bn_forward_fin_conv(const BnArgs& a);
 hipError_t bn_forward_apply(const BnArgs& a, hipStream_t s);
 // dx (and optionally dres = upstream gradient after the ReLU mask, for the residual
 // branch); dgamma / dbeta are ACCUMULATED (flat gradient buffer)
+// stats_ready: a dgrad epilogue already finalized the backward coefficients into a.ws
+// (conv2d_dgrad with a BnBwdFuse): the apply pass alone
 hipError_t bn_backward(const BnArgs& a, const uint16_t* dy, uint16_t* dx, uint16_t* dres, float* dgamma,
-                       float* dbeta, hipStream_t s, bool grad_assign = false);
+                       float* dbeta, hipStream_t s, bool grad_assign = false, bool stats_ready = false);
+// Backward finalize state of a BN for a producing dgrad's epilogue (its ws accumulators / coef).
+BnFin bn_backward_fin_conv(const BnArgs& a, float* dgamma, float* dbeta, bool grad_assign);
 // Residual block tail with a BatchNorm on both branches: y = relu(bn_a(a.x) + bn_b(b.x)), the
 // shortcut BN's output never stored (a.relu, both training mode; ready_*: statistics already
 // finalized into the ws by the producing convs).  a.y / a.mask: the output and its ReLU bits.

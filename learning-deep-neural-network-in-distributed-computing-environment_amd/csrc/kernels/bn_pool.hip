@@ -1247,7 +1247,7 @@ hipError_t bn_maxpool_backward(const BnArgs& a, int N, int H, int W, int P, int 
 }
 
 hipError_t bn_backward(const BnArgs& a, const uint16_t* dy, uint16_t* dx, uint16_t* dres, float* dgamma,
-                       float* dbeta, hipStream_t s, bool grad_assign) {
+                       float* dbeta, hipStream_t s, bool grad_assign, bool stats_ready) {
   const int M = a.M, C = a.C;
   if (C % 8) return hipErrorInvalidValue;
   if (M <= 0) return hipSuccess;
@@ -1269,7 +1269,9 @@ hipError_t bn_backward(const BnArgs& a, const uint16_t* dy, uint16_t* dx, uint16
   const dim3 gs((C + 63) / 64, gg.ny);
   float* part = grp_part(a);
   int* tk = grp_tickets(a);
-  if (gg.on) {
+  if (stats_ready) {
+    // (the producing dgrad's epilogue finalized f.coef / dgamma / dbeta)
+  } else if (gg.on) {
     if (a.relu && a.mask)
       bn_reduce_small_kernel<true, true, true><<<gs, 256, 0, s>>>(a.x, dy, nullptr, a.save_mean, a.save_invstd, M, C,
                                                                   f, a.mask, a.dy2, part, tk, gg.rpb);
@@ -1337,6 +1339,10 @@ BnFin bn_backward_fin(const BnArgs& a, float* dgamma, float* dbeta, bool grad_as
   return f;
 }
 }  // namespace
+
+BnFin bn_backward_fin_conv(const BnArgs& a, float* dgamma, float* dbeta, bool grad_assign) {
+  return bn_backward_fin(a, dgamma, dbeta, grad_assign);
+}
 
 hipError_t bn_dual_backward(const BnArgs& a, const BnArgs& b, const uint16_t* dy, uint16_t* dx, uint16_t* dr,
                             float* dgamma_a, float* dbeta_a, float* dgamma_b, float* dbeta_b, bool assign_a,

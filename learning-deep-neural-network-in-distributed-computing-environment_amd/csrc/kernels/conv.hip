@@ -341,10 +341,12 @@ hipError_t conv2d_fwd(const ConvShape& s, const uint16_t* x, const uint16_t* w, 
 }
 
 hipError_t conv2d_dgrad(const ConvShape& s, const uint16_t* dy, const uint16_t* w, uint16_t* dx, hipStream_t st,
-                        float* ws, int* cnt) {
+                        float* ws, int* cnt, const BnBwdFuse* bnb, bool* bn_done) {
+  if (bn_done) *bn_done = false;
   if (g_conv_impl == 0) {
-    const hipError_t e = conv2d_dgrad_lds(s, dy, w, dx, st, ws, cnt);
+    const hipError_t e = conv2d_dgrad_lds(s, dy, w, dx, st, ws, cnt, bnb, bn_done);
     if (e != hipErrorNotSupported) return e;
+    if (bn_done) *bn_done = false;
   }
   if (g_conv_impl == 0 && s.C == 8 && s.K % 8 == 0 && s.K * s.R * s.S * 8 <= kDgradC8MaxW && s.stride >= 1) {
     const int64_t pix = (int64_t)s.N * s.H * s.W;

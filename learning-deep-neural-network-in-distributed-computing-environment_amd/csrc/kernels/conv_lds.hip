@@ -69,8 +69,11 @@ struct LArgs {
   FastDiv f_cw[2], f_ch[2];      // stride-2 dgrad class rows: (W - pw + 1) / 2, (H - ph + 1) / 2
   float* ws;         // split-K: combine slabs (with cnt) or wgrad partial slabs [split][M][N] (without)
   int* cnt;          // split-K arrival counters of the in-launch combine
-  int bn_stats;      // fwd: accumulate + finalize the next BatchNorm's statistics (bn)
+  int bn_stats;      // fwd: accumulate + finalize the next BatchNorm's statistics (bn); dgrad: the
+                     // backward statistics of the BN whose output's gradient this dx is (bn_x / bn_mask)
   BnFin bn;
+  const uint16_t* bn_x;     // dgrad bn_stats: that BN's input [M][N]
+  const uint8_t* bn_mask;   // ... and its ReLU bits [M][N/8] (nullptr: no ReLU)
   int tap_major;     // fwd / dgrad K-tile order: 0 = channel block fastest, 1 = filter tap fastest
   int f32_rows;      // fp32 outputs (wgrad, split-K slabs) through the row-coalesced LDS epilogue
   int bf16_rows;     // bf16 outputs (fwd y, stride-1 dgrad dx) through the row-coalesced LDS epilogue
@@ -428,12 +431,41 @@ __device__ __forceinline__ int tiles_of(const LArgs& a) { return a.tiles_x; }
 // measured no faster, profiles/r3/bn_copies_ab_r3.txt).  The
 // last of the grid's `tiles` workgroups sums the copies and finalizes (mean,
 // invstd, running-stat EMA, apply coefficients), so the BN needs no reduce pass.
-template <int WM, int WN>
+//
+// BWD (dgrad): the same for the backward statistics of the BN whose output's gradient the
+// tile is -- sum g and sum g * (x - mean) * invstd with g = bf16(dx) * relu'(y) -- the loads
+// of x (4 channels, 8 B per fragment), the ReLU bit-mask bytes and the channels' saved
+// mean / invstd all issued before the first use; bn_finalize_last<true> turns the totals into
+// the apply coefficients and dgamma / dbeta (bn_reduce_small_kernel's job otherwise).
+template <int WM, int WN, bool BWD = false>
 __device__ __forceinline__ void bn_stats_epilogue(const LArgs& a, const Geo& g, floatx4 (&acc)[4][4], int mbase,
                                                   int n0, int wm, int wn, int lane, int tile, char* smem,
                                                   int lds_floats) {
   constexpr int BN = WN * 64;
   float* red = reinterpret_cast<float*>(smem);  // [WM][BN][2]
+  uint2 xv[4][4];
+  uint32_t mbits[4][4];
+  float mu[4][4], is[4][4];
+  if constexpr (BWD) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + wn * 64 + j * 16 + 4 * (lane >> 4);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const bool ok = n + r < a.N;
+        mu[j][r] = ok ? a.bn.save_mean[n + r] : 0.f;
+        is[j][r] = ok ? a.bn.save_invstd[n + r] : 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = mbase + i * 16 + (lane & 15);
+        const bool ok = m < g.M && n < a.N;
+        const size_t o = (size_t)m * a.N + n;
+        xv[i][j] = ok ? *reinterpret_cast<const uint2*>(a.bn_x + o) : make_uint2(0u, 0u);
+        mbits[i][j] = (ok && a.bn_mask != nullptr) ? (uint32_t)a.bn_mask[o >> 3] >> (n & 7) : 0xffu;
+      }
+    }
+  }
   __syncthreads();  // every wave is done with the operand stages
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -444,8 +476,16 @@ __device__ __forceinline__ void bn_stats_epilogue(const LArgs& a, const Geo& g, 
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const float v = bf2f(f2bf(acc[j][i][r]));
-        s0[r] += v;
-        s1[r] += v * v;
+        if constexpr (BWD) {
+          const float gv = ((mbits[i][j] >> r) & 1u) ? v : 0.f;
+          const uint32_t xw = r < 2 ? xv[i][j].x : xv[i][j].y;
+          const float xf = bf2f((uint16_t)((r & 1) ? (xw >> 16) : (xw & 0xffffu)));
+          s0[r] += gv;
+          s1[r] += gv * (xf - mu[j][r]) * is[j][r];
+        } else {
+          s0[r] += v;
+          s1[r] += v * v;
+        }
       }
     }
 #pragma unroll
@@ -480,7 +520,7 @@ __device__ __forceinline__ void bn_stats_epilogue(const LArgs& a, const Geo& g, 
     bn_acc_add(accc + a.N + c, s1);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's atomics have completed
-  bn_finalize_last<false, kBnCopies>(a.bn, g.M, a.N, tiles_of(a), red, lds_floats);
+  bn_finalize_last<BWD, kBnCopies>(a.bn, g.M, a.N, tiles_of(a), red, lds_floats);
 }
 
 // Direct epilogue with the class row remap: GEMM row m of a stride-2 dgrad
@@ -717,15 +757,15 @@ __device__ __forceinline__ void conv_tail(const LArgs& a, const Geo& g, floatx4 
         store_bf16_rows<EPI>(p, acc, smem + (size_t)(wm * WN + wn) * 16384, mb, nbase, lane);
       else
         store_bf16_rows<EPI, 2>(p, acc, smem + (size_t)(wm * WN + wn) * 8192, mb, nbase, lane);
-      if constexpr (!DGRAD && EPI == EPI_NONE) {
-        if (a.bn_stats) bn_stats_epilogue<WM, WN>(a, g, acc, mb, n0, wm, wn, lane, bx, smem, lds_floats);
+      if constexpr (EPI == EPI_NONE) {
+        if (a.bn_stats) bn_stats_epilogue<WM, WN, DGRAD>(a, g, acc, mb, n0, wm, wn, lane, bx, smem, lds_floats);
       }
       return;
     }
   }
   epilogue<EPI, OUT_F32, 4, 4>(p, acc, mb, nbase, lane);
-  if constexpr (!DGRAD && !OUT_F32 && EPI == EPI_NONE) {
-    if (a.bn_stats) bn_stats_epilogue<WM, WN>(a, g, acc, mb, n0, wm, wn, lane, bx, smem, lds_floats);
+  if constexpr (!OUT_F32 && EPI == EPI_NONE) {
+    if (a.bn_stats) bn_stats_epilogue<WM, WN, DGRAD>(a, g, acc, mb, n0, wm, wn, lane, bx, smem, lds_floats);
   }
 }
 
@@ -2234,22 +2274,39 @@ hipError_t conv_slab_epilogue(const float* ws, uint16_t* out, int M, int N, int 
 // row lanes, every slab's loads of a row in flight together -- summing the statistics of the
 // bf16-rounded outputs, then the per-column ticket finalize (ldnn_bn_fin.h).  (A round-2 variant
 // with 8-copy atomics and one finalizing block was slower than the pair, profiles/cnn_slab_bn_ab_r2.jsonl.)
-template <bool NT>
+// BWD: the slab sum of a small-M stride-1 dgrad AND the backward statistics of the BN whose
+// output's gradient it is (x / mask: that BN's input and ReLU bits; see bn_stats_epilogue).
+template <bool NT, bool BWD = false>
 __global__ __launch_bounds__(256) void conv_slab_bn_kernel(const float* __restrict__ ws, bf16_t* __restrict__ out,
-                                                           int M, int N, int splits, BnFin fin, int rpb) {
+                                                           int M, int N, int splits, BnFin fin, int rpb,
+                                                           const bf16_t* __restrict__ bx,
+                                                           const uint8_t* __restrict__ bmask) {
   constexpr int kLanes = 8, kRl = 32, kJs = 256 + kLanes;
   __shared__ float red[2][8 * kJs];
   __shared__ int last;
   const int tid = threadIdx.x, lane = tid % kLanes, rlane = tid / kLanes;
   const int c0 = blockIdx.x * 64 + lane * 8;
-  float s0[8], s1[8];
+  float s0[8], s1[8], mu[8], is[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) s0[j] = s1[j] = 0.f;
+  for (int j = 0; j < 8; ++j) s0[j] = s1[j] = mu[j] = is[j] = 0.f;
   if (c0 < N) {
+    if constexpr (BWD) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        mu[j] = fin.save_mean[c0 + j];
+        is[j] = fin.save_invstd[c0 + j];
+      }
+    }
     const int r_end = min(M, (int)(blockIdx.y + 1) * rpb);
     const size_t sstride = (size_t)M * N / 4;
     for (int r = blockIdx.y * rpb + rlane; r < r_end; r += kRl) {
       const size_t o = (size_t)r * N + c0;
+      u16x8 xv = {0, 0, 0, 0, 0, 0, 0, 0};
+      uint32_t mb = 0xffu;
+      if constexpr (BWD) {  // issued ahead of the slab loads
+        xv = *reinterpret_cast<const u16x8*>(bx + o);
+        if (bmask != nullptr) mb = bmask[o >> 3];
+      }
       floatx4 v0, v1;
       slab_sum8<NT>(reinterpret_cast<const floatx4*>(ws + o), (int64_t)sstride, splits, v0, v1);
       u16x8 ob;
@@ -2257,8 +2314,14 @@ __global__ __launch_bounds__(256) void conv_slab_bn_kernel(const float* __restri
       for (int j = 0; j < 8; ++j) {
         ob[j] = f2bf(j < 4 ? v0[j] : v1[j - 4]);
         const float v = bf2f(ob[j]);
-        s0[j] += v;
-        s1[j] += v * v;
+        if constexpr (BWD) {
+          const float gv = ((mb >> j) & 1u) ? v : 0.f;
+          s0[j] += gv;
+          s1[j] += gv * (bf2f(xv[j]) - mu[j]) * is[j];
+        } else {
+          s0[j] += v;
+          s1[j] += v * v;
+        }
       }
       *reinterpret_cast<u16x8*>(out + o) = ob;
     }
@@ -2279,13 +2342,13 @@ __global__ __launch_bounds__(256) void conv_slab_bn_kernel(const float* __restri
     }
     const int c = blockIdx.x * 64 + ln * 8 + j;
     if (gridDim.y == 1) {
-      if (c < N) bn_finalize_channel<false>(fin, M, N, c, t0, t1, 1.f / (float)M);
+      if (c < N) bn_finalize_channel<BWD>(fin, M, N, c, t0, t1, 1.f / (float)M);
     } else if (c < N) {
       grp_store(fin.part + (size_t)blockIdx.y * 2 * N + c, t0);
       grp_store(fin.part + ((size_t)blockIdx.y * 2 + 1) * N + c, t1);
     }
   }
-  if (blockIdx.x == 0 && blockIdx.y == 0 && tid == 0 && fin.num_batches) fin.num_batches[0] += 1;
+  if (!BWD && blockIdx.x == 0 && blockIdx.y == 0 && tid == 0 && fin.num_batches) fin.num_batches[0] += 1;
   if (gridDim.y == 1) return;
   if (!grp_ticket(fin.tickets + blockIdx.x, gridDim.y, last)) return;
   float* tot = &red[0][0];
@@ -2296,7 +2359,7 @@ __global__ __launch_bounds__(256) void conv_slab_bn_kernel(const float* __restri
   if (tid < 64 && cc < N) {
     const float S0 = tot[tid] + tot[64 + tid] + tot[128 + tid] + tot[192 + tid];
     const float S1 = tot[256 + tid] + tot[320 + tid] + tot[384 + tid] + tot[448 + tid];
-    bn_finalize_channel<false>(fin, M, N, cc, S0, S1, 1.f / (float)M);
+    bn_finalize_channel<BWD>(fin, M, N, cc, S0, S1, 1.f / (float)M);
   }
 }
 
@@ -2307,7 +2370,19 @@ int slab_bn_env() {
   static const int v = env_int("LDNN_CONV_SLAB_BN", 1);
   return v;
 }
-hipError_t conv_slab_bn(const float* ws, uint16_t* out, int M, int N, int splits, const BnFin& fin, hipStream_t st) {
+// LDNN_CONV_BN_BWD (A/B knob): stride-1 dgrads take the backward statistics of the BN whose
+// output's gradient they produce (conv2d_dgrad with a BnBwdFuse): 1 (default) in the slab split-K
+// sum only, 2 also in the direct / in-launch-combine epilogue, 0 never.  Measured on MI355X
+// (profiles/r5/conv_bn_bwd_ab.txt): the slab pass absorbs the reduce for ~1.5 us less per BN, while
+// the epilogue form -- x and mask loads, 8-copy atomics and one finalizing workgroup behind the
+// tile's own stores -- added 11-13 us to a 64 / 128-tile dgrad to save an 8-10 us reduce launch
+int g_bn_bwd = -1;
+int bn_bwd_env() {
+  if (g_bn_bwd < 0) g_bn_bwd = env_int("LDNN_CONV_BN_BWD", 1);
+  return g_bn_bwd;
+}
+hipError_t conv_slab_bn(const float* ws, uint16_t* out, int M, int N, int splits, const BnFin& fin, hipStream_t st,
+                        const BnBwdFuse* bnb = nullptr) {
   if (M <= 0) return hipSuccess;
   static const int target = std::max(1, env_int("LDNN_CONV_SLAB_BN_TARGET", 512));
   const int G = (N + 63) / 64;
@@ -2315,8 +2390,14 @@ hipError_t conv_slab_bn(const float* ws, uint16_t* out, int M, int N, int splits
   const int rpb = (M + ny - 1) / ny;
   ny = (M + rpb - 1) / rpb;
   const dim3 g(G, ny);
-  if (slab_nt_env()) conv_slab_bn_kernel<true><<<g, 256, 0, st>>>(ws, out, M, N, splits, fin, rpb);
-  else conv_slab_bn_kernel<false><<<g, 256, 0, st>>>(ws, out, M, N, splits, fin, rpb);
+  if (bnb != nullptr) {
+    const bf16_t* bx = reinterpret_cast<const bf16_t*>(bnb->x);
+    if (slab_nt_env()) conv_slab_bn_kernel<true, true><<<g, 256, 0, st>>>(ws, out, M, N, splits, fin, rpb, bx, bnb->mask);
+    else conv_slab_bn_kernel<false, true><<<g, 256, 0, st>>>(ws, out, M, N, splits, fin, rpb, bx, bnb->mask);
+    return hipGetLastError();
+  }
+  if (slab_nt_env()) conv_slab_bn_kernel<true><<<g, 256, 0, st>>>(ws, out, M, N, splits, fin, rpb, nullptr, nullptr);
+  else conv_slab_bn_kernel<false><<<g, 256, 0, st>>>(ws, out, M, N, splits, fin, rpb, nullptr, nullptr);
   return hipGetLastError();
 }
 
@@ -2849,6 +2930,9 @@ int get_conv_hb() { return hb_env(); }
 void set_conv_ws(int mode) { g_conv_ws = mode; }
 int get_conv_ws() { return ws_env(); }
 void set_conv_trace(uint64_t* buf) { g_conv_trace = buf; }
+void set_conv_bn_bwd(int mode) { g_bn_bwd = mode; }
+int get_conv_bn_bwd() { return bn_bwd_env(); }
+
 void set_conv_combine_last(int on) { g_combine_last = on; }
 int get_conv_combine_last() { return combine_last_env(); }
 void set_conv_wgrad_ring(int mode) { g_wgrad_ring = mode; }
@@ -3066,7 +3150,8 @@ hipError_t conv2d_fwd_lds(const ConvShape& s, const uint16_t* x, const uint16_t*
 }
 
 hipError_t conv2d_dgrad_lds(const ConvShape& s, const uint16_t* dy, const uint16_t* w, uint16_t* dx, hipStream_t st,
-                            float* ws, int* cnt) {
+                            float* ws, int* cnt, const BnBwdFuse* bnb, bool* bn_used) {
+  if (bn_used) *bn_used = false;
   if (s.K % 64 != 0 || !shape_ok(s)) return hipErrorNotSupported;
   if (s.N * s.H * s.W <= 0) return hipSuccess;
   const bool hbp = hb_takes(s, true);
@@ -3098,6 +3183,19 @@ hipError_t conv2d_dgrad_lds(const ConvShape& s, const uint16_t* dy, const uint16
     a.nk_split = a.nk_all;
     return launch_ws64<true>(a, dy, bdy, w, st);
   }
+  // the BN backward statistics of the BN whose output's gradient dx is: stride-1 dgrads (no
+  // class row remap) in the direct / in-launch combine epilogue, or in the slab sum
+  const BnBwdFuse* slab_bnb = nullptr;
+  if (bnb != nullptr && bn_bwd_env() && s.stride == 1 && pl.classes == 1 && s.C % 8 == 0) {
+    if (slab) {
+      if (slab_bn_env() && bnb->fin.part != nullptr && bnb->fin.tickets != nullptr) slab_bnb = bnb;
+    } else if (bn_bwd_env() >= 2) {
+      a.bn_stats = 1;
+      a.bn = bnb->fin;
+      a.bn_x = bnb->x;
+      a.bn_mask = bnb->mask;
+    }
+  }
   hipError_t e;
   if (hbp) {
     e = launch_hb<DgradB<128, 2, 8>, true>(a, EPI_NONE, pl.splits, dy, bdy, w, bw, st);
@@ -3111,7 +3209,15 @@ hipError_t conv2d_dgrad_lds(const ConvShape& s, const uint16_t* dy, const uint16
   } else {
     e = launch<2, 2, DgradA<128, 4, 4>, DgradB<128, 4, 4>, false, true>(a, EPI_NONE, pl.splits, dy, bdy, w, bw, st);
   }
-  if (e != hipSuccess || !slab) return e;
+  if (e != hipSuccess) return e;
+  if (!slab) {
+    if (bn_used) *bn_used = a.bn_stats != 0;
+    return e;
+  }
+  if (slab_bnb != nullptr) {
+    if (bn_used) *bn_used = true;
+    return conv_slab_bn(ws, dx, a.M, a.N, pl.splits, slab_bnb->fin, st, slab_bnb);
+  }
   return conv_slab_epilogue(ws, dx, a.M, a.N, pl.splits, nullptr, EPI_NONE, st);
 }
 

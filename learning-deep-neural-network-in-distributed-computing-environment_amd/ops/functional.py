@@ -299,6 +299,38 @@ def _fused_bn_ok(bn, K: int, kp: int, bias, relu: bool) -> bool:
             and not relu and getattr(bn, "_ldnn_flat", None) is not None)
 
 
+# The dgrad of a conv whose input is a training BatchNorm(+ReLU)'s output takes that BN's
+# backward statistics in its epilogue (conv2d_dgrad with a BnBwdFuse), and the BN backward runs
+# its apply pass alone -- one reduce launch less per such pair (LDNN_CONV_BN_BWD=0: off)
+CONV_BN_BWD = os.environ.get("LDNN_CONV_BN_BWD", "1") != "0"
+BN_BWD_FUSED = [0]   # BN backwards that found their statistics finalized by a dgrad (tests)
+
+
+class _BnBwdSrc:
+    """What a consumer conv's dgrad needs to take a BN's backward statistics (attached to the
+    BN's primary output as ``_ldnn_bnsrc``).  ``twin_used``: the output also feeds a shortcut
+    (its gradient arrives in two parts, so only the BN's own reduce sees the sum)."""
+
+    __slots__ = ("mod", "flat", "weight", "bias", "x2", "mask", "smean", "sinv", "ws", "C", "twin_used", "pre")
+
+    def __init__(self, mod, flat, weight, bias, x2, mask, smean, sinv, ws, C):
+        self.mod, self.flat, self.weight, self.bias = mod, flat, weight, bias
+        self.x2, self.mask, self.smean, self.sinv, self.ws, self.C = x2, mask, smean, sinv, ws, C
+        self.twin_used = False
+        self.pre = None   # (dx pointer, version) of a dgrad that finalized the statistics
+
+    def dgrad_kwargs(self):
+        """conv_dgrad keyword arguments, or None when the BN's gradients accumulate this step
+        (the fused finalize only overwrites: a recomputing fallback must be able to redo it)."""
+        f = self.flat
+        if not (f.grad_fresh(self.weight) and f.grad_fresh(self.bias)):   # (peeks: the BN's backward consumes)
+            return None
+        C = self.C
+        return dict(bn_x=self.x2, bn_mask=self.mask, bn_ws=self.ws, bn_gamma=f.master_storage(self.weight)[:C],
+                    bn_save_mean=self.smean, bn_save_invstd=self.sinv, bn_dgamma=f.grad_storage(self.weight)[:C],
+                    bn_dbeta=f.grad_storage(self.bias)[:C], bn_assign=True)
+
+
 class _Conv2dNative(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, stride, pad, flat, relu, bn=None):
@@ -340,6 +372,8 @@ class _Conv2dNative(torch.autograd.Function):
             C.conv_fwd(xb, w, y, stride, pad, b, epi)
         ctx.save_for_backward(xb, y)
         ctx.meta = (stride, pad, flat, weight, bias, relu, Cin, x.dtype)
+        src = getattr(x, "_ldnn_bnsrc", None)
+        ctx.bnsrc = src if (CONV_BN_BWD and src is not None and stride == 1 and src.C == cp == Cin) else None
         return nchw_view(y, K)
 
     @staticmethod
@@ -364,7 +398,14 @@ class _Conv2dNative(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0]:
             dxb = torch.empty_like(xb)
-            C.conv_dgrad(g, flat.shadow_storage(weight), dxb, stride, pad)
+            src = ctx.bnsrc
+            kw = src.dgrad_kwargs() if src is not None and not src.twin_used else None
+            if kw is not None and C.conv_dgrad(g, flat.shadow_storage(weight), dxb, stride, pad, **kw):
+                # the BN's backward finds its statistics finalized if this dx reaches it unchanged
+                src.pre = (dxb.data_ptr(), dxb._version)
+            elif kw is None:
+                C.conv_dgrad(g, flat.shadow_storage(weight), dxb, stride, pad)
+            ctx.bnsrc = None
             dx = _zpad(nchw_view(dxb, Cin))   # (weight pad channels are zero)
             if in_dtype != torch.bfloat16:
                 dx = dx.to(in_dtype)
@@ -413,6 +454,9 @@ def _with_twin(y: torch.Tensor, twin: torch.Tensor) -> torch.Tensor:
 def shortcut_input(x: torch.Tensor) -> torch.Tensor:
     """The tensor a residual block's shortcut branch should read (x's twin if it has one)."""
     t = getattr(x, "_ldnn_twin", None)
+    src = getattr(x, "_ldnn_bnsrc", None)
+    if src is not None:   # the producer BN's gradient arrives in two parts: no dgrad-side statistics
+        src.twin_used = True
     return x if t is None else t
 
 
@@ -454,7 +498,12 @@ class _BatchNormNative(torch.autograd.Function):
         ctx.save_for_backward(x2, y if mask is None else x2.new_empty(0), smean, sinv)
         ctx.meta = (flat, weight, bias, relu, residual is not None, ws, (N, C, H, W), x.dtype)
         ctx.set_materialize_grads(False)
-        return nchw_view(y, C), nchw_view(y, C)
+        out = nchw_view(y, C)
+        ctx.bnsrc = None
+        if (CONV_BN_BWD and mod.training and weight is not None and bias is not None
+                and (mask is not None or not relu) and any(ctx.needs_input_grad)):
+            ctx.bnsrc = out._ldnn_bnsrc = _BnBwdSrc(mod, flat, weight, bias, x2, mask, smean, sinv, ws, C)
+        return out, nchw_view(y, C)
 
     @staticmethod
     def backward(ctx, gy, gy_twin):
@@ -485,8 +534,15 @@ class _BatchNormNative(torch.autograd.Function):
                     t.zero_()
         mask = ctx.mask
         yv = y.view(-1, C) if mask is None else x2   # (y is not read when the mask is given)
+        pre = ctx.bnsrc.pre if ctx.bnsrc is not None else None
+        ctx.bnsrc = None
+        # statistics finalized by the consumer conv's dgrad epilogue, if its dx arrived unchanged
+        # (a second consumer's gradient -- an in-place accumulation bumps the version -- or a
+        # twin branch gradient sends the BN through its own reduce)
+        ready = (pre is not None and gt is None and assign and pre[0] == g2.data_ptr() and pre[1] == gy._version)
+        BN_BWD_FUSED[0] += int(ready)
         C_.bn_bwd(x2, yv, g2, dx.view(-1, C), dres.view(-1, C) if dres is not None else None, gamma,
-                  smean, sinv, ws, dg, db, relu, mask=mask, grad_assign=assign, dy2=gt)
+                  smean, sinv, ws, dg, db, relu, mask=mask, grad_assign=assign, dy2=gt, stats_ready=ready)
         flat.notify(weight, bias)
         dxv = nchw_view(dx, C)
         dresv = nchw_view(dres, C) if dres is not None else None

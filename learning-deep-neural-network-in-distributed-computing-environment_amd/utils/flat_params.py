@@ -214,6 +214,11 @@ class FlatParams:
             return 0.0
         return 1.0
 
+    def grad_fresh(self, p) -> bool:
+        """Whether ``p``'s gradient is still logically zero this step (grad_beta would return
+        0.0), without consuming that state."""
+        return id(p) in self._stale
+
     @torch.no_grad()
     def zero_grad(self, lazy: bool = False):
         """lazy: gradients that native ops write are only marked zero (their first

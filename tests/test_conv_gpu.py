@@ -465,3 +465,94 @@ def test_fixed_summer_split_k_combine_matches_last_arrival(N, C, H, K, stride):
     torch.testing.assert_close(dx1, dxr, rtol=1e-2, atol=1e-2 * dxr.abs().max().item())
     yb = y1.reshape(-1, K)
     torch.testing.assert_close(sm1, yb.mean(0), rtol=1e-3, atol=1e-4)
+
+
+@pytest.mark.parametrize("N,C,H,K", [(64, 128, 16, 128), (64, 256, 8, 256), (64, 512, 4, 512), (64, 1024, 2, 1024),
+                                     (8, 512, 7, 512), (5, 192, 9, 256)])
+@pytest.mark.parametrize("relu", [True, False])
+def test_dgrad_takes_bn_backward_statistics(N, C, H, K, relu):
+    """A stride-1 dgrad whose dx is the gradient of a training BN(+ReLU)'s output accumulates that
+    BN's backward statistics in its epilogue (direct, in-launch combine or slab sum) and finalizes
+    them: dx has the bits of the plain dgrad, and the BN backward's apply pass alone
+    (stats_ready) gives the dx / dgamma / dbeta of the BN's own reduce; a repeat (accumulators and
+    tickets left clear) agrees."""
+    torch.manual_seed(31)
+    Cc = _ext.C()
+    old_mode = Cc.get_conv_bn_bwd()
+    Cc.set_conv_bn_bwd(2)   # the epilogue forms too (the default takes the slab sums only)
+    try:
+        _dgrad_bn_stats_case(Cc, N, C, H, K, relu)
+    finally:
+        Cc.set_conv_bn_bwd(old_mode)
+
+
+def _dgrad_bn_stats_case(Cc, N, C, H, K, relu):
+    M = N * H * H
+    xb = (torch.randn(M, C, device="cuda") * 1.5 + 0.3).bfloat16()
+    gamma = torch.rand(C, device="cuda") + 0.5
+    beta = torch.rand(C, device="cuda") - 0.5
+    sm, si = torch.empty(C, device="cuda"), torch.empty(C, device="cuda")
+    yb = torch.empty_like(xb)
+    mask = torch.empty(M * C // 8, dtype=torch.uint8, device="cuda") if relu else None
+    Cc.bn_fwd(xb, yb, None, gamma, beta, None, None, sm, si, torch.zeros(Cc.bn_workspace_floats(C), device="cuda"),
+              1e-5, 0.0, True, relu, None, mask=mask)
+    w = (torch.randn(K, 3, 3, C, device="cuda") * (1.0 / (K * 9) ** 0.5)).bfloat16()
+    gy = torch.randn(N, H, H, K, device="cuda").bfloat16()
+
+    def bn_back(dx, ws, ready):
+        dg, db = torch.full((C,), 3.0, device="cuda"), torch.full((C,), 3.0, device="cuda")
+        out = torch.empty(M, C, device="cuda", dtype=torch.bfloat16)
+        if ready:
+            used = Cc.conv_dgrad(gy, w, dx, 1, 1, bn_x=xb, bn_mask=mask, bn_ws=ws, bn_gamma=gamma, bn_save_mean=sm,
+                                 bn_save_invstd=si, bn_dgamma=dg, bn_dbeta=db, bn_assign=True)
+            assert used
+        else:
+            Cc.conv_dgrad(gy, w, dx, 1, 1)
+        Cc.bn_bwd(xb, xb, dx.view(M, C), out, None, gamma, sm, si, ws, dg, db, relu, mask=mask, grad_assign=True,
+                  stats_ready=ready)
+        torch.cuda.synchronize()
+        return dx.float(), out.float(), dg, db
+
+    ws = torch.zeros(Cc.bn_workspace_floats(C), device="cuda")
+    ref = bn_back(torch.empty(N, H, H, C, device="cuda", dtype=torch.bfloat16), torch.zeros_like(ws), False)
+    for _ in range(2):
+        got = bn_back(torch.empty(N, H, H, C, device="cuda", dtype=torch.bfloat16), ws, True)
+        assert torch.equal(got[0], ref[0])
+        torch.testing.assert_close(got[2], ref[2], rtol=1e-3, atol=1e-3 * ref[2].abs().max().item())
+        torch.testing.assert_close(got[3], ref[3], rtol=1e-3, atol=1e-3 * ref[3].abs().max().item())
+        torch.testing.assert_close(got[1], ref[1], rtol=1e-2, atol=1e-2 * ref[1].abs().max().item())
+    # the plain statistics left the workspace clear for the fused ones and vice versa
+    assert torch.count_nonzero(ws[10 * C + 16: 10 * C + 17]) == 0
+
+
+def test_resblock_bn1_backward_statistics_come_from_conv2_dgrad():
+    """In a residual block, bn1's output feeds conv2 alone: its backward statistics come from
+    conv2's dgrad (here EnhancedCNN layer3's 512-channel 4x4 block: the slab split-K sum; one
+    fused BN backward per step), while the block input -- read by the shortcut through its twin
+    -- keeps the BN's own reduce; the gradients match the unfused path."""
+    from ldnn.models.cnn import ResBlock
+    from ldnn.ops import functional as LF
+
+    torch.manual_seed(37)
+    grads = []
+    for fused in (False, True):
+        torch.manual_seed(37)
+        blk = ResBlock(512, 512).cuda()
+        flat = ldnn.prepare(blk, "cuda")
+        x = torch.randn(64, 512, 4, 4, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+        old = LF.CONV_BN_BWD
+        LF.CONV_BN_BWD = fused
+        try:
+            for it in range(2):   # step 2: the lazily zeroed gradients (their first writer overwrites)
+                flat.zero_grad(lazy=True)
+                xi = x.detach().clone().requires_grad_(True)
+                n0 = LF.BN_BWD_FUSED[0]
+                y = blk(xi)
+                y.float().square().sum().backward()
+                torch.cuda.synchronize()
+            assert LF.BN_BWD_FUSED[0] - n0 == (1 if fused else 0)
+        finally:
+            LF.CONV_BN_BWD = old
+        grads.append([xi.grad.float()] + [p.grad.float().clone() for p in blk.parameters()])
+    for a, b in zip(grads[0], grads[1]):
+        torch.testing.assert_close(b, a, rtol=2e-2, atol=2e-2 * a.abs().max().item())
