@@ -956,19 +956,14 @@ bool conv_fwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& y, int
 // bn_x given: dx is the gradient of a training BatchNorm(+ReLU)'s output (bn_x = that BN's
 // input, bn_mask its ReLU bits); returns whether the dgrad's epilogue also accumulated and
 // finalized that BN's backward statistics (then bn_bwd(..., stats_ready=True) applies them).
-bool conv_dgrad(const at::Tensor& dy, const at::Tensor& w, const at::Tensor& dx, int64_t stride, int64_t pad,
-                const c10::optional<at::Tensor>& bn_x, const c10::optional<at::Tensor>& bn_mask,
-                const c10::optional<at::Tensor>& bn_ws, const c10::optional<at::Tensor>& bn_gamma,
-                const c10::optional<at::Tensor>& bn_save_mean, const c10::optional<at::Tensor>& bn_save_invstd,
-                const c10::optional<at::Tensor>& bn_dgamma, const c10::optional<at::Tensor>& bn_dbeta,
-                bool bn_assign) {
-  check_dev(dy, at::kBFloat16, "dy");
-  check_dev(w, at::kBFloat16, "w");
-  check_dev(dx, at::kBFloat16, "dx");
-  ldnn::ConvShape s = conv_shape(dx, w, dy, stride, pad);
-  c10::hip::HIPGuardMasqueradingAsCUDA g(dy.device());
-  const ConvWs ws = conv_ws(s, 1, dy);
-  ldnn::BnBwdFuse fuse{};
+// The BnBwdFuse of conv_dgrad / conv_bwd's optional BN arguments (nullptr without bn_x).
+const ldnn::BnBwdFuse* bn_bwd_fuse(ldnn::BnBwdFuse& fuse, const ldnn::ConvShape& s,
+                                   const c10::optional<at::Tensor>& bn_x, const c10::optional<at::Tensor>& bn_mask,
+                                   const c10::optional<at::Tensor>& bn_ws, const c10::optional<at::Tensor>& bn_gamma,
+                                   const c10::optional<at::Tensor>& bn_save_mean,
+                                   const c10::optional<at::Tensor>& bn_save_invstd,
+                                   const c10::optional<at::Tensor>& bn_dgamma,
+                                   const c10::optional<at::Tensor>& bn_dbeta, bool bn_assign) {
   const ldnn::BnBwdFuse* fp = nullptr;
   if (bn_x.has_value()) {
     const int C = s.C;
@@ -994,17 +989,32 @@ bool conv_dgrad(const at::Tensor& dy, const at::Tensor& w, const at::Tensor& dx,
     }
     fp = &fuse;
   }
+  return fp;
+}
+
+bool conv_dgrad(const at::Tensor& dy, const at::Tensor& w, const at::Tensor& dx, int64_t stride, int64_t pad,
+                const c10::optional<at::Tensor>& bn_x, const c10::optional<at::Tensor>& bn_mask,
+                const c10::optional<at::Tensor>& bn_ws, const c10::optional<at::Tensor>& bn_gamma,
+                const c10::optional<at::Tensor>& bn_save_mean, const c10::optional<at::Tensor>& bn_save_invstd,
+                const c10::optional<at::Tensor>& bn_dgamma, const c10::optional<at::Tensor>& bn_dbeta,
+                bool bn_assign) {
+  check_dev(dy, at::kBFloat16, "dy");
+  check_dev(w, at::kBFloat16, "w");
+  check_dev(dx, at::kBFloat16, "dx");
+  ldnn::ConvShape s = conv_shape(dx, w, dy, stride, pad);
+  c10::hip::HIPGuardMasqueradingAsCUDA g(dy.device());
+  const ConvWs ws = conv_ws(s, 1, dy);
+  ldnn::BnBwdFuse fuse{};
+  const ldnn::BnBwdFuse* fp = bn_bwd_fuse(fuse, s, bn_x, bn_mask, bn_ws, bn_gamma, bn_save_mean, bn_save_invstd,
+                                          bn_dgamma, bn_dbeta, bn_assign);
   bool done = false;
   check(ldnn::conv2d_dgrad(s, bf16_ptr(dy), bf16_ptr(w), bf16_mut(dx), cur_stream(dy), ws.ws(), ws.c(), fp, &done),
         "conv2d_dgrad");
   return done;
 }
 
-void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& dw, int64_t stride, int64_t pad,
-                double beta, int64_t real_channels) {
-  check_dev(dy, at::kBFloat16, "dy");
-  check_dev(x, at::kBFloat16, "x");
-  check_dev(dw, at::kFloat, "dw");
+ldnn::ConvShape wgrad_shape(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& dw, int64_t stride,
+                            int64_t pad, int64_t real_channels) {
   TORCH_CHECK(dw.dim() == 4 && dw.is_contiguous(), "conv_wgrad: dw must be a dense [K][R][S][C] fp32 tensor");
   ldnn::ConvShape s{};
   TORCH_CHECK(x.dim() == 4 && dy.dim() == 4 && x.is_contiguous() && dy.is_contiguous(), "conv_wgrad: layout");
@@ -1015,6 +1025,44 @@ void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& dw,
   s.c_real = real_channels > 0 && real_channels < s.C ? (int)real_channels : 0;
   TORCH_CHECK(dw.size(3) == s.C && dy.size(3) == s.K && dy.size(0) == s.N, "conv_wgrad: shape mismatch");
   TORCH_CHECK(s.C % 8 == 0 && s.K % 8 == 0, "conv_wgrad: channels must be multiples of 8");
+  return s;
+}
+
+// A conv layer's backward: dx (conv_dgrad, optional BN statistics) AND dw (conv_wgrad, beta /
+// real_channels) from one dy -- one launch for both where the kernels allow (conv2d_bwd).
+bool conv_bwd(const at::Tensor& dy, const at::Tensor& w, const at::Tensor& dx, const at::Tensor& x,
+              const at::Tensor& dw, int64_t stride, int64_t pad, double beta, int64_t real_channels,
+              const c10::optional<at::Tensor>& bn_x, const c10::optional<at::Tensor>& bn_mask,
+              const c10::optional<at::Tensor>& bn_ws, const c10::optional<at::Tensor>& bn_gamma,
+              const c10::optional<at::Tensor>& bn_save_mean, const c10::optional<at::Tensor>& bn_save_invstd,
+              const c10::optional<at::Tensor>& bn_dgamma, const c10::optional<at::Tensor>& bn_dbeta,
+              bool bn_assign) {
+  check_dev(dy, at::kBFloat16, "dy");
+  check_dev(w, at::kBFloat16, "w");
+  check_dev(dx, at::kBFloat16, "dx");
+  check_dev(x, at::kBFloat16, "x");
+  check_dev(dw, at::kFloat, "dw");
+  const ldnn::ConvShape sd = conv_shape(dx, w, dy, stride, pad);
+  const ldnn::ConvShape sw = wgrad_shape(dy, x, dw, stride, pad, real_channels);
+  c10::hip::HIPGuardMasqueradingAsCUDA g(dy.device());
+  const ConvWs wsd = conv_ws(sd, 1, dy);
+  const ConvWs wsw = conv_ws(sw, 2, dy);
+  ldnn::BnBwdFuse fuse{};
+  const ldnn::BnBwdFuse* fp = bn_bwd_fuse(fuse, sd, bn_x, bn_mask, bn_ws, bn_gamma, bn_save_mean, bn_save_invstd,
+                                          bn_dgamma, bn_dbeta, bn_assign);
+  bool done = false;
+  check(ldnn::conv2d_bwd(sd, bf16_ptr(dy), bf16_ptr(w), bf16_mut(dx), wsd.ws(), wsd.c(), fp, &done, sw, bf16_ptr(x),
+                         dw.data_ptr<float>(), (float)beta, wsw.ws(), cur_stream(dy)),
+        "conv2d_bwd");
+  return done;
+}
+
+void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& dw, int64_t stride, int64_t pad,
+                double beta, int64_t real_channels) {
+  check_dev(dy, at::kBFloat16, "dy");
+  check_dev(x, at::kBFloat16, "x");
+  check_dev(dw, at::kFloat, "dw");
+  const ldnn::ConvShape s = wgrad_shape(dy, x, dw, stride, pad, real_channels);
   c10::hip::HIPGuardMasqueradingAsCUDA g(dy.device());
   const ConvWs ws = conv_ws(s, 2, dy);
   check(ldnn::conv2d_wgrad(s, bf16_ptr(dy), bf16_ptr(x), dw.data_ptr<float>(), (float)beta, cur_stream(dy), ws.ws()),
@@ -1830,6 +1878,15 @@ PYBIND11_MODULE(_C, m) {
         py::arg("bn_gamma") = py::none(), py::arg("bn_save_mean") = py::none(),
         py::arg("bn_save_invstd") = py::none(), py::arg("bn_dgamma") = py::none(), py::arg("bn_dbeta") = py::none(),
         py::arg("bn_assign") = false);
+  m.def("conv_bwd", &conv_bwd, py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("x"), py::arg("dw"),
+        py::arg("stride"), py::arg("pad"), py::arg("beta") = 0.0, py::arg("real_channels") = 0,
+        py::arg("bn_x") = py::none(), py::arg("bn_mask") = py::none(), py::arg("bn_ws") = py::none(),
+        py::arg("bn_gamma") = py::none(), py::arg("bn_save_mean") = py::none(),
+        py::arg("bn_save_invstd") = py::none(), py::arg("bn_dgamma") = py::none(), py::arg("bn_dbeta") = py::none(),
+        py::arg("bn_assign") = false,
+        "conv_dgrad + conv_wgrad of one layer (one launch where the kernels allow); returns conv_dgrad's flag");
+  m.def("set_conv_pair", &ldnn::set_conv_pair, "dgrad + wgrad in one launch (1, default) or one by one (0)");
+  m.def("get_conv_pair", &ldnn::get_conv_pair);
   m.def("conv_wgrad", &conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("dw"), py::arg("stride"), py::arg("pad"),
         py::arg("beta") = 0.0, py::arg("real_channels") = 0,
         "real_channels: channels of x that carry data (the rest zero padding, e.g. 3 of a stem's 8); 0 = all");

@@ -88,17 +88,21 @@ __device__ __forceinline__ float apply_epi(float v, float bias, float aux) {
   return v;
 }
 
-// Tile id -> (tm, tn): XCD remap, then GROUP_M-row groups for L2 reuse.
-__device__ __forceinline__ void tile_coords(int M, int N, int BMt, int BNt, int& m0, int& n0) {
+// Tile id -> (tm, tn): XCD remap, then GROUP_M-row groups for L2 reuse.  (bid: the workgroup's
+// x index -- blockIdx.x, or a virtual one when two GEMMs share a launch)
+__device__ __forceinline__ void tile_coords_id(int M, int N, int BMt, int BNt, int bid, int& m0, int& n0) {
   const int tiles_m = (M + BMt - 1) / BMt, tiles_n = (N + BNt - 1) / BNt;
   const int nwg = tiles_m * tiles_n;
-  const int id = xcd_remap(blockIdx.x, nwg);
+  const int id = xcd_remap(bid, nwg);
   const int per_group = GROUP_M * tiles_n;
   const int group = id / per_group;
   const int first_m = group * GROUP_M;
   const int gsize = min(tiles_m - first_m, GROUP_M);
   m0 = (first_m + (id % per_group) % gsize) * BMt;
   n0 = ((id % per_group) / gsize) * BNt;
+}
+__device__ __forceinline__ void tile_coords(int M, int N, int BMt, int BNt, int& m0, int& n0) {
+  tile_coords_id(M, N, BMt, BNt, (int)blockIdx.x, m0, n0);
 }
 
 // ---- fused optimizer update of 4 consecutive weights (EPI_OPT_*) -------------

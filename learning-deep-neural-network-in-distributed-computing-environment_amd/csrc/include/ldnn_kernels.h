@@ -121,6 +121,11 @@ hipError_t conv2d_dgrad(const ConvShape& s, const uint16_t* dy, const uint16_t* 
                         bool* bn_done = nullptr);
 hipError_t conv2d_wgrad(const ConvShape& s, const uint16_t* dy, const uint16_t* x, float* dw, float beta,
                         hipStream_t st, float* ws = nullptr);
+// A layer's dgrad (shape sd, as conv2d_dgrad) and wgrad (shape sw, as conv2d_wgrad), both reading
+// dy: ONE launch when both take the 4-wave gather kernels (conv2d_bwd_lds), else one by one.
+hipError_t conv2d_bwd(const ConvShape& sd, const uint16_t* dy, const uint16_t* w, uint16_t* dx, float* ws_d,
+                      int* cnt_d, const BnBwdFuse* bnb, bool* bn_done, const ConvShape& sw, const uint16_t* x,
+                      float* dw, float beta, float* ws_w, hipStream_t st);
 // LDS-DMA fast path (conv_lds.hip): hipErrorNotSupported outside its shape set
 // (fwd needs C % 64 == 0, dgrad K % 64 == 0, stride 1 or 2).
 // bn_used: whether the epilogue accumulated the BN statistics (a slab split-K shape does not)
@@ -131,6 +136,13 @@ hipError_t conv2d_dgrad_lds(const ConvShape& s, const uint16_t* dy, const uint16
                             float* ws, int* cnt, const BnBwdFuse* bnb = nullptr, bool* bn_used = nullptr);
 hipError_t conv2d_wgrad_lds(const ConvShape& s, const uint16_t* dy, const uint16_t* x, float* dw, float beta,
                             hipStream_t st, float* ws);
+// hipErrorNotSupported: the pair does not share a launch (conv2d_bwd runs them one by one)
+hipError_t conv2d_bwd_lds(const ConvShape& sd, const uint16_t* dy, const uint16_t* w, uint16_t* dx, float* ws_d,
+                          int* cnt_d, const BnBwdFuse* bnb, bool* bn_used, const ConvShape& sw, const uint16_t* x,
+                          float* dw, float beta, float* ws_w, hipStream_t st);
+// dgrad + wgrad in one launch (LDNN_CONV_PAIR, default 1; the setter is for tests / A/B)
+void set_conv_pair(int on);
+int get_conv_pair();
 struct ConvWorkspace {
   size_t slab_bytes = 0;  // fp32 split-K slabs (0: the shape runs unsplit)
   int counters = 0;       // int arrival counters, zeroed

@@ -340,6 +340,19 @@ hipError_t conv2d_fwd(const ConvShape& s, const uint16_t* x, const uint16_t* w, 
   return hipGetLastError();
 }
 
+hipError_t conv2d_bwd(const ConvShape& sd, const uint16_t* dy, const uint16_t* w, uint16_t* dx, float* ws_d,
+                      int* cnt_d, const BnBwdFuse* bnb, bool* bn_done, const ConvShape& sw, const uint16_t* x,
+                      float* dw, float beta, float* ws_w, hipStream_t st) {
+  if (bn_done) *bn_done = false;
+  if (g_conv_impl == 0) {
+    const hipError_t e = conv2d_bwd_lds(sd, dy, w, dx, ws_d, cnt_d, bnb, bn_done, sw, x, dw, beta, ws_w, st);
+    if (e != hipErrorNotSupported) return e;
+  }
+  const hipError_t e = conv2d_dgrad(sd, dy, w, dx, st, ws_d, cnt_d, bnb, bn_done);
+  if (e != hipSuccess) return e;
+  return conv2d_wgrad(sw, dy, x, dw, beta, st, ws_w);
+}
+
 hipError_t conv2d_dgrad(const ConvShape& s, const uint16_t* dy, const uint16_t* w, uint16_t* dx, hipStream_t st,
                         float* ws, int* cnt, const BnBwdFuse* bnb, bool* bn_done) {
   if (bn_done) *bn_done = false;

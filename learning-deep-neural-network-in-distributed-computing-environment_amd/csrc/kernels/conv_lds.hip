@@ -88,13 +88,22 @@ struct LArgs {
 // of one slice -- which read the same activation rows (a wgrad's filter-tap / channel tiles
 // over one npq range) -- are dispatched to ONE XCD and share its L2 instead of each of 8
 // XCDs fetching those rows from the Infinity Cache / HBM.
-__device__ __forceinline__ void split_coords(const LArgs& a, int& bx, int& by) {
-  bx = blockIdx.x;
-  by = blockIdx.y;
-  if (a.xcd_split && gridDim.y > 1) {
-    const int id = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
-    bx = id % gridDim.x;
-    by = id / gridDim.x;
+// The workgroup's grid coordinates: the hardware's, or virtual ones when two convolutions share
+// one launch (conv_pair_kernel: a layer's dgrad and wgrad side by side).
+struct VB {
+  int x, y, z, gx, gy;
+};
+__device__ __forceinline__ VB hw_vb() {
+  return VB{(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z, (int)gridDim.x, (int)gridDim.y};
+}
+
+__device__ __forceinline__ void split_coords(const LArgs& a, const VB& vb, int& bx, int& by) {
+  bx = vb.x;
+  by = vb.y;
+  if (a.xcd_split && vb.gy > 1) {
+    const int id = xcd_remap(vb.x + vb.y * vb.gx, vb.gx * vb.gy);
+    bx = id % vb.gx;
+    by = id / vb.gx;
   }
 }
 
@@ -108,7 +117,7 @@ struct Geo {
   FastDiv f_rw, f_rh;      // division by rows_w / rows_h
 };
 
-__device__ __forceinline__ Geo make_geo(const LArgs& a, bool dgrad) {
+__device__ __forceinline__ Geo make_geo(const LArgs& a, bool dgrad, int cls) {
   Geo g;
   const ConvShape& s = a.s;
   g.hmul = 1; g.hoff = 0; g.woff = 0; g.r0 = 0; g.s0 = 0; g.step = 1; g.nS = s.S;
@@ -122,7 +131,7 @@ __device__ __forceinline__ Geo make_geo(const LArgs& a, bool dgrad) {
   g.rows_h = s.H; g.rows_w = s.W;
   g.f_rh = a.f_h; g.f_rw = a.f_w;
   if (a.classes == 4) {
-    const int ph = blockIdx.z >> 1, pw = blockIdx.z & 1;
+    const int ph = cls >> 1, pw = cls & 1;
     g.hmul = 2; g.hoff = ph; g.woff = pw;
     g.rows_h = (s.H - ph + 1) >> 1;
     g.rows_w = (s.W - pw + 1) >> 1;
@@ -672,21 +681,22 @@ __device__ __forceinline__ void wait_vm() {
 // (lds_floats floats), free once every wave is past its operand reads.
 template <int WM, int WN, int EPI, bool OUT_F32, bool DGRAD>
 __device__ __forceinline__ void conv_tail(const LArgs& a, const Geo& g, floatx4 (&acc)[4][4], int m0, int n0, int wm,
-                                          int wn, int lane, char* smem, int lds_floats, int bx, int by) {
+                                          int wn, int lane, char* smem, int lds_floats, int bx, int by,
+                                          const VB& vb) {
   constexpr int NW = WM * WN;
-  const bool combine = a.cnt != nullptr && gridDim.y > 1;
+  const bool combine = a.cnt != nullptr && vb.gy > 1;
   const int mb = m0 + wm * 64, nbase = n0 + wn * 64;
-  if (gridDim.y > 1) {
+  if (vb.gy > 1) {
     if (combine) {
       lds_barrier();  // every wave is done with the operand stages (the ticket word lives there)
-      const int tile = blockIdx.z * a.tiles_x + bx;
+      const int tile = vb.z * a.tiles_x + bx;
       // (phase-trace builds: stamps 4..6 of this workgroup's trace row, see splitk_combine)
       uint64_t* tr = (a.trace != nullptr && threadIdx.x == 0)
-                         ? a.trace + 8 * (size_t)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z))
+                         ? a.trace + 8 * (size_t)(vb.x + vb.gx * (vb.y + vb.gy * vb.z))
                          : nullptr;
       if (a.xcd_split || !a.combine_last) {
-        if (!splitk_combine<4, 4, NW * 64>(acc, a.ws, a.cnt, tile, gridDim.y, by, smem, tr)) return;
-      } else if (!splitk_combine_last<4, 4, NW * 64>(acc, a.ws, a.cnt, tile, gridDim.y, by, smem, tr)) {
+        if (!splitk_combine<4, 4, NW * 64>(acc, a.ws, a.cnt, tile, vb.gy, by, smem, tr)) return;
+      } else if (!splitk_combine_last<4, 4, NW * 64>(acc, a.ws, a.cnt, tile, vb.gy, by, smem, tr)) {
         return;
       }
     } else if (a.ws != nullptr) {
@@ -778,9 +788,10 @@ __device__ __forceinline__ void conv_tail(const LArgs& a, const Geo& g, floatx4 
 // 16-KiB-aligned chunks instead of the im2col gather, bit2 no fragment reads / MFMAs, bit5 phase
 // trace: wave 0 stamps s_memrealtime (100 MHz) at entry, after the first K-tile landed, after
 // the main loop and at exit into a.trace[workgroup][4] (scripts/conv_phase_trace.py)
+// (the body of conv_lds_kernel: smem = its NS-stage LDS ring, vb = its grid coordinates)
 template <int WM, int WN, class OA, class OB, int EPI, bool OUT_F32, bool DGRAD, int NS, int XF = 0>
-__global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void conv_lds_kernel(LArgs a, const bf16_t* pa, uint32_t bytes_a,
-                                                                       const bf16_t* pb, uint32_t bytes_b) {
+__device__ __forceinline__ void conv_lds_body(const LArgs& a, const bf16_t* pa, uint32_t bytes_a, const bf16_t* pb,
+                                              uint32_t bytes_b, const VB& vb, char* smem) {
   constexpr int NW = WM * WN, BM = WM * 64, BN = WN * 64;
   static_assert(NW == 4, "4-wave workgroups (the launch bounds and the split-K slab size assume it)");
   static_assert(OA::kRows == BM && OB::kRows == BN && OA::kPieces == BM / 8 / NW && OB::kPieces == BN / 8 / NW,
@@ -790,34 +801,33 @@ __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void conv_lds_kernel(LArgs a,
   static_assert(PPA >= 1 && PPB >= 1 && PPA * NW * 8 == BM && PPB * NW * 8 == BN, "DMA pieces");
   constexpr int PER_TILE = PPA + PPB;  // DMA instructions per lane per K-tile
   static_assert(NS >= 2 && NS * STAGE <= 160 * 1024 && PER_TILE * (NS - 2) < 64, "LDS ring");
-  __shared__ __attribute__((aligned(1024))) char smem[NS * STAGE];
 
-  const Geo g = make_geo(a, DGRAD);
+  const Geo g = make_geo(a, DGRAD, vb.z);
   const int tiles_m = (g.M + BM - 1) / BM, tiles_n = (a.N + BN - 1) / BN;
   uint64_t* trace = nullptr;
   if constexpr ((XF & 32) != 0) {
     if (threadIdx.x == 0 && a.trace != nullptr) {
-      trace = a.trace + 8 * (size_t)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z));
+      trace = a.trace + 8 * (size_t)(vb.x + vb.gx * (vb.y + vb.gy * vb.z));
       trace[0] = __builtin_amdgcn_s_memrealtime();
     }
   }
   int bx, by;
-  split_coords(a, bx, by);
+  split_coords(a, vb, bx, by);
   if (bx >= tiles_m * tiles_n) return;  // a smaller parity class: whole workgroup exits
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wid / WN, wn = wid % WN;
   int m0, n0;
-  if (a.xcd_split && gridDim.y > 1) {  // the XCD placement is split_coords'; tiles in row-major order
+  if (a.xcd_split && vb.gy > 1) {  // the XCD placement is split_coords'; tiles in row-major order
     m0 = (bx / tiles_n) * BM;
     n0 = (bx % tiles_n) * BN;
   } else {
-    tile_coords(g.M, a.N, BM, BN, m0, n0);
+    tile_coords_id(g.M, a.N, BM, BN, vb.x, m0, n0);
   }
   const int kt0 = by * a.nk_split;
   const int nk = max(0, min(g.nk - kt0, a.nk_split));
-  const bool combine = a.cnt != nullptr && gridDim.y > 1;
-  if (nk == 0 && gridDim.y > 1 && !combine && a.ws == nullptr) return;  // an empty atomic slice adds nothing
+  const bool combine = a.cnt != nullptr && vb.gy > 1;
+  if (nk == 0 && vb.gy > 1 && !combine && a.ws == nullptr) return;  // an empty atomic slice adds nothing
 
   floatx4 acc[4][4];
 #pragma unroll
@@ -909,10 +919,47 @@ __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void conv_lds_kernel(LArgs a,
   if constexpr ((XF & 32) != 0) {
     if (trace != nullptr) trace[2] = __builtin_amdgcn_s_memrealtime();
   }
-  conv_tail<WM, WN, EPI, OUT_F32, DGRAD>(a, g, acc, m0, n0, wm, wn, lane, smem, NS * STAGE / 4, bx, by);
+  conv_tail<WM, WN, EPI, OUT_F32, DGRAD>(a, g, acc, m0, n0, wm, wn, lane, smem, NS * STAGE / 4, bx, by, vb);
   if constexpr ((XF & 32) != 0) {
     if (trace != nullptr) trace[3] = __builtin_amdgcn_s_memrealtime();
   }
+}
+
+template <int WM, int WN, class OA, class OB, int EPI, bool OUT_F32, bool DGRAD, int NS, int XF = 0>
+__global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void conv_lds_kernel(LArgs a, const bf16_t* pa, uint32_t bytes_a,
+                                                                       const bf16_t* pb, uint32_t bytes_b) {
+  constexpr int STAGE = (WM + WN) * 64 * 128;
+  __shared__ __attribute__((aligned(1024))) char smem[NS * STAGE];
+  conv_lds_body<WM, WN, OA, OB, EPI, OUT_F32, DGRAD, NS, XF>(a, pa, bytes_a, pb, bytes_b, hw_vb(), smem);
+}
+
+// A layer's dgrad (body 0) and wgrad (body 1) in ONE launch: workgroups [0, n0) run the dgrad
+// over its (gx0, gy0, gz0) grid, the rest the wgrad over (gx1, gy1) -- the two GEMMs share the
+// chip instead of each leaving CUs idle behind a small grid (EnhancedCNN's 16x16 .. 2x2 stages,
+// ResNet-18 at b64).  n0 is a multiple of 8, so the wgrad's virtual ids keep their XCD placement.
+struct PairArgs {
+  LArgs a[2];
+  const bf16_t* pa[2];
+  const bf16_t* pb[2];
+  uint32_t ba[2], bb[2];
+  int gx[2], gy[2], gz[2];
+  int n0;
+};
+template <int WM0, int WN0, class OA0, class OB0, int WM1, int WN1, class OA1, class OB1>
+__global__ __launch_bounds__(256, 2) void conv_pair_kernel(PairArgs p) {
+  constexpr int ST0 = (WM0 + WN0) * 64 * 128, ST1 = (WM1 + WN1) * 64 * 128;
+  constexpr int LDS = 2 * (ST0 > ST1 ? ST0 : ST1);
+  __shared__ __attribute__((aligned(1024))) char smem[LDS];
+  int b = (int)blockIdx.x;
+  const int k = b >= p.n0 ? 1 : 0;
+  if (k) b -= p.n0;
+  const int gx = p.gx[k], gy = p.gy[k];
+  if (b >= gx * gy * p.gz[k]) return;  // (the dgrad's id range is padded to a multiple of 8)
+  const VB vb{b % gx, (b / gx) % gy, b / (gx * gy), gx, gy};
+  if (k == 0)
+    conv_lds_body<WM0, WN0, OA0, OB0, EPI_NONE, false, true, 2>(p.a[0], p.pa[0], p.ba[0], p.pb[0], p.bb[0], vb, smem);
+  else
+    conv_lds_body<WM1, WN1, OA1, OB1, EPI_NONE, true, false, 2>(p.a[1], p.pa[1], p.ba[1], p.pb[1], p.bb[1], vb, smem);
 }
 
 // ---- halo path: 3x3 stride-1 pad-1 fwd / dgrad with the A operand staged ONCE --
@@ -956,7 +1003,7 @@ __global__ __launch_bounds__(256, 2) void conv_halo_kernel(LArgs a, const bf16_t
   char* const zrow = smem + H_BYTES;  // 128 zero bytes: the A fragment of a tap outside the image
   char* const bst = smem + H_BYTES + Z_BYTES;
 
-  const Geo g = make_geo(a, DGRAD);
+  const Geo g = make_geo(a, DGRAD, (int)blockIdx.z);
   const int tiles_m = (g.M + BM - 1) / BM, tiles_n = (a.N + BN - 1) / BN;
   uint64_t* trace = nullptr;
   if constexpr ((XF & 32) != 0) {
@@ -1085,7 +1132,8 @@ __global__ __launch_bounds__(256, 2) void conv_halo_kernel(LArgs a, const bf16_t
   if constexpr ((XF & 32) != 0) {
     if (trace != nullptr) trace[2] = __builtin_amdgcn_s_memrealtime();
   }
-  conv_tail<WM, WN, EPI, false, DGRAD>(a, g, acc, m0, n0, wm, wn, lane, smem, LDS / 4, blockIdx.x, blockIdx.y);
+  conv_tail<WM, WN, EPI, false, DGRAD>(a, g, acc, m0, n0, wm, wn, lane, smem, LDS / 4, blockIdx.x, blockIdx.y,
+                                       hw_vb());
   if constexpr ((XF & 32) != 0) {
     if (trace != nullptr) trace[3] = __builtin_amdgcn_s_memrealtime();
   }
@@ -1151,7 +1199,7 @@ __global__ __launch_bounds__(512, 1) void conv_hb_kernel(LArgs a, const bf16_t* 
   char* const bst = smem + 2 * kHaloBytes;
   char* const zrow = bst + kNSB * kBBytes;  // 128 zero bytes: the A fragment of a tap outside the image
 
-  const Geo g = make_geo(a, DGRAD);
+  const Geo g = make_geo(a, DGRAD, (int)blockIdx.z);
   const int tiles_m = (g.M + BM - 1) / BM, tiles_n = (a.N + BN - 1) / BN;
   const int bx = blockIdx.x, by = blockIdx.y;
   if (bx >= tiles_m * tiles_n) return;
@@ -1269,7 +1317,7 @@ __global__ __launch_bounds__(512, 1) void conv_hb_kernel(LArgs a, const bf16_t* 
       }
     }
   }
-  conv_tail<WM, WN, EPI, false, DGRAD>(a, g, acc, m0, n0, wm, wn, lane, smem, hb::kLds / 4, bx, by);
+  conv_tail<WM, WN, EPI, false, DGRAD>(a, g, acc, m0, n0, wm, wn, lane, smem, hb::kLds / 4, bx, by, hw_vb());
 }
 
 // ---- weight-stationary persistent halo conv: 64 -> 64 channels, 3x3 stride 1 pad 1 ----
@@ -1327,7 +1375,7 @@ __global__ __launch_bounds__(256, 1) void conv_ws64_kernel(LArgs a, const bf16_t
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wid >> 1, wn = wid & 1;
-  const Geo g = make_geo(a, DGRAD);
+  const Geo g = make_geo(a, DGRAD, (int)blockIdx.z);
   const int W = g.rows_w, P = g.rows_h;
   const int T = (g.M + BM - 1) / BM;
   const int t0 = (int)((int64_t)blockIdx.x * T / gridDim.x);
@@ -1906,7 +1954,7 @@ __global__ __launch_bounds__(256, 2) void conv_patch_kernel(LArgs a, const bf16_
   constexpr int WM = 4, WN = 1, BM = 256, BN = 64;
   __shared__ __attribute__((aligned(1024))) char smem[kPatchBytes];
   const ConvShape& sh = a.s;
-  const Geo g = make_geo(a, false);
+  const Geo g = make_geo(a, false, (int)blockIdx.z);
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wid, wn = 0;
@@ -1990,7 +2038,7 @@ __global__ __launch_bounds__(256, 2) void conv_patch_kernel(LArgs a, const bf16_
         acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[k & 1][j], fa[i], acc[j][i], 0, 0, 0);
   }
   conv_tail<WM, WN, EPI, false, false>(a, g, acc, m0, n0, wm, wn, lane, smem, kPatchBytes / 4, blockIdx.x,
-                                       blockIdx.y);
+                                       blockIdx.y, hw_vb());
 }
 
 // Persistent weight-stationary variant of conv_patch_kernel for 64-filter stems (the ResNet-18
@@ -2011,7 +2059,7 @@ __global__ __launch_bounds__(256, 1) void conv_patch_ws_kernel(LArgs a, const bf
   constexpr int LDS = 2 * kPatchBytes + 16;
   __shared__ __attribute__((aligned(1024))) char smem[LDS];
   const ConvShape& sh = a.s;
-  const Geo g = make_geo(a, false);
+  const Geo g = make_geo(a, false, (int)blockIdx.z);
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int PQ = sh.P * sh.Q, PW = sh.W + 2 * sh.pad, RS = sh.R * sh.S;
@@ -3149,14 +3197,24 @@ hipError_t conv2d_fwd_lds(const ConvShape& s, const uint16_t* x, const uint16_t*
   return conv_slab_epilogue(ws, y, a.M, a.N, pl.splits, bias, epi, st);
 }
 
-hipError_t conv2d_dgrad_lds(const ConvShape& s, const uint16_t* dy, const uint16_t* w, uint16_t* dx, hipStream_t st,
-                            float* ws, int* cnt, const BnBwdFuse* bnb, bool* bn_used) {
-  if (bn_used) *bn_used = false;
-  if (s.K % 64 != 0 || !shape_ok(s)) return hipErrorNotSupported;
-  if (s.N * s.H * s.W <= 0) return hipSuccess;
-  const bool hbp = hb_takes(s, true);
-  Plan pl = hbp ? plan_hb(s, true) : plan_dgrad(s);
-  LArgs a = base_args(s);
+namespace {
+// What conv2d_dgrad_lds launches, planned without launching it (conv2d_bwd_lds can then
+// issue the main kernel together with the wgrad's).
+struct DgradPrep {
+  LArgs a;
+  Plan pl;
+  bool slab, hb, halo, ws64;
+  const BnBwdFuse* slab_bnb;
+  size_t bdy, bw;
+};
+
+DgradPrep dgrad_prep(const ConvShape& s, uint16_t* dx, float* ws, int* cnt, const BnBwdFuse* bnb) {
+  DgradPrep d{};
+  d.hb = hb_takes(s, true);
+  Plan& pl = d.pl;
+  pl = d.hb ? plan_hb(s, true) : plan_dgrad(s);
+  LArgs& a = d.a;
+  a = base_args(s);
   a.out = dx;
   a.M = s.N * s.H * s.W;
   a.N = s.C;
@@ -3164,8 +3222,8 @@ hipError_t conv2d_dgrad_lds(const ConvShape& s, const uint16_t* dy, const uint16
   a.classes = pl.classes;
   a.tiles_x = pl.tiles_x;
   a.nk_all = pl.nk_all;
-  const bool slab = pl.splits > 1 && pl.slab && ws != nullptr;
-  if (slab) {
+  d.slab = pl.splits > 1 && pl.slab && ws != nullptr;
+  if (d.slab) {
     a.ws = ws;
     a.nk_split = pl.nk_split;
   } else if (pl.splits > 1 && !pl.slab && ws != nullptr && cnt != nullptr) {
@@ -3176,19 +3234,21 @@ hipError_t conv2d_dgrad_lds(const ConvShape& s, const uint16_t* dy, const uint16
     pl.splits = 1;
     a.nk_split = pl.nk_all;
   }
-  const size_t bdy = (size_t)s.N * s.P * s.Q * s.K * 2, bw = (size_t)s.K * a.rsc * 2;
-  if (ws64_takes(s, EPI_NONE)) {
+  d.bdy = (size_t)s.N * s.P * s.Q * s.K * 2;
+  d.bw = (size_t)s.K * a.rsc * 2;
+  d.ws64 = ws64_takes(s, EPI_NONE);
+  if (d.ws64) {
     a.ws = nullptr;
     a.cnt = nullptr;
     a.nk_split = a.nk_all;
-    return launch_ws64<true>(a, dy, bdy, w, st);
+    return d;
   }
+  d.halo = !d.hb && halo_takes(s, pl.wm);
   // the BN backward statistics of the BN whose output's gradient dx is: stride-1 dgrads (no
   // class row remap) in the direct / in-launch combine epilogue, or in the slab sum
-  const BnBwdFuse* slab_bnb = nullptr;
   if (bnb != nullptr && bn_bwd_env() && s.stride == 1 && pl.classes == 1 && s.C % 8 == 0) {
-    if (slab) {
-      if (slab_bn_env() && bnb->fin.part != nullptr && bnb->fin.tickets != nullptr) slab_bnb = bnb;
+    if (d.slab) {
+      if (slab_bn_env() && bnb->fin.part != nullptr && bnb->fin.tickets != nullptr) d.slab_bnb = bnb;
     } else if (bn_bwd_env() >= 2) {
       a.bn_stats = 1;
       a.bn = bnb->fin;
@@ -3196,30 +3256,96 @@ hipError_t conv2d_dgrad_lds(const ConvShape& s, const uint16_t* dy, const uint16
       a.bn_mask = bnb->mask;
     }
   }
+  return d;
+}
+
+// after the main kernel: the slab split-K sum (with the BN statistics when taken)
+hipError_t dgrad_post(const DgradPrep& d, uint16_t* dx, float* ws, hipStream_t st, bool* bn_used) {
+  if (!d.slab) {
+    if (bn_used) *bn_used = d.a.bn_stats != 0;
+    return hipSuccess;
+  }
+  if (d.slab_bnb != nullptr) {
+    if (bn_used) *bn_used = true;
+    return conv_slab_bn(ws, dx, d.a.M, d.a.N, d.pl.splits, d.slab_bnb->fin, st, d.slab_bnb);
+  }
+  return conv_slab_epilogue(ws, dx, d.a.M, d.a.N, d.pl.splits, nullptr, EPI_NONE, st);
+}
+}  // namespace
+
+hipError_t conv2d_dgrad_lds(const ConvShape& s, const uint16_t* dy, const uint16_t* w, uint16_t* dx, hipStream_t st,
+                            float* ws, int* cnt, const BnBwdFuse* bnb, bool* bn_used) {
+  if (bn_used) *bn_used = false;
+  if (s.K % 64 != 0 || !shape_ok(s)) return hipErrorNotSupported;
+  if (s.N * s.H * s.W <= 0) return hipSuccess;
+  const DgradPrep d = dgrad_prep(s, dx, ws, cnt, bnb);
+  const LArgs& a = d.a;
+  const int splits = d.pl.splits;
+  if (d.ws64) return launch_ws64<true>(a, dy, d.bdy, w, st);
   hipError_t e;
-  if (hbp) {
-    e = launch_hb<DgradB<128, 2, 8>, true>(a, EPI_NONE, pl.splits, dy, bdy, w, bw, st);
-  } else if (halo_takes(s, pl.wm)) {
+  if (d.hb) {
+    e = launch_hb<DgradB<128, 2, 8>, true>(a, EPI_NONE, splits, dy, d.bdy, w, d.bw, st);
+  } else if (d.halo) {
     // dgrad likewise: C64 H56 38.9 -> 36.5 us; single-buffered on 128x128 tiles neutral to 1 us
     // slower (ResNet-18 C128-C512), up to 2.6 us slower on the EnhancedCNN 16x16 .. 2x2 stages
-    if (pl.wm == 4) e = launch_halo<4, 1, DgradB<64, 2, 4>, true>(a, EPI_NONE, pl.splits, dy, bdy, w, bw, st);
-    else e = launch_halo<2, 2, DgradB<128, 4, 4>, true>(a, EPI_NONE, pl.splits, dy, bdy, w, bw, st);
-  } else if (pl.wm == 4) {
-    e = launch<4, 1, DgradA<256, 8, 4>, DgradB<64, 2, 4>, false, true>(a, EPI_NONE, pl.splits, dy, bdy, w, bw, st);
+    if (d.pl.wm == 4) e = launch_halo<4, 1, DgradB<64, 2, 4>, true>(a, EPI_NONE, splits, dy, d.bdy, w, d.bw, st);
+    else e = launch_halo<2, 2, DgradB<128, 4, 4>, true>(a, EPI_NONE, splits, dy, d.bdy, w, d.bw, st);
+  } else if (d.pl.wm == 4) {
+    e = launch<4, 1, DgradA<256, 8, 4>, DgradB<64, 2, 4>, false, true>(a, EPI_NONE, splits, dy, d.bdy, w, d.bw, st);
   } else {
-    e = launch<2, 2, DgradA<128, 4, 4>, DgradB<128, 4, 4>, false, true>(a, EPI_NONE, pl.splits, dy, bdy, w, bw, st);
+    e = launch<2, 2, DgradA<128, 4, 4>, DgradB<128, 4, 4>, false, true>(a, EPI_NONE, splits, dy, d.bdy, w, d.bw, st);
   }
   if (e != hipSuccess) return e;
-  if (!slab) {
-    if (bn_used) *bn_used = a.bn_stats != 0;
-    return e;
-  }
-  if (slab_bnb != nullptr) {
-    if (bn_used) *bn_used = true;
-    return conv_slab_bn(ws, dx, a.M, a.N, pl.splits, slab_bnb->fin, st, slab_bnb);
-  }
-  return conv_slab_epilogue(ws, dx, a.M, a.N, pl.splits, nullptr, EPI_NONE, st);
+  return dgrad_post(d, dx, ws, st, bn_used);
 }
+
+namespace {
+// The 4-wave gather wgrad's launch (conv2d_wgrad_lds), planned without launching it.
+struct WgradPrep {
+  LArgs a;
+  int splits;
+  bool slab;
+  size_t bdy, bx;
+};
+
+WgradPrep wgrad_prep(const ConvShape& s, const WgradPlan& pl, float* dw, float beta, float* ws) {
+  WgradPrep w{};
+  LArgs& a = w.a;
+  a = base_args(s);
+  a.out = dw;
+  a.beta = beta;
+  a.M = s.K;
+  a.N = a.rsc;
+  a.Kd = s.N * s.P * s.Q;
+  a.nk_all = pl.nk_all;
+  a.nk_split = pl.nk_split;
+  a.tiles_x = pl.tiles;
+  a.nb = 0;
+  const int pq = s.P * s.Q;
+  a.dn = 64 / pq;
+  a.dp = (64 % pq) / s.Q;
+  a.dq = (64 % pq) % s.Q;
+  a.f_pq = make_fastdiv(pq);
+  a.f_q = make_fastdiv(s.Q);
+  a.f_c = make_fastdiv(s.C);
+  a.f_s = make_fastdiv(s.S);
+  w.splits = pl.splits;
+  a.xcd_split = w.splits > 1 ? wgrad_xcd_env() : 0;
+  w.slab = w.splits > 1 && ws != nullptr;
+  if (w.slab) a.ws = ws;  // partial slabs + slab_sum_kernel (else fp32 atomics into a cleared output)
+  w.bdy = (size_t)s.N * s.P * s.Q * s.K * 2;
+  w.bx = (size_t)s.N * s.H * s.W * s.C * 2;
+  return w;
+}
+
+hipError_t wgrad_post(const WgradPrep& w, float* dw, float beta, float* ws, hipStream_t st) {
+  if (!w.slab) return hipSuccess;
+  const int64_t n4 = (int64_t)w.a.M * w.a.N / 4;
+  if (slab_nt_env()) slab_sum_kernel<true><<<(unsigned)((n4 + 31) / 32), 256, 0, st>>>(ws, dw, n4, w.splits, beta);
+  else slab_sum_kernel<false><<<(unsigned)((n4 + 31) / 32), 256, 0, st>>>(ws, dw, n4, w.splits, beta);
+  return hipGetLastError();
+}
+}  // namespace
 
 hipError_t conv2d_wgrad_lds(const ConvShape& s, const uint16_t* dy, const uint16_t* x, float* dw, float beta,
                             hipStream_t st, float* ws) {
@@ -3270,45 +3396,83 @@ hipError_t conv2d_wgrad_lds(const ConvShape& s, const uint16_t* dy, const uint16
     else slab_sum_kernel<false><<<(unsigned)((n4 + 31) / 32), 256, 0, st>>>(ws, dw, n4, pl.splits, beta);
     return hipGetLastError();
   }
-  LArgs a = base_args(s);
-  a.out = dw;
-  a.beta = beta;
-  a.M = s.K;
-  a.N = a.rsc;
-  a.Kd = s.N * s.P * s.Q;
-  a.nk_all = pl.nk_all;
-  a.nk_split = pl.nk_split;
-  a.tiles_x = pl.tiles;
-  a.nb = 0;
-  const int pq = s.P * s.Q;
-  a.dn = 64 / pq;
-  a.dp = (64 % pq) / s.Q;
-  a.dq = (64 % pq) % s.Q;
-  a.f_pq = make_fastdiv(pq);
-  a.f_q = make_fastdiv(s.Q);
-  a.f_c = make_fastdiv(s.C);
-  a.f_s = make_fastdiv(s.S);
-  const int splits = pl.splits;
-  a.xcd_split = splits > 1 ? wgrad_xcd_env() : 0;
-  if (splits > 1) {
-    if (ws != nullptr) {
-      a.ws = ws;  // partial slabs + slab_sum_kernel
-    } else if (beta == 0.f) {  // no workspace: fp32 atomics into a cleared output
-      hipError_t e = zero2d_f32(dw, a.M, a.N, a.N, st);
-      if (e != hipSuccess) return e;
-    }
+  const WgradPrep wp = wgrad_prep(s, pl, dw, beta, ws);
+  if (pl.splits > 1 && ws == nullptr && beta == 0.f) {  // no workspace: fp32 atomics into a cleared output
+    hipError_t e = zero2d_f32(dw, wp.a.M, wp.a.N, wp.a.N, st);
+    if (e != hipSuccess) return e;
   }
-  const size_t bdy = (size_t)s.N * s.P * s.Q * s.K * 2, bx = (size_t)s.N * s.H * s.W * s.C * 2;
   hipError_t e;
   if (pl.narrow)
-    e = launch<1, 4, WgradA<64, 2, 4>, WgradB<256, 8, 4>, true, false>(a, EPI_NONE, splits, dy, bdy, x, bx, st);
+    e = launch<1, 4, WgradA<64, 2, 4>, WgradB<256, 8, 4>, true, false>(wp.a, EPI_NONE, pl.splits, dy, wp.bdy, x, wp.bx,
+                                                                       st);
   else
-    e = launch<2, 2, WgradA<128, 4, 4>, WgradB<128, 4, 4>, true, false>(a, EPI_NONE, splits, dy, bdy, x, bx, st);
-  if (e != hipSuccess || splits == 1 || ws == nullptr) return e;
-  const int64_t n4 = (int64_t)a.M * a.N / 4;
-  if (slab_nt_env()) slab_sum_kernel<true><<<(unsigned)((n4 + 31) / 32), 256, 0, st>>>(ws, dw, n4, splits, beta);
-  else slab_sum_kernel<false><<<(unsigned)((n4 + 31) / 32), 256, 0, st>>>(ws, dw, n4, splits, beta);
+    e = launch<2, 2, WgradA<128, 4, 4>, WgradB<128, 4, 4>, true, false>(wp.a, EPI_NONE, pl.splits, dy, wp.bdy, x,
+                                                                         wp.bx, st);
+  if (e != hipSuccess) return e;
+  return wgrad_post(wp, dw, beta, ws, st);
+}
+
+// A layer's dgrad and wgrad (both reading dy) as ONE launch (conv_pair_kernel) when both take
+// the 4-wave gather kernels; hipErrorNotSupported otherwise (the caller runs them one by one).
+// LDNN_CONV_PAIR (A/B knob, default 1).
+int g_conv_pair = -1;
+int pair_env() {
+  if (g_conv_pair < 0) g_conv_pair = env_int("LDNN_CONV_PAIR", 1);
+  return g_conv_pair;
+}
+void set_conv_pair(int on) { g_conv_pair = on; }
+int get_conv_pair() { return pair_env(); }
+
+template <int WM0, int WN0, class OA0, class OB0, int WM1, int WN1, class OA1, class OB1>
+hipError_t launch_pair(const PairArgs& p, hipStream_t st) {
+  const int n1 = p.gx[1] * p.gy[1] * p.gz[1];
+  conv_pair_kernel<WM0, WN0, OA0, OB0, WM1, WN1, OA1, OB1><<<(unsigned)(p.n0 + n1), 256, 0, st>>>(p);
   return hipGetLastError();
+}
+
+hipError_t conv2d_bwd_lds(const ConvShape& sd, const uint16_t* dy, const uint16_t* w, uint16_t* dx, float* ws_d,
+                          int* cnt_d, const BnBwdFuse* bnb, bool* bn_used, const ConvShape& sw, const uint16_t* x,
+                          float* dw, float beta, float* ws_w, hipStream_t st) {
+  if (bn_used) *bn_used = false;
+  if (!pair_env() || deep_ring(0) || conv_xf_env() != 0) return hipErrorNotSupported;
+  if (sd.K % 64 != 0 || !shape_ok(sd) || sd.N * sd.H * sd.W <= 0) return hipErrorNotSupported;
+  if (!shape_ok(sw) || sw.C % 8 != 0 || sw.K % 8 != 0 || (beta != 0.f && beta != 1.f)) return hipErrorNotSupported;
+  if (stem_s2d_ok(sw)) return hipErrorNotSupported;
+  const WgradPlan pw = plan_wgrad(sw);
+  if (pw.ring || (pw.splits > 1 && ws_w == nullptr)) return hipErrorNotSupported;
+  const DgradPrep d = dgrad_prep(sd, dx, ws_d, cnt_d, bnb);
+  if (d.ws64 || d.hb || d.halo) return hipErrorNotSupported;
+  const WgradPrep wp = wgrad_prep(sw, pw, dw, beta, ws_w);
+  PairArgs p{};
+  p.a[0] = d.a;
+  p.a[1] = wp.a;
+  p.pa[0] = reinterpret_cast<const bf16_t*>(dy);
+  p.pb[0] = reinterpret_cast<const bf16_t*>(w);
+  p.ba[0] = (uint32_t)d.bdy;
+  p.bb[0] = (uint32_t)d.bw;
+  p.pa[1] = reinterpret_cast<const bf16_t*>(dy);
+  p.pb[1] = reinterpret_cast<const bf16_t*>(x);
+  p.ba[1] = (uint32_t)wp.bdy;
+  p.bb[1] = (uint32_t)wp.bx;
+  p.gx[0] = d.a.tiles_x; p.gy[0] = d.pl.splits; p.gz[0] = d.a.classes;
+  p.gx[1] = wp.a.tiles_x; p.gy[1] = pw.splits; p.gz[1] = 1;
+  p.n0 = (p.gx[0] * p.gy[0] * p.gz[0] + 7) / 8 * 8;
+  hipError_t e;
+  if (d.pl.wm == 4) {
+    if (pw.narrow)
+      e = launch_pair<4, 1, DgradA<256, 8, 4>, DgradB<64, 2, 4>, 1, 4, WgradA<64, 2, 4>, WgradB<256, 8, 4>>(p, st);
+    else
+      e = launch_pair<4, 1, DgradA<256, 8, 4>, DgradB<64, 2, 4>, 2, 2, WgradA<128, 4, 4>, WgradB<128, 4, 4>>(p, st);
+  } else {
+    if (pw.narrow)
+      e = launch_pair<2, 2, DgradA<128, 4, 4>, DgradB<128, 4, 4>, 1, 4, WgradA<64, 2, 4>, WgradB<256, 8, 4>>(p, st);
+    else
+      e = launch_pair<2, 2, DgradA<128, 4, 4>, DgradB<128, 4, 4>, 2, 2, WgradA<128, 4, 4>, WgradB<128, 4, 4>>(p, st);
+  }
+  if (e != hipSuccess) return e;
+  e = dgrad_post(d, dx, ws_d, st, bn_used);
+  if (e != hipSuccess) return e;
+  return wgrad_post(wp, dw, beta, ws_w, st);
 }
 
 }  // namespace ldnn

@@ -393,22 +393,23 @@ class _Conv2dNative(torch.autograd.Function):
             g = gz
         elif bias is not None:
             C.colsum(g.contiguous().view(-1, kp), flat.grad_storage(bias), flat.grad_beta(bias) != 0.0)
-        C.conv_wgrad(g, xb, flat.grad_storage(weight), stride, pad, flat.grad_beta(weight), real_channels=Cin)
-        flat.notify(weight, bias)
+        dw, beta = flat.grad_storage(weight), flat.grad_beta(weight)
         dx = None
         if ctx.needs_input_grad[0]:
+            # dgrad + wgrad of the layer: one launch where the kernels allow (conv_bwd)
             dxb = torch.empty_like(xb)
             src = ctx.bnsrc
             kw = src.dgrad_kwargs() if src is not None and not src.twin_used else None
-            if kw is not None and C.conv_dgrad(g, flat.shadow_storage(weight), dxb, stride, pad, **kw):
+            if C.conv_bwd(g, flat.shadow_storage(weight), dxb, xb, dw, stride, pad, beta, Cin, **(kw or {})) and kw:
                 # the BN's backward finds its statistics finalized if this dx reaches it unchanged
                 src.pre = (dxb.data_ptr(), dxb._version)
-            elif kw is None:
-                C.conv_dgrad(g, flat.shadow_storage(weight), dxb, stride, pad)
             ctx.bnsrc = None
             dx = _zpad(nchw_view(dxb, Cin))   # (weight pad channels are zero)
             if in_dtype != torch.bfloat16:
                 dx = dx.to(in_dtype)
+        else:
+            C.conv_wgrad(g, xb, dw, stride, pad, beta, real_channels=Cin)
+        flat.notify(weight, bias)
         return dx, None, None, None, None, None, None, None
 
 

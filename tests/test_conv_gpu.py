@@ -556,3 +556,46 @@ def test_resblock_bn1_backward_statistics_come_from_conv2_dgrad():
         grads.append([xi.grad.float()] + [p.grad.float().clone() for p in blk.parameters()])
     for a, b in zip(grads[0], grads[1]):
         torch.testing.assert_close(b, a, rtol=2e-2, atol=2e-2 * a.abs().max().item())
+
+
+@pytest.mark.parametrize("N,C,H,K,stride", [(64, 128, 16, 128, 1), (64, 256, 8, 256, 1), (64, 512, 4, 512, 1),
+                                            (64, 1024, 2, 1024, 1), (64, 64, 32, 128, 2), (64, 256, 8, 512, 2),
+                                            (64, 64, 56, 64, 1), (16, 64, 32, 64, 1), (5, 192, 9, 320, 1),
+                                            (8, 96, 12, 64, 1)])
+def test_paired_dgrad_wgrad_launch_matches_separate(N, C, H, K, stride):
+    """conv_bwd: a layer's dgrad and wgrad in ONE launch (conv_pair_kernel: the dgrad's workgroups,
+    then the wgrad's, each over its own virtual grid) give the bits of the two separate launches
+    (split-K slabs / in-launch combine included), for accumulate (beta 1) and overwrite, and match
+    the fp32 reference."""
+    torch.manual_seed(41)
+    Cc = _ext.C()
+    P = (H + 2 - 3) // stride + 1
+    x = torch.randn(N, H, H, C, device="cuda").bfloat16()
+    w = (torch.randn(K, 3, 3, C, device="cuda") * (1.0 / (K * 9) ** 0.5)).bfloat16()
+    gy = torch.randn(N, P, P, K, device="cuda").bfloat16()
+    dw0 = torch.randn(K, 3, 3, C, device="cuda")
+    old = Cc.get_conv_pair()
+    res = []
+    try:
+        for mode in (0, 1, 1):
+            Cc.set_conv_pair(mode)
+            out = []
+            for beta in (0.0, 1.0):
+                dx = torch.empty_like(x)
+                dw = dw0.clone()
+                Cc.conv_bwd(gy, w, dx, x, dw, stride, 1, beta)
+                torch.cuda.synchronize()
+                out += [dx.float(), dw]
+            res.append(out)
+    finally:
+        Cc.set_conv_pair(old)
+    for a, b in zip(res[0], res[1]):
+        assert torch.equal(a, b)
+    for a, b in zip(res[1], res[2]):
+        assert torch.equal(a, b)
+    xf, wf, gf = x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), gy.float().permute(0, 3, 1, 2)
+    dxr = torch.nn.grad.conv2d_input(xf.shape, wf, gf, stride=stride, padding=1).permute(0, 2, 3, 1)
+    dwr = torch.nn.grad.conv2d_weight(xf, wf.shape, gf, stride=stride, padding=1).permute(0, 2, 3, 1)
+    torch.testing.assert_close(res[1][0], dxr, rtol=2e-2, atol=2e-2 * dxr.abs().max().item())
+    torch.testing.assert_close(res[1][1], dwr, rtol=1e-2, atol=1e-2 * dwr.abs().max().item())
+    torch.testing.assert_close(res[1][3], dwr + dw0, rtol=1e-2, atol=1e-2 * dwr.abs().max().item())
