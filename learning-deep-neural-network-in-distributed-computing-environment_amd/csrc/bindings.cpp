@@ -899,6 +899,13 @@ ConvWs conv_ws(const ldnn::ConvShape& s, int op, const at::Tensor& like) {
 }
 
 float* fptr_opt(const c10::optional<at::Tensor>& t, int64_t n, const char* name);
+const ldnn::BnFin* bn_fwd_fin(ldnn::BnFin& fin, const ldnn::ConvShape& s, const c10::optional<at::Tensor>& bn_ws,
+                              const c10::optional<at::Tensor>& bn_gamma, const c10::optional<at::Tensor>& bn_beta,
+                              const c10::optional<at::Tensor>& bn_running_mean,
+                              const c10::optional<at::Tensor>& bn_running_var,
+                              const c10::optional<at::Tensor>& bn_save_mean,
+                              const c10::optional<at::Tensor>& bn_save_invstd, double bn_eps, double bn_momentum,
+                              const c10::optional<at::Tensor>& bn_num_batches);
 
 // Returns whether the following BatchNorm's statistics were accumulated and
 // finalized by the conv epilogue (bn_ws given, LDS-DMA path, no epilogue op).
@@ -922,9 +929,26 @@ bool conv_fwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& y, int
   c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   const ConvWs ws = conv_ws(s, 0, x);
   ldnn::BnFin fin{};
+  TORCH_CHECK(!bn_ws.has_value() || epi == ldnn::EPI_NONE, "conv: fused BN statistics need a plain (EPI_NONE) conv");
+  const ldnn::BnFin* finp = bn_fwd_fin(fin, s, bn_ws, bn_gamma, bn_beta, bn_running_mean, bn_running_var, bn_save_mean,
+                                       bn_save_invstd, bn_eps, bn_momentum, bn_num_batches);
+  bool done = false;
+  check(ldnn::conv2d_fwd(s, bf16_ptr(x), bf16_ptr(w), bf16_mut(y), b, (int)epi, cur_stream(x), ws.ws(), ws.c(),
+                         finp, &done),
+        "conv2d_fwd");
+  return done;
+}
+
+// The fused next-BN statistics state of a forward conv (nullptr without bn_ws).
+const ldnn::BnFin* bn_fwd_fin(ldnn::BnFin& fin, const ldnn::ConvShape& s, const c10::optional<at::Tensor>& bn_ws,
+                              const c10::optional<at::Tensor>& bn_gamma, const c10::optional<at::Tensor>& bn_beta,
+                              const c10::optional<at::Tensor>& bn_running_mean,
+                              const c10::optional<at::Tensor>& bn_running_var,
+                              const c10::optional<at::Tensor>& bn_save_mean,
+                              const c10::optional<at::Tensor>& bn_save_invstd, double bn_eps, double bn_momentum,
+                              const c10::optional<at::Tensor>& bn_num_batches) {
   const ldnn::BnFin* finp = nullptr;
   if (bn_ws.has_value()) {
-    TORCH_CHECK(epi == ldnn::EPI_NONE, "conv: fused BN statistics need a plain (EPI_NONE) conv");
     const int C = s.K;
     ldnn::BnArgs a{};
     a.M = s.N * s.P * s.Q;
@@ -946,11 +970,47 @@ bool conv_fwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& y, int
     fin = ldnn::bn_forward_fin_conv(a);
     finp = &fin;
   }
-  bool done = false;
-  check(ldnn::conv2d_fwd(s, bf16_ptr(x), bf16_ptr(w), bf16_mut(y), b, (int)epi, cur_stream(x), ws.ws(), ws.c(),
-                         finp, &done),
-        "conv2d_fwd");
-  return done;
+  return finp;
+}
+
+c10::optional<at::Tensor> opt_item(const py::dict& d, const char* k) {
+  if (!d.contains(k) || d[k].is_none()) return c10::nullopt;
+  return d[k].cast<at::Tensor>();
+}
+const ldnn::BnFin* bn_fwd_fin_dict(ldnn::BnFin& fin, const ldnn::ConvShape& s, const py::object& bn) {
+  if (bn.is_none()) return nullptr;
+  const py::dict d = bn.cast<py::dict>();
+  const double eps = d.contains("eps") ? d["eps"].cast<double>() : 1e-5;
+  const double mom = d.contains("momentum") ? d["momentum"].cast<double>() : 0.1;
+  return bn_fwd_fin(fin, s, opt_item(d, "ws"), opt_item(d, "gamma"), opt_item(d, "beta"), opt_item(d, "running_mean"),
+                    opt_item(d, "running_var"), opt_item(d, "save_mean"), opt_item(d, "save_invstd"), eps, mom,
+                    opt_item(d, "num_batches"));
+}
+
+// A downsampling block's 3x3 conv (w0 -> y0) and 1x1 shortcut conv (w1 -> y1) of one input x,
+// each with its next BN's fused statistics (bn0 / bn1: None or a dict of conv_fwd's bn_*
+// arguments without the prefix): one launch where the kernels allow.  Returns the two flags.
+std::tuple<bool, bool> conv_fwd2(const at::Tensor& x, const at::Tensor& w0, const at::Tensor& y0, int64_t stride0,
+                                 int64_t pad0, const at::Tensor& w1, const at::Tensor& y1, int64_t stride1,
+                                 int64_t pad1, const py::object& bn0, const py::object& bn1) {
+  check_dev(x, at::kBFloat16, "x");
+  check_dev(w0, at::kBFloat16, "w0");
+  check_dev(y0, at::kBFloat16, "y0");
+  check_dev(w1, at::kBFloat16, "w1");
+  check_dev(y1, at::kBFloat16, "y1");
+  const ldnn::ConvShape s0 = conv_shape(x, w0, y0, stride0, pad0);
+  const ldnn::ConvShape s1 = conv_shape(x, w1, y1, stride1, pad1);
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  const ConvWs ws0 = conv_ws(s0, 0, x);
+  const ConvWs ws1 = conv_ws(s1, 0, x);
+  ldnn::BnFin f0{}, f1{};
+  const ldnn::BnFin* p0 = bn_fwd_fin_dict(f0, s0, bn0);
+  const ldnn::BnFin* p1 = bn_fwd_fin_dict(f1, s1, bn1);
+  bool d0 = false, d1 = false;
+  check(ldnn::conv2d_fwd2(s0, bf16_ptr(x), bf16_ptr(w0), bf16_mut(y0), ws0.ws(), ws0.c(), p0, &d0, s1, bf16_ptr(w1),
+                          bf16_mut(y1), ws1.ws(), ws1.c(), p1, &d1, cur_stream(x)),
+        "conv2d_fwd2");
+  return {d0, d1};
 }
 
 // bn_x given: dx is the gradient of a training BatchNorm(+ReLU)'s output (bn_x = that BN's
@@ -1878,6 +1938,10 @@ PYBIND11_MODULE(_C, m) {
         py::arg("bn_gamma") = py::none(), py::arg("bn_save_mean") = py::none(),
         py::arg("bn_save_invstd") = py::none(), py::arg("bn_dgamma") = py::none(), py::arg("bn_dbeta") = py::none(),
         py::arg("bn_assign") = false);
+  m.def("conv_fwd2", &conv_fwd2, py::arg("x"), py::arg("w0"), py::arg("y0"), py::arg("stride0"), py::arg("pad0"),
+        py::arg("w1"), py::arg("y1"), py::arg("stride1"), py::arg("pad1"), py::arg("bn0") = py::none(),
+        py::arg("bn1") = py::none(),
+        "two forward convs of one input in one launch where the kernels allow; returns the BN-statistics flags");
   m.def("conv_bwd", &conv_bwd, py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("x"), py::arg("dw"),
         py::arg("stride"), py::arg("pad"), py::arg("beta") = 0.0, py::arg("real_channels") = 0,
         py::arg("bn_x") = py::none(), py::arg("bn_mask") = py::none(), py::arg("bn_ws") = py::none(),

@@ -136,6 +136,15 @@ hipError_t conv2d_dgrad_lds(const ConvShape& s, const uint16_t* dy, const uint16
                             float* ws, int* cnt, const BnBwdFuse* bnb = nullptr, bool* bn_used = nullptr);
 hipError_t conv2d_wgrad_lds(const ConvShape& s, const uint16_t* dy, const uint16_t* x, float* dw, float beta,
                             hipStream_t st, float* ws);
+// A downsampling block's 3x3 conv (s0, w0 -> y0) and 1x1 shortcut conv (s1, w1 -> y1) of one
+// input x, each with its optional next-BN statistics: one launch where the kernels allow
+// (conv2d_fwd2_lds), else one by one (conv2d_fwd2).
+hipError_t conv2d_fwd2(const ConvShape& s0, const uint16_t* x, const uint16_t* w0, uint16_t* y0, float* ws0,
+                       int* cnt0, const BnFin* bn0, bool* done0, const ConvShape& s1, const uint16_t* w1,
+                       uint16_t* y1, float* ws1, int* cnt1, const BnFin* bn1, bool* done1, hipStream_t st);
+hipError_t conv2d_fwd2_lds(const ConvShape& s0, const uint16_t* x, const uint16_t* w0, uint16_t* y0, float* ws0,
+                           int* cnt0, const BnFin* bn0, bool* used0, const ConvShape& s1, const uint16_t* w1,
+                           uint16_t* y1, float* ws1, int* cnt1, const BnFin* bn1, bool* used1, hipStream_t st);
 // hipErrorNotSupported: the pair does not share a launch (conv2d_bwd runs them one by one)
 hipError_t conv2d_bwd_lds(const ConvShape& sd, const uint16_t* dy, const uint16_t* w, uint16_t* dx, float* ws_d,
                           int* cnt_d, const BnBwdFuse* bnb, bool* bn_used, const ConvShape& sw, const uint16_t* x,

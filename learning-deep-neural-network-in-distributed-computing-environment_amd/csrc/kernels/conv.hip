@@ -340,6 +340,18 @@ hipError_t conv2d_fwd(const ConvShape& s, const uint16_t* x, const uint16_t* w, 
   return hipGetLastError();
 }
 
+hipError_t conv2d_fwd2(const ConvShape& s0, const uint16_t* x, const uint16_t* w0, uint16_t* y0, float* ws0,
+                       int* cnt0, const BnFin* bn0, bool* done0, const ConvShape& s1, const uint16_t* w1,
+                       uint16_t* y1, float* ws1, int* cnt1, const BnFin* bn1, bool* done1, hipStream_t st) {
+  if (g_conv_impl == 0) {
+    const hipError_t e = conv2d_fwd2_lds(s0, x, w0, y0, ws0, cnt0, bn0, done0, s1, w1, y1, ws1, cnt1, bn1, done1, st);
+    if (e != hipErrorNotSupported) return e;
+  }
+  const hipError_t e = conv2d_fwd(s0, x, w0, y0, nullptr, EPI_NONE, st, ws0, cnt0, bn0, done0);
+  if (e != hipSuccess) return e;
+  return conv2d_fwd(s1, x, w1, y1, nullptr, EPI_NONE, st, ws1, cnt1, bn1, done1);
+}
+
 hipError_t conv2d_bwd(const ConvShape& sd, const uint16_t* dy, const uint16_t* w, uint16_t* dx, float* ws_d,
                       int* cnt_d, const BnBwdFuse* bnb, bool* bn_done, const ConvShape& sw, const uint16_t* x,
                       float* dw, float beta, float* ws_w, hipStream_t st) {

@@ -933,10 +933,12 @@ __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void conv_lds_kernel(LArgs a,
   conv_lds_body<WM, WN, OA, OB, EPI, OUT_F32, DGRAD, NS, XF>(a, pa, bytes_a, pb, bytes_b, hw_vb(), smem);
 }
 
-// A layer's dgrad (body 0) and wgrad (body 1) in ONE launch: workgroups [0, n0) run the dgrad
-// over its (gx0, gy0, gz0) grid, the rest the wgrad over (gx1, gy1) -- the two GEMMs share the
-// chip instead of each leaving CUs idle behind a small grid (EnhancedCNN's 16x16 .. 2x2 stages,
-// ResNet-18 at b64).  n0 is a multiple of 8, so the wgrad's virtual ids keep their XCD placement.
+// Two independent convolution GEMMs in ONE launch: workgroups [0, n0) run body 0 over its
+// (gx0, gy0, gz0) grid, the rest body 1 over (gx1, gy1, gz1) -- a layer's dgrad and wgrad (both
+// read dy), or a downsampling block's 3x3 and 1x1 shortcut forward convs (both read x) -- so the
+// two share the chip instead of each leaving CUs idle behind a small grid (EnhancedCNN's
+// 16x16 .. 2x2 stages, ResNet-18 at b64).  n0 is a multiple of 8, so body 1's virtual ids keep
+// their XCD placement.  F / D: the body's fp32-output / dgrad flags.
 struct PairArgs {
   LArgs a[2];
   const bf16_t* pa[2];
@@ -945,7 +947,8 @@ struct PairArgs {
   int gx[2], gy[2], gz[2];
   int n0;
 };
-template <int WM0, int WN0, class OA0, class OB0, int WM1, int WN1, class OA1, class OB1>
+template <int WM0, int WN0, class OA0, class OB0, bool F0, bool D0, int WM1, int WN1, class OA1, class OB1, bool F1,
+          bool D1>
 __global__ __launch_bounds__(256, 2) void conv_pair_kernel(PairArgs p) {
   constexpr int ST0 = (WM0 + WN0) * 64 * 128, ST1 = (WM1 + WN1) * 64 * 128;
   constexpr int LDS = 2 * (ST0 > ST1 ? ST0 : ST1);
@@ -957,9 +960,9 @@ __global__ __launch_bounds__(256, 2) void conv_pair_kernel(PairArgs p) {
   if (b >= gx * gy * p.gz[k]) return;  // (the dgrad's id range is padded to a multiple of 8)
   const VB vb{b % gx, (b / gx) % gy, b / (gx * gy), gx, gy};
   if (k == 0)
-    conv_lds_body<WM0, WN0, OA0, OB0, EPI_NONE, false, true, 2>(p.a[0], p.pa[0], p.ba[0], p.pb[0], p.bb[0], vb, smem);
+    conv_lds_body<WM0, WN0, OA0, OB0, EPI_NONE, F0, D0, 2>(p.a[0], p.pa[0], p.ba[0], p.pb[0], p.bb[0], vb, smem);
   else
-    conv_lds_body<WM1, WN1, OA1, OB1, EPI_NONE, true, false, 2>(p.a[1], p.pa[1], p.ba[1], p.pb[1], p.bb[1], vb, smem);
+    conv_lds_body<WM1, WN1, OA1, OB1, EPI_NONE, F1, D1, 2>(p.a[1], p.pa[1], p.ba[1], p.pb[1], p.bb[1], vb, smem);
 }
 
 // ---- halo path: 3x3 stride-1 pad-1 fwd / dgrad with the A operand staged ONCE --
@@ -2517,9 +2520,9 @@ int wgrad_xcd_env() {
   return v;
 }
 
-WgradPlan plan_wgrad(const ConvShape& s) {
+WgradPlan plan_wgrad(const ConvShape& s, bool allow_ring = true) {
   WgradPlan p;
-  p.ring = wgrad_ring_ok(s);
+  p.ring = allow_ring && wgrad_ring_ok(s);
   if (p.ring) {  // (64 filters x 576 tap-channels) blocks x npq slices of >= 12 K-tiles, ~512 workgroups
     // (two per CU: ResNet-18 b256 7.652 vs 7.705-7.711 ms at 384, 7.70 at 256, 7.78 at 1024; b64 capped by
     // the 12-K-tile floor either way, profiles/r4/ring_wgrad_target_ab.jsonl)
@@ -3025,11 +3028,23 @@ ConvWorkspace conv2d_lds_workspace(const ConvShape& s, int op) {
     return w;
   }
   if (op == 0 && s.C % 64 == 0) return ws_of(hb_takes(s, false) ? plan_hb(s, false) : plan_fwd(s));
-  if (op == 1 && s.K % 64 == 0) return ws_of(hb_takes(s, true) ? plan_hb(s, true) : plan_dgrad(s));
+  // dgrad / wgrad: the larger of the layer's own plan and the generic one a paired launch may
+  // take instead (conv2d_bwd_lds with LDNN_CONV_PAIR=2)
+  if (op == 1 && s.K % 64 == 0) {
+    ConvWorkspace w = ws_of(plan_dgrad(s));
+    if (hb_takes(s, true)) {
+      const ConvWorkspace h = ws_of(plan_hb(s, true));
+      w.slab_bytes = std::max(w.slab_bytes, h.slab_bytes);
+      w.counters = std::max(w.counters, h.counters);
+    }
+    return w;
+  }
   if (op == 2 && s.C % 8 == 0 && s.K % 8 == 0) {
-    const WgradPlan p = plan_wgrad(s);
     ConvWorkspace w{};
-    if (p.splits > 1) w.slab_bytes = (size_t)p.splits * s.K * s.R * s.S * s.C * 4;
+    for (int ring = 0; ring < 2; ++ring) {
+      const WgradPlan p = plan_wgrad(s, ring != 0);
+      if (p.splits > 1) w.slab_bytes = std::max(w.slab_bytes, (size_t)p.splits * s.K * s.R * s.S * s.C * 4);
+    }
     return w;
   }
   return ConvWorkspace{};
@@ -3127,26 +3142,30 @@ hipError_t conv2d_fwd_lds_small_c(const ConvShape& s, const uint16_t* x, const u
   return launch<2, 2, FwdASmallC<128, 4, 4>, WeightKC<128, 4, 4>, false, false>(a, epi, 1, x, bx, w, bw, st);
 }
 
-hipError_t conv2d_fwd_lds(const ConvShape& s, const uint16_t* x, const uint16_t* w, uint16_t* y, const float* bias,
-                          int epi, hipStream_t st, float* ws, int* cnt, const BnFin* bn, bool* bn_used) {
-  if (bn_used) *bn_used = bn != nullptr;
-  if (!shape_ok(s)) return hipErrorNotSupported;
-  if (bn != nullptr && epi != EPI_NONE) return hipErrorInvalidValue;
-  if (s.C == 8 || s.C == 16 || s.C == 32) {
-    if (s.N * s.P * s.Q <= 0) return hipErrorNotSupported;
-    return conv2d_fwd_lds_small_c(s, x, w, y, bias, epi, st, bn);
-  }
-  if (s.C % 64 != 0) return hipErrorNotSupported;
-  if (s.N * s.P * s.Q <= 0) return bn != nullptr ? hipErrorNotSupported : hipSuccess;
-  const bool hbp = hb_takes(s, false);
-  Plan pl = hbp ? plan_hb(s, false) : plan_fwd(s);
-  LArgs a = base_args(s);
+namespace {
+// What conv2d_fwd_lds launches for a C % 64 == 0 shape, planned without launching it.
+struct FwdPrep {
+  LArgs a;
+  Plan pl;
+  bool slab, hb, halo, ws64;
+  const BnFin* slab_fin;
+  bool bn_used;
+  size_t bx, bw;
+};
+
+FwdPrep fwd_prep(const ConvShape& s, uint16_t* y, const float* bias, int epi, float* ws, int* cnt, const BnFin* bn) {
+  FwdPrep f{};
+  f.bn_used = bn != nullptr;
+  f.hb = hb_takes(s, false);
+  Plan& pl = f.pl;
+  pl = f.hb ? plan_hb(s, false) : plan_fwd(s);
+  LArgs& a = f.a;
+  a = base_args(s);
   // slab split-K: the slab pass takes the next BN's statistics (conv_slab_bn), or with
   // LDNN_CONV_SLAB_BN=0 the BN runs its own statistics pass
-  const BnFin* slab_fin = nullptr;
   if (bn != nullptr && pl.slab) {
-    if (slab_bn_env() && bn->part != nullptr && bn->tickets != nullptr && s.K % 8 == 0) slab_fin = bn;
-    else if (bn_used) *bn_used = false;
+    if (slab_bn_env() && bn->part != nullptr && bn->tickets != nullptr && s.K % 8 == 0) f.slab_fin = bn;
+    else f.bn_used = false;
     bn = nullptr;
   }
   if (bn != nullptr) {
@@ -3160,8 +3179,8 @@ hipError_t conv2d_fwd_lds(const ConvShape& s, const uint16_t* x, const uint16_t*
   a.nb = s.C / 64;
   a.tiles_x = pl.tiles_x;
   a.nk_all = pl.nk_all;
-  const bool slab = pl.splits > 1 && pl.slab && ws != nullptr;
-  if (slab) {
+  f.slab = pl.splits > 1 && pl.slab && ws != nullptr;
+  if (f.slab) {
     a.ws = ws;
     a.nk_split = pl.nk_split;
   } else if (pl.splits > 1 && !pl.slab && ws != nullptr && cnt != nullptr) {
@@ -3172,29 +3191,57 @@ hipError_t conv2d_fwd_lds(const ConvShape& s, const uint16_t* x, const uint16_t*
     pl.splits = 1;
     a.nk_split = pl.nk_all;
   }
-  const size_t bx = (size_t)s.N * s.H * s.W * s.C * 2, bw = (size_t)s.K * a.rsc * 2;
-  if (ws64_takes(s, epi)) {  // persistent grid, no split-K: the plan's slab / combine is not used
+  f.bx = (size_t)s.N * s.H * s.W * s.C * 2;
+  f.bw = (size_t)s.K * a.rsc * 2;
+  f.ws64 = ws64_takes(s, epi);
+  if (f.ws64) {  // persistent grid, no split-K: the plan's slab / combine is not used
     a.ws = nullptr;
     a.cnt = nullptr;
     a.nk_split = a.nk_all;
-    return launch_ws64<false>(a, x, bx, w, st);
   }
+  f.halo = !f.ws64 && !f.hb && halo_takes(s, pl.wm);
+  return f;
+}
+
+// after the main kernel: the slab split-K sum (with the next BN's statistics when taken)
+hipError_t fwd_post(const FwdPrep& f, uint16_t* y, const float* bias, int epi, float* ws, hipStream_t st) {
+  if (!f.slab) return hipSuccess;
+  if (f.slab_fin != nullptr) return conv_slab_bn(ws, y, f.a.M, f.a.N, f.pl.splits, *f.slab_fin, st);
+  return conv_slab_epilogue(ws, y, f.a.M, f.a.N, f.pl.splits, bias, epi, st);
+}
+}  // namespace
+
+hipError_t conv2d_fwd_lds(const ConvShape& s, const uint16_t* x, const uint16_t* w, uint16_t* y, const float* bias,
+                          int epi, hipStream_t st, float* ws, int* cnt, const BnFin* bn, bool* bn_used) {
+  if (bn_used) *bn_used = bn != nullptr;
+  if (!shape_ok(s)) return hipErrorNotSupported;
+  if (bn != nullptr && epi != EPI_NONE) return hipErrorInvalidValue;
+  if (s.C == 8 || s.C == 16 || s.C == 32) {
+    if (s.N * s.P * s.Q <= 0) return hipErrorNotSupported;
+    return conv2d_fwd_lds_small_c(s, x, w, y, bias, epi, st, bn);
+  }
+  if (s.C % 64 != 0) return hipErrorNotSupported;
+  if (s.N * s.P * s.Q <= 0) return bn != nullptr ? hipErrorNotSupported : hipSuccess;
+  const FwdPrep f = fwd_prep(s, y, bias, epi, ws, cnt, bn);
+  if (bn_used) *bn_used = f.bn_used;
+  const LArgs& a = f.a;
+  const int splits = f.pl.splits;
+  if (f.ws64) return launch_ws64<false>(a, x, f.bx, w, st);
   hipError_t e;
-  if (hbp) {
-    e = launch_hb<WeightKC<128, 2, 8>, false>(a, epi, pl.splits, x, bx, w, bw, st);
-  } else if (halo_takes(s, pl.wm)) {
+  if (f.hb) {
+    e = launch_hb<WeightKC<128, 2, 8>, false>(a, epi, splits, x, f.bx, w, f.bw, st);
+  } else if (f.halo) {
     // fwd: the halo wins on the 256x64 tiles of 64-filter layers (C64 H56: 53.7 -> 35-37 us) and
     // loses on 128x128 ones (C128 H28 25.8 -> 27.7, C512 H7 34.9 -> 40.0 us; double-buffered too)
-    if (pl.wm == 4) e = launch_halo<4, 1, WeightKC<64, 2, 4>, false>(a, epi, pl.splits, x, bx, w, bw, st);
-    else e = launch_halo<2, 2, WeightKC<128, 4, 4>, false>(a, epi, pl.splits, x, bx, w, bw, st);
-  } else if (pl.wm == 4) {
-    e = launch<4, 1, FwdA<256, 8, 4>, WeightKC<64, 2, 4>, false, false>(a, epi, pl.splits, x, bx, w, bw, st);
+    if (f.pl.wm == 4) e = launch_halo<4, 1, WeightKC<64, 2, 4>, false>(a, epi, splits, x, f.bx, w, f.bw, st);
+    else e = launch_halo<2, 2, WeightKC<128, 4, 4>, false>(a, epi, splits, x, f.bx, w, f.bw, st);
+  } else if (f.pl.wm == 4) {
+    e = launch<4, 1, FwdA<256, 8, 4>, WeightKC<64, 2, 4>, false, false>(a, epi, splits, x, f.bx, w, f.bw, st);
   } else {
-    e = launch<2, 2, FwdA<128, 4, 4>, WeightKC<128, 4, 4>, false, false>(a, epi, pl.splits, x, bx, w, bw, st);
+    e = launch<2, 2, FwdA<128, 4, 4>, WeightKC<128, 4, 4>, false, false>(a, epi, splits, x, f.bx, w, f.bw, st);
   }
-  if (e != hipSuccess || !slab) return e;
-  if (slab_fin != nullptr) return conv_slab_bn(ws, y, a.M, a.N, pl.splits, *slab_fin, st);
-  return conv_slab_epilogue(ws, y, a.M, a.N, pl.splits, bias, epi, st);
+  if (e != hipSuccess) return e;
+  return fwd_post(f, y, bias, epi, ws, st);
 }
 
 namespace {
@@ -3208,9 +3255,11 @@ struct DgradPrep {
   size_t bdy, bw;
 };
 
-DgradPrep dgrad_prep(const ConvShape& s, uint16_t* dx, float* ws, int* cnt, const BnBwdFuse* bnb) {
+// generic: the 4-wave gather kernel only (no big-tile / halo / weight-stationary variant)
+DgradPrep dgrad_prep(const ConvShape& s, uint16_t* dx, float* ws, int* cnt, const BnBwdFuse* bnb,
+                     bool generic = false) {
   DgradPrep d{};
-  d.hb = hb_takes(s, true);
+  d.hb = !generic && hb_takes(s, true);
   Plan& pl = d.pl;
   pl = d.hb ? plan_hb(s, true) : plan_dgrad(s);
   LArgs& a = d.a;
@@ -3236,14 +3285,14 @@ DgradPrep dgrad_prep(const ConvShape& s, uint16_t* dx, float* ws, int* cnt, cons
   }
   d.bdy = (size_t)s.N * s.P * s.Q * s.K * 2;
   d.bw = (size_t)s.K * a.rsc * 2;
-  d.ws64 = ws64_takes(s, EPI_NONE);
+  d.ws64 = !generic && ws64_takes(s, EPI_NONE);
   if (d.ws64) {
     a.ws = nullptr;
     a.cnt = nullptr;
     a.nk_split = a.nk_all;
     return d;
   }
-  d.halo = !d.hb && halo_takes(s, pl.wm);
+  d.halo = !generic && !d.hb && halo_takes(s, pl.wm);
   // the BN backward statistics of the BN whose output's gradient dx is: stride-1 dgrads (no
   // class row remap) in the direct / in-launch combine epilogue, or in the slab sum
   if (bnb != nullptr && bn_bwd_env() && s.stride == 1 && pl.classes == 1 && s.C % 8 == 0) {
@@ -3423,12 +3472,19 @@ int pair_env() {
 void set_conv_pair(int on) { g_conv_pair = on; }
 int get_conv_pair() { return pair_env(); }
 
-template <int WM0, int WN0, class OA0, class OB0, int WM1, int WN1, class OA1, class OB1>
+template <int WM0, int WN0, class OA0, class OB0, bool F0, bool D0, int WM1, int WN1, class OA1, class OB1, bool F1,
+          bool D1>
 hipError_t launch_pair(const PairArgs& p, hipStream_t st) {
   const int n1 = p.gx[1] * p.gy[1] * p.gz[1];
-  conv_pair_kernel<WM0, WN0, OA0, OB0, WM1, WN1, OA1, OB1><<<(unsigned)(p.n0 + n1), 256, 0, st>>>(p);
+  conv_pair_kernel<WM0, WN0, OA0, OB0, F0, D0, WM1, WN1, OA1, OB1, F1, D1><<<(unsigned)(p.n0 + n1), 256, 0, st>>>(p);
   return hipGetLastError();
 }
+#define LDNN_DG128 2, 2, DgradA<128, 4, 4>, DgradB<128, 4, 4>, false, true
+#define LDNN_DG256 4, 1, DgradA<256, 8, 4>, DgradB<64, 2, 4>, false, true
+#define LDNN_WG128 2, 2, WgradA<128, 4, 4>, WgradB<128, 4, 4>, true, false
+#define LDNN_WGN 1, 4, WgradA<64, 2, 4>, WgradB<256, 8, 4>, true, false
+#define LDNN_FW128 2, 2, FwdA<128, 4, 4>, WeightKC<128, 4, 4>, false, false
+#define LDNN_FW256 4, 1, FwdA<256, 8, 4>, WeightKC<64, 2, 4>, false, false
 
 hipError_t conv2d_bwd_lds(const ConvShape& sd, const uint16_t* dy, const uint16_t* w, uint16_t* dx, float* ws_d,
                           int* cnt_d, const BnBwdFuse* bnb, bool* bn_used, const ConvShape& sw, const uint16_t* x,
@@ -3438,9 +3494,12 @@ hipError_t conv2d_bwd_lds(const ConvShape& sd, const uint16_t* dy, const uint16_
   if (sd.K % 64 != 0 || !shape_ok(sd) || sd.N * sd.H * sd.W <= 0) return hipErrorNotSupported;
   if (!shape_ok(sw) || sw.C % 8 != 0 || sw.K % 8 != 0 || (beta != 0.f && beta != 1.f)) return hipErrorNotSupported;
   if (stem_s2d_ok(sw)) return hipErrorNotSupported;
-  const WgradPlan pw = plan_wgrad(sw);
+  // LDNN_CONV_PAIR=2: pair on the generic kernels even where a layer alone takes the big-tile /
+  // weight-stationary dgrad or the ring wgrad
+  const bool generic = pair_env() >= 2;
+  const WgradPlan pw = plan_wgrad(sw, !generic);
   if (pw.ring || (pw.splits > 1 && ws_w == nullptr)) return hipErrorNotSupported;
-  const DgradPrep d = dgrad_prep(sd, dx, ws_d, cnt_d, bnb);
+  const DgradPrep d = dgrad_prep(sd, dx, ws_d, cnt_d, bnb, generic);
   if (d.ws64 || d.hb || d.halo) return hipErrorNotSupported;
   const WgradPrep wp = wgrad_prep(sw, pw, dw, beta, ws_w);
   PairArgs p{};
@@ -3459,20 +3518,61 @@ hipError_t conv2d_bwd_lds(const ConvShape& sd, const uint16_t* dy, const uint16_
   p.n0 = (p.gx[0] * p.gy[0] * p.gz[0] + 7) / 8 * 8;
   hipError_t e;
   if (d.pl.wm == 4) {
-    if (pw.narrow)
-      e = launch_pair<4, 1, DgradA<256, 8, 4>, DgradB<64, 2, 4>, 1, 4, WgradA<64, 2, 4>, WgradB<256, 8, 4>>(p, st);
-    else
-      e = launch_pair<4, 1, DgradA<256, 8, 4>, DgradB<64, 2, 4>, 2, 2, WgradA<128, 4, 4>, WgradB<128, 4, 4>>(p, st);
+    if (pw.narrow) e = launch_pair<LDNN_DG256, LDNN_WGN>(p, st);
+    else e = launch_pair<LDNN_DG256, LDNN_WG128>(p, st);
   } else {
-    if (pw.narrow)
-      e = launch_pair<2, 2, DgradA<128, 4, 4>, DgradB<128, 4, 4>, 1, 4, WgradA<64, 2, 4>, WgradB<256, 8, 4>>(p, st);
-    else
-      e = launch_pair<2, 2, DgradA<128, 4, 4>, DgradB<128, 4, 4>, 2, 2, WgradA<128, 4, 4>, WgradB<128, 4, 4>>(p, st);
+    if (pw.narrow) e = launch_pair<LDNN_DG128, LDNN_WGN>(p, st);
+    else e = launch_pair<LDNN_DG128, LDNN_WG128>(p, st);
   }
   if (e != hipSuccess) return e;
   e = dgrad_post(d, dx, ws_d, st, bn_used);
   if (e != hipSuccess) return e;
   return wgrad_post(wp, dw, beta, ws_w, st);
+}
+
+// A downsampling block's two forward convs of one input x (the 3x3 and the 1x1 shortcut) as ONE
+// launch when both take the 4-wave gather kernel (EPI_NONE, each with its BN's statistics);
+// hipErrorNotSupported otherwise (the caller runs them one by one).
+hipError_t conv2d_fwd2_lds(const ConvShape& s0, const uint16_t* x, const uint16_t* w0, uint16_t* y0, float* ws0,
+                           int* cnt0, const BnFin* bn0, bool* used0, const ConvShape& s1, const uint16_t* w1,
+                           uint16_t* y1, float* ws1, int* cnt1, const BnFin* bn1, bool* used1, hipStream_t st) {
+  if (used0) *used0 = false;
+  if (used1) *used1 = false;
+  if (!pair_env() || deep_ring(0) || conv_xf_env() != 0) return hipErrorNotSupported;
+  for (const ConvShape* s : {&s0, &s1})
+    if (!shape_ok(*s) || s->C % 64 != 0 || s->N * s->P * s->Q <= 0) return hipErrorNotSupported;
+  const FwdPrep f0 = fwd_prep(s0, y0, nullptr, EPI_NONE, ws0, cnt0, bn0);
+  const FwdPrep f1 = fwd_prep(s1, y1, nullptr, EPI_NONE, ws1, cnt1, bn1);
+  for (const FwdPrep* f : {&f0, &f1})
+    if (f->ws64 || f->hb || f->halo) return hipErrorNotSupported;
+  PairArgs p{};
+  const FwdPrep* fs[2] = {&f0, &f1};
+  const uint16_t* wk[2] = {w0, w1};
+  for (int k = 0; k < 2; ++k) {
+    p.a[k] = fs[k]->a;
+    p.pa[k] = reinterpret_cast<const bf16_t*>(x);
+    p.pb[k] = reinterpret_cast<const bf16_t*>(wk[k]);
+    p.ba[k] = (uint32_t)fs[k]->bx;
+    p.bb[k] = (uint32_t)fs[k]->bw;
+    p.gx[k] = fs[k]->a.tiles_x;
+    p.gy[k] = fs[k]->pl.splits;
+    p.gz[k] = 1;
+  }
+  p.n0 = (p.gx[0] * p.gy[0] + 7) / 8 * 8;
+  hipError_t e;
+  if (f0.pl.wm == 4) {
+    if (f1.pl.wm == 4) e = launch_pair<LDNN_FW256, LDNN_FW256>(p, st);
+    else e = launch_pair<LDNN_FW256, LDNN_FW128>(p, st);
+  } else {
+    if (f1.pl.wm == 4) e = launch_pair<LDNN_FW128, LDNN_FW256>(p, st);
+    else e = launch_pair<LDNN_FW128, LDNN_FW128>(p, st);
+  }
+  if (e != hipSuccess) return e;
+  if (used0) *used0 = f0.bn_used;
+  if (used1) *used1 = f1.bn_used;
+  e = fwd_post(f0, y0, nullptr, EPI_NONE, ws0, st);
+  if (e != hipSuccess) return e;
+  return fwd_post(f1, y1, nullptr, EPI_NONE, ws1, st);
 }
 
 }  // namespace ldnn

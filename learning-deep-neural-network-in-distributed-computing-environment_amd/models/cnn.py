@@ -55,10 +55,13 @@ class ResBlock(nn.Module):
         # BAR/model.py:67-72 with BN+ReLU and BN+residual-add+ReLU each fused into one pass;
         # the shortcut reads x's twin (LF.shortcut_input), so the producer of x sums the two
         # branch gradients in its own backward kernels instead of a separate add
+        if len(self.shortcut):
+            # the 3x3 and the 1x1 shortcut conv of x in one launch, then conv2 and both BNs, the add
+            # and the ReLU in one pass
+            c1, sc = LF.conv2d_pair(x, LF.shortcut_input(x), self.conv1, self.shortcut[0])
+            out = self.bn1.act(c1, relu=True)
+            return LF.batch_norm_dual_act(self.conv2(out), self.bn2, sc, self.shortcut[1])
         out = self.bn1.act(self.conv1(x), relu=True)
-        if len(self.shortcut):   # conv1x1 + BN shortcut: both BNs, the add and the ReLU in one pass
-            c2 = self.conv2(out)
-            return LF.batch_norm_dual_act(c2, self.bn2, self.shortcut[0](LF.shortcut_input(x)), self.shortcut[1])
         return self.bn2.act(self.conv2(out), residual=LF.shortcut_input(x), relu=True)
 
 

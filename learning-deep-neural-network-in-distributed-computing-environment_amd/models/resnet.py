@@ -28,10 +28,13 @@ class BasicBlock(nn.Module):
 
     def forward(self, x):
         xs = LF.shortcut_input(x)   # (x's twin: see models/cnn.py ResBlock)
+        if self.downsample is not None:
+            # conv1 and the 1x1 shortcut conv of x in one launch; conv2's BN, the shortcut BN, the add
+            # and the ReLU in one pass
+            c1, sc = LF.conv2d_pair(x, xs, self.conv1, self.downsample[0])
+            out = self.bn1.act(c1, relu=True)
+            return LF.batch_norm_dual_act(self.conv2(out), self.bn2, sc, self.downsample[1])
         out = self.bn1.act(self.conv1(x), relu=True)
-        if self.downsample is not None:   # conv1x1 + BN shortcut: both BNs, the add and the ReLU in one pass
-            c2 = self.conv2(out)
-            return LF.batch_norm_dual_act(c2, self.bn2, self.downsample[0](xs), self.downsample[1])
         return self.bn2.act(self.conv2(out), residual=xs, relu=True)
 
 

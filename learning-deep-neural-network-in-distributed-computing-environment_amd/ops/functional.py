@@ -331,6 +331,32 @@ class _BnBwdSrc:
                     bn_dbeta=f.grad_storage(self.bias)[:C], bn_assign=True)
 
 
+def _conv_bn_stats(bn, K: int, dev, C):
+    """(conv_fwd's bn_* arguments without the prefix, bookkeeping state) for a conv whose epilogue
+    takes the next training BN's statistics (_fused_bn_ok)."""
+    ws = _bn_workspace(bn, K, dev, C)
+    smean = torch.empty(K, dtype=torch.float32, device=dev)
+    sinv = torch.empty(K, dtype=torch.float32, device=dev)
+    bflat = bn._ldnn_flat
+    snap = (getattr(bn, "_ldnn_nbt", 0), bn.num_batches_tracked.clone()
+            if bn.track_running_stats and not bn.num_batches_tracked.is_cuda else None)
+    rm, rv, mom, nbt = _bn_train_state(bn, dev)
+    args = dict(ws=ws, gamma=bflat.master_storage(bn.weight)[:K], beta=bflat.master_storage(bn.bias)[:K],
+                running_mean=rm, running_var=rv, save_mean=smean, save_invstd=sinv, eps=bn.eps,
+                momentum=mom or 0.0, num_batches=nbt)
+    return args, (smean, sinv, snap)
+
+
+def _conv_bn_stats_done(bn, done: bool, y, state):
+    smean, sinv, snap = state
+    if done:
+        bn.__dict__["_ldnn_pre"] = (y.data_ptr(), smean, sinv)
+    else:  # generic conv path: the BN runs its own statistics pass (undo the bookkeeping)
+        bn._ldnn_nbt = snap[0]
+        if snap[1] is not None:
+            bn.num_batches_tracked.copy_(snap[1])
+
+
 class _Conv2dNative(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, stride, pad, flat, relu, bn=None):
@@ -349,25 +375,9 @@ class _Conv2dNative(torch.autograd.Function):
             epi = C.EPI_BIAS_RELU
         if _fused_bn_ok(bn, K, kp, bias, relu):
             # the conv epilogue accumulates + finalizes the next BN's batch statistics
-            dev = x.device
-            ws = _bn_workspace(bn, K, dev, C)
-            smean = torch.empty(K, dtype=torch.float32, device=dev)
-            sinv = torch.empty(K, dtype=torch.float32, device=dev)
-            bflat = bn._ldnn_flat
-            gamma = bflat.master_storage(bn.weight)[:K]
-            beta = bflat.master_storage(bn.bias)[:K]
-            snap = (getattr(bn, "_ldnn_nbt", 0), bn.num_batches_tracked.clone()
-                    if bn.track_running_stats and not bn.num_batches_tracked.is_cuda else None)
-            rm, rv, mom, nbt = _bn_train_state(bn, dev)
-            done = C.conv_fwd(xb, w, y, stride, pad, b, epi, bn_ws=ws, bn_gamma=gamma, bn_beta=beta,
-                              bn_running_mean=rm, bn_running_var=rv, bn_save_mean=smean, bn_save_invstd=sinv,
-                              bn_eps=bn.eps, bn_momentum=mom or 0.0, bn_num_batches=nbt)
-            if done:
-                bn.__dict__["_ldnn_pre"] = (y.data_ptr(), smean, sinv)
-            else:  # generic conv path: the BN runs its own statistics pass (undo the bookkeeping)
-                bn._ldnn_nbt = snap[0]
-                if snap[1] is not None:
-                    bn.num_batches_tracked.copy_(snap[1])
+            args, state = _conv_bn_stats(bn, K, x.device, C)
+            done = C.conv_fwd(xb, w, y, stride, pad, b, epi, **{"bn_" + k: v for k, v in args.items()})
+            _conv_bn_stats_done(bn, done, y, state)
         else:
             C.conv_fwd(xb, w, y, stride, pad, b, epi)
         ctx.save_for_backward(xb, y)
@@ -411,6 +421,89 @@ class _Conv2dNative(torch.autograd.Function):
             C.conv_wgrad(g, xb, dw, stride, pad, beta, real_channels=Cin)
         flat.notify(weight, bias)
         return dx, None, None, None, None, None, None, None
+
+
+class _Conv2dPairNative(torch.autograd.Function):
+    """A downsampling residual block's two convolutions of one input -- the 3x3 (conv0 on x) and
+    the 1x1 shortcut (conv1 on x's twin xt) -- as ONE forward launch (conv_fwd2: both GEMMs share
+    the chip), each with its BN's fused statistics; the backward runs each conv's dgrad + wgrad
+    pair and returns the two input gradients separately (the producer sums them)."""
+
+    @staticmethod
+    def forward(ctx, x, xt, w0, w1, flat, meta0, meta1):
+        C = _ext.C()
+        (st0, p0, bn0), (st1, p1, bn1) = meta0, meta1
+        sh0, sh1 = flat.shadow_storage(w0), flat.shadow_storage(w1)
+        (kp0, cp), kp1 = (sh0.shape[0], sh0.shape[3]), sh1.shape[0]
+        K0, Cin, R0, S0 = w0.shape
+        K1, _, R1, S1 = w1.shape
+        xb = as_nhwc(x, cp)
+        N, H, W, _ = xb.shape
+        dev = x.device
+        ys, args, states = [], [], []
+        for (K, kp, R, S, st, pd, bn) in ((K0, kp0, R0, S0, st0, p0, bn0), (K1, kp1, R1, S1, st1, p1, bn1)):
+            P, Q = (H + 2 * pd - R) // st + 1, (W + 2 * pd - S) // st + 1
+            ys.append(torch.empty(N, P, Q, kp, dtype=torch.bfloat16, device=dev))
+            a, stt = _conv_bn_stats(bn, K, dev, C) if _fused_bn_ok(bn, K, kp, None, False) else (None, None)
+            args.append(a)
+            states.append(stt)
+        done = C.conv_fwd2(xb, sh0, ys[0], st0, p0, sh1, ys[1], st1, p1, args[0], args[1])
+        for bn, d, y, stt in zip((bn0, bn1), done, ys, states):
+            if stt is not None:
+                _conv_bn_stats_done(bn, d, y, stt)
+        ctx.save_for_backward(xb)
+        ctx.meta = (flat, (w0, st0, p0), (w1, st1, p1), Cin, x.dtype)
+        return nchw_view(ys[0], K0), nchw_view(ys[1], K1)
+
+    @staticmethod
+    def backward(ctx, g0, g1):
+        C = _ext.C()
+        (xb,) = ctx.saved_tensors
+        flat, c0, c1, Cin, in_dtype = ctx.meta
+        dxs = []
+        for k, (g, (weight, st, pd)) in enumerate(((g0, c0), (g1, c1))):
+            if g is None:
+                dxs.append(None)
+                continue
+            sh = flat.shadow_storage(weight)
+            gb = as_nhwc(g if g.dtype == torch.bfloat16 else g.to(torch.bfloat16), sh.shape[0])
+            dw, beta = flat.grad_storage(weight), flat.grad_beta(weight)
+            if ctx.needs_input_grad[k]:
+                dxb = torch.empty_like(xb)
+                C.conv_bwd(gb, sh, dxb, xb, dw, st, pd, beta, Cin)
+                dx = _zpad(nchw_view(dxb, Cin))
+                dxs.append(dx if in_dtype == torch.bfloat16 else dx.to(in_dtype))
+            else:
+                C.conv_wgrad(gb, xb, dw, st, pd, beta, real_channels=Cin)
+                dxs.append(None)
+            flat.notify(weight)
+        return dxs[0], dxs[1], None, None, None, None, None
+
+
+def conv2d_pair(x, xt, mod0, mod1):
+    """(mod0(x), mod1(xt)) -- a downsampling block's 3x3 conv and 1x1 shortcut conv of one input
+    (xt: x's twin, LF.shortcut_input) -- as one native forward launch on the GPU (both bias-free,
+    no fused ReLU); otherwise the two module calls."""
+    if _ext.use_native(x) and xt.data_ptr() == x.data_ptr():
+        flat = getattr(mod0, "_ldnn_flat", None)
+        ok = (flat is not None and flat.shadow is not None and getattr(mod1, "_ldnn_flat", None) is flat
+              and all(m.groups == 1 and m.dilation == (1, 1) and m.bias is None and m.stride[0] == m.stride[1]
+                      and isinstance(m.padding, tuple) and m.padding[0] == m.padding[1]
+                      and getattr(m, "activation", None) != "relu" for m in (mod0, mod1))
+              and mod0.in_channels == mod1.in_channels)
+        if ok:
+            bn0 = mod0._ldnn_stats_bn if _layers_fuse_bn_stats() else None
+            bn1 = mod1._ldnn_stats_bn if _layers_fuse_bn_stats() else None
+            y0, y1 = _Conv2dPairNative.apply(x, xt, mod0.weight, mod1.weight, flat,
+                                             (mod0.stride[0], mod0.padding[0], bn0),
+                                             (mod1.stride[0], mod1.padding[0], bn1))
+            return _zpad(y0), _zpad(y1)
+    return mod0(x), mod1(xt)
+
+
+def _layers_fuse_bn_stats() -> bool:
+    from ..models import layers
+    return layers.FUSE_BN_STATS
 
 
 def conv2d(x, mod, relu: bool = False, bn=None):

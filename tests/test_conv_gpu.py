@@ -561,7 +561,7 @@ def test_resblock_bn1_backward_statistics_come_from_conv2_dgrad():
 @pytest.mark.parametrize("N,C,H,K,stride", [(64, 128, 16, 128, 1), (64, 256, 8, 256, 1), (64, 512, 4, 512, 1),
                                             (64, 1024, 2, 1024, 1), (64, 64, 32, 128, 2), (64, 256, 8, 512, 2),
                                             (64, 64, 56, 64, 1), (16, 64, 32, 64, 1), (5, 192, 9, 320, 1),
-                                            (8, 96, 12, 64, 1)])
+                                            (8, 96, 12, 64, 1), (64, 128, 28, 128, 1), (64, 256, 14, 256, 1)])
 def test_paired_dgrad_wgrad_launch_matches_separate(N, C, H, K, stride):
     """conv_bwd: a layer's dgrad and wgrad in ONE launch (conv_pair_kernel: the dgrad's workgroups,
     then the wgrad's, each over its own virtual grid) give the bits of the two separate launches
@@ -577,7 +577,7 @@ def test_paired_dgrad_wgrad_launch_matches_separate(N, C, H, K, stride):
     old = Cc.get_conv_pair()
     res = []
     try:
-        for mode in (0, 1, 1):
+        for mode in (0, 1, 1, 2):   # (2: paired on the generic kernels where a layer alone takes others)
             Cc.set_conv_pair(mode)
             out = []
             for beta in (0.0, 1.0):
@@ -599,3 +599,36 @@ def test_paired_dgrad_wgrad_launch_matches_separate(N, C, H, K, stride):
     torch.testing.assert_close(res[1][0], dxr, rtol=2e-2, atol=2e-2 * dxr.abs().max().item())
     torch.testing.assert_close(res[1][1], dwr, rtol=1e-2, atol=1e-2 * dwr.abs().max().item())
     torch.testing.assert_close(res[1][3], dwr + dw0, rtol=1e-2, atol=1e-2 * dwr.abs().max().item())
+    torch.testing.assert_close(res[3][0], dxr, rtol=2e-2, atol=2e-2 * dxr.abs().max().item())
+    torch.testing.assert_close(res[3][1], dwr, rtol=1e-2, atol=1e-2 * dwr.abs().max().item())
+
+
+@pytest.mark.parametrize("cin,cout,H", [(64, 128, 32), (256, 512, 8), (512, 1024, 4), (64, 128, 56)])
+def test_downsample_block_convs_share_a_launch(cin, cout, H):
+    """A downsampling residual block's 3x3 conv and 1x1 shortcut conv of one input run as ONE
+    forward launch (conv_fwd2) -- each with its BN's fused statistics -- and the block's outputs,
+    running statistics and gradients equal those of the launches one by one."""
+    from ldnn.models.cnn import ResBlock
+
+    Cc = _ext.C()
+    old = Cc.get_conv_pair()
+    res = []
+    try:
+        for mode in (0, 1):
+            Cc.set_conv_pair(mode)
+            torch.manual_seed(43)
+            blk = ResBlock(cin, cout, stride=2).cuda()
+            flat = ldnn.prepare(blk, "cuda")
+            x = torch.randn(16, cin, H, H, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+            for _ in range(2):
+                flat.zero_grad(lazy=True)
+                xi = x.detach().clone().requires_grad_(True)
+                y = blk(xi)
+                y.float().square().mean().backward()
+            torch.cuda.synchronize()
+            res.append([y.float(), xi.grad.float()] + [p.grad.float().clone() for p in blk.parameters()]
+                       + [b.float().clone() for b in blk.buffers()])
+    finally:
+        Cc.set_conv_pair(old)
+    for a, b in zip(res[0], res[1]):
+        torch.testing.assert_close(b, a, rtol=1e-2, atol=1e-2 * max(a.abs().max().item(), 1e-6))
