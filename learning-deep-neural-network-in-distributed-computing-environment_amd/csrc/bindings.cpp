@@ -875,6 +875,12 @@ struct ConvWs {
   int* c() const { return cnt; }
 };
 
+int* conv_counter_pool(const at::Tensor& like, int64_t n);
+// Workspaces of two convs issued in one launch: separate slabs, and counters from one pool
+// allocation (the second range after the first).
+std::pair<ConvWs, ConvWs> conv_ws2(const ldnn::ConvShape& s0, const ldnn::ConvShape& s1, int op,
+                                   const at::Tensor& like);
+
 int* conv_counter_pool(const at::Tensor& like, int64_t n) {
   static std::mutex mu;
   static std::map<std::pair<int, int64_t>, std::vector<at::Tensor>> pools;
@@ -886,6 +892,21 @@ int* conv_counter_pool(const at::Tensor& like, int64_t n) {
     v.push_back(at::zeros({cap}, like.options().dtype(at::kInt)));
   }
   return v.back().data_ptr<int>();
+}
+
+std::pair<ConvWs, ConvWs> conv_ws2(const ldnn::ConvShape& s0, const ldnn::ConvShape& s1, int op,
+                                   const at::Tensor& like) {
+  ConvWs w0, w1;
+  if (ldnn::get_conv_impl() != 0) return {w0, w1};
+  const ldnn::ConvWorkspace n0 = ldnn::conv2d_lds_workspace(s0, op), n1 = ldnn::conv2d_lds_workspace(s1, op);
+  if (n0.slab_bytes) w0.slabs = at::empty({(int64_t)(n0.slab_bytes / 4)}, like.options().dtype(at::kFloat));
+  if (n1.slab_bytes) w1.slabs = at::empty({(int64_t)(n1.slab_bytes / 4)}, like.options().dtype(at::kFloat));
+  if (n0.counters + n1.counters > 0) {
+    int* base = conv_counter_pool(like, n0.counters + n1.counters);
+    if (n0.counters > 0) w0.cnt = base;
+    if (n1.counters > 0) w1.cnt = base + n0.counters;
+  }
+  return {w0, w1};
 }
 
 ConvWs conv_ws(const ldnn::ConvShape& s, int op, const at::Tensor& like) {
@@ -1086,6 +1107,46 @@ ldnn::ConvShape wgrad_shape(const at::Tensor& dy, const at::Tensor& x, const at:
   TORCH_CHECK(dw.size(3) == s.C && dy.size(3) == s.K && dy.size(0) == s.N, "conv_wgrad: shape mismatch");
   TORCH_CHECK(s.C % 8 == 0 && s.K % 8 == 0, "conv_wgrad: channels must be multiples of 8");
   return s;
+}
+
+// A downsampling block's two convs of one input x, backward: (dy_k, w_k -> dx_k; dy_k, x -> dw_k
+// with beta_k) for k = 0, 1 -- both dgrads and wgrads in one launch where the kernels allow.
+void conv_bwd2(const at::Tensor& x, const at::Tensor& dy0, const at::Tensor& w0, const at::Tensor& dx0,
+               const at::Tensor& dw0, int64_t stride0, int64_t pad0, double beta0, const at::Tensor& dy1,
+               const at::Tensor& w1, const at::Tensor& dx1, const at::Tensor& dw1, int64_t stride1, int64_t pad1,
+               double beta1, int64_t real_channels) {
+  check_dev(x, at::kBFloat16, "x");
+  ldnn::BwdJob j[2];
+  const at::Tensor* dys[2] = {&dy0, &dy1};
+  const at::Tensor* ws[2] = {&w0, &w1};
+  const at::Tensor* dxs[2] = {&dx0, &dx1};
+  const at::Tensor* dws[2] = {&dw0, &dw1};
+  const int64_t strides[2] = {stride0, stride1}, pads[2] = {pad0, pad1};
+  const double betas[2] = {beta0, beta1};
+  for (int c = 0; c < 2; ++c) {
+    check_dev(*dys[c], at::kBFloat16, "dy");
+    check_dev(*ws[c], at::kBFloat16, "w");
+    check_dev(*dxs[c], at::kBFloat16, "dx");
+    check_dev(*dws[c], at::kFloat, "dw");
+    TORCH_CHECK(dxs[c]->sizes() == x.sizes(), "conv_bwd2: dx must have x's shape");
+    j[c].sd = conv_shape(*dxs[c], *ws[c], *dys[c], strides[c], pads[c]);
+    j[c].sw = wgrad_shape(*dys[c], x, *dws[c], strides[c], pads[c], real_channels);
+    j[c].dy = bf16_ptr(*dys[c]);
+    j[c].w = bf16_ptr(*ws[c]);
+    j[c].dx = bf16_mut(*dxs[c]);
+    j[c].dw = dws[c]->data_ptr<float>();
+    j[c].beta = (float)betas[c];
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  const auto wd = conv_ws2(j[0].sd, j[1].sd, 1, x);
+  const auto ww = conv_ws2(j[0].sw, j[1].sw, 2, x);
+  j[0].ws_d = wd.first.ws();
+  j[0].cnt_d = wd.first.c();
+  j[1].ws_d = wd.second.ws();
+  j[1].cnt_d = wd.second.c();
+  j[0].ws_w = ww.first.ws();
+  j[1].ws_w = ww.second.ws();
+  check(ldnn::conv2d_bwd2(j[0], j[1], bf16_ptr(x), cur_stream(x)), "conv2d_bwd2");
 }
 
 // A conv layer's backward: dx (conv_dgrad, optional BN statistics) AND dw (conv_wgrad, beta /
@@ -1942,6 +2003,10 @@ PYBIND11_MODULE(_C, m) {
         py::arg("w1"), py::arg("y1"), py::arg("stride1"), py::arg("pad1"), py::arg("bn0") = py::none(),
         py::arg("bn1") = py::none(),
         "two forward convs of one input in one launch where the kernels allow; returns the BN-statistics flags");
+  m.def("conv_bwd2", &conv_bwd2, py::arg("x"), py::arg("dy0"), py::arg("w0"), py::arg("dx0"), py::arg("dw0"),
+        py::arg("stride0"), py::arg("pad0"), py::arg("beta0"), py::arg("dy1"), py::arg("w1"), py::arg("dx1"),
+        py::arg("dw1"), py::arg("stride1"), py::arg("pad1"), py::arg("beta1"), py::arg("real_channels") = 0,
+        "two convs of one input x, backward (dgrads + wgrads) in one launch where the kernels allow");
   m.def("conv_bwd", &conv_bwd, py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("x"), py::arg("dw"),
         py::arg("stride"), py::arg("pad"), py::arg("beta") = 0.0, py::arg("real_channels") = 0,
         py::arg("bn_x") = py::none(), py::arg("bn_mask") = py::none(), py::arg("bn_ws") = py::none(),

@@ -145,6 +145,24 @@ hipError_t conv2d_fwd2(const ConvShape& s0, const uint16_t* x, const uint16_t* w
 hipError_t conv2d_fwd2_lds(const ConvShape& s0, const uint16_t* x, const uint16_t* w0, uint16_t* y0, float* ws0,
                            int* cnt0, const BnFin* bn0, bool* used0, const ConvShape& s1, const uint16_t* w1,
                            uint16_t* y1, float* ws1, int* cnt1, const BnFin* bn1, bool* used1, hipStream_t st);
+// One conv's backward job: dgrad (shape sd: dy, w -> dx; split-K workspace ws_d / counters
+// cnt_d) and wgrad (shape sw: dy, x -> dw with beta; slabs ws_w).
+struct BwdJob {
+  ConvShape sd, sw;
+  const uint16_t* dy;
+  const uint16_t* w;
+  uint16_t* dx;
+  float* ws_d;
+  int* cnt_d;
+  float* dw;
+  float beta;
+  float* ws_w;
+};
+// A downsampling block's two convs of one input x: both dgrads and wgrads in one launch where the
+// kernels allow (conv2d_bwd2_lds), else each conv's conv2d_bwd (conv2d_bwd2).  j0 / j1 need
+// distinct counter ranges.
+hipError_t conv2d_bwd2(const BwdJob& j0, const BwdJob& j1, const uint16_t* x, hipStream_t st);
+hipError_t conv2d_bwd2_lds(const BwdJob& j0, const BwdJob& j1, const uint16_t* x, hipStream_t st);
 // hipErrorNotSupported: the pair does not share a launch (conv2d_bwd runs them one by one)
 hipError_t conv2d_bwd_lds(const ConvShape& sd, const uint16_t* dy, const uint16_t* w, uint16_t* dx, float* ws_d,
                           int* cnt_d, const BnBwdFuse* bnb, bool* bn_used, const ConvShape& sw, const uint16_t* x,

@@ -352,6 +352,19 @@ hipError_t conv2d_fwd2(const ConvShape& s0, const uint16_t* x, const uint16_t* w
   return conv2d_fwd(s1, x, w1, y1, nullptr, EPI_NONE, st, ws1, cnt1, bn1, done1);
 }
 
+hipError_t conv2d_bwd2(const BwdJob& j0, const BwdJob& j1, const uint16_t* x, hipStream_t st) {
+  if (g_conv_impl == 0) {
+    const hipError_t e = conv2d_bwd2_lds(j0, j1, x, st);
+    if (e != hipErrorNotSupported) return e;
+  }
+  for (const BwdJob* j : {&j0, &j1}) {
+    const hipError_t e = conv2d_bwd(j->sd, j->dy, j->w, j->dx, j->ws_d, j->cnt_d, nullptr, nullptr, j->sw, x, j->dw,
+                                    j->beta, j->ws_w, st);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
 hipError_t conv2d_bwd(const ConvShape& sd, const uint16_t* dy, const uint16_t* w, uint16_t* dx, float* ws_d,
                       int* cnt_d, const BnBwdFuse* bnb, bool* bn_done, const ConvShape& sw, const uint16_t* x,
                       float* dw, float beta, float* ws_w, hipStream_t st) {

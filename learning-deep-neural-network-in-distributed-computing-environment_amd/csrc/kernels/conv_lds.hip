@@ -965,6 +965,51 @@ __global__ __launch_bounds__(256, 2) void conv_pair_kernel(PairArgs p) {
     conv_lds_body<WM1, WN1, OA1, OB1, EPI_NONE, F1, D1, 2>(p.a[1], p.pa[1], p.ba[1], p.pb[1], p.bb[1], vb, smem);
 }
 
+// A downsampling block's two convs' dgrads AND wgrads (four independent GEMMs) in ONE launch:
+// slots 0 / 2 are the dgrads (128x128 or 256x64 gather kind), 1 / 3 the wgrads (128x128 or
+// narrow); slot k's workgroups are [start[k], start[k+1]), every start a multiple of 8 (XCD
+// placement kept).  Slot fields are read with compile-time indices (a runtime index into the
+// kernel-argument arrays would copy them to scratch).
+enum MultiKind { MK_DG128 = 0, MK_DG256, MK_WG128, MK_WGN };
+struct MultiSlot {
+  LArgs a;
+  const bf16_t* pa;
+  const bf16_t* pb;
+  uint32_t ba, bb;
+  int gx, gy, gz, kind, start;
+};
+template <bool DG>
+__device__ __forceinline__ void multi_slot(const MultiSlot& q, int b, char* smem) {
+  b -= q.start;
+  const int gx = q.gx, gy = q.gy;
+  if (b >= gx * gy * q.gz) return;  // (slot ranges are padded to multiples of 8)
+  const VB vb{b % gx, (b / gx) % gy, b / (gx * gy), gx, gy};
+  if constexpr (DG) {
+    if (q.kind == MK_DG256)
+      conv_lds_body<4, 1, DgradA<256, 8, 4>, DgradB<64, 2, 4>, EPI_NONE, false, true, 2>(q.a, q.pa, q.ba, q.pb, q.bb,
+                                                                                        vb, smem);
+    else
+      conv_lds_body<2, 2, DgradA<128, 4, 4>, DgradB<128, 4, 4>, EPI_NONE, false, true, 2>(q.a, q.pa, q.ba, q.pb, q.bb,
+                                                                                         vb, smem);
+  } else {
+    if (q.kind == MK_WGN)
+      conv_lds_body<1, 4, WgradA<64, 2, 4>, WgradB<256, 8, 4>, EPI_NONE, true, false, 2>(q.a, q.pa, q.ba, q.pb, q.bb,
+                                                                                        vb, smem);
+    else
+      conv_lds_body<2, 2, WgradA<128, 4, 4>, WgradB<128, 4, 4>, EPI_NONE, true, false, 2>(q.a, q.pa, q.ba, q.pb, q.bb,
+                                                                                         vb, smem);
+  }
+}
+// (four kernel parameters rather than one array: each slot's fields stay kernel-argument loads)
+__global__ __launch_bounds__(256, 2) void conv_multi_kernel(MultiSlot q0, MultiSlot q1, MultiSlot q2, MultiSlot q3) {
+  __shared__ __attribute__((aligned(1024))) char smem[2 * 5 * 64 * 128];  // the largest kind's 2-stage ring
+  const int b = (int)blockIdx.x;
+  if (b >= q3.start) multi_slot<false>(q3, b, smem);
+  else if (b >= q2.start) multi_slot<true>(q2, b, smem);
+  else if (b >= q1.start) multi_slot<false>(q1, b, smem);
+  else multi_slot<true>(q0, b, smem);
+}
+
 // ---- halo path: 3x3 stride-1 pad-1 fwd / dgrad with the A operand staged ONCE --
 // The gather kernel above DMAs a fresh 64-channel A tile for every filter tap, so
 // each activation row crosses the L1 / texture path 9 times per channel block --
@@ -2483,6 +2528,43 @@ __global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__
   }
 }
 
+// Two wgrads' slab sums in one launch (blocks [0, nb0) the first): a downsampling block's
+// conv and shortcut conv after their shared backward launch.
+template <bool NT>
+__global__ __launch_bounds__(256) void slab_sum2_kernel(const float* __restrict__ ws0, float* __restrict__ out0,
+                                                        int64_t n40, int splits0, float beta0, int nb0,
+                                                        const float* __restrict__ ws1, float* __restrict__ out1,
+                                                        int64_t n41, int splits1, float beta1) {
+  __shared__ floatx4 part[8][32];
+  const bool second = (int)blockIdx.x >= nb0;
+  const float* ws = second ? ws1 : ws0;
+  float* out = second ? out1 : out0;
+  const int64_t n4 = second ? n41 : n40;
+  const int splits = second ? splits1 : splits0;
+  const float beta = second ? beta1 : beta0;
+  const int col = threadIdx.x & 31, sl = threadIdx.x >> 5;
+  const int64_t i = (int64_t)((int)blockIdx.x - (second ? nb0 : 0)) * 32 + col;
+  floatx4 v = {0.f, 0.f, 0.f, 0.f};
+  if (i < n4) {
+    const floatx4* w = reinterpret_cast<const floatx4*>(ws) + i;
+    int sp = sl;
+    for (; sp + 24 < splits; sp += 32) {
+      const floatx4 a = slab_ld<NT>(w + (int64_t)sp * n4), b = slab_ld<NT>(w + (int64_t)(sp + 8) * n4);
+      const floatx4 c = slab_ld<NT>(w + (int64_t)(sp + 16) * n4), d = slab_ld<NT>(w + (int64_t)(sp + 24) * n4);
+      v += (a + b) + (c + d);
+    }
+    for (; sp < splits; sp += 8) v += slab_ld<NT>(w + (int64_t)sp * n4);
+  }
+  part[sl][col] = v;
+  __syncthreads();
+  if (sl == 0 && i < n4) {
+#pragma unroll
+    for (int q = 1; q < 8; ++q) v += part[q][col];
+    if (beta != 0.f) v += beta * reinterpret_cast<const floatx4*>(out)[i];
+    reinterpret_cast<floatx4*>(out)[i] = v;
+  }
+}
+
 bool fits(size_t bytes) { return bytes < kOOBLimit; }
 
 int env_int(const char* name, int dflt) {
@@ -3573,6 +3655,66 @@ hipError_t conv2d_fwd2_lds(const ConvShape& s0, const uint16_t* x, const uint16_
   e = fwd_post(f0, y0, nullptr, EPI_NONE, ws0, st);
   if (e != hipSuccess) return e;
   return fwd_post(f1, y1, nullptr, EPI_NONE, ws1, st);
+}
+
+// A downsampling block's two convs of one input x, backward: both dgrads and both wgrads in ONE
+// launch (conv_multi_kernel), then the dgrads' slab passes and both wgrads' slab sums in one
+// (slab_sum2_kernel); hipErrorNotSupported where a GEMM takes another kernel.
+hipError_t conv2d_bwd2_lds(const BwdJob& j0, const BwdJob& j1, const uint16_t* x, hipStream_t st) {
+  if (!pair_env() || deep_ring(0) || conv_xf_env() != 0) return hipErrorNotSupported;
+  const BwdJob* js[2] = {&j0, &j1};
+  DgradPrep d[2];
+  WgradPrep w[2];
+  WgradPlan pw[2];
+  for (int c = 0; c < 2; ++c) {
+    const BwdJob& j = *js[c];
+    const ConvShape &sd = j.sd, &sw = j.sw;
+    if (sd.K % 64 != 0 || !shape_ok(sd) || sd.N * sd.H * sd.W <= 0) return hipErrorNotSupported;
+    if (!shape_ok(sw) || sw.C % 8 != 0 || sw.K % 8 != 0 || (j.beta != 0.f && j.beta != 1.f) || stem_s2d_ok(sw))
+      return hipErrorNotSupported;
+    pw[c] = plan_wgrad(sw);
+    if (pw[c].ring || (pw[c].splits > 1 && j.ws_w == nullptr)) return hipErrorNotSupported;
+    d[c] = dgrad_prep(sd, j.dx, j.ws_d, j.cnt_d, nullptr);
+    if (d[c].ws64 || d[c].hb || d[c].halo) return hipErrorNotSupported;
+    w[c] = wgrad_prep(sw, pw[c], j.dw, j.beta, j.ws_w);
+  }
+  MultiSlot q[4] = {};
+  int at = 0;
+  for (int c = 0; c < 2; ++c) {
+    for (int g = 0; g < 2; ++g) {
+      MultiSlot& m = q[2 * c + g];
+      const bool dg = g == 0;
+      m.a = dg ? d[c].a : w[c].a;
+      m.pa = reinterpret_cast<const bf16_t*>(js[c]->dy);
+      m.pb = reinterpret_cast<const bf16_t*>(dg ? js[c]->w : x);
+      m.ba = (uint32_t)(dg ? d[c].bdy : w[c].bdy);
+      m.bb = (uint32_t)(dg ? d[c].bw : w[c].bx);
+      m.gx = m.a.tiles_x;
+      m.gy = dg ? d[c].pl.splits : pw[c].splits;
+      m.gz = dg ? d[c].a.classes : 1;
+      m.kind = dg ? (d[c].pl.wm == 4 ? MK_DG256 : MK_DG128) : (pw[c].narrow ? MK_WGN : MK_WG128);
+      m.start = at;
+      at += (m.gx * m.gy * m.gz + 7) / 8 * 8;
+    }
+  }
+  conv_multi_kernel<<<(unsigned)at, 256, 0, st>>>(q[0], q[1], q[2], q[3]);
+  hipError_t e = hipGetLastError();
+  for (int c = 0; c < 2 && e == hipSuccess; ++c) e = dgrad_post(d[c], js[c]->dx, js[c]->ws_d, st, nullptr);
+  if (e != hipSuccess) return e;
+  if (w[0].slab && w[1].slab) {
+    const int64_t n40 = (int64_t)w[0].a.M * w[0].a.N / 4, n41 = (int64_t)w[1].a.M * w[1].a.N / 4;
+    const int nb0 = (int)((n40 + 31) / 32), nb1 = (int)((n41 + 31) / 32);
+    if (slab_nt_env())
+      slab_sum2_kernel<true><<<(unsigned)(nb0 + nb1), 256, 0, st>>>(j0.ws_w, j0.dw, n40, w[0].splits, j0.beta, nb0,
+                                                                     j1.ws_w, j1.dw, n41, w[1].splits, j1.beta);
+    else
+      slab_sum2_kernel<false><<<(unsigned)(nb0 + nb1), 256, 0, st>>>(j0.ws_w, j0.dw, n40, w[0].splits, j0.beta, nb0,
+                                                                      j1.ws_w, j1.dw, n41, w[1].splits, j1.beta);
+    return hipGetLastError();
+  }
+  e = wgrad_post(w[0], j0.dw, j0.beta, j0.ws_w, st);
+  if (e != hipSuccess) return e;
+  return wgrad_post(w[1], j1.dw, j1.beta, j1.ws_w, st);
 }
 
 }  // namespace ldnn

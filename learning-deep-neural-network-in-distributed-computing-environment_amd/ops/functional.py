@@ -460,6 +460,20 @@ class _Conv2dPairNative(torch.autograd.Function):
         C = _ext.C()
         (xb,) = ctx.saved_tensors
         flat, c0, c1, Cin, in_dtype = ctx.meta
+        if g0 is not None and g1 is not None and ctx.needs_input_grad[0] and ctx.needs_input_grad[1]:
+            # both convs' dgrads and wgrads in one launch (conv_bwd2)
+            job = []
+            for g, (weight, st, pd) in ((g0, c0), (g1, c1)):
+                sh = flat.shadow_storage(weight)
+                gb = as_nhwc(g if g.dtype == torch.bfloat16 else g.to(torch.bfloat16), sh.shape[0])
+                job.append((gb, sh, torch.empty_like(xb), flat.grad_storage(weight), st, pd, flat.grad_beta(weight)))
+            (ga, sa, xa, wa, sta, pa, ba), (gc, sc, xc, wc, stc, pc, bc) = job
+            C.conv_bwd2(xb, ga, sa, xa, wa, sta, pa, ba, gc, sc, xc, wc, stc, pc, bc, Cin)
+            flat.notify(c0[0], c1[0])
+            dxs = [_zpad(nchw_view(xa, Cin)), _zpad(nchw_view(xc, Cin))]
+            if in_dtype != torch.bfloat16:
+                dxs = [d.to(in_dtype) for d in dxs]
+            return dxs[0], dxs[1], None, None, None, None, None
         dxs = []
         for k, (g, (weight, st, pd)) in enumerate(((g0, c0), (g1, c1))):
             if g is None:
