@@ -167,7 +167,8 @@ hipError_t conv2d_bwd2_lds(const BwdJob& j0, const BwdJob& j1, const uint16_t* x
 hipError_t conv2d_bwd_lds(const ConvShape& sd, const uint16_t* dy, const uint16_t* w, uint16_t* dx, float* ws_d,
                           int* cnt_d, const BnBwdFuse* bnb, bool* bn_used, const ConvShape& sw, const uint16_t* x,
                           float* dw, float beta, float* ws_w, hipStream_t st);
-// dgrad + wgrad in one launch (LDNN_CONV_PAIR, default 1; the setter is for tests / A/B)
+// dgrad + wgrad in one launch (LDNN_CONV_PAIR: 0 off, 1 / 3 (default) / 2 see conv_lds.hip;
+// the setter is for tests / A/B)
 void set_conv_pair(int on);
 int get_conv_pair();
 struct ConvWorkspace {

@@ -3337,9 +3337,10 @@ struct DgradPrep {
   size_t bdy, bw;
 };
 
-// generic: the 4-wave gather kernel only (no big-tile / halo / weight-stationary variant)
+// generic: 1 = no big-tile halo kernel, 2 = the 4-wave gather kernel only (no big-tile / halo /
+// weight-stationary variant)
 DgradPrep dgrad_prep(const ConvShape& s, uint16_t* dx, float* ws, int* cnt, const BnBwdFuse* bnb,
-                     bool generic = false) {
+                     int generic = 0) {
   DgradPrep d{};
   d.hb = !generic && hb_takes(s, true);
   Plan& pl = d.pl;
@@ -3367,14 +3368,14 @@ DgradPrep dgrad_prep(const ConvShape& s, uint16_t* dx, float* ws, int* cnt, cons
   }
   d.bdy = (size_t)s.N * s.P * s.Q * s.K * 2;
   d.bw = (size_t)s.K * a.rsc * 2;
-  d.ws64 = !generic && ws64_takes(s, EPI_NONE);
+  d.ws64 = generic < 2 && ws64_takes(s, EPI_NONE);
   if (d.ws64) {
     a.ws = nullptr;
     a.cnt = nullptr;
     a.nk_split = a.nk_all;
     return d;
   }
-  d.halo = !generic && !d.hb && halo_takes(s, pl.wm);
+  d.halo = generic < 2 && !d.hb && halo_takes(s, pl.wm);
   // the BN backward statistics of the BN whose output's gradient dx is: stride-1 dgrads (no
   // class row remap) in the direct / in-launch combine epilogue, or in the slab sum
   if (bnb != nullptr && bn_bwd_env() && s.stride == 1 && pl.classes == 1 && s.C % 8 == 0) {
@@ -3545,10 +3546,13 @@ hipError_t conv2d_wgrad_lds(const ConvShape& s, const uint16_t* dy, const uint16
 
 // A layer's dgrad and wgrad (both reading dy) as ONE launch (conv_pair_kernel) when both take
 // the 4-wave gather kernels; hipErrorNotSupported otherwise (the caller runs them one by one).
-// LDNN_CONV_PAIR (A/B knob, default 1).
+// LDNN_CONV_PAIR (A/B knob): 0 off; 1 pair where both GEMMs take the gather kernels anyway;
+// 3 (default) also where the dgrad alone would take the big-tile halo kernel (ResNet-18 b64
+// 2.697 -> 2.675 ms, b256 7.343 -> 7.315: profiles/r5/conv_pair_hb_ab.txt); 2 also instead of
+// the weight-stationary dgrad and the ring wgrad (slower: profiles/r5/conv_pair_fwd_ab.txt)
 int g_conv_pair = -1;
 int pair_env() {
-  if (g_conv_pair < 0) g_conv_pair = env_int("LDNN_CONV_PAIR", 1);
+  if (g_conv_pair < 0) g_conv_pair = env_int("LDNN_CONV_PAIR", 3);
   return g_conv_pair;
 }
 void set_conv_pair(int on) { g_conv_pair = on; }
@@ -3577,9 +3581,9 @@ hipError_t conv2d_bwd_lds(const ConvShape& sd, const uint16_t* dy, const uint16_
   if (!shape_ok(sw) || sw.C % 8 != 0 || sw.K % 8 != 0 || (beta != 0.f && beta != 1.f)) return hipErrorNotSupported;
   if (stem_s2d_ok(sw)) return hipErrorNotSupported;
   // LDNN_CONV_PAIR=2: pair on the generic kernels even where a layer alone takes the big-tile /
-  // weight-stationary dgrad or the ring wgrad
-  const bool generic = pair_env() >= 2;
-  const WgradPlan pw = plan_wgrad(sw, !generic);
+  // weight-stationary dgrad or the ring wgrad; =3: instead of the big-tile dgrad only
+  const int generic = pair_env() == 2 ? 2 : pair_env() == 3 ? 1 : 0;
+  const WgradPlan pw = plan_wgrad(sw, generic < 2);
   if (pw.ring || (pw.splits > 1 && ws_w == nullptr)) return hipErrorNotSupported;
   const DgradPrep d = dgrad_prep(sd, dx, ws_d, cnt_d, bnb, generic);
   if (d.ws64 || d.hb || d.halo) return hipErrorNotSupported;
