@@ -2325,10 +2325,9 @@ __device__ __forceinline__ void slab_sum8(const floatx4* w, int64_t stride4, int
 // small-M fwd / dgrad slabs, 8 consecutive outputs per thread (two float4 per slab,
 // one 16-B store), all CUs.
 template <int EPI, bool NT>
-__global__ __launch_bounds__(256) void conv_slab_epilogue_kernel(const float* __restrict__ ws, bf16_t* __restrict__ out,
-                                                                 int64_t n8, int N, int splits,
-                                                                 const float* __restrict__ bias) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+__device__ __forceinline__ void slab_epi_body(const float* __restrict__ ws, bf16_t* __restrict__ out, int64_t n8,
+                                              int N, int splits, const float* __restrict__ bias, int bxi) {
+  const int64_t i = (int64_t)bxi * 256 + threadIdx.x;
   if (i >= n8) return;
   const floatx4* w = reinterpret_cast<const floatx4*>(ws) + 2 * i;
   floatx4 v0, v1;
@@ -2341,6 +2340,12 @@ __global__ __launch_bounds__(256) void conv_slab_epilogue_kernel(const float* __
     o[q] = f2bf(apply_epi<EPI>(q < 4 ? v0[q] : v1[q - 4], b, 0.f));
   }
   reinterpret_cast<u16x8*>(out)[i] = o;
+}
+template <int EPI, bool NT>
+__global__ __launch_bounds__(256) void conv_slab_epilogue_kernel(const float* __restrict__ ws, bf16_t* __restrict__ out,
+                                                                 int64_t n8, int N, int splits,
+                                                                 const float* __restrict__ bias) {
+  slab_epi_body<EPI, NT>(ws, out, n8, N, splits, bias, (int)blockIdx.x);
 }
 
 hipError_t conv_slab_epilogue(const float* ws, uint16_t* out, int M, int N, int splits, const float* bias, int epi,
@@ -2372,16 +2377,20 @@ hipError_t conv_slab_epilogue(const float* ws, uint16_t* out, int M, int N, int 
 // with 8-copy atomics and one finalizing block was slower than the pair, profiles/cnn_slab_bn_ab_r2.jsonl.)
 // BWD: the slab sum of a small-M stride-1 dgrad AND the backward statistics of the BN whose
 // output's gradient it is (x / mask: that BN's input and ReLU bits; see bn_stats_epilogue).
-template <bool NT, bool BWD = false>
-__global__ __launch_bounds__(256) void conv_slab_bn_kernel(const float* __restrict__ ws, bf16_t* __restrict__ out,
-                                                           int M, int N, int splits, BnFin fin, int rpb,
-                                                           const bf16_t* __restrict__ bx,
-                                                           const uint8_t* __restrict__ bmask) {
-  constexpr int kLanes = 8, kRl = 32, kJs = 256 + kLanes;
-  __shared__ float red[2][8 * kJs];
-  __shared__ int last;
+constexpr int kSlabBnJs = 256 + 8;
+constexpr int kSlabBnRed = 2 * 8 * kSlabBnJs;   // the body's LDS floats (red[2][8 * kJs])
+// (bxi, byi): the workgroup's (column group, row group) of the (G, gy) grid; red: kSlabBnRed LDS
+// floats + one int after them
+template <bool NT, bool BWD>
+__device__ __forceinline__ void slab_bn_body(const float* __restrict__ ws, bf16_t* __restrict__ out, int M, int N,
+                                             int splits, const BnFin& fin, int rpb, const bf16_t* __restrict__ bx,
+                                             const uint8_t* __restrict__ bmask, int bxi, int byi, int gy,
+                                             float* red_) {
+  constexpr int kLanes = 8, kRl = 32, kJs = kSlabBnJs;
+  float (*red)[8 * kJs] = reinterpret_cast<float (*)[8 * kJs]>(red_);
+  int& last = *reinterpret_cast<int*>(red_ + kSlabBnRed);
   const int tid = threadIdx.x, lane = tid % kLanes, rlane = tid / kLanes;
-  const int c0 = blockIdx.x * 64 + lane * 8;
+  const int c0 = bxi * 64 + lane * 8;
   float s0[8], s1[8], mu[8], is[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) s0[j] = s1[j] = mu[j] = is[j] = 0.f;
@@ -2393,9 +2402,9 @@ __global__ __launch_bounds__(256) void conv_slab_bn_kernel(const float* __restri
         is[j] = fin.save_invstd[c0 + j];
       }
     }
-    const int r_end = min(M, (int)(blockIdx.y + 1) * rpb);
+    const int r_end = min(M, (byi + 1) * rpb);
     const size_t sstride = (size_t)M * N / 4;
-    for (int r = blockIdx.y * rpb + rlane; r < r_end; r += kRl) {
+    for (int r = byi * rpb + rlane; r < r_end; r += kRl) {
       const size_t o = (size_t)r * N + c0;
       u16x8 xv = {0, 0, 0, 0, 0, 0, 0, 0};
       uint32_t mb = 0xffu;
@@ -2436,27 +2445,37 @@ __global__ __launch_bounds__(256) void conv_slab_bn_kernel(const float* __restri
       t0 += red[0][j * kJs + q * kLanes + ln];
       t1 += red[1][j * kJs + q * kLanes + ln];
     }
-    const int c = blockIdx.x * 64 + ln * 8 + j;
-    if (gridDim.y == 1) {
+    const int c = bxi * 64 + ln * 8 + j;
+    if (gy == 1) {
       if (c < N) bn_finalize_channel<BWD>(fin, M, N, c, t0, t1, 1.f / (float)M);
     } else if (c < N) {
-      grp_store(fin.part + (size_t)blockIdx.y * 2 * N + c, t0);
-      grp_store(fin.part + ((size_t)blockIdx.y * 2 + 1) * N + c, t1);
+      grp_store(fin.part + (size_t)byi * 2 * N + c, t0);
+      grp_store(fin.part + ((size_t)byi * 2 + 1) * N + c, t1);
     }
   }
-  if (!BWD && blockIdx.x == 0 && blockIdx.y == 0 && tid == 0 && fin.num_batches) fin.num_batches[0] += 1;
-  if (gridDim.y == 1) return;
-  if (!grp_ticket(fin.tickets + blockIdx.x, gridDim.y, last)) return;
+  if (!BWD && bxi == 0 && byi == 0 && tid == 0 && fin.num_batches) fin.num_batches[0] += 1;
+  if (gy == 1) return;
+  if (!grp_ticket(fin.tickets + bxi, gy, last)) return;
   float* tot = &red[0][0];
-  const int cc = blockIdx.x * 64 + (tid & 63);
-  grp_sum(fin.part, N, cc, 0, gridDim.y, tot);
-  grp_sum(fin.part, N, cc, 1, gridDim.y, tot);
+  const int cc = bxi * 64 + (tid & 63);
+  grp_sum(fin.part, N, cc, 0, gy, tot);
+  grp_sum(fin.part, N, cc, 1, gy, tot);
   __syncthreads();
   if (tid < 64 && cc < N) {
     const float S0 = tot[tid] + tot[64 + tid] + tot[128 + tid] + tot[192 + tid];
     const float S1 = tot[256 + tid] + tot[320 + tid] + tot[384 + tid] + tot[448 + tid];
     bn_finalize_channel<BWD>(fin, M, N, cc, S0, S1, 1.f / (float)M);
   }
+}
+
+template <bool NT, bool BWD = false>
+__global__ __launch_bounds__(256) void conv_slab_bn_kernel(const float* __restrict__ ws, bf16_t* __restrict__ out,
+                                                           int M, int N, int splits, BnFin fin, int rpb,
+                                                           const bf16_t* __restrict__ bx,
+                                                           const uint8_t* __restrict__ bmask) {
+  __shared__ float red[kSlabBnRed + 1];
+  slab_bn_body<NT, BWD>(ws, out, M, N, splits, fin, rpb, bx, bmask, (int)blockIdx.x, (int)blockIdx.y,
+                        (int)gridDim.y, red);
 }
 
 int env_int(const char* name, int dflt);
@@ -2502,11 +2521,10 @@ hipError_t conv_slab_bn(const float* ws, uint16_t* out, int M, int N, int splits
 // 4 loads in flight), reduced through LDS: enough blocks to cover the chip even
 // for a 64 x 576 weight, and a fixed summation order (deterministic).
 template <bool NT>
-__global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__ ws, float* __restrict__ out,
-                                                       int64_t n4, int splits, float beta) {
-  __shared__ floatx4 part[8][32];
+__device__ __forceinline__ void slab_sum_body(const float* __restrict__ ws, float* __restrict__ out, int64_t n4,
+                                              int splits, float beta, int bxi, floatx4 (*part)[32]) {
   const int col = threadIdx.x & 31, sl = threadIdx.x >> 5;
-  const int64_t i = (int64_t)blockIdx.x * 32 + col;
+  const int64_t i = (int64_t)bxi * 32 + col;
   floatx4 v = {0.f, 0.f, 0.f, 0.f};
   if (i < n4) {
     const floatx4* w = reinterpret_cast<const floatx4*>(ws) + i;
@@ -2527,42 +2545,56 @@ __global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__
     reinterpret_cast<floatx4*>(out)[i] = v;
   }
 }
-
-// Two wgrads' slab sums in one launch (blocks [0, nb0) the first): a downsampling block's
-// conv and shortcut conv after their shared backward launch.
 template <bool NT>
-__global__ __launch_bounds__(256) void slab_sum2_kernel(const float* __restrict__ ws0, float* __restrict__ out0,
-                                                        int64_t n40, int splits0, float beta0, int nb0,
-                                                        const float* __restrict__ ws1, float* __restrict__ out1,
-                                                        int64_t n41, int splits1, float beta1) {
+__global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__ ws, float* __restrict__ out,
+                                                       int64_t n4, int splits, float beta) {
   __shared__ floatx4 part[8][32];
-  const bool second = (int)blockIdx.x >= nb0;
-  const float* ws = second ? ws1 : ws0;
-  float* out = second ? out1 : out0;
-  const int64_t n4 = second ? n41 : n40;
-  const int splits = second ? splits1 : splits0;
-  const float beta = second ? beta1 : beta0;
-  const int col = threadIdx.x & 31, sl = threadIdx.x >> 5;
-  const int64_t i = (int64_t)((int)blockIdx.x - (second ? nb0 : 0)) * 32 + col;
-  floatx4 v = {0.f, 0.f, 0.f, 0.f};
-  if (i < n4) {
-    const floatx4* w = reinterpret_cast<const floatx4*>(ws) + i;
-    int sp = sl;
-    for (; sp + 24 < splits; sp += 32) {
-      const floatx4 a = slab_ld<NT>(w + (int64_t)sp * n4), b = slab_ld<NT>(w + (int64_t)(sp + 8) * n4);
-      const floatx4 c = slab_ld<NT>(w + (int64_t)(sp + 16) * n4), d = slab_ld<NT>(w + (int64_t)(sp + 24) * n4);
-      v += (a + b) + (c + d);
-    }
-    for (; sp < splits; sp += 8) v += slab_ld<NT>(w + (int64_t)sp * n4);
+  slab_sum_body<NT>(ws, out, n4, splits, beta, (int)blockIdx.x, part);
+}
+
+// The passes after a shared conv launch -- its GEMMs' slab sums (plain, with the next BN's
+// statistics, with a BN's backward statistics) and wgrad slab sums -- as ONE launch: task k owns
+// workgroups [start, start + gx * gy).  They are independent (disjoint outputs, per-BN tickets).
+enum PostKind { PK_EPI = 0, PK_BN_FWD, PK_BN_BWD, PK_SUM };
+struct PostTask {
+  int kind, start, gx, gy;
+  const float* ws;
+  void* out;
+  int M, N, splits, rpb;
+  float beta;
+  int64_t n;  // PK_EPI: outputs / 8; PK_SUM: floats / 4
+  BnFin fin;
+  const uint16_t* bx;
+  const uint8_t* mask;
+};
+template <bool NT>
+__device__ __forceinline__ void post_run(const PostTask& t, int b, float* lds) {
+  switch (t.kind) {
+    case PK_EPI:
+      slab_epi_body<EPI_NONE, NT>(t.ws, reinterpret_cast<bf16_t*>(t.out), t.n, t.N, t.splits, nullptr, b);
+      break;
+    case PK_BN_FWD:
+      slab_bn_body<NT, false>(t.ws, reinterpret_cast<bf16_t*>(t.out), t.M, t.N, t.splits, t.fin, t.rpb, nullptr,
+                              nullptr, b % t.gx, b / t.gx, t.gy, lds);
+      break;
+    case PK_BN_BWD:
+      slab_bn_body<NT, true>(t.ws, reinterpret_cast<bf16_t*>(t.out), t.M, t.N, t.splits, t.fin, t.rpb,
+                             reinterpret_cast<const bf16_t*>(t.bx), t.mask, b % t.gx, b / t.gx, t.gy, lds);
+      break;
+    default:
+      slab_sum_body<NT>(t.ws, reinterpret_cast<float*>(t.out), t.n, t.splits, t.beta, b,
+                        reinterpret_cast<floatx4(*)[32]>(lds));
+      break;
   }
-  part[sl][col] = v;
-  __syncthreads();
-  if (sl == 0 && i < n4) {
-#pragma unroll
-    for (int q = 1; q < 8; ++q) v += part[q][col];
-    if (beta != 0.f) v += beta * reinterpret_cast<const floatx4*>(out)[i];
-    reinterpret_cast<floatx4*>(out)[i] = v;
-  }
+}
+template <bool NT>
+__global__ __launch_bounds__(256) void conv_post_kernel(PostTask t0, PostTask t1, PostTask t2, PostTask t3) {
+  __shared__ __attribute__((aligned(16))) float lds[kSlabBnRed + 4];
+  const int b = (int)blockIdx.x;
+  if (t3.gx && b >= t3.start) post_run<NT>(t3, b - t3.start, lds);
+  else if (t2.gx && b >= t2.start) post_run<NT>(t2, b - t2.start, lds);
+  else if (t1.gx && b >= t1.start) post_run<NT>(t1, b - t1.start, lds);
+  else post_run<NT>(t0, b, lds);
 }
 
 bool fits(size_t bytes) { return bytes < kOOBLimit; }
@@ -3225,6 +3257,84 @@ hipError_t conv2d_fwd_lds_small_c(const ConvShape& s, const uint16_t* x, const u
 }
 
 namespace {
+// Post passes gathered for one conv_post_kernel launch (post_flush).
+struct PostBatch {
+  PostTask t[4] = {};
+  int n = 0, blocks = 0;
+  void push(PostTask task) {
+    task.start = blocks;
+    blocks += task.gx * task.gy;
+    t[n++] = task;
+  }
+};
+PostTask slab_bn_task(const float* ws, uint16_t* out, int M, int N, int splits, const BnFin& fin,
+                      const BnBwdFuse* bnb) {
+  static const int target = std::max(1, env_int("LDNN_CONV_SLAB_BN_TARGET", 512));
+  const int G = (N + 63) / 64;
+  int ny = std::max(1, std::min({(target + G - 1) / G, (M + 31) / 32, kGrpMax}));
+  const int rpb = (M + ny - 1) / ny;
+  ny = (M + rpb - 1) / rpb;
+  PostTask t{};
+  t.kind = bnb != nullptr ? PK_BN_BWD : PK_BN_FWD;
+  t.gx = G;
+  t.gy = ny;
+  t.ws = ws;
+  t.out = out;
+  t.M = M;
+  t.N = N;
+  t.splits = splits;
+  t.rpb = rpb;
+  t.fin = fin;
+  if (bnb != nullptr) {
+    t.bx = bnb->x;
+    t.mask = bnb->mask;
+  }
+  return t;
+}
+PostTask slab_epi_task(const float* ws, uint16_t* out, int M, int N, int splits) {
+  PostTask t{};
+  t.kind = PK_EPI;
+  t.n = (int64_t)M * N / 8;
+  t.gx = (int)((t.n + 255) / 256);
+  t.gy = 1;
+  t.ws = ws;
+  t.out = out;
+  t.N = N;
+  t.splits = splits;
+  return t;
+}
+PostTask slab_sum_task(const float* ws, float* out, int64_t n4, int splits, float beta) {
+  PostTask t{};
+  t.kind = PK_SUM;
+  t.n = n4;
+  t.gx = (int)((n4 + 31) / 32);
+  t.gy = 1;
+  t.ws = ws;
+  t.out = out;
+  t.splits = splits;
+  t.beta = beta;
+  return t;
+}
+// LDNN_CONV_POST_MERGE (A/B knob, default 1): 0 launches each post task on its own
+hipError_t post_flush(const PostBatch& pb, hipStream_t st) {
+  if (pb.n == 0 || pb.blocks == 0) return hipSuccess;
+  static const int merge = env_int("LDNN_CONV_POST_MERGE", 1);
+  if (!merge && pb.n > 1) {
+    for (int k = 0; k < pb.n; ++k) {
+      PostBatch one;
+      one.push(pb.t[k]);
+      const hipError_t e = post_flush(one, st);
+      if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+  }
+  if (slab_nt_env()) conv_post_kernel<true><<<(unsigned)pb.blocks, 256, 0, st>>>(pb.t[0], pb.t[1], pb.t[2], pb.t[3]);
+  else conv_post_kernel<false><<<(unsigned)pb.blocks, 256, 0, st>>>(pb.t[0], pb.t[1], pb.t[2], pb.t[3]);
+  return hipGetLastError();
+}
+}  // namespace
+
+namespace {
 // What conv2d_fwd_lds launches for a C % 64 == 0 shape, planned without launching it.
 struct FwdPrep {
   LArgs a;
@@ -3283,6 +3393,13 @@ FwdPrep fwd_prep(const ConvShape& s, uint16_t* y, const float* bias, int epi, fl
   }
   f.halo = !f.ws64 && !f.hb && halo_takes(s, pl.wm);
   return f;
+}
+
+// the same as a post task (bias-free EPI_NONE convs; conv2d_fwd2_lds)
+void fwd_post_task(const FwdPrep& f, uint16_t* y, float* ws, PostBatch& pb) {
+  if (!f.slab) return;
+  if (f.slab_fin != nullptr) pb.push(slab_bn_task(ws, y, f.a.M, f.a.N, f.pl.splits, *f.slab_fin, nullptr));
+  else pb.push(slab_epi_task(ws, y, f.a.M, f.a.N, f.pl.splits));
 }
 
 // after the main kernel: the slab split-K sum (with the next BN's statistics when taken)
@@ -3391,6 +3508,20 @@ DgradPrep dgrad_prep(const ConvShape& s, uint16_t* dx, float* ws, int* cnt, cons
   return d;
 }
 
+// the same as a post task (conv2d_bwd_lds / conv2d_bwd2_lds)
+void dgrad_post_task(const DgradPrep& d, uint16_t* dx, float* ws, PostBatch& pb, bool* bn_used) {
+  if (!d.slab) {
+    if (bn_used) *bn_used = d.a.bn_stats != 0;
+    return;
+  }
+  if (d.slab_bnb != nullptr) {
+    if (bn_used) *bn_used = true;
+    pb.push(slab_bn_task(ws, dx, d.a.M, d.a.N, d.pl.splits, d.slab_bnb->fin, d.slab_bnb));
+    return;
+  }
+  pb.push(slab_epi_task(ws, dx, d.a.M, d.a.N, d.pl.splits));
+}
+
 // after the main kernel: the slab split-K sum (with the BN statistics when taken)
 hipError_t dgrad_post(const DgradPrep& d, uint16_t* dx, float* ws, hipStream_t st, bool* bn_used) {
   if (!d.slab) {
@@ -3468,6 +3599,10 @@ WgradPrep wgrad_prep(const ConvShape& s, const WgradPlan& pl, float* dw, float b
   w.bdy = (size_t)s.N * s.P * s.Q * s.K * 2;
   w.bx = (size_t)s.N * s.H * s.W * s.C * 2;
   return w;
+}
+
+void wgrad_post_task(const WgradPrep& w, float* dw, float beta, float* ws, PostBatch& pb) {
+  if (w.slab) pb.push(slab_sum_task(ws, dw, (int64_t)w.a.M * w.a.N / 4, w.splits, beta));
 }
 
 hipError_t wgrad_post(const WgradPrep& w, float* dw, float beta, float* ws, hipStream_t st) {
@@ -3611,9 +3746,11 @@ hipError_t conv2d_bwd_lds(const ConvShape& sd, const uint16_t* dy, const uint16_
     else e = launch_pair<LDNN_DG128, LDNN_WG128>(p, st);
   }
   if (e != hipSuccess) return e;
-  e = dgrad_post(d, dx, ws_d, st, bn_used);
-  if (e != hipSuccess) return e;
-  return wgrad_post(wp, dw, beta, ws_w, st);
+  // the dgrad's slab pass and the wgrad's slab sum in one launch
+  PostBatch pb;
+  dgrad_post_task(d, dx, ws_d, pb, bn_used);
+  wgrad_post_task(wp, dw, beta, ws_w, pb);
+  return post_flush(pb, st);
 }
 
 // A downsampling block's two forward convs of one input x (the 3x3 and the 1x1 shortcut) as ONE
@@ -3656,9 +3793,10 @@ hipError_t conv2d_fwd2_lds(const ConvShape& s0, const uint16_t* x, const uint16_
   if (e != hipSuccess) return e;
   if (used0) *used0 = f0.bn_used;
   if (used1) *used1 = f1.bn_used;
-  e = fwd_post(f0, y0, nullptr, EPI_NONE, ws0, st);
-  if (e != hipSuccess) return e;
-  return fwd_post(f1, y1, nullptr, EPI_NONE, ws1, st);
+  PostBatch pb;
+  fwd_post_task(f0, y0, ws0, pb);
+  fwd_post_task(f1, y1, ws1, pb);
+  return post_flush(pb, st);
 }
 
 // A downsampling block's two convs of one input x, backward: both dgrads and both wgrads in ONE
@@ -3703,22 +3841,11 @@ hipError_t conv2d_bwd2_lds(const BwdJob& j0, const BwdJob& j1, const uint16_t* x
   }
   conv_multi_kernel<<<(unsigned)at, 256, 0, st>>>(q[0], q[1], q[2], q[3]);
   hipError_t e = hipGetLastError();
-  for (int c = 0; c < 2 && e == hipSuccess; ++c) e = dgrad_post(d[c], js[c]->dx, js[c]->ws_d, st, nullptr);
   if (e != hipSuccess) return e;
-  if (w[0].slab && w[1].slab) {
-    const int64_t n40 = (int64_t)w[0].a.M * w[0].a.N / 4, n41 = (int64_t)w[1].a.M * w[1].a.N / 4;
-    const int nb0 = (int)((n40 + 31) / 32), nb1 = (int)((n41 + 31) / 32);
-    if (slab_nt_env())
-      slab_sum2_kernel<true><<<(unsigned)(nb0 + nb1), 256, 0, st>>>(j0.ws_w, j0.dw, n40, w[0].splits, j0.beta, nb0,
-                                                                     j1.ws_w, j1.dw, n41, w[1].splits, j1.beta);
-    else
-      slab_sum2_kernel<false><<<(unsigned)(nb0 + nb1), 256, 0, st>>>(j0.ws_w, j0.dw, n40, w[0].splits, j0.beta, nb0,
-                                                                      j1.ws_w, j1.dw, n41, w[1].splits, j1.beta);
-    return hipGetLastError();
-  }
-  e = wgrad_post(w[0], j0.dw, j0.beta, j0.ws_w, st);
-  if (e != hipSuccess) return e;
-  return wgrad_post(w[1], j1.dw, j1.beta, j1.ws_w, st);
+  PostBatch pb;
+  for (int c = 0; c < 2; ++c) dgrad_post_task(d[c], js[c]->dx, js[c]->ws_d, pb, nullptr);
+  for (int c = 0; c < 2; ++c) wgrad_post_task(w[c], js[c]->dw, js[c]->beta, js[c]->ws_w, pb);
+  return post_flush(pb, st);
 }
 
 }  // namespace ldnn
