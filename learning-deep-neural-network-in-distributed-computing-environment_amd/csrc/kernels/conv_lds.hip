@@ -2654,10 +2654,16 @@ WgradPlan plan_wgrad(const ConvShape& s, bool allow_ring = true) {
   const int M = s.K, N = s.R * s.S * s.C;
   p.tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   p.nk_all = (s.N * s.P * s.Q + 63) / 64;
-  // split the npq reduction over ~1.5 workgroups per CU, >= 8 K-tiles per slice
+  // split the npq reduction over ~1.5 workgroups per CU, >= min_kt K-tiles per slice
   int splits = 1;
   static const int target = env_int("LDNN_CONV_WGRAD_TARGET", 384);  // workgroups to aim for (A/B knob)
-  if (p.tiles < 256) splits = std::max(1, std::min((target + p.tiles - 1) / p.tiles, p.nk_all / 8));
+  static const int min_kt1 = std::max(1, env_int("LDNN_CONV_WGRAD_MIN_KT", 8));     // 1x1 filters (A/B knob)
+  // larger filters: >= 16 K-tiles per slice since dgrad and wgrad share a launch (EnhancedCNN b64
+  // 1.642 -> 1.573 ms with LDNN_CONV_SLAB_TARGET 256, ResNet-18 b64 / b256 -0.3 / -0.2 %; the 1x1
+  // shortcut wgrads stay at 8: 16 there cost ResNet-18 b64 +0.6 %, profiles/r5/conv_split_knobs_ab.txt)
+  static const int min_kt3 = std::max(1, env_int("LDNN_CONV_WGRAD_MIN_KT3", 16));   // (A/B knob)
+  const int min_kt = s.R * s.S > 1 ? min_kt3 : min_kt1;
+  if (p.tiles < 256) splits = std::max(1, std::min((target + p.tiles - 1) / p.tiles, p.nk_all / min_kt));
   p.nk_split = (p.nk_all + splits - 1) / splits;
   p.splits = (p.nk_all + p.nk_split - 1) / p.nk_split;
   return p;
@@ -2987,7 +2993,9 @@ int small_m_splits(int tiles, int nk) {
 // per slice, at most 32 slices.
 int slab_splits(int tiles, int nk) {
   if (tiles >= 160 || nk < 8) return 1;
-  static const int target = env_int("LDNN_CONV_SLAB_TARGET", 512);     // workgroups to aim for (A/B knob)
+  // (256 since conv GEMMs share launches: EnhancedCNN b64 -1.2 %, ResNet-18 neutral,
+  // profiles/r5/conv_split_knobs_ab.txt)
+  static const int target = env_int("LDNN_CONV_SLAB_TARGET", 256);     // workgroups to aim for (A/B knob)
   static const int min_kt = env_int("LDNN_CONV_SLAB_MIN_KT", 3);        // K-tiles per slice at least (A/B knob)
   int sp = (target + tiles - 1) / tiles;
   sp = std::min(sp, nk / std::max(1, min_kt));
