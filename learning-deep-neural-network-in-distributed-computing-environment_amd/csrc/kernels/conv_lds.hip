@@ -2381,7 +2381,9 @@ constexpr int kSlabBnJs = 256 + 8;
 constexpr int kSlabBnRed = 2 * 8 * kSlabBnJs;   // the body's LDS floats (red[2][8 * kJs])
 // (bxi, byi): the workgroup's (column group, row group) of the (G, gy) grid; red: kSlabBnRed LDS
 // floats + one int after them
-template <bool NT, bool BWD>
+// SRC16 (BWD only): no slabs -- the statistics of the bf16 dgrad output already in `out` (an
+// in-launch combine / direct dgrad's dx), read instead of written.
+template <bool NT, bool BWD, bool SRC16 = false>
 __device__ __forceinline__ void slab_bn_body(const float* __restrict__ ws, bf16_t* __restrict__ out, int M, int N,
                                              int splits, const BnFin& fin, int rpb, const bf16_t* __restrict__ bx,
                                              const uint8_t* __restrict__ bmask, int bxi, int byi, int gy,
@@ -2412,12 +2414,17 @@ __device__ __forceinline__ void slab_bn_body(const float* __restrict__ ws, bf16_
         xv = *reinterpret_cast<const u16x8*>(bx + o);
         if (bmask != nullptr) mb = bmask[o >> 3];
       }
-      floatx4 v0, v1;
-      slab_sum8<NT>(reinterpret_cast<const floatx4*>(ws + o), (int64_t)sstride, splits, v0, v1);
       u16x8 ob;
+      if constexpr (SRC16) {
+        ob = *reinterpret_cast<const u16x8*>(out + o);
+      } else {
+        floatx4 v0, v1;
+        slab_sum8<NT>(reinterpret_cast<const floatx4*>(ws + o), (int64_t)sstride, splits, v0, v1);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ob[j] = f2bf(j < 4 ? v0[j] : v1[j - 4]);
+      }
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        ob[j] = f2bf(j < 4 ? v0[j] : v1[j - 4]);
         const float v = bf2f(ob[j]);
         if constexpr (BWD) {
           const float gv = ((mb >> j) & 1u) ? v : 0.f;
@@ -2428,7 +2435,7 @@ __device__ __forceinline__ void slab_bn_body(const float* __restrict__ ws, bf16_
           s1[j] += v * v;
         }
       }
-      *reinterpret_cast<u16x8*>(out + o) = ob;
+      if constexpr (!SRC16) *reinterpret_cast<u16x8*>(out + o) = ob;
     }
   }
 #pragma unroll
@@ -2487,7 +2494,9 @@ int slab_bn_env() {
 }
 // LDNN_CONV_BN_BWD (A/B knob): stride-1 dgrads take the backward statistics of the BN whose
 // output's gradient they produce (conv2d_dgrad with a BnBwdFuse): 1 (default) in the slab split-K
-// sum only, 2 also in the direct / in-launch-combine epilogue, 0 never.  Measured on MI355X
+// sum, and for a dgrad without slabs that shares its launch with the wgrad, as a pass over dx in
+// the shared post launch; 3 in the slab sum only; 2 also in the direct / in-launch-combine
+// epilogue; 0 never.  Measured on MI355X
 // (profiles/r5/conv_bn_bwd_ab.txt): the slab pass absorbs the reduce for ~1.5 us less per BN, while
 // the epilogue form -- x and mask loads, 8-copy atomics and one finalizing workgroup behind the
 // tile's own stores -- added 11-13 us to a 64 / 128-tile dgrad to save an 8-10 us reduce launch
@@ -2555,7 +2564,7 @@ __global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__
 // The passes after a shared conv launch -- its GEMMs' slab sums (plain, with the next BN's
 // statistics, with a BN's backward statistics) and wgrad slab sums -- as ONE launch: task k owns
 // workgroups [start, start + gx * gy).  They are independent (disjoint outputs, per-BN tickets).
-enum PostKind { PK_EPI = 0, PK_BN_FWD, PK_BN_BWD, PK_SUM };
+enum PostKind { PK_EPI = 0, PK_BN_FWD, PK_BN_BWD, PK_SUM, PK_BN_BWD_RED };
 struct PostTask {
   int kind, start, gx, gy;
   const float* ws;
@@ -2580,6 +2589,10 @@ __device__ __forceinline__ void post_run(const PostTask& t, int b, float* lds) {
     case PK_BN_BWD:
       slab_bn_body<NT, true>(t.ws, reinterpret_cast<bf16_t*>(t.out), t.M, t.N, t.splits, t.fin, t.rpb,
                              reinterpret_cast<const bf16_t*>(t.bx), t.mask, b % t.gx, b / t.gx, t.gy, lds);
+      break;
+    case PK_BN_BWD_RED:
+      slab_bn_body<NT, true, true>(nullptr, reinterpret_cast<bf16_t*>(t.out), t.M, t.N, 0, t.fin, t.rpb,
+                                   reinterpret_cast<const bf16_t*>(t.bx), t.mask, b % t.gx, b / t.gx, t.gy, lds);
       break;
     default:
       slab_sum_body<NT>(t.ws, reinterpret_cast<float*>(t.out), t.n, t.splits, t.beta, b,
@@ -3459,6 +3472,7 @@ struct DgradPrep {
   Plan pl;
   bool slab, hb, halo, ws64;
   const BnBwdFuse* slab_bnb;
+  const BnBwdFuse* red_bnb;   // no slabs: the BN statistics as a post task over dx (paired launches)
   size_t bdy, bw;
 };
 
@@ -3504,9 +3518,12 @@ DgradPrep dgrad_prep(const ConvShape& s, uint16_t* dx, float* ws, int* cnt, cons
   // the BN backward statistics of the BN whose output's gradient dx is: stride-1 dgrads (no
   // class row remap) in the direct / in-launch combine epilogue, or in the slab sum
   if (bnb != nullptr && bn_bwd_env() && s.stride == 1 && pl.classes == 1 && s.C % 8 == 0) {
+    const bool grp = bnb->fin.part != nullptr && bnb->fin.tickets != nullptr;
     if (d.slab) {
-      if (slab_bn_env() && bnb->fin.part != nullptr && bnb->fin.tickets != nullptr) d.slab_bnb = bnb;
-    } else if (bn_bwd_env() >= 2) {
+      if (slab_bn_env() && grp) d.slab_bnb = bnb;
+    } else if (bn_bwd_env() == 1 && grp) {
+      d.red_bnb = bnb;
+    } else if (bn_bwd_env() == 2) {
       a.bn_stats = 1;
       a.bn = bnb->fin;
       a.bn_x = bnb->x;
@@ -3519,6 +3536,18 @@ DgradPrep dgrad_prep(const ConvShape& s, uint16_t* dx, float* ws, int* cnt, cons
 // the same as a post task (conv2d_bwd_lds / conv2d_bwd2_lds)
 void dgrad_post_task(const DgradPrep& d, uint16_t* dx, float* ws, PostBatch& pb, bool* bn_used) {
   if (!d.slab) {
+    if (d.red_bnb != nullptr) {   // the BN's backward statistics over dx, beside the other post passes
+      PostTask t = slab_bn_task(nullptr, dx, d.a.M, d.a.N, 0, d.red_bnb->fin, d.red_bnb);
+      t.kind = PK_BN_BWD_RED;
+      // the BN reduce's own row grouping (bn_pool.hip grp_geo): >= 256 rows per group, ~512 workgroups
+      const int M = d.a.M, G = t.gx;
+      int ny = std::max(1, std::min({(512 + G - 1) / G, M / 256, kGrpMax}));
+      t.rpb = (M + ny - 1) / ny;
+      t.gy = (M + t.rpb - 1) / t.rpb;
+      pb.push(t);
+      if (bn_used) *bn_used = true;
+      return;
+    }
     if (bn_used) *bn_used = d.a.bn_stats != 0;
     return;
   }

@@ -525,11 +525,13 @@ def _dgrad_bn_stats_case(Cc, N, C, H, K, relu):
     assert torch.count_nonzero(ws[10 * C + 16: 10 * C + 17]) == 0
 
 
-def test_resblock_bn1_backward_statistics_come_from_conv2_dgrad():
+@pytest.mark.parametrize("C,H", [(512, 4), (128, 16), (256, 8)])
+def test_resblock_bn1_backward_statistics_come_from_conv2_dgrad(C, H):
     """In a residual block, bn1's output feeds conv2 alone: its backward statistics come from
-    conv2's dgrad (here EnhancedCNN layer3's 512-channel 4x4 block: the slab split-K sum; one
-    fused BN backward per step), while the block input -- read by the shortcut through its twin
-    -- keeps the BN's own reduce; the gradients match the unfused path."""
+    conv2's dgrad (EnhancedCNN layer3's 512-channel 4x4 block: in the slab split-K sum; the 16x16 /
+    8x8 blocks: as a pass over dx in the launch after the shared dgrad + wgrad launch; one fused BN
+    backward per step), while the block input -- read by the shortcut through its twin -- keeps the
+    BN's own reduce; the gradients match the unfused path."""
     from ldnn.models.cnn import ResBlock
     from ldnn.ops import functional as LF
 
@@ -537,9 +539,9 @@ def test_resblock_bn1_backward_statistics_come_from_conv2_dgrad():
     grads = []
     for fused in (False, True):
         torch.manual_seed(37)
-        blk = ResBlock(512, 512).cuda()
+        blk = ResBlock(C, C).cuda()
         flat = ldnn.prepare(blk, "cuda")
-        x = torch.randn(64, 512, 4, 4, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+        x = torch.randn(64, C, H, H, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
         old = LF.CONV_BN_BWD
         LF.CONV_BN_BWD = fused
         try:
