@@ -93,3 +93,37 @@ def test_flat_params_padding_stays_zero():
     w = f.master_storage(m.layers[1].weight)
     assert w.shape == (16, 24)
     assert w[10:].abs().max() == 0 and w[:, 20:].abs().max() == 0
+
+
+def test_grad_fresh_peeks_without_consuming():
+    """FlatParams.grad_fresh reports a lazily zeroed gradient without consuming that state, so the
+    dgrad-side BN statistics can check it before the BN's own backward calls grad_beta."""
+    m = mlp2(8, 16, 4)
+    flat = FlatParams(m)
+    w = m[0].weight if hasattr(m, "__getitem__") else next(m.parameters())
+    assert flat.grad_beta(w) == 1.0          # nothing marked stale yet: accumulate
+    flat.zero_grad(lazy=True)
+    assert flat.grad_fresh(w) and flat.grad_fresh(w)   # peeking twice leaves it fresh
+    assert flat.grad_beta(w) == 0.0          # the first writer overwrites ...
+    assert not flat.grad_fresh(w) and flat.grad_beta(w) == 1.0   # ... and later ones accumulate
+
+
+@pytest.mark.parametrize("name", ["enhanced_cnn_small", "resnet18"])
+def test_downsample_blocks_cpu_match_separate_convs(name):
+    """On the CPU (no native launch) LF.conv2d_pair is the two module calls: the downsampling
+    blocks that issue their 3x3 and 1x1 convs through it give the plain PyTorch forward."""
+    import torch.nn.functional as F
+
+    from ldnn.ops import functional as LF
+
+    torch.manual_seed(0)
+    m = build_model(name)
+    xavier_init(m)
+    blk = next(b for b in m.modules() if getattr(b, "downsample", None) is not None
+               or (hasattr(b, "shortcut") and len(getattr(b, "shortcut", [])) > 0))
+    conv1 = blk.conv1
+    sc = blk.downsample[0] if getattr(blk, "downsample", None) is not None else blk.shortcut[0]
+    x = torch.randn(2, conv1.in_channels, 16, 16)
+    y0, y1 = LF.conv2d_pair(x, x, conv1, sc)
+    torch.testing.assert_close(y0, F.conv2d(x, conv1.weight, conv1.bias, conv1.stride, conv1.padding))
+    torch.testing.assert_close(y1, F.conv2d(x, sc.weight, sc.bias, sc.stride, sc.padding))
