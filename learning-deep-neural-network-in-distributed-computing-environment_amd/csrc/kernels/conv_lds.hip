@@ -3838,7 +3838,7 @@ hipError_t conv2d_fwd2_lds(const ConvShape& s0, const uint16_t* x, const uint16_
 
 // A downsampling block's two convs of one input x, backward: both dgrads and both wgrads in ONE
 // launch (conv_multi_kernel), then the dgrads' slab passes and both wgrads' slab sums in one
-// (slab_sum2_kernel); hipErrorNotSupported where a GEMM takes another kernel.
+// (conv_post_kernel); hipErrorNotSupported where a GEMM takes another kernel.
 hipError_t conv2d_bwd2_lds(const BwdJob& j0, const BwdJob& j1, const uint16_t* x, hipStream_t st) {
   if (!pair_env() || deep_ring(0) || conv_xf_env() != 0) return hipErrorNotSupported;
   const BwdJob* js[2] = {&j0, &j1};
