@@ -2669,7 +2669,9 @@ WgradPlan plan_wgrad(const ConvShape& s, bool allow_ring = true) {
   p.nk_all = (s.N * s.P * s.Q + 63) / 64;
   // split the npq reduction over ~1.5 workgroups per CU, >= min_kt K-tiles per slice
   int splits = 1;
-  static const int target = env_int("LDNN_CONV_WGRAD_TARGET", 384);  // workgroups to aim for (A/B knob)
+  // (512 since dgrad and wgrad share launches: ResNet-18 b256 7.332 -> 7.256 ms, b64 -0.2 %, EnhancedCNN
+  // neutral, 6 alternated samples each, profiles/r5/conv_wgrad_target_ab.txt)
+  static const int target = env_int("LDNN_CONV_WGRAD_TARGET", 512);  // workgroups to aim for (A/B knob)
   static const int min_kt1 = std::max(1, env_int("LDNN_CONV_WGRAD_MIN_KT", 8));     // 1x1 filters (A/B knob)
   // larger filters: >= 16 K-tiles per slice since dgrad and wgrad share a launch (EnhancedCNN b64
   // 1.642 -> 1.573 ms with LDNN_CONV_SLAB_TARGET 256, ResNet-18 b64 / b256 -0.3 / -0.2 %; the 1x1
