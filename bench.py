@@ -12,8 +12,9 @@ at 1/2/4/8 MI355X".  Config (weak scaling, fixed per-GPU work):
              7.58 M at 8192, 7.98 M at 16384, before the library dgrad)
   compute    bf16 MFMA GEMMs, fp32 accumulation, fp32 master weights + grads
   optimizer  SGD momentum 0.9 (fused kernel, full update every step)
-  comm       fp32 gradient reduce-scatter on RCCL every step, bucketed and
-             overlapped with the backward pass, sharded SGD, bf16 weight all-gather
+  comm       bf16 gradient reduce-scatter on RCCL every step (--grad-comm fp32: fp32),
+             bucketed and overlapped with the backward pass, widened into the fp32
+             shard of a sharded SGD (fp32 master), bf16 weight all-gather
   data       synthetic (device-generated Gaussian inputs, uniform labels),
              random-init (Xavier) weights; no dataset download exists here
 
@@ -61,6 +62,11 @@ from ldnn.train.static_mlp import OptimConfig, StaticMLPEngine  # noqa: E402
 from ldnn.utils import distributed as D  # noqa: E402
 
 METRIC = "samples/sec (whole node) + DP scaling eff., 3-layer MLP at 1/2/4/8 MI355X"
+GRAD_COMM = {"dtype": "bf16"}   # gradient collective dtype at N > 1 (--grad-comm)
+
+
+def _grad_dtype():
+    return torch.bfloat16 if GRAD_COMM["dtype"] == "bf16" else None
 
 
 def xavier_init(model):
@@ -133,7 +139,8 @@ def run_ldnn(ctx, args):
                           library_gemms=args.gemms == "library",
                           fuse_head_dgrad=False if args.no_fuse_head_dgrad else None,
                           head_dgrad_mode=args.head_dgrad_mode, fuse_head_fwd=not args.no_fuse_head_fwd,
-                          fuse_head_bwd=not args.no_fuse_head_bwd)
+                          fuse_head_bwd=not args.no_fuse_head_bwd,
+                          comm_dtype=_grad_dtype() if not args.no_shard else None)
     if ctx.distributed:
         dist.broadcast(eng.flat.master, src=0)
         eng.flat.refresh_shadow()
@@ -168,12 +175,14 @@ def run_ldnn(ctx, args):
 
 
 def comm_micro(ctx, eng, iters: int = 10) -> dict:
-    """Standalone RCCL time of each bucket's fp32 reduce-scatter and bf16 all-gather
-    (the sharded engine's two collectives), max over ranks, in microseconds."""
+    """Standalone RCCL time of each bucket's gradient reduce-scatter (in the engine's comm
+    dtype) and bf16 all-gather (the sharded engine's two collectives), max over ranks, in
+    microseconds."""
     out = {}
+    gdt = torch.bfloat16 if getattr(eng, "comm_bf16", False) else torch.float32
     for i, (b, e, _) in enumerate(eng.buckets):
-        g = torch.empty(e - b, dtype=torch.float32, device=ctx.device)
-        gs = torch.empty((e - b) // ctx.world_size, dtype=torch.float32, device=ctx.device)
+        g = torch.empty(e - b, dtype=gdt, device=ctx.device)
+        gs = torch.empty((e - b) // ctx.world_size, dtype=gdt, device=ctx.device)
         w = torch.empty(e - b, dtype=torch.bfloat16, device=ctx.device)
         ws = torch.empty((e - b) // ctx.world_size, dtype=torch.bfloat16, device=ctx.device)
         res = []
@@ -192,7 +201,8 @@ def comm_micro(ctx, eng, iters: int = 10) -> dict:
             t = torch.tensor([(time.perf_counter() - t0) / iters * 1e6], device=ctx.device, dtype=torch.float64)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             res.append(round(t.item(), 1))
-        out[f"bucket{i}"] = {"mb_fp32": round((e - b) * 4 / 2**20, 2), "reduce_scatter_fp32_us": res[0],
+        out[f"bucket{i}"] = {"mb_fp32": round((e - b) * 4 / 2**20, 2),
+                             f"reduce_scatter_{'bf16' if gdt == torch.bfloat16 else 'fp32'}_us": res[0],
                              "all_gather_bf16_us": res[1]}
     return out
 
@@ -231,7 +241,8 @@ def run_cnn(ctx, name: str, batch: int, steps: int, optimizer: str = "sgd", warm
         m = build_model(name)
         xinit(m)
         ldnn.prepare(m, ctx.device)
-        dp = DataParallel(m, comm, bucket_cap_mb=32.0, shard_optimizer=True) if dp_on else None
+        dp = (DataParallel(m, comm, bucket_cap_mb=32.0, shard_optimizer=True, comm_dtype=_grad_dtype())
+              if dp_on else None)
         # (the optimizer after the wrapper: sharding re-lays the flat buffers out)
         opt = SGD(m.parameters(), lr=0.01, momentum=0.9) if optimizer == "sgd" else Adam(m.parameters(), lr=1e-3)
         net = dp if dp is not None else m
@@ -254,9 +265,9 @@ def run_cnn(ctx, name: str, batch: int, steps: int, optimizer: str = "sgd", warm
            "n_params": sum(p.numel() for p in m.parameters())}
     if ctx.world_size > 1:
         bk = gs.bk
-        rec["grad_sync"] = ("fp32 reduce-scatter per bucket (between backward graph links) + sharded "
-                            f"{optimizer} + bf16 weight all-gather; 1-D params all-reduced")
-        rec["comm_dtype"] = "fp32 gradients / bf16 weights"
+        rec["grad_sync"] = (f"{GRAD_COMM['dtype']} reduce-scatter per bucket (between backward graph links) + "
+                            f"sharded {optimizer} + bf16 weight all-gather; 1-D params all-reduced")
+        rec["comm_dtype"] = f"{GRAD_COMM['dtype']} gradients / bf16 weights"
         rec["oneshot_ipc"] = bool(getattr(comm, "oneshot", None) is not None)
         rec["buckets"] = len(bk.buckets)
         rec["sharded_buckets"] = sum(1 for b in bk.buckets if b["sharded"])
@@ -395,8 +406,12 @@ def main():
                     help="-1 auto (streaming dh kernel for <= 16 classes), 1 fused (h re-read), 2 fused (h in LDS)")
     ap.add_argument("--compare-stock", action="store_true")
     ap.add_argument("--backend", default="auto", help="auto (nccl = RCCL on GPUs) | gloo (testing only)")
+    ap.add_argument("--grad-comm", choices=["bf16", "fp32"], default="bf16",
+                    help="gradient reduce-scatter dtype at N > 1 (bf16: half the xGMI bytes, widened into the "
+                         "fp32 shard of the sharded optimizer)")
     ap.add_argument("--no-configs", action="store_true", help="skip the LeNet-5 / ResNet-18 config timings")
     args = ap.parse_args()
+    GRAD_COMM["dtype"] = args.grad_comm
 
     if args.gpus > 1 and D.launch_env()[1] == 1:
         sys.exit(self_launch(args))
@@ -452,7 +467,9 @@ def main():
             "comm": comm_info,
             "grad_sync": ("none (1 GPU)" if n == 1 else
                           f"fp32 {comm} all-reduce, bucketed, overlapped" if args.no_shard else
-                          f"fp32 {comm} reduce-scatter (bucketed, overlapped) + sharded SGD + bf16 weight all-gather"),
+                          f"{args.grad_comm} {comm} reduce-scatter (bucketed, overlapped) + sharded SGD (fp32 master) "
+                          "+ bf16 weight all-gather"),
+            "grad_comm_dtype": None if n == 1 else ("fp32" if args.no_shard else args.grad_comm),
         },
     }
     rec["per_gpu_local_ms"] = round(local_s / args.steps * 1e3, 4)

@@ -193,14 +193,15 @@ def main(argv=None):
     if use_engine:   # the engine synchronises its own gradients (per-step DP) or is a plain replica
         D.broadcast_module(model)
         flat.refresh_shadow()
-    elif args.sync_every == "step" and world > 1:
+    elif (args.sync_every == "step" and world > 1
+          and not (args.topology != "allreduce" and args.grad_comm_dtype != "fp32")):
+        # (per-step gossip buckets travel in fp32: with --grad_comm_dtype bf16 a gossip run
+        # takes the per-step Aggregator path below instead, as it did before round 5)
         weighted = args.aggregation_type == "weighted"
         gossip = {"allreduce": 0, "ring": 1, "double_ring": 2}[args.topology]
         if args.shard_optimizer == "on" and (weighted or gossip):
             raise SystemExit("--shard_optimizer on needs --topology allreduce --aggregation_type equal (the "
                              "weighted mix and gossip give every rank its own update)")
-        if gossip and args.grad_comm_dtype != "fp32":
-            raise SystemExit("per-step gossip exchanges fp32 gradient buckets (--grad_comm_dtype fp32)")
         shard = not weighted and not gossip and (args.shard_optimizer == "on" or (args.shard_optimizer == "auto"
                                                                                    and dev.type == "cuda"))
         dp = DataParallel(model, comm, bucket_cap_mb=args.bucket_mb,

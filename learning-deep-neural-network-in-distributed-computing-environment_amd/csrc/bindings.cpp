@@ -369,6 +369,13 @@ void cast_f32_bf16(const at::Tensor& x, const at::Tensor& y) {
   check(ldnn::cast_f32_bf16(x.data_ptr<float>(), bf16_mut(y), x.numel(), cur_stream(x)), "cast_f32_bf16");
 }
 
+void cast_bf16_f32(const at::Tensor& x, const at::Tensor& y) {
+  check_dev(x, at::kBFloat16, "x");
+  check_dev(y, at::kFloat, "y");
+  TORCH_CHECK(x.is_contiguous() && y.is_contiguous() && x.numel() == y.numel(), "cast: bad tensors");
+  check(ldnn::cast_bf16_f32(bf16_ptr(x), y.data_ptr<float>(), x.numel(), cur_stream(x)), "cast_bf16_f32");
+}
+
 void mix3(const at::Tensor& out, const at::Tensor& x, const c10::optional<at::Tensor>& y1,
           const c10::optional<at::Tensor>& y2, double a, double b, double c,
           const c10::optional<at::Tensor>& shadow) {
@@ -472,7 +479,8 @@ ldnn::GradZero grad_zero(const std::vector<std::pair<int64_t, int64_t>>& r, int6
 void sgd_step(const at::Tensor& param, const at::Tensor& grad, const at::Tensor& mom,
               const c10::optional<at::Tensor>& shadow, const at::Tensor& hp, double grad_scale, double momentum,
               double dampening, double weight_decay, bool nesterov, bool first_step,
-              const std::vector<std::pair<int64_t, int64_t>>& zero_ranges) {
+              const std::vector<std::pair<int64_t, int64_t>>& zero_ranges, int64_t t_begin,
+              const c10::optional<at::Tensor>& t_out) {
   check_dev(param, at::kFloat, "param");
   check_dev(grad, at::kFloat, "grad");
   check_dev(hp, at::kFloat, "hp");
@@ -492,8 +500,21 @@ void sgd_step(const at::Tensor& param, const at::Tensor& grad, const at::Tensor&
   }
   ldnn::SgdParams sp{(float)momentum, (float)dampening, (float)weight_decay, nesterov ? 1 : 0, first_step ? 1 : 0,
                      grad_zero(zero_ranges, n)};
+  ldnn::ShadowT tr{};
+  if (t_out.has_value()) {
+    // t_out [cols][rows] bf16: the transposed shadow of the [rows][cols] matrix at element t_begin
+    check_dev(*t_out, at::kBFloat16, "t_out");
+    TORCH_CHECK(t_out->dim() == 2 && t_out->is_contiguous() && t_begin >= 0 &&
+                    t_begin + t_out->numel() <= n && t_out->size(0) % 64 == 0 && t_out->size(1) % 64 == 0 &&
+                    t_begin % 4 == 0 && aligned16(t_out->data_ptr()),
+                "sgd: t_out must be a dense [cols][rows] bf16 tensor (multiples of 64) inside the range");
+    tr.begin = t_begin;
+    tr.rows = (int)t_out->size(1);
+    tr.cols = (int)t_out->size(0);
+    tr.out = bf16_mut(*t_out);
+  }
   check(ldnn::sgd_step(param.data_ptr<float>(), grad.data_ptr<float>(), mp, sh, hp.data_ptr<float>(),
-                       (float)grad_scale, sp, n, cur_stream(param)),
+                       (float)grad_scale, sp, n, cur_stream(param), t_out.has_value() ? &tr : nullptr),
         "sgd_step");
 }
 
@@ -1866,6 +1887,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("act_bwd_colsum", &act_bwd_colsum, py::arg("dy"), py::arg("y"), py::arg("dx"), py::arg("out"),
         py::arg("act"), py::arg("accumulate") = true);
   m.def("cast_f32_bf16", &cast_f32_bf16);
+  m.def("cast_bf16_f32", &cast_bf16_f32);
   m.def("mix3", &mix3, py::arg("out"), py::arg("x"), py::arg("y1") = py::none(), py::arg("y2") = py::none(),
         py::arg("a") = 1.0, py::arg("b") = 0.0, py::arg("c") = 0.0, py::arg("shadow") = py::none());
   m.def("softmax_xent", &softmax_xent, py::arg("logits"), py::arg("labels"), py::arg("dlogits"),
@@ -1911,7 +1933,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("sgd_step", &sgd_step, py::arg("param"), py::arg("grad"), py::arg("mom"), py::arg("shadow"),
         py::arg("hp"), py::arg("grad_scale"), py::arg("momentum"), py::arg("dampening"),
         py::arg("weight_decay"), py::arg("nesterov"), py::arg("first_step"),
-        py::arg("zero_ranges") = std::vector<std::pair<int64_t, int64_t>>{});
+        py::arg("zero_ranges") = std::vector<std::pair<int64_t, int64_t>>{}, py::arg("t_begin") = 0,
+        py::arg("t_out") = py::none());
   m.def("adam_step", &adam_step, py::arg("param"), py::arg("grad"), py::arg("m"), py::arg("v"),
         py::arg("shadow"), py::arg("hp"), py::arg("grad_scale"), py::arg("beta1"), py::arg("beta2"),
         py::arg("eps"), py::arg("weight_decay"), py::arg("decoupled"),

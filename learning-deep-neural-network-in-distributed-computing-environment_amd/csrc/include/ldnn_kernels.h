@@ -367,8 +367,15 @@ struct SgdParams {
 };
 // grid cap of the optimizer kernels launched from now on (0 = default 2048 blocks)
 void set_opt_max_blocks(int n);
+// one [rows][cols] matrix of the range (at element `begin`) whose bf16 shadow is also written
+// transposed into `out` ([cols][rows]); rows, cols multiples of 64
+struct ShadowT {
+  int64_t begin = 0;
+  int rows = 0, cols = 0;
+  uint16_t* out = nullptr;
+};
 hipError_t sgd_step(float* param, float* grad, float* mom, uint16_t* shadow, const float* hp,
-                    float grad_scale, SgdParams sp, int64_t n, hipStream_t s);
+                    float grad_scale, SgdParams sp, int64_t n, hipStream_t s, const ShadowT* tr = nullptr);
 struct AdamParams {
   float beta1, beta2, eps, weight_decay;
   int decoupled;  // AdamW

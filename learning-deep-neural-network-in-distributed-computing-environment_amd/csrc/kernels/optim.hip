@@ -51,30 +51,80 @@ __device__ __forceinline__ void clear4(const GradZero& z, float* grad, int64_t i
   }
 }
 
+// one float4 of the SGD(-momentum) update: master, momentum, gradient clear; returns the
+// new bf16 shadow values
 template <bool NT>
+__device__ __forceinline__ u16x4 sgd4(float* __restrict__ param, float* __restrict__ grad, float* __restrict__ mom,
+                                      float lr, float grad_scale, const SgdParams& sp, int64_t i) {
+  floatx4 p = ld4<NT>(param, i);
+  floatx4 g = ld4<NT>(grad, i) * grad_scale;
+  clear4(sp.zero, grad, i);
+  if (sp.weight_decay != 0.f) g += sp.weight_decay * p;
+  if (sp.momentum != 0.f) {
+    floatx4 b;
+    if (sp.first_step) b = g;
+    else b = sp.momentum * ld4<NT>(mom, i) + (1.f - sp.dampening) * g;
+    st4<NT>(mom, i, b);
+    g = sp.nesterov ? g + sp.momentum * b : b;
+  }
+  p -= lr * g;
+  st4<NT>(param, i, p);
+  return u16x4{f2bf(p[0]), f2bf(p[1]), f2bf(p[2]), f2bf(p[3])};
+}
+
+// TR: the flat range holds one [rows][cols] weight matrix at element `tr.begin` whose bf16
+// shadow is also kept TRANSPOSED (tr.out = [cols][rows]; the MLP dgrad reads it so both
+// GEMM operands are k-contiguous).  The first (rows / 64) x (cols / 64) workgroups update
+// that matrix one 64 x 64 tile each and write the transposed tile through LDS; the rest
+// stride over the remaining elements -- one launch instead of the update plus a
+// transpose pass that re-reads the 32 MB shadow.
+template <bool NT, bool TR>
 __global__ void sgd_kernel(float* __restrict__ param, float* __restrict__ grad, float* __restrict__ mom,
                            bf16_t* __restrict__ shadow, const float* __restrict__ hp, float grad_scale,
-                           SgdParams sp, int64_t n) {
+                           SgdParams sp, int64_t n, ShadowT tr) {
   const float lr = hp[0];
   const int64_t nv = n / 4;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nv; i += stride) {
-    floatx4 p = ld4<NT>(param, i);
-    floatx4 g = ld4<NT>(grad, i) * grad_scale;
-    clear4(sp.zero, grad, i);
-    if (sp.weight_decay != 0.f) g += sp.weight_decay * p;
-    if (sp.momentum != 0.f) {
-      floatx4 b;
-      if (sp.first_step) b = g;
-      else b = sp.momentum * ld4<NT>(mom, i) + (1.f - sp.dampening) * g;
-      st4<NT>(mom, i, b);
-      g = sp.nesterov ? g + sp.momentum * b : b;
+  int64_t bid = blockIdx.x, nblk = gridDim.x, skip_b = 0, skip_n = 0;
+  if constexpr (TR) {
+    __shared__ uint16_t t[64][66];
+    const int tiles_c = tr.cols >> 6;
+    const int ntiles = (tr.rows >> 6) * tiles_c;
+    if (blockIdx.x < (unsigned)ntiles) {
+      const int r0 = (blockIdx.x / tiles_c) * 64, c0 = (blockIdx.x % tiles_c) * 64;
+      const int c4 = threadIdx.x & 15, rg = threadIdx.x >> 4;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int r = rg * 4 + k;
+        const int64_t i = (tr.begin + (int64_t)(r0 + r) * tr.cols + c0 + c4 * 4) >> 2;
+        const u16x4 b = sgd4<NT>(param, grad, mom, lr, grad_scale, sp, i);
+        if (shadow) reinterpret_cast<u16x4*>(shadow)[i] = b;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) t[r][c4 * 4 + q] = b[q];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int ch = threadIdx.x + h * 256;
+        const int c = ch >> 3, r8 = (ch & 7) * 8;
+        u16x8 v;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = t[r8 + e][c];
+        *reinterpret_cast<u16x8*>(tr.out + (size_t)(c0 + c) * tr.rows + r0 + r8) = v;
+      }
+      return;
     }
-    p -= lr * g;
-    st4<NT>(param, i, p);
-    if (shadow) reinterpret_cast<u16x4*>(shadow)[i] = u16x4{f2bf(p[0]), f2bf(p[1]), f2bf(p[2]), f2bf(p[3])};
+    bid -= ntiles;
+    nblk -= ntiles;
+    skip_b = tr.begin >> 2;
+    skip_n = ((int64_t)tr.rows * tr.cols) >> 2;
   }
-  for (int64_t i = nv * 4 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride) {
+  const int64_t stride = nblk * blockDim.x;
+  for (int64_t j = bid * (int64_t)blockDim.x + threadIdx.x; j < nv - skip_n; j += stride) {
+    const int64_t i = (TR && j >= skip_b) ? j + skip_n : j;
+    const u16x4 b = sgd4<NT>(param, grad, mom, lr, grad_scale, sp, i);
+    if (shadow) reinterpret_cast<u16x4*>(shadow)[i] = b;
+  }
+  for (int64_t i = nv * 4 + bid * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride) {
     float p = param[i];
     float g = grad[i] * grad_scale;
     if (in_zero(sp.zero, i)) grad[i] = 0.f;
@@ -164,10 +214,21 @@ int opt_nt_env() {
 void set_opt_max_blocks(int n) { g_opt_max_blocks = n > 0 ? n : 2048; }
 
 hipError_t sgd_step(float* param, float* grad, float* mom, uint16_t* shadow, const float* hp,
-                    float grad_scale, SgdParams sp, int64_t n, hipStream_t s) {
+                    float grad_scale, SgdParams sp, int64_t n, hipStream_t s, const ShadowT* tr) {
   if (n <= 0) return hipSuccess;
-  if (opt_nt_env()) sgd_kernel<true><<<grid_for((n + 3) / 4), kBlock, 0, s>>>(param, grad, mom, shadow, hp, grad_scale, sp, n);
-  else sgd_kernel<false><<<grid_for((n + 3) / 4), kBlock, 0, s>>>(param, grad, mom, shadow, hp, grad_scale, sp, n);
+  if (tr != nullptr && tr->out != nullptr) {
+    // (the tile path needs whole 64 x 64 tiles and 16-B aligned transposed rows)
+    if (tr->rows <= 0 || tr->cols <= 0 || tr->rows % 64 || tr->cols % 64 || tr->begin % 4 || tr->begin < 0 ||
+        tr->begin + (int64_t)tr->rows * tr->cols > n || ((uintptr_t)tr->out & 15))
+      return hipErrorInvalidValue;
+    const int64_t ntiles = (int64_t)(tr->rows / 64) * (tr->cols / 64);
+    const int64_t rest = (n - (int64_t)tr->rows * tr->cols + 3) / 4;
+    const int grid = (int)ntiles + grid_for(rest);
+    sgd_kernel<true, true><<<grid, kBlock, 0, s>>>(param, grad, mom, shadow, hp, grad_scale, sp, n, *tr);
+    return hipGetLastError();
+  }
+  if (opt_nt_env()) sgd_kernel<true, false><<<grid_for((n + 3) / 4), kBlock, 0, s>>>(param, grad, mom, shadow, hp, grad_scale, sp, n, ShadowT{});
+  else sgd_kernel<false, false><<<grid_for((n + 3) / 4), kBlock, 0, s>>>(param, grad, mom, shadow, hp, grad_scale, sp, n, ShadowT{});
   return hipGetLastError();
 }
 

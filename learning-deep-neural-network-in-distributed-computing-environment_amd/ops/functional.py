@@ -23,6 +23,28 @@ from . import _ext
 ACTS = {"none": None, "relu": 0, "sigmoid": 1}
 
 
+def _fire_pre_hooks(mods, x) -> bool:
+    """A fused launch that stands in for the __call__ of several modules (conv2d_pair,
+    gap_linear) must still run their forward pre-hooks: the sharded DP step cuts its graph
+    chain there and waits for the bucket's weight all-gather (GraphedDPStep._on_forward).
+    Fires every module's pre-hooks with (x,) and returns True, or returns False without
+    firing any when a module carries hooks a fused launch cannot honour (post-forward
+    hooks, kwargs pre-hooks, global module hooks): the caller then runs the module calls."""
+    from torch.nn.modules import module as _m
+
+    if _m._global_forward_pre_hooks or _m._global_forward_hooks:
+        return False
+    for mod in mods:
+        if mod._forward_hooks or getattr(mod, "_forward_pre_hooks_with_kwargs", None):
+            return False
+    for mod in mods:
+        for hook in tuple(mod._forward_pre_hooks.values()):
+            if hook(mod, (x,)) is not None:
+                raise RuntimeError(f"a forward pre-hook of {type(mod).__name__} rewrote its input: "
+                                   "not supported on the fused launch")
+    return True
+
+
 def _to_bf16(x: torch.Tensor) -> torch.Tensor:
     if x.dtype == torch.bfloat16:
         return x if x.stride(-1) == 1 else x.contiguous()
@@ -505,7 +527,7 @@ def conv2d_pair(x, xt, mod0, mod1):
                       and isinstance(m.padding, tuple) and m.padding[0] == m.padding[1]
                       and getattr(m, "activation", None) != "relu" for m in (mod0, mod1))
               and mod0.in_channels == mod1.in_channels)
-        if ok:
+        if ok and _fire_pre_hooks((mod0, mod1), x):
             bn0 = mod0._ldnn_stats_bn if _layers_fuse_bn_stats() else None
             bn1 = mod1._ldnn_stats_bn if _layers_fuse_bn_stats() else None
             y0, y1 = _Conv2dPairNative.apply(x, xt, mod0.weight, mod1.weight, flat,
@@ -1050,7 +1072,8 @@ def gap_linear(x, pool, fc):
             and flat.shadow is not None and getattr(fc, "activation", "none") == "none"):
         N, C, H, W = x.shape
         w = flat.shadow_storage(fc.weight)
-        if w.shape[1] == C and C == fc.in_features and _ext.C().gap_linear_ok(N, H * W, C, fc.out_features):
+        if (w.shape[1] == C and C == fc.in_features and _ext.C().gap_linear_ok(N, H * W, C, fc.out_features)
+                and _fire_pre_hooks((pool, fc), x)):
             return _GapLinearNative.apply(x, fc.weight, fc.bias, flat)
     y = pool(x)
     return fc(y.reshape(y.size(0), -1))

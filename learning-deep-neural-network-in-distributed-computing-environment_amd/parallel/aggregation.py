@@ -38,6 +38,8 @@ TOPOLOGIES = ("allreduce", "ring", "double_ring")
 def _mix(out: torch.Tensor, x: torch.Tensor, y1=None, y2=None, a=1.0, b=0.0, c=0.0, shadow=None):
     if _ext.use_native(out) and out.dtype == torch.float32 and out.is_contiguous():
         _ext.C().mix3(out, x, y1, y2, a, b, c, shadow)
+        if shadow is not None:   # (native write: bump the version readers of derived copies key on)
+            torch.autograd.graph.increment_version(shadow)
         return
     r = a * x
     if y1 is not None:

@@ -49,6 +49,20 @@ from .comm import SUM, Comm, default_comm
 _OPT_ORDER = os.environ.get("LDNN_DP_OPT_ORDER", "ready")
 
 
+def _cast_into(dst: torch.Tensor, src: torch.Tensor):
+    """dst <- src across fp32 / bf16 (the bf16 gradient stage): the native cast kernels on the
+    GPU (no ATen launch in a captured step), else a plain copy."""
+    from ..ops import _ext
+
+    if dst.dtype != src.dtype and dst.is_cuda and _ext.use_native(dst):
+        C = _ext.C()
+        if src.dtype == torch.float32 and dst.dtype == torch.bfloat16:
+            return C.cast_f32_bf16(src, dst)
+        if src.dtype == torch.bfloat16 and dst.dtype == torch.float32:
+            return C.cast_bf16_f32(src, dst)
+    dst.copy_(src)
+
+
 def ensure_flat(module: nn.Module, device=None) -> FlatParams:
     for m in module.modules():
         f = getattr(m, "_ldnn_flat", None)
@@ -236,7 +250,7 @@ class GradBucketer:
             else:
                 self._own[i].copy_(g)
         if self._stage is not None:
-            self._stage[i].copy_(g)
+            _cast_into(self._stage[i], g)
 
     def collective(self, i):
         """Issue bucket i's collective (async): reduce-scatter into this rank's shard
@@ -266,11 +280,11 @@ class GradBucketer:
         if self.buckets[i]["sharded"]:
             lo, hi = self.shard_range(i)
             g = self.flat.grad[lo:hi]
-            g.copy_(self._gshard[i])
+            _cast_into(g, self._gshard[i])
         else:
             g = self.grad_view(i)
             if self._stage is not None:
-                g.copy_(self._stage[i])
+                _cast_into(g, self._stage[i])
         if self._own is not None:
             from .aggregation import _mix
 

@@ -150,14 +150,14 @@ def _timed(fn, steps):
 
 def measure_overlap(model_name: str, batch: int, bucket_mb: float = 32.0, reps: int = 4, steps: int = 20,
                     rounds: int = 3, blocks: int = 16, shard_world: int = 0, optimizer: str = "sgd",
-                    tail_steps: int = 0, gbps: float = 300.0) -> dict:
+                    tail_steps: int = 0, gbps: float = 300.0, comm_dtype: str = "fp32") -> dict:
     """shard_world > 0: the sharded step (reduce-scatter between backward links, sharded
     optimizer, bf16 weight all-gathers waited by the forward links) on a
     ShardProbeComm of that world size; the stand-ins then cover the reduce-scatter
     AND the all-gather bytes of each bucket."""
     if shard_world:
         return _measure_sharded(model_name, batch, bucket_mb, reps, steps, rounds, blocks, shard_world, optimizer,
-                                tail_steps, gbps)
+                                tail_steps, gbps, comm_dtype)
     import ldnn
     from ldnn.data.datasets import SHAPES
     from ldnn.models import CrossEntropyLoss, build_model, dataset_for, xavier_init
@@ -233,7 +233,7 @@ def _opt_order():
 
 
 def _measure_sharded(model_name, batch, bucket_mb, reps, steps, rounds, blocks, world, optimizer, tail_steps=0,
-                     gbps=300.0):
+                     gbps=300.0, comm_dtype="fp32"):
     import ldnn
     from ldnn.data.datasets import SHAPES
     from ldnn.models import CrossEntropyLoss, build_model, dataset_for, xavier_init
@@ -268,7 +268,8 @@ def _measure_sharded(model_name, batch, bucket_mb, reps, steps, rounds, blocks, 
     xavier_init(m)
     ldnn.prepare(m, dev)
     comm = ShardProbeComm(dev, world, reps, blocks, gbps)
-    dp = DataParallel(m, comm, bucket_cap_mb=bucket_mb, broadcast_init=False, shard_optimizer=True)
+    dp = DataParallel(m, comm, bucket_cap_mb=bucket_mb, broadcast_init=False, shard_optimizer=True,
+                      comm_dtype=torch.bfloat16 if comm_dtype == "bf16" else None)
     o = opt_for(m)
     o.zero_grad()
     crit(dp(x), y).backward()
@@ -309,6 +310,7 @@ def _measure_sharded(model_name, batch, bucket_mb, reps, steps, rounds, blocks, 
     hidden = best["single_ms"] + best["standin_alone_ms"] - best["with_standin_ms"]
     _tail(lambda: gd(x, y), tail_steps)
     return {"model": model_name, "batch": batch, "mode": f"sharded (world {world} stand-in)", "optimizer": optimizer,
+            "grad_comm_dtype": comm_dtype,
             "bucket_mb": bucket_mb, "buckets": len(bk.buckets),
             "sharded_buckets": sum(1 for b in bk.buckets if b["sharded"]),
             "bucket_mb_each": [round((b["end"] - b["begin"]) * 4 / 2**20, 2) for b in bk.buckets],
@@ -322,12 +324,13 @@ def _measure_sharded(model_name, batch, bucket_mb, reps, steps, rounds, blocks, 
 
 def measure_mlp_sharded(world: int = 8, batch: int = 16384, hidden: int = 4096, in_features: int = 784,
                         classes: int = 10, bucket_elems: int = 8 << 20, reps: int = 1, blocks: int = 0,
-                        steps: int = 20, rounds: int = 3, tail_steps: int = 0, gbps: float = 300.0) -> dict:
+                        steps: int = 20, rounds: int = 3, tail_steps: int = 0, gbps: float = 300.0,
+                        comm_dtype: str = "bf16") -> dict:
     """The headline engine's sharded data-parallel step (train/static_mlp.py
     StaticMLPEngine at world ``world``, rank 0: bench.py's mlp3 784-4096-4096-10 at
     16384 samples per GPU, SGD momentum) on ONE GPU, every reduce-scatter / all-gather
-    replaced by the stand-in copy of the bytes it moves over xGMI ((N-1)/N of the fp32
-    gradient bucket, resp. of the bf16 weight bucket).  The engine's own schedule runs:
+    replaced by the stand-in copy of the bytes it moves over xGMI ((N-1)/N of the
+    gradient bucket in ``comm_dtype``, resp. of the bf16 weight bucket).  The engine's own schedule runs:
     reduce-scatters issued between the backward's graph segments, shard updates and
     weight all-gathers in forward order, the next step's forward waiting for each
     bucket's gather right before its first GEMM.  Needs a (world-1) RCCL group for the
@@ -359,7 +362,8 @@ def measure_mlp_sharded(world: int = 8, batch: int = 16384, hidden: int = 4096, 
                 torch.nn.init.xavier_uniform_(mod.weight)
                 torch.nn.init.zeros_(mod.bias)
         e = StaticMLPEngine(m, batch, OptimConfig("sgd", lr=0.01, momentum=0.9), device=dev, world_size=w,
-                            bucket_cap_elems=bucket_elems, shard_optimizer=True if w > 1 else None)
+                            bucket_cap_elems=bucket_elems, shard_optimizer=True if w > 1 else None,
+                            comm_dtype=torch.bfloat16 if (w > 1 and comm_dtype == "bf16") else None)
         g = torch.Generator(device=dev).manual_seed(3)
         e.load_batch(torch.randn(batch, in_features, device=dev, generator=g).bfloat16(),
                      torch.randint(0, classes, (batch,), device=dev, generator=g))
@@ -375,9 +379,8 @@ def measure_mlp_sharded(world: int = 8, batch: int = 16384, hidden: int = 4096, 
         v = t.view(-1)[:max(n, 8)]
         return v if v.dtype == torch.float32 else v.view(torch.float32)
 
-    def rs(i):
-        b, e_, _ = eng.buckets[i]
-        return standin(("rs", i), moved(eng.flat.grad[b:e_])) if state["on"] else None
+    def rs(i):   # (the buffer the reduce-scatter reads: the bf16 stage or the fp32 gradient)
+        return standin(("rs", i), moved(eng._rs_buffers(i)[0])) if state["on"] else None
 
     def ag(i):
         b, e_, _ = eng.buckets[i]
@@ -419,6 +422,7 @@ def measure_mlp_sharded(world: int = 8, batch: int = 16384, hidden: int = 4096, 
     eng.sync()
     return {"model": f"mlp3 {in_features}-{hidden}-{hidden}-{classes}", "batch": batch,
             "mode": f"static engine, sharded (world {world} stand-in)", "optimizer": "sgd momentum 0.9",
+            "grad_comm_dtype": comm_dtype,
             "buckets": len(eng.buckets), "bucket_mb_fp32": [round((e_ - b) * 4 / 2**20, 2) for b, e_, _ in eng.buckets],
             "segments": len(eng.segments), "standin_reps": standin.reps, "standin_blocks": standin.blocks,
             "standin_calibration": standin.calibration,
@@ -440,6 +444,8 @@ def main():
                     help="xGMI bus bandwidth the calibrated stand-in moves a collective's bytes at")
     ap.add_argument("--shard", type=int, default=0, help="world size of the sharded-step probe (0 = all-reduce step)")
     ap.add_argument("--optimizer", choices=["sgd", "adam"], default="sgd")
+    ap.add_argument("--grad-comm", choices=["fp32", "bf16"], default="bf16",
+                    help="gradient collective dtype of the sharded step")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--tail-steps", type=int, default=0, help="then this many overlapped steps after an idle gap "
                     "(kernel-trace timelines: scripts/probe_timeline.py)")
@@ -447,11 +453,12 @@ def main():
     if a.model == "mlp3":   # the headline engine (StaticMLPEngine), sharded at world --shard (default 8)
         print(json.dumps(measure_mlp_sharded(a.shard or 8, a.batch if a.batch != 64 else 16384, reps=a.reps,
                                              blocks=a.blocks, steps=a.steps, rounds=a.rounds,
-                                             tail_steps=a.tail_steps, gbps=a.gbps)), flush=True)
+                                             tail_steps=a.tail_steps, gbps=a.gbps, comm_dtype=a.grad_comm)),
+              flush=True)
         return
     print(json.dumps(measure_overlap(a.model, a.batch, a.bucket_mb, a.reps, a.steps, rounds=a.rounds, blocks=a.blocks,
                                      shard_world=a.shard, optimizer=a.optimizer, tail_steps=a.tail_steps,
-                                     gbps=a.gbps)), flush=True)
+                                     gbps=a.gbps, comm_dtype=a.grad_comm)), flush=True)
 
 
 if __name__ == "__main__":

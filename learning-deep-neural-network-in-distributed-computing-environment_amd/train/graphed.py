@@ -76,6 +76,8 @@ def static_input(model, x_example: torch.Tensor):
         xs._ldnn_zpad = True   # the staging pass writes the pad channels' zeros
 
         def stage(xn: torch.Tensor, yn: torch.Tensor, ys: torch.Tensor):
+            if xn.device != buf.device or xn.dtype not in (torch.float32, torch.bfloat16):
+                xn = xn.to(buf.device, torch.float32)   # (a host batch, fp16 / uint8: what copy_ accepted)
             xn = xn if xn.is_contiguous() else xn.contiguous()
             if (yn.is_cuda and yn.is_contiguous() and yn.dtype == ys.dtype and yn.nbytes % 8 == 0
                     and yn.data_ptr() % 8 == 0):   # the labels ride along in the same launch

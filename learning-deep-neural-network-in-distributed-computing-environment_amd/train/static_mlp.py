@@ -99,7 +99,8 @@ class StaticMLPEngine:
                  shard_optimizer: bool | None = None, wgrad_combine: bool = True, library_gemms: bool | None = None,
                  fuse_head_dgrad: bool | None = None, library_dgrad: bool | None = None, head_dgrad_mode: int = -1,
                  relu_masks: bool = True, transposed_dgrad: bool = True, bias_ones_column: bool = True,
-                 fuse_head_fwd: bool = True, fuse_head_bwd: bool = True, grad_mix: tuple | None = None):
+                 fuse_head_fwd: bool = True, fuse_head_bwd: bool = True, grad_mix: tuple | None = None,
+                 comm_dtype: torch.dtype | None = None):
         """``grad_mix`` = (hops, local_weight): per-step gradient exchange other than the
         equal all-reduce (world > 1) -- hops 0 with a weight = the reference's
         self-weighted all-reduce (BAR/communication.py:4-10), hops 1 / 2 = ring /
@@ -108,7 +109,15 @@ class StaticMLPEngine:
         graph segments (grouped send/recv or all-reduce on RCCL's stream) and combined in
         place by the fused mix kernel (K18) before its optimizer segment.  Every rank
         then applies its OWN mixed gradient (decentralised SGD: replicas differ), so
-        these modes run the replicated optimizer."""
+        these modes run the replicated optimizer.
+
+        ``comm_dtype=torch.bfloat16`` (sharded optimizer, world > 1): the gradient buckets are
+        reduce-scattered in bf16 -- (N-1)/N x 2 B per element on xGMI instead of 4.  A plain
+        weight-gradient GEMM writes its bf16 output straight into the bf16 staging buffer
+        (no cast pass); whatever the wgrads leave in fp32 (split-K slabs, the head's atomics,
+        the biases) is cast right before the bucket's collective, and the reduce-scattered
+        bf16 shard is widened into the fp32 shard the fused optimizer reads (fp32 master
+        weights and optimizer state throughout)."""
         from ..models.mlp import MLP
 
         if not isinstance(model, MLP):
@@ -152,6 +161,11 @@ class StaticMLPEngine:
             raise ValueError("grad_mix modes give every rank its own update: no sharded optimizer")
         if self._mix_cfg is not None:
             shard_optimizer = False
+        if comm_dtype not in (None, torch.float32, torch.bfloat16):
+            raise ValueError(f"comm_dtype must be None, torch.float32 or torch.bfloat16, not {comm_dtype}")
+        if comm_dtype == torch.bfloat16 and self._mix_cfg is not None:
+            raise ValueError("grad_mix modes exchange fp32 gradient buckets (comm_dtype bf16 goes with the "
+                             "sharded all-reduce step)")
         self.shard = (self.world > 1) if shard_optimizer is None else bool(shard_optimizer)
         self.distributed = self.world > 1 or self.shard
         # ---- bucket plan: close a bucket after wgrad_l once it holds >= cap elements.
@@ -305,6 +319,20 @@ class StaticMLPEngine:
         for l in range(1, L):
             if transposed_dgrad and not self._lib_dgrad[l] and not (self.use_head and l == L - 1 and self.head_dgrad):
                 self.Wt[l] = torch.zeros(self.W[l].shape[1], self.W[l].shape[0], dtype=bf, device=dev)
+        # One transposed copy is written by the fused SGD itself (its bf16 shadow, transposed
+        # through LDS per 64 x 64 tile: optim.hip sgd_kernel<TR>) instead of a transpose pass
+        # before the dgrad that re-reads the 32 MB shadow: single-process SGD engines (a
+        # sharded optimizer updates only its shard; the all-gathered shadow is transposed).
+        # The largest eligible matrix takes it; Wt is re-derived whenever the shadow was
+        # rewritten outside the step (refresh_shadow / load_state_dict bump its version).
+        self._wt_fused = None
+        if not self.distributed and self.optim.name == "sgd":
+            cand = [l for l in range(1, L) if self.Wt[l] is not None and self.W[l].shape[0] % 64 == 0
+                    and self.W[l].shape[1] % 64 == 0 and self.W[l].stride(0) == self.W[l].shape[1]
+                    and self.W[l].storage_offset() - f.shadow.storage_offset() == f.seg(self.layers[l].weight).offset]
+            if cand:
+                self._wt_fused = max(cand, key=lambda l: self.W[l].numel())
+        self._wt_ver = None
         self._wgrad_splitk, self._wgrad_ws, self._wgrad_slab = [], [], []
         for l, layer in enumerate(self.layers):
             M, N = self.dW[l].shape
@@ -386,6 +414,9 @@ class StaticMLPEngine:
             self.gshard = [torch.zeros((e - b) // self.world, dtype=torch.float32, device=dev)
                            for b, e, _ in self.buckets]
             self._gloo = dist.get_backend(process_group) == "gloo"
+        self.comm_bf16 = comm_dtype == torch.bfloat16 and self.shard
+        if self.comm_bf16:
+            self._plan_bf16_comm()
         # fuse_head_bwd: the head's dgrad and wgrad in one pass over h_{L-1}, both on the MFMA
         # pipe (head.hip head_bwd; the wgrad accumulates into the gradient the optimizer cleared)
         self._fuse_head_bwd = bool(fuse_head_bwd and self._head_part is not None and L >= 2
@@ -393,6 +424,43 @@ class StaticMLPEngine:
                                    and self.layers[L - 1].in_features % 64 == 0 and self._wgrad_splitk[L - 1] > 1)
         self._build_segments()
         self._slots[0]["segs"] = (self.segments, self.opt_segments)
+
+    def _plan_bf16_comm(self):
+        """bf16 gradient reduce-scatter: the bf16 staging buffer (the flat gradient layout),
+        per bucket its bf16 shard, the wgrads that write bf16 directly and, per bucket, the
+        fp32 sub-ranges cast right before its collective."""
+        f, L, bf, dev = self.flat, len(self.layers), torch.bfloat16, self.device
+        self.gbf = torch.zeros(f.numel, dtype=bf, device=dev)
+        self.gshard_bf = [torch.zeros((e - b) // self.world, dtype=bf, device=dev) for b, e, _ in self.buckets]
+        self.dWb = [None] * L
+        for l in range(L):   # plain (unsplit, overwriting) GEMM wgrads: bf16 epilogue, no cast pass
+            if (not (self.use_head and l == L - 1) and not self._lib_wgrad[l] and self._wgrad_slab[l] is None
+                    and self._wgrad_ws[l] is None and self._wgrad_splitk[l] <= 1):
+                d = self.dW[l]
+                self.dWb[l] = torch.as_strided(self.gbf, d.shape, d.stride(),
+                                               d.storage_offset() - f.grad.storage_offset())
+        self._bf16_cast = []
+        for b, e, _ in self.buckets:
+            direct = sorted((sg.offset, sg.offset + sg.storage_numel)
+                            for sg in (f.seg(self.layers[l].weight) for l in range(L) if self.dWb[l] is not None)
+                            if b <= sg.offset < e)
+            ranges, cur = [], b
+            for lo, hi in direct:
+                if lo > cur:
+                    ranges.append((cur, lo))
+                cur = max(cur, hi)
+            if cur < e:
+                ranges.append((cur, e))
+            self._bf16_cast.append(ranges)
+
+    def _cast_bucket(self, bi, whole: bool = False):
+        """Stage bucket bi's fp32 gradient ranges into the bf16 buffer (bf16 comm)."""
+        b, e, _ = self.buckets[bi]
+        for lo, hi in ([(b, e)] if whole else self._bf16_cast[bi]):
+            self.C.cast_f32_bf16(self.flat.grad[lo:hi], self.gbf[lo:hi])
+
+    def _widen_shard(self, i):
+        self.C.cast_bf16_f32(self.gshard_bf[i], self.gshard[i])
 
     # ------------------------------------------------------------------ kernels
     def _forward(self, train: bool = False):
@@ -449,6 +517,8 @@ class StaticMLPEngine:
             self.C.gemm(self.dz[l + 1], self.h[l], self.dW[l], False, False, tile=tile, splitk=sk, ws=ws, cnt=cnt)
         elif sk > 1:   # accumulates into the grad the previous optimizer launch cleared
             self.C.gemm(self.dz[l + 1], self.h[l], self.dW[l], False, False, beta=1.0, tile=128, splitk=sk)
+        elif self.comm_bf16 and self.dWb[l] is not None:   # bf16 comm: straight into the bf16 stage
+            self.C.gemm(self.dz[l + 1], self.h[l], self.dWb[l], False, False)
         else:
             self.C.gemm(self.dz[l + 1], self.h[l], self.dW[l], False, False)
 
@@ -461,7 +531,8 @@ class StaticMLPEngine:
         db = None if (l == 1 and self._db0_from_wgrad) else self.db[l - 1]
         W, w_kc = self.W[l], False
         if self.Wt[l] is not None:
-            self.C.transpose_bf16(self.W[l], self.Wt[l])
+            if l != self._wt_fused:   # (else the previous SGD step wrote it)
+                self.C.transpose_bf16(self.W[l], self.Wt[l])
             W, w_kc = self.Wt[l], True
         if self.mask[l] is not None:
             self.C.gemm(self.dz[l + 1], W, self.dz[l], True, w_kc, self.C.EPI_DRELU, dbias=db, mask_in=self.mask[l])
@@ -471,6 +542,15 @@ class StaticMLPEngine:
             return
         self.C.gemm(self.dz[l + 1], self.W[l], self.dz[l], True, False, self._dgrad_epi[l], aux=self.h[l],
                     dbias=self.db[l - 1])
+
+    def _sync_wt(self):
+        """Re-derive the SGD-maintained transposed weight if the shadow was rewritten outside
+        the step (first step, refresh_shadow, load_state_dict: an ATen write bumps its version;
+        the native kernels' writes do not)."""
+        lf = self._wt_fused
+        if lf is not None and self._wt_ver != self.flat.shadow._version:
+            self.C.transpose_bf16(self.W[lf], self.Wt[lf])
+            self._wt_ver = self.flat.shadow._version
 
     def _shard_range(self, i):
         b, e, _ = self.buckets[i]
@@ -484,8 +564,14 @@ class StaticMLPEngine:
         zr = [(max(zb, b) - b, min(ze, e) - b) for zb, ze in self._opt_zero if zb < e and ze > b]
         if o.name == "sgd":
             mom = self.mom[b:e] if self.mom is not None else p
+            tk = {}
+            lf = self._wt_fused
+            if lf is not None and shadow is None:
+                off = self.flat.seg(self.layers[lf].weight).offset
+                if b <= off and off + self.Wt[lf].numel() <= e:
+                    tk = dict(t_begin=off - b, t_out=self.Wt[lf])
             C.sgd_step(p, g, mom, sh, self.hp, self._grad_scale, o.momentum, o.dampening, o.weight_decay,
-                       o.nesterov, False, zero_ranges=zr)
+                       o.nesterov, False, zero_ranges=zr, **tk)
         else:
             C.adam_step(p, g, self.exp_avg[b:e], self.exp_avg_sq[b:e], sh, self.hp, self._grad_scale,
                         o.betas[0], o.betas[1], o.eps, o.weight_decay, o.name == "adamw", zero_ranges=zr)
@@ -510,11 +596,15 @@ class StaticMLPEngine:
             wg._ldnn_wgrad = l
             pieces[-1].append(wg)
             if l in triggers:
+                if self.comm_bf16:
+                    pieces[-1].append(lambda i=triggers[l]: self._cast_bucket(i))
                 self._cut_buckets.append(triggers[l])
                 pieces.append([])
             if l > 0 and not (self.head_dgrad and l == L - 1):   # (else done by the head kernel)
                 pieces[-1].append(lambda l=l: self._dgrad(l))
         self._cut_buckets.append(len(self.buckets) - 1)
+        if self.comm_bf16:
+            pieces[-1].append(lambda: self._cast_bucket(len(self.buckets) - 1))
 
         def run(fns):
             def f():
@@ -573,8 +663,11 @@ class StaticMLPEngine:
         self._cut_after = [None] * (len(seg_fns) - 1) + list(self._cut_buckets)
         assert len(self._cut_after) == len(all_pieces)
         self.segments = [_Segment(run(p), self.use_graphs) for p in all_pieces]
-        self.opt_segments = [_Segment(run([lambda i=i: self._opt(*self._shard_range(i), grad=self.gshard[i])]),
-                                      self.use_graphs) for i in range(len(self.buckets))]
+        def opt(i):
+            if self.comm_bf16:
+                self._widen_shard(i)
+            self._opt(*self._shard_range(i), grad=self.gshard[i])
+        self.opt_segments = [_Segment(run([lambda i=i: opt(i)]), self.use_graphs) for i in range(len(self.buckets))]
 
     def _forward_layer(self, l, train: bool = False):
         C = self.C
@@ -652,6 +745,7 @@ class StaticMLPEngine:
         from ..models.layers import CrossEntropyLoss
 
         f = self.flat
+        self._sync_wt()
         f.grad.zero_()   # the engine's wgrads overwrite: their ranges hold the last step's values
         f._stale.clear()
         with torch.enable_grad():
@@ -701,6 +795,9 @@ class StaticMLPEngine:
             f.finalize_grads()
         if self._mix_cfg is None:   # (gossip / weighted modes: each rank keeps its own gradient's scale)
             f.grad.mul_(n * self.world / n_tot)
+        if self.comm_bf16:   # (autograd wrote every gradient in fp32)
+            for bi in range(len(self.buckets)):
+                self._cast_bucket(bi, whole=True)
         capturing = any(s.will_capture for s in self.opt_segments)
         if self.shard:
             works = []
@@ -813,15 +910,23 @@ class StaticMLPEngine:
         return g
 
     # ------------------------------------------------------------ collectives
-    def _reduce_scatter(self, i):
+    def _rs_buffers(self, i):
+        """(input, output) of bucket i's reduce-scatter: bf16 stage / bf16 shard, or fp32."""
         b, e, _ = self.buckets[i]
+        if self.comm_bf16:
+            return self.gbf[b:e], self.gshard_bf[i]
+        return self.flat.grad[b:e], self.gshard[i]
+
+    def _reduce_scatter(self, i):
+        src, out = self._rs_buffers(i)
         if self._gloo:   # gloo has no device reduce-scatter: all-reduce, keep this rank's slice
-            w = dist.all_reduce(self.flat.grad[b:e], group=self.pg, async_op=True)
+            w = dist.all_reduce(src, group=self.pg, async_op=True)
             w.wait()
             lo, hi = self._shard_range(i)
-            self.gshard[i].copy_(self.flat.grad[lo:hi])
+            b = self.buckets[i][0]
+            out.copy_(src[lo - b:hi - b])
             return None
-        return dist.reduce_scatter_tensor(self.gshard[i], self.flat.grad[b:e], group=self.pg, async_op=True)
+        return dist.reduce_scatter_tensor(out, src, group=self.pg, async_op=True)
 
     def _all_gather(self, i):
         b, e, _ = self.buckets[i]
@@ -913,14 +1018,18 @@ class StaticMLPEngine:
         for w in pend.values():
             if w is not None:
                 w.wait()
-        # shard updates + weight all-gathers in FORWARD order (the bucket holding W_0 and
-        # the biases first): the next step's first GEMM waits only for that one
-        for bi, w in sorted(works, key=lambda t: -t[0]):
+        # shard updates in reduce-scatter ISSUE order: the deep buckets (reduced long ago)
+        # update while the last bucket's reduce-scatter -- W_0's, fed by the backward's
+        # last kernel -- is still on the wire; each update waits only for its own bucket.
+        # The weight all-gathers then go out in FORWARD order (the bucket holding W_0 and
+        # the biases first): the next step's first GEMM waits only for that one.
+        for bi, w in works:
             if w is not None:
                 w.wait()
             self.opt_segments[bi]()
             if bi == self._bias_bucket:
                 self._broadcast_biases(bi, capturing)
+        for bi, _ in sorted(works, key=lambda t: -t[0]):
             g = self._all_gather(bi)
             if capturing and g is not None:
                 g.wait()
@@ -934,6 +1043,7 @@ class StaticMLPEngine:
             self._use_slot(slot)
         self._master_whole = False
         if not self.distributed:
+            self._sync_wt()
             self.segments[0]()
             return
         if self.shard:

@@ -201,6 +201,9 @@ class FlatParams:
 
         if _ext.use_native(self.master):
             _ext.C().cast_f32_bf16(self.master, self.shadow)
+            # (a native write leaves the version counter alone: bump it, readers that keep
+            # derived copies of the shadow -- StaticMLPEngine's transposed W -- key on it)
+            torch.autograd.graph.increment_version(self.shadow)
         else:
             self.shadow.copy_(self.master)
 

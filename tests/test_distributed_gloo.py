@@ -155,6 +155,21 @@ def test_cli_two_ranks_end_to_end(tmp_path):
     assert len(list((tmp_path / "ckpt").glob("*.pt"))) >= 2  # per-rank checkpoints for gossip
 
 
+@pytest.mark.slow
+def test_cli_step_gossip_with_bf16_flag_runs_the_aggregator_path(tmp_path):
+    """--sync_every step --topology ring --grad_comm_dtype bf16: gossip buckets are
+    fp32-only, so the run takes the per-step Aggregator path instead of exiting."""
+    port = _port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+           "--master-port", str(port), os.path.join(ROOT, "train.py"), "--model", "mlp2", "--dataset", "mnist",
+           "--n_train", "600", "--n_test", "100", "--epochs_global", "1", "--epochs_local", "1", "--device", "cpu",
+           "--quiet", "--out_dir", str(tmp_path), "--plots", "", "--topology", "ring", "--sync_every", "step",
+           "--grad_comm_dtype", "bf16"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert (tmp_path / "histories.json").exists()
+
+
 def test_mpirun_style_env_bootstrap():
     """`mpirun -np N python train.py` (BR/main.py:15-17) sets OMPI_COMM_WORLD_* / PMI_*,
     not RANK / WORLD_SIZE: setup() must still form the process group (no mpi4py)."""

@@ -213,3 +213,55 @@ def test_eager_fallback_and_replay_record_the_same_schedule():
         digests.append(c.schedule_digest())
     torch.cuda.synchronize()
     assert digests[0] == digests[1] and digests[0][0] == len(dp.bucketer.buckets), digests
+
+
+@pytest.mark.parametrize("name", ["resnet18", "enhanced_cnn"])
+def test_fused_launches_fire_every_module_pre_hook(name):
+    """conv2d_pair (a downsampling block's 3x3 + 1x1 shortcut in one launch) and gap_linear (pool +
+    fc) stand in for several module calls: each module's forward pre-hook must still fire -- the
+    sharded DP step cuts its graph chain there and waits for that bucket's weight all-gather
+    (the shortcut's weights sat in bucket 0 of ResNet-18 and were read unwaited)."""
+    (m,) = _models(name, 1)
+    calls = {}
+
+    def sharded(mod):   # (the sharded buckets hold the >= 2-D weights; 1-D ones are read from the
+        # replicated fp32 master tail, which no all-gather writes)
+        return any(p.dim() >= 2 for p in mod.parameters(recurse=False))
+
+    for mod in m.modules():
+        if sharded(mod):
+            mod.register_forward_pre_hook(lambda mod, args: calls.__setitem__(id(mod), calls.get(id(mod), 0) + 1))
+    shape = (8, 3, 224, 224) if name == "resnet18" else (8, 3, 32, 32)
+    x = torch.randn(*shape, device="cuda").bfloat16()
+    with torch.no_grad():
+        m(x)
+    owners = [mod for mod in m.modules() if sharded(mod)]
+    missed = [type(mod).__name__ for mod in owners if calls.get(id(mod), 0) != 1]
+    assert not missed, missed
+
+
+def test_sharded_chain_waits_for_every_sharded_bucket_before_the_optimizer_reads():
+    """With the shard layout of a world-8 stand-in, every sharded bucket holding a weight the
+    forward reads is waited for by some forward link of GraphedDPStep (the first reader's hook)."""
+    from ldnn.parallel.overlap_probe import ShardProbeComm
+
+    (m,) = _models("resnet18", 1)
+    comm = ShardProbeComm(torch.device("cuda"), world=8, reps=1, blocks=4)
+    dp = DataParallel(m, comm, bucket_cap_mb=32.0, broadcast_init=False, shard_optimizer=True)
+    opt = SGD(m.parameters(), lr=0.01, momentum=0.9)
+    crit = CrossEntropyLoss()
+    x = torch.randn(8, 3, 224, 224, device="cuda").bfloat16()
+    y = torch.randint(0, 1000, (8,), device="cuda")
+    opt.zero_grad()
+    crit(dp(x), y).backward()
+    dp.finish_gradient_sync()
+    opt.step()
+    dp.wait_gathers()
+    gd = GraphedDPStep(dp, crit, opt, x, y)
+    waited = {b for w in gd.waits for b in w}
+    sharded = {i for i, b in enumerate(dp.bucketer.buckets) if b["sharded"]}
+    assert sharded and sharded <= waited, (sharded, waited)
+    # the first link that reads the shortcut conv's weights waits for their bucket: the
+    # downsampling blocks' 1x1 convs are read by the paired launch, after their hooks fired
+    gd(x, y)
+    torch.cuda.synchronize()

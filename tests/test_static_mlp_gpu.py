@@ -74,7 +74,18 @@ def test_graph_replay_matches_eager_with_splitk():
 
 @pytest.mark.parametrize("nproc,extra", [(2, []), (3, []), (2, ["--tail", "2,0"]), (3, ["--tail", "5,256,0"]),
                                          (2, ["--tail", "7,3", "--optimizer", "adam"]),
-                                         (2, ["--tail", "7,3", "--shard", "0"])])
+                                         (2, ["--tail", "7,3", "--shard", "0"]),
+                                         # bf16 gradient reduce-scatter: 20 steps of the
+                                         # headline's bucket layout (W2+W1 | W0+biases) within the same
+                                         # 2e-2 x max|param| (+1e-3) of the fp32 single-rank reference
+                                         (3, ["--comm-dtype", "bf16", "--steps", "20", "--hidden", "4096",
+                                              "--cap", str(8 << 20)]),
+                                         (2, ["--comm-dtype", "bf16", "--tail", "7,3"]),
+                                         # Adam divides by sqrt(v): a near-zero gradient element whose bf16
+                                         # sum flips sign moves by 2 lr, so the bound is looser (measured
+                                         # 0.115 x max|param| after 7 steps + tail at lr 1e-3)
+                                         (2, ["--comm-dtype", "bf16", "--tail", "7,3", "--optimizer", "adam",
+                                              "--tol", "0.2"])])
 def test_multirank_static_engine_gloo_two_ranks_one_gpu(nproc, extra):
     """The bucketed multi-rank step (sharded optimizer: reduce-scatter between graph
     segments, shard update, weight all-gather, fp32 bias refresh from the shard
