@@ -45,37 +45,17 @@ struct RedGeo {
   int lanes, rl, gx, gy, rpb;
 };
 
-int env_int_or(const char* name, int dflt) {
-  const char* e = std::getenv(name);
-  return e ? std::atoi(e) : dflt;
-}
+// reduce geometry: total blocks and rows per row lane of the reduce kernels; 512 x 8 measured
+// best with 8 accumulator copies (profiles/cnn_bn_reduce_r2.jsonl)
+constexpr int kBnRedBlocks = 512, kBnRedRows = 8;
+// rows per row lane of the apply passes: 1 = the most blocks, one row per thread -- measured on
+// MI355X (profiles/r3/bn_apply_rows_ab_r3.jsonl, alternated) EnhancedCNN b64 2.145 -> 2.076 ms vs 8
+// rows, ResNet-18 b64 / b256 unchanged
+constexpr int kBnApplyRows = 1;
 
-// reduce geometry knobs (A/B): total blocks and rows per row lane of the reduce kernels;
-// 512 x 8 measured best with 8 accumulator copies (profiles/cnn_bn_reduce_r2.jsonl)
-int bn_red_blocks() {
-  static const int v = std::max(8, env_int_or("LDNN_BN_RED_BLOCKS", 512));
-  return v;
-}
-int bn_red_rows() {
-  static const int v = std::max(1, env_int_or("LDNN_BN_RED_ROWS", 8));
-  return v;
-}
-// rows per row lane of the apply passes (A/B knob LDNN_BN_APPLY_ROWS): 1 = the most blocks,
-// one row per thread -- measured on MI355X (profiles/r3/bn_apply_rows_ab_r3.jsonl, alternated)
-// EnhancedCNN b64 2.145 -> 2.076 ms vs 8 rows, ResNet-18 b64 / b256 unchanged
-int bn_apply_rows() {
-  static const int v = std::max(1, env_int_or("LDNN_BN_APPLY_ROWS", 1));
-  return v;
-}
-
-// accumulator copies the reduce blocks spread over (A/B: LDNN_BN_NCOP_FWD / _BWD)
-// (1 or kBnCopies: copies only pay when many blocks contend for the same addresses)
-int bn_ncop(bool bwd, int nblk) {
-  static const int f = env_int_or("LDNN_BN_NCOP_FWD", kBnCopies) > 1 ? kBnCopies : 1;
-  static const int b = env_int_or("LDNN_BN_NCOP_BWD", kBnCopies) > 1 ? kBnCopies : 1;
-  static const int min_blk = env_int_or("LDNN_BN_NCOP_MIN_BLOCKS", 64);
-  return nblk < min_blk ? 1 : (bwd ? b : f);
-}
+// accumulator copies the reduce blocks spread over (copies only pay when many blocks contend for
+// the same addresses: below 64 blocks one copy)
+int bn_ncop(bool, int nblk) { return nblk < 64 ? 1 : kBnCopies; }
 
 RedGeo red_geo(int M, int C, bool reduce = false) {
   RedGeo g;
@@ -83,8 +63,8 @@ RedGeo red_geo(int M, int C, bool reduce = false) {
   g.lanes = cv < 256 ? cv : 256;
   g.rl = 256 / g.lanes;
   g.gx = (cv + 255) / 256;
-  int gy = std::max(1, (reduce ? bn_red_blocks() : 1024) / g.gx);   // ~4 blocks per CU in total
-  const int min_rows = (reduce ? bn_red_rows() : bn_apply_rows()) * g.rl;  // >= 8 rows per row lane
+  int gy = std::max(1, (reduce ? kBnRedBlocks : 1024) / g.gx);   // ~4 blocks per CU in total
+  const int min_rows = (reduce ? kBnRedRows : kBnApplyRows) * g.rl;  // >= 8 rows per row lane
   gy = std::min(gy, std::max(1, (M + min_rows - 1) / min_rows));
   g.rpb = (M + gy - 1) / gy;
   g.gy = (M + g.rpb - 1) / g.rpb;
@@ -1115,39 +1095,35 @@ hipError_t bn_forward_apply(const BnArgs& a, hipStream_t s) {
   const dim3 grid(g.gx, g.gy);
   const float* sc = a.ws;
   const float* sh = a.ws + C;
-#define LDNN_BN_APPLY(RES, RELU, MASK)                                                                  \
+#define BN_APPLY_CASE(RES, RELU, MASK)                                                                  \
   bn_apply_kernel<RES, RELU, MASK><<<grid, 256, 0, s>>>(a.x, a.residual, sc, sh, a.y, M, C, g.rpb, g.lanes, g.rl, \
                                                         a.mask)
   const bool mk = a.relu && a.mask != nullptr;
   if (a.residual) {
-    if (mk) LDNN_BN_APPLY(true, true, true);
-    else if (a.relu) LDNN_BN_APPLY(true, true, false);
-    else LDNN_BN_APPLY(true, false, false);
+    if (mk) BN_APPLY_CASE(true, true, true);
+    else if (a.relu) BN_APPLY_CASE(true, true, false);
+    else BN_APPLY_CASE(true, false, false);
   } else {
-    if (mk) LDNN_BN_APPLY(false, true, true);
-    else if (a.relu) LDNN_BN_APPLY(false, true, false);
-    else LDNN_BN_APPLY(false, false, false);
+    if (mk) BN_APPLY_CASE(false, true, true);
+    else if (a.relu) BN_APPLY_CASE(false, true, false);
+    else BN_APPLY_CASE(false, false, false);
   }
-#undef LDNN_BN_APPLY
+#undef BN_APPLY_CASE
   return hipGetLastError();
 }
 
 // the small-M reduce (bn_reduce_small_kernel, one workgroup per 64 channels) below this many
-// rows; LDNN_BN_SMALL_ROWS (A/B knob, 0 = off)
-int bn_small_rows() {
-  static const int v = env_int_or("LDNN_BN_SMALL_ROWS", 2048);
-  return v;
-}
-// the same kernel with row groups up to this many rows (LDNN_BN_GRP_ROWS, A/B knob; 0 = off),
-// aiming at LDNN_BN_GRP_TARGET workgroups with >= LDNN_BN_GRP_MIN rows each
+// rows (round 5: EnhancedCNN b64 2.09 -> 1.98 ms)
+constexpr int kBnSmallRows = 2048;
+int bn_small_rows() { return kBnSmallRows; }
+// the same kernel with row groups up to 65536 rows, aiming at 512 workgroups with >= 256 rows
+// each (round 5: 1.96 -> 1.94 ms, profiles/r5/bn_grouped_reduce_ab.jsonl)
 struct Grp {
   int ny, rpb;
   bool on;
 };
 Grp grp_geo(int M, int C) {
-  static const int rows = env_int_or("LDNN_BN_GRP_ROWS", 65536);
-  static const int target = std::max(1, env_int_or("LDNN_BN_GRP_TARGET", 512));
-  static const int min_rows = std::max(32, env_int_or("LDNN_BN_GRP_MIN", 256));
+  constexpr int rows = 65536, target = 512, min_rows = 256;
   if (M > rows && M > bn_small_rows()) return {0, 0, false};
   if (M > rows) return {1, M, true};
   const int G = (C + 63) / 64;
@@ -1190,13 +1166,9 @@ hipError_t bn_forward(const BnArgs& a, hipStream_t s) {
   return bn_forward_apply(a, s);
 }
 
-// BN + ReLU + 3x3/2 max-pool (kernels above); grid knob LDNN_BNPOOL_BLOCKS (workgroups of the
-// backward statistics pass)
+// BN + ReLU + 3x3/2 max-pool (kernels above); 2048 workgroups in the backward statistics pass
 namespace {
-int bnpool_blocks() {
-  static const int v = std::max(64, env_int_or("LDNN_BNPOOL_BLOCKS", 2048));
-  return v;
-}
+int bnpool_blocks() { return 2048; }
 bool bnpool_ok(const BnArgs& a, int N, int H, int W, int P, int Q, int pad) {
   const int cv = a.C / 8;
   return a.C % 8 == 0 && cv <= 256 && 256 % cv == 0 && N > 0 && pad >= 0 && pad <= 1 &&

@@ -69,11 +69,8 @@ struct LArgs {
   FastDiv f_cw[2], f_ch[2];      // stride-2 dgrad class rows: (W - pw + 1) / 2, (H - ph + 1) / 2
   float* ws;         // split-K: combine slabs (with cnt) or wgrad partial slabs [split][M][N] (without)
   int* cnt;          // split-K arrival counters of the in-launch combine
-  int bn_stats;      // fwd: accumulate + finalize the next BatchNorm's statistics (bn); dgrad: the
-                     // backward statistics of the BN whose output's gradient this dx is (bn_x / bn_mask)
+  int bn_stats;      // fwd: accumulate + finalize the next BatchNorm's statistics (bn)
   BnFin bn;
-  const uint16_t* bn_x;     // dgrad bn_stats: that BN's input [M][N]
-  const uint8_t* bn_mask;   // ... and its ReLU bits [M][N/8] (nullptr: no ReLU)
   int tap_major;     // fwd / dgrad K-tile order: 0 = channel block fastest, 1 = filter tap fastest
   int f32_rows;      // fp32 outputs (wgrad, split-K slabs) through the row-coalesced LDS epilogue
   int bf16_rows;     // bf16 outputs (fwd y, stride-1 dgrad dx) through the row-coalesced LDS epilogue
@@ -415,7 +412,7 @@ struct Rsrc {  // buffer descriptor (a struct: the builtin type cannot be a host
 // DMA one operand tile (K-tile ks) into LDS at dst: PPW x buffer_load_dwordx4 ... lds per lane.
 // (The voffset goes through an explicit int: with the unsigned call result passed
 // straight to the builtin, hipcc silently emits no host launch stub.)
-#define LDNN_DMA_TILE(op, PPW, rsrc, dst, ks)                                                        \
+#define DMA_TILE(op, PPW, rsrc, dst, ks)                                                        \
   do {                                                                                               \
     _Pragma("unroll") for (int i_ = 0; i_ < (PPW); ++i_) {                                           \
       const int o_ = (int)(op).off(a, i_, (ks));                                                     \
@@ -440,41 +437,14 @@ __device__ __forceinline__ int tiles_of(const LArgs& a) { return a.tiles_x; }
 // measured no faster, profiles/r3/bn_copies_ab_r3.txt).  The
 // last of the grid's `tiles` workgroups sums the copies and finalizes (mean,
 // invstd, running-stat EMA, apply coefficients), so the BN needs no reduce pass.
-//
-// BWD (dgrad): the same for the backward statistics of the BN whose output's gradient the
-// tile is -- sum g and sum g * (x - mean) * invstd with g = bf16(dx) * relu'(y) -- the loads
-// of x (4 channels, 8 B per fragment), the ReLU bit-mask bytes and the channels' saved
-// mean / invstd all issued before the first use; bn_finalize_last<true> turns the totals into
-// the apply coefficients and dgamma / dbeta (bn_reduce_small_kernel's job otherwise).
-template <int WM, int WN, bool BWD = false>
+// (A dgrad's BN backward statistics come from the slab pass or a post pass over dx instead:
+// the epilogue form of round 5 cost 11-13 us per dgrad, profiles/r5/conv_bn_bwd_ab.txt.)
+template <int WM, int WN>
 __device__ __forceinline__ void bn_stats_epilogue(const LArgs& a, const Geo& g, floatx4 (&acc)[4][4], int mbase,
                                                   int n0, int wm, int wn, int lane, int tile, char* smem,
                                                   int lds_floats) {
   constexpr int BN = WN * 64;
   float* red = reinterpret_cast<float*>(smem);  // [WM][BN][2]
-  uint2 xv[4][4];
-  uint32_t mbits[4][4];
-  float mu[4][4], is[4][4];
-  if constexpr (BWD) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = n0 + wn * 64 + j * 16 + 4 * (lane >> 4);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const bool ok = n + r < a.N;
-        mu[j][r] = ok ? a.bn.save_mean[n + r] : 0.f;
-        is[j][r] = ok ? a.bn.save_invstd[n + r] : 0.f;
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int m = mbase + i * 16 + (lane & 15);
-        const bool ok = m < g.M && n < a.N;
-        const size_t o = (size_t)m * a.N + n;
-        xv[i][j] = ok ? *reinterpret_cast<const uint2*>(a.bn_x + o) : make_uint2(0u, 0u);
-        mbits[i][j] = (ok && a.bn_mask != nullptr) ? (uint32_t)a.bn_mask[o >> 3] >> (n & 7) : 0xffu;
-      }
-    }
-  }
   __syncthreads();  // every wave is done with the operand stages
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -485,16 +455,8 @@ __device__ __forceinline__ void bn_stats_epilogue(const LArgs& a, const Geo& g, 
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const float v = bf2f(f2bf(acc[j][i][r]));
-        if constexpr (BWD) {
-          const float gv = ((mbits[i][j] >> r) & 1u) ? v : 0.f;
-          const uint32_t xw = r < 2 ? xv[i][j].x : xv[i][j].y;
-          const float xf = bf2f((uint16_t)((r & 1) ? (xw >> 16) : (xw & 0xffffu)));
-          s0[r] += gv;
-          s1[r] += gv * (xf - mu[j][r]) * is[j][r];
-        } else {
-          s0[r] += v;
-          s1[r] += v * v;
-        }
+        s0[r] += v;
+        s1[r] += v * v;
       }
     }
 #pragma unroll
@@ -529,7 +491,7 @@ __device__ __forceinline__ void bn_stats_epilogue(const LArgs& a, const Geo& g, 
     bn_acc_add(accc + a.N + c, s1);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's atomics have completed
-  bn_finalize_last<BWD, kBnCopies>(a.bn, g.M, a.N, tiles_of(a), red, lds_floats);
+  bn_finalize_last<false, kBnCopies>(a.bn, g.M, a.N, tiles_of(a), red, lds_floats);
 }
 
 // Direct epilogue with the class row remap: GEMM row m of a stride-2 dgrad
@@ -767,15 +729,15 @@ __device__ __forceinline__ void conv_tail(const LArgs& a, const Geo& g, floatx4 
         store_bf16_rows<EPI>(p, acc, smem + (size_t)(wm * WN + wn) * 16384, mb, nbase, lane);
       else
         store_bf16_rows<EPI, 2>(p, acc, smem + (size_t)(wm * WN + wn) * 8192, mb, nbase, lane);
-      if constexpr (EPI == EPI_NONE) {
-        if (a.bn_stats) bn_stats_epilogue<WM, WN, DGRAD>(a, g, acc, mb, n0, wm, wn, lane, bx, smem, lds_floats);
+      if constexpr (EPI == EPI_NONE && !DGRAD) {
+        if (a.bn_stats) bn_stats_epilogue<WM, WN>(a, g, acc, mb, n0, wm, wn, lane, bx, smem, lds_floats);
       }
       return;
     }
   }
   epilogue<EPI, OUT_F32, 4, 4>(p, acc, mb, nbase, lane);
-  if constexpr (!OUT_F32 && EPI == EPI_NONE) {
-    if (a.bn_stats) bn_stats_epilogue<WM, WN, DGRAD>(a, g, acc, mb, n0, wm, wn, lane, bx, smem, lds_floats);
+  if constexpr (!OUT_F32 && EPI == EPI_NONE && !DGRAD) {
+    if (a.bn_stats) bn_stats_epilogue<WM, WN>(a, g, acc, mb, n0, wm, wn, lane, bx, smem, lds_floats);
   }
 }
 
@@ -787,7 +749,13 @@ __device__ __forceinline__ void conv_tail(const LArgs& a, const Geo& g, floatx4 
 // wgrad kernels): bit0 no in-loop DMA, bit1 (fwd only) the A operand DMAs contiguous
 // 16-KiB-aligned chunks instead of the im2col gather, bit2 no fragment reads / MFMAs, bit5 phase
 // trace: wave 0 stamps s_memrealtime (100 MHz) at entry, after the first K-tile landed, after
-// the main loop and at exit into a.trace[workgroup][4] (scripts/conv_phase_trace.py)
+// the main loop and at exit into a.trace[workgroup][4] (scripts/conv_phase_trace.py).
+// Round-6 prototypes (fwd 128x128 gather only; scripts/conv_micro.py):
+// bit7 the B (weight) fragments loaded straight to VGPRs in the MFMA layout, one K-tile ahead, so
+// only the A operand goes through LDS-DMA (bit-identical output); bit6 a BatchNorm + ReLU applied
+// to every A fragment after its LDS read, with the tap's row bounds re-checked (padding must stay
+// 0) -- the per-fragment VALU cost of folding the mid-block BN into its consumer conv (timing only:
+// affine from kernel arguments).
 // (the body of conv_lds_kernel: smem = its NS-stage LDS ring, vb = its grid coordinates)
 template <int WM, int WN, class OA, class OB, int EPI, bool OUT_F32, bool DGRAD, int NS, int XF = 0>
 __device__ __forceinline__ void conv_lds_body(const LArgs& a, const bf16_t* pa, uint32_t bytes_a, const bf16_t* pb,
@@ -801,6 +769,9 @@ __device__ __forceinline__ void conv_lds_body(const LArgs& a, const bf16_t* pa, 
   static_assert(PPA >= 1 && PPB >= 1 && PPA * NW * 8 == BM && PPB * NW * 8 == BN, "DMA pieces");
   constexpr int PER_TILE = PPA + PPB;  // DMA instructions per lane per K-tile
   static_assert(NS >= 2 && NS * STAGE <= 160 * 1024 && PER_TILE * (NS - 2) < 64, "LDS ring");
+  constexpr bool kBD = (XF & 128) != 0, kFold = (XF & 64) != 0;
+  static_assert(!(kBD || kFold) || (NS == 2 && std::is_same_v<OB, WeightKC<BN, PPB, NW>> && !DGRAD),
+                "prototype bits: fwd gather kernel only");
 
   const Geo g = make_geo(a, DGRAD, vb.z);
   const int tiles_m = (g.M + BM - 1) / BM, tiles_n = (a.N + BN - 1) / BN;
@@ -844,6 +815,39 @@ __device__ __forceinline__ void conv_lds_body(const LArgs& a, const bf16_t* pa, 
     ra.r = __builtin_amdgcn_make_buffer_rsrc((void*)pa, (short)0, (int)bytes_a, 0x00020000);
     rb.r = __builtin_amdgcn_make_buffer_rsrc((void*)pb, (short)0, (int)bytes_b, 0x00020000);
     KS ks = ks_init(a, g, kt0);
+    bf16x8 fbr[2][4], fbn[2][4];   // (kBD: this / the next K-tile's B fragments)
+    auto load_b = [&](bf16x8 (&f)[2][4], const KS& k) {
+      const int koff = (k.r * a.s.S + k.s) * a.s.C + k.cb * 64 + (lane >> 4) * 8;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = n0 + wn * 64 + j * 16 + (lane & 15);
+        const bf16_t* src = pb + (size_t)(n < a.N ? n : 0) * a.rsc + koff;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          const bf16x8 v = *reinterpret_cast<const bf16x8*>(src + kk * 32);
+          f[kk][j] = n < a.N ? v : bf16x8{};
+        }
+      }
+    };
+    int fih[4], fiw[4];   // (kFold: each A fragment row's top-left input pixel)
+    float fsc[2][8], fsh[2][8];
+    if constexpr (kFold) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = m0 + (wm * 4 + i) * 16 + (lane & 15);
+        const int t = fdiv(m, g.f_rw), q = m - t * a.s.Q, n = fdiv(t, g.f_rh), p = t - n * a.s.P;
+        fih[i] = m < g.M ? p * a.s.stride - a.s.pad : -(1 << 20);
+        fiw[i] = q * a.s.stride - a.s.pad;
+      }
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          fsc[kk][e] = 1.f + a.beta * (float)(kk * 8 + e);
+          fsh[kk][e] = a.beta * 0.5f;
+        }
+    }
+    if constexpr (kBD) load_b(fbr, ks);
     // prologue: K-tiles 0 .. NS-2 into stages 0 .. NS-2
 #pragma unroll
     for (int t = 0; t < NS - 1; ++t) {
@@ -853,8 +857,8 @@ __device__ __forceinline__ void conv_lds_body(const LArgs& a, const bf16_t* pa, 
           oa.advance(a);
           ob.advance(a);
         }
-        if constexpr (!(XF & 16)) LDNN_DMA_TILE(oa, PPA, ra, smem + t * STAGE, ks);
-        if constexpr (!(XF & 8)) LDNN_DMA_TILE(ob, PPB, rb, smem + t * STAGE + A_BYTES, ks);
+        if constexpr (!(XF & 16)) DMA_TILE(oa, PPA, ra, smem + t * STAGE, ks);
+        if constexpr (!(XF & 8) && !kBD) DMA_TILE(ob, PPB, rb, smem + t * STAGE + A_BYTES, ks);
       }
     }
 
@@ -870,6 +874,7 @@ __device__ __forceinline__ void conv_lds_body(const LArgs& a, const bf16_t* pa, 
       if constexpr ((XF & 32) != 0) {
         if (kt == 0 && trace != nullptr) trace[1] = __builtin_amdgcn_s_memrealtime();
       }
+      const KS kcur = ks;   // (NS == 2: the tap of tile kt, for the kFold bounds)
       if (!(XF & 1) && kt + NS - 1 < nk) {
         ks_next(a, g, ks);
         oa.advance(a);
@@ -883,9 +888,10 @@ __device__ __forceinline__ void conv_lds_body(const LArgs& a, const bf16_t* pa, 
             __builtin_amdgcn_raw_ptr_buffer_load_lds(ra.r, (lds_void*)(nxt + (i_ * NW + wid) * 1024), 16,
                                                      (int)(tb + (i_ * NW + wid) * 1024 + lane * 16), 0, 0, 0);
         } else if constexpr (!(XF & 16)) {
-          LDNN_DMA_TILE(oa, PPA, ra, nxt, ks);
+          DMA_TILE(oa, PPA, ra, nxt, ks);
         }
-        if constexpr (!(XF & 8)) LDNN_DMA_TILE(ob, PPB, rb, nxt + A_BYTES, ks);  // XF 8 / 16: no B / A fill
+        if constexpr (kBD) load_b(fbn, ks);
+        else if constexpr (!(XF & 8)) DMA_TILE(ob, PPB, rb, nxt + A_BYTES, ks);  // XF 8 / 16: no B / A fill
       }
       const char* la = smem + cur * STAGE;
       const char* lb = la + A_BYTES;
@@ -902,7 +908,20 @@ __device__ __forceinline__ void conv_lds_body(const LArgs& a, const bf16_t* pa, 
 #pragma unroll
         for (int i = 0; i < 4; ++i) fa[kk][i] = read_frag<OA::KC, BM>(la, wm * 4 + i, kk, lane);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) fb[kk][j] = read_frag<OB::KC, BN>(lb, wn * 4 + j, kk, lane);
+        for (int j = 0; j < 4; ++j) fb[kk][j] = kBD ? fbr[kk][j] : read_frag<OB::KC, BN>(lb, wn * 4 + j, kk, lane);
+      }
+      if constexpr (kFold) {   // relu(scale * x + shift) per channel, 0 where the tap is padding
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const bool ok = (unsigned)(fih[i] + kcur.r) < (unsigned)a.s.H && (unsigned)(fiw[i] + kcur.s) < (unsigned)a.s.W;
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk) {
+            bf16x8 v = fa[kk][i];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = (__bf16)(ok ? fmaxf((float)v[e] * fsc[kk][e] + fsh[kk][e], 0.f) : 0.f);
+            fa[kk][i] = v;
+          }
+        }
       }
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk)
@@ -912,6 +931,12 @@ __device__ __forceinline__ void conv_lds_body(const LArgs& a, const bf16_t* pa, 
           for (int i = 0; i < 4; ++i)
             acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[kk][j], fa[kk][i], acc[j][i], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
+      if constexpr (kBD) {
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) fbr[kk][j] = fbn[kk][j];
+      }
       cur = cur == NS - 1 ? 0 : cur + 1;
     }
   }
@@ -1120,7 +1145,7 @@ __global__ __launch_bounds__(256, 2) void conv_halo_kernel(LArgs a, const bf16_t
           ks_next(a, g, ks);
           ob.advance(a);
         }
-        LDNN_DMA_TILE(ob, PPB, rb, bst + t * B_BYTES, ks);
+        DMA_TILE(ob, PPB, rb, bst + t * B_BYTES, ks);
       }
     }
     int cur = 0;
@@ -1142,7 +1167,7 @@ __global__ __launch_bounds__(256, 2) void conv_halo_kernel(LArgs a, const bf16_t
       if (kt + NSB - 1 < nk) {  // B(kt+NSB-1) into the stage B(kt-1) used
         ks_next(a, g, ks);
         ob.advance(a);
-        LDNN_DMA_TILE(ob, PPB, rb, bst + (cur == 0 ? NSB - 1 : cur - 1) * B_BYTES, ks);
+        DMA_TILE(ob, PPB, rb, bst + (cur == 0 ? NSB - 1 : cur - 1) * B_BYTES, ks);
       }
       const int dr = DGRAD ? 1 - kc.r : kc.r - 1, ds = DGRAD ? 1 - kc.s : kc.s - 1;
       const int toff = dr * W + ds;
@@ -1308,11 +1333,11 @@ __global__ __launch_bounds__(512, 1) void conv_hb_kernel(LArgs a, const bf16_t* 
 
     // prologue: the first block's halo, weights of K-tiles 0 and 1
     load_halo(cb0, 0);
-    LDNN_DMA_TILE(ob, PPB, rb, bst, ks);
+    DMA_TILE(ob, PPB, rb, bst, ks);
     if (nk > 1) {
       ks_next(a, g, ks);
       ob.advance(a);
-      LDNN_DMA_TILE(ob, PPB, rb, bst + kBBytes, ks);
+      DMA_TILE(ob, PPB, rb, bst + kBBytes, ks);
       wait_vm<PPB>();  // halo + weights(0) landed (loads retire in order)
     } else {
       wait_vm<0>();
@@ -1335,7 +1360,7 @@ __global__ __launch_bounds__(512, 1) void conv_hb_kernel(LArgs a, const bf16_t* 
         if (kt + 2 < nk) {  // weights(kt+2) into the stage K-tile kt-1 used
           ks_next(a, g, ks);
           ob.advance(a);
-          LDNN_DMA_TILE(ob, PPB, rb, bst + ((kt + 2) % kNSB) * kBBytes, ks);
+          DMA_TILE(ob, PPB, rb, bst + ((kt + 2) % kNSB) * kBBytes, ks);
         }
         if (tap == 0 && blk + 1 < nblk) load_halo(cb0 + blk + 1, (blk + 1) & 1);  // its buffer's last reader was K-tile kt-1
         const int dr = DGRAD ? 1 - tap / 3 : tap / 3 - 1, ds = DGRAD ? 1 - tap % 3 : tap % 3 - 1;
@@ -2283,15 +2308,8 @@ __global__ __launch_bounds__(256, 1) void conv_patch_ws_kernel(LArgs a, const bf
   }
 }
 
-int slab_nt_env() {
-  static const int v = [] {
-    const char* e = std::getenv("LDNN_SLAB_NT");
-    return e ? std::atoi(e) : 1;
-  }();
-  return v;
-}
-
-// NT: the slabs are read for the last time -- streaming (nontemporal) loads (A/B knob LDNN_SLAB_NT)
+// NT: the slabs are read for the last time -- streaming (nontemporal) loads (measured -0.8 %
+// on EnhancedCNN, profiles/slab_nontemporal_ab_r2.jsonl; every launch uses NT = true)
 template <bool NT>
 __device__ __forceinline__ floatx4 slab_ld(const floatx4* p) {
   if constexpr (NT) return __builtin_nontemporal_load(p);
@@ -2353,17 +2371,12 @@ hipError_t conv_slab_epilogue(const float* ws, uint16_t* out, int M, int N, int 
   const int64_t n8 = (int64_t)M * N / 8;
   if (n8 <= 0) return hipSuccess;
   const unsigned g = (unsigned)((n8 + 255) / 256);
-  const bool nt = slab_nt_env();
   switch (epi) {
-#define LDNN_SLAB_EPI(E)                                                                                 \
-  case E:                                                                                                \
-    if (nt) conv_slab_epilogue_kernel<E, true><<<g, 256, 0, st>>>(ws, out, n8, N, splits, bias);       \
-    else conv_slab_epilogue_kernel<E, false><<<g, 256, 0, st>>>(ws, out, n8, N, splits, bias);         \
-    break;
-    LDNN_SLAB_EPI(EPI_NONE)
-    LDNN_SLAB_EPI(EPI_BIAS)
-    LDNN_SLAB_EPI(EPI_BIAS_RELU)
-#undef LDNN_SLAB_EPI
+    case EPI_NONE: conv_slab_epilogue_kernel<EPI_NONE, true><<<g, 256, 0, st>>>(ws, out, n8, N, splits, bias); break;
+    case EPI_BIAS: conv_slab_epilogue_kernel<EPI_BIAS, true><<<g, 256, 0, st>>>(ws, out, n8, N, splits, bias); break;
+    case EPI_BIAS_RELU:
+      conv_slab_epilogue_kernel<EPI_BIAS_RELU, true><<<g, 256, 0, st>>>(ws, out, n8, N, splits, bias);
+      break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -2486,20 +2499,16 @@ __global__ __launch_bounds__(256) void conv_slab_bn_kernel(const float* __restri
 }
 
 int env_int(const char* name, int dflt);
-// LDNN_CONV_SLAB_BN (A/B knob, default 1): slab-split forward convs followed by a training BN
-// take the BN statistics in conv_slab_bn_kernel; LDNN_CONV_SLAB_BN_TARGET workgroups aimed at
-int slab_bn_env() {
-  static const int v = env_int("LDNN_CONV_SLAB_BN", 1);
-  return v;
-}
-// LDNN_CONV_BN_BWD (A/B knob): stride-1 dgrads take the backward statistics of the BN whose
-// output's gradient they produce (conv2d_dgrad with a BnBwdFuse): 1 (default) in the slab split-K
-// sum, and for a dgrad without slabs that shares its launch with the wgrad, as a pass over dx in
-// the shared post launch; 3 in the slab sum only; 2 also in the direct / in-launch-combine
-// epilogue; 0 never.  Measured on MI355X
-// (profiles/r5/conv_bn_bwd_ab.txt): the slab pass absorbs the reduce for ~1.5 us less per BN, while
-// the epilogue form -- x and mask loads, 8-copy atomics and one finalizing workgroup behind the
-// tile's own stores -- added 11-13 us to a 64 / 128-tile dgrad to save an 8-10 us reduce launch
+// slab-split forward convs followed by a training BN take the BN statistics in
+// conv_slab_bn_kernel (9 fewer launches per EnhancedCNN step, profiles/r5/conv_slab_bn_ab.txt)
+constexpr int kSlabBnTarget = 512;   // conv_slab_bn workgroups aimed at
+// LDNN_CONV_BN_BWD (documented fallback): stride-1 dgrads take the backward statistics of the BN
+// whose output's gradient they produce (conv2d_dgrad with a BnBwdFuse): 1 (default) in the slab
+// split-K sum, and for a dgrad without slabs that shares its launch with the wgrad, as a pass over
+// dx in the shared post launch; 0 never (the BN runs its own reduce).  (The form inside the direct
+// / in-launch-combine epilogue -- x and mask loads, 8-copy atomics and one finalizing workgroup
+// behind the tile's own stores -- added 11-13 us to a 64 / 128-tile dgrad to save an 8-10 us reduce
+// launch, profiles/r5/conv_bn_bwd_ab.txt, and was removed in round 6.)
 int g_bn_bwd = -1;
 int bn_bwd_env() {
   if (g_bn_bwd < 0) g_bn_bwd = env_int("LDNN_CONV_BN_BWD", 1);
@@ -2508,7 +2517,7 @@ int bn_bwd_env() {
 hipError_t conv_slab_bn(const float* ws, uint16_t* out, int M, int N, int splits, const BnFin& fin, hipStream_t st,
                         const BnBwdFuse* bnb = nullptr) {
   if (M <= 0) return hipSuccess;
-  static const int target = std::max(1, env_int("LDNN_CONV_SLAB_BN_TARGET", 512));
+  constexpr int target = kSlabBnTarget;
   const int G = (N + 63) / 64;
   int ny = std::max(1, std::min({(target + G - 1) / G, (M + 31) / 32, kGrpMax}));
   const int rpb = (M + ny - 1) / ny;
@@ -2516,12 +2525,10 @@ hipError_t conv_slab_bn(const float* ws, uint16_t* out, int M, int N, int splits
   const dim3 g(G, ny);
   if (bnb != nullptr) {
     const bf16_t* bx = reinterpret_cast<const bf16_t*>(bnb->x);
-    if (slab_nt_env()) conv_slab_bn_kernel<true, true><<<g, 256, 0, st>>>(ws, out, M, N, splits, fin, rpb, bx, bnb->mask);
-    else conv_slab_bn_kernel<false, true><<<g, 256, 0, st>>>(ws, out, M, N, splits, fin, rpb, bx, bnb->mask);
+    conv_slab_bn_kernel<true, true><<<g, 256, 0, st>>>(ws, out, M, N, splits, fin, rpb, bx, bnb->mask);
     return hipGetLastError();
   }
-  if (slab_nt_env()) conv_slab_bn_kernel<true><<<g, 256, 0, st>>>(ws, out, M, N, splits, fin, rpb, nullptr, nullptr);
-  else conv_slab_bn_kernel<false><<<g, 256, 0, st>>>(ws, out, M, N, splits, fin, rpb, nullptr, nullptr);
+  conv_slab_bn_kernel<true><<<g, 256, 0, st>>>(ws, out, M, N, splits, fin, rpb, nullptr, nullptr);
   return hipGetLastError();
 }
 
@@ -2640,20 +2647,13 @@ bool wgrad_ring_ok(const ConvShape& s) {
          s.C % 64 == 0 && s.K % 64 == 0 && s.W >= 8 && s.W <= 63 && (m == 2 || (s.C == 64 && s.K == 64));
 }
 
-// LDNN_CONV_WGRAD_XCD (A/B knob, default 1): a split-K wgrad's tiles of one npq slice on
-// one XCD (split_coords)
-int wgrad_xcd_env() {
-  static const int v = env_int("LDNN_CONV_WGRAD_XCD", 1);
-  return v;
-}
-
 WgradPlan plan_wgrad(const ConvShape& s, bool allow_ring = true) {
   WgradPlan p;
   p.ring = allow_ring && wgrad_ring_ok(s);
   if (p.ring) {  // (64 filters x 576 tap-channels) blocks x npq slices of >= 12 K-tiles, ~512 workgroups
     // (two per CU: ResNet-18 b256 7.652 vs 7.705-7.711 ms at 384, 7.70 at 256, 7.78 at 1024; b64 capped by
     // the 12-K-tile floor either way, profiles/r4/ring_wgrad_target_ab.jsonl)
-    static const int target = env_int("LDNN_CONV_RING_TARGET", 512);
+    constexpr int target = 512;
     p.narrow = false;
     p.tiles = (s.K / 64) * (s.C / 64);
     p.nk_all = (s.N * s.P * s.Q + 63) / 64;
@@ -2671,12 +2671,12 @@ WgradPlan plan_wgrad(const ConvShape& s, bool allow_ring = true) {
   int splits = 1;
   // (512 since dgrad and wgrad share launches: ResNet-18 b256 7.332 -> 7.256 ms, b64 -0.2 %, EnhancedCNN
   // neutral, 6 alternated samples each, profiles/r5/conv_wgrad_target_ab.txt)
-  static const int target = env_int("LDNN_CONV_WGRAD_TARGET", 512);  // workgroups to aim for (A/B knob)
-  static const int min_kt1 = std::max(1, env_int("LDNN_CONV_WGRAD_MIN_KT", 8));     // 1x1 filters (A/B knob)
+  constexpr int target = 512;  // workgroups to aim for
+  constexpr int min_kt1 = 8;   // K-tiles per slice, 1x1 filters
   // larger filters: >= 16 K-tiles per slice since dgrad and wgrad share a launch (EnhancedCNN b64
-  // 1.642 -> 1.573 ms with LDNN_CONV_SLAB_TARGET 256, ResNet-18 b64 / b256 -0.3 / -0.2 %; the 1x1
+  // 1.642 -> 1.573 ms with the slab target at 256, ResNet-18 b64 / b256 -0.3 / -0.2 %; the 1x1
   // shortcut wgrads stay at 8: 16 there cost ResNet-18 b64 +0.6 %, profiles/r5/conv_split_knobs_ab.txt)
-  static const int min_kt3 = std::max(1, env_int("LDNN_CONV_WGRAD_MIN_KT3", 16));   // (A/B knob)
+  constexpr int min_kt3 = 16;
   const int min_kt = s.R * s.S > 1 ? min_kt3 : min_kt1;
   if (p.tiles < 256) splits = std::max(1, std::min((target + p.tiles - 1) / p.tiles, p.nk_all / min_kt));
   p.nk_split = (p.nk_all + splits - 1) / splits;
@@ -2684,55 +2684,25 @@ WgradPlan plan_wgrad(const ConvShape& s, bool allow_ring = true) {
   return p;
 }
 
-// Filter taps fastest in the fwd / dgrad K-tile order (default; LDNN_CONV_TAPMAJOR=0
-// restores channel blocks fastest): consecutive K-tiles re-read shifted rows of one
-// channel block, which the L2 / L1 serve warm -- alternated same-box A/B ResNet-18
-// b64 3.89 -> 3.85 ms (profiles/cnn_fuse_stats_tapmajor_ab_r2.jsonl)
-int tap_major_env() {
-  static const int v = [] {
-    const char* e = std::getenv("LDNN_CONV_TAPMAJOR");
-    return e ? std::atoi(e) : 1;
-  }();
-  return v;
-}
-
-// A/B knob: LDNN_CONV_F32_ROWS=0 stores fp32 conv outputs straight from the MFMA layout
-int f32_rows_env() {
-  static const int v = env_int("LDNN_CONV_F32_ROWS", 1);
-  return v;
-}
-
-// A/B knob: LDNN_CONV_BF16_ROWS=0 stores bf16 conv outputs straight from the MFMA layout,
-// 1 stages only in kernels with a 16 KiB LDS slice per wave, 2 (default) also in halves
-int bf16_rows_env() {
-  static const int v = env_int("LDNN_CONV_BF16_ROWS", 2);
-  return v;
-}
-
-// A/B knob: LDNN_CONV_REMAP_ROWS=0 keeps the direct remapped store of stride-2 dgrads
-int remap_rows_env() {
-  static const int v = env_int("LDNN_CONV_REMAP_ROWS", 1);
-  return v;
-}
-
 uint64_t* g_conv_trace = nullptr;  // phase-trace buffer of LDNN_CONV_XF=32 builds (set_conv_trace)
 
-// LDNN_CONV_COMBINE_LAST (A/B knob, default 1): the in-launch split-K combine's summer is the
-// tile's last K slice (splitk_combine_last) instead of the last workgroup to arrive
-int g_combine_last = -1;   // set_conv_combine_last (tests), else LDNN_CONV_COMBINE_LAST
-int combine_last_env() {
-  if (g_combine_last < 0) g_combine_last = env_int("LDNN_CONV_COMBINE_LAST", 1);
-  return g_combine_last;
-}
+// the in-launch split-K combine's summer is the tile's last K slice (splitk_combine_last, round 5)
+// instead of the last workgroup to arrive; set_conv_combine_last(0) (tests) selects the latter
+int g_combine_last = 1;
 
+// Fixed choices of earlier A/Bs (round 2, profiles/*_ab_r2.jsonl): filter taps fastest in the
+// fwd / dgrad K-tile order (consecutive K-tiles re-read shifted rows of one channel block, which
+// L2 / L1 serve warm: ResNet-18 b64 3.89 -> 3.85 ms); fp32 outputs, bf16 outputs (also in two
+// 32-row halves where a wave has only 8 KiB of LDS) and the stride-2 dgrad row remap all staged
+// through LDS for full-row stores.
 LArgs base_args(const ConvShape& s) {
   LArgs a{};
   a.trace = g_conv_trace;
-  a.combine_last = combine_last_env();
-  a.tap_major = tap_major_env();
-  a.f32_rows = f32_rows_env();
-  a.bf16_rows = bf16_rows_env();
-  a.remap_rows = remap_rows_env();
+  a.combine_last = g_combine_last;
+  a.tap_major = 1;
+  a.f32_rows = 1;
+  a.bf16_rows = 2;
+  a.remap_rows = 1;
   a.s = s;
   a.rsc = s.R * s.S * s.C;
   a.pq = s.P * s.Q;
@@ -2753,21 +2723,11 @@ bool shape_ok(const ConvShape& s) {
          fits((size_t)s.K * s.R * s.S * s.C * 2) && fits((size_t)s.N * s.P * s.Q * s.K * 2);
 }
 
-// LDS ring depth.  Default NS = 2 (two workgroups = 8 waves per CU).  The deep
-// ring (NS 3 / 4 at one workgroup per CU, 2-3 K-tiles in flight) is kept for
-// tuning behind LDNN_CONV_NS=4: measured on MI355X over the ResNet-18 @224 conv
-// shapes (scripts/conv_micro.py, profiles/conv_ring_depth_r1.txt) it is SLOWER on
-// every shape (fwd+dgrad+wgrad 922 vs 710 us): the second workgroup's waves hide
-// the per-wave ds_read / barrier latency better than deeper DMA prefetch does.
-int ring_env() {
-  static const int v = [] {
-    const char* e = std::getenv("LDNN_CONV_NS");
-    return e ? std::atoi(e) : 0;
-  }();
-  return v;
-}
-
-bool deep_ring(int) { return ring_env() >= 3; }
+// LDS ring depth NS = 2 (two workgroups = 8 waves per CU).  (A deep ring, NS 3 / 4 at one
+// workgroup per CU with 2-3 K-tiles in flight, measured SLOWER on every ResNet-18 @224 shape --
+// fwd+dgrad+wgrad 922 vs 710 us, profiles/conv_ring_depth_r1.txt; r4: 10.05 vs 7.71 ms -- and was
+// removed in round 6: the second workgroup's waves hide the per-wave ds_read / barrier latency
+// better than deeper DMA prefetch does.)
 
 // OA / OB = Policy<rows, DMA pieces per wave (= rows / 8 / 4 waves), 4 waves>.
 int conv_xf_env() {
@@ -2783,7 +2743,15 @@ hipError_t launch_ns(LArgs a, int epi, int splits, const bf16_t* pa, size_t ba, 
   if constexpr ((std::is_same_v<OA, FwdA<128, 4, 4>> || std::is_same_v<OA, WgradA<64, 2, 4>> ||
                  std::is_same_v<OA, WgradA<128, 4, 4>> || std::is_same_v<OA, DgradA<128, 4, 4>>) && NS == 2) {
     const int xf = conv_xf_env();
-    if (xf != 0 && epi == EPI_NONE) {
+    if constexpr (std::is_same_v<OA, FwdA<128, 4, 4>>) {   // (round-6 prototypes, fwd only; other passes run normally)
+      if ((xf == 64 || xf == 128 || xf == 192) && epi == EPI_NONE && a.nb > 0) {
+        if (xf == 64) conv_lds_kernel<WM, WN, OA, OB, EPI_NONE, OUT_F32, DGRAD, NS, 64><<<grid, block, 0, st>>>(a, pa, (uint32_t)ba, pb, (uint32_t)bb);
+        else if (xf == 128) conv_lds_kernel<WM, WN, OA, OB, EPI_NONE, OUT_F32, DGRAD, NS, 128><<<grid, block, 0, st>>>(a, pa, (uint32_t)ba, pb, (uint32_t)bb);
+        else conv_lds_kernel<WM, WN, OA, OB, EPI_NONE, OUT_F32, DGRAD, NS, 192><<<grid, block, 0, st>>>(a, pa, (uint32_t)ba, pb, (uint32_t)bb);
+        return hipGetLastError();
+      }
+    }
+    if (xf != 0 && xf != 64 && xf != 128 && xf != 192 && epi == EPI_NONE) {
       switch (xf) {
         case 1: conv_lds_kernel<WM, WN, OA, OB, EPI_NONE, OUT_F32, DGRAD, NS, 1><<<grid, block, 0, st>>>(a, pa, (uint32_t)ba, pb, (uint32_t)bb); break;
         case 2:
@@ -2803,35 +2771,31 @@ hipError_t launch_ns(LArgs a, int epi, int splits, const bf16_t* pa, size_t ba, 
       return hipGetLastError();
     }
   }
-#define LDNN_CONV_LDS(E)                                                                                      \
+#define CONV_LDS_CASE(E)                                                                                      \
   conv_lds_kernel<WM, WN, OA, OB, E, OUT_F32, DGRAD, NS><<<grid, block, 0, st>>>(a, pa, (uint32_t)ba, pb, \
                                                                                   (uint32_t)bb)
   switch (epi) {
     case EPI_NONE:
-      LDNN_CONV_LDS(EPI_NONE);
+      CONV_LDS_CASE(EPI_NONE);
       break;
     case EPI_BIAS:
       if constexpr (OUT_F32) return hipErrorInvalidValue;
-      else LDNN_CONV_LDS(EPI_BIAS);
+      else CONV_LDS_CASE(EPI_BIAS);
       break;
     case EPI_BIAS_RELU:
       if constexpr (OUT_F32) return hipErrorInvalidValue;
-      else LDNN_CONV_LDS(EPI_BIAS_RELU);
+      else CONV_LDS_CASE(EPI_BIAS_RELU);
       break;
     default:
       return hipErrorInvalidValue;
   }
-#undef LDNN_CONV_LDS
+#undef CONV_LDS_CASE
   return hipGetLastError();
 }
 
 template <int WM, int WN, class OA, class OB, bool OUT_F32, bool DGRAD>
 hipError_t launch(LArgs a, int epi, int splits, const bf16_t* pa, size_t ba, const bf16_t* pb, size_t bb,
                   hipStream_t st) {
-  constexpr int STAGE = (WM + WN) * 64 * 128;
-  constexpr int DEEP = 4 * STAGE <= 128 * 1024 ? 4 : 3;
-  if (deep_ring(a.tiles_x * splits * a.classes))
-    return launch_ns<WM, WN, OA, OB, OUT_F32, DGRAD, DEEP>(a, epi, splits, pa, ba, pb, bb, st);
   return launch_ns<WM, WN, OA, OB, OUT_F32, DGRAD, 2>(a, epi, splits, pa, ba, pb, bb, st);
 }
 
@@ -2851,7 +2815,7 @@ bool halo_ok(const ConvShape& s) {
 }
 // the halo path takes this plan (wm: its wave rows, 4 = 256x64 tiles, 2 = 128x128)
 bool halo_takes(const ConvShape& s, int wm) {
-  if (!halo_ok(s) || deep_ring(0)) return false;
+  if (!halo_ok(s)) return false;
   const int m = halo_env();
   if (wm == 4) return m != 0;
   return m == 2;
@@ -2916,28 +2880,28 @@ hipError_t launch_halo(LArgs a, int epi, int splits, const bf16_t* pa, size_t ba
     conv_halo_kernel<WM, WN, OB, EPI_NONE, DGRAD, 32><<<grid, block, 0, st>>>(a, pa, (uint32_t)ba, pb, (uint32_t)bb);
     return hipGetLastError();
   }
-#define LDNN_CONV_HALO(E) \
+#define HALO_CASE(E) \
   conv_halo_kernel<WM, WN, OB, E, DGRAD><<<grid, block, 0, st>>>(a, pa, (uint32_t)ba, pb, (uint32_t)bb)
   switch (epi) {
-    case EPI_NONE: LDNN_CONV_HALO(EPI_NONE); break;
-    case EPI_BIAS: LDNN_CONV_HALO(EPI_BIAS); break;
-    case EPI_BIAS_RELU: LDNN_CONV_HALO(EPI_BIAS_RELU); break;
+    case EPI_NONE: HALO_CASE(EPI_NONE); break;
+    case EPI_BIAS: HALO_CASE(EPI_BIAS); break;
+    case EPI_BIAS_RELU: HALO_CASE(EPI_BIAS_RELU); break;
     default: return hipErrorInvalidValue;
   }
-#undef LDNN_CONV_HALO
+#undef HALO_CASE
   return hipGetLastError();
 }
 
 // Big-tile halo path (conv_hb_kernel) for 3x3 stride-1 pad-1 fwd / dgrad with 64-multiple input
 // and 128-multiple output channels, W <= 32 (ResNet-18 layers 2-4, EnhancedCNN's stages).
-// LDNN_CONV_HB (A/B knob): 0 off; 1 (default) dgrad grids of >= 96 tiles; 2 fwd too; 3 every
-// eligible shape.  Measured (scripts/conv_micro.py, profiles/r5/conv_hb_micro.jsonl): the dgrad
+// LDNN_CONV_HB (documented fallback): 0 off; 1 (default) dgrad grids of >= 96 tiles.  (Test hooks
+// only, set_conv_hb: 2 fwd too; 3 every eligible shape.)  Measured (scripts/conv_micro.py, profiles/r5/conv_hb_micro.jsonl): the dgrad
 // wins at ResNet-18 b256 (C128 H28 108 -> 102 us, C256 H14 100 -> 93, C512 H7 104 -> 94) and
 // b64 C128 H28 (28.6 -> 26.5); the fwd loses to the gather kernel (C128 H28 b256 79 -> 94 us) and
 // the small split-K grids (EnhancedCNN b64) lose both ways.
 int g_conv_hb = -2;  // -2: not read yet
 int hb_env() {
-  if (g_conv_hb == -2) g_conv_hb = env_int("LDNN_CONV_HB", 1);
+  if (g_conv_hb == -2) g_conv_hb = env_int("LDNN_CONV_HB", 1) != 0 ? 1 : 0;
   return g_conv_hb;
 }
 bool hb_takes(const ConvShape& s, bool dgrad) {
@@ -2956,45 +2920,35 @@ hipError_t launch_hb(LArgs a, int epi, int splits, const bf16_t* pa, size_t ba, 
                      hipStream_t st) {
   a.tap_major = 1;  // taps fastest inside a channel block: one halo per block
   dim3 grid(a.tiles_x, splits, 1), block(hb::kNT);
-#define LDNN_CONV_HB(E) conv_hb_kernel<OB, E, DGRAD><<<grid, block, 0, st>>>(a, pa, (uint32_t)ba, pb, (uint32_t)bb)
+#define HB_CASE(E) conv_hb_kernel<OB, E, DGRAD><<<grid, block, 0, st>>>(a, pa, (uint32_t)ba, pb, (uint32_t)bb)
   switch (epi) {
-    case EPI_NONE: LDNN_CONV_HB(EPI_NONE); break;
+    case EPI_NONE: HB_CASE(EPI_NONE); break;
     case EPI_BIAS:
       if constexpr (DGRAD) return hipErrorInvalidValue;
-      else LDNN_CONV_HB(EPI_BIAS);
+      else HB_CASE(EPI_BIAS);
       break;
     case EPI_BIAS_RELU:
       if constexpr (DGRAD) return hipErrorInvalidValue;
-      else LDNN_CONV_HB(EPI_BIAS_RELU);
+      else HB_CASE(EPI_BIAS_RELU);
       break;
     default: return hipErrorInvalidValue;
   }
-#undef LDNN_CONV_HB
+#undef HB_CASE
   return hipGetLastError();
 }
 
-// LDNN_CONV_SLAB=0: small-M fwd / dgrad use the in-launch combine (A/B knob)
+// LDNN_CONV_SLAB=0 (documented fallback): small-M fwd / dgrad use the in-launch combine
 bool slab_env_off() {
-  static const bool v = [] {
-    const char* e = std::getenv("LDNN_CONV_SLAB");
-    return e != nullptr && e[0] == '0';
-  }();
+  static const bool v = env_int("LDNN_CONV_SLAB", 1) == 0;
   return v;
 }
 
 // In-launch split-K for small-M fwd / dgrad (below 256 tiles: ResNet-18's 14x14
 // stage, 196 tiles, A/B 3.76 -> 3.68 ms at b64, profiles/cnn_split_tiles_ab_r2.jsonl):
 // enough slices for ~1.5 workgroups per CU, >= 8 K-tiles each, at most 8.
-int split_tiles_env() {  // LDNN_CONV_SPLIT_TILES: tile count below which fwd / dgrad split K (A/B knob)
-  static const int v = [] {
-    const char* e = std::getenv("LDNN_CONV_SPLIT_TILES");
-    return e ? std::atoi(e) : 256;
-  }();
-  return v;
-}
 int small_m_splits(int tiles, int nk) {
-  if (tiles >= split_tiles_env() || nk < 16) return 1;
-  static const int target = env_int("LDNN_CONV_SPLIT_TARGET", 384);  // workgroups to aim for (A/B knob)
+  if (tiles >= 256 || nk < 16) return 1;
+  constexpr int target = 384;  // workgroups to aim for
   int sp = (target + tiles - 1) / tiles;
   sp = std::min(sp, nk / 8);
   sp = std::min(sp, 8);
@@ -3010,8 +2964,8 @@ int slab_splits(int tiles, int nk) {
   if (tiles >= 160 || nk < 8) return 1;
   // (256 since conv GEMMs share launches: EnhancedCNN b64 -1.2 %, ResNet-18 neutral,
   // profiles/r5/conv_split_knobs_ab.txt)
-  static const int target = env_int("LDNN_CONV_SLAB_TARGET", 256);     // workgroups to aim for (A/B knob)
-  static const int min_kt = env_int("LDNN_CONV_SLAB_MIN_KT", 3);        // K-tiles per slice at least (A/B knob)
+  constexpr int target = 256;  // workgroups to aim for
+  constexpr int min_kt = 3;    // K-tiles per slice at least
   int sp = (target + tiles - 1) / tiles;
   sp = std::min(sp, nk / std::max(1, min_kt));
   sp = std::min(sp, 32);
@@ -3030,7 +2984,7 @@ void finish_plan(Plan& p) {
   // tiles (EnhancedCNN 8x8 / 16x16 stages, ResNet-18 7x7) the slab traffic cost what
   // the in-launch combine does (ResNet-18 b64 3.94 vs 3.89 ms), at 16 / 32 tiles the
   // slabs win (EnhancedCNN 4x4 / 2x2 convs 28 / 38 -> 25 / 28 us)
-  static const int slab_tiles = env_int("LDNN_CONV_SLAB_TILES", 48);   // (A/B knob)
+  constexpr int slab_tiles = 48;
   p.slab = p.classes == 1 && p.tiles_x < slab_tiles && !slab_env_off();
   p.splits = p.slab ? slab_splits(p.tiles_x, p.nk_all) : small_m_splits(p.tiles_x * p.classes, p.nk_all);
   p.nk_split = (p.nk_all + p.splits - 1) / p.splits;
@@ -3085,7 +3039,7 @@ Plan plan_hb(const ConvShape& s, bool dgrad) {
   p.tiles_x = ((p.M + hb::kBM - 1) / hb::kBM) * (cout / hb::kBN);
   const int nblk = cin / 64;
   p.nk_all = 9 * nblk;
-  static const int target = env_int("LDNN_CONV_HB_TARGET", 256);  // workgroups to aim for (A/B knob)
+  constexpr int target = 256;  // workgroups to aim for
   int sp = 1;
   if (p.tiles_x < 192) sp = std::min(nblk, std::max(1, (target + p.tiles_x - 1) / p.tiles_x));
   const int bps = (nblk + sp - 1) / sp;  // channel blocks per slice
@@ -3122,7 +3076,7 @@ void set_conv_bn_bwd(int mode) { g_bn_bwd = mode; }
 int get_conv_bn_bwd() { return bn_bwd_env(); }
 
 void set_conv_combine_last(int on) { g_combine_last = on; }
-int get_conv_combine_last() { return combine_last_env(); }
+int get_conv_combine_last() { return g_combine_last; }
 void set_conv_wgrad_ring(int mode) { g_wgrad_ring = mode; }
 int get_conv_halo() { return halo_env(); }
 
@@ -3146,7 +3100,7 @@ S2dPlan plan_s2d(const ConvShape& s) {
   p.Ws = s.Q + 3;
   p.nchunk = (s.Q + 31) / 32;
   p.steps = s.N * s.P * p.nchunk;
-  static const int target = env_int("LDNN_CONV_S2D_TARGET", 512);
+  constexpr int target = 512;
   int slices = std::max(1, std::min(target, p.steps / 8));
   p.steps_per = (p.steps + slices - 1) / slices;
   p.slices = (p.steps + p.steps_per - 1) / p.steps_per;
@@ -3189,8 +3143,7 @@ ConvWorkspace conv2d_lds_workspace(const ConvShape& s, int op) {
 
 hipError_t slab_sum(const float* ws, float* out, int64_t n4, int splits, float beta, hipStream_t st) {
   if (n4 <= 0) return hipSuccess;
-  if (slab_nt_env()) slab_sum_kernel<true><<<(unsigned)((n4 + 31) / 32), 256, 0, st>>>(ws, out, n4, splits, beta);
-  else slab_sum_kernel<false><<<(unsigned)((n4 + 31) / 32), 256, 0, st>>>(ws, out, n4, splits, beta);
+  slab_sum_kernel<true><<<(unsigned)((n4 + 31) / 32), 256, 0, st>>>(ws, out, n4, splits, beta);
   return hipGetLastError();
 }
 
@@ -3292,7 +3245,7 @@ struct PostBatch {
 };
 PostTask slab_bn_task(const float* ws, uint16_t* out, int M, int N, int splits, const BnFin& fin,
                       const BnBwdFuse* bnb) {
-  static const int target = std::max(1, env_int("LDNN_CONV_SLAB_BN_TARGET", 512));
+  constexpr int target = kSlabBnTarget;
   const int G = (N + 63) / 64;
   int ny = std::max(1, std::min({(target + G - 1) / G, (M + 31) / 32, kGrpMax}));
   const int rpb = (M + ny - 1) / ny;
@@ -3338,21 +3291,11 @@ PostTask slab_sum_task(const float* ws, float* out, int64_t n4, int splits, floa
   t.beta = beta;
   return t;
 }
-// LDNN_CONV_POST_MERGE (A/B knob, default 1): 0 launches each post task on its own
+// every post task of a conv step in ONE launch (measured 1-2 % faster than a launch per task,
+// profiles/r5/conv_post_merge_ab.txt)
 hipError_t post_flush(const PostBatch& pb, hipStream_t st) {
   if (pb.n == 0 || pb.blocks == 0) return hipSuccess;
-  static const int merge = env_int("LDNN_CONV_POST_MERGE", 1);
-  if (!merge && pb.n > 1) {
-    for (int k = 0; k < pb.n; ++k) {
-      PostBatch one;
-      one.push(pb.t[k]);
-      const hipError_t e = post_flush(one, st);
-      if (e != hipSuccess) return e;
-    }
-    return hipSuccess;
-  }
-  if (slab_nt_env()) conv_post_kernel<true><<<(unsigned)pb.blocks, 256, 0, st>>>(pb.t[0], pb.t[1], pb.t[2], pb.t[3]);
-  else conv_post_kernel<false><<<(unsigned)pb.blocks, 256, 0, st>>>(pb.t[0], pb.t[1], pb.t[2], pb.t[3]);
+  conv_post_kernel<true><<<(unsigned)pb.blocks, 256, 0, st>>>(pb.t[0], pb.t[1], pb.t[2], pb.t[3]);
   return hipGetLastError();
 }
 }  // namespace
@@ -3377,9 +3320,8 @@ FwdPrep fwd_prep(const ConvShape& s, uint16_t* y, const float* bias, int epi, fl
   LArgs& a = f.a;
   a = base_args(s);
   // slab split-K: the slab pass takes the next BN's statistics (conv_slab_bn), or with
-  // LDNN_CONV_SLAB_BN=0 the BN runs its own statistics pass
   if (bn != nullptr && pl.slab) {
-    if (slab_bn_env() && bn->part != nullptr && bn->tickets != nullptr && s.K % 8 == 0) f.slab_fin = bn;
+    if (bn->part != nullptr && bn->tickets != nullptr && s.K % 8 == 0) f.slab_fin = bn;
     else f.bn_used = false;
     bn = nullptr;
   }
@@ -3519,18 +3461,10 @@ DgradPrep dgrad_prep(const ConvShape& s, uint16_t* dx, float* ws, int* cnt, cons
   d.halo = generic < 2 && !d.hb && halo_takes(s, pl.wm);
   // the BN backward statistics of the BN whose output's gradient dx is: stride-1 dgrads (no
   // class row remap) in the direct / in-launch combine epilogue, or in the slab sum
-  if (bnb != nullptr && bn_bwd_env() && s.stride == 1 && pl.classes == 1 && s.C % 8 == 0) {
-    const bool grp = bnb->fin.part != nullptr && bnb->fin.tickets != nullptr;
-    if (d.slab) {
-      if (slab_bn_env() && grp) d.slab_bnb = bnb;
-    } else if (bn_bwd_env() == 1 && grp) {
-      d.red_bnb = bnb;
-    } else if (bn_bwd_env() == 2) {
-      a.bn_stats = 1;
-      a.bn = bnb->fin;
-      a.bn_x = bnb->x;
-      a.bn_mask = bnb->mask;
-    }
+  if (bnb != nullptr && bn_bwd_env() && s.stride == 1 && pl.classes == 1 && s.C % 8 == 0 &&
+      bnb->fin.part != nullptr && bnb->fin.tickets != nullptr) {
+    if (d.slab) d.slab_bnb = bnb;
+    else d.red_bnb = bnb;
   }
   return d;
 }
@@ -3550,7 +3484,6 @@ void dgrad_post_task(const DgradPrep& d, uint16_t* dx, float* ws, PostBatch& pb,
       if (bn_used) *bn_used = true;
       return;
     }
-    if (bn_used) *bn_used = d.a.bn_stats != 0;
     return;
   }
   if (d.slab_bnb != nullptr) {
@@ -3563,9 +3496,11 @@ void dgrad_post_task(const DgradPrep& d, uint16_t* dx, float* ws, PostBatch& pb,
 
 // after the main kernel: the slab split-K sum (with the BN statistics when taken)
 hipError_t dgrad_post(const DgradPrep& d, uint16_t* dx, float* ws, hipStream_t st, bool* bn_used) {
-  if (!d.slab) {
-    if (bn_used) *bn_used = d.a.bn_stats != 0;
-    return hipSuccess;
+  if (!d.slab) {   // (the BN backward statistics, when taken: one pass over dx)
+    if (d.red_bnb == nullptr) return hipSuccess;
+    PostBatch pb;
+    dgrad_post_task(d, dx, ws, pb, bn_used);
+    return post_flush(pb, st);
   }
   if (d.slab_bnb != nullptr) {
     if (bn_used) *bn_used = true;
@@ -3632,7 +3567,7 @@ WgradPrep wgrad_prep(const ConvShape& s, const WgradPlan& pl, float* dw, float b
   a.f_c = make_fastdiv(s.C);
   a.f_s = make_fastdiv(s.S);
   w.splits = pl.splits;
-  a.xcd_split = w.splits > 1 ? wgrad_xcd_env() : 0;
+  a.xcd_split = w.splits > 1 ? 1 : 0;   // a slice's tiles on one XCD (split_coords)
   w.slab = w.splits > 1 && ws != nullptr;
   if (w.slab) a.ws = ws;  // partial slabs + slab_sum_kernel (else fp32 atomics into a cleared output)
   w.bdy = (size_t)s.N * s.P * s.Q * s.K * 2;
@@ -3647,8 +3582,7 @@ void wgrad_post_task(const WgradPrep& w, float* dw, float beta, float* ws, PostB
 hipError_t wgrad_post(const WgradPrep& w, float* dw, float beta, float* ws, hipStream_t st) {
   if (!w.slab) return hipSuccess;
   const int64_t n4 = (int64_t)w.a.M * w.a.N / 4;
-  if (slab_nt_env()) slab_sum_kernel<true><<<(unsigned)((n4 + 31) / 32), 256, 0, st>>>(ws, dw, n4, w.splits, beta);
-  else slab_sum_kernel<false><<<(unsigned)((n4 + 31) / 32), 256, 0, st>>>(ws, dw, n4, w.splits, beta);
+  slab_sum_kernel<true><<<(unsigned)((n4 + 31) / 32), 256, 0, st>>>(ws, dw, n4, w.splits, beta);
   return hipGetLastError();
 }
 }  // namespace
@@ -3698,8 +3632,7 @@ hipError_t conv2d_wgrad_lds(const ConvShape& s, const uint16_t* dy, const uint16
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || !slab) return e;
     const int64_t n4 = (int64_t)s.K * 9 * s.C / 4;
-    if (slab_nt_env()) slab_sum_kernel<true><<<(unsigned)((n4 + 31) / 32), 256, 0, st>>>(ws, dw, n4, pl.splits, beta);
-    else slab_sum_kernel<false><<<(unsigned)((n4 + 31) / 32), 256, 0, st>>>(ws, dw, n4, pl.splits, beta);
+    slab_sum_kernel<true><<<(unsigned)((n4 + 31) / 32), 256, 0, st>>>(ws, dw, n4, pl.splits, beta);
     return hipGetLastError();
   }
   const WgradPrep wp = wgrad_prep(s, pl, dw, beta, ws);
@@ -3739,18 +3672,18 @@ hipError_t launch_pair(const PairArgs& p, hipStream_t st) {
   conv_pair_kernel<WM0, WN0, OA0, OB0, F0, D0, WM1, WN1, OA1, OB1, F1, D1><<<(unsigned)(p.n0 + n1), 256, 0, st>>>(p);
   return hipGetLastError();
 }
-#define LDNN_DG128 2, 2, DgradA<128, 4, 4>, DgradB<128, 4, 4>, false, true
-#define LDNN_DG256 4, 1, DgradA<256, 8, 4>, DgradB<64, 2, 4>, false, true
-#define LDNN_WG128 2, 2, WgradA<128, 4, 4>, WgradB<128, 4, 4>, true, false
-#define LDNN_WGN 1, 4, WgradA<64, 2, 4>, WgradB<256, 8, 4>, true, false
-#define LDNN_FW128 2, 2, FwdA<128, 4, 4>, WeightKC<128, 4, 4>, false, false
-#define LDNN_FW256 4, 1, FwdA<256, 8, 4>, WeightKC<64, 2, 4>, false, false
+#define DG128 2, 2, DgradA<128, 4, 4>, DgradB<128, 4, 4>, false, true
+#define DG256 4, 1, DgradA<256, 8, 4>, DgradB<64, 2, 4>, false, true
+#define WG128 2, 2, WgradA<128, 4, 4>, WgradB<128, 4, 4>, true, false
+#define WGN 1, 4, WgradA<64, 2, 4>, WgradB<256, 8, 4>, true, false
+#define FW128 2, 2, FwdA<128, 4, 4>, WeightKC<128, 4, 4>, false, false
+#define FW256 4, 1, FwdA<256, 8, 4>, WeightKC<64, 2, 4>, false, false
 
 hipError_t conv2d_bwd_lds(const ConvShape& sd, const uint16_t* dy, const uint16_t* w, uint16_t* dx, float* ws_d,
                           int* cnt_d, const BnBwdFuse* bnb, bool* bn_used, const ConvShape& sw, const uint16_t* x,
                           float* dw, float beta, float* ws_w, hipStream_t st) {
   if (bn_used) *bn_used = false;
-  if (!pair_env() || deep_ring(0) || conv_xf_env() != 0) return hipErrorNotSupported;
+  if (!pair_env() || conv_xf_env() != 0) return hipErrorNotSupported;
   if (sd.K % 64 != 0 || !shape_ok(sd) || sd.N * sd.H * sd.W <= 0) return hipErrorNotSupported;
   if (!shape_ok(sw) || sw.C % 8 != 0 || sw.K % 8 != 0 || (beta != 0.f && beta != 1.f)) return hipErrorNotSupported;
   if (stem_s2d_ok(sw)) return hipErrorNotSupported;
@@ -3778,11 +3711,11 @@ hipError_t conv2d_bwd_lds(const ConvShape& sd, const uint16_t* dy, const uint16_
   p.n0 = (p.gx[0] * p.gy[0] * p.gz[0] + 7) / 8 * 8;
   hipError_t e;
   if (d.pl.wm == 4) {
-    if (pw.narrow) e = launch_pair<LDNN_DG256, LDNN_WGN>(p, st);
-    else e = launch_pair<LDNN_DG256, LDNN_WG128>(p, st);
+    if (pw.narrow) e = launch_pair<DG256, WGN>(p, st);
+    else e = launch_pair<DG256, WG128>(p, st);
   } else {
-    if (pw.narrow) e = launch_pair<LDNN_DG128, LDNN_WGN>(p, st);
-    else e = launch_pair<LDNN_DG128, LDNN_WG128>(p, st);
+    if (pw.narrow) e = launch_pair<DG128, WGN>(p, st);
+    else e = launch_pair<DG128, WG128>(p, st);
   }
   if (e != hipSuccess) return e;
   // the dgrad's slab pass and the wgrad's slab sum in one launch
@@ -3800,7 +3733,7 @@ hipError_t conv2d_fwd2_lds(const ConvShape& s0, const uint16_t* x, const uint16_
                            uint16_t* y1, float* ws1, int* cnt1, const BnFin* bn1, bool* used1, hipStream_t st) {
   if (used0) *used0 = false;
   if (used1) *used1 = false;
-  if (!pair_env() || deep_ring(0) || conv_xf_env() != 0) return hipErrorNotSupported;
+  if (!pair_env() || conv_xf_env() != 0) return hipErrorNotSupported;
   for (const ConvShape* s : {&s0, &s1})
     if (!shape_ok(*s) || s->C % 64 != 0 || s->N * s->P * s->Q <= 0) return hipErrorNotSupported;
   const FwdPrep f0 = fwd_prep(s0, y0, nullptr, EPI_NONE, ws0, cnt0, bn0);
@@ -3823,11 +3756,11 @@ hipError_t conv2d_fwd2_lds(const ConvShape& s0, const uint16_t* x, const uint16_
   p.n0 = (p.gx[0] * p.gy[0] + 7) / 8 * 8;
   hipError_t e;
   if (f0.pl.wm == 4) {
-    if (f1.pl.wm == 4) e = launch_pair<LDNN_FW256, LDNN_FW256>(p, st);
-    else e = launch_pair<LDNN_FW256, LDNN_FW128>(p, st);
+    if (f1.pl.wm == 4) e = launch_pair<FW256, FW256>(p, st);
+    else e = launch_pair<FW256, FW128>(p, st);
   } else {
-    if (f1.pl.wm == 4) e = launch_pair<LDNN_FW128, LDNN_FW256>(p, st);
-    else e = launch_pair<LDNN_FW128, LDNN_FW128>(p, st);
+    if (f1.pl.wm == 4) e = launch_pair<FW128, FW256>(p, st);
+    else e = launch_pair<FW128, FW128>(p, st);
   }
   if (e != hipSuccess) return e;
   if (used0) *used0 = f0.bn_used;
@@ -3842,7 +3775,7 @@ hipError_t conv2d_fwd2_lds(const ConvShape& s0, const uint16_t* x, const uint16_
 // launch (conv_multi_kernel), then the dgrads' slab passes and both wgrads' slab sums in one
 // (conv_post_kernel); hipErrorNotSupported where a GEMM takes another kernel.
 hipError_t conv2d_bwd2_lds(const BwdJob& j0, const BwdJob& j1, const uint16_t* x, hipStream_t st) {
-  if (!pair_env() || deep_ring(0) || conv_xf_env() != 0) return hipErrorNotSupported;
+  if (!pair_env() || conv_xf_env() != 0) return hipErrorNotSupported;
   const BwdJob* js[2] = {&j0, &j1};
   DgradPrep d[2];
   WgradPrep w[2];

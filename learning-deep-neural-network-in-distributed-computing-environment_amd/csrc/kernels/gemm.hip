@@ -548,7 +548,7 @@ hipError_t dispatch_epi(const GemmParams& p, int epi, hipStream_t s) {
   constexpr int T = TILE == 128 ? 128 : 256;
   const int tiles = ((p.M + T - 1) / T) * ((p.N + T - 1) / T);
   dim3 grid(tiles, TILE == 128 ? max(1, p.splitk) : 1);
-#define LDNN_GEMM_CASE(E)                                                                          \
+#define GEMM_EPI_CASE(E)                                                                          \
   case E:                                                                                          \
     if constexpr (TILE == 256) {                                                                   \
       if (p.variant == 2)                                                                          \
@@ -562,12 +562,12 @@ hipError_t dispatch_epi(const GemmParams& p, int epi, hipStream_t s) {
     }                                                                                              \
     break;
   switch (epi) {
-    LDNN_GEMM_CASE(EPI_NONE)
-    LDNN_GEMM_CASE(EPI_BIAS)
-    LDNN_GEMM_CASE(EPI_BIAS_RELU)
-    LDNN_GEMM_CASE(EPI_BIAS_SIGMOID)
-    LDNN_GEMM_CASE(EPI_DRELU)
-    LDNN_GEMM_CASE(EPI_DSIGMOID)
+    GEMM_EPI_CASE(EPI_NONE)
+    GEMM_EPI_CASE(EPI_BIAS)
+    GEMM_EPI_CASE(EPI_BIAS_RELU)
+    GEMM_EPI_CASE(EPI_BIAS_SIGMOID)
+    GEMM_EPI_CASE(EPI_DRELU)
+    GEMM_EPI_CASE(EPI_DSIGMOID)
     case EPI_OPT_SGD:
     case EPI_OPT_ADAM:
       if constexpr (OUT_F32 && TILE == 256) {  // the big weight gradients (plain 2-stage main loop)
@@ -587,7 +587,7 @@ hipError_t dispatch_epi(const GemmParams& p, int epi, hipStream_t s) {
     default:
       return hipErrorInvalidValue;
   }
-#undef LDNN_GEMM_CASE
+#undef GEMM_EPI_CASE
   return hipGetLastError();
 }
 

@@ -709,15 +709,15 @@ hipError_t dispatch_epi(const GemmParams& p, int epi, hipStream_t s) {
     return hipErrorInvalidValue;
   }
   switch (epi) {
-#define LDNN_Q_CASE(E) \
+#define Q_EPI_CASE(E) \
   case E: gemm_kernel<A_KC, B_KC, E, OUT_F32><<<grid, block, 0, s>>>(p); break;
-    LDNN_Q_CASE(EPI_NONE)
-    LDNN_Q_CASE(EPI_BIAS)
-    LDNN_Q_CASE(EPI_BIAS_RELU)
-    LDNN_Q_CASE(EPI_BIAS_SIGMOID)
-    LDNN_Q_CASE(EPI_DRELU)
-    LDNN_Q_CASE(EPI_DSIGMOID)
-#undef LDNN_Q_CASE
+    Q_EPI_CASE(EPI_NONE)
+    Q_EPI_CASE(EPI_BIAS)
+    Q_EPI_CASE(EPI_BIAS_RELU)
+    Q_EPI_CASE(EPI_BIAS_SIGMOID)
+    Q_EPI_CASE(EPI_DRELU)
+    Q_EPI_CASE(EPI_DSIGMOID)
+#undef Q_EPI_CASE
     case EPI_BIAS_RELU_MASK:
       if constexpr (!OUT_F32) {
         gemm_kernel<A_KC, B_KC, EPI_BIAS_RELU_MASK, false><<<grid, block, 0, s>>>(p);

@@ -786,11 +786,8 @@ hipError_t head_bwd(const HeadParams& p, hipStream_t s) {
       p.ldw_rows > 16 || p.nrows_w > 16 || (p.dgrad_epi != EPI_NONE && p.dgrad_epi != EPI_DRELU))
     return hipErrorInvalidValue;
   const int gx = p.K / 64;
-  // ~3 workgroups per CU (the register-bound occupancy); A/B knob LDNN_HEAD_BWD_WGS (total workgroups)
-  static const int target = [] {
-    const char* e = std::getenv("LDNN_HEAD_BWD_WGS");
-    return e ? std::max(64, std::atoi(e)) : 768;
-  }();
+  // ~3 workgroups per CU (the register-bound occupancy; profiles/r5/mlp_head_bwd_grid_ab.jsonl)
+  constexpr int target = 768;
   int gy = std::max(1, std::min(256, target / gx));
   int rpw = (p.B + gy - 1) / gy;
   rpw = (rpw + 63) & ~63;

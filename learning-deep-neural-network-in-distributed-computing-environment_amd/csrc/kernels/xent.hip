@@ -242,10 +242,10 @@ hipError_t softmax_xent(const uint16_t* logits, const int64_t* labels, uint16_t*
   if (vec_ok && ld <= 64) {
     const int g = (B + 255) / 256;
     switch (ld) {
-#define LDNN_XR(L) \
+#define XENT_ROWS_CASE(L) \
       case L: xent_rows_kernel<L><<<g, 256, 0, s>>>(logits, labels, dlogits, stats, dbias, B, C, ld, grad_scale, fin); break;
-      LDNN_XR(8) LDNN_XR(16) LDNN_XR(24) LDNN_XR(32) LDNN_XR(40) LDNN_XR(48) LDNN_XR(56)
-#undef LDNN_XR
+      XENT_ROWS_CASE(8) XENT_ROWS_CASE(16) XENT_ROWS_CASE(24) XENT_ROWS_CASE(32) XENT_ROWS_CASE(40) XENT_ROWS_CASE(48) XENT_ROWS_CASE(56)
+#undef XENT_ROWS_CASE
       default: xent_rows_kernel<64><<<g, 256, 0, s>>>(logits, labels, dlogits, stats, dbias, B, C, ld, grad_scale, fin); break;
     }
     return hipGetLastError();

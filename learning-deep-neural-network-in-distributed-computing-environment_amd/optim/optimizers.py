@@ -20,7 +20,6 @@ from ..ops import _ext
 from ..utils.flat_params import owner_of
 
 
-_LAZY_ZERO = __import__("os").environ.get("LDNN_LAZY_ZERO", "1") != "0"
 
 
 def _refuse_partial_sharded(params):
@@ -156,8 +155,8 @@ class _FlatOptimizer(torch.optim.Optimizer):
         for group in self.param_groups:
             f = self._flat_for_group(group)
             if f is not None:
-                # (set_to_none: the next backward's first write overwrites; LDNN_LAZY_ZERO=0 fills)
-                f.zero_grad(lazy=set_to_none and _LAZY_ZERO)
+                # (set_to_none: the next backward's first write overwrites instead of a fill)
+                f.zero_grad(lazy=set_to_none)
             else:
                 for p in group["params"]:
                     if p.grad is not None:

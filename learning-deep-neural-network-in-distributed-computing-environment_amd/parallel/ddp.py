@@ -39,14 +39,8 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 
-import os
-
 from ..utils.flat_params import FlatParams
 from .comm import SUM, Comm, default_comm
-
-# per-bucket optimizer order of GraphedDPStep: "ready" (reduce-scatter completion order,
-# gathers after the last update) or "forward" (round 4: each gather right after its update)
-_OPT_ORDER = os.environ.get("LDNN_DP_OPT_ORDER", "ready")
 
 
 def _cast_into(dst: torch.Tensor, src: torch.Tensor):
@@ -324,8 +318,6 @@ class GradBucketer:
         own bucket's collective; the weight all-gathers follow in forward order."""
         sh = [i for i, b in enumerate(self.buckets) if b["sharded"]]
         rep = [i for i, b in enumerate(self.buckets) if not b["sharded"]]
-        if _OPT_ORDER == "forward":   # (round-4 order, A/B only: tail first, then forward order)
-            return rep + sh[::-1]
         return sh + rep
 
     def issue_gather(self, i):

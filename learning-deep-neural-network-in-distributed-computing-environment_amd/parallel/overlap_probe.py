@@ -226,12 +226,6 @@ def _tail(fn, n):
     torch.cuda.synchronize()
 
 
-def _opt_order():
-    from . import ddp
-
-    return ddp._OPT_ORDER
-
-
 def _measure_sharded(model_name, batch, bucket_mb, reps, steps, rounds, blocks, world, optimizer, tail_steps=0,
                      gbps=300.0, comm_dtype="fp32"):
     import ldnn
@@ -316,7 +310,7 @@ def _measure_sharded(model_name, batch, bucket_mb, reps, steps, rounds, blocks, 
             "bucket_mb_each": [round((b["end"] - b["begin"]) * 4 / 2**20, 2) for b in bk.buckets],
             "segments": gd.n_segments, "forward_waits": sum(1 for w in gd.waits if w),
             "standin_reps": comm.standin.reps, "standin_blocks": comm.standin.blocks,
-            "standin_calibration": comm.standin.calibration, "opt_order": _opt_order(),
+            "standin_calibration": comm.standin.calibration,
             **{k: round(v, 4) for k, v in best.items()}, "hidden_ms": round(hidden, 4),
             "exposed_ms": round(best["with_standin_ms"] - best["single_ms"], 4),
             "hidden_fraction": round(hidden / max(best["standin_alone_ms"], 1e-9), 3)}

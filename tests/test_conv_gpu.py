@@ -471,19 +471,13 @@ def test_fixed_summer_split_k_combine_matches_last_arrival(N, C, H, K, stride):
                                      (8, 512, 7, 512), (5, 192, 9, 256)])
 @pytest.mark.parametrize("relu", [True, False])
 def test_dgrad_takes_bn_backward_statistics(N, C, H, K, relu):
-    """A stride-1 dgrad whose dx is the gradient of a training BN(+ReLU)'s output accumulates that
-    BN's backward statistics in its epilogue (direct, in-launch combine or slab sum) and finalizes
-    them: dx has the bits of the plain dgrad, and the BN backward's apply pass alone
-    (stats_ready) gives the dx / dgamma / dbeta of the BN's own reduce; a repeat (accumulators and
-    tickets left clear) agrees."""
+    """A stride-1 dgrad whose dx is the gradient of a training BN(+ReLU)'s output takes that BN's
+    backward statistics (in its slab split-K sum, or in one pass over dx right after an unsplit /
+    in-launch-combine dgrad) and finalizes them: dx has the bits of the plain dgrad, and the BN
+    backward's apply pass alone (stats_ready) gives the dx / dgamma / dbeta of the BN's own reduce;
+    a repeat (accumulators and tickets left clear) agrees."""
     torch.manual_seed(31)
-    Cc = _ext.C()
-    old_mode = Cc.get_conv_bn_bwd()
-    Cc.set_conv_bn_bwd(2)   # the epilogue forms too (the default takes the slab sums only)
-    try:
-        _dgrad_bn_stats_case(Cc, N, C, H, K, relu)
-    finally:
-        Cc.set_conv_bn_bwd(old_mode)
+    _dgrad_bn_stats_case(_ext.C(), N, C, H, K, relu)
 
 
 def _dgrad_bn_stats_case(Cc, N, C, H, K, relu):
