@@ -139,6 +139,137 @@ class ShardProbeComm:
         return None
 
 
+class _JoinAll:
+    def __init__(self, joins):
+        self.joins = [j for j in joins if j is not None]
+
+    def wait(self):
+        for j in self.joins:
+            j.wait()
+
+
+class P2PProbeComm:
+    """A world-of-``world`` stand-in for per-step data parallelism on ONE GPU without sharding:
+    ``gossip`` 1 / 2 (DataParallel(gossip=...), BR/communication.py:5-62, BDR/communication.py:5-77)
+    or 0 (the equal all-reduce).  Every collective is replaced by stand-in copies with RCCL's
+    stream behaviour: a gossip exchange of a bucket is, per neighbour, a copy of the bucket at
+    ~one xGMI link's bandwidth (``link_gbps``) on that neighbour's own stream -- the ring and the
+    double ring use one resp. two links side by side -- and an 8-rank ring all-reduce moves
+    2 (N-1)/N of the bucket at ~``bus_gbps``.  The post-collective work (the fused neighbour mix of
+    gossip) runs for real on the received buffers."""
+
+    device_collectives = True
+
+    def __init__(self, device, world: int = 8, link_gbps: float = 150.0, bus_gbps: float = 300.0):
+        from .comm import Comm
+
+        self._rec = Comm()
+        self.rank, self.world_size = 0, int(world)
+        self.links = [StandInComm(device, 1, 0, link_gbps), StandInComm(device, 1, 0, link_gbps)]
+        self.bus = StandInComm(device, 1, 0, bus_gbps)
+        self.bus.reps = 2
+        self.enabled = True
+
+    def record(self, *a, **k):
+        return self._rec.record(*a, **k)
+
+    def schedule_digest(self):
+        return self._rec.schedule_digest()
+
+    def sendrecv(self, sends, recvs, async_op=False):
+        if not self.enabled:
+            return None
+        return _JoinAll([self.links[k](("p2p", k, rt.data_ptr()), rt.view(-1)) for k, (rt, _) in enumerate(recvs)])
+
+    def all_reduce(self, t, op="sum", async_op=False):
+        if not self.enabled:
+            return None
+        n = t.numel() * (self.world_size - 1) // self.world_size // 8 * 8
+        v = t.view(-1)[:max(n, 8)]
+        return self.bus(("ar", t.data_ptr()), v if v.dtype == torch.float32 else v.view(torch.float32))
+
+    def broadcast(self, t, src=0):
+        return None
+
+    def barrier(self):
+        return None
+
+
+def measure_gossip(model_name: str = "enhanced_cnn", batch: int = 64, world: int = 8, bucket_mb: float = 32.0,
+                   optimizer: str = "adam", steps: int = 20, rounds: int = 3, link_gbps: float = 150.0,
+                   bus_gbps: float = 300.0) -> list:
+    """The graphed per-step DP step (GraphedDPStep, segmented: each bucket's exchange issued between
+    the backward's graph links) with the all-reduce (gossip 0), the ring (1) and the double ring (2)
+    on a P2PProbeComm world: one row per topology -- the chain with every collective a no-op, the
+    step with the stand-ins, the stand-ins alone back to back, and the exposed part."""
+    import ldnn
+    from ldnn.data.datasets import SHAPES
+    from ldnn.models import CrossEntropyLoss, build_model, dataset_for, xavier_init
+    from ldnn.optim import SGD, Adam
+    from ldnn.parallel.ddp import DataParallel
+    from ldnn.train.graphed import GraphedDPStep
+
+    dev = torch.device("cuda", torch.cuda.current_device())
+    shape = SHAPES[dataset_for(model_name)]
+    nc = 1000 if model_name == "resnet18" else 10
+    g = torch.Generator(device=dev).manual_seed(0)
+    x = torch.randn(batch, *shape, device=dev, generator=g).bfloat16()
+    y = torch.randint(0, nc, (batch,), device=dev, generator=g)
+    crit = CrossEntropyLoss()
+    rows = []
+    for gossip in (0, 1, 2):
+        torch.manual_seed(0)
+        m = build_model(model_name)
+        xavier_init(m)
+        ldnn.prepare(m, dev)
+        comm = P2PProbeComm(dev, world, link_gbps, bus_gbps)
+        dp = DataParallel(m, comm, bucket_cap_mb=bucket_mb, broadcast_init=False, gossip=gossip)
+        o = SGD(m.parameters(), lr=0.01, momentum=0.9) if optimizer == "sgd" else Adam(m.parameters(), lr=1e-3)
+        o.zero_grad()
+        crit(dp(x), y).backward()
+        dp.finish_gradient_sync()
+        o.step()
+        gd = GraphedDPStep(dp, crit, o, x, y)
+        bk = dp.bucketer
+
+        def chain_only():
+            comm.enabled = False
+            try:
+                gd(x, y)
+            finally:
+                comm.enabled = True
+
+        def standin_alone():
+            js = [bk.collective(i) for i in range(len(bk.buckets))]
+            for j in js:
+                if j is not None:
+                    j.wait()
+
+        fns = {"chain_ms": chain_only, "with_standin_ms": lambda: gd(x, y), "standin_alone_ms": standin_alone}
+        for f in fns.values():
+            for _ in range(3):
+                f()
+        best = {k: 1e9 for k in fns}
+        for _ in range(rounds):
+            for k, f in fns.items():
+                best[k] = min(best[k], _timed(f, steps))
+        exposed = best["with_standin_ms"] - best["chain_ms"]
+        rows.append({"model": model_name, "batch": batch, "optimizer": optimizer,
+                     "topology": {0: "allreduce", 1: "ring", 2: "double_ring"}[gossip],
+                     "mode": f"graphed per-step DP, world {world} stand-in (links {link_gbps:.0f} GB/s, "
+                             f"all-reduce bus {bus_gbps:.0f} GB/s)", "buckets": len(bk.buckets),
+                     "segments": gd.n_segments, **{k: round(v, 4) for k, v in best.items()},
+                     "exposed_ms": round(exposed, 4),
+                     "hidden_fraction": round(1.0 - exposed / max(best["standin_alone_ms"], 1e-9), 3),
+                     "link_calibration": comm.links[0].calibration, "bus_calibration": comm.bus.calibration})
+        del gd, dp, o, m
+        torch.cuda.empty_cache()
+    base = rows[0]["with_standin_ms"]
+    for r in rows:
+        r["vs_allreduce_step"] = round(r["with_standin_ms"] / base, 4)
+    return rows
+
+
 def _timed(fn, steps):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -440,10 +571,16 @@ def main():
     ap.add_argument("--optimizer", choices=["sgd", "adam"], default="sgd")
     ap.add_argument("--grad-comm", choices=["fp32", "bf16"], default="bf16",
                     help="gradient collective dtype of the sharded step")
+    ap.add_argument("--gossip", action="store_true",
+                    help="per-step all-reduce vs ring vs double-ring gossip rows (P2PProbeComm, world --shard or 8)")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--tail-steps", type=int, default=0, help="then this many overlapped steps after an idle gap "
                     "(kernel-trace timelines: scripts/probe_timeline.py)")
     a = ap.parse_args()
+    if a.gossip:
+        for row in measure_gossip(a.model, a.batch, a.shard or 8, a.bucket_mb, a.optimizer, a.steps, a.rounds):
+            print(json.dumps(row), flush=True)
+        return
     if a.model == "mlp3":   # the headline engine (StaticMLPEngine), sharded at world --shard (default 8)
         print(json.dumps(measure_mlp_sharded(a.shard or 8, a.batch if a.batch != 64 else 16384, reps=a.reps,
                                              blocks=a.blocks, steps=a.steps, rounds=a.rounds,
