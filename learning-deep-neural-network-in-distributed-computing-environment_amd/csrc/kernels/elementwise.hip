@@ -190,6 +190,45 @@ __global__ __launch_bounds__(256) void nchw_to_nhwc_kernel(const T* __restrict__
   reinterpret_cast<u16x8*>(dst)[i] = o;
 }
 
+// The same for the usual CNN input (<= 8 channels -> one 8-channel group, H*W % 4 == 0): a thread
+// converts 4 consecutive pixels of one image -- per channel one 16-B (fp32) / 8-B (bf16) load
+// instead of four 4 / 2-B ones, four 16-B stores in a row, 32-bit index math (the 64-bit divisions
+// of the generic kernel are its VALU cost): the ResNet-18 b256 input staging is 282 MB of traffic.
+template <typename T>
+__global__ __launch_bounds__(256) void nchw_to_nhwc4_kernel(const T* __restrict__ src, bf16_t* __restrict__ dst,
+                                                            int npix4, int C, int HW,
+                                                            const uint2* __restrict__ esrc, uint2* __restrict__ edst,
+                                                            int64_t e8) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < e8) edst[i] = esrc[i];   // a batch's labels staged in the same launch (8-B pieces)
+  if (i >= npix4) return;
+  const int pix = i * 4;
+  const int n = pix / HW;
+  const int hw = pix - n * HW;
+  const T* s = src + (size_t)n * C * HW + hw;
+  u16x8 o[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) o[k] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    if (c >= C) break;
+    if constexpr (sizeof(T) == 4) {
+      const floatx4 v = *reinterpret_cast<const floatx4*>(s + (size_t)c * HW);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) o[k][c] = f2bf(v[k]);
+    } else {
+      const uint2 v = *reinterpret_cast<const uint2*>(s + (size_t)c * HW);
+      o[0][c] = (uint16_t)(v.x & 0xffffu);
+      o[1][c] = (uint16_t)(v.x >> 16);
+      o[2][c] = (uint16_t)(v.y & 0xffffu);
+      o[3][c] = (uint16_t)(v.y >> 16);
+    }
+  }
+  u16x8* d = reinterpret_cast<u16x8*>(dst) + pix;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) d[k] = o[k];
+}
+
 // out[c][r] = in[r][c], 64 x 64 tiles.  The tile goes to LDS as whole 128-B rows (16-B chunks
 // XOR-swizzled by row, rows 8 apart shifted by 4 more chunks) and comes back COLUMN-wise through
 // ds_read_b64_tr_b16 (per 16-lane group: 4 rows x 16 columns, lane i receives column i):
@@ -348,6 +387,15 @@ hipError_t nchw_to_nhwc(const void* src, bool src_f32, uint16_t* dst, int N, int
   const unsigned g = (unsigned)((std::max(total, e8) + 255) / 256);
   const uint2* es = static_cast<const uint2*>(extra_src);
   uint2* ed = static_cast<uint2*>(extra_dst);
+  if (groups == 1 && HW % 4 == 0 && (int64_t)N * HW < (int64_t)1 << 30 && ((uintptr_t)src & 15) == 0) {
+    const int npix4 = N * HW / 4;
+    const unsigned g4 = (unsigned)((std::max((int64_t)npix4, e8) + 255) / 256);
+    if (src_f32)
+      nchw_to_nhwc4_kernel<float><<<g4, 256, 0, s>>>(static_cast<const float*>(src), dst, npix4, C, HW, es, ed, e8);
+    else
+      nchw_to_nhwc4_kernel<bf16_t><<<g4, 256, 0, s>>>(static_cast<const bf16_t*>(src), dst, npix4, C, HW, es, ed, e8);
+    return hipGetLastError();
+  }
   if (src_f32)
     nchw_to_nhwc_kernel<float><<<g, 256, 0, s>>>(static_cast<const float*>(src), dst, total, C, HW, groups, es, ed, e8);
   else

@@ -128,16 +128,23 @@ def test_lds_fast_path_matches_generic_kernel(N, C, H, W, K, R, st, pad):
     assert torch.equal(y0, y1) and torch.equal(dx0, dx1)
 
 
-@pytest.mark.parametrize("dtype,C,cp", [(torch.float32, 3, 8), (torch.bfloat16, 3, 8), (torch.float32, 16, 16),
-                                        (torch.bfloat16, 20, 32)])
-def test_nchw_to_nhwc_pad(dtype, C, cp):
-    """Native NCHW -> NHWC bf16 conversion with zeroed pad channels == permute + pad."""
-    x = torch.randn(3, C, 13, 17, device="cuda").to(dtype)
-    out = torch.full((3, 13, 17, cp), 7.0, device="cuda", dtype=torch.bfloat16)
-    _ext.C().nchw_to_nhwc(x, out)
-    ref = torch.zeros(3, 13, 17, cp, device="cuda", dtype=torch.bfloat16)
+@pytest.mark.parametrize("dtype,C,cp,H,W", [(torch.float32, 3, 8, 13, 17), (torch.bfloat16, 3, 8, 13, 17),
+                                            (torch.float32, 16, 16, 13, 17), (torch.bfloat16, 20, 32, 13, 17),
+                                            # H*W % 4 == 0, <= 8 channels: the 4-pixels-per-thread kernel
+                                            (torch.float32, 3, 8, 12, 16), (torch.bfloat16, 3, 8, 32, 32),
+                                            (torch.bfloat16, 1, 8, 28, 28), (torch.float32, 8, 8, 6, 6)])
+def test_nchw_to_nhwc_pad(dtype, C, cp, H, W):
+    """Native NCHW -> NHWC bf16 conversion with zeroed pad channels == permute + pad (and the
+    labels copied in the same launch)."""
+    x = torch.randn(3, C, H, W, device="cuda").to(dtype)
+    out = torch.full((3, H, W, cp), 7.0, device="cuda", dtype=torch.bfloat16)
+    y = torch.randint(0, 10, (6,), device="cuda")
+    ys = torch.full_like(y, -1)
+    _ext.C().nchw_to_nhwc(x, out, y, ys)
+    ref = torch.zeros(3, H, W, cp, device="cuda", dtype=torch.bfloat16)
     ref[..., :C] = x.permute(0, 2, 3, 1).to(torch.bfloat16)
     assert torch.equal(out, ref)
+    assert torch.equal(ys, y)
 
 
 @pytest.mark.parametrize("N,C,H,W,K", [(2, 64, 56, 56, 64), (2, 128, 28, 28, 128), (3, 256, 14, 14, 256),

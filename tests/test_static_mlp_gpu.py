@@ -113,24 +113,29 @@ def test_multirank_static_engine_gloo_two_ranks_one_gpu(nproc, extra):
     assert "STATIC_DP_OK" in r.stdout and "REPLICAS_IDENTICAL" in r.stdout, r.stdout[-3000:]
 
 
-@pytest.mark.parametrize("opt", ["sgd", "adam"])
-def test_sharded_optimizer_path_on_rccl_single_rank(opt, tmp_path):
+@pytest.mark.parametrize("opt,comm", [("sgd", None), ("adam", None), ("sgd", torch.bfloat16)])
+def test_sharded_optimizer_path_on_rccl_single_rank(opt, comm, tmp_path):
     """The reduce-scatter / sharded-optimizer / in-place all-gather path on a real RCCL
     communicator (world 1, forced), graphs on, several buckets: identical to the
-    single-segment engine."""
+    single-segment engine.  comm bf16: the gradient buckets staged in bf16 (the 4096-wide
+    layer's wgrad writes bf16 directly, the rest is cast) and reduce-scattered in bf16 --
+    equal to the fp32 engine up to the gradients' bf16 rounding."""
     import torch.distributed as dist
 
     store = dist.FileStore(str(tmp_path / "store"), 1)
     dist.init_process_group("nccl", store=store, rank=0, world_size=1, device_id=torch.device("cuda:0"))
     try:
         torch.manual_seed(0)
-        B = 512
-        m1, m2 = mlp3(784, 1024, 10), mlp3(784, 1024, 10)
+        B, H = (512, 1024) if comm is None else (512, 4096)
+        m1, m2 = mlp3(784, H, 10), mlp3(784, H, 10)
         m2.load_state_dict(m1.state_dict())
         cfg = OptimConfig(opt, lr=0.05 if opt == "sgd" else 1e-3, momentum=0.9)
-        e1 = StaticMLPEngine(m1, B, cfg, use_graphs=True, shard_optimizer=True, bucket_cap_elems=1 << 18)
+        e1 = StaticMLPEngine(m1, B, cfg, use_graphs=True, shard_optimizer=True,
+                             bucket_cap_elems=(1 << 18) if comm is None else (8 << 20), comm_dtype=comm)
         e2 = StaticMLPEngine(m2, B, cfg, use_graphs=True)
         assert e1.shard and len(e1.buckets) >= 2
+        if comm is not None:   # the 4096 x 4096 wgrad is a plain GEMM: its bf16 output goes straight to the stage
+            assert e1.comm_bf16 and e1.dWb[1] is not None
         g = torch.Generator(device="cuda").manual_seed(4)
         for step in range(6):
             x = torch.randn(B, 784, device="cuda", generator=g).bfloat16()
@@ -141,7 +146,10 @@ def test_sharded_optimizer_path_on_rccl_single_rank(opt, tmp_path):
         e1.gather_master()
         torch.cuda.synchronize()
         for p, q in zip(m1.parameters(), m2.parameters()):
-            torch.testing.assert_close(p.detach(), q.detach(), rtol=1e-5, atol=1e-6)
+            if comm is None:
+                torch.testing.assert_close(p.detach(), q.detach(), rtol=1e-5, atol=1e-6)
+            else:   # 6 SGD steps on bf16-rounded gradients
+                torch.testing.assert_close(p.detach(), q.detach(), rtol=1e-2, atol=2e-3 * q.abs().max().item())
         assert torch.equal(e1.flat.shadow, e1.flat.master.bfloat16())
     finally:
         dist.destroy_process_group()
