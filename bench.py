@@ -475,6 +475,8 @@ def main():
     rec["per_gpu_local_ms"] = round(local_s / args.steps * 1e3, 4)
     rec["scaling_efficiency"] = round(local_s / el, 4)
     rec["rccl_ranks"] = n if ctx.backend == "nccl" else 0
+    from ldnn.ops import _ext
+    rec["native_build"] = _ext.build_info()   # which _C.so ran, and whether it matches this tree's sources
     rec.update(extra)
     if not args.no_configs:
         rec["configs"] = run_configs(ctx, CNN_CONFIGS, run_cnn)

@@ -4,7 +4,11 @@ No hipify and no torch JIT cache: every `.hip` kernel file is compiled by
 `hipcc --offload-arch=gfx950` straight from CDNA4 source, the pybind layer
 (`bindings.cpp`) is compiled against the installed torch headers, and the
 objects are linked into `<package>/_C.so`, which travels with the repo
-snapshot to the GPU box.  Rebuilds are incremental (mtime based).
+snapshot to the GPU box.  Rebuilds are incremental (mtime based).  Every link
+also writes `<package>/_C.build.json` (sha256 over the sources it was built
+from, arch, hipcc version); `ops/_ext.build_info()` compares it with the tree
+it is imported from, and `bench.py` / `smoke()` report the result, so a stale
+`_C.so` is visible in every record.
 
 Usage:  python -m <pkg>.csrc.build   or   python <pkg>/csrc/build.py [-v] [--force]
 """
@@ -12,6 +16,8 @@ from __future__ import annotations
 
 import concurrent.futures as cf
 import glob
+import hashlib
+import json
 import os
 import subprocess
 import sys
@@ -22,6 +28,7 @@ PKG_DIR = os.path.dirname(HERE)
 REPO = os.path.dirname(PKG_DIR)
 BUILD_DIR = os.path.join(REPO, "build", "ldnn_C")
 OUT = os.path.join(PKG_DIR, "_C.so")
+INFO = os.path.join(PKG_DIR, "_C.build.json")
 ARCH = os.environ.get("LDNN_OFFLOAD_ARCH", "gfx950")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 HIPCC = os.path.join(ROCM, "bin", "hipcc")
@@ -40,6 +47,37 @@ def _torch_paths():
 def _deps(path):
     headers = glob.glob(os.path.join(HERE, "include", "*.h"))
     return [path] + headers
+
+
+def sources() -> list[str]:
+    """Every file the extension is compiled from (kernels, bindings, headers)."""
+    return sorted(glob.glob(os.path.join(HERE, "kernels", "*.hip")) + glob.glob(os.path.join(HERE, "include", "*.h"))
+                  + [os.path.join(HERE, "bindings.cpp")])
+
+
+def source_digest() -> str:
+    h = hashlib.sha256()
+    for f in sources():
+        h.update(os.path.relpath(f, HERE).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+        h.update(b"\0")
+    return h.hexdigest()
+
+
+def _write_info():
+    try:
+        ver = subprocess.run([HIPCC, "--version"], capture_output=True, text=True).stdout
+        ver = next((ln.strip() for ln in ver.splitlines() if "HIP version" in ln), ver.strip()[:80])
+    except OSError:
+        ver = "unknown"
+    import datetime
+
+    info = {"sources_sha256": source_digest(), "n_sources": len(sources()), "arch": ARCH, "hipcc": ver,
+            "built_utc": datetime.datetime.now(datetime.timezone.utc).strftime("%Y-%m-%dT%H:%M:%SZ")}
+    with open(INFO + ".tmp", "w") as f:
+        json.dump(info, f)
+    os.replace(INFO + ".tmp", INFO)
 
 
 def _stale(obj, deps):
@@ -102,6 +140,9 @@ def build(verbose: bool = False, force: bool = False, jobs: int | None = None) -
                  f"-L{ROCM}/lib", f"-Wl,-rpath,{ROCM}/lib", "-lrocprofiler-sdk-roctx"]
         _run(link, verbose)
         os.replace(OUT + ".tmp", OUT)
+        _write_info()
+    elif not os.path.exists(INFO):
+        _write_info()   # (an up-to-date .so from before the provenance file existed)
     return OUT
 
 

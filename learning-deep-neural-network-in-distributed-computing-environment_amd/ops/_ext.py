@@ -47,6 +47,29 @@ def use_native(t: torch.Tensor) -> bool:
     return True
 
 
+def build_info() -> dict:
+    """Provenance of the loaded `_C.so`: the record csrc/build.py wrote at link time and
+    whether its source digest equals the sources in this tree (`matches_sources`)."""
+    import importlib.util
+    import json
+
+    pkg = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    info: dict = {"loaded": _C is not None, "so": getattr(_C, "__file__", None)}
+    try:
+        with open(os.path.join(pkg, "_C.build.json")) as f:
+            info.update(json.load(f))
+        spec = importlib.util.spec_from_file_location("_ldnn_build", os.path.join(pkg, "csrc", "build.py"))
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        info["matches_sources"] = info.get("sources_sha256") == mod.source_digest()
+    except OSError as e:
+        info["matches_sources"] = None
+        info["error"] = f"no build record: {e.__class__.__name__}"
+    if "sources_sha256" in info:
+        info["sources_sha16"] = info.pop("sources_sha256")[:16]
+    return info
+
+
 def check_gpu_native() -> None:
     """Fail loudly on a GPU host without the native extension."""
     if torch.cuda.is_available() and not _DISABLED:

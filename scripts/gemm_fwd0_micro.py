@@ -42,7 +42,7 @@ def main():
     mask = torch.empty(M, N // 8, device="cuda", dtype=torch.uint8)
     rows = []
     cases = [("gemm_q 256x256 4-wave, bias+relu", dict(tile=256, variant=32), 2, None),
-             ("gemm_q 256x256 4-wave, bias+relu+mask (engine)", dict(tile=256, variant=32), 8, mask),
+             ("gemm_q 256x256 4-wave, bias+relu+mask (engine)", dict(tile=256, variant=32), 2, mask),
              ("k256 256x256 8-wave, bias+relu", dict(tile=256, variant=1), 2, None),
              ("k128 128x128 4-wave x2/CU, bias+relu", dict(tile=128), 2, None)]
     for rep in range(2):
