@@ -1466,10 +1466,17 @@ bool bn_pool_fwd(const at::Tensor& x, const at::Tensor& y, const at::Tensor& arg
                  const c10::optional<at::Tensor>& gamma, const c10::optional<at::Tensor>& beta,
                  const c10::optional<at::Tensor>& running_mean, const c10::optional<at::Tensor>& running_var,
                  const at::Tensor& save_mean, const at::Tensor& save_invstd, const at::Tensor& ws, double eps,
-                 double momentum, const c10::optional<at::Tensor>& num_batches, bool stats_ready, int64_t pad) {
+                 double momentum, const c10::optional<at::Tensor>& num_batches, bool stats_ready, int64_t pad,
+                 const c10::optional<at::Tensor>& xam) {
   check_dev(x, at::kBFloat16, "x");
   check_dev(y, at::kBFloat16, "y");
   check_dev(argmax, at::kByte, "argmax");
+  uint16_t* xam_p = nullptr;
+  if (xam.has_value()) {
+    check_dev(*xam, at::kBFloat16, "xam");
+    TORCH_CHECK(xam->sizes() == y.sizes() && xam->is_contiguous(), "bn_pool_fwd: xam must be laid out as y");
+    xam_p = bf16_mut(*xam);
+  }
   TORCH_CHECK(x.dim() == 4 && y.dim() == 4 && x.is_contiguous() && y.is_contiguous() && argmax.is_contiguous() &&
                   argmax.sizes() == y.sizes() && y.size(0) == x.size(0) && y.size(3) == x.size(3),
               "bn_pool_fwd: dense NHWC x / y / argmax");
@@ -1496,7 +1503,7 @@ bool bn_pool_fwd(const at::Tensor& x, const at::Tensor& y, const at::Tensor& arg
   uint8_t* am = argmax.data_ptr<uint8_t>();
   TORCH_CHECK(((uintptr_t)am & 7) == 0, "bn_pool_fwd: argmax must be 8-B aligned");
   check(ldnn::bn_maxpool_forward(a, (int)N, (int)H, (int)W, (int)y.size(1), (int)y.size(2), (int)pad, bf16_mut(y),
-                                 am, stats_ready, cur_stream(x)),
+                                 am, stats_ready, cur_stream(x), xam_p),
         "bn_maxpool_forward (3x3/2 window, C/8 dividing 256)");
   return true;
 }
@@ -1505,7 +1512,7 @@ void bn_pool_bwd(const at::Tensor& x, const at::Tensor& dy, const at::Tensor& ar
                  const c10::optional<at::Tensor>& gamma, const at::Tensor& save_mean, const at::Tensor& save_invstd,
                  const at::Tensor& ws, const c10::optional<at::Tensor>& dgamma,
                  const c10::optional<at::Tensor>& dbeta, bool grad_assign, const c10::optional<at::Tensor>& dy2,
-                 int64_t pad) {
+                 int64_t pad, const c10::optional<at::Tensor>& xam) {
   check_dev(x, at::kBFloat16, "x");
   check_dev(dy, at::kBFloat16, "dy");
   check_dev(dx, at::kBFloat16, "dx");
@@ -1531,9 +1538,15 @@ void bn_pool_bwd(const at::Tensor& x, const at::Tensor& dy, const at::Tensor& ar
   }
   const uint8_t* am = argmax.data_ptr<uint8_t>();
   TORCH_CHECK(((uintptr_t)am & 7) == 0, "bn_pool_bwd: argmax must be 8-B aligned");
+  const uint16_t* xam_p = nullptr;
+  if (xam.has_value()) {
+    check_dev(*xam, at::kBFloat16, "xam");
+    TORCH_CHECK(xam->sizes() == dy.sizes() && xam->is_contiguous(), "bn_pool_bwd: xam must be laid out as dy");
+    xam_p = bf16_ptr(*xam);
+  }
   check(ldnn::bn_maxpool_backward(a, (int)N, (int)H, (int)W, (int)dy.size(1), (int)dy.size(2), (int)pad,
                                   bf16_ptr(dy), am, bf16_mut(dx), fptr_opt(dgamma, C, "dgamma"),
-                                  fptr_opt(dbeta, C, "dbeta"), cur_stream(x), grad_assign),
+                                  fptr_opt(dbeta, C, "dbeta"), cur_stream(x), grad_assign, xam_p),
         "bn_maxpool_backward");
 }
 
@@ -1991,11 +2004,11 @@ PYBIND11_MODULE(_C, m) {
         py::arg("x"), py::arg("y"), py::arg("argmax"), py::arg("gamma"), py::arg("beta"), py::arg("running_mean"),
         py::arg("running_var"), py::arg("save_mean"), py::arg("save_invstd"), py::arg("ws"), py::arg("eps"),
         py::arg("momentum"), py::arg("num_batches") = py::none(), py::arg("stats_ready") = false,
-        py::arg("pad") = 1);
+        py::arg("pad") = 1, py::arg("xam") = py::none());
   m.def("bn_pool_bwd", &bn_pool_bwd, "backward of bn_pool_fwd: dx, dgamma / dbeta", py::arg("x"), py::arg("dy"),
         py::arg("argmax"), py::arg("dx"), py::arg("gamma"), py::arg("save_mean"), py::arg("save_invstd"),
         py::arg("ws"), py::arg("dgamma"), py::arg("dbeta"), py::arg("grad_assign") = false,
-        py::arg("dy2") = py::none(), py::arg("pad") = 1);
+        py::arg("dy2") = py::none(), py::arg("pad") = 1, py::arg("xam") = py::none());
   m.def("gap_fwd", &gap_fwd);
   m.def("gap_bwd", &gap_bwd);
   m.def("set_conv_combine_last", &ldnn::set_conv_combine_last,

@@ -279,11 +279,13 @@ hipError_t bn_dual_backward(const BnArgs& a, const BnArgs& b, const uint16_t* dy
 // stats_ready: scale / shift already in a.ws (the producing conv's epilogue finalized them).
 // Needs C / 8 to divide 256.
 hipError_t bn_maxpool_forward(const BnArgs& a, int N, int H, int W, int P, int Q, int pad, uint16_t* y,
-                              uint8_t* arg, bool stats_ready, hipStream_t s);
-// its backward: dx [N][H][W][C] from the pooled gradient dy (+ a.dy2), dgamma / dbeta as bn_backward
+                              uint8_t* arg, bool stats_ready, hipStream_t s, uint16_t* xam = nullptr);
+// (xam: optional [N][P][Q][C] output, the BN input at each argmax -- what the backward statistics read)
+// its backward: dx [N][H][W][C] from the pooled gradient dy (+ a.dy2), dgamma / dbeta as bn_backward;
+// with the forward's xam the statistics pass reads the pooled-size xam / dy / argmax instead of x
 hipError_t bn_maxpool_backward(const BnArgs& a, int N, int H, int W, int P, int Q, int pad, const uint16_t* dy,
                                const uint8_t* arg, uint16_t* dx, float* dgamma, float* dbeta, hipStream_t s,
-                               bool grad_assign = false);
+                               bool grad_assign = false, const uint16_t* xam = nullptr);
 hipError_t pool2d_fwd(const uint16_t* x, uint16_t* y, uint8_t* argmax, int N, int H, int W, int C, int P, int Q,
                       int R, int S, int stride, int pad, bool is_max, hipStream_t s, int nchw_c = 0);
 // nchw_c > 0: y (fwd) / dy (bwd) is a dense NCHW tensor of the first nchw_c channels (argmax stays NHWC)

@@ -806,8 +806,8 @@ template <int PAD>
 __global__ __launch_bounds__(256) void bn_maxpool_fwd_kernel(const bf16_t* __restrict__ x,
                                                              const float* __restrict__ scale,
                                                              const float* __restrict__ shift, bf16_t* __restrict__ y,
-                                                             uint8_t* __restrict__ arg, int N, int H, int W, int C,
-                                                             int P, int Q) {
+                                                             uint8_t* __restrict__ arg, bf16_t* __restrict__ xam,
+                                                             int N, int H, int W, int C, int P, int Q) {
   const int cv = C / 8;
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= Q * cv) return;
@@ -830,10 +830,12 @@ __global__ __launch_bounds__(256) void bn_maxpool_fwd_kernel(const bf16_t* __res
       }
     float best[8];
     uint32_t bidx[8];
+    u16x8 bx;   // the BN input at the argmax (xam: the backward statistics read it instead of x)
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
       best[t] = -INFINITY;
       bidx[t] = 0;
+      bx[t] = 0;
     }
 #pragma unroll
     for (int r = 0; r < 3; ++r)
@@ -846,6 +848,7 @@ __global__ __launch_bounds__(256) void bn_maxpool_fwd_kernel(const bf16_t* __res
           if (ok[r][s] && f > best[t]) {
             best[t] = f;
             bidx[t] = (uint32_t)(r * 3 + s);
+            bx[t] = v[r][s][t];
           }
         }
     u16x8 o;
@@ -856,6 +859,7 @@ __global__ __launch_bounds__(256) void bn_maxpool_fwd_kernel(const bf16_t* __res
     }
     const size_t oi = ((size_t)row * Q + q) * cv + c8;
     reinterpret_cast<u16x8*>(y)[oi] = o;
+    if (xam) reinterpret_cast<u16x8*>(xam)[oi] = bx;
     uint2 am;
     am.x = bidx[0] | (bidx[1] << 8) | (bidx[2] << 16) | (bidx[3] << 24);
     am.y = bidx[4] | (bidx[5] << 8) | (bidx[6] << 16) | (bidx[7] << 24);
@@ -935,6 +939,64 @@ __global__ __launch_bounds__(256) void bn_maxpool_bwd_reduce_kernel(
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's atomics have completed
   bn_finalize_last<true, kBnCopies>(fin, N * H * W, C, gridDim.x * gridDim.y, &red[0][0], 2 * 8 * kS, ncop);
+}
+
+// backward statistics from the pooled side: every input gradient of the pool is a sum of
+// window gradients routed to that window's argmax, so sum_in g xhat = sum_windows dy xhat(x at
+// the argmax) -- the forward's xam -- and sum_in g = sum of the routed dy.  Reads dy (+ dy2),
+// the argmax bytes and xam (the pooled size, ~1/4 of the input each) instead of the whole BN
+// input.  One thread per (pooled position, 8-channel group), grid-stride over positions.
+__global__ __launch_bounds__(256) void bn_maxpool_bwd_reduce_am_kernel(
+    const bf16_t* __restrict__ xam, const bf16_t* __restrict__ dy, const bf16_t* __restrict__ dy2,
+    const uint8_t* __restrict__ arg, const float* __restrict__ mean, const float* __restrict__ invstd,
+    float* __restrict__ acc, int npos, int M, int C, BnFin fin, int ncop) {
+  constexpr int kS = 264;   // (layout as bn_maxpool_bwd_reduce_kernel)
+  __shared__ float red[2][8 * kS];
+  const int cv = C / 8;
+  const int tid = threadIdx.x;
+  const int c8 = tid % cv;   // fixed per thread: 256 % cv == 0 and the stride below is a multiple of cv
+  float s0[8], s1[8], mu[8], is[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    s0[t] = 0.f;
+    s1[t] = 0.f;
+  }
+  load8(mean + c8 * 8, mu);
+  load8(invstd + c8 * 8, is);
+  const int64_t total = (int64_t)npos * cv, stride = (int64_t)gridDim.x * 256;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + tid; i < total; i += stride) {
+    const uint2 am = reinterpret_cast<const uint2*>(arg)[i];
+    const u16x8 gv = reinterpret_cast<const u16x8*>(dy)[i];
+    const u16x8 xv = reinterpret_cast<const u16x8*>(xam)[i];
+    u16x8 g2 = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    if (dy2) g2 = reinterpret_cast<const u16x8*>(dy2)[i];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const uint32_t bt = ((t < 4 ? am.x : am.y) >> (8 * (t & 3))) & 0xffu;
+      const float gg = bt != kNoGrad ? bf2f(gv[t]) + bf2f(g2[t]) : 0.f;
+      s0[t] += gg;
+      s1[t] += gg * (bf2f(xv[t]) - mu[t]) * is[t];
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    red[0][t * kS + tid] = s0[t];
+    red[1][t * kS + tid] = s1[t];
+  }
+  __syncthreads();
+  float* accc = acc + (size_t)(blockIdx.x % ncop) * 2 * C;
+  for (int ch = tid; ch < C; ch += 256) {
+    const int g8 = ch >> 3, t = ch & 7;
+    float t0 = 0.f, t1 = 0.f;
+    for (int k = g8; k < 256; k += cv) {
+      t0 += red[0][t * kS + k];
+      t1 += red[1][t * kS + k];
+    }
+    bn_acc_add(accc + ch, t0);
+    bn_acc_add(accc + C + ch, t1);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's atomics have completed
+  bn_finalize_last<true, kBnCopies>(fin, M, C, gridDim.x, &red[0][0], 2 * 8 * kS, ncop);
 }
 
 // backward apply: dx = A g + B x + D, same 2x2-block threads
@@ -1178,19 +1240,19 @@ bool bnpool_ok(const BnArgs& a, int N, int H, int W, int P, int Q, int pad) {
 }  // namespace
 
 hipError_t bn_maxpool_forward(const BnArgs& a, int N, int H, int W, int P, int Q, int pad, uint16_t* y,
-                              uint8_t* arg, bool stats_ready, hipStream_t s) {
+                              uint8_t* arg, bool stats_ready, hipStream_t s, uint16_t* xam) {
   if (!bnpool_ok(a, N, H, W, P, Q, pad) || !a.relu || !y || !arg) return hipErrorInvalidValue;
   if (!stats_ready) bn_forward_stats(a, s);
   const int cv = a.C / 8;
   const dim3 g((Q * cv + kBlock - 1) / kBlock, std::min(N * P, 65535));   // one output row per workgroup
-  if (pad) bn_maxpool_fwd_kernel<1><<<g, kBlock, 0, s>>>(a.x, a.ws, a.ws + a.C, y, arg, N, H, W, a.C, P, Q);
-  else bn_maxpool_fwd_kernel<0><<<g, kBlock, 0, s>>>(a.x, a.ws, a.ws + a.C, y, arg, N, H, W, a.C, P, Q);
+  if (pad) bn_maxpool_fwd_kernel<1><<<g, kBlock, 0, s>>>(a.x, a.ws, a.ws + a.C, y, arg, xam, N, H, W, a.C, P, Q);
+  else bn_maxpool_fwd_kernel<0><<<g, kBlock, 0, s>>>(a.x, a.ws, a.ws + a.C, y, arg, xam, N, H, W, a.C, P, Q);
   return hipGetLastError();
 }
 
 hipError_t bn_maxpool_backward(const BnArgs& a, int N, int H, int W, int P, int Q, int pad, const uint16_t* dy,
                                const uint8_t* arg, uint16_t* dx, float* dgamma, float* dbeta, hipStream_t s,
-                               bool grad_assign) {
+                               bool grad_assign, const uint16_t* xam) {
   if (!bnpool_ok(a, N, H, W, P, Q, pad) || !dy || !arg || !dx) return hipErrorInvalidValue;
   const int C = a.C, cv = C / 8;
   BnFin f{};
@@ -1206,7 +1268,14 @@ hipError_t bn_maxpool_backward(const BnArgs& a, int N, int H, int W, int P, int 
   const int gx = ((W + 1) / 2 * cv + kBlock - 1) / kBlock, rows = N * ((H + 1) / 2);
   const dim3 gr(gx, std::min(rows, std::max(1, bnpool_blocks() / gx)));   // reduce: bounded atomics
   const dim3 ga(gx, std::min(rows, 65535));                                // apply: one block row per workgroup
-  if (pad) {
+  if (xam) {   // statistics from the pooled side (the forward stored x at every argmax)
+    const int npos = N * P * Q;
+    const int nb = (int)std::min<int64_t>(((int64_t)npos * cv + kBlock - 1) / kBlock, bnpool_blocks());
+    bn_maxpool_bwd_reduce_am_kernel<<<nb, kBlock, 0, s>>>(xam, dy, a.dy2, arg, a.save_mean, a.save_invstd, f.acc,
+                                                          npos, N * H * W, C, f, bn_ncop(true, nb));
+    if (pad) bn_maxpool_bwd_apply_kernel<1><<<ga, kBlock, 0, s>>>(a.x, dy, a.dy2, arg, f.coef, dx, N, H, W, C, P, Q);
+    else bn_maxpool_bwd_apply_kernel<0><<<ga, kBlock, 0, s>>>(a.x, dy, a.dy2, arg, f.coef, dx, N, H, W, C, P, Q);
+  } else if (pad) {
     bn_maxpool_bwd_reduce_kernel<1><<<gr, kBlock, 0, s>>>(a.x, dy, a.dy2, arg, a.save_mean, a.save_invstd, f.acc, N,
                                                           H, W, C, P, Q, f, bn_ncop(true, gr.x * gr.y));
     bn_maxpool_bwd_apply_kernel<1><<<ga, kBlock, 0, s>>>(a.x, dy, a.dy2, arg, f.coef, dx, N, H, W, C, P, Q);

@@ -865,6 +865,8 @@ class _BnReluMaxPoolNative(torch.autograd.Function):
         dev = x.device
         y = torch.empty(N, P, Q, C, dtype=torch.bfloat16, device=dev)
         am = torch.empty(N, P, Q, C, dtype=torch.uint8, device=dev)
+        # the BN input at every argmax: the backward statistics read it (pooled size) instead of x
+        xam = torch.empty(N, P, Q, C, dtype=torch.bfloat16, device=dev) if BN_POOL_MODE == 1 else None
         ws = _bn_workspace(mod, C, dev, C_)
         gamma = flat.master_storage(weight)[:C] if weight is not None else None
         beta = flat.master_storage(bias)[:C] if bias is not None else None
@@ -872,13 +874,13 @@ class _BnReluMaxPoolNative(torch.autograd.Function):
         if pre is not None and pre[0] == xb.data_ptr():
             # statistics already accumulated + finalized by the producing conv's epilogue
             smean, sinv = pre[1], pre[2]
-            C_.bn_pool_fwd(xb, y, am, gamma, beta, None, None, smean, sinv, ws, mod.eps, 0.0, None, True, pad)
+            C_.bn_pool_fwd(xb, y, am, gamma, beta, None, None, smean, sinv, ws, mod.eps, 0.0, None, True, pad, xam)
         else:
             smean = torch.empty(C, dtype=torch.float32, device=dev)
             sinv = torch.empty(C, dtype=torch.float32, device=dev)
             rm, rv, mom, nbt = _bn_train_state(mod, dev)
-            C_.bn_pool_fwd(xb, y, am, gamma, beta, rm, rv, smean, sinv, ws, mod.eps, mom or 0.0, nbt, False, pad)
-        ctx.save_for_backward(xb, am, smean, sinv)
+            C_.bn_pool_fwd(xb, y, am, gamma, beta, rm, rv, smean, sinv, ws, mod.eps, mom or 0.0, nbt, False, pad, xam)
+        ctx.save_for_backward(xb, am, smean, sinv, xam)
         ctx.meta = (flat, weight, bias, ws, pad, C, x.dtype)
         ctx.set_materialize_grads(False)
         return nchw_view(y, C), nchw_view(y, C)
@@ -886,7 +888,7 @@ class _BnReluMaxPoolNative(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gy, gy_twin):
         C_ = _ext.C()
-        xb, am, smean, sinv = ctx.saved_tensors
+        xb, am, smean, sinv, xam = ctx.saved_tensors
         flat, weight, bias, ws, pad, C, in_dtype = ctx.meta
         if gy is None:
             gy, gy_twin = gy_twin, None
@@ -907,14 +909,16 @@ class _BnReluMaxPoolNative(torch.autograd.Function):
             for t, f in fresh:
                 if f:
                     t.zero_()
-        C_.bn_pool_bwd(xb, g, am, dx, gamma, smean, sinv, ws, dg, db, assign, gt, pad)
+        C_.bn_pool_bwd(xb, g, am, dx, gamma, smean, sinv, ws, dg, db, assign, gt, pad, xam)
         flat.notify(weight, bias)
         dxv = nchw_view(dx, C)
         return (dxv if in_dtype == torch.bfloat16 else dxv.to(in_dtype)), None, None, None, None, None
 
 
-# BN + ReLU + max-pool fused (LDNN_BN_POOL=0: the separate BN-apply and pool passes)
-BN_POOL_FUSED = __import__("os").environ.get("LDNN_BN_POOL", "1") != "0"
+# BN + ReLU + max-pool fused (LDNN_BN_POOL=0: the separate BN-apply and pool passes; 1: fused, the
+# backward statistics from the pooled side (x at the argmax); 2: fused, the statistics pass reads x)
+BN_POOL_MODE = int(__import__("os").environ.get("LDNN_BN_POOL", "1"))
+BN_POOL_FUSED = BN_POOL_MODE != 0
 
 
 def bn_relu_maxpool(x, bn, pool):

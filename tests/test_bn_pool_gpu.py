@@ -232,6 +232,43 @@ def test_bn_relu_maxpool_fused(N, C, H, W, pad, twin, monkeypatch):
     torch.testing.assert_close(rvf, ref.running_var, rtol=1e-3, atol=1e-3)
 
 
+@pytest.mark.parametrize("N,C,H,W,pad", [(4, 64, 20, 18, 1), (2, 16, 11, 13, 1), (3, 32, 12, 12, 0),
+                                         (2, 8, 9, 7, 0), (8, 64, 112, 112, 1)])
+@pytest.mark.parametrize("twin", [False, True])
+def test_bn_pool_backward_statistics_from_the_pooled_side(N, C, H, W, pad, twin, monkeypatch):
+    """LDNN_BN_POOL=1 (default): the forward stores the BN input at every argmax and the backward
+    statistics pass sums over pooled positions (dy routed to its argmax, xhat of the stored x)
+    instead of reading the whole input; == mode 2 (the pass over x) up to the fp32 summation
+    order of the two per-channel sums.  ResNet-18 b256 7.23 -> 7.16 ms
+    (profiles/r6/bn_pool_pooled_stats_ab.jsonl)."""
+    x = torch.randn(N, C, H, W, device="cuda") * 2 + 0.3
+    P, Q = (H + 2 * pad - 3) // 2 + 1, (W + 2 * pad - 3) // 2 + 1
+    g1 = torch.randn(N, C, P, Q, device="cuda").bfloat16().float()
+    g2 = torch.randn_like(g1).bfloat16().float()
+    res = []
+    for mode in (1, 2):
+        monkeypatch.setattr(LF, "BN_POOL_MODE", mode)
+        monkeypatch.setattr(LF, "BN_POOL_FUSED", True)
+        bn, ref, pool = _stem_pair(C, pad)
+        xb = _cl(x).requires_grad_(True)
+        y = LF.bn_relu_maxpool(xb, bn, pool)
+        loss = (y.float() * g1).sum()
+        if twin:
+            loss = loss + (LF.shortcut_input(y).float() * g2).sum()
+        loss.backward()
+        res.append((y.detach().float(), xb.grad.float(), bn.weight.grad.clone(), bn.bias.grad.clone()))
+    (y1, dx1, dg1, db1), (y2, dx2, dg2, db2) = res
+    # (above 2048 rows the forward statistics are summed with atomics: both runs' BN outputs may
+    # differ in the last bf16 bit, and an argmax tie within one bit may then move)
+    assert (y1 != y2).float().mean().item() < 1e-4
+    torch.testing.assert_close(y1, y2, rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(dg1, dg2, rtol=1e-3, atol=1e-4 * dg2.abs().max().item())
+    torch.testing.assert_close(db1, db2, rtol=1e-3, atol=1e-4 * db2.abs().max().item())
+    # dx = A g + B x + D: the coefficients differ in the last fp32 bits, dx is rounded to bf16
+    assert ((dx1 - dx2).abs() > 1e-2 * dx2.abs().max()).float().mean().item() < 1e-4
+    assert ((dx1 - dx2).norm() / dx2.norm()).item() < 2e-3
+
+
 @pytest.mark.parametrize("N,H", [(16, 112), (16, 224)])
 def test_resnet_stem_fused_bn_pool_vs_fp32_oracle(N, H, monkeypatch):
     """ResNet-18's stem -- conv1 7x7/2 (BN statistics from its epilogue) -> bn1 -> ReLU ->
