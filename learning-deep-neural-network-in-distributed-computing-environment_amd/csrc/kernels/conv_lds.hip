@@ -69,8 +69,11 @@ struct LArgs {
   FastDiv f_cw[2], f_ch[2];      // stride-2 dgrad class rows: (W - pw + 1) / 2, (H - ph + 1) / 2
   float* ws;         // split-K: combine slabs (with cnt) or wgrad partial slabs [split][M][N] (without)
   int* cnt;          // split-K arrival counters of the in-launch combine
-  int bn_stats;      // fwd: accumulate + finalize the next BatchNorm's statistics (bn)
+  int bn_stats;      // fwd: accumulate + finalize the next BatchNorm's statistics (bn); weight-stationary
+                     // dgrad: the backward statistics of the BN whose output's gradient dx is (bn, bnb_*)
   BnFin bn;
+  const bf16_t* bnb_x;     // (ws64 dgrad with bn_stats) that BN's input [M][64]
+  const uint8_t* bnb_mask; // its ReLU bits [M][8] (nullptr: no ReLU)
   int tap_major;     // fwd / dgrad K-tile order: 0 = channel block fastest, 1 = filter tap fastest
   int f32_rows;      // fp32 outputs (wgrad, split-K slabs) through the row-coalesced LDS epilogue
   int bf16_rows;     // bf16 outputs (fwd y, stride-1 dgrad dx) through the row-coalesced LDS epilogue
@@ -1472,11 +1475,25 @@ __global__ __launch_bounds__(256, 1) void conv_ws64_kernel(LArgs a, const bf16_t
     }
   };
 
-  float bs0[2][4], bs1[2][4];  // fwd: the next BN's per-channel sums over this workgroup's rows
+  float bs0[2][4], bs1[2][4];  // fwd: the next BN's per-channel sums over this workgroup's rows;
+                              // dgrad: sum g, sum g xhat of the BN whose output's gradient dx is
+  float bmu[2][4], bis[2][4];   // (dgrad: that BN's saved mean / invstd of this lane's channels)
 #pragma unroll
   for (int j = 0; j < 2; ++j)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) bs0[j][r] = bs1[j][r] = 0.f;
+    for (int r = 0; r < 4; ++r) bs0[j][r] = bs1[j][r] = bmu[j][r] = bis[j][r] = 0.f;
+  if constexpr (DGRAD) {
+    if (a.bn_stats) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int c = wn * 32 + j * 16 + 4 * (lane >> 4) + r;
+          bmu[j][r] = a.bn.save_mean[c];
+          bis[j][r] = a.bn.save_invstd[c];
+        }
+    }
+  }
 
   // the first two tiles' halos DMA while the weights are staged (separate LDS regions)
   if (t0 < t1) {
@@ -1562,6 +1579,24 @@ __global__ __launch_bounds__(256, 1) void conv_ws64_kernel(LArgs a, const bf16_t
         }
       }
     };
+    // (dgrad with bn_stats) the BN input and ReLU bits of this tile's dx elements, issued before
+    // the MFMA steps so their latency hides behind them (the epilogue reads them)
+    u16x4 bxv[RT][2];
+    uint32_t bmb[RT];
+    if constexpr (DGRAD) {
+      if (a.bn_stats) {
+#pragma unroll
+        for (int i = 0; i < RT; ++i) {
+          const int m = t * BM + wm * RT * 16 + i * 16 + (lane & 15);
+          const int mc = m < g.M ? m : g.M - 1;
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            bxv[i][j] = *reinterpret_cast<const u16x4*>(a.bnb_x + (size_t)mc * 64 + wn * 32 + j * 16 + 4 * (lane >> 4));
+          // the 32 ReLU bits of channels 32 wn .. 32 wn + 31: bytes 4 wn .. 4 wn + 3 of the row
+          bmb[i] = a.bnb_mask ? *reinterpret_cast<const uint32_t*>(a.bnb_mask + (size_t)mc * 8 + wn * 4) : 0xffffffffu;
+        }
+      }
+    }
     floatx4 acc[2][RT];
 #pragma unroll
     for (int j = 0; j < 2; ++j)
@@ -1635,6 +1670,17 @@ __global__ __launch_bounds__(256, 1) void conv_ws64_kernel(LArgs a, const bf16_t
             bs0[j][r] += b;
             bs1[j][r] += b * b;
           }
+        } else {
+          if (a.bn_stats) {
+            // channel c + r is bit (c + r) - 32 wn of the 32-bit word at byte 4 wn of the row
+            const uint32_t bits = bmb[i] >> (j * 16 + 4 * (lane >> 4));
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float gv = ((bits >> r) & 1u) ? bf2f(o[r]) : 0.f;
+              bs0[j][r] += gv;
+              bs1[j][r] += gv * (bf2f(bxv[i][j][r]) - bmu[j][r]) * bis[j][r];
+            }
+          }
         }
       }
     }
@@ -1642,7 +1688,7 @@ __global__ __launch_bounds__(256, 1) void conv_ws64_kernel(LArgs a, const bf16_t
   if constexpr ((XF & 32) != 0) {
     if (trace != nullptr) trace[2] = __builtin_amdgcn_s_memrealtime();
   }
-  if constexpr (!DGRAD) {
+  {
     if (a.bn_stats) {
 #pragma unroll
       for (int j = 0; j < 2; ++j)
@@ -1674,7 +1720,7 @@ __global__ __launch_bounds__(256, 1) void conv_ws64_kernel(LArgs a, const bf16_t
         bn_acc_add(accc + 64 + threadIdx.x, s1);
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's atomics have completed
-      bn_finalize_last<false, kBnCopies>(a.bn, g.M, 64, gridDim.x, red, LDS / 4);
+      bn_finalize_last<DGRAD, kBnCopies>(a.bn, g.M, 64, gridDim.x, red, LDS / 4);
     }
   }
   if constexpr ((XF & 32) != 0) {
@@ -2505,7 +2551,8 @@ constexpr int kSlabBnTarget = 512;   // conv_slab_bn workgroups aimed at
 // LDNN_CONV_BN_BWD (documented fallback): stride-1 dgrads take the backward statistics of the BN
 // whose output's gradient they produce (conv2d_dgrad with a BnBwdFuse): 1 (default) in the slab
 // split-K sum, and for a dgrad without slabs that shares its launch with the wgrad, as a pass over
-// dx in the shared post launch; 0 never (the BN runs its own reduce).  (The form inside the direct
+// dx in the shared post launch, and in the weight-stationary 64 -> 64 dgrad's persistent epilogue;
+// 2 all but the weight-stationary one; 0 never (the BN runs its own reduce).  (The form inside the direct
 // / in-launch-combine epilogue -- x and mask loads, 8-copy atomics and one finalizing workgroup
 // behind the tile's own stores -- added 11-13 us to a 64 / 128-tile dgrad to save an 8-10 us reduce
 // launch, profiles/r5/conv_bn_bwd_ab.txt, and was removed in round 6.)
@@ -3415,6 +3462,7 @@ struct DgradPrep {
   LArgs a;
   Plan pl;
   bool slab, hb, halo, ws64;
+  bool ws64_bnb;              // the weight-stationary dgrad's epilogue takes the BN backward statistics
   const BnBwdFuse* slab_bnb;
   const BnBwdFuse* red_bnb;   // no slabs: the BN statistics as a post task over dx (paired launches)
   size_t bdy, bw;
@@ -3456,6 +3504,16 @@ DgradPrep dgrad_prep(const ConvShape& s, uint16_t* dx, float* ws, int* cnt, cons
     a.ws = nullptr;
     a.cnt = nullptr;
     a.nk_split = a.nk_all;
+    // the BN backward statistics in the persistent epilogue (per-lane sums over all of the
+    // workgroup's tiles, one atomic pair per channel per workgroup, as its forward does)
+    if (bnb != nullptr && bn_bwd_env() == 1 && bnb->fin.acc != nullptr && bnb->fin.ticket != nullptr &&
+        bnb->fin.save_mean != nullptr && bnb->fin.save_invstd != nullptr && bnb->x != nullptr) {
+      a.bn_stats = 1;
+      a.bn = bnb->fin;
+      a.bnb_x = reinterpret_cast<const bf16_t*>(bnb->x);
+      a.bnb_mask = bnb->mask;
+      d.ws64_bnb = true;
+    }
     return d;
   }
   d.halo = generic < 2 && !d.hb && halo_takes(s, pl.wm);
@@ -3518,7 +3576,10 @@ hipError_t conv2d_dgrad_lds(const ConvShape& s, const uint16_t* dy, const uint16
   const DgradPrep d = dgrad_prep(s, dx, ws, cnt, bnb);
   const LArgs& a = d.a;
   const int splits = d.pl.splits;
-  if (d.ws64) return launch_ws64<true>(a, dy, d.bdy, w, st);
+  if (d.ws64) {
+    if (bn_used) *bn_used = d.ws64_bnb;
+    return launch_ws64<true>(a, dy, d.bdy, w, st);
+  }
   hipError_t e;
   if (d.hb) {
     e = launch_hb<DgradB<128, 2, 8>, true>(a, EPI_NONE, splits, dy, d.bdy, w, d.bw, st);

@@ -475,12 +475,15 @@ def test_fixed_summer_split_k_combine_matches_last_arrival(N, C, H, K, stride):
 
 
 @pytest.mark.parametrize("N,C,H,K", [(64, 128, 16, 128), (64, 256, 8, 256), (64, 512, 4, 512), (64, 1024, 2, 1024),
-                                     (8, 512, 7, 512), (5, 192, 9, 256)])
+                                     (8, 512, 7, 512), (5, 192, 9, 256),
+                                     (64, 64, 56, 64), (16, 64, 32, 64), (3, 64, 9, 64)])
 @pytest.mark.parametrize("relu", [True, False])
 def test_dgrad_takes_bn_backward_statistics(N, C, H, K, relu):
     """A stride-1 dgrad whose dx is the gradient of a training BN(+ReLU)'s output takes that BN's
-    backward statistics (in its slab split-K sum, or in one pass over dx right after an unsplit /
-    in-launch-combine dgrad) and finalizes them: dx has the bits of the plain dgrad, and the BN
+    backward statistics (in its slab split-K sum, in one pass over dx right after an unsplit /
+    in-launch-combine dgrad, or -- the 64 -> 64 weight-stationary dgrad -- in its persistent
+    epilogue, summed per lane over all of a workgroup's tiles) and finalizes them: dx has the bits
+    of the plain dgrad, and the BN
     backward's apply pass alone (stats_ready) gives the dx / dgamma / dbeta of the BN's own reduce;
     a repeat (accumulators and tickets left clear) agrees."""
     torch.manual_seed(31)
@@ -526,7 +529,7 @@ def _dgrad_bn_stats_case(Cc, N, C, H, K, relu):
     assert torch.count_nonzero(ws[10 * C + 16: 10 * C + 17]) == 0
 
 
-@pytest.mark.parametrize("C,H", [(512, 4), (128, 16), (256, 8)])
+@pytest.mark.parametrize("C,H", [(512, 4), (128, 16), (256, 8), (64, 56)])
 def test_resblock_bn1_backward_statistics_come_from_conv2_dgrad(C, H):
     """In a residual block, bn1's output feeds conv2 alone: its backward statistics come from
     conv2's dgrad (EnhancedCNN layer3's 512-channel 4x4 block: in the slab split-K sum; the 16x16 /
