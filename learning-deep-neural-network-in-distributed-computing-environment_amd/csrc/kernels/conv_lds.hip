@@ -1459,6 +1459,19 @@ __global__ __launch_bounds__(256, 1) void conv_ws64_kernel(LArgs a, const bf16_t
 
   Rsrc ra;
   ra.r = __builtin_amdgcn_make_buffer_rsrc((void*)pa, (short)0, (int)bytes_a, 0x00020000);
+  // dgrad with bn_stats: the BN input tile (BM rows at kHPitch, as the halo) and its ReLU bits,
+  // staged in the weight region; mask rows beyond M (or no mask: all ones) read as ...
+  constexpr int XPW = BM * ws64::kHPitch / 1024 / NW;   // BN-input pieces per wave per tile
+  static_assert(XPW * NW * 1024 == BM * ws64::kHPitch && BM * ws64::kHPitch + 1024 <= ws64::kWBytes, "x stage");
+  char* const xst = wst;
+  char* const mst = wst + BM * ws64::kHPitch;
+  Rsrc rbx, rbm;
+  if constexpr (DGRAD) {
+    rbx.r = __builtin_amdgcn_make_buffer_rsrc((void*)a.bnb_x, (short)0, a.bn_stats ? (int)((uint32_t)g.M * 128u) : 0,
+                                              0x00020000);
+    rbm.r = __builtin_amdgcn_make_buffer_rsrc((void*)a.bnb_mask, (short)0,
+                                              a.bn_stats && a.bnb_mask ? (int)((uint32_t)g.M * 8u) : 0, 0x00020000);
+  }
   // the halo of tile t into buffer b, lane-linear 16-B slots of kHPitch-B rows (slots 8.. of a
   // row are padding: zero reads); rows outside the tensor read as zeros
   auto dma = [&](int t, int b) {
@@ -1579,30 +1592,31 @@ __global__ __launch_bounds__(256, 1) void conv_ws64_kernel(LArgs a, const bf16_t
         }
       }
     };
-    // (dgrad with bn_stats) the BN input and ReLU bits of this tile's dx elements, issued before
-    // the MFMA steps so their latency hides behind them (the epilogue reads them)
-    u16x4 bxv[RT][2];
-    uint32_t bmb[RT];
-    if constexpr (DGRAD) {
-      if (a.bn_stats) {
-#pragma unroll
-        for (int i = 0; i < RT; ++i) {
-          const int m = t * BM + wm * RT * 16 + i * 16 + (lane & 15);
-          const int mc = m < g.M ? m : g.M - 1;
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-            bxv[i][j] = *reinterpret_cast<const u16x4*>(a.bnb_x + (size_t)mc * 64 + wn * 32 + j * 16 + 4 * (lane >> 4));
-          // the 32 ReLU bits of channels 32 wn .. 32 wn + 31: bytes 4 wn .. 4 wn + 3 of the row
-          bmb[i] = a.bnb_mask ? *reinterpret_cast<const uint32_t*>(a.bnb_mask + (size_t)mc * 8 + wn * 4) : 0xffffffffu;
-        }
-      }
-    }
     floatx4 acc[2][RT];
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int i = 0; i < RT; ++i) acc[j][i] = floatx4{0.f, 0.f, 0.f, 0.f};
     lds_barrier();  // every wave waited for its own pieces of tile t: the whole halo is visible
+    if constexpr (DGRAD) {
+      // (bn_stats) this tile's BN input rows and ReLU bits DMA'd into the weight staging region
+      // (free after the prologue; every wave is past the last tile's epilogue reads here) while
+      // the MFMA steps run; the epilogue reads them after the tile's vmcnt wait + a barrier
+      if (a.bn_stats) {
+#pragma unroll
+        for (int i = 0; i < XPW; ++i) {
+          const int pc = i * NW + wid;
+          const int slot = pc * 64 + lane;
+          const int j = slot / ws64::kSlots, c = slot - j * ws64::kSlots;
+          const int gp = t * BM + j;
+          const int o = gp < g.M && c < 8 ? (int)(((unsigned)gp * 64u + (unsigned)c * 8u) * 2u) : (int)kOOB;
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rbx.r, (lds_void*)(xst + pc * 1024), 16, o, 0, 0, 0);
+        }
+        if (wid == 0)   // 128 rows x 8 B of ReLU bits: one piece
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rbm.r, (lds_void*)mst, 16, (int)((unsigned)t * BM * 8u + lane * 16u),
+                                                   0, 0, 0);
+      }
+    }
     __builtin_amdgcn_s_setprio(1);
     uint32_t sink = 0;
     // step st = tap * 2 + kk: its RT fragment reads are issued two steps ahead
@@ -1653,6 +1667,23 @@ __global__ __launch_bounds__(256, 1) void conv_ws64_kernel(LArgs a, const bf16_t
       continue;
     }
     // epilogue: bf16 rows (8 B = 4 channels per lane), the BN sums of the rounded values
+    u16x4 bxv[RT][2];
+    uint32_t bmb[RT];
+    if constexpr (DGRAD) {
+      if (a.bn_stats) {
+        if (t + 1 >= t1) wait_vm<0>();   // (the last tile has no vmcnt wait above)
+        lds_barrier();   // every wave's BN-input pieces of this tile landed
+#pragma unroll
+        for (int i = 0; i < RT; ++i) {
+          const int r = wm * RT * 16 + i * 16 + (lane & 15);
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            bxv[i][j] = *reinterpret_cast<const u16x4*>(xst + r * ws64::kHPitch + (wn * 32 + j * 16 + 4 * (lane >> 4)) * 2);
+          // the 32 ReLU bits of channels 32 wn .. 32 wn + 31: bytes 4 wn .. 4 wn + 3 of the row
+          bmb[i] = a.bnb_mask ? *reinterpret_cast<const uint32_t*>(mst + r * 8 + wn * 4) : 0xffffffffu;
+        }
+      }
+    }
 #pragma unroll
     for (int i = 0; i < RT; ++i) {
       const int m = t * BM + wm * RT * 16 + i * 16 + (lane & 15);
