@@ -1465,6 +1465,11 @@ __global__ __launch_bounds__(256, 1) void conv_ws64_kernel(LArgs a, const bf16_t
   static_assert(XPW * NW * 1024 == BM * ws64::kHPitch && BM * ws64::kHPitch + 1024 <= ws64::kWBytes, "x stage");
   char* const xst = wst;
   char* const mst = wst + BM * ws64::kHPitch;
+  // output staging (also in the weight region): the tile's BM rows x 128 B at a 144-B pitch,
+  // written in the MFMA layout and stored row-wise as whole 128-B rows
+  constexpr int kOPitch = 144, kOStage = 24 * 1024;
+  static_assert(kOStage >= BM * ws64::kHPitch + 1024 && kOStage + BM * kOPitch <= ws64::kWBytes, "out stage");
+  char* const ost = wst + kOStage;
   Rsrc rbx, rbm;
   if constexpr (DGRAD) {
     rbx.r = __builtin_amdgcn_make_buffer_rsrc((void*)a.bnb_x, (short)0, a.bn_stats ? (int)((uint32_t)g.M * 128u) : 0,
@@ -1686,14 +1691,15 @@ __global__ __launch_bounds__(256, 1) void conv_ws64_kernel(LArgs a, const bf16_t
     }
 #pragma unroll
     for (int i = 0; i < RT; ++i) {
-      const int m = t * BM + wm * RT * 16 + i * 16 + (lane & 15);
+      const int r = wm * RT * 16 + i * 16 + (lane & 15);
+      const int m = t * BM + r;
       if (m >= g.M) continue;
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int c = wn * 32 + j * 16 + 4 * (lane >> 4);
         const floatx4 v = acc[j][i];
         const u16x4 o = u16x4{f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
-        *reinterpret_cast<u16x4*>(out + (size_t)m * 64 + c) = o;
+        *reinterpret_cast<u16x4*>(ost + r * kOPitch + c * 2) = o;
         if constexpr (!DGRAD) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
@@ -1714,6 +1720,15 @@ __global__ __launch_bounds__(256, 1) void conv_ws64_kernel(LArgs a, const bf16_t
           }
         }
       }
+    }
+    lds_barrier();   // both column halves of every row are staged
+#pragma unroll
+    for (int q = 0; q < BM * 8 / NT; ++q) {   // 8 lanes x 16 B per 128-B row
+      const int idx = q * NT + (int)threadIdx.x, r = idx >> 3, ch = idx & 7;
+      const int m = t * BM + r;
+      if (m < g.M)
+        *reinterpret_cast<u32x4*>(out + (size_t)m * 64 + ch * 8) =
+            *reinterpret_cast<const u32x4*>(ost + r * kOPitch + ch * 16);
     }
   }
   if constexpr ((XF & 32) != 0) {
@@ -2200,14 +2215,21 @@ __global__ __launch_bounds__(256, 2) void conv_patch_kernel(LArgs a, const bf16_
 // fragments two k-steps ahead (asm + counted lgkmcnt, as conv_ws64_kernel).  Padding taps
 // (t >= R*S) read cell 0: their weights are zero.  The next BN's statistics stay in registers
 // over all tiles.  EPI_NONE, K = 64.
+__device__ __forceinline__ int wid_stage_offset(int wid, int bytes) { return wid * bytes; }
+
 template <int KS, int STR, int XF = 0>
 __global__ __launch_bounds__(256, 1) void conv_patch_ws_kernel(LArgs a, const bf16_t* px, uint32_t bytes_x,
                                                                const bf16_t* pw) {
   constexpr int BM = 256, NW = 4;
   constexpr int PIECES = kPatchBytes / 1024, PPW = PIECES / NW;
   static_assert(PPW * NW == PIECES && KS >= 3, "patch pieces / k-steps");
-  constexpr int LDS = 2 * kPatchBytes + 16;
+  // output staging: each wave's 64 rows x 128 B at a 144-B pitch, re-read row-wise so the stores
+  // are whole 128-B rows (16 B per lane) instead of 8-B pieces of 16 rows per instruction
+  constexpr int kOutPitch = 144, kOutWave = 64 * kOutPitch;
+  constexpr int LDS = 2 * kPatchBytes + NW * kOutWave + 16;
+  static_assert(LDS <= 160 * 1024, "LDS");
   __shared__ __attribute__((aligned(1024))) char smem[LDS];
+  char* const ostage = smem + 2 * kPatchBytes + wid_stage_offset(threadIdx.x >> 6, kOutWave);
   const ConvShape& sh = a.s;
   const Geo g = make_geo(a, false, (int)blockIdx.z);
   const int lane = threadIdx.x & 63;
@@ -2324,13 +2346,13 @@ __global__ __launch_bounds__(256, 1) void conv_patch_ws_kernel(LArgs a, const bf
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int m = m0 + wid * 64 + i * 16 + (lane & 15);
+      const int rl = i * 16 + (lane & 15);   // this wave's row
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int c = j * 16 + 4 * (lane >> 4);
         const floatx4 v = acc[j][i];
         const u16x4 o = u16x4{f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
-        *reinterpret_cast<u16x4*>(out + (size_t)m * 64 + c) = o;
+        *reinterpret_cast<u16x4*>(ostage + rl * kOutPitch + c * 2) = o;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float bv = bf2f(o[r]);
@@ -2338,6 +2360,13 @@ __global__ __launch_bounds__(256, 1) void conv_patch_ws_kernel(LArgs a, const bf
           bs1[j][r] += bv * bv;
         }
       }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // (a wave's LDS operations run in order)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {   // 8 rows x 8 lanes x 16 B per store
+      const int rl = q * 8 + (lane >> 3);
+      const u32x4 v = *reinterpret_cast<const u32x4*>(ostage + rl * kOutPitch + (lane & 7) * 16);
+      *reinterpret_cast<u32x4*>(out + (size_t)(m0 + wid * 64 + rl) * 64 + (lane & 7) * 8) = v;
     }
   }
   if constexpr ((XF & 32) != 0) {
