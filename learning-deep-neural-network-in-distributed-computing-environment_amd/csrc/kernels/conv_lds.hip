@@ -1986,7 +1986,7 @@ struct S2dArgs {
   float* slab;              // [slices][64][256]
 };
 
-__global__ __launch_bounds__(256, 2) void stem_s2d_wgrad_kernel(S2dArgs a, const bf16_t* pdy, uint32_t bytes_dy,
+__global__ __launch_bounds__(256, 3) void stem_s2d_wgrad_kernel(S2dArgs a, const bf16_t* pdy, uint32_t bytes_dy,
                                                                 const bf16_t* pxs, uint32_t bytes_xs) {
   using namespace s2d;
   __shared__ __attribute__((aligned(1024))) char smem[kStages * kStage];  // 48 KiB
@@ -2020,10 +2020,13 @@ __global__ __launch_bounds__(256, 2) void stem_s2d_wgrad_kernel(S2dArgs a, const
       }
       const uint32_t pix0 = ((uint32_t)(n * a.Hs + p + wid) * (uint32_t)a.Ws + (uint32_t)q0);
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {  // 64 s2d pixels x 32 B from q0 (only 35 are read)
-        const uint32_t o = (pix0 + (uint32_t)(h * 32 + (lane >> 1))) * 32u + (uint32_t)(lane & 1) * 16u;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rxs.r, (lds_void*)(dst + kDy + wid * kSeg + h * 1024), 16, (int)o, 0,
-                                                 0, 0);
+      for (int h = 0; h < 2; ++h) {  // s2d pixels q0 .. q0 + 34 x 32 B (the taps read 35): the second
+        // piece's lanes past pixel 34 are out of range (no memory traffic; the per-CU fill rate
+        // bounds this kernel)
+        const int px = h * 32 + (lane >> 1);
+        const uint32_t o = (pix0 + (uint32_t)px) * 32u + (uint32_t)(lane & 1) * 16u;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rxs.r, (lds_void*)(dst + kDy + wid * kSeg + h * 1024), 16,
+                                                 px < 35 ? (int)o : (int)kOOB, 0, 0, 0);
       }
     };
     // three DMA instructions per wave per K-step; steps 0..2 in the prologue, step t+3 after
@@ -3207,7 +3210,9 @@ S2dPlan plan_s2d(const ConvShape& s) {
   p.Ws = s.Q + 3;
   p.nchunk = (s.Q + 31) / 32;
   p.steps = s.N * s.P * p.nchunk;
-  constexpr int target = 512;
+  // three 48-KiB workgroups per CU: the K-step loop is bound by the DMA round trip of its 3 steps
+  // in flight, not by bytes, so throughput scales with the workgroups resident per CU
+  constexpr int target = 768;
   int slices = std::max(1, std::min(target, p.steps / 8));
   p.steps_per = (p.steps + slices - 1) / slices;
   p.slices = (p.steps + p.steps_per - 1) / p.steps_per;
