@@ -956,11 +956,22 @@ bool conv_fwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& y, int
               const c10::optional<at::Tensor>& bn_gamma, const c10::optional<at::Tensor>& bn_beta,
               const c10::optional<at::Tensor>& bn_running_mean, const c10::optional<at::Tensor>& bn_running_var,
               const c10::optional<at::Tensor>& bn_save_mean, const c10::optional<at::Tensor>& bn_save_invstd,
-              double bn_eps, double bn_momentum, const c10::optional<at::Tensor>& bn_num_batches) {
+              double bn_eps, double bn_momentum, const c10::optional<at::Tensor>& bn_num_batches,
+              int64_t real_channels, const c10::optional<at::Tensor>& s2d_xs) {
   check_dev(x, at::kBFloat16, "x");
   check_dev(w, at::kBFloat16, "w");
   check_dev(y, at::kBFloat16, "y");
   ldnn::ConvShape s = conv_shape(x, w, y, stride, pad);
+  s.c_real = real_channels > 0 && real_channels < s.C ? (int)real_channels : 0;
+  uint16_t* xs = nullptr;
+  if (s2d_xs.has_value()) {
+    check_dev(*s2d_xs, at::kBFloat16, "s2d_xs");
+    TORCH_CHECK(ldnn::stem_s2d_fwd_ok(s), "conv_fwd: s2d_xs given for a shape the s2d stem forward does not take");
+    TORCH_CHECK(s2d_xs->is_contiguous() && s2d_xs->dim() == 4 && s2d_xs->size(0) == s.N && s2d_xs->size(1) == s.P + 3 &&
+                    s2d_xs->size(2) == s.Q + 3 && s2d_xs->size(3) == 16,
+                "conv_fwd: s2d_xs must be a dense [N][P+3][Q+3][16] bf16 tensor");
+    xs = bf16_mut(*s2d_xs);
+  }
   const float* b = nullptr;
   if (bias.has_value()) {
     check_dev(*bias, at::kFloat, "bias");
@@ -976,7 +987,7 @@ bool conv_fwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& y, int
                                        bn_save_invstd, bn_eps, bn_momentum, bn_num_batches);
   bool done = false;
   check(ldnn::conv2d_fwd(s, bf16_ptr(x), bf16_ptr(w), bf16_mut(y), b, (int)epi, cur_stream(x), ws.ws(), ws.c(),
-                         finp, &done),
+                         finp, &done, xs),
         "conv2d_fwd");
   return done;
 }
@@ -1200,14 +1211,22 @@ bool conv_bwd(const at::Tensor& dy, const at::Tensor& w, const at::Tensor& dx, c
 }
 
 void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& dw, int64_t stride, int64_t pad,
-                double beta, int64_t real_channels) {
+                double beta, int64_t real_channels, const c10::optional<at::Tensor>& s2d_xs) {
   check_dev(dy, at::kBFloat16, "dy");
   check_dev(x, at::kBFloat16, "x");
   check_dev(dw, at::kFloat, "dw");
   const ldnn::ConvShape s = wgrad_shape(dy, x, dw, stride, pad, real_channels);
+  const uint16_t* xs = nullptr;
+  if (s2d_xs.has_value()) {
+    check_dev(*s2d_xs, at::kBFloat16, "s2d_xs");
+    TORCH_CHECK(ldnn::stem_s2d_fwd_ok(s) && s2d_xs->is_contiguous() && s2d_xs->numel() == (int64_t)s.N * (s.P + 3) * (s.Q + 3) * 16,
+                "conv_wgrad: s2d_xs must be the forward's packed [N][P+3][Q+3][16] image");
+    xs = bf16_ptr(*s2d_xs);
+  }
   c10::hip::HIPGuardMasqueradingAsCUDA g(dy.device());
   const ConvWs ws = conv_ws(s, 2, dy);
-  check(ldnn::conv2d_wgrad(s, bf16_ptr(dy), bf16_ptr(x), dw.data_ptr<float>(), (float)beta, cur_stream(dy), ws.ws()),
+  check(ldnn::conv2d_wgrad(s, bf16_ptr(dy), bf16_ptr(x), dw.data_ptr<float>(), (float)beta, cur_stream(dy), ws.ws(),
+                           xs),
         "conv2d_wgrad");
 }
 
@@ -2029,7 +2048,18 @@ PYBIND11_MODULE(_C, m) {
         py::arg("bn_gamma") = py::none(), py::arg("bn_beta") = py::none(), py::arg("bn_running_mean") = py::none(),
         py::arg("bn_running_var") = py::none(), py::arg("bn_save_mean") = py::none(),
         py::arg("bn_save_invstd") = py::none(), py::arg("bn_eps") = 1e-5, py::arg("bn_momentum") = 0.1,
-        py::arg("bn_num_batches") = py::none());
+        py::arg("bn_num_batches") = py::none(), py::arg("real_channels") = 0, py::arg("s2d_xs") = py::none());
+  m.def("stem_s2d_fwd_ok", [](int64_t N, int64_t H, int64_t W, int64_t C, int64_t K, int64_t R, int64_t S,
+                              int64_t stride, int64_t pad, int64_t real_channels) {
+        ldnn::ConvShape s{};
+        s.N = (int)N; s.H = (int)H; s.W = (int)W; s.C = (int)C; s.K = (int)K; s.R = (int)R; s.S = (int)S;
+        s.stride = (int)stride; s.pad = (int)pad;
+        s.P = (int)((H + 2 * pad - R) / stride + 1); s.Q = (int)((W + 2 * pad - S) / stride + 1);
+        s.c_real = real_channels > 0 && real_channels < C ? (int)real_channels : 0;
+        return ldnn::get_conv_impl() == 0 && ldnn::stem_s2d_fwd_ok(s);
+      }, "whether conv_fwd takes s2d_xs for this stem shape (the 7x7 / 2 stem on its space-to-depth image)",
+      py::arg("N"), py::arg("H"), py::arg("W"), py::arg("C"), py::arg("K"), py::arg("R"), py::arg("S"),
+      py::arg("stride"), py::arg("pad"), py::arg("real_channels"));
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("stride"), py::arg("pad"),
         py::arg("bn_x") = py::none(), py::arg("bn_mask") = py::none(), py::arg("bn_ws") = py::none(),
         py::arg("bn_gamma") = py::none(), py::arg("bn_save_mean") = py::none(),
@@ -2053,8 +2083,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("set_conv_pair", &ldnn::set_conv_pair, "dgrad + wgrad in one launch (1, default) or one by one (0)");
   m.def("get_conv_pair", &ldnn::get_conv_pair);
   m.def("conv_wgrad", &conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("dw"), py::arg("stride"), py::arg("pad"),
-        py::arg("beta") = 0.0, py::arg("real_channels") = 0,
-        "real_channels: channels of x that carry data (the rest zero padding, e.g. 3 of a stem's 8); 0 = all");
+        py::arg("beta") = 0.0, py::arg("real_channels") = 0, py::arg("s2d_xs") = py::none(),
+        "real_channels: channels of x that carry data (the rest zero padding, e.g. 3 of a stem's 8); 0 = all; "
+        "s2d_xs: the forward's packed space-to-depth image (conv_fwd(s2d_xs=...))");
   m.def("synth_normal", &synth_normal);
   m.def("synth_labels", &synth_labels);
   m.def("augment_batch", &augment_batch, "gather + AutoAugment / flip+crop + normalise (augment.hip)");

@@ -112,7 +112,10 @@ struct BnFin;  // (BatchNorm finalize state, below)
 // (only the LDS-DMA path does it, for EPI_NONE).
 hipError_t conv2d_fwd(const ConvShape& s, const uint16_t* x, const uint16_t* w, uint16_t* y, const float* bias,
                       int epi, hipStream_t st, float* ws = nullptr, int* cnt = nullptr, const BnFin* bn = nullptr,
-                      bool* bn_done = nullptr);
+                      bool* bn_done = nullptr, uint16_t* s2d_xs = nullptr);
+// s2d_xs (ResNet-type 7x7 / 2 stems, stem_s2d_fwd_ok): [N][P+3][Q+3][16] buffer the forward packs the
+// space-to-depth image into and runs on (conv_s2d_ws_kernel); the weight gradient reuses it
+bool stem_s2d_fwd_ok(const ConvShape& s);
 struct BnBwdFuse;  // (a BatchNorm backward whose statistics a dgrad epilogue takes, below)
 // bnb (optional): dx is the gradient of a training BatchNorm(+ReLU)'s output; also accumulate
 // that BN's backward statistics over the bf16 dx and finalize them (*bn_done: whether it did)
@@ -120,7 +123,7 @@ hipError_t conv2d_dgrad(const ConvShape& s, const uint16_t* dy, const uint16_t* 
                         float* ws = nullptr, int* cnt = nullptr, const BnBwdFuse* bnb = nullptr,
                         bool* bn_done = nullptr);
 hipError_t conv2d_wgrad(const ConvShape& s, const uint16_t* dy, const uint16_t* x, float* dw, float beta,
-                        hipStream_t st, float* ws = nullptr);
+                        hipStream_t st, float* ws = nullptr, const uint16_t* s2d_xs = nullptr);
 // A layer's dgrad (shape sd, as conv2d_dgrad) and wgrad (shape sw, as conv2d_wgrad), both reading
 // dy: ONE launch when both take the 4-wave gather kernels (conv2d_bwd_lds), else one by one.
 hipError_t conv2d_bwd(const ConvShape& sd, const uint16_t* dy, const uint16_t* w, uint16_t* dx, float* ws_d,
@@ -131,11 +134,11 @@ hipError_t conv2d_bwd(const ConvShape& sd, const uint16_t* dy, const uint16_t* w
 // bn_used: whether the epilogue accumulated the BN statistics (a slab split-K shape does not)
 hipError_t conv2d_fwd_lds(const ConvShape& s, const uint16_t* x, const uint16_t* w, uint16_t* y, const float* bias,
                           int epi, hipStream_t st, float* ws, int* cnt, const BnFin* bn = nullptr,
-                          bool* bn_used = nullptr);
+                          bool* bn_used = nullptr, uint16_t* s2d_xs = nullptr);
 hipError_t conv2d_dgrad_lds(const ConvShape& s, const uint16_t* dy, const uint16_t* w, uint16_t* dx, hipStream_t st,
                             float* ws, int* cnt, const BnBwdFuse* bnb = nullptr, bool* bn_used = nullptr);
 hipError_t conv2d_wgrad_lds(const ConvShape& s, const uint16_t* dy, const uint16_t* x, float* dw, float beta,
-                            hipStream_t st, float* ws);
+                            hipStream_t st, float* ws, const uint16_t* s2d_xs = nullptr);
 // A downsampling block's 3x3 conv (s0, w0 -> y0) and 1x1 shortcut conv (s1, w1 -> y1) of one
 // input x, each with its optional next-BN statistics: one launch where the kernels allow
 // (conv2d_fwd2_lds), else one by one (conv2d_fwd2).

@@ -308,11 +308,13 @@ void set_conv_impl(int impl) { g_conv_impl = impl; }
 int get_conv_impl() { return g_conv_impl; }
 
 hipError_t conv2d_fwd(const ConvShape& s, const uint16_t* x, const uint16_t* w, uint16_t* y, const float* bias,
-                      int epi, hipStream_t st, float* ws, int* cnt, const BnFin* bn, bool* bn_done) {
+                      int epi, hipStream_t st, float* ws, int* cnt, const BnFin* bn, bool* bn_done,
+                      uint16_t* s2d_xs) {
   if (bn_done) *bn_done = false;
+  if (s2d_xs != nullptr && g_conv_impl != 0) return hipErrorInvalidValue;
   if (g_conv_impl == 0) {
     bool used = false;
-    const hipError_t e = conv2d_fwd_lds(s, x, w, y, bias, epi, st, ws, cnt, bn, &used);
+    const hipError_t e = conv2d_fwd_lds(s, x, w, y, bias, epi, st, ws, cnt, bn, &used, s2d_xs);
     if (e != hipErrorNotSupported) {
       if (bn_done) *bn_done = used && e == hipSuccess;
       return e;
@@ -409,9 +411,10 @@ hipError_t conv2d_dgrad(const ConvShape& s, const uint16_t* dy, const uint16_t* 
 }
 
 hipError_t conv2d_wgrad(const ConvShape& s, const uint16_t* dy, const uint16_t* x, float* dw, float beta,
-                        hipStream_t st, float* ws) {
+                        hipStream_t st, float* ws, const uint16_t* s2d_xs) {
+  if (s2d_xs != nullptr && g_conv_impl != 0) return hipErrorInvalidValue;
   if (g_conv_impl == 0) {
-    const hipError_t e = conv2d_wgrad_lds(s, dy, x, dw, beta, st, ws);
+    const hipError_t e = conv2d_wgrad_lds(s, dy, x, dw, beta, st, ws, s2d_xs);
     if (e != hipErrorNotSupported) return e;
   }
   ConvArgs a{};

@@ -1774,6 +1774,200 @@ __global__ __launch_bounds__(256, 1) void conv_ws64_kernel(LArgs a, const bf16_t
   }
 }
 
+// ---- stem forward on the space-to-depth image (the mapping of stem_s2d_wgrad_kernel below) ----
+//   y[n][p][q][k] = sum_{a,b < 4} w'[k][a][b][.] . xs[n][p + a][q + b][.],  16 s2d channels (32 B)
+// per pixel, w'[k][a][b][(dh, dw, c)] = w[k][2a + dh - 1][2b + dw - 1][c]: K = 256 (8 MFMA k-steps)
+// instead of the 7x7x8 patch kernel's 13, and the input of a 256-pixel tile is <= kRows whole s2d rows,
+// ONE contiguous run of bytes (a linear DMA, no gather).  Persistent: one 4-wave workgroup per CU keeps
+// w' in registers (8 k-steps x 4 filter tiles, gathered from w once), walks a contiguous run of
+// 256-pixel tiles through a 3-buffer ring (the DMA of tiles t+1 and t+2 in flight behind tile t's
+// MFMAs: the patch kernels' loops are bound by the DMA round trip), stages the outputs through LDS
+// for whole-row stores and keeps the next BN's statistics in registers.  Needs P*Q % 256 == 0 (a
+// tile never spans two images) and rows * Ws * 32 <= kBuf (stem_s2d_fwd_ok).
+namespace s2dfwd {
+constexpr int kPieces = 28, kBuf = kPieces * 1024, kNB = 3;
+}
+__global__ __launch_bounds__(256, 1) void conv_s2d_ws_kernel(LArgs a, const bf16_t* pxs, uint32_t bytes_xs, int Hs,
+                                                             int Ws, const bf16_t* pw) {
+  using namespace s2dfwd;
+  constexpr int BM = 256, NW = 4, PPW = kPieces / NW, KS = 8;
+  constexpr int kOutPitch = 144, kOutWave = 64 * kOutPitch;
+  constexpr int LDS = kNB * kBuf + NW * kOutWave + 16;
+  static_assert(PPW * NW == kPieces && LDS <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(1024))) char smem[LDS];
+  const ConvShape& sh = a.s;
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  char* const ostage = smem + kNB * kBuf + wid * kOutWave;
+  const int PQ = sh.P * sh.Q;
+  const int T = a.M / BM;
+  const int t0 = (int)((int64_t)blockIdx.x * T / gridDim.x);
+  const int t1 = (int)((int64_t)(blockIdx.x + 1) * T / gridDim.x);
+  const int g4 = lane >> 4;   // k-elements 8 g4 .. 8 g4 + 7 of a step: tap 2k + (g4 >> 1), channels 8 (g4 & 1) ..
+
+  // w' fragments of every k-step (filter j*16 + (lane & 15)): registers for the launch, all loads in flight
+  bf16x8 fb[KS][4];
+#pragma unroll
+  for (int k = 0; k < KS; ++k)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int t = 2 * k + (g4 >> 1), ta = t >> 2, tb = t & 3;
+      const bf16_t* wn = pw + (size_t)(j * 16 + (lane & 15)) * a.rsc;
+      u16x8 v;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int cc = (g4 & 1) * 8 + e, d = cc >> 2, c = cc & 3;
+        const int r = 2 * ta + (d >> 1) - 1, s = 2 * tb + (d & 1) - 1;
+        v[e] = (r >= 0 && s >= 0) ? reinterpret_cast<const uint16_t*>(wn)[(r * 7 + s) * 8 + c] : (uint16_t)0;
+      }
+      fb[k][j] = __builtin_bit_cast(bf16x8, v);
+    }
+  Rsrc rx;
+  rx.r = __builtin_amdgcn_make_buffer_rsrc((void*)pxs, (short)0, (int)bytes_xs, 0x00020000);
+  // tile t: s2d rows (n, p_lo ..) are contiguous from ((n Hs + p_lo) Ws) * 32 B; bytes past the
+  // buffer read as zeros, bytes of rows past the tile's are loaded and never read
+  auto dma = [&](int t, int b) {
+    const int m0 = t * BM, n_img = m0 / PQ, p_lo = (m0 - n_img * PQ) / sh.Q;
+    const uint32_t base = (uint32_t)(n_img * Hs + p_lo) * (uint32_t)Ws * 32u;
+    char* const dst = smem + b * kBuf;
+#pragma unroll
+    for (int q = 0; q < PPW; ++q) {
+      const int pc = q * NW + wid;
+      const uint32_t o = base + (uint32_t)pc * 1024u + (uint32_t)lane * 16u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx.r, (lds_void*)(dst + pc * 1024), 16, o < bytes_xs ? (int)o : (int)kOOB,
+                                               0, 0, 0);
+    }
+  };
+  if (t0 < t1) {
+    dma(t0, 0);
+    if (t0 + 1 < t1) dma(t0 + 1, 1);
+  }
+  // this lane's tap offset (bytes) per k-step
+  uint32_t toff[KS];
+#pragma unroll
+  for (int k = 0; k < KS; ++k) {
+    const int t = 2 * k + (g4 >> 1);
+    toff[k] = (uint32_t)(((t >> 2) * Ws + (t & 3)) * 32 + (g4 & 1) * 16);
+  }
+  if (t0 < t1) {
+    if (t0 + 1 < t1) wait_vm<PPW>();  // tile t0's pieces landed (and the w' loads, issued before them)
+    else wait_vm<0>();
+  }
+  float bs0[4][4], bs1[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bs0[j][r] = bs1[j][r] = 0.f;
+  bf16_t* const out = reinterpret_cast<bf16_t*>(a.out);
+  for (int t = t0; t < t1; ++t) {
+    const int m0 = t * BM, n_img = m0 / PQ, mi0 = m0 - n_img * PQ, p_lo = mi0 / sh.Q;
+    lds_barrier();  // every wave waited for its own pieces of tile t; every wave is done with tile t-1's buffer
+    if (t + 2 < t1) dma(t + 2, (t + 2 - t0) % kNB);
+    const uint32_t patch = lds_off(smem + ((t - t0) % kNB) * kBuf);
+    uint32_t base[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int mi = mi0 + wid * 64 + i * 16 + (lane & 15);
+      const int p = fdiv(mi, a.f_q), q = mi - p * sh.Q;
+      base[i] = patch + (uint32_t)(((p - p_lo) * Ws + q) * 32);
+    }
+    auto read_step = [&](int k, bf16x8 (&f)[4]) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t ad = base[i] + toff[k];
+        asm volatile("ds_read_b128 %0, %1" : "=v"(f[i]) : "v"(ad));
+      }
+    };
+    floatx4 acc[4][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[j][i] = floatx4{0.f, 0.f, 0.f, 0.f};
+    bf16x8 fa[3][4];
+    read_step(0, fa[0]);
+    read_step(1, fa[1]);
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+      bf16x8 (&f)[4] = fa[k % 3];
+      if (k + 2 < KS) read_step(k + 2, fa[(k + 2) % 3]);
+      if (k + 2 < KS) asm volatile("s_waitcnt lgkmcnt(8)" : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]));
+      else if (k + 1 < KS) asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]));
+      else asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]));
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[k][j], f[i], acc[j][i], 0, 0, 0);
+    }
+    // tile t+1's pieces (issued a tile ago; only tile t+2's were issued after them)
+    if (t + 1 < t1) {
+      if (t + 2 < t1) wait_vm<PPW>();
+      else wait_vm<0>();
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int rl = i * 16 + (lane & 15);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = j * 16 + 4 * (lane >> 4);
+        const floatx4 v = acc[j][i];
+        const u16x4 o = u16x4{f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+        *reinterpret_cast<u16x4*>(ostage + rl * kOutPitch + c * 2) = o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float bv = bf2f(o[r]);
+          bs0[j][r] += bv;
+          bs1[j][r] += bv * bv;
+        }
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // (a wave's LDS operations run in order)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int rl = q * 8 + (lane >> 3);
+      const u32x4 v = *reinterpret_cast<const u32x4*>(ostage + rl * kOutPitch + (lane & 7) * 16);
+      *reinterpret_cast<u32x4*>(out + (size_t)(m0 + wid * 64 + rl) * 64 + (lane & 7) * 8) = v;
+    }
+  }
+  if (a.bn_stats) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          bs0[j][r] += __shfl_xor(bs0[j][r], o, 64);
+          bs1[j][r] += __shfl_xor(bs1[j][r], o, 64);
+        }
+    float* red = reinterpret_cast<float*>(smem);  // [4][64][2]
+    __syncthreads();
+    if ((lane & 15) == 0) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int c = j * 16 + 4 * (lane >> 4) + r;
+          red[(wid * 64 + c) * 2] = bs0[j][r];
+          red[(wid * 64 + c) * 2 + 1] = bs1[j][r];
+        }
+    }
+    __syncthreads();
+    float* accc = a.bn.acc + (size_t)(blockIdx.x % kBnCopies) * 2 * 64;
+    if (threadIdx.x < 64) {
+      float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+      for (int q = 0; q < NW; ++q) {
+        s0 += red[(q * 64 + threadIdx.x) * 2];
+        s1 += red[(q * 64 + threadIdx.x) * 2 + 1];
+      }
+      bn_acc_add(accc + threadIdx.x, s0);
+      bn_acc_add(accc + 64 + threadIdx.x, s1);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's atomics have completed
+    bn_finalize_last<false, kBnCopies>(a.bn, a.M, 64, gridDim.x, red, LDS / 4);
+  }
+}
+
 // ---- ring wgrad: 3x3 stride-1 pad-1 weight gradient, activation rows staged once ----
 // The split-K wgrad above re-gathers x for every filter tap: a 128x128 tile's K-tile
 // moves 32 KiB through the LDS-DMA path for 2 MFLOP, and the pass is fill-bound (its
@@ -3200,6 +3394,14 @@ bool stem_s2d_ok(const ConvShape& s) {
          s.stride == 2 && s.pad == 3 && s.H % 2 == 0 && s.W % 2 == 0 && s.P == s.H / 2 && s.Q == s.W / 2 &&
          (size_t)s.N * (s.P + 3) * (s.Q + 3) * 32 < kOOBLimit;
 }
+// The stem forward on the packed s2d image (conv_s2d_ws_kernel): the wgrad's conditions, bf16 EPI_NONE,
+// tiles that never span two images and whose s2d rows fit one ring buffer.
+bool stem_s2d_fwd_ok(const ConvShape& s) {
+  if (!stem_s2d_ok(s) || g_stem_s2d != 1 || ws_env() == 0) return false;   // (LDNN_CONV_STEM_S2D=2: wgrad only)
+  const int PQ = s.P * s.Q, Ws = s.Q + 3;
+  const int rows = (s.Q - 1 + 255) / s.Q + 1 + 3;   // output rows a 256-pixel tile touches, + the 4x4 taps
+  return PQ % 256 == 0 && (int64_t)rows * Ws * 32 <= s2dfwd::kBuf && (int64_t)s.N * PQ >= 256;
+}
 struct S2dPlan {
   int Hs, Ws, nchunk, steps, slices, steps_per;
   size_t slab_floats, tmp_floats, xs_floats;
@@ -3321,7 +3523,7 @@ hipError_t launch_patch(LArgs a, int epi, const bf16_t* x, size_t bx, const bf16
 // Stems and other small-C convolutions (C in {8, 16, 32}, e.g. the 7x7 ResNet stem
 // on 3 -> 8 padded channels): K-tiles span several taps, one 256x64 / 128x128 tile.
 hipError_t conv2d_fwd_lds_small_c(const ConvShape& s, const uint16_t* x, const uint16_t* w, uint16_t* y,
-                                  const float* bias, int epi, hipStream_t st, const BnFin* bn) {
+                                  const float* bias, int epi, hipStream_t st, const BnFin* bn, uint16_t* s2d_xs) {
   LArgs a = base_args(s);
   if (bn != nullptr && epi == EPI_NONE) {
     a.bn_stats = 1;
@@ -3339,6 +3541,19 @@ hipError_t conv2d_fwd_lds_small_c(const ConvShape& s, const uint16_t* x, const u
   const bool narrow = s.K <= 64;
   a.tiles_x = ((a.M + (narrow ? 255 : 127)) / (narrow ? 256 : 128)) * ((s.K + (narrow ? 63 : 127)) / (narrow ? 64 : 128));
   const size_t bx = (size_t)s.N * s.H * s.W * s.C * 2, bw = (size_t)s.K * a.rsc * 2;
+  if (s2d_xs != nullptr) {   // the caller keeps the packed image for the weight gradient
+    if (epi != EPI_NONE || !stem_s2d_fwd_ok(s)) return hipErrorInvalidValue;
+    const int Hs = s.P + 3, Ws = s.Q + 3;
+    const int64_t npix = (int64_t)s.N * Hs * Ws;
+    stem_s2d_pack_kernel<<<(unsigned)((npix + 255) / 256), 256, 0, st>>>(reinterpret_cast<const bf16_t*>(x),
+                                                                          reinterpret_cast<bf16_t*>(s2d_xs), s.N,
+                                                                          s.H, s.W, Hs, Ws);
+    const int grid = std::max(1, std::min(a.M / 256, cu_count()));
+    a.tiles_x = grid;
+    conv_s2d_ws_kernel<<<grid, 256, 0, st>>>(a, reinterpret_cast<const bf16_t*>(s2d_xs), (uint32_t)(npix * 32), Hs,
+                                             Ws, reinterpret_cast<const bf16_t*>(w));
+    return hipGetLastError();
+  }
   if (patch_ok(s)) return launch_patch(a, epi, x, bx, w, st);
   if (narrow) return launch<4, 1, FwdASmallC<256, 8, 4>, WeightKC<64, 2, 4>, false, false>(a, epi, 1, x, bx, w, bw, st);
   return launch<2, 2, FwdASmallC<128, 4, 4>, WeightKC<128, 4, 4>, false, false>(a, epi, 1, x, bx, w, bw, st);
@@ -3488,14 +3703,16 @@ hipError_t fwd_post(const FwdPrep& f, uint16_t* y, const float* bias, int epi, f
 }  // namespace
 
 hipError_t conv2d_fwd_lds(const ConvShape& s, const uint16_t* x, const uint16_t* w, uint16_t* y, const float* bias,
-                          int epi, hipStream_t st, float* ws, int* cnt, const BnFin* bn, bool* bn_used) {
+                          int epi, hipStream_t st, float* ws, int* cnt, const BnFin* bn, bool* bn_used,
+                          uint16_t* s2d_xs) {
   if (bn_used) *bn_used = bn != nullptr;
-  if (!shape_ok(s)) return hipErrorNotSupported;
+  if (!shape_ok(s)) return s2d_xs ? hipErrorInvalidValue : hipErrorNotSupported;
   if (bn != nullptr && epi != EPI_NONE) return hipErrorInvalidValue;
   if (s.C == 8 || s.C == 16 || s.C == 32) {
-    if (s.N * s.P * s.Q <= 0) return hipErrorNotSupported;
-    return conv2d_fwd_lds_small_c(s, x, w, y, bias, epi, st, bn);
+    if (s.N * s.P * s.Q <= 0) return s2d_xs ? hipErrorInvalidValue : hipErrorNotSupported;
+    return conv2d_fwd_lds_small_c(s, x, w, y, bias, epi, st, bn, s2d_xs);
   }
+  if (s2d_xs != nullptr) return hipErrorInvalidValue;
   if (s.C % 64 != 0) return hipErrorNotSupported;
   if (s.N * s.P * s.Q <= 0) return bn != nullptr ? hipErrorNotSupported : hipSuccess;
   const FwdPrep f = fwd_prep(s, y, bias, epi, ws, cnt, bn);
@@ -3714,16 +3931,21 @@ hipError_t wgrad_post(const WgradPrep& w, float* dw, float beta, float* ws, hipS
 }  // namespace
 
 hipError_t conv2d_wgrad_lds(const ConvShape& s, const uint16_t* dy, const uint16_t* x, float* dw, float beta,
-                            hipStream_t st, float* ws) {
-  if (!shape_ok(s) || s.C % 8 != 0 || s.K % 8 != 0) return hipErrorNotSupported;
-  if (beta != 0.f && beta != 1.f) return hipErrorNotSupported;
+                            hipStream_t st, float* ws, const uint16_t* s2d_xs) {
+  if (!shape_ok(s) || s.C % 8 != 0 || s.K % 8 != 0) return s2d_xs ? hipErrorInvalidValue : hipErrorNotSupported;
+  if (beta != 0.f && beta != 1.f) return s2d_xs ? hipErrorInvalidValue : hipErrorNotSupported;
+  if (s2d_xs != nullptr && !(stem_s2d_ok(s) && ws != nullptr)) return hipErrorInvalidValue;
   if (stem_s2d_ok(s) && ws != nullptr) {
     const S2dPlan p = plan_s2d(s);
     float* slab = ws;
     float* tmp = ws + p.slab_floats;
-    bf16_t* xs = reinterpret_cast<bf16_t*>(tmp + p.tmp_floats);
     const int64_t npix = (int64_t)s.N * p.Hs * p.Ws;
-    stem_s2d_pack_kernel<<<(unsigned)((npix + 255) / 256), 256, 0, st>>>(x, xs, s.N, s.H, s.W, p.Hs, p.Ws);
+    const bf16_t* xs = reinterpret_cast<const bf16_t*>(s2d_xs);
+    if (xs == nullptr) {   // (the forward's packed image when it ran conv_s2d_ws_kernel)
+      bf16_t* xsw = reinterpret_cast<bf16_t*>(tmp + p.tmp_floats);
+      stem_s2d_pack_kernel<<<(unsigned)((npix + 255) / 256), 256, 0, st>>>(x, xsw, s.N, s.H, s.W, p.Hs, p.Ws);
+      xs = xsw;
+    }
     S2dArgs a{};
     a.N = s.N; a.P = s.P; a.Q = s.Q; a.Hs = p.Hs; a.Ws = p.Ws; a.K = s.K;
     a.nchunk = p.nchunk;

@@ -395,14 +395,21 @@ class _Conv2dNative(torch.autograd.Function):
         if relu and b is None:
             b = torch.zeros(kp, dtype=torch.float32, device=x.device)
             epi = C.EPI_BIAS_RELU
+        xs = None
+        if (epi == C.EPI_NONE and cp == 8 and R == 7 and S == 7 and stride == 2
+                and C.stem_s2d_fwd_ok(N, H, W, cp, kp, R, S, stride, pad, Cin)):
+            # a 7x7 / 2 stem: the forward runs on the packed space-to-depth image, which the weight
+            # gradient then reuses (conv_lds.hip conv_s2d_ws_kernel / stem_s2d_wgrad_kernel)
+            xs = torch.empty(N, P + 3, Q + 3, 16, dtype=torch.bfloat16, device=x.device)
         if _fused_bn_ok(bn, K, kp, bias, relu):
             # the conv epilogue accumulates + finalizes the next BN's batch statistics
             args, state = _conv_bn_stats(bn, K, x.device, C)
-            done = C.conv_fwd(xb, w, y, stride, pad, b, epi, **{"bn_" + k: v for k, v in args.items()})
+            done = C.conv_fwd(xb, w, y, stride, pad, b, epi, real_channels=Cin, s2d_xs=xs,
+                              **{"bn_" + k: v for k, v in args.items()})
             _conv_bn_stats_done(bn, done, y, state)
         else:
-            C.conv_fwd(xb, w, y, stride, pad, b, epi)
-        ctx.save_for_backward(xb, y)
+            C.conv_fwd(xb, w, y, stride, pad, b, epi, real_channels=Cin, s2d_xs=xs)
+        ctx.save_for_backward(xb, y, xs)
         ctx.meta = (stride, pad, flat, weight, bias, relu, Cin, x.dtype)
         src = getattr(x, "_ldnn_bnsrc", None)
         ctx.bnsrc = src if (CONV_BN_BWD and src is not None and stride == 1 and src.C == cp == Cin) else None
@@ -411,7 +418,7 @@ class _Conv2dNative(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gy):
         C = _ext.C()
-        xb, y = ctx.saved_tensors
+        xb, y, xs = ctx.saved_tensors
         stride, pad, flat, weight, bias, relu, Cin, in_dtype = ctx.meta
         kp = y.shape[3]
         g = as_nhwc(gy if gy.dtype == torch.bfloat16 else gy.to(torch.bfloat16), kp)
@@ -440,7 +447,7 @@ class _Conv2dNative(torch.autograd.Function):
             if in_dtype != torch.bfloat16:
                 dx = dx.to(in_dtype)
         else:
-            C.conv_wgrad(g, xb, dw, stride, pad, beta, real_channels=Cin)
+            C.conv_wgrad(g, xb, dw, stride, pad, beta, real_channels=Cin, s2d_xs=xs)
         flat.notify(weight, bias)
         return dx, None, None, None, None, None, None, None
 

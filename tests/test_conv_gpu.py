@@ -316,6 +316,51 @@ def test_stem_s2d_wgrad_matches_fp32_and_split_k(N, Cin, H, W):
     assert (outs[1][0][..., 4:] == 0).all()
 
 
+@pytest.mark.parametrize("N,Cin,H,W", [(2, 3, 224, 224), (3, 3, 64, 64), (1, 4, 64, 128), (5, 3, 32, 32)])
+def test_stem_s2d_forward_matches_fp32_and_its_image_feeds_the_wgrad(N, Cin, H, W):
+    """The 7x7 / 2 stem forward on the packed space-to-depth image (conv_fwd(s2d_xs=...),
+    conv_s2d_ws_kernel): == the fp32 reference, == the patch kernel up to fp32 summation order,
+    the next BN's fused statistics == the output's; the weight gradient on the forward's packed
+    image == the one that packs its own (bit for bit)."""
+    torch.manual_seed(19)
+    Cc = _ext.C()
+    K = 64
+    assert Cc.stem_s2d_fwd_ok(N, H, W, 8, K, 7, 7, 2, 3, Cin)
+    assert not Cc.stem_s2d_fwd_ok(3, 112, 112, 8, K, 7, 7, 2, 3, 3)   # (56 x 56 outputs: not 256-aligned)
+    x = torch.zeros(N, H, W, 8, device="cuda", dtype=torch.bfloat16)
+    x[..., :Cin] = torch.randn(N, H, W, Cin, device="cuda").bfloat16()
+    w = torch.zeros(K, 7, 7, 8, device="cuda", dtype=torch.bfloat16)
+    w[..., :Cin] = (torch.randn(K, 7, 7, Cin, device="cuda") * 0.1).bfloat16()
+    P, Q = H // 2, W // 2
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), stride=2, padding=3)
+    ref = ref.permute(0, 2, 3, 1)
+    outs = {}
+    for use in (True, False):
+        y = torch.empty(N, P, Q, K, device="cuda", dtype=torch.bfloat16)
+        xs = torch.empty(N, P + 3, Q + 3, 16, device="cuda", dtype=torch.bfloat16) if use else None
+        ws = torch.zeros(Cc.bn_workspace_floats(K), device="cuda")
+        sm, si = torch.empty(K, device="cuda"), torch.empty(K, device="cuda")
+        done = Cc.conv_fwd(x, w, y, 2, 3, None, 0, bn_ws=ws, bn_gamma=torch.ones(K, device="cuda"),
+                           bn_beta=torch.zeros(K, device="cuda"), bn_save_mean=sm, bn_save_invstd=si,
+                           real_channels=Cin, s2d_xs=xs)
+        assert done
+        outs[use] = (y.float(), sm.clone(), si.clone(), xs)
+    y1, sm1, si1, xs = outs[True]
+    y0 = outs[False][0]
+    scale = ref.abs().max().item()
+    torch.testing.assert_close(y1, ref, rtol=1e-2, atol=1e-2 * scale)
+    torch.testing.assert_close(y1, y0, rtol=1e-2, atol=4e-3 * scale)
+    yb = y1.reshape(-1, K)
+    torch.testing.assert_close(sm1, yb.mean(0), rtol=1e-3, atol=1e-4 * scale)
+    torch.testing.assert_close(1.0 / si1 ** 2, yb.var(0, unbiased=False) + 1e-5, rtol=2e-3, atol=1e-4 * scale ** 2)
+    gy = torch.randn(N, P, Q, K, device="cuda").bfloat16()
+    d0 = torch.full((K, 7, 7, 8), float("nan"), device="cuda")
+    d1 = torch.full((K, 7, 7, 8), float("nan"), device="cuda")
+    Cc.conv_wgrad(gy, x, d0, 2, 3, 0.0, real_channels=Cin)
+    Cc.conv_wgrad(gy, x, d1, 2, 3, 0.0, real_channels=Cin, s2d_xs=xs)
+    assert torch.equal(d0, d1)
+
+
 @pytest.mark.parametrize("N,C,H,W,K", [(2, 128, 28, 28, 128), (8, 128, 31, 31, 128), (64, 128, 16, 16, 128),
                                        (16, 256, 14, 14, 256), (4, 512, 7, 7, 512), (4, 1024, 2, 2, 1024),
                                        (5, 384, 9, 9, 128), (64, 256, 8, 8, 256), (64, 128, 28, 28, 128),
