@@ -193,10 +193,9 @@ def main(argv=None):
     if use_engine:   # the engine synchronises its own gradients (per-step DP) or is a plain replica
         D.broadcast_module(model)
         flat.refresh_shadow()
-    elif (args.sync_every == "step" and world > 1
-          and not (args.topology != "allreduce" and args.grad_comm_dtype != "fp32")):
-        # (per-step gossip buckets travel in fp32: with --grad_comm_dtype bf16 a gossip run
-        # takes the per-step Aggregator path below instead, as it did before round 5)
+    elif args.sync_every == "step" and world > 1:
+        # (--grad_comm_dtype bf16: all-reduce / reduce-scatter buckets and the gossip exchange travel
+        # as bf16 copies of the fp32 gradient)
         weighted = args.aggregation_type == "weighted"
         gossip = {"allreduce": 0, "ring": 1, "double_ring": 2}[args.topology]
         if args.shard_optimizer == "on" and (weighted or gossip):

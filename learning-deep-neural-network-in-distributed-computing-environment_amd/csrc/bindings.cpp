@@ -383,6 +383,26 @@ void mix3(const at::Tensor& out, const at::Tensor& x, const c10::optional<at::Te
   check_dev(x, at::kFloat, "x");
   const int64_t n = out.numel();
   TORCH_CHECK(out.is_contiguous() && x.is_contiguous() && x.numel() == n, "mix3: bad x/out");
+  if (y1.has_value() && y1->scalar_type() == at::kBFloat16) {   // bf16 neighbour copies (gossip exchange)
+    check_dev(*y1, at::kBFloat16, "y1");
+    TORCH_CHECK(y1->is_contiguous() && y1->numel() == n, "mix3: bad y1");
+    const uint16_t* q2 = nullptr;
+    if (y2.has_value()) {
+      check_dev(*y2, at::kBFloat16, "y2");
+      TORCH_CHECK(y2->is_contiguous() && y2->numel() == n, "mix3: bad y2");
+      q2 = bf16_ptr(*y2);
+    }
+    uint16_t* sh16 = nullptr;
+    if (shadow.has_value()) {
+      check_dev(*shadow, at::kBFloat16, "shadow");
+      TORCH_CHECK(shadow->is_contiguous() && shadow->numel() == n, "mix3: bad shadow");
+      sh16 = bf16_mut(*shadow);
+    }
+    check(ldnn::mix3_y16(out.data_ptr<float>(), x.data_ptr<float>(), bf16_ptr(*y1), q2, (float)a, (float)b, (float)c, n,
+                         sh16, cur_stream(out)),
+          "mix3");
+    return;
+  }
   const float* p1 = nullptr;
   const float* p2 = nullptr;
   if (y1.has_value()) {

@@ -322,6 +322,9 @@ hipError_t cast_bf16_f32(const uint16_t* x, float* y, int64_t n, hipStream_t s);
 // y = a*x + b*y1 + c*y2 (fp32, in place on x allowed); optional bf16 shadow of y
 hipError_t mix3_f32(float* out, const float* x, const float* y1, const float* y2, float a, float b, float c,
                     int64_t n, uint16_t* shadow, hipStream_t s);
+// mix3_f32 with bf16 y1 / y2 (the bf16 copies a per-step gossip exchange receives)
+hipError_t mix3_y16(float* out, const float* x, const uint16_t* y1, const uint16_t* y2, float a, float b, float c,
+                    int64_t n, uint16_t* shadow, hipStream_t s);
 // x *= scale (fp32), optional bf16 shadow
 hipError_t scale_f32(float* x, float scale, int64_t n, uint16_t* shadow, hipStream_t s);
 

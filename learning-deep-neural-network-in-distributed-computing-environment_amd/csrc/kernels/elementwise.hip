@@ -333,6 +333,32 @@ __global__ void mix_kernel(float* out, const float* x, const float* y1, const fl
   }
 }
 
+// The same with bf16 neighbour inputs (per-step gossip with a bf16 exchange: the own fp32
+// gradient x mixed with the bf16 copies received from the ring neighbours).
+template <int NIN>
+__global__ void mix_y16_kernel(float* out, const float* x, const uint16_t* y1, const uint16_t* y2, float a, float b,
+                               float c, int64_t n, bf16_t* shadow) {
+  const int64_t nv = n / 4;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nv; i += stride) {
+    floatx4 v = a * reinterpret_cast<const floatx4*>(x)[i];
+    const u16x4 u1 = reinterpret_cast<const u16x4*>(y1)[i];
+    v += b * floatx4{bf2f(u1[0]), bf2f(u1[1]), bf2f(u1[2]), bf2f(u1[3])};
+    if constexpr (NIN >= 3) {
+      const u16x4 u2 = reinterpret_cast<const u16x4*>(y2)[i];
+      v += c * floatx4{bf2f(u2[0]), bf2f(u2[1]), bf2f(u2[2]), bf2f(u2[3])};
+    }
+    reinterpret_cast<floatx4*>(out)[i] = v;
+    if (shadow) reinterpret_cast<u16x4*>(shadow)[i] = u16x4{f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+  }
+  for (int64_t i = nv * 4 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride) {
+    float v = a * x[i] + b * bf2f(y1[i]);
+    if constexpr (NIN >= 3) v += c * bf2f(y2[i]);
+    out[i] = v;
+    if (shadow) shadow[i] = f2bf(v);
+  }
+}
+
 // splitmix64 counter hash -> two uniforms -> Box-Muller normal.
 __device__ __forceinline__ uint64_t smix(uint64_t z) {
   z += 0x9E3779B97F4A7C15ull;
@@ -478,6 +504,16 @@ hipError_t mix3_f32(float* out, const float* x, const float* y1, const float* y2
   if (y2) mix_kernel<3><<<g, kBlock, 0, s>>>(out, x, y1, y2, a, b, c, n, shadow);
   else if (y1) mix_kernel<2><<<g, kBlock, 0, s>>>(out, x, y1, y2, a, b, c, n, shadow);
   else mix_kernel<1><<<g, kBlock, 0, s>>>(out, x, y1, y2, a, b, c, n, shadow);
+  return hipGetLastError();
+}
+
+hipError_t mix3_y16(float* out, const float* x, const uint16_t* y1, const uint16_t* y2, float a, float b, float c,
+                    int64_t n, uint16_t* shadow, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  if (!y1) return hipErrorInvalidValue;
+  const int g = grid_for((n + 3) / 4);
+  if (y2) mix_y16_kernel<3><<<g, kBlock, 0, s>>>(out, x, y1, y2, a, b, c, n, shadow);
+  else mix_y16_kernel<2><<<g, kBlock, 0, s>>>(out, x, y1, y2, a, b, c, n, shadow);
   return hipGetLastError();
 }
 

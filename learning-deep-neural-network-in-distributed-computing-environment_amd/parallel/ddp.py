@@ -126,8 +126,8 @@ class GradBucketer:
         self.flat, self.comm = flat, comm
         self.comm_dtype = None if comm_dtype in (None, torch.float32) else comm_dtype
         self.gossip = int(gossip)
-        if self.gossip and (groups is not None or self.comm_dtype is not None):
-            raise ValueError("per-step gossip exchanges whole fp32 buckets (no sharding, no bf16 stage)")
+        if self.gossip and groups is not None:
+            raise ValueError("per-step gossip exchanges whole buckets (no sharding)")
         self.buckets: list[dict] = []
         N = comm.world_size
         self.shard = groups is not None
@@ -173,7 +173,9 @@ class GradBucketer:
             # hop h: from (r - h), to (r + h); the 2-hop neighbour of a 2-rank world is this
             # rank itself (its own gradient stands in, as parallel.aggregation.gossip_mix)
             self._hops = [((self.rank - h) % N, (self.rank + h) % N) for h in range(1, self.gossip + 1)]
-            self._recv = [[torch.zeros(b["end"] - b["begin"], dtype=torch.float32, device=dev)
+            # (comm_dtype bf16: each bucket's bf16 copy goes out, the neighbours' bf16 copies come in
+            # and are mixed into the own fp32 gradient -- half the bytes on every link)
+            self._recv = [[torch.zeros(b["end"] - b["begin"], dtype=self.comm_dtype or torch.float32, device=dev)
                            if src != self.rank else None for src, _ in self._hops] for b in self.buckets]
             self.weighted = False   # (the all-reduce's self-weighted mix is not used)
         elif self.weighted:
@@ -250,7 +252,7 @@ class GradBucketer:
         """Issue bucket i's collective (async): reduce-scatter into this rank's shard
         buffer for a sharded bucket, else an in-place SUM all-reduce."""
         if self.gossip:
-            g = self.grad_view(i)
+            g = self.comm_buffer(i)   # (the bf16 stage with comm_dtype, else the fp32 gradient)
             recvs = [(rb, src) for rb, (src, _) in zip(self._recv[i], self._hops) if rb is not None]
             sends = [(g, dst) for rb, (_, dst) in zip(self._recv[i], self._hops) if rb is not None]
             return self.comm.sendrecv(sends, recvs, async_op=True) if recvs else None
@@ -267,9 +269,17 @@ class GradBucketer:
                 from .aggregation import _mix
 
                 g = self.grad_view(i)
-                ys = [rb if rb is not None else g for rb in self._recv[i]]
-                a, b, c = self._mix_abc
-                _mix(g, g, ys[0], ys[1] if len(ys) > 1 else None, a=a, b=b, c=c)
+                # a hop whose neighbour is this rank itself (the 2-rank double ring) mixes the own
+                # gradient: its coefficient folds into the own term
+                a, *cs = self._mix_abc[:1 + len(self._recv[i])]
+                ys = []
+                for rb, cf in zip(self._recv[i], cs):
+                    if rb is None:
+                        a += cf
+                    else:
+                        ys.append((rb, cf))
+                _mix(g, g, ys[0][0] if ys else None, ys[1][0] if len(ys) > 1 else None, a=a,
+                     b=ys[0][1] if ys else 0.0, c=ys[1][1] if len(ys) > 1 else 0.0)
             return
         if self.buckets[i]["sharded"]:
             lo, hi = self.shard_range(i)

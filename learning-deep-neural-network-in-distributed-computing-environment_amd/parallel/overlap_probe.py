@@ -148,6 +148,14 @@ class _JoinAll:
             j.wait()
 
 
+def _as_f32(t):
+    """The bytes of a received buffer as fp32 words (a bf16 exchange moves half the bytes)."""
+    v = t.view(-1)
+    if v.dtype == torch.float32:
+        return v
+    return v[:v.numel() // 2 * 2].view(torch.float32)
+
+
 class P2PProbeComm:
     """A world-of-``world`` stand-in for per-step data parallelism on ONE GPU without sharding:
     ``gossip`` 1 / 2 (DataParallel(gossip=...), BR/communication.py:5-62, BDR/communication.py:5-77)
@@ -179,7 +187,7 @@ class P2PProbeComm:
     def sendrecv(self, sends, recvs, async_op=False):
         if not self.enabled:
             return None
-        return _JoinAll([self.links[k](("p2p", k, rt.data_ptr()), rt.view(-1)) for k, (rt, _) in enumerate(recvs)])
+        return _JoinAll([self.links[k](("p2p", k, rt.data_ptr()), _as_f32(rt)) for k, (rt, _) in enumerate(recvs)])
 
     def all_reduce(self, t, op="sum", async_op=False):
         if not self.enabled:
@@ -197,7 +205,7 @@ class P2PProbeComm:
 
 def measure_gossip(model_name: str = "enhanced_cnn", batch: int = 64, world: int = 8, bucket_mb: float = 32.0,
                    optimizer: str = "adam", steps: int = 20, rounds: int = 3, link_gbps: float = 150.0,
-                   bus_gbps: float = 300.0) -> list:
+                   bus_gbps: float = 300.0, comm_dtype: str = "fp32") -> list:
     """The graphed per-step DP step (GraphedDPStep, segmented: each bucket's exchange issued between
     the backward's graph links) with the all-reduce (gossip 0), the ring (1) and the double ring (2)
     on a P2PProbeComm world: one row per topology -- the chain with every collective a no-op, the
@@ -223,7 +231,8 @@ def measure_gossip(model_name: str = "enhanced_cnn", batch: int = 64, world: int
         xavier_init(m)
         ldnn.prepare(m, dev)
         comm = P2PProbeComm(dev, world, link_gbps, bus_gbps)
-        dp = DataParallel(m, comm, bucket_cap_mb=bucket_mb, broadcast_init=False, gossip=gossip)
+        dp = DataParallel(m, comm, bucket_cap_mb=bucket_mb, broadcast_init=False, gossip=gossip,
+                          comm_dtype=torch.bfloat16 if comm_dtype == "bf16" else None)
         o = SGD(m.parameters(), lr=0.01, momentum=0.9) if optimizer == "sgd" else Adam(m.parameters(), lr=1e-3)
         o.zero_grad()
         crit(dp(x), y).backward()
@@ -255,7 +264,7 @@ def measure_gossip(model_name: str = "enhanced_cnn", batch: int = 64, world: int
                 best[k] = min(best[k], _timed(f, steps))
         exposed = best["with_standin_ms"] - best["chain_ms"]
         rows.append({"model": model_name, "batch": batch, "optimizer": optimizer,
-                     "topology": {0: "allreduce", 1: "ring", 2: "double_ring"}[gossip],
+                     "topology": {0: "allreduce", 1: "ring", 2: "double_ring"}[gossip], "grad_comm_dtype": comm_dtype,
                      "mode": f"graphed per-step DP, world {world} stand-in (links {link_gbps:.0f} GB/s, "
                              f"all-reduce bus {bus_gbps:.0f} GB/s)", "buckets": len(bk.buckets),
                      "segments": gd.n_segments, **{k: round(v, 4) for k, v in best.items()},
@@ -570,7 +579,7 @@ def main():
     ap.add_argument("--shard", type=int, default=0, help="world size of the sharded-step probe (0 = all-reduce step)")
     ap.add_argument("--optimizer", choices=["sgd", "adam"], default="sgd")
     ap.add_argument("--grad-comm", choices=["fp32", "bf16"], default="bf16",
-                    help="gradient collective dtype of the sharded step")
+                    help="gradient collective dtype of the sharded step and of the --gossip rows")
     ap.add_argument("--gossip", action="store_true",
                     help="per-step all-reduce vs ring vs double-ring gossip rows (P2PProbeComm, world --shard or 8)")
     ap.add_argument("--rounds", type=int, default=3)
@@ -578,7 +587,8 @@ def main():
                     "(kernel-trace timelines: scripts/probe_timeline.py)")
     a = ap.parse_args()
     if a.gossip:
-        for row in measure_gossip(a.model, a.batch, a.shard or 8, a.bucket_mb, a.optimizer, a.steps, a.rounds):
+        for row in measure_gossip(a.model, a.batch, a.shard or 8, a.bucket_mb, a.optimizer, a.steps, a.rounds,
+                                  comm_dtype=a.grad_comm):
             print(json.dumps(row), flush=True)
         return
     if a.model == "mlp3":   # the headline engine (StaticMLPEngine), sharded at world --shard (default 8)

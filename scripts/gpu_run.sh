@@ -23,9 +23,9 @@ for step in "$@"; do
     probe:*) IFS=@ read -r m b sh reps opt <<< "${step#probe:}"
              $T 300 python -u scripts/overlap_probe.py --model $m --batch $b --shard ${sh:-0} --reps ${reps:-1} \
                --optimizer ${opt:-sgd} ${PROBE_ARGS:-} >> $O/overlap_probe.jsonl 2>> $O/overlap_probe.err ;;
-    gossip:*) IFS=@ read -r m b opt <<< "${step#gossip:}"
+    gossip:*) IFS=@ read -r m b opt dt <<< "${step#gossip:}"
              $T 400 python -u scripts/overlap_probe.py --gossip --model $m --batch $b --optimizer ${opt:-adam} \
-               >> $O/gossip_probe.jsonl 2>> $O/gossip_probe.err ;;
+               --grad-comm ${dt:-bf16} >> $O/gossip_probe.jsonl 2>> $O/gossip_probe.err ;;
     proto) rc=0   # round-6 conv prototypes (XF 128: B to VGPRs, XF 64: BN fold on A), alternated 2x
            for r in 1 2; do for xf in 0 128 64; do
              LDNN_CONV_XF=$xf $T 150 python -u scripts/conv_proto_ab.py --batch 256 >> $O/proto_rn256.jsonl 2>> $O/proto.err || { rc=$?; break 2; }

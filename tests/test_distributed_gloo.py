@@ -217,9 +217,9 @@ def test_cli_two_ranks_end_to_end(tmp_path):
 
 
 @pytest.mark.slow
-def test_cli_step_gossip_with_bf16_flag_runs_the_aggregator_path(tmp_path):
-    """--sync_every step --topology ring --grad_comm_dtype bf16: gossip buckets are
-    fp32-only, so the run takes the per-step Aggregator path instead of exiting."""
+def test_cli_step_gossip_with_bf16_flag_runs(tmp_path):
+    """--sync_every step --topology ring --grad_comm_dtype bf16: the per-step gossip
+    exchange sends each bucket's bf16 copy (DataParallel(gossip=1, comm_dtype=bf16))."""
     port = _port()
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
            "--master-port", str(port), os.path.join(ROOT, "train.py"), "--model", "mlp2", "--dataset", "mnist",

@@ -121,7 +121,7 @@ def test_rccl_world1_overlap_path(tmp_path):
 
 @pytest.mark.parametrize("extra", [[], ["--shard"], ["--shard", "--optimizer", "adam"],
                                    ["--shard", "--comm-dtype", "bf16"], ["--gossip", "1"],
-                                   ["--gossip", "2", "--optimizer", "adam"]])
+                                   ["--gossip", "2", "--optimizer", "adam"], ["--gossip", "1", "--comm-dtype", "bf16"]])
 def test_graphed_dp_two_ranks_gloo_equals_big_batch(extra):
     """2 ranks (gloo, sharing the GPU) through train_local_epoch(graphs=True, dp=...)
     end with the parameters of ONE graphed rank on the concatenated batches -- also

@@ -225,6 +225,22 @@ def test_adam_matches_torch():
     torch.testing.assert_close(p, p_ref.detach(), rtol=1e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("two", [False, True])
+def test_mix3_with_bf16_neighbour_inputs(two):
+    """The gossip exchange's combine: own fp32 gradient + the neighbours' bf16 copies, fp32 out
+    (+ the bf16 shadow) == the fp32 formula on the widened inputs."""
+    torch.manual_seed(8)
+    n = 4099
+    x = torch.randn(n, device="cuda")
+    y1, y2 = torch.randn(n, device="cuda").bfloat16(), torch.randn(n, device="cuda").bfloat16()
+    out = torch.empty_like(x)
+    sh = torch.empty(n, device="cuda", dtype=torch.bfloat16)
+    C().mix3(out, x, y1, y2 if two else None, 0.4, 0.3, 0.3 if two else 0.0, sh)
+    ref = 0.4 * x + 0.3 * y1.float() + (0.3 * y2.float() if two else 0.0)
+    torch.testing.assert_close(out, ref, rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(sh, ref.bfloat16(), rtol=0, atol=0)
+
+
 def test_mix3_and_colsum_and_act():
     torch.manual_seed(7)
     n = 5003
