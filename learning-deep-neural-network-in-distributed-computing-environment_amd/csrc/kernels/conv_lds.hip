@@ -753,12 +753,9 @@ __device__ __forceinline__ void conv_tail(const LArgs& a, const Geo& g, floatx4 
 // 16-KiB-aligned chunks instead of the im2col gather, bit2 no fragment reads / MFMAs, bit5 phase
 // trace: wave 0 stamps s_memrealtime (100 MHz) at entry, after the first K-tile landed, after
 // the main loop and at exit into a.trace[workgroup][4] (scripts/conv_phase_trace.py).
-// Round-6 prototypes (fwd 128x128 gather only; scripts/conv_micro.py):
-// bit7 the B (weight) fragments loaded straight to VGPRs in the MFMA layout, one K-tile ahead, so
-// only the A operand goes through LDS-DMA (bit-identical output); bit6 a BatchNorm + ReLU applied
-// to every A fragment after its LDS read, with the tap's row bounds re-checked (padding must stay
-// 0) -- the per-fragment VALU cost of folding the mid-block BN into its consumer conv (timing only:
-// affine from kernel arguments).
+// (Round 6 built and measured two more operand forms here -- B fragments straight to VGPRs and a
+// BN + ReLU fold on the A fragments -- 1.8x / 1.74x slower, profiles/r6/conv_proto_ab.jsonl; their
+// code was removed after the A/B, commit 0e684d8 has it.)
 // (the body of conv_lds_kernel: smem = its NS-stage LDS ring, vb = its grid coordinates)
 template <int WM, int WN, class OA, class OB, int EPI, bool OUT_F32, bool DGRAD, int NS, int XF = 0>
 __device__ __forceinline__ void conv_lds_body(const LArgs& a, const bf16_t* pa, uint32_t bytes_a, const bf16_t* pb,
@@ -772,9 +769,6 @@ __device__ __forceinline__ void conv_lds_body(const LArgs& a, const bf16_t* pa, 
   static_assert(PPA >= 1 && PPB >= 1 && PPA * NW * 8 == BM && PPB * NW * 8 == BN, "DMA pieces");
   constexpr int PER_TILE = PPA + PPB;  // DMA instructions per lane per K-tile
   static_assert(NS >= 2 && NS * STAGE <= 160 * 1024 && PER_TILE * (NS - 2) < 64, "LDS ring");
-  constexpr bool kBD = (XF & 128) != 0, kFold = (XF & 64) != 0;
-  static_assert(!(kBD || kFold) || (NS == 2 && std::is_same_v<OB, WeightKC<BN, PPB, NW>> && !DGRAD),
-                "prototype bits: fwd gather kernel only");
 
   const Geo g = make_geo(a, DGRAD, vb.z);
   const int tiles_m = (g.M + BM - 1) / BM, tiles_n = (a.N + BN - 1) / BN;
@@ -818,39 +812,6 @@ __device__ __forceinline__ void conv_lds_body(const LArgs& a, const bf16_t* pa, 
     ra.r = __builtin_amdgcn_make_buffer_rsrc((void*)pa, (short)0, (int)bytes_a, 0x00020000);
     rb.r = __builtin_amdgcn_make_buffer_rsrc((void*)pb, (short)0, (int)bytes_b, 0x00020000);
     KS ks = ks_init(a, g, kt0);
-    bf16x8 fbr[2][4], fbn[2][4];   // (kBD: this / the next K-tile's B fragments)
-    auto load_b = [&](bf16x8 (&f)[2][4], const KS& k) {
-      const int koff = (k.r * a.s.S + k.s) * a.s.C + k.cb * 64 + (lane >> 4) * 8;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int n = n0 + wn * 64 + j * 16 + (lane & 15);
-        const bf16_t* src = pb + (size_t)(n < a.N ? n : 0) * a.rsc + koff;
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
-          const bf16x8 v = *reinterpret_cast<const bf16x8*>(src + kk * 32);
-          f[kk][j] = n < a.N ? v : bf16x8{};
-        }
-      }
-    };
-    int fih[4], fiw[4];   // (kFold: each A fragment row's top-left input pixel)
-    float fsc[2][8], fsh[2][8];
-    if constexpr (kFold) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int m = m0 + (wm * 4 + i) * 16 + (lane & 15);
-        const int t = fdiv(m, g.f_rw), q = m - t * a.s.Q, n = fdiv(t, g.f_rh), p = t - n * a.s.P;
-        fih[i] = m < g.M ? p * a.s.stride - a.s.pad : -(1 << 20);
-        fiw[i] = q * a.s.stride - a.s.pad;
-      }
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          fsc[kk][e] = 1.f + a.beta * (float)(kk * 8 + e);
-          fsh[kk][e] = a.beta * 0.5f;
-        }
-    }
-    if constexpr (kBD) load_b(fbr, ks);
     // prologue: K-tiles 0 .. NS-2 into stages 0 .. NS-2
 #pragma unroll
     for (int t = 0; t < NS - 1; ++t) {
@@ -861,7 +822,7 @@ __device__ __forceinline__ void conv_lds_body(const LArgs& a, const bf16_t* pa, 
           ob.advance(a);
         }
         if constexpr (!(XF & 16)) DMA_TILE(oa, PPA, ra, smem + t * STAGE, ks);
-        if constexpr (!(XF & 8) && !kBD) DMA_TILE(ob, PPB, rb, smem + t * STAGE + A_BYTES, ks);
+        if constexpr (!(XF & 8)) DMA_TILE(ob, PPB, rb, smem + t * STAGE + A_BYTES, ks);
       }
     }
 
@@ -877,7 +838,6 @@ __device__ __forceinline__ void conv_lds_body(const LArgs& a, const bf16_t* pa, 
       if constexpr ((XF & 32) != 0) {
         if (kt == 0 && trace != nullptr) trace[1] = __builtin_amdgcn_s_memrealtime();
       }
-      const KS kcur = ks;   // (NS == 2: the tap of tile kt, for the kFold bounds)
       if (!(XF & 1) && kt + NS - 1 < nk) {
         ks_next(a, g, ks);
         oa.advance(a);
@@ -893,8 +853,7 @@ __device__ __forceinline__ void conv_lds_body(const LArgs& a, const bf16_t* pa, 
         } else if constexpr (!(XF & 16)) {
           DMA_TILE(oa, PPA, ra, nxt, ks);
         }
-        if constexpr (kBD) load_b(fbn, ks);
-        else if constexpr (!(XF & 8)) DMA_TILE(ob, PPB, rb, nxt + A_BYTES, ks);  // XF 8 / 16: no B / A fill
+        if constexpr (!(XF & 8)) DMA_TILE(ob, PPB, rb, nxt + A_BYTES, ks);  // XF 8 / 16: no B / A fill
       }
       const char* la = smem + cur * STAGE;
       const char* lb = la + A_BYTES;
@@ -911,20 +870,7 @@ __device__ __forceinline__ void conv_lds_body(const LArgs& a, const bf16_t* pa, 
 #pragma unroll
         for (int i = 0; i < 4; ++i) fa[kk][i] = read_frag<OA::KC, BM>(la, wm * 4 + i, kk, lane);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) fb[kk][j] = kBD ? fbr[kk][j] : read_frag<OB::KC, BN>(lb, wn * 4 + j, kk, lane);
-      }
-      if constexpr (kFold) {   // relu(scale * x + shift) per channel, 0 where the tap is padding
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const bool ok = (unsigned)(fih[i] + kcur.r) < (unsigned)a.s.H && (unsigned)(fiw[i] + kcur.s) < (unsigned)a.s.W;
-#pragma unroll
-          for (int kk = 0; kk < 2; ++kk) {
-            bf16x8 v = fa[kk][i];
-#pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] = (__bf16)(ok ? fmaxf((float)v[e] * fsc[kk][e] + fsh[kk][e], 0.f) : 0.f);
-            fa[kk][i] = v;
-          }
-        }
+        for (int j = 0; j < 4; ++j) fb[kk][j] = read_frag<OB::KC, BN>(lb, wn * 4 + j, kk, lane);
       }
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk)
@@ -934,12 +880,6 @@ __device__ __forceinline__ void conv_lds_body(const LArgs& a, const bf16_t* pa, 
           for (int i = 0; i < 4; ++i)
             acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[kk][j], fa[kk][i], acc[j][i], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
-      if constexpr (kBD) {
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) fbr[kk][j] = fbn[kk][j];
-      }
       cur = cur == NS - 1 ? 0 : cur + 1;
     }
   }
@@ -1423,9 +1363,9 @@ constexpr int kSlots = kHPitch / 16;
 constexpr int kWBytes = 64 * kPitch;   // 74,752 B
 }  // namespace ws64
 
-// XF (LDNN_CONV_XF experiment builds): bit0 no halo DMA after the first two tiles, bit1 no
-// epilogue stores, bit2 no A fragment reads, bit3 no waits on the fragment reads (results wrong
-// by construction), bit4 reads kept but the MFMAs take register operands, bit5 phase trace.
+// XF = 32 (LDNN_CONV_XF=32 builds): the phase trace.  (The round-4 knockout builds -- no halo DMA,
+// no stores, no fragment reads, no waits, register operands: profiles/r4/conv_ws64_micro.jsonl --
+// were removed in round 6.)
 template <int RT, bool DGRAD, int XF = 0>
 __global__ __launch_bounds__(256, 1) void conv_ws64_kernel(LArgs a, const bf16_t* pa, uint32_t bytes_a,
                                                            const bf16_t* pw) {
@@ -1588,9 +1528,7 @@ __global__ __launch_bounds__(256, 1) void conv_ws64_kernel(LArgs a, const bf16_t
     auto read_step = [&](int st, bf16x8 (&f)[RT]) {
 #pragma unroll
       for (int i = 0; i < RT; ++i) {
-        if constexpr ((XF & 4) != 0) {
-          f[i] = fb[st >> 1][st & 1][i & 1];  // knockout: no A fragment reads
-        } else if ((st & 1) == 0) {
+        if ((st & 1) == 0) {
           asm volatile("ds_read_b128 %0, %1" : "=v"(f[i]) : "v"(ab[i][st >> 1]));
         } else {
           asm volatile("ds_read_b128 %0, %1 offset:64" : "=v"(f[i]) : "v"(ab[i][st >> 1]));
@@ -1623,7 +1561,6 @@ __global__ __launch_bounds__(256, 1) void conv_ws64_kernel(LArgs a, const bf16_t
       }
     }
     __builtin_amdgcn_s_setprio(1);
-    uint32_t sink = 0;
     // step st = tap * 2 + kk: its RT fragment reads are issued two steps ahead
     static_assert(RT == 4, "the counted waits below name 4 fragments");
     bf16x8 fa[3][RT];
@@ -1633,43 +1570,24 @@ __global__ __launch_bounds__(256, 1) void conv_ws64_kernel(LArgs a, const bf16_t
     for (int st = 0; st < 18; ++st) {
       bf16x8 (&f)[RT] = fa[st % 3];
       if (st + 2 < 18) read_step(st + 2, fa[(st + 2) % 3]);
-      if constexpr ((XF & 12) == 0) {  // step st's reads landed; steps st+1, st+2 (<= 2 RT reads) may be in flight
-        if (st + 2 < 18) asm volatile("s_waitcnt lgkmcnt(8)" : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]));
-        else if (st + 1 < 18) asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]));
-        else asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]));
-      }
+      // step st's reads landed; steps st+1, st+2 (<= 2 RT reads) may be in flight
+      if (st + 2 < 18) asm volatile("s_waitcnt lgkmcnt(8)" : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]));
+      else if (st + 1 < 18) asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]));
+      else asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]));
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int i = 0; i < RT; ++i)
-          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[st >> 1][st & 1][j],
-                                                              (XF & 16) != 0 ? fb[st >> 1][st & 1][i & 1] : f[i], acc[j][i], 0, 0, 0);
-      if constexpr ((XF & 16) != 0) {  // knockout: reads kept (consumed by a VALU xor), MFMAs on registers
-#pragma unroll
-        for (int i = 0; i < RT; ++i) sink ^= __builtin_bit_cast(uint4, f[i]).x;
-      }
+          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[st >> 1][st & 1][j], f[i], acc[j][i], 0, 0, 0);
     }
-    if constexpr ((XF & 8) != 0) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_setprio(0);
-    if constexpr ((XF & 16) != 0) {
-      if (sink == 0x12345679u) out[lane] = 0;
-    }
     lds_barrier();  // every wave is done reading this buffer
-    if (t + 2 < t1 && (XF & 1) == 0) dma(t + 2, (t - t0) & 1);
+    if (t + 2 < t1) dma(t + 2, (t - t0) & 1);
     if (t + 1 < t1) {
       // tile t+1's pieces: issued a whole tile ago, followed only by the stores of tile t-1 and
       // tile t+2's pieces -- vmcnt(PPW) holds whether or not stores retire in order with loads
-      if (t + 2 < t1 && (XF & 1) == 0) wait_vm<PPW>();
+      if (t + 2 < t1) wait_vm<PPW>();
       else wait_vm<0>();
-    }
-    if constexpr ((XF & 2) != 0) {  // knockout: no epilogue stores (keep the accumulators live)
-      float z = 0.f;
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int i = 0; i < RT; ++i) z += acc[j][i][0] + acc[j][i][1] + acc[j][i][2] + acc[j][i][3];
-      if (z == 12345.f) out[lane] = 0;
-      continue;
     }
     // epilogue: bf16 rows (8 B = 4 channels per lane), the BN sums of the rounded values
     u16x4 bxv[RT][2];
@@ -3047,15 +2965,7 @@ hipError_t launch_ns(LArgs a, int epi, int splits, const bf16_t* pa, size_t ba, 
   if constexpr ((std::is_same_v<OA, FwdA<128, 4, 4>> || std::is_same_v<OA, WgradA<64, 2, 4>> ||
                  std::is_same_v<OA, WgradA<128, 4, 4>> || std::is_same_v<OA, DgradA<128, 4, 4>>) && NS == 2) {
     const int xf = conv_xf_env();
-    if constexpr (std::is_same_v<OA, FwdA<128, 4, 4>>) {   // (round-6 prototypes, fwd only; other passes run normally)
-      if ((xf == 64 || xf == 128 || xf == 192) && epi == EPI_NONE && a.nb > 0) {
-        if (xf == 64) conv_lds_kernel<WM, WN, OA, OB, EPI_NONE, OUT_F32, DGRAD, NS, 64><<<grid, block, 0, st>>>(a, pa, (uint32_t)ba, pb, (uint32_t)bb);
-        else if (xf == 128) conv_lds_kernel<WM, WN, OA, OB, EPI_NONE, OUT_F32, DGRAD, NS, 128><<<grid, block, 0, st>>>(a, pa, (uint32_t)ba, pb, (uint32_t)bb);
-        else conv_lds_kernel<WM, WN, OA, OB, EPI_NONE, OUT_F32, DGRAD, NS, 192><<<grid, block, 0, st>>>(a, pa, (uint32_t)ba, pb, (uint32_t)bb);
-        return hipGetLastError();
-      }
-    }
-    if (xf != 0 && xf != 64 && xf != 128 && xf != 192 && epi == EPI_NONE) {
+    if (xf != 0 && epi == EPI_NONE) {
       switch (xf) {
         case 1: conv_lds_kernel<WM, WN, OA, OB, EPI_NONE, OUT_F32, DGRAD, NS, 1><<<grid, block, 0, st>>>(a, pa, (uint32_t)ba, pb, (uint32_t)bb); break;
         case 2:
@@ -3154,15 +3064,6 @@ hipError_t launch_ws64_m(LArgs a, int grid, const bf16_t* pa, size_t ba, const b
   const int xf = conv_xf_env();
   if (xf == 32) {
     conv_ws64_kernel<RT, DGRAD, 32><<<grid, 256, 0, st>>>(a, pa, (uint32_t)ba, pw);
-  } else if (xf == 1 || xf == 2 || xf == 4 || xf == 7 || xf == 8 || xf == 10 || xf == 16) {  // knockouts (fwd timing only)
-    if constexpr (DGRAD) return hipErrorInvalidValue;
-    else if (xf == 1) conv_ws64_kernel<RT, false, 1><<<grid, 256, 0, st>>>(a, pa, (uint32_t)ba, pw);
-    else if (xf == 2) conv_ws64_kernel<RT, false, 2><<<grid, 256, 0, st>>>(a, pa, (uint32_t)ba, pw);
-    else if (xf == 4) conv_ws64_kernel<RT, false, 4><<<grid, 256, 0, st>>>(a, pa, (uint32_t)ba, pw);
-    else if (xf == 8) conv_ws64_kernel<RT, false, 8><<<grid, 256, 0, st>>>(a, pa, (uint32_t)ba, pw);
-    else if (xf == 10) conv_ws64_kernel<RT, false, 10><<<grid, 256, 0, st>>>(a, pa, (uint32_t)ba, pw);
-    else if (xf == 16) conv_ws64_kernel<RT, false, 16><<<grid, 256, 0, st>>>(a, pa, (uint32_t)ba, pw);
-    else conv_ws64_kernel<RT, false, 7><<<grid, 256, 0, st>>>(a, pa, (uint32_t)ba, pw);
   } else
     conv_ws64_kernel<RT, DGRAD><<<grid, 256, 0, st>>>(a, pa, (uint32_t)ba, pw);
   return hipGetLastError();

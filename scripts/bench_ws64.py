@@ -5,7 +5,8 @@ against the halo kernel (set_conv_ws 0).  One JSON line per (batch, mode): media
 event-timed launches for fwd (with the fused BN statistics when --bn) and dgrad.
 
     python scripts/bench_ws64.py [--batches 64,256]
-    LDNN_CONV_XF=1|2|4|7 python scripts/bench_ws64.py --modes 1 --fwd-only   # knockouts
+    (the LDNN_CONV_XF=1|2|4|7 knockout builds of the ws64 forward were removed in round 6;
+    profiles/r4/conv_ws64_micro.jsonl holds their results)
 """
 import argparse
 import json
@@ -41,7 +42,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batches", default="64,256")
     ap.add_argument("--modes", default="0,1")
-    ap.add_argument("--fwd-only", action="store_true", help="LDNN_CONV_XF knockout builds exist for fwd only")
+    ap.add_argument("--fwd-only", action="store_true", help="time the forward pass only")
     ap.add_argument("--no-stem", action="store_true")
     a = ap.parse_args()
     for N in (int(b) for b in a.batches.split(",")):

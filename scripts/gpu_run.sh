@@ -26,11 +26,6 @@ for step in "$@"; do
     gossip:*) IFS=@ read -r m b opt dt <<< "${step#gossip:}"
              $T 400 python -u scripts/overlap_probe.py --gossip --model $m --batch $b --optimizer ${opt:-adam} \
                --grad-comm ${dt:-bf16} >> $O/gossip_probe.jsonl 2>> $O/gossip_probe.err ;;
-    proto) rc=0   # round-6 conv prototypes (XF 128: B to VGPRs, XF 64: BN fold on A), alternated 2x
-           for r in 1 2; do for xf in 0 128 64; do
-             LDNN_CONV_XF=$xf $T 150 python -u scripts/conv_proto_ab.py --batch 256 >> $O/proto_rn256.jsonl 2>> $O/proto.err || { rc=$?; break 2; }
-             LDNN_CONV_XF=$xf $T 150 python -u scripts/conv_proto_ab.py --batch 64 --model enhanced_cnn >> $O/proto_ecnn64.jsonl 2>> $O/proto.err || { rc=$?; break 2; }
-           done; done; (exit $rc) ;;
     probetrace:*) IFS=@ read -r m b sh reps opt <<< "${step#probetrace:}"
              (cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
              $T 400 rocprofv3 --kernel-trace -d $O/probetrace_${m}_$sh -o run -- python -u scripts/overlap_probe.py \
@@ -71,9 +66,6 @@ for step in "$@"; do
            else $T 400 bash scripts/pmc_step.sh $tg python3 scripts/bench_cnn.py --model $m --batch $b --steps 3 --warmup 2 --no-stock > $O/pmc_$tg.txt 2>&1; fi
            rc=$?; cp -f gpurun_out/pmc_$tg/table.txt $O/pmc_${tg}_table.txt 2>/dev/null; (exit $rc) ;;
     wsbench) $T 200 python -u scripts/bench_ws64.py >> $O/bench_ws64.jsonl 2>> $O/bench_ws64.err ;;
-    wsko) rc=0   # knockout builds of the weight-stationary conv (fwd, b256): XF bits, see conv_ws64_kernel
-          for xf in ${WS_XF:-1 2 4 8}; do LDNN_CONV_XF=$xf $T 100 python -u scripts/bench_ws64.py --modes 1 --fwd-only --no-stem \
-            --batches 256 >> $O/ws_knockouts.jsonl 2>> $O/bench_ws64.err || { rc=$?; break; }; done; (exit $rc) ;;
     wspmc) (cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
            timeout -s KILL 90 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_LDS \
              SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_WAVES GRBM_GUI_ACTIVE --output-format csv -d $O/wspmc/p1 -o run -- \
