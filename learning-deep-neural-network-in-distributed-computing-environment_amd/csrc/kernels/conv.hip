@@ -250,6 +250,70 @@ inline int splitk_for(int tiles, int Kd) {
 // 4 pixels per thread 48 us and 4 channels per thread 29 us -- the loop is load-latency
 // bound -- and the weights through scalar loads as SGPR operands 35 us.)
 constexpr int kDgradC8MaxW = 8192;
+
+// K == 16 (LeNet-5's second conv: 6 -> 16 channels, 5x5) on the MFMA pipe instead:
+// dx[pixel][c] = sum_{tap, k} dy[the tap's output pixel][k] w[k][tap][c] with MFMA A = w^T
+// (16 rows = channels, 8 of them real, held in registers for the launch: one fragment per
+// 32-deep k-step = 2 taps x 16 filters) and B = a 16-pixel tile's dy fragments, one 16-B
+// gather per lane per k-step (a tap outside the output reads nothing: zero).  A lane ends with
+// 4 consecutive channels of one pixel: 8-B stores, 256 contiguous bytes per tile.  One wave per
+// tile.
+template <int KS, int SS, bool ST1>   // SS = R = S (5 / 3); ST1: stride 1 (no tap divisibility tests)
+__global__ __launch_bounds__(256) void conv_dgrad_c8k16_kernel(ConvShape s, const bf16_t* __restrict__ dy,
+                                                               const bf16_t* __restrict__ w, bf16_t* __restrict__ dx,
+                                                               int tiles) {
+  __shared__ __attribute__((aligned(16))) uint16_t wl[16 * 2 * KS * 8];   // w [16][RS][8] (16-B staged)
+  const int lane = threadIdx.x & 63, g = lane >> 4, l16 = lane & 15;
+  constexpr int RS = SS * SS;
+  static_assert(2 * KS >= RS, "k-steps");
+  for (int i = threadIdx.x; i < 16 * RS; i += 256)   // (scattered 2-B global gathers per lane were the cost)
+    reinterpret_cast<u16x8*>(wl)[i] = reinterpret_cast<const u16x8*>(w)[i];
+  __syncthreads();
+  bf16x8 fa[KS];
+#pragma unroll
+  for (int k = 0; k < KS; ++k) {
+    const int tap = 2 * k + (g >> 1);
+    u16x8 v;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int kf = (g & 1) * 8 + e;
+      v[e] = (l16 < 8 && tap < RS) ? wl[(kf * RS + tap) * 8 + l16] : (uint16_t)0;
+    }
+    fa[k] = __builtin_bit_cast(bf16x8, v);
+  }
+  const int npix = s.N * s.H * s.W;   // (the dispatcher checks it fits 31 bits)
+  for (int t = blockIdx.x * 4 + (threadIdx.x >> 6); t < tiles; t += gridDim.x * 4) {
+  const int pix = t * 16 + l16;
+  const bool pv = pix < npix;
+  const int tt = pv ? pix / s.W : 0;
+  const int wq = pv ? pix - tt * s.W : 0;
+  const int n = tt / s.H, h = tt - n * s.H;
+  const bf16_t* dyn = dy + (size_t)n * s.P * s.Q * 16 + (g & 1) * 8;
+  floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < KS; ++k) {
+    const int tap = 2 * k + (g >> 1);
+    const int r = tap / SS, sx = tap - r * SS;   // (compile-time divisor)
+    const int ph = h + s.pad - r, qw = wq + s.pad - sx;
+    int p, q;
+    bool ok;
+    if constexpr (ST1) {
+      p = ph;
+      q = qw;
+      ok = pv && tap < RS && ph >= 0 && qw >= 0 && p < s.P && q < s.Q;
+    } else {
+      p = ph / s.stride;
+      q = qw / s.stride;
+      ok = pv && tap < RS && ph >= 0 && qw >= 0 && ph == p * s.stride && qw == q * s.stride && p < s.P && q < s.Q;
+    }
+    u16x8 b = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (ok) b = *reinterpret_cast<const u16x8*>(dyn + ((size_t)p * s.Q + q) * 16);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[k], __builtin_bit_cast(bf16x8, b), acc, 0, 0, 0);
+  }
+  if (g < 2 && pv)
+    *reinterpret_cast<u16x4*>(dx + pix * 8 + 4 * g) = u16x4{f2bf(acc[0]), f2bf(acc[1]), f2bf(acc[2]), f2bf(acc[3])};
+  }
+}
 constexpr int kDgradC8Threads = 64;
 
 __global__ __launch_bounds__(kDgradC8Threads) void conv_dgrad_c8_kernel(ConvShape s, const bf16_t* __restrict__ dy,
@@ -257,7 +321,12 @@ __global__ __launch_bounds__(kDgradC8Threads) void conv_dgrad_c8_kernel(ConvShap
                                                                         bf16_t* __restrict__ dx) {
   __shared__ __attribute__((aligned(16))) float wl[kDgradC8MaxW];
   const int RS = s.R * s.S, nw = s.K * RS * 8;
-  for (int i = threadIdx.x; i < nw; i += kDgradC8Threads) wl[i] = bf2f(w[i]);
+  // (16-B weight loads: the 2-B ones left each workgroup's staging a chain of ~50 loads per lane)
+  for (int i = threadIdx.x; i < nw / 8; i += kDgradC8Threads) {
+    const u16x8 v = reinterpret_cast<const u16x8*>(w)[i];
+    reinterpret_cast<floatx4*>(wl)[2 * i] = floatx4{bf2f(v[0]), bf2f(v[1]), bf2f(v[2]), bf2f(v[3])};
+    reinterpret_cast<floatx4*>(wl)[2 * i + 1] = floatx4{bf2f(v[4]), bf2f(v[5]), bf2f(v[6]), bf2f(v[7])};
+  }
   __syncthreads();
   const int64_t pix = (int64_t)blockIdx.x * kDgradC8Threads + threadIdx.x;
   if (pix >= (int64_t)s.N * s.H * s.W) return;
@@ -387,6 +456,22 @@ hipError_t conv2d_dgrad(const ConvShape& s, const uint16_t* dy, const uint16_t* 
     const hipError_t e = conv2d_dgrad_lds(s, dy, w, dx, st, ws, cnt, bnb, bn_done);
     if (e != hipErrorNotSupported) return e;
     if (bn_done) *bn_done = false;
+  }
+  if (g_conv_impl == 0 && s.C == 8 && s.K == 16 && s.stride >= 1 && s.R == s.S && (s.R == 5 || s.R == 3) &&
+      (int64_t)s.N * s.H * s.W + 16 < (1ll << 31)) {
+    const int64_t pix = (int64_t)s.N * s.H * s.W;
+    if (pix <= 0) return hipSuccess;
+    const int tiles = (int)((pix + 15) / 16);
+    const unsigned blocks = (unsigned)std::min((tiles + 3) / 4, 512);   // (a few tiles per wave: w staged once)
+    const bf16_t* dy16 = reinterpret_cast<const bf16_t*>(dy);
+    const bf16_t* w16 = reinterpret_cast<const bf16_t*>(w);
+    bf16_t* dx16 = reinterpret_cast<bf16_t*>(dx);
+    const bool st1 = s.stride == 1;
+    if (s.R == 5 && st1) conv_dgrad_c8k16_kernel<13, 5, true><<<blocks, 256, 0, st>>>(s, dy16, w16, dx16, tiles);
+    else if (s.R == 5) conv_dgrad_c8k16_kernel<13, 5, false><<<blocks, 256, 0, st>>>(s, dy16, w16, dx16, tiles);
+    else if (st1) conv_dgrad_c8k16_kernel<5, 3, true><<<blocks, 256, 0, st>>>(s, dy16, w16, dx16, tiles);
+    else conv_dgrad_c8k16_kernel<5, 3, false><<<blocks, 256, 0, st>>>(s, dy16, w16, dx16, tiles);
+    return hipGetLastError();
   }
   if (g_conv_impl == 0 && s.C == 8 && s.K % 8 == 0 && s.K * s.R * s.S * 8 <= kDgradC8MaxW && s.stride >= 1) {
     const int64_t pix = (int64_t)s.N * s.H * s.W;
