@@ -249,6 +249,64 @@ inline int splitk_for(int tiles, int Kd) {
 // reads the same address: LDS broadcasts): 22 us.  (Measured alternatives, all slower:
 // 4 pixels per thread 48 us and 4 channels per thread 29 us -- the loop is load-latency
 // bound -- and the weights through scalar loads as SGPR operands 35 us.)
+// The forward of the same small convs (C == 8 padded input channels, K <= 16 filters, 3x3 / 5x5
+// stride 1: LeNet-5's two convs) on the MFMA pipe: MFMA A = w (16 rows = filters, one 16-B row of
+// 8 channels per lane per tap: the fragments are plain loads, held for the launch), B = a 16-pixel
+// tile's input patch, one 16-B gather per lane per 4-tap k-step (a tap in the padding reads
+// nothing: zero).  A lane ends with 4 consecutive filters of one pixel: bias (+ ReLU), 8-B store.
+template <int KS, int SS, int EPI>
+__global__ __launch_bounds__(256) void conv_fwd_c8_mfma_kernel(ConvShape s, const bf16_t* __restrict__ x,
+                                                               const bf16_t* __restrict__ w,
+                                                               const float* __restrict__ bias, bf16_t* __restrict__ y,
+                                                               int tiles) {
+  constexpr int RS = SS * SS;
+  static_assert(4 * KS >= RS, "k-steps");
+  const int lane = threadIdx.x & 63, g = lane >> 4, l16 = lane & 15;
+  bf16x8 fa[KS];
+#pragma unroll
+  for (int k = 0; k < KS; ++k) {
+    const int tap = 4 * k + g;
+    u16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (tap < RS && l16 < s.K) v = *reinterpret_cast<const u16x8*>(w + ((size_t)l16 * RS + tap) * 8);
+    fa[k] = __builtin_bit_cast(bf16x8, v);
+  }
+  float bv[4] = {0.f, 0.f, 0.f, 0.f};
+  if constexpr (EPI != EPI_NONE) {
+#pragma unroll
+    for (int v = 0; v < 4; ++v) bv[v] = 4 * g + v < s.K ? bias[4 * g + v] : 0.f;
+  }
+  const int npix = s.N * s.P * s.Q;   // (the dispatcher checks it fits 31 bits)
+  for (int t = blockIdx.x * 4 + (threadIdx.x >> 6); t < tiles; t += gridDim.x * 4) {
+    const int pix = t * 16 + l16;
+    const bool pv = pix < npix;
+    const int tt = pv ? pix / s.Q : 0;
+    const int q = pv ? pix - tt * s.Q : 0;
+    const int n = tt / s.P, p = tt - n * s.P;
+    const bf16_t* xn = x + (size_t)n * s.H * s.W * 8;
+    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+      const int tap = 4 * k + g;
+      const int r = tap / SS, sx = tap - r * SS;   // (compile-time divisor)
+      const int ih = p - s.pad + r, iw = q - s.pad + sx;
+      const bool ok = pv && tap < RS && ih >= 0 && iw >= 0 && ih < s.H && iw < s.W;
+      u16x8 b = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (ok) b = *reinterpret_cast<const u16x8*>(xn + ((size_t)ih * s.W + iw) * 8);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[k], __builtin_bit_cast(bf16x8, b), acc, 0, 0, 0);
+    }
+    if (pv && 4 * g < s.K) {
+      u16x4 o;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        float z = acc[v] + bv[v];
+        if constexpr (EPI == EPI_BIAS_RELU) z = fmaxf(z, 0.f);
+        o[v] = f2bf(z);
+      }
+      *reinterpret_cast<u16x4*>(y + (size_t)pix * s.K + 4 * g) = o;
+    }
+  }
+}
+
 constexpr int kDgradC8MaxW = 8192;
 
 // K == 16 (LeNet-5's second conv: 6 -> 16 channels, 5x5) on the MFMA pipe instead:
@@ -381,6 +439,31 @@ hipError_t conv2d_fwd(const ConvShape& s, const uint16_t* x, const uint16_t* w, 
                       uint16_t* s2d_xs) {
   if (bn_done) *bn_done = false;
   if (s2d_xs != nullptr && g_conv_impl != 0) return hipErrorInvalidValue;
+  if (g_conv_impl == 0 && s2d_xs == nullptr && bn == nullptr && s.C == 8 && (s.K == 8 || s.K == 16) &&
+      s.stride == 1 && s.R == s.S && (s.R == 5 || s.R == 3) && (epi == EPI_NONE || bias != nullptr) &&
+      (epi == EPI_NONE || epi == EPI_BIAS || epi == EPI_BIAS_RELU) && (int64_t)s.N * s.P * s.Q + 16 < (1ll << 31)) {
+    // the small-channel convs (LeNet-5) on the MFMA kernel above
+    const int64_t npix = (int64_t)s.N * s.P * s.Q;
+    if (npix <= 0) return hipSuccess;
+    const int tiles = (int)((npix + 15) / 16);
+    const unsigned blocks = (unsigned)std::min((tiles + 3) / 4, 1024);
+    const bf16_t* x16 = reinterpret_cast<const bf16_t*>(x);
+    const bf16_t* w16 = reinterpret_cast<const bf16_t*>(w);
+    bf16_t* y16 = reinterpret_cast<bf16_t*>(y);
+#define C8F_CASE(KS_, SS_)                                                                                     \
+  switch (epi) {                                                                                               \
+    case EPI_NONE: conv_fwd_c8_mfma_kernel<KS_, SS_, EPI_NONE><<<blocks, 256, 0, st>>>(s, x16, w16, bias, y16, tiles); break;      \
+    case EPI_BIAS: conv_fwd_c8_mfma_kernel<KS_, SS_, EPI_BIAS><<<blocks, 256, 0, st>>>(s, x16, w16, bias, y16, tiles); break;      \
+    default: conv_fwd_c8_mfma_kernel<KS_, SS_, EPI_BIAS_RELU><<<blocks, 256, 0, st>>>(s, x16, w16, bias, y16, tiles); break;       \
+  }
+    if (s.R == 5) {
+      C8F_CASE(7, 5)
+    } else {
+      C8F_CASE(3, 3)
+    }
+#undef C8F_CASE
+    return hipGetLastError();
+  }
   if (g_conv_impl == 0) {
     bool used = false;
     const hipError_t e = conv2d_fwd_lds(s, x, w, y, bias, epi, st, ws, cnt, bn, &used, s2d_xs);

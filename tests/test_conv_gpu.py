@@ -96,7 +96,7 @@ def test_conv_fwd_dgrad_wgrad(N, C, H, W, K, R, st, pad):
                                                 (3, 8, 32, 32, 128, 3, 1, 1), (3, 8, 17, 17, 24, 3, 2, 1),
                                                 (4, 8, 14, 14, 16, 5, 1, 0), (3, 8, 13, 13, 16, 3, 1, 1),
                                                 (2, 8, 15, 15, 16, 3, 2, 1), (2, 8, 12, 12, 16, 5, 1, 2),
-                                                (256, 8, 14, 14, 16, 5, 1, 0)])
+                                                (256, 8, 14, 14, 16, 5, 1, 0), (4, 8, 28, 28, 8, 5, 1, 2), (3, 8, 9, 9, 8, 3, 1, 1)])
 def test_lds_fast_path_matches_generic_kernel(N, C, H, W, K, R, st, pad):
     """The LDS-DMA kernels (set_conv_impl(0)) agree with the generic register-staged
     kernels (set_conv_impl(1)) on every output, and repeated launches of the
