@@ -2899,7 +2899,8 @@ WgradPlan plan_wgrad(const ConvShape& s, bool allow_ring = true) {
   // 1.642 -> 1.573 ms with the slab target at 256, ResNet-18 b64 / b256 -0.3 / -0.2 %; the 1x1
   // shortcut wgrads stay at 8: 16 there cost ResNet-18 b64 +0.6 %, profiles/r5/conv_split_knobs_ab.txt)
   constexpr int min_kt3 = 16;
-  const int min_kt = s.R * s.S > 1 ? min_kt3 : min_kt1;
+  // (C = 8 / K <= 16 -- LeNet-5 -- : one 64x256 tile, the slices' K loops are the whole pass)
+  const int min_kt = (s.C <= 8 && s.K <= 16) ? 4 : s.R * s.S > 1 ? min_kt3 : min_kt1;
   if (p.tiles < 256) splits = std::max(1, std::min((target + p.tiles - 1) / p.tiles, p.nk_all / min_kt));
   p.nk_split = (p.nk_all + splits - 1) / splits;
   p.splits = (p.nk_all + p.nk_split - 1) / p.nk_split;
