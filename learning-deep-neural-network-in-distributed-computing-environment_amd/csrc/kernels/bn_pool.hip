@@ -1270,7 +1270,9 @@ hipError_t bn_maxpool_backward(const BnArgs& a, int N, int H, int W, int P, int 
   const dim3 ga(gx, std::min(rows, 65535));                                // apply: one block row per workgroup
   if (xam) {   // statistics from the pooled side (the forward stored x at every argmax)
     const int npos = N * P * Q;
-    const int nb = (int)std::min<int64_t>(((int64_t)npos * cv + kBlock - 1) / kBlock, bnpool_blocks());
+    // (512 workgroups: each adds its 2 x C partial sums into the accumulator copies -- with the 2048
+    // of bnpool_blocks that same-address atomic traffic bounded the pass, 37 us at b64)
+    const int nb = (int)std::min<int64_t>(((int64_t)npos * cv + kBlock - 1) / kBlock, 512);
     bn_maxpool_bwd_reduce_am_kernel<<<nb, kBlock, 0, s>>>(xam, dy, a.dy2, arg, a.save_mean, a.save_invstd, f.acc,
                                                           npos, N * H * W, C, f, bn_ncop(true, nb));
     if (pad) bn_maxpool_bwd_apply_kernel<1><<<ga, kBlock, 0, s>>>(a.x, dy, a.dy2, arg, f.coef, dx, N, H, W, C, P, Q);
