@@ -977,7 +977,7 @@ bool conv_fwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& y, int
               const c10::optional<at::Tensor>& bn_running_mean, const c10::optional<at::Tensor>& bn_running_var,
               const c10::optional<at::Tensor>& bn_save_mean, const c10::optional<at::Tensor>& bn_save_invstd,
               double bn_eps, double bn_momentum, const c10::optional<at::Tensor>& bn_num_batches,
-              int64_t real_channels, const c10::optional<at::Tensor>& s2d_xs) {
+              int64_t real_channels, const c10::optional<at::Tensor>& s2d_xs, bool s2d_packed) {
   check_dev(x, at::kBFloat16, "x");
   check_dev(w, at::kBFloat16, "w");
   check_dev(y, at::kBFloat16, "y");
@@ -991,7 +991,9 @@ bool conv_fwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& y, int
                     s2d_xs->size(2) == s.Q + 3 && s2d_xs->size(3) == 16,
                 "conv_fwd: s2d_xs must be a dense [N][P+3][Q+3][16] bf16 tensor");
     xs = bf16_mut(*s2d_xs);
+    s.s2d_packed = s2d_packed ? 1 : 0;
   }
+  TORCH_CHECK(!s2d_packed || s2d_xs.has_value(), "conv_fwd: s2d_packed needs s2d_xs");
   const float* b = nullptr;
   if (bias.has_value()) {
     check_dev(*bias, at::kFloat, "bias");
@@ -1818,7 +1820,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("ws") = py::none(), py::arg("cnt") = py::none(), py::arg("mask_out") = py::none(),
         py::arg("mask_in") = py::none(), py::arg("head_w") = py::none(), py::arg("head_part") = py::none());
   m.def("nchw_to_nhwc", [](const at::Tensor& src, const at::Tensor& dst, const c10::optional<at::Tensor>& extra_src,
-                           const c10::optional<at::Tensor>& extra_dst) {
+                           const c10::optional<at::Tensor>& extra_dst, const c10::optional<at::Tensor>& s2d) {
         TORCH_CHECK(src.is_cuda() && src.dim() == 4 && src.is_contiguous() &&
                         (src.scalar_type() == at::kFloat || src.scalar_type() == at::kBFloat16),
                     "nchw_to_nhwc: src must be a contiguous NCHW fp32 / bf16 CUDA tensor");
@@ -1841,11 +1843,26 @@ PYBIND11_MODULE(_C, m) {
           eb = (int64_t)extra_src->nbytes();
         }
         c10::hip::HIPGuardMasqueradingAsCUDA g(src.device());
+        if (s2d.has_value()) {   // also the stem's space-to-depth image (conv_fwd(s2d_xs=..., s2d_packed=True))
+          check_dev(*s2d, at::kBFloat16, "s2d");
+          TORCH_CHECK(C <= 4 && dst.size(3) == 8 && H % 2 == 0 && W % 2 == 0 && s2d->is_contiguous() && s2d->dim() == 4 &&
+                          s2d->size(0) == N && s2d->size(1) == H / 2 + 3 && s2d->size(2) == W / 2 + 3 &&
+                          s2d->size(3) == 16 && aligned16(s2d->data_ptr()) &&
+                          ((uintptr_t)src.data_ptr() % (src.scalar_type() == at::kFloat ? 8 : 4)) == 0,
+                      "nchw_to_nhwc: s2d needs C <= 4, an 8-channel dst, even H and W and a dense "
+                      "[N][H/2+3][W/2+3][16] bf16 image");
+          check(ldnn::nchw_to_nhwc_s2d(src.data_ptr(), src.scalar_type() == at::kFloat, bf16_mut(dst), bf16_mut(*s2d),
+                                       (int)N, (int)C, (int)H, (int)W, cur_stream(src), es, ed, eb),
+                "nchw_to_nhwc_s2d");
+          return;
+        }
         check(ldnn::nchw_to_nhwc(src.data_ptr(), src.scalar_type() == at::kFloat, bf16_mut(dst), (int)N, (int)C,
                                  (int)(H * W), (int)dst.size(3), cur_stream(src), es, ed, eb),
               "nchw_to_nhwc");
-      }, "NCHW fp32/bf16 -> NHWC bf16 with zeroed pad channels (+ an extra same-launch copy, e.g. labels)",
-      py::arg("src"), py::arg("dst"), py::arg("extra_src") = py::none(), py::arg("extra_dst") = py::none());
+      }, "NCHW fp32/bf16 -> NHWC bf16 with zeroed pad channels (+ an extra same-launch copy, e.g. labels; + the "
+         "7x7 / 2 stem's packed space-to-depth image when s2d is given)",
+      py::arg("src"), py::arg("dst"), py::arg("extra_src") = py::none(), py::arg("extra_dst") = py::none(),
+      py::arg("s2d") = py::none());
   m.def("transpose_bf16", [](const at::Tensor& in, const at::Tensor& out) {
         check_dev(in, at::kBFloat16, "in");
         check_dev(out, at::kBFloat16, "out");
@@ -2068,7 +2085,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("bn_gamma") = py::none(), py::arg("bn_beta") = py::none(), py::arg("bn_running_mean") = py::none(),
         py::arg("bn_running_var") = py::none(), py::arg("bn_save_mean") = py::none(),
         py::arg("bn_save_invstd") = py::none(), py::arg("bn_eps") = 1e-5, py::arg("bn_momentum") = 0.1,
-        py::arg("bn_num_batches") = py::none(), py::arg("real_channels") = 0, py::arg("s2d_xs") = py::none());
+        py::arg("bn_num_batches") = py::none(), py::arg("real_channels") = 0, py::arg("s2d_xs") = py::none(),
+        py::arg("s2d_packed") = false);
   m.def("stem_s2d_fwd_ok", [](int64_t N, int64_t H, int64_t W, int64_t C, int64_t K, int64_t R, int64_t S,
                               int64_t stride, int64_t pad, int64_t real_channels) {
         ldnn::ConvShape s{};

@@ -103,6 +103,7 @@ struct ConvShape {
   int P, Q;         // output spatial size
   int stride, pad;
   int c_real;       // channels of C that carry data (the rest are zero padding); 0 = all C
+  int s2d_packed;   // conv2d_fwd with s2d_xs: the image is already packed (nchw_to_nhwc's s2d output)
 };
 // ws / cnt: optional in-launch split-K workspace for small-M shapes (conv2d_lds_workspace);
 // without it those shapes run unsplit.
@@ -315,6 +316,10 @@ hipError_t transpose_bf16(const uint16_t* in, uint16_t* out, int rows, int cols,
 // NCHW (fp32 / bf16) -> NHWC bf16 [N][HW][cp], pad channels zeroed (cp % 8 == 0)
 hipError_t nchw_to_nhwc(const void* src, bool src_f32, uint16_t* dst, int N, int C, int HW, int cp, hipStream_t s,
                         const void* extra_src = nullptr, void* extra_dst = nullptr, int64_t extra_bytes = 0);
+// The same for a <= 4-channel input of even H, W into an 8-channel dst, also writing the stem's 2x2
+// space-to-depth image s2d[N][H/2+3][W/2+3][16] (conv_stem.hip stem_s2d_pack_kernel's layout) in the pass.
+hipError_t nchw_to_nhwc_s2d(const void* src, bool src_f32, uint16_t* dst, uint16_t* s2d, int N, int C, int H,
+                            int W, hipStream_t s, const void* extra_src, void* extra_dst, int64_t extra_bytes);
 // sum split-K slabs [splits][rows][ldw] into out[rows][ncols] (stride ldo); extra[r] = column ncols
 hipError_t slab_sum_cols(const float* ws, int splits, int rows, int ldw, float* out, int ldo, int ncols, float* extra,
                          hipStream_t s);

@@ -32,170 +32,17 @@
 // across the MFMAs of tile t (one raw s_barrier per K-tile, never
 // __syncthreads while a DMA is outstanding); 2 workgroups per CU.  LDS images
 // and fragment reads are those of gemm.hip (ldnn_gemm_tile.h).
+// The launch arguments, geometry and epilogues shared with the C = 8 stem kernels live in
+// ldnn_conv_lds.h; the stem kernels themselves (space-to-depth, patch) in conv_stem.hip.
 #include <algorithm>
 #include <cstdlib>
 #include <type_traits>
 
-#include "ldnn_common.h"
-#include "ldnn_fastdiv.h"
-#include "ldnn_bn_fin.h"
-#include "ldnn_gemm_tile.h"
-#include "ldnn_kernels.h"
+#include "ldnn_conv_lds.h"
 
 namespace ldnn {
 
 namespace convlds {
-
-constexpr uint32_t kOOB = 0x80000000u;      // >= num_records: reads as zero
-constexpr int kSlabBytes4 = 16 * 256 * 16;  // one 4-wave workgroup's fp32 accumulators
-
-struct LArgs {
-  ConvShape s;
-  void* out;
-  const float* bias;
-  float beta;        // fp32 outputs: out = acc + beta * out
-  int M, N;          // GEMM rows / columns
-  int nk_all;        // K-tiles of the reduction (largest class)
-  int nk_split;      // K-tiles per gridDim.y slice
-  int nb;            // fwd: C/64, dgrad: K/64 channel blocks per tap; 0 = wgrad
-  int Kd;            // wgrad: NPQ (reduction length)
-  int rsc, pq;
-  int classes;       // 4 = stride-2 dgrad parity classes (grid.z), else 1
-  int tiles_x;       // gridDim.x
-  int dn, dp, dq;    // wgrad: 64 = dn*PQ + dp*Q + dq
-  int taps_per_tile; // fwd with C < 64: 64 / C
-  FastDiv f_pq, f_q, f_c, f_s;
-  FastDiv f_p, f_w, f_h;         // row decompositions: fwd (P, Q), dgrad (H, W)
-  FastDiv f_cw[2], f_ch[2];      // stride-2 dgrad class rows: (W - pw + 1) / 2, (H - ph + 1) / 2
-  float* ws;         // split-K: combine slabs (with cnt) or wgrad partial slabs [split][M][N] (without)
-  int* cnt;          // split-K arrival counters of the in-launch combine
-  int bn_stats;      // fwd: accumulate + finalize the next BatchNorm's statistics (bn); weight-stationary
-                     // dgrad: the backward statistics of the BN whose output's gradient dx is (bn, bnb_*)
-  BnFin bn;
-  const bf16_t* bnb_x;     // (ws64 dgrad with bn_stats) that BN's input [M][64]
-  const uint8_t* bnb_mask; // its ReLU bits [M][8] (nullptr: no ReLU)
-  int tap_major;     // fwd / dgrad K-tile order: 0 = channel block fastest, 1 = filter tap fastest
-  int f32_rows;      // fp32 outputs (wgrad, split-K slabs) through the row-coalesced LDS epilogue
-  int bf16_rows;     // bf16 outputs (fwd y, stride-1 dgrad dx) through the row-coalesced LDS epilogue
-  int remap_rows;    // stride-2 dgrad dx (class row remap) through the row-coalesced LDS epilogue
-  int xcd_split;     // split-K grids: the tiles of one K slice share an XCD (see split_coords)
-  uint64_t* trace;   // XF bit 5 (phase-trace builds): [workgroup][8] s_memrealtime stamps
-  int combine_last;  // in-launch split-K: the last K slice sums (splitk_combine_last), else the last arrival
-};
-
-// (tile, K slice) of this workgroup.  Default: tile = blockIdx.x, slice = blockIdx.y.  With
-// xcd_split the linear workgroup id goes through the XCD remap first, so the gridDim.x tiles
-// of one slice -- which read the same activation rows (a wgrad's filter-tap / channel tiles
-// over one npq range) -- are dispatched to ONE XCD and share its L2 instead of each of 8
-// XCDs fetching those rows from the Infinity Cache / HBM.
-// The workgroup's grid coordinates: the hardware's, or virtual ones when two convolutions share
-// one launch (conv_pair_kernel: a layer's dgrad and wgrad side by side).
-struct VB {
-  int x, y, z, gx, gy;
-};
-__device__ __forceinline__ VB hw_vb() {
-  return VB{(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z, (int)gridDim.x, (int)gridDim.y};
-}
-
-__device__ __forceinline__ void split_coords(const LArgs& a, const VB& vb, int& bx, int& by) {
-  bx = vb.x;
-  by = vb.y;
-  if (a.xcd_split && vb.gy > 1) {
-    const int id = xcd_remap(vb.x + vb.y * vb.gx, vb.gx * vb.gy);
-    bx = id % vb.gx;
-    by = id / vb.gx;
-  }
-}
-
-// Per-workgroup geometry: which rows its class covers and which taps it sums.
-struct Geo {
-  int M;                   // GEMM rows of this class
-  int rows_h, rows_w;      // row = (n, h2, w2) over rows_h x rows_w
-  int hmul, hoff, woff;    // pixel h = hmul*h2 + hoff
-  int r0, s0, step, nS;    // taps r = r0 + step*i (< R), s likewise
-  int nk;                  // K-tiles of this class
-  FastDiv f_rw, f_rh;      // division by rows_w / rows_h
-};
-
-__device__ __forceinline__ Geo make_geo(const LArgs& a, bool dgrad, int cls) {
-  Geo g;
-  const ConvShape& s = a.s;
-  g.hmul = 1; g.hoff = 0; g.woff = 0; g.r0 = 0; g.s0 = 0; g.step = 1; g.nS = s.S;
-  g.M = a.M;
-  g.nk = a.nk_all;
-  if (!dgrad) {  // fwd rows = output pixels
-    g.rows_h = s.P; g.rows_w = s.Q;
-    g.f_rh = a.f_p; g.f_rw = a.f_q;
-    return g;
-  }
-  g.rows_h = s.H; g.rows_w = s.W;
-  g.f_rh = a.f_h; g.f_rw = a.f_w;
-  if (a.classes == 4) {
-    const int ph = cls >> 1, pw = cls & 1;
-    g.hmul = 2; g.hoff = ph; g.woff = pw;
-    g.rows_h = (s.H - ph + 1) >> 1;
-    g.rows_w = (s.W - pw + 1) >> 1;
-    g.f_rh = a.f_ch[ph];
-    g.f_rw = a.f_cw[pw];
-    g.M = s.N * g.rows_h * g.rows_w;
-    g.r0 = (ph + s.pad) & 1;
-    g.s0 = (pw + s.pad) & 1;
-    g.step = 2;
-    const int nR = g.r0 < s.R ? (s.R - g.r0 + 1) >> 1 : 0;
-    g.nS = g.s0 < s.S ? (s.S - g.s0 + 1) >> 1 : 0;
-    g.nk = nR * g.nS * a.nb;
-  }
-  return g;
-}
-
-// Per-K-tile scalar state: tap (r, s) and channel block cb of K-tile kt.
-struct KS {
-  int kt, r, s, cb;
-};
-
-__device__ __forceinline__ KS ks_init(const LArgs& a, const Geo& g, int kt) {
-  KS k;
-  k.kt = kt;
-  if (a.nb > 0 && g.nS > 0 && a.tap_major) {
-    const int ntaps = g.nk / a.nb;  // taps of this class
-    k.cb = kt / ntaps;
-    const int t = kt - k.cb * ntaps;
-    k.r = g.r0 + g.step * (t / g.nS);
-    k.s = g.s0 + g.step * (t % g.nS);
-  } else if (a.nb > 0 && g.nS > 0) {
-    k.cb = kt % a.nb;
-    const int t = kt / a.nb;
-    k.r = g.r0 + g.step * (t / g.nS);
-    k.s = g.s0 + g.step * (t % g.nS);
-  } else {
-    k.cb = k.r = k.s = 0;
-  }
-  return k;
-}
-
-__device__ __forceinline__ void ks_next(const LArgs& a, const Geo& g, KS& k) {
-  ++k.kt;
-  if (a.tap_major && a.nb > 0) {  // taps fastest: consecutive K-tiles re-read shifted rows of one channel block
-    k.s += g.step;
-    if (k.s >= a.s.S) {
-      k.s = g.s0;
-      k.r += g.step;
-      if (k.r >= a.s.R) {
-        k.r = g.r0;
-        ++k.cb;
-      }
-    }
-    return;
-  }
-  if (++k.cb == a.nb) {
-    k.cb = 0;
-    k.s += g.step;
-    if (k.s >= a.s.S) {
-      k.s = g.s0;
-      k.r += g.step;
-    }
-  }
-}
 
 // ---- operand gather policies ------------------------------------------------
 // init(): per-lane state of this wave's PPW DMA pieces (1 KiB of LDS each);
@@ -408,9 +255,6 @@ struct WgradB {  // x gathered: row = j = (r, s, c..c+7), k = npq (carried incre
   }
 };
 
-struct Rsrc {  // buffer descriptor (a struct: the builtin type cannot be a host-visible parameter)
-  __amdgpu_buffer_rsrc_t r;
-};
 
 // DMA one operand tile (K-tile ks) into LDS at dst: PPW x buffer_load_dwordx4 ... lds per lane.
 // (The voffset goes through an explicit int: with the unsigned call result passed
@@ -423,326 +267,6 @@ struct Rsrc {  // buffer descriptor (a struct: the builtin type cannot be a host
                                                16, o_, 0, 0, 0);                                     \
     }                                                                                                \
   } while (0)
-
-__device__ __forceinline__ void lds_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
-
-__device__ __forceinline__ int tiles_of(const LArgs& a) { return a.tiles_x; }
-
-// The following training-mode BatchNorm's statistics from this tile's bf16 outputs
-// (exactly the values BN reads): per channel sum and sum of squares over the
-// tile's valid rows -- 16 row lanes by shuffles, the WM wave rows through LDS --
-// then ONE pair of fp32 atomics per channel per tile, into one of bn_ncop
-// accumulator copies (tile % kBnCopies: 8x less same-address serialisation; 64 copies
-// measured no faster, profiles/r3/bn_copies_ab_r3.txt).  The
-// last of the grid's `tiles` workgroups sums the copies and finalizes (mean,
-// invstd, running-stat EMA, apply coefficients), so the BN needs no reduce pass.
-// (A dgrad's BN backward statistics come from the slab pass or a post pass over dx instead:
-// the epilogue form of round 5 cost 11-13 us per dgrad, profiles/r5/conv_bn_bwd_ab.txt.)
-template <int WM, int WN>
-__device__ __forceinline__ void bn_stats_epilogue(const LArgs& a, const Geo& g, floatx4 (&acc)[4][4], int mbase,
-                                                  int n0, int wm, int wn, int lane, int tile, char* smem,
-                                                  int lds_floats) {
-  constexpr int BN = WN * 64;
-  float* red = reinterpret_cast<float*>(smem);  // [WM][BN][2]
-  __syncthreads();  // every wave is done with the operand stages
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    float s0[4] = {0.f, 0.f, 0.f, 0.f}, s1[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      if (mbase + i * 16 + (lane & 15) >= g.M) continue;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float v = bf2f(f2bf(acc[j][i][r]));
-        s0[r] += v;
-        s1[r] += v * v;
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) {
-        s0[r] += __shfl_xor(s0[r], o, 64);
-        s1[r] += __shfl_xor(s1[r], o, 64);
-      }
-    }
-    if ((lane & 15) == 0) {
-      const int lc = wn * 64 + j * 16 + 4 * (lane >> 4);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        red[(wm * BN + lc + r) * 2] = s0[r];
-        red[(wm * BN + lc + r) * 2 + 1] = s1[r];
-      }
-    }
-  }
-  __syncthreads();
-  float* accc = a.bn.acc + (size_t)(tile % kBnCopies) * 2 * a.N;
-  for (int t = threadIdx.x; t < BN; t += blockDim.x) {
-    const int c = n0 + t;
-    if (c >= a.N) continue;
-    float s0 = 0.f, s1 = 0.f;
-#pragma unroll
-    for (int q = 0; q < WM; ++q) {
-      s0 += red[(q * BN + t) * 2];
-      s1 += red[(q * BN + t) * 2 + 1];
-    }
-    bn_acc_add(accc + c, s0);
-    bn_acc_add(accc + a.N + c, s1);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's atomics have completed
-  bn_finalize_last<false, kBnCopies>(a.bn, g.M, a.N, tiles_of(a), red, lds_floats);
-}
-
-// Direct epilogue with the class row remap: GEMM row m of a stride-2 dgrad
-// class is pixel (n, 2*h2 + hoff, 2*w2 + woff) of dx.
-__device__ __forceinline__ void store_remapped(const LArgs& a, const Geo& g, floatx4 (&acc)[4][4], int mbase,
-                                               int nbase, int lane) {
-  const ConvShape& s = a.s;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int m = mbase + i * 16 + (lane & 15);
-    if (m >= g.M) continue;
-    const int t = fdiv(m, g.f_rw), w2 = m - t * g.rows_w, n = fdiv(t, g.f_rh), h2 = t - n * g.rows_h;
-    const size_t row = ((size_t)n * s.H + g.hmul * h2 + g.hoff) * s.W + g.hmul * w2 + g.woff;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int c = nbase + j * 16 + 4 * (lane >> 4);
-      if (c >= a.N) continue;
-      const floatx4 v = acc[j][i];
-      *reinterpret_cast<u16x4*>(reinterpret_cast<bf16_t*>(a.out) + row * a.N + c) =
-          u16x4{f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
-    }
-  }
-}
-
-// Row-coalesced fp32 store of a wave's 64 x 64 tile (wgrad outputs, split-K slabs):
-// the accumulators go to the wave's 16 KiB LDS slice ([64][64] fp32, 16-B chunks
-// XOR-swizzled by row), then 16 lanes write each 256-B row run -- 4 full rows per
-// instruction instead of 16 rows x 64 B straight from the MFMA layout.  The caller
-// has barriered the operand stages away.  out = acc (+ beta * out).
-__device__ __forceinline__ void store_f32_rows(const GemmParams& p, floatx4 (&acc)[4][4], char* wsm, int mbase,
-                                               int nbase, int lane) {
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int row = i * 16 + (lane & 15);
-      const int chunk = j * 4 + (lane >> 4);
-      *reinterpret_cast<floatx4*>(wsm + row * 256 + ((chunk ^ (row & 15)) << 4)) = acc[j][i];
-    }
-  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's staging writes landed (private slice)
-  __builtin_amdgcn_wave_barrier();
-  const int c = lane & 15;
-  const int n = nbase + c * 4;
-#pragma unroll 4
-  for (int it = 0; it < 16; ++it) {
-    const int row = it * 4 + (lane >> 4);
-    const int m = mbase + row;
-    floatx4 v = *reinterpret_cast<const floatx4*>(wsm + row * 256 + ((c ^ (row & 15)) << 4));
-    if (m < p.M && n < p.N) {
-      float* o = reinterpret_cast<float*>(p.C) + (size_t)m * p.ldc + n;
-      if (p.beta != 0.f) v = v + p.beta * *reinterpret_cast<const floatx4*>(o);
-      *reinterpret_cast<floatx4*>(o) = v;
-    }
-  }
-}
-
-// The same staging for bf16 outputs with the bias / ReLU epilogue: 8 lanes write each
-// 128-B row run (8 rows per instruction instead of 16 rows x 32 B).  HALVES = 2 stages
-// the 64 rows as two 32-row halves (8 KiB per wave) for kernels with less LDS (the
-// C = 8 stem's patch kernel).
-template <int EPI, int HALVES = 1>
-__device__ __forceinline__ void store_bf16_rows(const GemmParams& p, floatx4 (&acc)[4][4], char* wsm, int mbase,
-                                                int nbase, int lane) {
-  constexpr int RH = 64 / HALVES;  // rows staged per pass
-  const int c8 = lane & 7;
-  const int n = nbase + c8 * 8;
-  const bool nok = n < p.N;
-  float bias[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_RELU) {
-    if (nok) {
-      const floatx4 b0 = *reinterpret_cast<const floatx4*>(p.bias + n);
-      const floatx4 b1 = *reinterpret_cast<const floatx4*>(p.bias + n + 4);
-      bias[0] = b0[0]; bias[1] = b0[1]; bias[2] = b0[2]; bias[3] = b0[3];
-      bias[4] = b1[0]; bias[5] = b1[1]; bias[6] = b1[2]; bias[7] = b1[3];
-    }
-  }
-#pragma unroll
-  for (int h = 0; h < HALVES; ++h) {
-#pragma unroll
-    for (int i = 0; i < 4 / HALVES; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int row = i * 16 + (lane & 15);
-        const int chunk = j * 4 + (lane >> 4);
-        *reinterpret_cast<floatx4*>(wsm + row * 256 + ((chunk ^ (row & 15)) << 4)) = acc[j][h * (4 / HALVES) + i];
-      }
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's staging writes landed (private slice)
-    __builtin_amdgcn_wave_barrier();
-#pragma unroll 4
-    for (int it = 0; it < RH / 8; ++it) {
-      const int row = it * 8 + (lane >> 3);
-      const int m = mbase + h * RH + row;
-      const char* rb = wsm + row * 256;
-      const floatx4 v0 = *reinterpret_cast<const floatx4*>(rb + (((2 * c8) ^ (row & 15)) << 4));
-      const floatx4 v1 = *reinterpret_cast<const floatx4*>(rb + (((2 * c8 + 1) ^ (row & 15)) << 4));
-      if (!(nok && m < p.M)) continue;
-      u16x8 o;
-#pragma unroll
-      for (int q = 0; q < 8; ++q) o[q] = f2bf(apply_epi<EPI>(q < 4 ? v0[q] : v1[q - 4], bias[q], 0.f));
-      *reinterpret_cast<u16x8*>(reinterpret_cast<bf16_t*>(p.C) + (size_t)m * p.ldc + n) = o;
-    }
-    __builtin_amdgcn_wave_barrier();  // the slice is re-staged by the next half
-  }
-}
-
-// store_remapped through the wave's LDS slice: each GEMM row (one dx pixel's
-// channels) leaves as 128-B runs, 8 lanes a row, instead of 16 rows x 32 B.
-__device__ __forceinline__ void store_remapped_rows(const LArgs& a, const Geo& g, floatx4 (&acc)[4][4], char* wsm,
-                                                    int mbase, int nbase, int lane) {
-  const ConvShape& s = a.s;
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int row = i * 16 + (lane & 15);
-      const int chunk = j * 4 + (lane >> 4);
-      *reinterpret_cast<floatx4*>(wsm + row * 256 + ((chunk ^ (row & 15)) << 4)) = acc[j][i];
-    }
-  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's staging writes landed (private slice)
-  __builtin_amdgcn_wave_barrier();
-  const int c8 = lane & 7;
-  const int c = nbase + c8 * 8;
-  const bool cok = c < a.N;
-#pragma unroll 4
-  for (int it = 0; it < 8; ++it) {
-    const int row = it * 8 + (lane >> 3);
-    const int m = mbase + row;
-    const char* rb = wsm + row * 256;
-    const floatx4 v0 = *reinterpret_cast<const floatx4*>(rb + (((2 * c8) ^ (row & 15)) << 4));
-    const floatx4 v1 = *reinterpret_cast<const floatx4*>(rb + (((2 * c8 + 1) ^ (row & 15)) << 4));
-    if (!(cok && m < g.M)) continue;
-    const int t = fdiv(m, g.f_rw), w2 = m - t * g.rows_w, n = fdiv(t, g.f_rh), h2 = t - n * g.rows_h;
-    const size_t px = ((size_t)n * s.H + g.hmul * h2 + g.hoff) * s.W + g.hmul * w2 + g.woff;
-    u16x8 o;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) o[q] = f2bf(q < 4 ? v0[q] : v1[q - 4]);
-    *reinterpret_cast<u16x8*>(reinterpret_cast<bf16_t*>(a.out) + px * a.N + c) = o;
-  }
-}
-
-template <int N>
-__device__ __forceinline__ void wait_vm() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-// Shared tail of the fwd / dgrad / wgrad kernels: split-K hand-off (in-launch
-// combine, fp32 slab, or fp32 atomics), the stride-2 dgrad row remap, the fused
-// epilogue and the next BatchNorm's statistics.  smem: the kernel's whole LDS
-// (lds_floats floats), free once every wave is past its operand reads.
-template <int WM, int WN, int EPI, bool OUT_F32, bool DGRAD>
-__device__ __forceinline__ void conv_tail(const LArgs& a, const Geo& g, floatx4 (&acc)[4][4], int m0, int n0, int wm,
-                                          int wn, int lane, char* smem, int lds_floats, int bx, int by,
-                                          const VB& vb) {
-  constexpr int NW = WM * WN;
-  const bool combine = a.cnt != nullptr && vb.gy > 1;
-  const int mb = m0 + wm * 64, nbase = n0 + wn * 64;
-  if (vb.gy > 1) {
-    if (combine) {
-      lds_barrier();  // every wave is done with the operand stages (the ticket word lives there)
-      const int tile = vb.z * a.tiles_x + bx;
-      // (phase-trace builds: stamps 4..6 of this workgroup's trace row, see splitk_combine)
-      uint64_t* tr = (a.trace != nullptr && threadIdx.x == 0)
-                         ? a.trace + 8 * (size_t)(vb.x + vb.gx * (vb.y + vb.gy * vb.z))
-                         : nullptr;
-      if (a.xcd_split || !a.combine_last) {
-        if (!splitk_combine<4, 4, NW * 64>(acc, a.ws, a.cnt, tile, vb.gy, by, smem, tr)) return;
-      } else if (!splitk_combine_last<4, 4, NW * 64>(acc, a.ws, a.cnt, tile, vb.gy, by, smem, tr)) {
-        return;
-      }
-    } else if (a.ws != nullptr) {
-      // wgrad, and small-M fwd / stride-1 dgrad: this slice's fp32 partial tile into
-      // its own slab; a separate chip-wide kernel sums the slabs (slab_sum_kernel /
-      // conv_slab_epilogue_kernel with the bias / ReLU epilogue) -- deterministic, no
-      // atomics, and no single workgroup re-reading every slice of its tile
-      GemmParams p{};
-      p.C = a.ws + (size_t)by * a.M * a.N;
-      p.M = g.M;
-      p.N = a.N;
-      p.ldc = a.N;
-      if (a.f32_rows && lds_floats >= NW * 4096) {
-        lds_barrier();  // every wave is done with the operand stages
-        store_f32_rows(p, acc, smem + (size_t)(wm * WN + wn) * 16384, mb, nbase, lane);
-        return;
-      }
-      epilogue<EPI_NONE, true, 4, 4>(p, acc, mb, nbase, lane);
-      return;
-    } else {
-      if constexpr (OUT_F32 && EPI == EPI_NONE) {  // fp32 atomics into the (cleared / accumulated) output
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int n = nbase + j * 16 + 4 * (lane >> 4);
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int m = mb + i * 16 + (lane & 15);
-            if (n < a.N && m < g.M) {
-              float* c = reinterpret_cast<float*>(a.out) + (size_t)m * a.N + n;
-#pragma unroll
-              for (int r = 0; r < 4; ++r) atomicAdd(c + r, acc[j][i][r]);
-            }
-          }
-        }
-      }
-      return;
-    }
-  }
-  if constexpr (DGRAD && !OUT_F32) {
-    if (g.hmul == 2) {
-      if (a.remap_rows && lds_floats >= NW * 4096 && !combine) {
-        lds_barrier();  // every wave is done with the operand stages
-        store_remapped_rows(a, g, acc, smem + (size_t)(wm * WN + wn) * 16384, mb, nbase, lane);
-        return;
-      }
-      store_remapped(a, g, acc, mb, nbase, lane);
-      return;
-    }
-  }
-  GemmParams p{};
-  p.C = a.out;
-  p.M = g.M;
-  p.N = a.N;
-  p.ldc = a.N;
-  p.bias = a.bias;
-  p.beta = a.beta;
-  if constexpr (OUT_F32 && EPI == EPI_NONE) {
-    if (a.f32_rows && lds_floats >= NW * 4096 && !combine) {
-      lds_barrier();  // every wave is done with the operand stages
-      store_f32_rows(p, acc, smem + (size_t)(wm * WN + wn) * 16384, mb, nbase, lane);
-      return;
-    }
-  }
-  if constexpr (!OUT_F32 && (EPI == EPI_NONE || EPI == EPI_BIAS || EPI == EPI_BIAS_RELU)) {
-    if (a.bf16_rows && lds_floats >= NW * (a.bf16_rows >= 2 ? 2048 : 4096) && !combine) {
-      lds_barrier();  // every wave is done with the operand stages
-      if (lds_floats >= NW * 4096)
-        store_bf16_rows<EPI>(p, acc, smem + (size_t)(wm * WN + wn) * 16384, mb, nbase, lane);
-      else
-        store_bf16_rows<EPI, 2>(p, acc, smem + (size_t)(wm * WN + wn) * 8192, mb, nbase, lane);
-      if constexpr (EPI == EPI_NONE && !DGRAD) {
-        if (a.bn_stats) bn_stats_epilogue<WM, WN>(a, g, acc, mb, n0, wm, wn, lane, bx, smem, lds_floats);
-      }
-      return;
-    }
-  }
-  epilogue<EPI, OUT_F32, 4, 4>(p, acc, mb, nbase, lane);
-  if constexpr (!OUT_F32 && EPI == EPI_NONE && !DGRAD) {
-    if (a.bn_stats) bn_stats_epilogue<WM, WN>(a, g, acc, mb, n0, wm, wn, lane, bx, smem, lds_floats);
-  }
-}
 
 // NS = LDS stages in the ring.  NS = 2: two workgroups per CU, the DMA of K-tile
 // kt+1 in flight while kt is multiplied.  NS = 3 / 4 (grids of at most one
@@ -1353,7 +877,6 @@ __global__ __launch_bounds__(512, 1) void conv_hb_kernel(LArgs a, const bf16_t* 
 // per accumulator as conv_halo_kernel (taps r-major, then kk), so the two agree bit for bit.  The
 // fwd epilogue accumulates the next BatchNorm's statistics per lane over all of the workgroup's
 // tiles and adds them once per workgroup.
-__device__ __forceinline__ uint32_t lds_off(const void* p) { return (uint32_t)(uintptr_t)(lds_void*)p; }
 namespace ws64 {
 constexpr int kPitch = 1152 + 16;      // LDS row pitch of the staged weights (16-B aligned, rows spread over banks)
 constexpr int kHPitch = 160;           // LDS row pitch of the halo: 8 chunks + 2 pad slots -- no swizzle, so a
@@ -1692,200 +1215,6 @@ __global__ __launch_bounds__(256, 1) void conv_ws64_kernel(LArgs a, const bf16_t
   }
 }
 
-// ---- stem forward on the space-to-depth image (the mapping of stem_s2d_wgrad_kernel below) ----
-//   y[n][p][q][k] = sum_{a,b < 4} w'[k][a][b][.] . xs[n][p + a][q + b][.],  16 s2d channels (32 B)
-// per pixel, w'[k][a][b][(dh, dw, c)] = w[k][2a + dh - 1][2b + dw - 1][c]: K = 256 (8 MFMA k-steps)
-// instead of the 7x7x8 patch kernel's 13, and the input of a 256-pixel tile is <= kRows whole s2d rows,
-// ONE contiguous run of bytes (a linear DMA, no gather).  Persistent: one 4-wave workgroup per CU keeps
-// w' in registers (8 k-steps x 4 filter tiles, gathered from w once), walks a contiguous run of
-// 256-pixel tiles through a 3-buffer ring (the DMA of tiles t+1 and t+2 in flight behind tile t's
-// MFMAs: the patch kernels' loops are bound by the DMA round trip), stages the outputs through LDS
-// for whole-row stores and keeps the next BN's statistics in registers.  Needs P*Q % 256 == 0 (a
-// tile never spans two images) and rows * Ws * 32 <= kBuf (stem_s2d_fwd_ok).
-namespace s2dfwd {
-constexpr int kPieces = 28, kBuf = kPieces * 1024, kNB = 3;
-}
-__global__ __launch_bounds__(256, 1) void conv_s2d_ws_kernel(LArgs a, const bf16_t* pxs, uint32_t bytes_xs, int Hs,
-                                                             int Ws, const bf16_t* pw) {
-  using namespace s2dfwd;
-  constexpr int BM = 256, NW = 4, PPW = kPieces / NW, KS = 8;
-  constexpr int kOutPitch = 144, kOutWave = 64 * kOutPitch;
-  constexpr int LDS = kNB * kBuf + NW * kOutWave + 16;
-  static_assert(PPW * NW == kPieces && LDS <= 160 * 1024, "LDS");
-  __shared__ __attribute__((aligned(1024))) char smem[LDS];
-  const ConvShape& sh = a.s;
-  const int lane = threadIdx.x & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  char* const ostage = smem + kNB * kBuf + wid * kOutWave;
-  const int PQ = sh.P * sh.Q;
-  const int T = a.M / BM;
-  const int t0 = (int)((int64_t)blockIdx.x * T / gridDim.x);
-  const int t1 = (int)((int64_t)(blockIdx.x + 1) * T / gridDim.x);
-  const int g4 = lane >> 4;   // k-elements 8 g4 .. 8 g4 + 7 of a step: tap 2k + (g4 >> 1), channels 8 (g4 & 1) ..
-
-  // w' fragments of every k-step (filter j*16 + (lane & 15)): registers for the launch, all loads in flight
-  bf16x8 fb[KS][4];
-#pragma unroll
-  for (int k = 0; k < KS; ++k)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int t = 2 * k + (g4 >> 1), ta = t >> 2, tb = t & 3;
-      const bf16_t* wn = pw + (size_t)(j * 16 + (lane & 15)) * a.rsc;
-      u16x8 v;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int cc = (g4 & 1) * 8 + e, d = cc >> 2, c = cc & 3;
-        const int r = 2 * ta + (d >> 1) - 1, s = 2 * tb + (d & 1) - 1;
-        v[e] = (r >= 0 && s >= 0) ? reinterpret_cast<const uint16_t*>(wn)[(r * 7 + s) * 8 + c] : (uint16_t)0;
-      }
-      fb[k][j] = __builtin_bit_cast(bf16x8, v);
-    }
-  Rsrc rx;
-  rx.r = __builtin_amdgcn_make_buffer_rsrc((void*)pxs, (short)0, (int)bytes_xs, 0x00020000);
-  // tile t: s2d rows (n, p_lo ..) are contiguous from ((n Hs + p_lo) Ws) * 32 B; bytes past the
-  // buffer read as zeros, bytes of rows past the tile's are loaded and never read
-  auto dma = [&](int t, int b) {
-    const int m0 = t * BM, n_img = m0 / PQ, p_lo = (m0 - n_img * PQ) / sh.Q;
-    const uint32_t base = (uint32_t)(n_img * Hs + p_lo) * (uint32_t)Ws * 32u;
-    char* const dst = smem + b * kBuf;
-#pragma unroll
-    for (int q = 0; q < PPW; ++q) {
-      const int pc = q * NW + wid;
-      const uint32_t o = base + (uint32_t)pc * 1024u + (uint32_t)lane * 16u;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx.r, (lds_void*)(dst + pc * 1024), 16, o < bytes_xs ? (int)o : (int)kOOB,
-                                               0, 0, 0);
-    }
-  };
-  if (t0 < t1) {
-    dma(t0, 0);
-    if (t0 + 1 < t1) dma(t0 + 1, 1);
-  }
-  // this lane's tap offset (bytes) per k-step
-  uint32_t toff[KS];
-#pragma unroll
-  for (int k = 0; k < KS; ++k) {
-    const int t = 2 * k + (g4 >> 1);
-    toff[k] = (uint32_t)(((t >> 2) * Ws + (t & 3)) * 32 + (g4 & 1) * 16);
-  }
-  if (t0 < t1) {
-    if (t0 + 1 < t1) wait_vm<PPW>();  // tile t0's pieces landed (and the w' loads, issued before them)
-    else wait_vm<0>();
-  }
-  float bs0[4][4], bs1[4][4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) bs0[j][r] = bs1[j][r] = 0.f;
-  bf16_t* const out = reinterpret_cast<bf16_t*>(a.out);
-  for (int t = t0; t < t1; ++t) {
-    const int m0 = t * BM, n_img = m0 / PQ, mi0 = m0 - n_img * PQ, p_lo = mi0 / sh.Q;
-    lds_barrier();  // every wave waited for its own pieces of tile t; every wave is done with tile t-1's buffer
-    if (t + 2 < t1) dma(t + 2, (t + 2 - t0) % kNB);
-    const uint32_t patch = lds_off(smem + ((t - t0) % kNB) * kBuf);
-    uint32_t base[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int mi = mi0 + wid * 64 + i * 16 + (lane & 15);
-      const int p = fdiv(mi, a.f_q), q = mi - p * sh.Q;
-      base[i] = patch + (uint32_t)(((p - p_lo) * Ws + q) * 32);
-    }
-    auto read_step = [&](int k, bf16x8 (&f)[4]) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const uint32_t ad = base[i] + toff[k];
-        asm volatile("ds_read_b128 %0, %1" : "=v"(f[i]) : "v"(ad));
-      }
-    };
-    floatx4 acc[4][4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) acc[j][i] = floatx4{0.f, 0.f, 0.f, 0.f};
-    bf16x8 fa[3][4];
-    read_step(0, fa[0]);
-    read_step(1, fa[1]);
-#pragma unroll
-    for (int k = 0; k < KS; ++k) {
-      bf16x8 (&f)[4] = fa[k % 3];
-      if (k + 2 < KS) read_step(k + 2, fa[(k + 2) % 3]);
-      if (k + 2 < KS) asm volatile("s_waitcnt lgkmcnt(8)" : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]));
-      else if (k + 1 < KS) asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]));
-      else asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]));
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[k][j], f[i], acc[j][i], 0, 0, 0);
-    }
-    // tile t+1's pieces (issued a tile ago; only tile t+2's were issued after them)
-    if (t + 1 < t1) {
-      if (t + 2 < t1) wait_vm<PPW>();
-      else wait_vm<0>();
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int rl = i * 16 + (lane & 15);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int c = j * 16 + 4 * (lane >> 4);
-        const floatx4 v = acc[j][i];
-        const u16x4 o = u16x4{f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
-        *reinterpret_cast<u16x4*>(ostage + rl * kOutPitch + c * 2) = o;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float bv = bf2f(o[r]);
-          bs0[j][r] += bv;
-          bs1[j][r] += bv * bv;
-        }
-      }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // (a wave's LDS operations run in order)
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int rl = q * 8 + (lane >> 3);
-      const u32x4 v = *reinterpret_cast<const u32x4*>(ostage + rl * kOutPitch + (lane & 7) * 16);
-      *reinterpret_cast<u32x4*>(out + (size_t)(m0 + wid * 64 + rl) * 64 + (lane & 7) * 8) = v;
-    }
-  }
-  if (a.bn_stats) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-          bs0[j][r] += __shfl_xor(bs0[j][r], o, 64);
-          bs1[j][r] += __shfl_xor(bs1[j][r], o, 64);
-        }
-    float* red = reinterpret_cast<float*>(smem);  // [4][64][2]
-    __syncthreads();
-    if ((lane & 15) == 0) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int c = j * 16 + 4 * (lane >> 4) + r;
-          red[(wid * 64 + c) * 2] = bs0[j][r];
-          red[(wid * 64 + c) * 2 + 1] = bs1[j][r];
-        }
-    }
-    __syncthreads();
-    float* accc = a.bn.acc + (size_t)(blockIdx.x % kBnCopies) * 2 * 64;
-    if (threadIdx.x < 64) {
-      float s0 = 0.f, s1 = 0.f;
-#pragma unroll
-      for (int q = 0; q < NW; ++q) {
-        s0 += red[(q * 64 + threadIdx.x) * 2];
-        s1 += red[(q * 64 + threadIdx.x) * 2 + 1];
-      }
-      bn_acc_add(accc + threadIdx.x, s0);
-      bn_acc_add(accc + 64 + threadIdx.x, s1);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's atomics have completed
-    bn_finalize_last<false, kBnCopies>(a.bn, a.M, 64, gridDim.x, red, LDS / 4);
-  }
-}
-
 // ---- ring wgrad: 3x3 stride-1 pad-1 weight gradient, activation rows staged once ----
 // The split-K wgrad above re-gathers x for every filter tap: a 128x128 tile's K-tile
 // moves 32 KiB through the LDS-DMA path for 2 MFLOP, and the pass is fill-bound (its
@@ -2050,482 +1379,6 @@ __global__ __launch_bounds__(256, 2) void wgrad_ring_kernel(WRArgs a, const bf16
       if (gridDim.x == (unsigned)ntiles && a.beta != 0.f) v += a.beta * *reinterpret_cast<const floatx4*>(o);
       *reinterpret_cast<floatx4*>(o) = v;
     }
-  }
-}
-
-// ---- stem wgrad via space-to-depth (7x7 stride-2 pad-3, C = 8 with <= 4 real channels) ----
-// The split-K wgrad gathers the C = 8 stem's activation as one 16-B pixel per (tap, pixel)
-// element: 40 KiB of 16-B pieces per K-tile, ~300 TFLOP/s, the largest kernel of the
-// ResNet-18 b64 step (131 us).  Rewritten on the 2x2 space-to-depth image
-//   xs[n][i][j][(dh*2 + dw)*4 + c] = x[n][2(i-2) + dh][2(j-2) + dw][c]   (zero outside),
-// the stem is a 4x4 stride-1 unpadded conv with 16 channels:
-//   y[p][q] = sum_{a,b<4} w'[a][b][.] . xs[p+a][q+b][.],  w'[a][b][dh,dw,c] = w[2a+dh-1][2b+dw-1][c]
-// so its weight gradient dW'[k][a][b][16] = sum_pq dy[p][q][k] xs[p+a][q+b][.] needs no
-// gather and no masks: per K-step (32 output pixels of one row) a workgroup DMAs the dy rows
-// (4 KiB) and 4 activation row segments of 36 s2d pixels (4 x 1.1 KiB), wave a multiplies
-// taps (a, 0..3) -- 16 MFMAs; 256 x 64 fp32 partial blocks per slice, summed and scattered
-// back to dW[k][r][s][c] by stem_s2d_sum_kernel.
-namespace s2d {
-constexpr int kDy = 32 * 128, kSeg = 2048, kStage = kDy + 4 * kSeg;  // 12 KiB per stage
-constexpr int kStages = 4;  // K-steps t+1 .. t+2 in flight while t is multiplied (t+3 issued after its barrier)
-}
-
-__global__ __launch_bounds__(256) void stem_s2d_pack_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ xs,
-                                                            int N, int H, int W, int Hs, int Ws) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // s2d pixel
-  if (i >= (int64_t)N * Hs * Ws) return;
-  const int jj = (int)(i % Ws);
-  const int64_t t = i / Ws;
-  const int ii = (int)(t % Hs), n = (int)(t / Hs);
-  u16x8 o[2];
-#pragma unroll
-  for (int d = 0; d < 4; ++d) {  // d = dh*2 + dw
-    const int h = 2 * (ii - 2) + (d >> 1), w = 2 * (jj - 2) + (d & 1);
-    u16x4 v = {0, 0, 0, 0};
-    if (h >= 0 && h < H && w >= 0 && w < W)
-      v = *reinterpret_cast<const u16x4*>(x + (((size_t)n * H + h) * W + w) * 8);  // channels 0..3
-#pragma unroll
-    for (int c = 0; c < 4; ++c) o[d >> 1][(d & 1) * 4 + c] = v[c];
-  }
-  u16x8* dst = reinterpret_cast<u16x8*>(xs + i * 16);
-  dst[0] = o[0];
-  dst[1] = o[1];
-}
-
-struct S2dArgs {
-  int N, P, Q, Hs, Ws, K;   // output P x Q, s2d image Hs x Ws (= P + 3, Q + 3), filters K (= 64)
-  int nchunk, steps, steps_per;  // 32-pixel chunks per output row; total K-steps; per slice
-  float* slab;              // [slices][64][256]
-};
-
-__global__ __launch_bounds__(256, 3) void stem_s2d_wgrad_kernel(S2dArgs a, const bf16_t* pdy, uint32_t bytes_dy,
-                                                                const bf16_t* pxs, uint32_t bytes_xs) {
-  using namespace s2d;
-  __shared__ __attribute__((aligned(1024))) char smem[kStages * kStage];  // 48 KiB
-  typedef __attribute__((address_space(3))) bf16x4 lds_b4;
-  const int lane = threadIdx.x & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // = filter-row tap a
-  const int g = lane >> 4, r16 = lane & 15, qq = r16 >> 2, pp = r16 & 3;
-  const int st0 = blockIdx.x * a.steps_per;
-  const int nst = min(a.steps - st0, a.steps_per);
-  floatx4 acc[4][4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) acc[j][i] = floatx4{0.f, 0.f, 0.f, 0.f};
-  if (nst > 0) {
-    Rsrc rdy, rxs;
-    rdy.r = __builtin_amdgcn_make_buffer_rsrc((void*)pdy, (short)0, (int)bytes_dy, 0x00020000);
-    rxs.r = __builtin_amdgcn_make_buffer_rsrc((void*)pxs, (short)0, (int)bytes_xs, 0x00020000);
-    // K-step st = (n * P + p) * nchunk + chunk: dy rows of pixels (n, p, 32 chunk ..), the 4 s2d
-    // row segments (n, p + a, 32 chunk .. + 35); wave `wid` DMAs dy piece wid and segment a = wid
-    auto load = [&](int st, char* dst) {
-      const int chunk = st % a.nchunk, row = st / a.nchunk;  // row = n * P + p
-      const int p = row % a.P, n = row / a.P;
-      const int q0 = chunk * 32;
-      {
-        const int j = wid * 8 + (lane >> 3);
-        const int k = (lane & 7) ^ (j & 7);
-        const int o = q0 + j < a.Q ? (int)(((uint32_t)(row * a.Q + q0 + j) * (uint32_t)a.K + (uint32_t)(k * 8)) * 2u)
-                                   : (int)kOOB;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rdy.r, (lds_void*)(dst + wid * 1024), 16, o, 0, 0, 0);
-      }
-      const uint32_t pix0 = ((uint32_t)(n * a.Hs + p + wid) * (uint32_t)a.Ws + (uint32_t)q0);
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {  // s2d pixels q0 .. q0 + 34 x 32 B (the taps read 35): the second
-        // piece's lanes past pixel 34 are out of range (no memory traffic; the per-CU fill rate
-        // bounds this kernel)
-        const int px = h * 32 + (lane >> 1);
-        const uint32_t o = (pix0 + (uint32_t)px) * 32u + (uint32_t)(lane & 1) * 16u;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rxs.r, (lds_void*)(dst + kDy + wid * kSeg + h * 1024), 16,
-                                                 px < 35 ? (int)o : (int)kOOB, 0, 0, 0);
-      }
-    };
-    // three DMA instructions per wave per K-step; steps 0..2 in the prologue, step t+3 after
-    // the barrier of step t (into the stage of step t-1), a counted wait keeps two in flight
-#pragma unroll
-    for (int t = 0; t < kStages - 1; ++t)
-      if (t < nst) load(st0 + t, smem + t * kStage);
-    for (int t = 0; t < nst; ++t) {
-      const int ahead = min(nst, t + kStages - 1) - t - 1;  // steps issued after t
-      if (ahead >= 2) wait_vm<6>();
-      else if (ahead == 1) wait_vm<3>();
-      else wait_vm<0>();
-      lds_barrier();  // publishes step t; every wave is done with step t-1's stage
-      if (t + kStages - 1 < nst) load(st0 + t + kStages - 1, smem + ((t + kStages - 1) % kStages) * kStage);
-      const char* stg = smem + (t % kStages) * kStage;
-      const int rl = 8 * g + qq;
-      bf16x8 fa[4];  // dy: rows = filters 16i + r16, k = the step's 32 pixels
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int c = 2 * i + (pp >> 1);
-        const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
-            (lds_b4*)(stg + rl * 128 + ((c ^ (rl & 7)) << 4) + 8 * (pp & 1)));
-        const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
-            (lds_b4*)(stg + (rl + 4) * 128 + ((c ^ ((rl + 4) & 7)) << 4) + 8 * (pp & 1)));
-        fa[i] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      }
-      const char* seg = stg + kDy + wid * kSeg;
-#pragma unroll
-      for (int b = 0; b < 4; ++b) {  // tap (a = wid, b): s2d pixel q + b, 16 channels
-        const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_b4*)(seg + (rl + b) * 32 + 8 * pp));
-        const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_b4*)(seg + (rl + 4 + b) * 32 + 8 * pp));
-        const bf16x8 fb = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-#pragma unroll
-        for (int i = 0; i < 4; ++i) acc[b][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb, fa[i], acc[b][i], 0, 0, 0);
-      }
-    }
-  }
-  // lane holds dW'[filter 16i + r16][tap (wid, b) * 16 + 4g + 0..3]
-  float* o = a.slab + (size_t)blockIdx.x * 64 * 256;
-#pragma unroll
-  for (int b = 0; b < 4; ++b)
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      *reinterpret_cast<floatx4*>(o + (size_t)(16 * i + r16) * 256 + (wid * 4 + b) * 16 + 4 * g) = acc[b][i];
-}
-
-// dW[k][r][s][c] (7 x 7 x 8) = sum over slices of dW'[k][a][b][(dh,dw,c)], r = 2a+dh-1, s = 2b+dw-1
-// (channels 4..7 of the padded C = 8 carry no activation: their gradient is 0) (+ beta * dW)
-__global__ __launch_bounds__(256) void stem_s2d_sum_kernel(const float* __restrict__ slab, float* __restrict__ dw,
-                                                           int slices, float beta) {
-  const int e = blockIdx.x * 256 + threadIdx.x;  // dW element
-  if (e >= 64 * 49 * 8) return;
-  const int c = e & 7, rs = (e >> 3) % 49, k = e / (49 * 8);
-  float v = 0.f;
-  if (c < 4) {
-    const int r = rs / 7, sx = rs % 7;
-    const int aa = (r + 1) >> 1, dh = (r + 1) & 1, bb = (sx + 1) >> 1, dwv = (sx + 1) & 1;
-    const int j = (aa * 4 + bb) * 16 + (dh * 2 + dwv) * 4 + c;
-    const float* p = slab + (size_t)k * 256 + j;
-    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-    int sl = 0;
-    for (; sl + 3 < slices; sl += 4) {
-      s0 += p[(size_t)sl * 64 * 256];
-      s1 += p[(size_t)(sl + 1) * 64 * 256];
-      s2 += p[(size_t)(sl + 2) * 64 * 256];
-      s3 += p[(size_t)(sl + 3) * 64 * 256];
-    }
-    for (; sl < slices; ++sl) s0 += p[(size_t)sl * 64 * 256];
-    v = (s0 + s1) + (s2 + s3);
-  }
-  dw[e] = beta != 0.f ? v + beta * dw[e] : v;
-}
-
-
-// ---- patch path: small-C stems (C = 8: 3 / 1 real channels) -------------------
-// FwdASmallC gathers one 16-B (tap, 8-channel) chunk per lane per tap: every input
-// pixel crosses the L1 / texture path once per filter tap that covers it (49x for
-// the 7x7 ResNet stem, ~12x per output at stride 2), each chunk its own address --
-// the stem ran at ~75 TFLOP/s (profiles/).  Here a 256-pixel output tile (one
-// image, P*Q % 256 == 0) DMAs its whole input patch ONCE: input rows
-// stride*p_lo - pad ... , every column -pad .. W+pad-1, 16 B per pixel, zero-filled
-// outside the image by the buffer range check.  The A fragment of tap t for output
-// pixel (p, q) is the 16-B patch cell (stride*(p - p_lo) + r, stride*q + s): one
-// ds_read_b128 at a per-lane base plus a per-(k-step, lane-group) tap offset.
-// B (the [K][R*S*8] weights, a few tens of KB, L2-resident) is read straight from
-// global memory into registers, one k-step ahead.  4 waves x 64 output pixels x
-// 64 filters, v_mfma_f32_16x16x32_bf16 (a k-step = 4 taps x 8 channels).
-constexpr int kPatchBytes = 48 * 1024;
-
-template <int KS, int STR, int EPI>
-__global__ __launch_bounds__(256, 2) void conv_patch_kernel(LArgs a, const bf16_t* px, uint32_t bytes_x,
-                                                            const bf16_t* pw) {
-  constexpr int WM = 4, WN = 1, BM = 256, BN = 64;
-  __shared__ __attribute__((aligned(1024))) char smem[kPatchBytes];
-  const ConvShape& sh = a.s;
-  const Geo g = make_geo(a, false, (int)blockIdx.z);
-  const int lane = threadIdx.x & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = wid, wn = 0;
-  int m0, n0;
-  tile_coords(g.M, a.N, BM, BN, m0, n0);
-  const int PQ = sh.P * sh.Q;
-  const int n_img = m0 / PQ, mi0 = m0 - n_img * PQ;  // tiles never straddle images (PQ % 256 == 0)
-  const int p_lo = mi0 / sh.Q;
-  const int PW = sh.W + 2 * sh.pad;                   // patch columns
-  const int PH = ((mi0 + BM - 1) / sh.Q - p_lo) * STR + sh.R;
-  const int cells = PH * PW;
-
-  // ---- patch DMA: cell e = (i, j) -> input (STR*p_lo - pad + i, j - pad)
-  {
-    Rsrc rx;
-    rx.r = __builtin_amdgcn_make_buffer_rsrc((void*)px, (short)0, (int)bytes_x, 0x00020000);
-    const int ih0 = STR * p_lo - sh.pad;
-    const int npieces = (cells + 63) >> 6;
-    for (int pc = wid; pc < npieces; pc += 4) {
-      const int e = pc * 64 + lane;
-      const int i = fdiv(e, a.f_w), j = e - i * PW;   // f_w: division by PW (host)
-      const int ih = ih0 + i, iw = j - sh.pad;
-      const bool ok = e < cells && (unsigned)ih < (unsigned)sh.H && (unsigned)iw < (unsigned)sh.W;
-      const int o = ok ? (int)((((unsigned)n_img * sh.H + ih) * (unsigned)sh.W + iw) * 16u) : (int)kOOB;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx.r, (lds_void*)(smem + pc * 1024), 16, o, 0, 0, 0);
-    }
-  }
-  // ---- per-lane geometry: patch cell of tap (0, 0) for each of the wave's 4 row tiles,
-  // and this lane group's tap offsets for each k-step (-1: a padding tap past R*S)
-  int base[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int mi = mi0 + wm * 64 + i * 16 + (lane & 15);
-    const int p = mi / sh.Q, q = mi - p * sh.Q;
-    base[i] = (STR * (p - p_lo)) * PW + STR * q;
-  }
-  int toff[KS];
-  const int RS = sh.R * sh.S;
-#pragma unroll
-  for (int k = 0; k < KS; ++k) {
-    const int t = k * 4 + (lane >> 4);
-    const int r = t / sh.S;
-    toff[k] = t < RS ? r * PW + (t - r * sh.S) : -1;
-  }
-  // B fragment of k-step k, filter tile j: filter n0 + j*16 + (lane & 15), k = 8 * tap
-  const int rsc = a.rsc;
-  auto bfrag = [&](int k, int j) -> bf16x8 {
-    const int t = k * 4 + (lane >> 4);
-    const int n = n0 + j * 16 + (lane & 15);
-    if (t >= RS || n >= a.N) return bf16x8{};
-    return *reinterpret_cast<const bf16x8*>(pw + (size_t)n * rsc + t * 8);
-  };
-
-  floatx4 acc[4][4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) acc[j][i] = floatx4{0.f, 0.f, 0.f, 0.f};
-  bf16x8 fb[2][4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) fb[0][j] = bfrag(0, j);
-  wait_vm<0>();
-  lds_barrier();  // the patch landed
-#pragma unroll
-  for (int k = 0; k < KS; ++k) {
-    if (k + 1 < KS) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) fb[(k + 1) & 1][j] = bfrag(k + 1, j);
-    }
-    bf16x8 fa[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int cell = base[i] + toff[k];
-      const bf16x8 v = *reinterpret_cast<const bf16x8*>(smem + (toff[k] >= 0 ? cell : 0) * 16);
-      fa[i] = toff[k] >= 0 ? v : bf16x8{};
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[k & 1][j], fa[i], acc[j][i], 0, 0, 0);
-  }
-  conv_tail<WM, WN, EPI, false, false>(a, g, acc, m0, n0, wm, wn, lane, smem, kPatchBytes / 4, blockIdx.x,
-                                       blockIdx.y, hw_vb());
-}
-
-// Persistent weight-stationary variant of conv_patch_kernel for 64-filter stems (the ResNet-18
-// 7x7 / 2 stem: 384 us of the b256 step, ~15 us per 256-pixel tile-pair per CU, its B fragments
-// streamed from L2 one k-step ahead).  One 4-wave workgroup per CU keeps the whole [64][R*S*8]
-// weight matrix in registers (each wave: 64 rows x all 64 filters, KS x 4 fragments), walks a
-// contiguous run of 256-pixel tiles, DMAs each tile's input patch into a double buffer one tile
-// ahead (a fixed 48 pieces per tile: rows below the patch load harmlessly), and reads the A
-// fragments two k-steps ahead (asm + counted lgkmcnt, as conv_ws64_kernel).  Padding taps
-// (t >= R*S) read cell 0: their weights are zero.  The next BN's statistics stay in registers
-// over all tiles.  EPI_NONE, K = 64.
-__device__ __forceinline__ int wid_stage_offset(int wid, int bytes) { return wid * bytes; }
-
-template <int KS, int STR, int XF = 0>
-__global__ __launch_bounds__(256, 1) void conv_patch_ws_kernel(LArgs a, const bf16_t* px, uint32_t bytes_x,
-                                                               const bf16_t* pw) {
-  constexpr int BM = 256, NW = 4;
-  constexpr int PIECES = kPatchBytes / 1024, PPW = PIECES / NW;
-  static_assert(PPW * NW == PIECES && KS >= 3, "patch pieces / k-steps");
-  // output staging: each wave's 64 rows x 128 B at a 144-B pitch, re-read row-wise so the stores
-  // are whole 128-B rows (16 B per lane) instead of 8-B pieces of 16 rows per instruction
-  constexpr int kOutPitch = 144, kOutWave = 64 * kOutPitch;
-  constexpr int LDS = 2 * kPatchBytes + NW * kOutWave + 16;
-  static_assert(LDS <= 160 * 1024, "LDS");
-  __shared__ __attribute__((aligned(1024))) char smem[LDS];
-  char* const ostage = smem + 2 * kPatchBytes + wid_stage_offset(threadIdx.x >> 6, kOutWave);
-  const ConvShape& sh = a.s;
-  const Geo g = make_geo(a, false, (int)blockIdx.z);
-  const int lane = threadIdx.x & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int PQ = sh.P * sh.Q, PW = sh.W + 2 * sh.pad, RS = sh.R * sh.S;
-  const int T = g.M / BM;
-  const int t0 = (int)((int64_t)blockIdx.x * T / gridDim.x);
-  const int t1 = (int)((int64_t)(blockIdx.x + 1) * T / gridDim.x);
-  uint64_t* trace = nullptr;
-  if constexpr ((XF & 32) != 0) {
-    if (threadIdx.x == 0 && a.trace != nullptr) {
-      trace = a.trace + 8 * (size_t)blockIdx.x;
-      trace[0] = __builtin_amdgcn_s_memrealtime();
-    }
-  }
-
-  Rsrc rx;
-  rx.r = __builtin_amdgcn_make_buffer_rsrc((void*)px, (short)0, (int)bytes_x, 0x00020000);
-  // patch of tile t into buffer b: cell e = (i, j) -> input (STR*p_lo - pad + i, j - pad)
-  auto dma = [&](int t, int b) {
-    const int m0 = t * BM, n_img = m0 / PQ, p_lo = (m0 - n_img * PQ) / sh.Q;
-    const int ih0 = STR * p_lo - sh.pad;
-    char* const dst = smem + b * kPatchBytes;
-#pragma unroll
-    for (int q = 0; q < PPW; ++q) {
-      const int pc = q * NW + wid;
-      const int e = pc * 64 + lane;
-      const int i = fdiv(e, a.f_w), j = e - i * PW;
-      const int ih = ih0 + i, iw = j - sh.pad;
-      const bool ok = (unsigned)ih < (unsigned)sh.H && (unsigned)iw < (unsigned)sh.W;
-      const int o = ok ? (int)((((unsigned)n_img * sh.H + ih) * (unsigned)sh.W + iw) * 16u) : (int)kOOB;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx.r, (lds_void*)(dst + pc * 1024), 16, o, 0, 0, 0);
-    }
-  };
-  if (t0 < t1) {
-    dma(t0, 0);
-    if (t0 + 1 < t1) dma(t0 + 1, 1);
-  }
-  // B fragments of every k-step (filter j*16 + (lane & 15), taps 4k + lane/16): registers for the launch
-  bf16x8 fb[KS][4];
-#pragma unroll
-  for (int k = 0; k < KS; ++k)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int t = k * 4 + (lane >> 4);
-      fb[k][j] = t < RS ? *reinterpret_cast<const bf16x8*>(pw + (size_t)(j * 16 + (lane & 15)) * a.rsc + t * 8)
-                        : bf16x8{};
-    }
-  // this lane group's tap offset (in patch cells) per k-step; padding taps read cell 0 (zero weights)
-  int toff[KS];
-#pragma unroll
-  for (int k = 0; k < KS; ++k) {
-    const int t = k * 4 + (lane >> 4);
-    const int r = t / sh.S;
-    toff[k] = t < RS ? r * PW + (t - r * sh.S) : 0;
-  }
-  if (t0 < t1) {
-    if (t0 + 1 < t1) wait_vm<PPW>();  // tile t0's patch landed (loads retire in order)
-    else wait_vm<0>();
-  }
-  if constexpr ((XF & 32) != 0) {
-    if (trace != nullptr) trace[1] = __builtin_amdgcn_s_memrealtime();
-  }
-  float bs0[4][4], bs1[4][4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) bs0[j][r] = bs1[j][r] = 0.f;
-  bf16_t* const out = reinterpret_cast<bf16_t*>(a.out);
-  for (int t = t0; t < t1; ++t) {
-    const int m0 = t * BM, n_img = m0 / PQ, mi0 = m0 - n_img * PQ, p_lo = mi0 / sh.Q;
-    const uint32_t patch = lds_off(smem + ((t - t0) & 1) * kPatchBytes);
-    uint32_t base[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int mi = mi0 + wid * 64 + i * 16 + (lane & 15);
-      const int p = fdiv(mi, a.f_q), q = mi - p * sh.Q;
-      base[i] = patch + (uint32_t)((STR * (p - p_lo)) * PW + STR * q) * 16u;
-    }
-    auto read_step = [&](int k, bf16x8 (&f)[4]) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const uint32_t ad = base[i] + (uint32_t)toff[k] * 16u;
-        asm volatile("ds_read_b128 %0, %1" : "=v"(f[i]) : "v"(ad));
-      }
-    };
-    floatx4 acc[4][4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) acc[j][i] = floatx4{0.f, 0.f, 0.f, 0.f};
-    lds_barrier();  // every wave waited for its own pieces of tile t: the whole patch is visible
-    bf16x8 fa[3][4];
-    read_step(0, fa[0]);
-    read_step(1, fa[1]);
-#pragma unroll
-    for (int k = 0; k < KS; ++k) {
-      bf16x8 (&f)[4] = fa[k % 3];
-      if (k + 2 < KS) read_step(k + 2, fa[(k + 2) % 3]);
-      if (k + 2 < KS) asm volatile("s_waitcnt lgkmcnt(8)" : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]));
-      else if (k + 1 < KS) asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]));
-      else asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]));
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[k][j], f[i], acc[j][i], 0, 0, 0);
-    }
-    lds_barrier();  // every wave is done reading this buffer
-    if (t + 2 < t1) dma(t + 2, (t - t0) & 1);
-    if (t + 1 < t1) {  // tile t+1's patch (issued a tile ago; see conv_ws64_kernel for why vmcnt(PPW) holds)
-      if (t + 2 < t1) wait_vm<PPW>();
-      else wait_vm<0>();
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int rl = i * 16 + (lane & 15);   // this wave's row
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int c = j * 16 + 4 * (lane >> 4);
-        const floatx4 v = acc[j][i];
-        const u16x4 o = u16x4{f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
-        *reinterpret_cast<u16x4*>(ostage + rl * kOutPitch + c * 2) = o;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float bv = bf2f(o[r]);
-          bs0[j][r] += bv;
-          bs1[j][r] += bv * bv;
-        }
-      }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // (a wave's LDS operations run in order)
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {   // 8 rows x 8 lanes x 16 B per store
-      const int rl = q * 8 + (lane >> 3);
-      const u32x4 v = *reinterpret_cast<const u32x4*>(ostage + rl * kOutPitch + (lane & 7) * 16);
-      *reinterpret_cast<u32x4*>(out + (size_t)(m0 + wid * 64 + rl) * 64 + (lane & 7) * 8) = v;
-    }
-  }
-  if constexpr ((XF & 32) != 0) {
-    if (trace != nullptr) trace[2] = __builtin_amdgcn_s_memrealtime();
-  }
-  if (a.bn_stats) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-          bs0[j][r] += __shfl_xor(bs0[j][r], o, 64);
-          bs1[j][r] += __shfl_xor(bs1[j][r], o, 64);
-        }
-    float* red = reinterpret_cast<float*>(smem);  // [4][64][2]
-    __syncthreads();
-    if ((lane & 15) == 0) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int c = j * 16 + 4 * (lane >> 4) + r;
-          red[(wid * 64 + c) * 2] = bs0[j][r];
-          red[(wid * 64 + c) * 2 + 1] = bs1[j][r];
-        }
-    }
-    __syncthreads();
-    float* accc = a.bn.acc + (size_t)(blockIdx.x % kBnCopies) * 2 * 64;
-    if (threadIdx.x < 64) {
-      float s0 = 0.f, s1 = 0.f;
-#pragma unroll
-      for (int q = 0; q < NW; ++q) {
-        s0 += red[(q * 64 + threadIdx.x) * 2];
-        s1 += red[(q * 64 + threadIdx.x) * 2 + 1];
-      }
-      bn_acc_add(accc + threadIdx.x, s0);
-      bn_acc_add(accc + 64 + threadIdx.x, s1);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's atomics have completed
-    bn_finalize_last<false, kBnCopies>(a.bn, g.M, 64, gridDim.x, red, LDS / 4);
-  }
-  if constexpr ((XF & 32) != 0) {
-    if (trace != nullptr) trace[3] = __builtin_amdgcn_s_memrealtime();
   }
 }
 
@@ -3286,52 +2139,11 @@ int get_conv_combine_last() { return g_combine_last; }
 void set_conv_wgrad_ring(int mode) { g_wgrad_ring = mode; }
 int get_conv_halo() { return halo_env(); }
 
-// Space-to-depth stem wgrad (stem_s2d_*): the 7x7 / 2 / pad-3 C = 8 stem with <= 4 data
-// channels (ResNet-18's 3), even H and W.  LDNN_CONV_STEM_S2D=0 turns it off (A/B knob).
-int g_stem_s2d = -2;
-void set_conv_stem_s2d(int mode) { g_stem_s2d = mode; }
-bool stem_s2d_ok(const ConvShape& s) {
-  if (g_stem_s2d == -2) g_stem_s2d = env_int("LDNN_CONV_STEM_S2D", 1);
-  return g_stem_s2d != 0 && s.C == 8 && s.c_real > 0 && s.c_real <= 4 && s.K == 64 && s.R == 7 && s.S == 7 &&
-         s.stride == 2 && s.pad == 3 && s.H % 2 == 0 && s.W % 2 == 0 && s.P == s.H / 2 && s.Q == s.W / 2 &&
-         (size_t)s.N * (s.P + 3) * (s.Q + 3) * 32 < kOOBLimit;
-}
-// The stem forward on the packed s2d image (conv_s2d_ws_kernel): the wgrad's conditions, bf16 EPI_NONE,
-// tiles that never span two images and whose s2d rows fit one ring buffer.
-bool stem_s2d_fwd_ok(const ConvShape& s) {
-  if (!stem_s2d_ok(s) || g_stem_s2d != 1 || ws_env() == 0) return false;   // (LDNN_CONV_STEM_S2D=2: wgrad only)
-  const int PQ = s.P * s.Q, Ws = s.Q + 3;
-  const int rows = (s.Q - 1 + 255) / s.Q + 1 + 3;   // output rows a 256-pixel tile touches, + the 4x4 taps
-  return PQ % 256 == 0 && (int64_t)rows * Ws * 32 <= s2dfwd::kBuf && (int64_t)s.N * PQ >= 256;
-}
-struct S2dPlan {
-  int Hs, Ws, nchunk, steps, slices, steps_per;
-  size_t slab_floats, tmp_floats, xs_floats;
-};
-S2dPlan plan_s2d(const ConvShape& s) {
-  S2dPlan p;
-  p.Hs = s.P + 3;
-  p.Ws = s.Q + 3;
-  p.nchunk = (s.Q + 31) / 32;
-  p.steps = s.N * s.P * p.nchunk;
-  // three 48-KiB workgroups per CU: the K-step loop is bound by the DMA round trip of its 3 steps
-  // in flight, not by bytes, so throughput scales with the workgroups resident per CU
-  constexpr int target = 768;
-  int slices = std::max(1, std::min(target, p.steps / 8));
-  p.steps_per = (p.steps + slices - 1) / slices;
-  p.slices = (p.steps + p.steps_per - 1) / p.steps_per;
-  p.slab_floats = (size_t)p.slices * 64 * 256;
-  p.tmp_floats = 64 * 256;
-  p.xs_floats = (size_t)s.N * p.Hs * p.Ws * 8;  // bf16 x 16 channels
-  return p;
-}
-
 ConvWorkspace conv2d_lds_workspace(const ConvShape& s, int op) {
   if (!shape_ok(s)) return ConvWorkspace{};
   if (op == 2 && stem_s2d_ok(s)) {
-    const S2dPlan p = plan_s2d(s);
     ConvWorkspace w{};
-    w.slab_bytes = (p.slab_floats + p.tmp_floats + p.xs_floats) * 4;
+    w.slab_bytes = stem_s2d_ws_bytes(s);
     return w;
   }
   if (op == 0 && s.C % 64 == 0) return ws_of(hb_takes(s, false) ? plan_hb(s, false) : plan_fwd(s));
@@ -3363,63 +2175,6 @@ hipError_t slab_sum(const float* ws, float* out, int64_t n4, int splits, float b
   return hipGetLastError();
 }
 
-// Patch path for C = 8 stems (conv_patch_kernel): 3x3 / 5x5 / 7x7 taps, stride 1 or 2,
-// P*Q % 256 == 0 (tiles inside one image), K % 64 == 0, the patch within 48 KiB.
-// LDNN_CONV_PATCH=0 turns it off (A/B knob).
-int patch_env() {
-  static const int v = env_int("LDNN_CONV_PATCH", 1);
-  return v;
-}
-int patch_ks(const ConvShape& s) {
-  const int rs = s.R * s.S;
-  return rs == 9 ? 3 : rs == 25 ? 7 : rs == 49 ? 13 : 0;
-}
-bool patch_ok(const ConvShape& s) {
-  if (patch_env() == 0 || s.C != 8 || s.K % 64 != 0 || patch_ks(s) == 0 || (s.stride != 1 && s.stride != 2)) return false;
-  const int pq = s.P * s.Q;
-  if (pq % 256 != 0) return false;
-  const int rows_out = (255 + s.Q - 1) / s.Q + 1;  // output rows a 256-pixel tile can touch
-  const int ph = (rows_out - 1) * s.stride + s.R;
-  return (size_t)ph * (s.W + 2 * s.pad) * 16 <= (size_t)kPatchBytes;
-}
-template <int KS, int STR>
-hipError_t launch_patch_e(const LArgs& a, int epi, const bf16_t* x, size_t bx, const bf16_t* w, hipStream_t st) {
-  const dim3 grid(a.tiles_x), block(256);
-  switch (epi) {
-    case EPI_NONE: conv_patch_kernel<KS, STR, EPI_NONE><<<grid, block, 0, st>>>(a, x, (uint32_t)bx, w); break;
-    case EPI_BIAS: conv_patch_kernel<KS, STR, EPI_BIAS><<<grid, block, 0, st>>>(a, x, (uint32_t)bx, w); break;
-    case EPI_BIAS_RELU: conv_patch_kernel<KS, STR, EPI_BIAS_RELU><<<grid, block, 0, st>>>(a, x, (uint32_t)bx, w); break;
-    default: return hipErrorInvalidValue;
-  }
-  return hipGetLastError();
-}
-template <int KS, int STR>
-hipError_t launch_patch_ws_e(LArgs a, const bf16_t* x, size_t bx, const bf16_t* w, hipStream_t st) {
-  const int grid = std::max(1, std::min(a.M / 256, cu_count()));
-  a.tiles_x = grid;
-  if (conv_xf_env() == 32)
-    conv_patch_ws_kernel<KS, STR, 32><<<grid, 256, 0, st>>>(a, x, (uint32_t)bx, w);
-  else
-    conv_patch_ws_kernel<KS, STR><<<grid, 256, 0, st>>>(a, x, (uint32_t)bx, w);
-  return hipGetLastError();
-}
-
-hipError_t launch_patch(LArgs a, int epi, const bf16_t* x, size_t bx, const bf16_t* w, hipStream_t st) {
-  a.f_w = make_fastdiv(a.s.W + 2 * a.s.pad);  // patch row length (cell -> row, column)
-  a.tiles_x = (a.M / 256) * (a.N / 64);
-  const int ks = patch_ks(a.s);
-  if (ws_env() != 0 && epi == EPI_NONE && a.N == 64 && ks == 13 && a.s.stride == 2)  // (LDNN_CONV_WS, as ws64)
-    return launch_patch_ws_e<13, 2>(a, x, bx, w, st);
-  if (a.s.stride == 1) {
-    if (ks == 3) return launch_patch_e<3, 1>(a, epi, x, bx, w, st);
-    if (ks == 7) return launch_patch_e<7, 1>(a, epi, x, bx, w, st);
-    return launch_patch_e<13, 1>(a, epi, x, bx, w, st);
-  }
-  if (ks == 3) return launch_patch_e<3, 2>(a, epi, x, bx, w, st);
-  if (ks == 7) return launch_patch_e<7, 2>(a, epi, x, bx, w, st);
-  return launch_patch_e<13, 2>(a, epi, x, bx, w, st);
-}
-
 // Each returns hipErrorNotSupported when the shape is outside the fast path
 // (conv.hip then runs its generic register-staged kernel).
 // Stems and other small-C convolutions (C in {8, 16, 32}, e.g. the 7x7 ResNet stem
@@ -3443,18 +2198,9 @@ hipError_t conv2d_fwd_lds_small_c(const ConvShape& s, const uint16_t* x, const u
   const bool narrow = s.K <= 64;
   a.tiles_x = ((a.M + (narrow ? 255 : 127)) / (narrow ? 256 : 128)) * ((s.K + (narrow ? 63 : 127)) / (narrow ? 64 : 128));
   const size_t bx = (size_t)s.N * s.H * s.W * s.C * 2, bw = (size_t)s.K * a.rsc * 2;
-  if (s2d_xs != nullptr) {   // the caller keeps the packed image for the weight gradient
+  if (s2d_xs != nullptr) {   // the caller keeps the packed image for the weight gradient (conv_stem.hip)
     if (epi != EPI_NONE || !stem_s2d_fwd_ok(s)) return hipErrorInvalidValue;
-    const int Hs = s.P + 3, Ws = s.Q + 3;
-    const int64_t npix = (int64_t)s.N * Hs * Ws;
-    stem_s2d_pack_kernel<<<(unsigned)((npix + 255) / 256), 256, 0, st>>>(reinterpret_cast<const bf16_t*>(x),
-                                                                          reinterpret_cast<bf16_t*>(s2d_xs), s.N,
-                                                                          s.H, s.W, Hs, Ws);
-    const int grid = std::max(1, std::min(a.M / 256, cu_count()));
-    a.tiles_x = grid;
-    conv_s2d_ws_kernel<<<grid, 256, 0, st>>>(a, reinterpret_cast<const bf16_t*>(s2d_xs), (uint32_t)(npix * 32), Hs,
-                                             Ws, reinterpret_cast<const bf16_t*>(w));
-    return hipGetLastError();
+    return stem_s2d_fwd(a, x, w, s2d_xs, st);
   }
   if (patch_ok(s)) return launch_patch(a, epi, x, bx, w, st);
   if (narrow) return launch<4, 1, FwdASmallC<256, 8, 4>, WeightKC<64, 2, 4>, false, false>(a, epi, 1, x, bx, w, bw, st);
@@ -3548,8 +2294,12 @@ FwdPrep fwd_prep(const ConvShape& s, uint16_t* y, const float* bias, int epi, fl
   pl = f.hb ? plan_hb(s, false) : plan_fwd(s);
   LArgs& a = f.a;
   a = base_args(s);
+  // the weight-stationary 64 -> 64 kernel runs unsplit on a persistent grid and takes the BN
+  // statistics in its own epilogue, whatever the plan says for the gather kernels (with the slab
+  // hand-off below its small-M launches -- ResNet-18 at 64 x 64 inputs -- took them nowhere)
+  f.ws64 = ws64_takes(s, epi);
   // slab split-K: the slab pass takes the next BN's statistics (conv_slab_bn), or with
-  if (bn != nullptr && pl.slab) {
+  if (bn != nullptr && pl.slab && !f.ws64) {
     if (bn->part != nullptr && bn->tickets != nullptr && s.K % 8 == 0) f.slab_fin = bn;
     else f.bn_used = false;
     bn = nullptr;
@@ -3579,8 +2329,8 @@ FwdPrep fwd_prep(const ConvShape& s, uint16_t* y, const float* bias, int epi, fl
   }
   f.bx = (size_t)s.N * s.H * s.W * s.C * 2;
   f.bw = (size_t)s.K * a.rsc * 2;
-  f.ws64 = ws64_takes(s, epi);
   if (f.ws64) {  // persistent grid, no split-K: the plan's slab / combine is not used
+    f.slab = false;
     a.ws = nullptr;
     a.cnt = nullptr;
     a.nk_split = a.nk_all;
@@ -3685,6 +2435,7 @@ DgradPrep dgrad_prep(const ConvShape& s, uint16_t* dx, float* ws, int* cnt, cons
   d.bw = (size_t)s.K * a.rsc * 2;
   d.ws64 = generic < 2 && ws64_takes(s, EPI_NONE);
   if (d.ws64) {
+    d.slab = false;
     a.ws = nullptr;
     a.cnt = nullptr;
     a.nk_split = a.nk_all;
@@ -3837,30 +2588,7 @@ hipError_t conv2d_wgrad_lds(const ConvShape& s, const uint16_t* dy, const uint16
   if (!shape_ok(s) || s.C % 8 != 0 || s.K % 8 != 0) return s2d_xs ? hipErrorInvalidValue : hipErrorNotSupported;
   if (beta != 0.f && beta != 1.f) return s2d_xs ? hipErrorInvalidValue : hipErrorNotSupported;
   if (s2d_xs != nullptr && !(stem_s2d_ok(s) && ws != nullptr)) return hipErrorInvalidValue;
-  if (stem_s2d_ok(s) && ws != nullptr) {
-    const S2dPlan p = plan_s2d(s);
-    float* slab = ws;
-    float* tmp = ws + p.slab_floats;
-    const int64_t npix = (int64_t)s.N * p.Hs * p.Ws;
-    const bf16_t* xs = reinterpret_cast<const bf16_t*>(s2d_xs);
-    if (xs == nullptr) {   // (the forward's packed image when it ran conv_s2d_ws_kernel)
-      bf16_t* xsw = reinterpret_cast<bf16_t*>(tmp + p.tmp_floats);
-      stem_s2d_pack_kernel<<<(unsigned)((npix + 255) / 256), 256, 0, st>>>(x, xsw, s.N, s.H, s.W, p.Hs, p.Ws);
-      xs = xsw;
-    }
-    S2dArgs a{};
-    a.N = s.N; a.P = s.P; a.Q = s.Q; a.Hs = p.Hs; a.Ws = p.Ws; a.K = s.K;
-    a.nchunk = p.nchunk;
-    a.steps = p.steps;
-    a.steps_per = p.steps_per;
-    a.slab = slab;
-    const size_t bdy = (size_t)s.N * s.P * s.Q * s.K * 2, bxs = (size_t)npix * 32;
-    stem_s2d_wgrad_kernel<<<p.slices, 256, 0, st>>>(a, dy, (uint32_t)bdy, xs, (uint32_t)bxs);
-    const int64_t n4 = 64 * 256 / 4;
-    slab_sum_kernel<false><<<(unsigned)((n4 + 31) / 32), 256, 0, st>>>(slab, tmp, n4, p.slices, 0.f);
-    stem_s2d_sum_kernel<<<(64 * 49 * 8 + 255) / 256, 256, 0, st>>>(tmp, dw, 1, beta);
-    return hipGetLastError();
-  }
+  if (stem_s2d_ok(s) && ws != nullptr) return stem_s2d_wgrad(s, dy, x, dw, beta, st, ws, s2d_xs);   // conv_stem.hip
   const WgradPlan pl = plan_wgrad(s);
   if (pl.ring) {
     WRArgs r{};

@@ -229,6 +229,67 @@ __global__ __launch_bounds__(256) void nchw_to_nhwc4_kernel(const T* __restrict_
   for (int k = 0; k < 4; ++k) d[k] = o[k];
 }
 
+// The staging pass of a graph whose first layer is the 7x7 / 2 stem on its space-to-depth image
+// (conv_stem.hip): one thread per s2d pixel (n, i, j) reads the 2x2 input block at rows 2(i-2) + dh,
+// columns 2(j-2) + dw of each of the C <= 4 channels (one 8-B / 4-B load per channel and row,
+// coalesced across j), writes the block's four NHWC pixels (two 32-B runs) when it lies in the image
+// and the 32-B s2d pixel xs[(dh*2 + dw)*4 + c] always (zeros outside the image) -- the conv then
+// skips its own pack pass, which re-read the whole NHWC image (ResNet-18 b256: 54 us).
+template <typename T>
+__global__ __launch_bounds__(256) void nchw_to_nhwc_s2d_kernel(const T* __restrict__ src, bf16_t* __restrict__ dst,
+                                                               bf16_t* __restrict__ s2d, int npix, int C, int H, int W,
+                                                               int Hs, int Ws, const uint2* __restrict__ esrc,
+                                                               uint2* __restrict__ edst, int64_t e8) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < e8) edst[i] = esrc[i];   // a batch's labels staged in the same launch (8-B pieces)
+  if (i >= npix) return;
+  const int jj = i % Ws, t = i / Ws;
+  const int ii = t % Hs, n = t / Hs;
+  const int h0 = 2 * (ii - 2), w0 = 2 * (jj - 2);
+  const bool in = h0 >= 0 && h0 < H && w0 >= 0 && w0 < W;   // (H, W even: the whole 2x2 block)
+  u16x8 px[2][2];   // [dh][dw]: 8-channel NHWC pixels (channels >= C zero)
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) px[a][b] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+  if (in) {
+    const T* s = src + ((size_t)n * C * H + h0) * W + w0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      if (c >= C) break;
+#pragma unroll
+      for (int dh = 0; dh < 2; ++dh) {
+        const T* r = s + ((size_t)c * H + dh) * W;
+        if constexpr (sizeof(T) == 4) {
+          const float2 v = *reinterpret_cast<const float2*>(r);
+          px[dh][0][c] = f2bf(v.x);
+          px[dh][1][c] = f2bf(v.y);
+        } else {
+          const uint32_t v = *reinterpret_cast<const uint32_t*>(r);
+          px[dh][0][c] = (uint16_t)(v & 0xffffu);
+          px[dh][1][c] = (uint16_t)(v >> 16);
+        }
+      }
+    }
+#pragma unroll
+    for (int dh = 0; dh < 2; ++dh) {
+      u16x8* d = reinterpret_cast<u16x8*>(dst) + ((size_t)n * H + h0 + dh) * W + w0;
+      d[0] = px[dh][0];
+      d[1] = px[dh][1];
+    }
+  }
+  u16x8 o[2];   // s2d channel (dh*2 + dw)*4 + c: o[dh][dw*4 + c]
+#pragma unroll
+  for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+    for (int dw = 0; dw < 2; ++dw)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) o[dh][dw * 4 + c] = px[dh][dw][c];
+  u16x8* xs = reinterpret_cast<u16x8*>(s2d) + (size_t)i * 2;
+  xs[0] = o[0];
+  xs[1] = o[1];
+}
+
 // out[c][r] = in[r][c], 64 x 64 tiles.  The tile goes to LDS as whole 128-B rows (16-B chunks
 // XOR-swizzled by row, rows 8 apart shifted by 4 more chunks) and comes back COLUMN-wise through
 // ds_read_b64_tr_b16 (per 16-lane group: 4 rows x 16 columns, lane i receives column i):
@@ -426,6 +487,29 @@ hipError_t nchw_to_nhwc(const void* src, bool src_f32, uint16_t* dst, int N, int
     nchw_to_nhwc_kernel<float><<<g, 256, 0, s>>>(static_cast<const float*>(src), dst, total, C, HW, groups, es, ed, e8);
   else
     nchw_to_nhwc_kernel<bf16_t><<<g, 256, 0, s>>>(static_cast<const bf16_t*>(src), dst, total, C, HW, groups, es, ed, e8);
+  return hipGetLastError();
+}
+
+hipError_t nchw_to_nhwc_s2d(const void* src, bool src_f32, uint16_t* dst, uint16_t* s2d, int N, int C, int H, int W,
+                            hipStream_t s, const void* extra_src, void* extra_dst, int64_t extra_bytes) {
+  if (N <= 0) return hipSuccess;
+  if (C <= 0 || C > 4 || H % 2 || W % 2 || H <= 0 || W <= 0) return hipErrorInvalidValue;
+  if (extra_bytes % 8 || ((uintptr_t)extra_src & 7) || ((uintptr_t)extra_dst & 7)) return hipErrorInvalidValue;
+  const int Hs = H / 2 + 3, Ws = W / 2 + 3;
+  if ((int64_t)N * Hs * Ws >= (int64_t)1 << 30 || (int64_t)N * C * H * W >= (int64_t)1 << 40) return hipErrorInvalidValue;
+  const int npix = N * Hs * Ws;
+  const int64_t e8 = extra_bytes / 8;
+  const unsigned g = (unsigned)((std::max((int64_t)npix, e8) + 255) / 256);
+  const uint2* es = static_cast<const uint2*>(extra_src);
+  uint2* ed = static_cast<uint2*>(extra_dst);
+  bf16_t* d = reinterpret_cast<bf16_t*>(dst);
+  bf16_t* x2 = reinterpret_cast<bf16_t*>(s2d);
+  if (src_f32)
+    nchw_to_nhwc_s2d_kernel<float><<<g, 256, 0, s>>>(static_cast<const float*>(src), d, x2, npix, C, H, W, Hs, Ws, es,
+                                                      ed, e8);
+  else
+    nchw_to_nhwc_s2d_kernel<bf16_t><<<g, 256, 0, s>>>(static_cast<const bf16_t*>(src), d, x2, npix, C, H, W, Hs, Ws,
+                                                       es, ed, e8);
   return hipGetLastError();
 }
 

@@ -84,7 +84,7 @@ FUSE_BN_STATS = os.environ.get("LDNN_FUSE_BN_STATS", "1") == "1"
 def pair_conv_bn(conv: "Conv2d", bn: "BatchNorm2d") -> None:
     """Declare that `bn` consumes exactly `conv`'s output: in training mode the conv
     kernel's epilogue then accumulates and finalizes the BN's batch statistics
-    (conv_lds.hip bn_stats_epilogue) and the BN runs only its apply pass.  Only for
+    (ldnn_conv_lds.h bn_stats_epilogue) and the BN runs only its apply pass.  Only for
     architectures where that dataflow is fixed (the BN also checks it is handed the
     very buffer the conv wrote before it trusts the statistics)."""
     conv.__dict__["_ldnn_stats_bn"] = bn

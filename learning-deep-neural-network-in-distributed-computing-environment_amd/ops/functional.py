@@ -395,20 +395,26 @@ class _Conv2dNative(torch.autograd.Function):
         if relu and b is None:
             b = torch.zeros(kp, dtype=torch.float32, device=x.device)
             epi = C.EPI_BIAS_RELU
-        xs = None
+        xs, packed = None, False
         if (epi == C.EPI_NONE and cp == 8 and R == 7 and S == 7 and stride == 2
                 and C.stem_s2d_fwd_ok(N, H, W, cp, kp, R, S, stride, pad, Cin)):
             # a 7x7 / 2 stem: the forward runs on the packed space-to-depth image, which the weight
-            # gradient then reuses (conv_lds.hip conv_s2d_ws_kernel / stem_s2d_wgrad_kernel)
-            xs = torch.empty(N, P + 3, Q + 3, 16, dtype=torch.bfloat16, device=x.device)
+            # gradient then reuses (conv_stem.hip conv_s2d_ws_kernel / stem_s2d_wgrad_kernel) -- the
+            # one a graph's input staging wrote along with x (graphed.static_input), or packed here
+            img, ver = getattr(x, "_ldnn_s2d", (None, None))
+            if (img is not None and ver == x._version and tuple(img.shape) == (N, P + 3, Q + 3, 16)
+                    and img.device == x.device):
+                xs, packed = img, True
+            else:
+                xs = torch.empty(N, P + 3, Q + 3, 16, dtype=torch.bfloat16, device=x.device)
         if _fused_bn_ok(bn, K, kp, bias, relu):
             # the conv epilogue accumulates + finalizes the next BN's batch statistics
             args, state = _conv_bn_stats(bn, K, x.device, C)
-            done = C.conv_fwd(xb, w, y, stride, pad, b, epi, real_channels=Cin, s2d_xs=xs,
+            done = C.conv_fwd(xb, w, y, stride, pad, b, epi, real_channels=Cin, s2d_xs=xs, s2d_packed=packed,
                               **{"bn_" + k: v for k, v in args.items()})
             _conv_bn_stats_done(bn, done, y, state)
         else:
-            C.conv_fwd(xb, w, y, stride, pad, b, epi, real_channels=Cin, s2d_xs=xs)
+            C.conv_fwd(xb, w, y, stride, pad, b, epi, real_channels=Cin, s2d_xs=xs, s2d_packed=packed)
         ctx.save_for_backward(xb, y, xs)
         ctx.meta = (stride, pad, flat, weight, bias, relu, Cin, x.dtype)
         src = getattr(x, "_ldnn_bnsrc", None)

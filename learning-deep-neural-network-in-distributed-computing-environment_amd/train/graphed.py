@@ -38,6 +38,25 @@ from .static_mlp import no_gc
 
 # LDNN_NHWC_INPUT=0: the graph's static input stays an NCHW copy of the batch (A/B knob)
 NHWC_INPUT = os.environ.get("LDNN_NHWC_INPUT", "1") == "1"
+# LDNN_STAGE_S2D=0: a 7x7 / 2 stem packs its space-to-depth image itself instead of the staging
+# pass writing it (A/B knob)
+STAGE_S2D = os.environ.get("LDNN_STAGE_S2D", "1") == "1"
+
+
+def _stem_s2d_image(first, x, cp, C_):
+    """The packed space-to-depth image [N][H/2+3][W/2+3][16] the staging pass writes for a first
+    layer that is a 7x7 / 2 / pad-3 bias-free stem the s2d forward takes (conv_stem.hip), or None."""
+    N, C, H, W = x.shape
+    fl = getattr(first, "_ldnn_flat", None)
+    if not (STAGE_S2D and fl is not None and fl.shadow is not None and cp == 8 and C <= 4 and H % 2 == 0
+            and W % 2 == 0 and first.bias is None and getattr(first, "activation", "none") != "relu"
+            and first.groups == 1 and first.dilation == (1, 1) and tuple(first.kernel_size) == (7, 7)
+            and tuple(first.stride) == (2, 2) and tuple(first.padding) == (3, 3) and first.in_channels == C):
+        return None
+    kp = fl.shadow_storage(first.weight).shape[0]
+    if not C_.stem_s2d_fwd_ok(N, H, W, cp, kp, 7, 7, 2, 3, C):
+        return None
+    return torch.empty(N, H // 2 + 3, W // 2 + 3, 16, dtype=torch.bfloat16, device=x.device)
 
 
 def unit_seed(device) -> torch.Tensor:
@@ -71,19 +90,24 @@ def static_input(model, x_example: torch.Tensor):
         cp = fl.shadow_storage(first.weight).shape[3] if fl is not None and fl.shadow is not None else LF._up8(C)
         buf = torch.empty(N, H, W, cp, dtype=torch.bfloat16, device=x.device)
         C_ = _ext.C()
-        C_.nchw_to_nhwc(x, buf)
+        # a 7x7 / 2 stem: the same pass also writes its space-to-depth image, which the conv then
+        # reads instead of packing it from buf (ResNet-18 b256: one 313 MB pass less)
+        img = _stem_s2d_image(first, x, cp, C_) if x.data_ptr() % 8 == 0 else None
+        C_.nchw_to_nhwc(x, buf, s2d=img)
         xs = LF.nchw_view(buf, C)
         xs._ldnn_zpad = True   # the staging pass writes the pad channels' zeros
+        if img is not None:   # (with x's version: an in-place change of x after staging voids the image)
+            xs._ldnn_s2d = (img, xs._version)
 
         def stage(xn: torch.Tensor, yn: torch.Tensor, ys: torch.Tensor):
             if xn.device != buf.device or xn.dtype not in (torch.float32, torch.bfloat16):
                 xn = xn.to(buf.device, torch.float32)   # (a host batch, fp16 / uint8: what copy_ accepted)
-            xn = xn if xn.is_contiguous() else xn.contiguous()
+            xn = xn if xn.is_contiguous() and xn.data_ptr() % 8 == 0 else xn.clone()
             if (yn.is_cuda and yn.is_contiguous() and yn.dtype == ys.dtype and yn.nbytes % 8 == 0
                     and yn.data_ptr() % 8 == 0):   # the labels ride along in the same launch
-                C_.nchw_to_nhwc(xn, buf, yn, ys)
+                C_.nchw_to_nhwc(xn, buf, yn, ys, s2d=img)
             else:
-                C_.nchw_to_nhwc(xn, buf)
+                C_.nchw_to_nhwc(xn, buf, s2d=img)
                 ys.copy_(yn, non_blocking=True)
         return xs, stage
 

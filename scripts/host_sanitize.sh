@@ -11,7 +11,7 @@ mkdir -p "$OUT"
 HIPCC=${HIPCC:-/opt/rocm/bin/hipcc}
 SAN="-Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host -fno-sanitize-recover=all -Xarch_host -fno-omit-frame-pointer"
 FLAGS="--offload-arch=gfx950 -O1 -g -std=c++17 -I$CS/include $SAN"
-SRCS="conv_lds bn_pool head elementwise"
+SRCS="conv_lds conv_stem bn_pool head elementwise"
 pids=()
 for f in $SRCS; do
   src="$CS/kernels/$f.hip"; obj="$OUT/$f.o"

@@ -253,6 +253,32 @@ def test_weight_stationary_conv64_matches_halo_and_fp32(N, H, W):
     torch.testing.assert_close(outs[mode][1].float(), dxr, rtol=1e-2, atol=1e-2 * dxr.abs().max().item())
 
 
+@pytest.mark.parametrize("N,H,W", [(16, 16, 16), (3, 9, 11), (2, 8, 8), (64, 56, 56), (8, 28, 28)])
+def test_weight_stationary_conv64_takes_the_next_bn_statistics_at_any_m(N, H, W):
+    """conv_fwd with the next BN's statistics on the weight-stationary 64 -> 64 kernel: the kernel's
+    epilogue computes them (done) == the statistics of its own bf16 output -- also for the small-M
+    shapes whose gather-kernel plan is slab split-K (the slab hand-off used to leave them
+    uncomputed while reporting done: ResNet-18 at 64 x 64 inputs trained on garbage there)."""
+    torch.manual_seed(29)
+    Cc = _ext.C()
+    x = torch.randn(N, H, W, 64, device="cuda").bfloat16()
+    w = (torch.randn(64, 3, 3, 64, device="cuda") * (1.0 / 576 ** 0.5)).bfloat16()
+    ws = torch.zeros(Cc.bn_workspace_floats(64), device="cuda")
+    for rep in range(2):   # (the second call: the accumulators the first one left clear)
+        y = torch.full((N, H, W, 64), 7.0, device="cuda", dtype=torch.bfloat16)
+        sm = torch.full((64,), float("nan"), device="cuda")
+        si = torch.full((64,), float("nan"), device="cuda")
+        done = Cc.conv_fwd(x, w, y, 1, 1, None, 0, bn_ws=ws, bn_gamma=torch.ones(64, device="cuda"),
+                           bn_beta=torch.zeros(64, device="cuda"), bn_save_mean=sm, bn_save_invstd=si)
+        assert done
+        yr = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2),
+                                        padding=1).permute(0, 2, 3, 1)
+        torch.testing.assert_close(y.float(), yr, rtol=1e-2, atol=1e-2 * yr.abs().max().item())
+        yb = y.float().reshape(-1, 64)
+        torch.testing.assert_close(sm, yb.mean(0), rtol=1e-3, atol=1e-4)
+        torch.testing.assert_close(si, torch.rsqrt(yb.var(0, unbiased=False) + 1e-5), rtol=1e-3, atol=1e-4)
+
+
 @pytest.mark.parametrize("N,C,H,W,K", [(2, 64, 56, 56, 64), (3, 128, 28, 28, 128), (2, 256, 14, 14, 512),
                                        (4, 512, 7, 7, 512), (5, 64, 9, 9, 128), (2, 128, 16, 16, 256),
                                        (1, 64, 63, 63, 64), (7, 192, 4, 4, 64), (3, 64, 5, 5, 64), (2, 64, 8, 8, 128), (3, 128, 9, 11, 64)])
@@ -361,6 +387,53 @@ def test_stem_s2d_forward_matches_fp32_and_its_image_feeds_the_wgrad(N, Cin, H, 
     Cc.conv_wgrad(gy, x, d0, 2, 3, 0.0, real_channels=Cin)
     Cc.conv_wgrad(gy, x, d1, 2, 3, 0.0, real_channels=Cin, s2d_xs=xs)
     assert torch.equal(d0, d1)
+
+
+def _s2d_reference(x):
+    """xs[n][i][j][(dh*2 + dw)*4 + c] = x[n][c][2(i-2) + dh][2(j-2) + dw] (bf16-rounded; zeros outside)."""
+    N, C, H, W = x.shape
+    Hs, Ws = H // 2 + 3, W // 2 + 3
+    pad = torch.zeros(N, C, 2 * Hs, 2 * Ws, device=x.device)
+    pad[:, :, 4:4 + H, 4:4 + W] = x.bfloat16().float()
+    t = pad.view(N, C, Hs, 2, Ws, 2).permute(0, 2, 4, 3, 5, 1)   # [n][i][j][dh][dw][c]
+    ref = torch.zeros(N, Hs, Ws, 2, 2, 4, device=x.device)
+    ref[..., :C] = t
+    return ref.reshape(N, Hs, Ws, 16).bfloat16()
+
+
+@pytest.mark.parametrize("N,C,H,W,f32", [(2, 3, 224, 224, True), (3, 3, 30, 40, True), (2, 1, 64, 64, False),
+                                         (1, 4, 18, 22, False), (5, 2, 6, 8, True)])
+def test_input_staging_writes_the_stem_s2d_image(N, C, H, W, f32):
+    """nchw_to_nhwc(..., s2d=img), the graph's input staging ahead of a 7x7 / 2 stem
+    (elementwise.hip nchw_to_nhwc_s2d_kernel): its NHWC image == the plain staging's bit for bit,
+    the s2d image == the mapping above, the labels ride along; and where the s2d stem forward
+    takes the shape, conv_fwd on the staged image (s2d_packed) == conv_fwd packing its own."""
+    torch.manual_seed(23)
+    Cc = _ext.C()
+    x = torch.randn(N, C, H, W, device="cuda")
+    x = x if f32 else x.bfloat16()
+    lab = torch.randint(0, 10, (16,), device="cuda")
+    lab_out = torch.full_like(lab, -1)
+    buf0 = torch.full((N, H, W, 8), float("nan"), device="cuda").bfloat16()
+    buf1 = torch.full((N, H, W, 8), float("nan"), device="cuda").bfloat16()
+    img = torch.full((N, H // 2 + 3, W // 2 + 3, 16), float("nan"), device="cuda").bfloat16()
+    Cc.nchw_to_nhwc(x, buf0)
+    Cc.nchw_to_nhwc(x, buf1, lab, lab_out, s2d=img)
+    torch.cuda.synchronize()
+    assert torch.equal(buf0, buf1)
+    assert torch.equal(lab, lab_out)
+    assert torch.equal(img, _s2d_reference(x.float()))
+    if Cc.stem_s2d_fwd_ok(N, H, W, 8, 64, 7, 7, 2, 3, C):
+        w = torch.zeros(64, 7, 7, 8, device="cuda", dtype=torch.bfloat16)
+        w[..., :C] = (torch.randn(64, 7, 7, C, device="cuda") * 0.1).bfloat16()
+        ys = []
+        for packed in (False, True):
+            y = torch.empty(N, H // 2, W // 2, 64, device="cuda", dtype=torch.bfloat16)
+            xs = img if packed else torch.empty_like(img)
+            Cc.conv_fwd(buf1, w, y, 2, 3, None, 0, real_channels=C, s2d_xs=xs, s2d_packed=packed)
+            ys.append((y, xs))
+        assert torch.equal(ys[0][0], ys[1][0])
+        assert torch.equal(ys[0][1], img)
 
 
 @pytest.mark.parametrize("N,C,H,W,K", [(2, 128, 28, 28, 128), (8, 128, 31, 31, 128), (64, 128, 16, 16, 128),

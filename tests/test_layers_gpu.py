@@ -139,11 +139,13 @@ def test_cnn_native_matches_cpu_fp32(name, shape):
 
 @pytest.mark.parametrize("name,shape,opt_name", [("lenet5", (256, 1, 28, 28), "sgd"),
                                                 ("enhanced_cnn_small", (32, 3, 32, 32), "sgd"),
-                                                ("lenet5", (256, 1, 28, 28), "adam")])
+                                                ("lenet5", (256, 1, 28, 28), "adam"),
+                                                ("resnet18", (16, 3, 64, 64), "sgd")])
 def test_graphed_step_matches_eager(name, shape, opt_name):
     """A training step replayed from one hipGraph (train.graphed.GraphedStep) gives the
     same parameters as the same steps run eagerly, including an lr change between
-    replays (the graph reads lr from the optimizer's device tensor)."""
+    replays (the graph reads lr from the optimizer's device tensor).  ResNet-18: the graph's
+    input staging also writes the stem's space-to-depth image (the eager steps pack their own)."""
     from ldnn.optim import SGD, Adam
     from ldnn.train.graphed import GraphedStep
 
@@ -167,6 +169,9 @@ def test_graphed_step_matches_eager(name, shape, opt_name):
         o.step()
     p0 = [q.detach().clone() for q in m2.parameters()]
     gs = GraphedStep(m1, crit, o1, xs[1], ys[1], warmup=0)
+    from ldnn.train import graphed
+    if name == "resnet18" and graphed.STAGE_S2D:
+        assert getattr(gs.x, "_ldnn_s2d", None) is not None
     for i in range(1, 5):
         if i == 3:
             for o in (o1, o2, o3):
@@ -186,9 +191,11 @@ def test_graphed_step_matches_eager(name, shape, opt_name):
         eg, ee = (d1 - d2).norm().item(), (d3 - d2).norm().item()
         assert eg <= 3.0 * ee + 2e-3 * d2.norm().item(), (n, eg, ee, d2.norm().item())
         cos = torch.nn.functional.cosine_similarity(d1, d2, dim=0).item()
+        cos_ee = torch.nn.functional.cosine_similarity(d3, d2, dim=0).item()
         # (Adam normalises each element's update: on the 1-D BatchNorm / bias parameters at
-        # batch 32 the arrival-order noise alone turns the update direction by up to ~25 degrees)
-        assert cos > (0.8 if opt_name == "adam" and p.dim() == 1 else 0.9), (n, cos)
+        # batch 32 the arrival-order noise alone turns the update direction by up to ~25 degrees;
+        # ResNet-18 at batch 16: the two eager runs' stem updates already part by ~50 degrees)
+        assert cos > min(0.8 if opt_name == "adam" and p.dim() == 1 else 0.9, cos_ee - 0.1), (n, cos, cos_ee)
     for (n, b), (_, c), (_, e) in zip(m1.named_buffers(), m2.named_buffers(), m3.named_buffers()):
         b, c, e = b.double(), c.double(), e.double()
         assert (b - c).norm().item() <= 3.0 * (e - c).norm().item() + 1e-3 * c.norm().item() + 1e-6, n
@@ -225,7 +232,7 @@ def test_train_global_with_graphs_matches_eager():
                                                   (64, 256, 8, 256, 1)])
 def test_conv_epilogue_bn_statistics_layer_vs_fp32(N, Cin, H, Cout, stride, monkeypatch):
     """A conv whose epilogue accumulates + finalizes the next BatchNorm's statistics
-    (conv_lds.hip bn_stats_epilogue; ResNet-18 layer1 / a stride-2 stage entry, two
+    (ldnn_conv_lds.h bn_stats_epilogue; ResNet-18 layer1 / a stride-2 stage entry, two
     EnhancedCNN stages) == the same conv + the BN's own reduce pass == a plain fp32
     torch conv + BN, on ONE seeded upstream gradient injected at relu(bn(conv x)):
     running statistics, outputs, dgamma / dbeta / dx, and dW against an fp32 oracle
