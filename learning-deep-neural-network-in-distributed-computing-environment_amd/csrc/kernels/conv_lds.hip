@@ -2299,7 +2299,7 @@ FwdPrep fwd_prep(const ConvShape& s, uint16_t* y, const float* bias, int epi, fl
   // hand-off below its small-M launches -- ResNet-18 at 64 x 64 inputs -- took them nowhere)
   f.ws64 = ws64_takes(s, epi);
   // slab split-K: the slab pass takes the next BN's statistics (conv_slab_bn), or with
-  if (bn != nullptr && pl.slab && !f.ws64) {
+  if (bn != nullptr && pl.slab && pl.splits > 1 && ws != nullptr && !f.ws64) {   // (the slab pass will run)
     if (bn->part != nullptr && bn->tickets != nullptr && s.K % 8 == 0) f.slab_fin = bn;
     else f.bn_used = false;
     bn = nullptr;
