@@ -431,3 +431,25 @@ def test_optimizer_range_updates_equal_full_step(opt_name):
             assert torch.equal(a, b), k
     assert o1._ls()["step"] == o2._ls()["step"] == 2
 
+
+
+def test_staged_stem_image_is_dropped_after_an_in_place_change_of_the_input():
+    """graphed.static_input stages a 7x7 / 2 stem's space-to-depth image with the batch; an in-place
+    change of the staged input afterwards bumps its version, and the stem then packs its own image
+    from the changed input instead of reading the stale one."""
+    from ldnn.train.graphed import STAGE_S2D, static_input
+
+    if not STAGE_S2D:
+        pytest.skip("LDNN_STAGE_S2D=0")
+    torch.manual_seed(3)
+    m = build_model("resnet18")
+    xavier_init(m)
+    ldnn.prepare(m, "cuda")
+    x = torch.randn(16, 3, 64, 64, device="cuda")
+    xs, _ = static_input(m, x)
+    assert getattr(xs, "_ldnn_s2d", None) is not None
+    ref = m.conv1((x.bfloat16().float() * 2.0).contiguous())   # (x 2: exact in bf16)
+    with torch.no_grad():
+        xs.mul_(2.0)
+    out = m.conv1(xs)
+    assert torch.equal(out.float(), ref.float())
