@@ -336,18 +336,26 @@ void act_bwd(const at::Tensor& dy, const at::Tensor& y, const at::Tensor& dx, in
   check(ldnn::act_bwd(bf16_ptr(dy), bf16_ptr(y), bf16_mut(dx), y.numel(), (int)act, cur_stream(y)), "act_bwd");
 }
 
-void colsum(const at::Tensor& x, const at::Tensor& out, bool accumulate) {
+// the optional ticketed scratch of colsum / act_bwd_colsum: >= cols + 1 zeroed fp32 (kept zero by the kernel)
+float* colsum_ws(const c10::optional<at::Tensor>& ws, int64_t cols) {
+  if (!ws.has_value()) return nullptr;
+  check_dev(*ws, at::kFloat, "ws");
+  TORCH_CHECK(ws->is_contiguous() && ws->numel() >= cols + 1, "colsum: ws needs cols + 1 zeroed floats");
+  return ws->data_ptr<float>();
+}
+
+void colsum(const at::Tensor& x, const at::Tensor& out, bool accumulate, const c10::optional<at::Tensor>& ws) {
   check_dev(x, at::kBFloat16, "x");
   check_dev(out, at::kFloat, "out");
   TORCH_CHECK(x.dim() == 2 && x.is_contiguous() && x.size(1) % 8 == 0, "colsum: x must be [R][C], C%8==0");
   TORCH_CHECK(out.is_contiguous() && out.numel() >= x.size(1), "colsum: bad out");
   check(ldnn::colsum_bf16(bf16_ptr(x), out.data_ptr<float>(), (int)x.size(0), (int)x.size(1), accumulate,
-                          cur_stream(x)),
+                          cur_stream(x), colsum_ws(ws, x.size(1))),
         "colsum");
 }
 
 void act_bwd_colsum(const at::Tensor& dy, const at::Tensor& y, const at::Tensor& dx, const at::Tensor& out,
-                    int64_t act, bool accumulate) {
+                    int64_t act, bool accumulate, const c10::optional<at::Tensor>& ws) {
   check_dev(dy, at::kBFloat16, "dy");
   check_dev(y, at::kBFloat16, "y");
   check_dev(dx, at::kBFloat16, "dx");
@@ -358,7 +366,7 @@ void act_bwd_colsum(const at::Tensor& dy, const at::Tensor& y, const at::Tensor&
   TORCH_CHECK(y.size(1) % 8 == 0 && out.numel() >= y.size(1), "act_bwd_colsum: cols % 8 != 0 or short out");
   TORCH_CHECK(act == ldnn::ACT_RELU || act == ldnn::ACT_SIGMOID, "act_bwd_colsum: act must be relu/sigmoid");
   check(ldnn::act_bwd_colsum(bf16_ptr(dy), bf16_ptr(y), bf16_mut(dx), out.data_ptr<float>(), (int)y.size(0),
-                             (int)y.size(1), (int)act, accumulate, cur_stream(y)),
+                             (int)y.size(1), (int)act, accumulate, cur_stream(y), colsum_ws(ws, y.size(1))),
         "act_bwd_colsum");
 }
 
@@ -1952,9 +1960,9 @@ PYBIND11_MODULE(_C, m) {
         py::arg("cnt") = py::none());
   m.def("act_fwd", &act_fwd);
   m.def("act_bwd", &act_bwd);
-  m.def("colsum", &colsum, py::arg("x"), py::arg("out"), py::arg("accumulate") = false);
+  m.def("colsum", &colsum, py::arg("x"), py::arg("out"), py::arg("accumulate") = false, py::arg("ws") = py::none());
   m.def("act_bwd_colsum", &act_bwd_colsum, py::arg("dy"), py::arg("y"), py::arg("dx"), py::arg("out"),
-        py::arg("act"), py::arg("accumulate") = true);
+        py::arg("act"), py::arg("accumulate") = true, py::arg("ws") = py::none());
   m.def("cast_f32_bf16", &cast_f32_bf16);
   m.def("cast_bf16_f32", &cast_bf16_f32);
   m.def("mix3", &mix3, py::arg("out"), py::arg("x"), py::arg("y1") = py::none(), py::arg("y2") = py::none(),

@@ -303,11 +303,14 @@ hipError_t global_avgpool_bwd(const uint16_t* dy, uint16_t* dx, int N, int HW, i
 enum Act : int { ACT_RELU = 0, ACT_SIGMOID = 1 };
 hipError_t act_fwd(const uint16_t* x, uint16_t* y, int64_t n, int act, hipStream_t s);
 hipError_t act_bwd(const uint16_t* dy, const uint16_t* y, uint16_t* dx, int64_t n, int act, hipStream_t s);
-// dbias[c] (+)= sum_r x[r][c] over a [rows][cols] bf16 matrix (ld = cols)
-hipError_t colsum_bf16(const uint16_t* x, float* out, int rows, int cols, bool accumulate, hipStream_t s);
-// dx = act'(y) * dy with the column sums of dx added to out (dy may alias dx)
+// dbias[c] (+)= sum_r x[r][c] over a [rows][cols] bf16 matrix (ld = cols).  ws (optional): a zeroed
+// scratch of cols floats + one int the caller keeps; an overwriting sum over several row groups then
+// runs as ONE launch (ticketed: the last group moves the sums into out and re-zeroes ws)
+hipError_t colsum_bf16(const uint16_t* x, float* out, int rows, int cols, bool accumulate, hipStream_t s,
+                       float* ws = nullptr);
+// dx = act'(y) * dy with the column sums of dx added to out (dy may alias dx); ws as colsum_bf16
 hipError_t act_bwd_colsum(const uint16_t* dy, const uint16_t* y, uint16_t* dx, float* out, int rows, int cols,
-                          int act, bool accumulate, hipStream_t s);
+                          int act, bool accumulate, hipStream_t s, float* ws = nullptr);
 hipError_t cast_f32_bf16(const float* x, uint16_t* y, int64_t n, hipStream_t s);
 // graph-capture-safe zero fill of a strided fp32 block (instead of hipMemset2DAsync)
 hipError_t zero2d_f32(float* p, int rows, int cols, int ld, hipStream_t s);

@@ -94,11 +94,17 @@ inline CsGeo cs_geo(int rows, int cols) {
   return g;
 }
 
+// acc / ticket (optional, a caller-kept zeroed scratch of cols floats + one int): the row groups
+// add into acc instead of out, and the last workgroup to finish moves acc into out (= or +=) and
+// leaves acc and the ticket zero -- one launch where a multi-group sum that overwrites out needed a
+// zero-fill launch first (LeNet-5's conv bias gradients: 2 of its 30 kernels)
 template <int ACT, bool BWD>
 __global__ __launch_bounds__(256) void colsum_geo_kernel(const bf16_t* dy, const bf16_t* __restrict__ y, bf16_t* dx,
                                                          float* __restrict__ out, int rows, int cols, int rpb,
-                                                         int lanes, int rl, int store) {
+                                                         int lanes, int rl, int store, float* __restrict__ acc,
+                                                         int* __restrict__ ticket, int accum_out) {
   __shared__ float part[256 * 8];
+  __shared__ int s_last;
   const int tid = threadIdx.x, lane = tid % lanes, ty = tid / lanes;
   const int c0 = (blockIdx.x * lanes + lane) * 8;
   const int r_begin = blockIdx.y * rpb;
@@ -140,8 +146,23 @@ __global__ __launch_bounds__(256) void colsum_geo_kernel(const bf16_t* dy, const
     if (c >= cols) continue;
     float t = 0.f;
     for (int q = 0; q < rl; ++q) t += part[q * w + ch];
-    if (store) out[c] = t;
+    if (acc != nullptr) atomicAdd(acc + c, t);
+    else if (store) out[c] = t;
     else atomicAdd(out + c, t);
+  }
+  if (acc == nullptr) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this thread's adds have completed
+  __syncthreads();
+  if (tid == 0) {
+    const int tk = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = tk == (int)(gridDim.x * gridDim.y) - 1;
+    if (s_last) __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (!s_last) return;
+  for (int c = tid; c < cols; c += 256) {
+    const float v = atomicExch(acc + c, 0.f);
+    out[c] = accum_out ? out[c] + v : v;
   }
 }
 
@@ -535,37 +556,42 @@ hipError_t zero2d_f32(float* p, int rows, int cols, int ld, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t colsum_bf16(const uint16_t* x, float* out, int rows, int cols, bool accumulate, hipStream_t s) {
+hipError_t colsum_bf16(const uint16_t* x, float* out, int rows, int cols, bool accumulate, hipStream_t s, float* ws) {
   if (cols <= 0) return hipSuccess;
   if (cols % 8) return hipErrorInvalidValue;
   const CsGeo g = cs_geo(std::max(rows, 1), cols);
   const bool store = !accumulate && g.gy == 1;
-  if (!accumulate && !store) {
+  const bool self = ws != nullptr && !accumulate && !store;   // (one launch: the ticketed scratch)
+  if (!accumulate && !store && !self) {
     hipError_t e = zero2d_f32(out, 1, cols, cols, s);
     if (e != hipSuccess) return e;
   }
-  colsum_geo_kernel<ACT_RELU, false><<<dim3(g.gx, g.gy), kBlock, 0, s>>>(x, nullptr, nullptr, out, rows, cols, g.rpb,
-                                                                      g.lanes, g.rl, store ? 1 : 0);
+  colsum_geo_kernel<ACT_RELU, false><<<dim3(g.gx, g.gy), kBlock, 0, s>>>(
+      x, nullptr, nullptr, out, rows, cols, g.rpb, g.lanes, g.rl, store ? 1 : 0, self ? ws : nullptr,
+      self ? reinterpret_cast<int*>(ws + cols) : nullptr, 0);
   return hipGetLastError();
 }
 
 hipError_t act_bwd_colsum(const uint16_t* dy, const uint16_t* y, uint16_t* dx, float* out, int rows, int cols,
-                          int act, bool accumulate, hipStream_t s) {
+                          int act, bool accumulate, hipStream_t s, float* ws) {
   if (cols <= 0) return hipSuccess;
   if (cols % 8) return hipErrorInvalidValue;
   const CsGeo g = cs_geo(std::max(rows, 1), cols);
   const bool store = !accumulate && g.gy == 1;
-  if (!accumulate && !store) {
+  const bool self = ws != nullptr && !accumulate && !store;
+  if (!accumulate && !store && !self) {
     hipError_t e = zero2d_f32(out, 1, cols, cols, s);
     if (e != hipSuccess) return e;
   }
   const dim3 grid(g.gx, g.gy);
+  float* acc = self ? ws : nullptr;
+  int* tk = self ? reinterpret_cast<int*>(ws + cols) : nullptr;
   if (act == ACT_RELU)
     colsum_geo_kernel<ACT_RELU, true><<<grid, kBlock, 0, s>>>(dy, y, dx, out, rows, cols, g.rpb, g.lanes, g.rl,
-                                                              store ? 1 : 0);
+                                                              store ? 1 : 0, acc, tk, 0);
   else
     colsum_geo_kernel<ACT_SIGMOID, true><<<grid, kBlock, 0, s>>>(dy, y, dx, out, rows, cols, g.rpb, g.lanes, g.rl,
-                                                                 store ? 1 : 0);
+                                                                 store ? 1 : 0, acc, tk, 0);
   return hipGetLastError();
 }
 

@@ -379,6 +379,17 @@ def _conv_bn_stats_done(bn, done: bool, y, state):
             bn.num_batches_tracked.copy_(snap[1])
 
 
+def _colsum_ws(flat, bias, cols: int, dev) -> torch.Tensor:
+    """A conv bias's persistent colsum scratch (cols floats + a ticket, zeroed once; the kernel leaves it
+    zero): its column sums over many row groups then take one launch, no zero fill (elementwise.hip)."""
+    cache = flat.__dict__.setdefault("_ldnn_colsum_ws", {})
+    ws = cache.get(id(bias))
+    if ws is None or ws.device != dev or ws.numel() < cols + 1:
+        ws = torch.zeros(cols + 1, dtype=torch.float32, device=dev)
+        cache[id(bias)] = ws
+    return ws
+
+
 class _Conv2dNative(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, stride, pad, flat, relu, bn=None):
@@ -432,12 +443,14 @@ class _Conv2dNative(torch.autograd.Function):
             gz = torch.empty_like(y)
             if bias is not None:   # ReLU backward + the bias gradient's column sums in one pass
                 C.act_bwd_colsum(g.contiguous().view(-1, kp), y.view(-1, kp), gz.view(-1, kp),
-                                 flat.grad_storage(bias), 0, flat.grad_beta(bias) != 0.0)
+                                 flat.grad_storage(bias), 0, flat.grad_beta(bias) != 0.0,
+                                 ws=_colsum_ws(flat, bias, kp, y.device))
             else:
                 C.act_bwd(g.contiguous(), y, gz, 0)
             g = gz
         elif bias is not None:
-            C.colsum(g.contiguous().view(-1, kp), flat.grad_storage(bias), flat.grad_beta(bias) != 0.0)
+            C.colsum(g.contiguous().view(-1, kp), flat.grad_storage(bias), flat.grad_beta(bias) != 0.0,
+                     ws=_colsum_ws(flat, bias, kp, g.device))
         dw, beta = flat.grad_storage(weight), flat.grad_beta(weight)
         dx = None
         if ctx.needs_input_grad[0]:

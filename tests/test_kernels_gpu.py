@@ -474,3 +474,29 @@ def test_colsum_geometries(rows, cols, accumulate):
     C().colsum(x, out, accumulate)
     ref = x.float().sum(0) + (base if accumulate else 0)
     torch.testing.assert_close(out, ref, rtol=1e-3, atol=1e-3 * max(1.0, rows ** 0.5))
+
+
+@pytest.mark.parametrize("rows,cols", [(200704, 8), (25600, 16), (12345, 48), (40000, 2056), (256, 128), (0, 16)])
+def test_colsum_with_ticketed_scratch_is_one_launch_and_leaves_it_clean(rows, cols):
+    """colsum / act_bwd_colsum with ws (the conv bias path): the overwriting multi-group sum runs
+    through the caller's zeroed scratch and a ticket instead of a zero fill + atomics into out --
+    == torch fp32, and ws (sums and ticket) is zero again after each call, so back-to-back calls
+    (a graph replay) give the same result."""
+    torch.manual_seed(rows + 7 * cols)
+    x = torch.randn(rows, cols, device="cuda").bfloat16()
+    ws = torch.zeros(cols + 1, device="cuda")
+    ref = x.float().sum(0)
+    for _ in range(2):
+        out = torch.full((cols,), float("nan"), device="cuda")
+        C().colsum(x, out, False, ws=ws)
+        torch.testing.assert_close(out, ref, rtol=1e-3, atol=1e-3 * max(1.0, rows ** 0.5))
+        assert int((ws != 0).sum().item()) == 0
+    y = torch.randn(rows, cols, device="cuda").relu().bfloat16()
+    dx = torch.empty_like(x)
+    ref_dx = x.float() * (y.float() > 0).float()
+    for _ in range(2):
+        out = torch.full((cols,), float("nan"), device="cuda")
+        C().act_bwd_colsum(x, y, dx, out, C().ACT_RELU, False, ws=ws)
+        torch.testing.assert_close(dx.float(), ref_dx, rtol=1e-2, atol=1e-2)
+        torch.testing.assert_close(out, ref_dx.sum(0), rtol=1e-3, atol=1e-3 * max(1.0, rows ** 0.5))
+        assert int((ws != 0).sum().item()) == 0
